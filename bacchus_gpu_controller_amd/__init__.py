@@ -1,0 +1,49 @@
+"""bacchus-gpu-controller, MI355X-native edition.
+
+A from-scratch rebuild of the bacchus-snu/bacchus-gpu-controller Kubernetes tenancy
+controller (UserBootstrap CRD, admission webhook, reconciler, Google-Sheet quota
+synchronizer) as native C++17 services, plus an MI355X node agent (amdsmi discovery,
+telemetry side thread, HIP/CDNA4 health diagnostics) and an RCCL/xGMI placement probe.
+
+Python is the test/bench surface:
+  * ``native()``          -> the pybind11 module over the C++ core (``_native``)
+  * ``models``            -> UserBootstrap object builders (CRD data model)
+  * ``ops``               -> HIP/CDNA4 GPU health kernels (``_gpu_ops``)
+  * ``parallel``          -> RCCL-over-xGMI all-reduce probe and hive topology
+  * ``utils``             -> build + process helpers (binaries under ``bin/``)
+  * ``testing``           -> fake Google OAuth2/Drive endpoint, cluster harness
+  * ``bench``             -> churn benchmark driver used by ``bench.py``
+"""
+import importlib
+import os
+
+__version__ = "0.1.0"
+
+REPO_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN_DIR = os.path.join(REPO_ROOT, "bin")
+
+_native_mod = None
+
+
+def native():
+    """Return the compiled C++ core module, building it first if needed."""
+    global _native_mod
+    if _native_mod is None:
+        try:
+            _native_mod = importlib.import_module("bacchus_gpu_controller_amd._native")
+        except ImportError:
+            from .utils.build import ensure_built
+
+            ensure_built()
+            _native_mod = importlib.import_module("bacchus_gpu_controller_amd._native")
+    return _native_mod
+
+
+def binary(name):
+    """Absolute path of a native binary (controller, admission, kube-lite, ...)."""
+    path = os.path.join(BIN_DIR, name)
+    if not os.path.exists(path):
+        from .utils.build import ensure_built
+
+        ensure_built()
+    return path

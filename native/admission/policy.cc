@@ -1,0 +1,249 @@
+#include "admission/policy.h"
+
+#include <algorithm>
+
+#include "core/crypto.h"
+#include "core/json_patch.h"
+#include "core/log.h"
+#include "crd/schema.h"
+
+namespace bgc::admission {
+
+using json::Value;
+
+Config Config::from_env(const EnvConfig& env) {
+  Config c;
+  c.listen_addr = env.str("listen_addr");
+  c.listen_port = env.u16("listen_port");
+  c.cert_path = env.str("cert_path");
+  c.key_path = env.str("key_path");
+  c.oidc_username_prefix = env.str("oidc_username_prefix");
+  c.default_role_name = env.str("default_role_name");
+  c.authorized_group_names = env.comma_list("authorized_group_names");
+  c.log_full_request = env.boolean_or("log_full_request", true);
+  c.cert_reload_interval_secs = env.u64_or("cert_reload_interval_secs", 60);
+  return c;
+}
+
+Username Username::classify(const std::string& username, const std::string& prefix) {
+  Username u;
+  u.original_username = username;
+  if (username.compare(0, prefix.size(), prefix) == 0) {
+    u.kube_username = username.substr(prefix.size());
+    u.kind = UserKind::Normal;
+  } else {
+    u.kube_username = username;
+    u.kind = UserKind::Admin;
+  }
+  return u;
+}
+
+namespace {
+
+Decision allow(const std::string& uid, int rule) {
+  Decision d;
+  d.uid = uid;
+  d.rule = rule;
+  return d;
+}
+
+Decision deny(const std::string& uid, const std::string& msg, int rule) {
+  LOG_ERROR("admission") << msg;
+  Decision d;
+  d.uid = uid;
+  d.allowed = false;
+  d.message = msg;
+  d.rule = rule;
+  return d;
+}
+
+// Q3 fix: the uid is echoed so the apiserver reports a clean rejection
+// rather than a webhook protocol error; the outcome (request refused) is unchanged.
+Decision invalid(const std::string& uid, const std::string& msg, int rule) {
+  LOG_ERROR("admission") << msg;
+  Decision d;
+  d.uid = uid;
+  d.allowed = false;
+  d.invalid = true;
+  d.message = msg;
+  d.rule = rule;
+  return d;
+}
+
+}  // namespace
+
+Decision mutate(const Value& req, const Config& cfg) {
+  const std::string uid = req.get_string("uid");
+  const Value& user_info = req.get("userInfo");
+
+  // rule 1: username missing
+  const Value& uname = user_info.get("username");
+  if (!uname.is_string()) return invalid(uid, "cannot get requester's username from request", 1);
+  // rule 2
+  Username username = Username::classify(uname.as_string(), cfg.oidc_username_prefix);
+
+  // rule 3: any group in authorized_group_names
+  bool is_in_group = false;
+  for (const Value& g : user_info.get("groups").items()) {
+    if (g.is_string() && std::find(cfg.authorized_group_names.begin(), cfg.authorized_group_names.end(),
+                                   g.as_string()) != cfg.authorized_group_names.end()) {
+      is_in_group = true;
+      break;
+    }
+  }
+
+  const std::string op = req.get_string("operation");
+  if (op == "CREATE") {
+    if (username.kind == UserKind::Normal && !is_in_group) return deny(uid, "user is not in authorized group", 4);
+  } else if (op == "DELETE") {
+    if (username.kind == UserKind::Normal) return deny(uid, "normal user is not allowed to delete resource", 5);
+    return allow(uid, 6);
+  } else if (op == "UPDATE") {
+    if (username.kind == UserKind::Normal) return deny(uid, "normal user is not allowed to update resource", 7);
+  } else {
+    return invalid(uid, "invalid operation", 8);
+  }
+
+  // rule 9: no object
+  const Value& obj = req.get("object");
+  if (obj.is_null()) return allow(uid, 9);
+
+  // rule 10: resource name
+  const Value& name_v = obj.get("metadata").get("name");
+  if (!name_v.is_string()) return invalid(uid, "cannot get resource name from request", 10);
+  const std::string& resource_name = name_v.as_string();
+
+  // rule 11
+  if (username.kind == UserKind::Normal && username.kube_username != resource_name) {
+    return deny(uid, "username not match with resource name", 11);
+  }
+
+  // rule 12: must parse as UserBootstrap
+  crd::UserBootstrap ub;
+  try {
+    ub = crd::parse_userbootstrap(obj);
+  } catch (const std::exception& e) {
+    LOG_ERROR("admission") << "Request is not UserBootstrap resource: " << e.what();
+    return invalid(uid, e.what(), 12);
+  }
+
+  json::PatchBuilder patches;
+  if (username.kind == UserKind::Normal) {
+    // rule 13: always (over)write kube_username for normal users
+    patches.add("/spec/kube_username", Value(username.kube_username));
+  } else if (!ub.has_kube_username || ub.kube_username.empty()) {
+    // rule 14
+    return deny(uid, "kube_username field is empty. you are an admin, so fill it", 14);
+  }
+
+  // rule 15
+  if (ub.has_quota && username.kind == UserKind::Normal) {
+    return deny(uid, "quota field is not empty. you are a normal user, so leave it empty", 15);
+  }
+
+  if (!ub.has_rolebinding) {
+    // rule 16: default RoleBinding (two ops, exactly as the reference emits them)
+    patches.add("/spec/rolebinding", Value::object());
+    const std::string subject_name =
+        username.kind == UserKind::Normal ? username.original_username : ub.kube_username;
+    Value rb = Value::object();
+    rb["role_ref"] = Value::object({{"apiGroup", "rbac.authorization.k8s.io"},
+                                    {"kind", "ClusterRole"},
+                                    {"name", cfg.default_role_name}});
+    rb["subjects"] = Value::array({Value::object({{"apiGroup", "rbac.authorization.k8s.io"},
+                                                  {"kind", "User"},
+                                                  {"name", subject_name}})});
+    patches.add("/spec/rolebinding", std::move(rb));
+  } else if (username.kind == UserKind::Normal) {
+    // rule 17
+    return deny(uid, "rolebinding field is not empty. you are a normal user, so leave it empty", 17);
+  }
+
+  Decision d = allow(uid, patches.empty() ? 18 : 19);
+  if (!patches.empty()) d.patch = patches.ops();
+  return d;
+}
+
+Value review_response(const Decision& d, const std::string& api_version) {
+  Value resp = Value::object();
+  resp["uid"] = d.uid;
+  resp["allowed"] = d.allowed;
+  if (!d.allowed) {
+    Value status = Value::object();
+    if (d.invalid) {
+      status["status"] = "Failure";
+      status["code"] = 400;
+      status["reason"] = "BadRequest";
+    }
+    status["message"] = d.message;
+    resp["status"] = std::move(status);
+  }
+  if (!d.patch.is_null()) {
+    resp["patch"] = crypto::base64_encode(d.patch.dump());
+    resp["patchType"] = "JSONPatch";
+  }
+  Value review = Value::object();
+  review["apiVersion"] = api_version.empty() ? "admission.k8s.io/v1" : api_version;
+  review["kind"] = "AdmissionReview";
+  review["response"] = std::move(resp);
+  return review;
+}
+
+HttpResult handle_review(const std::string& body, const std::string& content_type, const Config& cfg) {
+  HttpResult r;
+  if (content_type.find("application/json") == std::string::npos) {
+    r.status = 415;
+    r.content_type = "text/plain; charset=utf-8";
+    r.body = "Expected request with `Content-Type: application/json`";
+    return r;
+  }
+  Value review;
+  std::string err;
+  if (!json::try_parse(body, review, &err)) {
+    r.status = 400;
+    r.content_type = "text/plain; charset=utf-8";
+    r.body = "Failed to parse the request body as JSON: " + err;
+    return r;
+  }
+  // Shape checks of AdmissionReview<DynamicObject> (kube-core deserialization).
+  auto reject = [&](const std::string& why) {
+    r.status = 422;
+    r.content_type = "text/plain; charset=utf-8";
+    r.body = "Failed to deserialize the JSON body into the target type: " + why;
+    return r;
+  };
+  if (!review.is_object()) return reject("invalid type: expected struct AdmissionReview");
+  const std::string api_version = review.get_string("apiVersion", "admission.k8s.io/v1");
+  const Value& req = review.get("request");
+  if (req.is_null()) {
+    // try_into() fails -> AdmissionResponse::invalid
+    r.decision = invalid("", "request missing in AdmissionReview", 0);
+    r.body = review_response(r.decision, api_version).dump();
+    return r;
+  }
+  if (!req.is_object()) return reject("request: invalid type, expected struct AdmissionRequest");
+  for (const char* f : {"uid", "kind", "resource", "operation", "userInfo"}) {
+    if (!req.contains(f)) return reject(std::string("request: missing field `") + f + "`");
+  }
+  if (!req.get("uid").is_string()) return reject("request.uid: invalid type, expected a string");
+  const std::string op = req.get_string("operation");
+  if (op != "CREATE" && op != "UPDATE" && op != "DELETE" && op != "CONNECT") {
+    return reject("request.operation: unknown variant `" + op + "`");
+  }
+  for (const char* f : {"object", "oldObject"}) {
+    const Value& o = req.get(f);
+    if (!o.is_null() && (!o.is_object() || !o.get("metadata").is_object())) {
+      return reject(std::string("request.") + f + ": missing field `metadata`");
+    }
+  }
+  if (cfg.log_full_request) {
+    LOG_INFO("admission") << "received admission request req=" << req.dump();
+  } else {
+    LOG_DEBUG("admission") << "received admission request uid=" << req.get_string("uid");
+  }
+  r.decision = mutate(req, cfg);
+  r.body = review_response(r.decision, api_version).dump();
+  return r;
+}
+
+}  // namespace bgc::admission

@@ -1,0 +1,822 @@
+#include "core/http.h"
+
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <poll.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <arpa/inet.h>
+#include <cctype>
+#include <charconv>
+#include <cstring>
+
+#include "core/log.h"
+#include "core/metrics.h"
+
+namespace bgc::http {
+
+static bool ieq(const std::string& a, const std::string& b) {
+  if (a.size() != b.size()) return false;
+  for (size_t i = 0; i < a.size(); ++i) {
+    if (std::tolower(static_cast<unsigned char>(a[i])) != std::tolower(static_cast<unsigned char>(b[i]))) return false;
+  }
+  return true;
+}
+
+static std::string lower(std::string s) {
+  for (auto& c : s) c = static_cast<char>(std::tolower(static_cast<unsigned char>(c)));
+  return s;
+}
+
+void Headers::set(const std::string& name, std::string value) {
+  remove(name);
+  add(name, std::move(value));
+}
+
+const std::string* Headers::get(const std::string& name) const {
+  for (const auto& kv : items_) {
+    if (ieq(kv.first, name)) return &kv.second;
+  }
+  return nullptr;
+}
+
+std::string Headers::get_or(const std::string& name, const std::string& dflt) const {
+  const std::string* v = get(name);
+  return v ? *v : dflt;
+}
+
+void Headers::remove(const std::string& name) {
+  items_.erase(std::remove_if(items_.begin(), items_.end(), [&](auto& kv) { return ieq(kv.first, name); }),
+               items_.end());
+}
+
+const char* status_text(int code) {
+  switch (code) {
+    case 100: return "Continue";
+    case 200: return "OK";
+    case 201: return "Created";
+    case 202: return "Accepted";
+    case 204: return "No Content";
+    case 301: return "Moved Permanently";
+    case 302: return "Found";
+    case 304: return "Not Modified";
+    case 400: return "Bad Request";
+    case 401: return "Unauthorized";
+    case 403: return "Forbidden";
+    case 404: return "Not Found";
+    case 405: return "Method Not Allowed";
+    case 406: return "Not Acceptable";
+    case 408: return "Request Timeout";
+    case 409: return "Conflict";
+    case 410: return "Gone";
+    case 413: return "Payload Too Large";
+    case 415: return "Unsupported Media Type";
+    case 422: return "Unprocessable Entity";
+    case 429: return "Too Many Requests";
+    case 500: return "Internal Server Error";
+    case 501: return "Not Implemented";
+    case 502: return "Bad Gateway";
+    case 503: return "Service Unavailable";
+    case 504: return "Gateway Timeout";
+    default: return "Unknown";
+  }
+}
+
+std::string url_encode(const std::string& s, bool keep_slash) {
+  static const char kHex[] = "0123456789ABCDEF";
+  std::string out;
+  for (unsigned char c : s) {
+    if (std::isalnum(c) || c == '-' || c == '_' || c == '.' || c == '~' || (keep_slash && c == '/')) {
+      out.push_back(static_cast<char>(c));
+    } else {
+      out.push_back('%');
+      out.push_back(kHex[c >> 4]);
+      out.push_back(kHex[c & 15]);
+    }
+  }
+  return out;
+}
+
+std::string url_decode(const std::string& s) {
+  std::string out;
+  for (size_t i = 0; i < s.size(); ++i) {
+    if (s[i] == '%' && i + 2 < s.size()) {
+      int v = 0;
+      auto r = std::from_chars(s.data() + i + 1, s.data() + i + 3, v, 16);
+      if (r.ec == std::errc() && r.ptr == s.data() + i + 3) {
+        out.push_back(static_cast<char>(v));
+        i += 2;
+        continue;
+      }
+    }
+    out.push_back(s[i] == '+' ? ' ' : s[i]);
+  }
+  return out;
+}
+
+std::map<std::string, std::string> Request::query_params() const {
+  std::map<std::string, std::string> out;
+  size_t start = 0;
+  while (start < query.size()) {
+    size_t amp = query.find('&', start);
+    std::string kv = query.substr(start, amp == std::string::npos ? std::string::npos : amp - start);
+    size_t eq = kv.find('=');
+    if (!kv.empty()) {
+      if (eq == std::string::npos) out[url_decode(kv)] = "";
+      else out[url_decode(kv.substr(0, eq))] = url_decode(kv.substr(eq + 1));
+    }
+    if (amp == std::string::npos) break;
+    start = amp + 1;
+  }
+  return out;
+}
+
+std::string Request::query_param(const std::string& name, const std::string& dflt) const {
+  auto q = query_params();
+  auto it = q.find(name);
+  return it == q.end() ? dflt : it->second;
+}
+
+bool Request::has_query_param(const std::string& name) const { return query_params().count(name) > 0; }
+
+Url parse_url(const std::string& url) {
+  Url u;
+  size_t p = url.find("://");
+  if (p == std::string::npos) throw HttpError("invalid URL (no scheme): " + url);
+  u.scheme = lower(url.substr(0, p));
+  std::string rest = url.substr(p + 3);
+  size_t slash = rest.find('/');
+  std::string hostport = rest.substr(0, slash);
+  u.path = slash == std::string::npos ? "" : rest.substr(slash);
+  size_t at = hostport.rfind('@');
+  if (at != std::string::npos) hostport = hostport.substr(at + 1);
+  if (!hostport.empty() && hostport[0] == '[') {
+    size_t rb = hostport.find(']');
+    u.host = hostport.substr(1, rb - 1);
+    if (rb + 1 < hostport.size() && hostport[rb + 1] == ':') u.port = static_cast<uint16_t>(std::stoi(hostport.substr(rb + 2)));
+  } else {
+    size_t colon = hostport.rfind(':');
+    if (colon != std::string::npos) {
+      u.host = hostport.substr(0, colon);
+      u.port = static_cast<uint16_t>(std::stoi(hostport.substr(colon + 1)));
+    } else {
+      u.host = hostport;
+    }
+  }
+  if (u.port == 0) u.port = u.scheme == "https" ? 443 : 80;
+  if (u.scheme != "http" && u.scheme != "https") throw HttpError("unsupported scheme: " + u.scheme);
+  return u;
+}
+
+// ---------------------------------------------------------------------------
+// Reader
+
+ssize_t Reader::fill(int timeout_ms) {
+  if (pos_ > 0 && pos_ == buf_.size()) {
+    buf_.clear();
+    pos_ = 0;
+  } else if (pos_ > (1 << 16)) {
+    buf_.erase(0, pos_);
+    pos_ = 0;
+  }
+  char tmp[16384];
+  ssize_t r = s_.read_some(tmp, sizeof(tmp), timeout_ms);
+  if (r > 0) {
+    buf_.append(tmp, static_cast<size_t>(r));
+    consumed_any_ = true;
+  }
+  return r;
+}
+
+bool Reader::read_line(std::string& line, int timeout_ms, size_t max_len) {
+  while (true) {
+    size_t nl = buf_.find('\n', pos_);
+    if (nl != std::string::npos) {
+      size_t end = nl;
+      if (end > pos_ && buf_[end - 1] == '\r') --end;
+      line.assign(buf_, pos_, end - pos_);
+      pos_ = nl + 1;
+      return true;
+    }
+    if (buf_.size() - pos_ > max_len) return false;
+    ssize_t r = fill(timeout_ms);
+    if (r <= 0) return false;
+  }
+}
+
+bool Reader::read_exact(std::string& out, size_t n, int timeout_ms) {
+  while (buf_.size() - pos_ < n) {
+    ssize_t r = fill(timeout_ms);
+    if (r <= 0) return false;
+  }
+  out.append(buf_, pos_, n);
+  pos_ += n;
+  return true;
+}
+
+ssize_t Reader::read_available(std::string& out, int timeout_ms) {
+  if (pos_ < buf_.size()) {
+    size_t n = buf_.size() - pos_;
+    out.append(buf_, pos_, n);
+    pos_ = buf_.size();
+    return static_cast<ssize_t>(n);
+  }
+  ssize_t r = fill(timeout_ms);
+  if (r <= 0) return r;
+  size_t n = buf_.size() - pos_;
+  out.append(buf_, pos_, n);
+  pos_ = buf_.size();
+  return static_cast<ssize_t>(n);
+}
+
+static bool parse_headers(Reader& r, Headers& h, int timeout_ms) {
+  std::string line;
+  for (int i = 0; i < 256; ++i) {
+    if (!r.read_line(line, timeout_ms)) return false;
+    if (line.empty()) return true;
+    size_t c = line.find(':');
+    if (c == std::string::npos) return false;
+    std::string v = line.substr(c + 1);
+    size_t a = v.find_first_not_of(" \t");
+    v = a == std::string::npos ? "" : v.substr(a);
+    while (!v.empty() && (v.back() == ' ' || v.back() == '\t')) v.pop_back();
+    h.add(line.substr(0, c), v);
+  }
+  return false;
+}
+
+static bool read_chunked(Reader& r, std::string& body, int timeout_ms, size_t max_body) {
+  std::string line;
+  while (true) {
+    if (!r.read_line(line, timeout_ms)) return false;
+    size_t semi = line.find(';');
+    std::string hex = line.substr(0, semi);
+    size_t n = 0;
+    auto res = std::from_chars(hex.data(), hex.data() + hex.size(), n, 16);
+    if (res.ec != std::errc()) return false;
+    if (n == 0) {
+      // trailers
+      while (r.read_line(line, timeout_ms)) {
+        if (line.empty()) return true;
+      }
+      return false;
+    }
+    if (body.size() + n > max_body) return false;
+    if (!r.read_exact(body, n, timeout_ms)) return false;
+    if (!r.read_line(line, timeout_ms)) return false;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Server
+
+void ResponseWriter::send(int status, const std::string& body, const std::string& content_type,
+                          const Headers* extra) {
+  if (sent_) return;
+  sent_ = true;
+  std::string out;
+  out.reserve(body.size() + 160);
+  out.append("HTTP/1.1 ").append(std::to_string(status)).append(" ").append(status_text(status)).append("\r\n");
+  if (!content_type.empty()) out.append("Content-Type: ").append(content_type).append("\r\n");
+  out.append("Content-Length: ").append(std::to_string(body.size())).append("\r\n");
+  if (extra) {
+    for (auto& kv : extra->items()) out.append(kv.first).append(": ").append(kv.second).append("\r\n");
+  }
+  out.append(keep_alive_ ? "Connection: keep-alive\r\n\r\n" : "Connection: close\r\n\r\n");
+  out.append(body);
+  s_.write_all(out);
+}
+
+bool ResponseWriter::start_chunked(int status, const std::string& content_type) {
+  if (sent_) return false;
+  sent_ = true;
+  chunked_ = true;
+  keep_alive_ = false;  // long-lived stream: close afterwards
+  std::string out = "HTTP/1.1 " + std::to_string(status) + " " + status_text(status) + "\r\n";
+  out += "Content-Type: " + content_type + "\r\nTransfer-Encoding: chunked\r\nConnection: close\r\n\r\n";
+  return s_.write_all(out);
+}
+
+bool ResponseWriter::write_chunk(const std::string& data) {
+  if (data.empty()) return true;
+  char hdr[32];
+  int n = std::snprintf(hdr, sizeof(hdr), "%zx\r\n", data.size());
+  std::string out;
+  out.reserve(data.size() + 16);
+  out.append(hdr, static_cast<size_t>(n)).append(data).append("\r\n");
+  return s_.write_all(out);
+}
+
+void ResponseWriter::end_chunked() {
+  if (chunked_) s_.write_all("0\r\n\r\n", 5);
+}
+
+bool ResponseWriter::peer_closed() {
+  struct pollfd p {};
+  p.fd = s_.fd();
+  p.events = POLLIN | POLLRDHUP;
+  int r = ::poll(&p, 1, 0);
+  if (r <= 0) return false;
+  if (p.revents & (POLLHUP | POLLERR | POLLRDHUP)) return true;
+  if (p.revents & POLLIN) {
+    char c;
+    ssize_t n = ::recv(s_.fd(), &c, 1, MSG_PEEK | MSG_DONTWAIT);
+    return n == 0;
+  }
+  return false;
+}
+
+Server::Server(ServerOptions opts) : opts_(std::move(opts)) {}
+
+Server::~Server() {
+  if (started_) stop(std::chrono::milliseconds(0));
+}
+
+void Server::handle(const std::string& method, const std::string& path, Handler h) {
+  exact_[{method, path}] = std::move(h);
+}
+
+void Server::handle_prefix(const std::string& prefix, Handler h) {
+  prefix_.emplace_back(prefix, std::move(h));
+  std::stable_sort(prefix_.begin(), prefix_.end(),
+                   [](const auto& a, const auto& b) { return a.first.size() > b.first.size(); });
+}
+
+void Server::start() {
+  listen_fd_ = net::listen_tcp(opts_.addr, opts_.port, 1024, &port_);
+  if (::pipe2(wake_pipe_, O_CLOEXEC) != 0) throw net::NetError("pipe2 failed");
+  started_ = true;
+  accept_thread_ = std::thread([this] { accept_loop(); });
+}
+
+void Server::accept_loop() {
+  while (!stop_.cancelled()) {
+    struct pollfd fds[2] = {};
+    fds[0].fd = listen_fd_;
+    fds[0].events = POLLIN;
+    fds[1].fd = wake_pipe_[0];
+    fds[1].events = POLLIN;
+    int r = ::poll(fds, 2, 1000);
+    if (r < 0 && errno != EINTR) break;
+    if (r <= 0) continue;
+    if (fds[1].revents) break;
+    if (!(fds[0].revents & POLLIN)) continue;
+    struct sockaddr_storage ss {};
+    socklen_t len = sizeof(ss);
+    int fd = ::accept4(listen_fd_, reinterpret_cast<sockaddr*>(&ss), &len, SOCK_CLOEXEC);
+    if (fd < 0) continue;
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, 1 /*TCP_NODELAY*/, &one, sizeof(one));
+    char host[INET6_ADDRSTRLEN] = {0};
+    if (ss.ss_family == AF_INET) {
+      inet_ntop(AF_INET, &reinterpret_cast<sockaddr_in*>(&ss)->sin_addr, host, sizeof(host));
+    } else {
+      inet_ntop(AF_INET6, &reinterpret_cast<sockaddr_in6*>(&ss)->sin6_addr, host, sizeof(host));
+    }
+    if (active_.load() >= opts_.max_connections) {
+      ::close(fd);
+      continue;
+    }
+    active_.fetch_add(1);
+    std::thread([this, fd, remote = std::string(host)] {
+      serve_conn(fd, remote);
+      {
+        std::lock_guard<std::mutex> lk(conns_mu_);
+        active_.fetch_sub(1);
+      }
+      conns_cv_.notify_all();
+    }).detach();
+  }
+}
+
+void Server::serve_conn(int fd, std::string remote) {
+  std::unique_ptr<net::Stream> s;
+  try {
+    if (opts_.tls) {
+      s = std::make_unique<net::TlsStream>(fd, opts_.tls->get(), true, "", false, opts_.header_timeout_ms);
+    } else {
+      s = std::make_unique<net::TcpStream>(fd);
+    }
+  } catch (const std::exception& e) {
+    LOG_DEBUG(opts_.name) << "connection setup failed from " << remote << ": " << e.what();
+    return;
+  }
+  {
+    std::lock_guard<std::mutex> lk(conns_mu_);
+    conns_[fd] = s.get();
+  }
+  Reader r(*s);
+  while (!stop_.cancelled()) {
+    Request req;
+    req.remote = remote;
+    std::string line;
+    // wait for the request line, waking periodically to observe shutdown
+    int idle = 0;
+    bool got = false;
+    while (!stop_.cancelled()) {
+      if (r.read_line(line, 500)) {
+        got = true;
+        break;
+      }
+      // read_line false: timeout (no new bytes) or EOF/error. Distinguish by polling.
+      struct pollfd p {};
+      p.fd = fd;
+      p.events = POLLIN;
+      if (!r.buffered() && ::poll(&p, 1, 0) > 0) {
+        char c;
+        ssize_t n = ::recv(fd, &c, 1, MSG_PEEK | MSG_DONTWAIT);
+        if (n <= 0) break;  // peer closed
+        continue;
+      }
+      idle += 500;
+      if (idle >= opts_.idle_timeout_ms) break;
+    }
+    if (!got) break;
+    if (line.empty()) continue;  // tolerate stray CRLF between requests
+    size_t sp1 = line.find(' ');
+    size_t sp2 = line.rfind(' ');
+    if (sp1 == std::string::npos || sp2 == sp1) break;
+    req.method = line.substr(0, sp1);
+    req.target = line.substr(sp1 + 1, sp2 - sp1 - 1);
+    std::string version = line.substr(sp2 + 1);
+    if (!parse_headers(r, req.headers, opts_.header_timeout_ms)) break;
+    size_t q = req.target.find('?');
+    req.path = url_decode(req.target.substr(0, q));
+    req.query = q == std::string::npos ? "" : req.target.substr(q + 1);
+    bool keep_alive = version == "HTTP/1.1";
+    if (const std::string* c = req.headers.get("Connection")) {
+      std::string lc = lower(*c);
+      if (lc.find("close") != std::string::npos) keep_alive = false;
+      if (lc.find("keep-alive") != std::string::npos) keep_alive = true;
+    }
+    if (const std::string* ex = req.headers.get("Expect")) {
+      if (lower(*ex) == "100-continue") s->write_all("HTTP/1.1 100 Continue\r\n\r\n");
+    }
+    bool body_ok = true;
+    if (const std::string* te = req.headers.get("Transfer-Encoding"); te && lower(*te).find("chunked") != std::string::npos) {
+      body_ok = read_chunked(r, req.body, opts_.header_timeout_ms, opts_.max_body);
+    } else if (const std::string* cl = req.headers.get("Content-Length")) {
+      size_t n = 0;
+      auto res = std::from_chars(cl->data(), cl->data() + cl->size(), n);
+      if (res.ec != std::errc() || n > opts_.max_body) {
+        ResponseWriter w(*s, false, stop_);
+        w.send(413, "request body too large\n");
+        break;
+      }
+      body_ok = r.read_exact(req.body, n, opts_.header_timeout_ms);
+    }
+    if (!body_ok) break;
+    ResponseWriter w(*s, keep_alive && !stop_.cancelled(), stop_);
+    try {
+      if (!dispatch(req, w)) w.send(404, "404 page not found\n");
+    } catch (const std::exception& e) {
+      LOG_ERROR(opts_.name) << "handler error for " << req.method << " " << req.path << ": " << e.what();
+      if (!w.sent()) w.send(500, std::string("internal error: ") + e.what() + "\n");
+    }
+    if (!w.sent()) w.send(500, "handler produced no response\n");
+    if (!w.keep_alive()) break;
+  }
+  {
+    std::lock_guard<std::mutex> lk(conns_mu_);
+    conns_.erase(fd);
+  }
+}
+
+bool Server::dispatch(Request& req, ResponseWriter& w) {
+  auto it = exact_.find({req.method, req.path});
+  if (it != exact_.end()) {
+    it->second(req, w);
+    return true;
+  }
+  bool path_known = false;
+  for (auto& kv : exact_) {
+    if (kv.first.second == req.path) path_known = true;
+  }
+  for (auto& [prefix, h] : prefix_) {
+    if (req.path.compare(0, prefix.size(), prefix) == 0) {
+      h(req, w);
+      return true;
+    }
+  }
+  if (path_known) {
+    w.send(405, "method not allowed\n");
+    return true;
+  }
+  return false;
+}
+
+void Server::stop(std::chrono::milliseconds grace) {
+  if (!started_) return;
+  stop_.cancel();
+  if (wake_pipe_[1] >= 0) {
+    char c = 1;
+    (void)!::write(wake_pipe_[1], &c, 1);
+  }
+  if (accept_thread_.joinable()) accept_thread_.join();
+  if (listen_fd_ >= 0) {
+    ::close(listen_fd_);
+    listen_fd_ = -1;
+  }
+  {
+    std::unique_lock<std::mutex> lk(conns_mu_);
+    conns_cv_.wait_for(lk, grace, [&] { return active_.load() == 0; });
+    for (auto& kv : conns_) kv.second->shutdown();
+    conns_cv_.wait_for(lk, std::chrono::milliseconds(2000), [&] { return active_.load() == 0; });
+  }
+  for (int& p : wake_pipe_) {
+    if (p >= 0) ::close(p);
+    p = -1;
+  }
+  started_ = false;
+}
+
+void add_standard_routes(Server& s) {
+  s.handle("GET", "/health", [](Request&, ResponseWriter& w) { w.send(200, "pong"); });
+  s.handle("GET", "/metrics", [](Request&, ResponseWriter& w) {
+    w.send(200, metrics::Registry::global().render(), "text/plain; version=0.0.4");
+  });
+  s.handle_prefix("/debug/samples/", [](Request& r, ResponseWriter& w) {
+    std::string name = r.path.substr(std::strlen("/debug/samples/"));
+    if (r.method == "DELETE") {
+      metrics::Registry::global().samples(name).clear();
+      w.send(200, "{}", "application/json");
+      return;
+    }
+    w.send(200, metrics::Registry::global().render_samples_json(name), "application/json");
+  });
+}
+
+// ---------------------------------------------------------------------------
+// Client
+
+Client::Client(ClientOptions opts) : opts_(std::move(opts)) {
+  url_ = parse_url(opts_.base_url);
+  if (url_.scheme == "https" && !opts_.tls) opts_.tls = net::TlsContext::client("", false);
+}
+
+Client::~Client() = default;
+
+void Client::set_default_header(const std::string& name, const std::string& value) {
+  std::lock_guard<std::mutex> lk(mu_);
+  opts_.default_headers.set(name, value);
+}
+
+void Client::close_idle() {
+  std::lock_guard<std::mutex> lk(mu_);
+  idle_.clear();
+}
+
+std::unique_ptr<net::Stream> Client::connect() {
+  int fd = net::connect_tcp(url_.host, url_.port, opts_.connect_timeout_ms);
+  if (url_.scheme == "https") {
+    std::string host = opts_.tls_server_name.empty() ? url_.host : opts_.tls_server_name;
+    return std::make_unique<net::TlsStream>(fd, opts_.tls->get(), false, host, !opts_.tls->insecure(),
+                                            opts_.connect_timeout_ms);
+  }
+  return std::make_unique<net::TcpStream>(fd);
+}
+
+std::unique_ptr<net::Stream> Client::take_idle() {
+  std::lock_guard<std::mutex> lk(mu_);
+  while (!idle_.empty()) {
+    auto s = std::move(idle_.back());
+    idle_.pop_back();
+    // discard connections the server already closed
+    struct pollfd p {};
+    p.fd = s->fd();
+    p.events = POLLIN;
+    if (::poll(&p, 1, 0) > 0 && !s->has_buffered()) continue;
+    return s;
+  }
+  return nullptr;
+}
+
+void Client::give_back(std::unique_ptr<net::Stream> s) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (idle_.size() < opts_.max_idle) idle_.push_back(std::move(s));
+}
+
+std::string Client::build_request(const std::string& method, const std::string& path, const std::string& body,
+                                  const Headers* headers) {
+  std::string p = path.empty() ? "/" : path;
+  std::string out;
+  out.reserve(body.size() + 256);
+  out.append(method).append(" ").append(p).append(" HTTP/1.1\r\n");
+  out.append("Host: ").append(url_.host);
+  if (!((url_.scheme == "http" && url_.port == 80) || (url_.scheme == "https" && url_.port == 443))) {
+    out.append(":").append(std::to_string(url_.port));
+  }
+  out.append("\r\n");
+  Headers merged;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    merged = opts_.default_headers;
+  }
+  if (headers) {
+    for (auto& kv : headers->items()) merged.set(kv.first, kv.second);
+  }
+  if (!merged.has("User-Agent")) merged.set("User-Agent", "bgc-amd/0.1");
+  for (auto& kv : merged.items()) out.append(kv.first).append(": ").append(kv.second).append("\r\n");
+  if (!body.empty() || method == "POST" || method == "PUT" || method == "PATCH") {
+    out.append("Content-Length: ").append(std::to_string(body.size())).append("\r\n");
+  }
+  out.append("\r\n").append(body);
+  return out;
+}
+
+Response Client::request(const std::string& method, const std::string& path, const std::string& body,
+                         const Headers* headers, int timeout_ms) {
+  int to = timeout_ms < 0 ? opts_.timeout_ms : timeout_ms;
+  std::string wire = build_request(method, path, body, headers);
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    auto s = take_idle();
+    bool reused = s != nullptr;
+    if (!s) s = connect();
+    if (!s->write_all(wire)) {
+      if (reused) continue;
+      throw HttpError("write failed: " + method + " " + path);
+    }
+    Reader r(*s);
+    std::string line;
+    if (!r.read_line(line, to)) {
+      if (reused && !r.consumed_any()) continue;
+      throw HttpError("no response (timeout or connection closed): " + method + " " + path);
+    }
+    Response resp;
+    if (line.size() < 12 || line.compare(0, 5, "HTTP/") != 0) throw HttpError("malformed status line: " + line);
+    resp.status = std::atoi(line.c_str() + 9);
+    if (!parse_headers(r, resp.headers, to)) throw HttpError("malformed response headers");
+    bool keep = line.compare(0, 8, "HTTP/1.1") == 0;
+    if (const std::string* c = resp.headers.get("Connection")) {
+      if (lower(*c).find("close") != std::string::npos) keep = false;
+    }
+    bool no_body = method == "HEAD" || resp.status == 204 || resp.status == 304 || resp.status / 100 == 1;
+    if (!no_body) {
+      if (const std::string* te = resp.headers.get("Transfer-Encoding");
+          te && lower(*te).find("chunked") != std::string::npos) {
+        if (!read_chunked(r, resp.body, to, size_t(1) << 31)) throw HttpError("truncated chunked body");
+      } else if (const std::string* cl = resp.headers.get("Content-Length")) {
+        size_t n = static_cast<size_t>(std::stoull(*cl));
+        if (!r.read_exact(resp.body, n, to)) throw HttpError("truncated body");
+      } else {
+        // read until close
+        while (true) {
+          ssize_t n = r.read_available(resp.body, to);
+          if (n <= 0) break;
+        }
+        keep = false;
+      }
+    }
+    if (keep) give_back(std::move(s));
+    return resp;
+  }
+  throw HttpError("request failed after retry: " + method + " " + path);
+}
+
+std::unique_ptr<StreamingResponse> Client::stream(const std::string& method, const std::string& path,
+                                                  const Headers* headers, const std::string& body) {
+  std::string wire = build_request(method, path, body, headers);
+  auto s = connect();  // long-lived streams never share pooled connections
+  if (!s->write_all(wire)) throw HttpError("write failed: " + path);
+  auto sr = std::make_unique<StreamingResponse>();
+  sr->reader_ = std::make_unique<Reader>(*s);
+  std::string line;
+  if (!sr->reader_->read_line(line, opts_.timeout_ms)) throw HttpError("no response to stream request: " + path);
+  if (line.size() < 12 || line.compare(0, 5, "HTTP/") != 0) throw HttpError("malformed status line: " + line);
+  sr->status = std::atoi(line.c_str() + 9);
+  if (!parse_headers(*sr->reader_, sr->headers, opts_.timeout_ms)) throw HttpError("malformed response headers");
+  if (const std::string* te = sr->headers.get("Transfer-Encoding"); te && lower(*te).find("chunked") != std::string::npos) {
+    sr->chunked_ = true;
+  } else if (const std::string* cl = sr->headers.get("Content-Length")) {
+    sr->remaining_ = static_cast<int64_t>(std::stoll(*cl));
+  }
+  sr->stream_ = std::move(s);
+  return sr;
+}
+
+StreamingResponse::~StreamingResponse() { reader_.reset(); }
+
+void StreamingResponse::close() {
+  if (stream_) stream_->shutdown();
+  done_ = true;
+}
+
+bool StreamingResponse::pull(const CancelToken* cancel, int poll_ms) {
+  // Reads more body bytes into pending_. Returns false at end of body.
+  while (!done_) {
+    if (cancel && cancel->cancelled()) return false;
+    if (chunked_) {
+      std::string line;
+      if (!reader_->read_line(line, poll_ms)) {
+        if (reader_->consumed_any() || true) {
+          // distinguish timeout from EOF via a zero-timeout probe of the socket
+          struct pollfd p {};
+          p.fd = stream_->fd();
+          p.events = POLLIN;
+          if (::poll(&p, 1, 0) > 0 && !reader_->buffered()) {
+            char c;
+            if (::recv(stream_->fd(), &c, 1, MSG_PEEK | MSG_DONTWAIT) <= 0) {
+              done_ = true;
+              return false;
+            }
+          }
+        }
+        continue;  // timeout: re-check cancel
+      }
+      size_t n = 0;
+      size_t semi = line.find(';');
+      std::string hex = line.substr(0, semi);
+      auto res = std::from_chars(hex.data(), hex.data() + hex.size(), n, 16);
+      if (res.ec != std::errc()) {
+        done_ = true;
+        return false;
+      }
+      if (n == 0) {
+        done_ = true;
+        return false;
+      }
+      std::string data;
+      while (!reader_->read_exact(data, n, poll_ms)) {
+        if (cancel && cancel->cancelled()) return false;
+        struct pollfd p {};
+        p.fd = stream_->fd();
+        p.events = POLLIN;
+        if (::poll(&p, 1, 0) > 0) {
+          char c;
+          if (::recv(stream_->fd(), &c, 1, MSG_PEEK | MSG_DONTWAIT) <= 0 && !reader_->buffered()) {
+            done_ = true;
+            return false;
+          }
+        }
+      }
+      pending_ += data;
+      std::string crlf;
+      reader_->read_line(crlf, 10000);
+      return true;
+    }
+    if (remaining_ == 0) {
+      done_ = true;
+      return false;
+    }
+    std::string data;
+    ssize_t r = reader_->read_available(data, poll_ms);
+    if (r == -2) continue;
+    if (r <= 0) {
+      done_ = true;
+      return false;
+    }
+    if (remaining_ > 0) {
+      if (static_cast<int64_t>(data.size()) > remaining_) data.resize(static_cast<size_t>(remaining_));
+      remaining_ -= static_cast<int64_t>(data.size());
+    }
+    pending_ += data;
+    return true;
+  }
+  return false;
+}
+
+bool StreamingResponse::next_line(std::string& line, const CancelToken* cancel, int poll_ms) {
+  while (true) {
+    size_t nl = pending_.find('\n');
+    if (nl != std::string::npos) {
+      line = pending_.substr(0, nl);
+      pending_.erase(0, nl + 1);
+      if (!line.empty() && line.back() == '\r') line.pop_back();
+      return true;
+    }
+    if (!pull(cancel, poll_ms)) {
+      if (!pending_.empty()) {
+        line.swap(pending_);
+        pending_.clear();
+        return true;
+      }
+      return false;
+    }
+  }
+}
+
+std::string StreamingResponse::read_all(int timeout_ms) {
+  std::string out;
+  std::string line;
+  auto deadline = metrics::now_ns() + static_cast<int64_t>(timeout_ms) * 1000000;
+  while (metrics::now_ns() < deadline && next_line(line, nullptr, 200)) {
+    out += line;
+    out += "\n";
+  }
+  return out;
+}
+
+Response fetch(const std::string& method, const std::string& url, const std::string& body, const Headers* headers,
+               std::shared_ptr<net::TlsContext> tls, int timeout_ms) {
+  Url u = parse_url(url);
+  ClientOptions o;
+  o.base_url = u.scheme + "://" + u.host + ":" + std::to_string(u.port);
+  o.tls = std::move(tls);
+  o.timeout_ms = timeout_ms;
+  Client c(o);
+  return c.request(method, u.path.empty() ? "/" : u.path, body, headers, timeout_ms);
+}
+
+}  // namespace bgc::http

@@ -1,0 +1,244 @@
+// HTTP/1.1 server and keep-alive client.
+//
+// Server: one thread per connection (blocking I/O, TCP_NODELAY) — latency-optimal for
+// the handful of keep-alive connections the apiserver and kubelet probes open; a
+// request is served on the thread that read it, with no hand-off.  Replaces axum 0.6
+// (`/health`, `/mutate`, reference src/controller.rs:256-263, src/admission.rs:149-177).
+//
+// Client: per-endpoint pool of keep-alive connections (plain or TLS) plus streaming
+// responses for WATCH.  Replaces hyper 0.14 inside kube-client / google-drive3.
+#pragma once
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "core/cancel.h"
+#include "core/net.h"
+
+namespace bgc::http {
+
+class Headers {
+ public:
+  void add(std::string name, std::string value) { items_.emplace_back(std::move(name), std::move(value)); }
+  void set(const std::string& name, std::string value);
+  const std::string* get(const std::string& name) const;  // case-insensitive
+  std::string get_or(const std::string& name, const std::string& dflt = "") const;
+  bool has(const std::string& name) const { return get(name) != nullptr; }
+  void remove(const std::string& name);
+  const std::vector<std::pair<std::string, std::string>>& items() const { return items_; }
+
+ private:
+  std::vector<std::pair<std::string, std::string>> items_;
+};
+
+struct Request {
+  std::string method;
+  std::string target;  // raw request-target
+  std::string path;    // decoded path component
+  std::string query;   // raw query string (no '?')
+  Headers headers;
+  std::string body;
+  std::string remote;
+  std::string query_param(const std::string& name, const std::string& dflt = "") const;
+  bool has_query_param(const std::string& name) const;
+  std::map<std::string, std::string> query_params() const;
+};
+
+struct Response {
+  int status = 200;
+  Headers headers;
+  std::string body;
+};
+
+const char* status_text(int code);
+std::string url_encode(const std::string& s, bool keep_slash = false);
+std::string url_decode(const std::string& s);
+
+struct Url {
+  std::string scheme;  // http | https
+  std::string host;
+  uint16_t port = 0;
+  std::string path;  // includes query if any; "" when absent
+};
+Url parse_url(const std::string& url);
+
+// Buffered reader over a Stream (request/response parsing, chunked decoding).
+class Reader {
+ public:
+  explicit Reader(net::Stream& s) : s_(s) {}
+  // Returns false on EOF/error/timeout. `got_any` reports whether any byte arrived.
+  bool read_line(std::string& line, int timeout_ms, size_t max_len = 1 << 16);
+  bool read_exact(std::string& out, size_t n, int timeout_ms);
+  // Reads whatever is available (at least 1 byte). Returns -1 error, 0 EOF, -2 timeout.
+  ssize_t read_available(std::string& out, int timeout_ms);
+  bool buffered() const { return pos_ < buf_.size() || s_.has_buffered(); }
+  bool consumed_any() const { return consumed_any_; }
+
+ private:
+  ssize_t fill(int timeout_ms);
+  net::Stream& s_;
+  std::string buf_;
+  size_t pos_ = 0;
+  bool consumed_any_ = false;
+};
+
+// ---------------------------------------------------------------------------
+// Server
+
+class ResponseWriter {
+ public:
+  ResponseWriter(net::Stream& s, bool keep_alive, const CancelToken& server_stop)
+      : s_(s), keep_alive_(keep_alive), stop_(server_stop) {}
+  void send(int status, const std::string& body, const std::string& content_type = "text/plain; charset=utf-8",
+            const Headers* extra = nullptr);
+  void send_json(int status, const std::string& body) { send(status, body, "application/json"); }
+  // Streaming (chunked) responses for WATCH.
+  bool start_chunked(int status, const std::string& content_type);
+  bool write_chunk(const std::string& data);
+  void end_chunked();
+  bool sent() const { return sent_; }
+  bool keep_alive() const { return keep_alive_; }
+  // True once the server is shutting down; streaming handlers should return.
+  bool stopping() const { return stop_.cancelled(); }
+  // Non-blocking peer liveness probe for long-lived streams.
+  bool peer_closed();
+
+ private:
+  net::Stream& s_;
+  bool keep_alive_;
+  const CancelToken& stop_;
+  bool sent_ = false;
+  bool chunked_ = false;
+};
+
+using Handler = std::function<void(Request&, ResponseWriter&)>;
+
+struct ServerOptions {
+  std::string addr = "0.0.0.0";
+  uint16_t port = 0;
+  std::shared_ptr<net::TlsContext> tls;  // null = plain HTTP
+  size_t max_body = 64 << 20;
+  int idle_timeout_ms = 90000;
+  int header_timeout_ms = 10000;
+  size_t max_connections = 4096;
+  std::string name = "http";
+};
+
+class Server {
+ public:
+  explicit Server(ServerOptions opts);
+  ~Server();
+  void handle(const std::string& method, const std::string& path, Handler h);
+  // Fallback for any path with this prefix (longest prefix wins).
+  void handle_prefix(const std::string& prefix, Handler h);
+  void start();  // binds and spawns the accept thread; throws on bind failure
+  uint16_t port() const { return port_; }
+  // Stops accepting, waits up to `grace` for in-flight requests, then force-closes.
+  void stop(std::chrono::milliseconds grace = std::chrono::milliseconds(10000));
+  size_t active_connections() const { return active_.load(); }
+
+ private:
+  void accept_loop();
+  void serve_conn(int fd, std::string remote);
+  bool dispatch(Request& req, ResponseWriter& w);
+
+  ServerOptions opts_;
+  std::map<std::pair<std::string, std::string>, Handler> exact_;
+  std::vector<std::pair<std::string, Handler>> prefix_;
+  int listen_fd_ = -1;
+  int wake_pipe_[2] = {-1, -1};
+  uint16_t port_ = 0;
+  std::thread accept_thread_;
+  CancelToken stop_;
+  std::atomic<size_t> active_{0};
+  std::mutex conns_mu_;
+  std::condition_variable conns_cv_;
+  std::map<int, net::Stream*> conns_;
+  bool started_ = false;
+};
+
+// Attaches `/health` (-> "pong"), `/metrics` and `/debug/samples/<name>`.
+void add_standard_routes(Server& s);
+
+// ---------------------------------------------------------------------------
+// Client
+
+struct ClientOptions {
+  std::string base_url;                   // http(s)://host:port
+  std::shared_ptr<net::TlsContext> tls;   // required for https (defaults to system roots)
+  std::string tls_server_name;            // override verify host (defaults to URL host)
+  int connect_timeout_ms = 5000;
+  int timeout_ms = 30000;
+  size_t max_idle = 256;
+  Headers default_headers;
+};
+
+class HttpError : public std::runtime_error {
+ public:
+  using std::runtime_error::runtime_error;
+};
+
+class Client;
+
+// A response whose body is consumed incrementally (chunked/line-delimited).
+class StreamingResponse {
+ public:
+  int status = 0;
+  Headers headers;
+  // Next '\n'-terminated line (without the newline). false on end/error/cancel.
+  bool next_line(std::string& line, const CancelToken* cancel = nullptr, int poll_ms = 500);
+  // Reads the whole remaining body (non-2xx error bodies).
+  std::string read_all(int timeout_ms = 10000);
+  void close();
+  ~StreamingResponse();
+
+ private:
+  friend class Client;
+  bool pull(const CancelToken* cancel, int poll_ms);
+  std::unique_ptr<net::Stream> stream_;
+  std::unique_ptr<Reader> reader_;
+  bool chunked_ = false;
+  int64_t remaining_ = -1;  // content-length mode
+  bool done_ = false;
+  std::string pending_;
+};
+
+class Client {
+ public:
+  explicit Client(ClientOptions opts);
+  ~Client();
+  Response request(const std::string& method, const std::string& path, const std::string& body = "",
+                   const Headers* headers = nullptr, int timeout_ms = -1);
+  std::unique_ptr<StreamingResponse> stream(const std::string& method, const std::string& path,
+                                            const Headers* headers = nullptr, const std::string& body = "");
+  const Url& url() const { return url_; }
+  void set_default_header(const std::string& name, const std::string& value);
+  void close_idle();
+
+ private:
+  std::unique_ptr<net::Stream> connect();
+  std::unique_ptr<net::Stream> take_idle();
+  void give_back(std::unique_ptr<net::Stream> s);
+  std::string build_request(const std::string& method, const std::string& path, const std::string& body,
+                            const Headers* headers);
+
+  ClientOptions opts_;
+  Url url_;
+  std::mutex mu_;
+  std::vector<std::unique_ptr<net::Stream>> idle_;
+};
+
+// One-shot convenience (no pooling).
+Response fetch(const std::string& method, const std::string& url, const std::string& body = "",
+               const Headers* headers = nullptr, std::shared_ptr<net::TlsContext> tls = nullptr,
+               int timeout_ms = 30000);
+
+}  // namespace bgc::http

@@ -1,0 +1,249 @@
+#include "core/metrics.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <sstream>
+
+#include "core/json.h"
+
+namespace bgc::metrics {
+
+namespace {
+uint64_t to_bits(double d) {
+  uint64_t u;
+  std::memcpy(&u, &d, sizeof(u));
+  return u;
+}
+double from_bits(uint64_t u) {
+  double d;
+  std::memcpy(&d, &u, sizeof(d));
+  return d;
+}
+void atomic_add(std::atomic<uint64_t>& a, double v) {
+  uint64_t cur = a.load(std::memory_order_relaxed);
+  while (!a.compare_exchange_weak(cur, to_bits(from_bits(cur) + v), std::memory_order_relaxed)) {
+  }
+}
+std::string fmt_double(double v) {
+  if (std::isinf(v)) return v > 0 ? "+Inf" : "-Inf";
+  std::ostringstream os;
+  os.precision(17);
+  os << v;
+  return os.str();
+}
+}  // namespace
+
+int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+void Counter::inc(double v) { atomic_add(bits_, v); }
+double Counter::value() const { return from_bits(bits_.load(std::memory_order_relaxed)); }
+void Gauge::set(double v) { bits_.store(to_bits(v), std::memory_order_relaxed); }
+double Gauge::value() const { return from_bits(bits_.load(std::memory_order_relaxed)); }
+
+Histogram::Histogram(std::vector<double> buckets) : bounds_(std::move(buckets)) {
+  std::sort(bounds_.begin(), bounds_.end());
+  counts_.reset(new std::atomic<uint64_t>[bounds_.size() + 1]);
+  for (size_t i = 0; i <= bounds_.size(); ++i) counts_[i].store(0);
+}
+
+void Histogram::observe(double v) {
+  size_t idx = static_cast<size_t>(std::lower_bound(bounds_.begin(), bounds_.end(), v) - bounds_.begin());
+  counts_[idx].fetch_add(1, std::memory_order_relaxed);
+  atomic_add(sum_bits_, v);
+  count_.fetch_add(1, std::memory_order_relaxed);
+}
+
+std::vector<uint64_t> Histogram::bucket_counts() const {
+  std::vector<uint64_t> out(bounds_.size() + 1);
+  for (size_t i = 0; i <= bounds_.size(); ++i) out[i] = counts_[i].load(std::memory_order_relaxed);
+  return out;
+}
+double Histogram::sum() const { return from_bits(sum_bits_.load(std::memory_order_relaxed)); }
+uint64_t Histogram::count() const { return count_.load(std::memory_order_relaxed); }
+
+SampleRing::SampleRing(size_t capacity) : cap_(capacity ? capacity : 1) {}
+
+void SampleRing::add(double v) {
+  std::lock_guard<std::mutex> lk(mu_);
+  ++total_;
+  if (buf_.size() < cap_) {
+    buf_.push_back(v);
+  } else {
+    buf_[next_] = v;
+    next_ = (next_ + 1) % buf_.size();
+  }
+}
+
+std::vector<double> SampleRing::snapshot() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return buf_;
+}
+
+void SampleRing::clear() {
+  std::lock_guard<std::mutex> lk(mu_);
+  buf_.clear();
+  next_ = 0;
+  total_ = 0;
+}
+
+uint64_t SampleRing::total() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return total_;
+}
+
+double quantile(std::vector<double> v, double q) {
+  if (v.empty()) return std::nan("");
+  std::sort(v.begin(), v.end());
+  // nearest-rank
+  double rank = std::ceil(q * static_cast<double>(v.size()));
+  size_t idx = rank < 1 ? 0 : static_cast<size_t>(rank) - 1;
+  if (idx >= v.size()) idx = v.size() - 1;
+  return v[idx];
+}
+
+std::vector<double> default_latency_buckets() {
+  std::vector<double> b;
+  double x = 50e-6;
+  while (x < 30.0) {
+    b.push_back(x);
+    x *= 1.5;
+  }
+  b.push_back(30.0);
+  return b;
+}
+
+Registry& Registry::global() {
+  static Registry* r = new Registry();
+  return *r;
+}
+
+std::string render_labels(const Labels& labels, const std::string& extra_key, const std::string& extra_val) {
+  if (labels.empty() && extra_key.empty()) return "";
+  std::string out = "{";
+  bool first = true;
+  auto add = [&](const std::string& k, const std::string& v) {
+    if (!first) out += ",";
+    first = false;
+    out += k + "=\"";
+    for (char c : v) {
+      if (c == '\\' || c == '"') out.push_back('\\');
+      if (c == '\n') {
+        out += "\\n";
+        continue;
+      }
+      out.push_back(c);
+    }
+    out += "\"";
+  };
+  for (auto& kv : labels) add(kv.first, kv.second);
+  if (!extra_key.empty()) add(extra_key, extra_val);
+  return out + "}";
+}
+
+Counter& Registry::counter(const std::string& name, const std::string& help, const Labels& labels) {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto& f = families_[name];
+  f.type = "counter";
+  f.help = help;
+  auto& slot = f.counters[render_labels(labels)];
+  if (!slot) slot = std::make_unique<Counter>();
+  return *slot;
+}
+
+Gauge& Registry::gauge(const std::string& name, const std::string& help, const Labels& labels) {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto& f = families_[name];
+  f.type = "gauge";
+  f.help = help;
+  auto& slot = f.gauges[render_labels(labels)];
+  if (!slot) slot = std::make_unique<Gauge>();
+  return *slot;
+}
+
+Histogram& Registry::histogram(const std::string& name, const std::string& help, const Labels& labels,
+                               std::vector<double> buckets) {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto& f = families_[name];
+  f.type = "histogram";
+  f.help = help;
+  auto& slot = f.histograms[render_labels(labels)];
+  if (!slot) slot = std::make_unique<Histogram>(std::move(buckets));
+  return *slot;
+}
+
+SampleRing& Registry::samples(const std::string& name) {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto& slot = samples_[name];
+  if (!slot) slot = std::make_unique<SampleRing>();
+  return *slot;
+}
+
+std::string Registry::render() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  std::string out;
+  for (const auto& [name, f] : families_) {
+    out += "# HELP " + name + " " + f.help + "\n";
+    out += "# TYPE " + name + " " + f.type + "\n";
+    for (const auto& [lbl, c] : f.counters) out += name + lbl + " " + fmt_double(c->value()) + "\n";
+    for (const auto& [lbl, g] : f.gauges) out += name + lbl + " " + fmt_double(g->value()) + "\n";
+    for (const auto& [lbl, h] : f.histograms) {
+      // re-open label set to add `le`
+      std::string base = lbl.empty() ? "" : lbl.substr(1, lbl.size() - 2);
+      auto counts = h->bucket_counts();
+      uint64_t cum = 0;
+      for (size_t i = 0; i < h->buckets().size(); ++i) {
+        cum += counts[i];
+        out += name + "_bucket{" + base + (base.empty() ? "" : ",") + "le=\"" + fmt_double(h->buckets()[i]) +
+               "\"} " + std::to_string(cum) + "\n";
+      }
+      cum += counts.back();
+      out += name + "_bucket{" + base + (base.empty() ? "" : ",") + "le=\"+Inf\"} " + std::to_string(cum) + "\n";
+      out += name + "_sum" + lbl + " " + fmt_double(h->sum()) + "\n";
+      out += name + "_count" + lbl + " " + std::to_string(h->count()) + "\n";
+    }
+  }
+  return out;
+}
+
+std::vector<std::string> Registry::sample_names() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  std::vector<std::string> out;
+  for (auto& kv : samples_) out.push_back(kv.first);
+  return out;
+}
+
+std::string Registry::render_samples_json(const std::string& name) const {
+  const SampleRing* ring = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = samples_.find(name);
+    if (it != samples_.end()) ring = it->second.get();
+  }
+  json::Value out = json::Value::object();
+  out["name"] = name;
+  json::Value arr = json::Value::array();
+  uint64_t total = 0;
+  if (ring) {
+    for (double d : ring->snapshot()) arr.push_back(d);
+    total = ring->total();
+  }
+  out["total"] = static_cast<unsigned long long>(total);
+  out["samples"] = std::move(arr);
+  return out.dump();
+}
+
+Timer::Timer(Histogram* h, SampleRing* s) : h_(h), s_(s), start_ns_(now_ns()) {}
+Timer::~Timer() {
+  double e = elapsed();
+  if (h_) h_->observe(e);
+  if (s_) s_->add(e);
+}
+double Timer::elapsed() const { return static_cast<double>(now_ns() - start_ns_) * 1e-9; }
+
+}  // namespace bgc::metrics

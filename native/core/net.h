@@ -1,0 +1,103 @@
+// Sockets and TLS streams (OpenSSL 3).
+//
+// Replaces hyper/rustls (clients) and axum-server's `tls_rustls` (webhook server with
+// live certificate reload, reference src/admission.rs:104-126,141,174).
+#pragma once
+
+#include <openssl/ssl.h>
+
+#include <atomic>
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <sys/types.h>
+
+namespace bgc::net {
+
+class NetError : public std::runtime_error {
+ public:
+  using std::runtime_error::runtime_error;
+};
+
+class Stream {
+ public:
+  virtual ~Stream() = default;
+  // Returns bytes read, 0 on orderly EOF, -1 on error, -2 on timeout.
+  virtual ssize_t read_some(char* buf, size_t n, int timeout_ms) = 0;
+  virtual bool write_all(const char* buf, size_t n) = 0;
+  // Unblocks readers from another thread.
+  virtual void shutdown() = 0;
+  virtual int fd() const = 0;
+  virtual bool has_buffered() const { return false; }
+  bool write_all(const std::string& s) { return write_all(s.data(), s.size()); }
+};
+
+class TcpStream : public Stream {
+ public:
+  explicit TcpStream(int fd) : fd_(fd) {}
+  ~TcpStream() override;
+  ssize_t read_some(char* buf, size_t n, int timeout_ms) override;
+  bool write_all(const char* buf, size_t n) override;
+  void shutdown() override;
+  int fd() const override { return fd_; }
+
+ private:
+  int fd_;
+};
+
+// Shared SSL_CTX holder whose context can be swapped atomically (hot reload): new
+// connections pick up the new certificate, established ones keep the old context.
+class TlsContext {
+ public:
+  static std::shared_ptr<TlsContext> server_from_files(const std::string& cert_path,
+                                                       const std::string& key_path);
+  static std::shared_ptr<TlsContext> server_from_pem(const std::string& cert_pem,
+                                                     const std::string& key_pem);
+  // ca_pem empty + insecure=false => system roots (with_native_roots).
+  static std::shared_ptr<TlsContext> client(const std::string& ca_pem, bool insecure,
+                                            const std::string& client_cert_pem = "",
+                                            const std::string& client_key_pem = "");
+
+  void reload_from_files(const std::string& cert_path, const std::string& key_path);
+  std::shared_ptr<SSL_CTX> get() const;
+  bool is_server() const { return server_; }
+  bool insecure() const { return insecure_; }
+
+ private:
+  mutable std::mutex mu_;
+  std::shared_ptr<SSL_CTX> ctx_;
+  bool server_ = false;
+  bool insecure_ = false;
+};
+
+class TlsStream : public Stream {
+ public:
+  // Takes ownership of fd. Performs the handshake; throws NetError on failure.
+  TlsStream(int fd, std::shared_ptr<SSL_CTX> ctx, bool server, const std::string& verify_host,
+            bool verify_peer, int timeout_ms);
+  ~TlsStream() override;
+  ssize_t read_some(char* buf, size_t n, int timeout_ms) override;
+  bool write_all(const char* buf, size_t n) override;
+  void shutdown() override;
+  int fd() const override { return fd_; }
+  bool has_buffered() const override;
+
+ private:
+  int fd_;
+  std::shared_ptr<SSL_CTX> ctx_;
+  SSL* ssl_ = nullptr;
+  std::mutex write_mu_;
+};
+
+// Resolves and connects (IPv4/IPv6); throws NetError.
+int connect_tcp(const std::string& host, uint16_t port, int timeout_ms);
+// Listens; port 0 picks an ephemeral port (returned through bound_port).
+int listen_tcp(const std::string& addr, uint16_t port, int backlog, uint16_t* bound_port);
+
+std::string ssl_errors();
+std::string read_file(const std::string& path);
+void write_file(const std::string& path, const std::string& data);
+
+}  // namespace bgc::net

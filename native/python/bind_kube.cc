@@ -1,0 +1,5 @@
+#include <pybind11/pybind11.h>
+namespace py = pybind11;
+namespace bgc_py {
+void register_kube(py::module_& m) {}
+}  // namespace bgc_py

@@ -1,0 +1,130 @@
+// pybind11 surface of the native core: used by the pytest suite (unit tests of every
+// C++ component) and by the bench harness (native churn driver).
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "core/crypto.h"
+#include "core/env_config.h"
+#include "core/json.h"
+#include "core/json_patch.h"
+#include "core/yaml.h"
+#include "crd/schema.h"
+
+namespace py = pybind11;
+using bgc::json::Value;
+
+namespace bgc_py {
+void register_admission(py::module_& m);
+void register_sync(py::module_& m);
+void register_kube(py::module_& m);
+void register_gpu(py::module_& m);
+}  // namespace bgc_py
+
+namespace {
+
+// JSON text is the interchange format with Python: json.loads/dumps on the Python side.
+std::string yaml_to_json(const std::string& y) { return bgc::yaml::parse(y).dump(); }
+std::string json_to_yaml(const std::string& j) { return bgc::yaml::emit(bgc::json::parse(j)); }
+
+std::string json_roundtrip(const std::string& j) { return bgc::json::parse(j).dump(); }
+
+std::string apply_json_patch(const std::string& doc, const std::string& patch) {
+  Value d = bgc::json::parse(doc);
+  bgc::json::apply_patch(d, bgc::json::parse(patch));
+  return d.dump();
+}
+
+std::string apply_merge_patch(const std::string& doc, const std::string& patch) {
+  Value d = bgc::json::parse(doc);
+  bgc::json::apply_merge_patch(d, bgc::json::parse(patch));
+  return d.dump();
+}
+
+py::dict env_config(const std::map<std::string, std::string>& env, const std::string& kind) {
+  bgc::EnvConfig c("CONF_", env);
+  py::dict d;
+  d["listen_addr"] = c.str("listen_addr");
+  d["listen_port"] = c.u16("listen_port");
+  if (kind == "admission") {
+    d["cert_path"] = c.str("cert_path");
+    d["key_path"] = c.str("key_path");
+    d["oidc_username_prefix"] = c.str("oidc_username_prefix");
+    d["default_role_name"] = c.str("default_role_name");
+    d["authorized_group_names"] = c.comma_list("authorized_group_names");
+  } else if (kind == "synchronizer") {
+    d["google_service_account_json_path"] = c.str("google_service_account_json_path");
+    d["google_file_id"] = c.str("google_file_id");
+    d["sync_interval_secs"] = c.u64_or("sync_interval_secs", 60);
+    d["gpu_server_name"] = c.str("gpu_server_name");
+  }
+  return d;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_native, m) {
+  m.doc() = "bacchus-gpu-controller (MI355X-native) C++ core bindings";
+
+  py::register_exception<bgc::json::ParseError>(m, "JsonParseError", PyExc_ValueError);
+  py::register_exception<bgc::json::PatchError>(m, "JsonPatchError", PyExc_ValueError);
+  py::register_exception<bgc::yaml::Error>(m, "YamlError", PyExc_ValueError);
+  py::register_exception<bgc::ConfigError>(m, "ConfigError", PyExc_ValueError);
+
+  m.def("json_roundtrip", &json_roundtrip);
+  m.def("yaml_to_json", &yaml_to_json);
+  m.def("json_to_yaml", &json_to_yaml);
+  m.def("apply_json_patch", &apply_json_patch);
+  m.def("apply_merge_patch", &apply_merge_patch);
+
+  m.def("sha256_hex", [](py::bytes b) { return bgc::crypto::sha256_hex(std::string(b)); });
+  m.def("base64_encode", [](py::bytes b, bool url, bool pad) { return bgc::crypto::base64_encode(std::string(b), url, pad); },
+        py::arg("data"), py::arg("url") = false, py::arg("pad") = true);
+  m.def("base64_decode", [](const std::string& s) { return py::bytes(bgc::crypto::base64_decode(s)); });
+  m.def("jwt_rs256", &bgc::crypto::jwt_rs256);
+  m.def("rs256_verify", [](const std::string& pem, const std::string& data, py::bytes sig) {
+    return bgc::crypto::rs256_verify(pem, data, std::string(sig));
+  });
+  m.def("generate_rsa", [](int bits) {
+    auto k = bgc::crypto::generate_rsa(bits);
+    return py::make_tuple(k.private_key_pem, k.public_key_pem);
+  }, py::arg("bits") = 2048);
+  m.def("make_ca_and_leaf", [](const std::string& cn, const std::vector<std::string>& dns, int days) {
+    auto b = bgc::crypto::make_ca_and_leaf(cn, dns, days);
+    py::dict d;
+    d["ca_cert"] = b.ca_cert_pem;
+    d["ca_key"] = b.ca_key_pem;
+    d["cert"] = b.cert_pem;
+    d["key"] = b.key_pem;
+    return d;
+  }, py::arg("common_name"), py::arg("dns_names"), py::arg("valid_days") = 90);
+  m.def("uuid_v4", &bgc::crypto::uuid_v4);
+
+  m.def("env_config", &env_config, py::arg("env"), py::arg("kind"));
+
+  m.def("crd_yaml", &bgc::crd::crd_yaml);
+  m.def("crd_json", [] { return bgc::crd::userbootstrap_crd().dump(); });
+  m.def("ub_schema_json", [] { return bgc::crd::userbootstrap_schema().dump(); });
+  m.def("validate_ub", [](const std::string& obj) {
+    std::vector<py::tuple> out;
+    for (auto& e : bgc::crd::validate(bgc::json::parse(obj), bgc::crd::userbootstrap_schema())) {
+      out.push_back(py::make_tuple(e.path, e.kind, e.detail));
+    }
+    return out;
+  });
+  m.def("parse_userbootstrap", [](const std::string& obj) {
+    auto ub = bgc::crd::parse_userbootstrap(bgc::json::parse(obj));
+    py::dict d;
+    d["name"] = ub.name;
+    d["kube_username"] = ub.has_kube_username ? py::object(py::str(ub.kube_username)) : py::object(py::none());
+    d["has_quota"] = ub.has_quota;
+    d["has_role"] = ub.has_role;
+    d["has_rolebinding"] = ub.has_rolebinding;
+    d["synchronized_with_sheet"] = ub.synchronized_with_sheet;
+    return d;
+  });
+
+  bgc_py::register_admission(m);
+  bgc_py::register_sync(m);
+  bgc_py::register_kube(m);
+  bgc_py::register_gpu(m);
+}
