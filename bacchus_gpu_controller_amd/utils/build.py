@@ -2,7 +2,7 @@
 
 * C++ core, binaries and the pybind11 module: CMake + Ninja into ``build/`` (binaries
   land in ``bin/``, ``_native*.so`` next to this package).
-* HIP/CDNA4 kernels: ``hipcc --offload-arch=gfx950`` into ``_gpu_ops*.so`` (see
+* HIP/CDNA4 kernels: ``hipcc --offload-arch=gfx950`` into ``libbgc_gpu_diag.so`` (see
   ``native/gpu/hip/``).  hipcc cross-compiles without a GPU.
 
 Everything is built in-tree so the artefacts travel with the repo snapshot to the GPU box.
@@ -40,29 +40,31 @@ def hip_sources():
     return sorted(glob.glob(os.path.join(HIP_DIR, "*.hip")) + glob.glob(os.path.join(HIP_DIR, "*.cc")))
 
 
-def gpu_ops_path():
-    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
-    return os.path.join(PKG_DIR, "_gpu_ops" + suffix)
+def gpu_diag_path():
+    return os.path.join(PKG_DIR, "libbgc_gpu_diag.so")
 
 
 def build_hip(force=False):
-    """Compile the HIP health-diagnostic kernels + their pybind11 bindings for gfx950."""
+    """Compile the HIP/CDNA4 health-diagnostic kernels (C ABI) for gfx950.
+
+    The library is dlopen()ed by the node agent and by ``_native`` (native/gpu/diag.cc).
+    ``-amdgpu-mfma-vgpr-form`` keeps MFMA accumulators in the unified VGPR file on gfx950,
+    which removes the AGPR shuffles hipcc otherwise emits around the throughput loop.
+    """
     srcs = hip_sources()
     if not srcs:
         return None
-    out = gpu_ops_path()
+    out = gpu_diag_path()
     if not force and os.path.exists(out):
         newest = max(os.path.getmtime(s) for s in srcs + glob.glob(os.path.join(HIP_DIR, "*.h")))
         if os.path.getmtime(out) >= newest:
             return out
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
-    import pybind11
-
-    inc = [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}",
-           f"-I{os.path.join(REPO_ROOT, 'native')}"]
     cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wno-unused-result", *inc, *srcs, "-o", out]
+           "-mllvm", "-amdgpu-mfma-vgpr-form=1", "-Wno-unused-result",
+           f"-I{HIP_DIR}", *srcs, "-o", out + ".tmp"]
     _run(cmd)
+    os.replace(out + ".tmp", out)
     return out
 
 

@@ -1,0 +1,52 @@
+#include "core/roctx.h"
+
+#include <dlfcn.h>
+
+#include <mutex>
+
+namespace bgc::roctx {
+
+namespace {
+
+using PushFn = int (*)(const char*);
+using PopFn = int (*)();
+using MarkFn = void (*)(const char*);
+
+struct Api {
+  PushFn push = nullptr;
+  PopFn pop = nullptr;
+  MarkFn mark = nullptr;
+};
+
+const Api& api() {
+  static Api a;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    const char* libs[] = {"librocprofiler-sdk-roctx.so.1", "librocprofiler-sdk-roctx.so",
+                          "/opt/rocm/lib/librocprofiler-sdk-roctx.so.1"};
+    for (const char* l : libs) {
+      void* h = dlopen(l, RTLD_NOW | RTLD_LOCAL);
+      if (!h) continue;
+      a.push = reinterpret_cast<PushFn>(dlsym(h, "roctxRangePushA"));
+      a.pop = reinterpret_cast<PopFn>(dlsym(h, "roctxRangePop"));
+      a.mark = reinterpret_cast<MarkFn>(dlsym(h, "roctxMarkA"));
+      if (a.push && a.pop) break;
+    }
+  });
+  return a;
+}
+
+}  // namespace
+
+void push(const char* name) {
+  if (auto f = api().push) f(name);
+}
+void pop() {
+  if (auto f = api().pop) f();
+}
+void mark(const char* name) {
+  if (auto f = api().mark) f(name);
+}
+bool available() { return api().push != nullptr; }
+
+}  // namespace bgc::roctx

@@ -1,0 +1,55 @@
+// C ABI of the MI355X (gfx950) health-diagnostic kernels (libbgc_gpu_diag.so).
+//
+// The reference has no GPU code; these kernels implement the north
+// star's "GPU discovery, health" for the node agent: before a GPU is advertised as
+// schedulable `amd.com/gpu`, its HBM3E is pattern-tested at streaming bandwidth and
+// every CU's matrix cores are checked with exact-integer MFMA tiles.  The library is
+// dlopen()ed by the node agent and by the Python bindings so CPU-only hosts never need
+// a HIP runtime.
+#pragma once
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BGC_DIAG_ABI_VERSION 1
+#define BGC_DIAG_MAX_CU_KEYS 2048
+
+typedef struct {
+  uint64_t bytes;          // buffer size tested
+  int iters;               // timed iterations per phase
+  double write_gbps;       // pattern fill (store-only)
+  double read_gbps;        // verify pass (load-only, compare in registers)
+  double copy_gbps;        // device-to-device copy kernel (load+store bytes)
+  uint64_t mismatches;     // words that failed the pattern check
+  uint64_t first_bad_word; // index of the first failing word (UINT64_MAX if none)
+  double elapsed_ms;
+} bgc_hbm_result;
+
+typedef struct {
+  uint64_t tiles_checked;   // 16x16x32 bf16 MFMA tiles verified element-wise
+  uint64_t mismatches;      // output elements that differed from the exact result
+  int cus_seen;             // distinct (XCC, SE, SH, CU) that executed the test
+  int bad_cus;              // CUs with >= 1 mismatch
+  int xccs_seen;            // distinct XCC ids
+  double tflops;            // dense bf16 MFMA rate of the throughput phase
+  int throughput_ok;        // throughput phase accumulators matched exactly
+  double elapsed_ms;
+  int bad_cu_keys[64];      // first bad CU keys (xcc<<8 | se<<5 | sh<<4 | cu)
+} bgc_mfma_result;
+
+int bgc_diag_abi_version(void);
+int bgc_diag_device_count(void);
+// Returns 0 on success, non-zero on HIP error (message via bgc_diag_last_error()).
+int bgc_diag_hbm(int device, uint64_t bytes, int iters, uint32_t seed, bgc_hbm_result* out);
+int bgc_diag_mfma(int device, int waves_per_cu, int throughput_iters, uint32_t seed, bgc_mfma_result* out);
+// Device name / gfx arch string, e.g. "gfx950".
+int bgc_diag_device_arch(int device, char* buf, size_t len);
+const char* bgc_diag_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif

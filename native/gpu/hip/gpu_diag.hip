@@ -1,0 +1,386 @@
+// MI355X (gfx950 / CDNA4) GPU health diagnostics: HBM3E pattern + bandwidth test and a
+// per-CU MFMA functional/throughput test.  See gpu_diag.h for the C ABI.
+//
+// Design notes (CDNA4, see /opt/skills/guides):
+//  * HBM phases are pure streams: 16 B per lane (global_load/store_dwordx4), 256-thread
+//    blocks, 8 blocks per CU (2048 WGs >> 256 CUs), 4 independent 16 B accesses in
+//    flight per lane so each CU keeps ~128 KiB outstanding; nontemporal hints since
+//    every byte is touched exactly once per pass.  Buffers default to 2 GiB each, far
+//    past the 256 MiB Infinity Cache, so the numbers are HBM numbers.
+//  * The MFMA test runs one v_mfma_f32_16x16x32_bf16 tile per wave per round with
+//    operands in {-1,0,1} generated from a hash in registers (no memory traffic), so
+//    every product sum is an exact fp32 integer and is checked element-wise against a
+//    VALU recomputation.  Each wave records its physical CU (HW_REG_XCC_ID + HW_ID),
+//    so a faulty matrix core is attributed to (XCC, SE, SH, CU).
+//  * The throughput phase chains 4 independent accumulators per wave (dependent MFMA
+//    latency hidden by 8 waves/SIMD) and verifies acc == iters * tile exactly.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "gpu_diag.h"
+
+namespace {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kBlock = 256;
+constexpr int kUnroll = 4;
+
+thread_local std::string g_last_error;
+
+__host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+
+__device__ __forceinline__ u32x4 pattern16(uint64_t i, uint32_t seed) {
+  uint32_t w = static_cast<uint32_t>(i << 2) ^ static_cast<uint32_t>(i >> 30) * 0x9e3779b9U;
+  u32x4 v;
+  v.x = mix32(w ^ seed);
+  v.y = mix32((w + 1) ^ seed);
+  v.z = mix32((w + 2) ^ seed);
+  v.w = mix32((w + 3) ^ seed);
+  return v;
+}
+
+__global__ __launch_bounds__(kBlock) void hbm_fill(u32x4* __restrict__ buf, uint64_t n16, uint32_t seed) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kBlock;
+  for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; base < n16; base += stride * kUnroll) {
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      uint64_t i = base + u * stride;
+      if (i < n16) __builtin_nontemporal_store(pattern16(i, seed), &buf[i]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void hbm_copy(const u32x4* __restrict__ src, u32x4* __restrict__ dst, uint64_t n16) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kBlock;
+  for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; base < n16; base += stride * kUnroll) {
+    u32x4 v[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      uint64_t i = base + u * stride;
+      if (i < n16) v[u] = __builtin_nontemporal_load(&src[i]);
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      uint64_t i = base + u * stride;
+      if (i < n16) __builtin_nontemporal_store(v[u], &dst[i]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void hbm_check(const u32x4* __restrict__ buf, uint64_t n16, uint32_t seed,
+                                                    unsigned long long* __restrict__ bad,
+                                                    unsigned long long* __restrict__ first_bad) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kBlock;
+  unsigned long long local_bad = 0;
+  unsigned long long local_first = ~0ULL;
+  for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; base < n16; base += stride * kUnroll) {
+    u32x4 v[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      uint64_t i = base + u * stride;
+      if (i < n16) v[u] = __builtin_nontemporal_load(&buf[i]);
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      uint64_t i = base + u * stride;
+      if (i < n16) {
+        u32x4 e = pattern16(i, seed);
+        int nb = (v[u].x != e.x) + (v[u].y != e.y) + (v[u].z != e.z) + (v[u].w != e.w);
+        if (nb) {
+          local_bad += nb;
+          local_first = std::min<unsigned long long>(local_first, i * 4);
+        }
+      }
+    }
+  }
+  if (local_bad) {
+    atomicAdd(bad, local_bad);
+    atomicMin(first_bad, local_first);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// MFMA
+
+__device__ __forceinline__ int operand(uint32_t seed, uint32_t tile, int r, int c, uint32_t which) {
+  uint32_t h = mix32(seed ^ mix32(tile * 0x9e3779b9U + which) ^ static_cast<uint32_t>(r * 64 + c));
+  return static_cast<int>(h % 3u) - 1;
+}
+
+__device__ __forceinline__ uint32_t cu_key() {
+  uint32_t xcc, hwid;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+  uint32_t cu = (hwid >> 8) & 0xF;
+  uint32_t sh = (hwid >> 12) & 0x1;
+  uint32_t se = (hwid >> 13) & 0x7;
+  return ((xcc & 0x7) << 8) | (se << 5) | (sh << 4) | cu;
+}
+
+// One wave = one 16x16x32 tile per round. A is 16x32, B is 32x16.
+__global__ __launch_bounds__(kBlock) void mfma_check(uint32_t seed, int rounds, unsigned* __restrict__ cu_tiles,
+                                                     unsigned* __restrict__ cu_bad) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = (blockIdx.x * (kBlock / 64)) + (threadIdx.x >> 6);
+  const uint32_t key = cu_key();
+  unsigned bad = 0;
+  for (int r = 0; r < rounds; ++r) {
+    const uint32_t tile = wave * static_cast<uint32_t>(rounds) + static_cast<uint32_t>(r);
+    bf16x8 a, b;
+    const int row = lane & 15;
+    const int kb = 8 * (lane >> 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      a[j] = static_cast<__bf16>(static_cast<float>(operand(seed, tile, row, kb + j, 0xA)));
+      b[j] = static_cast<__bf16>(static_cast<float>(operand(seed, tile, kb + j, row, 0xB)));
+    }
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+    const int col = lane & 15;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int orow = (lane >> 4) * 4 + i;
+      int expect = 0;
+      for (int k = 0; k < 32; ++k) expect += operand(seed, tile, orow, k, 0xA) * operand(seed, tile, k, col, 0xB);
+      bad += (acc[i] != static_cast<float>(expect));
+    }
+  }
+  // one atomic per wave (lane 0 after a wave reduction)
+  for (int off = 32; off > 0; off >>= 1) bad += __shfl_down(bad, off, 64);
+  if (lane == 0) {
+    atomicAdd(&cu_tiles[key], static_cast<unsigned>(rounds));
+    if (bad) atomicAdd(&cu_bad[key], bad);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void mfma_throughput(uint32_t seed, int iters, unsigned* __restrict__ fails) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t tile = (blockIdx.x * (kBlock / 64)) + (threadIdx.x >> 6);
+  const int row = lane & 15;
+  const int kb = 8 * (lane >> 4);
+  bf16x8 a, b;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    a[j] = static_cast<__bf16>(static_cast<float>(operand(seed, tile, row, kb + j, 0xA)));
+    b[j] = static_cast<__bf16>(static_cast<float>(operand(seed, tile, kb + j, row, 0xB)));
+  }
+  // Distinct initial values keep the compiler from merging the four chains.
+  f32x4 acc[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) acc[c] = f32x4{float(c), float(c), float(c), float(c)};
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[c], 0, 0, 0);
+  }
+  const int col = lane & 15;
+  unsigned bad = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int orow = (lane >> 4) * 4 + i;
+    int expect = 0;
+    for (int k = 0; k < 32; ++k) expect += operand(seed, tile, orow, k, 0xA) * operand(seed, tile, k, col, 0xB);
+    const float e = static_cast<float>(expect) * static_cast<float>(iters);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) bad += (acc[c][i] != e + float(c));
+  }
+  for (int off = 32; off > 0; off >>= 1) bad += __shfl_down(bad, off, 64);
+  if (lane == 0 && bad) atomicAdd(fails, bad);
+}
+
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess) {                                                             \
+      g_last_error = std::string(#expr) + ": " + hipGetErrorString(_e);                 \
+      return 1;                                                                         \
+    }                                                                                   \
+  } while (0)
+
+int cu_count(int device) {
+  int n = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n <= 0) n = 256;
+  return n;
+}
+
+struct DeviceBuffer {
+  void* p = nullptr;
+  ~DeviceBuffer() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+struct Events {
+  hipEvent_t a = nullptr, b = nullptr;
+  ~Events() {
+    if (a) (void)hipEventDestroy(a);
+    if (b) (void)hipEventDestroy(b);
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+int bgc_diag_abi_version(void) { return BGC_DIAG_ABI_VERSION; }
+
+const char* bgc_diag_last_error(void) { return g_last_error.c_str(); }
+
+int bgc_diag_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int bgc_diag_device_arch(int device, char* buf, size_t len) {
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  std::snprintf(buf, len, "%s", prop.gcnArchName);
+  return 0;
+}
+
+int bgc_diag_hbm(int device, uint64_t bytes, int iters, uint32_t seed, bgc_hbm_result* out) {
+  if (!out || iters <= 0 || bytes < (1u << 20)) {
+    g_last_error = "invalid arguments";
+    return 1;
+  }
+  std::memset(out, 0, sizeof(*out));
+  bytes &= ~static_cast<uint64_t>(15);
+  const uint64_t n16 = bytes / 16;
+  HIP_TRY(hipSetDevice(device));
+  DeviceBuffer a, b, counters;
+  HIP_TRY(hipMalloc(&a.p, bytes));
+  HIP_TRY(hipMalloc(&b.p, bytes));
+  HIP_TRY(hipMalloc(&counters.p, 2 * sizeof(unsigned long long)));
+  auto* bad = static_cast<unsigned long long*>(counters.p);
+  unsigned long long init[2] = {0ULL, ~0ULL};
+  HIP_TRY(hipMemcpy(bad, init, sizeof(init), hipMemcpyHostToDevice));
+  const int grid = cu_count(device) * 8;
+  Events ev;
+  HIP_TRY(hipEventCreate(&ev.a));
+  HIP_TRY(hipEventCreate(&ev.b));
+  auto t0 = hipEventRecord(ev.a, nullptr);
+  (void)t0;
+  float best_fill = 1e30f, best_copy = 1e30f, best_check = 1e30f, ms = 0.f;
+  float total = 0.f;
+  // warm-up (also first-touch of the pages)
+  hipLaunchKernelGGL(hbm_fill, dim3(grid), dim3(kBlock), 0, nullptr, static_cast<u32x4*>(a.p), n16, seed);
+  HIP_TRY(hipGetLastError());
+  for (int it = 0; it < iters; ++it) {
+    HIP_TRY(hipEventRecord(ev.a, nullptr));
+    hipLaunchKernelGGL(hbm_fill, dim3(grid), dim3(kBlock), 0, nullptr, static_cast<u32x4*>(a.p), n16, seed);
+    HIP_TRY(hipEventRecord(ev.b, nullptr));
+    HIP_TRY(hipEventSynchronize(ev.b));
+    HIP_TRY(hipEventElapsedTime(&ms, ev.a, ev.b));
+    best_fill = std::min(best_fill, ms);
+    total += ms;
+    HIP_TRY(hipEventRecord(ev.a, nullptr));
+    hipLaunchKernelGGL(hbm_copy, dim3(grid), dim3(kBlock), 0, nullptr, static_cast<const u32x4*>(a.p),
+                       static_cast<u32x4*>(b.p), n16);
+    HIP_TRY(hipEventRecord(ev.b, nullptr));
+    HIP_TRY(hipEventSynchronize(ev.b));
+    HIP_TRY(hipEventElapsedTime(&ms, ev.a, ev.b));
+    best_copy = std::min(best_copy, ms);
+    total += ms;
+    HIP_TRY(hipEventRecord(ev.a, nullptr));
+    hipLaunchKernelGGL(hbm_check, dim3(grid), dim3(kBlock), 0, nullptr, static_cast<const u32x4*>(b.p), n16, seed,
+                       bad, bad + 1);
+    HIP_TRY(hipEventRecord(ev.b, nullptr));
+    HIP_TRY(hipEventSynchronize(ev.b));
+    HIP_TRY(hipEventElapsedTime(&ms, ev.a, ev.b));
+    best_check = std::min(best_check, ms);
+    total += ms;
+  }
+  HIP_TRY(hipGetLastError());
+  unsigned long long res[2];
+  HIP_TRY(hipMemcpy(res, bad, sizeof(res), hipMemcpyDeviceToHost));
+  out->bytes = bytes;
+  out->iters = iters;
+  out->write_gbps = static_cast<double>(bytes) / (best_fill * 1e-3) / 1e9;
+  out->copy_gbps = 2.0 * static_cast<double>(bytes) / (best_copy * 1e-3) / 1e9;
+  out->read_gbps = static_cast<double>(bytes) / (best_check * 1e-3) / 1e9;
+  out->mismatches = res[0];
+  out->first_bad_word = res[1];
+  out->elapsed_ms = total;
+  return 0;
+}
+
+int bgc_diag_mfma(int device, int waves_per_cu, int throughput_iters, uint32_t seed, bgc_mfma_result* out) {
+  if (!out || waves_per_cu <= 0 || throughput_iters <= 0 || throughput_iters > (1 << 18)) {
+    g_last_error = "invalid arguments";
+    return 1;
+  }
+  std::memset(out, 0, sizeof(*out));
+  HIP_TRY(hipSetDevice(device));
+  const int cus = cu_count(device);
+  const int blocks = std::max(1, cus * waves_per_cu / (kBlock / 64));
+  const int rounds = 8;
+  DeviceBuffer tiles, bad, fails;
+  HIP_TRY(hipMalloc(&tiles.p, BGC_DIAG_MAX_CU_KEYS * sizeof(unsigned)));
+  HIP_TRY(hipMalloc(&bad.p, BGC_DIAG_MAX_CU_KEYS * sizeof(unsigned)));
+  HIP_TRY(hipMalloc(&fails.p, sizeof(unsigned)));
+  HIP_TRY(hipMemset(tiles.p, 0, BGC_DIAG_MAX_CU_KEYS * sizeof(unsigned)));
+  HIP_TRY(hipMemset(bad.p, 0, BGC_DIAG_MAX_CU_KEYS * sizeof(unsigned)));
+  HIP_TRY(hipMemset(fails.p, 0, sizeof(unsigned)));
+  Events ev;
+  HIP_TRY(hipEventCreate(&ev.a));
+  HIP_TRY(hipEventCreate(&ev.b));
+  float ms_check = 0.f, ms_tp = 0.f;
+  HIP_TRY(hipEventRecord(ev.a, nullptr));
+  hipLaunchKernelGGL(mfma_check, dim3(blocks), dim3(kBlock), 0, nullptr, seed, rounds,
+                     static_cast<unsigned*>(tiles.p), static_cast<unsigned*>(bad.p));
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(ev.b, nullptr));
+  HIP_TRY(hipEventSynchronize(ev.b));
+  HIP_TRY(hipEventElapsedTime(&ms_check, ev.a, ev.b));
+  // warm-up then timed throughput pass
+  hipLaunchKernelGGL(mfma_throughput, dim3(blocks), dim3(kBlock), 0, nullptr, seed, 64, static_cast<unsigned*>(fails.p));
+  HIP_TRY(hipMemset(fails.p, 0, sizeof(unsigned)));
+  HIP_TRY(hipEventRecord(ev.a, nullptr));
+  hipLaunchKernelGGL(mfma_throughput, dim3(blocks), dim3(kBlock), 0, nullptr, seed, throughput_iters,
+                     static_cast<unsigned*>(fails.p));
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(ev.b, nullptr));
+  HIP_TRY(hipEventSynchronize(ev.b));
+  HIP_TRY(hipEventElapsedTime(&ms_tp, ev.a, ev.b));
+  std::vector<unsigned> h_tiles(BGC_DIAG_MAX_CU_KEYS), h_bad(BGC_DIAG_MAX_CU_KEYS);
+  unsigned h_fails = 0;
+  HIP_TRY(hipMemcpy(h_tiles.data(), tiles.p, h_tiles.size() * sizeof(unsigned), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(h_bad.data(), bad.p, h_bad.size() * sizeof(unsigned), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(&h_fails, fails.p, sizeof(unsigned), hipMemcpyDeviceToHost));
+  bool xcc_seen[8] = {false};
+  for (int k = 0; k < BGC_DIAG_MAX_CU_KEYS; ++k) {
+    if (!h_tiles[static_cast<size_t>(k)]) continue;
+    out->cus_seen++;
+    out->tiles_checked += h_tiles[static_cast<size_t>(k)];
+    xcc_seen[(k >> 8) & 7] = true;
+    if (h_bad[static_cast<size_t>(k)]) {
+      out->mismatches += h_bad[static_cast<size_t>(k)];
+      if (out->bad_cus < 64) out->bad_cu_keys[out->bad_cus] = k;
+      out->bad_cus++;
+    }
+  }
+  for (bool s : xcc_seen) out->xccs_seen += s ? 1 : 0;
+  const double waves = static_cast<double>(blocks) * (kBlock / 64);
+  const double flops = waves * throughput_iters * 4.0 * (2.0 * 16 * 16 * 32);
+  out->tflops = flops / (ms_tp * 1e-3) / 1e12;
+  out->throughput_ok = h_fails == 0;
+  out->elapsed_ms = ms_check + ms_tp;
+  return 0;
+}
+
+}  // extern "C"

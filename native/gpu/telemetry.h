@@ -1,0 +1,83 @@
+// Side-thread telemetry poller + health evaluation (north-star N2).
+//
+// One background thread samples every managed device each `interval` (amdsmi
+// gpu_metrics: activity, power, temperatures, clocks, throttle, xGMI link status; VRAM
+// usage; ECC totals), publishes an immutable snapshot (readers never block the poll),
+// exports `amd_gpu_*` Prometheus gauges, and drives a per-device health state machine
+// with hysteresis.  Each poll is bracketed by a roctx range so rocprofv3 --marker-trace
+// shows its cost; the reconcile/admission paths never touch it.
+#pragma once
+
+#include <atomic>
+#include <chrono>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "core/cancel.h"
+#include "gpu/device.h"
+
+namespace bgc::gpu {
+
+struct HealthPolicy {
+  double max_hotspot_c = 105.0;      // above -> unhealthy
+  double max_mem_c = 95.0;
+  uint64_t max_new_uncorrectable = 0;  // new uncorrectable ECC errors tolerated since start
+  bool require_all_xgmi_links = true;  // a down xGMI link breaks TP=8 all-reduce placement
+  int fail_threshold = 3;              // consecutive bad polls before flipping to unhealthy
+  int recover_threshold = 3;           // consecutive good polls before flipping back
+};
+
+struct DeviceHealth {
+  int index = 0;
+  bool healthy = true;
+  std::string reason;
+  int consecutive_bad = 0;
+  int consecutive_good = 0;
+  uint64_t baseline_uncorrectable = 0;
+  bool baseline_set = false;
+};
+
+struct Snapshot {
+  int64_t ts_ns = 0;
+  uint64_t poll_seq = 0;
+  double poll_us = 0;  // wall time of the whole poll
+  std::vector<Telemetry> devices;
+  std::vector<DeviceHealth> health;
+};
+
+class TelemetryPoller {
+ public:
+  TelemetryPoller(Backend& backend, std::vector<int> indices, std::chrono::milliseconds interval,
+                  HealthPolicy policy = {});
+  ~TelemetryPoller();
+  void start();
+  void stop();
+  // Runs one poll synchronously (tests, and the first poll before start()).
+  void poll_once();
+  std::shared_ptr<const Snapshot> snapshot() const;
+  // Invoked (on the poller thread) whenever any device's health flips.
+  void on_health_change(std::function<void(const Snapshot&)> cb);
+  uint64_t polls() const { return polls_.load(); }
+
+  // Pure health step (exposed for tests).
+  static void evaluate(const Telemetry& t, const HealthPolicy& p, DeviceHealth& h);
+
+ private:
+  Backend& backend_;
+  std::vector<int> indices_;
+  std::chrono::milliseconds interval_;
+  HealthPolicy policy_;
+  std::vector<DeviceHealth> health_;
+  mutable std::mutex snap_mu_;
+  std::shared_ptr<const Snapshot> snap_;
+  std::function<void(const Snapshot&)> cb_;
+  std::atomic<uint64_t> polls_{0};
+  CancelToken stop_;
+  std::thread thread_;
+};
+
+}  // namespace bgc::gpu

@@ -1,0 +1,122 @@
+// Kubernetes API client: config inference + typed REST verbs (kube-client 0.84
+// equivalent; reference uses `Client::try_default()` at src/controller.rs:224 and
+// src/synchronizer.rs:392, `PatchParams::apply(..).force()` at src/controller.rs:67,
+// `replace_status` at src/synchronizer.rs:302, JSON patch at :323-330).
+#pragma once
+
+#include <chrono>
+#include <memory>
+#include <mutex>
+#include <optional>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "core/http.h"
+#include "core/json.h"
+#include "kube/resource.h"
+
+namespace bgc::kube {
+
+struct KubeConfig {
+  std::string server;           // https://10.96.0.1:443 or http://127.0.0.1:port
+  std::string token;            // bearer token (static)
+  std::string token_file;       // re-read periodically (bound SA tokens rotate)
+  std::string ca_pem;
+  std::string client_cert_pem;
+  std::string client_key_pem;
+  bool insecure = false;
+  std::string tls_server_name;
+  std::string impersonate_user;
+  std::vector<std::string> impersonate_groups;
+  int timeout_ms = 30000;
+  std::string source;           // "in-cluster" | "kubeconfig:<path>" | "env"
+
+  // Inference order (kube-client `Config::infer`): $BGC_KUBE_SERVER override (tests),
+  // $KUBECONFIG / ~/.kube/config, then the in-cluster service account.
+  static KubeConfig infer();
+  static KubeConfig in_cluster();
+  static KubeConfig from_kubeconfig(const std::string& path, const std::string& context = "");
+};
+
+class ApiError : public std::runtime_error {
+ public:
+  ApiError(int code, std::string reason, const std::string& message, json::Value status = {})
+      : std::runtime_error("ApiError(" + std::to_string(code) + " " + reason + "): " + message),
+        code_(code), reason_(std::move(reason)), message_(message), status_(std::move(status)) {}
+  int code() const { return code_; }
+  const std::string& reason() const { return reason_; }
+  const std::string& message() const { return message_; }
+  const json::Value& status() const { return status_; }
+
+ private:
+  int code_;
+  std::string reason_;
+  std::string message_;
+  json::Value status_;
+};
+
+struct ListOptions {
+  std::string label_selector;
+  std::string field_selector;
+  std::string resource_version;
+  int64_t limit = 0;
+  std::string continue_token;
+};
+
+struct WatchOptions {
+  std::string resource_version;
+  std::string label_selector;
+  std::string field_selector;
+  int timeout_seconds = 290;
+  bool allow_bookmarks = true;
+};
+
+class KubeClient {
+ public:
+  explicit KubeClient(KubeConfig cfg);
+
+  json::Value get(const ResourceType& rt, const std::string& ns, const std::string& name);
+  std::optional<json::Value> get_opt(const ResourceType& rt, const std::string& ns, const std::string& name);
+  json::Value list(const ResourceType& rt, const std::string& ns = "", const ListOptions& opts = {});
+  json::Value create(const ResourceType& rt, const std::string& ns, const json::Value& body,
+                     const std::string& field_manager = "");
+  json::Value replace(const ResourceType& rt, const std::string& ns, const std::string& name, const json::Value& body,
+                      const std::string& field_manager = "");
+  json::Value replace_status(const ResourceType& rt, const std::string& ns, const std::string& name,
+                             const json::Value& body);
+  // Server-side apply (application/apply-patch+yaml; JSON is valid YAML).
+  json::Value apply(const ResourceType& rt, const std::string& ns, const std::string& name, const json::Value& body,
+                    const std::string& field_manager, bool force);
+  json::Value apply_status(const ResourceType& rt, const std::string& ns, const std::string& name,
+                           const json::Value& body, const std::string& field_manager, bool force);
+  json::Value patch_json(const ResourceType& rt, const std::string& ns, const std::string& name,
+                         const json::Value& ops, const std::string& field_manager = "");
+  json::Value patch_merge(const ResourceType& rt, const std::string& ns, const std::string& name,
+                          const json::Value& patch, const std::string& subresource = "",
+                          const std::string& field_manager = "");
+  json::Value remove(const ResourceType& rt, const std::string& ns, const std::string& name,
+                     const std::string& propagation = "Background");
+  std::unique_ptr<http::StreamingResponse> watch(const ResourceType& rt, const std::string& ns,
+                                                 const WatchOptions& opts);
+
+  // Low level: throws ApiError on non-2xx.
+  json::Value call(const std::string& method, const std::string& path, const std::string& body = "",
+                   const std::string& content_type = "application/json");
+  http::Response raw(const std::string& method, const std::string& path, const std::string& body = "",
+                     const std::string& content_type = "application/json");
+  const KubeConfig& config() const { return cfg_; }
+
+ private:
+  http::Headers auth_headers();
+  KubeConfig cfg_;
+  std::unique_ptr<http::Client> http_;
+  std::mutex token_mu_;
+  std::string token_;
+  std::chrono::steady_clock::time_point token_read_{};
+};
+
+// Raises ApiError for a non-2xx response (parsing a metav1.Status body when present).
+[[noreturn]] void throw_api_error(const http::Response& r);
+
+}  // namespace bgc::kube
