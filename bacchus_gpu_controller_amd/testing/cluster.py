@@ -1,0 +1,235 @@
+"""Process-level harness: kube-lite + the native admission/controller/synchronizer/
+node-agent binaries wired together the way the Helm chart wires them in a real cluster
+(webhook registered through a MutatingWebhookConfiguration with a caBundle, TLS to the
+webhook, service-account tokens for each component).
+
+Used by tests/integration and by bench.py.
+"""
+import base64
+import json
+import os
+import socket
+import subprocess
+import tempfile
+import time
+
+import requests
+
+from .. import REPO_ROOT, binary, native
+from .kubeapi import KubeApi, wait_for
+
+NAMESPACE = "bgc"
+RELEASE = "bgc"
+WEBHOOK_SERVICE = f"{RELEASE}-admission"
+
+ADMIN_TOKEN = "admin-token"
+CONTROLLER_TOKEN = "controller-token"
+SYNC_TOKEN = "synchronizer-token"
+NODE_AGENT_TOKEN = "node-agent-token"
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class Proc:
+    def __init__(self, name, cmd, env, workdir):
+        self.name = name
+        self.log_path = os.path.join(workdir, f"{name}.log")
+        self.log = open(self.log_path, "wb")
+        full_env = dict(os.environ)
+        full_env.update(env)
+        self.p = subprocess.Popen(cmd, env=full_env, stdout=self.log, stderr=subprocess.STDOUT,
+                                  start_new_session=True)
+
+    def alive(self):
+        return self.p.poll() is None
+
+    def stop(self, timeout=15):
+        if self.p.poll() is None:
+            self.p.terminate()
+            try:
+                self.p.wait(timeout=timeout)
+            except subprocess.TimeoutExpired:
+                self.p.kill()
+                self.p.wait()
+        self.log.close()
+        return self.p.returncode
+
+    def output(self):
+        try:
+            with open(self.log_path, "rb") as f:
+                return f.read().decode(errors="replace")
+        except OSError:
+            return ""
+
+
+def webhook_configuration(ca_pem, port, timeout_seconds=10):
+    """What charts/bacchus-gpu-controller/templates/webhook.yaml renders (reference
+    templates/webhook.yaml:1-27), with cert-manager's CA injection done inline."""
+    return {
+        "apiVersion": "admissionregistration.k8s.io/v1",
+        "kind": "MutatingWebhookConfiguration",
+        "metadata": {"name": RELEASE},
+        "webhooks": [{
+            "name": f"{RELEASE}-admission.bacchus.io",
+            "rules": [{"apiGroups": ["bacchus.io"], "apiVersions": ["v1"], "resources": ["userbootstraps"],
+                       "scope": "*", "operations": ["CREATE", "UPDATE", "DELETE"]}],
+            "clientConfig": {"service": {"namespace": NAMESPACE, "name": WEBHOOK_SERVICE, "path": "/mutate",
+                                         "port": port},
+                             "caBundle": base64.b64encode(ca_pem.encode()).decode()},
+            "timeoutSeconds": timeout_seconds,
+            "sideEffects": "None",
+            "admissionReviewVersions": ["v1"],
+            "failurePolicy": "Fail",
+        }],
+    }
+
+
+class Cluster:
+    def __init__(self, workdir=None, admission=True, controller=True, controller_env=None, admission_env=None,
+                 apiserver_args=None, log_level="warn"):
+        self._tmp = None
+        if workdir is None:
+            self._tmp = tempfile.TemporaryDirectory(prefix="bgc-cluster-")
+            workdir = self._tmp.name
+        self.workdir = workdir
+        self.want_admission = admission
+        self.want_controller = controller
+        self.controller_env = controller_env or {}
+        self.admission_env = admission_env or {}
+        self.apiserver_args = apiserver_args or []
+        self.log_level = log_level
+        self.procs = {}
+        self.server = None
+        self.ca_pem = None
+        self.admission_port = None
+        self.controller_port = None
+
+    # ------------------------------------------------------------------ setup
+    def _write_tokens(self):
+        path = os.path.join(self.workdir, "tokens.csv")
+        with open(path, "w") as f:
+            f.write(f'{ADMIN_TOKEN},kubernetes-admin,uid-admin,"system:masters"\n')
+            f.write(f'{CONTROLLER_TOKEN},system:serviceaccount:{NAMESPACE}:{RELEASE}-controller,uid-ctrl,"system:serviceaccounts"\n')
+            f.write(f'{SYNC_TOKEN},system:serviceaccount:{NAMESPACE}:{RELEASE}-synchronizer,uid-sync,"system:serviceaccounts"\n')
+            f.write(f'{NODE_AGENT_TOKEN},system:serviceaccount:{NAMESPACE}:{RELEASE}-node-agent,uid-na,"system:serviceaccounts"\n')
+        return path
+
+    def _certs(self):
+        dns = [f"{WEBHOOK_SERVICE}.{NAMESPACE}", f"{WEBHOOK_SERVICE}.{NAMESPACE}.svc", "localhost", "127.0.0.1"]
+        b = native().make_ca_and_leaf(WEBHOOK_SERVICE, dns, 90)
+        d = os.path.join(self.workdir, "cert")
+        os.makedirs(d, exist_ok=True)
+        for k, fn in (("cert", "tls.crt"), ("key", "tls.key"), ("ca_cert", "ca.crt"), ("ca_key", "ca.key")):
+            with open(os.path.join(d, fn), "w") as f:
+                f.write(b[k])
+        self.ca_pem = b["ca_cert"]
+        self.cert_dir = d
+        return d
+
+    def start(self):
+        tokens = self._write_tokens()
+        self.admission_port = free_port() if self.want_admission else 1
+        port_file = os.path.join(self.workdir, "apiserver.port")
+        args = [binary("kube-lite"), "--port", "0", "--port-file", port_file, "--token-file", tokens,
+                "--no-anonymous", "--bookmark-ms", "1000",
+                "--service-override", f"{NAMESPACE}/{WEBHOOK_SERVICE}=127.0.0.1:{self.admission_port}"]
+        args += self.apiserver_args
+        self.procs["apiserver"] = Proc("apiserver", args, {"RUST_LOG": self.log_level}, self.workdir)
+        wait_for(lambda: os.path.exists(port_file), 20, desc="kube-lite port file")
+        self.server = f"http://127.0.0.1:{open(port_file).read().strip()}"
+        self.admin = KubeApi(self.server, ADMIN_TOKEN)
+        self.admin.create("namespaces", {"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": NAMESPACE}})
+        self.admin.create("customresourcedefinitions", json.loads(native().crd_json()))
+        if self.want_admission:
+            self._certs()
+            self.start_admission()
+            self.admin.create("mutatingwebhookconfigurations", webhook_configuration(self.ca_pem, self.admission_port))
+        if self.want_controller:
+            self.start_controller()
+        return self
+
+    def component_env(self, token, port):
+        return {"BGC_KUBE_SERVER": self.server, "BGC_KUBE_TOKEN": token, "CONF_LISTEN_ADDR": "127.0.0.1",
+                "CONF_LISTEN_PORT": str(port), "RUST_LOG": self.log_level}
+
+    def start_admission(self):
+        env = {
+            "CONF_LISTEN_ADDR": "127.0.0.1", "CONF_LISTEN_PORT": str(self.admission_port),
+            "CONF_CERT_PATH": os.path.join(self.cert_dir, "tls.crt"),
+            "CONF_KEY_PATH": os.path.join(self.cert_dir, "tls.key"),
+            "CONF_OIDC_USERNAME_PREFIX": "oidc:", "CONF_DEFAULT_ROLE_NAME": "edit",
+            "CONF_AUTHORIZED_GROUP_NAMES": "gpu,admin", "RUST_LOG": self.log_level,
+        }
+        env.update(self.admission_env)
+        self.procs["admission"] = Proc("admission", [binary("admission")], env, self.workdir)
+        ca = os.path.join(self.cert_dir, "ca.crt")
+        wait_for(lambda: requests.get(f"https://127.0.0.1:{self.admission_port}/health", verify=ca, timeout=1).text == "pong",
+                 20, desc="admission /health")
+
+    def start_controller(self, extra_env=None):
+        self.controller_port = free_port()
+        env = self.component_env(CONTROLLER_TOKEN, self.controller_port)
+        env.update(self.controller_env)
+        env.update(extra_env or {})
+        self.procs["controller"] = Proc("controller", [binary("controller")], env, self.workdir)
+        wait_for(lambda: requests.get(f"http://127.0.0.1:{self.controller_port}/health", timeout=1).text == "pong",
+                 20, desc="controller /health")
+
+    def start_process(self, name, exe, env):
+        self.procs[name] = Proc(name, [binary(exe)], env, self.workdir)
+        return self.procs[name]
+
+    # ------------------------------------------------------------------ access
+    def as_user(self, username, groups=()):
+        return KubeApi(self.server, ADMIN_TOKEN, as_user=username, as_groups=list(groups))
+
+    def fault(self, rules, append=False):
+        r = requests.post(self.server + "/_kl/faults" + ("?append=true" if append else ""), json=rules, timeout=5)
+        r.raise_for_status()
+
+    def clear_faults(self):
+        requests.delete(self.server + "/_kl/faults", timeout=5)
+
+    def compact_and_drop_watches(self):
+        requests.post(self.server + "/_kl/compact", timeout=5).raise_for_status()
+        requests.post(self.server + "/_kl/drop-watches", timeout=5).raise_for_status()
+
+    def stats(self):
+        return requests.get(self.server + "/_kl/stats", timeout=5).json()
+
+    def samples(self, component, name):
+        port = {"apiserver": None, "controller": self.controller_port}.get(component)
+        base = self.server if component == "apiserver" else f"http://127.0.0.1:{port}"
+        return requests.get(f"{base}/debug/samples/{name}", timeout=5).json()
+
+    def stop(self):
+        codes = {}
+        for name in reversed(list(self.procs)):
+            codes[name] = self.procs[name].stop()
+        if self._tmp:
+            self._tmp.cleanup()
+        return codes
+
+    def logs(self):
+        return {n: p.output() for n, p in self.procs.items()}
+
+    def __enter__(self):
+        try:
+            return self.start()
+        except Exception:
+            for n, p in self.procs.items():
+                print(f"--- {n} ---\n{p.output()[-4000:]}")
+            self.stop()
+            raise
+
+    def __exit__(self, *exc):
+        if exc[0] is not None:
+            for n, p in self.procs.items():
+                print(f"--- {n} log tail ---\n{p.output()[-3000:]}")
+        self.stop()

@@ -1,0 +1,1606 @@
+#include "apiserver/server.h"
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <mutex>
+#include <regex>
+#include <set>
+#include <sstream>
+#include <thread>
+#include <unordered_map>
+
+#include "apiserver/fieldset.h"
+#include "core/crypto.h"
+#include "core/http.h"
+#include "core/json_patch.h"
+#include "core/log.h"
+#include "core/metrics.h"
+#include "core/net.h"
+#include "core/yaml.h"
+#include "crd/schema.h"
+#include "kube/leader.h"
+#include "kube/resource.h"
+
+namespace bgc::apiserver {
+
+using json::Value;
+using kube::ResourceType;
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// Errors as metav1.Status
+
+struct StatusError : std::runtime_error {
+  int code;
+  std::string reason;
+  Value details;
+  StatusError(int c, std::string r, const std::string& msg, Value d = {})
+      : std::runtime_error(msg), code(c), reason(std::move(r)), details(std::move(d)) {}
+};
+
+Value status_body(int code, const std::string& reason, const std::string& message, const Value& details = {}) {
+  Value s = Value::object({{"kind", "Status"}, {"apiVersion", "v1"}, {"metadata", Value::object()},
+                           {"status", code < 400 ? "Success" : "Failure"}, {"message", message},
+                           {"reason", reason}});
+  if (!details.is_null()) s["details"] = details;
+  s["code"] = code;
+  return s;
+}
+
+std::string resource_ref(const ResourceType& rt) {
+  return rt.group.empty() ? rt.plural : rt.plural + "." + rt.group;
+}
+
+StatusError not_found(const ResourceType& rt, const std::string& name) {
+  return StatusError(404, "NotFound", resource_ref(rt) + " \"" + name + "\" not found",
+                     Value::object({{"name", name}, {"group", rt.group}, {"kind", rt.plural}}));
+}
+
+StatusError already_exists(const ResourceType& rt, const std::string& name) {
+  return StatusError(409, "AlreadyExists", resource_ref(rt) + " \"" + name + "\" already exists",
+                     Value::object({{"name", name}, {"group", rt.group}, {"kind", rt.plural}}));
+}
+
+StatusError conflict(const ResourceType& rt, const std::string& name) {
+  return StatusError(409, "Conflict",
+                     "Operation cannot be fulfilled on " + resource_ref(rt) + " \"" + name +
+                         "\": the object has been modified; please apply your changes to the latest version and try again",
+                     Value::object({{"name", name}, {"group", rt.group}, {"kind", rt.plural}}));
+}
+
+StatusError invalid(const ResourceType& rt, const std::string& name, const std::string& msg) {
+  return StatusError(422, "Invalid", rt.kind + "." + rt.group + " \"" + name + "\" is invalid: " + msg,
+                     Value::object({{"name", name}, {"group", rt.group}, {"kind", rt.kind}}));
+}
+
+std::string now_rfc3339() {
+  std::string s = kube::rfc3339_micro_now();
+  return s.substr(0, 19) + "Z";
+}
+
+bool dns1123_label(const std::string& s) {
+  if (s.empty() || s.size() > 63) return false;
+  for (size_t i = 0; i < s.size(); ++i) {
+    char c = s[i];
+    bool ok = (c >= 'a' && c <= 'z') || (c >= '0' && c <= '9') || (c == '-' && i != 0 && i + 1 != s.size());
+    if (!ok) return false;
+  }
+  return true;
+}
+
+bool dns1123_subdomain(const std::string& s) {
+  if (s.empty() || s.size() > 253) return false;
+  size_t start = 0;
+  while (true) {
+    size_t dot = s.find('.', start);
+    std::string part = s.substr(start, dot == std::string::npos ? std::string::npos : dot - start);
+    if (!dns1123_label(part)) return false;
+    if (dot == std::string::npos) return true;
+    start = dot + 1;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Label selectors
+
+struct Requirement {
+  std::string key;
+  std::string op;  // = != exists !exists in notin
+  std::vector<std::string> values;
+};
+
+std::string trim(std::string s) {
+  while (!s.empty() && s.front() == ' ') s.erase(0, 1);
+  while (!s.empty() && s.back() == ' ') s.pop_back();
+  return s;
+}
+
+std::vector<Requirement> parse_selector(const std::string& sel) {
+  std::vector<Requirement> out;
+  // split on commas not inside parentheses
+  std::vector<std::string> parts;
+  int depth = 0;
+  std::string cur;
+  for (char c : sel) {
+    if (c == '(') ++depth;
+    if (c == ')') --depth;
+    if (c == ',' && depth == 0) {
+      parts.push_back(cur);
+      cur.clear();
+    } else {
+      cur.push_back(c);
+    }
+  }
+  if (!cur.empty()) parts.push_back(cur);
+  for (auto p : parts) {
+    p = trim(p);
+    if (p.empty()) continue;
+    Requirement r;
+    size_t pos;
+    if (p[0] == '!') {
+      r.key = trim(p.substr(1));
+      r.op = "!exists";
+    } else if ((pos = p.find(" notin ")) != std::string::npos || (pos = p.find(" in ")) != std::string::npos) {
+      bool notin = p.compare(pos, 7, " notin ") == 0;
+      r.key = trim(p.substr(0, pos));
+      r.op = notin ? "notin" : "in";
+      size_t lp = p.find('('), rp = p.rfind(')');
+      if (lp == std::string::npos || rp == std::string::npos) throw StatusError(400, "BadRequest", "invalid selector: " + p);
+      std::string inner = p.substr(lp + 1, rp - lp - 1);
+      std::stringstream ss(inner);
+      std::string v;
+      while (std::getline(ss, v, ',')) r.values.push_back(trim(v));
+    } else if ((pos = p.find("!=")) != std::string::npos) {
+      r.key = trim(p.substr(0, pos));
+      r.op = "!=";
+      r.values.push_back(trim(p.substr(pos + 2)));
+    } else if ((pos = p.find("==")) != std::string::npos) {
+      r.key = trim(p.substr(0, pos));
+      r.op = "=";
+      r.values.push_back(trim(p.substr(pos + 2)));
+    } else if ((pos = p.find('=')) != std::string::npos) {
+      r.key = trim(p.substr(0, pos));
+      r.op = "=";
+      r.values.push_back(trim(p.substr(pos + 1)));
+    } else {
+      r.key = p;
+      r.op = "exists";
+    }
+    out.push_back(r);
+  }
+  return out;
+}
+
+bool selector_matches(const std::vector<Requirement>& reqs, const Value& obj) {
+  const Value& labels = obj.get("metadata").get("labels");
+  for (const auto& r : reqs) {
+    const Value* v = labels.find(r.key);
+    bool has = v && v->is_string();
+    std::string val = has ? v->as_string() : "";
+    if (r.op == "exists" && !has) return false;
+    if (r.op == "!exists" && has) return false;
+    if (r.op == "=" && (!has || val != r.values[0])) return false;
+    if (r.op == "!=" && has && val == r.values[0]) return false;
+    if (r.op == "in" && (!has || std::find(r.values.begin(), r.values.end(), val) == r.values.end())) return false;
+    if (r.op == "notin" && has && std::find(r.values.begin(), r.values.end(), val) != r.values.end()) return false;
+  }
+  return true;
+}
+
+struct FieldFilter {
+  std::string name, ns;
+};
+
+FieldFilter parse_field_selector(const std::string& s) {
+  FieldFilter f;
+  std::stringstream ss(s);
+  std::string part;
+  while (std::getline(ss, part, ',')) {
+    size_t eq = part.find('=');
+    if (eq == std::string::npos) continue;
+    std::string k = trim(part.substr(0, eq));
+    std::string v = trim(part.substr(part[eq + 1] == '=' ? eq + 2 : eq + 1));
+    if (k == "metadata.name") f.name = v;
+    else if (k == "metadata.namespace") f.ns = v;
+  }
+  return f;
+}
+
+// ---------------------------------------------------------------------------
+
+struct UserInfo {
+  std::string username;
+  std::string uid;
+  std::vector<std::string> groups;
+  bool is_admin() const { return std::find(groups.begin(), groups.end(), "system:masters") != groups.end(); }
+  Value to_json() const {
+    Value g = Value::array();
+    for (auto& x : groups) g.push_back(x);
+    Value v = Value::object({{"username", username}});
+    if (!uid.empty()) v["uid"] = uid;
+    v["groups"] = g;
+    return v;
+  }
+};
+
+struct TypeInfo {
+  ResourceType rt;
+  Value schema;  // openAPIV3Schema for CRDs (null for built-ins)
+  bool custom = false;
+  std::string key() const { return rt.group + "/" + rt.version + "/" + rt.plural; }
+};
+
+struct ManagerEntry {
+  std::string operation;  // Apply | Update
+  std::string api_version;
+  std::string time;
+  std::string subresource;
+  FieldSet fields;
+  bool operator==(const ManagerEntry& o) const {
+    return operation == o.operation && fields == o.fields && subresource == o.subresource;
+  }
+};
+using Managers = std::map<std::string, ManagerEntry>;
+
+struct Stored {
+  std::shared_ptr<const Value> obj;
+  uint64_t rv = 0;
+  Managers managers;
+};
+
+struct EventRec {
+  uint64_t rv;
+  std::string type_key;
+  std::string ns;
+  std::shared_ptr<const Value> obj;
+  std::shared_ptr<const std::string> line;  // {"type":..,"object":..}\n
+};
+
+struct WatchSub {
+  std::string type_key;
+  std::string ns;
+  std::vector<Requirement> sel;
+  FieldFilter fields;
+  std::deque<std::shared_ptr<const EventRec>> q;
+  std::condition_variable cv;
+  bool closed = false;
+  bool overflow = false;
+};
+
+struct FaultRule {
+  std::string method;  // empty = any
+  std::regex path;
+  std::string path_src;
+  int status = 0;
+  int delay_ms = 0;
+  int remaining = -1;  // -1 = unlimited
+  std::string message;
+};
+
+struct ParsedPath {
+  TypeInfo* ti = nullptr;
+  std::string ns;
+  std::string name;
+  std::string sub;
+  bool collection = false;
+};
+
+struct WriteResult {
+  std::shared_ptr<const Value> obj;
+  int code = 200;
+};
+
+std::string obj_key(const ResourceType& rt, const std::string& ns, const std::string& name) { return rt.key(ns, name); }
+
+}  // namespace
+
+// ===========================================================================
+
+struct ApiServer::Impl {
+  Options opts;
+  std::unique_ptr<http::Server> server;
+
+  std::mutex mu;
+  std::map<std::string, TypeInfo> types;  // key() -> info
+  std::unordered_map<std::string, std::unordered_map<std::string, Stored>> data;  // type key -> obj key -> stored
+  std::unordered_map<std::string, std::pair<std::string, std::string>> by_uid;      // uid -> (type key, obj key)
+  uint64_t rv = 1000;
+  std::deque<std::shared_ptr<const EventRec>> history;
+  uint64_t compacted_rv = 0;  // watches from rv < compacted_rv get 410
+  std::set<WatchSub*> watches;
+
+  std::unordered_map<std::string, UserInfo> tokens;
+
+  std::mutex fault_mu;
+  std::vector<FaultRule> faults;
+
+  std::mutex hook_mu;
+  std::map<std::string, std::shared_ptr<http::Client>> hook_clients;
+
+  std::atomic<uint64_t> requests{0};
+
+  explicit Impl(Options o) : opts(std::move(o)) {
+    for (const ResourceType* rt : kube::types::builtin()) {
+      TypeInfo ti;
+      ti.rt = *rt;
+      types[ti.key()] = ti;
+    }
+    if (!opts.token_file.empty()) load_tokens(opts.token_file);
+  }
+
+  void load_tokens(const std::string& path) {
+    std::stringstream ss(net::read_file(path));
+    std::string line;
+    while (std::getline(ss, line)) {
+      if (line.empty() || line[0] == '#') continue;
+      std::vector<std::string> cols;
+      std::string cur;
+      bool q = false;
+      for (char c : line) {
+        if (c == '"') {
+          q = !q;
+          continue;
+        }
+        if (c == ',' && !q) {
+          cols.push_back(cur);
+          cur.clear();
+          continue;
+        }
+        cur.push_back(c);
+      }
+      cols.push_back(cur);
+      if (cols.size() < 2) continue;
+      UserInfo u;
+      u.username = cols[1];
+      if (cols.size() > 2) u.uid = cols[2];
+      if (cols.size() > 3 && !cols[3].empty()) {
+        std::stringstream gs(cols[3]);
+        std::string g;
+        while (std::getline(gs, g, ',')) u.groups.push_back(g);
+      }
+      u.groups.push_back("system:authenticated");
+      tokens[cols[0]] = u;
+    }
+  }
+
+  // ---------------------------------------------------------------- auth
+  UserInfo authenticate(const http::Request& req) {
+    UserInfo u;
+    std::string auth = req.headers.get_or("Authorization");
+    if (auth.rfind("Bearer ", 0) == 0) {
+      auto it = tokens.find(auth.substr(7));
+      if (it == tokens.end()) throw StatusError(401, "Unauthorized", "Unauthorized");
+      u = it->second;
+    } else if (opts.anonymous_admin) {
+      u.username = "system:admin";
+      u.groups = {"system:masters", "system:authenticated"};
+    } else {
+      throw StatusError(401, "Unauthorized", "Unauthorized");
+    }
+    if (const std::string* imp = req.headers.get("Impersonate-User")) {
+      if (!u.is_admin()) {
+        throw StatusError(403, "Forbidden", "users \"" + *imp + "\" is forbidden: User \"" + u.username +
+                                                "\" cannot impersonate resource \"users\" in API group \"\" at the cluster scope");
+      }
+      UserInfo imp_u;
+      imp_u.username = *imp;
+      for (const auto& kv : req.headers.items()) {
+        std::string lk = kv.first;
+        for (auto& c : lk) c = static_cast<char>(std::tolower(static_cast<unsigned char>(c)));
+        if (lk == "impersonate-group") {
+          // one header per group per the spec; comma-joined values are split too
+          // because common HTTP client libraries fold repeated headers.
+          std::stringstream gs(kv.second);
+          std::string g;
+          while (std::getline(gs, g, ',')) {
+            if (!trim(g).empty()) imp_u.groups.push_back(trim(g));
+          }
+        }
+      }
+      imp_u.groups.push_back("system:authenticated");
+      u = imp_u;
+    }
+    return u;
+  }
+
+  // ---------------------------------------------------------------- paths
+  TypeInfo* find_type(const std::string& group, const std::string& version, const std::string& plural) {
+    auto it = types.find(group + "/" + version + "/" + plural);
+    return it == types.end() ? nullptr : &it->second;
+  }
+
+  // Returns false for non-resource (discovery) paths.
+  bool parse_path(const std::string& path, ParsedPath& out, std::string& group, std::string& version,
+                  std::vector<std::string>& rest) {
+    std::vector<std::string> segs;
+    std::stringstream ss(path);
+    std::string s;
+    while (std::getline(ss, s, '/')) {
+      if (!s.empty()) segs.push_back(s);
+    }
+    size_t i = 0;
+    if (segs.size() >= 2 && segs[0] == "api") {
+      group = "";
+      version = segs[1];
+      i = 2;
+    } else if (segs.size() >= 3 && segs[0] == "apis") {
+      group = segs[1];
+      version = segs[2];
+      i = 3;
+    } else {
+      return false;
+    }
+    rest.assign(segs.begin() + static_cast<long>(i), segs.end());
+    if (rest.empty()) return false;
+    std::lock_guard<std::mutex> lk(mu);
+    if (rest[0] == "namespaces" && rest.size() >= 3) {
+      TypeInfo* ti = find_type(group, version, rest[2]);
+      if (ti && ti->rt.namespaced) {
+        out.ti = ti;
+        out.ns = rest[1];
+        out.collection = rest.size() == 3;
+        if (rest.size() >= 4) out.name = rest[3];
+        if (rest.size() >= 5) out.sub = rest[4];
+        return true;
+      }
+    }
+    TypeInfo* ti = find_type(group, version, rest[0]);
+    if (!ti) throw StatusError(404, "NotFound", "the server could not find the requested resource");
+    out.ti = ti;
+    out.collection = rest.size() == 1;
+    if (rest.size() >= 2) out.name = rest[1];
+    if (rest.size() >= 3) out.sub = rest[2];
+    return true;
+  }
+
+  // ---------------------------------------------------------------- events
+  void emit_locked(const std::string& type, const TypeInfo& ti, const std::string& ns,
+                   const std::shared_ptr<const Value>& obj, uint64_t ev_rv) {
+    auto rec = std::make_shared<EventRec>();
+    rec->rv = ev_rv;
+    rec->type_key = ti.key();
+    rec->ns = ns;
+    rec->obj = obj;
+    std::string line = "{\"type\":\"" + type + "\",\"object\":";
+    obj->dump_to(line);
+    line += "}\n";
+    rec->line = std::make_shared<const std::string>(std::move(line));
+    history.push_back(rec);
+    while (history.size() > opts.history_limit) {
+      compacted_rv = history.front()->rv;
+      history.pop_front();
+    }
+    for (WatchSub* w : watches) {
+      if (w->type_key != rec->type_key) continue;
+      if (!w->ns.empty() && w->ns != ns) continue;
+      if (!w->fields.name.empty() && obj->get("metadata").get_string("name") != w->fields.name) continue;
+      if (!w->sel.empty() && !selector_matches(w->sel, *obj)) continue;
+      if (w->q.size() > 100000) {
+        w->overflow = true;
+        w->cv.notify_one();
+        continue;
+      }
+      w->q.push_back(rec);
+      w->cv.notify_one();
+    }
+  }
+
+  // ---------------------------------------------------------------- webhooks
+  struct HookMatch {
+    std::string name;
+    Value hook;
+  };
+
+  std::vector<HookMatch> matching_webhooks(const TypeInfo& ti, const std::string& sub, const std::string& op) {
+    std::vector<HookMatch> out;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = data.find(kube::types::MutatingWebhookConfiguration.group + "/v1/mutatingwebhookconfigurations");
+    if (it == data.end()) return out;
+    std::string res = ti.rt.plural + (sub.empty() ? "" : "/" + sub);
+    for (auto& kv : it->second) {
+      for (const auto& hook : kv.second.obj->get("webhooks").items()) {
+        for (const auto& rule : hook.get("rules").items()) {
+          auto contains = [](const Value& arr, const std::string& v) {
+            for (const auto& x : arr.items()) {
+              if (x.is_string() && (x.as_string() == "*" || x.as_string() == v)) return true;
+            }
+            return false;
+          };
+          bool res_ok = false;
+          for (const auto& r : rule.get("resources").items()) {
+            std::string rs = r.as_string();
+            if (rs == res || rs == "*/*" || (rs == "*" && sub.empty()) ||
+                (sub.size() && rs == "*/" + sub) || (rs == ti.rt.plural + "/*")) {
+              res_ok = true;
+            }
+          }
+          if (contains(rule.get("apiGroups"), ti.rt.group) && contains(rule.get("apiVersions"), ti.rt.version) &&
+              contains(rule.get("operations"), op) && res_ok) {
+            out.push_back({hook.get_string("name"), hook});
+            break;
+          }
+        }
+      }
+    }
+    return out;
+  }
+
+  std::shared_ptr<http::Client> hook_client(const Value& hook, std::string& path_out) {
+    const Value& cc = hook.get("clientConfig");
+    std::string ca = cc.get_string("caBundle");
+    std::string base, server_name;
+    if (cc.get("url").is_string()) {
+      http::Url u = http::parse_url(cc.get_string("url"));
+      base = u.scheme + "://" + u.host + ":" + std::to_string(u.port);
+      path_out = u.path.empty() ? "/" : u.path;
+    } else {
+      const Value& svc = cc.get("service");
+      std::string ns = svc.get_string("namespace"), name = svc.get_string("name");
+      int port = svc.get("port").is_int() ? static_cast<int>(svc.get("port").as_int()) : 443;
+      path_out = svc.get_string("path", "/");
+      server_name = name + "." + ns + ".svc";
+      auto ov = opts.service_overrides.find(ns + "/" + name);
+      std::string hostport = ov != opts.service_overrides.end() ? ov->second : server_name + ":" + std::to_string(port);
+      base = "https://" + hostport;
+    }
+    std::string key = base + "|" + server_name + "|" + crypto::sha256_hex(ca);
+    std::lock_guard<std::mutex> lk(hook_mu);
+    auto it = hook_clients.find(key);
+    if (it != hook_clients.end()) return it->second;
+    http::ClientOptions o;
+    o.base_url = base;
+    o.tls_server_name = server_name;
+    if (base.rfind("https", 0) == 0) {
+      o.tls = net::TlsContext::client(ca.empty() ? "" : crypto::base64_decode(ca), false);
+    }
+    auto c = std::make_shared<http::Client>(o);
+    hook_clients[key] = c;
+    return c;
+  }
+
+  // Runs mutating webhooks; may modify `obj`. Throws StatusError on deny/failure.
+  void call_webhooks(const TypeInfo& ti, const std::string& sub, const std::string& op, const std::string& ns,
+                     const std::string& name, Value* obj, const Value* old, const UserInfo& user) {
+    auto hooks = matching_webhooks(ti, sub, op);
+    if (hooks.empty()) return;
+    static auto& ring = metrics::Registry::global().samples("webhook");
+    static auto& hist = metrics::Registry::global().histogram("kl_webhook_duration_seconds", "Webhook callout latency");
+    for (const auto& hm : hooks) {
+      const Value& hook = hm.hook;
+      std::string fail_policy = hook.get_string("failurePolicy", "Fail");
+      int timeout_s = hook.get("timeoutSeconds").is_int() ? static_cast<int>(hook.get("timeoutSeconds").as_int()) : 10;
+      std::string uid = crypto::uuid_v4();
+      Value req = Value::object();
+      req["uid"] = uid;
+      req["kind"] = Value::object({{"group", ti.rt.group}, {"version", ti.rt.version}, {"kind", ti.rt.kind}});
+      req["resource"] = Value::object({{"group", ti.rt.group}, {"version", ti.rt.version}, {"resource", ti.rt.plural}});
+      if (!sub.empty()) req["subResource"] = sub;
+      req["requestKind"] = req["kind"];
+      req["requestResource"] = req["resource"];
+      if (!sub.empty()) req["requestSubResource"] = sub;
+      req["name"] = name;
+      if (!ns.empty()) req["namespace"] = ns;
+      req["operation"] = op;
+      req["userInfo"] = user.to_json();
+      req["object"] = obj ? *obj : Value();
+      req["oldObject"] = old ? *old : Value();
+      req["dryRun"] = false;
+      std::string opts_kind = op == "CREATE" ? "CreateOptions" : op == "DELETE" ? "DeleteOptions" : "UpdateOptions";
+      req["options"] = Value::object({{"kind", opts_kind}, {"apiVersion", "meta.k8s.io/v1"}});
+      Value review = Value::object({{"kind", "AdmissionReview"}, {"apiVersion", "admission.k8s.io/v1"}, {"request", req}});
+      std::string err;
+      Value resp_review;
+      int64_t t0 = metrics::now_ns();
+      try {
+        std::string path;
+        auto client = hook_client(hook, path);
+        http::Headers h;
+        h.set("Content-Type", "application/json");
+        h.set("Accept", "application/json");
+        http::Response r = client->request("POST", path + "?timeout=" + std::to_string(timeout_s) + "s",
+                                           review.dump(), &h, timeout_s * 1000);
+        if (r.status != 200) {
+          err = "expected webhook response status code 200, got " + std::to_string(r.status) + ": " + r.body;
+        } else if (!json::try_parse(r.body, resp_review, &err)) {
+          err = "failed to parse webhook response: " + err;
+        }
+      } catch (const std::exception& e) {
+        err = e.what();
+      }
+      double secs = static_cast<double>(metrics::now_ns() - t0) * 1e-9;
+      ring.add(secs);
+      hist.observe(secs);
+      const Value& resp = resp_review.get("response");
+      if (err.empty() && !resp.is_object()) err = "webhook response was absent";
+      if (err.empty() && resp.get_string("uid") != uid) {
+        err = "expected response.uid=\"" + uid + "\", got \"" + resp.get_string("uid") + "\"";
+      }
+      if (!err.empty()) {
+        if (fail_policy == "Ignore") {
+          LOG_WARN("apiserver") << "failed calling webhook " << hm.name << " (ignored): " << err;
+          continue;
+        }
+        throw StatusError(500, "InternalError",
+                          "Internal error occurred: failed calling webhook \"" + hm.name + "\": " + err);
+      }
+      if (!resp.get("allowed").is_bool() || !resp.get("allowed").as_bool()) {
+        const Value& st = resp.get("status");
+        int code = st.get("code").is_int() ? static_cast<int>(st.get("code").as_int()) : 0;
+        if (code < 400) code = 400;
+        std::string reason = st.get_string("reason", code == 403 ? "Forbidden" : "BadRequest");
+        std::string msg = "admission webhook \"" + hm.name + "\" denied the request";
+        std::string m = st.get_string("message");
+        msg += m.empty() ? " without explanation" : ": " + m;
+        throw StatusError(code, reason, msg);
+      }
+      if (resp.get("patch").is_string() && obj) {
+        if (resp.get_string("patchType", "JSONPatch") != "JSONPatch") {
+          throw StatusError(500, "InternalError", "unsupported patchType from webhook " + hm.name);
+        }
+        Value patch;
+        std::string perr;
+        if (!json::try_parse(crypto::base64_decode(resp.get_string("patch")), patch, &perr)) {
+          throw StatusError(500, "InternalError", "invalid patch from webhook " + hm.name + ": " + perr);
+        }
+        try {
+          json::apply_patch(*obj, patch);
+        } catch (const std::exception& e) {
+          throw StatusError(500, "InternalError",
+                            "Internal error occurred: failed calling webhook \"" + hm.name + "\": " + e.what());
+        }
+      }
+    }
+  }
+
+  // ---------------------------------------------------------------- validation
+  void validate_object(const TypeInfo& ti, const std::string& name, const std::string& ns, const Value& obj) {
+    const Value& meta = obj.get("metadata");
+    if (ti.rt.plural == "namespaces") {
+      if (!dns1123_label(name)) {
+        throw invalid(ti.rt, name, "metadata.name: Invalid value: \"" + name +
+                                       "\": a lowercase RFC 1123 label must consist of lower case alphanumeric characters or '-', and must start and end with an alphanumeric character");
+      }
+    } else if (!dns1123_subdomain(name)) {
+      throw invalid(ti.rt, name, "metadata.name: Invalid value: \"" + name +
+                                     "\": a lowercase RFC 1123 subdomain must consist of lower case alphanumeric characters, '-' or '.', and must start and end with an alphanumeric character");
+    }
+    if (meta.get("namespace").is_string() && ti.rt.namespaced && meta.get_string("namespace") != ns) {
+      throw StatusError(400, "BadRequest", "the namespace of the provided object does not match the namespace sent on the request");
+    }
+    for (const auto& ref : meta.get("ownerReferences").items()) {
+      for (const char* f : {"apiVersion", "kind", "name", "uid"}) {
+        if (!ref.get(f).is_string() || ref.get_string(f).empty()) {
+          throw invalid(ti.rt, name, std::string("metadata.ownerReferences.") + f + ": Invalid value: \"\": " + f +
+                                         " must not be empty");
+        }
+      }
+    }
+    if (ti.rt.plural == "rolebindings" || ti.rt.plural == "clusterrolebindings") {
+      if (!obj.get("roleRef").is_object()) throw invalid(ti.rt, name, "roleRef: Required value");
+    }
+    if (opts.validate_schema && ti.custom && ti.schema.is_object()) {
+      auto errs = crd::validate(obj, ti.schema);
+      if (!errs.empty()) {
+        std::string msg;
+        for (size_t i = 0; i < errs.size() && i < 5; ++i) {
+          if (i) msg += ", ";
+          const auto& e = errs[i];
+          if (e.kind == "required") msg += e.path + ": Required value";
+          else msg += e.path + ": Invalid value: " + e.detail;
+        }
+        throw invalid(ti.rt, name, msg);
+      }
+    }
+  }
+
+  // ---------------------------------------------------------------- CRDs
+  void register_crd_locked(const Value& crd) {
+    const Value& spec = crd.get("spec");
+    std::string group = spec.get_string("group");
+    const Value& names = spec.get("names");
+    bool namespaced = spec.get_string("scope") == "Namespaced";
+    for (const auto& v : spec.get("versions").items()) {
+      if (v.get("served").is_bool() && !v.get("served").as_bool()) continue;
+      TypeInfo ti;
+      ti.rt.group = group;
+      ti.rt.version = v.get_string("name");
+      ti.rt.kind = names.get_string("kind");
+      ti.rt.plural = names.get_string("plural");
+      ti.rt.namespaced = namespaced;
+      ti.rt.has_status = v.get("subresources").get("status").is_object();
+      ti.schema = v.get("schema").get("openAPIV3Schema");
+      ti.custom = true;
+      types[ti.key()] = ti;
+    }
+  }
+
+  // ---------------------------------------------------------------- storage helpers
+  std::unordered_map<std::string, Stored>& bucket(const TypeInfo& ti) { return data[ti.key()]; }
+
+  bool namespace_exists_locked(const std::string& ns) {
+    auto& b = data[kube::types::Namespace.group + "/v1/namespaces"];
+    auto it = b.find(ns);
+    return it != b.end() && !it->second.obj->get("metadata").contains("deletionTimestamp");
+  }
+
+  static void render_managed(Value& obj, const Managers& m, const std::string& api_version) {
+    Value arr = Value::array();
+    for (const auto& [mgr, e] : m) {
+      if (e.fields.empty()) continue;
+      Value ent = Value::object({{"manager", mgr}, {"operation", e.operation},
+                                 {"apiVersion", e.api_version.empty() ? api_version : e.api_version},
+                                 {"time", e.time}, {"fieldsType", "FieldsV1"}, {"fieldsV1", fields_v1(e.fields)}});
+      if (!e.subresource.empty()) ent["subresource"] = e.subresource;
+      arr.push_back(ent);
+    }
+    if (arr.empty()) obj["metadata"].erase("managedFields");
+    else obj["metadata"]["managedFields"] = arr;
+  }
+
+  static Value strip_volatile(const Value& obj) {
+    Value v = obj;
+    if (Value* m = v.find_mut("metadata")) {
+      m->erase("managedFields");
+      m->erase("resourceVersion");
+    }
+    return v;
+  }
+
+  static bool spec_changed(const Value& a, const Value& b) {
+    Value x = a, y = b;
+    x.erase("metadata");
+    x.erase("status");
+    y.erase("metadata");
+    y.erase("status");
+    return !(x == y);
+  }
+
+  // Assign fields changed by a non-apply write to `manager`.
+  static void attribute_update(Managers& m, const std::string& manager, const Value& before, const Value& after,
+                               bool status_write, const std::string& api_version) {
+    FieldSet changed, removed;
+    diff_leaves(before, after, changed, removed, /*include_status=*/status_write);
+    if (status_write) {
+      FieldSet keep;
+      for (const auto& p : changed) {
+        if (p == "/status" || p.rfind("/status/", 0) == 0) keep.insert(p);
+      }
+      changed.swap(keep);
+    }
+    for (auto& [name, e] : m) {
+      for (const auto& p : changed) e.fields.erase(p);
+      for (const auto& p : removed) e.fields.erase(p);
+    }
+    if (!changed.empty()) {
+      auto& e = m[manager];
+      if (e.operation.empty()) {
+        e.operation = "Update";
+        e.api_version = api_version;
+      }
+      if (e.operation == "Apply") {
+        // an Update by an apply manager is tracked separately in k8s; keep it simple
+        e.operation = "Update";
+      }
+      e.time = now_rfc3339();
+      if (status_write) e.subresource = "status";
+      for (const auto& p : changed) e.fields.insert(p);
+    }
+    for (auto it = m.begin(); it != m.end();) {
+      if (it->second.fields.empty()) it = m.erase(it);
+      else ++it;
+    }
+  }
+
+  // Commits `obj` (already validated) under the lock. Returns stored object.
+  std::shared_ptr<const Value> commit_locked(const TypeInfo& ti, const std::string& ns, const std::string& name,
+                                            Value obj, Managers managers, const Stored* prev) {
+    uint64_t new_rv = ++rv;
+    Value& meta = obj["metadata"];
+    meta["resourceVersion"] = std::to_string(new_rv);
+    render_managed(obj, managers, ti.rt.api_version());
+    auto ptr = std::make_shared<const Value>(std::move(obj));
+    auto& b = bucket(ti);
+    Stored s;
+    s.obj = ptr;
+    s.rv = new_rv;
+    s.managers = std::move(managers);
+    std::string key = obj_key(ti.rt, ns, name);
+    b[key] = std::move(s);
+    by_uid[ptr->get("metadata").get_string("uid")] = {ti.key(), key};
+    emit_locked(prev ? "MODIFIED" : "ADDED", ti, ns, ptr, new_rv);
+    return ptr;
+  }
+
+  void erase_locked(const TypeInfo& ti, const std::string& ns, const std::string& name,
+                    std::vector<std::string>* deleted_uids) {
+    auto& b = bucket(ti);
+    std::string key = obj_key(ti.rt, ns, name);
+    auto it = b.find(key);
+    if (it == b.end()) return;
+    uint64_t new_rv = ++rv;
+    Value final_obj = *it->second.obj;
+    final_obj["metadata"]["resourceVersion"] = std::to_string(new_rv);
+    auto ptr = std::make_shared<const Value>(std::move(final_obj));
+    std::string uid = ptr->get("metadata").get_string("uid");
+    by_uid.erase(uid);
+    b.erase(it);
+    emit_locked("DELETED", ti, ns, ptr, new_rv);
+    if (deleted_uids) deleted_uids->push_back(uid);
+    // namespace deletion removes everything inside it
+    if (ti.rt.plural == "namespaces" && ti.rt.group.empty()) {
+      for (auto& [tk, tb] : data) {
+        auto tit = types.find(tk);
+        if (tit == types.end() || !tit->second.rt.namespaced) continue;
+        std::vector<std::string> victims;
+        for (auto& [k, st] : tb) {
+          if (st.obj->get("metadata").get_string("namespace") == name) victims.push_back(st.obj->get("metadata").get_string("name"));
+        }
+        for (const auto& v : victims) erase_locked(tit->second, name, v, deleted_uids);
+      }
+    }
+  }
+
+  bool dangling_owners_locked(const Value& obj) {
+    const Value& refs = obj.get("metadata").get("ownerReferences");
+    if (refs.empty()) return false;
+    for (const auto& r : refs.items()) {
+      if (by_uid.count(r.get_string("uid"))) return false;
+    }
+    return true;
+  }
+
+  // Garbage collector: delete dependents whose owners are all gone.
+  void collect_garbage_locked(std::vector<std::string> dead_uids) {
+    while (!dead_uids.empty()) {
+      std::set<std::string> dead(dead_uids.begin(), dead_uids.end());
+      dead_uids.clear();
+      std::vector<std::tuple<TypeInfo*, std::string, std::string>> victims;
+      for (auto& [tk, tb] : data) {
+        auto tit = types.find(tk);
+        if (tit == types.end()) continue;
+        for (auto& [k, st] : tb) {
+          const Value& refs = st.obj->get("metadata").get("ownerReferences");
+          if (refs.empty()) continue;
+          bool any_dead = false, any_alive = false;
+          for (const auto& r : refs.items()) {
+            std::string u = r.get_string("uid");
+            if (dead.count(u)) any_dead = true;
+            else if (by_uid.count(u)) any_alive = true;
+          }
+          if (any_dead && !any_alive) {
+            victims.emplace_back(&tit->second, st.obj->get("metadata").get_string("namespace"),
+                                 st.obj->get("metadata").get_string("name"));
+          }
+        }
+      }
+      for (auto& [ti, ns, name] : victims) erase_locked(*ti, ns, name, &dead_uids);
+    }
+  }
+
+  // ---------------------------------------------------------------- write path
+  using Compute = std::function<std::pair<Value, Managers>(const Stored* cur)>;
+
+  // Generic optimistic write: compute (unlocked) -> admission (unlocked) -> validate ->
+  // commit if the object did not change meanwhile (else retry).
+  WriteResult write(TypeInfo& ti, const std::string& ns, const std::string& name, const std::string& sub,
+                    const UserInfo& user, const Compute& compute, bool allow_create, bool is_status) {
+    for (int attempt = 0; attempt < 8; ++attempt) {
+      Stored cur_copy;
+      bool exists = false;
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        auto& b = bucket(ti);
+        auto it = b.find(obj_key(ti.rt, ns, name));
+        if (it != b.end()) {
+          cur_copy = it->second;
+          exists = true;
+        }
+      }
+      if (!exists && !allow_create) throw not_found(ti.rt, name);
+      auto [obj, managers] = compute(exists ? &cur_copy : nullptr);
+      std::string op = exists ? "UPDATE" : "CREATE";
+      if (!exists && ti.rt.namespaced) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!namespace_exists_locked(ns)) {
+          throw StatusError(404, "NotFound", "namespaces \"" + ns + "\" not found",
+                            Value::object({{"name", ns}, {"kind", "namespaces"}}));
+        }
+      }
+      // no-op short-circuit (before admission, like the apiserver's update path)
+      if (exists && strip_volatile(obj) == strip_volatile(*cur_copy.obj) && managers == cur_copy.managers) {
+        return {cur_copy.obj, 200};
+      }
+      call_webhooks(ti, sub, op, ns, name, &obj, exists ? cur_copy.obj.get() : nullptr, user);
+      // identity fields cannot be changed by mutation
+      obj["metadata"]["name"] = name;
+      if (ti.rt.namespaced) obj["metadata"]["namespace"] = ns;
+      else obj["metadata"].erase("namespace");
+      validate_object(ti, name, ns, obj);
+      std::lock_guard<std::mutex> lk(mu);
+      auto& b = bucket(ti);
+      auto it = b.find(obj_key(ti.rt, ns, name));
+      bool now_exists = it != b.end();
+      if (now_exists != exists || (exists && it->second.rv != cur_copy.rv)) continue;  // raced: retry
+      if (exists) {
+        // non-apply writers: attribute changed fields after mutation
+        if (exists && strip_volatile(obj) == strip_volatile(*cur_copy.obj) && managers == cur_copy.managers) {
+          return {cur_copy.obj, 200};
+        }
+        if (spec_changed(*cur_copy.obj, obj)) {
+          int64_t gen = cur_copy.obj->get("metadata").get("generation").is_int()
+                            ? cur_copy.obj->get("metadata").get("generation").as_int()
+                            : 1;
+          obj["metadata"]["generation"] = gen + 1;
+        }
+        // finalizer-gated deletion completes when the last finalizer is removed
+        if (obj.get("metadata").contains("deletionTimestamp") && obj.get("metadata").get("finalizers").empty()) {
+          std::vector<std::string> dead;
+          erase_locked(ti, ns, name, &dead);
+          collect_garbage_locked(dead);
+          return {cur_copy.obj, 200};
+        }
+        (void)is_status;
+        return {commit_locked(ti, ns, name, std::move(obj), std::move(managers), &it->second), 200};
+      }
+      if (ti.rt.plural == "customresourcedefinitions") register_crd_locked(obj);
+      auto created = commit_locked(ti, ns, name, std::move(obj), std::move(managers), nullptr);
+      // The garbage collector also removes dependents created with only dangling owner
+      // references (e.g. a controller re-applying a child right after its owner was
+      // deleted, before the owner's DELETED event reached it).
+      if (dangling_owners_locked(*created)) {
+        std::vector<std::string> dead;
+        erase_locked(ti, ns, name, &dead);
+        collect_garbage_locked(dead);
+      }
+      return {created, 201};
+    }
+    throw conflict(ti.rt, name);
+  }
+
+  // Fill server-populated metadata for a new object.
+  void init_new(const TypeInfo& ti, Value& obj, const std::string& ns, const std::string& name) {
+    obj["apiVersion"] = ti.rt.api_version();
+    obj["kind"] = ti.rt.kind;
+    Value& meta = obj["metadata"];
+    meta["name"] = name;
+    if (ti.rt.namespaced) meta["namespace"] = ns;
+    meta["uid"] = crypto::uuid_v4();
+    meta["creationTimestamp"] = now_rfc3339();
+    meta["generation"] = 1;
+    meta.erase("resourceVersion");
+    meta.erase("deletionTimestamp");
+    meta.erase("managedFields");
+    if (ti.rt.has_status && ti.custom) obj.erase("status");
+    if (ti.rt.plural == "namespaces" && ti.rt.group.empty()) {
+      obj["spec"] = Value::object({{"finalizers", Value::array({"kubernetes"})}});
+      obj["status"] = Value::object({{"phase", "Active"}});
+    }
+  }
+
+  // Carry server-owned metadata from the stored object into an updated one.
+  static void carry_meta(Value& obj, const Value& cur) {
+    const Value& cm = cur.get("metadata");
+    Value& m = obj["metadata"];
+    for (const char* f : {"uid", "creationTimestamp", "generation", "deletionTimestamp"}) {
+      if (cm.contains(f)) m[f] = cm.get(f);
+      else m.erase(f);
+    }
+    obj["apiVersion"] = cur.get("apiVersion");
+    obj["kind"] = cur.get("kind");
+  }
+
+  std::string field_manager(const http::Request& req, const std::string& dflt) {
+    std::string fm = req.query_param("fieldManager");
+    if (!fm.empty()) return fm;
+    std::string ua = req.headers.get_or("User-Agent", dflt);
+    size_t slash = ua.find('/');
+    return slash == std::string::npos ? ua : ua.substr(0, slash);
+  }
+
+  Value parse_body(const http::Request& req) {
+    Value v;
+    std::string err;
+    std::string ct = req.headers.get_or("Content-Type");
+    if (ct.find("yaml") != std::string::npos && !req.body.empty() && req.body[0] != '{') {
+      try {
+        return yaml::parse(req.body);
+      } catch (const std::exception& e) {
+        throw StatusError(400, "BadRequest", std::string("error decoding YAML: ") + e.what());
+      }
+    }
+    if (!json::try_parse(req.body, v, &err)) throw StatusError(400, "BadRequest", "couldn't get version/kind; json parse error: " + err);
+    return v;
+  }
+
+  // ---------------------------------------------------------------- verbs
+  void do_create(ParsedPath& p, const http::Request& req, const UserInfo& user, http::ResponseWriter& w) {
+    Value body = parse_body(req);
+    if (!body.is_object()) throw StatusError(400, "BadRequest", "object must be a JSON object");
+    std::string name = body.get("metadata").get_string("name");
+    if (name.empty()) {
+      std::string gen = body.get("metadata").get_string("generateName");
+      if (gen.empty()) throw invalid(p.ti->rt, "", "metadata.name: Required value: name or generateName is required");
+      static const char* alnum = "bcdfghjklmnpqrstvwxz2456789";
+      std::string rnd = crypto::random_bytes(5);
+      name = gen;
+      for (unsigned char c : rnd) name.push_back(alnum[c % 27]);
+    }
+    std::string manager = field_manager(req, "unknown");
+    auto res = write(*p.ti, p.ns, name, "", user,
+                     [&](const Stored* cur) -> std::pair<Value, Managers> {
+                       if (cur) throw already_exists(p.ti->rt, name);
+                       Value obj = body;
+                       init_new(*p.ti, obj, p.ns, name);
+                       Managers m;
+                       attribute_update(m, manager, Value::object(), obj, false, p.ti->rt.api_version());
+                       return {obj, m};
+                     },
+                     true, false);
+    w.send_json(res.code, res.obj->dump());
+  }
+
+  void do_update(ParsedPath& p, const http::Request& req, const UserInfo& user, http::ResponseWriter& w) {
+    Value body = parse_body(req);
+    if (!body.is_object()) throw StatusError(400, "BadRequest", "object must be a JSON object");
+    std::string bname = body.get("metadata").get_string("name");
+    if (!bname.empty() && bname != p.name) {
+      throw StatusError(400, "BadRequest", "the name of the object (" + bname +
+                                               ") does not match the name on the URL (" + p.name + ")");
+    }
+    bool is_status = p.sub == "status";
+    std::string manager = field_manager(req, "unknown");
+    auto res = write(*p.ti, p.ns, p.name, p.sub, user,
+                     [&](const Stored* cur) -> std::pair<Value, Managers> {
+                       std::string want_rv = body.get("metadata").get_string("resourceVersion");
+                       if (!want_rv.empty() && want_rv != cur->obj->get("metadata").get_string("resourceVersion")) {
+                         throw conflict(p.ti->rt, p.name);
+                       }
+                       Value obj;
+                       if (is_status) {
+                         obj = *cur->obj;
+                         if (body.contains("status")) obj["status"] = body.get("status");
+                         else obj.erase("status");
+                       } else {
+                         obj = body;
+                         carry_meta(obj, *cur->obj);
+                         if (p.ti->rt.has_status) {
+                           if (cur->obj->contains("status")) obj["status"] = cur->obj->get("status");
+                           else obj.erase("status");
+                         }
+                       }
+                       Managers m = cur->managers;
+                       attribute_update(m, manager, *cur->obj, obj, is_status, p.ti->rt.api_version());
+                       return {obj, m};
+                     },
+                     false, is_status);
+    w.send_json(res.code, res.obj->dump());
+  }
+
+  std::pair<Value, Managers> apply_ssa(const TypeInfo& ti, const Stored* cur, const Value& config,
+                                       const std::string& manager, bool force, bool is_status,
+                                       const std::string& ns, const std::string& name) {
+    FieldSet cfg_fields = leaves(config, is_status);
+    if (is_status) {
+      FieldSet only;
+      for (const auto& f : cfg_fields) {
+        if (f == "/status" || f.rfind("/status/", 0) == 0) only.insert(f);
+      }
+      cfg_fields.swap(only);
+    }
+    Value live;
+    Managers m;
+    if (cur) {
+      live = *cur->obj;
+      m = cur->managers;
+    } else {
+      live = Value::object();
+      init_new(ti, live, ns, name);
+    }
+    // conflicts with other managers owning a field with a different value
+    std::vector<std::pair<std::string, std::string>> conflicts;
+    for (const auto& f : cfg_fields) {
+      const Value* want = get_path(config, f);
+      const Value* have = get_path(live, f);
+      for (auto& [other, e] : m) {
+        if (other == manager || !e.fields.count(f)) continue;
+        if (have && want && *have == *want) continue;
+        conflicts.emplace_back(other, f);
+      }
+    }
+    if (!conflicts.empty() && !force) {
+      std::string msg = "Apply failed with " + std::to_string(conflicts.size()) + " conflict" +
+                        (conflicts.size() > 1 ? "s" : "") + ": ";
+      for (size_t i = 0; i < conflicts.size(); ++i) {
+        if (i) msg += "; ";
+        msg += "conflict with \"" + conflicts[i].first + "\": " + display_path(conflicts[i].second);
+      }
+      throw StatusError(409, "Conflict", msg);
+    }
+    if (force) {
+      for (const auto& [other, f] : conflicts) m[other].fields.erase(f);
+    }
+    // prune fields this manager owned but no longer applies (and nobody else owns)
+    if (auto it = m.find(manager); it != m.end()) {
+      for (const auto& f : it->second.fields) {
+        if (cfg_fields.count(f)) continue;
+        bool other_owner = false;
+        for (auto& [other, e] : m) {
+          if (other != manager && e.fields.count(f)) other_owner = true;
+        }
+        if (!other_owner) remove_path(live, f);
+      }
+    }
+    for (const auto& f : cfg_fields) {
+      if (const Value* v = get_path(config, f)) set_path(live, f, *v);
+    }
+    // shared fields: other managers co-own identical values
+    auto& me = m[manager];
+    me.operation = "Apply";
+    me.api_version = ti.rt.api_version();
+    me.time = now_rfc3339();
+    me.subresource = is_status ? "status" : "";
+    me.fields = cfg_fields;
+    for (auto it = m.begin(); it != m.end();) {
+      if (it->second.fields.empty()) it = m.erase(it);
+      else ++it;
+    }
+    if (cur && ti.rt.has_status && !is_status) {
+      if (cur->obj->contains("status")) live["status"] = cur->obj->get("status");
+    }
+    return {live, m};
+  }
+
+  void do_patch(ParsedPath& p, const http::Request& req, const UserInfo& user, http::ResponseWriter& w) {
+    std::string ct = req.headers.get_or("Content-Type");
+    bool is_status = p.sub == "status";
+    bool is_apply = ct.find("apply-patch") != std::string::npos;
+    std::string manager = field_manager(req, is_apply ? "" : "unknown");
+    if (is_apply && req.query_param("fieldManager").empty()) {
+      throw StatusError(400, "BadRequest", "PatchOptions.meta.k8s.io \"\" is invalid: fieldManager: Required value: is required for apply patch");
+    }
+    Value patch = parse_body(req);
+    bool force = req.query_param("force") == "true";
+    auto res = write(*p.ti, p.ns, p.name, p.sub, user,
+                     [&](const Stored* cur) -> std::pair<Value, Managers> {
+                       if (is_apply) {
+                         std::string pname = patch.get("metadata").get_string("name");
+                         if (!pname.empty() && pname != p.name) {
+                           throw StatusError(400, "BadRequest", "the name of the object (" + pname +
+                                                                    ") does not match the name on the URL (" + p.name + ")");
+                         }
+                         return apply_ssa(*p.ti, cur, patch, manager, force, is_status, p.ns, p.name);
+                       }
+                       Value obj = *cur->obj;
+                       try {
+                         if (ct.find("json-patch") != std::string::npos) {
+                           json::apply_patch(obj, patch);
+                         } else {
+                           json::apply_merge_patch(obj, patch);
+                         }
+                       } catch (const json::PatchError& e) {
+                         throw StatusError(422, "Invalid", std::string("the server rejected our request due to an error in our request: ") + e.what());
+                       }
+                       std::string want_rv = obj.get("metadata").get_string("resourceVersion");
+                       if (!want_rv.empty() && want_rv != cur->obj->get("metadata").get_string("resourceVersion")) {
+                         throw conflict(p.ti->rt, p.name);
+                       }
+                       if (is_status) {
+                         Value keep = *cur->obj;
+                         if (obj.contains("status")) keep["status"] = obj.get("status");
+                         else keep.erase("status");
+                         obj = keep;
+                       } else {
+                         carry_meta(obj, *cur->obj);
+                         if (p.ti->rt.has_status) {
+                           if (cur->obj->contains("status")) obj["status"] = cur->obj->get("status");
+                           else obj.erase("status");
+                         }
+                       }
+                       Managers m = cur->managers;
+                       attribute_update(m, manager, *cur->obj, obj, is_status, p.ti->rt.api_version());
+                       return {obj, m};
+                     },
+                     is_apply, is_status);
+    w.send_json(res.code, res.obj->dump());
+  }
+
+  void do_delete(ParsedPath& p, const http::Request& req, const UserInfo& user, http::ResponseWriter& w) {
+    std::shared_ptr<const Value> cur;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      auto& b = bucket(*p.ti);
+      auto it = b.find(obj_key(p.ti->rt, p.ns, p.name));
+      if (it == b.end()) throw not_found(p.ti->rt, p.name);
+      cur = it->second.obj;
+    }
+    call_webhooks(*p.ti, "", "DELETE", p.ns, p.name, nullptr, cur.get(), user);
+    std::lock_guard<std::mutex> lk(mu);
+    auto& b = bucket(*p.ti);
+    auto it = b.find(obj_key(p.ti->rt, p.ns, p.name));
+    if (it == b.end()) throw not_found(p.ti->rt, p.name);
+    const Value& meta = it->second.obj->get("metadata");
+    if (!meta.get("finalizers").empty()) {
+      if (!meta.contains("deletionTimestamp")) {
+        Value obj = *it->second.obj;
+        obj["metadata"]["deletionTimestamp"] = now_rfc3339();
+        obj["metadata"]["deletionGracePeriodSeconds"] = 0;
+        auto ptr = commit_locked(*p.ti, p.ns, p.name, std::move(obj), it->second.managers, &it->second);
+        w.send_json(202, ptr->dump());
+        return;
+      }
+      w.send_json(202, it->second.obj->dump());
+      return;
+    }
+    Value last = *it->second.obj;
+    std::vector<std::string> dead;
+    erase_locked(*p.ti, p.ns, p.name, &dead);
+    collect_garbage_locked(dead);
+    (void)req;
+    w.send_json(200, status_body(200, "", "").dump());
+  }
+
+  void do_get(ParsedPath& p, http::ResponseWriter& w) {
+    std::shared_ptr<const Value> obj;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      auto& b = bucket(*p.ti);
+      auto it = b.find(obj_key(p.ti->rt, p.ns, p.name));
+      if (it == b.end()) throw not_found(p.ti->rt, p.name);
+      obj = it->second.obj;
+    }
+    w.send_json(200, obj->dump());
+  }
+
+  void do_list(ParsedPath& p, const http::Request& req, http::ResponseWriter& w) {
+    auto sel = parse_selector(req.query_param("labelSelector"));
+    auto ff = parse_field_selector(req.query_param("fieldSelector"));
+    std::vector<std::shared_ptr<const Value>> items;
+    uint64_t list_rv;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      list_rv = rv;
+      for (auto& [k, st] : bucket(*p.ti)) {
+        const Value& meta = st.obj->get("metadata");
+        if (!p.ns.empty() && meta.get_string("namespace") != p.ns) continue;
+        if (!ff.name.empty() && meta.get_string("name") != ff.name) continue;
+        if (!ff.ns.empty() && meta.get_string("namespace") != ff.ns) continue;
+        if (!sel.empty() && !selector_matches(sel, *st.obj)) continue;
+        items.push_back(st.obj);
+      }
+    }
+    std::sort(items.begin(), items.end(), [](const auto& a, const auto& b) {
+      const Value& ma = a->get("metadata");
+      const Value& mb = b->get("metadata");
+      return std::make_pair(ma.get_string("namespace"), ma.get_string("name")) <
+             std::make_pair(mb.get_string("namespace"), mb.get_string("name"));
+    });
+    std::string out = "{\"apiVersion\":" + json::quote(p.ti->rt.api_version()) + ",\"kind\":" +
+                      json::quote(p.ti->rt.kind + "List") + ",\"metadata\":{\"resourceVersion\":\"" +
+                      std::to_string(list_rv) + "\"},\"items\":[";
+    for (size_t i = 0; i < items.size(); ++i) {
+      if (i) out.push_back(',');
+      items[i]->dump_to(out);
+    }
+    out += "]}";
+    w.send_json(200, out);
+  }
+
+  void do_watch(ParsedPath& p, const http::Request& req, http::ResponseWriter& w) {
+    WatchSub sub;
+    sub.type_key = p.ti->key();
+    sub.ns = p.ns;
+    sub.sel = parse_selector(req.query_param("labelSelector"));
+    sub.fields = parse_field_selector(req.query_param("fieldSelector"));
+    if (!sub.fields.ns.empty()) sub.ns = sub.fields.ns;
+    std::string rv_s = req.query_param("resourceVersion");
+    int timeout_s = opts.max_watch_seconds;
+    if (req.has_query_param("timeoutSeconds")) timeout_s = std::min(timeout_s, std::atoi(req.query_param("timeoutSeconds").c_str()));
+    bool bookmarks = req.query_param("allowWatchBookmarks") == "true";
+    std::vector<std::shared_ptr<const std::string>> initial;
+    bool gone = false;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      uint64_t from = rv_s.empty() ? 0 : std::strtoull(rv_s.c_str(), nullptr, 10);
+      if (rv_s.empty() || rv_s == "0") {
+        for (auto& [k, st] : bucket(*p.ti)) {
+          const Value& meta = st.obj->get("metadata");
+          if (!sub.ns.empty() && meta.get_string("namespace") != sub.ns) continue;
+          if (!sub.fields.name.empty() && meta.get_string("name") != sub.fields.name) continue;
+          if (!sub.sel.empty() && !selector_matches(sub.sel, *st.obj)) continue;
+          std::string line = "{\"type\":\"ADDED\",\"object\":";
+          st.obj->dump_to(line);
+          line += "}\n";
+          initial.push_back(std::make_shared<const std::string>(std::move(line)));
+        }
+      } else if (from < compacted_rv) {
+        gone = true;
+      } else {
+        auto it = std::upper_bound(history.begin(), history.end(), from,
+                                   [](uint64_t v, const std::shared_ptr<const EventRec>& e) { return v < e->rv; });
+        for (; it != history.end(); ++it) {
+          const auto& e = *it;
+          if (e->type_key != sub.type_key) continue;
+          if (!sub.ns.empty() && e->ns != sub.ns) continue;
+          if (!sub.fields.name.empty() && e->obj->get("metadata").get_string("name") != sub.fields.name) continue;
+          if (!sub.sel.empty() && !selector_matches(sub.sel, *e->obj)) continue;
+          initial.push_back(e->line);
+        }
+      }
+      if (!gone) watches.insert(&sub);
+    }
+    if (!w.start_chunked(200, "application/json")) {
+      std::lock_guard<std::mutex> lk(mu);
+      watches.erase(&sub);
+      return;
+    }
+    if (gone) {
+      Value ev = Value::object({{"type", "ERROR"},
+                                {"object", status_body(410, "Expired", "too old resource version: " + rv_s + " (" +
+                                                                           std::to_string(compacted_rv) + ")")}});
+      w.write_chunk(ev.dump() + "\n");
+      w.end_chunked();
+      return;
+    }
+    bool ok = true;
+    for (auto& l : initial) {
+      if (!(ok = w.write_chunk(*l))) break;
+    }
+    auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(timeout_s);
+    auto next_bookmark = std::chrono::steady_clock::now() + std::chrono::milliseconds(opts.bookmark_interval_ms);
+    while (ok && !w.stopping()) {
+      std::vector<std::shared_ptr<const EventRec>> batch;
+      bool closed = false, overflow = false;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        sub.cv.wait_for(lk, std::chrono::milliseconds(500), [&] { return !sub.q.empty() || sub.closed || sub.overflow; });
+        batch.assign(sub.q.begin(), sub.q.end());
+        sub.q.clear();
+        closed = sub.closed;
+        overflow = sub.overflow;
+      }
+      if (!batch.empty()) {
+        std::string buf;
+        for (auto& e : batch) buf += *e->line;
+        if (!w.write_chunk(buf)) break;
+      }
+      if (closed || overflow) break;
+      auto now = std::chrono::steady_clock::now();
+      if (now >= deadline) break;
+      if (bookmarks && now >= next_bookmark) {
+        uint64_t cur_rv;
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          cur_rv = rv;
+        }
+        Value bm = Value::object({{"type", "BOOKMARK"},
+                                  {"object", Value::object({{"kind", p.ti->rt.kind},
+                                                            {"apiVersion", p.ti->rt.api_version()},
+                                                            {"metadata", Value::object({{"resourceVersion", std::to_string(cur_rv)}})}})}});
+        if (!w.write_chunk(bm.dump() + "\n")) break;
+        next_bookmark = now + std::chrono::milliseconds(opts.bookmark_interval_ms);
+      }
+      if (batch.empty() && w.peer_closed()) break;
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      watches.erase(&sub);
+    }
+    w.end_chunked();
+  }
+
+  // ---------------------------------------------------------------- discovery
+  void discovery(const std::string& path, http::ResponseWriter& w) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (path == "/api") {
+      w.send_json(200, Value::object({{"kind", "APIVersions"}, {"versions", Value::array({"v1"})}}).dump());
+      return;
+    }
+    if (path == "/apis") {
+      std::map<std::string, std::set<std::string>> groups;
+      for (auto& [k, ti] : types) {
+        if (!ti.rt.group.empty()) groups[ti.rt.group].insert(ti.rt.version);
+      }
+      Value gl = Value::array();
+      for (auto& [g, vs] : groups) {
+        Value versions = Value::array();
+        for (auto& v : vs) versions.push_back(Value::object({{"groupVersion", g + "/" + v}, {"version", v}}));
+        gl.push_back(Value::object({{"name", g}, {"versions", versions}, {"preferredVersion", versions[0]}}));
+      }
+      w.send_json(200, Value::object({{"kind", "APIGroupList"}, {"apiVersion", "v1"}, {"groups", gl}}).dump());
+      return;
+    }
+    std::string gv = path.rfind("/api/", 0) == 0 ? path.substr(5) : path.substr(6);
+    Value res = Value::array();
+    for (auto& [k, ti] : types) {
+      if (ti.rt.api_version() != gv) continue;
+      Value verbs = Value::array({"create", "delete", "get", "list", "patch", "update", "watch"});
+      res.push_back(Value::object({{"name", ti.rt.plural}, {"namespaced", ti.rt.namespaced}, {"kind", ti.rt.kind}, {"verbs", verbs}}));
+      if (ti.rt.has_status) {
+        res.push_back(Value::object({{"name", ti.rt.plural + "/status"}, {"namespaced", ti.rt.namespaced}, {"kind", ti.rt.kind},
+                                     {"verbs", Value::array({"get", "patch", "update"})}}));
+      }
+    }
+    if (res.empty()) throw StatusError(404, "NotFound", "the server could not find the requested resource");
+    w.send_json(200, Value::object({{"kind", "APIResourceList"}, {"apiVersion", "v1"}, {"groupVersion", gv}, {"resources", res}}).dump());
+  }
+
+  // ---------------------------------------------------------------- faults
+  bool inject_fault(const http::Request& req, http::ResponseWriter& w) {
+    FaultRule hit;
+    bool found = false;
+    {
+      std::lock_guard<std::mutex> lk(fault_mu);
+      for (auto& f : faults) {
+        if (f.remaining == 0) continue;
+        if (!f.method.empty() && f.method != req.method) continue;
+        std::string target = req.path + (req.query.empty() ? "" : "?" + req.query);
+        if (!std::regex_search(target, f.path)) continue;
+        if (f.remaining > 0) --f.remaining;
+        hit = f;
+        found = true;
+        break;
+      }
+    }
+    if (!found) return false;
+    if (hit.delay_ms > 0) std::this_thread::sleep_for(std::chrono::milliseconds(hit.delay_ms));
+    if (hit.status > 0) {
+      std::string reason = hit.status == 409 ? "Conflict" : hit.status == 410 ? "Expired" : hit.status >= 500 ? "InternalError" : "BadRequest";
+      w.send_json(hit.status, status_body(hit.status, reason, hit.message.empty() ? "injected fault" : hit.message).dump());
+      return true;
+    }
+    return false;
+  }
+
+  void control(http::Request& req, http::ResponseWriter& w) {
+    if (req.path == "/_kl/faults" && req.method == "POST") {
+      Value rules = json::parse(req.body);
+      std::lock_guard<std::mutex> lk(fault_mu);
+      if (req.query_param("append") != "true") faults.clear();
+      for (const auto& r : rules.items()) {
+        FaultRule f;
+        f.method = r.get_string("method");
+        f.path_src = r.get_string("path", ".*");
+        f.path = std::regex(f.path_src);
+        f.status = r.get("status").is_int() ? static_cast<int>(r.get("status").as_int()) : 0;
+        f.delay_ms = r.get("delay_ms").is_int() ? static_cast<int>(r.get("delay_ms").as_int()) : 0;
+        f.remaining = r.get("count").is_int() ? static_cast<int>(r.get("count").as_int()) : -1;
+        f.message = r.get_string("message");
+        faults.push_back(std::move(f));
+      }
+      w.send_json(200, "{}");
+      return;
+    }
+    if (req.path == "/_kl/faults" && req.method == "DELETE") {
+      std::lock_guard<std::mutex> lk(fault_mu);
+      faults.clear();
+      w.send_json(200, "{}");
+      return;
+    }
+    if (req.path == "/_kl/compact" && req.method == "POST") {
+      std::lock_guard<std::mutex> lk(mu);
+      compacted_rv = rv;
+      history.clear();
+      w.send_json(200, Value::object({{"compacted_rv", static_cast<unsigned long long>(compacted_rv)}}).dump());
+      return;
+    }
+    if (req.path == "/_kl/drop-watches" && req.method == "POST") {
+      std::lock_guard<std::mutex> lk(mu);
+      size_t n = watches.size();
+      for (WatchSub* ws : watches) {
+        ws->closed = true;
+        ws->cv.notify_one();
+      }
+      w.send_json(200, Value::object({{"dropped", static_cast<unsigned long long>(n)}}).dump());
+      return;
+    }
+    if (req.path == "/_kl/stats") {
+      std::lock_guard<std::mutex> lk(mu);
+      Value counts = Value::object();
+      size_t total = 0;
+      for (auto& [k, b] : data) {
+        counts[k] = static_cast<unsigned long long>(b.size());
+        total += b.size();
+      }
+      w.send_json(200, Value::object({{"resourceVersion", static_cast<unsigned long long>(rv)},
+                                      {"objects", static_cast<unsigned long long>(total)},
+                                      {"watches", static_cast<unsigned long long>(watches.size())},
+                                      {"requests", static_cast<unsigned long long>(requests.load())},
+                                      {"by_type", counts}}).dump());
+      return;
+    }
+    w.send(404, "not found\n");
+  }
+
+  // ---------------------------------------------------------------- dispatch
+  void handle(http::Request& req, http::ResponseWriter& w) {
+    requests.fetch_add(1, std::memory_order_relaxed);
+    try {
+      if (inject_fault(req, w)) return;
+      UserInfo user = authenticate(req);
+      if (req.path == "/api" || req.path == "/apis") {
+        discovery(req.path, w);
+        return;
+      }
+      ParsedPath p;
+      std::string group, version;
+      std::vector<std::string> rest;
+      if (!parse_path(req.path, p, group, version, rest)) {
+        discovery(req.path, w);
+        return;
+      }
+      if (!p.sub.empty() && p.sub != "status") throw StatusError(404, "NotFound", "subresource not supported: " + p.sub);
+      if (!p.sub.empty() && !p.ti->rt.has_status) throw StatusError(404, "NotFound", "the server could not find the requested resource");
+      const std::string& m = req.method;
+      if (p.collection) {
+        if (m == "GET") {
+          std::string wq = req.query_param("watch");
+          if (wq == "1" || wq == "true") do_watch(p, req, w);
+          else do_list(p, req, w);
+        } else if (m == "POST") {
+          do_create(p, req, user, w);
+        } else {
+          throw StatusError(405, "MethodNotAllowed", "method not allowed");
+        }
+        return;
+      }
+      if (m == "GET") do_get(p, w);
+      else if (m == "PUT") do_update(p, req, user, w);
+      else if (m == "PATCH") do_patch(p, req, user, w);
+      else if (m == "DELETE") do_delete(p, req, user, w);
+      else throw StatusError(405, "MethodNotAllowed", "method not allowed");
+    } catch (const StatusError& e) {
+      if (!w.sent()) w.send_json(e.code, status_body(e.code, e.reason, e.what(), e.details).dump());
+    } catch (const std::exception& e) {
+      if (!w.sent()) w.send_json(500, status_body(500, "InternalError", e.what()).dump());
+    }
+  }
+};
+
+ApiServer::ApiServer(Options o) : impl_(std::make_unique<Impl>(std::move(o))) {}
+ApiServer::~ApiServer() { stop(); }
+
+void ApiServer::start() {
+  http::ServerOptions so;
+  so.addr = impl_->opts.addr;
+  so.port = impl_->opts.port;
+  so.name = "apiserver";
+  so.idle_timeout_ms = 300000;
+  if (!impl_->opts.tls_cert_file.empty()) {
+    so.tls = net::TlsContext::server_from_files(impl_->opts.tls_cert_file, impl_->opts.tls_key_file);
+  }
+  impl_->server = std::make_unique<http::Server>(so);
+  Impl* im = impl_.get();
+  http::add_standard_routes(*impl_->server);
+  impl_->server->handle("GET", "/healthz", [](http::Request&, http::ResponseWriter& w) { w.send(200, "ok"); });
+  impl_->server->handle("GET", "/readyz", [](http::Request&, http::ResponseWriter& w) { w.send(200, "ok"); });
+  impl_->server->handle("GET", "/livez", [](http::Request&, http::ResponseWriter& w) { w.send(200, "ok"); });
+  impl_->server->handle("GET", "/version", [](http::Request&, http::ResponseWriter& w) {
+    w.send_json(200, Value::object({{"major", "1"}, {"minor", "26"}, {"gitVersion", "v1.26.0-kube-lite"}, {"platform", "linux/amd64"}}).dump());
+  });
+  impl_->server->handle_prefix("/api", [im](http::Request& r, http::ResponseWriter& w) { im->handle(r, w); });
+  impl_->server->handle_prefix("/_kl/", [im](http::Request& r, http::ResponseWriter& w) { im->control(r, w); });
+  impl_->server->start();
+}
+
+uint16_t ApiServer::port() const { return impl_->server ? impl_->server->port() : 0; }
+
+void ApiServer::stop() {
+  if (impl_ && impl_->server) {
+    {
+      std::lock_guard<std::mutex> lk(impl_->mu);
+      for (WatchSub* ws : impl_->watches) {
+        ws->closed = true;
+        ws->cv.notify_one();
+      }
+    }
+    impl_->server->stop(std::chrono::milliseconds(2000));
+    impl_->server.reset();
+  }
+}
+
+}  // namespace bgc::apiserver

@@ -1,0 +1,56 @@
+// kube-lite: an in-process Kubernetes API server for tests, the bench harness and
+// offline e2e runs (north-star component N7; no kind/etcd exist in this environment).
+//
+// Fidelity targets (what the controller/admission/synchronizer/node-agent rely on):
+//  * REST: GET/LIST/WATCH (resourceVersion resume, bookmarks, 410 Gone after compaction),
+//    POST, PUT (optimistic concurrency), PATCH (json-patch, merge-patch,
+//    strategic-merge as merge, apply-patch+yaml = server-side apply with field managers,
+//    conflicts and force), DELETE (finalizers, ownerReference GC, namespace cascade);
+//  * status subresource semantics for CRDs and built-ins;
+//  * CustomResourceDefinitions registered dynamically, with structural schema
+//    validation (422 Invalid);
+//  * MutatingWebhookConfiguration callouts over TLS with caBundle verification,
+//    JSONPatch responses, timeouts and failurePolicy (the reference's webhook path,
+//    charts/.../templates/webhook.yaml:11-27);
+//  * static-token authentication (kube-apiserver --token-auth-file format) and
+//    impersonation for system:masters;
+//  * fault injection (/_kl/faults) and watch compaction/drops for resilience tests.
+#pragma once
+
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <string>
+
+namespace bgc::apiserver {
+
+struct Options {
+  std::string addr = "127.0.0.1";
+  uint16_t port = 0;
+  std::string token_file;         // CSV: token,user,uid,"group1,group2"
+  bool anonymous_admin = true;    // no token => system:admin in system:masters
+  std::string tls_cert_file;      // serve HTTPS when set
+  std::string tls_key_file;
+  // "namespace/service" -> "host:port": where a webhook's clientConfig.service is reachable.
+  std::map<std::string, std::string> service_overrides;
+  size_t history_limit = 200000;  // watch cache events kept for resume
+  int bookmark_interval_ms = 60000;
+  bool validate_schema = true;
+  int max_watch_seconds = 1800;
+};
+
+class ApiServer {
+ public:
+  explicit ApiServer(Options o);
+  ~ApiServer();
+  void start();
+  uint16_t port() const;
+  void stop();
+
+  struct Impl;
+
+ private:
+  std::unique_ptr<Impl> impl_;
+};
+
+}  // namespace bgc::apiserver

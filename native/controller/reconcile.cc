@@ -1,0 +1,185 @@
+#include "controller/reconcile.h"
+
+#include <cctype>
+#include <future>
+
+#include "core/log.h"
+#include "core/metrics.h"
+
+namespace bgc::controller {
+
+using json::Value;
+namespace types = kube::types;
+
+Config Config::from_env(const EnvConfig& env) {
+  Config c;
+  c.listen_addr = env.str("listen_addr");
+  c.listen_port = env.u16("listen_port");
+  c.workers = static_cast<int>(env.u64_or("workers", 16));
+  c.skip_unchanged = env.boolean_or("skip_unchanged", true);
+  c.parallel_children = env.boolean_or("parallel_children", true);
+  c.requeue_secs = static_cast<int64_t>(env.u64_or("requeue_secs", 30));
+  c.error_requeue_ms = static_cast<int64_t>(env.u64_or("error_requeue_ms", 3000));
+  c.leader_election = env.boolean_or("leader_election", false);
+  c.lease_namespace = env.str_or("lease_namespace", "default");
+  c.lease_name = env.str_or("lease_name", "bacchus-gpu-controller");
+  return c;
+}
+
+Value controller_owner_ref(const Value& ub) {
+  const Value& meta = ub.get("metadata");
+  if (!meta.get("uid").is_string() || !meta.get("name").is_string()) {
+    throw std::runtime_error("missing object key: .metadata.uid");
+  }
+  // kube `controller_owner_ref`: apiVersion, kind, name, uid, controller=true
+  // (blockOwnerDeletion unset), serialized in k8s-openapi field order.
+  return Value::object({{"apiVersion", "bacchus.io/v1"},
+                        {"controller", true},
+                        {"kind", "UserBootstrap"},
+                        {"name", meta.get_string("name")},
+                        {"uid", meta.get_string("uid")}});
+}
+
+std::vector<DesiredChild> desired_children(const Value& ub) {
+  const Value& name_v = ub.get("metadata").get("name");
+  if (!name_v.is_string()) throw std::runtime_error("missing object key: .metadata.name");
+  std::string name = name_v.as_string();
+  for (auto& ch : name) ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
+  Value oref = controller_owner_ref(ub);
+  auto meta = [&]() {
+    return Value::object({{"name", name}, {"ownerReferences", Value::array({oref})}});
+  };
+  std::vector<DesiredChild> out;
+  // (1) Namespace (controller.rs:69-87)
+  out.push_back({&types::Namespace, "", name,
+                 Value::object({{"apiVersion", "v1"}, {"kind", "Namespace"}, {"metadata", meta()}})});
+  const Value& spec = ub.get("spec");
+  // (2) ResourceQuota (controller.rs:89-110)
+  if (const Value* q = spec.find("quota"); q && !q->is_null()) {
+    out.push_back({&types::ResourceQuota, name, name,
+                   Value::object({{"apiVersion", "v1"}, {"kind", "ResourceQuota"}, {"metadata", meta()}, {"spec", *q}})});
+  }
+  // (3) Role: the user's object with ownerReferences overwritten (controller.rs:112-124)
+  if (const Value* r = spec.find("role"); r && !r->is_null()) {
+    Value role = Value::object({{"apiVersion", "rbac.authorization.k8s.io/v1"}, {"kind", "Role"}});
+    Value m = r->get("metadata").is_object() ? r->get("metadata") : Value::object();
+    m["ownerReferences"] = Value::array({oref});
+    role["metadata"] = m;
+    if (const Value* rules = r->find("rules"); rules && !rules->is_null()) role["rules"] = *rules;
+    // The URL name is the namespace name; a Role whose metadata.name differs is
+    // rejected by the apiserver on every reconcile, exactly like the reference (Q9).
+    out.push_back({&types::Role, name, name, role});
+  }
+  // (4) RoleBinding, gated on status.synchronized_with_sheet (controller.rs:126-152)
+  if (const Value* rb = spec.find("rolebinding"); rb && !rb->is_null()) {
+    const Value& st = ub.get("status");
+    if (st.is_object() && st.get("synchronized_with_sheet").is_bool() && st.get("synchronized_with_sheet").as_bool()) {
+      Value body = Value::object({{"apiVersion", "rbac.authorization.k8s.io/v1"}, {"kind", "RoleBinding"}, {"metadata", meta()}});
+      body["roleRef"] = rb->get("role_ref");
+      if (const Value* s = rb->find("subjects"); s && !s->is_null()) body["subjects"] = *s;
+      out.push_back({&types::RoleBinding, name, name, body});
+    }
+  }
+  return out;
+}
+
+Reconciler::Reconciler(kube::KubeClient& client, kube::Controller& ctrl, Config cfg)
+    : client_(client), ctrl_(ctrl), cfg_(cfg), pool_(static_cast<size_t>(std::max(4, cfg.workers * 3))) {}
+
+Reconciler::Stats Reconciler::stats() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return stats_;
+}
+
+static std::string child_key(const DesiredChild& c) { return c.rt->plural + "/" + c.ns + "/" + c.name; }
+
+bool Reconciler::up_to_date(const DesiredChild& c, const std::string& body_hash) {
+  if (!cfg_.skip_unchanged) return false;
+  kube::Store* store = ctrl_.child_store(c.rt->plural);
+  if (!store) return false;
+  kube::ObjPtr cur = store->get(c.ns, c.name);
+  if (!cur) return false;
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = last_applied_.find(child_key(c));
+  return it != last_applied_.end() && it->second.body_hash == body_hash && it->second.rv == kube::meta_rv(*cur);
+}
+
+void Reconciler::apply_child(const DesiredChild& c, const std::string& body_hash) {
+  static auto& applied = metrics::Registry::global().counter("bgc_apply_total", "Server-side applies issued");
+  Value res = client_.apply(*c.rt, c.ns, c.name, c.body, kFieldManager, /*force=*/true);
+  applied.inc();
+  std::lock_guard<std::mutex> lk(mu_);
+  last_applied_[child_key(c)] = {body_hash, kube::meta_rv(res)};
+  stats_.applied++;
+}
+
+kube::Action Reconciler::reconcile(const kube::ObjPtr& ub_ptr) {
+  auto& reg = metrics::Registry::global();
+  static auto& hist = reg.histogram("bgc_reconcile_duration_seconds", "Wall time of one reconcile");
+  static auto& ring = reg.samples("reconcile");
+  static auto& skipped = reg.counter("bgc_apply_skipped_total", "Applies skipped: child already as last written");
+  metrics::Timer timer(&hist, &ring);
+  const Value& ub = *ub_ptr;
+  std::vector<DesiredChild> children = desired_children(ub);
+  LOG_INFO("controller") << "reconciling " << children.front().name;
+
+  std::vector<std::string> hashes;
+  hashes.reserve(children.size());
+  for (const auto& c : children) hashes.push_back(std::to_string(std::hash<std::string>{}(c.body.dump())));
+
+  auto run_one = [&](size_t i) {
+    if (up_to_date(children[i], hashes[i])) {
+      skipped.inc();
+      std::lock_guard<std::mutex> lk(mu_);
+      stats_.skipped++;
+      return;
+    }
+    try {
+      apply_child(children[i], hashes[i]);
+    } catch (const std::exception& e) {
+      LOG_ERROR("controller") << "failed to patch " << children[i].rt->kind << ": " << e.what();
+      throw;
+    }
+  };
+
+  // Stage 1: the Namespace (namespaced children cannot exist before it).
+  // Stage 2: ResourceQuota and Role, concurrently (independent objects).
+  // Stage 3: the RoleBinding — only after every earlier apply succeeded, so a user is
+  //          never bound into a namespace whose quota failed to apply (the reference
+  //          gets the same guarantee from its sequential `?` chain).
+  run_one(0);
+  std::vector<size_t> middle, last;
+  for (size_t i = 1; i < children.size(); ++i) {
+    (children[i].rt == &types::RoleBinding ? last : middle).push_back(i);
+  }
+  if (cfg_.parallel_children && middle.size() > 1) {
+    std::vector<std::future<void>> futs;
+    for (size_t i : middle) futs.push_back(pool_.submit([&, i] { run_one(i); }));
+    std::exception_ptr first;
+    for (auto& f : futs) {
+      try {
+        f.get();
+      } catch (...) {
+        if (!first) first = std::current_exception();
+      }
+    }
+    if (first) std::rethrow_exception(first);
+  } else {
+    for (size_t i : middle) run_one(i);
+  }
+  for (size_t i : last) run_one(i);
+  static auto& ok = reg.counter("bgc_reconcile_total", "Reconciles", {{"result", "ok"}});
+  ok.inc();
+  return kube::Action::requeue_after(std::chrono::milliseconds(cfg_.requeue_secs * 1000));
+}
+
+kube::Action Reconciler::error_policy(const kube::ObjPtr& ub, const std::exception& err) {
+  static auto& fail = metrics::Registry::global().counter("bgc_reconcile_total", "Reconciles", {{"result", "error"}});
+  fail.inc();
+  const Value& meta = ub->get("metadata");
+  LOG_ERROR("controller") << "error reconciling \"" << meta.get_string("namespace", "<unknown>") << "/"
+                          << meta.get_string("name", "<unknown>") << "\": " << err.what();
+  return kube::Action::requeue_after(std::chrono::milliseconds(cfg_.error_requeue_ms));
+}
+
+}  // namespace bgc::controller

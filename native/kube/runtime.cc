@@ -1,0 +1,334 @@
+#include "kube/runtime.h"
+
+#include <algorithm>
+
+#include "core/log.h"
+#include "core/metrics.h"
+
+namespace bgc::kube {
+
+using json::Value;
+
+std::string meta_name(const Value& obj) { return obj.get("metadata").get_string("name"); }
+std::string meta_namespace(const Value& obj) { return obj.get("metadata").get_string("namespace"); }
+std::string meta_rv(const Value& obj) { return obj.get("metadata").get_string("resourceVersion"); }
+
+// ---------------------------------------------------------------------------
+// Watcher
+
+Watcher::Watcher(KubeClient& client, ResourceType rt, std::string ns, std::string label_selector)
+    : client_(client), rt_(std::move(rt)), ns_(std::move(ns)), selector_(std::move(label_selector)) {}
+
+void Watcher::run(CancelToken& stop, const std::function<void(const WatchEvent&)>& on_event) {
+  std::string rv;
+  bool need_list = true;
+  auto backoff = std::chrono::milliseconds(800);
+  const auto max_backoff = std::chrono::milliseconds(30000);
+  auto& errors = metrics::Registry::global().counter("bgc_watch_errors_total", "Watch stream failures",
+                                                     {{"resource", rt_.plural}});
+  while (!stop.cancelled()) {
+    try {
+      if (need_list) {
+        ListOptions lo;
+        lo.label_selector = selector_;
+        Value list = client_.list(rt_, ns_, lo);
+        rv = list.get("metadata").get_string("resourceVersion");
+        WatchEvent ev{WatchEvent::Type::Restarted, nullptr, {}};
+        for (const auto& item : list.get("items").items()) {
+          Value obj = item;
+          if (!obj.contains("apiVersion")) obj["apiVersion"] = rt_.api_version();
+          if (!obj.contains("kind")) obj["kind"] = rt_.kind;
+          ev.objects.push_back(std::make_shared<const Value>(std::move(obj)));
+        }
+        on_event(ev);
+        need_list = false;
+        relists_.fetch_add(1);
+      }
+      WatchOptions wo;
+      wo.resource_version = rv;
+      wo.label_selector = selector_;
+      auto stream = client_.watch(rt_, ns_, wo);
+      backoff = std::chrono::milliseconds(800);
+      std::string line;
+      while (stream->next_line(line, &stop, 500)) {
+        if (line.empty()) continue;
+        Value ev = json::parse(line);
+        const std::string type = ev.get_string("type");
+        const Value& obj = ev.get("object");
+        if (type == "ERROR") {
+          int code = obj.get("code").is_int() ? static_cast<int>(obj.get("code").as_int()) : 0;
+          if (code == 410) {
+            LOG_DEBUG("kube::watcher") << rt_.plural << ": resourceVersion too old, relisting";
+          } else {
+            LOG_WARN("kube::watcher") << rt_.plural << ": watch error event: " << obj.dump();
+          }
+          need_list = true;
+          break;
+        }
+        std::string new_rv = meta_rv(obj);
+        if (!new_rv.empty()) rv = new_rv;
+        if (type == "BOOKMARK") continue;
+        WatchEvent we{WatchEvent::Type::Added, std::make_shared<const Value>(obj), {}};
+        if (type == "MODIFIED") we.type = WatchEvent::Type::Modified;
+        else if (type == "DELETED") we.type = WatchEvent::Type::Deleted;
+        else if (type != "ADDED") continue;
+        on_event(we);
+      }
+      stream->close();
+      if (!stop.cancelled()) reconnects_.fetch_add(1);
+    } catch (const ApiError& e) {
+      errors.inc();
+      if (e.code() == 410) {
+        need_list = true;
+        continue;
+      }
+      LOG_WARN("kube::watcher") << rt_.plural << ": " << e.what() << " (retry in " << backoff.count() << "ms)";
+      if (stop.wait_for(backoff)) break;
+      backoff = std::min(backoff * 2, max_backoff);
+      need_list = true;
+    } catch (const std::exception& e) {
+      errors.inc();
+      LOG_WARN("kube::watcher") << rt_.plural << ": " << e.what() << " (retry in " << backoff.count() << "ms)";
+      if (stop.wait_for(backoff)) break;
+      backoff = std::min(backoff * 2, max_backoff);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Store
+
+void Store::apply(const WatchEvent& ev) {
+  std::lock_guard<std::mutex> lk(mu_);
+  switch (ev.type) {
+    case WatchEvent::Type::Restarted:
+      items_.clear();
+      for (const auto& o : ev.objects) items_[rt_.key(meta_namespace(*o), meta_name(*o))] = o;
+      synced_.store(true);
+      cv_.notify_all();
+      break;
+    case WatchEvent::Type::Added:
+    case WatchEvent::Type::Modified:
+      items_[rt_.key(meta_namespace(*ev.object), meta_name(*ev.object))] = ev.object;
+      break;
+    case WatchEvent::Type::Deleted:
+      items_.erase(rt_.key(meta_namespace(*ev.object), meta_name(*ev.object)));
+      break;
+  }
+}
+
+ObjPtr Store::get(const std::string& key) const {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = items_.find(key);
+  return it == items_.end() ? nullptr : it->second;
+}
+
+std::vector<ObjPtr> Store::list() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  std::vector<ObjPtr> out;
+  out.reserve(items_.size());
+  for (auto& kv : items_) out.push_back(kv.second);
+  return out;
+}
+
+size_t Store::size() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return items_.size();
+}
+
+bool Store::wait_synced(std::chrono::milliseconds timeout) const {
+  std::unique_lock<std::mutex> lk(mu_);
+  return cv_.wait_for(lk, timeout, [&] { return synced_.load(); });
+}
+
+// ---------------------------------------------------------------------------
+// WorkQueue
+
+void WorkQueue::add_after(const std::string& key, std::chrono::milliseconds delay) {
+  auto t = Clock::now() + delay;
+  std::lock_guard<std::mutex> lk(mu_);
+  if (shutdown_) return;
+  if (processing_.count(key)) {
+    auto it = deferred_.find(key);
+    if (it == deferred_.end() || t < it->second) deferred_[key] = t;
+    return;
+  }
+  auto it = due_.find(key);
+  if (it != due_.end() && it->second <= t) return;
+  due_[key] = t;
+  timeline_.emplace(t, key);
+  cv_.notify_one();
+}
+
+bool WorkQueue::get(std::string& key) {
+  std::unique_lock<std::mutex> lk(mu_);
+  while (true) {
+    if (shutdown_) return false;
+    auto now = Clock::now();
+    while (!timeline_.empty()) {
+      auto it = timeline_.begin();
+      auto d = due_.find(it->second);
+      if (d == due_.end() || d->second != it->first) {
+        timeline_.erase(it);  // stale entry (superseded by an earlier due time)
+        continue;
+      }
+      if (it->first > now) break;
+      key = it->second;
+      timeline_.erase(it);
+      due_.erase(d);
+      processing_.insert(key);
+      return true;
+    }
+    if (timeline_.empty()) {
+      cv_.wait(lk);
+    } else {
+      cv_.wait_until(lk, timeline_.begin()->first);
+    }
+  }
+}
+
+void WorkQueue::done(const std::string& key) {
+  std::lock_guard<std::mutex> lk(mu_);
+  processing_.erase(key);
+  auto it = deferred_.find(key);
+  if (it != deferred_.end()) {
+    auto t = it->second;
+    deferred_.erase(it);
+    auto d = due_.find(key);
+    if (d == due_.end() || t < d->second) {
+      due_[key] = t;
+      timeline_.emplace(t, key);
+    }
+    cv_.notify_one();
+  }
+}
+
+void WorkQueue::shutdown() {
+  std::lock_guard<std::mutex> lk(mu_);
+  shutdown_ = true;
+  cv_.notify_all();
+}
+
+size_t WorkQueue::pending() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return due_.size() + deferred_.size();
+}
+
+size_t WorkQueue::in_flight() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return processing_.size();
+}
+
+// ---------------------------------------------------------------------------
+// Controller
+
+Controller::Mapper owner_mapper(const ResourceType& owner) {
+  std::string api_version = owner.api_version();
+  std::string kind = owner.kind;
+  return [api_version, kind](const Value& child) {
+    std::vector<std::string> keys;
+    for (const auto& ref : child.get("metadata").get("ownerReferences").items()) {
+      if (ref.get_string("kind") == kind && ref.get_string("apiVersion") == api_version) {
+        keys.push_back(ref.get_string("name"));
+      }
+    }
+    return keys;
+  };
+}
+
+Controller::Controller(KubeClient& client, ResourceType primary, Options opts)
+    : client_(client), primary_(std::move(primary)), opts_(opts), primary_store_(std::make_unique<Store>(primary_)) {}
+
+Controller::~Controller() { queue_.shutdown(); }
+
+void Controller::owns(const ResourceType& child, Mapper mapper) {
+  auto c = std::make_unique<Child>();
+  c->rt = child;
+  c->mapper = mapper ? std::move(mapper) : owner_mapper(primary_);
+  c->store = std::make_unique<Store>(child);
+  children_.push_back(std::move(c));
+}
+
+Store* Controller::child_store(const std::string& plural) {
+  for (auto& c : children_) {
+    if (c->rt.plural == plural) return c->store.get();
+  }
+  return nullptr;
+}
+
+void Controller::enqueue_all() {
+  for (const auto& o : primary_store_->list()) queue_.add(primary_.key(meta_namespace(*o), meta_name(*o)));
+}
+
+bool Controller::wait_synced(std::chrono::milliseconds timeout) {
+  auto deadline = std::chrono::steady_clock::now() + timeout;
+  if (!primary_store_->wait_synced(timeout)) return false;
+  for (auto& c : children_) {
+    auto left = std::chrono::duration_cast<std::chrono::milliseconds>(deadline - std::chrono::steady_clock::now());
+    if (left.count() < 0 || !c->store->wait_synced(left)) return false;
+  }
+  return true;
+}
+
+void Controller::run(CancelToken& stop, Reconciler reconcile, ErrorPolicy error_policy) {
+  std::vector<std::thread> threads;
+  // primary watcher: trigger_self
+  threads.emplace_back([&] {
+    Watcher w(client_, primary_);
+    w.run(stop, [&](const WatchEvent& ev) {
+      primary_store_->apply(ev);
+      if (ev.type == WatchEvent::Type::Restarted) {
+        for (const auto& o : ev.objects) queue_.add(primary_.key(meta_namespace(*o), meta_name(*o)));
+      } else if (ev.type != WatchEvent::Type::Deleted) {
+        queue_.add(primary_.key(meta_namespace(*ev.object), meta_name(*ev.object)));
+      }
+    });
+  });
+  // owned watchers: trigger_owners
+  for (auto& cp : children_) {
+    Child* c = cp.get();
+    threads.emplace_back([&, c] {
+      Watcher w(client_, c->rt);
+      w.run(stop, [&, c](const WatchEvent& ev) {
+        c->store->apply(ev);
+        if (ev.type == WatchEvent::Type::Restarted) {
+          for (const auto& o : ev.objects) {
+            for (const auto& k : c->mapper(*o)) queue_.add(k);
+          }
+        } else {
+          for (const auto& k : c->mapper(*ev.object)) queue_.add(k);
+        }
+      });
+    });
+  }
+  auto& reg = metrics::Registry::global();
+  auto& q_depth = reg.gauge("bgc_controller_queue_depth", "Keys waiting in the work queue");
+  std::vector<std::thread> workers;
+  for (int i = 0; i < std::max(1, opts_.workers); ++i) {
+    workers.emplace_back([&] {
+      std::string key;
+      while (queue_.get(key)) {
+        q_depth.set(static_cast<double>(queue_.pending()));
+        ObjPtr obj = primary_store_->get(key);
+        if (!obj) {
+          queue_.done(key);
+          continue;
+        }
+        Action a;
+        try {
+          a = reconcile(obj);
+        } catch (const std::exception& e) {
+          a = error_policy(obj, e);
+        }
+        if (a.requeue) queue_.add_after(key, a.after);
+        queue_.done(key);
+      }
+    });
+  }
+  stop.wait();
+  queue_.shutdown();
+  for (auto& t : workers) t.join();  // in-flight reconciles complete (graceful shutdown)
+  for (auto& t : threads) t.join();
+}
+
+}  // namespace bgc::kube

@@ -1,0 +1,117 @@
+"""End-to-end onboarding flow through kube-lite + TLS webhook +
+controller: create as an OIDC user, quota/status as the synchronizer would write them,
+RoleBinding only after sync, GC on delete."""
+import pytest
+
+from bacchus_gpu_controller_amd.testing.cluster import Cluster
+from bacchus_gpu_controller_amd.testing.kubeapi import ApiError, wait_for
+
+pytestmark = pytest.mark.slow
+
+
+@pytest.fixture(scope="module")
+def cluster():
+    with Cluster(controller_env={"CONF_REQUEUE_SECS": "2", "CONF_ERROR_REQUEUE_MS": "200"}) as c:
+        yield c
+
+
+def ub(name, spec=None):
+    return {"apiVersion": "bacchus.io/v1", "kind": "UserBootstrap", "metadata": {"name": name}, "spec": spec or {}}
+
+
+def test_full_onboarding_flow(cluster):
+    alice = cluster.as_user("oidc:alice", ["gpu"])
+    created = alice.create("userbootstraps", ub("alice"))
+    # webhook mutations (rules 13 + 16)
+    assert created["spec"]["kube_username"] == "alice"
+    assert created["spec"]["rolebinding"]["subjects"][0]["name"] == "oidc:alice"
+    assert created["spec"]["rolebinding"]["role_ref"] == {"apiGroup": "rbac.authorization.k8s.io",
+                                                          "kind": "ClusterRole", "name": "edit"}
+    admin = cluster.admin
+    ns = wait_for(lambda: admin.get_or_none("namespaces", "alice"), desc="namespace alice")
+    ref = ns["metadata"]["ownerReferences"][0]
+    assert ref == {"apiVersion": "bacchus.io/v1", "controller": True, "kind": "UserBootstrap", "name": "alice",
+                   "uid": created["metadata"]["uid"]}
+    # not synchronized yet: no RoleBinding, no quota
+    assert admin.get_or_none("rolebindings", "alice", "alice") is None
+    assert admin.get_or_none("resourcequotas", "alice", "alice") is None
+
+    # what the synchronizer writes (quota first, then status: Q5 ordering)
+    sync = cluster.as_user("system:serviceaccount:bgc:bgc-synchronizer", ["system:serviceaccounts"])
+    hard = {"limits.cpu": "8", "limits.memory": "64Gi", "requests.amd.com/gpu": "1", "requests.cpu": "8",
+            "requests.memory": "64Gi", "requests.storage": "100Gi", "requests.amd.com/gpu-partition": "0"}
+    sync.json_patch("userbootstraps", "alice", [{"op": "add", "path": "/spec/quota", "value": {}},
+                                                {"op": "replace", "path": "/spec/quota", "value": {"hard": hard}}])
+    rq = wait_for(lambda: admin.get_or_none("resourcequotas", "alice", "alice"), desc="quota")
+    assert rq["spec"] == {"hard": hard}
+    assert admin.get_or_none("rolebindings", "alice", "alice") is None
+    cur = admin.get("userbootstraps", "alice")
+    sync.replace("userbootstraps", "alice", {"apiVersion": "bacchus.io/v1", "kind": "UserBootstrap",
+                                             "metadata": {"name": "alice", "resourceVersion": cur["metadata"]["resourceVersion"]},
+                                             "status": {"synchronized_with_sheet": True}}, sub="status")
+    rb = wait_for(lambda: admin.get_or_none("rolebindings", "alice", "alice"), desc="rolebinding")
+    assert rb["roleRef"]["name"] == "edit"
+    assert rb["subjects"] == [{"apiGroup": "rbac.authorization.k8s.io", "kind": "User", "name": "oidc:alice"}]
+    # managed by the controller's field manager
+    managers = {m["manager"] for m in rb["metadata"]["managedFields"]}
+    assert "bacchus-gpu-controller.bacchus.io" in managers
+
+    # normal user may not delete; admin may, and GC removes everything
+    with pytest.raises(ApiError) as ei:
+        alice.delete("userbootstraps", "alice")
+    assert "normal user is not allowed to delete resource" in ei.value.message
+    admin.delete("userbootstraps", "alice")
+    wait_for(lambda: admin.get_or_none("namespaces", "alice") is None, desc="namespace GC")
+    assert admin.get_or_none("rolebindings", "alice", "alice") is None
+
+
+def test_admission_denials_via_apiserver(cluster):
+    with pytest.raises(ApiError) as e1:
+        cluster.as_user("oidc:eve", ["students"]).create("userbootstraps", ub("eve"))
+    assert e1.value.code == 400
+    assert 'admission webhook "bgc-admission.bacchus.io" denied the request: user is not in authorized group' == e1.value.message
+    with pytest.raises(ApiError) as e2:
+        cluster.as_user("oidc:bob", ["gpu"]).create("userbootstraps", ub("alice2"))
+    assert "username not match with resource name" in e2.value.message
+    with pytest.raises(ApiError) as e3:
+        cluster.as_user("oidc:carol", ["gpu"]).create("userbootstraps", ub("carol", {"quota": {"hard": {"cpu": "1"}}}))
+    assert "quota field is not empty" in e3.value.message
+    with pytest.raises(ApiError) as e4:
+        cluster.admin.create("userbootstraps", ub("dave"))
+    assert "kube_username field is empty" in e4.value.message
+
+
+def test_admin_create_with_kube_username(cluster):
+    obj = cluster.admin.create("userbootstraps", ub("frank", {"kube_username": "frank"}))
+    assert obj["spec"]["rolebinding"]["subjects"][0]["name"] == "frank"  # Q12: verbatim
+    wait_for(lambda: cluster.admin.get_or_none("namespaces", "frank"), desc="namespace frank")
+    cluster.admin.delete("userbootstraps", "frank")
+
+
+def test_crd_schema_validation(cluster):
+    with pytest.raises(ApiError) as e:
+        cluster.admin.create("userbootstraps", ub("gina", {"kube_username": "gina", "rolebinding": {"subjects": []}}))
+    # webhook parse (rule 12) or schema (422) rejects a rolebinding without role_ref
+    assert e.value.code in (400, 422)
+
+
+def test_controller_repairs_drift(cluster):
+    admin = cluster.admin
+    admin.create("userbootstraps", ub("henry", {"kube_username": "henry", "quota": {"hard": {"requests.cpu": "2"}}}))
+    wait_for(lambda: admin.get_or_none("resourcequotas", "henry", "henry"), desc="quota henry")
+    # another manager edits the quota; SSA force restores it on the next reconcile
+    admin.merge_patch("resourcequotas", "henry", {"spec": {"hard": {"requests.cpu": "99"}}}, namespace="henry",
+                      field_manager="kubectl-edit")
+    wait_for(lambda: admin.get("resourcequotas", "henry", "henry")["spec"]["hard"]["requests.cpu"] == "2",
+             timeout=10, desc="drift repaired")
+    admin.delete("userbootstraps", "henry")
+
+
+def test_invalid_namespace_name_error_loop(cluster):
+    # Q10: a dotted name is a valid CR name but an invalid Namespace -> controller keeps erroring
+    cluster.admin.create("userbootstraps", ub("ivy.x", {"kube_username": "ivy.x"}))
+    import time
+    time.sleep(1.0)
+    assert cluster.admin.get_or_none("namespaces", "ivy.x") is None
+    assert cluster.procs["controller"].alive()
+    cluster.admin.delete("userbootstraps", "ivy.x")
