@@ -181,6 +181,23 @@ class Cluster:
         wait_for(lambda: requests.get(f"http://127.0.0.1:{self.controller_port}/health", timeout=1).text == "pong",
                  20, desc="controller /health")
 
+    def start_synchronizer(self, google, interval=60, server_name="mi355x-01", extra_env=None, wait_healthy=True):
+        """Start the native synchronizer against a FakeGoogle (testing/fake_google.py)."""
+        key_path = os.path.join(self.workdir, "key.json")
+        with open(key_path, "w") as f:
+            f.write(google.service_account_json())
+        self.sync_port = free_port()
+        env = self.component_env(SYNC_TOKEN, self.sync_port)
+        env.update({"CONF_GOOGLE_SERVICE_ACCOUNT_JSON_PATH": key_path, "CONF_GOOGLE_FILE_ID": google.file_id,
+                    "CONF_SYNC_INTERVAL_SECS": str(interval), "CONF_GPU_SERVER_NAME": server_name})
+        env.update(google.env())
+        env.update(extra_env or {})
+        p = self.start_process("synchronizer", "synchronizer", env)
+        if wait_healthy:
+            wait_for(lambda: requests.get(f"http://127.0.0.1:{self.sync_port}/health", timeout=1).text == "pong",
+                     20, desc="synchronizer /health")
+        return p
+
     def start_process(self, name, exe, env):
         self.procs[name] = Proc(name, [binary(exe)], env, self.workdir)
         return self.procs[name]

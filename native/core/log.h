@@ -42,10 +42,11 @@ class Line {
 
 }  // namespace bgc::log
 
-#define BGC_LOG(lvl, target)                                             \
-  if (!::bgc::log::enabled(::bgc::log::Level::lvl, target)) {            \
-  } else                                                                 \
-    ::bgc::log::Line(::bgc::log::Level::lvl, target)
+// for-loop form: safe inside un-braced if/else (no dangling-else), evaluates once.
+#define BGC_LOG(lvl, target)                                                                    \
+  for (bool bgc_log_on_ = ::bgc::log::enabled(::bgc::log::Level::lvl, target); bgc_log_on_;    \
+       bgc_log_on_ = false)                                                                     \
+  ::bgc::log::Line(::bgc::log::Level::lvl, target)
 
 #define LOG_ERROR(t) BGC_LOG(Error, t)
 #define LOG_WARN(t) BGC_LOG(Warn, t)

@@ -1,0 +1,198 @@
+#include "sync/synchronizer.h"
+
+#include <thread>
+
+#include "core/json_patch.h"
+#include "core/log.h"
+#include "core/metrics.h"
+
+namespace bgc::sync {
+
+using json::Value;
+namespace types = kube::types;
+
+Config Config::from_env(const EnvConfig& env) {
+  Config c;
+  c.listen_addr = env.str("listen_addr");
+  c.listen_port = env.u16("listen_port");
+  c.google_service_account_json_path = env.str("google_service_account_json_path");
+  c.google_file_id = env.str("google_file_id");
+  c.sync_interval_secs = env.u64_or("sync_interval_secs", 60);
+  c.gpu_server_name = env.str("gpu_server_name");
+  c.quota_keys.gpu_resource = env.str_or("gpu_resource_name", "amd.com/gpu");
+  c.quota_keys.partition_resource = env.str_or("partition_resource_name", "amd.com/gpu-partition");
+  c.watch = env.boolean_or("watch", true);
+  c.min_refresh_ms = env.u64_or("min_refresh_ms", 5000);
+  c.exit_on_error = env.boolean_or("exit_on_error", true);
+  c.skip_unchanged = env.boolean_or("skip_unchanged", true);
+  c.workers = static_cast<int>(env.u64_or("workers", 8));
+  if (c.sync_interval_secs == 0) throw ConfigError("invalid value for field sync_interval_secs: must be > 0");
+  return c;
+}
+
+Synchronizer::Synchronizer(kube::KubeClient& client, SheetSource source, Config cfg)
+    : client_(client), source_(std::move(source)), cfg_(std::move(cfg)), index_(std::make_shared<RowIndex>()) {}
+
+std::shared_ptr<const RowIndex> Synchronizer::index() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return index_;
+}
+
+void Synchronizer::refresh() {
+  std::lock_guard<std::mutex> rl(refresh_mu_);
+  std::string csv = source_();
+  LOG_INFO("synchronizer") << "downloaded csv file";
+  std::vector<std::string> warnings;
+  auto rows = parse_csv(csv, &warnings);
+  for (const auto& w : warnings) LOG_WARN("synchronizer") << w;
+  auto idx = std::make_shared<RowIndex>(rows, cfg_.gpu_server_name);
+  LOG_INFO("synchronizer") << "target rows: " << idx->target_rows();
+  metrics::Registry::global().gauge("bgc_sync_rows", "Sheet rows targeting this GPU server").set(static_cast<double>(idx->target_rows()));
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    index_ = idx;
+  }
+  last_refresh_ns_.store(metrics::now_ns());
+}
+
+bool Synchronizer::sync_one(const Value& ub) {
+  const std::string name = ub.get("metadata").get_string("name");
+  if (name.empty()) return false;
+  auto idx = index();
+  const Row* row = idx->find(name);
+  if (!row) return false;
+  Value desired = quota_spec(*row, cfg_.quota_keys);
+  const Value& quota = ub.get("spec").get("quota");
+  bool has_quota = !quota.is_null();
+  bool quota_same = has_quota && quota == desired;
+  const Value& st = ub.get("status");
+  bool synced = st.is_object() && st.get("synchronized_with_sheet").is_bool() && st.get("synchronized_with_sheet").as_bool();
+  if (cfg_.skip_unchanged && quota_same && synced) return false;
+
+  LOG_INFO("synchronizer") << "updating quota id_username=" << row->id_username << " cpu_request=" << row->cpu_request
+                           << " memory_request=" << row->memory_request << " gpu_request=" << row->gpu_request
+                           << " storage_request=" << row->storage_request << " mig_request=" << row->mig_request;
+  LOG_DEBUG("synchronizer") << "row name=" << row->name << " department=" << row->department;
+  std::string rv = ub.get("metadata").get_string("resourceVersion");
+  if (!quota_same || !cfg_.skip_unchanged) {
+    json::PatchBuilder ops;
+    if (!has_quota) ops.add("/spec/quota", Value::object());
+    ops.replace("/spec/quota", desired);
+    Value res = client_.patch_json(types::UserBootstrap, "", name, ops.ops(), kPatchManager);
+    rv = res.get("metadata").get_string("resourceVersion");
+    LOG_INFO("synchronizer") << "quota updated";
+  }
+  if (!synced || !cfg_.skip_unchanged) {
+    for (int attempt = 0; attempt < 3; ++attempt) {
+      Value body = Value::object({{"apiVersion", "bacchus.io/v1"}, {"kind", "UserBootstrap"}});
+      body["metadata"] = Value::object({{"name", name}, {"resourceVersion", rv}});
+      body["status"] = Value::object({{"synchronized_with_sheet", true}});
+      try {
+        LOG_INFO("synchronizer") << "updating status";
+        client_.replace_status(types::UserBootstrap, "", name, body);
+        break;
+      } catch (const kube::ApiError& e) {
+        if (e.code() != 409 || attempt == 2) throw;
+        rv = client_.get(types::UserBootstrap, "", name).get("metadata").get_string("resourceVersion");
+      }
+    }
+  }
+  static auto& written = metrics::Registry::global().counter("bgc_sync_writes_total", "UserBootstraps written by the synchronizer");
+  written.inc();
+  return true;
+}
+
+TickStats Synchronizer::tick() {
+  auto& reg = metrics::Registry::global();
+  static auto& hist = reg.histogram("bgc_sync_duration_seconds", "Wall time of one synchronization tick");
+  static auto& ring = reg.samples("sync_tick");
+  metrics::Timer timer(&hist, &ring);
+  LOG_INFO("synchronizer") << "starting synchronization";
+  refresh();
+  TickStats ts;
+  auto idx = index();
+  ts.target_rows = idx->target_rows();
+  Value list = client_.list(types::UserBootstrap);
+  for (const auto& ub : list.get("items").items()) {
+    ++ts.userbootstraps;
+    if (idx->find(ub.get("metadata").get_string("name"))) ++ts.matched;
+    if (sync_one(ub)) ++ts.written;
+  }
+  return ts;
+}
+
+int Synchronizer::run(CancelToken& stop) {
+  std::unique_ptr<std::thread> watch_thread;
+  std::vector<std::thread> workers;
+  kube::WorkQueue queue;
+  kube::Store store(types::UserBootstrap);
+  std::atomic<bool> fatal{false};
+  auto& ub_latency = metrics::Registry::global().samples("sync_ub");
+
+  if (cfg_.watch) {
+    watch_thread = std::make_unique<std::thread>([&] {
+      kube::Watcher w(client_, types::UserBootstrap);
+      w.run(stop, [&](const kube::WatchEvent& ev) {
+        store.apply(ev);
+        if (ev.type == kube::WatchEvent::Type::Restarted) {
+          for (const auto& o : ev.objects) queue.add(kube::meta_name(*o));
+        } else if (ev.type != kube::WatchEvent::Type::Deleted) {
+          queue.add(kube::meta_name(*ev.object));
+        }
+      });
+    });
+    for (int i = 0; i < std::max(1, cfg_.workers); ++i) {
+      workers.emplace_back([&] {
+        std::string key;
+        while (queue.get(key)) {
+          kube::ObjPtr ub = store.get(key);
+          if (ub) {
+            int64_t t0 = metrics::now_ns();
+            try {
+              auto idx = index();
+              if (!idx->find(key)) {
+                // unknown user: the sheet may have changed since the last fetch
+                int64_t age_ms = (metrics::now_ns() - last_refresh_ns_.load()) / 1000000;
+                if (last_refresh_ns_.load() != 0 && age_ms >= static_cast<int64_t>(cfg_.min_refresh_ms)) refresh();
+              }
+              if (sync_one(*ub)) ub_latency.add(static_cast<double>(metrics::now_ns() - t0) * 1e-9);
+            } catch (const std::exception& e) {
+              LOG_ERROR("synchronizer") << "sync of " << key << " failed (retrying): " << e.what();
+              queue.add_after(key, std::chrono::milliseconds(1000));
+            }
+          }
+          queue.done(key);
+        }
+      });
+    }
+  }
+
+  int rc = 0;
+  while (!stop.cancelled()) {
+    try {
+      if (cfg_.watch) {
+        // Workers own the writes; a tick refreshes the sheet and re-offers every
+        // UserBootstrap so rows approved since the last tick get applied.
+        refresh();
+        for (const auto& o : store.list()) queue.add(kube::meta_name(*o));
+      } else {
+        tick();
+      }
+    } catch (const std::exception& e) {
+      LOG_ERROR("synchronizer") << "synchronization failed: " << e.what();
+      if (cfg_.exit_on_error) {
+        rc = 1;
+        fatal = true;
+        stop.cancel();
+        break;
+      }
+    }
+    if (stop.wait_for(std::chrono::seconds(cfg_.sync_interval_secs))) break;
+  }
+  queue.shutdown();
+  for (auto& t : workers) t.join();
+  if (watch_thread) watch_thread->join();
+  return rc;
+}
+
+}  // namespace bgc::sync

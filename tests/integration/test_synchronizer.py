@@ -1,0 +1,109 @@
+"""Synchronizer end to end (R7): native synchronizer + fake Google (JWT-verified OAuth2
+and Drive export) + kube-lite + webhook + controller."""
+import time
+
+import pytest
+import requests
+
+from bacchus_gpu_controller_amd.testing.cluster import Cluster
+from bacchus_gpu_controller_amd.testing.fake_google import FakeGoogle
+from bacchus_gpu_controller_amd.testing.kubeapi import wait_for
+
+pytestmark = pytest.mark.slow
+
+
+def ub(name):
+    return {"apiVersion": "bacchus.io/v1", "kind": "UserBootstrap", "metadata": {"name": name}, "spec": {}}
+
+
+@pytest.fixture()
+def google():
+    g = FakeGoogle().start()
+    yield g
+    g.stop()
+
+
+def expected_hard(gpu=1, cpu=8, mem=64, storage=100, mig=0):
+    return {"limits.cpu": str(cpu), "limits.memory": f"{mem}Gi", "requests.amd.com/gpu": str(gpu),
+            "requests.amd.com/gpu-partition": str(mig), "requests.cpu": str(cpu),
+            "requests.memory": f"{mem}Gi", "requests.storage": f"{storage}Gi"}
+
+
+@pytest.mark.parametrize("watch", ["true", "false"])
+def test_sheet_approval_provisions_user(google, watch):
+    google.set_rows([{"id_username": "alice", "gpu": 2, "cpu": 16, "mem": 128},
+                     {"id_username": "bob", "authorized": "X"},
+                     {"id_username": "carol", "gpu_server": "other"}])
+    with Cluster(controller_env={"CONF_REQUEUE_SECS": "2"}) as c:
+        for u in ("alice", "bob", "carol"):
+            c.as_user(f"oidc:{u}", ["gpu"]).create("userbootstraps", ub(u))
+        c.start_synchronizer(google, interval=1, extra_env={"CONF_WATCH": watch})
+        a = c.admin
+        obj = wait_for(lambda: (lambda o: o if o.get("status", {}).get("synchronized_with_sheet") else None)(
+            a.get("userbootstraps", "alice")), timeout=10, desc="alice synced")
+        assert obj["spec"]["quota"] == {"hard": expected_hard(2, 16, 128)}
+        rq = wait_for(lambda: a.get_or_none("resourcequotas", "alice", "alice"), desc="alice quota")
+        assert rq["spec"]["hard"]["requests.amd.com/gpu"] == "2"
+        wait_for(lambda: a.get_or_none("rolebindings", "alice", "alice"), desc="alice rolebinding")
+        time.sleep(1.5)
+        # not approved / other server: untouched
+        for u in ("bob", "carol"):
+            o = a.get("userbootstraps", u)
+            assert "quota" not in o["spec"] and "status" not in o
+            assert a.get_or_none("rolebindings", u, u) is None
+        # Q6: steady state does not rewrite the object every tick
+        rv1 = a.get("userbootstraps", "alice")["metadata"]["resourceVersion"]
+        time.sleep(2.5)
+        assert a.get("userbootstraps", "alice")["metadata"]["resourceVersion"] == rv1
+        assert google.token_requests >= 1 and google.export_requests >= 2
+        assert not google.errors
+
+
+def test_watch_mode_is_event_driven(google):
+    google.set_rows([{"id_username": "dave"}])
+    with Cluster() as c:
+        c.start_synchronizer(google, interval=3600, extra_env={"CONF_WATCH": "true"})
+        time.sleep(0.5)
+        t0 = time.time()
+        c.as_user("oidc:dave", ["gpu"]).create("userbootstraps", ub("dave"))
+        wait_for(lambda: c.admin.get_or_none("rolebindings", "dave", "dave"), timeout=10, desc="dave ready")
+        # With a one-hour interval only the watch path can have provisioned dave.
+        assert time.time() - t0 < 5
+
+
+def test_quota_update_propagates(google):
+    google.set_rows([{"id_username": "erin", "gpu": 1}])
+    with Cluster(controller_env={"CONF_REQUEUE_SECS": "1"}) as c:
+        c.as_user("oidc:erin", ["gpu"]).create("userbootstraps", ub("erin"))
+        c.start_synchronizer(google, interval=1)
+        wait_for(lambda: c.admin.get_or_none("resourcequotas", "erin", "erin"), desc="erin quota")
+        google.set_rows([{"id_username": "erin", "gpu": 1}, {"id_username": "erin", "gpu": 4}])
+        wait_for(lambda: c.admin.get("resourcequotas", "erin", "erin")["spec"]["hard"]["requests.amd.com/gpu"] == "4",
+                 timeout=10, desc="quota raised to 4")
+
+
+def test_drive_failure_exits_process(google):
+    """Q7: any tick error ends the process (kubelet restarts it)."""
+    google.fail_export = 500
+    with Cluster(controller=False) as c:
+        p = c.start_synchronizer(google, interval=1, wait_healthy=False)
+        wait_for(lambda: p.p.poll() is not None, timeout=10, desc="synchronizer exit")
+        assert p.p.returncode != 0
+        assert "request failed" in p.output()
+
+
+def test_bad_header_exits(google):
+    google.set_csv("이름,뭔지모를헤더\nx,y\n")
+    with Cluster(controller=False) as c:
+        p = c.start_synchronizer(google, interval=1, wait_healthy=False)
+        wait_for(lambda: p.p.poll() is not None, timeout=10, desc="synchronizer exit")
+        assert "unknown header" in p.output()
+
+
+def test_missing_config_fails_fast():
+    import subprocess
+
+    from bacchus_gpu_controller_amd import binary
+
+    r = subprocess.run([binary("synchronizer")], env={"PATH": "/usr/bin"}, capture_output=True, text=True, timeout=10)
+    assert r.returncode != 0 and "missing value for field listen_addr" in r.stderr
