@@ -730,8 +730,9 @@ struct ApiServer::Impl {
 
   static void render_managed(Value& obj, const Managers& m, const std::string& api_version) {
     Value arr = Value::array();
-    for (const auto& [mgr, e] : m) {
+    for (const auto& [key, e] : m) {
       if (e.fields.empty()) continue;
+      std::string mgr = key.substr(0, key.find('\x1f'));
       Value ent = Value::object({{"manager", mgr}, {"operation", e.operation},
                                  {"apiVersion", e.api_version.empty() ? api_version : e.api_version},
                                  {"time", e.time}, {"fieldsType", "FieldsV1"}, {"fieldsV1", fields_v1(e.fields)}});
@@ -777,7 +778,8 @@ struct ApiServer::Impl {
       for (const auto& p : removed) e.fields.erase(p);
     }
     if (!changed.empty()) {
-      auto& e = m[manager];
+      // managedFields entries are per (manager, subresource)
+      auto& e = m[status_write ? manager + "\x1fstatus" : manager];
       if (e.operation.empty()) {
         e.operation = "Update";
         e.api_version = api_version;
@@ -1082,8 +1084,9 @@ struct ApiServer::Impl {
   }
 
   std::pair<Value, Managers> apply_ssa(const TypeInfo& ti, const Stored* cur, const Value& config,
-                                       const std::string& manager, bool force, bool is_status,
+                                       const std::string& manager_name, bool force, bool is_status,
                                        const std::string& ns, const std::string& name) {
+    const std::string manager = is_status ? manager_name + "\x1fstatus" : manager_name;
     FieldSet cfg_fields = leaves(config, is_status);
     if (is_status) {
       FieldSet only;
@@ -1117,7 +1120,8 @@ struct ApiServer::Impl {
                         (conflicts.size() > 1 ? "s" : "") + ": ";
       for (size_t i = 0; i < conflicts.size(); ++i) {
         if (i) msg += "; ";
-        msg += "conflict with \"" + conflicts[i].first + "\": " + display_path(conflicts[i].second);
+        msg += "conflict with \"" + conflicts[i].first.substr(0, conflicts[i].first.find('\x1f')) + "\": " +
+               display_path(conflicts[i].second);
       }
       throw StatusError(409, "Conflict", msg);
     }

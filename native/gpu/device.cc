@@ -2,6 +2,7 @@
 
 #include <amd_smi/amdsmi.h>
 #include <dlfcn.h>
+#include <sys/stat.h>
 
 #include <cstdio>
 #include <cstring>
@@ -149,8 +150,27 @@ namespace {
 class MockBackend : public Backend {
  public:
   explicit MockBackend(const Value& fixture) : fixture_(fixture) {}
+  // File-backed: the fixture is re-read when its mtime changes, so tests can flip a
+  // device's telemetry (GPU flap / drain scenarios) while the agent runs.
+  explicit MockBackend(std::string path) : path_(std::move(path)) { reload(); }
+  void reload() {
+    if (path_.empty()) return;
+    struct stat st {};
+    if (::stat(path_.c_str(), &st) != 0) return;
+    if (st.st_mtim.tv_sec == mtime_.tv_sec && st.st_mtim.tv_nsec == mtime_.tv_nsec) return;
+    try {
+      Value v = json::parse(net::read_file(path_));
+      std::lock_guard<std::mutex> lk(mu_);
+      fixture_ = std::move(v);
+      mtime_ = st.st_mtim;
+    } catch (const std::exception& e) {
+      LOG_WARN("gpu") << "mock fixture reload failed: " << e.what();
+    }
+  }
   std::string name() const override { return "mock"; }
   std::vector<GpuInfo> discover() override {
+    reload();
+    std::lock_guard<std::mutex> lk(mu_);
     std::vector<GpuInfo> out;
     int i = 0;
     for (const auto& g : fixture_.get("gpus").items()) {
@@ -162,6 +182,8 @@ class MockBackend : public Backend {
     return out;
   }
   Telemetry sample(int index) override {
+    reload();
+    std::lock_guard<std::mutex> lk(mu_);
     int64_t t0 = metrics::now_ns();
     Telemetry t;
     t.index = index;
@@ -200,6 +222,9 @@ class MockBackend : public Backend {
 
  private:
   Value fixture_;
+  std::string path_;
+  struct timespec mtime_ {};
+  std::mutex mu_;
 };
 
 // ---------------------------------------------------------------------------
@@ -440,7 +465,7 @@ std::unique_ptr<Backend> make_mock_backend(const Value& fixture) { return std::m
 std::unique_ptr<Backend> make_backend(const std::string& kind, const std::string& mock_fixture_path) {
   auto load_mock = [&]() -> std::unique_ptr<Backend> {
     if (mock_fixture_path.empty()) return make_mock_backend(default_mi355x_fixture());
-    return make_mock_backend(json::parse(net::read_file(mock_fixture_path)));
+    return std::make_unique<MockBackend>(mock_fixture_path);
   };
   if (kind == "mock") return load_mock();
   if (kind == "amdsmi") return make_amdsmi_backend();

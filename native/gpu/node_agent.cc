@@ -1,0 +1,235 @@
+#include "gpu/node_agent.h"
+
+#include <cctype>
+#include <cmath>
+#include <cstdio>
+#include <set>
+
+#include "core/log.h"
+#include "gpu/diag.h"
+#include "kube/leader.h"
+
+namespace bgc::gpu {
+
+using json::Value;
+namespace types = kube::types;
+
+NodeAgentConfig NodeAgentConfig::from_env(const EnvConfig& env) {
+  NodeAgentConfig c;
+  c.listen_addr = env.str("listen_addr");
+  c.listen_port = env.u16("listen_port");
+  c.node_name = env.str("node_name");
+  c.backend = env.str_or("gpu_backend", "auto");
+  c.mock_fixture_path = env.str_or("mock_fixture_path", "");
+  c.poll_interval_ms = env.u64_or("poll_interval_ms", 1000);
+  c.heartbeat_secs = env.u64_or("heartbeat_secs", 30);
+  c.resource_name = env.str_or("resource_name", "amd.com/gpu");
+  c.label_prefix = env.str_or("label_prefix", "amd.com/gpu");
+  c.max_gpus = static_cast<int>(env.u64_or("max_gpus", 0));
+  c.run_diag = env.boolean_or("run_diag", false);
+  c.diag_hbm_bytes = env.u64_or("diag_hbm_bytes", 1ULL << 30);
+  c.create_node = env.boolean_or("create_node", false);
+  return c;
+}
+
+std::string sanitize_label_value(const std::string& v) {
+  std::string out;
+  for (char c : v) {
+    if (std::isalnum(static_cast<unsigned char>(c)) || c == '-' || c == '_' || c == '.') out.push_back(c);
+    else if (c == ' ' || c == '/' || c == ':') out.push_back('_');
+  }
+  while (!out.empty() && !std::isalnum(static_cast<unsigned char>(out.front()))) out.erase(0, 1);
+  while (!out.empty() && !std::isalnum(static_cast<unsigned char>(out.back()))) out.pop_back();
+  if (out.size() > 63) out.resize(63);
+  while (!out.empty() && !std::isalnum(static_cast<unsigned char>(out.back()))) out.pop_back();
+  return out;
+}
+
+std::string product_label(const GpuInfo& g) {
+  const std::string& m = g.market_name;
+  if (m.find("MI355") != std::string::npos) return "MI355X";
+  if (m.find("MI350") != std::string::npos) return "MI350X";
+  if (g.gfx_target.rfind("gfx950", 0) == 0) return "MI355X";
+  std::string s = m;
+  const std::string prefix = "AMD Instinct ";
+  if (s.rfind(prefix, 0) == 0) s = s.substr(prefix.size());
+  return sanitize_label_value(s);
+}
+
+static std::string hex16(uint64_t v) {
+  char buf[32];
+  std::snprintf(buf, sizeof(buf), "%016llx", static_cast<unsigned long long>(v));
+  return buf;
+}
+
+Value node_labels_patch(const NodeAgentConfig& cfg, const std::vector<GpuInfo>& gpus, int healthy,
+                        const DiagOutcome& diag) {
+  const std::string& p = cfg.label_prefix;
+  Value labels = Value::object();
+  labels[p + ".present"] = gpus.empty() ? "false" : "true";
+  labels[p + ".count"] = std::to_string(gpus.size());
+  labels[p + ".healthy-count"] = std::to_string(healthy);
+  if (!gpus.empty()) {
+    const GpuInfo& g = gpus.front();
+    std::string family = g.gfx_target;
+    size_t colon = family.find(':');
+    if (colon != std::string::npos) family = family.substr(0, colon);
+    labels[p + ".family"] = sanitize_label_value(family);
+    labels[p + ".product"] = product_label(g);
+    labels[p + ".market-name"] = sanitize_label_value(g.market_name);
+    uint64_t min_vram = UINT64_MAX;
+    std::set<uint64_t> hives;
+    for (const auto& x : gpus) {
+      min_vram = std::min(min_vram, x.vram_total_mb);
+      hives.insert(x.xgmi_hive_id);
+    }
+    labels[p + ".vram-gb"] = std::to_string(static_cast<uint64_t>(std::llround(static_cast<double>(min_vram) / 1024.0)));
+    // One hive id when every GPU sits on the same xGMI island; otherwise "mixed" plus
+    // the number of islands (TP groups must then be pinned per island).
+    labels[p + ".xgmi-hive-id"] = hives.size() == 1 ? hex16(*hives.begin()) : "mixed";
+    labels[p + ".xgmi-hives"] = std::to_string(hives.size());
+    labels[p + ".compute-partition"] = sanitize_label_value(g.compute_partition.empty() ? "unknown" : g.compute_partition);
+    labels[p + ".memory-partition"] = sanitize_label_value(g.memory_partition.empty() ? "unknown" : g.memory_partition);
+    if (g.num_cus) labels[p + ".cu-count"] = std::to_string(g.num_cus);
+  }
+  labels[p + ".diag"] = !diag.ran ? "skipped" : diag.passed ? "passed" : "failed";
+  Value topo = Value::array();
+  for (const auto& g : gpus) {
+    topo.push_back(Value::object({{"index", g.index}, {"uuid", g.uuid}, {"bdf", g.bdf}, {"hive", hex16(g.xgmi_hive_id)},
+                                  {"node", static_cast<unsigned long long>(g.xgmi_node_id)}, {"numa", g.numa_node}}));
+  }
+  Value meta = Value::object({{"name", cfg.node_name}, {"labels", labels},
+                              {"annotations", Value::object({{p + ".topology", topo.dump()}})}});
+  return Value::object({{"apiVersion", "v1"}, {"kind", "Node"}, {"metadata", meta}});
+}
+
+Value node_status_patch(const NodeAgentConfig& cfg, const std::vector<GpuInfo>& gpus, int healthy,
+                        const std::string& unhealthy_reason) {
+  Value status = Value::object();
+  status["capacity"] = Value::object({{cfg.resource_name, std::to_string(gpus.size())}});
+  status["allocatable"] = Value::object({{cfg.resource_name, std::to_string(healthy)}});
+  bool all_ok = healthy == static_cast<int>(gpus.size()) && !gpus.empty();
+  Value cond = Value::object({{"type", "AMDGPUHealthy"},
+                              {"status", all_ok ? "True" : "False"},
+                              {"reason", all_ok ? "AllGPUsHealthy" : "GPUUnhealthy"},
+                              {"message", all_ok ? std::to_string(healthy) + " MI355X GPUs healthy" : unhealthy_reason},
+                              {"lastHeartbeatTime", kube::rfc3339_micro_now().substr(0, 19) + "Z"}});
+  status["conditions"] = Value::array({cond});
+  return Value::object({{"apiVersion", "v1"}, {"kind", "Node"}, {"metadata", Value::object({{"name", cfg.node_name}})},
+                        {"status", status}});
+}
+
+NodeAgent::NodeAgent(kube::KubeClient& client, std::unique_ptr<Backend> backend, NodeAgentConfig cfg)
+    : client_(client), backend_(std::move(backend)), cfg_(std::move(cfg)) {}
+
+NodeAgent::~NodeAgent() { stop(); }
+
+void NodeAgent::init() {
+  gpus_ = backend_->discover();
+  if (cfg_.max_gpus > 0 && static_cast<int>(gpus_.size()) > cfg_.max_gpus) gpus_.resize(static_cast<size_t>(cfg_.max_gpus));
+  if (gpus_.empty()) throw std::runtime_error("no GPUs discovered via " + backend_->name());
+  LOG_INFO("node_agent") << "discovered " << gpus_.size() << " GPU(s) via " << backend_->name() << ": "
+                         << gpus_.front().market_name << " " << gpus_.front().gfx_target << " "
+                         << gpus_.front().vram_total_mb << " MB";
+  if (cfg_.run_diag) {
+    diag_.ran = true;
+    Diag& d = Diag::instance();
+    for (const auto& g : gpus_) {
+      int dev = g.hip_id >= 0 ? g.hip_id : g.index;
+      Value hbm = d.hbm(dev, cfg_.diag_hbm_bytes, 2, 0x5eed + static_cast<uint32_t>(dev));
+      Value mfma = d.mfma(dev, 16, 2048, 0x5eed + static_cast<uint32_t>(dev));
+      bool ok = hbm.get("passed").as_bool() && mfma.get("passed").as_bool();
+      diag_.passed = diag_.passed && ok;
+      diag_.per_gpu.push_back(Value::object({{"index", g.index}, {"hbm", hbm}, {"mfma", mfma}, {"passed", ok}}));
+      LOG_INFO("node_agent") << "diag gpu " << g.index << ": " << (ok ? "passed" : "FAILED") << " read "
+                             << hbm.get("read_gbps").as_double() << " GB/s, mfma " << mfma.get("tflops").as_double()
+                             << " TFLOP/s";
+    }
+  }
+  std::vector<int> idx;
+  for (const auto& g : gpus_) idx.push_back(g.index);
+  poller_ = std::make_unique<TelemetryPoller>(*backend_, idx, std::chrono::milliseconds(cfg_.poll_interval_ms));
+  poller_->poll_once();
+  if (cfg_.create_node && !client_.get_opt(types::Node, "", cfg_.node_name)) {
+    client_.create(types::Node, "", Value::object({{"apiVersion", "v1"}, {"kind", "Node"},
+                                                   {"metadata", Value::object({{"name", cfg_.node_name}})}}));
+  }
+}
+
+int NodeAgent::healthy_count(std::string* reason) const {
+  auto snap = poller_ ? poller_->snapshot() : nullptr;
+  int healthy = 0;
+  std::string why;
+  for (size_t i = 0; i < gpus_.size(); ++i) {
+    bool ok = true;
+    if (snap && i < snap->health.size()) {
+      ok = snap->health[i].healthy;
+      if (!ok) why += "gpu" + std::to_string(gpus_[i].index) + ": " + snap->health[i].reason + "; ";
+    }
+    if (diag_.ran && i < diag_.per_gpu.size() && !diag_.per_gpu[i].get("passed").as_bool()) {
+      ok = false;
+      why += "gpu" + std::to_string(gpus_[i].index) + ": diagnostics failed; ";
+    }
+    if (ok) ++healthy;
+  }
+  if (reason) *reason = why;
+  return healthy;
+}
+
+void NodeAgent::publish() {
+  std::lock_guard<std::mutex> lk(publish_mu_);
+  std::string reason;
+  int healthy = healthy_count(&reason);
+  client_.apply(types::Node, "", cfg_.node_name, node_labels_patch(cfg_, gpus_, healthy, diag_), kNodeAgentManager, true);
+  client_.apply_status(types::Node, "", cfg_.node_name, node_status_patch(cfg_, gpus_, healthy, reason),
+                       kNodeAgentManager, true);
+  LOG_INFO("node_agent") << "published node " << cfg_.node_name << ": " << cfg_.resource_name << " capacity "
+                         << gpus_.size() << ", allocatable " << healthy;
+}
+
+void NodeAgent::start() {
+  poller_->on_health_change([this](const Snapshot&) {
+    try {
+      publish();
+    } catch (const std::exception& e) {
+      LOG_ERROR("node_agent") << "publish after health change failed: " << e.what();
+    }
+  });
+  poller_->start();
+  heartbeat_ = std::thread([this] {
+    while (!stop_.wait_for(std::chrono::seconds(cfg_.heartbeat_secs))) {
+      try {
+        publish();
+      } catch (const std::exception& e) {
+        LOG_ERROR("node_agent") << "heartbeat publish failed: " << e.what();
+      }
+    }
+  });
+}
+
+void NodeAgent::stop() {
+  stop_.cancel();
+  if (poller_) poller_->stop();
+  if (heartbeat_.joinable()) heartbeat_.join();
+}
+
+Value NodeAgent::describe() const {
+  Value gpus = Value::array();
+  for (const auto& g : gpus_) gpus.push_back(to_json(g));
+  Value out = Value::object({{"node", cfg_.node_name}, {"backend", backend_->name()}, {"gpus", gpus}});
+  if (poller_) {
+    auto snap = poller_->snapshot();
+    Value tel = Value::array();
+    for (const auto& t : snap->devices) tel.push_back(to_json(t));
+    out["telemetry"] = tel;
+    out["poll_us"] = snap->poll_us;
+    out["polls"] = static_cast<unsigned long long>(poller_->polls());
+  }
+  std::string reason;
+  out["healthy"] = healthy_count(&reason);
+  out["unhealthy_reason"] = reason;
+  out["diag"] = diag_.per_gpu;
+  return out;
+}
+
+}  // namespace bgc::gpu

@@ -1,0 +1,90 @@
+// MI355X node agent (north-star N3): advertises each healthy MI355X as an `amd.com/gpu`
+// extended resource and publishes topology labels so RCCL TP/DP/PP pods can be
+// co-scheduled on one xGMI island.
+//
+//   labels       amd.com/gpu.present=true, .family=gfx950, .product=MI355X, .count=8,
+//                .vram-gb=288, .xgmi-hive-id=<hex>, .compute-partition=SPX,
+//                .memory-partition=NPS1, .cu-count=256, .healthy-count=8, .diag=passed
+//   annotation   amd.com/gpu.topology = JSON [{index,uuid,bdf,hive,node,numa}]
+//   status       capacity/allocatable amd.com/gpu, condition AMDGPUHealthy
+//
+// Labels go through server-side apply on the Node, capacity/condition through SSA on
+// nodes/status, both with field manager "bacchus-gpu-node-agent" so kubelet-owned
+// fields are untouched.  Health flips from the telemetry side thread re-apply status.
+#pragma once
+
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "core/env_config.h"
+#include "core/json.h"
+#include "gpu/device.h"
+#include "gpu/telemetry.h"
+#include "kube/client.h"
+
+namespace bgc::gpu {
+
+constexpr const char* kNodeAgentManager = "bacchus-gpu-node-agent";
+
+struct NodeAgentConfig {
+  std::string listen_addr = "0.0.0.0";
+  uint16_t listen_port = 12324;
+  std::string node_name;
+  std::string backend = "auto";       // auto | amdsmi | mock
+  std::string mock_fixture_path;
+  uint64_t poll_interval_ms = 1000;
+  uint64_t heartbeat_secs = 30;
+  std::string resource_name = "amd.com/gpu";
+  std::string label_prefix = "amd.com/gpu";
+  int max_gpus = 0;                    // 0 = all discovered
+  bool run_diag = false;               // HIP HBM + MFMA check before advertising
+  uint64_t diag_hbm_bytes = 1ULL << 30;
+  bool create_node = false;            // test clusters without a kubelet
+  static NodeAgentConfig from_env(const EnvConfig& env);
+};
+
+struct DiagOutcome {
+  bool ran = false;
+  bool passed = true;
+  json::Value per_gpu = json::Value::array();
+};
+
+std::string sanitize_label_value(const std::string& v);
+std::string product_label(const GpuInfo& g);
+
+// Pure rendering of the Node patches (unit-tested).
+json::Value node_labels_patch(const NodeAgentConfig& cfg, const std::vector<GpuInfo>& gpus, int healthy,
+                              const DiagOutcome& diag);
+json::Value node_status_patch(const NodeAgentConfig& cfg, const std::vector<GpuInfo>& gpus, int healthy,
+                              const std::string& unhealthy_reason);
+
+class NodeAgent {
+ public:
+  NodeAgent(kube::KubeClient& client, std::unique_ptr<Backend> backend, NodeAgentConfig cfg);
+  ~NodeAgent();
+  // Discovery (+ optional diagnostics); throws if no GPU is found.
+  void init();
+  // Apply labels + status now.
+  void publish();
+  void start();  // telemetry thread + heartbeat thread
+  void stop();
+  json::Value describe() const;  // for GET /gpus
+  const std::vector<GpuInfo>& gpus() const { return gpus_; }
+  TelemetryPoller* poller() { return poller_.get(); }
+
+ private:
+  int healthy_count(std::string* reason) const;
+  kube::KubeClient& client_;
+  std::unique_ptr<Backend> backend_;
+  NodeAgentConfig cfg_;
+  std::vector<GpuInfo> gpus_;
+  DiagOutcome diag_;
+  std::unique_ptr<TelemetryPoller> poller_;
+  std::mutex publish_mu_;
+  CancelToken stop_;
+  std::thread heartbeat_;
+};
+
+}  // namespace bgc::gpu

@@ -10,6 +10,7 @@
 #include "core/roctx.h"
 #include "gpu/device.h"
 #include "gpu/diag.h"
+#include "gpu/node_agent.h"
 #include "gpu/telemetry.h"
 
 namespace py = pybind11;
@@ -147,6 +148,23 @@ void register_gpu(py::module_& m) {
     return v.dump();
   }, py::arg("device"), py::arg("waves_per_cu") = 32, py::arg("iters") = 4096, py::arg("seed") = 0x5eed);
   m.def("roctx_available", &bgc::roctx::available);
+
+  // Node agent rendering (pure functions).
+  m.def("node_patches", [](const std::string& gpus_json, int healthy, const std::string& node, bool diag_ran,
+                           bool diag_passed, const std::string& reason) {
+    bgc::gpu::NodeAgentConfig cfg;
+    cfg.node_name = node;
+    std::vector<bgc::gpu::GpuInfo> gpus;
+    bgc::json::Value parsed = bgc::json::parse(gpus_json);
+    for (const auto& g : parsed.items()) gpus.push_back(bgc::gpu::gpu_info_from_json(g));
+    bgc::gpu::DiagOutcome d;
+    d.ran = diag_ran;
+    d.passed = diag_passed;
+    return py::make_tuple(bgc::gpu::node_labels_patch(cfg, gpus, healthy, d).dump(),
+                          bgc::gpu::node_status_patch(cfg, gpus, healthy, reason).dump());
+  }, py::arg("gpus_json"), py::arg("healthy"), py::arg("node") = "node-0", py::arg("diag_ran") = false,
+     py::arg("diag_passed") = true, py::arg("reason") = "");
+  m.def("sanitize_label_value", &bgc::gpu::sanitize_label_value);
 }
 
 }  // namespace bgc_py

@@ -1,0 +1,53 @@
+"""Node agent against kube-lite with the file-backed mock amdsmi backend: Node labels,
+amd.com/gpu capacity/allocatable, and GPU flap handling (BASELINE config #5)."""
+import json
+import os
+
+import pytest
+import requests
+
+from bacchus_gpu_controller_amd.testing.cluster import NODE_AGENT_TOKEN, Cluster, free_port
+from bacchus_gpu_controller_amd.testing.kubeapi import wait_for
+
+pytestmark = pytest.mark.slow
+
+
+def test_node_agent_advertises_and_flaps(nat):
+    with Cluster(admission=False, controller=False) as c:
+        fixture = os.path.join(c.workdir, "gpus.json")
+        f = json.loads(nat.default_mi355x_fixture(8))
+        with open(fixture, "w") as fh:
+            json.dump(f, fh)
+        port = free_port()
+        env = c.component_env(NODE_AGENT_TOKEN, port)
+        env.update({"CONF_NODE_NAME": "mi355x-0", "CONF_GPU_BACKEND": "mock", "CONF_MOCK_FIXTURE_PATH": fixture,
+                    "CONF_POLL_INTERVAL_MS": "50", "CONF_CREATE_NODE": "true", "CONF_HEARTBEAT_SECS": "1"})
+        c.start_process("node-agent", "node-agent", env)
+        node = wait_for(lambda: (lambda n: n if n and n.get("status", {}).get("capacity") else None)(
+            c.admin.get_or_none("nodes", "mi355x-0")), timeout=10, desc="node published")
+        labels = node["metadata"]["labels"]
+        assert labels["amd.com/gpu.product"] == "MI355X" and labels["amd.com/gpu.count"] == "8"
+        assert labels["amd.com/gpu.vram-gb"] == "288"
+        assert node["status"]["capacity"]["amd.com/gpu"] == "8"
+        assert node["status"]["allocatable"]["amd.com/gpu"] == "8"
+        managers = {m["manager"] for m in node["metadata"]["managedFields"]}
+        assert "bacchus-gpu-node-agent" in managers
+        gp = requests.get(f"http://127.0.0.1:{port}/gpus", timeout=5).json()
+        assert len(gp["gpus"]) == 8 and gp["polls"] >= 1
+        metrics = requests.get(f"http://127.0.0.1:{port}/metrics", timeout=5).text
+        assert 'amd_gpu_power_watts{gpu="0"}' in metrics
+
+        # flap: gpu 3 overheats -> allocatable 7, condition False
+        f["gpus"][3]["telemetry"]["temp_hotspot_c"] = 121
+        with open(fixture, "w") as fh:
+            json.dump(f, fh)
+        wait_for(lambda: c.admin.get("nodes", "mi355x-0")["status"]["allocatable"]["amd.com/gpu"] == "7",
+                 timeout=10, desc="allocatable drops to 7")
+        cond = c.admin.get("nodes", "mi355x-0")["status"]["conditions"][0]
+        assert cond["status"] == "False" and "gpu3" in cond["message"]
+        # recovery
+        f["gpus"][3]["telemetry"]["temp_hotspot_c"] = 50
+        with open(fixture, "w") as fh:
+            json.dump(f, fh)
+        wait_for(lambda: c.admin.get("nodes", "mi355x-0")["status"]["allocatable"]["amd.com/gpu"] == "8",
+                 timeout=10, desc="allocatable back to 8")
