@@ -1,0 +1,266 @@
+"""Headline benchmark: UserBootstrap onboarding churn on an MI355X node.
+
+Metric (BASELINE.json): "reconcile p99 (ms) + admission p50 (ms); CR apply→Ready/sec on
+8×MI355X node", reported at 1/2/4/8 advertised GPUs.
+
+One rank per GPU (torchrun).  Rank 0 brings up the control plane: kube-lite (API
+server), the TLS admission webhook, the controller, the synchronizer (watch mode, fed by
+a fake Google Drive sheet that approves every benchmark tenant) and the node agent,
+which advertises the N GPUs of this job as `amd.com/gpu` (amdsmi discovery + telemetry
+side thread).  Every rank then acts as a tenant population on its GPU: each step it
+applies B UserBootstraps as OIDC users in group `gpu` and waits until each is Ready
+(Namespace + ResourceQuota with requests.amd.com/gpu + RoleBinding — BASELINE.md's
+definition), deleting the previous step's tenants (GC churn) in the same step.
+
+Weak scaling: per-rank work (B CRs/step) is fixed; the whole-job value is
+total Ready CRs / wall time of the K timed steps (max over ranks).
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+METRIC = "reconcile p99 (ms) + admission p50 (ms); CR apply→Ready/sec on 8×MI355X node"
+
+
+def _pct(v, q):
+    if not v:
+        return None
+    v = sorted(v)
+    k = max(0, min(len(v) - 1, int(round(q * len(v) + 0.5)) - 1))
+    return v[k]
+
+
+class Dist:
+    """torch.distributed wrapper (RCCL on GPUs, gloo on CPU); trivial for one rank."""
+
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.torch = None
+        self.cuda = False
+        try:
+            import torch
+
+            self.torch = torch
+            self.cuda = torch.cuda.is_available()
+        except Exception:  # noqa: BLE001
+            self.torch = None
+        if self.cuda:
+            self.torch.cuda.set_device(self.local_rank % max(1, self.torch.cuda.device_count()))
+        if self.world > 1:
+            import torch.distributed as dist
+
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group(backend="nccl" if self.cuda else "gloo")
+            self.dist = dist
+        else:
+            self.dist = None
+
+    def barrier(self):
+        if self.dist:
+            if self.cuda:
+                self.dist.barrier(device_ids=[self.torch.cuda.current_device()])
+            else:
+                self.dist.barrier()
+
+    def sync(self):
+        if self.cuda:
+            self.torch.cuda.synchronize()
+
+    def broadcast_obj(self, obj):
+        if not self.dist:
+            return obj
+        lst = [obj]
+        self.dist.broadcast_object_list(lst, src=0)
+        return lst[0]
+
+    def gather_obj(self, obj):
+        if not self.dist:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
+    def max_scalar(self, x):
+        if not self.dist:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64, device="cuda" if self.cuda else "cpu")
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def _names(rank, step, batch):
+    return [f"r{rank}-s{step}-u{i}" for i in range(batch)]
+
+
+def _samples(url, verify=None):
+    import requests
+
+    return requests.get(url, timeout=10, verify=verify).json()["samples"]
+
+
+def _clear(url, verify=None):
+    import requests
+
+    requests.delete(url, timeout=10, verify=verify)
+
+
+def run(args):
+    d = Dist()
+    n = args.gpus if args.gpus else d.world
+    from bacchus_gpu_controller_amd import native
+    from bacchus_gpu_controller_amd.testing.cluster import ADMIN_TOKEN, Cluster
+    from bacchus_gpu_controller_amd.testing.fake_google import FakeGoogle
+
+    nat = native()
+    cluster = google = None
+    info = None
+    total_steps = args.warmup + args.steps
+    if d.rank == 0:
+        google = FakeGoogle().start()
+        rows = [{"id_username": name, "gpu": 1, "cpu": 8, "mem": 64, "storage": 100}
+                for r in range(d.world) for s in range(total_steps) for name in _names(r, s, args.batch)]
+        google.set_rows(rows)
+        cluster = Cluster(controller_env={"CONF_WORKERS": str(args.controller_workers)},
+                          log_level=args.log_level)
+        cluster.start()
+        cluster.start_synchronizer(google, interval=60, extra_env={"CONF_WATCH": "true",
+                                                                   "CONF_WORKERS": str(args.sync_workers),
+                                                                   "RUST_LOG": args.log_level})
+        cluster.start_node_agent(max_gpus=n, n_mock_gpus=n, poll_interval_ms=args.poll_ms,
+                                 extra_env={"RUST_LOG": args.log_level})
+        info = {"server": cluster.server, "controller": f"http://127.0.0.1:{cluster.controller_port}",
+                "admission": f"https://127.0.0.1:{cluster.admission_port}",
+                "ca": os.path.join(cluster.cert_dir, "ca.crt"),
+                "node_agent": f"http://127.0.0.1:{cluster.node_agent_port}"}
+    info = d.broadcast_obj(info)
+    try:
+        driver = nat.ChurnDriver(info["server"], ADMIN_TOKEN, f"r{d.rank}-", args.concurrency)
+        driver.start()
+        time.sleep(0.2)
+        prev = None
+        lat, clat = [], []
+        ready = failed = timeouts = 0
+        t_start = None
+        errors = []
+        for s in range(total_steps):
+            if s == args.warmup:
+                d.barrier()
+                d.sync()
+                if d.rank == 0:
+                    _clear(info["controller"] + "/debug/samples/reconcile")
+                    _clear(info["server"] + "/debug/samples/webhook")
+                    _clear(info["admission"] + "/debug/samples/admission", verify=info["ca"])
+                    _clear(info["node_agent"] + "/debug/samples/telemetry_poll")
+                d.barrier()
+                t_start = time.perf_counter()
+            names = _names(d.rank, s, args.batch)
+            res = json.loads(driver.step(names, args.timeout))
+            if prev:
+                driver.remove(prev)
+            prev = names
+            if s >= args.warmup:
+                lat += res["ready_latency_s"]
+                clat += res["create_latency_s"]
+                ready += res["ready"]
+                failed += res["failed"]
+                timeouts += res["timeouts"]
+                errors += res["errors"]
+        d.sync()
+        d.barrier()
+        elapsed = time.perf_counter() - t_start
+        elapsed = d.max_scalar(elapsed)
+        driver.remove(prev)
+        driver.stop()
+        per_rank = d.gather_obj({"ready": ready, "failed": failed, "timeouts": timeouts, "lat": lat, "clat": clat,
+                                 "errors": errors[:3]})
+        if d.rank != 0:
+            return None
+        rec = _samples(info["controller"] + "/debug/samples/reconcile")
+        hook = _samples(info["server"] + "/debug/samples/webhook")
+        adm = _samples(info["admission"] + "/debug/samples/admission", verify=info["ca"])
+        tel = _samples(info["node_agent"] + "/debug/samples/telemetry_poll")
+        all_lat = [x for p in per_rank for x in p["lat"]]
+        all_clat = [x for p in per_rank for x in p["clat"]]
+        total_ready = sum(p["ready"] for p in per_rank)
+        total_failed = sum(p["failed"] + p["timeouts"] for p in per_rank)
+        value = total_ready / elapsed if elapsed > 0 else 0.0
+        ms = lambda v: None if v is None else round(v * 1e3, 4)  # noqa: E731
+        out = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "CR/s",
+            "n_gpus": n,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic",
+            "config": {"model": "UserBootstrap onboarding churn (kube-lite + TLS admission + controller + "
+                                "synchronizer + MI355X node-agent)",
+                       "global_batch": args.batch * d.world, "seq_len": None, "parallelism": f"dp{d.world}"},
+            "reconcile_p99_ms": ms(_pct(rec, 0.99)),
+            "reconcile_p50_ms": ms(_pct(rec, 0.50)),
+            "reconciles": len(rec),
+            "admission_p50_ms": ms(_pct(hook, 0.50)),
+            "admission_p99_ms": ms(_pct(hook, 0.99)),
+            "admission_handler_p50_ms": ms(_pct(adm, 0.50)),
+            "apply_to_ready_p50_ms": ms(_pct(all_lat, 0.50)),
+            "apply_to_ready_p99_ms": ms(_pct(all_lat, 0.99)),
+            "create_p50_ms": ms(_pct(all_clat, 0.50)),
+            "telemetry_poll_p50_ms": ms(_pct(tel, 0.50)),
+            "ready_crs": total_ready,
+            "failed_crs": total_failed,
+            "reference_structural": {"apply_to_ready_p50_s": 30.0, "apply_to_ready_p99_s": 59.4,
+                                     "note": "reference gates readiness on a 60 s sheet poll (synchronizer.rs:192)"},
+        }
+        if total_failed:
+            out["errors"] = [e for p in per_rank for e in p["errors"]][:5]
+        return out
+    finally:
+        if d.rank == 0:
+            d_barrier_safe = True  # noqa: F841
+        if cluster is not None:
+            cluster.stop()
+        if google is not None:
+            google.stop()
+        d.close()
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=100, help="UserBootstraps applied per rank per step")
+    ap.add_argument("--concurrency", type=int, default=32)
+    ap.add_argument("--timeout", type=float, default=120.0)
+    ap.add_argument("--controller-workers", type=int, default=16)
+    ap.add_argument("--sync-workers", type=int, default=8)
+    ap.add_argument("--poll-ms", type=int, default=250)
+    ap.add_argument("--log-level", default="warn")
+    ap.add_argument("--json-out", default="")
+    args = ap.parse_args(argv)
+    out = run(args)
+    if out is not None:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -198,6 +198,23 @@ class Cluster:
                      20, desc="synchronizer /health")
         return p
 
+    def start_node_agent(self, node_name="mi355x-0", max_gpus=0, backend="auto", n_mock_gpus=8, extra_env=None,
+                         poll_interval_ms=1000):
+        """Start the native node agent; amdsmi when available, else a mock MI355X hive."""
+        fixture = os.path.join(self.workdir, "gpus.json")
+        with open(fixture, "w") as f:
+            f.write(native().default_mi355x_fixture(n_mock_gpus))
+        self.node_agent_port = free_port()
+        env = self.component_env(NODE_AGENT_TOKEN, self.node_agent_port)
+        env.update({"CONF_NODE_NAME": node_name, "CONF_GPU_BACKEND": backend, "CONF_MOCK_FIXTURE_PATH": fixture,
+                    "CONF_MAX_GPUS": str(max_gpus), "CONF_CREATE_NODE": "true",
+                    "CONF_POLL_INTERVAL_MS": str(poll_interval_ms)})
+        env.update(extra_env or {})
+        p = self.start_process("node-agent", "node-agent", env)
+        wait_for(lambda: requests.get(f"http://127.0.0.1:{self.node_agent_port}/health", timeout=1).text == "pong",
+                 60, desc="node-agent /health")
+        return p
+
     def start_process(self, name, exe, env):
         self.procs[name] = Proc(name, [binary(exe)], env, self.workdir)
         return self.procs[name]

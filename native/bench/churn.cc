@@ -1,0 +1,189 @@
+#include "bench/churn.h"
+
+#include <array>
+#include <future>
+
+#include "core/log.h"
+#include "core/metrics.h"
+#include "kube/runtime.h"
+
+namespace bgc::bench {
+
+using json::Value;
+namespace types = kube::types;
+
+ChurnDriver::ChurnDriver(ChurnOptions o) : opts_(std::move(o)) {
+  kube::KubeConfig kc;
+  kc.server = opts_.server;
+  kc.token = opts_.admin_token;
+  kc.timeout_ms = 60000;
+  admin_ = std::make_unique<kube::KubeClient>(kc);
+  http::ClientOptions ho;
+  ho.base_url = opts_.server;
+  ho.timeout_ms = 60000;
+  ho.max_idle = static_cast<size_t>(opts_.concurrency) * 2;
+  http_ = std::make_unique<http::Client>(ho);
+  pool_ = std::make_unique<ThreadPool>(static_cast<size_t>(std::max(1, opts_.concurrency)));
+}
+
+ChurnDriver::~ChurnDriver() { stop(); }
+
+void ChurnDriver::mark(const std::string& name, int which, int64_t t) {
+  if (name.compare(0, opts_.name_prefix.size(), opts_.name_prefix) != 0) return;
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = tracks_.find(name);
+  if (it == tracks_.end()) {
+    auto& e = early_[name];
+    if (!e[static_cast<size_t>(which)]) e[static_cast<size_t>(which)] = t;
+    return;
+  }
+  Track& tr = it->second;
+  int64_t* slot = which == 0 ? &tr.t_ns : which == 1 ? &tr.t_rq : &tr.t_rb;
+  if (!*slot) *slot = t;
+  if (ready_locked(tr)) cv_.notify_all();
+}
+
+void ChurnDriver::start() {
+  struct W {
+    const kube::ResourceType* rt;
+    int which;
+  };
+  for (W w : {W{&types::Namespace, 0}, W{&types::ResourceQuota, 1}, W{&types::RoleBinding, 2}}) {
+    watchers_.emplace_back([this, w] {
+      kube::Watcher watcher(*admin_, *w.rt);
+      std::string key = opts_.gpu_quota_key;
+      watcher.run(stop_, [&](const kube::WatchEvent& ev) {
+        auto handle = [&](const Value& o) {
+          std::string name = kube::meta_name(o);
+          if (w.which == 1 && !o.get("spec").get("hard").contains(key)) return;
+          mark(name, w.which, metrics::now_ns());
+        };
+        if (ev.type == kube::WatchEvent::Type::Restarted) {
+          for (const auto& o : ev.objects) handle(*o);
+        } else if (ev.type != kube::WatchEvent::Type::Deleted) {
+          handle(*ev.object);
+        }
+      });
+    });
+  }
+}
+
+json::Value ChurnDriver::step(const std::vector<std::string>& names, double timeout_s) {
+  int64_t t0 = metrics::now_ns();
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (const auto& n : names) {
+      Track t;
+      t.t_start = t0;
+      auto e = early_.find(n);
+      if (e != early_.end()) {
+        t.t_ns = e->second[0];
+        t.t_rq = e->second[1];
+        t.t_rb = e->second[2];
+        early_.erase(e);
+      }
+      tracks_[n] = t;
+    }
+  }
+  std::vector<std::future<void>> futs;
+  futs.reserve(names.size());
+  for (const auto& n : names) {
+    futs.push_back(pool_->submit([this, n] {
+      int64_t ts = metrics::now_ns();
+      Value body = Value::object({{"apiVersion", "bacchus.io/v1"}, {"kind", "UserBootstrap"},
+                                  {"metadata", Value::object({{"name", n}})}, {"spec", Value::object()}});
+      http::Headers h;
+      h.set("Authorization", "Bearer " + opts_.admin_token);
+      h.set("Impersonate-User", opts_.user_prefix + n);
+      h.set("Impersonate-Group", opts_.group);
+      h.set("Content-Type", "application/json");
+      std::string err;
+      try {
+        http::Response r = http_->request("POST", types::UserBootstrap.collection_path(), body.dump(), &h);
+        if (r.status != 201 && r.status != 200) err = std::to_string(r.status) + " " + r.body;
+      } catch (const std::exception& e) {
+        err = e.what();
+      }
+      std::lock_guard<std::mutex> lk(mu_);
+      Track& t = tracks_[n];
+      t.t_start = ts;
+      t.t_created = metrics::now_ns();
+      if (!err.empty()) {
+        t.failed = true;
+        t.error = err;
+      }
+      cv_.notify_all();
+    }));
+  }
+  for (auto& f : futs) f.get();
+  auto deadline = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s);
+  Value out = Value::object();
+  std::unique_lock<std::mutex> lk(mu_);
+  auto all_done = [&] {
+    for (const auto& n : names) {
+      const Track& t = tracks_[n];
+      if (!t.failed && !ready_locked(t)) return false;
+    }
+    return true;
+  };
+  cv_.wait_until(lk, deadline, all_done);
+  int64_t t_end = metrics::now_ns();
+  Value lat = Value::array(), clat = Value::array(), errs = Value::array();
+  int ready = 0, failed = 0, timeouts = 0;
+  int64_t last_ready = t0;
+  for (const auto& n : names) {
+    const Track& t = tracks_[n];
+    if (t.failed) {
+      ++failed;
+      if (errs.size() < 5) errs.push_back(n + ": " + t.error);
+    } else if (ready_locked(t)) {
+      ++ready;
+      int64_t tr = std::max({t.t_ns, t.t_rq, t.t_rb});
+      last_ready = std::max(last_ready, tr);
+      lat.push_back(static_cast<double>(tr - t.t_start) * 1e-9);
+      clat.push_back(static_cast<double>(t.t_created - t.t_start) * 1e-9);
+    } else {
+      ++timeouts;
+    }
+    tracks_.erase(n);
+  }
+  out["ready"] = ready;
+  out["failed"] = failed;
+  out["timeouts"] = timeouts;
+  out["elapsed_s"] = static_cast<double>((ready == static_cast<int>(names.size()) ? last_ready : t_end) - t0) * 1e-9;
+  out["ready_latency_s"] = lat;
+  out["create_latency_s"] = clat;
+  out["errors"] = errs;
+  return out;
+}
+
+int ChurnDriver::remove(const std::vector<std::string>& names) {
+  std::vector<std::future<bool>> futs;
+  for (const auto& n : names) {
+    futs.push_back(pool_->submit([this, n] {
+      try {
+        admin_->remove(types::UserBootstrap, "", n);
+        return true;
+      } catch (const kube::ApiError& e) {
+        return e.code() == 404;
+      } catch (const std::exception&) {
+        return false;
+      }
+    }));
+  }
+  int failures = 0;
+  for (auto& f : futs) failures += f.get() ? 0 : 1;
+  std::lock_guard<std::mutex> lk(mu_);
+  for (const auto& n : names) early_.erase(n);
+  return failures;
+}
+
+void ChurnDriver::stop() {
+  stop_.cancel();
+  for (auto& t : watchers_) {
+    if (t.joinable()) t.join();
+  }
+  watchers_.clear();
+}
+
+}  // namespace bgc::bench

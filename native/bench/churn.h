@@ -1,0 +1,77 @@
+// Native churn driver for the headline benchmark (BASELINE.json: "reconcile p99 (ms) +
+// admission p50 (ms); CR apply->Ready/sec").
+//
+// One driver per benchmark rank.  It creates UserBootstraps as OIDC users (through the
+// apiserver -> TLS webhook path, exactly like `kubectl apply` by a tenant), and watches
+// Namespaces, ResourceQuotas and RoleBindings to timestamp "Ready" — the harness
+// definition from BASELINE.md: Namespace, ResourceQuota (with the GPU key) and
+// RoleBinding all exist.  Everything runs on native threads so the load generator is
+// never the bottleneck being measured.
+#pragma once
+
+#include <array>
+#include <atomic>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "core/cancel.h"
+#include "core/http.h"
+#include "core/json.h"
+#include "core/threadpool.h"
+#include "kube/client.h"
+
+namespace bgc::bench {
+
+struct ChurnOptions {
+  std::string server;
+  std::string admin_token;
+  std::string user_prefix = "oidc:";
+  std::string group = "gpu";
+  std::string gpu_quota_key = "requests.amd.com/gpu";
+  int concurrency = 32;
+  std::string name_prefix;  // only names with this prefix are tracked (one driver per rank)
+};
+
+class ChurnDriver {
+ public:
+  explicit ChurnDriver(ChurnOptions o);
+  ~ChurnDriver();
+  void start();
+  // Creates every name concurrently and waits for all to be Ready (or timeout).
+  // Returns {"ready": n, "failed": n, "timeouts": n, "elapsed_s": x,
+  //          "ready_latency_s": [...], "create_latency_s": [...], "errors": [...]}.
+  json::Value step(const std::vector<std::string>& names, double timeout_s);
+  // Deletes (as cluster admin) concurrently; returns number of failures.
+  int remove(const std::vector<std::string>& names);
+  void stop();
+
+ private:
+  struct Track {
+    int64_t t_start = 0;
+    int64_t t_created = 0;
+    int64_t t_ns = 0, t_rq = 0, t_rb = 0;
+    bool failed = false;
+    std::string error;
+  };
+  void mark(const std::string& name, int which, int64_t t);
+  bool ready_locked(const Track& t) const { return t.t_ns && t.t_rq && t.t_rb; }
+
+  ChurnOptions opts_;
+  std::unique_ptr<kube::KubeClient> admin_;
+  std::unique_ptr<http::Client> http_;
+  std::unique_ptr<ThreadPool> pool_;
+  CancelToken stop_;
+  std::vector<std::thread> watchers_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::unordered_map<std::string, Track> tracks_;
+  // events that arrived before the step registered the name
+  std::unordered_map<std::string, std::array<int64_t, 3>> early_;
+};
+
+}  // namespace bgc::bench

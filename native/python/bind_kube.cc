@@ -1,5 +1,68 @@
+// Kube-side bindings: native churn driver (bench), in-process kube-lite, workqueue.
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <chrono>
+
+#include "apiserver/server.h"
+#include "bench/churn.h"
+#include "kube/runtime.h"
+
 namespace py = pybind11;
+
 namespace bgc_py {
-void register_kube(py::module_& m) {}
+
+void register_kube(py::module_& m) {
+  py::class_<bgc::bench::ChurnDriver>(m, "ChurnDriver")
+      .def(py::init([](const std::string& server, const std::string& token, const std::string& prefix,
+                       int concurrency, const std::string& gpu_key, const std::string& group) {
+             bgc::bench::ChurnOptions o;
+             o.server = server;
+             o.admin_token = token;
+             o.name_prefix = prefix;
+             o.concurrency = concurrency;
+             o.gpu_quota_key = gpu_key;
+             o.group = group;
+             return std::make_unique<bgc::bench::ChurnDriver>(o);
+           }),
+           py::arg("server"), py::arg("admin_token"), py::arg("name_prefix"), py::arg("concurrency") = 32,
+           py::arg("gpu_quota_key") = "requests.amd.com/gpu", py::arg("group") = "gpu")
+      .def("start", &bgc::bench::ChurnDriver::start)
+      .def("step", [](bgc::bench::ChurnDriver& d, const std::vector<std::string>& names, double timeout) {
+        bgc::json::Value v;
+        {
+          py::gil_scoped_release nogil;
+          v = d.step(names, timeout);
+        }
+        return v.dump();
+      })
+      .def("remove", [](bgc::bench::ChurnDriver& d, const std::vector<std::string>& names) {
+        py::gil_scoped_release nogil;
+        return d.remove(names);
+      })
+      .def("stop", [](bgc::bench::ChurnDriver& d) {
+        py::gil_scoped_release nogil;
+        d.stop();
+      });
+
+  // WorkQueue (unit tests of dedup / delay / exclusivity semantics)
+  py::class_<bgc::kube::WorkQueue>(m, "WorkQueue")
+      .def(py::init<>())
+      .def("add", [](bgc::kube::WorkQueue& q, const std::string& k) { q.add(k); })
+      .def("add_after", [](bgc::kube::WorkQueue& q, const std::string& k, int ms) { q.add_after(k, std::chrono::milliseconds(ms)); })
+      .def("get", [](bgc::kube::WorkQueue& q) {
+        std::string k;
+        bool ok;
+        {
+          py::gil_scoped_release nogil;
+          ok = q.get(k);
+        }
+        return ok ? py::object(py::str(k)) : py::object(py::none());
+      })
+      .def("done", &bgc::kube::WorkQueue::done)
+      .def("shutdown", &bgc::kube::WorkQueue::shutdown)
+      .def("pending", &bgc::kube::WorkQueue::pending)
+      .def("in_flight", &bgc::kube::WorkQueue::in_flight);
+}
+
 }  // namespace bgc_py
