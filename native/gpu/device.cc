@@ -181,7 +181,8 @@ class MockBackend : public Backend {
     }
     return out;
   }
-  Telemetry sample(int index) override {
+  Telemetry sample(int index, bool full) override {
+    (void)full;
     reload();
     std::lock_guard<std::mutex> lk(mu_);
     int64_t t0 = metrics::now_ns();
@@ -385,7 +386,7 @@ class AmdSmiBackend : public Backend {
     return out;
   }
 
-  Telemetry sample(int index) override {
+  Telemetry sample(int index, bool full) override {
     Telemetry t;
     t.index = index;
     int64_t t0 = metrics::now_ns();
@@ -431,14 +432,14 @@ class AmdSmiBackend : public Backend {
       t.xgmi_links_up = up;
       t.xgmi_links_total = total;
     }
-    if (api_.get_vram_usage) {
+    if (full && api_.get_vram_usage) {
       amdsmi_vram_usage_t u{};
       if (api_.get_vram_usage(h, &u) == AMDSMI_STATUS_SUCCESS) {
         t.vram_used_mb = u.vram_used;
         t.vram_total_mb = u.vram_total;
       }
     }
-    if (api_.get_ecc) {
+    if (full && api_.get_ecc) {
       amdsmi_error_count_t e{};
       if (api_.get_ecc(h, &e) == AMDSMI_STATUS_SUCCESS) {
         t.ecc_correctable = e.correctable_count;

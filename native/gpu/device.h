@@ -66,7 +66,10 @@ class Backend {
   virtual ~Backend() = default;
   virtual std::string name() const = 0;
   virtual std::vector<GpuInfo> discover() = 0;
-  virtual Telemetry sample(int index) = 0;
+  // `full` also reads the slow counters (ECC totals ~670 us, VRAM usage ~80 us per
+  // device on MI355X/ROCm 7.2, vs ~280 us for the gpu_metrics blob); when false those
+  // fields are left zero and the caller keeps its cached values.
+  virtual Telemetry sample(int index, bool full = true) = 0;
 };
 
 // Throws std::runtime_error when libamd_smi is missing or amdsmi_init fails.

@@ -1,5 +1,7 @@
 #include "gpu/telemetry.h"
 
+#include <future>
+
 #include "core/log.h"
 #include "core/metrics.h"
 #include "core/roctx.h"
@@ -7,12 +9,30 @@
 namespace bgc::gpu {
 
 TelemetryPoller::TelemetryPoller(Backend& backend, std::vector<int> indices, std::chrono::milliseconds interval,
-                                 HealthPolicy policy)
-    : backend_(backend), indices_(std::move(indices)), interval_(interval), policy_(policy) {
+                                 HealthPolicy policy, int slow_every)
+    : backend_(backend), indices_(std::move(indices)), interval_(interval), policy_(policy),
+      slow_every_(std::max(1, slow_every)) {
   for (int i : indices_) {
     DeviceHealth h;
     h.index = i;
     health_.push_back(h);
+  }
+  slow_cache_.resize(indices_.size());
+  if (indices_.size() > 1) pool_ = std::make_unique<ThreadPool>(indices_.size());
+  auto& reg = metrics::Registry::global();
+  for (int i : indices_) {
+    metrics::Labels l{{"gpu", std::to_string(i)}};
+    gauges_.push_back({&reg.gauge("amd_gpu_gfx_activity_percent", "GFX engine activity", l),
+                       &reg.gauge("amd_gpu_umc_activity_percent", "Memory controller activity", l),
+                       &reg.gauge("amd_gpu_power_watts", "Socket power", l),
+                       &reg.gauge("amd_gpu_temperature_hotspot_celsius", "Hotspot temperature", l),
+                       &reg.gauge("amd_gpu_temperature_mem_celsius", "HBM temperature", l),
+                       &reg.gauge("amd_gpu_vram_used_bytes", "VRAM in use", l),
+                       &reg.gauge("amd_gpu_vram_total_bytes", "VRAM capacity", l),
+                       &reg.gauge("amd_gpu_gfxclk_mhz", "GFX clock", l),
+                       &reg.gauge("amd_gpu_ecc_uncorrectable_total", "Uncorrectable ECC errors", l),
+                       &reg.gauge("amd_gpu_xgmi_links_up", "xGMI links up", l),
+                       &reg.gauge("amd_gpu_healthy", "1 when the device passes the health policy", l)});
   }
   snap_ = std::make_shared<Snapshot>();
 }
@@ -68,8 +88,27 @@ void TelemetryPoller::poll_once() {
   auto snap = std::make_shared<Snapshot>();
   snap->devices.reserve(indices_.size());
   bool changed = false;
+  const bool full = polls_.load() % static_cast<uint64_t>(slow_every_) == 0;
+  std::vector<Telemetry> samples(indices_.size());
+  if (pool_) {
+    std::vector<std::future<void>> futs;
+    for (size_t k = 0; k < indices_.size(); ++k) {
+      futs.push_back(pool_->submit([&, k] { samples[k] = backend_.sample(indices_[k], full); }));
+    }
+    for (auto& f : futs) f.get();
+  } else {
+    for (size_t k = 0; k < indices_.size(); ++k) samples[k] = backend_.sample(indices_[k], full);
+  }
   for (size_t k = 0; k < indices_.size(); ++k) {
-    Telemetry t = backend_.sample(indices_[k]);
+    Telemetry t = std::move(samples[k]);
+    if (full) {
+      slow_cache_[k] = t;
+    } else if (t.ok) {
+      t.ecc_correctable = slow_cache_[k].ecc_correctable;
+      t.ecc_uncorrectable = slow_cache_[k].ecc_uncorrectable;
+      t.vram_used_mb = slow_cache_[k].vram_used_mb;
+      t.vram_total_mb = slow_cache_[k].vram_total_mb;
+    }
     bool was = health_[k].healthy;
     evaluate(t, policy_, health_[k]);
     if (was != health_[k].healthy) {
@@ -80,19 +119,18 @@ void TelemetryPoller::poll_once() {
         LOG_WARN("gpu") << "gpu " << indices_[k] << " unhealthy: " << health_[k].reason;
       }
     }
-    std::string idx = std::to_string(t.index);
-    metrics::Labels l{{"gpu", idx}};
-    reg.gauge("amd_gpu_gfx_activity_percent", "GFX engine activity", l).set(t.gfx_activity_pct);
-    reg.gauge("amd_gpu_umc_activity_percent", "Memory controller activity", l).set(t.umc_activity_pct);
-    reg.gauge("amd_gpu_power_watts", "Socket power", l).set(t.power_w);
-    reg.gauge("amd_gpu_temperature_hotspot_celsius", "Hotspot temperature", l).set(t.temp_hotspot_c);
-    reg.gauge("amd_gpu_temperature_mem_celsius", "HBM temperature", l).set(t.temp_mem_c);
-    reg.gauge("amd_gpu_vram_used_bytes", "VRAM in use", l).set(static_cast<double>(t.vram_used_mb) * 1048576.0);
-    reg.gauge("amd_gpu_vram_total_bytes", "VRAM capacity", l).set(static_cast<double>(t.vram_total_mb) * 1048576.0);
-    reg.gauge("amd_gpu_gfxclk_mhz", "GFX clock", l).set(t.gfxclk_mhz);
-    reg.gauge("amd_gpu_ecc_uncorrectable_total", "Uncorrectable ECC errors", l).set(static_cast<double>(t.ecc_uncorrectable));
-    reg.gauge("amd_gpu_xgmi_links_up", "xGMI links up", l).set(t.xgmi_links_up);
-    reg.gauge("amd_gpu_healthy", "1 when the device passes the health policy", l).set(health_[k].healthy ? 1 : 0);
+    const Gauges& g = gauges_[k];
+    g.gfx->set(t.gfx_activity_pct);
+    g.umc->set(t.umc_activity_pct);
+    g.power->set(t.power_w);
+    g.hotspot->set(t.temp_hotspot_c);
+    g.mem_temp->set(t.temp_mem_c);
+    g.vram_used->set(static_cast<double>(t.vram_used_mb) * 1048576.0);
+    g.vram_total->set(static_cast<double>(t.vram_total_mb) * 1048576.0);
+    g.gfxclk->set(t.gfxclk_mhz);
+    g.ecc_ue->set(static_cast<double>(t.ecc_uncorrectable));
+    g.xgmi_up->set(t.xgmi_links_up);
+    g.healthy->set(health_[k].healthy ? 1 : 0);
     snap->devices.push_back(std::move(t));
   }
   snap->health = health_;

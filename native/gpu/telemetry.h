@@ -18,6 +18,8 @@
 #include <vector>
 
 #include "core/cancel.h"
+#include "core/metrics.h"
+#include "core/threadpool.h"
 #include "gpu/device.h"
 
 namespace bgc::gpu {
@@ -51,8 +53,11 @@ struct Snapshot {
 
 class TelemetryPoller {
  public:
+  // slow_every: the expensive counters (ECC totals, VRAM usage) are read every Nth poll
+  // and cached in between; devices are sampled concurrently (one task per GPU), so a
+  // poll over 8 MI355X costs about one device's latency, not eight.
   TelemetryPoller(Backend& backend, std::vector<int> indices, std::chrono::milliseconds interval,
-                  HealthPolicy policy = {});
+                  HealthPolicy policy = {}, int slow_every = 10);
   ~TelemetryPoller();
   void start();
   void stop();
@@ -72,6 +77,13 @@ class TelemetryPoller {
   std::chrono::milliseconds interval_;
   HealthPolicy policy_;
   std::vector<DeviceHealth> health_;
+  int slow_every_;
+  std::vector<Telemetry> slow_cache_;
+  std::unique_ptr<ThreadPool> pool_;
+  struct Gauges {
+    metrics::Gauge *gfx, *umc, *power, *hotspot, *mem_temp, *vram_used, *vram_total, *gfxclk, *ecc_ue, *xgmi_up, *healthy;
+  };
+  std::vector<Gauges> gauges_;  // resolved once: the poll path does no registry lookups
   mutable std::mutex snap_mu_;
   std::shared_ptr<const Snapshot> snap_;
   std::function<void(const Snapshot&)> cb_;

@@ -57,14 +57,14 @@ void register_gpu(py::module_& m) {
         }
         return arr.dump();
       })
-      .def("sample", [](PyBackend& b, int idx) {
+      .def("sample", [](PyBackend& b, int idx, bool full) {
         bgc::gpu::Telemetry t;
         {
           py::gil_scoped_release nogil;
-          t = b.b->sample(idx);
+          t = b.b->sample(idx, full);
         }
         return bgc::gpu::to_json(t).dump();
-      });
+      }, py::arg("index"), py::arg("full") = true);
 
   m.def("gpu_backend", [](const std::string& kind, const std::string& fixture_json) {
     auto pb = std::make_shared<PyBackend>();
