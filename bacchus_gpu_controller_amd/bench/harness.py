@@ -97,6 +97,17 @@ class Dist:
             self.dist.destroy_process_group()
 
 
+def _cpu_seconds(pid):
+    """utime+stime of a process (for per-component CPU cost reporting)."""
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            fields = f.read().rsplit(")", 1)[1].split()
+        tck = os.sysconf("SC_CLK_TCK")
+        return round((int(fields[11]) + int(fields[12])) / tck, 3)
+    except (OSError, IndexError, ValueError):
+        return None
+
+
 def _names(rank, step, batch):
     return [f"r{rank}-s{step}-u{i}" for i in range(batch)]
 
@@ -163,9 +174,7 @@ def run(args):
                 d.barrier()
                 t_start = time.perf_counter()
             names = _names(d.rank, s, args.batch)
-            res = json.loads(driver.step(names, args.timeout))
-            if prev:
-                driver.remove(prev)
+            res = json.loads(driver.step_with_delete(names, prev or [], args.timeout))
             prev = names
             if s >= args.warmup:
                 lat += res["ready_latency_s"]
@@ -227,6 +236,8 @@ def run(args):
         }
         if total_failed:
             out["errors"] = [e for p in per_rank for e in p["errors"]][:5]
+        if args.report_cpu and cluster is not None:
+            out["component_cpu_s"] = {name: _cpu_seconds(p.p.pid) for name, p in cluster.procs.items()}
         return out
     finally:
         if d.rank == 0:
@@ -246,11 +257,12 @@ def main(argv=None):
     ap.add_argument("--batch", type=int, default=100, help="UserBootstraps applied per rank per step")
     ap.add_argument("--concurrency", type=int, default=32)
     ap.add_argument("--timeout", type=float, default=120.0)
-    ap.add_argument("--controller-workers", type=int, default=16)
-    ap.add_argument("--sync-workers", type=int, default=8)
+    ap.add_argument("--controller-workers", type=int, default=32)
+    ap.add_argument("--sync-workers", type=int, default=16)
     ap.add_argument("--poll-ms", type=int, default=250)
     ap.add_argument("--log-level", default="warn")
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--report-cpu", action="store_true", help="add per-component CPU seconds to the JSON")
     args = ap.parse_args(argv)
     out = run(args)
     if out is not None:

@@ -12,6 +12,7 @@
 #include <sstream>
 #include <thread>
 #include <unordered_map>
+#include <unordered_set>
 
 #include "apiserver/fieldset.h"
 #include "core/crypto.h"
@@ -309,6 +310,14 @@ struct ApiServer::Impl {
   std::map<std::string, TypeInfo> types;  // key() -> info
   std::unordered_map<std::string, std::unordered_map<std::string, Stored>> data;  // type key -> obj key -> stored
   std::unordered_map<std::string, std::pair<std::string, std::string>> by_uid;      // uid -> (type key, obj key)
+  // Secondary indexes so garbage collection and namespace cascades touch only the
+  // affected objects (O(dependents), not O(all objects)).
+  using Ref = std::pair<std::string, std::string>;  // (type key, obj key)
+  struct RefHash {
+    size_t operator()(const Ref& r) const { return std::hash<std::string>{}(r.first) * 31 + std::hash<std::string>{}(r.second); }
+  };
+  std::unordered_map<std::string, std::unordered_set<Ref, RefHash>> by_owner;      // owner uid -> dependents
+  std::unordered_map<std::string, std::unordered_set<Ref, RefHash>> by_namespace;  // namespace -> objects
   uint64_t rv = 1000;
   std::deque<std::shared_ptr<const EventRec>> history;
   uint64_t compacted_rv = 0;  // watches from rv < compacted_rv get 410
@@ -743,13 +752,38 @@ struct ApiServer::Impl {
     else obj["metadata"]["managedFields"] = arr;
   }
 
-  static Value strip_volatile(const Value& obj) {
-    Value v = obj;
-    if (Value* m = v.find_mut("metadata")) {
-      m->erase("managedFields");
-      m->erase("resourceVersion");
+  // a == b ignoring metadata.managedFields and metadata.resourceVersion (no copies).
+  static bool same_content(const Value& a, const Value& b) {
+    if (!a.is_object() || !b.is_object()) return a == b;
+    auto volatile_key = [](const std::string& k) { return k == "managedFields" || k == "resourceVersion"; };
+    auto count = [&](const Value& v, bool meta) {
+      size_t n = 0;
+      for (const auto& k : v.keys()) n += (meta && volatile_key(k)) ? 0 : 1;
+      return n;
+    };
+    if (a.size() != b.size()) return false;
+    for (size_t i = 0; i < a.keys().size(); ++i) {
+      const std::string& k = a.keys()[i];
+      const Value* bv = b.find(k);
+      if (!bv) return false;
+      const Value& av = a.values()[i];
+      if (k != "metadata") {
+        if (!(av == *bv)) return false;
+        continue;
+      }
+      if (!av.is_object() || !bv->is_object()) {
+        if (!(av == *bv)) return false;
+        continue;
+      }
+      if (count(av, true) != count(*bv, true)) return false;
+      for (size_t j = 0; j < av.keys().size(); ++j) {
+        const std::string& mk = av.keys()[j];
+        if (volatile_key(mk)) continue;
+        const Value* bm = bv->find(mk);
+        if (!bm || !(av.values()[j] == *bm)) return false;
+      }
     }
-    return v;
+    return true;
   }
 
   static bool spec_changed(const Value& a, const Value& b) {
@@ -812,10 +846,23 @@ struct ApiServer::Impl {
     s.rv = new_rv;
     s.managers = std::move(managers);
     std::string key = obj_key(ti.rt, ns, name);
+    Ref ref{ti.key(), key};
+    if (prev) unindex_owners_locked(*prev->obj, ref);
     b[key] = std::move(s);
-    by_uid[ptr->get("metadata").get_string("uid")] = {ti.key(), key};
+    by_uid[ptr->get("metadata").get_string("uid")] = ref;
+    for (const auto& r : ptr->get("metadata").get("ownerReferences").items()) by_owner[r.get_string("uid")].insert(ref);
+    if (ti.rt.namespaced) by_namespace[ns].insert(ref);
     emit_locked(prev ? "MODIFIED" : "ADDED", ti, ns, ptr, new_rv);
     return ptr;
+  }
+
+  void unindex_owners_locked(const Value& obj, const Ref& ref) {
+    for (const auto& r : obj.get("metadata").get("ownerReferences").items()) {
+      auto it = by_owner.find(r.get_string("uid"));
+      if (it == by_owner.end()) continue;
+      it->second.erase(ref);
+      if (it->second.empty()) by_owner.erase(it);
+    }
   }
 
   void erase_locked(const TypeInfo& ti, const std::string& ns, const std::string& name,
@@ -829,22 +876,39 @@ struct ApiServer::Impl {
     final_obj["metadata"]["resourceVersion"] = std::to_string(new_rv);
     auto ptr = std::make_shared<const Value>(std::move(final_obj));
     std::string uid = ptr->get("metadata").get_string("uid");
+    Ref ref{ti.key(), key};
     by_uid.erase(uid);
+    unindex_owners_locked(*ptr, ref);
+    if (ti.rt.namespaced) {
+      auto nit = by_namespace.find(ns);
+      if (nit != by_namespace.end()) {
+        nit->second.erase(ref);
+        if (nit->second.empty()) by_namespace.erase(nit);
+      }
+    }
     b.erase(it);
     emit_locked("DELETED", ti, ns, ptr, new_rv);
     if (deleted_uids) deleted_uids->push_back(uid);
     // namespace deletion removes everything inside it
     if (ti.rt.plural == "namespaces" && ti.rt.group.empty()) {
-      for (auto& [tk, tb] : data) {
-        auto tit = types.find(tk);
-        if (tit == types.end() || !tit->second.rt.namespaced) continue;
-        std::vector<std::string> victims;
-        for (auto& [k, st] : tb) {
-          if (st.obj->get("metadata").get_string("namespace") == name) victims.push_back(st.obj->get("metadata").get_string("name"));
-        }
-        for (const auto& v : victims) erase_locked(tit->second, name, v, deleted_uids);
+      auto nit = by_namespace.find(name);
+      if (nit != by_namespace.end()) {
+        std::vector<Ref> victims(nit->second.begin(), nit->second.end());
+        for (const auto& v : victims) erase_ref_locked(v, deleted_uids);
       }
     }
+  }
+
+  void erase_ref_locked(const Ref& ref, std::vector<std::string>* deleted_uids) {
+    auto tit = types.find(ref.first);
+    if (tit == types.end()) return;
+    auto& b = bucket(tit->second);
+    auto it = b.find(ref.second);
+    if (it == b.end()) return;
+    const Value& meta = it->second.obj->get("metadata");
+    std::string ns = meta.get_string("namespace");
+    std::string name = meta.get_string("name");
+    erase_locked(tit->second, ns, name, deleted_uids);
   }
 
   bool dangling_owners_locked(const Value& obj) {
@@ -859,28 +923,23 @@ struct ApiServer::Impl {
   // Garbage collector: delete dependents whose owners are all gone.
   void collect_garbage_locked(std::vector<std::string> dead_uids) {
     while (!dead_uids.empty()) {
-      std::set<std::string> dead(dead_uids.begin(), dead_uids.end());
-      dead_uids.clear();
-      std::vector<std::tuple<TypeInfo*, std::string, std::string>> victims;
-      for (auto& [tk, tb] : data) {
-        auto tit = types.find(tk);
+      std::string dead = dead_uids.back();
+      dead_uids.pop_back();
+      auto oit = by_owner.find(dead);
+      if (oit == by_owner.end()) continue;
+      std::vector<Ref> deps(oit->second.begin(), oit->second.end());
+      for (const auto& dep : deps) {
+        auto tit = types.find(dep.first);
         if (tit == types.end()) continue;
-        for (auto& [k, st] : tb) {
-          const Value& refs = st.obj->get("metadata").get("ownerReferences");
-          if (refs.empty()) continue;
-          bool any_dead = false, any_alive = false;
-          for (const auto& r : refs.items()) {
-            std::string u = r.get_string("uid");
-            if (dead.count(u)) any_dead = true;
-            else if (by_uid.count(u)) any_alive = true;
-          }
-          if (any_dead && !any_alive) {
-            victims.emplace_back(&tit->second, st.obj->get("metadata").get_string("namespace"),
-                                 st.obj->get("metadata").get_string("name"));
-          }
+        auto& b = bucket(tit->second);
+        auto it = b.find(dep.second);
+        if (it == b.end()) continue;
+        bool any_alive = false;
+        for (const auto& r : it->second.obj->get("metadata").get("ownerReferences").items()) {
+          if (by_uid.count(r.get_string("uid"))) any_alive = true;
         }
+        if (!any_alive) erase_ref_locked(dep, &dead_uids);
       }
-      for (auto& [ti, ns, name] : victims) erase_locked(*ti, ns, name, &dead_uids);
     }
   }
 
@@ -914,7 +973,7 @@ struct ApiServer::Impl {
         }
       }
       // no-op short-circuit (before admission, like the apiserver's update path)
-      if (exists && strip_volatile(obj) == strip_volatile(*cur_copy.obj) && managers == cur_copy.managers) {
+      if (exists && same_content(obj, *cur_copy.obj) && managers == cur_copy.managers) {
         return {cur_copy.obj, 200};
       }
       call_webhooks(ti, sub, op, ns, name, &obj, exists ? cur_copy.obj.get() : nullptr, user);
@@ -930,7 +989,7 @@ struct ApiServer::Impl {
       if (now_exists != exists || (exists && it->second.rv != cur_copy.rv)) continue;  // raced: retry
       if (exists) {
         // non-apply writers: attribute changed fields after mutation
-        if (exists && strip_volatile(obj) == strip_volatile(*cur_copy.obj) && managers == cur_copy.managers) {
+        if (exists && same_content(obj, *cur_copy.obj) && managers == cur_copy.managers) {
           return {cur_copy.obj, 200};
         }
         if (spec_changed(*cur_copy.obj, obj)) {

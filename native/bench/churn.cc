@@ -24,6 +24,33 @@ ChurnDriver::ChurnDriver(ChurnOptions o) : opts_(std::move(o)) {
   ho.max_idle = static_cast<size_t>(opts_.concurrency) * 2;
   http_ = std::make_unique<http::Client>(ho);
   pool_ = std::make_unique<ThreadPool>(static_cast<size_t>(std::max(1, opts_.concurrency)));
+  delete_pool_ = std::make_unique<ThreadPool>(static_cast<size_t>(std::max(1, opts_.concurrency / 2)));
+}
+
+json::Value ChurnDriver::step_with_delete(const std::vector<std::string>& names,
+                                          const std::vector<std::string>& previous, double timeout_s) {
+  std::vector<std::future<bool>> dels;
+  for (const auto& n : previous) {
+    dels.push_back(delete_pool_->submit([this, n] {
+      try {
+        admin_->remove(types::UserBootstrap, "", n);
+        return true;
+      } catch (const kube::ApiError& e) {
+        return e.code() == 404;
+      } catch (const std::exception&) {
+        return false;
+      }
+    }));
+  }
+  Value out = step(names, timeout_s);
+  int failures = 0;
+  for (auto& f : dels) failures += f.get() ? 0 : 1;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (const auto& n : previous) early_.erase(n);
+  }
+  out["delete_failures"] = failures;
+  return out;
 }
 
 ChurnDriver::~ChurnDriver() { stop(); }

@@ -46,6 +46,10 @@ class ChurnDriver {
   // Returns {"ready": n, "failed": n, "timeouts": n, "elapsed_s": x,
   //          "ready_latency_s": [...], "create_latency_s": [...], "errors": [...]}.
   json::Value step(const std::vector<std::string>& names, double timeout_s);
+  // Same, while deleting `previous` concurrently (churn: the previous step's tenants
+  // leave while the next ones arrive); the step ends when both are done.
+  json::Value step_with_delete(const std::vector<std::string>& names, const std::vector<std::string>& previous,
+                               double timeout_s);
   // Deletes (as cluster admin) concurrently; returns number of failures.
   int remove(const std::vector<std::string>& names);
   void stop();
@@ -65,6 +69,7 @@ class ChurnDriver {
   std::unique_ptr<kube::KubeClient> admin_;
   std::unique_ptr<http::Client> http_;
   std::unique_ptr<ThreadPool> pool_;
+  std::unique_ptr<ThreadPool> delete_pool_;
   CancelToken stop_;
   std::vector<std::thread> watchers_;
   std::mutex mu_;

@@ -36,6 +36,15 @@ void register_kube(py::module_& m) {
         }
         return v.dump();
       })
+      .def("step_with_delete", [](bgc::bench::ChurnDriver& d, const std::vector<std::string>& names,
+                                  const std::vector<std::string>& prev, double timeout) {
+        bgc::json::Value v;
+        {
+          py::gil_scoped_release nogil;
+          v = d.step_with_delete(names, prev, timeout);
+        }
+        return v.dump();
+      })
       .def("remove", [](bgc::bench::ChurnDriver& d, const std::vector<std::string>& names) {
         py::gil_scoped_release nogil;
         return d.remove(names);
