@@ -1,0 +1,127 @@
+"""RCCL-over-xGMI placement probe (north-star N5; BASELINE config #4).
+
+Run one rank per GPU:
+
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
+        -m bacchus_gpu_controller_amd.parallel.rccl_probe --sizes-mb 1,16,256,1024
+
+Each rank:
+  * reads its GPU's xGMI hive id through amdsmi (native backend) and all-gathers it, so a
+    TP group that was NOT co-scheduled on one xGMI island is reported (and, with
+    --require-single-hive, fails);
+  * runs bf16 all-reduce over a size sweep with the `nccl` backend (= RCCL on ROCm),
+    checks the result exactly, and reports algbw and busbw (busbw = algbw * 2(n-1)/n,
+    the per-link figure comparable to the ~153 GB/s xGMI link rate).
+
+A TP=8 group on one hive should show busbw in the hundreds of GB/s; a group that fell
+back to PCIe/NIC shows an order of magnitude less — the co-scheduling signal the node
+agent's `amd.com/gpu.xgmi-hive-id` label is meant to protect.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+
+def busbw_factor(world):
+    return 2.0 * (world - 1) / world if world > 1 else 1.0
+
+
+def local_hive_id(local_rank):
+    try:
+        from .. import native
+
+        gpus = json.loads(native().gpu_backend("amdsmi", "").discover())
+        for g in gpus:
+            if g.get("hip_id", g["index"]) == local_rank:
+                return g["xgmi_hive_id"]
+        return gpus[local_rank % len(gpus)]["xgmi_hive_id"] if gpus else "unknown"
+    except Exception as e:  # noqa: BLE001
+        return f"unavailable:{type(e).__name__}"
+
+
+def run(sizes_mb, iters=10, warmup=3, require_single_hive=False, dtype="bf16"):
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    cuda = torch.cuda.is_available()
+    if cuda:
+        torch.cuda.set_device(local % torch.cuda.device_count())
+    backend = "nccl" if cuda else "gloo"
+    if world > 1 or not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29555")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
+        dist.init_process_group(backend=backend)
+    dev = torch.device("cuda", torch.cuda.current_device()) if cuda else torch.device("cpu")
+    tdtype = {"bf16": torch.bfloat16, "fp32": torch.float32}[dtype]
+    hive = local_hive_id(local) if cuda else "cpu"
+    hives = [None] * world
+    dist.all_gather_object(hives, hive)
+    single_hive = len(set(hives)) == 1
+    results = []
+    for mb in sizes_mb:
+        n = int(mb * (1 << 20) // torch.tensor([], dtype=tdtype).element_size())
+        # small integers keep bf16 sums exact: every rank contributes (rank+1)
+        buf = torch.full((n,), float(rank + 1), dtype=tdtype, device=dev)
+        expect = float(world * (world + 1) // 2)
+        for _ in range(warmup):
+            buf.fill_(float(rank + 1))
+            dist.all_reduce(buf)
+        if cuda:
+            torch.cuda.synchronize()
+        times = []
+        ok = True
+        for _ in range(iters):
+            buf.fill_(float(rank + 1))
+            if cuda:
+                torch.cuda.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            dist.all_reduce(buf)
+            if cuda:
+                torch.cuda.synchronize()
+            times.append(time.perf_counter() - t0)
+            ok = ok and bool(torch.all(buf == expect).item())
+        t = sorted(times)[len(times) // 2]
+        tmax = torch.tensor([t], dtype=torch.float64, device=dev)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        t = float(tmax.item())
+        nbytes = n * buf.element_size()
+        algbw = nbytes / t / 1e9
+        results.append({"size_mb": mb, "time_us": round(t * 1e6, 2), "algbw_gbps": round(algbw, 2),
+                        "busbw_gbps": round(algbw * busbw_factor(world), 2), "correct": ok})
+    out = {"world_size": world, "backend": backend, "dtype": dtype, "hives": hives, "single_hive": single_hive,
+           "results": results, "max_busbw_gbps": max(r["busbw_gbps"] for r in results) if results else 0.0,
+           "all_correct": all(r["correct"] for r in results)}
+    dist.barrier()
+    dist.destroy_process_group()
+    if require_single_hive and not single_hive:
+        raise SystemExit(f"TP group spans multiple xGMI hives: {hives}")
+    return out if rank == 0 else None
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--sizes-mb", default="1,16,256")
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--require-single-hive", action="store_true")
+    args = ap.parse_args(argv)
+    sizes = [float(s) for s in args.sizes_mb.split(",") if s]
+    out = run(sizes, args.iters, args.warmup, args.require_single_hive, args.dtype)
+    if out is not None:
+        print(json.dumps(out), flush=True)
+        if not out["all_correct"]:
+            return 1
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

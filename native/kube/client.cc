@@ -74,6 +74,8 @@ KubeConfig KubeConfig::from_kubeconfig(const std::string& path, const std::strin
     const Value& uv = u.get("user");
     c.token = uv.get_string("token");
     c.token_file = uv.get_string("tokenFile");
+    // relative paths in a kubeconfig are relative to the kubeconfig file (client-go)
+    if (!c.token_file.empty() && c.token_file[0] != '/') c.token_file = base_dir + "/" + c.token_file;
     if (!c.token_file.empty() && c.token.empty()) c.token = trim(net::read_file(c.token_file));
     c.client_cert_pem = data_or_file(uv, "client-certificate", base_dir);
     c.client_key_pem = data_or_file(uv, "client-key", base_dir);

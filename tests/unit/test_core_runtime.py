@@ -1,0 +1,144 @@
+"""Core runtime pieces: work queue semantics, RUST_LOG targets, envy config, kubeconfig,
+crypto helpers (checked against Python stdlib / the openssl CLI)."""
+import base64
+import hashlib
+import os
+import re
+import subprocess
+import tempfile
+import threading
+import time
+
+import pytest
+
+
+def test_workqueue_dedup_and_delay(nat):
+    q = nat.WorkQueue()
+    q.add("a")
+    q.add("a")
+    q.add_after("b", 50)
+    assert q.pending() == 2
+    assert q.get() == "a"
+    t0 = time.time()
+    assert q.get() == "b"
+    assert time.time() - t0 >= 0.04
+    q.done("a")
+    q.done("b")
+
+
+def test_workqueue_earliest_due_wins(nat):
+    q = nat.WorkQueue()
+    q.add_after("k", 5000)   # requeue(30s)-style entry
+    q.add("k")               # event arrives: run now
+    t0 = time.time()
+    assert q.get() == "k"
+    assert time.time() - t0 < 1.0
+    q.done("k")
+    assert q.pending() == 0  # the later entry was superseded, not duplicated
+
+
+def test_workqueue_per_key_exclusivity(nat):
+    q = nat.WorkQueue()
+    q.add("x")
+    assert q.get() == "x"
+    q.add("x")                       # re-added while in flight: deferred
+    got = []
+    th = threading.Thread(target=lambda: got.append(q.get()))
+    th.start()
+    time.sleep(0.1)
+    assert not got                   # not handed to a second worker
+    q.done("x")
+    th.join(2)
+    assert got == ["x"]
+    q.done("x")
+    q.shutdown()
+    assert q.get() is None
+
+
+@pytest.mark.parametrize("spec,level,target,on", [
+    ("info", "info", "controller", True),
+    ("info", "debug", "controller", False),
+    ("warn,controller=debug", "debug", "controller", True),
+    ("warn,controller=debug", "info", "admission", False),
+    ("controller=trace", "info", "admission", False),     # no default => off for others
+    ("kube=debug,info", "debug", "kube::watcher", True),  # module-path prefix
+    ("", "info", "x", True),                              # empty => INFO default
+])
+def test_rust_log_targets(nat, spec, level, target, on):
+    assert nat.log_enabled(spec, level, target) is on
+
+
+def test_env_config_envy_semantics(nat):
+    base = {"CONF_LISTEN_ADDR": "0.0.0.0", "CONF_LISTEN_PORT": "12321", "CONF_CERT_PATH": "c",
+            "CONF_KEY_PATH": "k", "CONF_OIDC_USERNAME_PREFIX": "oidc:", "CONF_DEFAULT_ROLE_NAME": "edit",
+            "CONF_AUTHORIZED_GROUP_NAMES": "gpu,admin"}
+    d = nat.env_config(base, "admission")
+    assert d["authorized_group_names"] == ["gpu", "admin"] and d["listen_port"] == 12321
+    assert nat.env_config(dict(base, CONF_AUTHORIZED_GROUP_NAMES=""), "admission")["authorized_group_names"] == [""]
+    assert nat.env_config(dict(base, CONF_AUTHORIZED_GROUP_NAMES=" gpu , x"), "admission")["authorized_group_names"] == [" gpu ", " x"]
+    with pytest.raises(ValueError, match="missing value for field cert_path"):
+        nat.env_config({k: v for k, v in base.items() if k != "CONF_CERT_PATH"}, "admission")
+    with pytest.raises(ValueError, match="listen_port"):
+        nat.env_config(dict(base, CONF_LISTEN_PORT="70000"), "admission")
+    s = nat.env_config({"CONF_LISTEN_ADDR": "a", "CONF_LISTEN_PORT": "1", "CONF_GOOGLE_SERVICE_ACCOUNT_JSON_PATH": "p",
+                        "CONF_GOOGLE_FILE_ID": "f", "CONF_GPU_SERVER_NAME": ""}, "synchronizer")
+    assert s["sync_interval_secs"] == 60
+
+
+def test_kubeconfig(nat, tmp_path):
+    ca = base64.b64encode(b"-----BEGIN CERTIFICATE-----\nx\n-----END CERTIFICATE-----\n").decode()
+    (tmp_path / "tok").write_text("file-token\n")
+    (tmp_path / "config").write_text(f"""
+apiVersion: v1
+kind: Config
+current-context: dev
+clusters:
+- name: c1
+  cluster:
+    server: https://10.0.0.1:6443
+    certificate-authority-data: {ca}
+- name: c2
+  cluster: {{server: "http://127.0.0.1:8080", insecure-skip-tls-verify: true}}
+contexts:
+- name: dev
+  context: {{cluster: c1, user: u1}}
+- name: local
+  context: {{cluster: c2, user: u2}}
+users:
+- name: u1
+  user:
+    token: abc
+    as: oidc:alice
+    as-groups: [gpu]
+- name: u2
+  user:
+    tokenFile: tok
+""")
+    d = nat.kubeconfig_parse(str(tmp_path / "config"))
+    assert d["server"] == "https://10.0.0.1:6443" and d["token"] == "abc"
+    assert d["ca_pem"].startswith("-----BEGIN CERTIFICATE-----")
+    assert d["impersonate_user"] == "oidc:alice" and d["impersonate_groups"] == ["gpu"]
+    d2 = nat.kubeconfig_parse(str(tmp_path / "config"), "local")
+    assert d2["server"] == "http://127.0.0.1:8080" and d2["insecure"] and d2["token"] == "file-token"
+
+
+def test_crypto_against_stdlib(nat):
+    data = os.urandom(1000)
+    assert nat.sha256_hex(data) == hashlib.sha256(data).hexdigest()
+    for n in range(0, 7):
+        assert nat.base64_encode(data[:n]) == base64.b64encode(data[:n]).decode()
+        assert nat.base64_encode(data[:n], True, False) == base64.urlsafe_b64encode(data[:n]).decode().rstrip("=")
+        assert nat.base64_decode(base64.b64encode(data[:n]).decode()) == data[:n]
+    assert re.fullmatch(r"[0-9a-f]{8}-[0-9a-f]{4}-4[0-9a-f]{3}-[89ab][0-9a-f]{3}-[0-9a-f]{12}", nat.uuid_v4())
+
+
+def test_certificates_verify_with_openssl(nat, tmp_path):
+    b = nat.make_ca_and_leaf("bgc-admission", ["bgc-admission.bgc.svc", "127.0.0.1"], 90)
+    (tmp_path / "ca.crt").write_text(b["ca_cert"])
+    (tmp_path / "tls.crt").write_text(b["cert"])
+    r = subprocess.run(["openssl", "verify", "-CAfile", str(tmp_path / "ca.crt"), str(tmp_path / "tls.crt")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    txt = subprocess.run(["openssl", "x509", "-in", str(tmp_path / "tls.crt"), "-noout", "-text"],
+                         capture_output=True, text=True).stdout
+    assert "DNS:bgc-admission.bgc.svc" in txt and "IP Address:127.0.0.1" in txt

@@ -1,0 +1,62 @@
+"""xGMI placement planning + the RCCL probe's logic (gloo, world_size 2, on CPU)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from bacchus_gpu_controller_amd import REPO_ROOT
+from bacchus_gpu_controller_amd.parallel import placement
+
+
+def node(name, hive, count=8, healthy=None, mixed=None):
+    topo = [{"index": i, "hive": (mixed[i] if mixed else hive)} for i in range(count)]
+    return {"metadata": {"name": name,
+                         "labels": {"amd.com/gpu.xgmi-hive-id": hive if not mixed else "mixed",
+                                    "amd.com/gpu.count": str(count)},
+                         "annotations": {"amd.com/gpu.topology": json.dumps(topo)}},
+            "status": {"allocatable": {"amd.com/gpu": str(count if healthy is None else healthy)}}}
+
+
+def test_plan_tp8_one_group_per_island():
+    nodes = [node("a", "h1"), node("b", "h2"), node("c", "h3", healthy=7)]
+    plan = placement.plan_tp_groups(nodes, 8, 2)
+    assert {p["hive"] for p in plan} == {"h1", "h2"}  # h3 has only 7 healthy GPUs
+    with pytest.raises(ValueError):
+        placement.plan_tp_groups(nodes, 8, 3)
+
+
+def test_plan_tp4_packs_islands():
+    plan = placement.plan_tp_groups([node("a", "h1")], 4, 2)
+    assert [p["hive"] for p in plan] == ["h1", "h1"]
+
+
+def test_mixed_node_never_splits_tp_group():
+    n = node("m", "x", mixed=["h1"] * 4 + ["h2"] * 4)
+    with pytest.raises(ValueError):
+        placement.plan_tp_groups([n], 8, 1)
+    assert len(placement.plan_tp_groups([n], 4, 2)) == 2
+    inv = placement.hive_inventory([n])
+    assert inv["h1"]["gpus"] == 4 and inv["h2"]["gpus"] == 4
+
+
+def test_tp_pod_affinity():
+    spec = placement.tp_pod_affinity("4ca22c3b0ce7816e", 8)
+    assert spec["nodeSelector"]["amd.com/gpu.xgmi-hive-id"] == "4ca22c3b0ce7816e"
+    assert spec["resources"]["limits"]["amd.com/gpu"] == "8"
+
+
+@pytest.mark.slow
+def test_rccl_probe_logic_gloo_world2():
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29561",
+           "-m", "bacchus_gpu_controller_amd.parallel.rccl_probe", "--sizes-mb", "0.25,1", "--iters", "3",
+           "--warmup", "1", "--dtype", "fp32"]
+    r = subprocess.run(cmd, cwd=REPO_ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    out = json.loads(line)
+    assert out["world_size"] == 2 and out["backend"] == "gloo" and out["all_correct"]
+    assert out["single_hive"] and len(out["results"]) == 2
