@@ -20,7 +20,8 @@ import os
 __version__ = "0.1.0"
 
 REPO_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-BIN_DIR = os.path.join(REPO_ROOT, "bin")
+# BGC_BIN_DIR lets the test-suite run against sanitizer builds (tools/sanitize.sh).
+BIN_DIR = os.environ.get("BGC_BIN_DIR") or os.path.join(REPO_ROOT, "bin")
 
 _native_mod = None
 

@@ -94,6 +94,10 @@ class Cluster:
     def __init__(self, workdir=None, admission=True, controller=True, controller_env=None, admission_env=None,
                  apiserver_args=None, log_level="warn"):
         self._tmp = None
+        keep = os.environ.get("BGC_CLUSTER_LOGDIR")  # keep component logs (sanitizer runs)
+        if workdir is None and keep:
+            os.makedirs(keep, exist_ok=True)
+            workdir = tempfile.mkdtemp(prefix="cluster-", dir=keep)
         if workdir is None:
             self._tmp = tempfile.TemporaryDirectory(prefix="bgc-cluster-")
             workdir = self._tmp.name

@@ -589,8 +589,10 @@ struct ApiServer::Impl {
       req["kind"] = Value::object({{"group", ti.rt.group}, {"version", ti.rt.version}, {"kind", ti.rt.kind}});
       req["resource"] = Value::object({{"group", ti.rt.group}, {"version", ti.rt.version}, {"resource", ti.rt.plural}});
       if (!sub.empty()) req["subResource"] = sub;
-      req["requestKind"] = req["kind"];
-      req["requestResource"] = req["resource"];
+      // copy first: operator[] may grow the object and invalidate references into it
+      Value kind_copy = req.get("kind"), resource_copy = req.get("resource");
+      req["requestKind"] = std::move(kind_copy);
+      req["requestResource"] = std::move(resource_copy);
       if (!sub.empty()) req["requestSubResource"] = sub;
       req["name"] = name;
       if (!ns.empty()) req["namespace"] = ns;

@@ -382,10 +382,9 @@ void Server::accept_loop() {
     active_.fetch_add(1);
     std::thread([this, fd, remote = std::string(host)] {
       serve_conn(fd, remote);
-      {
-        std::lock_guard<std::mutex> lk(conns_mu_);
-        active_.fetch_sub(1);
-      }
+      // notify under the lock: once stop() observes active_==0 the Server (and the cv) may be destroyed
+      std::lock_guard<std::mutex> lk(conns_mu_);
+      active_.fetch_sub(1);
       conns_cv_.notify_all();
     }).detach();
   }

@@ -155,6 +155,7 @@ class MockBackend : public Backend {
   explicit MockBackend(std::string path) : path_(std::move(path)) { reload(); }
   void reload() {
     if (path_.empty()) return;
+    std::lock_guard<std::mutex> rl(reload_mu_);  // per-GPU samplers call this concurrently
     struct stat st {};
     if (::stat(path_.c_str(), &st) != 0) return;
     if (st.st_mtim.tv_sec == mtime_.tv_sec && st.st_mtim.tv_nsec == mtime_.tv_nsec) return;
@@ -225,7 +226,8 @@ class MockBackend : public Backend {
   Value fixture_;
   std::string path_;
   struct timespec mtime_ {};
-  std::mutex mu_;
+  std::mutex reload_mu_;  // guards mtime_ and serializes file reads
+  std::mutex mu_;         // guards fixture_
 };
 
 // ---------------------------------------------------------------------------

@@ -182,7 +182,9 @@ bool WorkQueue::get(std::string& key) {
     if (timeline_.empty()) {
       cv_.wait(lk);
     } else {
-      cv_.wait_until(lk, timeline_.begin()->first);
+      // copy: wait_until re-reads its deadline after re-locking, when another worker may have erased the node
+      const auto deadline = timeline_.begin()->first;
+      cv_.wait_until(lk, deadline);
     }
   }
 }

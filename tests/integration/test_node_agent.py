@@ -12,12 +12,19 @@ from bacchus_gpu_controller_amd.testing.kubeapi import wait_for
 pytestmark = pytest.mark.slow
 
 
+def _write_atomic(path, obj):
+    # rename, so the agent's mtime-triggered reload never sees a truncated fixture
+    tmp = str(path) + ".tmp"
+    with open(tmp, "w") as fh:
+        json.dump(obj, fh)
+    os.replace(tmp, path)
+
+
 def test_node_agent_advertises_and_flaps(nat):
     with Cluster(admission=False, controller=False) as c:
         fixture = os.path.join(c.workdir, "gpus.json")
         f = json.loads(nat.default_mi355x_fixture(8))
-        with open(fixture, "w") as fh:
-            json.dump(f, fh)
+        _write_atomic(fixture, f)
         port = free_port()
         env = c.component_env(NODE_AGENT_TOKEN, port)
         env.update({"CONF_NODE_NAME": "mi355x-0", "CONF_GPU_BACKEND": "mock", "CONF_MOCK_FIXTURE_PATH": fixture,
@@ -39,15 +46,13 @@ def test_node_agent_advertises_and_flaps(nat):
 
         # flap: gpu 3 overheats -> allocatable 7, condition False
         f["gpus"][3]["telemetry"]["temp_hotspot_c"] = 121
-        with open(fixture, "w") as fh:
-            json.dump(f, fh)
+        _write_atomic(fixture, f)
         wait_for(lambda: c.admin.get("nodes", "mi355x-0")["status"]["allocatable"]["amd.com/gpu"] == "7",
                  timeout=10, desc="allocatable drops to 7")
         cond = c.admin.get("nodes", "mi355x-0")["status"]["conditions"][0]
         assert cond["status"] == "False" and "gpu3" in cond["message"]
         # recovery
         f["gpus"][3]["telemetry"]["temp_hotspot_c"] = 50
-        with open(fixture, "w") as fh:
-            json.dump(f, fh)
+        _write_atomic(fixture, f)
         wait_for(lambda: c.admin.get("nodes", "mi355x-0")["status"]["allocatable"]["amd.com/gpu"] == "8",
                  timeout=10, desc="allocatable back to 8")
