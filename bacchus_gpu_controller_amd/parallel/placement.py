@@ -25,7 +25,14 @@ def _labels(node):
     return node.get("metadata", {}).get("labels", {})
 
 
+def node_schedulable(node):
+    """False for cordoned nodes (``kubectl drain``/``cordon`` set spec.unschedulable)."""
+    return not node.get("spec", {}).get("unschedulable", False)
+
+
 def node_healthy_gpus(node):
+    if not node_schedulable(node):
+        return 0
     alloc = node.get("status", {}).get("allocatable", {}).get(RESOURCE)
     if alloc is not None:
         return int(alloc)

@@ -203,21 +203,37 @@ class Cluster:
         return p
 
     def start_node_agent(self, node_name="mi355x-0", max_gpus=0, backend="auto", n_mock_gpus=8, extra_env=None,
-                         poll_interval_ms=1000):
-        """Start the native node agent; amdsmi when available, else a mock MI355X hive."""
-        fixture = os.path.join(self.workdir, "gpus.json")
+                         poll_interval_ms=1000, hive_id=None, proc_name=None):
+        """Start the native node agent; amdsmi when available, else a mock MI355X hive.
+        Several agents (one per synthetic node) may run side by side: each gets its own
+        fixture file (`self.fixtures[node_name]`), process name and port."""
+        fixture = os.path.join(self.workdir, f"gpus-{node_name}.json")
+        fx = native().default_mi355x_fixture(n_mock_gpus, *([hive_id] if hive_id is not None else []))
         with open(fixture, "w") as f:
-            f.write(native().default_mi355x_fixture(n_mock_gpus))
-        self.node_agent_port = free_port()
-        env = self.component_env(NODE_AGENT_TOKEN, self.node_agent_port)
+            f.write(fx)
+        self.fixtures = getattr(self, "fixtures", {})
+        self.fixtures[node_name] = fixture
+        port = free_port()
+        self.node_agent_port = port
+        self.node_agent_ports = getattr(self, "node_agent_ports", {})
+        self.node_agent_ports[node_name] = port
+        env = self.component_env(NODE_AGENT_TOKEN, port)
         env.update({"CONF_NODE_NAME": node_name, "CONF_GPU_BACKEND": backend, "CONF_MOCK_FIXTURE_PATH": fixture,
                     "CONF_MAX_GPUS": str(max_gpus), "CONF_CREATE_NODE": "true",
                     "CONF_POLL_INTERVAL_MS": str(poll_interval_ms)})
         env.update(extra_env or {})
-        p = self.start_process("node-agent", "node-agent", env)
-        wait_for(lambda: requests.get(f"http://127.0.0.1:{self.node_agent_port}/health", timeout=1).text == "pong",
-                 60, desc="node-agent /health")
+        p = self.start_process(proc_name or "node-agent", "node-agent", env)
+        wait_for(lambda: requests.get(f"http://127.0.0.1:{port}/health", timeout=1).text == "pong",
+                 60, desc=f"node-agent {node_name} /health")
         return p
+
+    def set_gpu_fixture(self, node_name, fixture_obj):
+        """Atomically replace a mock node's GPU fixture (the agent reloads it on mtime change)."""
+        path = self.fixtures[node_name]
+        tmp = path + ".tmp"
+        with open(tmp, "w") as f:
+            json.dump(fixture_obj, f)
+        os.replace(tmp, path)
 
     def start_process(self, name, exe, env):
         self.procs[name] = Proc(name, [binary(exe)], env, self.workdir)

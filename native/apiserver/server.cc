@@ -280,6 +280,7 @@ struct FaultRule {
   int status = 0;
   int delay_ms = 0;
   int remaining = -1;  // -1 = unlimited
+  bool reset = false;  // drop the connection without a response
   std::string message;
 };
 
@@ -332,6 +333,7 @@ struct ApiServer::Impl {
   std::map<std::string, std::shared_ptr<http::Client>> hook_clients;
 
   std::atomic<uint64_t> requests{0};
+  std::atomic<uint64_t> faults_hit{0};
 
   explicit Impl(Options o) : opts(std::move(o)) {
     for (const ResourceType* rt : kube::types::builtin()) {
@@ -1512,7 +1514,12 @@ struct ApiServer::Impl {
       }
     }
     if (!found) return false;
+    faults_hit.fetch_add(1);
     if (hit.delay_ms > 0) std::this_thread::sleep_for(std::chrono::milliseconds(hit.delay_ms));
+    if (hit.reset) {
+      w.abort();
+      return true;
+    }
     if (hit.status > 0) {
       std::string reason = hit.status == 409 ? "Conflict" : hit.status == 410 ? "Expired" : hit.status >= 500 ? "InternalError" : "BadRequest";
       w.send_json(hit.status, status_body(hit.status, reason, hit.message.empty() ? "injected fault" : hit.message).dump());
@@ -1535,6 +1542,7 @@ struct ApiServer::Impl {
         f.delay_ms = r.get("delay_ms").is_int() ? static_cast<int>(r.get("delay_ms").as_int()) : 0;
         f.remaining = r.get("count").is_int() ? static_cast<int>(r.get("count").as_int()) : -1;
         f.message = r.get_string("message");
+        f.reset = r.get("reset").is_bool() && r.get("reset").as_bool();
         faults.push_back(std::move(f));
       }
       w.send_json(200, "{}");
@@ -1575,6 +1583,7 @@ struct ApiServer::Impl {
                                       {"objects", static_cast<unsigned long long>(total)},
                                       {"watches", static_cast<unsigned long long>(watches.size())},
                                       {"requests", static_cast<unsigned long long>(requests.load())},
+                                      {"faults_hit", static_cast<unsigned long long>(faults_hit.load())},
                                       {"by_type", counts}}).dump());
       return;
     }

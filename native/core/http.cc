@@ -272,6 +272,12 @@ static bool read_chunked(Reader& r, std::string& body, int timeout_ms, size_t ma
 // ---------------------------------------------------------------------------
 // Server
 
+void ResponseWriter::abort() {
+  s_.shutdown();
+  sent_ = true;
+  keep_alive_ = false;
+}
+
 void ResponseWriter::send(int status, const std::string& body, const std::string& content_type,
                           const Headers* extra) {
   if (sent_) return;

@@ -104,6 +104,8 @@ class ResponseWriter {
   bool start_chunked(int status, const std::string& content_type);
   bool write_chunk(const std::string& data);
   void end_chunked();
+  // Drops the connection without a response (fault injection: connection reset).
+  void abort();
   bool sent() const { return sent_; }
   bool keep_alive() const { return keep_alive_; }
   // True once the server is shutting down; streaming handlers should return.

@@ -8,6 +8,7 @@
 #include "core/log.h"
 #include "gpu/diag.h"
 #include "kube/leader.h"
+#include "kube/runtime.h"
 
 namespace bgc::gpu {
 
@@ -150,10 +151,24 @@ void NodeAgent::init() {
   for (const auto& g : gpus_) idx.push_back(g.index);
   poller_ = std::make_unique<TelemetryPoller>(*backend_, idx, std::chrono::milliseconds(cfg_.poll_interval_ms));
   poller_->poll_once();
-  if (cfg_.create_node && !client_.get_opt(types::Node, "", cfg_.node_name)) {
+  bool exists = client_.get_opt(types::Node, "", cfg_.node_name).has_value();
+  if (cfg_.create_node && !exists) {
     client_.create(types::Node, "", Value::object({{"apiVersion", "v1"}, {"kind", "Node"},
                                                    {"metadata", Value::object({{"name", cfg_.node_name}})}}));
+    exists = true;
   }
+  node_present_ = exists;
+  if (!exists) LOG_WARN("node_agent") << "node " << cfg_.node_name << " is not registered yet; waiting for the kubelet";
+}
+
+bool NodeAgent::node_up_to_date(const Value& node) const {
+  const Value& labels = node.get("metadata").get("labels");
+  if (labels.get_string(cfg_.label_prefix + ".count") != std::to_string(gpus_.size())) return false;
+  int healthy = healthy_count(nullptr);
+  if (labels.get_string(cfg_.label_prefix + ".healthy-count") != std::to_string(healthy)) return false;
+  const Value& st = node.get("status");
+  return st.get("capacity").get_string(cfg_.resource_name) == std::to_string(gpus_.size()) &&
+         st.get("allocatable").get_string(cfg_.resource_name) == std::to_string(healthy);
 }
 
 int NodeAgent::healthy_count(std::string* reason) const {
@@ -178,11 +193,13 @@ int NodeAgent::healthy_count(std::string* reason) const {
 
 void NodeAgent::publish() {
   std::lock_guard<std::mutex> lk(publish_mu_);
+  if (!cfg_.create_node && !node_present_) return;  // the kubelet registers the Node, not us
   std::string reason;
   int healthy = healthy_count(&reason);
   client_.apply(types::Node, "", cfg_.node_name, node_labels_patch(cfg_, gpus_, healthy, diag_), kNodeAgentManager, true);
   client_.apply_status(types::Node, "", cfg_.node_name, node_status_patch(cfg_, gpus_, healthy, reason),
                        kNodeAgentManager, true);
+  publishes_.fetch_add(1);
   LOG_INFO("node_agent") << "published node " << cfg_.node_name << ": " << cfg_.resource_name << " capacity "
                          << gpus_.size() << ", allocatable " << healthy;
 }
@@ -205,12 +222,47 @@ void NodeAgent::start() {
       }
     }
   });
+  node_watch_ = std::thread([this] {
+    kube::Watcher w(client_, types::Node, "", "", "metadata.name=" + cfg_.node_name);
+    auto consider = [this](const kube::ObjPtr& obj) {
+      if (!obj) {
+        node_present_ = false;
+        if (!cfg_.create_node) {
+          LOG_WARN("node_agent") << "node " << cfg_.node_name << " deleted; waiting for re-registration";
+          return;
+        }
+        LOG_WARN("node_agent") << "node " << cfg_.node_name << " deleted; re-creating";
+      } else {
+        node_present_ = true;
+        if (node_up_to_date(*obj)) return;
+        LOG_INFO("node_agent") << "node " << cfg_.node_name << " (re)registered or drifted; re-publishing";
+      }
+      try {
+        publish();
+      } catch (const std::exception& e) {
+        LOG_ERROR("node_agent") << "publish after node change failed: " << e.what();
+      }
+    };
+    w.run(stop_, [&](const kube::WatchEvent& ev) {
+      switch (ev.type) {
+        case kube::WatchEvent::Type::Restarted:
+          consider(ev.objects.empty() ? nullptr : ev.objects.front());
+          break;
+        case kube::WatchEvent::Type::Deleted:
+          consider(nullptr);
+          break;
+        default:
+          consider(ev.object);
+      }
+    });
+  });
 }
 
 void NodeAgent::stop() {
   stop_.cancel();
   if (poller_) poller_->stop();
   if (heartbeat_.joinable()) heartbeat_.join();
+  if (node_watch_.joinable()) node_watch_.join();
 }
 
 Value NodeAgent::describe() const {

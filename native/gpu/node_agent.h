@@ -11,8 +11,13 @@
 // Labels go through server-side apply on the Node, capacity/condition through SSA on
 // nodes/status, both with field manager "bacchus-gpu-node-agent" so kubelet-owned
 // fields are untouched.  Health flips from the telemetry side thread re-apply status.
+// The agent also watches its own Node (fieldSelector metadata.name=<node>): a Node that
+// is deleted and re-registered (drain / re-add) or whose labels/capacity drift is
+// re-published immediately instead of on the next heartbeat.  Without create_node the
+// agent never creates the Node itself; it waits for the kubelet to register it.
 #pragma once
 
+#include <atomic>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -68,7 +73,10 @@ class NodeAgent {
   void init();
   // Apply labels + status now.
   void publish();
-  void start();  // telemetry thread + heartbeat thread
+  void start();  // telemetry thread + heartbeat thread + Node watch
+  // True when `node` already carries what publish() would write (labels + capacity).
+  bool node_up_to_date(const json::Value& node) const;
+  uint64_t publishes() const { return publishes_.load(); }
   void stop();
   json::Value describe() const;  // for GET /gpus
   const std::vector<GpuInfo>& gpus() const { return gpus_; }
@@ -85,6 +93,9 @@ class NodeAgent {
   std::mutex publish_mu_;
   CancelToken stop_;
   std::thread heartbeat_;
+  std::thread node_watch_;
+  std::atomic<bool> node_present_{true};
+  std::atomic<uint64_t> publishes_{0};
 };
 
 }  // namespace bgc::gpu

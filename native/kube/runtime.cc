@@ -16,8 +16,13 @@ std::string meta_rv(const Value& obj) { return obj.get("metadata").get_string("r
 // ---------------------------------------------------------------------------
 // Watcher
 
-Watcher::Watcher(KubeClient& client, ResourceType rt, std::string ns, std::string label_selector)
-    : client_(client), rt_(std::move(rt)), ns_(std::move(ns)), selector_(std::move(label_selector)) {}
+Watcher::Watcher(KubeClient& client, ResourceType rt, std::string ns, std::string label_selector,
+                 std::string field_selector)
+    : client_(client),
+      rt_(std::move(rt)),
+      ns_(std::move(ns)),
+      selector_(std::move(label_selector)),
+      field_selector_(std::move(field_selector)) {}
 
 void Watcher::run(CancelToken& stop, const std::function<void(const WatchEvent&)>& on_event) {
   std::string rv;
@@ -31,6 +36,7 @@ void Watcher::run(CancelToken& stop, const std::function<void(const WatchEvent&)
       if (need_list) {
         ListOptions lo;
         lo.label_selector = selector_;
+        lo.field_selector = field_selector_;
         Value list = client_.list(rt_, ns_, lo);
         rv = list.get("metadata").get_string("resourceVersion");
         WatchEvent ev{WatchEvent::Type::Restarted, nullptr, {}};
@@ -47,6 +53,7 @@ void Watcher::run(CancelToken& stop, const std::function<void(const WatchEvent&)
       WatchOptions wo;
       wo.resource_version = rv;
       wo.label_selector = selector_;
+      wo.field_selector = field_selector_;
       auto stream = client_.watch(rt_, ns_, wo);
       backoff = std::chrono::milliseconds(800);
       std::string line;

@@ -48,7 +48,8 @@ std::string meta_rv(const json::Value& obj);
 // events trigger a relist; connection failures back off exponentially (0.8s..30s).
 class Watcher {
  public:
-  Watcher(KubeClient& client, ResourceType rt, std::string ns = "", std::string label_selector = "");
+  Watcher(KubeClient& client, ResourceType rt, std::string ns = "", std::string label_selector = "",
+          std::string field_selector = "");
   void run(CancelToken& stop, const std::function<void(const WatchEvent&)>& on_event);
   uint64_t relists() const { return relists_.load(); }
   uint64_t reconnects() const { return reconnects_.load(); }
@@ -58,6 +59,7 @@ class Watcher {
   ResourceType rt_;
   std::string ns_;
   std::string selector_;
+  std::string field_selector_;
   std::atomic<uint64_t> relists_{0};
   std::atomic<uint64_t> reconnects_{0};
 };

@@ -77,7 +77,9 @@ void register_gpu(py::module_& m) {
     return pb;
   }, py::arg("kind") = "auto", py::arg("fixture_json") = "");
 
-  m.def("default_mi355x_fixture", [](int n) { return bgc::gpu::default_mi355x_fixture(n).dump(); }, py::arg("n") = 8);
+  m.def("default_mi355x_fixture",
+        [](int n, uint64_t hive_id) { return bgc::gpu::default_mi355x_fixture(n, hive_id).dump(); }, py::arg("n") = 8,
+        py::arg("hive_id") = 0x1a2b3c4d5e6f7788ULL);
 
   py::class_<PyPoller>(m, "TelemetryPoller")
       .def(py::init([](std::shared_ptr<PyBackend> b, std::vector<int> idx, int interval_ms) {

@@ -2,6 +2,7 @@
 amd.com/gpu capacity/allocatable, and GPU flap handling (BASELINE config #5)."""
 import json
 import os
+import time
 
 import pytest
 import requests
@@ -56,3 +57,20 @@ def test_node_agent_advertises_and_flaps(nat):
         _write_atomic(fixture, f)
         wait_for(lambda: c.admin.get("nodes", "mi355x-0")["status"]["allocatable"]["amd.com/gpu"] == "8",
                  timeout=10, desc="allocatable back to 8")
+
+
+def test_node_agent_waits_for_kubelet_registration():
+    """Real clusters (CONF_CREATE_NODE=false): the agent never creates the Node; when the
+    kubelet registers it, the agent's Node watch publishes immediately (heartbeat is 30 s)."""
+    with Cluster(admission=False, controller=False) as c:
+        c.start_node_agent(node_name="mi355x-9", backend="mock", proc_name="na",
+                           extra_env={"CONF_CREATE_NODE": "false", "CONF_HEARTBEAT_SECS": "30"})
+        time.sleep(1.0)
+        assert c.admin.get_or_none("nodes", "mi355x-9") is None
+        c.admin.create("nodes", {"apiVersion": "v1", "kind": "Node",
+                                 "metadata": {"name": "mi355x-9", "labels": {"kubernetes.io/hostname": "mi355x-9"}}})
+        node = wait_for(lambda: (lambda n: n if n.get("status", {}).get("allocatable", {}).get("amd.com/gpu") == "8"
+                                 else None)(c.admin.get("nodes", "mi355x-9")), timeout=5, desc="published on registration")
+        labels = node["metadata"]["labels"]
+        assert labels["kubernetes.io/hostname"] == "mi355x-9" and labels["amd.com/gpu.count"] == "8"
+        assert c.procs["na"].alive()

@@ -43,6 +43,21 @@ def test_injected_api_errors_are_retried():
         assert 'bgc_reconcile_total{result="error"}' in m
 
 
+def test_connection_resets_and_patch_latency_are_survived():
+    """kube-lite drops the connection (no response) on the Namespace apply and delays the
+    ResourceQuota apply; the controller must retry and converge (SURVEY §4.2 fault rows)."""
+    with Cluster(admission=False, controller_env={"CONF_ERROR_REQUEUE_MS": "200"}) as c:
+        c.fault([{"method": "PATCH", "path": "/api/v1/namespaces/r1$|/api/v1/namespaces/r1\\?", "reset": True, "count": 4},
+                 {"method": "PATCH", "path": "/resourcequotas/r1", "delay_ms": 400}])
+        c.admin.create("userbootstraps", ub("r1", {"kube_username": "r1", "quota": {"hard": {"requests.amd.com/gpu": "1"}}}))
+        wait_for(lambda: c.admin.get_or_none("resourcequotas", "r1", "r1"), timeout=15, desc="r1 quota after resets")
+        assert c.admin.get("namespaces", "r1")["metadata"]["ownerReferences"][0]["name"] == "r1"
+        assert c.procs["controller"].alive()
+        assert c.stats()["faults_hit"] >= 5
+        m = requests.get(f"http://127.0.0.1:{c.controller_port}/metrics", timeout=5).text
+        assert 'bgc_reconcile_total{result="error"}' in m
+
+
 def test_webhook_unavailable_blocks_writes_failure_policy_fail():
     with Cluster(controller=False) as c:
         c.procs["admission"].stop()

@@ -107,3 +107,17 @@ def test_missing_config_fails_fast():
 
     r = subprocess.run([binary("synchronizer")], env={"PATH": "/usr/bin"}, capture_output=True, text=True, timeout=10)
     assert r.returncode != 0 and "missing value for field listen_addr" in r.stderr
+
+
+def test_status_put_conflict_is_retried(google):
+    """Two injected 409s on the status PUT: the synchronizer re-reads the resourceVersion and
+    retries (synchronizer.rs:294 optimistic concurrency) instead of exiting."""
+    google.set_rows([{"id_username": "erin", "gpu": 1}])
+    with Cluster(controller_env={"CONF_REQUEUE_SECS": "2"}) as c:
+        c.as_user("oidc:erin", ["gpu"]).create("userbootstraps", ub("erin"))
+        c.fault([{"method": "PUT", "path": "/userbootstraps/erin/status", "status": 409, "count": 2}])
+        p = c.start_synchronizer(google, interval=1)
+        wait_for(lambda: c.admin.get("userbootstraps", "erin").get("status", {}).get("synchronized_with_sheet"),
+                 timeout=10, desc="erin synced despite conflicts")
+        assert p.alive()
+        assert c.stats()["faults_hit"] == 2
