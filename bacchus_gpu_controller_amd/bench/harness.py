@@ -141,7 +141,7 @@ def run(args):
                 for r in range(d.world) for s in range(total_steps) for name in _names(r, s, args.batch)]
         google.set_rows(rows)
         cluster = Cluster(controller_env={"CONF_WORKERS": str(args.controller_workers)},
-                          log_level=args.log_level)
+                          log_level=args.log_level, tls_apiserver=args.tls_apiserver)
         cluster.start()
         cluster.start_synchronizer(google, interval=60, extra_env={"CONF_WATCH": "true",
                                                                    "CONF_WORKERS": str(args.sync_workers),
@@ -151,10 +151,13 @@ def run(args):
         info = {"server": cluster.server, "controller": f"http://127.0.0.1:{cluster.controller_port}",
                 "admission": f"https://127.0.0.1:{cluster.admission_port}",
                 "ca": os.path.join(cluster.cert_dir, "ca.crt"),
-                "node_agent": f"http://127.0.0.1:{cluster.node_agent_port}"}
+                "node_agent": f"http://127.0.0.1:{cluster.node_agent_port}",
+                "apiserver_ca": open(cluster.apiserver_ca).read() if args.tls_apiserver else "",
+                "apiserver_verify": cluster.verify}
     info = d.broadcast_obj(info)
     try:
-        driver = nat.ChurnDriver(info["server"], ADMIN_TOKEN, f"r{d.rank}-", args.concurrency)
+        driver = nat.ChurnDriver(info["server"], ADMIN_TOKEN, f"r{d.rank}-", args.concurrency,
+                                 ca_pem=info["apiserver_ca"])
         driver.start()
         time.sleep(0.2)
         prev = None
@@ -168,7 +171,7 @@ def run(args):
                 d.sync()
                 if d.rank == 0:
                     _clear(info["controller"] + "/debug/samples/reconcile")
-                    _clear(info["server"] + "/debug/samples/webhook")
+                    _clear(info["server"] + "/debug/samples/webhook", verify=info["apiserver_verify"])
                     _clear(info["admission"] + "/debug/samples/admission", verify=info["ca"])
                     _clear(info["node_agent"] + "/debug/samples/telemetry_poll")
                 d.barrier()
@@ -194,7 +197,7 @@ def run(args):
         if d.rank != 0:
             return None
         rec = _samples(info["controller"] + "/debug/samples/reconcile")
-        hook = _samples(info["server"] + "/debug/samples/webhook")
+        hook = _samples(info["server"] + "/debug/samples/webhook", verify=info["apiserver_verify"])
         adm = _samples(info["admission"] + "/debug/samples/admission", verify=info["ca"])
         tel = _samples(info["node_agent"] + "/debug/samples/telemetry_poll")
         all_lat = [x for p in per_rank for x in p["lat"]]
@@ -216,8 +219,8 @@ def run(args):
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic",
-            "config": {"model": "UserBootstrap onboarding churn (kube-lite + TLS admission + controller + "
-                                "synchronizer + MI355X node-agent)",
+            "config": {"model": "UserBootstrap onboarding churn (kube-lite" + (" over HTTPS" if args.tls_apiserver else "")
+                                + " + TLS admission + controller + synchronizer + MI355X node-agent)",
                        "global_batch": args.batch * d.world, "seq_len": None, "parallelism": f"dp{d.world}"},
             "reconcile_p99_ms": ms(_pct(rec, 0.99)),
             "reconcile_p50_ms": ms(_pct(rec, 0.50)),
@@ -240,8 +243,6 @@ def run(args):
             out["component_cpu_s"] = {name: _cpu_seconds(p.p.pid) for name, p in cluster.procs.items()}
         return out
     finally:
-        if d.rank == 0:
-            d_barrier_safe = True  # noqa: F841
         if cluster is not None:
             cluster.stop()
         if google is not None:
@@ -263,6 +264,8 @@ def main(argv=None):
     ap.add_argument("--log-level", default="warn")
     ap.add_argument("--json-out", default="")
     ap.add_argument("--report-cpu", action="store_true", help="add per-component CPU seconds to the JSON")
+    ap.add_argument("--tls-apiserver", action=argparse.BooleanOptionalAction, default=True,
+                    help="components reach kube-lite over HTTPS via kubeconfigs, as in a real cluster")
     args = ap.parse_args(argv)
     out = run(args)
     if out is not None:

@@ -92,7 +92,10 @@ def webhook_configuration(ca_pem, port, timeout_seconds=10):
 
 class Cluster:
     def __init__(self, workdir=None, admission=True, controller=True, controller_env=None, admission_env=None,
-                 apiserver_args=None, log_level="warn"):
+                 apiserver_args=None, log_level="warn", tls_apiserver=False):
+        """tls_apiserver: kube-lite serves HTTPS with its own CA and every component reaches it
+        through a kubeconfig (certificate-authority + tokenFile, paths relative to the
+        kubeconfig) instead of the BGC_KUBE_* test overrides."""
         self._tmp = None
         keep = os.environ.get("BGC_CLUSTER_LOGDIR")  # keep component logs (sanitizer runs)
         if workdir is None and keep:
@@ -108,6 +111,8 @@ class Cluster:
         self.admission_env = admission_env or {}
         self.apiserver_args = apiserver_args or []
         self.log_level = log_level
+        self.tls_apiserver = tls_apiserver
+        self.verify = True
         self.procs = {}
         self.server = None
         self.ca_pem = None
@@ -143,11 +148,14 @@ class Cluster:
         args = [binary("kube-lite"), "--port", "0", "--port-file", port_file, "--token-file", tokens,
                 "--no-anonymous", "--bookmark-ms", "1000",
                 "--service-override", f"{NAMESPACE}/{WEBHOOK_SERVICE}=127.0.0.1:{self.admission_port}"]
+        if self.tls_apiserver:
+            args += self._apiserver_certs()
         args += self.apiserver_args
         self.procs["apiserver"] = Proc("apiserver", args, {"RUST_LOG": self.log_level}, self.workdir)
         wait_for(lambda: os.path.exists(port_file), 20, desc="kube-lite port file")
-        self.server = f"http://127.0.0.1:{open(port_file).read().strip()}"
-        self.admin = KubeApi(self.server, ADMIN_TOKEN)
+        scheme = "https" if self.tls_apiserver else "http"
+        self.server = f"{scheme}://127.0.0.1:{open(port_file).read().strip()}"
+        self.admin = KubeApi(self.server, ADMIN_TOKEN, verify=self.verify)
         self.admin.create("namespaces", {"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": NAMESPACE}})
         self.admin.create("customresourcedefinitions", json.loads(native().crd_json()))
         if self.want_admission:
@@ -158,9 +166,58 @@ class Cluster:
             self.start_controller()
         return self
 
+    def _apiserver_certs(self):
+        b = native().make_ca_and_leaf("kube-apiserver", ["kubernetes", "kubernetes.default.svc", "localhost",
+                                                         "127.0.0.1"], 30)
+        d = os.path.join(self.workdir, "apiserver-pki")
+        os.makedirs(d, exist_ok=True)
+        for k, fn in (("cert", "apiserver.crt"), ("key", "apiserver.key"), ("ca_cert", "ca.crt")):
+            with open(os.path.join(d, fn), "w") as f:
+                f.write(b[k])
+        self.apiserver_ca = os.path.join(d, "ca.crt")
+        self.verify = self.apiserver_ca
+        return ["--tls-cert", os.path.join(d, "apiserver.crt"), "--tls-key", os.path.join(d, "apiserver.key")]
+
+    def write_kubeconfig(self, token, name, ca_file=None):
+        """kubeconfig for one component: relative certificate-authority and tokenFile (both
+        resolved against the kubeconfig's directory, like client-go)."""
+        d = os.path.join(self.workdir, "kubeconfigs", name)
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, "token"), "w") as f:
+            f.write(token + "\n")
+        with open(os.path.join(d, "ca.crt"), "w") as f:
+            f.write(open(ca_file or self.apiserver_ca).read())
+        path = os.path.join(d, "config")
+        with open(path, "w") as f:
+            f.write(f"""apiVersion: v1
+kind: Config
+clusters:
+- name: kube-lite
+  cluster:
+    server: {self.server}
+    certificate-authority: ca.crt
+users:
+- name: {name}
+  user:
+    tokenFile: token
+contexts:
+- name: {name}@kube-lite
+  context:
+    cluster: kube-lite
+    user: {name}
+current-context: {name}@kube-lite
+""")
+        return path
+
     def component_env(self, token, port):
-        return {"BGC_KUBE_SERVER": self.server, "BGC_KUBE_TOKEN": token, "CONF_LISTEN_ADDR": "127.0.0.1",
-                "CONF_LISTEN_PORT": str(port), "RUST_LOG": self.log_level}
+        env = {"CONF_LISTEN_ADDR": "127.0.0.1", "CONF_LISTEN_PORT": str(port), "RUST_LOG": self.log_level}
+        if self.tls_apiserver:
+            name = {CONTROLLER_TOKEN: "controller", SYNC_TOKEN: "synchronizer",
+                    NODE_AGENT_TOKEN: "node-agent"}.get(token, "admin")
+            env["KUBECONFIG"] = self.write_kubeconfig(token, name)
+        else:
+            env.update({"BGC_KUBE_SERVER": self.server, "BGC_KUBE_TOKEN": token})
+        return env
 
     def start_admission(self):
         env = {
@@ -241,26 +298,26 @@ class Cluster:
 
     # ------------------------------------------------------------------ access
     def as_user(self, username, groups=()):
-        return KubeApi(self.server, ADMIN_TOKEN, as_user=username, as_groups=list(groups))
+        return KubeApi(self.server, ADMIN_TOKEN, as_user=username, as_groups=list(groups), verify=self.verify)
 
     def fault(self, rules, append=False):
-        r = requests.post(self.server + "/_kl/faults" + ("?append=true" if append else ""), json=rules, timeout=5)
+        r = requests.post(self.server + "/_kl/faults" + ("?append=true" if append else ""), json=rules, timeout=5, verify=self.verify)
         r.raise_for_status()
 
     def clear_faults(self):
-        requests.delete(self.server + "/_kl/faults", timeout=5)
+        requests.delete(self.server + "/_kl/faults", timeout=5, verify=self.verify)
 
     def compact_and_drop_watches(self):
-        requests.post(self.server + "/_kl/compact", timeout=5).raise_for_status()
-        requests.post(self.server + "/_kl/drop-watches", timeout=5).raise_for_status()
+        requests.post(self.server + "/_kl/compact", timeout=5, verify=self.verify).raise_for_status()
+        requests.post(self.server + "/_kl/drop-watches", timeout=5, verify=self.verify).raise_for_status()
 
     def stats(self):
-        return requests.get(self.server + "/_kl/stats", timeout=5).json()
+        return requests.get(self.server + "/_kl/stats", timeout=5, verify=self.verify).json()
 
     def samples(self, component, name):
         port = {"apiserver": None, "controller": self.controller_port}.get(component)
         base = self.server if component == "apiserver" else f"http://127.0.0.1:{port}"
-        return requests.get(f"{base}/debug/samples/{name}", timeout=5).json()
+        return requests.get(f"{base}/debug/samples/{name}", timeout=5, verify=self.verify).json()
 
     def stop(self):
         codes = {}

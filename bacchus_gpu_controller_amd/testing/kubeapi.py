@@ -60,9 +60,10 @@ def path_for(plural, name=None, namespace=None, sub=None):
 
 
 class KubeApi:
-    def __init__(self, server, token=None, as_user=None, as_groups=None, timeout=15):
+    def __init__(self, server, token=None, as_user=None, as_groups=None, timeout=15, verify=True):
         self.server = server.rstrip("/")
         self.s = requests.Session()
+        self.s.verify = verify  # CA bundle path for an HTTPS apiserver
         self.timeout = timeout
         if token:
             self.s.headers["Authorization"] = f"Bearer {token}"

@@ -30,6 +30,7 @@ namespace bgc::bench {
 struct ChurnOptions {
   std::string server;
   std::string admin_token;
+  std::string ca_pem;  // trust root for an HTTPS apiserver
   std::string user_prefix = "oidc:";
   std::string group = "gpu";
   std::string gpu_quota_key = "requests.amd.com/gpu";

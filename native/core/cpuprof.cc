@@ -1,0 +1,154 @@
+#include "core/cpuprof.h"
+
+#include <fcntl.h>
+#include <signal.h>
+#include <sys/time.h>
+#include <ucontext.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cerrno>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <mutex>
+#include <sstream>
+#include <vector>
+
+namespace bgc::cpuprof {
+
+namespace {
+
+constexpr int kMaxFrames = 40;
+constexpr size_t kMaxSamples = size_t(1) << 17;  // ~43 MB at 40 frames; ~2 min of one busy core at 997 Hz
+
+struct Sample {
+  uint32_t n;
+  uintptr_t pc[kMaxFrames];
+};
+
+Sample* g_buf = nullptr;
+std::atomic<size_t> g_next{0};
+std::atomic<bool> g_on{false};
+std::atomic<uint64_t> g_dropped{0};
+int g_probe[2] = {-1, -1};
+std::string g_path;
+std::mutex g_mu;
+bool g_started = false;
+
+// True when [p, p+16) is readable: write() reports EFAULT instead of faulting.
+bool readable(uintptr_t p) {
+  if (p < 4096) return false;
+  ssize_t w = ::write(g_probe[1], reinterpret_cast<const void*>(p), 16);
+  if (w != 16) return false;
+  char sink[16];
+  (void)!::read(g_probe[0], sink, sizeof(sink));
+  return true;
+}
+
+void on_sigprof(int, siginfo_t*, void* ucv) {
+  if (!g_on.load(std::memory_order_relaxed)) return;
+  int saved_errno = errno;
+  size_t i = g_next.fetch_add(1, std::memory_order_relaxed);
+  if (i >= kMaxSamples) {
+    g_dropped.fetch_add(1, std::memory_order_relaxed);
+    errno = saved_errno;
+    return;
+  }
+  auto* uc = static_cast<ucontext_t*>(ucv);
+  Sample& s = g_buf[i];
+  uint32_t n = 0;
+  s.pc[n++] = static_cast<uintptr_t>(uc->uc_mcontext.gregs[REG_RIP]);
+  uintptr_t sp = static_cast<uintptr_t>(uc->uc_mcontext.gregs[REG_RSP]);
+  uintptr_t fp = static_cast<uintptr_t>(uc->uc_mcontext.gregs[REG_RBP]);
+  // [fp] = caller's fp, [fp + 8] = return address; frames grow toward higher addresses
+  while (n < kMaxFrames && fp >= sp && fp - sp < (uintptr_t(64) << 20) && (fp & 7) == 0 && readable(fp)) {
+    const uintptr_t* f = reinterpret_cast<const uintptr_t*>(fp);
+    uintptr_t next = f[0];
+    uintptr_t ret = f[1];
+    if (ret < 4096) break;
+    s.pc[n++] = ret - 1;  // attribute to the call instruction
+    if (next <= fp) break;
+    fp = next;
+  }
+  s.n = n;
+  errno = saved_errno;
+}
+
+void write_profile() {
+  if (g_path.empty() || !g_buf) return;
+  size_t n = std::min(g_next.load(), kMaxSamples);
+  std::map<std::vector<uintptr_t>, uint64_t> stacks;
+  for (size_t i = 0; i < n; ++i) {
+    const Sample& s = g_buf[i];
+    if (s.n == 0 || s.n > kMaxFrames) continue;  // slot claimed but not filled
+    stacks[std::vector<uintptr_t>(s.pc, s.pc + s.n)]++;
+  }
+  std::ofstream out(g_path);
+  if (!out) return;
+  std::ifstream maps("/proc/self/maps");
+  out << "# bgc cpuprof v1 samples=" << n << " dropped=" << g_dropped.load() << "\n";
+  out << "maps\n" << maps.rdbuf() << "end maps\n";
+  char buf[32];
+  for (const auto& [st, cnt] : stacks) {
+    out << cnt;
+    for (uintptr_t pc : st) {
+      std::snprintf(buf, sizeof(buf), " %lx", static_cast<unsigned long>(pc));
+      out << buf;
+    }
+    out << "\n";
+  }
+}
+
+}  // namespace
+
+bool start(const std::string& path, int hz) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_started) return true;
+  if (::pipe2(g_probe, O_CLOEXEC | O_NONBLOCK) != 0) return false;
+  g_buf = static_cast<Sample*>(std::calloc(kMaxSamples, sizeof(Sample)));
+  if (!g_buf) return false;
+  g_path = path;
+  struct sigaction sa {};
+  sa.sa_sigaction = on_sigprof;
+  sa.sa_flags = SA_SIGINFO | SA_RESTART;
+  sigemptyset(&sa.sa_mask);
+  if (sigaction(SIGPROF, &sa, nullptr) != 0) return false;
+  g_on = true;
+  struct itimerval it {};
+  long us = 1000000L / std::max(1, hz);
+  it.it_interval.tv_sec = us / 1000000L;
+  it.it_interval.tv_usec = us % 1000000L;
+  it.it_value = it.it_interval;
+  if (setitimer(ITIMER_PROF, &it, nullptr) != 0) return false;
+  g_started = true;
+  std::atexit([] { stop(); });
+  return true;
+}
+
+void start_from_env() {
+  const char* p = std::getenv("BGC_CPU_PROFILE");
+  if (!p || !*p) return;
+  int hz = 997;
+  if (const char* h = std::getenv("BGC_CPU_PROFILE_HZ")) hz = std::max(1, std::atoi(h));
+  std::string path = p;
+  // one file per process: a "%p" in the path becomes the pid
+  size_t at = path.find("%p");
+  if (at != std::string::npos) path.replace(at, 2, std::to_string(::getpid()));
+  if (!start(path, hz)) std::fprintf(stderr, "cpuprof: failed to start (%s)\n", std::strerror(errno));
+}
+
+void stop() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_started) return;
+  struct itimerval it {};
+  setitimer(ITIMER_PROF, &it, nullptr);
+  g_on = false;
+  write_profile();
+  g_started = false;
+}
+
+}  // namespace bgc::cpuprof

@@ -1,0 +1,15 @@
+// Common process start-up for the native services: RUST_LOG-style logging, glibc malloc
+// tuning and the optional sampling profiler (core/cpuprof.h).
+#pragma once
+
+namespace bgc {
+
+// Call first thing in main().
+void process_init();
+
+// glibc malloc tuning for many short-lived JSON allocations across thread-per-connection
+// servers: no heap trimming (the sbrk grow/trim cycle cost ~10% of kube-lite CPU), heap
+// growth in 64 MiB steps and a fixed 4 MiB mmap threshold. BGC_MALLOC_TUNE=0 disables it.
+void tune_malloc();
+
+}  // namespace bgc
