@@ -1,0 +1,239 @@
+"""Helm chart (R8) rendered with testing/helm_lite.py, since there is no helm binary here.
+
+The checks cover: the manifest inventory; selector and label consistency; the webhook →
+Service → Deployment → Certificate wiring (including the Q1 fix); RBAC grants for every API
+call each component makes; value overrides; and that the env each Deployment/DaemonSet sets
+is accepted by the native binary's CONF_* parser. Reference chart parity covers values keys
+and the chart name.
+"""
+import json
+import os
+import subprocess
+
+import pytest
+import yaml
+
+from bacchus_gpu_controller_amd import REPO_ROOT, binary, native
+from bacchus_gpu_controller_amd.testing.helm_lite import TemplateError, _go_float, manifests, render_chart
+
+CHART = os.path.join(REPO_ROOT, "charts", "bacchus-gpu-controller")
+REF_CHART = "/root/reference/charts/bacchus-gpu-controller"
+NS = "bgc-system"
+
+
+def render(values=None):
+    return manifests(render_chart(CHART, values, {"Name": "bgc", "Namespace": NS}))
+
+
+def by_kind(objs, kind):
+    return {o["metadata"]["name"]: o for o in objs if o["kind"] == kind}
+
+
+@pytest.fixture(scope="module")
+def objs():
+    return render()
+
+
+def test_inventory(objs):
+    kinds = sorted((o["kind"], o["metadata"]["name"]) for o in objs)
+    deps = by_kind(objs, "Deployment")
+    assert set(deps) == {f"bgc-bacchus-gpu-{c}" for c in ("controller", "admission", "synchronizer")}
+    assert set(by_kind(objs, "DaemonSet")) == {"bgc-bacchus-gpu-node-agent"}
+    assert set(by_kind(objs, "Service")) == {"bgc-bacchus-gpu-admission"}
+    assert set(by_kind(objs, "MutatingWebhookConfiguration")) == {"bgc-bacchus-gpu"}
+    assert "userbootstraps.bacchus.io" in by_kind(objs, "CustomResourceDefinition")
+    assert len(by_kind(objs, "Certificate")) == 2 and len(by_kind(objs, "Issuer")) == 2
+    assert len(kinds) == len(set(kinds)), "duplicate objects"
+
+
+def test_crd_matches_crdgen(objs):
+    crd = by_kind(objs, "CustomResourceDefinition")["userbootstraps.bacchus.io"]
+    crd.pop("__source__")
+    assert crd == json.loads(native().crd_json())
+
+
+def test_selectors_and_service_accounts(objs):
+    sas = set(by_kind(objs, "ServiceAccount"))
+    for o in list(by_kind(objs, "Deployment").values()) + list(by_kind(objs, "DaemonSet").values()):
+        sel = o["spec"]["selector"]["matchLabels"]
+        labels = o["spec"]["template"]["metadata"]["labels"]
+        assert sel.items() <= labels.items(), o["metadata"]["name"]
+        assert o["spec"]["template"]["spec"]["serviceAccountName"] in sas
+    # Q1 fix: each component's selector matches only its own pods
+    sels = [frozenset(o["spec"]["selector"]["matchLabels"].items()) for o in by_kind(objs, "Deployment").values()]
+    assert len(set(sels)) == 3
+
+
+def test_webhook_service_deployment_certificate_wiring(objs):
+    svc = by_kind(objs, "Service")["bgc-bacchus-gpu-admission"]
+    adm = by_kind(objs, "Deployment")["bgc-bacchus-gpu-admission"]
+    pod_labels = adm["spec"]["template"]["metadata"]["labels"]
+    assert svc["spec"]["selector"].items() <= pod_labels.items()
+    for other in ("controller", "synchronizer"):
+        d = by_kind(objs, "Deployment")[f"bgc-bacchus-gpu-{other}"]
+        assert not svc["spec"]["selector"].items() <= d["spec"]["template"]["metadata"]["labels"].items()
+    port = svc["spec"]["ports"][0]
+    container = adm["spec"]["template"]["spec"]["containers"][0]
+    cport = {p["name"]: p["containerPort"] for p in container["ports"]}
+    assert port["targetPort"] in cport or port["targetPort"] in cport.values()
+
+    wh = by_kind(objs, "MutatingWebhookConfiguration")["bgc-bacchus-gpu"]
+    hook = wh["webhooks"][0]
+    ref = hook["clientConfig"]["service"]
+    assert (ref["name"], ref["namespace"], ref["path"]) == (svc["metadata"]["name"], NS, "/mutate")
+    assert ref.get("port", 443) == port["port"]
+    assert hook["failurePolicy"] == "Fail" and hook["timeoutSeconds"] == 10
+    rule = hook["rules"][0]
+    assert rule["apiGroups"] == ["bacchus.io"] and rule["resources"] == ["userbootstraps"]
+    assert set(rule["operations"]) >= {"CREATE", "UPDATE", "DELETE"}
+
+    # caBundle <- CA Certificate; its secret backs the Issuer that signs the serving cert
+    inject = wh["metadata"]["annotations"]["cert-manager.io/inject-ca-from"]
+    cns, cname = inject.split("/")
+    certs = by_kind(objs, "Certificate")
+    ca = certs[cname]
+    assert cns == NS and ca["spec"]["isCA"] is True
+    issuer = next(i for i in by_kind(objs, "Issuer").values()
+                  if i["spec"].get("ca", {}).get("secretName") == ca["spec"]["secretName"])
+    cert = next(c for c in certs.values() if c["spec"]["issuerRef"]["name"] == issuer["metadata"]["name"])
+    dns = set(cert["spec"]["dnsNames"])
+    assert {f"{svc['metadata']['name']}.{NS}", f"{svc['metadata']['name']}.{NS}.svc"} <= dns
+    vols = {v["name"]: v for v in adm["spec"]["template"]["spec"]["volumes"]}
+    assert vols["cert"]["secret"]["secretName"] == cert["spec"]["secretName"]
+    mounts = {m["name"]: m["mountPath"] for m in container["volumeMounts"]}
+    env = {e["name"]: e.get("value") for e in container["env"]}
+    assert env["CONF_CERT_PATH"].startswith(mounts["cert"] + "/")
+
+
+# (apiGroup, resource, verb) each component issues (native/controller, native/sync, native/gpu)
+NEEDED = {
+    "controller": [("bacchus.io", "userbootstraps", v) for v in ("get", "list", "watch")]
+    + [("", r, v) for r in ("namespaces", "resourcequotas") for v in ("get", "list", "watch", "create", "patch")]
+    + [("rbac.authorization.k8s.io", r, v) for r in ("roles", "rolebindings") for v in ("get", "list", "watch", "create", "patch")]
+    + [("rbac.authorization.k8s.io", "roles", "bind"), ("rbac.authorization.k8s.io", "roles", "escalate")]
+    + [("coordination.k8s.io", "leases", v) for v in ("get", "create", "update")],
+    "synchronizer": [("bacchus.io", "userbootstraps", v) for v in ("get", "list", "watch", "patch")]
+    + [("bacchus.io", "userbootstraps/status", "update")],
+    "node-agent": [("", "nodes", v) for v in ("get", "list", "watch", "patch")]
+    + [("", "nodes/status", "patch")],
+}
+
+
+def _allowed(rules, group, resource, verb):
+    for r in rules:
+        if (group in r.get("apiGroups", []) or "*" in r.get("apiGroups", [])) and \
+           (resource in r.get("resources", []) or "*" in r.get("resources", [])) and \
+           (verb in r.get("verbs", []) or "*" in r.get("verbs", [])):
+            return True
+    return False
+
+
+def test_rbac_covers_every_call(objs):
+    roles = by_kind(objs, "ClusterRole")
+    bindings = by_kind(objs, "ClusterRoleBinding")
+    for comp, needed in NEEDED.items():
+        sa = f"bgc-bacchus-gpu-{comp}"
+        rules = []
+        for b in bindings.values():
+            if any(s["kind"] == "ServiceAccount" and s["name"] == sa and s["namespace"] == NS for s in b["subjects"]):
+                rules += roles[b["roleRef"]["name"]]["rules"]
+        missing = [n for n in needed if not _allowed(rules, *n)]
+        assert not missing, f"{comp} lacks {missing}"
+
+
+def _rendered_env(container, extra=None):
+    env = {}
+    for e in container["env"]:
+        if "value" in e:
+            env[e["name"]] = e["value"]
+        else:
+            path = e["valueFrom"]["fieldRef"]["fieldPath"]
+            env[e["name"]] = {"metadata.namespace": NS, "spec.nodeName": "mi355x-0"}[path]
+    env.update(extra or {})
+    return env
+
+
+@pytest.mark.parametrize("component", ["controller", "admission", "synchronizer", "node-agent"])
+def test_binaries_accept_rendered_env(objs, component, tmp_path):
+    if component == "node-agent":
+        pod = by_kind(objs, "DaemonSet")["bgc-bacchus-gpu-node-agent"]
+    else:
+        pod = by_kind(objs, "Deployment")[f"bgc-bacchus-gpu-{component}"]
+    c = pod["spec"]["template"]["spec"]["containers"][0]
+    assert c["command"][0] == f"/app/{component}"
+    env = _rendered_env(c)
+    assert all(isinstance(v, str) for v in env.values())
+    # no kube credentials: the binary gets past config parsing and fails later
+    run_env = {"PATH": os.environ.get("PATH", ""), "HOME": str(tmp_path), **env}
+    run_env["CONF_LISTEN_ADDR"] = "127.0.0.1"
+    run_env["CONF_LISTEN_PORT"] = "0"
+    p = subprocess.run([binary(component)], env=run_env, capture_output=True, text=True, timeout=30)
+    out = p.stdout + p.stderr
+    assert "missing value for field" not in out and "invalid value for field" not in out, out
+    expected = {"controller": "not running in a cluster", "admission": "/cert/tls.",
+                "synchronizer": "/google_service_account_json/key.json", "node-agent": "not running in a cluster"}
+    assert p.returncode != 0 and expected[component] in out, out  # failed after config parsing
+
+
+def test_value_overrides():
+    objs = render({"nodeAgent": {"enabled": False},
+                   "admission": {"configs": {"authorized_group_names": ["a", "b", "c"]}, "replicaCount": 3},
+                   "controller": {"fullnameOverride": "gpuctl"}})
+    assert not by_kind(objs, "DaemonSet")
+    adm = by_kind(objs, "Deployment")["gpuctl-admission"]
+    assert adm["spec"]["replicas"] == 3
+    env = {e["name"]: e.get("value") for e in adm["spec"]["template"]["spec"]["containers"][0]["env"]}
+    assert env["CONF_AUTHORIZED_GROUP_NAMES"] == "a,b,c"
+    # large integers keep integer form (Helm would print float64 1e9 as 1.073741824e+09 without int64)
+    objs = render({"nodeAgent": {"configs": {"diag_hbm_bytes": 4294967296}}})
+    ds = by_kind(objs, "DaemonSet")["bgc-bacchus-gpu-node-agent"]
+    env = {e["name"]: e.get("value") for e in ds["spec"]["template"]["spec"]["containers"][0]["env"]}
+    assert env["CONF_DIAG_HBM_BYTES"] == "4294967296"
+
+
+def test_go_float_formatting_matches_helm():
+    assert _go_float(12322.0) == "12322"
+    assert _go_float(1073741824.0) == "1.073741824e+09"
+    assert _go_float(1e6) == "1e+06" and _go_float(0.5) == "0.5" and _go_float(1e-5) == "1e-05"
+
+
+def test_renderer_rejects_nil_field_access(tmp_path):
+    d = tmp_path / "c"
+    (d / "templates").mkdir(parents=True)
+    (d / "Chart.yaml").write_text("name: x\nversion: 0.1.0\n")
+    (d / "values.yaml").write_text("a: {}\n")
+    (d / "templates" / "t.yaml").write_text("v: {{ .Values.a.b.c }}\n")
+    with pytest.raises(TemplateError):
+        render_chart(str(d))
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_CHART), reason="reference chart not available")
+def test_values_and_name_parity_with_reference():
+    with open(os.path.join(REF_CHART, "values.yaml")) as f:
+        ref = yaml.safe_load(f)
+    with open(os.path.join(CHART, "values.yaml")) as f:
+        ours = yaml.safe_load(f)
+
+    def paths(d, p=()):
+        for k, v in d.items():
+            if isinstance(v, dict) and v:
+                yield from paths(v, p + (k,))
+            else:
+                yield p + (k,)
+
+    def get(o, p):
+        for k in p:
+            if not isinstance(o, dict) or k not in o:
+                raise KeyError(".".join(p))
+            o = o[k]
+        return o
+
+    for p in paths(ref):
+        get(ours, p)  # every reference key exists
+        if p[-1] != "repository":
+            assert get(ours, p) == get(ref, p), ".".join(p)
+    with open(os.path.join(REF_CHART, "Chart.yaml")) as f:
+        ref_chart = yaml.safe_load(f)
+    with open(os.path.join(CHART, "Chart.yaml")) as f:
+        our_chart = yaml.safe_load(f)
+    assert our_chart["name"] == ref_chart["name"]
