@@ -162,6 +162,7 @@ def run(args):
         time.sleep(0.2)
         prev = None
         lat, clat = [], []
+        stage = {"ns": [], "rq": [], "rb": []}
         ready = failed = timeouts = 0
         t_start = None
         errors = []
@@ -182,6 +183,8 @@ def run(args):
             if s >= args.warmup:
                 lat += res["ready_latency_s"]
                 clat += res["create_latency_s"]
+                for k in stage:
+                    stage[k] += res[f"{k}_latency_s"]
                 ready += res["ready"]
                 failed += res["failed"]
                 timeouts += res["timeouts"]
@@ -193,7 +196,7 @@ def run(args):
         driver.remove(prev)
         driver.stop()
         per_rank = d.gather_obj({"ready": ready, "failed": failed, "timeouts": timeouts, "lat": lat, "clat": clat,
-                                 "errors": errors[:3]})
+                                 "stage": stage, "errors": errors[:3]})
         if d.rank != 0:
             return None
         rec = _samples(info["controller"] + "/debug/samples/reconcile")
@@ -231,6 +234,9 @@ def run(args):
             "apply_to_ready_p50_ms": ms(_pct(all_lat, 0.50)),
             "apply_to_ready_p99_ms": ms(_pct(all_lat, 0.99)),
             "create_p50_ms": ms(_pct(all_clat, 0.50)),
+            # apply -> first observation of each child (Namespace; ResourceQuota with the sheet's
+            # quota; RoleBinding after the status write)
+            "stage_p50_ms": {k: ms(_pct([x for p in per_rank for x in p["stage"][k]], 0.50)) for k in ("ns", "rq", "rb")},
             "telemetry_poll_p50_ms": ms(_pct(tel, 0.50)),
             "ready_crs": total_ready,
             "failed_crs": total_failed,

@@ -267,10 +267,21 @@ struct WatchSub {
   std::string ns;
   std::vector<Requirement> sel;
   FieldFilter fields;
-  std::deque<std::shared_ptr<const EventRec>> q;
+  // q/closed/overflow are guarded by m (not the store mutex): a watch stream waking up for
+  // an event never contends with writers. Lock order: store mutex -> m.
+  std::mutex m;
   std::condition_variable cv;
+  std::deque<std::shared_ptr<const EventRec>> q;
   bool closed = false;
   bool overflow = false;
+
+  void close() {
+    {
+      std::lock_guard<std::mutex> g(m);
+      closed = true;
+    }
+    cv.notify_one();
+  }
 };
 
 struct FaultRule {
@@ -491,12 +502,11 @@ struct ApiServer::Impl {
       if (!w->ns.empty() && w->ns != ns) continue;
       if (!w->fields.name.empty() && obj->get("metadata").get_string("name") != w->fields.name) continue;
       if (!w->sel.empty() && !selector_matches(w->sel, *obj)) continue;
-      if (w->q.size() > 100000) {
-        w->overflow = true;
-        w->cv.notify_one();
-        continue;
+      {
+        std::lock_guard<std::mutex> g(w->m);
+        if (w->q.size() > 100000) w->overflow = true;
+        else w->q.push_back(rec);
       }
-      w->q.push_back(rec);
       w->cv.notify_one();
     }
   }
@@ -1423,7 +1433,7 @@ struct ApiServer::Impl {
       std::vector<std::shared_ptr<const EventRec>> batch;
       bool closed = false, overflow = false;
       {
-        std::unique_lock<std::mutex> lk(mu);
+        std::unique_lock<std::mutex> lk(sub.m);
         sub.cv.wait_for(lk, std::chrono::milliseconds(500), [&] { return !sub.q.empty() || sub.closed || sub.overflow; });
         batch.assign(sub.q.begin(), sub.q.end());
         sub.q.clear();
@@ -1564,10 +1574,7 @@ struct ApiServer::Impl {
     if (req.path == "/_kl/drop-watches" && req.method == "POST") {
       std::lock_guard<std::mutex> lk(mu);
       size_t n = watches.size();
-      for (WatchSub* ws : watches) {
-        ws->closed = true;
-        ws->cv.notify_one();
-      }
+      for (WatchSub* ws : watches) ws->close();
       w.send_json(200, Value::object({{"dropped", static_cast<unsigned long long>(n)}}).dump());
       return;
     }
@@ -1667,10 +1674,7 @@ void ApiServer::stop() {
   if (impl_ && impl_->server) {
     {
       std::lock_guard<std::mutex> lk(impl_->mu);
-      for (WatchSub* ws : impl_->watches) {
-        ws->closed = true;
-        ws->cv.notify_one();
-      }
+      for (WatchSub* ws : impl_->watches) ws->close();
     }
     impl_->server->stop(std::chrono::milliseconds(2000));
     impl_->server.reset();

@@ -159,6 +159,7 @@ json::Value ChurnDriver::step(const std::vector<std::string>& names, double time
   cv_.wait_until(lk, deadline, all_done);
   int64_t t_end = metrics::now_ns();
   Value lat = Value::array(), clat = Value::array(), errs = Value::array();
+  Value ns_lat = Value::array(), rq_lat = Value::array(), rb_lat = Value::array();
   int ready = 0, failed = 0, timeouts = 0;
   int64_t last_ready = t0;
   for (const auto& n : names) {
@@ -172,6 +173,9 @@ json::Value ChurnDriver::step(const std::vector<std::string>& names, double time
       last_ready = std::max(last_ready, tr);
       lat.push_back(static_cast<double>(tr - t.t_start) * 1e-9);
       clat.push_back(static_cast<double>(t.t_created - t.t_start) * 1e-9);
+      ns_lat.push_back(static_cast<double>(t.t_ns - t.t_start) * 1e-9);
+      rq_lat.push_back(static_cast<double>(t.t_rq - t.t_start) * 1e-9);
+      rb_lat.push_back(static_cast<double>(t.t_rb - t.t_start) * 1e-9);
     } else {
       ++timeouts;
     }
@@ -183,6 +187,9 @@ json::Value ChurnDriver::step(const std::vector<std::string>& names, double time
   out["elapsed_s"] = static_cast<double>((ready == static_cast<int>(names.size()) ? last_ready : t_end) - t0) * 1e-9;
   out["ready_latency_s"] = lat;
   out["create_latency_s"] = clat;
+  out["ns_latency_s"] = ns_lat;  // stage breakdown: Namespace, quota'd ResourceQuota, RoleBinding seen
+  out["rq_latency_s"] = rq_lat;
+  out["rb_latency_s"] = rb_lat;
   out["errors"] = errs;
   return out;
 }

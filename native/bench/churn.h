@@ -45,7 +45,8 @@ class ChurnDriver {
   void start();
   // Creates every name concurrently and waits for all to be Ready (or timeout).
   // Returns {"ready": n, "failed": n, "timeouts": n, "elapsed_s": x,
-  //          "ready_latency_s": [...], "create_latency_s": [...], "errors": [...]}.
+  //          "ready_latency_s": [...], "create_latency_s": [...], "ns_latency_s": [...],
+  //          "rq_latency_s": [...], "rb_latency_s": [...], "errors": [...]}.
   json::Value step(const std::vector<std::string>& names, double timeout_s);
   // Same, while deleting `previous` concurrently (churn: the previous step's tenants
   // leave while the next ones arrive); the step ends when both are done.

@@ -93,6 +93,14 @@ Reconciler::Stats Reconciler::stats() const {
 
 static std::string child_key(const DesiredChild& c) { return c.rt->plural + "/" + c.ns + "/" + c.name; }
 
+bool Reconciler::is_own_write(const kube::ResourceType& rt, const Value& child) const {
+  if (!cfg_.skip_unchanged) return false;
+  std::string key = rt.plural + "/" + kube::meta_namespace(child) + "/" + kube::meta_name(child);
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = last_applied_.find(key);
+  return it != last_applied_.end() && it->second.rv == kube::meta_rv(child);
+}
+
 bool Reconciler::up_to_date(const DesiredChild& c, const std::string& body_hash) {
   if (!cfg_.skip_unchanged) return false;
   kube::Store* store = ctrl_.child_store(c.rt->plural);

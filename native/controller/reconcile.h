@@ -66,6 +66,9 @@ class Reconciler {
   Reconciler(kube::KubeClient& client, kube::Controller& ctrl, Config cfg);
   kube::Action reconcile(const kube::ObjPtr& ub);
   kube::Action error_policy(const kube::ObjPtr& ub, const std::exception& err);
+  // True when `child` is exactly the object our last apply returned (same resourceVersion):
+  // the watch echo of our own write, which needs no reconcile.
+  bool is_own_write(const kube::ResourceType& rt, const json::Value& child) const;
 
   struct Stats {
     uint64_t applied = 0;

@@ -305,6 +305,10 @@ void Controller::run(CancelToken& stop, Reconciler reconcile, ErrorPolicy error_
             for (const auto& k : c->mapper(*o)) queue_.add(k);
           }
         } else {
+          if (ev.type != WatchEvent::Type::Deleted && child_filter_ && !child_filter_(c->rt, *ev.object)) {
+            filtered_.fetch_add(1, std::memory_order_relaxed);
+            return;
+          }
           for (const auto& k : c->mapper(*ev.object)) queue_.add(k);
         }
       });

@@ -135,6 +135,11 @@ class Controller {
   // Watches `child` and enqueues its owners (by default: ownerReferences whose kind
   // and apiVersion match the primary type, mapped by name).
   void owns(const ResourceType& child, Mapper mapper = nullptr);
+  // Child ADDED/MODIFIED events for which `filter` returns false do not enqueue the owner
+  // (e.g. the echo of the reconciler's own apply). DELETED events and relists always do.
+  using ChildFilter = std::function<bool(const ResourceType& child_type, const json::Value& child)>;
+  void set_child_filter(ChildFilter f) { child_filter_ = std::move(f); }
+  uint64_t filtered_events() const { return filtered_.load(); }
   // Extra trigger source (e.g. a periodic external refresh).
   void enqueue(const std::string& key) { queue_.add(key); }
   void enqueue_all();
@@ -156,6 +161,8 @@ class Controller {
   std::unique_ptr<Store> primary_store_;
   std::vector<std::unique_ptr<Child>> children_;
   WorkQueue queue_;
+  ChildFilter child_filter_;
+  std::atomic<uint64_t> filtered_{0};
 };
 
 Controller::Mapper owner_mapper(const ResourceType& owner);
