@@ -124,6 +124,12 @@ def _clear(url, verify=None):
     requests.delete(url, timeout=10, verify=verify)
 
 
+def _kl_lock(info):
+    import requests
+
+    return requests.get(info["server"] + "/_kl/stats", timeout=10, verify=info["apiserver_verify"]).json()["store_lock"]
+
+
 def run(args):
     d = Dist()
     n = args.gpus if args.gpus else d.world
@@ -164,6 +170,7 @@ def run(args):
         lat, clat = [], []
         stage = {"ns": [], "rq": [], "rb": []}
         ready = failed = timeouts = 0
+        lock0 = None
         t_start = None
         errors = []
         for s in range(total_steps):
@@ -175,6 +182,7 @@ def run(args):
                     _clear(info["server"] + "/debug/samples/webhook", verify=info["apiserver_verify"])
                     _clear(info["admission"] + "/debug/samples/admission", verify=info["ca"])
                     _clear(info["node_agent"] + "/debug/samples/telemetry_poll")
+                    lock0 = _kl_lock(info)
                 d.barrier()
                 t_start = time.perf_counter()
             names = _names(d.rank, s, args.batch)
@@ -199,6 +207,7 @@ def run(args):
                                  "stage": stage, "errors": errors[:3]})
         if d.rank != 0:
             return None
+        lock1 = _kl_lock(info)
         rec = _samples(info["controller"] + "/debug/samples/reconcile")
         hook = _samples(info["server"] + "/debug/samples/webhook", verify=info["apiserver_verify"])
         adm = _samples(info["admission"] + "/debug/samples/admission", verify=info["ca"])
@@ -238,6 +247,14 @@ def run(args):
             # quota; RoleBinding after the status write)
             "stage_p50_ms": {k: ms(_pct([x for p in per_rank for x in p["stage"][k]], 0.50)) for k in ("ns", "rq", "rb")},
             "telemetry_poll_p50_ms": ms(_pct(tel, 0.50)),
+            # kube-lite store mutex over the timed region: utilisation near 1.0 means the
+            # in-memory API server (not the controller) bounds throughput
+            "apiserver_store_lock": {
+                "acquisitions": lock1["acquisitions"] - lock0["acquisitions"],
+                "contended": lock1["contended"] - lock0["contended"],
+                "hold_ms": round(lock1["hold_ms"] - lock0["hold_ms"], 3),
+                "wait_ms": round(lock1["wait_ms"] - lock0["wait_ms"], 3),
+                "utilisation": round((lock1["hold_ms"] - lock0["hold_ms"]) / (elapsed * 1e3), 4)},
             "ready_crs": total_ready,
             "failed_crs": total_failed,
             "reference_structural": {"apply_to_ready_p50_s": 30.0, "apply_to_ready_p99_s": 59.4,

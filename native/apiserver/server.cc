@@ -284,6 +284,94 @@ struct WatchSub {
   }
 };
 
+// Store lock: a writer-preferring reader/writer lock (glibc's default rwlock prefers
+// readers, which starves commits under a steady GET/LIST load). Reads (path parsing, GET,
+// LIST, the optimistic pre-read of a write) share it; commits are exclusive.
+class RwLock {
+ public:
+  RwLock() {
+    pthread_rwlockattr_t a;
+    pthread_rwlockattr_init(&a);
+    const char* kind = std::getenv("BGC_KL_RWLOCK");  // "reader" switches to reader preference
+    pthread_rwlockattr_setkind_np(&a, kind && std::string(kind) == "reader" ? PTHREAD_RWLOCK_PREFER_READER_NP
+                                                                           : PTHREAD_RWLOCK_PREFER_WRITER_NONRECURSIVE_NP);
+    pthread_rwlock_init(&l_, &a);
+    pthread_rwlockattr_destroy(&a);
+  }
+  ~RwLock() { pthread_rwlock_destroy(&l_); }
+  RwLock(const RwLock&) = delete;
+  RwLock& operator=(const RwLock&) = delete;
+  void lock() { pthread_rwlock_wrlock(&l_); }
+  bool try_lock() { return pthread_rwlock_trywrlock(&l_) == 0; }
+  void unlock() { pthread_rwlock_unlock(&l_); }
+  void lock_shared() { pthread_rwlock_rdlock(&l_); }
+  bool try_lock_shared() { return pthread_rwlock_tryrdlock(&l_) == 0; }
+  void unlock_shared() { pthread_rwlock_unlock(&l_); }
+
+ private:
+  pthread_rwlock_t l_;
+};
+
+// Watch wake-ups are deferred until the exclusive store lock is released (a futex wake per
+// subscriber inside the critical section would stretch every commit).
+thread_local std::vector<std::shared_ptr<WatchSub>> t_pending_wakeups;
+
+inline void flush_watch_wakeups() {
+  for (auto& w : t_pending_wakeups) w->cv.notify_one();
+  t_pending_wakeups.clear();
+}
+
+// Store-lock accounting (exported in /_kl/stats): exclusive hold time bounds kube-lite's
+// commit throughput (commits/s <= 1 / mean exclusive hold).
+struct LockStats {
+  std::atomic<uint64_t> acquisitions{0}, shared{0}, contended{0}, wait_ns{0}, hold_ns{0};
+};
+
+class StoreLock {  // exclusive
+ public:
+  StoreLock(RwLock& m, LockStats& st) : m_(m), st_(st) {
+    if (!m_.try_lock()) {
+      int64_t t0 = metrics::now_ns();
+      m_.lock();
+      st_.contended.fetch_add(1, std::memory_order_relaxed);
+      st_.wait_ns.fetch_add(static_cast<uint64_t>(metrics::now_ns() - t0), std::memory_order_relaxed);
+    }
+    t_acq_ = metrics::now_ns();
+  }
+  ~StoreLock() {
+    st_.acquisitions.fetch_add(1, std::memory_order_relaxed);
+    st_.hold_ns.fetch_add(static_cast<uint64_t>(metrics::now_ns() - t_acq_), std::memory_order_relaxed);
+    m_.unlock();
+    flush_watch_wakeups();
+  }
+  StoreLock(const StoreLock&) = delete;
+  StoreLock& operator=(const StoreLock&) = delete;
+
+ private:
+  RwLock& m_;
+  LockStats& st_;
+  int64_t t_acq_ = 0;
+};
+
+class SharedStoreLock {
+ public:
+  SharedStoreLock(RwLock& m, LockStats& st) : m_(m) {
+    if (!m_.try_lock_shared()) {
+      int64_t t0 = metrics::now_ns();
+      m_.lock_shared();
+      st.contended.fetch_add(1, std::memory_order_relaxed);
+      st.wait_ns.fetch_add(static_cast<uint64_t>(metrics::now_ns() - t0), std::memory_order_relaxed);
+    }
+    st.shared.fetch_add(1, std::memory_order_relaxed);
+  }
+  ~SharedStoreLock() { m_.unlock_shared(); }
+  SharedStoreLock(const SharedStoreLock&) = delete;
+  SharedStoreLock& operator=(const SharedStoreLock&) = delete;
+
+ private:
+  RwLock& m_;
+};
+
 struct FaultRule {
   std::string method;  // empty = any
   std::regex path;
@@ -318,7 +406,8 @@ struct ApiServer::Impl {
   Options opts;
   std::unique_ptr<http::Server> server;
 
-  std::mutex mu;
+  RwLock mu;                // store lock (see RwLock)
+  std::mutex watches_mu;    // guards `watches`; lock order: mu -> watches_mu -> WatchSub::m
   std::map<std::string, TypeInfo> types;  // key() -> info
   std::unordered_map<std::string, std::unordered_map<std::string, Stored>> data;  // type key -> obj key -> stored
   std::unordered_map<std::string, std::pair<std::string, std::string>> by_uid;      // uid -> (type key, obj key)
@@ -333,7 +422,7 @@ struct ApiServer::Impl {
   uint64_t rv = 1000;
   std::deque<std::shared_ptr<const EventRec>> history;
   uint64_t compacted_rv = 0;  // watches from rv < compacted_rv get 410
-  std::set<WatchSub*> watches;
+  std::set<std::shared_ptr<WatchSub>> watches;
 
   std::unordered_map<std::string, UserInfo> tokens;
 
@@ -345,12 +434,14 @@ struct ApiServer::Impl {
 
   std::atomic<uint64_t> requests{0};
   std::atomic<uint64_t> faults_hit{0};
+  LockStats lock_stats;
 
   explicit Impl(Options o) : opts(std::move(o)) {
     for (const ResourceType* rt : kube::types::builtin()) {
       TypeInfo ti;
       ti.rt = *rt;
       types[ti.key()] = ti;
+      data[ti.key()];  // buckets exist before any shared-lock reader looks them up
     }
     if (!opts.token_file.empty()) load_tokens(opts.token_file);
   }
@@ -459,7 +550,7 @@ struct ApiServer::Impl {
     }
     rest.assign(segs.begin() + static_cast<long>(i), segs.end());
     if (rest.empty()) return false;
-    std::lock_guard<std::mutex> lk(mu);
+    SharedStoreLock lk(mu, lock_stats);
     if (rest[0] == "namespaces" && rest.size() >= 3) {
       TypeInfo* ti = find_type(group, version, rest[2]);
       if (ti && ti->rt.namespaced) {
@@ -482,22 +573,26 @@ struct ApiServer::Impl {
 
   // ---------------------------------------------------------------- events
   void emit_locked(const std::string& type, const TypeInfo& ti, const std::string& ns,
-                   const std::shared_ptr<const Value>& obj, uint64_t ev_rv) {
+                   const std::shared_ptr<const Value>& obj, uint64_t ev_rv, std::string preline = {}) {
     auto rec = std::make_shared<EventRec>();
     rec->rv = ev_rv;
     rec->type_key = ti.key();
     rec->ns = ns;
     rec->obj = obj;
-    std::string line = "{\"type\":\"" + type + "\",\"object\":";
-    obj->dump_to(line);
-    line += "}\n";
+    std::string line = std::move(preline);
+    if (line.empty()) {
+      line = "{\"type\":\"" + type + "\",\"object\":";
+      obj->dump_to(line);
+      line += "}\n";
+    }
     rec->line = std::make_shared<const std::string>(std::move(line));
     history.push_back(rec);
     while (history.size() > opts.history_limit) {
       compacted_rv = history.front()->rv;
       history.pop_front();
     }
-    for (WatchSub* w : watches) {
+    std::lock_guard<std::mutex> wg(watches_mu);
+    for (const auto& w : watches) {
       if (w->type_key != rec->type_key) continue;
       if (!w->ns.empty() && w->ns != ns) continue;
       if (!w->fields.name.empty() && obj->get("metadata").get_string("name") != w->fields.name) continue;
@@ -507,7 +602,7 @@ struct ApiServer::Impl {
         if (w->q.size() > 100000) w->overflow = true;
         else w->q.push_back(rec);
       }
-      w->cv.notify_one();
+      t_pending_wakeups.push_back(w);
     }
   }
 
@@ -519,7 +614,7 @@ struct ApiServer::Impl {
 
   std::vector<HookMatch> matching_webhooks(const TypeInfo& ti, const std::string& sub, const std::string& op) {
     std::vector<HookMatch> out;
-    std::lock_guard<std::mutex> lk(mu);
+    SharedStoreLock lk(mu, lock_stats);
     auto it = data.find(kube::types::MutatingWebhookConfiguration.group + "/v1/mutatingwebhookconfigurations");
     if (it == data.end()) return out;
     std::string res = ti.rt.plural + (sub.empty() ? "" : "/" + sub);
@@ -739,14 +834,23 @@ struct ApiServer::Impl {
       ti.schema = v.get("schema").get("openAPIV3Schema");
       ti.custom = true;
       types[ti.key()] = ti;
+      data[ti.key()];  // created under the exclusive lock (see bucket())
     }
   }
 
   // ---------------------------------------------------------------- storage helpers
-  std::unordered_map<std::string, Stored>& bucket(const TypeInfo& ti) { return data[ti.key()]; }
+  // Find-only: every registered type's bucket is created at registration, so lookups under
+  // the shared lock never insert into `data`.
+  std::unordered_map<std::string, Stored>& bucket(const TypeInfo& ti) {
+    auto it = data.find(ti.key());
+    if (it == data.end()) throw StatusError(500, "InternalError", "no storage for " + ti.key());
+    return it->second;
+  }
 
   bool namespace_exists_locked(const std::string& ns) {
-    auto& b = data[kube::types::Namespace.group + "/v1/namespaces"];
+    auto bit = data.find(kube::types::Namespace.group + "/v1/namespaces");
+    if (bit == data.end()) return false;
+    auto& b = bit->second;
     auto it = b.find(ns);
     return it != b.end() && !it->second.obj->get("metadata").contains("deletionTimestamp");
   }
@@ -846,13 +950,51 @@ struct ApiServer::Impl {
     }
   }
 
+  // Work moved out of the exclusive section: managedFields are rendered and the watch event
+  // is serialized around a resourceVersion placeholder; commit_locked splices in the digits.
+  struct PreparedEvent {
+    std::string head, tail;  // event line = head + rv digits + tail
+    bool ok = false;
+  };
+  static const std::string& rv_placeholder() {
+    static const std::string p = "\x01rv\x01";
+    return p;
+  }
+  static PreparedEvent prepare_commit(Value& obj, const Managers& managers, const std::string& api_version,
+                                      const char* type) {
+    obj["metadata"]["resourceVersion"] = rv_placeholder();
+    render_managed(obj, managers, api_version);
+    std::string line = std::string("{\"type\":\"") + type + "\",\"object\":";
+    obj.dump_to(line);
+    line += "}\n";
+    static const std::string needle = "\"resourceVersion\":" + Value(rv_placeholder()).dump();
+    PreparedEvent pe;
+    size_t pos = line.find(needle);
+    if (pos == std::string::npos) return pe;
+    pe.head.assign(line, 0, pos);
+    pe.head += "\"resourceVersion\":\"";
+    pe.tail.assign(line, pos + needle.size() - 1, std::string::npos);  // from the closing quote
+    pe.ok = true;
+    return pe;
+  }
+
   // Commits `obj` (already validated) under the lock. Returns stored object.
   std::shared_ptr<const Value> commit_locked(const TypeInfo& ti, const std::string& ns, const std::string& name,
-                                            Value obj, Managers managers, const Stored* prev) {
+                                            Value obj, Managers managers, const Stored* prev,
+                                            const PreparedEvent* pe = nullptr) {
     uint64_t new_rv = ++rv;
+    std::string digits = std::to_string(new_rv);
     Value& meta = obj["metadata"];
-    meta["resourceVersion"] = std::to_string(new_rv);
-    render_managed(obj, managers, ti.rt.api_version());
+    meta["resourceVersion"] = digits;
+    std::string preline;
+    if (pe && pe->ok) {
+      preline.reserve(pe->head.size() + digits.size() + pe->tail.size());
+      preline += pe->head;
+      preline += digits;
+      preline += pe->tail;
+    } else {
+      render_managed(obj, managers, ti.rt.api_version());
+    }
     auto ptr = std::make_shared<const Value>(std::move(obj));
     auto& b = bucket(ti);
     Stored s;
@@ -866,7 +1008,7 @@ struct ApiServer::Impl {
     by_uid[ptr->get("metadata").get_string("uid")] = ref;
     for (const auto& r : ptr->get("metadata").get("ownerReferences").items()) by_owner[r.get_string("uid")].insert(ref);
     if (ti.rt.namespaced) by_namespace[ns].insert(ref);
-    emit_locked(prev ? "MODIFIED" : "ADDED", ti, ns, ptr, new_rv);
+    emit_locked(prev ? "MODIFIED" : "ADDED", ti, ns, ptr, new_rv, std::move(preline));
     return ptr;
   }
 
@@ -968,7 +1110,7 @@ struct ApiServer::Impl {
       Stored cur_copy;
       bool exists = false;
       {
-        std::lock_guard<std::mutex> lk(mu);
+        SharedStoreLock lk(mu, lock_stats);
         auto& b = bucket(ti);
         auto it = b.find(obj_key(ti.rt, ns, name));
         if (it != b.end()) {
@@ -980,7 +1122,7 @@ struct ApiServer::Impl {
       auto [obj, managers] = compute(exists ? &cur_copy : nullptr);
       std::string op = exists ? "UPDATE" : "CREATE";
       if (!exists && ti.rt.namespaced) {
-        std::lock_guard<std::mutex> lk(mu);
+        SharedStoreLock lk(mu, lock_stats);
         if (!namespace_exists_locked(ns)) {
           throw StatusError(404, "NotFound", "namespaces \"" + ns + "\" not found",
                             Value::object({{"name", ns}, {"kind", "namespaces"}}));
@@ -996,22 +1138,23 @@ struct ApiServer::Impl {
       if (ti.rt.namespaced) obj["metadata"]["namespace"] = ns;
       else obj["metadata"].erase("namespace");
       validate_object(ti, name, ns, obj);
-      std::lock_guard<std::mutex> lk(mu);
+      // everything below up to the lock depends only on cur_copy, which the commit re-checks
+      if (exists && same_content(obj, *cur_copy.obj) && managers == cur_copy.managers) {
+        return {cur_copy.obj, 200};  // mutation turned it into a no-op
+      }
+      if (exists && spec_changed(*cur_copy.obj, obj)) {
+        int64_t gen = cur_copy.obj->get("metadata").get("generation").is_int()
+                          ? cur_copy.obj->get("metadata").get("generation").as_int()
+                          : 1;
+        obj["metadata"]["generation"] = gen + 1;
+      }
+      PreparedEvent pe = prepare_commit(obj, managers, ti.rt.api_version(), exists ? "MODIFIED" : "ADDED");
+      StoreLock lk(mu, lock_stats);
       auto& b = bucket(ti);
       auto it = b.find(obj_key(ti.rt, ns, name));
       bool now_exists = it != b.end();
       if (now_exists != exists || (exists && it->second.rv != cur_copy.rv)) continue;  // raced: retry
       if (exists) {
-        // non-apply writers: attribute changed fields after mutation
-        if (exists && same_content(obj, *cur_copy.obj) && managers == cur_copy.managers) {
-          return {cur_copy.obj, 200};
-        }
-        if (spec_changed(*cur_copy.obj, obj)) {
-          int64_t gen = cur_copy.obj->get("metadata").get("generation").is_int()
-                            ? cur_copy.obj->get("metadata").get("generation").as_int()
-                            : 1;
-          obj["metadata"]["generation"] = gen + 1;
-        }
         // finalizer-gated deletion completes when the last finalizer is removed
         if (obj.get("metadata").contains("deletionTimestamp") && obj.get("metadata").get("finalizers").empty()) {
           std::vector<std::string> dead;
@@ -1020,10 +1163,10 @@ struct ApiServer::Impl {
           return {cur_copy.obj, 200};
         }
         (void)is_status;
-        return {commit_locked(ti, ns, name, std::move(obj), std::move(managers), &it->second), 200};
+        return {commit_locked(ti, ns, name, std::move(obj), std::move(managers), &it->second, &pe), 200};
       }
       if (ti.rt.plural == "customresourcedefinitions") register_crd_locked(obj);
-      auto created = commit_locked(ti, ns, name, std::move(obj), std::move(managers), nullptr);
+      auto created = commit_locked(ti, ns, name, std::move(obj), std::move(managers), nullptr, &pe);
       // The garbage collector also removes dependents created with only dangling owner
       // references (e.g. a controller re-applying a child right after its owner was
       // deleted, before the owner's DELETED event reached it).
@@ -1289,14 +1432,14 @@ struct ApiServer::Impl {
   void do_delete(ParsedPath& p, const http::Request& req, const UserInfo& user, http::ResponseWriter& w) {
     std::shared_ptr<const Value> cur;
     {
-      std::lock_guard<std::mutex> lk(mu);
+      SharedStoreLock lk(mu, lock_stats);
       auto& b = bucket(*p.ti);
       auto it = b.find(obj_key(p.ti->rt, p.ns, p.name));
       if (it == b.end()) throw not_found(p.ti->rt, p.name);
       cur = it->second.obj;
     }
     call_webhooks(*p.ti, "", "DELETE", p.ns, p.name, nullptr, cur.get(), user);
-    std::lock_guard<std::mutex> lk(mu);
+    StoreLock lk(mu, lock_stats);
     auto& b = bucket(*p.ti);
     auto it = b.find(obj_key(p.ti->rt, p.ns, p.name));
     if (it == b.end()) throw not_found(p.ti->rt, p.name);
@@ -1324,7 +1467,7 @@ struct ApiServer::Impl {
   void do_get(ParsedPath& p, http::ResponseWriter& w) {
     std::shared_ptr<const Value> obj;
     {
-      std::lock_guard<std::mutex> lk(mu);
+      SharedStoreLock lk(mu, lock_stats);
       auto& b = bucket(*p.ti);
       auto it = b.find(obj_key(p.ti->rt, p.ns, p.name));
       if (it == b.end()) throw not_found(p.ti->rt, p.name);
@@ -1339,7 +1482,7 @@ struct ApiServer::Impl {
     std::vector<std::shared_ptr<const Value>> items;
     uint64_t list_rv;
     {
-      std::lock_guard<std::mutex> lk(mu);
+      SharedStoreLock lk(mu, lock_stats);
       list_rv = rv;
       for (auto& [k, st] : bucket(*p.ti)) {
         const Value& meta = st.obj->get("metadata");
@@ -1368,7 +1511,8 @@ struct ApiServer::Impl {
   }
 
   void do_watch(ParsedPath& p, const http::Request& req, http::ResponseWriter& w) {
-    WatchSub sub;
+    auto subp = std::make_shared<WatchSub>();  // shared: a committer may still hold it for a wake-up
+    WatchSub& sub = *subp;
     sub.type_key = p.ti->key();
     sub.ns = p.ns;
     sub.sel = parse_selector(req.query_param("labelSelector"));
@@ -1381,7 +1525,7 @@ struct ApiServer::Impl {
     std::vector<std::shared_ptr<const std::string>> initial;
     bool gone = false;
     {
-      std::lock_guard<std::mutex> lk(mu);
+      SharedStoreLock lk(mu, lock_stats);
       uint64_t from = rv_s.empty() ? 0 : std::strtoull(rv_s.c_str(), nullptr, 10);
       if (rv_s.empty() || rv_s == "0") {
         for (auto& [k, st] : bucket(*p.ti)) {
@@ -1408,11 +1552,14 @@ struct ApiServer::Impl {
           initial.push_back(e->line);
         }
       }
-      if (!gone) watches.insert(&sub);
+      if (!gone) {
+        std::lock_guard<std::mutex> wg(watches_mu);
+        watches.insert(subp);
+      }
     }
     if (!w.start_chunked(200, "application/json")) {
-      std::lock_guard<std::mutex> lk(mu);
-      watches.erase(&sub);
+      std::lock_guard<std::mutex> wg(watches_mu);
+      watches.erase(subp);
       return;
     }
     if (gone) {
@@ -1451,7 +1598,7 @@ struct ApiServer::Impl {
       if (bookmarks && now >= next_bookmark) {
         uint64_t cur_rv;
         {
-          std::lock_guard<std::mutex> lk(mu);
+          SharedStoreLock lk(mu, lock_stats);
           cur_rv = rv;
         }
         Value bm = Value::object({{"type", "BOOKMARK"},
@@ -1464,15 +1611,15 @@ struct ApiServer::Impl {
       if (batch.empty() && w.peer_closed()) break;
     }
     {
-      std::lock_guard<std::mutex> lk(mu);
-      watches.erase(&sub);
+      std::lock_guard<std::mutex> wg(watches_mu);
+      watches.erase(subp);
     }
     w.end_chunked();
   }
 
   // ---------------------------------------------------------------- discovery
   void discovery(const std::string& path, http::ResponseWriter& w) {
-    std::lock_guard<std::mutex> lk(mu);
+    SharedStoreLock lk(mu, lock_stats);
     if (path == "/api") {
       w.send_json(200, Value::object({{"kind", "APIVersions"}, {"versions", Value::array({"v1"})}}).dump());
       return;
@@ -1565,21 +1712,21 @@ struct ApiServer::Impl {
       return;
     }
     if (req.path == "/_kl/compact" && req.method == "POST") {
-      std::lock_guard<std::mutex> lk(mu);
+      StoreLock lk(mu, lock_stats);
       compacted_rv = rv;
       history.clear();
       w.send_json(200, Value::object({{"compacted_rv", static_cast<unsigned long long>(compacted_rv)}}).dump());
       return;
     }
     if (req.path == "/_kl/drop-watches" && req.method == "POST") {
-      std::lock_guard<std::mutex> lk(mu);
+      std::lock_guard<std::mutex> wg(watches_mu);
       size_t n = watches.size();
-      for (WatchSub* ws : watches) ws->close();
+      for (const auto& ws : watches) ws->close();
       w.send_json(200, Value::object({{"dropped", static_cast<unsigned long long>(n)}}).dump());
       return;
     }
     if (req.path == "/_kl/stats") {
-      std::lock_guard<std::mutex> lk(mu);
+      SharedStoreLock lk(mu, lock_stats);
       Value counts = Value::object();
       size_t total = 0;
       for (auto& [k, b] : data) {
@@ -1591,6 +1738,11 @@ struct ApiServer::Impl {
                                       {"watches", static_cast<unsigned long long>(watches.size())},
                                       {"requests", static_cast<unsigned long long>(requests.load())},
                                       {"faults_hit", static_cast<unsigned long long>(faults_hit.load())},
+                                      {"store_lock", Value::object({
+                                          {"acquisitions", static_cast<unsigned long long>(lock_stats.acquisitions.load())},
+                                          {"contended", static_cast<unsigned long long>(lock_stats.contended.load())},
+                                          {"wait_ms", static_cast<double>(lock_stats.wait_ns.load()) * 1e-6},
+                                          {"hold_ms", static_cast<double>(lock_stats.hold_ns.load()) * 1e-6}})},
                                       {"by_type", counts}}).dump());
       return;
     }
@@ -1673,8 +1825,8 @@ uint16_t ApiServer::port() const { return impl_->server ? impl_->server->port() 
 void ApiServer::stop() {
   if (impl_ && impl_->server) {
     {
-      std::lock_guard<std::mutex> lk(impl_->mu);
-      for (WatchSub* ws : impl_->watches) ws->close();
+      std::lock_guard<std::mutex> wg(impl_->watches_mu);
+      for (const auto& ws : impl_->watches) ws->close();
     }
     impl_->server->stop(std::chrono::milliseconds(2000));
     impl_->server.reset();

@@ -12,6 +12,7 @@ from bacchus_gpu_controller_amd.testing.cluster import Cluster
 pytestmark = pytest.mark.slow
 
 
+@pytest.mark.skipif(bool(os.environ.get("BGC_BIN_DIR")), reason="sanitizer builds own signal delivery")
 def test_cpu_profile_of_kube_lite(tmp_path, monkeypatch):
     monkeypatch.setenv("BGC_CPU_PROFILE", str(tmp_path / "kl.%p.prof"))
     with Cluster(admission=False, controller=False) as c:
