@@ -1733,9 +1733,14 @@ struct ApiServer::Impl {
         counts[k] = static_cast<unsigned long long>(b.size());
         total += b.size();
       }
+      size_t n_watches;
+      {
+        std::lock_guard<std::mutex> wg(watches_mu);
+        n_watches = watches.size();
+      }
       w.send_json(200, Value::object({{"resourceVersion", static_cast<unsigned long long>(rv)},
                                       {"objects", static_cast<unsigned long long>(total)},
-                                      {"watches", static_cast<unsigned long long>(watches.size())},
+                                      {"watches", static_cast<unsigned long long>(n_watches)},
                                       {"requests", static_cast<unsigned long long>(requests.load())},
                                       {"faults_hit", static_cast<unsigned long long>(faults_hit.load())},
                                       {"store_lock", Value::object({
