@@ -229,10 +229,13 @@ struct UserInfo {
   }
 };
 
+struct TypeStore;
+
 struct TypeInfo {
   ResourceType rt;
-  Value schema;  // openAPIV3Schema for CRDs (null for built-ins)
+  std::shared_ptr<const Value> schema;  // openAPIV3Schema for CRDs (null for built-ins); atomic swap on CRD update
   bool custom = false;
+  std::shared_ptr<TypeStore> store;     // set at registration, never replaced
   std::string key() const { return rt.group + "/" + rt.version + "/" + rt.plural; }
 };
 
@@ -372,6 +375,19 @@ class SharedStoreLock {
   RwLock& m_;
 };
 
+// Per-resource-type storage shard (like the apiserver's per-resource storage and watch
+// cache): its own lock, objects, event history and watchers, so commits to different
+// types never serialize on each other.
+struct TypeStore {
+  RwLock mu;
+  LockStats stats;
+  std::unordered_map<std::string, Stored> objs;              // obj key -> stored (guarded by mu)
+  std::deque<std::shared_ptr<const EventRec>> history;       // rv-ordered (appended under exclusive mu)
+  uint64_t compacted_rv = 0;                                 // resumes from rv < compacted_rv get 410
+  std::mutex watches_mu;                                     // lock order: mu -> watches_mu -> WatchSub::m
+  std::set<std::shared_ptr<WatchSub>> watches;
+};
+
 struct FaultRule {
   std::string method;  // empty = any
   std::regex path;
@@ -406,10 +422,12 @@ struct ApiServer::Impl {
   Options opts;
   std::unique_ptr<http::Server> server;
 
-  RwLock mu;                // store lock (see RwLock)
-  std::mutex watches_mu;    // guards `watches`; lock order: mu -> watches_mu -> WatchSub::m
-  std::map<std::string, TypeInfo> types;  // key() -> info
-  std::unordered_map<std::string, std::unordered_map<std::string, Stored>> data;  // type key -> obj key -> stored
+  // Lock order: one TypeStore::mu at a time -> types_mu / index_mu -> TypeStore::watches_mu
+  // -> WatchSub::m. Nothing that holds types_mu or index_mu acquires a TypeStore lock.
+  RwLock types_mu;                        // guards `types` (CRD registration is the only writer)
+  std::map<std::string, TypeInfo> types;  // key() -> info; nodes are never erased (stable pointers)
+  std::atomic<uint64_t> rv{1000};         // global resourceVersion; fetched under the owning type's exclusive lock
+  std::mutex index_mu;                    // guards the three indexes below
   std::unordered_map<std::string, std::pair<std::string, std::string>> by_uid;      // uid -> (type key, obj key)
   // Secondary indexes so garbage collection and namespace cascades touch only the
   // affected objects (O(dependents), not O(all objects)).
@@ -419,10 +437,19 @@ struct ApiServer::Impl {
   };
   std::unordered_map<std::string, std::unordered_set<Ref, RefHash>> by_owner;      // owner uid -> dependents
   std::unordered_map<std::string, std::unordered_set<Ref, RefHash>> by_namespace;  // namespace -> objects
-  uint64_t rv = 1000;
-  std::deque<std::shared_ptr<const EventRec>> history;
-  uint64_t compacted_rv = 0;  // watches from rv < compacted_rv get 410
-  std::set<std::shared_ptr<WatchSub>> watches;
+
+  // Background garbage collector (the apiserver's GC controller does cascading deletion
+  // asynchronously too): deletions enqueue owner uids / namespace names.
+  struct GcItem {
+    bool is_namespace = false;
+    std::string id;  // owner uid or namespace name
+  };
+  std::mutex gc_mu;
+  std::condition_variable gc_cv;
+  std::deque<GcItem> gc_queue;
+  bool gc_stop = false;
+  std::atomic<uint64_t> gc_collected{0};
+  std::thread gc_thread;
 
   std::unordered_map<std::string, UserInfo> tokens;
 
@@ -434,16 +461,42 @@ struct ApiServer::Impl {
 
   std::atomic<uint64_t> requests{0};
   std::atomic<uint64_t> faults_hit{0};
-  LockStats lock_stats;
+  LockStats types_stats;  // types_mu accounting
 
   explicit Impl(Options o) : opts(std::move(o)) {
     for (const ResourceType* rt : kube::types::builtin()) {
       TypeInfo ti;
       ti.rt = *rt;
+      ti.store = std::make_shared<TypeStore>();
       types[ti.key()] = ti;
-      data[ti.key()];  // buckets exist before any shared-lock reader looks them up
     }
     if (!opts.token_file.empty()) load_tokens(opts.token_file);
+    gc_thread = std::thread([this] { gc_loop(); });
+  }
+
+  ~Impl() {
+    {
+      std::lock_guard<std::mutex> g(gc_mu);
+      gc_stop = true;
+    }
+    gc_cv.notify_all();
+    if (gc_thread.joinable()) gc_thread.join();
+  }
+
+  template <typename F>
+  void for_each_store(F f) {
+    std::vector<std::pair<std::string, std::shared_ptr<TypeStore>>> stores;
+    {
+      SharedStoreLock lk(types_mu, types_stats);
+      for (auto& [k, ti] : types) stores.emplace_back(k, ti.store);
+    }
+    for (auto& [k, st] : stores) f(k, *st);
+  }
+
+  TypeInfo* type_by_key(const std::string& key) {
+    SharedStoreLock lk(types_mu, types_stats);
+    auto it = types.find(key);
+    return it == types.end() ? nullptr : &it->second;
   }
 
   void load_tokens(const std::string& path) {
@@ -550,7 +603,7 @@ struct ApiServer::Impl {
     }
     rest.assign(segs.begin() + static_cast<long>(i), segs.end());
     if (rest.empty()) return false;
-    SharedStoreLock lk(mu, lock_stats);
+    SharedStoreLock lk(types_mu, types_stats);
     if (rest[0] == "namespaces" && rest.size() >= 3) {
       TypeInfo* ti = find_type(group, version, rest[2]);
       if (ti && ti->rt.namespaced) {
@@ -572,8 +625,10 @@ struct ApiServer::Impl {
   }
 
   // ---------------------------------------------------------------- events
+  // Caller holds ti.store->mu exclusively.
   void emit_locked(const std::string& type, const TypeInfo& ti, const std::string& ns,
                    const std::shared_ptr<const Value>& obj, uint64_t ev_rv, std::string preline = {}) {
+    TypeStore& st = *ti.store;
     auto rec = std::make_shared<EventRec>();
     rec->rv = ev_rv;
     rec->type_key = ti.key();
@@ -586,14 +641,13 @@ struct ApiServer::Impl {
       line += "}\n";
     }
     rec->line = std::make_shared<const std::string>(std::move(line));
-    history.push_back(rec);
-    while (history.size() > opts.history_limit) {
-      compacted_rv = history.front()->rv;
-      history.pop_front();
+    st.history.push_back(rec);
+    while (st.history.size() > opts.history_limit) {
+      st.compacted_rv = st.history.front()->rv;
+      st.history.pop_front();
     }
-    std::lock_guard<std::mutex> wg(watches_mu);
-    for (const auto& w : watches) {
-      if (w->type_key != rec->type_key) continue;
+    std::lock_guard<std::mutex> wg(st.watches_mu);
+    for (const auto& w : st.watches) {
       if (!w->ns.empty() && w->ns != ns) continue;
       if (!w->fields.name.empty() && obj->get("metadata").get_string("name") != w->fields.name) continue;
       if (!w->sel.empty() && !selector_matches(w->sel, *obj)) continue;
@@ -614,11 +668,11 @@ struct ApiServer::Impl {
 
   std::vector<HookMatch> matching_webhooks(const TypeInfo& ti, const std::string& sub, const std::string& op) {
     std::vector<HookMatch> out;
-    SharedStoreLock lk(mu, lock_stats);
-    auto it = data.find(kube::types::MutatingWebhookConfiguration.group + "/v1/mutatingwebhookconfigurations");
-    if (it == data.end()) return out;
+    TypeInfo* mwc = type_by_key(kube::types::MutatingWebhookConfiguration.group + "/v1/mutatingwebhookconfigurations");
+    if (!mwc) return out;
+    SharedStoreLock lk(mwc->store->mu, mwc->store->stats);
     std::string res = ti.rt.plural + (sub.empty() ? "" : "/" + sub);
-    for (auto& kv : it->second) {
+    for (auto& kv : mwc->store->objs) {
       for (const auto& hook : kv.second.obj->get("webhooks").items()) {
         for (const auto& rule : hook.get("rules").items()) {
           auto contains = [](const Value& arr, const std::string& v) {
@@ -801,8 +855,9 @@ struct ApiServer::Impl {
     if (ti.rt.plural == "rolebindings" || ti.rt.plural == "clusterrolebindings") {
       if (!obj.get("roleRef").is_object()) throw invalid(ti.rt, name, "roleRef: Required value");
     }
-    if (opts.validate_schema && ti.custom && ti.schema.is_object()) {
-      auto errs = crd::validate(obj, ti.schema);
+    std::shared_ptr<const Value> schema = std::atomic_load(&ti.schema);
+    if (opts.validate_schema && ti.custom && schema && schema->is_object()) {
+      auto errs = crd::validate(obj, *schema);
       if (!errs.empty()) {
         std::string msg;
         for (size_t i = 0; i < errs.size() && i < 5; ++i) {
@@ -817,11 +872,13 @@ struct ApiServer::Impl {
   }
 
   // ---------------------------------------------------------------- CRDs
-  void register_crd_locked(const Value& crd) {
+  // Called while holding the CRD type's exclusive lock; takes types_mu (lock order above).
+  void register_crd(const Value& crd) {
     const Value& spec = crd.get("spec");
     std::string group = spec.get_string("group");
     const Value& names = spec.get("names");
     bool namespaced = spec.get_string("scope") == "Namespaced";
+    StoreLock lk(types_mu, types_stats);
     for (const auto& v : spec.get("versions").items()) {
       if (v.get("served").is_bool() && !v.get("served").as_bool()) continue;
       TypeInfo ti;
@@ -831,28 +888,28 @@ struct ApiServer::Impl {
       ti.rt.plural = names.get_string("plural");
       ti.rt.namespaced = namespaced;
       ti.rt.has_status = v.get("subresources").get("status").is_object();
-      ti.schema = v.get("schema").get("openAPIV3Schema");
+      auto schema = std::make_shared<const Value>(v.get("schema").get("openAPIV3Schema"));
       ti.custom = true;
+      auto it = types.find(ti.key());
+      if (it != types.end()) {
+        std::atomic_store(&it->second.schema, schema);  // CRD update: keep the storage, swap the schema
+        continue;
+      }
+      ti.schema = schema;
+      ti.store = std::make_shared<TypeStore>();
       types[ti.key()] = ti;
-      data[ti.key()];  // created under the exclusive lock (see bucket())
     }
   }
 
   // ---------------------------------------------------------------- storage helpers
-  // Find-only: every registered type's bucket is created at registration, so lookups under
-  // the shared lock never insert into `data`.
-  std::unordered_map<std::string, Stored>& bucket(const TypeInfo& ti) {
-    auto it = data.find(ti.key());
-    if (it == data.end()) throw StatusError(500, "InternalError", "no storage for " + ti.key());
-    return it->second;
-  }
+  static std::unordered_map<std::string, Stored>& bucket(const TypeInfo& ti) { return ti.store->objs; }
 
-  bool namespace_exists_locked(const std::string& ns) {
-    auto bit = data.find(kube::types::Namespace.group + "/v1/namespaces");
-    if (bit == data.end()) return false;
-    auto& b = bit->second;
-    auto it = b.find(ns);
-    return it != b.end() && !it->second.obj->get("metadata").contains("deletionTimestamp");
+  bool namespace_exists(const std::string& ns) {
+    TypeInfo* nti = type_by_key(kube::types::Namespace.group + "/v1/namespaces");
+    if (!nti) return false;
+    SharedStoreLock lk(nti->store->mu, nti->store->stats);
+    auto it = nti->store->objs.find(ns);
+    return it != nti->store->objs.end() && !it->second.obj->get("metadata").contains("deletionTimestamp");
   }
 
   static void render_managed(Value& obj, const Managers& m, const std::string& api_version) {
@@ -978,10 +1035,11 @@ struct ApiServer::Impl {
     return pe;
   }
 
-  // Commits `obj` (already validated) under the lock. Returns stored object.
+  // Commits `obj` (already validated) under the type's exclusive lock. Returns the stored
+  // object; *dangling is set when every owner reference points at a deleted object.
   std::shared_ptr<const Value> commit_locked(const TypeInfo& ti, const std::string& ns, const std::string& name,
                                             Value obj, Managers managers, const Stored* prev,
-                                            const PreparedEvent* pe = nullptr) {
+                                            const PreparedEvent* pe = nullptr, bool* dangling = nullptr) {
     uint64_t new_rv = ++rv;
     std::string digits = std::to_string(new_rv);
     Value& meta = obj["metadata"];
@@ -1003,16 +1061,27 @@ struct ApiServer::Impl {
     s.managers = std::move(managers);
     std::string key = obj_key(ti.rt, ns, name);
     Ref ref{ti.key(), key};
-    if (prev) unindex_owners_locked(*prev->obj, ref);
+    {
+      std::lock_guard<std::mutex> ig(index_mu);
+      if (prev) unindex_owners_locked(*prev->obj, ref);
+      by_uid[ptr->get("metadata").get_string("uid")] = ref;
+      const Value& owners = ptr->get("metadata").get("ownerReferences");
+      for (const auto& r : owners.items()) by_owner[r.get_string("uid")].insert(ref);
+      if (ti.rt.namespaced) by_namespace[ns].insert(ref);
+      // indexed and checked in one critical section: either the owner's deletion sees this
+      // dependent in by_owner (and the GC removes it) or this check sees the owner gone
+      if (dangling && !prev && !owners.empty()) {
+        bool alive = false;
+        for (const auto& r : owners.items()) alive = alive || by_uid.count(r.get_string("uid")) > 0;
+        *dangling = !alive;
+      }
+    }
     b[key] = std::move(s);
-    by_uid[ptr->get("metadata").get_string("uid")] = ref;
-    for (const auto& r : ptr->get("metadata").get("ownerReferences").items()) by_owner[r.get_string("uid")].insert(ref);
-    if (ti.rt.namespaced) by_namespace[ns].insert(ref);
     emit_locked(prev ? "MODIFIED" : "ADDED", ti, ns, ptr, new_rv, std::move(preline));
     return ptr;
   }
 
-  void unindex_owners_locked(const Value& obj, const Ref& ref) {
+  void unindex_owners_locked(const Value& obj, const Ref& ref) {  // index_mu held
     for (const auto& r : obj.get("metadata").get("ownerReferences").items()) {
       auto it = by_owner.find(r.get_string("uid"));
       if (it == by_owner.end()) continue;
@@ -1021,8 +1090,9 @@ struct ApiServer::Impl {
     }
   }
 
-  void erase_locked(const TypeInfo& ti, const std::string& ns, const std::string& name,
-                    std::vector<std::string>* deleted_uids) {
+  // Removes an object under its type's exclusive lock and hands its dependents (and, for a
+  // Namespace, its contents) to the garbage collector.
+  void erase_locked(const TypeInfo& ti, const std::string& ns, const std::string& name) {
     auto& b = bucket(ti);
     std::string key = obj_key(ti.rt, ns, name);
     auto it = b.find(key);
@@ -1033,68 +1103,68 @@ struct ApiServer::Impl {
     auto ptr = std::make_shared<const Value>(std::move(final_obj));
     std::string uid = ptr->get("metadata").get_string("uid");
     Ref ref{ti.key(), key};
-    by_uid.erase(uid);
-    unindex_owners_locked(*ptr, ref);
-    if (ti.rt.namespaced) {
-      auto nit = by_namespace.find(ns);
-      if (nit != by_namespace.end()) {
-        nit->second.erase(ref);
-        if (nit->second.empty()) by_namespace.erase(nit);
+    bool has_dependents;
+    {
+      std::lock_guard<std::mutex> ig(index_mu);
+      by_uid.erase(uid);
+      unindex_owners_locked(*ptr, ref);
+      if (ti.rt.namespaced) {
+        auto nit = by_namespace.find(ns);
+        if (nit != by_namespace.end()) {
+          nit->second.erase(ref);
+          if (nit->second.empty()) by_namespace.erase(nit);
+        }
       }
+      has_dependents = by_owner.count(uid) > 0;
     }
     b.erase(it);
     emit_locked("DELETED", ti, ns, ptr, new_rv);
-    if (deleted_uids) deleted_uids->push_back(uid);
-    // namespace deletion removes everything inside it
-    if (ti.rt.plural == "namespaces" && ti.rt.group.empty()) {
-      auto nit = by_namespace.find(name);
-      if (nit != by_namespace.end()) {
-        std::vector<Ref> victims(nit->second.begin(), nit->second.end());
-        for (const auto& v : victims) erase_ref_locked(v, deleted_uids);
+    bool is_ns = ti.rt.plural == "namespaces" && ti.rt.group.empty();
+    if (has_dependents || is_ns) {
+      std::lock_guard<std::mutex> g(gc_mu);
+      if (has_dependents) gc_queue.push_back({false, uid});
+      if (is_ns) gc_queue.push_back({true, name});
+      gc_cv.notify_one();
+    }
+  }
+
+  // Garbage collector thread: deletes dependents whose owners are all gone and the contents
+  // of deleted namespaces, one type lock at a time.
+  void gc_loop() {
+    while (true) {
+      GcItem item;
+      {
+        std::unique_lock<std::mutex> g(gc_mu);
+        gc_cv.wait(g, [&] { return gc_stop || !gc_queue.empty(); });
+        if (gc_stop) return;
+        item = std::move(gc_queue.front());
+        gc_queue.pop_front();
       }
-    }
-  }
-
-  void erase_ref_locked(const Ref& ref, std::vector<std::string>* deleted_uids) {
-    auto tit = types.find(ref.first);
-    if (tit == types.end()) return;
-    auto& b = bucket(tit->second);
-    auto it = b.find(ref.second);
-    if (it == b.end()) return;
-    const Value& meta = it->second.obj->get("metadata");
-    std::string ns = meta.get_string("namespace");
-    std::string name = meta.get_string("name");
-    erase_locked(tit->second, ns, name, deleted_uids);
-  }
-
-  bool dangling_owners_locked(const Value& obj) {
-    const Value& refs = obj.get("metadata").get("ownerReferences");
-    if (refs.empty()) return false;
-    for (const auto& r : refs.items()) {
-      if (by_uid.count(r.get_string("uid"))) return false;
-    }
-    return true;
-  }
-
-  // Garbage collector: delete dependents whose owners are all gone.
-  void collect_garbage_locked(std::vector<std::string> dead_uids) {
-    while (!dead_uids.empty()) {
-      std::string dead = dead_uids.back();
-      dead_uids.pop_back();
-      auto oit = by_owner.find(dead);
-      if (oit == by_owner.end()) continue;
-      std::vector<Ref> deps(oit->second.begin(), oit->second.end());
-      for (const auto& dep : deps) {
-        auto tit = types.find(dep.first);
-        if (tit == types.end()) continue;
-        auto& b = bucket(tit->second);
-        auto it = b.find(dep.second);
-        if (it == b.end()) continue;
-        bool any_alive = false;
-        for (const auto& r : it->second.obj->get("metadata").get("ownerReferences").items()) {
-          if (by_uid.count(r.get_string("uid"))) any_alive = true;
+      std::vector<Ref> victims;
+      {
+        std::lock_guard<std::mutex> ig(index_mu);
+        auto& idx = item.is_namespace ? by_namespace : by_owner;
+        auto it = idx.find(item.id);
+        if (it != idx.end()) victims.assign(it->second.begin(), it->second.end());
+      }
+      for (const auto& v : victims) {
+        TypeInfo* vti = type_by_key(v.first);
+        if (!vti) continue;
+        StoreLock lk(vti->store->mu, vti->store->stats);
+        auto it = vti->store->objs.find(v.second);
+        if (it == vti->store->objs.end()) continue;
+        const Value& meta = it->second.obj->get("metadata");
+        if (!item.is_namespace) {
+          bool alive = false;
+          {
+            std::lock_guard<std::mutex> ig(index_mu);
+            for (const auto& r : meta.get("ownerReferences").items()) alive = alive || by_uid.count(r.get_string("uid")) > 0;
+          }
+          if (alive) continue;
         }
-        if (!any_alive) erase_ref_locked(dep, &dead_uids);
+        std::string vns = meta.get_string("namespace"), vname = meta.get_string("name");
+        erase_locked(*vti, vns, vname);
+        gc_collected.fetch_add(1, std::memory_order_relaxed);
       }
     }
   }
@@ -1110,7 +1180,7 @@ struct ApiServer::Impl {
       Stored cur_copy;
       bool exists = false;
       {
-        SharedStoreLock lk(mu, lock_stats);
+        SharedStoreLock lk(ti.store->mu, ti.store->stats);
         auto& b = bucket(ti);
         auto it = b.find(obj_key(ti.rt, ns, name));
         if (it != b.end()) {
@@ -1122,8 +1192,7 @@ struct ApiServer::Impl {
       auto [obj, managers] = compute(exists ? &cur_copy : nullptr);
       std::string op = exists ? "UPDATE" : "CREATE";
       if (!exists && ti.rt.namespaced) {
-        SharedStoreLock lk(mu, lock_stats);
-        if (!namespace_exists_locked(ns)) {
+        if (!namespace_exists(ns)) {
           throw StatusError(404, "NotFound", "namespaces \"" + ns + "\" not found",
                             Value::object({{"name", ns}, {"kind", "namespaces"}}));
         }
@@ -1149,7 +1218,7 @@ struct ApiServer::Impl {
         obj["metadata"]["generation"] = gen + 1;
       }
       PreparedEvent pe = prepare_commit(obj, managers, ti.rt.api_version(), exists ? "MODIFIED" : "ADDED");
-      StoreLock lk(mu, lock_stats);
+      StoreLock lk(ti.store->mu, ti.store->stats);
       auto& b = bucket(ti);
       auto it = b.find(obj_key(ti.rt, ns, name));
       bool now_exists = it != b.end();
@@ -1157,24 +1226,19 @@ struct ApiServer::Impl {
       if (exists) {
         // finalizer-gated deletion completes when the last finalizer is removed
         if (obj.get("metadata").contains("deletionTimestamp") && obj.get("metadata").get("finalizers").empty()) {
-          std::vector<std::string> dead;
-          erase_locked(ti, ns, name, &dead);
-          collect_garbage_locked(dead);
+          erase_locked(ti, ns, name);
           return {cur_copy.obj, 200};
         }
         (void)is_status;
         return {commit_locked(ti, ns, name, std::move(obj), std::move(managers), &it->second, &pe), 200};
       }
-      if (ti.rt.plural == "customresourcedefinitions") register_crd_locked(obj);
-      auto created = commit_locked(ti, ns, name, std::move(obj), std::move(managers), nullptr, &pe);
+      if (ti.rt.plural == "customresourcedefinitions") register_crd(obj);
+      bool dangling = false;
+      auto created = commit_locked(ti, ns, name, std::move(obj), std::move(managers), nullptr, &pe, &dangling);
       // The garbage collector also removes dependents created with only dangling owner
       // references (e.g. a controller re-applying a child right after its owner was
       // deleted, before the owner's DELETED event reached it).
-      if (dangling_owners_locked(*created)) {
-        std::vector<std::string> dead;
-        erase_locked(ti, ns, name, &dead);
-        collect_garbage_locked(dead);
-      }
+      if (dangling) erase_locked(ti, ns, name);
       return {created, 201};
     }
     throw conflict(ti.rt, name);
@@ -1432,14 +1496,14 @@ struct ApiServer::Impl {
   void do_delete(ParsedPath& p, const http::Request& req, const UserInfo& user, http::ResponseWriter& w) {
     std::shared_ptr<const Value> cur;
     {
-      SharedStoreLock lk(mu, lock_stats);
+      SharedStoreLock lk(p.ti->store->mu, p.ti->store->stats);
       auto& b = bucket(*p.ti);
       auto it = b.find(obj_key(p.ti->rt, p.ns, p.name));
       if (it == b.end()) throw not_found(p.ti->rt, p.name);
       cur = it->second.obj;
     }
     call_webhooks(*p.ti, "", "DELETE", p.ns, p.name, nullptr, cur.get(), user);
-    StoreLock lk(mu, lock_stats);
+    StoreLock lk(p.ti->store->mu, p.ti->store->stats);
     auto& b = bucket(*p.ti);
     auto it = b.find(obj_key(p.ti->rt, p.ns, p.name));
     if (it == b.end()) throw not_found(p.ti->rt, p.name);
@@ -1456,10 +1520,7 @@ struct ApiServer::Impl {
       w.send_json(202, it->second.obj->dump());
       return;
     }
-    Value last = *it->second.obj;
-    std::vector<std::string> dead;
-    erase_locked(*p.ti, p.ns, p.name, &dead);
-    collect_garbage_locked(dead);
+    erase_locked(*p.ti, p.ns, p.name);
     (void)req;
     w.send_json(200, status_body(200, "", "").dump());
   }
@@ -1467,7 +1528,7 @@ struct ApiServer::Impl {
   void do_get(ParsedPath& p, http::ResponseWriter& w) {
     std::shared_ptr<const Value> obj;
     {
-      SharedStoreLock lk(mu, lock_stats);
+      SharedStoreLock lk(p.ti->store->mu, p.ti->store->stats);
       auto& b = bucket(*p.ti);
       auto it = b.find(obj_key(p.ti->rt, p.ns, p.name));
       if (it == b.end()) throw not_found(p.ti->rt, p.name);
@@ -1482,8 +1543,10 @@ struct ApiServer::Impl {
     std::vector<std::shared_ptr<const Value>> items;
     uint64_t list_rv;
     {
-      SharedStoreLock lk(mu, lock_stats);
-      list_rv = rv;
+      // no commit of this type is in flight while we hold its shared lock, so every event
+      // of this type with rv <= list_rv is reflected in the items
+      SharedStoreLock lk(p.ti->store->mu, p.ti->store->stats);
+      list_rv = rv.load();
       for (auto& [k, st] : bucket(*p.ti)) {
         const Value& meta = st.obj->get("metadata");
         if (!p.ns.empty() && meta.get_string("namespace") != p.ns) continue;
@@ -1524,11 +1587,16 @@ struct ApiServer::Impl {
     bool bookmarks = req.query_param("allowWatchBookmarks") == "true";
     std::vector<std::shared_ptr<const std::string>> initial;
     bool gone = false;
+    TypeStore& ts = *p.ti->store;
+    uint64_t compacted = 0;
     {
-      SharedStoreLock lk(mu, lock_stats);
+      // shared: no commit of this type can interleave between the snapshot/history scan and
+      // the registration below
+      SharedStoreLock lk(ts.mu, ts.stats);
+      compacted = ts.compacted_rv;
       uint64_t from = rv_s.empty() ? 0 : std::strtoull(rv_s.c_str(), nullptr, 10);
       if (rv_s.empty() || rv_s == "0") {
-        for (auto& [k, st] : bucket(*p.ti)) {
+        for (auto& [k, st] : ts.objs) {
           const Value& meta = st.obj->get("metadata");
           if (!sub.ns.empty() && meta.get_string("namespace") != sub.ns) continue;
           if (!sub.fields.name.empty() && meta.get_string("name") != sub.fields.name) continue;
@@ -1538,12 +1606,12 @@ struct ApiServer::Impl {
           line += "}\n";
           initial.push_back(std::make_shared<const std::string>(std::move(line)));
         }
-      } else if (from < compacted_rv) {
+      } else if (from < ts.compacted_rv) {
         gone = true;
       } else {
-        auto it = std::upper_bound(history.begin(), history.end(), from,
+        auto it = std::upper_bound(ts.history.begin(), ts.history.end(), from,
                                    [](uint64_t v, const std::shared_ptr<const EventRec>& e) { return v < e->rv; });
-        for (; it != history.end(); ++it) {
+        for (; it != ts.history.end(); ++it) {
           const auto& e = *it;
           if (e->type_key != sub.type_key) continue;
           if (!sub.ns.empty() && e->ns != sub.ns) continue;
@@ -1553,19 +1621,19 @@ struct ApiServer::Impl {
         }
       }
       if (!gone) {
-        std::lock_guard<std::mutex> wg(watches_mu);
-        watches.insert(subp);
+        std::lock_guard<std::mutex> wg(ts.watches_mu);
+        ts.watches.insert(subp);
       }
     }
     if (!w.start_chunked(200, "application/json")) {
-      std::lock_guard<std::mutex> wg(watches_mu);
-      watches.erase(subp);
+      std::lock_guard<std::mutex> wg(ts.watches_mu);
+      ts.watches.erase(subp);
       return;
     }
     if (gone) {
       Value ev = Value::object({{"type", "ERROR"},
                                 {"object", status_body(410, "Expired", "too old resource version: " + rv_s + " (" +
-                                                                           std::to_string(compacted_rv) + ")")}});
+                                                                           std::to_string(compacted) + ")")}});
       w.write_chunk(ev.dump() + "\n");
       w.end_chunked();
       return;
@@ -1596,10 +1664,21 @@ struct ApiServer::Impl {
       auto now = std::chrono::steady_clock::now();
       if (now >= deadline) break;
       if (bookmarks && now >= next_bookmark) {
+        // Under the type's shared lock every event of this type with rv <= cur_rv is already
+        // in sub.q; flush those before the bookmark so it never skips an undelivered event.
         uint64_t cur_rv;
+        std::vector<std::shared_ptr<const EventRec>> pending;
         {
-          SharedStoreLock lk(mu, lock_stats);
-          cur_rv = rv;
+          SharedStoreLock lk(ts.mu, ts.stats);
+          cur_rv = rv.load();
+          std::lock_guard<std::mutex> g(sub.m);
+          pending.assign(sub.q.begin(), sub.q.end());
+          sub.q.clear();
+        }
+        if (!pending.empty()) {
+          std::string buf;
+          for (auto& e : pending) buf += *e->line;
+          if (!w.write_chunk(buf)) break;
         }
         Value bm = Value::object({{"type", "BOOKMARK"},
                                   {"object", Value::object({{"kind", p.ti->rt.kind},
@@ -1611,15 +1690,15 @@ struct ApiServer::Impl {
       if (batch.empty() && w.peer_closed()) break;
     }
     {
-      std::lock_guard<std::mutex> wg(watches_mu);
-      watches.erase(subp);
+      std::lock_guard<std::mutex> wg(ts.watches_mu);
+      ts.watches.erase(subp);
     }
     w.end_chunked();
   }
 
   // ---------------------------------------------------------------- discovery
   void discovery(const std::string& path, http::ResponseWriter& w) {
-    SharedStoreLock lk(mu, lock_stats);
+    SharedStoreLock lk(types_mu, types_stats);
     if (path == "/api") {
       w.send_json(200, Value::object({{"kind", "APIVersions"}, {"versions", Value::array({"v1"})}}).dump());
       return;
@@ -1712,42 +1791,62 @@ struct ApiServer::Impl {
       return;
     }
     if (req.path == "/_kl/compact" && req.method == "POST") {
-      StoreLock lk(mu, lock_stats);
-      compacted_rv = rv;
-      history.clear();
-      w.send_json(200, Value::object({{"compacted_rv", static_cast<unsigned long long>(compacted_rv)}}).dump());
+      uint64_t at = 0;
+      for_each_store([&](const std::string&, TypeStore& ts) {
+        StoreLock lk(ts.mu, ts.stats);
+        at = rv.load();
+        ts.compacted_rv = at;
+        ts.history.clear();
+      });
+      w.send_json(200, Value::object({{"compacted_rv", static_cast<unsigned long long>(at)}}).dump());
       return;
     }
     if (req.path == "/_kl/drop-watches" && req.method == "POST") {
-      std::lock_guard<std::mutex> wg(watches_mu);
-      size_t n = watches.size();
-      for (const auto& ws : watches) ws->close();
+      size_t n = 0;
+      for_each_store([&](const std::string&, TypeStore& ts) {
+        std::lock_guard<std::mutex> wg(ts.watches_mu);
+        n += ts.watches.size();
+        for (const auto& ws : ts.watches) ws->close();
+      });
       w.send_json(200, Value::object({{"dropped", static_cast<unsigned long long>(n)}}).dump());
       return;
     }
     if (req.path == "/_kl/stats") {
-      SharedStoreLock lk(mu, lock_stats);
       Value counts = Value::object();
-      size_t total = 0;
-      for (auto& [k, b] : data) {
-        counts[k] = static_cast<unsigned long long>(b.size());
-        total += b.size();
-      }
-      size_t n_watches;
-      {
-        std::lock_guard<std::mutex> wg(watches_mu);
-        n_watches = watches.size();
-      }
-      w.send_json(200, Value::object({{"resourceVersion", static_cast<unsigned long long>(rv)},
+      Value locks = Value::object();
+      size_t total = 0, n_watches = 0;
+      uint64_t acq = 0, contended = 0, wait_ns = 0, hold_ns = 0;
+      for_each_store([&](const std::string& key, TypeStore& ts) {
+        {
+          SharedStoreLock lk(ts.mu, ts.stats);
+          counts[key] = static_cast<unsigned long long>(ts.objs.size());
+          total += ts.objs.size();
+        }
+        {
+          std::lock_guard<std::mutex> wg(ts.watches_mu);
+          n_watches += ts.watches.size();
+        }
+        uint64_t a = ts.stats.acquisitions.load(), h = ts.stats.hold_ns.load();
+        acq += a;
+        hold_ns += h;
+        contended += ts.stats.contended.load();
+        wait_ns += ts.stats.wait_ns.load();
+        if (a) locks[key] = Value::object({{"acquisitions", static_cast<unsigned long long>(a)},
+                                           {"hold_ms", static_cast<double>(h) * 1e-6}});
+      });
+      w.send_json(200, Value::object({{"resourceVersion", static_cast<unsigned long long>(rv.load())},
                                       {"objects", static_cast<unsigned long long>(total)},
                                       {"watches", static_cast<unsigned long long>(n_watches)},
                                       {"requests", static_cast<unsigned long long>(requests.load())},
                                       {"faults_hit", static_cast<unsigned long long>(faults_hit.load())},
+                                      {"gc_collected", static_cast<unsigned long long>(gc_collected.load())},
+                                      // summed over the per-type store locks; by_type_lock has the split
                                       {"store_lock", Value::object({
-                                          {"acquisitions", static_cast<unsigned long long>(lock_stats.acquisitions.load())},
-                                          {"contended", static_cast<unsigned long long>(lock_stats.contended.load())},
-                                          {"wait_ms", static_cast<double>(lock_stats.wait_ns.load()) * 1e-6},
-                                          {"hold_ms", static_cast<double>(lock_stats.hold_ns.load()) * 1e-6}})},
+                                          {"acquisitions", static_cast<unsigned long long>(acq)},
+                                          {"contended", static_cast<unsigned long long>(contended)},
+                                          {"wait_ms", static_cast<double>(wait_ns) * 1e-6},
+                                          {"hold_ms", static_cast<double>(hold_ns) * 1e-6}})},
+                                      {"by_type_lock", locks},
                                       {"by_type", counts}}).dump());
       return;
     }
@@ -1829,10 +1928,10 @@ uint16_t ApiServer::port() const { return impl_->server ? impl_->server->port() 
 
 void ApiServer::stop() {
   if (impl_ && impl_->server) {
-    {
-      std::lock_guard<std::mutex> wg(impl_->watches_mu);
-      for (const auto& ws : impl_->watches) ws->close();
-    }
+    impl_->for_each_store([](const std::string&, TypeStore& ts) {
+      std::lock_guard<std::mutex> wg(ts.watches_mu);
+      for (const auto& ws : ts.watches) ws->close();
+    });
     impl_->server->stop(std::chrono::milliseconds(2000));
     impl_->server.reset();
   }

@@ -1,0 +1,30 @@
+"""bench.py under torchrun with 2 ranks (gloo on CPU): the multi-GPU contract the driver
+uses for the 2/4/8-GPU scaling runs (one rank per GPU, rank 0 prints one JSON line, the
+value aggregates every rank's Ready CRs)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from bacchus_gpu_controller_amd import REPO_ROOT
+from bacchus_gpu_controller_amd.testing.cluster import free_port
+
+pytestmark = pytest.mark.slow
+
+
+def test_bench_two_ranks_gloo():
+    env = dict(os.environ, BGC_BENCH_CPU="1", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(REPO_ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "20"]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=REPO_ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout  # only rank 0 prints
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 1
+    assert d["config"]["global_batch"] == 40 and d["config"]["parallelism"] == "dp2"
+    assert d["ready_crs"] == 2 * 2 * 20 and d["failed_crs"] == 0
+    assert d["value"] > 0 and d["scaling"] == "weak"
