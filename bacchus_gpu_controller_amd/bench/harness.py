@@ -175,6 +175,7 @@ def run(args):
                 "admission": f"https://127.0.0.1:{cluster.admission_port}",
                 "ca": os.path.join(cluster.cert_dir, "ca.crt"),
                 "node_agent": f"http://127.0.0.1:{cluster.node_agent_port}",
+                "synchronizer": f"http://127.0.0.1:{cluster.sync_port}",
                 "apiserver_ca": open(cluster.apiserver_ca).read() if args.tls_apiserver else "",
                 "apiserver_verify": cluster.verify}
     info = d.broadcast_obj(info)
@@ -199,6 +200,7 @@ def run(args):
                     _clear(info["server"] + "/debug/samples/webhook", verify=info["apiserver_verify"])
                     _clear(info["admission"] + "/debug/samples/admission", verify=info["ca"])
                     _clear(info["node_agent"] + "/debug/samples/telemetry_poll")
+                    _clear(info["synchronizer"] + "/debug/samples/sync_ub")
                     lock0 = _kl_lock(info)
                 d.barrier()
                 t_start = time.perf_counter()
@@ -229,6 +231,7 @@ def run(args):
         hook = _samples(info["server"] + "/debug/samples/webhook", verify=info["apiserver_verify"])
         adm = _samples(info["admission"] + "/debug/samples/admission", verify=info["ca"])
         tel = _samples(info["node_agent"] + "/debug/samples/telemetry_poll")
+        syn = _samples(info["synchronizer"] + "/debug/samples/sync_ub")
         all_lat = [x for p in per_rank for x in p["lat"]]
         all_clat = [x for p in per_rank for x in p["clat"]]
         total_ready = sum(p["ready"] for p in per_rank)
@@ -264,6 +267,7 @@ def run(args):
             # quota; RoleBinding after the status write)
             "stage_p50_ms": {k: ms(_pct([x for p in per_rank for x in p["stage"][k]], 0.50)) for k in ("ns", "rq", "rb")},
             "telemetry_poll_p50_ms": ms(_pct(tel, 0.50)),
+            "sync_one_p50_ms": ms(_pct(syn, 0.50)),  # synchronizer: quota patch + status write for one tenant
             # kube-lite per-type store locks over the timed region: a busiest-type utilisation
             # near 1.0 means the in-memory API server (not the controller) bounds throughput
             "apiserver_store_lock": _lock_report(lock0, lock1, elapsed),
