@@ -1,6 +1,8 @@
 """Synchronizer sheet handling (R7c-R7e, N4): header inference, CSV, row parsing,
 authorization filter, quota mapping (reference src/synchronizer.rs:63-286)."""
 import json
+import shutil
+import subprocess
 
 import pytest
 
@@ -99,3 +101,26 @@ def test_google_assertion_verifies(nat):
                       "aud": "https://oauth2.googleapis.com/token", "exp": 1_800_003_600, "iat": 1_800_000_000}
     assert json.loads(nat.base64_decode(h)) == {"alg": "RS256", "typ": "JWT", "kid": "kid-1"}
     assert not nat.rs256_verify(fg.public_key, h + "." + c + "x", nat.base64_decode(s))
+
+
+@pytest.mark.skipif(shutil.which("openssl") is None, reason="openssl CLI not available")
+def test_google_assertion_verifies_with_openssl_cli(nat, tmp_path):
+    """Independent check of the RS256 JWT: `openssl dgst -verify` on the
+    signing input, not our own verifier."""
+    from bacchus_gpu_controller_amd.testing.fake_google import FakeGoogle
+
+    fg = FakeGoogle()
+    jwt = nat.google_assertion(fg.service_account_json(), "https://www.googleapis.com/auth/drive.readonly", 1_800_000_000)
+    h, c, s = jwt.split(".")
+    (tmp_path / "pub.pem").write_text(fg.public_key)
+    (tmp_path / "input").write_bytes((h + "." + c).encode())
+    sig = nat.base64_decode(s)
+    (tmp_path / "sig").write_bytes(sig if isinstance(sig, bytes) else sig.encode("latin-1"))
+
+    def verify(inp):
+        return subprocess.run(["openssl", "dgst", "-sha256", "-verify", str(tmp_path / "pub.pem"), "-signature",
+                               str(tmp_path / "sig"), str(inp)], capture_output=True, text=True)
+    ok = verify(tmp_path / "input")
+    assert ok.returncode == 0 and "Verified OK" in ok.stdout, ok.stdout + ok.stderr
+    (tmp_path / "tampered").write_bytes((h + "." + c + "x").encode())
+    assert verify(tmp_path / "tampered").returncode != 0
