@@ -140,3 +140,76 @@ def test_label_and_field_selectors(c):
     assert [i["metadata"]["name"] for i in gold["items"]] == ["s0", "s2"]
     notgold = c.admin.list("configmaps", namespace="sel", label_selector="tier notin (gold)")
     assert [i["metadata"]["name"] for i in notgold["items"]] == ["s1"]
+
+
+def _watch_lines(c, path, rv, seconds):
+    out = []
+    with requests.get(c.server + f"{path}?watch=1&resourceVersion={rv}&timeoutSeconds={seconds}",
+                      headers={"Authorization": "Bearer admin-token"}, stream=True, timeout=seconds + 10) as r:
+        for line in r.iter_lines():
+            if line:
+                out.append(json.loads(line))
+    return out
+
+
+def test_namespace_deletion_cascades_across_types(c):
+    ns(c, "casc")
+    for i in range(5):
+        c.admin.create("configmaps", {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": f"cm{i}"}},
+                       namespace="casc")
+    c.admin.create("resourcequotas", {"apiVersion": "v1", "kind": "ResourceQuota", "metadata": {"name": "q"},
+                                      "spec": {"hard": {"requests.amd.com/gpu": "1"}}}, namespace="casc")
+    c.admin.delete("namespaces", "casc")
+    wait_for(lambda: not c.admin.list("configmaps", namespace="casc")["items"], desc="configmaps collected")
+    wait_for(lambda: c.admin.get_or_none("resourcequotas", "q", namespace="casc") is None, desc="quota collected")
+
+
+def test_gc_cascades_through_owner_chain(c):
+    """owner (ConfigMap) -> Secret -> ConfigMap: deleting the root collects both levels (the
+    background collector handles each type under its own lock)."""
+    ns(c, "chain")
+    root = c.admin.create("configmaps", {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "root"}},
+                          namespace="chain")
+    mid = c.admin.create("secrets", {"apiVersion": "v1", "kind": "Secret", "metadata": {
+        "name": "mid", "ownerReferences": [{"apiVersion": "v1", "kind": "ConfigMap", "name": "root",
+                                            "uid": root["metadata"]["uid"]}]}}, namespace="chain")
+    c.admin.create("configmaps", {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {
+        "name": "leaf", "ownerReferences": [{"apiVersion": "v1", "kind": "Secret", "name": "mid",
+                                             "uid": mid["metadata"]["uid"]}]}}, namespace="chain")
+    c.admin.delete("configmaps", "root", namespace="chain")
+    wait_for(lambda: c.admin.get_or_none("secrets", "mid", namespace="chain") is None, desc="mid collected")
+    wait_for(lambda: c.admin.get_or_none("configmaps", "leaf", namespace="chain") is None, desc="leaf collected")
+    assert c.stats()["gc_collected"] >= 2
+
+
+def test_concurrent_writers_keep_per_type_watch_order(c):
+    """Writers on two types at once (per-type shards, one global resourceVersion): a watch on
+    one type sees each of its events exactly once, in increasing resourceVersion order, and a
+    resume from a mid-stream resourceVersion yields exactly the suffix."""
+    ns(c, "order")
+    rv0 = c.admin.list("configmaps", namespace="order")["metadata"]["resourceVersion"]
+    n_threads, per = 4, 25
+
+    def cm_writer(t):
+        for i in range(per):
+            c.admin.create("configmaps", {"apiVersion": "v1", "kind": "ConfigMap",
+                                          "metadata": {"name": f"w{t}-{i}"}}, namespace="order")
+
+    def ns_writer(t):
+        for i in range(per):
+            ns(c, f"order-ns-{t}-{i}")
+
+    threads = [threading.Thread(target=cm_writer, args=(t,)) for t in range(n_threads)]
+    threads += [threading.Thread(target=ns_writer, args=(t,)) for t in range(n_threads)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(60)
+    events = [e for e in _watch_lines(c, "/api/v1/namespaces/order/configmaps", rv0, 2) if e["type"] == "ADDED"]
+    names = [e["object"]["metadata"]["name"] for e in events]
+    rvs = [int(e["object"]["metadata"]["resourceVersion"]) for e in events]
+    assert sorted(names) == sorted(f"w{t}-{i}" for t in range(n_threads) for i in range(per))
+    assert rvs == sorted(rvs) and len(set(rvs)) == len(rvs)
+    mid = rvs[len(rvs) // 2]
+    suffix = [e for e in _watch_lines(c, "/api/v1/namespaces/order/configmaps", mid, 2) if e["type"] == "ADDED"]
+    assert [int(e["object"]["metadata"]["resourceVersion"]) for e in suffix] == [r for r in rvs if r > mid]
