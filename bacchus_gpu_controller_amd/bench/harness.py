@@ -144,7 +144,8 @@ def _kl_lock(info):
     import requests
 
     st = requests.get(info["server"] + "/_kl/stats", timeout=10, verify=info["apiserver_verify"]).json()
-    return {"total": st["store_lock"], "by_type": st.get("by_type_lock", {}), "requests": st["requests"]}
+    return {"total": st["store_lock"], "by_type": st.get("by_type_lock", {}), "requests": st["requests"],
+            "by_kind": st.get("requests_by_kind", {})}
 
 
 def run(args):
@@ -272,6 +273,9 @@ def run(args):
             # near 1.0 means the in-memory API server (not the controller) bounds throughput
             "apiserver_store_lock": _lock_report(lock0, lock1, elapsed),
             "apiserver_requests_per_cr": round((lock1["requests"] - lock0["requests"]) / max(1, total_ready), 2),
+            "apiserver_requests_per_cr_by_kind": {
+                k: round((v - lock0["by_kind"].get(k, 0)) / max(1, total_ready), 3)
+                for k, v in sorted(lock1["by_kind"].items()) if v - lock0["by_kind"].get(k, 0) > 0},
             "ready_crs": total_ready,
             "failed_crs": total_failed,
             "reference_structural": {"apply_to_ready_p50_s": 30.0, "apply_to_ready_p99_s": 59.4,

@@ -1847,6 +1847,12 @@ struct ApiServer::Impl {
                                           {"wait_ms", static_cast<double>(wait_ns) * 1e-6},
                                           {"hold_ms", static_cast<double>(hold_ns) * 1e-6}})},
                                       {"by_type_lock", locks},
+                                      {"requests_by_kind", [&] {
+                                         Value rq = Value::object();
+                                         std::lock_guard<std::mutex> g(req_count_mu);
+                                         for (auto& [k, v] : req_counts) rq[k] = static_cast<unsigned long long>(v);
+                                         return rq;
+                                       }()},
                                       {"by_type", counts}}).dump());
       return;
     }
@@ -1854,8 +1860,24 @@ struct ApiServer::Impl {
   }
 
   // ---------------------------------------------------------------- dispatch
+  // Request accounting by "METHOD resource[/sub][ watch] code" (exported in /_kl/stats).
+  std::mutex req_count_mu;
+  std::map<std::string, uint64_t> req_counts;
+
   void handle(http::Request& req, http::ResponseWriter& w) {
     requests.fetch_add(1, std::memory_order_relaxed);
+    std::string res_key = "-";
+    struct Count {
+      Impl* im;
+      const http::Request& req;
+      http::ResponseWriter& w;
+      std::string& res;
+      ~Count() {
+        std::string k = req.method + " " + res + " " + std::to_string(w.status_code());
+        std::lock_guard<std::mutex> g(im->req_count_mu);
+        im->req_counts[k]++;
+      }
+    } count{this, req, w, res_key};
     try {
       if (inject_fault(req, w)) return;
       UserInfo user = authenticate(req);
@@ -1869,6 +1891,11 @@ struct ApiServer::Impl {
       if (!parse_path(req.path, p, group, version, rest)) {
         discovery(req.path, w);
         return;
+      }
+      res_key = p.ti->rt.plural + (p.sub.empty() ? "" : "/" + p.sub);
+      if (p.collection && req.method == "GET") {
+        std::string wq = req.query_param("watch");
+        if (wq == "1" || wq == "true") res_key += " watch";
       }
       if (!p.sub.empty() && p.sub != "status") throw StatusError(404, "NotFound", "subresource not supported: " + p.sub);
       if (!p.sub.empty() && !p.ti->rt.has_status) throw StatusError(404, "NotFound", "the server could not find the requested resource");

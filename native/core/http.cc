@@ -280,6 +280,7 @@ void ResponseWriter::abort() {
 
 void ResponseWriter::send(int status, const std::string& body, const std::string& content_type,
                           const Headers* extra) {
+  status_ = status;
   if (sent_) return;
   sent_ = true;
   std::string out;
@@ -296,6 +297,7 @@ void ResponseWriter::send(int status, const std::string& body, const std::string
 }
 
 bool ResponseWriter::start_chunked(int status, const std::string& content_type) {
+  status_ = status;
   if (sent_) return false;
   sent_ = true;
   chunked_ = true;

@@ -107,6 +107,7 @@ class ResponseWriter {
   // Drops the connection without a response (fault injection: connection reset).
   void abort();
   bool sent() const { return sent_; }
+  int status_code() const { return status_; }  // 0 until a response (or stream) has started
   bool keep_alive() const { return keep_alive_; }
   // True once the server is shutting down; streaming handlers should return.
   bool stopping() const { return stop_.cancelled(); }
@@ -119,6 +120,7 @@ class ResponseWriter {
   const CancelToken& stop_;
   bool sent_ = false;
   bool chunked_ = false;
+  int status_ = 0;
 };
 
 using Handler = std::function<void(Request&, ResponseWriter&)>;
