@@ -18,6 +18,7 @@ Config Config::from_env(const EnvConfig& env) {
   c.workers = static_cast<int>(env.u64_or("workers", 16));
   c.skip_unchanged = env.boolean_or("skip_unchanged", true);
   c.parallel_children = env.boolean_or("parallel_children", true);
+  c.child_delete_delay_ms = static_cast<int64_t>(env.u64_or("child_delete_delay_ms", 50));
   c.requeue_secs = static_cast<int64_t>(env.u64_or("requeue_secs", 30));
   c.error_requeue_ms = static_cast<int64_t>(env.u64_or("error_requeue_ms", 3000));
   c.leader_election = env.boolean_or("leader_election", false);

@@ -41,6 +41,7 @@ struct Config {
   bool parallel_children = true;
   int64_t requeue_secs = 30;
   int64_t error_requeue_ms = 3000;
+  int64_t child_delete_delay_ms = 50;
   bool leader_election = false;
   std::string lease_namespace = "default";
   std::string lease_name = "bacchus-gpu-controller";

@@ -305,7 +305,11 @@ void Controller::run(CancelToken& stop, Reconciler reconcile, ErrorPolicy error_
             for (const auto& k : c->mapper(*o)) queue_.add(k);
           }
         } else {
-          if (ev.type != WatchEvent::Type::Deleted && child_filter_ && !child_filter_(c->rt, *ev.object)) {
+          if (ev.type == WatchEvent::Type::Deleted) {
+            for (const auto& k : c->mapper(*ev.object)) queue_.add_after(k, opts_.child_delete_delay);
+            return;
+          }
+          if (child_filter_ && !child_filter_(c->rt, *ev.object)) {
             filtered_.fetch_add(1, std::memory_order_relaxed);
             return;
           }

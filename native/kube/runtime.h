@@ -128,6 +128,10 @@ class Controller {
 
   struct Options {
     int workers = 8;
+    // Owners of a DELETED child are enqueued after this delay: during cascading deletion the
+    // children's DELETED events can overtake the owner's own DELETED event, and reconciling
+    // the stale owner would re-create children the garbage collector is removing.
+    std::chrono::milliseconds child_delete_delay{50};
   };
 
   Controller(KubeClient& client, ResourceType primary, Options opts);

@@ -1,6 +1,7 @@
 #include "sync/synchronizer.h"
 
 #include <thread>
+#include <unordered_map>
 
 #include "core/json_patch.h"
 #include "core/log.h"
@@ -128,6 +129,10 @@ int Synchronizer::run(CancelToken& stop) {
   kube::Store store(types::UserBootstrap);
   std::atomic<bool> fatal{false};
   auto& ub_latency = metrics::Registry::global().samples("sync_ub");
+  // resourceVersion of the UB version we last wrote for: a deferred re-offer of that same
+  // version (the watch has not yet delivered our own writes) needs no second look
+  std::mutex acted_mu;
+  std::unordered_map<std::string, std::string> acted;
 
   if (cfg_.watch) {
     watch_thread = std::make_unique<std::thread>([&] {
@@ -138,6 +143,9 @@ int Synchronizer::run(CancelToken& stop) {
           for (const auto& o : ev.objects) queue.add(kube::meta_name(*o));
         } else if (ev.type != kube::WatchEvent::Type::Deleted) {
           queue.add(kube::meta_name(*ev.object));
+        } else {
+          std::lock_guard<std::mutex> g(acted_mu);
+          acted.erase(kube::meta_name(*ev.object));
         }
       });
     });
@@ -147,6 +155,15 @@ int Synchronizer::run(CancelToken& stop) {
         while (queue.get(key)) {
           kube::ObjPtr ub = store.get(key);
           if (ub) {
+            const std::string ub_rv = kube::meta_rv(*ub);
+            {
+              std::lock_guard<std::mutex> g(acted_mu);
+              auto a = acted.find(key);
+              if (a != acted.end() && a->second == ub_rv) {
+                queue.done(key);
+                continue;
+              }
+            }
             int64_t t0 = metrics::now_ns();
             try {
               auto idx = index();
@@ -155,7 +172,11 @@ int Synchronizer::run(CancelToken& stop) {
                 int64_t age_ms = (metrics::now_ns() - last_refresh_ns_.load()) / 1000000;
                 if (last_refresh_ns_.load() != 0 && age_ms >= static_cast<int64_t>(cfg_.min_refresh_ms)) refresh();
               }
-              if (sync_one(*ub)) ub_latency.add(static_cast<double>(metrics::now_ns() - t0) * 1e-9);
+              if (sync_one(*ub)) {
+                ub_latency.add(static_cast<double>(metrics::now_ns() - t0) * 1e-9);
+                std::lock_guard<std::mutex> g(acted_mu);
+                acted[key] = ub_rv;
+              }
             } catch (const std::exception& e) {
               LOG_ERROR("synchronizer") << "sync of " << key << " failed (retrying): " << e.what();
               queue.add_after(key, std::chrono::milliseconds(1000));
