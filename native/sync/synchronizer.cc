@@ -1,5 +1,6 @@
 #include "sync/synchronizer.h"
 
+#include <algorithm>
 #include <thread>
 #include <unordered_map>
 
@@ -54,9 +55,10 @@ void Synchronizer::refresh() {
     index_ = idx;
   }
   last_refresh_ns_.store(metrics::now_ns());
+  index_gen_.fetch_add(1);
 }
 
-bool Synchronizer::sync_one(const Value& ub) {
+bool Synchronizer::sync_one(const Value& ub, std::vector<std::string>* produced) {
   const std::string name = ub.get("metadata").get_string("name");
   if (name.empty()) return false;
   auto idx = index();
@@ -81,6 +83,7 @@ bool Synchronizer::sync_one(const Value& ub) {
     ops.replace("/spec/quota", desired);
     Value res = client_.patch_json(types::UserBootstrap, "", name, ops.ops(), kPatchManager);
     rv = res.get("metadata").get_string("resourceVersion");
+    if (produced) produced->push_back(rv);
     LOG_INFO("synchronizer") << "quota updated";
   }
   if (!synced || !cfg_.skip_unchanged) {
@@ -90,7 +93,8 @@ bool Synchronizer::sync_one(const Value& ub) {
       body["status"] = Value::object({{"synchronized_with_sheet", true}});
       try {
         LOG_INFO("synchronizer") << "updating status";
-        client_.replace_status(types::UserBootstrap, "", name, body);
+        Value res = client_.replace_status(types::UserBootstrap, "", name, body);
+        if (produced) produced->push_back(res.get("metadata").get_string("resourceVersion"));
         break;
       } catch (const kube::ApiError& e) {
         if (e.code() != 409 || attempt == 2) throw;
@@ -132,7 +136,11 @@ int Synchronizer::run(CancelToken& stop) {
   // resourceVersion of the UB version we last wrote for: a deferred re-offer of that same
   // version (the watch has not yet delivered our own writes) needs no second look
   std::mutex acted_mu;
-  std::unordered_map<std::string, std::string> acted;
+  struct Acted {
+    uint64_t sheet_gen;                 // a newer sheet re-evaluates every UB
+    std::vector<std::string> versions;  // UB versions acted on or produced by our writes
+  };
+  std::unordered_map<std::string, Acted> acted;
 
   if (cfg_.watch) {
     watch_thread = std::make_unique<std::thread>([&] {
@@ -159,7 +167,8 @@ int Synchronizer::run(CancelToken& stop) {
             {
               std::lock_guard<std::mutex> g(acted_mu);
               auto a = acted.find(key);
-              if (a != acted.end() && a->second == ub_rv) {
+              if (a != acted.end() && a->second.sheet_gen == index_gen_.load() &&
+                  std::find(a->second.versions.begin(), a->second.versions.end(), ub_rv) != a->second.versions.end()) {
                 queue.done(key);
                 continue;
               }
@@ -172,10 +181,12 @@ int Synchronizer::run(CancelToken& stop) {
                 int64_t age_ms = (metrics::now_ns() - last_refresh_ns_.load()) / 1000000;
                 if (last_refresh_ns_.load() != 0 && age_ms >= static_cast<int64_t>(cfg_.min_refresh_ms)) refresh();
               }
-              if (sync_one(*ub)) {
+              std::vector<std::string> produced{ub_rv};
+              uint64_t gen = index_gen_.load();
+              if (sync_one(*ub, &produced)) {
                 ub_latency.add(static_cast<double>(metrics::now_ns() - t0) * 1e-9);
                 std::lock_guard<std::mutex> g(acted_mu);
-                acted[key] = ub_rv;
+                acted[key] = Acted{gen, std::move(produced)};
               }
             } catch (const std::exception& e) {
               LOG_ERROR("synchronizer") << "sync of " << key << " failed (retrying): " << e.what();

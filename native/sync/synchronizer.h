@@ -70,7 +70,9 @@ class Synchronizer {
   // One reference-style pass over every UserBootstrap. Throws on the first error.
   TickStats tick();
   // Syncs one UserBootstrap object against the current index; returns true if it wrote.
-  bool sync_one(const json::Value& ub);
+  // Writes quota then status for one UserBootstrap. Returns true when it wrote; `produced`
+  // receives the resourceVersions of the versions its own writes created.
+  bool sync_one(const json::Value& ub, std::vector<std::string>* produced = nullptr);
   // Main loop; returns non-zero exit status on fatal error.
   int run(CancelToken& stop);
 
@@ -82,6 +84,7 @@ class Synchronizer {
   mutable std::mutex mu_;
   std::shared_ptr<const RowIndex> index_;
   std::atomic<int64_t> last_refresh_ns_{0};
+  std::atomic<uint64_t> index_gen_{0};  // bumped by every refresh()
   std::mutex refresh_mu_;
 };
 
