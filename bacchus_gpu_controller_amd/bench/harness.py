@@ -140,6 +140,17 @@ def _lock_report(l0, l1, elapsed):
             "busiest_type": busiest, "busiest_utilisation": round(util, 4)}
 
 
+def _gpu_telemetry(url):
+    import requests
+
+    d = requests.get(url + "/gpus", timeout=10).json()
+    keep = ("index", "power_w", "temp_hotspot_c", "temp_mem_c", "gfx_activity_pct", "umc_activity_pct",
+            "vram_used_mb", "gfxclk_mhz", "uclk_mhz", "xgmi_links_up", "ecc_uncorrectable")
+    return {"backend": d.get("backend"), "advertised": len(d.get("gpus", [])), "healthy": d.get("healthy"),
+            "product": (d.get("gpus") or [{}])[0].get("market_name"),
+            "devices": [{k: t[k] for k in keep if k in t} for t in d.get("telemetry", [])]}
+
+
 def _kl_lock(info):
     import requests
 
@@ -233,6 +244,7 @@ def run(args):
         adm = _samples(info["admission"] + "/debug/samples/admission", verify=info["ca"])
         tel = _samples(info["node_agent"] + "/debug/samples/telemetry_poll")
         syn = _samples(info["synchronizer"] + "/debug/samples/sync_ub")
+        gpu_tel = _gpu_telemetry(info["node_agent"])
         all_lat = [x for p in per_rank for x in p["lat"]]
         all_clat = [x for p in per_rank for x in p["clat"]]
         total_ready = sum(p["ready"] for p in per_rank)
@@ -268,7 +280,9 @@ def run(args):
             # quota; RoleBinding after the status write)
             "stage_p50_ms": {k: ms(_pct([x for p in per_rank for x in p["stage"][k]], 0.50)) for k in ("ns", "rq", "rb")},
             "telemetry_poll_p50_ms": ms(_pct(tel, 0.50)),
-            "sync_one_p50_ms": ms(_pct(syn, 0.50)),  # synchronizer: quota patch + status write for one tenant
+            "sync_one_p50_ms": ms(_pct(syn, 0.50)),
+            # amdsmi counters of the advertised GPUs at the end of the timed region (node agent)
+            "gpu_telemetry": gpu_tel,  # synchronizer: quota patch + status write for one tenant
             # kube-lite per-type store locks over the timed region: a busiest-type utilisation
             # near 1.0 means the in-memory API server (not the controller) bounds throughput
             "apiserver_store_lock": _lock_report(lock0, lock1, elapsed),
