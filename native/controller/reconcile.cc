@@ -94,6 +94,20 @@ Reconciler::Stats Reconciler::stats() const {
 
 static std::string child_key(const DesiredChild& c) { return c.rt->plural + "/" + c.ns + "/" + c.name; }
 
+void Reconciler::forget(const kube::ResourceType& rt, const Value& child) {
+  std::string key = rt.plural + "/" + kube::meta_namespace(child) + "/" + kube::meta_name(child);
+  static auto& gauge = metrics::Registry::global().gauge("bgc_controller_apply_cache_entries",
+                                                         "Children with a remembered last apply");
+  std::lock_guard<std::mutex> lk(mu_);
+  last_applied_.erase(key);
+  gauge.set(static_cast<double>(last_applied_.size()));
+}
+
+size_t Reconciler::cached_children() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return last_applied_.size();
+}
+
 bool Reconciler::is_own_write(const kube::ResourceType& rt, const Value& child) const {
   if (!cfg_.skip_unchanged) return false;
   std::string key = rt.plural + "/" + kube::meta_namespace(child) + "/" + kube::meta_name(child);
@@ -117,8 +131,11 @@ void Reconciler::apply_child(const DesiredChild& c, const std::string& body_hash
   static auto& applied = metrics::Registry::global().counter("bgc_apply_total", "Server-side applies issued");
   Value res = client_.apply(*c.rt, c.ns, c.name, c.body, kFieldManager, /*force=*/true);
   applied.inc();
+  static auto& gauge = metrics::Registry::global().gauge("bgc_controller_apply_cache_entries",
+                                                         "Children with a remembered last apply");
   std::lock_guard<std::mutex> lk(mu_);
   last_applied_[child_key(c)] = {body_hash, kube::meta_rv(res)};
+  gauge.set(static_cast<double>(last_applied_.size()));
   stats_.applied++;
 }
 

@@ -70,6 +70,9 @@ class Reconciler {
   // True when `child` is exactly the object our last apply returned (same resourceVersion):
   // the watch echo of our own write, which needs no reconcile.
   bool is_own_write(const kube::ResourceType& rt, const json::Value& child) const;
+  // Drops the last-applied record of a deleted child (keeps the cache bounded under churn).
+  void forget(const kube::ResourceType& rt, const json::Value& child);
+  size_t cached_children() const;
 
   struct Stats {
     uint64_t applied = 0;

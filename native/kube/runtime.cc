@@ -306,6 +306,7 @@ void Controller::run(CancelToken& stop, Reconciler reconcile, ErrorPolicy error_
           }
         } else {
           if (ev.type == WatchEvent::Type::Deleted) {
+            if (child_deleted_) child_deleted_(c->rt, *ev.object);
             for (const auto& k : c->mapper(*ev.object)) queue_.add_after(k, opts_.child_delete_delay);
             return;
           }

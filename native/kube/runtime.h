@@ -143,6 +143,8 @@ class Controller {
   // (e.g. the echo of the reconciler's own apply). DELETED events and relists always do.
   using ChildFilter = std::function<bool(const ResourceType& child_type, const json::Value& child)>;
   void set_child_filter(ChildFilter f) { child_filter_ = std::move(f); }
+  // Called for every child DELETED event (e.g. to drop per-child caches).
+  void set_child_deleted_hook(ChildFilter f) { child_deleted_ = std::move(f); }
   uint64_t filtered_events() const { return filtered_.load(); }
   // Extra trigger source (e.g. a periodic external refresh).
   void enqueue(const std::string& key) { queue_.add(key); }
@@ -166,6 +168,7 @@ class Controller {
   std::vector<std::unique_ptr<Child>> children_;
   WorkQueue queue_;
   ChildFilter child_filter_;
+  ChildFilter child_deleted_;
   std::atomic<uint64_t> filtered_{0};
 };
 

@@ -1,7 +1,9 @@
 """End-to-end onboarding flow through kube-lite + TLS webhook +
 controller: create as an OIDC user, quota/status as the synchronizer would write them,
 RoleBinding only after sync, GC on delete."""
+import re
 import pytest
+import requests
 
 from bacchus_gpu_controller_amd.testing.cluster import Cluster
 from bacchus_gpu_controller_amd.testing.kubeapi import ApiError, wait_for
@@ -115,3 +117,26 @@ def test_invalid_namespace_name_error_loop(cluster):
     assert cluster.admin.get_or_none("namespaces", "ivy.x") is None
     assert cluster.procs["controller"].alive()
     cluster.admin.delete("userbootstraps", "ivy.x")
+
+
+def test_controller_caches_stay_bounded_under_churn():
+    """Tenants come and go; the controller's per-child apply cache drains back to empty."""
+    with Cluster(admission=False) as c:
+        names = [f"churn{i}" for i in range(20)]
+        for n in names:
+            c.admin.create("userbootstraps", {"apiVersion": "bacchus.io/v1", "kind": "UserBootstrap",
+                                              "metadata": {"name": n},
+                                              "spec": {"kube_username": n,
+                                                       "quota": {"hard": {"requests.amd.com/gpu": "1"}}}})
+        for n in names:
+            wait_for(lambda: c.admin.get_or_none("resourcequotas", n, n), desc=f"{n} quota")
+
+        def cache_entries():
+            m = requests.get(f"http://127.0.0.1:{c.controller_port}/metrics", timeout=5).text
+            hit = re.search(r"^bgc_controller_apply_cache_entries (\S+)$", m, re.M)
+            return float(hit.group(1)) if hit else None
+
+        assert cache_entries() >= 40  # namespace + quota per tenant
+        for n in names:
+            c.admin.delete("userbootstraps", n)
+        wait_for(lambda: cache_entries() == 0, timeout=15, desc="apply cache drained")
