@@ -2,6 +2,7 @@
 controller: create as an OIDC user, quota/status as the synchronizer would write them,
 RoleBinding only after sync, GC on delete."""
 import re
+
 import pytest
 import requests
 
