@@ -100,7 +100,27 @@ void Reconciler::forget(const kube::ResourceType& rt, const Value& child) {
                                                          "Children with a remembered last apply");
   std::lock_guard<std::mutex> lk(mu_);
   last_applied_.erase(key);
+  for (const auto& ref : child.get("metadata").get("ownerReferences").items()) {
+    if (ref.get_string("kind") == types::UserBootstrap.kind) ub_state_.erase(ref.get_string("name"));
+  }
   gauge.set(static_cast<double>(last_applied_.size()));
+}
+
+bool Reconciler::fresh(const std::string& owner_name, const std::string& owner_rv) {
+  std::vector<ChildRef> children;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = ub_state_.find(owner_name);
+    if (it == ub_state_.end() || it->second.owner_rv != owner_rv) return false;
+    children = it->second.children;
+  }
+  for (const auto& c : children) {
+    kube::Store* store = ctrl_.child_store(c.rt->plural);
+    if (!store) return false;
+    kube::ObjPtr cur = store->get(c.ns, c.name);
+    if (!cur || kube::meta_rv(*cur) != c.rv) return false;
+  }
+  return true;
 }
 
 size_t Reconciler::cached_children() const {
@@ -146,6 +166,12 @@ kube::Action Reconciler::reconcile(const kube::ObjPtr& ub_ptr) {
   static auto& skipped = reg.counter("bgc_apply_skipped_total", "Applies skipped: child already as last written");
   metrics::Timer timer(&hist, &ring);
   const Value& ub = *ub_ptr;
+  const std::string owner_name = kube::meta_name(ub), owner_rv = kube::meta_rv(ub);
+  if (cfg_.skip_unchanged && fresh(owner_name, owner_rv)) {
+    static auto& fast = reg.counter("bgc_reconcile_fast_total", "Reconciles with UB and children unchanged since the last one");
+    fast.inc();
+    return kube::Action::requeue_after(std::chrono::milliseconds(cfg_.requeue_secs * 1000));
+  }
   std::vector<DesiredChild> children = desired_children(ub);
   LOG_INFO("controller") << "reconciling " << children.front().name;
 
@@ -194,6 +220,21 @@ kube::Action Reconciler::reconcile(const kube::ObjPtr& ub_ptr) {
     for (size_t i : middle) run_one(i);
   }
   for (size_t i : last) run_one(i);
+  if (cfg_.skip_unchanged) {
+    UbState st;
+    st.owner_rv = owner_rv;
+    std::lock_guard<std::mutex> lk(mu_);
+    bool complete = true;
+    for (const auto& c : children) {
+      auto it = last_applied_.find(child_key(c));
+      if (it == last_applied_.end()) {
+        complete = false;
+        break;
+      }
+      st.children.push_back({c.rt, c.ns, c.name, it->second.rv});
+    }
+    if (complete) ub_state_[owner_name] = std::move(st);
+  }
   static auto& ok = reg.counter("bgc_reconcile_total", "Reconciles", {{"result", "ok"}});
   ok.inc();
   return kube::Action::requeue_after(std::chrono::milliseconds(cfg_.requeue_secs * 1000));

@@ -94,6 +94,19 @@ class Reconciler {
   ThreadPool pool_;
   mutable std::mutex mu_;
   std::unordered_map<std::string, Applied> last_applied_;
+  // Fast path for periodic resyncs: after a fully successful reconcile, the UB's
+  // resourceVersion and each child's resourceVersion. A later reconcile of the same UB
+  // version whose children are still at those versions in the watch cache does nothing.
+  struct ChildRef {
+    const kube::ResourceType* rt;
+    std::string ns, name, rv;
+  };
+  struct UbState {
+    std::string owner_rv;
+    std::vector<ChildRef> children;
+  };
+  std::unordered_map<std::string, UbState> ub_state_;
+  bool fresh(const std::string& owner_name, const std::string& owner_rv);
   Stats stats_;
 };
 

@@ -151,6 +151,19 @@ bool Store::wait_synced(std::chrono::milliseconds timeout) const {
 // ---------------------------------------------------------------------------
 // WorkQueue
 
+void WorkQueue::schedule_locked(const std::string& key, Clock::time_point t) {
+  due_[key] = t;
+  timeline_.emplace(t, key);
+  if (t <= Clock::now()) {
+    if (idle_ > 0) cv_.notify_one();
+    else if (timer_waiter_) timer_cv_.notify_one();
+  } else if (timer_waiter_) {
+    if (t < timer_target_) timer_cv_.notify_one();  // new earliest deadline
+  } else if (idle_ > 0) {
+    cv_.notify_one();  // someone must become the timer waiter
+  }
+}
+
 void WorkQueue::add_after(const std::string& key, std::chrono::milliseconds delay) {
   auto t = Clock::now() + delay;
   std::lock_guard<std::mutex> lk(mu_);
@@ -162,9 +175,7 @@ void WorkQueue::add_after(const std::string& key, std::chrono::milliseconds dela
   }
   auto it = due_.find(key);
   if (it != due_.end() && it->second <= t) return;
-  due_[key] = t;
-  timeline_.emplace(t, key);
-  cv_.notify_one();
+  schedule_locked(key, t);
 }
 
 bool WorkQueue::get(std::string& key) {
@@ -184,14 +195,21 @@ bool WorkQueue::get(std::string& key) {
       timeline_.erase(it);
       due_.erase(d);
       processing_.insert(key);
+      // hand the timer role on if more work is waiting and nobody is timing it
+      if (!timeline_.empty() && !timer_waiter_ && idle_ > 0) cv_.notify_one();
       return true;
     }
-    if (timeline_.empty()) {
-      cv_.wait(lk);
-    } else {
+    if (!timeline_.empty() && !timer_waiter_) {
+      timer_waiter_ = true;
       // copy: wait_until re-reads its deadline after re-locking, when another worker may have erased the node
-      const auto deadline = timeline_.begin()->first;
-      cv_.wait_until(lk, deadline);
+      timer_target_ = timeline_.begin()->first;
+      const auto deadline = timer_target_;
+      timer_cv_.wait_until(lk, deadline);
+      timer_waiter_ = false;
+    } else {
+      ++idle_;
+      cv_.wait(lk);
+      --idle_;
     }
   }
 }
@@ -204,11 +222,7 @@ void WorkQueue::done(const std::string& key) {
     auto t = it->second;
     deferred_.erase(it);
     auto d = due_.find(key);
-    if (d == due_.end() || t < d->second) {
-      due_[key] = t;
-      timeline_.emplace(t, key);
-    }
-    cv_.notify_one();
+    if (d == due_.end() || t < d->second) schedule_locked(key, t);
   }
 }
 
@@ -216,6 +230,7 @@ void WorkQueue::shutdown() {
   std::lock_guard<std::mutex> lk(mu_);
   shutdown_ = true;
   cv_.notify_all();
+  timer_cv_.notify_all();
 }
 
 size_t WorkQueue::pending() const {

@@ -103,8 +103,15 @@ class WorkQueue {
   size_t in_flight() const;
 
  private:
+  void schedule_locked(const std::string& key, Clock::time_point t);  // insert + wake exactly one waiter
   mutable std::mutex mu_;
+  // One idle worker (the timer waiter) sleeps until the earliest deadline on timer_cv_;
+  // the others wait untimed on cv_. A due item wakes one worker, not every idle one.
   std::condition_variable cv_;
+  std::condition_variable timer_cv_;
+  int idle_ = 0;                  // workers waiting on cv_
+  bool timer_waiter_ = false;     // a worker is waiting on timer_cv_
+  Clock::time_point timer_target_{};
   std::map<std::string, Clock::time_point> due_;           // key -> due time
   std::multimap<Clock::time_point, std::string> timeline_;  // due time -> key (may hold stale entries)
   std::set<std::string> processing_;

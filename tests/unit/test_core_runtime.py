@@ -142,3 +142,56 @@ def test_certificates_verify_with_openssl(nat, tmp_path):
     txt = subprocess.run(["openssl", "x509", "-in", str(tmp_path / "tls.crt"), "-noout", "-text"],
                          capture_output=True, text=True).stdout
     assert "DNS:bgc-admission.bgc.svc" in txt and "IP Address:127.0.0.1" in txt
+
+
+def test_workqueue_many_workers_no_lost_wakeups(nat):
+    """8 workers, 600 keys with mixed immediate/delayed due times, re-adds while in flight:
+    every key is processed, never by two workers at once, and nothing waits past its due
+    time by more than a scheduling slack (one timer waiter, no thundering herd)."""
+    import random
+
+    q = nat.WorkQueue()
+    rnd = random.Random(7)
+    due = {}
+    t0 = time.time()
+    for i in range(600):
+        d = rnd.choice([0, 0, 5, 20, 60])
+        due[f"k{i}"] = t0 + d / 1000.0
+        q.add_after(f"k{i}", d)
+    seen, late, active, lock = {}, [], set(), threading.Lock()
+    readded = set()
+
+    def worker():
+        while True:
+            k = q.get()
+            if k is None:
+                return
+            now = time.time()
+            with lock:
+                assert k not in active
+                active.add(k)
+                seen[k] = seen.get(k, 0) + 1
+                late.append(now - due[k])
+                again = k not in readded and int(k[1:]) % 10 == 0
+                if again:
+                    readded.add(k)
+                    due[k] = now  # deferred re-add while in flight runs right after done()
+            if again:
+                q.add(k)
+            time.sleep(0.0005)
+            with lock:
+                active.discard(k)
+            q.done(k)
+
+    threads = [threading.Thread(target=worker) for _ in range(8)]
+    for th in threads:
+        th.start()
+    deadline = time.time() + 10
+    while time.time() < deadline and (len(seen) < 600 or sum(seen.values()) < 660 or q.pending()):
+        time.sleep(0.01)
+    q.shutdown()
+    for th in threads:
+        th.join(5)
+    assert len(seen) == 600 and sum(seen.values()) == 660
+    late.sort()
+    assert late[len(late) // 2] < 0.05 and late[-1] < 1.0
