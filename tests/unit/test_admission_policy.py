@@ -171,6 +171,8 @@ def test_http_review_invalid_echoes_uid(nat, cfg):
     ("{}", "text/plain", 415),
     ('{"request": {"uid": "x"}}', "application/json", 422),
     ('{"request": {"uid":"x","kind":{},"resource":{},"operation":"PATCH","userInfo":{}}}', "application/json", 422),
+    ('{"request": ' + "[" * 5000 + "]" * 5000 + "}", "application/json", 400),  # nesting past the parser's depth cap
+    ('{"request": {"object": ' + '{"a":' * 600 + "1" + "}" * 600 + "}}", "application/json", 400),
 ])
 def test_http_review_rejections(nat, cfg, body, ctype, code):
     assert nat.admission_handle_review(body, ctype, cfg)[0] == code
