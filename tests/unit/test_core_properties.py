@@ -1,0 +1,75 @@
+"""Property-based tests of the native core codecs (hypothesis): JSON parse/dump, the
+serde_yaml-style YAML emitter against our parser and PyYAML, and RFC 7386 merge patch
+against an independent Python implementation."""
+import json
+import string
+
+import pytest
+import yaml
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+I64 = st.integers(min_value=-(2 ** 63), max_value=2 ** 63 - 1)
+U64_HI = st.integers(min_value=2 ** 63, max_value=2 ** 64 - 1)
+FLOATS = st.floats(allow_nan=False, allow_infinity=False, width=64)
+TEXT = st.text(max_size=20)
+KEYS = st.text(max_size=8)
+
+
+def json_values(leaf):
+    return st.recursive(leaf, lambda kids: st.lists(kids, max_size=4) | st.dictionaries(KEYS, kids, max_size=4),
+                        max_leaves=25)
+
+
+@settings(max_examples=300, deadline=None)
+@given(json_values(st.none() | st.booleans() | I64 | U64_HI | FLOATS | TEXT))
+def test_json_roundtrip_matches_python(nat, v):
+    assert json.loads(nat.json_roundtrip(json.dumps(v))) == v
+
+
+@settings(max_examples=200, deadline=None)
+@given(json_values(st.none() | st.booleans() | I64 | TEXT))
+def test_yaml_emit_parses_back_with_our_parser(nat, v):
+    assert json.loads(nat.yaml_to_json(nat.json_to_yaml(json.dumps(v)))) == v
+
+
+SAFE = st.text(alphabet=string.ascii_letters + string.digits + " -_./:", min_size=1, max_size=16).filter(
+    lambda s: s.lower() not in {"y", "n", "yes", "no", "on", "off", "true", "false", "null", "~"})
+
+
+@settings(max_examples=200, deadline=None)
+@given(json_values(st.none() | st.booleans() | st.integers(min_value=-10 ** 9, max_value=10 ** 9) | SAFE))
+def test_yaml_emit_loads_in_pyyaml(nat, v):
+    # YAML 1.1/1.2-neutral scalars: PyYAML (1.1) must read exactly what we emitted
+    assert yaml.safe_load(nat.json_to_yaml(json.dumps(v))) == v
+
+
+def merge_patch_ref(target, patch):
+    """RFC 7386 section 2, literally."""
+    if not isinstance(patch, dict):
+        return patch
+    if not isinstance(target, dict):
+        target = {}
+    out = dict(target)
+    for k, v in patch.items():
+        if v is None:
+            out.pop(k, None)
+        else:
+            out[k] = merge_patch_ref(out.get(k), v)
+    return out
+
+
+@settings(max_examples=300, deadline=None)
+@given(json_values(st.none() | st.booleans() | I64 | TEXT), json_values(st.none() | st.booleans() | I64 | TEXT))
+def test_merge_patch_matches_rfc7386(nat, doc, patch):
+    got = json.loads(nat.apply_merge_patch(json.dumps(doc), json.dumps(patch)))
+    assert got == merge_patch_ref(doc, patch)
+
+
+@pytest.mark.parametrize("text", ["1e400", "-1e400"])
+def test_json_out_of_range_numbers_rejected_or_finite(nat, text):
+    try:
+        out = json.loads(nat.json_roundtrip(text))
+    except ValueError:
+        return
+    assert out not in (float("inf"), float("-inf"))
