@@ -1,0 +1,88 @@
+// controller: watches UserBootstraps (+ owned Namespaces, ResourceQuotas, Roles,
+// RoleBindings) and reconciles them; serves /health, /metrics on CONF_LISTEN_ADDR:PORT.
+// Reference: src/controller.rs:215-287.
+#include <cstdio>
+#include <memory>
+
+#include "controller/reconcile.h"
+#include "core/cancel.h"
+#include "core/env_config.h"
+#include "core/http.h"
+#include "core/log.h"
+#include "core/metrics.h"
+#include "core/process.h"
+#include "kube/leader.h"
+#include "kube/runtime.h"
+
+using namespace bgc;
+
+int main() {
+  process_init();
+  controller::Config cfg;
+  try {
+    cfg = controller::Config::from_env(EnvConfig("CONF_"));
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "Error: %s\n", e.what());
+    return 1;
+  }
+  auto stop = std::make_shared<CancelToken>();
+  install_shutdown_signals(stop);
+
+  std::unique_ptr<kube::KubeClient> client;
+  try {
+    client = std::make_unique<kube::KubeClient>(kube::KubeConfig::infer());
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "Error: failed to infer kubernetes config: %s\n", e.what());
+    return 1;
+  }
+
+  http::ServerOptions so;
+  so.addr = cfg.listen_addr;
+  so.port = cfg.listen_port;
+  so.name = "controller";
+  http::Server health(so);
+  http::add_standard_routes(health);
+  try {
+    health.start();
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "Error: %s\n", e.what());
+    return 1;
+  }
+  LOG_INFO("controller") << "starting server on " << cfg.listen_addr << ":" << health.port();
+
+  if (cfg.leader_election) {
+    kube::LeaderElector le(*client, cfg.lease_namespace, cfg.lease_name);
+    if (!le.acquire(*stop)) {
+      health.stop();
+      return 0;
+    }
+    le.keep_renewing(stop);
+  }
+
+  kube::Controller::Options co;
+  co.workers = cfg.workers;
+  co.child_delete_delay = std::chrono::milliseconds(cfg.child_delete_delay_ms);
+  kube::Controller ctrl(*client, kube::types::UserBootstrap, co);
+  ctrl.owns(kube::types::Namespace);
+  ctrl.owns(kube::types::ResourceQuota);
+  ctrl.owns(kube::types::Role);
+  ctrl.owns(kube::types::RoleBinding);
+  controller::Reconciler rec(*client, ctrl, cfg);
+  auto& echoes = metrics::Registry::global().counter(
+      "bgc_controller_own_write_events_total", "Child watch events dropped as echoes of our own applies");
+  ctrl.set_child_filter([&](const kube::ResourceType& rt, const json::Value& child) {
+    if (!rec.is_own_write(rt, child)) return true;
+    echoes.inc();
+    return false;
+  });
+  ctrl.set_child_deleted_hook([&](const kube::ResourceType& rt, const json::Value& child) {
+    rec.forget(rt, child);
+    return true;
+  });
+  ctrl.run(
+      *stop, [&](const kube::ObjPtr& o) { return rec.reconcile(o); },
+      [&](const kube::ObjPtr& o, const std::exception& e) { return rec.error_policy(o, e); });
+  health.stop(std::chrono::milliseconds(1000));
+  LOG_INFO("controller") << "controller gracefully shutted down";
+  return 0;
+}

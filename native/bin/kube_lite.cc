@@ -1,0 +1,110 @@
+// kube-lite: standalone in-memory Kubernetes API server (see apiserver/server.h).
+//
+//   kube-lite --port 0 --port-file /tmp/port --token-file tokens.csv
+//             --service-override bgc/bgc-admission=127.0.0.1:12321 --manifest crd.yaml
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "apiserver/server.h"
+#include "core/cancel.h"
+#include "core/http.h"
+#include "core/json.h"
+#include "core/log.h"
+#include "core/net.h"
+#include "core/process.h"
+#include "core/yaml.h"
+
+using namespace bgc;
+
+static void usage() {
+  std::fprintf(stderr,
+               "usage: kube-lite [--addr A] [--port P] [--port-file F] [--token-file F] [--no-anonymous]\n"
+               "                 [--tls-cert F --tls-key F] [--service-override ns/name=host:port]...\n"
+               "                 [--bookmark-ms N] [--history N] [--manifest file.{json,yaml}]...\n");
+}
+
+int main(int argc, char** argv) {
+  process_init();
+  apiserver::Options o;
+  std::string port_file;
+  std::vector<std::string> manifests;
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    auto next = [&]() -> std::string {
+      if (i + 1 >= argc) {
+        usage();
+        std::exit(2);
+      }
+      return argv[++i];
+    };
+    if (a == "--addr") o.addr = next();
+    else if (a == "--port") o.port = static_cast<uint16_t>(std::atoi(next().c_str()));
+    else if (a == "--port-file") port_file = next();
+    else if (a == "--token-file") o.token_file = next();
+    else if (a == "--no-anonymous") o.anonymous_admin = false;
+    else if (a == "--tls-cert") o.tls_cert_file = next();
+    else if (a == "--tls-key") o.tls_key_file = next();
+    else if (a == "--bookmark-ms") o.bookmark_interval_ms = std::atoi(next().c_str());
+    else if (a == "--history") o.history_limit = static_cast<size_t>(std::atol(next().c_str()));
+    else if (a == "--manifest") manifests.push_back(next());
+    else if (a == "--service-override") {
+      std::string v = next();
+      size_t eq = v.find('=');
+      if (eq == std::string::npos) {
+        usage();
+        return 2;
+      }
+      o.service_overrides[v.substr(0, eq)] = v.substr(eq + 1);
+    } else if (a == "-h" || a == "--help") {
+      usage();
+      return 0;
+    } else {
+      usage();
+      return 2;
+    }
+  }
+  auto stop = std::make_shared<CancelToken>();
+  install_shutdown_signals(stop);
+  apiserver::ApiServer srv(o);
+  try {
+    srv.start();
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "Error: %s\n", e.what());
+    return 1;
+  }
+  std::string base = std::string(o.tls_cert_file.empty() ? "http" : "https") + "://" + o.addr + ":" +
+                     std::to_string(srv.port());
+  // preload manifests (e.g. the CRD) through the regular API
+  for (const auto& m : manifests) {
+    std::string text = net::read_file(m);
+    std::vector<json::Value> docs;
+    if (!text.empty() && text[0] == '{') docs.push_back(json::parse(text));
+    else docs = yaml::parse_all(text);
+    for (const auto& d : docs) {
+      std::string api_version = d.get_string("apiVersion");
+      std::string kind = d.get_string("kind");
+      std::string plural;
+      for (char c : kind) plural.push_back(static_cast<char>(std::tolower(static_cast<unsigned char>(c))));
+      plural += plural.back() == 's' ? "es" : (plural.back() == 'y' ? "" : "s");
+      if (kind.back() == 'y') plural = plural.substr(0, plural.size() - 1) + "ies";
+      std::string path = (api_version.find('/') == std::string::npos ? "/api/" : "/apis/") + api_version + "/" + plural;
+      auto r = http::fetch("POST", "http://127.0.0.1:" + std::to_string(srv.port()) + path, d.dump());
+      if (r.status >= 300) {
+        std::fprintf(stderr, "Error: manifest %s (%s): %d %s\n", m.c_str(), kind.c_str(), r.status, r.body.c_str());
+        return 1;
+      }
+    }
+  }
+  if (!port_file.empty()) {
+    net::write_file(port_file + ".tmp", std::to_string(srv.port()));
+    std::rename((port_file + ".tmp").c_str(), port_file.c_str());
+  }
+  LOG_INFO("apiserver") << "kube-lite serving on " << base;
+  stop->wait();
+  srv.stop();
+  return 0;
+}
