@@ -10,12 +10,15 @@
 #include <openssl/x509v3.h>
 #include <poll.h>
 #include <sys/socket.h>
+#include <sys/un.h>
 #include <unistd.h>
 
 #include <cerrno>
 #include <cstring>
 #include <fstream>
 #include <sstream>
+#include <thread>
+#include <chrono>
 
 namespace bgc::net {
 
@@ -378,6 +381,46 @@ int listen_tcp(const std::string& addr, uint16_t port, int backlog, uint16_t* bo
     getsockname(fd, reinterpret_cast<sockaddr*>(&ss), &len);
     if (ss.ss_family == AF_INET) *bound_port = ntohs(reinterpret_cast<sockaddr_in*>(&ss)->sin_port);
     else *bound_port = ntohs(reinterpret_cast<sockaddr_in6*>(&ss)->sin6_port);
+  }
+  return fd;
+}
+
+
+static sockaddr_un unix_addr(const std::string& path) {
+  sockaddr_un sa{};
+  sa.sun_family = AF_UNIX;
+  if (path.size() >= sizeof(sa.sun_path)) throw NetError("unix socket path too long: " + path);
+  std::memcpy(sa.sun_path, path.data(), path.size());
+  return sa;
+}
+
+int connect_unix(const std::string& path, int timeout_ms) {
+  sockaddr_un sa = unix_addr(path);
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+  while (true) {
+    int fd = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+    if (fd < 0) throw NetError(std::string("socket: ") + std::strerror(errno));
+    if (::connect(fd, reinterpret_cast<sockaddr*>(&sa), sizeof(sa)) == 0) return fd;
+    int e = errno;
+    ::close(fd);
+    // The listener may be between unlink and bind (kubelet restart): retry until the deadline.
+    if ((e == ENOENT || e == ECONNREFUSED || e == EAGAIN) && std::chrono::steady_clock::now() < deadline) {
+      std::this_thread::sleep_for(std::chrono::milliseconds(20));
+      continue;
+    }
+    throw NetError("connect " + path + ": " + std::strerror(e));
+  }
+}
+
+int listen_unix(const std::string& path, int backlog) {
+  sockaddr_un sa = unix_addr(path);
+  ::unlink(path.c_str());
+  int fd = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  if (fd < 0) throw NetError(std::string("socket: ") + std::strerror(errno));
+  if (::bind(fd, reinterpret_cast<sockaddr*>(&sa), sizeof(sa)) != 0 || ::listen(fd, backlog) != 0) {
+    int e = errno;
+    ::close(fd);
+    throw NetError("listen " + path + ": " + std::strerror(e));
   }
   return fd;
 }

@@ -95,6 +95,10 @@ class TlsStream : public Stream {
 int connect_tcp(const std::string& host, uint16_t port, int timeout_ms);
 // Listens; port 0 picks an ephemeral port (returned through bound_port).
 int listen_tcp(const std::string& addr, uint16_t port, int backlog, uint16_t* bound_port);
+// Unix-domain stream sockets (kubelet device-plugin gRPC).  listen_unix unlinks a stale
+// socket file first; both throw NetError.
+int connect_unix(const std::string& path, int timeout_ms);
+int listen_unix(const std::string& path, int backlog);
 
 std::string ssl_errors();
 std::string read_file(const std::string& path);

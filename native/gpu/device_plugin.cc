@@ -1,0 +1,579 @@
+#include "gpu/device_plugin.h"
+
+#include <dirent.h>
+#include <sys/stat.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <set>
+#include <stdexcept>
+
+#include "core/log.h"
+#include "core/metrics.h"
+#include "core/protobuf.h"
+
+namespace bgc::gpu {
+
+// ------------------------------------------------------------------ wire codecs
+namespace dp {
+
+using pb::Reader;
+using pb::Writer;
+
+std::string encode_options(bool pre_start_required, bool get_preferred_allocation_available) {
+  Writer w;
+  w.boolean(1, pre_start_required);
+  w.boolean(2, get_preferred_allocation_available);
+  return w.take();
+}
+
+std::string encode_register_request(const RegisterRequest& r) {
+  Writer w;
+  w.str(1, r.version);
+  w.str(2, r.endpoint);
+  w.str(3, r.resource_name);
+  Writer o;
+  o.boolean(1, r.pre_start_required);
+  o.boolean(2, r.get_preferred_allocation_available);
+  w.message(4, o);
+  return w.take();
+}
+
+RegisterRequest decode_register_request(std::string_view buf) {
+  RegisterRequest r;
+  Reader rd(buf);
+  while (rd.next()) {
+    switch (rd.field()) {
+      case 1: r.version = rd.string_value(); break;
+      case 2: r.endpoint = rd.string_value(); break;
+      case 3: r.resource_name = rd.string_value(); break;
+      case 4: {
+        Reader o(rd.bytes_value());
+        while (o.next()) {
+          if (o.field() == 1) r.pre_start_required = o.bool_value();
+          else if (o.field() == 2) r.get_preferred_allocation_available = o.bool_value();
+        }
+        break;
+      }
+      default: break;
+    }
+  }
+  return r;
+}
+
+std::string encode_list_and_watch(const std::vector<Device>& devices) {
+  Writer w;
+  for (const auto& d : devices) {
+    Writer dw;
+    dw.str(1, d.id);
+    dw.str(2, d.healthy ? kHealthy : kUnhealthy);
+    if (!d.numa_nodes.empty()) {
+      Writer topo;
+      for (int64_t n : d.numa_nodes) {
+        Writer node;
+        node.i64(1, n);
+        topo.message(1, node);
+      }
+      dw.message(3, topo);
+    }
+    w.message(1, dw);
+  }
+  return w.take();
+}
+
+std::vector<Device> decode_list_and_watch(std::string_view buf) {
+  std::vector<Device> out;
+  Reader rd(buf);
+  while (rd.next()) {
+    if (rd.field() != 1) continue;
+    Device d;
+    Reader dr(rd.bytes_value());
+    while (dr.next()) {
+      if (dr.field() == 1) {
+        d.id = dr.string_value();
+      } else if (dr.field() == 2) {
+        d.healthy = dr.string_value() == kHealthy;
+      } else if (dr.field() == 3) {
+        Reader tr(dr.bytes_value());
+        while (tr.next()) {
+          if (tr.field() != 1) continue;
+          int64_t id = 0;
+          Reader nr(tr.bytes_value());
+          while (nr.next())
+            if (nr.field() == 1) id = nr.int64_value();
+          d.numa_nodes.push_back(id);
+        }
+      }
+    }
+    out.push_back(std::move(d));
+  }
+  return out;
+}
+
+static std::vector<std::string> read_strings(std::string_view buf, uint32_t field) {
+  std::vector<std::string> out;
+  Reader r(buf);
+  while (r.next())
+    if (r.field() == field) out.push_back(r.string_value());
+  return out;
+}
+
+std::string encode_allocate_request(const std::vector<std::vector<std::string>>& containers) {
+  Writer w;
+  for (const auto& ids : containers) {
+    Writer c;
+    for (const auto& id : ids) c.bytes(1, id);
+    w.message(1, c);
+  }
+  return w.take();
+}
+
+std::vector<std::vector<std::string>> decode_allocate_request(std::string_view buf) {
+  std::vector<std::vector<std::string>> out;
+  Reader r(buf);
+  while (r.next())
+    if (r.field() == 1) out.push_back(read_strings(r.bytes_value(), 1));
+  return out;
+}
+
+std::string encode_allocate_response(const std::vector<ContainerAllocation>& containers) {
+  Writer w;
+  for (const auto& c : containers) {
+    Writer cw;
+    for (const auto& [k, v] : c.envs) cw.map_entry(1, k, v);
+    for (const auto& m : c.mounts) {
+      Writer mw;
+      mw.str(1, m.container_path);
+      mw.str(2, m.host_path);
+      mw.boolean(3, m.read_only);
+      cw.message(2, mw);
+    }
+    for (const auto& d : c.devices) {
+      Writer dw;
+      dw.str(1, d.container_path);
+      dw.str(2, d.host_path);
+      dw.str(3, d.permissions);
+      cw.message(3, dw);
+    }
+    for (const auto& [k, v] : c.annotations) cw.map_entry(4, k, v);
+    w.message(1, cw);
+  }
+  return w.take();
+}
+
+std::vector<ContainerAllocation> decode_allocate_response(std::string_view buf) {
+  std::vector<ContainerAllocation> out;
+  Reader r(buf);
+  while (r.next()) {
+    if (r.field() != 1) continue;
+    ContainerAllocation c;
+    Reader cr(r.bytes_value());
+    while (cr.next()) {
+      switch (cr.field()) {
+        case 1: c.envs.insert(pb::read_map_entry(cr.bytes_value())); break;
+        case 4: c.annotations.insert(pb::read_map_entry(cr.bytes_value())); break;
+        case 2: {
+          Mount m;
+          Reader mr(cr.bytes_value());
+          while (mr.next()) {
+            if (mr.field() == 1) m.container_path = mr.string_value();
+            else if (mr.field() == 2) m.host_path = mr.string_value();
+            else if (mr.field() == 3) m.read_only = mr.bool_value();
+          }
+          c.mounts.push_back(std::move(m));
+          break;
+        }
+        case 3: {
+          DeviceSpec d;
+          Reader dr(cr.bytes_value());
+          while (dr.next()) {
+            if (dr.field() == 1) d.container_path = dr.string_value();
+            else if (dr.field() == 2) d.host_path = dr.string_value();
+            else if (dr.field() == 3) d.permissions = dr.string_value();
+          }
+          c.devices.push_back(std::move(d));
+          break;
+        }
+        default: break;
+      }
+    }
+    out.push_back(std::move(c));
+  }
+  return out;
+}
+
+std::string encode_preferred_request(const std::vector<PreferredRequest>& reqs) {
+  Writer w;
+  for (const auto& q : reqs) {
+    Writer c;
+    for (const auto& id : q.available) c.bytes(1, id);
+    for (const auto& id : q.must_include) c.bytes(2, id);
+    c.i32(3, q.size);
+    w.message(1, c);
+  }
+  return w.take();
+}
+
+std::vector<PreferredRequest> decode_preferred_request(std::string_view buf) {
+  std::vector<PreferredRequest> out;
+  Reader r(buf);
+  while (r.next()) {
+    if (r.field() != 1) continue;
+    PreferredRequest q;
+    Reader cr(r.bytes_value());
+    while (cr.next()) {
+      if (cr.field() == 1) q.available.push_back(cr.string_value());
+      else if (cr.field() == 2) q.must_include.push_back(cr.string_value());
+      else if (cr.field() == 3) q.size = static_cast<int32_t>(cr.int64_value());
+    }
+    out.push_back(std::move(q));
+  }
+  return out;
+}
+
+std::string encode_preferred_response(const std::vector<std::vector<std::string>>& per_container) {
+  Writer w;
+  for (const auto& ids : per_container) {
+    Writer c;
+    for (const auto& id : ids) c.bytes(1, id);
+    w.message(1, c);
+  }
+  return w.take();
+}
+
+std::vector<std::vector<std::string>> decode_preferred_response(std::string_view buf) {
+  return decode_allocate_request(buf);  // same shape: repeated {repeated string = 1} = 1
+}
+
+}  // namespace dp
+
+// ------------------------------------------------------------------ allocation policy
+std::vector<std::string> preferred_allocation(const std::vector<GpuInfo>& gpus, const std::vector<std::string>& ids,
+                                              const std::vector<std::string>& available,
+                                              const std::vector<std::string>& must_include, int size) {
+  std::map<std::string, size_t> pos;
+  for (size_t i = 0; i < ids.size() && i < gpus.size(); ++i) pos[ids[i]] = i;
+  std::vector<std::string> out;
+  std::set<std::string> taken;
+  for (const auto& id : must_include) {
+    if (static_cast<int>(out.size()) >= size) break;
+    if (taken.insert(id).second) out.push_back(id);
+  }
+  int need = size - static_cast<int>(out.size());
+  if (need <= 0) return out;
+
+  // Candidates grouped by hive; unknown ids (not ours) go last in their given order.
+  std::map<uint64_t, std::vector<size_t>> by_hive;
+  std::vector<std::string> unknown;
+  for (const auto& id : available) {
+    if (taken.count(id)) continue;
+    auto it = pos.find(id);
+    if (it == pos.end()) {
+      unknown.push_back(id);
+      continue;
+    }
+    by_hive[gpus[it->second].xgmi_hive_id].push_back(it->second);
+  }
+  // Hive and NUMA of the must-include set pull the rest of the allocation toward them.
+  std::map<uint64_t, int> must_hive;
+  std::map<int, int> must_numa;
+  for (const auto& id : out) {
+    auto it = pos.find(id);
+    if (it == pos.end()) continue;
+    must_hive[gpus[it->second].xgmi_hive_id]++;
+    must_numa[gpus[it->second].numa_node]++;
+  }
+  std::vector<uint64_t> hive_order;
+  for (auto& [h, v] : by_hive) hive_order.push_back(h);
+  auto fits = [&](uint64_t h) { return static_cast<int>(by_hive[h].size()) >= need; };
+  std::stable_sort(hive_order.begin(), hive_order.end(), [&](uint64_t a, uint64_t b) {
+    int ma = must_hive.count(a) ? must_hive[a] : 0, mb = must_hive.count(b) ? must_hive[b] : 0;
+    if (ma != mb) return ma > mb;                      // the must-include hive first
+    if (fits(a) != fits(b)) return fits(a);            // then hives that hold the whole request
+    if (fits(a)) return by_hive[a].size() < by_hive[b].size();  // best fit keeps big islands whole
+    return by_hive[a].size() > by_hive[b].size();      // else fewest hives: biggest first
+  });
+  for (uint64_t h : hive_order) {
+    auto& cand = by_hive[h];
+    // Within a hive: prefer the NUMA node of the must-include set, else the NUMA group that
+    // best fits what is still needed, then adjacent xGMI node ids.
+    std::map<int, int> numa_count;
+    for (size_t i : cand) numa_count[gpus[i].numa_node]++;
+    const int want = need;
+    std::stable_sort(cand.begin(), cand.end(), [&](size_t a, size_t b) {
+      const int na = gpus[a].numa_node, nb = gpus[b].numa_node;
+      if (na != nb) {
+        int ma = must_numa.count(na) ? must_numa[na] : 0, mb = must_numa.count(nb) ? must_numa[nb] : 0;
+        if (ma != mb) return ma > mb;
+        bool fa = numa_count[na] >= want, fb = numa_count[nb] >= want;
+        if (fa != fb) return fa;
+        if (fa && numa_count[na] != numa_count[nb]) return numa_count[na] < numa_count[nb];
+        if (!fa && numa_count[na] != numa_count[nb]) return numa_count[na] > numa_count[nb];
+        return na < nb;
+      }
+      if (gpus[a].xgmi_node_id != gpus[b].xgmi_node_id) return gpus[a].xgmi_node_id < gpus[b].xgmi_node_id;
+      return gpus[a].index < gpus[b].index;
+    });
+    for (size_t i : cand) {
+      if (need == 0) break;
+      out.push_back(ids[i]);
+      --need;
+    }
+    if (need == 0) break;
+  }
+  for (const auto& id : unknown) {
+    if (need == 0) break;
+    out.push_back(id);
+    --need;
+  }
+  return out;
+}
+
+// ------------------------------------------------------------------ plugin
+namespace {
+
+std::string join_path(const std::string& dir, const std::string& name) {
+  if (dir.empty()) return name;
+  return dir.back() == '/' ? dir + name : dir + "/" + name;
+}
+
+uint64_t inode_of(const std::string& path) {
+  struct stat st {};
+  return ::stat(path.c_str(), &st) == 0 ? static_cast<uint64_t>(st.st_ino) : 0;
+}
+
+std::string hex16(uint64_t v) {
+  char buf[32];
+  std::snprintf(buf, sizeof(buf), "%016llx", static_cast<unsigned long long>(v));
+  return buf;
+}
+
+// card* / renderD* names of a PCI function's DRM nodes (empty when sysfs lacks them).
+void drm_nodes(const std::string& sysfs_root, const std::string& bdf, std::string* card, std::string* render) {
+  if (bdf.empty()) return;
+  const std::string dir = sysfs_root + "/bus/pci/devices/" + bdf + "/drm";
+  DIR* d = ::opendir(dir.c_str());
+  if (!d) return;
+  while (dirent* e = ::readdir(d)) {
+    std::string n = e->d_name;
+    if (n.rfind("renderD", 0) == 0) *render = n;
+    else if (n.rfind("card", 0) == 0 && n.find('-') == std::string::npos) *card = n;
+  }
+  ::closedir(d);
+}
+
+}  // namespace
+
+DevicePlugin::DevicePlugin(std::vector<GpuInfo> gpus, DevicePluginConfig cfg)
+    : gpus_(std::move(gpus)), cfg_(std::move(cfg)), healthy_(gpus_.size(), true) {
+  for (const auto& g : gpus_) ids_.push_back(g.bdf.empty() ? "gpu-" + std::to_string(g.index) : g.bdf);
+}
+
+DevicePlugin::~DevicePlugin() { stop(); }
+
+std::string DevicePlugin::socket_path() const { return join_path(cfg_.plugin_dir, cfg_.socket_name); }
+
+std::vector<dp::Device> DevicePlugin::devices() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  std::vector<dp::Device> out;
+  for (size_t i = 0; i < gpus_.size(); ++i) {
+    dp::Device d;
+    d.id = ids_[i];
+    d.healthy = healthy_[i];
+    if (gpus_[i].numa_node >= 0) d.numa_nodes.push_back(gpus_[i].numa_node);
+    out.push_back(std::move(d));
+  }
+  return out;
+}
+
+void DevicePlugin::set_health(const std::vector<bool>& healthy) {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    bool changed = false;
+    for (size_t i = 0; i < healthy_.size() && i < healthy.size(); ++i) {
+      if (healthy_[i] != healthy[i]) {
+        healthy_[i] = healthy[i];
+        changed = true;
+        LOG_INFO("device_plugin") << cfg_.resource_name << " " << ids_[i] << " -> "
+                                  << (healthy[i] ? dp::kHealthy : dp::kUnhealthy);
+      }
+    }
+    if (!changed) return;
+    ++version_;
+  }
+  cv_.notify_all();
+}
+
+dp::ContainerAllocation DevicePlugin::allocate(const std::vector<std::string>& req_ids) const {
+  dp::ContainerAllocation c;
+  c.devices.push_back({"/dev/kfd", join_path(cfg_.dev_root, "kfd"), "rw"});
+  std::set<uint64_t> hives;
+  std::string id_list;
+  for (const auto& id : req_ids) {
+    auto it = std::find(ids_.begin(), ids_.end(), id);
+    if (it == ids_.end()) throw std::invalid_argument("unknown " + cfg_.resource_name + " device id " + id);
+    const GpuInfo& g = gpus_[static_cast<size_t>(it - ids_.begin())];
+    std::string card, render;
+    drm_nodes(cfg_.sysfs_root, g.bdf, &card, &render);
+    if (card.empty()) card = "card" + std::to_string(g.index);
+    if (render.empty()) render = "renderD" + std::to_string(128 + g.index);
+    c.devices.push_back({"/dev/dri/" + card, join_path(cfg_.dev_root, "dri/" + card), "rw"});
+    c.devices.push_back({"/dev/dri/" + render, join_path(cfg_.dev_root, "dri/" + render), "rw"});
+    hives.insert(g.xgmi_hive_id);
+    if (!id_list.empty()) id_list += ",";
+    id_list += id;
+  }
+  std::string hive_list;
+  for (uint64_t h : hives) hive_list += (hive_list.empty() ? "" : ",") + hex16(h);
+  c.envs["BGC_AMD_GPU_IDS"] = id_list;
+  c.envs["BGC_AMD_GPU_XGMI_HIVES"] = hive_list;
+  c.envs["BGC_AMD_GPU_SINGLE_XGMI_HIVE"] = hives.size() <= 1 ? "true" : "false";
+  return c;
+}
+
+grpc::Status DevicePlugin::list_and_watch(grpc::ServerCall& call) {
+  uint64_t sent = 0;
+  while (!call.cancelled() && !stop_.cancelled()) {
+    bool send = false;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait_for(lk, std::chrono::milliseconds(200), [&] { return version_ != sent || stop_.cancelled(); });
+      if (stop_.cancelled()) break;
+      if (version_ != sent) {
+        sent = version_;
+        send = true;
+      }
+    }
+    if (send && !call.send_message(dp::encode_list_and_watch(devices()))) break;
+  }
+  return grpc::Status::Ok();
+}
+
+void DevicePlugin::start_server() {
+  auto srv = std::make_unique<grpc::Server>(socket_path());
+  srv->add("/v1beta1.DevicePlugin/GetDevicePluginOptions", [](grpc::ServerCall& call) {
+    call.send_message(dp::encode_options(false, true));
+    return grpc::Status::Ok();
+  });
+  srv->add("/v1beta1.DevicePlugin/ListAndWatch", [this](grpc::ServerCall& call) { return list_and_watch(call); });
+  srv->add("/v1beta1.DevicePlugin/GetPreferredAllocation", [this](grpc::ServerCall& call) {
+    std::vector<std::vector<std::string>> resp;
+    for (const auto& q : dp::decode_preferred_request(call.request()))
+      resp.push_back(preferred_allocation(gpus_, ids_, q.available, q.must_include, q.size));
+    call.send_message(dp::encode_preferred_response(resp));
+    return grpc::Status::Ok();
+  });
+  srv->add("/v1beta1.DevicePlugin/Allocate", [this](grpc::ServerCall& call) {
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<dp::ContainerAllocation> resp;
+    try {
+      for (const auto& ids : dp::decode_allocate_request(call.request())) resp.push_back(allocate(ids));
+    } catch (const std::invalid_argument& e) {
+      return grpc::Status{grpc::kInvalidArgument, e.what()};
+    }
+    call.send_message(dp::encode_allocate_response(resp));
+    allocations_.fetch_add(1);
+    metrics::Registry::global()
+        .histogram("device_plugin_allocate_duration_seconds", "kubelet Allocate RPC handling time")
+        .observe(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+    return grpc::Status::Ok();
+  });
+  srv->add("/v1beta1.DevicePlugin/PreStartContainer", [](grpc::ServerCall& call) {
+    call.send_message("");
+    return grpc::Status::Ok();
+  });
+  srv->start();
+  std::lock_guard<std::mutex> lk(server_mu_);
+  server_ = std::move(srv);
+}
+
+bool DevicePlugin::register_once() {
+  const std::string kubelet = join_path(cfg_.plugin_dir, cfg_.kubelet_socket);
+  dp::RegisterRequest r;
+  r.version = dp::kVersion;
+  r.endpoint = cfg_.socket_name;
+  r.resource_name = cfg_.resource_name;
+  r.pre_start_required = false;
+  r.get_preferred_allocation_available = true;
+  grpc::Channel ch(kubelet, 2000);
+  std::string resp;
+  grpc::Status st = ch.unary("/v1beta1.Registration/Register", dp::encode_register_request(r), &resp,
+                             std::chrono::seconds(5));
+  if (!st.ok()) {
+    LOG_WARN("device_plugin") << "register " << cfg_.resource_name << " with " << kubelet << " failed: " << st.message
+                              << " (code " << st.code << ")";
+    return false;
+  }
+  registrations_.fetch_add(1);
+  LOG_INFO("device_plugin") << "registered " << cfg_.resource_name << " (" << gpus_.size() << " devices) at "
+                            << socket_path();
+  return true;
+}
+
+void DevicePlugin::watch_loop() {
+  const std::string kubelet = join_path(cfg_.plugin_dir, cfg_.kubelet_socket);
+  do {
+    try {
+      bool present;
+      {
+        std::lock_guard<std::mutex> lk(server_mu_);
+        present = server_ && server_->socket_present();
+      }
+      if (!present) {  // kubelet restart wiped the directory: serve again, then re-register
+        LOG_WARN("device_plugin") << socket_path() << " disappeared; restarting the plugin server";
+        std::unique_ptr<grpc::Server> old;
+        {
+          std::lock_guard<std::mutex> lk(server_mu_);
+          old = std::move(server_);
+        }
+        if (old) old->stop();
+        start_server();
+        server_restarts_.fetch_add(1);
+        registered_ = false;
+      }
+      if (cfg_.register_with_kubelet) {
+        uint64_t ino = inode_of(kubelet);
+        if (ino && ino != kubelet_inode_) {
+          kubelet_inode_ = ino;
+          registered_ = false;  // a new kubelet instance
+        }
+        if (!registered_ && ino) registered_ = register_once();
+      }
+    } catch (const std::exception& e) {
+      LOG_ERROR("device_plugin") << "watch loop: " << e.what();
+    }
+  } while (!stop_.wait_for(std::chrono::milliseconds(cfg_.watch_interval_ms)));
+}
+
+void DevicePlugin::start() {
+  ::mkdir(cfg_.plugin_dir.c_str(), 0755);
+  start_server();
+  watcher_ = std::thread([this] { watch_loop(); });
+}
+
+void DevicePlugin::stop() {
+  stop_.cancel();
+  cv_.notify_all();
+  if (watcher_.joinable()) watcher_.join();
+  std::unique_ptr<grpc::Server> srv;
+  {
+    std::lock_guard<std::mutex> lk(server_mu_);
+    srv = std::move(server_);
+  }
+  if (srv) srv->stop();
+}
+
+json::Value DevicePlugin::describe() const {
+  json::Value devs = json::Value::array();
+  for (const auto& d : devices()) {
+    devs.push_back(json::Value::object({{"id", d.id}, {"health", d.healthy ? dp::kHealthy : dp::kUnhealthy}}));
+  }
+  return json::Value::object({{"resource", cfg_.resource_name},
+                              {"socket", socket_path()},
+                              {"registrations", static_cast<unsigned long long>(registrations_.load())},
+                              {"server_restarts", static_cast<unsigned long long>(server_restarts_.load())},
+                              {"allocations", static_cast<unsigned long long>(allocations_.load())},
+                              {"devices", devs}});
+}
+
+}  // namespace bgc::gpu

@@ -30,6 +30,11 @@ NodeAgentConfig NodeAgentConfig::from_env(const EnvConfig& env) {
   c.run_diag = env.boolean_or("run_diag", false);
   c.diag_hbm_bytes = env.u64_or("diag_hbm_bytes", 1ULL << 30);
   c.create_node = env.boolean_or("create_node", false);
+  c.device_plugin = env.boolean_or("device_plugin", false);
+  c.device_plugin_dir = env.str_or("device_plugin_dir", c.device_plugin_dir);
+  c.device_plugin_socket = env.str_or("device_plugin_socket", c.device_plugin_socket);
+  c.dev_root = env.str_or("dev_root", c.dev_root);
+  c.sysfs_root = env.str_or("sysfs_root", c.sysfs_root);
   return c;
 }
 
@@ -107,8 +112,10 @@ Value node_labels_patch(const NodeAgentConfig& cfg, const std::vector<GpuInfo>& 
 Value node_status_patch(const NodeAgentConfig& cfg, const std::vector<GpuInfo>& gpus, int healthy,
                         const std::string& unhealthy_reason) {
   Value status = Value::object();
-  status["capacity"] = Value::object({{cfg.resource_name, std::to_string(gpus.size())}});
-  status["allocatable"] = Value::object({{cfg.resource_name, std::to_string(healthy)}});
+  if (!cfg.device_plugin) {  // with the device plugin the kubelet owns these counts
+    status["capacity"] = Value::object({{cfg.resource_name, std::to_string(gpus.size())}});
+    status["allocatable"] = Value::object({{cfg.resource_name, std::to_string(healthy)}});
+  }
   bool all_ok = healthy == static_cast<int>(gpus.size()) && !gpus.empty();
   Value cond = Value::object({{"type", "AMDGPUHealthy"},
                               {"status", all_ok ? "True" : "False"},
@@ -166,9 +173,20 @@ bool NodeAgent::node_up_to_date(const Value& node) const {
   if (labels.get_string(cfg_.label_prefix + ".count") != std::to_string(gpus_.size())) return false;
   int healthy = healthy_count(nullptr);
   if (labels.get_string(cfg_.label_prefix + ".healthy-count") != std::to_string(healthy)) return false;
+  if (cfg_.device_plugin) return true;
   const Value& st = node.get("status");
   return st.get("capacity").get_string(cfg_.resource_name) == std::to_string(gpus_.size()) &&
          st.get("allocatable").get_string(cfg_.resource_name) == std::to_string(healthy);
+}
+
+std::vector<bool> NodeAgent::healthy_flags() const {
+  auto snap = poller_ ? poller_->snapshot() : nullptr;
+  std::vector<bool> out(gpus_.size(), true);
+  for (size_t i = 0; i < gpus_.size(); ++i) {
+    if (snap && i < snap->health.size() && !snap->health[i].healthy) out[i] = false;
+    if (diag_.ran && i < diag_.per_gpu.size() && !diag_.per_gpu[i].get("passed").as_bool()) out[i] = false;
+  }
+  return out;
 }
 
 int NodeAgent::healthy_count(std::string* reason) const {
@@ -205,7 +223,19 @@ void NodeAgent::publish() {
 }
 
 void NodeAgent::start() {
+  if (cfg_.device_plugin) {
+    DevicePluginConfig pc;
+    pc.plugin_dir = cfg_.device_plugin_dir;
+    pc.socket_name = cfg_.device_plugin_socket;
+    pc.resource_name = cfg_.resource_name;
+    pc.dev_root = cfg_.dev_root;
+    pc.sysfs_root = cfg_.sysfs_root;
+    plugin_ = std::make_unique<DevicePlugin>(gpus_, pc);
+    plugin_->set_health(healthy_flags());
+    plugin_->start();
+  }
   poller_->on_health_change([this](const Snapshot&) {
+    if (plugin_) plugin_->set_health(healthy_flags());
     try {
       publish();
     } catch (const std::exception& e) {
@@ -261,6 +291,7 @@ void NodeAgent::start() {
 void NodeAgent::stop() {
   stop_.cancel();
   if (poller_) poller_->stop();
+  if (plugin_) plugin_->stop();
   if (heartbeat_.joinable()) heartbeat_.join();
   if (node_watch_.joinable()) node_watch_.join();
 }
@@ -281,6 +312,7 @@ Value NodeAgent::describe() const {
   out["healthy"] = healthy_count(&reason);
   out["unhealthy_reason"] = reason;
   out["diag"] = diag_.per_gpu;
+  if (plugin_) out["device_plugin"] = plugin_->describe();
   return out;
 }
 

@@ -26,6 +26,7 @@
 #include "core/env_config.h"
 #include "core/json.h"
 #include "gpu/device.h"
+#include "gpu/device_plugin.h"
 #include "gpu/telemetry.h"
 #include "kube/client.h"
 
@@ -47,6 +48,14 @@ struct NodeAgentConfig {
   bool run_diag = false;               // HIP HBM + MFMA check before advertising
   uint64_t diag_hbm_bytes = 1ULL << 30;
   bool create_node = false;            // test clusters without a kubelet
+  // Kubelet device plugin (gpu/device_plugin.h).  When on, the kubelet owns the
+  // amd.com/gpu capacity/allocatable counts, so the Node status patch carries only the
+  // AMDGPUHealthy condition; labels and topology are published as before.
+  bool device_plugin = false;
+  std::string device_plugin_dir = "/var/lib/kubelet/device-plugins";
+  std::string device_plugin_socket = "bgc-amd-gpu.sock";
+  std::string dev_root = "/dev";
+  std::string sysfs_root = "/sys";
   static NodeAgentConfig from_env(const EnvConfig& env);
 };
 
@@ -81,6 +90,9 @@ class NodeAgent {
   json::Value describe() const;  // for GET /gpus
   const std::vector<GpuInfo>& gpus() const { return gpus_; }
   TelemetryPoller* poller() { return poller_.get(); }
+  DevicePlugin* device_plugin() { return plugin_.get(); }
+  // Per-GPU health: telemetry state machine AND (when run) the HIP diagnostics.
+  std::vector<bool> healthy_flags() const;
 
  private:
   int healthy_count(std::string* reason) const;
@@ -90,6 +102,7 @@ class NodeAgent {
   std::vector<GpuInfo> gpus_;
   DiagOutcome diag_;
   std::unique_ptr<TelemetryPoller> poller_;
+  std::unique_ptr<DevicePlugin> plugin_;
   std::mutex publish_mu_;
   CancelToken stop_;
   std::thread heartbeat_;

@@ -1,0 +1,250 @@
+"""Native kubelet device plugin (native/gpu/device_plugin.cc over core/http2.cc) against a
+fake kubelet written with python grpcio — an independent HTTP/2 + gRPC + protobuf stack,
+as grpc-go is in a real kubelet.
+
+Covers: registration, ListAndWatch (initial list, health flips), Allocate (device nodes
+from sysfs, envs), GetPreferredAllocation (xGMI packing), errors as gRPC statuses, kubelet
+restart (directory wipe -> re-serve + re-register), concurrent calls, responses larger
+than the peer's flow-control window, and the node agent running the plugin."""
+import json
+import os
+import threading
+import time
+
+import grpc
+import pytest
+
+from bacchus_gpu_controller_amd.testing.cluster import Cluster
+from bacchus_gpu_controller_amd.testing.kubeapi import wait_for
+from bacchus_gpu_controller_amd.testing.kubelet import FakeKubelet, PluginClient, pb
+
+pytestmark = pytest.mark.slow
+
+
+@pytest.fixture
+def plugin_env(nat, tmp_path):
+    d = str(tmp_path / "dp")
+    os.makedirs(d)
+    kubelet = FakeKubelet(d).start()
+    fixture = nat.default_mi355x_fixture(8)
+    plugin = nat.DevicePlugin(fixture, {"plugin_dir": d, "watch_interval_ms": "50",
+                                        "sysfs_root": str(tmp_path / "sys"), "dev_root": "/dev"})
+    yield kubelet, plugin, json.loads(fixture)["gpus"]
+    plugin.stop()
+    kubelet.stop()
+
+
+def test_register_list_allocate(plugin_env, tmp_path):
+    kubelet, plugin, gpus = plugin_env
+    # sysfs for gpu 2: the plugin must hand out *these* DRM nodes, not index-derived ones
+    drm = tmp_path / "sys" / "bus" / "pci" / "devices" / gpus[2]["bdf"] / "drm"
+    os.makedirs(drm / "card7")
+    os.makedirs(drm / "renderD135")
+    plugin.start()
+    assert kubelet.wait(lambda: kubelet.registrations and kubelet.device_lists)
+    reg = kubelet.registrations[0]
+    assert (reg.version, reg.endpoint, reg.resource_name) == ("v1beta1", "bgc-amd-gpu.sock", "amd.com/gpu")
+    assert reg.options.get_preferred_allocation_available and not reg.options.pre_start_required
+    endpoint, devs = kubelet.device_lists[-1]
+    assert [d[0] for d in devs] == [g["bdf"] for g in gpus]
+    assert all(d[1] == "Healthy" for d in devs)
+    assert [d[2] for d in devs] == [[g["numa_node"]] for g in gpus]
+
+    c = PluginClient(plugin.socket_path)
+    try:
+        opts = c.options(pb["Empty"](), timeout=5)
+        assert opts.get_preferred_allocation_available and not opts.pre_start_required
+        req = pb["AllocateRequest"]()
+        req.container_requests.add().devices_ids.extend([gpus[0]["bdf"], gpus[2]["bdf"]])
+        req.container_requests.add().devices_ids.extend([gpus[5]["bdf"]])
+        resp = c.allocate(req, timeout=5)
+        assert len(resp.container_responses) == 2
+        r0 = resp.container_responses[0]
+        paths = [(d.container_path, d.host_path, d.permissions) for d in r0.devices]
+        assert paths[0] == ("/dev/kfd", "/dev/kfd", "rw")
+        assert ("/dev/dri/card7", "/dev/dri/card7", "rw") in paths
+        assert ("/dev/dri/renderD135", "/dev/dri/renderD135", "rw") in paths
+        assert ("/dev/dri/renderD128", "/dev/dri/renderD128", "rw") in paths  # no sysfs entry: index-derived
+        assert r0.envs["BGC_AMD_GPU_IDS"] == f"{gpus[0]['bdf']},{gpus[2]['bdf']}"
+        assert r0.envs["BGC_AMD_GPU_SINGLE_XGMI_HIVE"] == "true"
+        assert r0.envs["BGC_AMD_GPU_XGMI_HIVES"] == gpus[0]["xgmi_hive_id"]
+
+        q = pb["PreferredAllocationRequest"]()
+        cq = q.container_requests.add()
+        cq.available_deviceIDs.extend([g["bdf"] for g in gpus])
+        cq.must_include_deviceIDs.append(gpus[6]["bdf"])
+        cq.allocation_size = 4
+        pref = c.preferred(q, timeout=5).container_responses[0].deviceIDs
+        assert pref[0] == gpus[6]["bdf"] and set(pref) == {g["bdf"] for g in gpus[4:8]}  # NUMA 1 quad
+
+        c.prestart(pb["PreStartContainerRequest"](devices_ids=[gpus[0]["bdf"]]), timeout=5)
+
+        bad = pb["AllocateRequest"]()
+        bad.container_requests.add().devices_ids.append("0000:ff:00.0")
+        with pytest.raises(grpc.RpcError) as ei:
+            c.allocate(bad, timeout=5)
+        assert ei.value.code() == grpc.StatusCode.INVALID_ARGUMENT
+        assert "0000:ff:00.0" in ei.value.details()
+    finally:
+        c.close()
+
+
+def test_health_flip_resends_list(plugin_env):
+    kubelet, plugin, gpus = plugin_env
+    plugin.start()
+    assert kubelet.wait(lambda: kubelet.device_lists)
+    n0 = len(kubelet.device_lists)
+    plugin.set_health([i != 3 for i in range(8)])
+    assert kubelet.wait(lambda: len(kubelet.device_lists) > n0)
+    devs = kubelet.device_lists[-1][1]
+    assert [d[1] for d in devs] == ["Healthy"] * 3 + ["Unhealthy"] + ["Healthy"] * 4
+    plugin.set_health([True] * 8)
+    assert kubelet.wait(lambda: all(d[1] == "Healthy" for d in kubelet.device_lists[-1][1]))
+
+
+def test_kubelet_restart_reregisters(plugin_env):
+    kubelet, plugin, gpus = plugin_env
+    plugin.start()
+    assert kubelet.wait(lambda: len(kubelet.registrations) == 1)
+    wait_for(lambda: plugin.registrations == 1, timeout=10, desc="first registration acknowledged")
+    kubelet.restart()  # wipes the directory, including the plugin's socket
+    assert kubelet.wait(lambda: len(kubelet.registrations) >= 2, timeout=15)
+    wait_for(lambda: plugin.registrations >= 2, timeout=10, desc="plugin saw its re-registration succeed")
+    assert plugin.server_restarts >= 1
+    n = len(kubelet.device_lists)
+    assert kubelet.wait(lambda: len(kubelet.device_lists) > n or n > 0)
+    assert os.path.exists(plugin.socket_path)
+
+
+def test_registration_retries_until_kubelet_appears(nat, tmp_path):
+    d = str(tmp_path / "dp")
+    os.makedirs(d)
+    plugin = nat.DevicePlugin(nat.default_mi355x_fixture(2), {"plugin_dir": d, "watch_interval_ms": "50"})
+    plugin.start()
+    try:
+        time.sleep(0.3)
+        assert plugin.registrations == 0
+        kubelet = FakeKubelet(d).start()
+        try:
+            assert kubelet.wait(lambda: kubelet.registrations and kubelet.device_lists)
+            assert len(kubelet.device_lists[-1][1]) == 2
+        finally:
+            kubelet.stop()
+    finally:
+        plugin.stop()
+
+
+def test_concurrent_calls_and_large_responses(plugin_env, nat):
+    kubelet, plugin, gpus = plugin_env
+    plugin.start()
+    ids = [g["bdf"] for g in gpus]
+    errors = []
+
+    def worker(k):
+        c = PluginClient(plugin.socket_path)
+        try:
+            for i in range(40):
+                req = pb["AllocateRequest"]()
+                req.container_requests.add().devices_ids.append(ids[(k + i) % 8])
+                r = c.allocate(req, timeout=10)
+                assert r.container_responses[0].envs["BGC_AMD_GPU_IDS"] == ids[(k + i) % 8]
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+        finally:
+            c.close()
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(60)
+    assert not errors, errors[:3]
+
+    # ~500 KB response: far beyond the 64 KiB default window, so our sender must honour
+    # the peer's WINDOW_UPDATEs (unknown ids are allowed in `available` and fill the tail)
+    many = [f"extra-device-{i:06d}" for i in range(30000)]
+    q = pb["PreferredAllocationRequest"]()
+    cq = q.container_requests.add()
+    cq.available_deviceIDs.extend(ids + many)
+    cq.allocation_size = len(ids) + len(many)
+    c = PluginClient(plugin.socket_path)
+    try:
+        got = list(c.preferred(q, timeout=20).container_responses[0].deviceIDs)
+    finally:
+        c.close()
+    assert len(got) == 30008 and set(got[:8]) == set(ids) and got[8:] == many
+
+
+def test_native_channel_against_grpcio_server(nat, tmp_path):
+    """Our gRPC client (used for Registration) against grpcio's server: unary, server
+    streaming with many messages, status propagation, deadline."""
+    from concurrent import futures
+
+    sock = str(tmp_path / "echo.sock")
+    srv = grpc.server(futures.ThreadPoolExecutor(max_workers=4))
+
+    def echo(req, ctx):
+        return req
+
+    def fail(req, ctx):
+        ctx.abort(grpc.StatusCode.FAILED_PRECONDITION, "nope: ünïcode")
+
+    def stream(req, ctx):
+        for i in range(int(req)):
+            yield f"msg-{i}".encode() * 100
+
+    def slow(req, ctx):
+        time.sleep(2)
+        return req
+
+    ident = (lambda b: b)
+    srv.add_generic_rpc_handlers((grpc.method_handlers_generic_handler("t.S", {
+        "Echo": grpc.unary_unary_rpc_method_handler(echo, ident, ident),
+        "Fail": grpc.unary_unary_rpc_method_handler(fail, ident, ident),
+        "Slow": grpc.unary_unary_rpc_method_handler(slow, ident, ident),
+        "Stream": grpc.unary_stream_rpc_method_handler(stream, ident, ident)}),))
+    srv.add_insecure_port("unix://" + sock)
+    srv.start()
+    try:
+        ch = nat.GrpcChannel(sock)
+        code, msg, body = ch.unary("/t.S/Echo", b"x" * 200000)
+        assert (code, msg) == (0, "") and body == b"x" * 200000
+        code, msg, _ = ch.unary("/t.S/Fail", b"")
+        assert code == 9 and msg == "nope: ünïcode"
+        code, msg, msgs = ch.server_stream("/t.S/Stream", b"500")
+        assert code == 0 and len(msgs) == 500 and msgs[499] == b"msg-499" * 100
+        code, msg, _ = ch.unary("/t.S/Missing", b"")
+        assert code == 12
+        code, msg, _ = ch.unary("/t.S/Slow", b"", timeout_ms=200)
+        assert code == 4
+        code, msg, body = ch.unary("/t.S/Echo", b"still-usable")
+        assert code == 0 and body == b"still-usable"
+        ch.close()
+    finally:
+        srv.stop(None)
+
+
+def test_node_agent_runs_device_plugin(tmp_path):
+    """CONF_DEVICE_PLUGIN=true: the kubelet gets amd.com/gpu through the plugin, so the
+    node agent leaves capacity/allocatable to it and keeps labels + condition; a GPU flap
+    reaches the kubelet as an Unhealthy device."""
+    d = str(tmp_path / "dp")
+    kubelet = FakeKubelet(d).start()
+    try:
+        with Cluster(admission=False, controller=False) as c:
+            c.start_node_agent(node_name="mi355x-dp", backend="mock", poll_interval_ms=50,
+                               extra_env={"CONF_DEVICE_PLUGIN": "true", "CONF_DEVICE_PLUGIN_DIR": d,
+                                          "CONF_HEARTBEAT_SECS": "1"})
+            assert kubelet.wait(lambda: kubelet.registrations and kubelet.device_lists, timeout=15)
+            assert len(kubelet.device_lists[-1][1]) == 8
+            node = wait_for(lambda: (lambda n: n if n and n.get("status", {}).get("conditions") else None)(
+                c.admin.get_or_none("nodes", "mi355x-dp")), timeout=10, desc="node condition published")
+            assert "amd.com/gpu" not in node["status"].get("capacity", {})
+            assert node["metadata"]["labels"]["amd.com/gpu.count"] == "8"
+            fx = json.loads(open(c.fixtures["mi355x-dp"]).read())
+            fx["gpus"][5]["telemetry"]["temp_hotspot_c"] = 125
+            c.set_gpu_fixture("mi355x-dp", fx)
+            assert kubelet.wait(lambda: kubelet.device_lists[-1][1][5][1] == "Unhealthy", timeout=15)
+            assert sum(x[1] == "Healthy" for x in kubelet.device_lists[-1][1]) == 7
+    finally:
+        kubelet.stop()

@@ -237,3 +237,19 @@ def test_values_and_name_parity_with_reference():
     with open(os.path.join(CHART, "Chart.yaml")) as f:
         our_chart = yaml.safe_load(f)
     assert our_chart["name"] == ref_chart["name"]
+
+
+def test_node_agent_device_plugin_wiring():
+    ds = by_kind(render({}), "DaemonSet")["bgc-bacchus-gpu-node-agent"]
+    spec = ds["spec"]["template"]["spec"]
+    c = spec["containers"][0]
+    env = {e["name"]: e.get("value") for e in c["env"]}
+    assert env["CONF_DEVICE_PLUGIN"] == "true"
+    assert env["CONF_DEVICE_PLUGIN_DIR"] == "/var/lib/kubelet/device-plugins"
+    assert {"name": "device-plugins", "mountPath": "/var/lib/kubelet/device-plugins"} in c["volumeMounts"]
+    assert {"name": "device-plugins", "hostPath": {"path": "/var/lib/kubelet/device-plugins"}} in spec["volumes"]
+    ds = by_kind(render({"nodeAgent": {"devicePlugin": {"enabled": False}}}), "DaemonSet")["bgc-bacchus-gpu-node-agent"]
+    c = ds["spec"]["template"]["spec"]["containers"][0]
+    env = {e["name"]: e.get("value") for e in c["env"]}
+    assert env["CONF_DEVICE_PLUGIN"] == "false" and "CONF_DEVICE_PLUGIN_DIR" not in env
+    assert all(m["name"] != "device-plugins" for m in c["volumeMounts"])
