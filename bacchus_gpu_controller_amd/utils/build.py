@@ -69,13 +69,20 @@ def build_hip(force=False):
 
 
 def ensure_built(hip=True):
-    build_core()
-    if hip:
-        try:
-            build_hip()
-        except (subprocess.CalledProcessError, FileNotFoundError) as e:  # pragma: no cover
-            print(f"warning: HIP build failed: {e}", file=sys.stderr)
-            raise
+    # pytest-xdist workers (and torchrun ranks) call this concurrently: serialize them,
+    # two ninja runs in one build directory race on the same outputs.
+    import fcntl
+
+    os.makedirs(BUILD_DIR, exist_ok=True)
+    with open(os.path.join(BUILD_DIR, ".build.lock"), "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        build_core()
+        if hip:
+            try:
+                build_hip()
+            except (subprocess.CalledProcessError, FileNotFoundError) as e:  # pragma: no cover
+                print(f"warning: HIP build failed: {e}", file=sys.stderr)
+                raise
 
 
 if __name__ == "__main__":
