@@ -46,6 +46,7 @@ class Dist:
             import torch
 
             self.torch = torch
+            torch.set_num_threads(1)  # ranks do no tensor math on the CPU: keep thread count low
             # BGC_BENCH_CPU=1: gloo and no device work, to rehearse several ranks on a box
             # with fewer GPUs than ranks
             self.cuda = os.environ.get("BGC_BENCH_CPU") != "1" and torch.cuda.is_available()

@@ -36,12 +36,20 @@ def free_port():
     return p
 
 
+# glibc malloc: a deeper per-thread cache (default 7 chunks per size class) keeps the
+# services' many short-lived JSON allocations off the shared arenas.  Measured on the
+# MI355X box: +14% CR/s, -12% control-plane CPU per CR (profiles/malloc_tunables_r1/).
+# The container image sets the same value (Dockerfile ENV).
+SERVICE_GLIBC_TUNABLES = "glibc.malloc.tcache_count=1024:glibc.malloc.tcache_max=16384"
+
+
 class Proc:
     def __init__(self, name, cmd, env, workdir):
         self.name = name
         self.log_path = os.path.join(workdir, f"{name}.log")
         self.log = open(self.log_path, "wb")
         full_env = dict(os.environ)
+        full_env.setdefault("GLIBC_TUNABLES", SERVICE_GLIBC_TUNABLES)
         full_env.update(env)
         self.p = subprocess.Popen(cmd, env=full_env, stdout=self.log, stderr=subprocess.STDOUT,
                                   start_new_session=True)
