@@ -52,42 +52,56 @@ void collect(const Value& v, const std::string& path, FieldSet& out, bool includ
   if (!path.empty()) out.insert(path);
 }
 
-std::vector<std::string> split(const std::string& path) {
-  std::vector<std::string> toks;
-  size_t i = 1;
-  while (i <= path.size() && !path.empty()) {
-    size_t j = path.find('/', i);
-    std::string t = path.substr(i, j == std::string::npos ? std::string::npos : j - i);
-    // unescape
-    std::string u;
-    for (size_t k = 0; k < t.size(); ++k) {
-      if (t[k] == '~' && k + 1 < t.size()) {
-        u.push_back(t[k + 1] == '1' ? '/' : '~');
+// RFC 6901 tokens of a field path without allocating: a token is a view into the path,
+// unescaped into a scratch buffer only when it contains '~' (rare in field paths).
+class Tokens {
+ public:
+  explicit Tokens(std::string_view p) : p_(p), i_(p.empty() ? 1 : 1), end_(p.empty()) {}
+  bool next(std::string_view& tok) {
+    if (end_ || i_ > p_.size()) return false;
+    size_t j = p_.find('/', i_);
+    std::string_view raw = p_.substr(i_, j == std::string_view::npos ? std::string_view::npos : j - i_);
+    if (j == std::string_view::npos) end_ = true;
+    else i_ = j + 1;
+    if (raw.find('~') == std::string_view::npos) {
+      tok = raw;
+      return true;
+    }
+    scratch_.clear();
+    for (size_t k = 0; k < raw.size(); ++k) {
+      if (raw[k] == '~' && k + 1 < raw.size()) {
+        scratch_.push_back(raw[k + 1] == '1' ? '/' : '~');
         ++k;
       } else {
-        u.push_back(t[k]);
+        scratch_.push_back(raw[k]);
       }
     }
-    toks.push_back(u);
-    if (j == std::string::npos) break;
-    i = j + 1;
+    tok = scratch_;
+    return true;
   }
-  return toks;
-}
+  bool last() const { return end_; }  // after next(): the token just returned was the final one
 
-bool is_item_token(const std::string& t) { return t.size() >= 3 && t.front() == '[' && t.back() == ']'; }
+ private:
+  std::string_view p_;
+  size_t i_;
+  bool end_;
+  std::string scratch_;
+};
+
+bool is_item_token(std::string_view t) { return t.size() >= 3 && t.front() == '[' && t.back() == ']'; }
 
 // index of the list item matching an item token, or -1
-long find_item(const Value& arr, const std::string& tok) {
-  std::string inner = tok.substr(1, tok.size() - 2);
-  if (inner.rfind("uid=", 0) == 0) {
-    std::string uid = inner.substr(4);
+long find_item(const Value& arr, std::string_view tok) {
+  std::string_view inner = tok.substr(1, tok.size() - 2);
+  if (inner.substr(0, 4) == "uid=") {
+    std::string_view uid = inner.substr(4);
     for (size_t i = 0; i < arr.size(); ++i) {
-      if (arr[i].get_string("uid") == uid) return static_cast<long>(i);
+      const Value& u = arr[i].get("uid");
+      if (u.is_string() && u.as_string() == uid) return static_cast<long>(i);
     }
     return -1;
   }
-  if (inner.rfind("=", 0) == 0) {
+  if (!inner.empty() && inner.front() == '=') {
     Value want;
     if (!json::try_parse(inner.substr(1), want, nullptr)) return -1;
     for (size_t i = 0; i < arr.size(); ++i) {
@@ -107,7 +121,9 @@ FieldSet leaves(const Value& obj, bool include_status) {
 
 const Value* get_path(const Value& root, const std::string& path) {
   const Value* cur = &root;
-  for (const auto& t : split(path)) {
+  Tokens ts(path);
+  std::string_view t;
+  while (ts.next(t)) {
     if (is_item_token(t)) {
       if (!cur->is_array()) return nullptr;
       long i = find_item(*cur, t);
@@ -122,38 +138,35 @@ const Value* get_path(const Value& root, const std::string& path) {
 }
 
 bool remove_path(Value& root, const std::string& path) {
-  auto toks = split(path);
-  if (toks.empty()) return false;
   Value* cur = &root;
-  for (size_t k = 0; k + 1 < toks.size(); ++k) {
-    const auto& t = toks[k];
+  Tokens ts(path);
+  std::string_view t;
+  while (ts.next(t)) {
+    const bool last = ts.last();
     if (is_item_token(t)) {
       if (!cur->is_array()) return false;
       long i = find_item(*cur, t);
       if (i < 0) return false;
+      if (last) {
+        cur->erase_index(static_cast<size_t>(i));
+        return true;
+      }
       cur = &(*cur)[static_cast<size_t>(i)];
     } else {
+      if (last) return cur->erase(t);
       cur = cur->find_mut(t);
       if (!cur) return false;
     }
   }
-  const auto& last = toks.back();
-  if (is_item_token(last)) {
-    if (!cur->is_array()) return false;
-    long i = find_item(*cur, last);
-    if (i < 0) return false;
-    cur->erase_index(static_cast<size_t>(i));
-    return true;
-  }
-  return cur->erase(last);
+  return false;
 }
 
 void set_path(Value& root, const std::string& path, const Value& v) {
-  auto toks = split(path);
   Value* cur = &root;
-  for (size_t k = 0; k < toks.size(); ++k) {
-    const auto& t = toks[k];
-    bool last = k + 1 == toks.size();
+  Tokens ts(path);
+  std::string_view t;
+  while (ts.next(t)) {
+    const bool last = ts.last();
     if (is_item_token(t)) {
       if (!cur->is_array()) *cur = Value::array();
       long i = find_item(*cur, t);
@@ -190,9 +203,11 @@ void diff_leaves(const Value& before, const Value& after, FieldSet& changed, Fie
 
 std::string display_path(const std::string& path) {
   std::string out;
-  for (const auto& t : split(path)) {
-    if (is_item_token(t)) out += t;
-    else out += "." + t;
+  Tokens ts(path);
+  std::string_view t;
+  while (ts.next(t)) {
+    if (!is_item_token(t)) out += '.';
+    out.append(t.data(), t.size());
   }
   return out;
 }
@@ -201,14 +216,17 @@ Value fields_v1(const FieldSet& fs) {
   Value root = Value::object();
   for (const auto& p : fs) {
     Value* cur = &root;
-    for (const auto& t : split(p)) {
-      std::string key;
+    Tokens ts(p);
+    std::string_view t;
+    std::string key;
+    while (ts.next(t)) {
+      key.clear();
       if (is_item_token(t)) {
-        std::string inner = t.substr(1, t.size() - 2);
-        if (inner.rfind("uid=", 0) == 0) key = "k:{\"uid\":" + json::quote(inner.substr(4)) + "}";
-        else key = "v:" + inner.substr(1);
+        std::string_view inner = t.substr(1, t.size() - 2);
+        if (inner.substr(0, 4) == "uid=") key = "k:{\"uid\":" + json::quote(std::string(inner.substr(4))) + "}";
+        else key.append("v:").append(inner.substr(1));
       } else {
-        key = "f:" + t;
+        key.append("f:").append(t);
       }
       cur = &(*cur)[key];
       if (cur->is_null()) *cur = Value::object();

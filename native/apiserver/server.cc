@@ -457,6 +457,12 @@ struct ApiServer::Impl {
   std::vector<FaultRule> faults;
 
   std::mutex hook_mu;
+  struct FastHook {
+    std::shared_ptr<const Value> cfg;
+    std::shared_ptr<http::Client> client;
+    std::string path;
+  };
+  std::map<const Value*, FastHook> hook_fast;  // guarded by hook_mu
   std::map<std::string, std::shared_ptr<http::Client>> hook_clients;
 
   std::atomic<uint64_t> requests{0};
@@ -663,7 +669,8 @@ struct ApiServer::Impl {
   // ---------------------------------------------------------------- webhooks
   struct HookMatch {
     std::string name;
-    Value hook;
+    std::shared_ptr<const Value> cfg;  // keeps `hook` alive (stored objects are immutable)
+    const Value* hook;
   };
 
   std::vector<HookMatch> matching_webhooks(const TypeInfo& ti, const std::string& sub, const std::string& op) {
@@ -691,7 +698,7 @@ struct ApiServer::Impl {
           }
           if (contains(rule.get("apiGroups"), ti.rt.group) && contains(rule.get("apiVersions"), ti.rt.version) &&
               contains(rule.get("operations"), op) && res_ok) {
-            out.push_back({hook.get_string("name"), hook});
+            out.push_back({hook.get_string("name"), kv.second.obj, &hook});
             break;
           }
         }
@@ -700,7 +707,25 @@ struct ApiServer::Impl {
     return out;
   }
 
-  std::shared_ptr<http::Client> hook_client(const Value& hook, std::string& path_out) {
+  // Per-hook client cache keyed by the hook's address inside its (immutable, kept-alive)
+  // configuration object: no re-hashing of the caBundle per call.
+  std::shared_ptr<http::Client> hook_client(const HookMatch& hm, std::string& path_out) {
+    {
+      std::lock_guard<std::mutex> lk(hook_mu);
+      auto it = hook_fast.find(hm.hook);
+      if (it != hook_fast.end()) {
+        path_out = it->second.path;
+        return it->second.client;
+      }
+    }
+    auto c = hook_client_slow(*hm.hook, path_out);
+    std::lock_guard<std::mutex> lk(hook_mu);
+    if (hook_fast.size() > 256) hook_fast.clear();
+    hook_fast[hm.hook] = {hm.cfg, c, path_out};
+    return c;
+  }
+
+  std::shared_ptr<http::Client> hook_client_slow(const Value& hook, std::string& path_out) {
     const Value& cc = hook.get("clientConfig");
     std::string ca = cc.get_string("caBundle");
     std::string base, server_name;
@@ -741,41 +766,49 @@ struct ApiServer::Impl {
     static auto& ring = metrics::Registry::global().samples("webhook");
     static auto& hist = metrics::Registry::global().histogram("kl_webhook_duration_seconds", "Webhook callout latency");
     for (const auto& hm : hooks) {
-      const Value& hook = hm.hook;
+      const Value& hook = *hm.hook;
       std::string fail_policy = hook.get_string("failurePolicy", "Fail");
       int timeout_s = hook.get("timeoutSeconds").is_int() ? static_cast<int>(hook.get("timeoutSeconds").as_int()) : 10;
       std::string uid = crypto::uuid_v4();
-      Value req = Value::object();
-      req["uid"] = uid;
-      req["kind"] = Value::object({{"group", ti.rt.group}, {"version", ti.rt.version}, {"kind", ti.rt.kind}});
-      req["resource"] = Value::object({{"group", ti.rt.group}, {"version", ti.rt.version}, {"resource", ti.rt.plural}});
-      if (!sub.empty()) req["subResource"] = sub;
-      // copy first: operator[] may grow the object and invalidate references into it
-      Value kind_copy = req.get("kind"), resource_copy = req.get("resource");
-      req["requestKind"] = std::move(kind_copy);
-      req["requestResource"] = std::move(resource_copy);
-      if (!sub.empty()) req["requestSubResource"] = sub;
-      req["name"] = name;
-      if (!ns.empty()) req["namespace"] = ns;
-      req["operation"] = op;
-      req["userInfo"] = user.to_json();
-      req["object"] = obj ? *obj : Value();
-      req["oldObject"] = old ? *old : Value();
-      req["dryRun"] = false;
-      std::string opts_kind = op == "CREATE" ? "CreateOptions" : op == "DELETE" ? "DeleteOptions" : "UpdateOptions";
-      req["options"] = Value::object({{"kind", opts_kind}, {"apiVersion", "meta.k8s.io/v1"}});
-      Value review = Value::object({{"kind", "AdmissionReview"}, {"apiVersion", "admission.k8s.io/v1"}, {"request", req}});
+      // AdmissionReview serialized in place: object/oldObject are dumped straight from the
+      // caller's trees instead of being deep-copied into a request Value first.
+      const std::string opts_kind = op == "CREATE" ? "CreateOptions" : op == "DELETE" ? "DeleteOptions" : "UpdateOptions";
+      const std::string gvk = "{\"group\":" + json::quote(ti.rt.group) + ",\"version\":" + json::quote(ti.rt.version) +
+                              ",\"kind\":" + json::quote(ti.rt.kind) + "}";
+      const std::string gvr = "{\"group\":" + json::quote(ti.rt.group) + ",\"version\":" + json::quote(ti.rt.version) +
+                              ",\"resource\":" + json::quote(ti.rt.plural) + "}";
+      std::string body;
+      body.reserve(1024 + (obj ? 2048 : 0) + (old ? 2048 : 0));
+      body += "{\"kind\":\"AdmissionReview\",\"apiVersion\":\"admission.k8s.io/v1\",\"request\":{\"uid\":";
+      body += json::quote(uid);
+      body += ",\"kind\":" + gvk + ",\"resource\":" + gvr;
+      if (!sub.empty()) body += ",\"subResource\":" + json::quote(sub);
+      body += ",\"requestKind\":" + gvk + ",\"requestResource\":" + gvr;
+      if (!sub.empty()) body += ",\"requestSubResource\":" + json::quote(sub);
+      body += ",\"name\":" + json::quote(name);
+      if (!ns.empty()) body += ",\"namespace\":" + json::quote(ns);
+      body += ",\"operation\":" + json::quote(op);
+      body += ",\"userInfo\":";
+      user.to_json().dump_to(body);
+      body += ",\"object\":";
+      if (obj) obj->dump_to(body);
+      else body += "null";
+      body += ",\"oldObject\":";
+      if (old) old->dump_to(body);
+      else body += "null";
+      body += ",\"dryRun\":false,\"options\":{\"kind\":" + json::quote(opts_kind) +
+              ",\"apiVersion\":\"meta.k8s.io/v1\"}}}";
       std::string err;
       Value resp_review;
       int64_t t0 = metrics::now_ns();
       try {
         std::string path;
-        auto client = hook_client(hook, path);
+        auto client = hook_client(hm, path);
         http::Headers h;
         h.set("Content-Type", "application/json");
         h.set("Accept", "application/json");
         http::Response r = client->request("POST", path + "?timeout=" + std::to_string(timeout_s) + "s",
-                                           review.dump(), &h, timeout_s * 1000);
+                                           body, &h, timeout_s * 1000);
         if (r.status != 200) {
           err = "expected webhook response status code 200, got " + std::to_string(r.status) + ": " + r.body;
         } else if (!json::try_parse(r.body, resp_review, &err)) {
@@ -921,10 +954,10 @@ struct ApiServer::Impl {
                                  {"apiVersion", e.api_version.empty() ? api_version : e.api_version},
                                  {"time", e.time}, {"fieldsType", "FieldsV1"}, {"fieldsV1", fields_v1(e.fields)}});
       if (!e.subresource.empty()) ent["subresource"] = e.subresource;
-      arr.push_back(ent);
+      arr.push_back(std::move(ent));
     }
     if (arr.empty()) obj["metadata"].erase("managedFields");
-    else obj["metadata"]["managedFields"] = arr;
+    else obj["metadata"]["managedFields"] = std::move(arr);
   }
 
   // a == b ignoring metadata.managedFields and metadata.resourceVersion (no copies).
@@ -961,13 +994,20 @@ struct ApiServer::Impl {
     return true;
   }
 
+  // a != b outside metadata and status (no copies).
   static bool spec_changed(const Value& a, const Value& b) {
-    Value x = a, y = b;
-    x.erase("metadata");
-    x.erase("status");
-    y.erase("metadata");
-    y.erase("status");
-    return !(x == y);
+    if (!a.is_object() || !b.is_object()) return !(a == b);
+    auto skip = [](const std::string& k) { return k == "metadata" || k == "status"; };
+    size_t na = 0, nb = 0;
+    for (size_t i = 0; i < a.keys().size(); ++i) {
+      const std::string& k = a.keys()[i];
+      if (skip(k)) continue;
+      ++na;
+      const Value* bv = b.find(k);
+      if (!bv || !(a.values()[i] == *bv)) return true;
+    }
+    for (const auto& k : b.keys()) nb += skip(k) ? 0 : 1;
+    return na != nb;
   }
 
   // Assign fields changed by a non-apply write to `manager`.
@@ -1320,7 +1360,7 @@ struct ApiServer::Impl {
                        init_new(*p.ti, obj, p.ns, name);
                        Managers m;
                        attribute_update(m, manager, Value::object(), obj, false, p.ti->rt.api_version());
-                       return {obj, m};
+                       return {std::move(obj), std::move(m)};
                      },
                      true, false);
     w.send_json(res.code, res.obj->dump());
@@ -1357,7 +1397,7 @@ struct ApiServer::Impl {
                        }
                        Managers m = cur->managers;
                        attribute_update(m, manager, *cur->obj, obj, is_status, p.ti->rt.api_version());
-                       return {obj, m};
+                       return {std::move(obj), std::move(m)};
                      },
                      false, is_status);
     w.send_json(res.code, res.obj->dump());
@@ -1436,7 +1476,7 @@ struct ApiServer::Impl {
     if (cur && ti.rt.has_status && !is_status) {
       if (cur->obj->contains("status")) live["status"] = cur->obj->get("status");
     }
-    return {live, m};
+    return {std::move(live), std::move(m)};
   }
 
   void do_patch(ParsedPath& p, const http::Request& req, const UserInfo& user, http::ResponseWriter& w) {
@@ -1477,7 +1517,7 @@ struct ApiServer::Impl {
                          Value keep = *cur->obj;
                          if (obj.contains("status")) keep["status"] = obj.get("status");
                          else keep.erase("status");
-                         obj = keep;
+                         obj = std::move(keep);
                        } else {
                          carry_meta(obj, *cur->obj);
                          if (p.ti->rt.has_status) {
@@ -1487,7 +1527,7 @@ struct ApiServer::Impl {
                        }
                        Managers m = cur->managers;
                        attribute_update(m, manager, *cur->obj, obj, is_status, p.ti->rt.api_version());
-                       return {obj, m};
+                       return {std::move(obj), std::move(m)};
                      },
                      is_apply, is_status);
     w.send_json(res.code, res.obj->dump());
