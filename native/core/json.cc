@@ -32,6 +32,8 @@ Value Value::array(std::initializer_list<Value> items) {
 
 Value Value::object(std::initializer_list<std::pair<std::string, Value>> items) {
   Value v = object();
+  v.keys_.reserve(items.size());
+  v.arr_.reserve(items.size());
   for (auto& kv : items) v.set(kv.first, kv.second);
   return v;
 }
@@ -165,6 +167,10 @@ Value& Value::operator[](std::string_view key) {
   require_object("operator[]");
   for (size_t i = 0; i < keys_.size(); ++i) {
     if (keys_[i] == key) return arr_[i];
+  }
+  if (keys_.capacity() == 0) {  // skip the 1 -> 2 -> 4 regrowth of small objects
+    keys_.reserve(4);
+    arr_.reserve(4);
   }
   keys_.emplace_back(key);
   arr_.emplace_back();
@@ -400,9 +406,23 @@ static void dump_impl(const Value& v, std::string& out, int indent, int depth) {
 // ---------------------------------------------------------------------------
 // Parsing
 
+// Per-thread staging stacks for container children (see parse_value); a Parser never
+// nests on one thread, so the stacks start empty for every document.
+static thread_local std::vector<Value> t_stage_vals;
+static thread_local std::vector<std::string> t_stage_keys;
+
 class Parser {
  public:
-  explicit Parser(std::string_view t) : s_(t) {}
+  explicit Parser(std::string_view t) : s_(t), vals_(t_stage_vals), keys_(t_stage_keys) {
+    vals_.clear();
+    keys_.clear();
+  }
+  ~Parser() {
+    vals_.clear();
+    keys_.clear();
+    if (vals_.capacity() > 4096) std::vector<Value>().swap(vals_);  // don't pin a huge LIST's worth per thread
+    if (keys_.capacity() > 4096) std::vector<std::string>().swap(keys_);
+  }
 
   Value parse_document() {
     Value v;
@@ -462,10 +482,15 @@ class Parser {
           ++p_;
           return;
         }
+        // Children are staged on a parser-wide stack and moved into an exactly-sized
+        // vector at the closing bracket: one allocation per container instead of the
+        // 1->2->4->8 regrowth of push_back.
+        const size_t base = vals_.size();
         while (true) {
           skip_ws();
-          out.arr_.emplace_back();
-          parse_value(out.arr_.back(), depth + 1);
+          Value child;
+          parse_value(child, depth + 1);
+          vals_.push_back(std::move(child));
           skip_ws();
           if (p_ >= s_.size()) fail("EOF while parsing a list");
           if (s_[p_] == ',') {
@@ -474,6 +499,9 @@ class Parser {
           }
           if (s_[p_] == ']') {
             ++p_;
+            out.arr_.reserve(vals_.size() - base);
+            for (size_t i = base; i < vals_.size(); ++i) out.arr_.push_back(std::move(vals_[i]));
+            vals_.resize(base);
             return;
           }
           fail("expected `,` or `]`");
@@ -487,6 +515,8 @@ class Parser {
           ++p_;
           return;
         }
+        const size_t base = vals_.size();
+        const size_t kbase = keys_.size();
         while (true) {
           skip_ws();
           if (p_ >= s_.size() || s_[p_] != '"') fail("key must be a string");
@@ -496,17 +526,20 @@ class Parser {
           if (p_ >= s_.size() || s_[p_] != ':') fail("expected `:`");
           ++p_;
           skip_ws();
+          Value child;
+          parse_value(child, depth + 1);
           // Duplicate keys: last one wins (serde_json Value behaviour).
-          Value* existing = nullptr;
-          for (size_t i = 0; i < out.keys_.size(); ++i) {
-            if (out.keys_[i] == key) existing = &out.arr_[i];
+          bool dup = false;
+          for (size_t i = kbase; i < keys_.size(); ++i) {
+            if (keys_[i] == key) {
+              vals_[base + (i - kbase)] = std::move(child);
+              dup = true;
+              break;
+            }
           }
-          if (existing) {
-            parse_value(*existing, depth + 1);
-          } else {
-            out.keys_.push_back(std::move(key));
-            out.arr_.emplace_back();
-            parse_value(out.arr_.back(), depth + 1);
+          if (!dup) {
+            keys_.push_back(std::move(key));
+            vals_.push_back(std::move(child));
           }
           skip_ws();
           if (p_ >= s_.size()) fail("EOF while parsing an object");
@@ -516,6 +549,15 @@ class Parser {
           }
           if (s_[p_] == '}') {
             ++p_;
+            const size_t n = keys_.size() - kbase;
+            out.arr_.reserve(n);
+            out.keys_.reserve(n);
+            for (size_t i = 0; i < n; ++i) {
+              out.keys_.push_back(std::move(keys_[kbase + i]));
+              out.arr_.push_back(std::move(vals_[base + i]));
+            }
+            keys_.resize(kbase);
+            vals_.resize(base);
             return;
           }
           fail("expected `,` or `}`");
@@ -675,6 +717,8 @@ class Parser {
 
   std::string_view s_;
   size_t p_ = 0;
+  std::vector<Value>& vals_;
+  std::vector<std::string>& keys_;
 };
 
 Value parse(std::string_view text) { return Parser(text).parse_document(); }
