@@ -1138,9 +1138,27 @@ struct ApiServer::Impl {
     auto it = b.find(key);
     if (it == b.end()) return;
     uint64_t new_rv = ++rv;
-    Value final_obj = *it->second.obj;
-    final_obj["metadata"]["resourceVersion"] = std::to_string(new_rv);
-    auto ptr = std::make_shared<const Value>(std::move(final_obj));
+    // The DELETED event carries the object at the new resourceVersion: splice the digits
+    // into its serialization instead of deep-copying the tree under the exclusive lock.
+    std::shared_ptr<const Value> ptr = it->second.obj;
+    std::string line = "{\"type\":\"DELETED\",\"object\":";
+    const size_t obj_at = line.size();
+    ptr->dump_to(line);
+    line += "}\n";
+    {
+      const std::string old_rv = "\"resourceVersion\":" + json::quote(ptr->get("metadata").get_string("resourceVersion"));
+      size_t pos = line.find(old_rv, obj_at);
+      if (pos != std::string::npos) {
+        line.replace(pos, old_rv.size(), "\"resourceVersion\":\"" + std::to_string(new_rv) + "\"");
+      } else {  // no resourceVersion in the stored object (never for committed objects)
+        Value final_obj = *ptr;
+        final_obj["metadata"]["resourceVersion"] = std::to_string(new_rv);
+        ptr = std::make_shared<const Value>(std::move(final_obj));
+        line = "{\"type\":\"DELETED\",\"object\":";
+        ptr->dump_to(line);
+        line += "}\n";
+      }
+    }
     std::string uid = ptr->get("metadata").get_string("uid");
     Ref ref{ti.key(), key};
     bool has_dependents;
@@ -1158,7 +1176,7 @@ struct ApiServer::Impl {
       has_dependents = by_owner.count(uid) > 0;
     }
     b.erase(it);
-    emit_locked("DELETED", ti, ns, ptr, new_rv);
+    emit_locked("DELETED", ti, ns, ptr, new_rv, std::move(line));
     bool is_ns = ti.rt.plural == "namespaces" && ti.rt.group.empty();
     if (has_dependents || is_ns) {
       std::lock_guard<std::mutex> g(gc_mu);

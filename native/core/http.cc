@@ -133,13 +133,35 @@ std::map<std::string, std::string> Request::query_params() const {
   return out;
 }
 
-std::string Request::query_param(const std::string& name, const std::string& dflt) const {
-  auto q = query_params();
-  auto it = q.find(name);
-  return it == q.end() ? dflt : it->second;
+// Single-key lookups scan the raw query (no map): the last occurrence wins, as with
+// query_params().  Keys are decoded only when they contain an escape.
+static bool find_query_param(const std::string& query, const std::string& name, std::string* value) {
+  bool found = false;
+  size_t start = 0;
+  while (start < query.size()) {
+    size_t amp = query.find('&', start);
+    size_t end = amp == std::string::npos ? query.size() : amp;
+    size_t eq = query.find('=', start);
+    if (eq == std::string::npos || eq > end) eq = end;
+    std::string_view key(query.data() + start, eq - start);
+    bool match = key.find_first_of("%+") == std::string_view::npos ? key == name
+                                                                    : url_decode(std::string(key)) == name;
+    if (match && end > start) {
+      found = true;
+      if (value) *value = eq < end ? url_decode(query.substr(eq + 1, end - eq - 1)) : "";
+    }
+    if (amp == std::string::npos) break;
+    start = amp + 1;
+  }
+  return found;
 }
 
-bool Request::has_query_param(const std::string& name) const { return query_params().count(name) > 0; }
+std::string Request::query_param(const std::string& name, const std::string& dflt) const {
+  std::string v;
+  return find_query_param(query, name, &v) ? v : dflt;
+}
+
+bool Request::has_query_param(const std::string& name) const { return find_query_param(query, name, nullptr); }
 
 Url parse_url(const std::string& url) {
   Url u;

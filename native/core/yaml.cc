@@ -209,9 +209,13 @@ class Emitter {
     } else if (v.is_array() && !v.empty()) {
       sequence(v, 0, true);
     } else {
-      scalar_node(v, 0, false);
+      // a top-level block scalar's content sits at the default indentation (2), as in
+      // libyaml; plain/quoted scalars ignore the indent
+      scalar_node(v, 2, false);
     }
-    out.push_back('\n');
+    // a literal scalar already ends with its own line break(s): another one would add a
+    // blank line that keep-chomping ("|+") readers count as content
+    if (out.empty() || out.back() != '\n') out.push_back('\n');
   }
 
  private:
@@ -528,7 +532,8 @@ class Parser {
   void split(const std::string& text) {
     size_t start = 0;
     int num = 1;
-    while (start <= text.size()) {
+    // a final line break terminates the last line; it does not start an empty one
+    while (start < text.size()) {
       size_t nl = text.find('\n', start);
       std::string raw = text.substr(start, nl == std::string::npos ? std::string::npos : nl - start);
       if (!raw.empty() && raw.back() == '\r') raw.pop_back();
@@ -609,6 +614,7 @@ class Parser {
     // scalar / flow spanning lines
     int ind = l.indent;
     ++pos_;
+    if (l.text[0] == '|' || l.text[0] == '>') return parse_block_scalar(l.text, ind, l.number);
     return parse_inline_value_cont(l.text, ind - 1, l.number);
   }
 

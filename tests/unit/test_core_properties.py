@@ -73,3 +73,16 @@ def test_json_out_of_range_numbers_rejected_or_finite(nat, text):
     except ValueError:
         return
     assert out not in (float("inf"), float("-inf"))
+
+
+MULTILINE = st.text(alphabet=string.ascii_letters + " \n", max_size=16)
+
+
+@settings(max_examples=300, deadline=None)
+@given(MULTILINE | st.dictionaries(st.sampled_from(["a", "b", "c"]), MULTILINE, max_size=3)
+       | st.lists(MULTILINE, max_size=3))
+def test_yaml_block_scalars_roundtrip_in_both_parsers(nat, v):
+    # literal block scalars (|, |-, |+, |2+) at the top level, in mappings and in sequences
+    y = nat.json_to_yaml(json.dumps(v))
+    assert json.loads(nat.yaml_to_json(y)) == v
+    assert yaml.safe_load(y) == v
