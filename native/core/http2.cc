@@ -73,7 +73,10 @@ void Connection::start() {
     ok = ok && write_frame_locked(kSettings, 0, 0, settings) && write_frame_locked(kWindowUpdate, 0, 0, wu);
     if (!ok) closed_ = true;
   }
-  reader_ = std::thread([this] { reader_loop(); });
+  // The reader owns a reference for its whole run, so the Connection is never destroyed
+  // under it; if that reference is the last one, the destructor runs at thread exit and
+  // join() detaches instead of joining itself.
+  reader_ = std::thread([self = shared_from_this()] { self->reader_loop(); });
 }
 
 void Connection::close(uint32_t code) {
@@ -90,7 +93,11 @@ void Connection::close(uint32_t code) {
 }
 
 void Connection::join() {
-  if (reader_.joinable() && reader_.get_id() != std::this_thread::get_id()) reader_.join();
+  if (!reader_.joinable()) return;
+  // The last reference can be dropped on the reader thread itself (a request dispatch
+  // that outlived both the server's list and the handler): it cannot join itself.
+  if (reader_.get_id() == std::this_thread::get_id()) reader_.detach();
+  else reader_.join();
 }
 
 bool Connection::write_frame_locked(uint8_t type, uint8_t flags, uint32_t sid, std::string_view payload) {

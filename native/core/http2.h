@@ -80,7 +80,8 @@ class Connection : public std::enable_shared_from_this<Connection> {
   Connection(const Connection&) = delete;
   Connection& operator=(const Connection&) = delete;
 
-  // Sends the preface/SETTINGS and starts the reader thread.
+  // Sends the preface/SETTINGS and starts the reader thread (the object must be owned by
+  // a shared_ptr: the reader keeps it alive until the socket closes).
   void start();
   // GOAWAY (best effort) + socket shutdown; the reader thread ends, all streams reset.
   void close(uint32_t code = kNoError);
