@@ -81,6 +81,12 @@ void ChurnDriver::start() {
   for (W w : {W{&types::Namespace, 0}, W{&types::ResourceQuota, 1}, W{&types::RoleBinding, 2}}) {
     watchers_.emplace_back([this, w] {
       kube::Watcher watcher(*admin_, *w.rt);
+      if (!opts_.name_prefix.empty()) {
+        // one driver per rank: skip other ranks' tenants without parsing their events
+        // (each child's name, and its owner reference, carry the tenant name)
+        std::string needle = "\"name\":\"" + opts_.name_prefix;
+        watcher.set_line_filter([needle](std::string_view l) { return l.find(needle) != std::string_view::npos; });
+      }
       std::string key = opts_.gpu_quota_key;
       watcher.run(stop_, [&](const kube::WatchEvent& ev) {
         auto handle = [&](const Value& o) {

@@ -40,8 +40,10 @@ void Watcher::run(CancelToken& stop, const std::function<void(const WatchEvent&)
         Value list = client_.list(rt_, ns_, lo);
         rv = list.get("metadata").get_string("resourceVersion");
         WatchEvent ev{WatchEvent::Type::Restarted, nullptr, {}};
-        for (const auto& item : list.get("items").items()) {
-          Value obj = item;
+        Value* items = list.find_mut("items");
+        std::vector<Value> none;
+        for (auto& item : items && items->is_array() ? items->items_mut() : none) {
+          Value obj = std::move(item);
           if (!obj.contains("apiVersion")) obj["apiVersion"] = rt_.api_version();
           if (!obj.contains("kind")) obj["kind"] = rt_.kind;
           ev.objects.push_back(std::make_shared<const Value>(std::move(obj)));
@@ -59,9 +61,16 @@ void Watcher::run(CancelToken& stop, const std::function<void(const WatchEvent&)
       std::string line;
       while (stream->next_line(line, &stop, 500)) {
         if (line.empty()) continue;
+        // Events the consumer does not want are dropped before JSON parsing; ERROR and
+        // BOOKMARK lines always go through (they drive relists and resumption).
+        if (line_filter_ && !line_filter_(line) && line.find("\"type\":\"ERROR\"") == std::string::npos &&
+            line.find("\"type\":\"BOOKMARK\"") == std::string::npos) {
+          continue;
+        }
         Value ev = json::parse(line);
         const std::string type = ev.get_string("type");
-        const Value& obj = ev.get("object");
+        Value* objp = ev.find_mut("object");
+        Value obj = objp ? std::move(*objp) : Value();  // no deep copy of the event object
         if (type == "ERROR") {
           int code = obj.get("code").is_int() ? static_cast<int>(obj.get("code").as_int()) : 0;
           if (code == 410) {
@@ -75,7 +84,7 @@ void Watcher::run(CancelToken& stop, const std::function<void(const WatchEvent&)
         std::string new_rv = meta_rv(obj);
         if (!new_rv.empty()) rv = new_rv;
         if (type == "BOOKMARK") continue;
-        WatchEvent we{WatchEvent::Type::Added, std::make_shared<const Value>(obj), {}};
+        WatchEvent we{WatchEvent::Type::Added, std::make_shared<const Value>(std::move(obj)), {}};
         if (type == "MODIFIED") we.type = WatchEvent::Type::Modified;
         else if (type == "DELETED") we.type = WatchEvent::Type::Deleted;
         else if (type != "ADDED") continue;

@@ -51,6 +51,11 @@ class Watcher {
   Watcher(KubeClient& client, ResourceType rt, std::string ns = "", std::string label_selector = "",
           std::string field_selector = "");
   void run(CancelToken& stop, const std::function<void(const WatchEvent&)>& on_event);
+  // Optional pre-parse filter on raw watch lines (e.g. a name prefix): ADDED/MODIFIED/
+  // DELETED lines it rejects are skipped without JSON parsing.  A consumer whose filter
+  // drops events must not rely on them (the resume resourceVersion may lag; a resumed
+  // watch replays them, and they are filtered again).
+  void set_line_filter(std::function<bool(std::string_view)> f) { line_filter_ = std::move(f); }
   uint64_t relists() const { return relists_.load(); }
   uint64_t reconnects() const { return reconnects_.load(); }
 
@@ -60,6 +65,7 @@ class Watcher {
   std::string ns_;
   std::string selector_;
   std::string field_selector_;
+  std::function<bool(std::string_view)> line_filter_;
   std::atomic<uint64_t> relists_{0};
   std::atomic<uint64_t> reconnects_{0};
 };
