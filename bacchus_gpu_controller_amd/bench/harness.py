@@ -111,6 +111,28 @@ def _cpu_seconds(pid):
         return None
 
 
+def effective_cpus():
+    """CPUs this job may use: the affinity mask capped by a cgroup v2 cpu.max quota (the
+    MI355X boxes expose every host CPU but grant a 16-CPU quota per GPU)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max" and int(period) > 0:
+            n = min(n, -(-int(quota) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def auto_concurrency(world, cpus):
+    """In-flight creates per rank.  The control plane is CPU-bound, so the total in flight
+    is sized to its CPU share rather than fixed per rank: measured on the MI355X box
+    (16 CPUs, profiles/concurrency_sweep_r1/), 32 per rank costs 20-45 % throughput and
+    2x apply->Ready latency at every N against ~cpus/(2*sqrt(N)) per rank."""
+    return int(min(32, max(4, round(cpus / (2.0 * world ** 0.5)))))
+
+
 def _names(rank, step, batch):
     return [f"r{rank}-s{step}-u{i}" for i in range(batch)]
 
@@ -171,16 +193,20 @@ def run(args):
     cluster = google = None
     info = None
     total_steps = args.warmup + args.steps
+    # Reconcile/sync workers spend most of their time waiting on API round trips, so they
+    # are not sized to the CPU share like the offered load is (16 = the binaries' default).
+    controller_workers = args.controller_workers or 16
+    sync_workers = args.sync_workers or 16
     if d.rank == 0:
         google = FakeGoogle().start()
         rows = [{"id_username": name, "gpu": 1, "cpu": 8, "mem": 64, "storage": 100}
                 for r in range(d.world) for s in range(total_steps) for name in _names(r, s, args.batch)]
         google.set_rows(rows)
-        cluster = Cluster(controller_env={"CONF_WORKERS": str(args.controller_workers)},
+        cluster = Cluster(controller_env={"CONF_WORKERS": str(controller_workers)},
                           log_level=args.log_level, tls_apiserver=args.tls_apiserver)
         cluster.start()
         cluster.start_synchronizer(google, interval=60, extra_env={"CONF_WATCH": "true",
-                                                                   "CONF_WORKERS": str(args.sync_workers),
+                                                                   "CONF_WORKERS": str(sync_workers),
                                                                    "RUST_LOG": args.log_level})
         cluster.start_node_agent(max_gpus=n, n_mock_gpus=n, poll_interval_ms=args.poll_ms,
                                  extra_env={"RUST_LOG": args.log_level})
@@ -192,8 +218,10 @@ def run(args):
                 "apiserver_ca": open(cluster.apiserver_ca).read() if args.tls_apiserver else "",
                 "apiserver_verify": cluster.verify}
     info = d.broadcast_obj(info)
+    cpus = effective_cpus()
+    concurrency = args.concurrency if args.concurrency > 0 else auto_concurrency(d.world, cpus)
     try:
-        driver = nat.ChurnDriver(info["server"], ADMIN_TOKEN, f"r{d.rank}-", args.concurrency,
+        driver = nat.ChurnDriver(info["server"], ADMIN_TOKEN, f"r{d.rank}-", concurrency,
                                  ca_pem=info["apiserver_ca"])
         driver.start()
         time.sleep(0.2)
@@ -267,7 +295,9 @@ def run(args):
             "data": "synthetic",
             "config": {"model": "UserBootstrap onboarding churn (kube-lite" + (" over HTTPS" if args.tls_apiserver else "")
                                 + " + TLS admission + controller + synchronizer + MI355X node-agent)",
-                       "global_batch": args.batch * d.world, "seq_len": None, "parallelism": f"dp{d.world}"},
+                       "global_batch": args.batch * d.world, "seq_len": None, "parallelism": f"dp{d.world}",
+                       "concurrency_per_rank": concurrency, "control_plane_cpus": cpus,
+                       "controller_workers": controller_workers, "sync_workers": sync_workers},
             "reconcile_p99_ms": ms(_pct(rec, 0.99)),
             "reconcile_p50_ms": ms(_pct(rec, 0.50)),
             "reconciles": len(rec),
@@ -315,10 +345,11 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=100, help="UserBootstraps applied per rank per step")
-    ap.add_argument("--concurrency", type=int, default=32)
+    ap.add_argument("--concurrency", type=int, default=0,
+                    help="in-flight creates per rank (0 = sized to the CPU share, see auto_concurrency)")
     ap.add_argument("--timeout", type=float, default=120.0)
-    ap.add_argument("--controller-workers", type=int, default=32)
-    ap.add_argument("--sync-workers", type=int, default=16)
+    ap.add_argument("--controller-workers", type=int, default=0, help="0 = 16")
+    ap.add_argument("--sync-workers", type=int, default=0, help="0 = 16")
     ap.add_argument("--poll-ms", type=int, default=250)
     ap.add_argument("--log-level", default="warn")
     ap.add_argument("--json-out", default="")

@@ -28,3 +28,14 @@ def test_bench_two_ranks_gloo():
     assert d["config"]["global_batch"] == 40 and d["config"]["parallelism"] == "dp2"
     assert d["ready_crs"] == 2 * 2 * 20 and d["failed_crs"] == 0
     assert d["value"] > 0 and d["scaling"] == "weak"
+    assert d["config"]["concurrency_per_rank"] >= 4 and d["config"]["control_plane_cpus"] >= 1
+
+
+def test_auto_concurrency_follows_cpu_share():
+    from bacchus_gpu_controller_amd.bench.harness import auto_concurrency, effective_cpus
+
+    # the MI355X box: 16-CPU quota -> 8 per rank alone, 4 per rank from 4 ranks up
+    assert [auto_concurrency(n, 16) for n in (1, 2, 4, 8)] == [8, 6, 4, 4]
+    # a bigger share keeps more tenants in flight, capped at 32 per rank
+    assert [auto_concurrency(n, 128) for n in (1, 2, 4, 8)] == [32, 32, 32, 23]
+    assert 1 <= effective_cpus() <= (os.cpu_count() or 1)
