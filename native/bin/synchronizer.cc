@@ -9,6 +9,7 @@
 #include "core/log.h"
 #include "core/process.h"
 #include "kube/client.h"
+#include "kube/leader.h"
 #include "sync/google.h"
 #include "sync/synchronizer.h"
 
@@ -61,6 +62,14 @@ int main() {
   } catch (const std::exception& e) {
     std::fprintf(stderr, "Error: %s\n", e.what());
     return 1;
+  }
+  if (cfg.leader_election) {  // standbys wait here; losing the lease stops the loop (kubelet restarts us)
+    kube::LeaderElector le(*client, cfg.lease_namespace, cfg.lease_name);
+    if (!le.acquire(*stop)) {
+      health.stop();
+      return 0;
+    }
+    le.keep_renewing(stop);
   }
   std::string file_id = cfg.google_file_id;
   sync::Synchronizer s(*client, [&] { return drive->export_file(file_id, "text/csv"); }, cfg);

@@ -48,6 +48,11 @@ struct Config {
   bool exit_on_error = true;
   bool skip_unchanged = true;
   int workers = 8;
+  // Lease-based leader election (reference: none; two synchronizer replicas would both
+  // write every tenant).  Off by default like the controller's.
+  bool leader_election = false;
+  std::string lease_namespace = "default";
+  std::string lease_name = "bacchus-gpu-synchronizer";
   static Config from_env(const EnvConfig& env);
 };
 

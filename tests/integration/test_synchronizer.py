@@ -121,3 +121,31 @@ def test_status_put_conflict_is_retried(google):
                  timeout=10, desc="erin synced despite conflicts")
         assert p.alive()
         assert c.stats()["faults_hit"] == 2
+
+
+def test_synchronizer_leader_election_failover(google):
+    """Two synchronizer replicas with CONF_LEADER_ELECTION: only the lease holder writes;
+    when it dies without releasing, the standby takes over and keeps syncing."""
+    import signal
+
+    google.set_rows([{"id_username": "alice", "gpu": 1}, {"id_username": "bob", "gpu": 2}])
+    env = {"CONF_LEADER_ELECTION": "true", "CONF_LEASE_NAMESPACE": "bgc", "CONF_WATCH": "true", "RUST_LOG": "info"}
+    with Cluster() as c:
+        c.start_synchronizer(google, interval=60, extra_env=env)
+        leader = c.procs["synchronizer"]
+        wait_for(lambda: c.admin.get_or_none("leases", "bacchus-gpu-synchronizer", "bgc"), desc="lease")
+        holder = c.admin.get("leases", "bacchus-gpu-synchronizer", "bgc")["spec"]["holderIdentity"]
+        c.procs["synchronizer-leader"] = c.procs.pop("synchronizer")
+        c.start_synchronizer(google, interval=60, extra_env=env)
+        standby = c.procs["synchronizer"]
+        c.as_user("oidc:alice", ["gpu"]).create("userbootstraps", ub("alice"))
+        wait_for(lambda: (c.admin.get("userbootstraps", "alice").get("spec", {}).get("quota") or None),
+                 timeout=20, desc="alice synced by the leader")
+        assert "attempting to acquire lease" in standby.output() and "acquired lease" not in standby.output()
+        leader.p.send_signal(signal.SIGKILL)
+        wait_for(lambda: "acquired lease" in standby.output(), timeout=30, desc="standby takes over")
+        assert c.admin.get("leases", "bacchus-gpu-synchronizer", "bgc")["spec"]["holderIdentity"] != holder
+        c.as_user("oidc:bob", ["gpu"]).create("userbootstraps", ub("bob"))
+        q = wait_for(lambda: (c.admin.get("userbootstraps", "bob").get("spec", {}).get("quota") or None),
+                     timeout=30, desc="bob synced by the new leader")
+        assert q["hard"]["requests.amd.com/gpu"] == "2"

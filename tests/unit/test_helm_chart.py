@@ -113,7 +113,8 @@ NEEDED = {
     + [("rbac.authorization.k8s.io", "roles", "bind"), ("rbac.authorization.k8s.io", "roles", "escalate")]
     + [("coordination.k8s.io", "leases", v) for v in ("get", "create", "update")],
     "synchronizer": [("bacchus.io", "userbootstraps", v) for v in ("get", "list", "watch", "patch")]
-    + [("bacchus.io", "userbootstraps/status", "update")],
+    + [("bacchus.io", "userbootstraps/status", "update")]
+    + [("coordination.k8s.io", "leases", v) for v in ("get", "create", "update")],
     "node-agent": [("", "nodes", v) for v in ("get", "list", "watch", "patch")]
     + [("", "nodes/status", "patch")],
 }
