@@ -366,7 +366,15 @@ void drm_nodes(const std::string& sysfs_root, const std::string& bdf, std::strin
 
 DevicePlugin::DevicePlugin(std::vector<GpuInfo> gpus, DevicePluginConfig cfg)
     : gpus_(std::move(gpus)), cfg_(std::move(cfg)), healthy_(gpus_.size(), true) {
-  for (const auto& g : gpus_) ids_.push_back(g.bdf.empty() ? "gpu-" + std::to_string(g.index) : g.bdf);
+  // ID = PCI BDF; compute partitions of one GPU can share a BDF, so duplicates get the
+  // logical device index appended.
+  std::map<std::string, int> seen;
+  for (const auto& g : gpus_) seen[g.bdf]++;
+  for (const auto& g : gpus_) {
+    if (g.bdf.empty()) ids_.push_back("gpu-" + std::to_string(g.index));
+    else if (seen[g.bdf] > 1) ids_.push_back(g.bdf + "-p" + std::to_string(g.index));
+    else ids_.push_back(g.bdf);
+  }
 }
 
 DevicePlugin::~DevicePlugin() { stop(); }

@@ -25,6 +25,7 @@ NodeAgentConfig NodeAgentConfig::from_env(const EnvConfig& env) {
   c.poll_interval_ms = env.u64_or("poll_interval_ms", 1000);
   c.heartbeat_secs = env.u64_or("heartbeat_secs", 30);
   c.resource_name = env.str_or("resource_name", "amd.com/gpu");
+  c.partition_resource_name = env.str_or("partition_resource_name", c.partition_resource_name);
   c.label_prefix = env.str_or("label_prefix", "amd.com/gpu");
   c.max_gpus = static_cast<int>(env.u64_or("max_gpus", 0));
   c.run_diag = env.boolean_or("run_diag", false);
@@ -49,6 +50,15 @@ std::string sanitize_label_value(const std::string& v) {
   if (out.size() > 63) out.resize(63);
   while (!out.empty() && !std::isalnum(static_cast<unsigned char>(out.back()))) out.pop_back();
   return out;
+}
+
+std::string advertised_resource(const NodeAgentConfig& cfg, const std::vector<GpuInfo>& gpus) {
+  if (cfg.partition_resource_name.empty() || gpus.empty()) return cfg.resource_name;
+  for (const auto& g : gpus) {
+    const std::string& p = g.compute_partition;
+    if (p.empty() || p == "SPX" || p == "unknown") return cfg.resource_name;
+  }
+  return cfg.partition_resource_name;
 }
 
 std::string product_label(const GpuInfo& g) {
@@ -136,6 +146,12 @@ void NodeAgent::init() {
   gpus_ = backend_->discover();
   if (cfg_.max_gpus > 0 && static_cast<int>(gpus_.size()) > cfg_.max_gpus) gpus_.resize(static_cast<size_t>(cfg_.max_gpus));
   if (gpus_.empty()) throw std::runtime_error("no GPUs discovered via " + backend_->name());
+  const std::string res = advertised_resource(cfg_, gpus_);
+  if (res != cfg_.resource_name) {
+    LOG_INFO("node_agent") << "GPUs run " << gpus_.front().compute_partition << " compute partitions: advertising "
+                           << gpus_.size() << " x " << res << " instead of " << cfg_.resource_name;
+    cfg_.resource_name = res;
+  }
   LOG_INFO("node_agent") << "discovered " << gpus_.size() << " GPU(s) via " << backend_->name() << ": "
                          << gpus_.front().market_name << " " << gpus_.front().gfx_target << " "
                          << gpus_.front().vram_total_mb << " MB";

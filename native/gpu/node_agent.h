@@ -43,6 +43,11 @@ struct NodeAgentConfig {
   uint64_t poll_interval_ms = 1000;
   uint64_t heartbeat_secs = 30;
   std::string resource_name = "amd.com/gpu";
+  // When every GPU runs a sub-device compute partition (DPX/QPX/CPX: one logical device
+  // per partition), the devices are advertised under this name instead — the key the
+  // synchronizer writes for the sheet's partition column (reference: the MIG column,
+  // src/synchronizer.rs:276).  Empty = always `resource_name`.
+  std::string partition_resource_name = "amd.com/gpu-partition";
   std::string label_prefix = "amd.com/gpu";
   int max_gpus = 0;                    // 0 = all discovered
   bool run_diag = false;               // HIP HBM + MFMA check before advertising
@@ -66,6 +71,8 @@ struct DiagOutcome {
 };
 
 std::string sanitize_label_value(const std::string& v);
+// The extended-resource name for a set of discovered devices (see partition_resource_name).
+std::string advertised_resource(const NodeAgentConfig& cfg, const std::vector<GpuInfo>& gpus);
 std::string product_label(const GpuInfo& g);
 
 // Pure rendering of the Node patches (unit-tested).

@@ -248,3 +248,36 @@ def test_node_agent_runs_device_plugin(tmp_path):
             assert sum(x[1] == "Healthy" for x in kubelet.device_lists[-1][1]) == 7
     finally:
         kubelet.stop()
+
+
+def test_compute_partitions_advertised_as_partition_resource(nat, tmp_path):
+    """GPUs in a sub-device compute partition (here CPX, two logical devices per BDF) are
+    advertised as amd.com/gpu-partition — the quota key the synchronizer writes for the
+    sheet's partition column — with unique device IDs."""
+    fx = json.loads(nat.default_mi355x_fixture(8))
+    for i, g in enumerate(fx["gpus"]):
+        g["compute_partition"] = "CPX"
+        g["bdf"] = fx["gpus"][i - i % 2]["bdf"]  # partitions 2k, 2k+1 share a PCI function
+    fixture = str(tmp_path / "cpx.json")
+    with open(fixture, "w") as f:
+        json.dump(fx, f)
+    d = str(tmp_path / "dp")
+    kubelet = FakeKubelet(d).start()
+    try:
+        with Cluster(admission=False, controller=False) as c:
+            c.start_node_agent(node_name="mi355x-cpx", backend="mock", proc_name="na-cpx",
+                               extra_env={"CONF_MOCK_FIXTURE_PATH": fixture})
+            node = wait_for(lambda: (lambda n: n if n and n.get("status", {}).get("capacity") else None)(
+                c.admin.get_or_none("nodes", "mi355x-cpx")), timeout=10, desc="capacity published")
+            assert node["status"]["capacity"] == {"amd.com/gpu-partition": "8"}
+            c.procs["na-cpx"].stop()
+            c.start_node_agent(node_name="mi355x-cpx2", backend="mock", proc_name="na-cpx2",
+                               extra_env={"CONF_MOCK_FIXTURE_PATH": fixture, "CONF_DEVICE_PLUGIN": "true",
+                                          "CONF_DEVICE_PLUGIN_DIR": d})
+            assert kubelet.wait(lambda: kubelet.registrations and kubelet.device_lists, timeout=15)
+            assert kubelet.registrations[-1].resource_name == "amd.com/gpu-partition"
+            ids = [x[0] for x in kubelet.device_lists[-1][1]]
+            assert len(ids) == 8 and len(set(ids)) == 8
+            assert ids[0] == fx["gpus"][0]["bdf"] + "-p0" and ids[1] == fx["gpus"][0]["bdf"] + "-p1"
+    finally:
+        kubelet.stop()
