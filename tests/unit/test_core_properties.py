@@ -33,12 +33,32 @@ def test_yaml_emit_parses_back_with_our_parser(nat, v):
     assert json.loads(nat.yaml_to_json(nat.json_to_yaml(json.dumps(v)))) == v
 
 
+def _yaml11_only_nonstring(s):
+    """Plain scalars YAML 1.1 (PyYAML) resolves to a non-string although the emitter (like
+    serde_yaml, YAML 1.2) leaves them unquoted as strings, e.g. "0_" (1.1 int with a digit
+    separator), "1:20" (sexagesimal) or "2001-12-14" (timestamp): not 1.1/1.2-neutral."""
+    from bacchus_gpu_controller_amd import native
+
+    try:
+        v11 = yaml.safe_load(s)
+    except yaml.YAMLError:
+        return False
+    emitted_plain = native().json_to_yaml(json.dumps(s)).rstrip("\n") == s
+    return emitted_plain and not isinstance(v11, str)
+
+
 SAFE = st.text(alphabet=string.ascii_letters + string.digits + " -_./:", min_size=1, max_size=16).filter(
-    lambda s: s.lower() not in {"y", "n", "yes", "no", "on", "off", "true", "false", "null", "~"})
+    lambda s: s.lower() not in {"y", "n", "yes", "no", "on", "off", "true", "false", "null", "~"}
+    and not _yaml11_only_nonstring(s))
+
+
+NEUTRAL_KEYS = KEYS.filter(lambda k: not _yaml11_only_nonstring(k))
 
 
 @settings(max_examples=200, deadline=None)
-@given(json_values(st.none() | st.booleans() | st.integers(min_value=-10 ** 9, max_value=10 ** 9) | SAFE))
+@given(st.recursive(st.none() | st.booleans() | st.integers(min_value=-10 ** 9, max_value=10 ** 9) | SAFE,
+                    lambda kids: st.lists(kids, max_size=4) | st.dictionaries(NEUTRAL_KEYS, kids, max_size=4),
+                    max_leaves=25))
 def test_yaml_emit_loads_in_pyyaml(nat, v):
     # YAML 1.1/1.2-neutral scalars: PyYAML (1.1) must read exactly what we emitted
     assert yaml.safe_load(nat.json_to_yaml(json.dumps(v))) == v
@@ -75,7 +95,8 @@ def test_json_out_of_range_numbers_rejected_or_finite(nat, text):
     assert out not in (float("inf"), float("-inf"))
 
 
-MULTILINE = st.text(alphabet=string.ascii_letters + " \n", max_size=16)
+MULTILINE = st.text(alphabet=string.ascii_letters + " \n", max_size=16).filter(
+    lambda s: not _yaml11_only_nonstring(s))  # "NO", "on", ...: YAML 1.1 booleans
 
 
 @settings(max_examples=300, deadline=None)
