@@ -342,8 +342,9 @@ def run(args):
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    # a step is ~10 ms at N=1: 50 timed steps keep the measured window around half a second
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=100, help="UserBootstraps applied per rank per step")
     ap.add_argument("--concurrency", type=int, default=0,
                     help="in-flight creates per rank (0 = sized to the CPU share, see auto_concurrency)")
