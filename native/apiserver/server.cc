@@ -410,6 +410,17 @@ struct ParsedPath {
 struct WriteResult {
   std::shared_ptr<const Value> obj;
   int code = 200;
+  // The committed watch-event line, whose "object" member is exactly the response body:
+  // a write serializes its object once (for the event) and answers with a view into it.
+  std::shared_ptr<const std::string> line;
+  std::string_view body() const {
+    static const std::string kPrefixEnd = ",\"object\":";
+    if (!line) return {};
+    size_t at = line->find(kPrefixEnd);
+    if (at == std::string::npos || line->size() < at + kPrefixEnd.size() + 2) return {};
+    at += kPrefixEnd.size();
+    return std::string_view(*line).substr(at, line->size() - at - 2);  // drop the closing "}\n"
+  }
 };
 
 std::string obj_key(const ResourceType& rt, const std::string& ns, const std::string& name) { return rt.key(ns, name); }
@@ -632,8 +643,9 @@ struct ApiServer::Impl {
 
   // ---------------------------------------------------------------- events
   // Caller holds ti.store->mu exclusively.
-  void emit_locked(const std::string& type, const TypeInfo& ti, const std::string& ns,
-                   const std::shared_ptr<const Value>& obj, uint64_t ev_rv, std::string preline = {}) {
+  std::shared_ptr<const std::string> emit_locked(const std::string& type, const TypeInfo& ti, const std::string& ns,
+                                                 const std::shared_ptr<const Value>& obj, uint64_t ev_rv,
+                                                 std::string preline = {}) {
     TypeStore& st = *ti.store;
     auto rec = std::make_shared<EventRec>();
     rec->rv = ev_rv;
@@ -664,6 +676,7 @@ struct ApiServer::Impl {
       }
       t_pending_wakeups.push_back(w);
     }
+    return rec->line;
   }
 
   // ---------------------------------------------------------------- webhooks
@@ -1079,7 +1092,8 @@ struct ApiServer::Impl {
   // object; *dangling is set when every owner reference points at a deleted object.
   std::shared_ptr<const Value> commit_locked(const TypeInfo& ti, const std::string& ns, const std::string& name,
                                             Value obj, Managers managers, const Stored* prev,
-                                            const PreparedEvent* pe = nullptr, bool* dangling = nullptr) {
+                                            const PreparedEvent* pe = nullptr, bool* dangling = nullptr,
+                                            std::shared_ptr<const std::string>* line_out = nullptr) {
     uint64_t new_rv = ++rv;
     std::string digits = std::to_string(new_rv);
     Value& meta = obj["metadata"];
@@ -1117,7 +1131,8 @@ struct ApiServer::Impl {
       }
     }
     b[key] = std::move(s);
-    emit_locked(prev ? "MODIFIED" : "ADDED", ti, ns, ptr, new_rv, std::move(preline));
+    auto line = emit_locked(prev ? "MODIFIED" : "ADDED", ti, ns, ptr, new_rv, std::move(preline));
+    if (line_out) *line_out = std::move(line);
     return ptr;
   }
 
@@ -1288,16 +1303,23 @@ struct ApiServer::Impl {
           return {cur_copy.obj, 200};
         }
         (void)is_status;
-        return {commit_locked(ti, ns, name, std::move(obj), std::move(managers), &it->second, &pe), 200};
+        WriteResult wr;
+        wr.obj = commit_locked(ti, ns, name, std::move(obj), std::move(managers), &it->second, &pe, nullptr, &wr.line);
+        return wr;
       }
       if (ti.rt.plural == "customresourcedefinitions") register_crd(obj);
       bool dangling = false;
-      auto created = commit_locked(ti, ns, name, std::move(obj), std::move(managers), nullptr, &pe, &dangling);
+      std::shared_ptr<const std::string> line;
+      auto created = commit_locked(ti, ns, name, std::move(obj), std::move(managers), nullptr, &pe, &dangling, &line);
       // The garbage collector also removes dependents created with only dangling owner
       // references (e.g. a controller re-applying a child right after its owner was
       // deleted, before the owner's DELETED event reached it).
       if (dangling) erase_locked(ti, ns, name);
-      return {created, 201};
+      WriteResult wr;
+      wr.obj = created;
+      wr.code = 201;
+      wr.line = std::move(line);
+      return wr;
     }
     throw conflict(ti.rt, name);
   }
@@ -1381,7 +1403,11 @@ struct ApiServer::Impl {
                        return {std::move(obj), std::move(m)};
                      },
                      true, false);
-    w.send_json(res.code, res.obj->dump());
+    {
+      std::string_view b = res.body();
+      if (!b.empty()) w.send_json(res.code, b);
+      else w.send_json(res.code, res.obj->dump());
+    }
   }
 
   void do_update(ParsedPath& p, const http::Request& req, const UserInfo& user, http::ResponseWriter& w) {
@@ -1418,7 +1444,11 @@ struct ApiServer::Impl {
                        return {std::move(obj), std::move(m)};
                      },
                      false, is_status);
-    w.send_json(res.code, res.obj->dump());
+    {
+      std::string_view b = res.body();
+      if (!b.empty()) w.send_json(res.code, b);
+      else w.send_json(res.code, res.obj->dump());
+    }
   }
 
   std::pair<Value, Managers> apply_ssa(const TypeInfo& ti, const Stored* cur, const Value& config,
@@ -1548,7 +1578,11 @@ struct ApiServer::Impl {
                        return {std::move(obj), std::move(m)};
                      },
                      is_apply, is_status);
-    w.send_json(res.code, res.obj->dump());
+    {
+      std::string_view b = res.body();
+      if (!b.empty()) w.send_json(res.code, b);
+      else w.send_json(res.code, res.obj->dump());
+    }
   }
 
   void do_delete(ParsedPath& p, const http::Request& req, const UserInfo& user, http::ResponseWriter& w) {

@@ -300,7 +300,7 @@ void ResponseWriter::abort() {
   keep_alive_ = false;
 }
 
-void ResponseWriter::send(int status, const std::string& body, const std::string& content_type,
+void ResponseWriter::send(int status, std::string_view body, const std::string& content_type,
                           const Headers* extra) {
   status_ = status;
   if (sent_) return;

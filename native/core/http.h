@@ -17,6 +17,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <string_view>
 #include <thread>
 #include <vector>
 
@@ -97,9 +98,9 @@ class ResponseWriter {
  public:
   ResponseWriter(net::Stream& s, bool keep_alive, const CancelToken& server_stop)
       : s_(s), keep_alive_(keep_alive), stop_(server_stop) {}
-  void send(int status, const std::string& body, const std::string& content_type = "text/plain; charset=utf-8",
+  void send(int status, std::string_view body, const std::string& content_type = "text/plain; charset=utf-8",
             const Headers* extra = nullptr);
-  void send_json(int status, const std::string& body) { send(status, body, "application/json"); }
+  void send_json(int status, std::string_view body) { send(status, body, "application/json"); }
   // Streaming (chunked) responses for WATCH.
   bool start_chunked(int status, const std::string& content_type);
   bool write_chunk(const std::string& data);
