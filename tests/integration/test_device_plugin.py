@@ -246,6 +246,35 @@ def test_node_agent_runs_device_plugin(tmp_path):
             c.set_gpu_fixture("mi355x-dp", fx)
             assert kubelet.wait(lambda: kubelet.device_lists[-1][1][5][1] == "Unhealthy", timeout=15)
             assert sum(x[1] == "Healthy" for x in kubelet.device_lists[-1][1]) == 7
+            # concurrent kubelet calls into the node agent's own server (this path runs
+            # under tools/sanitize.sh asan|tsan, unlike the pybind-hosted plugin above)
+            ids = [x[0] for x in kubelet.device_lists[-1][1]]
+            sock = os.path.join(d, kubelet.registrations[-1].endpoint)
+            errors = []
+
+            def worker(k):
+                cl = PluginClient(sock)
+                try:
+                    for i in range(25):
+                        req = pb["AllocateRequest"]()
+                        req.container_requests.add().devices_ids.append(ids[(k + i) % 8])
+                        assert cl.allocate(req, timeout=10).container_responses[0].devices
+                        q = pb["PreferredAllocationRequest"]()
+                        cq = q.container_requests.add()
+                        cq.available_deviceIDs.extend(ids)
+                        cq.allocation_size = 1 + (k + i) % 8
+                        assert len(cl.preferred(q, timeout=10).container_responses[0].deviceIDs) == 1 + (k + i) % 8
+                except Exception as e:  # noqa: BLE001
+                    errors.append(repr(e))
+                finally:
+                    cl.close()
+
+            ts = [threading.Thread(target=worker, args=(k,)) for k in range(8)]
+            for t in ts:
+                t.start()
+            for t in ts:
+                t.join(60)
+            assert not errors, errors[:3]
     finally:
         kubelet.stop()
 
