@@ -202,12 +202,17 @@ def run(args):
         rows = [{"id_username": name, "gpu": 1, "cpu": 8, "mem": 64, "storage": 100}
                 for r in range(d.world) for s in range(total_steps) for name in _names(r, s, args.batch)]
         google.set_rows(rows)
-        cluster = Cluster(controller_env={"CONF_WORKERS": str(controller_workers)},
-                          log_level=args.log_level, tls_apiserver=args.tls_apiserver)
+        ctrl_env = {"CONF_WORKERS": str(controller_workers)}
+        sync_env = {"CONF_WATCH": "true", "CONF_WORKERS": str(sync_workers), "RUST_LOG": args.log_level}
+        if args.reference_semantics:
+            # the reference's behaviour on this same stack: sheet read only on the periodic
+            # tick (synchronizer.rs:192), every tick rewrites every matched tenant, children
+            # applied one after another and re-applied on every reconcile (controller.rs:81-149)
+            ctrl_env.update({"CONF_SKIP_UNCHANGED": "false", "CONF_PARALLEL_CHILDREN": "false"})
+            sync_env.update({"CONF_WATCH": "false", "CONF_SKIP_UNCHANGED": "false"})
+        cluster = Cluster(controller_env=ctrl_env, log_level=args.log_level, tls_apiserver=args.tls_apiserver)
         cluster.start()
-        cluster.start_synchronizer(google, interval=60, extra_env={"CONF_WATCH": "true",
-                                                                   "CONF_WORKERS": str(sync_workers),
-                                                                   "RUST_LOG": args.log_level})
+        cluster.start_synchronizer(google, interval=args.sync_interval, extra_env=sync_env)
         cluster.start_node_agent(max_gpus=n, n_mock_gpus=n, poll_interval_ms=args.poll_ms,
                                  extra_env={"RUST_LOG": args.log_level})
         info = {"server": cluster.server, "controller": f"http://127.0.0.1:{cluster.controller_port}",
@@ -294,7 +299,8 @@ def run(args):
             "dtype": "bf16",
             "data": "synthetic",
             "config": {"model": "UserBootstrap onboarding churn (kube-lite" + (" over HTTPS" if args.tls_apiserver else "")
-                                + " + TLS admission + controller + synchronizer + MI355X node-agent)",
+                                + " + TLS admission + controller + synchronizer + MI355X node-agent)"
+                                + (" [reference semantics]" if args.reference_semantics else ""),
                        "global_batch": args.batch * d.world, "seq_len": None, "parallelism": f"dp{d.world}",
                        "concurrency_per_rank": concurrency, "control_plane_cpus": cpus,
                        "controller_workers": controller_workers, "sync_workers": sync_workers},
@@ -354,6 +360,10 @@ def main(argv=None):
     ap.add_argument("--poll-ms", type=int, default=250)
     ap.add_argument("--log-level", default="warn")
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--reference-semantics", action="store_true",
+                    help="measure the reference's behaviour on this stack: periodic sheet sync only, "
+                         "sequential and unconditional child applies")
+    ap.add_argument("--sync-interval", type=int, default=60, help="synchronizer tick (s); the reference default is 60")
     ap.add_argument("--report-cpu", action="store_true", help="add per-component CPU seconds to the JSON")
     ap.add_argument("--tls-apiserver", action=argparse.BooleanOptionalAction, default=True,
                     help="components reach kube-lite over HTTPS via kubeconfigs, as in a real cluster")
