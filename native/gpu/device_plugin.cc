@@ -266,7 +266,7 @@ std::vector<std::string> preferred_allocation(const std::vector<GpuInfo>& gpus, 
   std::map<uint64_t, std::vector<size_t>> by_hive;
   std::vector<std::string> unknown;
   for (const auto& id : available) {
-    if (taken.count(id)) continue;
+    if (!taken.insert(id).second) continue;  // must-include, or listed twice
     auto it = pos.find(id);
     if (it == pos.end()) {
       unknown.push_back(id);

@@ -229,3 +229,9 @@ def test_preferred_allocation_spans_fewest_hives(nat):
     avail = ids[:3] + ids[8:]  # 3 left on hive A, 4 on hive B
     got = nat.preferred_allocation(json.dumps(gpus), ids, avail, [], 6)
     assert len(got) == 6 and set(ids[8:]) <= set(got)  # the whole bigger remainder first
+
+
+def test_preferred_allocation_ignores_duplicate_ids(nat):
+    gpus, ids = _two_hives(nat)
+    got = nat.preferred_allocation(json.dumps(gpus), ids, ids[:2] * 3 + ids[2:4], [ids[0]], 3)
+    assert len(got) == len(set(got)) == 3 and got[0] == ids[0]
