@@ -133,6 +133,18 @@ def auto_concurrency(world, cpus):
     return int(min(32, max(4, round(cpus / (2.0 * world ** 0.5)))))
 
 
+def _rss_mb(pid):
+    """Resident set size of a component (leak check over long runs)."""
+    try:
+        with open(f"/proc/{pid}/status") as f:
+            for line in f:
+                if line.startswith("VmRSS:"):
+                    return round(int(line.split()[1]) / 1024.0, 1)
+    except (OSError, ValueError, IndexError):
+        pass
+    return None
+
+
 def _names(rank, step, batch):
     return [f"r{rank}-s{step}-u{i}" for i in range(batch)]
 
@@ -336,6 +348,7 @@ def run(args):
             out["errors"] = [e for p in per_rank for e in p["errors"]][:5]
         if args.report_cpu and cluster is not None:
             out["component_cpu_s"] = {name: _cpu_seconds(p.p.pid) for name, p in cluster.procs.items()}
+            out["component_rss_mb"] = {name: _rss_mb(p.p.pid) for name, p in cluster.procs.items()}
         return out
     finally:
         if cluster is not None:

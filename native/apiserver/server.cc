@@ -261,9 +261,19 @@ struct EventRec {
   uint64_t rv;
   std::string type_key;
   std::string ns;
-  std::shared_ptr<const Value> obj;
+  // Only what a resuming watch filters on ({"metadata":{"name","labels"}}), not the
+  // object: the watch cache must not pin every old version's full tree in memory.
+  std::shared_ptr<const Value> meta;
   std::shared_ptr<const std::string> line;  // {"type":..,"object":..}\n
 };
+
+// {"metadata":{"name":..,"labels":..}} of an object: the fields watch filters read.
+std::shared_ptr<const Value> filter_view(const Value& obj) {
+  const Value& m = obj.get("metadata");
+  Value meta = Value::object({{"name", m.get("name")}});
+  if (m.contains("labels")) meta["labels"] = m.get("labels");
+  return std::make_shared<const Value>(Value::object({{"metadata", std::move(meta)}}));
+}
 
 struct WatchSub {
   std::string type_key;
@@ -651,7 +661,7 @@ struct ApiServer::Impl {
     rec->rv = ev_rv;
     rec->type_key = ti.key();
     rec->ns = ns;
-    rec->obj = obj;
+    rec->meta = filter_view(*obj);
     std::string line = std::move(preline);
     if (line.empty()) {
       line = "{\"type\":\"" + type + "\",\"object\":";
@@ -1707,8 +1717,8 @@ struct ApiServer::Impl {
           const auto& e = *it;
           if (e->type_key != sub.type_key) continue;
           if (!sub.ns.empty() && e->ns != sub.ns) continue;
-          if (!sub.fields.name.empty() && e->obj->get("metadata").get_string("name") != sub.fields.name) continue;
-          if (!sub.sel.empty() && !selector_matches(sub.sel, *e->obj)) continue;
+          if (!sub.fields.name.empty() && e->meta->get("metadata").get_string("name") != sub.fields.name) continue;
+          if (!sub.sel.empty() && !selector_matches(sub.sel, *e->meta)) continue;
           initial.push_back(e->line);
         }
       }

@@ -33,7 +33,7 @@ struct Options {
   std::string tls_key_file;
   // "namespace/service" -> "host:port": where a webhook's clientConfig.service is reachable.
   std::map<std::string, std::string> service_overrides;
-  size_t history_limit = 200000;  // watch cache events kept for resume
+  size_t history_limit = 50000;  // watch-cache events kept per type for resume (k8s keeps ~100)
   int bookmark_interval_ms = 60000;
   bool validate_schema = true;
   int max_watch_seconds = 1800;
