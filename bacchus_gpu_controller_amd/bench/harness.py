@@ -222,7 +222,8 @@ def run(args):
             # applied one after another and re-applied on every reconcile (controller.rs:81-149)
             ctrl_env.update({"CONF_SKIP_UNCHANGED": "false", "CONF_PARALLEL_CHILDREN": "false"})
             sync_env.update({"CONF_WATCH": "false", "CONF_SKIP_UNCHANGED": "false"})
-        cluster = Cluster(controller_env=ctrl_env, log_level=args.log_level, tls_apiserver=args.tls_apiserver)
+        cluster = Cluster(controller_env=ctrl_env, log_level=args.log_level, tls_apiserver=args.tls_apiserver,
+                          apiserver_args=list(args.apiserver_arg))
         cluster.start()
         cluster.start_synchronizer(google, interval=args.sync_interval, extra_env=sync_env)
         cluster.start_node_agent(max_gpus=n, n_mock_gpus=n, poll_interval_ms=args.poll_ms,
@@ -377,6 +378,7 @@ def main(argv=None):
                     help="measure the reference's behaviour on this stack: periodic sheet sync only, "
                          "sequential and unconditional child applies")
     ap.add_argument("--sync-interval", type=int, default=60, help="synchronizer tick (s); the reference default is 60")
+    ap.add_argument("--apiserver-arg", action="append", default=[], help="extra kube-lite flag (repeatable)")
     ap.add_argument("--report-cpu", action="store_true", help="add per-component CPU seconds to the JSON")
     ap.add_argument("--tls-apiserver", action=argparse.BooleanOptionalAction, default=True,
                     help="components reach kube-lite over HTTPS via kubeconfigs, as in a real cluster")

@@ -1752,6 +1752,11 @@ struct ApiServer::Impl {
       {
         std::unique_lock<std::mutex> lk(sub.m);
         sub.cv.wait_for(lk, std::chrono::milliseconds(500), [&] { return !sub.q.empty() || sub.closed || sub.overflow; });
+        if (opts.watch_coalesce_us > 0 && !sub.q.empty() && sub.q.size() < 16 && !sub.closed) {
+          // let a burst accumulate into one write (see Options::watch_coalesce_us)
+          sub.cv.wait_for(lk, std::chrono::microseconds(opts.watch_coalesce_us),
+                          [&] { return sub.q.size() >= 16 || sub.closed || sub.overflow; });
+        }
         batch.assign(sub.q.begin(), sub.q.end());
         sub.q.clear();
         closed = sub.closed;

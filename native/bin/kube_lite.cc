@@ -50,6 +50,7 @@ int main(int argc, char** argv) {
     else if (a == "--tls-key") o.tls_key_file = next();
     else if (a == "--bookmark-ms") o.bookmark_interval_ms = std::atoi(next().c_str());
     else if (a == "--history") o.history_limit = static_cast<size_t>(std::atol(next().c_str()));
+    else if (a == "--watch-coalesce-us") o.watch_coalesce_us = std::atoi(next().c_str());
     else if (a == "--manifest") manifests.push_back(next());
     else if (a == "--service-override") {
       std::string v = next();
