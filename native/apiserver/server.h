@@ -40,7 +40,7 @@ struct Options {
   // Watch write coalescing: after a wake-up with few events queued, wait this long for
   // more before writing (fewer wake-ups/syscalls per event at high event rates, at the
   // cost of up to this much added delivery latency).  0 = write immediately.
-  int watch_coalesce_us = 0;
+  int watch_coalesce_us = 50;  // measured on MI355X: +7 % CR/s, -6 % CPU/CR, lower p50 (profiles/watch_coalesce_r1/)
 };
 
 class ApiServer {
