@@ -79,6 +79,7 @@ int main() {
     rec.forget(rt, child);
     return true;
   });
+  ctrl.set_primary_deleted_hook([&](const json::Value& ub) { rec.forget_owner(kube::meta_name(ub)); });
   ctrl.run(
       *stop, [&](const kube::ObjPtr& o) { return rec.reconcile(o); },
       [&](const kube::ObjPtr& o, const std::exception& e) { return rec.error_policy(o, e); });

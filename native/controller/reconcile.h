@@ -72,6 +72,9 @@ class Reconciler {
   bool is_own_write(const kube::ResourceType& rt, const json::Value& child) const;
   // Drops the last-applied record of a deleted child (keeps the cache bounded under churn).
   void forget(const kube::ResourceType& rt, const json::Value& child);
+  // The UserBootstrap itself is gone: drop its fast-path state and its children's apply
+  // records (their DELETED events may be missed across a watch relist).
+  void forget_owner(const std::string& ub_name);
   size_t cached_children() const;
 
   struct Stats {

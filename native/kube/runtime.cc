@@ -314,6 +314,8 @@ void Controller::run(CancelToken& stop, Reconciler reconcile, ErrorPolicy error_
         for (const auto& o : ev.objects) queue_.add(primary_.key(meta_namespace(*o), meta_name(*o)));
       } else if (ev.type != WatchEvent::Type::Deleted) {
         queue_.add(primary_.key(meta_namespace(*ev.object), meta_name(*ev.object)));
+      } else if (primary_deleted_) {
+        primary_deleted_(*ev.object);
       }
     });
   });

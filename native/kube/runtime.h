@@ -158,6 +158,9 @@ class Controller {
   void set_child_filter(ChildFilter f) { child_filter_ = std::move(f); }
   // Called for every child DELETED event (e.g. to drop per-child caches).
   void set_child_deleted_hook(ChildFilter f) { child_deleted_ = std::move(f); }
+  // Called for every primary DELETED event (drop per-owner caches).
+  using PrimaryHook = std::function<void(const json::Value& primary)>;
+  void set_primary_deleted_hook(PrimaryHook f) { primary_deleted_ = std::move(f); }
   uint64_t filtered_events() const { return filtered_.load(); }
   // Extra trigger source (e.g. a periodic external refresh).
   void enqueue(const std::string& key) { queue_.add(key); }
@@ -182,6 +185,7 @@ class Controller {
   WorkQueue queue_;
   ChildFilter child_filter_;
   ChildFilter child_deleted_;
+  PrimaryHook primary_deleted_;
   std::atomic<uint64_t> filtered_{0};
 };
 
