@@ -106,11 +106,11 @@ void Reconciler::forget(const kube::ResourceType& rt, const Value& child) {
   gauge.set(static_cast<double>(last_applied_.size()));
 }
 
-void Reconciler::forget_owner(const std::string& ub_name) {
-  std::string ns = ub_name;
+void Reconciler::forget_owner(const std::string& owner) {
+  std::string ns = owner;
   for (auto& ch : ns) ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
   std::lock_guard<std::mutex> lk(mu_);
-  ub_state_.erase(ub_name);
+  ub_state_.erase(owner);
   last_applied_.erase(types::Namespace.plural + "//" + ns);
   for (const auto* rt : {&types::ResourceQuota, &types::Role, &types::RoleBinding})
     last_applied_.erase(rt->plural + "/" + ns + "/" + ns);

@@ -74,7 +74,7 @@ class Reconciler {
   void forget(const kube::ResourceType& rt, const json::Value& child);
   // The UserBootstrap itself is gone: drop its fast-path state and its children's apply
   // records (their DELETED events may be missed across a watch relist).
-  void forget_owner(const std::string& ub_name);
+  void forget_owner(const std::string& owner);
   size_t cached_children() const;
 
   struct Stats {
