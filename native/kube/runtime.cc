@@ -187,6 +187,21 @@ void WorkQueue::add_after(const std::string& key, std::chrono::milliseconds dela
   schedule_locked(key, t);
 }
 
+void WorkQueue::forget(const std::string& key) {
+  std::lock_guard<std::mutex> lk(mu_);
+  deferred_.erase(key);
+  auto d = due_.find(key);
+  if (d == due_.end()) return;
+  auto range = timeline_.equal_range(d->second);
+  for (auto it = range.first; it != range.second; ++it) {
+    if (it->second == key) {
+      timeline_.erase(it);
+      break;
+    }
+  }
+  due_.erase(d);
+}
+
 bool WorkQueue::get(std::string& key) {
   std::unique_lock<std::mutex> lk(mu_);
   while (true) {
@@ -314,8 +329,10 @@ void Controller::run(CancelToken& stop, Reconciler reconcile, ErrorPolicy error_
         for (const auto& o : ev.objects) queue_.add(primary_.key(meta_namespace(*o), meta_name(*o)));
       } else if (ev.type != WatchEvent::Type::Deleted) {
         queue_.add(primary_.key(meta_namespace(*ev.object), meta_name(*ev.object)));
-      } else if (primary_deleted_) {
-        primary_deleted_(*ev.object);
+      } else {
+        // the object is gone: its periodic requeue would only find nothing
+        queue_.forget(primary_.key(meta_namespace(*ev.object), meta_name(*ev.object)));
+        if (primary_deleted_) primary_deleted_(*ev.object);
       }
     });
   });

@@ -104,6 +104,9 @@ class WorkQueue {
   // Blocks until a key is due or the queue shuts down (returns false).
   bool get(std::string& key);
   void done(const std::string& key);
+  // Drops a pending (not in-flight) entry, e.g. the periodic requeue of an object that
+  // was deleted: keeps the queue proportional to live objects under churn.
+  void forget(const std::string& key);
   void shutdown();
   size_t pending() const;
   size_t in_flight() const;

@@ -71,6 +71,7 @@ void register_kube(py::module_& m) {
         return ok ? py::object(py::str(k)) : py::object(py::none());
       })
       .def("done", &bgc::kube::WorkQueue::done)
+      .def("forget", &bgc::kube::WorkQueue::forget)
       .def("shutdown", &bgc::kube::WorkQueue::shutdown)
       .def("pending", &bgc::kube::WorkQueue::pending)
       .def("in_flight", &bgc::kube::WorkQueue::in_flight);

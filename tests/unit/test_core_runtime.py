@@ -195,3 +195,32 @@ def test_workqueue_many_workers_no_lost_wakeups(nat):
     assert len(seen) == 600 and sum(seen.values()) == 660
     late.sort()
     assert late[len(late) // 2] < 0.05 and late[-1] < 1.0
+
+
+def test_workqueue_forget_drops_pending_requeue(nat):
+    import threading
+    import time
+
+    q = nat.WorkQueue()
+    q.add_after("gone", 50)   # e.g. the 30 s requeue of an object deleted since
+    q.add_after("kept", 80)
+    assert q.pending() == 2
+    q.forget("gone")
+    q.forget("never-added")   # no-op
+    assert q.pending() == 1
+    t0 = time.time()
+    assert q.get() == "kept"  # the forgotten key is never handed out
+    assert time.time() - t0 >= 0.06
+    q.done("kept")
+    # an in-flight key is not affected: forget only drops pending entries
+    q.add("busy")
+    assert q.get() == "busy"
+    q.forget("busy")
+    q.add("busy")             # deferred re-add while processing
+    q.done("busy")
+    got = []
+    th = threading.Thread(target=lambda: got.append(q.get()))
+    th.start()
+    th.join(2)
+    assert got == ["busy"]
+    q.shutdown()
