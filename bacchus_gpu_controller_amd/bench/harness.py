@@ -350,6 +350,15 @@ def run(args):
         if args.report_cpu and cluster is not None:
             out["component_cpu_s"] = {name: _cpu_seconds(p.p.pid) for name, p in cluster.procs.items()}
             out["component_rss_mb"] = {name: _rss_mb(p.p.pid) for name, p in cluster.procs.items()}
+            try:  # controller cache sizes (bounded-memory check under churn)
+                import requests
+
+                txt = requests.get(info["controller"] + "/metrics", timeout=10).text
+                out["controller_gauges"] = {l.split()[0]: float(l.split()[1]) for l in txt.splitlines()
+                                            if l.startswith(("bgc_controller_apply_cache_entries",
+                                                             "bgc_controller_queue_depth"))}
+            except Exception:  # noqa: BLE001
+                pass
         return out
     finally:
         if cluster is not None:

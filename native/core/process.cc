@@ -4,6 +4,8 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
+#include <thread>
 
 #include "core/cpuprof.h"
 #include "core/log.h"
@@ -18,8 +20,25 @@ void tune_malloc() {
   mallopt(M_MMAP_THRESHOLD, 4 << 20);
 }
 
+// The trim threshold above keeps freed heap resident between bursts (no madvise churn on
+// the hot path); a low-frequency malloc_trim hands memory that stayed free back to the OS,
+// so a long-running service's RSS follows its live data instead of its historical peak.
+// BGC_MALLOC_TRIM_SECS (default 30; 0 disables).
+void start_malloc_trimmer() {
+  const char* e = std::getenv("BGC_MALLOC_TRIM_SECS");
+  const long secs = e ? std::atol(e) : 30;
+  if (secs <= 0) return;
+  std::thread([secs] {
+    while (true) {
+      std::this_thread::sleep_for(std::chrono::seconds(secs));
+      malloc_trim(0);
+    }
+  }).detach();
+}
+
 void process_init() {
   tune_malloc();
+  start_malloc_trimmer();
   log::init_from_env();
   cpuprof::start_from_env();
 }

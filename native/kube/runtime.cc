@@ -161,7 +161,22 @@ bool Store::wait_synced(std::chrono::milliseconds timeout) const {
 // WorkQueue
 
 void WorkQueue::schedule_locked(const std::string& key, Clock::time_point t) {
-  due_[key] = t;
+  auto d = due_.find(key);
+  if (d != due_.end()) {
+    // Moving a key earlier (an event arriving for a key with a pending 30 s requeue):
+    // drop its old timeline node now rather than leaving a stale one for up to the
+    // requeue period, which under churn piles up by the hundreds of thousands.
+    auto range = timeline_.equal_range(d->second);
+    for (auto it = range.first; it != range.second; ++it) {
+      if (it->second == key) {
+        timeline_.erase(it);
+        break;
+      }
+    }
+    d->second = t;
+  } else {
+    due_.emplace(key, t);
+  }
   timeline_.emplace(t, key);
   if (t <= Clock::now()) {
     if (idle_ > 0) cv_.notify_one();
