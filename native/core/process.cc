@@ -1,6 +1,8 @@
 #include "core/process.h"
 
 #include <malloc.h>
+#include <pthread.h>
+#include <signal.h>
 
 #include <cstdlib>
 #include <cstring>
@@ -29,6 +31,11 @@ void start_malloc_trimmer() {
   const long secs = e ? std::atol(e) : 30;
   if (secs <= 0) return;
   std::thread([secs] {
+    // Never take process signals here: SIGTERM/SIGINT are collected by the sigwait thread
+    // that install_shutdown_signals starts (this thread exists before that mask is set).
+    sigset_t all;
+    sigfillset(&all);
+    pthread_sigmask(SIG_BLOCK, &all, nullptr);
     while (true) {
       std::this_thread::sleep_for(std::chrono::seconds(secs));
       malloc_trim(0);
