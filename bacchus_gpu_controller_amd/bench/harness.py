@@ -350,6 +350,11 @@ def run(args):
         if args.report_cpu and cluster is not None:
             out["component_cpu_s"] = {name: _cpu_seconds(p.p.pid) for name, p in cluster.procs.items()}
             out["component_rss_mb"] = {name: _rss_mb(p.p.pid) for name, p in cluster.procs.items()}
+            try:
+                st = cluster.stats()
+                out["apiserver_objects"] = {"live": st.get("objects"), "gc_collected": st.get("gc_collected")}
+            except Exception:  # noqa: BLE001
+                pass
             try:  # controller cache sizes (bounded-memory check under churn)
                 import requests
 
