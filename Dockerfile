@@ -25,5 +25,5 @@ COPY --from=build /src/bin/ /app/
 # GLIBC_TUNABLES: deeper malloc tcache (+14% CR/s measured, profiles/malloc_tunables_r1/)
 ENV BGC_GPU_DIAG_LIB=/app/libbgc_gpu_diag.so \
     LD_LIBRARY_PATH=/opt/rocm/lib \
-    GLIBC_TUNABLES=glibc.malloc.tcache_count=1024:glibc.malloc.tcache_max=16384
+    GLIBC_TUNABLES=glibc.malloc.tcache_count=64:glibc.malloc.tcache_max=16384
 USER 65532:65532

@@ -40,7 +40,7 @@ def free_port():
 # services' many short-lived JSON allocations off the shared arenas.  Measured on the
 # MI355X box: +14% CR/s, -12% control-plane CPU per CR (profiles/malloc_tunables_r1/).
 # The container image sets the same value (Dockerfile ENV).
-SERVICE_GLIBC_TUNABLES = "glibc.malloc.tcache_count=1024:glibc.malloc.tcache_max=16384"
+SERVICE_GLIBC_TUNABLES = "glibc.malloc.tcache_count=64:glibc.malloc.tcache_max=16384"
 
 
 class Proc:
