@@ -413,7 +413,8 @@ static thread_local std::vector<std::string> t_stage_keys;
 
 class Parser {
  public:
-  explicit Parser(std::string_view t) : s_(t), vals_(t_stage_vals), keys_(t_stage_keys) {
+  explicit Parser(std::string_view t, std::string_view drop_key = {})
+      : s_(t), drop_key_(drop_key), vals_(t_stage_vals), keys_(t_stage_keys) {
     vals_.clear();
     keys_.clear();
   }
@@ -526,6 +527,19 @@ class Parser {
           if (p_ >= s_.size() || s_[p_] != ':') fail("expected `:`");
           ++p_;
           skip_ws();
+          if (!drop_key_.empty() && key == drop_key_) {
+            skip_value();
+            skip_ws();
+            if (p_ >= s_.size()) fail("EOF while parsing an object");
+            if (s_[p_] == ',') {
+              ++p_;
+              continue;
+            }
+            if (s_[p_] != '}') fail("expected `,` or `}`");
+            ++p_;
+            finish_object(out, base, kbase);
+            return;
+          }
           Value child;
           parse_value(child, depth + 1);
           // Duplicate keys: last one wins (serde_json Value behaviour).
@@ -549,15 +563,7 @@ class Parser {
           }
           if (s_[p_] == '}') {
             ++p_;
-            const size_t n = keys_.size() - kbase;
-            out.arr_.reserve(n);
-            out.keys_.reserve(n);
-            for (size_t i = 0; i < n; ++i) {
-              out.keys_.push_back(std::move(keys_[kbase + i]));
-              out.arr_.push_back(std::move(vals_[base + i]));
-            }
-            keys_.resize(kbase);
-            vals_.resize(base);
+            finish_object(out, base, kbase);
             return;
           }
           fail("expected `,` or `}`");
@@ -607,6 +613,71 @@ class Parser {
       out.push_back(static_cast<char>(0x80 | ((cp >> 6) & 0x3F)));
       out.push_back(static_cast<char>(0x80 | (cp & 0x3F)));
     }
+  }
+
+  void finish_object(Value& out, size_t base, size_t kbase) {
+    const size_t n = keys_.size() - kbase;
+    out.arr_.reserve(n);
+    out.keys_.reserve(n);
+    for (size_t i = 0; i < n; ++i) {
+      out.keys_.push_back(std::move(keys_[kbase + i]));
+      out.arr_.push_back(std::move(vals_[base + i]));
+    }
+    keys_.resize(kbase);
+    vals_.resize(base);
+  }
+
+  void skip_string() {
+    ++p_;  // opening quote
+    while (p_ < s_.size()) {
+      const char c = s_[p_];
+      if (c == '\\') {
+        p_ += 2;
+      } else if (c == '"') {
+        ++p_;
+        return;
+      } else {
+        ++p_;
+      }
+    }
+    fail("EOF while parsing a string");
+  }
+
+  // Steps over one value without materialising it (see parse(text, drop_key)).
+  void skip_value() {
+    if (p_ >= s_.size()) fail("EOF while parsing a value");
+    const char c = s_[p_];
+    if (c == '"') {
+      skip_string();
+      return;
+    }
+    if (c == '{' || c == '[') {
+      int nest = 0;
+      while (p_ < s_.size()) {
+        const char d = s_[p_];
+        if (d == '"') {
+          skip_string();
+          continue;
+        }
+        if (d == '{' || d == '[') {
+          if (++nest > 512) fail("recursion limit exceeded");
+        } else if (d == '}' || d == ']') {
+          if (--nest == 0) {
+            ++p_;
+            return;
+          }
+        }
+        ++p_;
+      }
+      fail("EOF while parsing a value");
+    }
+    const size_t start = p_;
+    while (p_ < s_.size()) {
+      const char d = s_[p_];
+      if (d == ',' || d == '}' || d == ']' || d == ' ' || d == '\n' || d == '\r' || d == '\t') break;
+      ++p_;
+    }
+    if (p_ == start) fail("expected value");
   }
 
   void parse_string(std::string& out) {
@@ -716,12 +787,14 @@ class Parser {
   }
 
   std::string_view s_;
+  std::string_view drop_key_;
   size_t p_ = 0;
   std::vector<Value>& vals_;
   std::vector<std::string>& keys_;
 };
 
 Value parse(std::string_view text) { return Parser(text).parse_document(); }
+Value parse(std::string_view text, std::string_view drop_key) { return Parser(text, drop_key).parse_document(); }
 
 bool try_parse(std::string_view text, Value& out, std::string* err) {
   try {

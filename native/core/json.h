@@ -132,6 +132,11 @@ class Value {
 };
 
 Value parse(std::string_view text);
+// Parses, dropping every object member named `drop_key` (at any depth) without building its
+// value: a watch consumer that never reads metadata.managedFields skips the largest part of
+// an SSA-managed object.  The dropped value is scanned for balanced brackets and closed
+// strings only, not fully validated.
+Value parse(std::string_view text, std::string_view drop_key);
 // Parses; returns false (and fills err) instead of throwing.
 bool try_parse(std::string_view text, Value& out, std::string* err = nullptr);
 

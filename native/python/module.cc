@@ -29,7 +29,9 @@ namespace {
 std::string yaml_to_json(const std::string& y) { return bgc::yaml::parse(y).dump(); }
 std::string json_to_yaml(const std::string& j) { return bgc::yaml::emit(bgc::json::parse(j)); }
 
-std::string json_roundtrip(const std::string& j) { return bgc::json::parse(j).dump(); }
+std::string json_roundtrip(const std::string& j, const std::string& drop_key) {
+  return (drop_key.empty() ? bgc::json::parse(j) : bgc::json::parse(j, drop_key)).dump();
+}
 
 std::string apply_json_patch(const std::string& doc, const std::string& patch) {
   Value d = bgc::json::parse(doc);
@@ -73,7 +75,7 @@ PYBIND11_MODULE(_native, m) {
   py::register_exception<bgc::yaml::Error>(m, "YamlError", PyExc_ValueError);
   py::register_exception<bgc::ConfigError>(m, "ConfigError", PyExc_ValueError);
 
-  m.def("json_roundtrip", &json_roundtrip);
+  m.def("json_roundtrip", &json_roundtrip, py::arg("text"), py::arg("drop_key") = "");
   m.def("yaml_to_json", &yaml_to_json);
   m.def("json_to_yaml", &json_to_yaml);
   m.def("apply_json_patch", &apply_json_patch);

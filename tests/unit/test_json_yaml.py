@@ -18,6 +18,23 @@ def test_json_rejects_invalid(nat, bad):
         nat.json_roundtrip(bad)
 
 
+def test_json_parse_drops_key_at_any_depth(nat):
+    """Watchers parse events with managedFields skipped (native/kube/runtime.cc)."""
+    mf = [{"manager": "m", "fieldsV1": {"f:spec": {"f:hard": {".": {}, 'f:"x}]': {}}}}, "time": "t"}]
+    obj = {"type": "ADDED", "object": {"metadata": {"name": "a", "managedFields": mf, "labels": {"k": "v"}},
+                                       "spec": {"managedFields": "s\\\"]}", "n": [1, {"managedFields": 1.5e3}]},
+                                       "managedFields": None}}
+    out = json.loads(nat.json_roundtrip(json.dumps(obj), drop_key="managedFields"))
+    assert out == {"type": "ADDED", "object": {"metadata": {"name": "a", "labels": {"k": "v"}},
+                                               "spec": {"n": [1, {}]}}}
+    # last member dropped, whitespace around it, and an empty object left behind
+    assert json.loads(nat.json_roundtrip('{"a":1, "managedFields" : [ ] }', drop_key="managedFields")) == {"a": 1}
+    assert nat.json_roundtrip('{"managedFields":{"x":[1,2]}}', drop_key="managedFields") == "{}"
+    for bad in ('{"managedFields":', '{"managedFields":[1,2}', '{"managedFields":"abc}', '{"managedFields":}'):
+        with pytest.raises(ValueError):
+            nat.json_roundtrip(bad, drop_key="managedFields")
+
+
 def test_json_surrogate_pairs(nat):
     assert json.loads(nat.json_roundtrip('"\\ud83d\\ude00"')) == "\U0001F600"
 
