@@ -27,6 +27,25 @@ def test_json_roundtrip_matches_python(nat, v):
     assert json.loads(nat.json_roundtrip(json.dumps(v))) == v
 
 
+def _drop(v, key):
+    if isinstance(v, dict):
+        return {k: _drop(x, key) for k, x in v.items() if k != key}
+    if isinstance(v, list):
+        return [_drop(x, key) for x in v]
+    return v
+
+
+@settings(max_examples=300, deadline=None)
+@given(json_values(st.none() | st.booleans() | I64 | FLOATS | TEXT), st.sampled_from(["", "a", "managedFields"]),
+       st.booleans())
+def test_json_drop_key_parse_matches_python(nat, v, key, pretty):
+    """parse(text, drop_key) == python parse with that key removed at every depth."""
+    text = json.dumps({"managedFields": v, "x": [v, {"a": v}]} if key else v, indent=2 if pretty else None)
+    if not key:
+        key = "managedFields"
+    assert json.loads(nat.json_roundtrip(text, drop_key=key)) == _drop(json.loads(text), key)
+
+
 @settings(max_examples=200, deadline=None)
 @given(json_values(st.none() | st.booleans() | I64 | TEXT))
 def test_yaml_emit_parses_back_with_our_parser(nat, v):
