@@ -18,6 +18,7 @@ total Ready CRs / wall time of the K timed steps (max over ranks).
 import argparse
 import json
 import os
+import resource
 import statistics
 import sys
 import time
@@ -263,6 +264,7 @@ def run(args):
                     lock0 = _kl_lock(info)
                 d.barrier()
                 t_start = time.perf_counter()
+                ru0 = resource.getrusage(resource.RUSAGE_SELF)
             names = _names(d.rank, s, args.batch)
             res = json.loads(driver.step_with_delete(names, prev or [], args.timeout))
             prev = names
@@ -278,11 +280,13 @@ def run(args):
         d.sync()
         d.barrier()
         elapsed = time.perf_counter() - t_start
+        ru1 = resource.getrusage(resource.RUSAGE_SELF)
+        driver_cpu = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
         elapsed = d.max_scalar(elapsed)
         driver.remove(prev)
         driver.stop()
         per_rank = d.gather_obj({"ready": ready, "failed": failed, "timeouts": timeouts, "lat": lat, "clat": clat,
-                                 "stage": stage, "errors": errors[:3]})
+                                 "stage": stage, "errors": errors[:3], "driver_cpu_s": driver_cpu})
         if d.rank != 0:
             return None
         lock1 = _kl_lock(info)
@@ -349,6 +353,8 @@ def run(args):
             out["errors"] = [e for p in per_rank for e in p["errors"]][:5]
         if args.report_cpu and cluster is not None:
             out["component_cpu_s"] = {name: _cpu_seconds(p.p.pid) for name, p in cluster.procs.items()}
+            # the load generator (native churn driver in each rank) shares the CPU quota
+            out["driver_cpu_s_timed"] = round(sum(p["driver_cpu_s"] for p in per_rank), 3)
             out["component_rss_mb"] = {name: _rss_mb(p.p.pid) for name, p in cluster.procs.items()}
             try:
                 st = cluster.stats()
