@@ -4,6 +4,9 @@
 #include <chrono>
 #include <cmath>
 #include <cstring>
+#include <fstream>
+#include <malloc.h>
+#include <unistd.h>
 #include <sstream>
 
 #include "core/json.h"
@@ -184,6 +187,8 @@ SampleRing& Registry::samples(const std::string& name) {
   return *slot;
 }
 
+void append_process_memory(std::string& out);
+
 std::string Registry::render() const {
   std::lock_guard<std::mutex> lk(mu_);
   std::string out;
@@ -208,7 +213,29 @@ std::string Registry::render() const {
       out += name + "_count" + lbl + " " + std::to_string(h->count()) + "\n";
     }
   }
+  append_process_memory(out);
   return out;
+}
+
+// Process memory next to the registry's families: RSS from /proc/self/statm and the glibc
+// heap split into bytes handed out (including chunks parked in per-thread caches) and free
+// bytes kept by the arenas (address space, not RSS: malloc_trim returns their pages).
+void append_process_memory(std::string& out) {
+  long pages_total = 0, pages_rss = 0;
+  {
+    std::ifstream statm("/proc/self/statm");
+    statm >> pages_total >> pages_rss;
+  }
+  const double page = static_cast<double>(sysconf(_SC_PAGESIZE));
+  const struct mallinfo2 mi = mallinfo2();
+  auto gauge = [&out](const char* name, const char* help, double v) {
+    out += std::string("# HELP ") + name + " " + help + "\n# TYPE " + name + " gauge\n" + name + " " + fmt_double(v) + "\n";
+  };
+  gauge("bgc_process_resident_memory_bytes", "Resident set size", static_cast<double>(pages_rss) * page);
+  gauge("bgc_heap_allocated_bytes", "malloc bytes in use (arena + mmapped chunks, incl. thread caches)",
+        static_cast<double>(mi.uordblks + mi.hblkhd));
+  gauge("bgc_heap_free_bytes", "free bytes in malloc arenas (address space; trimmed pages are not resident)",
+        static_cast<double>(mi.fordblks));
 }
 
 std::vector<std::string> Registry::sample_names() const {

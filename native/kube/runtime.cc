@@ -193,6 +193,18 @@ void WorkQueue::schedule_locked(const std::string& key, Clock::time_point t) {
 void WorkQueue::add_after(const std::string& key, std::chrono::milliseconds delay) {
   auto t = Clock::now() + delay;
   std::lock_guard<std::mutex> lk(mu_);
+  if (!forgotten_.empty()) forgotten_.erase(key);
+  add_after_locked(key, t);
+}
+
+void WorkQueue::requeue(const std::string& key, std::chrono::milliseconds delay) {
+  auto t = Clock::now() + delay;
+  std::lock_guard<std::mutex> lk(mu_);
+  if (!forgotten_.empty() && forgotten_.count(key)) return;
+  add_after_locked(key, t);
+}
+
+void WorkQueue::add_after_locked(const std::string& key, Clock::time_point t) {
   if (shutdown_) return;
   if (processing_.count(key)) {
     auto it = deferred_.find(key);
@@ -207,6 +219,7 @@ void WorkQueue::add_after(const std::string& key, std::chrono::milliseconds dela
 void WorkQueue::forget(const std::string& key) {
   std::lock_guard<std::mutex> lk(mu_);
   deferred_.erase(key);
+  if (processing_.count(key)) forgotten_.insert(key);
   auto d = due_.find(key);
   if (d == due_.end()) return;
   auto range = timeline_.equal_range(d->second);
@@ -258,6 +271,7 @@ bool WorkQueue::get(std::string& key) {
 void WorkQueue::done(const std::string& key) {
   std::lock_guard<std::mutex> lk(mu_);
   processing_.erase(key);
+  if (!forgotten_.empty()) forgotten_.erase(key);
   auto it = deferred_.find(key);
   if (it != deferred_.end()) {
     auto t = it->second;
@@ -367,7 +381,11 @@ void Controller::run(CancelToken& stop, Reconciler reconcile, ErrorPolicy error_
         } else {
           if (ev.type == WatchEvent::Type::Deleted) {
             if (child_deleted_) child_deleted_(c->rt, *ev.object);
-            for (const auto& k : c->mapper(*ev.object)) queue_.add_after(k, opts_.child_delete_delay);
+            // An owner that is already gone (the usual cascade after a UserBootstrap is
+            // deleted) has nothing to repair: no trigger.
+            for (const auto& k : c->mapper(*ev.object)) {
+              if (primary_store_->get(k)) queue_.add_after(k, opts_.child_delete_delay);
+            }
             return;
           }
           if (child_filter_ && !child_filter_(c->rt, *ev.object)) {
@@ -398,8 +416,9 @@ void Controller::run(CancelToken& stop, Reconciler reconcile, ErrorPolicy error_
         } catch (const std::exception& e) {
           a = error_policy(obj, e);
         }
-        if (a.requeue) queue_.add_after(key, a.after);
+        if (a.requeue) queue_.requeue(key, a.after);
         queue_.done(key);
+        q_depth.set(static_cast<double>(queue_.pending()));
       }
     });
   }

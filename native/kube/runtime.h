@@ -104,9 +104,13 @@ class WorkQueue {
   // Blocks until a key is due or the queue shuts down (returns false).
   bool get(std::string& key);
   void done(const std::string& key);
-  // Drops a pending (not in-flight) entry, e.g. the periodic requeue of an object that
-  // was deleted: keeps the queue proportional to live objects under churn.
+  // Drops a pending entry, e.g. the periodic requeue of an object that was deleted: keeps
+  // the queue proportional to live objects under churn.  A key forgotten while in flight
+  // also ignores the worker's own requeue() of it (the reconcile that raced the deletion);
+  // an add()/add_after() (a new event, e.g. the object re-created) clears that.
   void forget(const std::string& key);
+  // The worker's periodic/error requeue of the key it is processing.
+  void requeue(const std::string& key, std::chrono::milliseconds delay);
   void shutdown();
   size_t pending() const;
   size_t in_flight() const;
@@ -125,6 +129,8 @@ class WorkQueue {
   std::multimap<Clock::time_point, std::string> timeline_;  // due time -> key (may hold stale entries)
   std::set<std::string> processing_;
   std::map<std::string, Clock::time_point> deferred_;      // re-added while processing
+  std::set<std::string> forgotten_;                        // forgotten while processing
+  void add_after_locked(const std::string& key, Clock::time_point t);
   bool shutdown_ = false;
 };
 

@@ -72,6 +72,7 @@ void register_kube(py::module_& m) {
       })
       .def("done", &bgc::kube::WorkQueue::done)
       .def("forget", &bgc::kube::WorkQueue::forget)
+      .def("requeue", [](bgc::kube::WorkQueue& q, const std::string& k, int ms) { q.requeue(k, std::chrono::milliseconds(ms)); })
       .def("shutdown", &bgc::kube::WorkQueue::shutdown)
       .def("pending", &bgc::kube::WorkQueue::pending)
       .def("in_flight", &bgc::kube::WorkQueue::in_flight);

@@ -224,3 +224,31 @@ def test_workqueue_forget_drops_pending_requeue(nat):
     th.join(2)
     assert got == ["busy"]
     q.shutdown()
+
+
+def test_workqueue_forget_while_in_flight_drops_the_workers_requeue(nat):
+    """The object is deleted while its reconcile runs: the reconcile's 30 s requeue is not kept
+    (native/kube/runtime.cc WorkQueue::requeue), unless a new event re-adds the key."""
+    q = nat.WorkQueue()
+    q.add("gone")
+    assert q.get() == "gone"
+    q.forget("gone")          # DELETED event arrives mid-reconcile
+    q.requeue("gone", 30000)  # the reconcile finishes and asks for its periodic requeue
+    q.done("gone")
+    assert q.pending() == 0
+    # re-created while in flight: the ADDED event's add() wins over the forget
+    q.add("back")
+    assert q.get() == "back"
+    q.forget("back")
+    q.add_after("back", 30000)
+    q.requeue("back", 30000)
+    q.done("back")
+    assert q.pending() == 1
+    # the forgotten mark ends with the reconcile: a later requeue of the key is kept
+    q.add("again")
+    assert q.get() == "again"
+    q.forget("again")
+    q.done("again")
+    q.requeue("again", 30000)
+    assert q.pending() == 2
+    q.shutdown()
