@@ -367,7 +367,9 @@ def run(args):
                 txt = requests.get(info["controller"] + "/metrics", timeout=10).text
                 out["controller_gauges"] = {l.split()[0]: float(l.split()[1]) for l in txt.splitlines()
                                             if l.startswith(("bgc_controller_apply_cache_entries",
-                                                             "bgc_controller_queue_depth", "bgc_heap_"))}
+                                                             "bgc_controller_queue_depth", "bgc_heap_",
+                                                             "bgc_controller_owner_state_entries",
+                                                             "bgc_controller_store_objects"))}
             except Exception:  # noqa: BLE001
                 pass
         return out

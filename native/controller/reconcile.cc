@@ -94,16 +94,23 @@ Reconciler::Stats Reconciler::stats() const {
 
 static std::string child_key(const DesiredChild& c) { return c.rt->plural + "/" + c.ns + "/" + c.name; }
 
+// Publishes the sizes of the two per-tenant caches (bounded-memory check under churn).
+static void publish_cache_sizes(size_t applied, size_t owners) {
+  static auto& reg = metrics::Registry::global();
+  static auto& a = reg.gauge("bgc_controller_apply_cache_entries", "Children with a remembered last apply");
+  static auto& o = reg.gauge("bgc_controller_owner_state_entries", "UserBootstraps with fast-path state");
+  a.set(static_cast<double>(applied));
+  o.set(static_cast<double>(owners));
+}
+
 void Reconciler::forget(const kube::ResourceType& rt, const Value& child) {
   std::string key = rt.plural + "/" + kube::meta_namespace(child) + "/" + kube::meta_name(child);
-  static auto& gauge = metrics::Registry::global().gauge("bgc_controller_apply_cache_entries",
-                                                         "Children with a remembered last apply");
   std::lock_guard<std::mutex> lk(mu_);
   last_applied_.erase(key);
   for (const auto& ref : child.get("metadata").get("ownerReferences").items()) {
     if (ref.get_string("kind") == types::UserBootstrap.kind) ub_state_.erase(ref.get_string("name"));
   }
-  gauge.set(static_cast<double>(last_applied_.size()));
+  publish_cache_sizes(last_applied_.size(), ub_state_.size());
 }
 
 void Reconciler::forget_owner(const std::string& owner) {
@@ -114,6 +121,7 @@ void Reconciler::forget_owner(const std::string& owner) {
   last_applied_.erase(types::Namespace.plural + "//" + ns);
   for (const auto* rt : {&types::ResourceQuota, &types::Role, &types::RoleBinding})
     last_applied_.erase(rt->plural + "/" + ns + "/" + ns);
+  publish_cache_sizes(last_applied_.size(), ub_state_.size());
 }
 
 bool Reconciler::fresh(const std::string& owner_name, const std::string& owner_rv) {
@@ -161,11 +169,9 @@ void Reconciler::apply_child(const DesiredChild& c, const std::string& body_hash
   static auto& applied = metrics::Registry::global().counter("bgc_apply_total", "Server-side applies issued");
   Value res = client_.apply(*c.rt, c.ns, c.name, c.body, kFieldManager, /*force=*/true);
   applied.inc();
-  static auto& gauge = metrics::Registry::global().gauge("bgc_controller_apply_cache_entries",
-                                                         "Children with a remembered last apply");
   std::lock_guard<std::mutex> lk(mu_);
   last_applied_[child_key(c)] = {body_hash, kube::meta_rv(res)};
-  gauge.set(static_cast<double>(last_applied_.size()));
+  publish_cache_sizes(last_applied_.size(), ub_state_.size());
   stats_.applied++;
 }
 
@@ -244,6 +250,7 @@ kube::Action Reconciler::reconcile(const kube::ObjPtr& ub_ptr) {
       st.children.push_back({c.rt, c.ns, c.name, it->second.rv});
     }
     if (complete) ub_state_[owner_name] = std::move(st);
+    publish_cache_sizes(last_applied_.size(), ub_state_.size());
   }
   static auto& ok = reg.counter("bgc_reconcile_total", "Reconciles", {{"result", "ok"}});
   ok.inc();

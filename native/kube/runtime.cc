@@ -351,11 +351,18 @@ bool Controller::wait_synced(std::chrono::milliseconds timeout) {
 
 void Controller::run(CancelToken& stop, Reconciler reconcile, ErrorPolicy error_policy) {
   std::vector<std::thread> threads;
+  auto store_gauge = [](const ResourceType& rt) -> metrics::Gauge& {
+    return metrics::Registry::global().gauge("bgc_controller_store_objects", "Objects in the controller's watch cache",
+                                             {{"resource", rt.plural}});
+  };
+  auto& primary_gauge = store_gauge(primary_);
+  for (auto& cp : children_) cp->gauge = &store_gauge(cp->rt);
   // primary watcher: trigger_self
   threads.emplace_back([&] {
     Watcher w(client_, primary_);
     w.run(stop, [&](const WatchEvent& ev) {
       primary_store_->apply(ev);
+      primary_gauge.set(static_cast<double>(primary_store_->size()));
       if (ev.type == WatchEvent::Type::Restarted) {
         for (const auto& o : ev.objects) queue_.add(primary_.key(meta_namespace(*o), meta_name(*o)));
       } else if (ev.type != WatchEvent::Type::Deleted) {
@@ -374,6 +381,7 @@ void Controller::run(CancelToken& stop, Reconciler reconcile, ErrorPolicy error_
       Watcher w(client_, c->rt);
       w.run(stop, [&, c](const WatchEvent& ev) {
         c->store->apply(ev);
+        c->gauge->set(static_cast<double>(c->store->size()));
         if (ev.type == WatchEvent::Type::Restarted) {
           for (const auto& o : ev.objects) {
             for (const auto& k : c->mapper(*o)) queue_.add(k);

@@ -22,6 +22,8 @@
 #include <string>
 #include <thread>
 #include <unordered_map>
+
+#include "core/metrics.h"
 #include <vector>
 
 #include "core/cancel.h"
@@ -185,6 +187,7 @@ class Controller {
     ResourceType rt;
     Mapper mapper;
     std::unique_ptr<Store> store;
+    metrics::Gauge* gauge = nullptr;  // bgc_controller_store_objects{resource=...}
   };
   KubeClient& client_;
   ResourceType primary_;
