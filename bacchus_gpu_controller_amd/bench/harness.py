@@ -358,7 +358,8 @@ def run(args):
             out["component_rss_mb"] = {name: _rss_mb(p.p.pid) for name, p in cluster.procs.items()}
             try:
                 st = cluster.stats()
-                out["apiserver_objects"] = {"live": st.get("objects"), "gc_collected": st.get("gc_collected")}
+                out["apiserver_objects"] = {"live": st.get("objects"), "gc_collected": st.get("gc_collected"),
+                                            "gc_pending": st.get("gc_pending")}
             except Exception:  # noqa: BLE001
                 pass
             try:  # controller cache sizes (bounded-memory check under churn)

@@ -1947,6 +1947,10 @@ struct ApiServer::Impl {
                                       {"requests", static_cast<unsigned long long>(requests.load())},
                                       {"faults_hit", static_cast<unsigned long long>(faults_hit.load())},
                                       {"gc_collected", static_cast<unsigned long long>(gc_collected.load())},
+                                      {"gc_pending", static_cast<unsigned long long>([&] {
+                                         std::lock_guard<std::mutex> g(gc_mu);
+                                         return gc_queue.size();
+                                       }())},
                                       // summed over the per-type store locks; by_type_lock has the split
                                       {"store_lock", Value::object({
                                           {"acquisitions", static_cast<unsigned long long>(acq)},
