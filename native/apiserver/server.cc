@@ -470,7 +470,7 @@ struct ApiServer::Impl {
   std::deque<GcItem> gc_queue;
   bool gc_stop = false;
   std::atomic<uint64_t> gc_collected{0};
-  std::thread gc_thread;
+  std::vector<std::thread> gc_threads;
 
   std::unordered_map<std::string, UserInfo> tokens;
 
@@ -498,7 +498,7 @@ struct ApiServer::Impl {
       types[ti.key()] = ti;
     }
     if (!opts.token_file.empty()) load_tokens(opts.token_file);
-    gc_thread = std::thread([this] { gc_loop(); });
+    for (int i = 0; i < std::max(1, opts.gc_workers); ++i) gc_threads.emplace_back([this] { gc_loop(); });
   }
 
   ~Impl() {
@@ -507,7 +507,7 @@ struct ApiServer::Impl {
       gc_stop = true;
     }
     gc_cv.notify_all();
-    if (gc_thread.joinable()) gc_thread.join();
+    for (auto& t : gc_threads) t.join();
   }
 
   template <typename F>

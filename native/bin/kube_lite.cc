@@ -24,7 +24,8 @@ static void usage() {
   std::fprintf(stderr,
                "usage: kube-lite [--addr A] [--port P] [--port-file F] [--token-file F] [--no-anonymous]\n"
                "                 [--tls-cert F --tls-key F] [--service-override ns/name=host:port]...\n"
-               "                 [--bookmark-ms N] [--history N] [--manifest file.{json,yaml}]...\n");
+               "                 [--bookmark-ms N] [--history N] [--watch-coalesce-us N] [--gc-workers N]\n"
+               "                 [--manifest file.{json,yaml}]...\n");
 }
 
 int main(int argc, char** argv) {
@@ -51,6 +52,7 @@ int main(int argc, char** argv) {
     else if (a == "--bookmark-ms") o.bookmark_interval_ms = std::atoi(next().c_str());
     else if (a == "--history") o.history_limit = static_cast<size_t>(std::atol(next().c_str()));
     else if (a == "--watch-coalesce-us") o.watch_coalesce_us = std::atoi(next().c_str());
+    else if (a == "--gc-workers") o.gc_workers = std::atoi(next().c_str());
     else if (a == "--manifest") manifests.push_back(next());
     else if (a == "--service-override") {
       std::string v = next();
