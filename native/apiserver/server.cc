@@ -1282,7 +1282,7 @@ struct ApiServer::Impl {
       }
       // no-op short-circuit (before admission, like the apiserver's update path)
       if (exists && same_content(obj, *cur_copy.obj) && managers == cur_copy.managers) {
-        return {cur_copy.obj, 200};
+        return {cur_copy.obj, 200, nullptr};
       }
       call_webhooks(ti, sub, op, ns, name, &obj, exists ? cur_copy.obj.get() : nullptr, user);
       // identity fields cannot be changed by mutation
@@ -1292,7 +1292,7 @@ struct ApiServer::Impl {
       validate_object(ti, name, ns, obj);
       // everything below up to the lock depends only on cur_copy, which the commit re-checks
       if (exists && same_content(obj, *cur_copy.obj) && managers == cur_copy.managers) {
-        return {cur_copy.obj, 200};  // mutation turned it into a no-op
+        return {cur_copy.obj, 200, nullptr};  // mutation turned it into a no-op
       }
       if (exists && spec_changed(*cur_copy.obj, obj)) {
         int64_t gen = cur_copy.obj->get("metadata").get("generation").is_int()
@@ -1310,7 +1310,7 @@ struct ApiServer::Impl {
         // finalizer-gated deletion completes when the last finalizer is removed
         if (obj.get("metadata").contains("deletionTimestamp") && obj.get("metadata").get("finalizers").empty()) {
           erase_locked(ti, ns, name);
-          return {cur_copy.obj, 200};
+          return {cur_copy.obj, 200, nullptr};
         }
         (void)is_status;
         WriteResult wr;
