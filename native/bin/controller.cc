@@ -50,13 +50,12 @@ int main() {
   }
   LOG_INFO("controller") << "starting server on " << cfg.listen_addr << ":" << health.port();
 
-  if (cfg.leader_election) {
-    kube::LeaderElector le(*client, cfg.lease_namespace, cfg.lease_name);
-    if (!le.acquire(*stop)) {
-      health.stop();
-      return 0;
-    }
-    le.keep_renewing(stop);
+  // The elector lives in main's scope so its renew thread runs until the controller exits.
+  bool standby_stopped = false;
+  std::unique_ptr<kube::LeaderElector> leader = kube::lead_or_wait(*client, cfg.lease, stop, &standby_stopped);
+  if (standby_stopped) {
+    health.stop();
+    return 0;
   }
 
   kube::Controller::Options co;

@@ -63,13 +63,13 @@ int main() {
     std::fprintf(stderr, "Error: %s\n", e.what());
     return 1;
   }
-  if (cfg.leader_election) {  // standbys wait here; losing the lease stops the loop (kubelet restarts us)
-    kube::LeaderElector le(*client, cfg.lease_namespace, cfg.lease_name);
-    if (!le.acquire(*stop)) {
-      health.stop();
-      return 0;
-    }
-    le.keep_renewing(stop);
+  // Standbys wait here; losing the lease stops the loop (kubelet restarts us).  The elector
+  // lives in main's scope so its renew thread runs as long as the loop does.
+  bool standby_stopped = false;
+  std::unique_ptr<kube::LeaderElector> leader = kube::lead_or_wait(*client, cfg.lease, stop, &standby_stopped);
+  if (standby_stopped) {
+    health.stop();
+    return 0;
   }
   std::string file_id = cfg.google_file_id;
   sync::Synchronizer s(*client, [&] { return drive->export_file(file_id, "text/csv"); }, cfg);

@@ -21,9 +21,7 @@ Config Config::from_env(const EnvConfig& env) {
   c.child_delete_delay_ms = static_cast<int64_t>(env.u64_or("child_delete_delay_ms", 50));
   c.requeue_secs = static_cast<int64_t>(env.u64_or("requeue_secs", 30));
   c.error_requeue_ms = static_cast<int64_t>(env.u64_or("error_requeue_ms", 3000));
-  c.leader_election = env.boolean_or("leader_election", false);
-  c.lease_namespace = env.str_or("lease_namespace", "default");
-  c.lease_name = env.str_or("lease_name", "bacchus-gpu-controller");
+  c.lease = kube::LeaseSettings::from_env(env, "bacchus-gpu-controller");
   return c;
 }
 

@@ -27,6 +27,7 @@
 #include "core/json.h"
 #include "core/threadpool.h"
 #include "kube/client.h"
+#include "kube/leader.h"
 #include "kube/runtime.h"
 
 namespace bgc::controller {
@@ -42,9 +43,7 @@ struct Config {
   int64_t requeue_secs = 30;
   int64_t error_requeue_ms = 3000;
   int64_t child_delete_delay_ms = 50;
-  bool leader_election = false;
-  std::string lease_namespace = "default";
-  std::string lease_name = "bacchus-gpu-controller";
+  kube::LeaseSettings lease;  // optional leader election (CONF_LEADER_ELECTION, ...)
   // reference fields are required (controller.rs:24-28); the rest default
   static Config from_env(const EnvConfig& env);
 };

@@ -60,10 +60,23 @@ static int64_t now_micros() {
       .count();
 }
 
-LeaderElector::LeaderElector(KubeClient& client, std::string ns, std::string name, std::string identity,
-                             int lease_seconds, int renew_seconds)
-    : client_(client), ns_(std::move(ns)), name_(std::move(name)), identity_(std::move(identity)),
-      lease_seconds_(lease_seconds), renew_seconds_(renew_seconds) {
+LeaseSettings LeaseSettings::from_env(const EnvConfig& env, const std::string& default_name) {
+  LeaseSettings s;
+  s.enabled = env.boolean_or("leader_election", false);
+  s.ns = env.str_or("lease_namespace", s.ns);
+  s.name = env.str_or("lease_name", default_name);
+  s.lease_seconds = static_cast<int>(env.u64_or("lease_duration_secs", 15));
+  s.renew_deadline_seconds = static_cast<int>(env.u64_or("lease_renew_deadline_secs", 10));
+  s.retry_seconds = static_cast<int>(env.u64_or("lease_retry_period_secs", 2));
+  if (s.retry_seconds < 1 || s.renew_deadline_seconds <= s.retry_seconds ||
+      s.lease_seconds <= s.renew_deadline_seconds) {
+    throw ConfigError("lease timing must satisfy 1 <= retry_period < renew_deadline < lease_duration");
+  }
+  return s;
+}
+
+LeaderElector::LeaderElector(KubeClient& client, LeaseSettings s, std::string identity)
+    : client_(client), s_(std::move(s)), identity_(std::move(identity)) {
   if (identity_.empty()) {
     char host[256] = {0};
     gethostname(host, sizeof(host) - 1);
@@ -76,22 +89,22 @@ LeaderElector::~LeaderElector() {
   if (renew_thread_.joinable()) renew_thread_.join();
 }
 
-bool LeaderElector::try_acquire_or_renew() {
+LeaderElector::Attempt LeaderElector::try_acquire_or_renew() {
   std::string now = rfc3339_micro_now();
-  auto cur = client_.get_opt(types::Lease, ns_, name_);
+  auto cur = client_.get_opt(types::Lease, s_.ns, s_.name);
   if (!cur) {
     Value lease = Value::object({{"apiVersion", "coordination.k8s.io/v1"}, {"kind", "Lease"}});
-    lease["metadata"] = Value::object({{"name", name_}, {"namespace", ns_}});
+    lease["metadata"] = Value::object({{"name", s_.name}, {"namespace", s_.ns}});
     lease["spec"] = Value::object({{"holderIdentity", identity_},
-                                   {"leaseDurationSeconds", lease_seconds_},
+                                   {"leaseDurationSeconds", s_.lease_seconds},
                                    {"acquireTime", now},
                                    {"renewTime", now},
                                    {"leaseTransitions", 0}});
     try {
-      client_.create(types::Lease, ns_, lease);
-      return true;
+      client_.create(types::Lease, s_.ns, lease);
+      return Attempt::Held;
     } catch (const ApiError& e) {
-      if (e.code() == 409) return false;  // somebody else created it first
+      if (e.code() == 409) return Attempt::HeldByOther;  // somebody else created it first
       throw;
     }
   }
@@ -99,62 +112,87 @@ bool LeaderElector::try_acquire_or_renew() {
   Value& spec = lease["spec"];
   std::string holder = spec.get_string("holderIdentity");
   int64_t renew = parse_rfc3339_micros(spec.get_string("renewTime"));
-  int64_t dur = spec.get("leaseDurationSeconds").is_int() ? spec.get("leaseDurationSeconds").as_int() : lease_seconds_;
+  int64_t dur = spec.get("leaseDurationSeconds").is_int() ? spec.get("leaseDurationSeconds").as_int() : s_.lease_seconds;
   bool expired = renew < 0 || now_micros() > renew + dur * 1000000;
-  if (holder != identity_ && !expired && !holder.empty()) return false;
+  if (holder != identity_ && !expired && !holder.empty()) return Attempt::HeldByOther;
   if (holder != identity_) {
     spec["acquireTime"] = now;
     int64_t transitions = spec.get("leaseTransitions").is_int() ? spec.get("leaseTransitions").as_int() : 0;
     spec["leaseTransitions"] = transitions + 1;
   }
   spec["holderIdentity"] = identity_;
-  spec["leaseDurationSeconds"] = lease_seconds_;
+  spec["leaseDurationSeconds"] = s_.lease_seconds;
   spec["renewTime"] = now;
   try {
-    client_.replace(types::Lease, ns_, name_, lease);  // resourceVersion precondition
-    return true;
+    client_.replace(types::Lease, s_.ns, s_.name, lease);  // resourceVersion precondition
+    return Attempt::Held;
   } catch (const ApiError& e) {
-    if (e.code() == 409) return false;
+    if (e.code() == 409) return Attempt::HeldByOther;  // lost a write race: re-read next time
     throw;
   }
 }
 
 bool LeaderElector::acquire(CancelToken& stop) {
-  LOG_INFO("leader") << "attempting to acquire lease " << ns_ << "/" << name_ << " as " << identity_;
+  LOG_INFO("leader") << "attempting to acquire lease " << s_.ns << "/" << s_.name << " as " << identity_;
   while (!stop.cancelled()) {
     try {
-      if (try_acquire_or_renew()) {
-        LOG_INFO("leader") << "acquired lease " << ns_ << "/" << name_;
+      if (try_acquire_or_renew() == Attempt::Held) {
+        LOG_INFO("leader") << "acquired lease " << s_.ns << "/" << s_.name;
         return true;
       }
     } catch (const std::exception& e) {
       LOG_WARN("leader") << "lease attempt failed: " << e.what();
     }
-    if (stop.wait_for(std::chrono::seconds(2))) break;
+    if (stop.wait_for(std::chrono::seconds(s_.retry_seconds))) break;
   }
   return false;
 }
 
 void LeaderElector::keep_renewing(std::shared_ptr<CancelToken> stop_on_loss) {
   renew_thread_ = std::thread([this, stop_on_loss] {
-    auto last_ok = std::chrono::steady_clock::now();
-    while (!stop_renew_.wait_for(std::chrono::seconds(renew_seconds_))) {
+    // the deadline runs from when the last successful renew was *sent*: the lease's
+    // renewTime is at or after that instant, so a standby (waiting lease_seconds from
+    // renewTime by its own clock) cannot take over before we stop.
+    auto last_ok_sent = std::chrono::steady_clock::now();
+    const auto deadline = std::chrono::seconds(s_.renew_deadline_seconds);
+    while (!stop_renew_.wait_for(std::chrono::seconds(s_.retry_seconds))) {
       if (stop_on_loss->cancelled()) return;
-      bool ok = false;
+      auto sent = std::chrono::steady_clock::now();
+      Attempt a = Attempt::Failed;
       try {
-        ok = try_acquire_or_renew();
+        a = try_acquire_or_renew();
       } catch (const std::exception& e) {
         LOG_WARN("leader") << "lease renew failed: " << e.what();
       }
-      if (ok) {
-        last_ok = std::chrono::steady_clock::now();
-      } else if (std::chrono::steady_clock::now() - last_ok > std::chrono::seconds(lease_seconds_)) {
-        LOG_ERROR("leader") << "lost lease " << ns_ << "/" << name_ << "; shutting down";
-        stop_on_loss->cancel();
-        return;
+      if (a == Attempt::Held) {
+        last_ok_sent = sent;
+        continue;
       }
+      if (a == Attempt::HeldByOther) {
+        LOG_ERROR("leader") << "lease " << s_.ns << "/" << s_.name << " is held by another replica; stepping down";
+      } else if (std::chrono::steady_clock::now() - last_ok_sent < deadline) {
+        continue;  // transient failure: retry until the renew deadline
+      } else {
+        LOG_ERROR("leader") << "lost lease " << s_.ns << "/" << s_.name << " (renew deadline " << s_.renew_deadline_seconds
+                            << " s passed); shutting down";
+      }
+      stop_on_loss->cancel();
+      return;
     }
   });
+}
+
+std::unique_ptr<LeaderElector> lead_or_wait(KubeClient& client, const LeaseSettings& s,
+                                            const std::shared_ptr<CancelToken>& stop, bool* standby_stopped) {
+  *standby_stopped = false;
+  if (!s.enabled) return nullptr;
+  auto le = std::make_unique<LeaderElector>(client, s);
+  if (!le->acquire(*stop)) {
+    *standby_stopped = true;
+    return nullptr;
+  }
+  le->keep_renewing(stop);
+  return le;
 }
 
 }  // namespace bgc::kube

@@ -2,37 +2,68 @@
 // grants the controller `leases` get/create/update/patch (reference
 // charts/.../templates/serviceaccount.yaml:26-28) but never uses it, so two controller
 // replicas double-write; CONF_LEADER_ELECTION=true enables this.
+//
+// Timing follows client-go's leaderelection: a lease lasts `lease_seconds` (15), the
+// holder renews every `retry_seconds` (2) and steps down once no renew has succeeded
+// within `renew_deadline_seconds` (10) of the last successful renew's *send* time, so it
+// stops acting before a standby (which waits the full lease duration by its own clock)
+// can take over.  It also steps down at once when the lease names another holder.
 #pragma once
 
+#include <chrono>
 #include <memory>
 #include <string>
 #include <thread>
 
 #include "core/cancel.h"
+#include "core/env_config.h"
 #include "kube/client.h"
 
 namespace bgc::kube {
 
+struct LeaseSettings {
+  bool enabled = false;
+  std::string ns = "default";
+  std::string name;
+  int lease_seconds = 15;
+  int renew_deadline_seconds = 10;
+  int retry_seconds = 2;
+  // CONF_LEADER_ELECTION, CONF_LEASE_NAMESPACE, CONF_LEASE_NAME, CONF_LEASE_DURATION_SECS,
+  // CONF_LEASE_RENEW_DEADLINE_SECS, CONF_LEASE_RETRY_PERIOD_SECS.
+  static LeaseSettings from_env(const EnvConfig& env, const std::string& default_name);
+};
+
 class LeaderElector {
  public:
-  LeaderElector(KubeClient& client, std::string ns, std::string name, std::string identity = "",
-                int lease_seconds = 15, int renew_seconds = 5);
+  enum class Attempt { Held, HeldByOther, Failed };
+
+  LeaderElector(KubeClient& client, LeaseSettings s, std::string identity = "");
   ~LeaderElector();
+  LeaderElector(const LeaderElector&) = delete;
+  LeaderElector& operator=(const LeaderElector&) = delete;
   // Blocks until leadership is acquired (true) or `stop` is cancelled (false).
   bool acquire(CancelToken& stop);
-  // One attempt; true when this identity holds the lease afterwards.
-  bool try_acquire_or_renew();
-  // Renews in the background; on loss of the lease cancels `stop_on_loss`.
+  // One attempt.  Held: this identity holds the lease afterwards.  HeldByOther: another
+  // identity holds an unexpired lease (or won a write race).  Failed: API error.
+  Attempt try_acquire_or_renew();
+  // Renews in the background until destroyed; on loss of the lease cancels `stop_on_loss`.
+  // The elector must outlive the work it guards (keep it in main's scope).
   void keep_renewing(std::shared_ptr<CancelToken> stop_on_loss);
   const std::string& identity() const { return identity_; }
 
  private:
   KubeClient& client_;
-  std::string ns_, name_, identity_;
-  int lease_seconds_, renew_seconds_;
+  LeaseSettings s_;
+  std::string identity_;
   std::thread renew_thread_;
   CancelToken stop_renew_;
 };
+
+// Acquires leadership when `s.enabled` (blocking until acquired or stopped) and keeps it
+// renewed.  Returns nullptr with *standby_stopped=false when election is disabled; returns
+// nullptr with *standby_stopped=true when `stop` fired before this replica became leader.
+std::unique_ptr<LeaderElector> lead_or_wait(KubeClient& client, const LeaseSettings& s,
+                                            const std::shared_ptr<CancelToken>& stop, bool* standby_stopped);
 
 std::string rfc3339_micro_now();
 int64_t parse_rfc3339_micros(const std::string& s);  // micros since epoch, -1 on error

@@ -28,9 +28,7 @@ Config Config::from_env(const EnvConfig& env) {
   c.exit_on_error = env.boolean_or("exit_on_error", true);
   c.skip_unchanged = env.boolean_or("skip_unchanged", true);
   c.workers = static_cast<int>(env.u64_or("workers", 8));
-  c.leader_election = env.boolean_or("leader_election", false);
-  c.lease_namespace = env.str_or("lease_namespace", c.lease_namespace);
-  c.lease_name = env.str_or("lease_name", c.lease_name);
+  c.lease = kube::LeaseSettings::from_env(env, "bacchus-gpu-synchronizer");
   if (c.sync_interval_secs == 0) throw ConfigError("invalid value for field sync_interval_secs: must be > 0");
   return c;
 }

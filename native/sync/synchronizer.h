@@ -26,6 +26,7 @@
 #include "core/cancel.h"
 #include "core/env_config.h"
 #include "kube/client.h"
+#include "kube/leader.h"
 #include "kube/runtime.h"
 #include "sync/google.h"
 #include "sync/sheet.h"
@@ -50,9 +51,7 @@ struct Config {
   int workers = 8;
   // Lease-based leader election (reference: none; two synchronizer replicas would both
   // write every tenant).  Off by default like the controller's.
-  bool leader_election = false;
-  std::string lease_namespace = "default";
-  std::string lease_name = "bacchus-gpu-synchronizer";
+  kube::LeaseSettings lease;
   static Config from_env(const EnvConfig& env);
 };
 

@@ -112,6 +112,54 @@ def test_leader_election_failover():
         wait_for(lambda: c.admin.get_or_none("namespaces", "le2"), desc="le2 reconciled by new leader")
 
 
+FAST_LEASE = {"CONF_LEADER_ELECTION": "true", "CONF_LEASE_NAMESPACE": "bgc", "RUST_LOG": "info",
+              "CONF_LEASE_DURATION_SECS": "4", "CONF_LEASE_RENEW_DEADLINE_SECS": "3",
+              "CONF_LEASE_RETRY_PERIOD_SECS": "1"}
+
+
+def test_leader_keeps_lease_beyond_lease_duration():
+    """the elector used to be destroyed right after acquiring, so the
+    leader stopped renewing and a standby took over one lease duration later while the
+    first replica kept reconciling.  A live leader must hold the lease indefinitely."""
+    with Cluster(admission=False, controller=False) as c:
+        c.start_controller(extra_env=FAST_LEASE)
+        leader = c.procs["controller"]
+        wait_for(lambda: "acquired lease" in leader.output(), desc="leader acquires")
+        c.procs["controller-leader"] = c.procs.pop("controller")
+        c.start_controller(extra_env=FAST_LEASE)
+        standby = c.procs["controller"]
+        wait_for(lambda: "attempting to acquire lease" in standby.output(), desc="standby waits")
+        t0 = c.admin.get("leases", "bacchus-gpu-controller", "bgc")["spec"]["renewTime"]
+        time.sleep(3 * 4)  # three lease durations
+        lease = c.admin.get("leases", "bacchus-gpu-controller", "bgc")
+        assert lease["spec"]["renewTime"] != t0, "leader stopped renewing"
+        assert "acquired lease" not in standby.output()
+        assert leader.alive() and "stepping down" not in leader.output()
+        c.admin.create("userbootstraps", ub("keep1"))
+        wait_for(lambda: c.admin.get_or_none("namespaces", "keep1"), desc="leader still reconciles")
+
+
+def test_leader_steps_down_when_lease_taken():
+    """when the lease names another holder the leader stops at once
+    instead of acting until its own renew deadline."""
+    with Cluster(admission=False, controller=False) as c:
+        c.start_controller(extra_env=FAST_LEASE)
+        leader = c.procs["controller"]
+        wait_for(lambda: "acquired lease" in leader.output(), desc="leader acquires")
+        for _ in range(20):  # another replica takes the lease (retry on resourceVersion races)
+            lease = c.admin.get("leases", "bacchus-gpu-controller", "bgc")
+            lease["spec"]["holderIdentity"] = "intruder"
+            lease["spec"]["leaseDurationSeconds"] = 3600
+            try:
+                c.admin.replace("leases", "bacchus-gpu-controller", lease, namespace="bgc")
+                break
+            except ApiError as e:
+                if e.code != 409:
+                    raise
+        wait_for(lambda: not leader.alive(), timeout=10, desc="leader exits")
+        assert "held by another replica; stepping down" in leader.output()
+
+
 def test_graceful_shutdown_exit_codes():
     with Cluster() as c:
         codes = {}
