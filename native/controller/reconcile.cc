@@ -111,15 +111,24 @@ void Reconciler::forget(const kube::ResourceType& rt, const Value& child) {
   publish_cache_sizes(last_applied_.size(), ub_state_.size());
 }
 
-void Reconciler::forget_owner(const std::string& owner) {
+void Reconciler::forget_owner_locked(const std::string& owner) {
   std::string ns = owner;
   for (auto& ch : ns) ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
-  std::lock_guard<std::mutex> lk(mu_);
   ub_state_.erase(owner);
   last_applied_.erase(types::Namespace.plural + "//" + ns);
   for (const auto* rt : {&types::ResourceQuota, &types::Role, &types::RoleBinding})
     last_applied_.erase(rt->plural + "/" + ns + "/" + ns);
   publish_cache_sizes(last_applied_.size(), ub_state_.size());
+}
+
+void Reconciler::forget_owner(const std::string& owner) {
+  std::lock_guard<std::mutex> lk(mu_);
+  forget_owner_locked(owner);
+}
+
+bool Reconciler::owner_live(const std::string& name, const std::string& uid) {
+  kube::ObjPtr cur = ctrl_.store().get("", name);
+  return cur && cur->get("metadata").get_string("uid") == uid;
 }
 
 bool Reconciler::fresh(const std::string& owner_name, const std::string& owner_rv) {
@@ -213,6 +222,44 @@ kube::Action Reconciler::reconcile(const kube::ObjPtr& ub_ptr) {
   // Stage 3: the RoleBinding — only after every earlier apply succeeded, so a user is
   //          never bound into a namespace whose quota failed to apply (the reference
   //          gets the same guarantee from its sequential `?` chain).
+  // A reconcile can still be running when its UserBootstrap is deleted: forget_owner()
+  // then runs first (on the watcher thread) and the applies below would re-insert cache
+  // entries that nothing removes.  Every exit re-checks the watch cache under mu_ and
+  // drops the owner's entries when the UB (this uid) is gone.
+  const std::string owner_uid = ub.get("metadata").get_string("uid");
+  try {
+    apply_all(children, run_one);
+  } catch (...) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!owner_live(owner_name, owner_uid)) forget_owner_locked(owner_name);
+    throw;
+  }
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!owner_live(owner_name, owner_uid)) {
+      forget_owner_locked(owner_name);
+    } else if (cfg_.skip_unchanged) {
+      UbState st;
+      st.owner_rv = owner_rv;
+      bool complete = true;
+      for (const auto& c : children) {
+        auto it = last_applied_.find(child_key(c));
+        if (it == last_applied_.end()) {
+          complete = false;
+          break;
+        }
+        st.children.push_back({c.rt, c.ns, c.name, it->second.rv});
+      }
+      if (complete) ub_state_[owner_name] = std::move(st);
+      publish_cache_sizes(last_applied_.size(), ub_state_.size());
+    }
+  }
+  static auto& ok = reg.counter("bgc_reconcile_total", "Reconciles", {{"result", "ok"}});
+  ok.inc();
+  return kube::Action::requeue_after(std::chrono::milliseconds(cfg_.requeue_secs * 1000));
+}
+
+void Reconciler::apply_all(const std::vector<DesiredChild>& children, const std::function<void(size_t)>& run_one) {
   run_one(0);
   std::vector<size_t> middle, last;
   for (size_t i = 1; i < children.size(); ++i) {
@@ -234,25 +281,6 @@ kube::Action Reconciler::reconcile(const kube::ObjPtr& ub_ptr) {
     for (size_t i : middle) run_one(i);
   }
   for (size_t i : last) run_one(i);
-  if (cfg_.skip_unchanged) {
-    UbState st;
-    st.owner_rv = owner_rv;
-    std::lock_guard<std::mutex> lk(mu_);
-    bool complete = true;
-    for (const auto& c : children) {
-      auto it = last_applied_.find(child_key(c));
-      if (it == last_applied_.end()) {
-        complete = false;
-        break;
-      }
-      st.children.push_back({c.rt, c.ns, c.name, it->second.rv});
-    }
-    if (complete) ub_state_[owner_name] = std::move(st);
-    publish_cache_sizes(last_applied_.size(), ub_state_.size());
-  }
-  static auto& ok = reg.counter("bgc_reconcile_total", "Reconciles", {{"result", "ok"}});
-  ok.inc();
-  return kube::Action::requeue_after(std::chrono::milliseconds(cfg_.requeue_secs * 1000));
 }
 
 kube::Action Reconciler::error_policy(const kube::ObjPtr& ub, const std::exception& err) {

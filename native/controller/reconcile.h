@@ -17,6 +17,7 @@
 //    drift-repair pass costs zero API writes unless something actually drifted.
 #pragma once
 
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -88,6 +89,10 @@ class Reconciler {
     std::string rv;
   };
   bool up_to_date(const DesiredChild& c, const std::string& body_hash);
+  // Stage order: Namespace, then ResourceQuota ‖ Role, then RoleBinding.
+  void apply_all(const std::vector<DesiredChild>& children, const std::function<void(size_t)>& run_one);
+  void forget_owner_locked(const std::string& owner);  // mu_ held
+  bool owner_live(const std::string& name, const std::string& uid);
   void apply_child(const DesiredChild& c, const std::string& body_hash);
 
   kube::KubeClient& client_;

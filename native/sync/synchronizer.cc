@@ -41,8 +41,37 @@ std::shared_ptr<const RowIndex> Synchronizer::index() const {
   return index_;
 }
 
+static metrics::Counter& drive_exports(const char* reason) {
+  return metrics::Registry::global().counter("bgc_drive_exports_total", "Google Drive sheet exports issued",
+                                             {{"reason", reason}});
+}
+
 void Synchronizer::refresh() {
   std::lock_guard<std::mutex> rl(refresh_mu_);
+  static auto& tick_exports = drive_exports("tick");
+  tick_exports.inc();
+  refresh_locked();
+}
+
+bool Synchronizer::refresh_if_stale() {
+  // Single flight: every worker that finds an unknown user queues here, and only the first
+  // one past the lock re-downloads; the rest see the fresh timestamp and reuse its index.
+  // A burst of unapproved UserBootstraps therefore costs at most one export per
+  // min_refresh_ms (the reference exports once per 60 s tick only).
+  auto stale = [&] {
+    int64_t last = last_refresh_ns_.load();
+    return last != 0 && (metrics::now_ns() - last) / 1000000 >= static_cast<int64_t>(cfg_.min_refresh_ms);
+  };
+  if (!stale()) return false;
+  std::lock_guard<std::mutex> rl(refresh_mu_);
+  if (!stale()) return false;
+  static auto& on_demand = drive_exports("on_demand");
+  on_demand.inc();
+  refresh_locked();
+  return true;
+}
+
+void Synchronizer::refresh_locked() {
   std::string csv = source_();
   LOG_INFO("synchronizer") << "downloaded csv file";
   std::vector<std::string> warnings;
@@ -177,11 +206,8 @@ int Synchronizer::run(CancelToken& stop) {
             int64_t t0 = metrics::now_ns();
             try {
               auto idx = index();
-              if (!idx->find(key)) {
-                // unknown user: the sheet may have changed since the last fetch
-                int64_t age_ms = (metrics::now_ns() - last_refresh_ns_.load()) / 1000000;
-                if (last_refresh_ns_.load() != 0 && age_ms >= static_cast<int64_t>(cfg_.min_refresh_ms)) refresh();
-              }
+              // unknown user: the sheet may have changed since the last fetch
+              if (!idx->find(key)) refresh_if_stale();
               std::vector<std::string> produced{ub_rv};
               uint64_t gen = index_gen_.load();
               if (sync_one(*ub, &produced)) {

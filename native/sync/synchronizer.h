@@ -71,6 +71,9 @@ class Synchronizer {
   Synchronizer(kube::KubeClient& client, SheetSource source, Config cfg);
   // Fetch + parse + index. Throws on fetch/parse errors.
   void refresh();
+  // refresh() when the index is older than min_refresh_ms; concurrent callers share one
+  // export.  Returns true when this call downloaded the sheet.
+  bool refresh_if_stale();
   // One reference-style pass over every UserBootstrap. Throws on the first error.
   TickStats tick();
   // Syncs one UserBootstrap object against the current index; returns true if it wrote.
@@ -82,6 +85,7 @@ class Synchronizer {
 
  private:
   std::shared_ptr<const RowIndex> index() const;
+  void refresh_locked();  // refresh_mu_ held
   kube::KubeClient& client_;
   SheetSource source_;
   Config cfg_;

@@ -2,6 +2,7 @@
 controller: create as an OIDC user, quota/status as the synchronizer would write them,
 RoleBinding only after sync, GC on delete."""
 import re
+import time
 
 import pytest
 import requests
@@ -141,3 +142,34 @@ def test_controller_caches_stay_bounded_under_churn():
         for n in names:
             c.admin.delete("userbootstraps", n)
         wait_for(lambda: cache_entries() == 0, timeout=15, desc="apply cache drained")
+
+
+def test_owner_deleted_mid_reconcile_leaves_no_cache_state():
+    """a reconcile still applying children when its UserBootstrap is deleted
+    must not leave fast-path/apply-cache entries behind (the UB's forget runs first)."""
+    with Cluster(admission=False, controller_env={"CONF_REQUEUE_SECS": "3600"}) as c:
+        names = [f"race{i}" for i in range(6)]
+        # hold every ResourceQuota apply for 1.5 s so the UB deletions land mid-reconcile
+        c.fault([{"method": "PATCH", "path": "/resourcequotas/race", "delay_ms": 1500, "count": -1}])
+        for n in names:
+            c.admin.create("userbootstraps", {"apiVersion": "bacchus.io/v1", "kind": "UserBootstrap",
+                                              "metadata": {"name": n},
+                                              "spec": {"kube_username": n,
+                                                       "quota": {"hard": {"requests.amd.com/gpu": "1"}}}})
+        for n in names:
+            wait_for(lambda: c.admin.get_or_none("namespaces", n), desc=f"{n} namespace")
+        for n in names:
+            c.admin.delete("userbootstraps", n)
+        c.clear_faults()
+
+        def gauges():
+            m = requests.get(f"http://127.0.0.1:{c.controller_port}/metrics", timeout=5).text
+            out = {}
+            for k in ("bgc_controller_apply_cache_entries", "bgc_controller_owner_state_entries"):
+                hit = re.search(rf"^{k} (\S+)$", m, re.M)
+                out[k] = float(hit.group(1)) if hit else 0.0
+            return out
+
+        wait_for(lambda: all(v == 0 for v in gauges().values()), timeout=20, desc="caches drained")
+        time.sleep(2.0)  # the delayed applies have all returned by now
+        assert all(v == 0 for v in gauges().values()), gauges()

@@ -149,3 +149,34 @@ def test_synchronizer_leader_election_failover(google):
         q = wait_for(lambda: (c.admin.get("userbootstraps", "bob").get("spec", {}).get("quota") or None),
                      timeout=30, desc="bob synced by the new leader")
         assert q["hard"]["requests.amd.com/gpu"] == "2"
+
+
+def test_drive_exports_bounded_under_unapproved_churn(google):
+    """VERDICT r1 #6 / ADVICE r1: in watch mode every unknown UserBootstrap may trigger a
+    sheet refresh.  A burst of unapproved tenants (handled by 8 workers at once) must cost
+    at most one export per CONF_MIN_REFRESH_MS (single flight), plus the periodic ticks."""
+    google.set_rows([{"id_username": "approved"}])
+    google.export_delay = 0.3  # widen the window in which workers would pile up
+    min_refresh_ms, window_s = 2000, 8.0
+    with Cluster(admission=False) as c:
+        c.start_synchronizer(google, interval=60, extra_env={"CONF_WATCH": "true", "CONF_WORKERS": "8",
+                                                            "CONF_MIN_REFRESH_MS": str(min_refresh_ms)})
+        wait_for(lambda: google.export_requests >= 1, desc="first tick export")
+        base = google.export_requests
+        t0 = time.time()
+        i = 0
+        while time.time() - t0 < window_s:
+            for _ in range(10):
+                c.admin.create("userbootstraps", {"apiVersion": "bacchus.io/v1", "kind": "UserBootstrap",
+                                                  "metadata": {"name": f"stranger{i}"},
+                                                  "spec": {"kube_username": f"stranger{i}"}})
+                i += 1
+            time.sleep(0.1)
+        elapsed = time.time() - t0
+        time.sleep(1.0)
+        on_demand = google.export_requests - base
+        cap = int(elapsed * 1000 // min_refresh_ms) + 1
+        assert 1 <= on_demand <= cap, (on_demand, cap, i)
+        m = requests.get(f"http://127.0.0.1:{c.sync_port}/metrics", timeout=5).text
+        assert 'bgc_drive_exports_total{reason="on_demand"}' in m
+        assert 'bgc_drive_exports_total{reason="tick"} 1' in m
