@@ -6,6 +6,10 @@
   tested end to end, not mocked.
 * ``GET /drive/v3/files/<id>/export?mimeType=text/csv``: returns the current CSV for a
   valid bearer token.
+* ``GET /drive/v3/files/<id>?fields=version``: file metadata; ``version`` goes up on every
+  sheet edit, like Drive's.
+* ``POST /_fake/rows`` ``{"rows": [...], "append": bool}``: edit the sheet over HTTP (the
+  operator approving rows; used by bench ranks that do not own this object).
 * Fault knobs: ``fail_export`` / ``fail_token`` (HTTP status to return), ``export_delay``.
 """
 import json
@@ -54,6 +58,9 @@ class FakeGoogle:
         self.tokens = set()
         self.token_requests = 0
         self.export_requests = 0
+        self.metadata_requests = 0
+        self.version = 1
+        self.rows = []
         self.fail_export = 0
         self.fail_token = 0
         self.export_delay = 0.0
@@ -82,6 +89,10 @@ class FakeGoogle:
             def do_POST(self):
                 n = int(self.headers.get("Content-Length", "0"))
                 body = self.rfile.read(n).decode()
+                if self.path == "/_fake/rows":
+                    req = json.loads(body or "{}")
+                    fg.set_rows(req.get("rows", []), append=bool(req.get("append")))
+                    return self._send(200, json.dumps({"version": fg.version}))
                 if self.path != "/token":
                     return self._send(404, "{}")
                 code, payload = fg._token(body)
@@ -119,13 +130,16 @@ class FakeGoogle:
         """Test-only endpoint overrides for the synchronizer."""
         return {"BGC_GOOGLE_TOKEN_URL": self.token_url, "BGC_GOOGLE_API_BASE": self.base}
 
-    def set_rows(self, rows, headers=FORM_HEADERS):
+    def set_rows(self, rows, headers=FORM_HEADERS, append=False):
         with self.lock:
-            self.csv = make_csv(rows, headers)
+            self.rows = (self.rows + list(rows)) if append else list(rows)
+            self.csv = make_csv(self.rows, headers)
+            self.version += 1
 
     def set_csv(self, text):
         with self.lock:
             self.csv = text
+            self.version += 1
 
     # ---------------------------------------------------------------- endpoints
     def _token(self, body):
@@ -171,6 +185,8 @@ class FakeGoogle:
     def _export(self, path, auth):
         u = urllib.parse.urlparse(path)
         q = urllib.parse.parse_qs(u.query)
+        if u.path == f"/drive/v3/files/{self.file_id}":
+            return self._metadata(q, auth)
         with self.lock:
             self.export_requests += 1
             fail = self.fail_export
@@ -188,3 +204,14 @@ class FakeGoogle:
         if q.get("mimeType", [""])[0] != "text/csv":
             return 400, json.dumps({"error": {"code": 400, "message": "bad mimeType"}}), "application/json"
         return 200, csv.encode(), "text/csv"
+
+    def _metadata(self, q, auth):
+        with self.lock:
+            self.metadata_requests += 1
+            version = self.version
+            tokens = set(self.tokens)
+        if not auth.startswith("Bearer ") or auth[7:] not in tokens:
+            return 401, json.dumps({"error": {"code": 401, "message": "Invalid Credentials"}}), "application/json"
+        if q.get("fields", [""])[0] != "version":
+            return 400, json.dumps({"error": {"code": 400, "message": "unsupported fields"}}), "application/json"
+        return 200, json.dumps({"version": str(version)}), "application/json"

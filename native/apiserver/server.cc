@@ -2011,6 +2011,11 @@ struct ApiServer::Impl {
       if (!p.sub.empty() && p.sub != "status") throw StatusError(404, "NotFound", "subresource not supported: " + p.sub);
       if (!p.sub.empty() && !p.ti->rt.has_status) throw StatusError(404, "NotFound", "the server could not find the requested resource");
       const std::string& m = req.method;
+      // etcd model: a write is visible (response, watch event) only after a storage
+      // commit round trip.  Writes wait concurrently, as they pipeline through raft.
+      if (opts.write_latency_us > 0 && m != "GET") {
+        std::this_thread::sleep_for(std::chrono::microseconds(opts.write_latency_us));
+      }
       if (p.collection) {
         if (m == "GET") {
           std::string wq = req.query_param("watch");

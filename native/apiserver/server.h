@@ -45,6 +45,10 @@ struct Options {
   // One thread fell 10-14k deletions behind over 100k tenants at ~10k CR/s on the MI355X
   // box; two keep the backlog at 0 with unchanged CR/s (profiles/gc_workers_r1/).
   int gc_workers = 2;
+  // Storage commit latency added to every write (POST/PUT/PATCH/DELETE) before it is
+  // applied: a real apiserver answers a write only after etcd's raft commit + fsync
+  // (typically 1-10 ms).  0 = in-memory speed.
+  int64_t write_latency_us = 0;
 };
 
 class ApiServer {

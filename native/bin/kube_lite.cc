@@ -25,6 +25,8 @@ static void usage() {
                "usage: kube-lite [--addr A] [--port P] [--port-file F] [--token-file F] [--no-anonymous]\n"
                "                 [--tls-cert F --tls-key F] [--service-override ns/name=host:port]...\n"
                "                 [--bookmark-ms N] [--history N] [--watch-coalesce-us N] [--gc-workers N]\n"
+               "                 [--write-latency-ms F]\n"
+               "                 [--write-latency-ms F]\n"
                "                 [--manifest file.{json,yaml}]...\n");
 }
 

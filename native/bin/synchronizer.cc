@@ -73,6 +73,7 @@ int main() {
   }
   std::string file_id = cfg.google_file_id;
   sync::Synchronizer s(*client, [&] { return drive->export_file(file_id, "text/csv"); }, cfg);
+  s.set_version_source([&] { return drive->file_version(file_id); });
   int rc = s.run(*stop);
   health.stop(std::chrono::milliseconds(1000));
   if (rc == 0) {

@@ -110,4 +110,17 @@ std::string DriveClient::export_file(const std::string& file_id, const std::stri
   return r.body;
 }
 
+std::string DriveClient::file_version(const std::string& file_id) {
+  http::Headers h;
+  h.set("Authorization", "Bearer " + auth_.token());
+  std::string path = base_path_ + "/drive/v3/files/" + http::url_encode(file_id) + "?fields=version";
+  http::Response r = http_->request("GET", path, "", &h);
+  if (r.status < 200 || r.status >= 300) throw GoogleApiError(r.status, "request failed");
+  Value v = json::parse(r.body);
+  const Value& ver = v.get("version");  // int64 rendered as a JSON string by Drive
+  if (ver.is_string()) return ver.as_string();
+  if (ver.is_int()) return std::to_string(ver.as_int());
+  throw GoogleApiError(r.status, "no version in file metadata");
+}
+
 }  // namespace bgc::sync

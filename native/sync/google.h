@@ -62,6 +62,10 @@ class DriveClient {
   // GET /drive/v3/files/{id}/export?mimeType=... ; throws GoogleApiError on non-2xx
   // ("request failed", synchronizer.rs:202-204) and on non-UTF-8 bodies.
   std::string export_file(const std::string& file_id, const std::string& mime = "text/csv");
+  // GET /drive/v3/files/{id}?fields=version: Drive bumps `version` on every change to the
+  // file, so polling this metadata call (a few hundred bytes) tells when an export is
+  // worth doing.  Returns the version string; throws GoogleApiError on non-2xx.
+  std::string file_version(const std::string& file_id);
 
  private:
   GoogleAuth& auth_;

@@ -25,6 +25,7 @@ Config Config::from_env(const EnvConfig& env) {
   c.quota_keys.partition_resource = env.str_or("partition_resource_name", "amd.com/gpu-partition");
   c.watch = env.boolean_or("watch", true);
   c.min_refresh_ms = env.u64_or("min_refresh_ms", 5000);
+  c.sheet_poll_ms = env.u64_or("sheet_poll_ms", c.sheet_poll_ms);
   c.exit_on_error = env.boolean_or("exit_on_error", true);
   c.skip_unchanged = env.boolean_or("skip_unchanged", true);
   c.workers = static_cast<int>(env.u64_or("workers", 8));
@@ -226,6 +227,40 @@ int Synchronizer::run(CancelToken& stop) {
     }
   }
 
+  // Sheet change poll (watch mode): a metadata request per sheet_poll_ms, an export only
+  // when Drive reports a new version.  Poll errors are logged, never fatal: the periodic
+  // tick still re-reads the sheet and keeps the reference's exit-on-error semantics.
+  std::unique_ptr<std::thread> poll_thread;
+  if (cfg_.watch && cfg_.sheet_poll_ms > 0 && version_source_) {
+    poll_thread = std::make_unique<std::thread>([&] {
+      static auto& polls = metrics::Registry::global().counter("bgc_drive_version_polls_total",
+                                                               "Drive file-version metadata requests");
+      static auto& changed = drive_exports("changed");
+      std::string last;
+      while (!stop.wait_for(std::chrono::milliseconds(cfg_.sheet_poll_ms))) {
+        try {
+          polls.inc();
+          std::string v = version_source_();
+          if (last.empty()) {
+            last = v;  // the first tick's export already covers this version
+            continue;
+          }
+          if (v == last) continue;
+          last = v;
+          LOG_INFO("synchronizer") << "sheet changed (version " << v << "); re-reading";
+          {
+            std::lock_guard<std::mutex> rl(refresh_mu_);
+            changed.inc();
+            refresh_locked();
+          }
+          for (const auto& o : store.list()) queue.add(kube::meta_name(*o));
+        } catch (const std::exception& e) {
+          LOG_WARN("synchronizer") << "sheet version poll failed: " << e.what();
+        }
+      }
+    });
+  }
+
   int rc = 0;
   while (!stop.cancelled()) {
     try {
@@ -248,6 +283,7 @@ int Synchronizer::run(CancelToken& stop) {
     }
     if (stop.wait_for(std::chrono::seconds(cfg_.sync_interval_secs))) break;
   }
+  if (poll_thread) poll_thread->join();
   queue.shutdown();
   for (auto& t : workers) t.join();
   if (watch_thread) watch_thread->join();

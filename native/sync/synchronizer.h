@@ -46,6 +46,10 @@ struct Config {
   QuotaKeys quota_keys;
   bool watch = true;
   uint64_t min_refresh_ms = 5000;
+  // Watch mode: poll the sheet's Drive `version` (a metadata call) this often and export
+  // only when it changed, so an operator's approval reaches the cluster within about one
+  // poll instead of one sync tick (reference: export every 60 s tick only).  0 = off.
+  uint64_t sheet_poll_ms = 5000;
   bool exit_on_error = true;
   bool skip_unchanged = true;
   int workers = 8;
@@ -82,12 +86,15 @@ class Synchronizer {
   bool sync_one(const json::Value& ub, std::vector<std::string>* produced = nullptr);
   // Main loop; returns non-zero exit status on fatal error.
   int run(CancelToken& stop);
+  // Cheap change detector for the sheet (Drive file version); enables sheet_poll_ms.
+  void set_version_source(std::function<std::string()> v) { version_source_ = std::move(v); }
 
  private:
   std::shared_ptr<const RowIndex> index() const;
   void refresh_locked();  // refresh_mu_ held
   kube::KubeClient& client_;
   SheetSource source_;
+  std::function<std::string()> version_source_;
   Config cfg_;
   mutable std::mutex mu_;
   std::shared_ptr<const RowIndex> index_;

@@ -180,3 +180,27 @@ def test_drive_exports_bounded_under_unapproved_churn(google):
         m = requests.get(f"http://127.0.0.1:{c.sync_port}/metrics", timeout=5).text
         assert 'bgc_drive_exports_total{reason="on_demand"}' in m
         assert 'bgc_drive_exports_total{reason="tick"} 1' in m
+
+
+def test_approval_after_create_is_picked_up_by_version_poll(google):
+    """The reference's onboarding order: the tenant applies first, the
+    operator approves the sheet row later.  With the Drive version poll the approval is
+    applied within about one poll, not one 60 s tick, and the sheet is exported only when
+    its version changed."""
+    google.set_rows([])
+    with Cluster(controller_env={"CONF_REQUEUE_SECS": "3600"}) as c:
+        c.start_synchronizer(google, interval=60, extra_env={"CONF_WATCH": "true", "CONF_SHEET_POLL_MS": "300",
+                                                            "CONF_MIN_REFRESH_MS": "600000"})
+        c.as_user("oidc:late", ["gpu"]).create("userbootstraps", ub("late"))
+        wait_for(lambda: c.admin.get_or_none("namespaces", "late"), desc="namespace before approval")
+        time.sleep(1.0)
+        exports_before = google.export_requests
+        assert c.admin.get_or_none("rolebindings", "late", "late") is None
+        t0 = time.time()
+        google.set_rows([{"id_username": "late", "gpu": 4}])  # the operator marks the row O
+        wait_for(lambda: c.admin.get_or_none("rolebindings", "late", "late"), timeout=10, desc="late ready")
+        assert time.time() - t0 < 5.0
+        rq = c.admin.get("resourcequotas", "late", "late")
+        assert rq["spec"]["hard"]["requests.amd.com/gpu"] == "4"
+        assert google.export_requests - exports_before == 1  # one export for one sheet edit
+        assert google.metadata_requests >= 3
