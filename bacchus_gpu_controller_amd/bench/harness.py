@@ -146,8 +146,8 @@ def _rss_mb(pid):
     return None
 
 
-def _names(rank, step, batch):
-    return [f"r{rank}-s{step}-u{i}" for i in range(batch)]
+def _names(rank, phase, step, batch):
+    return [f"r{rank}-{phase}{step}-u{i}" for i in range(batch)]
 
 
 def _samples(url, verify=None):
@@ -195,62 +195,30 @@ def _kl_lock(info):
             "by_kind": st.get("requests_by_kind", {})}
 
 
-def run(args):
-    d = Dist()
-    n = args.gpus if args.gpus else d.world
-    from bacchus_gpu_controller_amd import native
-    from bacchus_gpu_controller_amd.testing.cluster import ADMIN_TOKEN, Cluster
-    from bacchus_gpu_controller_amd.testing.fake_google import FakeGoogle
+PRODUCT = ("controller", "admission", "synchronizer", "node-agent")
 
-    nat = native()
-    cluster = google = None
-    info = None
-    total_steps = args.warmup + args.steps
-    # Reconcile/sync workers spend most of their time waiting on API round trips, so they
-    # are not sized to the CPU share like the offered load is (16 = the binaries' default).
-    controller_workers = args.controller_workers or 16
-    sync_workers = args.sync_workers or 16
-    if d.rank == 0:
-        google = FakeGoogle().start()
-        rows = [{"id_username": name, "gpu": 1, "cpu": 8, "mem": 64, "storage": 100}
-                for r in range(d.world) for s in range(total_steps) for name in _names(r, s, args.batch)]
-        google.set_rows(rows)
-        ctrl_env = {"CONF_WORKERS": str(controller_workers)}
-        sync_env = {"CONF_WATCH": "true", "CONF_WORKERS": str(sync_workers), "RUST_LOG": args.log_level}
-        if args.reference_semantics:
-            # the reference's behaviour on this same stack: sheet read only on the periodic
-            # tick (synchronizer.rs:192), every tick rewrites every matched tenant, children
-            # applied one after another and re-applied on every reconcile (controller.rs:81-149)
-            ctrl_env.update({"CONF_SKIP_UNCHANGED": "false", "CONF_PARALLEL_CHILDREN": "false"})
-            sync_env.update({"CONF_WATCH": "false", "CONF_SKIP_UNCHANGED": "false"})
-        cluster = Cluster(controller_env=ctrl_env, log_level=args.log_level, tls_apiserver=args.tls_apiserver,
-                          apiserver_args=list(args.apiserver_arg))
-        cluster.start()
-        cluster.start_synchronizer(google, interval=args.sync_interval, extra_env=sync_env)
-        cluster.start_node_agent(max_gpus=n, n_mock_gpus=n, poll_interval_ms=args.poll_ms,
-                                 extra_env={"RUST_LOG": args.log_level})
-        info = {"server": cluster.server, "controller": f"http://127.0.0.1:{cluster.controller_port}",
-                "admission": f"https://127.0.0.1:{cluster.admission_port}",
-                "ca": os.path.join(cluster.cert_dir, "ca.crt"),
-                "node_agent": f"http://127.0.0.1:{cluster.node_agent_port}",
-                "synchronizer": f"http://127.0.0.1:{cluster.sync_port}",
-                "apiserver_ca": open(cluster.apiserver_ca).read() if args.tls_apiserver else "",
-                "apiserver_verify": cluster.verify}
-    info = d.broadcast_obj(info)
-    cpus = effective_cpus()
-    concurrency = args.concurrency if args.concurrency > 0 else auto_concurrency(d.world, cpus)
+
+def _cpu_snapshot(cluster):
+    return {name: _cpu_seconds(p.p.pid) for name, p in cluster.procs.items()}
+
+
+def _phase(d, nat, info, args, phase, concurrency, total_steps, cluster):
+    """One measured phase: W warmup + K timed steps at `concurrency` creates in flight per
+    rank.  Returns the per-phase record on rank 0 (None elsewhere)."""
+    from bacchus_gpu_controller_amd.testing.cluster import ADMIN_TOKEN
+
+    driver = nat.ChurnDriver(info["server"], ADMIN_TOKEN, f"r{d.rank}-", concurrency,
+                             ca_pem=info["apiserver_ca"], approve_url=info.get("approve_url", ""))
+    driver.start()
+    time.sleep(0.2)
+    prev = None
+    lat, clat, ap_lat, ap_ready = [], [], [], []
+    stage = {"ns": [], "rq": [], "rb": []}
+    ready = failed = timeouts = 0
+    lock0 = cpu0 = None
+    t_start = None
+    errors = []
     try:
-        driver = nat.ChurnDriver(info["server"], ADMIN_TOKEN, f"r{d.rank}-", concurrency,
-                                 ca_pem=info["apiserver_ca"])
-        driver.start()
-        time.sleep(0.2)
-        prev = None
-        lat, clat = [], []
-        stage = {"ns": [], "rq": [], "rb": []}
-        ready = failed = timeouts = 0
-        lock0 = None
-        t_start = None
-        errors = []
         for s in range(total_steps):
             if s == args.warmup:
                 d.barrier()
@@ -262,15 +230,18 @@ def run(args):
                     _clear(info["node_agent"] + "/debug/samples/telemetry_poll")
                     _clear(info["synchronizer"] + "/debug/samples/sync_ub")
                     lock0 = _kl_lock(info)
+                    cpu0 = _cpu_snapshot(cluster)
                 d.barrier()
                 t_start = time.perf_counter()
                 ru0 = resource.getrusage(resource.RUSAGE_SELF)
-            names = _names(d.rank, s, args.batch)
+            names = _names(d.rank, phase, s, args.batch)
             res = json.loads(driver.step_with_delete(names, prev or [], args.timeout))
             prev = names
             if s >= args.warmup:
                 lat += res["ready_latency_s"]
                 clat += res["create_latency_s"]
+                ap_lat += res.get("approve_latency_s", [])
+                ap_ready += res.get("approve_to_ready_latency_s", [])
                 for k in stage:
                     stage[k] += res[f"{k}_latency_s"]
                 ready += res["ready"]
@@ -281,30 +252,144 @@ def run(args):
         d.barrier()
         elapsed = time.perf_counter() - t_start
         ru1 = resource.getrusage(resource.RUSAGE_SELF)
+        cpu1 = _cpu_snapshot(cluster) if d.rank == 0 else None
         driver_cpu = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
         elapsed = d.max_scalar(elapsed)
         driver.remove(prev)
+    finally:
         driver.stop()
-        per_rank = d.gather_obj({"ready": ready, "failed": failed, "timeouts": timeouts, "lat": lat, "clat": clat,
-                                 "stage": stage, "errors": errors[:3], "driver_cpu_s": driver_cpu})
+    per_rank = d.gather_obj({"ready": ready, "failed": failed, "timeouts": timeouts, "lat": lat, "clat": clat,
+                             "ap_lat": ap_lat, "ap_ready": ap_ready, "stage": stage, "errors": errors[:3],
+                             "driver_cpu_s": driver_cpu})
+    if d.rank != 0:
+        return None
+    lock1 = _kl_lock(info)
+    rec = _samples(info["controller"] + "/debug/samples/reconcile")
+    hook = _samples(info["server"] + "/debug/samples/webhook", verify=info["apiserver_verify"])
+    adm = _samples(info["admission"] + "/debug/samples/admission", verify=info["ca"])
+    tel = _samples(info["node_agent"] + "/debug/samples/telemetry_poll")
+    syn = _samples(info["synchronizer"] + "/debug/samples/sync_ub")
+    total_ready = sum(p["ready"] for p in per_rank)
+    total_failed = sum(p["failed"] + p["timeouts"] for p in per_rank)
+    flat = lambda key: [x for p in per_rank for x in p[key]]  # noqa: E731
+    all_lat, all_clat = flat("lat"), flat("clat")
+    ms = lambda v: None if v is None else round(v * 1e3, 4)  # noqa: E731
+    per_cr = max(1, total_ready)
+    cpu_ms = {}
+    for name in cpu0:
+        if cpu0[name] is not None and cpu1.get(name) is not None:
+            cpu_ms["kube_lite" if name == "apiserver" else name.replace("-", "_")] = round(
+                (cpu1[name] - cpu0[name]) * 1e3 / per_cr, 4)
+    cpu_ms["load_driver"] = round(sum(p["driver_cpu_s"] for p in per_rank) * 1e3 / per_cr, 4)
+    cpu_ms["product_total"] = round(sum(cpu_ms.get(c.replace("-", "_"), 0.0) for c in PRODUCT), 4)
+    out = {
+        "value": round(total_ready / elapsed if elapsed > 0 else 0.0, 3),
+        "elapsed_s": elapsed,
+        "concurrency_per_rank": concurrency,
+        "reconcile_p99_ms": ms(_pct(rec, 0.99)),
+        "reconcile_p50_ms": ms(_pct(rec, 0.50)),
+        "reconciles": len(rec),
+        # webhook round trip as the API server measures it (TLS + handler + response)
+        "admission_p50_ms": ms(_pct(hook, 0.50)),
+        "admission_p99_ms": ms(_pct(hook, 0.99)),
+        "admission_handler_p50_ms": ms(_pct(adm, 0.50)),
+        "apply_to_ready_p50_ms": ms(_pct(all_lat, 0.50)),
+        "apply_to_ready_p99_ms": ms(_pct(all_lat, 0.99)),
+        "create_p50_ms": ms(_pct(all_clat, 0.50)),
+        # apply -> first observation of each child (Namespace; ResourceQuota with the sheet's
+        # quota; RoleBinding after the status write)
+        "stage_p50_ms": {k: ms(_pct([x for p in per_rank for x in p["stage"][k]], 0.50)) for k in ("ns", "rq", "rb")},
+        "telemetry_poll_p50_ms": ms(_pct(tel, 0.50)),
+        "sync_one_p50_ms": ms(_pct(syn, 0.50)),
+        # CPU time each process spent in the timed region, per Ready CR.  kube_lite is the
+        # test API server and load_driver the tenant simulator: neither ships.
+        "cpu_ms_per_cr": cpu_ms,
+        "apiserver_store_lock": _lock_report(lock0, lock1, elapsed),
+        "apiserver_requests_per_cr": round((lock1["requests"] - lock0["requests"]) / per_cr, 2),
+        "apiserver_requests_per_cr_by_kind": {
+            k: round((v - lock0["by_kind"].get(k, 0)) / per_cr, 3)
+            for k, v in sorted(lock1["by_kind"].items()) if v - lock0["by_kind"].get(k, 0) > 0},
+        "ready_crs": total_ready,
+        "failed_crs": total_failed,
+    }
+    if info.get("approve_url"):
+        out["approve_to_ready_p50_ms"] = ms(_pct(flat("ap_ready"), 0.50))
+        out["approve_to_ready_p99_ms"] = ms(_pct(flat("ap_ready"), 0.99))
+        out["create_to_approve_p50_ms"] = ms(_pct(flat("ap_lat"), 0.50))
+    if total_failed:
+        out["errors"] = [e for p in per_rank for e in p["errors"]][:5]
+    return out
+
+
+def run(args):
+    d = Dist()
+    n = args.gpus if args.gpus else d.world
+    from bacchus_gpu_controller_amd import native
+    from bacchus_gpu_controller_amd.testing.cluster import Cluster
+    from bacchus_gpu_controller_amd.testing.fake_google import FakeGoogle
+
+    nat = native()
+    cluster = google = None
+    info = None
+    total_steps = args.warmup + args.steps
+    cpus = effective_cpus()
+    tuned = args.tuned_concurrency if args.tuned_concurrency > 0 else auto_concurrency(d.world, cpus)
+    phases = [("m", args.concurrency)]
+    if args.tuned_phase and tuned != args.concurrency:
+        phases.append(("t", tuned))
+    semantics = "reference" if args.reference_semantics else args.semantics
+    # Reconcile/sync workers spend most of their time waiting on API round trips, so they
+    # are not sized to the CPU share like the offered load is (16 = the binaries' default).
+    controller_workers = args.controller_workers or 16
+    sync_workers = args.sync_workers or 16
+    if d.rank == 0:
+        google = FakeGoogle().start()
+        if not args.approve_after_create:
+            # pre-approved sheet: every tenant's row is marked O before it applies
+            google.set_rows([{"id_username": name} for r in range(d.world) for ph, _ in phases
+                             for s in range(total_steps) for name in _names(r, ph, s, args.batch)])
+        ctrl_env = {"CONF_WORKERS": str(controller_workers)}
+        sync_env = {"CONF_WATCH": "true", "CONF_WORKERS": str(sync_workers), "RUST_LOG": args.log_level,
+                    "CONF_SHEET_POLL_MS": str(args.sheet_poll_ms)}
+        if semantics in ("reference", "reference-controller"):
+            # the reference's controller on this same stack: children applied one after
+            # another and re-applied on every reconcile (controller.rs:81-149)
+            ctrl_env.update({"CONF_SKIP_UNCHANGED": "false", "CONF_PARALLEL_CHILDREN": "false"})
+        if semantics == "reference":
+            # ... and its synchronizer: sheet read only on the periodic tick
+            # (synchronizer.rs:192), every tick rewrites every matched tenant
+            sync_env.update({"CONF_WATCH": "false", "CONF_SKIP_UNCHANGED": "false"})
+        apiserver_args = list(args.apiserver_arg)
+        if args.write_latency_ms > 0:
+            apiserver_args += ["--write-latency-ms", str(args.write_latency_ms)]
+        cluster = Cluster(controller_env=ctrl_env, log_level=args.log_level, tls_apiserver=args.tls_apiserver,
+                          apiserver_args=apiserver_args)
+        cluster.start()
+        cluster.start_synchronizer(google, interval=args.sync_interval, extra_env=sync_env)
+        cluster.start_node_agent(max_gpus=n, n_mock_gpus=n, poll_interval_ms=args.poll_ms,
+                                 extra_env={"RUST_LOG": args.log_level})
+        info = {"server": cluster.server, "controller": f"http://127.0.0.1:{cluster.controller_port}",
+                "admission": f"https://127.0.0.1:{cluster.admission_port}",
+                "ca": os.path.join(cluster.cert_dir, "ca.crt"),
+                "node_agent": f"http://127.0.0.1:{cluster.node_agent_port}",
+                "synchronizer": f"http://127.0.0.1:{cluster.sync_port}",
+                "apiserver_ca": open(cluster.apiserver_ca).read() if args.tls_apiserver else "",
+                "apiserver_verify": cluster.verify,
+                "approve_url": google.base + "/_fake/rows" if args.approve_after_create else ""}
+    info = d.broadcast_obj(info)
+    try:
+        results = {ph: _phase(d, nat, info, args, ph, conc, total_steps, cluster) for ph, conc in phases}
         if d.rank != 0:
             return None
-        lock1 = _kl_lock(info)
-        rec = _samples(info["controller"] + "/debug/samples/reconcile")
-        hook = _samples(info["server"] + "/debug/samples/webhook", verify=info["apiserver_verify"])
-        adm = _samples(info["admission"] + "/debug/samples/admission", verify=info["ca"])
-        tel = _samples(info["node_agent"] + "/debug/samples/telemetry_poll")
-        syn = _samples(info["synchronizer"] + "/debug/samples/sync_ub")
+        main_r = results["m"]
         gpu_tel = _gpu_telemetry(info["node_agent"])
-        all_lat = [x for p in per_rank for x in p["lat"]]
-        all_clat = [x for p in per_rank for x in p["clat"]]
-        total_ready = sum(p["ready"] for p in per_rank)
-        total_failed = sum(p["failed"] + p["timeouts"] for p in per_rank)
-        value = total_ready / elapsed if elapsed > 0 else 0.0
-        ms = lambda v: None if v is None else round(v * 1e3, 4)  # noqa: E731
+        elapsed = main_r.pop("elapsed_s")
+        model = ("UserBootstrap onboarding churn (kube-lite" + (" over HTTPS" if args.tls_apiserver else "")
+                 + " + TLS admission + controller + synchronizer + MI355X node-agent)")
+        flow = "create->approve->Ready" if args.approve_after_create else "pre-approved sheet"
         out = {
             "metric": METRIC,
-            "value": round(value, 3),
+            "value": main_r.pop("value"),
             "unit": "CR/s",
             "n_gpus": n,
             "steps": args.steps,
@@ -313,48 +398,28 @@ def run(args):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
-            "data": "synthetic",
-            "config": {"model": "UserBootstrap onboarding churn (kube-lite" + (" over HTTPS" if args.tls_apiserver else "")
-                                + " + TLS admission + controller + synchronizer + MI355X node-agent)"
-                                + (" [reference semantics]" if args.reference_semantics else ""),
-                       "global_batch": args.batch * d.world, "seq_len": None, "parallelism": f"dp{d.world}",
-                       "concurrency_per_rank": concurrency, "control_plane_cpus": cpus,
-                       "controller_workers": controller_workers, "sync_workers": sync_workers},
-            "reconcile_p99_ms": ms(_pct(rec, 0.99)),
-            "reconcile_p50_ms": ms(_pct(rec, 0.50)),
-            "reconciles": len(rec),
-            "admission_p50_ms": ms(_pct(hook, 0.50)),
-            "admission_p99_ms": ms(_pct(hook, 0.99)),
-            "admission_handler_p50_ms": ms(_pct(adm, 0.50)),
-            "apply_to_ready_p50_ms": ms(_pct(all_lat, 0.50)),
-            "apply_to_ready_p99_ms": ms(_pct(all_lat, 0.99)),
-            "create_p50_ms": ms(_pct(all_clat, 0.50)),
-            # apply -> first observation of each child (Namespace; ResourceQuota with the sheet's
-            # quota; RoleBinding after the status write)
-            "stage_p50_ms": {k: ms(_pct([x for p in per_rank for x in p["stage"][k]], 0.50)) for k in ("ns", "rq", "rb")},
-            "telemetry_poll_p50_ms": ms(_pct(tel, 0.50)),
-            "sync_one_p50_ms": ms(_pct(syn, 0.50)),
-            # amdsmi counters of the advertised GPUs at the end of the timed region (node agent)
-            "gpu_telemetry": gpu_tel,  # synchronizer: quota patch + status write for one tenant
-            # kube-lite per-type store locks over the timed region: a busiest-type utilisation
-            # near 1.0 means the in-memory API server (not the controller) bounds throughput
-            "apiserver_store_lock": _lock_report(lock0, lock1, elapsed),
-            "apiserver_requests_per_cr": round((lock1["requests"] - lock0["requests"]) / max(1, total_ready), 2),
-            "apiserver_requests_per_cr_by_kind": {
-                k: round((v - lock0["by_kind"].get(k, 0)) / max(1, total_ready), 3)
-                for k, v in sorted(lock1["by_kind"].items()) if v - lock0["by_kind"].get(k, 0) > 0},
-            "ready_crs": total_ready,
-            "failed_crs": total_failed,
-            "reference_structural": {"apply_to_ready_p50_s": 30.0, "apply_to_ready_p99_s": 59.4,
-                                     "note": "reference gates readiness on a 60 s sheet poll (synchronizer.rs:192)"},
+            # a control plane: no tensor math, so no compute dtype (BASELINE names none)
+            "dtype": "none",
+            "data": "synthetic tenants (UserBootstrap CRs), fake Google sheet",
+            "config": {"model": model, "global_batch": args.batch * d.world, "seq_len": None,
+                       "parallelism": f"dp{d.world}", "semantics": semantics, "flow": flow,
+                       "concurrency_per_rank": args.concurrency, "log_level": args.log_level,
+                       "apiserver_write_latency_ms": args.write_latency_ms, "control_plane_cpus": cpus,
+                       "controller_workers": controller_workers, "sync_workers": sync_workers,
+                       "sheet_poll_ms": args.sheet_poll_ms, "sync_interval_s": args.sync_interval},
         }
-        if total_failed:
-            out["errors"] = [e for p in per_rank for e in p["errors"]][:5]
+        out.update(main_r)
+        if "t" in results:
+            # secondary: same stack, offered load sized to the CPU share (auto_concurrency)
+            t = results["t"]
+            out["tuned"] = {k: t.get(k) for k in ("value", "concurrency_per_rank", "reconcile_p99_ms",
+                                                  "admission_p50_ms", "apply_to_ready_p50_ms",
+                                                  "apply_to_ready_p99_ms", "cpu_ms_per_cr", "failed_crs")}
+        # amdsmi counters of the advertised GPUs at the end of the timed region (node agent)
+        out["gpu_telemetry"] = gpu_tel
+        out["reference_structural"] = {"apply_to_ready_p50_s": 30.0, "apply_to_ready_p99_s": 59.4,
+                                       "note": "reference gates readiness on a 60 s sheet poll (synchronizer.rs:192)"}
         if args.report_cpu and cluster is not None:
-            out["component_cpu_s"] = {name: _cpu_seconds(p.p.pid) for name, p in cluster.procs.items()}
-            # the load generator (native churn driver in each rank) shares the CPU quota
-            out["driver_cpu_s_timed"] = round(sum(p["driver_cpu_s"] for p in per_rank), 3)
             out["component_rss_mb"] = {name: _rss_mb(p.p.pid) for name, p in cluster.procs.items()}
             try:
                 st = cluster.stats()
@@ -389,20 +454,32 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=100, help="UserBootstraps applied per rank per step")
-    ap.add_argument("--concurrency", type=int, default=0,
-                    help="in-flight creates per rank (0 = sized to the CPU share, see auto_concurrency)")
+    ap.add_argument("--concurrency", type=int, default=100,
+                    help="in-flight creates per rank (BASELINE config #3: 100 concurrent CRs)")
+    ap.add_argument("--tuned-phase", action=argparse.BooleanOptionalAction, default=True,
+                    help="also measure a secondary phase with the offered load sized to the CPU share")
+    ap.add_argument("--tuned-concurrency", type=int, default=0, help="0 = auto_concurrency()")
     ap.add_argument("--timeout", type=float, default=120.0)
     ap.add_argument("--controller-workers", type=int, default=0, help="0 = 16")
     ap.add_argument("--sync-workers", type=int, default=0, help="0 = 16")
     ap.add_argument("--poll-ms", type=int, default=250)
-    ap.add_argument("--log-level", default="warn")
+    ap.add_argument("--log-level", default="info", help="RUST_LOG of every service (chart default: info)")
     ap.add_argument("--json-out", default="")
-    ap.add_argument("--reference-semantics", action="store_true",
-                    help="measure the reference's behaviour on this stack: periodic sheet sync only, "
-                         "sequential and unconditional child applies")
+    ap.add_argument("--semantics", choices=("this", "reference", "reference-controller"), default="this",
+                    help="reference: the reference's controller and synchronizer behaviour on this stack "
+                         "(periodic sheet sync only, sequential unconditional child applies); "
+                         "reference-controller: only the controller side")
+    ap.add_argument("--reference-semantics", action="store_true", help="alias for --semantics reference")
+    ap.add_argument("--approve-after-create", action="store_true",
+                    help="tenants apply first; each step's batch is approved by one sheet edit once its "
+                         "Namespaces exist (the reference's onboarding order); times create->approve->Ready")
+    ap.add_argument("--sheet-poll-ms", type=int, default=5000,
+                    help="synchronizer Drive version poll (CONF_SHEET_POLL_MS; product default 5000)")
+    ap.add_argument("--write-latency-ms", type=float, default=0.0,
+                    help="kube-lite storage commit latency per write (etcd model)")
     ap.add_argument("--sync-interval", type=int, default=60, help="synchronizer tick (s); the reference default is 60")
     ap.add_argument("--apiserver-arg", action="append", default=[], help="extra kube-lite flag (repeatable)")
-    ap.add_argument("--report-cpu", action="store_true", help="add per-component CPU seconds to the JSON")
+    ap.add_argument("--report-cpu", action="store_true", help="add RSS, object counts and controller gauges")
     ap.add_argument("--tls-apiserver", action=argparse.BooleanOptionalAction, default=True,
                     help="components reach kube-lite over HTTPS via kubeconfigs, as in a real cluster")
     args = ap.parse_args(argv)

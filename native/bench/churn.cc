@@ -70,7 +70,8 @@ void ChurnDriver::mark(const std::string& name, int which, int64_t t) {
   Track& tr = it->second;
   int64_t* slot = which == 0 ? &tr.t_ns : which == 1 ? &tr.t_rq : &tr.t_rb;
   if (!*slot) *slot = t;
-  if (ready_locked(tr)) cv_.notify_all();
+  // approve-after-create waits on Namespaces alone; otherwise only Ready matters
+  if (ready_locked(tr) || (which == 0 && !opts_.approve_url.empty())) cv_.notify_all();
 }
 
 void ChurnDriver::start() {
@@ -152,7 +153,9 @@ json::Value ChurnDriver::step(const std::vector<std::string>& names, double time
     }));
   }
   for (auto& f : futs) f.get();
-  auto deadline = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s);
+  auto deadline = std::chrono::steady_clock::now() +
+                  std::chrono::duration_cast<std::chrono::steady_clock::duration>(std::chrono::duration<double>(timeout_s));
+  if (!opts_.approve_url.empty()) approve_batch(names, deadline);
   Value out = Value::object();
   std::unique_lock<std::mutex> lk(mu_);
   auto all_done = [&] {
@@ -166,6 +169,7 @@ json::Value ChurnDriver::step(const std::vector<std::string>& names, double time
   int64_t t_end = metrics::now_ns();
   Value lat = Value::array(), clat = Value::array(), errs = Value::array();
   Value ns_lat = Value::array(), rq_lat = Value::array(), rb_lat = Value::array();
+  Value ap_lat = Value::array(), ap_ready = Value::array();
   int ready = 0, failed = 0, timeouts = 0;
   int64_t last_ready = t0;
   for (const auto& n : names) {
@@ -182,6 +186,10 @@ json::Value ChurnDriver::step(const std::vector<std::string>& names, double time
       ns_lat.push_back(static_cast<double>(t.t_ns - t.t_start) * 1e-9);
       rq_lat.push_back(static_cast<double>(t.t_rq - t.t_start) * 1e-9);
       rb_lat.push_back(static_cast<double>(t.t_rb - t.t_start) * 1e-9);
+      if (t.t_approved) {
+        ap_lat.push_back(static_cast<double>(t.t_approved - t.t_start) * 1e-9);
+        ap_ready.push_back(static_cast<double>(tr - t.t_approved) * 1e-9);
+      }
     } else {
       ++timeouts;
     }
@@ -197,7 +205,35 @@ json::Value ChurnDriver::step(const std::vector<std::string>& names, double time
   out["rq_latency_s"] = rq_lat;
   out["rb_latency_s"] = rb_lat;
   out["errors"] = errs;
+  if (!opts_.approve_url.empty()) {
+    out["approve_latency_s"] = ap_lat;
+    out["approve_to_ready_latency_s"] = ap_ready;
+  }
   return out;
+}
+
+void ChurnDriver::approve_batch(const std::vector<std::string>& names,
+                                std::chrono::steady_clock::time_point deadline) {
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait_until(lk, deadline, [&] {
+      for (const auto& n : names) {
+        const Track& t = tracks_[n];
+        if (!t.failed && !t.t_ns) return false;
+      }
+      return true;
+    });
+  }
+  Value rows = Value::array();
+  for (const auto& n : names) rows.push_back(Value::object({{"id_username", n}}));
+  Value body = Value::object({{"rows", rows}, {"append", true}});
+  http::Headers h;
+  h.set("Content-Type", "application/json");
+  int64_t t = metrics::now_ns();
+  http::Response r = http::fetch("POST", opts_.approve_url, body.dump(), &h);
+  if (r.status != 200) throw std::runtime_error("approve: sheet edit failed: " + std::to_string(r.status) + " " + r.body);
+  std::lock_guard<std::mutex> lk(mu_);
+  for (const auto& n : names) tracks_[n].t_approved = t;
 }
 
 int ChurnDriver::remove(const std::vector<std::string>& names) {

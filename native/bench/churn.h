@@ -36,6 +36,11 @@ struct ChurnOptions {
   std::string gpu_quota_key = "requests.amd.com/gpu";
   int concurrency = 32;
   std::string name_prefix;  // only names with this prefix are tracked (one driver per rank)
+  // Approve-after-create (the reference's real onboarding order):
+  // when set, a step first waits for every tenant's Namespace, then approves the whole
+  // batch with one sheet edit (POST {"rows":[{"id_username":...}],"append":true} to this
+  // URL, the fake Google's operator endpoint), then waits for Ready.
+  std::string approve_url;
 };
 
 class ChurnDriver {
@@ -46,7 +51,8 @@ class ChurnDriver {
   // Creates every name concurrently and waits for all to be Ready (or timeout).
   // Returns {"ready": n, "failed": n, "timeouts": n, "elapsed_s": x,
   //          "ready_latency_s": [...], "create_latency_s": [...], "ns_latency_s": [...],
-  //          "rq_latency_s": [...], "rb_latency_s": [...], "errors": [...]}.
+  //          "rq_latency_s": [...], "rb_latency_s": [...], "errors": [...]}; with approve_url
+  //          also "approve_to_ready_latency_s" and "approve_latency_s" (create -> approval).
   json::Value step(const std::vector<std::string>& names, double timeout_s);
   // Same, while deleting `previous` concurrently (churn: the previous step's tenants
   // leave while the next ones arrive); the step ends when both are done.
@@ -60,11 +66,14 @@ class ChurnDriver {
   struct Track {
     int64_t t_start = 0;
     int64_t t_created = 0;
+    int64_t t_approved = 0;
     int64_t t_ns = 0, t_rq = 0, t_rb = 0;
     bool failed = false;
     std::string error;
   };
   void mark(const std::string& name, int which, int64_t t);
+  // Approve-after-create: waits for the batch's Namespaces, then edits the sheet once.
+  void approve_batch(const std::vector<std::string>& names, std::chrono::steady_clock::time_point deadline);
   bool ready_locked(const Track& t) const { return t.t_ns && t.t_rq && t.t_rb; }
 
   ChurnOptions opts_;

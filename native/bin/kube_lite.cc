@@ -26,7 +26,6 @@ static void usage() {
                "                 [--tls-cert F --tls-key F] [--service-override ns/name=host:port]...\n"
                "                 [--bookmark-ms N] [--history N] [--watch-coalesce-us N] [--gc-workers N]\n"
                "                 [--write-latency-ms F]\n"
-               "                 [--write-latency-ms F]\n"
                "                 [--manifest file.{json,yaml}]...\n");
 }
 
@@ -55,6 +54,7 @@ int main(int argc, char** argv) {
     else if (a == "--history") o.history_limit = static_cast<size_t>(std::atol(next().c_str()));
     else if (a == "--watch-coalesce-us") o.watch_coalesce_us = std::atoi(next().c_str());
     else if (a == "--gc-workers") o.gc_workers = std::atoi(next().c_str());
+    else if (a == "--write-latency-ms") o.write_latency_us = static_cast<int64_t>(std::atof(next().c_str()) * 1000.0);
     else if (a == "--manifest") manifests.push_back(next());
     else if (a == "--service-override") {
       std::string v = next();

@@ -28,7 +28,29 @@ def test_bench_two_ranks_gloo():
     assert d["config"]["global_batch"] == 40 and d["config"]["parallelism"] == "dp2"
     assert d["ready_crs"] == 2 * 2 * 20 and d["failed_crs"] == 0
     assert d["value"] > 0 and d["scaling"] == "weak"
-    assert d["config"]["concurrency_per_rank"] >= 4 and d["config"]["control_plane_cpus"] >= 1
+    assert d["config"]["concurrency_per_rank"] == 100 and d["config"]["control_plane_cpus"] >= 1
+    assert d["config"]["log_level"] == "info" and d["dtype"] == "none"
+    # per-component CPU cost of the timed region, split product vs test scaffolding
+    cpu = d["cpu_ms_per_cr"]
+    for k in ("controller", "admission", "synchronizer", "node_agent", "kube_lite", "load_driver", "product_total"):
+        assert k in cpu and cpu[k] >= 0
+    assert d["apiserver_requests_per_cr"] > 0
+    assert d["tuned"]["concurrency_per_rank"] < 100 and d["tuned"]["failed_crs"] == 0
+
+
+def test_bench_approve_after_create():
+    """--approve-after-create: tenants apply, then one sheet edit per step approves them
+    (the reference's onboarding order); the JSON times approve -> Ready."""
+    cmd = [sys.executable, os.path.join(REPO_ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--batch", "20",
+           "--approve-after-create", "--sheet-poll-ms", "300", "--no-tuned-phase", "--write-latency-ms", "1"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=REPO_ROOT,
+                       env=dict(os.environ, BGC_BENCH_CPU="1"))
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["ready_crs"] == 40 and d["failed_crs"] == 0
+    assert d["config"]["flow"] == "create->approve->Ready" and d["config"]["apiserver_write_latency_ms"] == 1
+    assert 0 < d["approve_to_ready_p50_ms"] < 5000
+    assert d["create_to_approve_p50_ms"] > 0
 
 
 def test_auto_concurrency_follows_cpu_share():
