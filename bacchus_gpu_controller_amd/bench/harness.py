@@ -218,8 +218,13 @@ def _phase(d, nat, info, args, phase, concurrency, total_steps, cluster):
     lock0 = cpu0 = None
     t_start = None
     errors = []
+    last_note = time.perf_counter()
     try:
         for s in range(total_steps):
+            if d.rank == 0 and time.perf_counter() - last_note > 15:
+                # slow modes (the reference's 60 s sheet tick) must still show progress
+                print(f"[bench] phase {phase} step {s}/{total_steps}", file=sys.stderr, flush=True)
+                last_note = time.perf_counter()
             if s == args.warmup:
                 d.barrier()
                 d.sync()
