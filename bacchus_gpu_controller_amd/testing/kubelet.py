@@ -184,3 +184,78 @@ class FakeKubelet:
                     return False
                 self.cv.wait(left)
         return True
+
+
+def _build_podresources():
+    """k8s.io/kubelet/pkg/apis/podresources/v1 (List only)."""
+    fd = descriptor_pb2.FileDescriptorProto(name="bgc_podresources_v1.proto", package="v1", syntax="proto3")
+    opt, rep = _F.LABEL_OPTIONAL, _F.LABEL_REPEATED
+    S, I64, M = _F.TYPE_STRING, _F.TYPE_INT64, _F.TYPE_MESSAGE
+
+    def msg(name, *fields):
+        m = fd.message_type.add(name=name)
+        for num, fname, ftype, label, tname in fields:
+            f = m.field.add(name=fname, number=num, type=ftype, label=label)
+            if tname:
+                f.type_name = tname
+
+    msg("ListPodResourcesRequest")
+    msg("NUMANode", (1, "ID", I64, opt, None))
+    msg("TopologyInfo", (1, "nodes", M, rep, ".v1.NUMANode"))
+    msg("ContainerDevices", (1, "resource_name", S, opt, None), (2, "device_ids", S, rep, None),
+        (3, "topology", M, opt, ".v1.TopologyInfo"))
+    msg("ContainerResources", (1, "name", S, opt, None), (2, "devices", M, rep, ".v1.ContainerDevices"),
+        (3, "cpu_ids", I64, rep, None))
+    msg("PodResources", (1, "name", S, opt, None), (2, "namespace", S, opt, None),
+        (3, "containers", M, rep, ".v1.ContainerResources"))
+    msg("ListPodResourcesResponse", (1, "pod_resources", M, rep, ".v1.PodResources"))
+    pool = descriptor_pool.DescriptorPool()
+    pool.Add(fd)
+    return {m.name: message_factory.GetMessageClass(pool.FindMessageTypeByName(f"v1.{m.name}"))
+            for m in fd.message_type}
+
+
+podres_pb = _build_podresources()
+
+
+class FakePodResources:
+    """The kubelet's pod-resources endpoint (v1.PodResourcesLister/List) on a unix socket.
+    `assign(pod, resource, ids)` sets what a pod's container holds; `lists` counts calls."""
+
+    def __init__(self, socket_path):
+        self.path = socket_path
+        self.pods = {}  # pod -> (resource, [ids])
+        self.lists = 0
+        self.server = None
+
+    def assign(self, pod, resource, ids):
+        self.pods[pod] = (resource, list(ids))
+
+    def release(self, pod):
+        self.pods.pop(pod, None)
+
+    def _list(self, req, ctx):
+        self.lists += 1
+        r = podres_pb["ListPodResourcesResponse"]()
+        for pod, (res, ids) in sorted(self.pods.items()):
+            p = r.pod_resources.add(name=pod, namespace="default")
+            c = p.containers.add(name="main")
+            c.devices.add(resource_name=res, device_ids=ids)
+        return r
+
+    def start(self):
+        os.makedirs(os.path.dirname(self.path), exist_ok=True)
+        self.server = grpc.server(futures.ThreadPoolExecutor(max_workers=2))
+        handler = grpc.method_handlers_generic_handler("v1.PodResourcesLister", {
+            "List": grpc.unary_unary_rpc_method_handler(
+                self._list, request_deserializer=podres_pb["ListPodResourcesRequest"].FromString,
+                response_serializer=podres_pb["ListPodResourcesResponse"].SerializeToString)})
+        self.server.add_generic_rpc_handlers((handler,))
+        self.server.add_insecure_port("unix://" + self.path)
+        self.server.start()
+        return self
+
+    def stop(self):
+        if self.server is not None:
+            self.server.stop(grace=None)
+            self.server = None

@@ -3,10 +3,15 @@
 #include <amd_smi/amdsmi.h>
 #include <dlfcn.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
+#include <chrono>
+#include <map>
 #include <mutex>
+#include <thread>
 #include <stdexcept>
 
 #include "core/log.h"
@@ -42,7 +47,64 @@ Value to_json(const GpuInfo& g) {
   v["memory_partition"] = g.memory_partition;
   v["power_cap_w"] = g.power_cap_w;
   v["hip_id"] = g.hip_id;
+  v["drm_render"] = g.drm_render;
+  v["drm_card"] = g.drm_card;
+  v["bad_page_threshold"] = g.bad_page_threshold;
+  Value links = Value::array();
+  for (const auto& l : g.links) links.push_back(to_json(l));
+  v["links"] = links;
+  Value phys = Value::array();
+  for (const auto& l : g.phys_links) phys.push_back(to_json(l));
+  v["phys_links"] = phys;
   return v;
+}
+
+Value to_json(const PeerLink& l) {
+  return Value::object({{"peer", l.peer}, {"type", l.type}, {"hops", static_cast<unsigned long long>(l.hops)},
+                        {"weight", static_cast<unsigned long long>(l.weight)},
+                        {"min_bw_mbps", static_cast<unsigned long long>(l.min_bw_mbps)},
+                        {"max_bw_mbps", static_cast<unsigned long long>(l.max_bw_mbps)}});
+}
+
+Value to_json(const PhysLink& l) {
+  return Value::object({{"peer_bdf", l.peer_bdf}, {"type", l.type}, {"bit_rate_gbps", l.bit_rate_gbps},
+                        {"max_bandwidth_gbps", l.max_bandwidth_gbps},
+                        {"read_kb", static_cast<unsigned long long>(l.read_kb)},
+                        {"write_kb", static_cast<unsigned long long>(l.write_kb)}});
+}
+
+static uint64_t u64_or(const Value& v, const char* k, uint64_t d) { return v.get(k).is_int() ? v.get(k).as_uint() : d; }
+
+PeerLink peer_link_from_json(const Value& v) {
+  PeerLink l;
+  l.peer = v.get("peer").is_int() ? static_cast<int>(v.get("peer").as_int()) : -1;
+  l.type = v.get_string("type", "unknown");
+  l.hops = u64_or(v, "hops", 0);
+  l.weight = u64_or(v, "weight", 0);
+  l.min_bw_mbps = u64_or(v, "min_bw_mbps", 0);
+  l.max_bw_mbps = u64_or(v, "max_bw_mbps", 0);
+  return l;
+}
+
+PhysLink phys_link_from_json(const Value& v) {
+  PhysLink l;
+  l.peer_bdf = v.get_string("peer_bdf");
+  l.type = v.get_string("type", "xgmi");
+  l.bit_rate_gbps = static_cast<uint32_t>(u64_or(v, "bit_rate_gbps", 0));
+  l.max_bandwidth_gbps = static_cast<uint32_t>(u64_or(v, "max_bandwidth_gbps", 0));
+  l.read_kb = u64_or(v, "read_kb", 0);
+  l.write_kb = u64_or(v, "write_kb", 0);
+  return l;
+}
+
+const char* link_type_name(int t) {
+  switch (t) {
+    case AMDSMI_LINK_TYPE_INTERNAL: return "internal";
+    case AMDSMI_LINK_TYPE_PCIE: return "pcie";
+    case AMDSMI_LINK_TYPE_XGMI: return "xgmi";
+    case AMDSMI_LINK_TYPE_NOT_APPLICABLE: return "n/a";
+    default: return "unknown";
+  }
 }
 
 Value to_json(const Telemetry& t) {
@@ -60,11 +122,29 @@ Value to_json(const Telemetry& t) {
   v["vram_total_mb"] = static_cast<unsigned long long>(t.vram_total_mb);
   v["gfxclk_mhz"] = t.gfxclk_mhz;
   v["uclk_mhz"] = t.uclk_mhz;
-  v["throttle_status"] = static_cast<unsigned long long>(t.throttle_status);
+  v["throttle_status"] = t.throttle_valid ? Value(static_cast<unsigned long long>(t.throttle_status)) : Value();
+  v["violation_ppt_pct"] = t.violation_ppt_pct < 0 ? Value() : Value(t.violation_ppt_pct);
+  v["violation_thermal_pct"] = t.violation_thermal_pct < 0 ? Value() : Value(t.violation_thermal_pct);
   v["ecc_correctable"] = static_cast<unsigned long long>(t.ecc_correctable);
   v["ecc_uncorrectable"] = static_cast<unsigned long long>(t.ecc_uncorrectable);
+  v["ecc_deferred"] = static_cast<unsigned long long>(t.ecc_deferred);
   v["xgmi_links_up"] = t.xgmi_links_up;
   v["xgmi_links_total"] = t.xgmi_links_total;
+  if (t.ras_ok) {
+    v["retired_pages"] = static_cast<unsigned long long>(t.retired_pages);
+    v["unreservable_pages"] = static_cast<unsigned long long>(t.unreservable_pages);
+    Value blocks = Value::object();
+    for (const auto& b : t.ecc_blocks) {
+      blocks[b.block] = Value::object({{"ce", static_cast<unsigned long long>(b.correctable)},
+                                       {"ue", static_cast<unsigned long long>(b.uncorrectable)},
+                                       {"de", static_cast<unsigned long long>(b.deferred)}});
+    }
+    v["ecc_blocks"] = blocks;
+    Value links = Value::array();
+    for (const auto& l : t.links) links.push_back(to_json(l));
+    v["links"] = links;
+  }
+  if (t.acc_counter != Telemetry::kNoAcc) v["acc_counter"] = static_cast<unsigned long long>(t.acc_counter);
   v["poll_us"] = t.poll_us;
   return v;
 }
@@ -95,7 +175,38 @@ GpuInfo gpu_info_from_json(const Value& v) {
   g.memory_partition = v.get_string("memory_partition", "NPS1");
   if (v.get("power_cap_w").is_int()) g.power_cap_w = static_cast<uint32_t>(v.get("power_cap_w").as_int());
   g.hip_id = v.get("hip_id").is_int() ? static_cast<int>(v.get("hip_id").as_int()) : g.index;
+  g.drm_render = v.get("drm_render").is_int() ? static_cast<int>(v.get("drm_render").as_int()) : -1;
+  g.drm_card = v.get("drm_card").is_int() ? static_cast<int>(v.get("drm_card").as_int()) : -1;
+  g.bad_page_threshold = static_cast<uint32_t>(u64_or(v, "bad_page_threshold", 0));
+  for (const auto& l : v.get("links").items()) g.links.push_back(peer_link_from_json(l));
+  for (const auto& l : v.get("phys_links").items()) g.phys_links.push_back(phys_link_from_json(l));
   return g;
+}
+
+Telemetry telemetry_from_json(const Value& v) {
+  Telemetry t;
+  auto num = [&](const char* k, double d) { return v.get(k).is_number() ? v.get(k).as_double() : d; };
+  t.index = static_cast<int>(num("index", 0));
+  t.ok = v.get("ok").is_bool() ? v.get("ok").as_bool() : true;
+  t.error = v.get_string("error");
+  t.temp_hotspot_c = num("temp_hotspot_c", 40);
+  t.temp_mem_c = num("temp_mem_c", 40);
+  t.ecc_uncorrectable = static_cast<uint64_t>(num("ecc_uncorrectable", 0));
+  t.xgmi_links_up = static_cast<int>(num("xgmi_links_up", -1));
+  t.xgmi_links_total = static_cast<int>(num("xgmi_links_total", -1));
+  t.violation_ppt_pct = num("violation_ppt_pct", -1);
+  t.violation_thermal_pct = num("violation_thermal_pct", -1);
+  if (v.get("acc_counter").is_number()) {
+    t.acc_counter = static_cast<uint64_t>(num("acc_counter", 0));
+    t.acc_ppt = v.get("acc_ppt").is_number() ? static_cast<uint64_t>(num("acc_ppt", 0)) : Telemetry::kNoAcc;
+    t.acc_thermal = v.get("acc_thermal").is_number() ? static_cast<uint64_t>(num("acc_thermal", 0)) : Telemetry::kNoAcc;
+  }
+  if (v.get("retired_pages").is_number() || v.get("unreservable_pages").is_number()) {
+    t.ras_ok = true;
+    t.retired_pages = static_cast<uint64_t>(num("retired_pages", 0));
+    t.unreservable_pages = static_cast<uint64_t>(num("unreservable_pages", 0));
+  }
+  return t;
 }
 
 Value default_mi355x_fixture(int n_gpus, uint64_t hive_id) {
@@ -122,6 +233,20 @@ Value default_mi355x_fixture(int n_gpus, uint64_t hive_id) {
     g["compute_partition"] = "SPX";
     g["memory_partition"] = "NPS1";
     g["power_cap_w"] = 1400;
+    g["drm_card"] = 1 + i;
+    g["drm_render"] = 128 + i;
+    // 8x MI355X UBB: a full xGMI mesh, one link to every peer (7 x ~153 GB/s per GPU).
+    Value links = Value::array(), phys = Value::array();
+    for (int j = 0; j < n_gpus; ++j) {
+      if (j == i) continue;
+      links.push_back(Value::object({{"peer", j}, {"type", "xgmi"}, {"hops", 1}, {"weight", 15},
+                                     {"min_bw_mbps", 50000}, {"max_bw_mbps", 153600}}));
+      std::snprintf(buf, sizeof(buf), "0000:%02x:00.0", 0x05 + 0x10 * j);
+      phys.push_back(Value::object({{"peer_bdf", std::string(buf)}, {"type", "xgmi"}, {"bit_rate_gbps", 32},
+                                    {"max_bandwidth_gbps", 1228}}));
+    }
+    g["links"] = links;
+    g["phys_links"] = phys;
     Value t = Value::object();
     t["gfx_activity_pct"] = 0;
     t["umc_activity_pct"] = 0;
@@ -182,10 +307,9 @@ class MockBackend : public Backend {
     }
     return out;
   }
-  Telemetry sample(int index, bool full) override {
-    (void)full;
+  Telemetry sample(int index, SampleLevel level) override {
     reload();
-    std::lock_guard<std::mutex> lk(mu_);
+    std::unique_lock<std::mutex> lk(mu_);
     int64_t t0 = metrics::now_ns();
     Telemetry t;
     t.index = index;
@@ -213,13 +337,60 @@ class MockBackend : public Backend {
     t.vram_total_mb = g.get("vram_total_mb").is_int() ? g.get("vram_total_mb").as_uint() : 0;
     t.gfxclk_mhz = static_cast<uint32_t>(num("gfxclk_mhz", 0));
     t.uclk_mhz = static_cast<uint32_t>(num("uclk_mhz", 0));
+    t.throttle_valid = tv.get("throttle_status").is_number();
     t.throttle_status = static_cast<uint64_t>(num("throttle_status", 0));
-    t.ecc_correctable = static_cast<uint64_t>(num("ecc_correctable", 0));
-    t.ecc_uncorrectable = static_cast<uint64_t>(num("ecc_uncorrectable", 0));
+    // Violation accumulators: either given directly, or synthesised from a steady
+    // "violation_*_pct" so a fixture can model sustained throttling without rewriting
+    // the file every poll (the counter advances 1000 per sample).
+    if (tv.get("acc_counter").is_number()) {
+      t.acc_counter = static_cast<uint64_t>(num("acc_counter", 0));
+      t.acc_ppt = static_cast<uint64_t>(num("acc_ppt", 0));
+      t.acc_thermal = static_cast<uint64_t>(num("acc_thermal", 0));
+    } else {
+      uint64_t& seq = acc_seq_[index];
+      seq += 1000;
+      t.acc_counter = seq;
+      t.acc_ppt = static_cast<uint64_t>(static_cast<double>(seq) * num("violation_ppt_pct", 0) / 100.0);
+      t.acc_thermal = static_cast<uint64_t>(static_cast<double>(seq) * num("violation_thermal_pct", 0) / 100.0);
+    }
+    if (level >= SampleLevel::Slow) {
+      t.ecc_correctable = static_cast<uint64_t>(num("ecc_correctable", 0));
+      t.ecc_uncorrectable = static_cast<uint64_t>(num("ecc_uncorrectable", 0));
+      t.ecc_deferred = static_cast<uint64_t>(num("ecc_deferred", 0));
+    } else {
+      t.vram_used_mb = 0;
+    }
     t.xgmi_links_up = static_cast<int>(num("xgmi_links_up", -1));
     t.xgmi_links_total = static_cast<int>(num("xgmi_links_total", -1));
+    if (level == SampleLevel::Ras) {
+      t.ras_ok = true;
+      t.retired_pages = static_cast<uint64_t>(num("retired_pages", 0));
+      t.unreservable_pages = static_cast<uint64_t>(num("unreservable_pages", 0));
+      for (const auto& b : tv.get("ecc_blocks").items()) {
+        EccBlock e;
+        e.block = b.get_string("block");
+        e.correctable = u64_or(b, "ce", 0);
+        e.uncorrectable = u64_or(b, "ue", 0);
+        e.deferred = u64_or(b, "de", 0);
+        t.ecc_blocks.push_back(std::move(e));
+      }
+      const Value& links = tv.get("links").is_array() ? tv.get("links") : g.get("phys_links");
+      for (const auto& l : links.items()) t.links.push_back(phys_link_from_json(l));
+    }
+    if (const double d = num("sample_delay_us", 0); d > 0) {  // models amdsmi's per-call cost
+      lk.unlock();
+      std::this_thread::sleep_for(std::chrono::microseconds(static_cast<int64_t>(d)));
+    }
     t.poll_us = static_cast<double>(metrics::now_ns() - t0) / 1e3;
     return t;
+  }
+  int busy_processes(int index) override {
+    reload();
+    std::lock_guard<std::mutex> lk(mu_);
+    const auto& gpus = fixture_.get("gpus").items();
+    if (index < 0 || static_cast<size_t>(index) >= gpus.size()) return -1;
+    const Value& b = gpus[static_cast<size_t>(index)].get("telemetry").get("busy_processes");
+    return b.is_int() ? static_cast<int>(b.as_int()) : 0;
   }
 
  private:
@@ -227,7 +398,8 @@ class MockBackend : public Backend {
   std::string path_;
   struct timespec mtime_ {};
   std::mutex reload_mu_;  // guards mtime_ and serializes file reads
-  std::mutex mu_;         // guards fixture_
+  std::mutex mu_;         // guards fixture_ and acc_seq_
+  std::map<int, uint64_t> acc_seq_;
 };
 
 // ---------------------------------------------------------------------------
@@ -252,7 +424,38 @@ struct AmdSmiApi {
   decltype(&amdsmi_get_gpu_total_ecc_count) get_ecc = nullptr;
   decltype(&amdsmi_get_power_info) get_power = nullptr;
   decltype(&amdsmi_get_gpu_enumeration_info) get_enum = nullptr;
+  decltype(&amdsmi_topo_get_link_type) topo_link_type = nullptr;
+  decltype(&amdsmi_topo_get_link_weight) topo_link_weight = nullptr;
+  decltype(&amdsmi_get_minmax_bandwidth_between_processors) minmax_bw = nullptr;
+  decltype(&amdsmi_get_link_metrics) link_metrics = nullptr;
+  decltype(&amdsmi_get_gpu_bad_page_info) bad_pages = nullptr;
+  decltype(&amdsmi_get_gpu_bad_page_threshold) bad_page_threshold = nullptr;
+  decltype(&amdsmi_get_gpu_ecc_enabled) ecc_enabled = nullptr;
+  decltype(&amdsmi_get_gpu_ecc_count) ecc_count = nullptr;
+  decltype(&amdsmi_get_gpu_process_list) process_list = nullptr;
 };
+
+struct BlockName {
+  amdsmi_gpu_block_t block;
+  const char* name;
+};
+constexpr BlockName kEccBlocks[] = {
+    {AMDSMI_GPU_BLOCK_UMC, "umc"},       {AMDSMI_GPU_BLOCK_SDMA, "sdma"},   {AMDSMI_GPU_BLOCK_GFX, "gfx"},
+    {AMDSMI_GPU_BLOCK_MMHUB, "mmhub"},   {AMDSMI_GPU_BLOCK_ATHUB, "athub"}, {AMDSMI_GPU_BLOCK_PCIE_BIF, "pcie_bif"},
+    {AMDSMI_GPU_BLOCK_HDP, "hdp"},       {AMDSMI_GPU_BLOCK_XGMI_WAFL, "xgmi_wafl"}, {AMDSMI_GPU_BLOCK_DF, "df"},
+    {AMDSMI_GPU_BLOCK_SMN, "smn"},       {AMDSMI_GPU_BLOCK_SEM, "sem"},     {AMDSMI_GPU_BLOCK_MP0, "mp0"},
+    {AMDSMI_GPU_BLOCK_MP1, "mp1"},       {AMDSMI_GPU_BLOCK_FUSE, "fuse"},   {AMDSMI_GPU_BLOCK_MCA, "mca"},
+    {AMDSMI_GPU_BLOCK_VCN, "vcn"},       {AMDSMI_GPU_BLOCK_JPEG, "jpeg"},   {AMDSMI_GPU_BLOCK_IH, "ih"},
+    {AMDSMI_GPU_BLOCK_MPIO, "mpio"},
+};
+
+std::string bdf_string(const amdsmi_bdf_t& bdf) {
+  char buf[32];
+  std::snprintf(buf, sizeof(buf), "%04llx:%02x:%02x.%x", static_cast<unsigned long long>(bdf.domain_number),
+                static_cast<unsigned>(bdf.bus_number), static_cast<unsigned>(bdf.device_number),
+                static_cast<unsigned>(bdf.function_number));
+  return buf;
+}
 
 template <typename F>
 void resolve(void* lib, F& fn, const char* sym, bool required) {
@@ -286,6 +489,15 @@ class AmdSmiBackend : public Backend {
     resolve(api_.lib, api_.get_ecc, "amdsmi_get_gpu_total_ecc_count", false);
     resolve(api_.lib, api_.get_power, "amdsmi_get_power_info", false);
     resolve(api_.lib, api_.get_enum, "amdsmi_get_gpu_enumeration_info", false);
+    resolve(api_.lib, api_.topo_link_type, "amdsmi_topo_get_link_type", false);
+    resolve(api_.lib, api_.topo_link_weight, "amdsmi_topo_get_link_weight", false);
+    resolve(api_.lib, api_.minmax_bw, "amdsmi_get_minmax_bandwidth_between_processors", false);
+    resolve(api_.lib, api_.link_metrics, "amdsmi_get_link_metrics", false);
+    resolve(api_.lib, api_.bad_pages, "amdsmi_get_gpu_bad_page_info", false);
+    resolve(api_.lib, api_.bad_page_threshold, "amdsmi_get_gpu_bad_page_threshold", false);
+    resolve(api_.lib, api_.ecc_enabled, "amdsmi_get_gpu_ecc_enabled", false);
+    resolve(api_.lib, api_.ecc_count, "amdsmi_get_gpu_ecc_count", false);
+    resolve(api_.lib, api_.process_list, "amdsmi_get_gpu_process_list", false);
     amdsmi_status_t st = api_.init(AMDSMI_INIT_AMD_GPUS);
     if (st != AMDSMI_STATUS_SUCCESS) throw std::runtime_error("amdsmi_init failed: status " + std::to_string(st));
     initialized_ = true;
@@ -322,13 +534,7 @@ class AmdSmiBackend : public Backend {
       }
       if (api_.get_bdf) {
         amdsmi_bdf_t bdf{};
-        if (api_.get_bdf(h, &bdf) == AMDSMI_STATUS_SUCCESS) {
-          char buf[32];
-          std::snprintf(buf, sizeof(buf), "%04llx:%02x:%02x.%x", static_cast<unsigned long long>(bdf.domain_number),
-                        static_cast<unsigned>(bdf.bus_number), static_cast<unsigned>(bdf.device_number),
-                        static_cast<unsigned>(bdf.function_number));
-          g.bdf = buf;
-        }
+        if (api_.get_bdf(h, &bdf) == AMDSMI_STATUS_SUCCESS) g.bdf = bdf_string(bdf);
       }
       if (api_.get_asic) {
         amdsmi_asic_info_t a{};
@@ -381,14 +587,87 @@ class AmdSmiBackend : public Backend {
       }
       if (api_.get_enum) {
         amdsmi_enumeration_info_t e{};
-        if (api_.get_enum(h, &e) == AMDSMI_STATUS_SUCCESS) g.hip_id = static_cast<int>(e.hip_id);
+        if (api_.get_enum(h, &e) == AMDSMI_STATUS_SUCCESS) {
+          g.hip_id = static_cast<int>(e.hip_id);
+          if (e.drm_render != 0xFFFFFFFFu && e.drm_render != 0) g.drm_render = static_cast<int>(e.drm_render);
+          if (e.drm_card != 0xFFFFFFFFu) g.drm_card = static_cast<int>(e.drm_card);
+        }
+      }
+      if (api_.bad_page_threshold) {
+        uint32_t thr = 0;
+        if (api_.bad_page_threshold(h, &thr) == AMDSMI_STATUS_SUCCESS && thr != 0xFFFFFFFFu) g.bad_page_threshold = thr;
+      }
+      g.phys_links = read_links(h);
+      // Peer links: one amdsmi topology query per ordered pair (8 GPUs: 56 pairs, once
+      // at discovery, never on the poll path).
+      for (size_t j = 0; j < handles_.size(); ++j) {
+        if (j == i) continue;
+        PeerLink l;
+        l.peer = static_cast<int>(j);
+        if (api_.topo_link_type) {
+          uint64_t hops = 0;
+          amdsmi_link_type_t type = AMDSMI_LINK_TYPE_UNKNOWN;
+          if (api_.topo_link_type(h, handles_[j], &hops, &type) == AMDSMI_STATUS_SUCCESS) {
+            l.hops = hops;
+            l.type = link_type_name(type);
+          }
+        }
+        if (l.type.empty()) l.type = "unknown";
+        if (api_.topo_link_weight) {
+          uint64_t w = 0;
+          if (api_.topo_link_weight(h, handles_[j], &w) == AMDSMI_STATUS_SUCCESS) l.weight = w;
+        }
+        if (api_.minmax_bw && l.type == "xgmi") {
+          uint64_t lo = 0, hi = 0;
+          if (api_.minmax_bw(h, handles_[j], &lo, &hi) == AMDSMI_STATUS_SUCCESS) {
+            l.min_bw_mbps = lo;
+            l.max_bw_mbps = hi;
+          }
+        }
+        g.links.push_back(std::move(l));
       }
       out.push_back(g);
     }
     return out;
   }
 
-  Telemetry sample(int index, bool full) override {
+  int busy_processes(int index) override {
+    if (index < 0 || static_cast<size_t>(index) >= handles_.size() || !api_.process_list) return -1;
+    // Processes other than this one (the agent's own diagnostics hold a HIP context).
+    std::vector<amdsmi_proc_info_t> procs(64);
+    uint32_t n = static_cast<uint32_t>(procs.size());
+    amdsmi_status_t st = api_.process_list(handles_[static_cast<size_t>(index)], &n, procs.data());
+    if (st != AMDSMI_STATUS_SUCCESS && st != AMDSMI_STATUS_OUT_OF_RESOURCES) return -1;
+    const uint32_t self = static_cast<uint32_t>(::getpid());
+    int others = 0;
+    for (uint32_t k = 0; k < n && k < procs.size(); ++k) others += procs[k].pid != self ? 1 : 0;
+    if (n > procs.size()) others += static_cast<int>(n - procs.size());
+    return others;
+  }
+
+  std::vector<PhysLink> read_links(amdsmi_processor_handle h) {
+    std::vector<PhysLink> out;
+    if (!api_.link_metrics) return out;
+    amdsmi_link_metrics_t lm;
+    std::memset(&lm, 0, sizeof(lm));
+    if (api_.link_metrics(h, &lm) != AMDSMI_STATUS_SUCCESS) return out;
+    const uint32_t n = std::min<uint32_t>(lm.num_links, AMDSMI_MAX_NUM_XGMI_PHYSICAL_LINK);
+    for (uint32_t k = 0; k < n; ++k) {
+      const auto& x = lm.links[k];
+      PhysLink l;
+      l.peer_bdf = x.bdf.as_uint == ~0ULL ? "" : bdf_string(x.bdf);  // all-ones: peer not reported
+      l.type = link_type_name(x.link_type);
+      l.bit_rate_gbps = x.bit_rate == 0xFFFFFFFFu ? 0 : x.bit_rate;
+      l.max_bandwidth_gbps = x.max_bandwidth == 0xFFFFFFFFu ? 0 : x.max_bandwidth;
+      l.read_kb = x.read == ~0ULL ? 0 : x.read;
+      l.write_kb = x.write == ~0ULL ? 0 : x.write;
+      out.push_back(std::move(l));
+    }
+    return out;
+  }
+
+  Telemetry sample(int index, SampleLevel level) override {
+    const bool full = level >= SampleLevel::Slow;
     Telemetry t;
     t.index = index;
     int64_t t0 = metrics::now_ns();
@@ -422,7 +701,28 @@ class AmdSmiBackend : public Backend {
     if (valid16(m.current_gfxclk)) t.gfxclk_mhz = m.current_gfxclk;
     else if (valid16(m.current_gfxclks[0])) t.gfxclk_mhz = m.current_gfxclks[0];
     if (valid16(m.current_uclk)) t.uclk_mhz = m.current_uclk;
-    t.throttle_status = m.indep_throttle_status != 0xFFFFFFFFFFFFFFFFULL ? m.indep_throttle_status : m.throttle_status;
+    // Both throttle words use all-ones as "not reported" (MI355X firmware leaves the
+    // 32-bit legacy word at 0xFFFFFFFF; round 1 exported that as if it were a state).
+    if (m.indep_throttle_status != ~0ULL) {
+      t.throttle_valid = true;
+      t.throttle_status = m.indep_throttle_status;
+    } else if (m.throttle_status != 0xFFFFFFFFu) {
+      t.throttle_valid = true;
+      t.throttle_status = m.throttle_status;
+    }
+    // Violation residency accumulators (the cheap path amdsmi_get_violation_status's own
+    // documentation points bare-metal callers to; that call blocks >= 100 ms per device).
+    if (m.accumulation_counter != ~0ULL && m.accumulation_counter != 0) {
+      t.acc_counter = m.accumulation_counter;
+      if (m.ppt_residency_acc != ~0ULL) t.acc_ppt = m.ppt_residency_acc;
+      uint64_t thermal = Telemetry::kNoAcc;
+      for (uint64_t a : {m.socket_thm_residency_acc, m.hbm_thm_residency_acc, m.vr_thm_residency_acc,
+                         m.prochot_residency_acc}) {
+        if (a == ~0ULL) continue;
+        thermal = thermal == Telemetry::kNoAcc ? a : std::max(thermal, a);
+      }
+      t.acc_thermal = thermal;
+    }
     int up = 0, total = 0;
     for (int l = 0; l < AMDSMI_MAX_NUM_XGMI_LINKS; ++l) {
       uint16_t s = m.xgmi_link_status[l];
@@ -446,13 +746,42 @@ class AmdSmiBackend : public Backend {
       if (api_.get_ecc(h, &e) == AMDSMI_STATUS_SUCCESS) {
         t.ecc_correctable = e.correctable_count;
         t.ecc_uncorrectable = e.uncorrectable_count;
+        t.ecc_deferred = e.deferred_count;
       }
     }
+    if (level == SampleLevel::Ras) sample_ras(h, t);
     t.poll_us = static_cast<double>(metrics::now_ns() - t0) / 1e3;
     return t;
   }
 
  private:
+  void sample_ras(amdsmi_processor_handle h, Telemetry& t) {
+    t.ras_ok = true;
+    if (api_.bad_pages) {
+      uint32_t n = 0;
+      if (api_.bad_pages(h, &n, nullptr) == AMDSMI_STATUS_SUCCESS && n > 0) {
+        std::vector<amdsmi_retired_page_record_t> recs(n);
+        if (api_.bad_pages(h, &n, recs.data()) == AMDSMI_STATUS_SUCCESS) {
+          for (uint32_t k = 0; k < n && k < recs.size(); ++k) {
+            if (recs[k].status == AMDSMI_MEM_PAGE_STATUS_UNRESERVABLE) ++t.unreservable_pages;
+            else ++t.retired_pages;
+          }
+        }
+      }
+    }
+    if (api_.ecc_count) {
+      uint64_t enabled = ~0ULL;
+      if (api_.ecc_enabled && api_.ecc_enabled(h, &enabled) != AMDSMI_STATUS_SUCCESS) enabled = ~0ULL;
+      for (const auto& b : kEccBlocks) {
+        if (!(enabled & static_cast<uint64_t>(b.block))) continue;
+        amdsmi_error_count_t e{};
+        if (api_.ecc_count(h, b.block, &e) != AMDSMI_STATUS_SUCCESS) continue;
+        t.ecc_blocks.push_back({b.name, e.correctable_count, e.uncorrectable_count, e.deferred_count});
+      }
+    }
+    t.links = read_links(h);
+  }
+
   AmdSmiApi api_;
   bool initialized_ = false;
   std::vector<amdsmi_processor_handle> handles_;

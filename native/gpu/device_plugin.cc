@@ -4,6 +4,7 @@
 #include <sys/stat.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <set>
 #include <stdexcept>
@@ -247,7 +248,149 @@ std::vector<std::vector<std::string>> decode_preferred_response(std::string_view
 
 }  // namespace dp
 
+// ------------------------------------------------------------------ pod resources
+// podresources/v1: ListPodResourcesResponse{1: repeated PodResources}
+// PodResources{1: name, 2: namespace, 3: repeated ContainerResources}
+// ContainerResources{1: name, 2: repeated ContainerDevices, ...}
+// ContainerDevices{1: resource_name, 2: repeated device_ids, 3: TopologyInfo}
+std::vector<PodDevices> decode_pod_resources(std::string_view buf) {
+  std::vector<PodDevices> out;
+  pb::Reader r(buf);
+  while (r.next()) {
+    if (r.field() != 1) continue;
+    std::string pod, ns;
+    std::vector<std::string_view> containers;
+    pb::Reader pr(r.bytes_value());
+    while (pr.next()) {
+      if (pr.field() == 1) pod = pr.string_value();
+      else if (pr.field() == 2) ns = pr.string_value();
+      else if (pr.field() == 3) containers.push_back(pr.bytes_value());
+    }
+    for (auto c : containers) {
+      std::string cname;
+      std::vector<std::string_view> devs;
+      pb::Reader cr(c);
+      while (cr.next()) {
+        if (cr.field() == 1) cname = cr.string_value();
+        else if (cr.field() == 2) devs.push_back(cr.bytes_value());
+      }
+      for (auto d : devs) {
+        PodDevices pd{pod, ns, cname, "", {}};
+        pb::Reader dr(d);
+        while (dr.next()) {
+          if (dr.field() == 1) pd.resource = dr.string_value();
+          else if (dr.field() == 2) pd.ids.push_back(dr.string_value());
+        }
+        out.push_back(std::move(pd));
+      }
+    }
+  }
+  return out;
+}
+
+std::string encode_pod_resources(const std::vector<PodDevices>& v) {
+  pb::Writer w;
+  for (const auto& p : v) {
+    pb::Writer d;
+    d.str(1, p.resource);
+    for (const auto& id : p.ids) d.bytes(2, id);
+    pb::Writer c;
+    c.str(1, p.container);
+    c.message(2, d);
+    pb::Writer pr;
+    pr.str(1, p.pod);
+    pr.str(2, p.ns);
+    pr.message(3, c);
+    w.message(1, pr);
+  }
+  return w.take();
+}
+
+std::set<std::string> allocated_device_ids(const std::string& socket, const std::string& resource_name) {
+  grpc::Channel ch(socket, 2000);
+  std::string resp;
+  grpc::Status st = ch.unary("/v1.PodResourcesLister/List", "", &resp, std::chrono::seconds(5));
+  if (!st.ok()) throw std::runtime_error("PodResourcesLister/List: " + st.message);
+  std::set<std::string> out;
+  for (const auto& p : decode_pod_resources(resp)) {
+    if (p.resource != resource_name) continue;
+    out.insert(p.ids.begin(), p.ids.end());
+  }
+  return out;
+}
+
 // ------------------------------------------------------------------ allocation policy
+namespace {
+
+// Direct-link score between two GPUs from the amdsmi link map: xGMI bandwidth (or a
+// nominal value when only the type is known), PCIe a distant second, 0 = no data.
+double link_score(const GpuInfo& a, int peer) {
+  for (const auto& l : a.links) {
+    if (l.peer != peer) continue;
+    if (l.type == "xgmi") return 1.0 + (l.hops <= 1 ? static_cast<double>(l.max_bw_mbps ? l.max_bw_mbps : 50000) : 0.0);
+    if (l.type == "pcie") return 0.5;
+    return 0.0;
+  }
+  return 0.0;
+}
+
+bool have_link_map(const std::vector<GpuInfo>& gpus, const std::vector<size_t>& cand) {
+  for (size_t i : cand)
+    if (gpus[i].links.empty()) return false;
+  return cand.size() > 1;
+}
+
+// Greedy max-bandwidth clique growth: start from `seed` (the must-include GPUs of this
+// hive), then repeatedly add the candidate with the highest summed link score to
+// everything chosen so far (with nothing chosen yet: to every candidate).  Ties — e.g.
+// a healthy full xGMI mesh — fall back to the NUMA rules of the no-link-map path:
+// NUMA node of the chosen set, then the NUMA group that best fits the request, then
+// xGMI node id and index.
+std::vector<size_t> pick_by_links(const std::vector<GpuInfo>& gpus, std::vector<size_t> cand,
+                                  const std::vector<size_t>& seed, int need) {
+  std::vector<size_t> chosen = seed, out;
+  std::map<int, int> numa_count;
+  for (size_t i : cand) numa_count[gpus[i].numa_node]++;
+  const int want = need;
+  auto score_to = [&](size_t i, const std::vector<size_t>& set) {
+    double sc = 0;
+    for (size_t j : set) sc += link_score(gpus[i], gpus[j].index);
+    return std::round(sc);
+  };
+  auto better = [&](size_t a, size_t b) {
+    const double sa = chosen.empty() ? score_to(a, cand) : score_to(a, chosen);
+    const double sb = chosen.empty() ? score_to(b, cand) : score_to(b, chosen);
+    if (sa != sb) return sa > sb;
+    const int na = gpus[a].numa_node, nb = gpus[b].numa_node;
+    if (na != nb) {
+      int aa = 0, ab = 0;
+      for (size_t j : chosen) {
+        aa += gpus[j].numa_node == na;
+        ab += gpus[j].numa_node == nb;
+      }
+      if (aa != ab) return aa > ab;
+      const bool fa = numa_count[na] >= want, fb = numa_count[nb] >= want;
+      if (fa != fb) return fa;
+      if (numa_count[na] != numa_count[nb]) return fa ? numa_count[na] < numa_count[nb] : numa_count[na] > numa_count[nb];
+      return na < nb;
+    }
+    if (gpus[a].xgmi_node_id != gpus[b].xgmi_node_id) return gpus[a].xgmi_node_id < gpus[b].xgmi_node_id;
+    return gpus[a].index < gpus[b].index;
+  };
+  while (need > 0 && !cand.empty()) {
+    size_t best = 0;
+    for (size_t k = 1; k < cand.size(); ++k)
+      if (better(cand[k], cand[best])) best = k;
+    chosen.push_back(cand[best]);
+    out.push_back(cand[best]);
+    cand.erase(cand.begin() + static_cast<std::ptrdiff_t>(best));
+    --need;
+  }
+  return out;
+}
+
+}  // namespace
+
 std::vector<std::string> preferred_allocation(const std::vector<GpuInfo>& gpus, const std::vector<std::string>& ids,
                                               const std::vector<std::string>& available,
                                               const std::vector<std::string>& must_include, int size) {
@@ -293,8 +436,24 @@ std::vector<std::string> preferred_allocation(const std::vector<GpuInfo>& gpus, 
     if (fits(a)) return by_hive[a].size() < by_hive[b].size();  // best fit keeps big islands whole
     return by_hive[a].size() > by_hive[b].size();      // else fewest hives: biggest first
   });
+  std::vector<size_t> must_idx;
+  for (const auto& id : out) {
+    auto it = pos.find(id);
+    if (it != pos.end()) must_idx.push_back(it->second);
+  }
   for (uint64_t h : hive_order) {
     auto& cand = by_hive[h];
+    if (have_link_map(gpus, cand)) {
+      std::vector<size_t> seed;
+      for (size_t i : must_idx)
+        if (gpus[i].xgmi_hive_id == h) seed.push_back(i);
+      for (size_t i : pick_by_links(gpus, cand, seed, need)) {
+        out.push_back(ids[i]);
+        --need;
+      }
+      if (need == 0) break;
+      continue;
+    }
     // Within a hive: prefer the NUMA node of the must-include set, else the NUMA group that
     // best fits what is still needed, then adjacent xGMI node ids.
     std::map<int, int> numa_count;
@@ -371,6 +530,7 @@ DevicePlugin::DevicePlugin(std::vector<GpuInfo> gpus, DevicePluginConfig cfg)
   std::map<std::string, int> seen;
   for (const auto& g : gpus_) seen[g.bdf]++;
   for (const auto& g : gpus_) {
+    shared_bdf_.push_back(!g.bdf.empty() && seen[g.bdf] > 1);
     if (g.bdf.empty()) ids_.push_back("gpu-" + std::to_string(g.index));
     else if (seen[g.bdf] > 1) ids_.push_back(g.bdf + "-p" + std::to_string(g.index));
     else ids_.push_back(g.bdf);
@@ -420,9 +580,23 @@ dp::ContainerAllocation DevicePlugin::allocate(const std::vector<std::string>& r
   for (const auto& id : req_ids) {
     auto it = std::find(ids_.begin(), ids_.end(), id);
     if (it == ids_.end()) throw std::invalid_argument("unknown " + cfg_.resource_name + " device id " + id);
-    const GpuInfo& g = gpus_[static_cast<size_t>(it - ids_.begin())];
+    const size_t gi = static_cast<size_t>(it - ids_.begin());
+    const GpuInfo& g = gpus_[gi];
     std::string card, render;
-    drm_nodes(cfg_.sysfs_root, g.bdf, &card, &render);
+    if (shared_bdf_[gi]) {
+      // A compute partition: the BDF's DRM nodes belong to partition 0, so only the
+      // minors amdsmi reported for this logical device are correct.
+      if (g.drm_render <= 0) {
+        throw std::invalid_argument(cfg_.resource_name + " device " + id +
+                                    " shares its PCI function with another partition and its render node is unknown");
+      }
+      render = "renderD" + std::to_string(g.drm_render);
+      if (g.drm_card >= 0) card = "card" + std::to_string(g.drm_card);
+    } else {
+      drm_nodes(cfg_.sysfs_root, g.bdf, &card, &render);
+      if (render.empty() && g.drm_render > 0) render = "renderD" + std::to_string(g.drm_render);
+      if (card.empty() && g.drm_card >= 0) card = "card" + std::to_string(g.drm_card);
+    }
     if (card.empty()) card = "card" + std::to_string(g.index);
     if (render.empty()) render = "renderD" + std::to_string(128 + g.index);
     c.devices.push_back({"/dev/dri/" + card, join_path(cfg_.dev_root, "dri/" + card), "rw"});

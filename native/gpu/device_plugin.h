@@ -16,8 +16,11 @@
 //   GetPreferredAllocation  xGMI-aware: an allocation of k GPUs is packed onto one
 //                 xGMI hive (best fit, so big islands stay whole for TP=8 jobs), then onto
 //                 one NUMA node, then by xGMI node id — RCCL rings then run over xGMI links.
-//   Allocate      /dev/kfd plus each GPU's /dev/dri/card* and renderD* (resolved through
-//                 sysfs from the BDF), and env/annotations naming the GPUs and their hive.
+//   Allocate      /dev/kfd plus each GPU's /dev/dri/card* and renderD*: the DRM minors
+//                 amdsmi reports per logical device (so each compute partition gets its
+//                 own render node), else resolved through sysfs from the BDF; ids that
+//                 share a BDF with no known minor are refused rather than handed the
+//                 parent's node.  Env/annotations name the GPUs and their hive.
 //
 // Transport: core/http2.h (h2c gRPC) + core/protobuf.h (wire format).
 #pragma once
@@ -28,6 +31,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <string>
 #include <string_view>
 #include <thread>
@@ -107,9 +111,23 @@ struct DevicePluginConfig {
   bool register_with_kubelet = true;
 };
 
+// Kubelet pod-resources API (k8s.io/kubelet/pkg/apis/podresources/v1,
+// PodResourcesLister/List): the device ids of `resource_name` currently assigned to
+// containers.  Throws on transport errors.
+std::set<std::string> allocated_device_ids(const std::string& socket, const std::string& resource_name);
+// Wire codecs for the List response (unit-tested against grpcio/protobuf).
+struct PodDevices {
+  std::string pod, ns, container, resource;
+  std::vector<std::string> ids;
+};
+std::vector<PodDevices> decode_pod_resources(std::string_view buf);
+std::string encode_pod_resources(const std::vector<PodDevices>& v);
+
 // Pure allocation policy (unit-tested): choose `size` ids from `available` (must include
-// `must_include`) preferring one xGMI hive (best fit), then one NUMA node, then adjacent
-// xGMI node ids.  `ids[i]` is the device id of gpus[i].
+// `must_include`) preferring one xGMI hive (best fit), then — when the amdsmi link map is
+// known (GpuInfo::links) — the set with the most direct xGMI bandwidth between its
+// members (greedy, seeded by must_include), else one NUMA node and adjacent xGMI node
+// ids.  `ids[i]` is the device id of gpus[i].
 std::vector<std::string> preferred_allocation(const std::vector<GpuInfo>& gpus, const std::vector<std::string>& ids,
                                               const std::vector<std::string>& available,
                                               const std::vector<std::string>& must_include, int size);
@@ -138,6 +156,7 @@ class DevicePlugin {
 
   std::vector<GpuInfo> gpus_;
   std::vector<std::string> ids_;
+  std::vector<bool> shared_bdf_;  // logical devices (partitions) sharing a PCI function
   DevicePluginConfig cfg_;
   mutable std::mutex mu_;
   std::condition_variable cv_;

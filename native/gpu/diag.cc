@@ -3,7 +3,12 @@
 #include <dlfcn.h>
 #include <unistd.h>
 
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <vector>
 #include <mutex>
 #include <stdexcept>
 
@@ -39,9 +44,11 @@ Diag::Diag(const std::string& path) : path_(path) {
   hbm_ = reinterpret_cast<int (*)(int, uint64_t, int, uint32_t, bgc_hbm_result*)>(dlsym(lib_, "bgc_diag_hbm"));
   mfma_ = reinterpret_cast<int (*)(int, int, int, uint32_t, bgc_mfma_result*)>(dlsym(lib_, "bgc_diag_mfma"));
   arch_ = reinterpret_cast<int (*)(int, char*, size_t)>(dlsym(lib_, "bgc_diag_device_arch"));
+  gemm_ = reinterpret_cast<int (*)(int, int, int, int, const uint16_t*, const uint16_t*, float*)>(
+      dlsym(lib_, "bgc_diag_gemm"));
   last_error_ = reinterpret_cast<const char* (*)()>(dlsym(lib_, "bgc_diag_last_error"));
   auto abi = reinterpret_cast<int (*)()>(dlsym(lib_, "bgc_diag_abi_version"));
-  if (!device_count_ || !hbm_ || !mfma_ || !arch_ || !last_error_ || !abi || abi() != BGC_DIAG_ABI_VERSION) {
+  if (!device_count_ || !hbm_ || !mfma_ || !arch_ || !gemm_ || !last_error_ || !abi || abi() != BGC_DIAG_ABI_VERSION) {
     throw std::runtime_error(path + " is not a compatible bgc diag library");
   }
 }
@@ -112,9 +119,136 @@ json::Value Diag::mfma(int device, int waves_per_cu, int throughput_iters, uint3
   v["bad_cu_keys"] = bad;
   v["tflops"] = r.tflops;
   v["throughput_ok"] = r.throughput_ok != 0;
+  json::Value xw = json::Value::array(), xus = json::Value::array();
+  for (int x = 0; x < 8; ++x) {
+    xw.push_back(r.xcc_waves[x]);
+    xus.push_back(r.xcc_wave_us[x]);
+  }
+  v["xcc_waves"] = xw;
+  v["xcc_wave_us"] = xus;
+  v["xcc_balance"] = r.xcc_balance;
   v["elapsed_ms"] = r.elapsed_ms;
   v["passed"] = r.mismatches == 0 && r.throughput_ok != 0;
   return v;
+}
+
+void Diag::gemm(int device, int m, int n, int k, const uint16_t* a, const uint16_t* b, float* c) {
+  if (gemm_(device, m, n, k, a, b, c) != 0) throw std::runtime_error(std::string("gemm diag: ") + last_error_());
+}
+
+namespace {
+
+uint32_t mix(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+
+// bf16 bit pattern of a pseudo-random value in [-1, 1] (round-to-nearest-even), and the
+// exact float it encodes.
+uint16_t rand_bf16(uint32_t seed, uint32_t i, float* exact) {
+  float f = static_cast<float>(mix(seed ^ mix(i * 0x9e3779b9U))) / 4294967295.0f * 2.0f - 1.0f;
+  uint32_t bits;
+  std::memcpy(&bits, &f, 4);
+  bits += 0x7fff + ((bits >> 16) & 1);
+  uint16_t h = static_cast<uint16_t>(bits >> 16);
+  uint32_t back = static_cast<uint32_t>(h) << 16;
+  std::memcpy(exact, &back, 4);
+  return h;
+}
+
+}  // namespace
+
+json::Value Diag::gemm_check(int device, int m, int n, int k, uint32_t seed) {
+  std::vector<uint16_t> a(static_cast<size_t>(m) * k), b(static_cast<size_t>(k) * n);
+  std::vector<float> af(a.size()), bf(b.size()), c(static_cast<size_t>(m) * n);
+  for (size_t i = 0; i < a.size(); ++i) a[i] = rand_bf16(seed, static_cast<uint32_t>(i), &af[i]);
+  for (size_t i = 0; i < b.size(); ++i) b[i] = rand_bf16(seed ^ 0xB0B0B0B0U, static_cast<uint32_t>(i), &bf[i]);
+  gemm(device, m, n, k, a.data(), b.data(), c.data());
+  // fp32 MFMA accumulation of exact bf16 products: |err| <= K * 2^-24 * sum|a||b| (plus
+  // slack); measured against a double-precision host product.
+  double max_err = 0, max_ratio = 0;
+  uint64_t bad = 0;
+  for (int i = 0; i < m; ++i) {
+    for (int j = 0; j < n; ++j) {
+      double ref = 0, mag = 0;
+      for (int kk = 0; kk < k; ++kk) {
+        const double p = static_cast<double>(af[static_cast<size_t>(i) * k + kk]) * bf[static_cast<size_t>(kk) * n + j];
+        ref += p;
+        mag += std::fabs(p);
+      }
+      const double err = std::fabs(static_cast<double>(c[static_cast<size_t>(i) * n + j]) - ref);
+      const double bound = 4.0 * k * 5.96e-8 * mag + 1e-6;
+      max_err = std::max(max_err, err);
+      max_ratio = std::max(max_ratio, err / bound);
+      if (err > bound || !std::isfinite(c[static_cast<size_t>(i) * n + j])) ++bad;
+    }
+  }
+  return json::Value::object({{"m", m}, {"n", n}, {"k", k}, {"max_abs_err", max_err},
+                              {"max_err_over_bound", max_ratio}, {"bad_elements", static_cast<unsigned long long>(bad)},
+                              {"passed", bad == 0}});
+}
+
+DiagFloors DiagFloors::mi355x_defaults() {
+  DiagFloors f;
+  // MI355X, ROCm 7.2, 1 GiB buffers / 16 waves per CU x 2048 MFMA iterations
+  // (profiles/diag_floors_r2.json): read 6.33-6.57 TB/s, copy 5.36-5.42, write 5.11-5.25,
+  // MFMA bf16 1.92-2.06 PF/s, XCC balance 0.96.  At 256 MiB (Infinity-Cache-sized, the
+  // smallest sensible buffer) read is still 5.56 TB/s, so these floors hold down to it.
+  f.min_read_gbps = 4750;
+  f.min_copy_gbps = 4000;
+  f.min_write_gbps = 3800;
+  f.min_mfma_tflops = 1500;
+  f.min_xcc_balance = 0.85;
+  f.min_xccs = 8;
+  return f;
+}
+
+json::Value judge_diag(const json::Value& result, const DiagFloors& fl) {
+  json::Value out = result;
+  json::Value failures = json::Value::array();
+  auto num = [](const json::Value& v, const char* k) { return v.get(k).is_number() ? v.get(k).as_double() : 0.0; };
+  auto floor_check = [&](const json::Value& v, const char* key, double floor, const char* what) {
+    if (floor <= 0) return;
+    const double got = num(v, key);
+    if (got < floor) {
+      char buf[160];
+      std::snprintf(buf, sizeof(buf), "%s %.0f below floor %.0f", what, got, floor);
+      failures.push_back(std::string(buf));
+    }
+  };
+  const json::Value& hbm = result.get("hbm");
+  if (hbm.is_object()) {
+    if (num(hbm, "mismatches") > 0) failures.push_back("HBM pattern mismatches: " + std::to_string(static_cast<uint64_t>(num(hbm, "mismatches"))));
+    floor_check(hbm, "read_gbps", fl.min_read_gbps, "HBM read GB/s");
+    floor_check(hbm, "copy_gbps", fl.min_copy_gbps, "HBM copy GB/s");
+    floor_check(hbm, "write_gbps", fl.min_write_gbps, "HBM write GB/s");
+  }
+  const json::Value& mf = result.get("mfma");
+  if (mf.is_object()) {
+    if (num(mf, "mismatches") > 0) failures.push_back("MFMA tile mismatches on " + std::to_string(static_cast<int>(num(mf, "bad_cus"))) + " CU(s)");
+    if (mf.get("throughput_ok").is_bool() && !mf.get("throughput_ok").as_bool()) failures.push_back("MFMA throughput accumulators wrong");
+    floor_check(mf, "tflops", fl.min_mfma_tflops, "MFMA bf16 TFLOP/s");
+    if (fl.min_xcc_balance > 0 && num(mf, "xcc_balance") < fl.min_xcc_balance) {
+      char buf[160];
+      std::snprintf(buf, sizeof(buf), "XCC balance %.2f below floor %.2f", num(mf, "xcc_balance"), fl.min_xcc_balance);
+      failures.push_back(std::string(buf));
+    }
+    if (fl.min_xccs > 0 && num(mf, "xccs_seen") < fl.min_xccs) {
+      failures.push_back("only " + std::to_string(static_cast<int>(num(mf, "xccs_seen"))) + " XCCs ran MFMA work");
+    }
+  }
+  const json::Value& gm = result.get("gemm");
+  if (gm.is_object() && gm.get("passed").is_bool() && !gm.get("passed").as_bool()) {
+    failures.push_back("MFMA GEMM differs from the host fp32 product");
+  }
+  if (result.get("error").is_string()) failures.push_back(result.get_string("error"));
+  out["failures"] = failures;
+  out["passed"] = failures.items().empty();
+  return out;
 }
 
 }  // namespace bgc::gpu

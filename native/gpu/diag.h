@@ -1,12 +1,31 @@
 // Loader for libbgc_gpu_diag.so (HIP/CDNA4 health kernels, native/gpu/hip/).
 #pragma once
 
+#include <cstdint>
 #include <string>
 
 #include "core/json.h"
 #include "gpu/hip/gpu_diag.h"
 
 namespace bgc::gpu {
+
+// Performance floors that turn the diagnostics into a health gate: a GPU whose HBM or
+// matrix cores run well below what an MI355X delivers is not advertised, even when every
+// pattern and tile checks out.  Defaults sit ~25 % under the rates measured on MI355X at
+// the node agent's default sizes (profiles/diag_floors_r2.json); 0 disables a floor.
+struct DiagFloors {
+  double min_read_gbps = 0;
+  double min_copy_gbps = 0;
+  double min_write_gbps = 0;
+  double min_mfma_tflops = 0;
+  double min_xcc_balance = 0;  // slowest XCC mean wave time / fastest, inverted (0..1]
+  int min_xccs = 0;            // XCCs that must have run MFMA work
+  static DiagFloors mi355x_defaults();
+};
+
+// Pure verdict over one GPU's results ({"hbm":…, "mfma":…, "gemm":…}): adds "passed" and
+// "failures" (one string per violated check) to a copy of `result`.
+json::Value judge_diag(const json::Value& result, const DiagFloors& floors);
 
 class Diag {
  public:
@@ -17,6 +36,11 @@ class Diag {
   std::string device_arch(int device);
   json::Value hbm(int device, uint64_t bytes, int iters, uint32_t seed);
   json::Value mfma(int device, int waves_per_cu, int throughput_iters, uint32_t seed);
+  // MFMA GEMM on the device vs a host fp32 product of the same bf16 operands
+  // (deterministic pseudo-random values in [-1, 1]).  Returns max error and the bound.
+  json::Value gemm_check(int device, int m, int n, int k, uint32_t seed);
+  // Raw GEMM: A/B as bf16 bit patterns, C fp32 (row-major).
+  void gemm(int device, int m, int n, int k, const uint16_t* a, const uint16_t* b, float* c);
   const std::string& path() const { return path_; }
 
  private:
@@ -27,6 +51,7 @@ class Diag {
   int (*hbm_)(int, uint64_t, int, uint32_t, bgc_hbm_result*) = nullptr;
   int (*mfma_)(int, int, int, uint32_t, bgc_mfma_result*) = nullptr;
   int (*arch_)(int, char*, size_t) = nullptr;
+  int (*gemm_)(int, int, int, int, const uint16_t*, const uint16_t*, float*) = nullptr;
   const char* (*last_error_)() = nullptr;
 };
 

@@ -15,7 +15,7 @@
 extern "C" {
 #endif
 
-#define BGC_DIAG_ABI_VERSION 1
+#define BGC_DIAG_ABI_VERSION 2
 #define BGC_DIAG_MAX_CU_KEYS 2048
 
 typedef struct {
@@ -39,6 +39,9 @@ typedef struct {
   int throughput_ok;        // throughput phase accumulators matched exactly
   double elapsed_ms;
   int bad_cu_keys[64];      // first bad CU keys (xcc<<8 | se<<5 | sh<<4 | cu)
+  int xcc_waves[8];         // throughput-phase waves that ran on each XCC
+  double xcc_wave_us[8];    // their mean duration (constant 100 MHz clock)
+  double xcc_balance;       // fastest / slowest XCC mean wave time (1.0 = balanced)
 } bgc_mfma_result;
 
 int bgc_diag_abi_version(void);
@@ -46,6 +49,9 @@ int bgc_diag_device_count(void);
 // Returns 0 on success, non-zero on HIP error (message via bgc_diag_last_error()).
 int bgc_diag_hbm(int device, uint64_t bytes, int iters, uint32_t seed, bgc_hbm_result* out);
 int bgc_diag_mfma(int device, int waves_per_cu, int throughput_iters, uint32_t seed, bgc_mfma_result* out);
+// C[m,n] (fp32) = A[m,k] * B[k,n], A/B bf16 bit patterns, row-major, via MFMA; the host
+// compares C with its own fp32 product (m, n multiples of 16; k a multiple of 32).
+int bgc_diag_gemm(int device, int m, int n, int k, const uint16_t* a_bf16, const uint16_t* b_bf16, float* c);
 // Device name / gfx arch string, e.g. "gfx950".
 int bgc_diag_device_arch(int device, char* buf, size_t len);
 const char* bgc_diag_last_error(void);

@@ -180,7 +180,13 @@ __global__ __launch_bounds__(kBlock) void mfma_check(uint32_t seed, int rounds, 
   }
 }
 
-__global__ __launch_bounds__(kBlock) void mfma_throughput(uint32_t seed, int iters, unsigned* __restrict__ fails) {
+// Each wave also times itself on the 100 MHz constant clock and adds its duration to
+// its XCC's bin, so a slow (throttled / degraded) XCC shows up as an imbalance even when
+// the whole-chip rate still clears its floor.
+__global__ __launch_bounds__(kBlock) void mfma_throughput(uint32_t seed, int iters, unsigned* __restrict__ fails,
+                                                          unsigned long long* __restrict__ xcc_ticks,
+                                                          unsigned* __restrict__ xcc_waves) {
+  const uint64_t t_start = wall_clock64();
   const int lane = threadIdx.x & 63;
   const uint32_t tile = (blockIdx.x * (kBlock / 64)) + (threadIdx.x >> 6);
   const int row = lane & 15;
@@ -211,7 +217,38 @@ __global__ __launch_bounds__(kBlock) void mfma_throughput(uint32_t seed, int ite
     for (int c = 0; c < 4; ++c) bad += (acc[c][i] != e + float(c));
   }
   for (int off = 32; off > 0; off >>= 1) bad += __shfl_down(bad, off, 64);
-  if (lane == 0 && bad) atomicAdd(fails, bad);
+  const uint64_t t_end = wall_clock64();  // after the accumulators were consumed above
+  if (lane == 0) {
+    if (bad) atomicAdd(fails, bad);
+    const uint32_t xcc = (cu_key() >> 8) & 7;
+    atomicAdd(&xcc_ticks[xcc], static_cast<unsigned long long>(t_end - t_start));
+    atomicAdd(&xcc_waves[xcc], 1u);
+  }
+}
+
+// Plain MFMA GEMM for the host cross-check: C[M,N] (fp32) = A[M,K] * B[K,N] (bf16,
+// row-major).  One wave per 16x16 output tile, K consumed 32 at a time by
+// v_mfma_f32_16x16x32_bf16 with the same operand layout as the tests above: lane l
+// holds A row (l & 15) / B column (l & 15), k = 8 * (l >> 4) + j; the result lane l
+// holds column (l & 15), rows 4 * (l >> 4) + i.
+__global__ __launch_bounds__(64) void mfma_gemm(const __bf16* __restrict__ A, const __bf16* __restrict__ B,
+                                                float* __restrict__ C, int M, int N, int K) {
+  const int lane = threadIdx.x;
+  const int tm = blockIdx.y * 16, tn = blockIdx.x * 16;
+  const int rc = lane & 15, kb = 8 * (lane >> 4);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < K; k0 += 32) {
+    bf16x8 a, b;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      a[j] = A[static_cast<size_t>(tm + rc) * K + k0 + kb + j];
+      b[j] = B[static_cast<size_t>(k0 + kb + j) * N + tn + rc];
+    }
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) C[static_cast<size_t>(tm + 4 * (lane >> 4) + i) * N + tn + rc] = acc[i];
+  (void)M;
 }
 
 #define HIP_TRY(expr)                                                                   \
@@ -341,10 +378,12 @@ int bgc_diag_mfma(int device, int waves_per_cu, int throughput_iters, uint32_t s
   const int cus = cu_count(device);
   const int blocks = std::max(1, cus * waves_per_cu / (kBlock / 64));
   const int rounds = 8;
-  DeviceBuffer tiles, bad, fails;
+  DeviceBuffer tiles, bad, fails, xticks, xwaves;
   HIP_TRY(hipMalloc(&tiles.p, BGC_DIAG_MAX_CU_KEYS * sizeof(unsigned)));
   HIP_TRY(hipMalloc(&bad.p, BGC_DIAG_MAX_CU_KEYS * sizeof(unsigned)));
   HIP_TRY(hipMalloc(&fails.p, sizeof(unsigned)));
+  HIP_TRY(hipMalloc(&xticks.p, 8 * sizeof(unsigned long long)));
+  HIP_TRY(hipMalloc(&xwaves.p, 8 * sizeof(unsigned)));
   HIP_TRY(hipMemset(tiles.p, 0, BGC_DIAG_MAX_CU_KEYS * sizeof(unsigned)));
   HIP_TRY(hipMemset(bad.p, 0, BGC_DIAG_MAX_CU_KEYS * sizeof(unsigned)));
   HIP_TRY(hipMemset(fails.p, 0, sizeof(unsigned)));
@@ -360,11 +399,16 @@ int bgc_diag_mfma(int device, int waves_per_cu, int throughput_iters, uint32_t s
   HIP_TRY(hipEventSynchronize(ev.b));
   HIP_TRY(hipEventElapsedTime(&ms_check, ev.a, ev.b));
   // warm-up then timed throughput pass
-  hipLaunchKernelGGL(mfma_throughput, dim3(blocks), dim3(kBlock), 0, nullptr, seed, 64, static_cast<unsigned*>(fails.p));
+  auto* xt = static_cast<unsigned long long*>(xticks.p);
+  auto* xw = static_cast<unsigned*>(xwaves.p);
+  hipLaunchKernelGGL(mfma_throughput, dim3(blocks), dim3(kBlock), 0, nullptr, seed, 64, static_cast<unsigned*>(fails.p),
+                     xt, xw);
   HIP_TRY(hipMemset(fails.p, 0, sizeof(unsigned)));
+  HIP_TRY(hipMemset(xticks.p, 0, 8 * sizeof(unsigned long long)));
+  HIP_TRY(hipMemset(xwaves.p, 0, 8 * sizeof(unsigned)));
   HIP_TRY(hipEventRecord(ev.a, nullptr));
   hipLaunchKernelGGL(mfma_throughput, dim3(blocks), dim3(kBlock), 0, nullptr, seed, throughput_iters,
-                     static_cast<unsigned*>(fails.p));
+                     static_cast<unsigned*>(fails.p), xt, xw);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(ev.b, nullptr));
   HIP_TRY(hipEventSynchronize(ev.b));
@@ -374,6 +418,23 @@ int bgc_diag_mfma(int device, int waves_per_cu, int throughput_iters, uint32_t s
   HIP_TRY(hipMemcpy(h_tiles.data(), tiles.p, h_tiles.size() * sizeof(unsigned), hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(h_bad.data(), bad.p, h_bad.size() * sizeof(unsigned), hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(&h_fails, fails.p, sizeof(unsigned), hipMemcpyDeviceToHost));
+  unsigned long long h_ticks[8];
+  unsigned h_waves[8];
+  HIP_TRY(hipMemcpy(h_ticks, xticks.p, sizeof(h_ticks), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(h_waves, xwaves.p, sizeof(h_waves), hipMemcpyDeviceToHost));
+  int rate_khz = 0;
+  if (hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || rate_khz <= 0) {
+    rate_khz = 100000;  // CDNA constant clock: 100 MHz
+  }
+  double lo = 0, hi = 0;
+  for (int x = 0; x < 8; ++x) {
+    out->xcc_waves[x] = static_cast<int>(h_waves[x]);
+    out->xcc_wave_us[x] = h_waves[x] ? static_cast<double>(h_ticks[x]) / h_waves[x] / (rate_khz * 1e-3) : 0.0;
+    if (!h_waves[x]) continue;
+    lo = lo == 0 ? out->xcc_wave_us[x] : std::min(lo, out->xcc_wave_us[x]);
+    hi = std::max(hi, out->xcc_wave_us[x]);
+  }
+  out->xcc_balance = hi > 0 ? lo / hi : 0.0;
   bool xcc_seen[8] = {false};
   for (int k = 0; k < BGC_DIAG_MAX_CU_KEYS; ++k) {
     if (!h_tiles[static_cast<size_t>(k)]) continue;
@@ -392,6 +453,28 @@ int bgc_diag_mfma(int device, int waves_per_cu, int throughput_iters, uint32_t s
   out->tflops = flops / (ms_tp * 1e-3) / 1e12;
   out->throughput_ok = h_fails == 0;
   out->elapsed_ms = ms_check + ms_tp;
+  return 0;
+}
+
+int bgc_diag_gemm(int device, int m, int n, int k, const uint16_t* a_bf16, const uint16_t* b_bf16, float* c) {
+  if (!a_bf16 || !b_bf16 || !c || m <= 0 || n <= 0 || k <= 0 || m % 16 || n % 16 || k % 32 || m > 4096 ||
+      n > 4096 || k > 8192) {
+    g_last_error = "invalid arguments (M, N multiples of 16 up to 4096; K a multiple of 32 up to 8192)";
+    return 1;
+  }
+  HIP_TRY(hipSetDevice(device));
+  const size_t a_bytes = static_cast<size_t>(m) * k * 2, b_bytes = static_cast<size_t>(k) * n * 2;
+  const size_t c_bytes = static_cast<size_t>(m) * n * 4;
+  DeviceBuffer da, db, dc;
+  HIP_TRY(hipMalloc(&da.p, a_bytes));
+  HIP_TRY(hipMalloc(&db.p, b_bytes));
+  HIP_TRY(hipMalloc(&dc.p, c_bytes));
+  HIP_TRY(hipMemcpy(da.p, a_bf16, a_bytes, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(db.p, b_bf16, b_bytes, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(mfma_gemm, dim3(n / 16, m / 16), dim3(64), 0, nullptr, static_cast<const __bf16*>(da.p),
+                     static_cast<const __bf16*>(db.p), static_cast<float*>(dc.p), m, n, k);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpy(c, dc.p, c_bytes, hipMemcpyDeviceToHost));
   return 0;
 }
 

@@ -5,7 +5,10 @@
 #include <cstdio>
 #include <set>
 
+#include <unistd.h>
+
 #include "core/log.h"
+#include "core/metrics.h"
 #include "gpu/diag.h"
 #include "kube/leader.h"
 #include "kube/runtime.h"
@@ -30,6 +33,28 @@ NodeAgentConfig NodeAgentConfig::from_env(const EnvConfig& env) {
   c.max_gpus = static_cast<int>(env.u64_or("max_gpus", 0));
   c.run_diag = env.boolean_or("run_diag", false);
   c.diag_hbm_bytes = env.u64_or("diag_hbm_bytes", 1ULL << 30);
+  c.diag_interval_secs = env.u64_or("diag_interval_secs", 0);
+  c.diag_floors.min_read_gbps = env.f64_or("diag_min_read_gbps", c.diag_floors.min_read_gbps);
+  c.diag_floors.min_copy_gbps = env.f64_or("diag_min_copy_gbps", c.diag_floors.min_copy_gbps);
+  c.diag_floors.min_write_gbps = env.f64_or("diag_min_write_gbps", c.diag_floors.min_write_gbps);
+  c.diag_floors.min_mfma_tflops = env.f64_or("diag_min_mfma_tflops", c.diag_floors.min_mfma_tflops);
+  c.diag_floors.min_xcc_balance = env.f64_or("diag_min_xcc_balance", c.diag_floors.min_xcc_balance);
+  c.diag_floors.min_xccs = static_cast<int>(env.u64_or("diag_min_xccs", static_cast<uint64_t>(c.diag_floors.min_xccs)));
+  c.pod_resources_socket = env.str_or("pod_resources_socket", c.pod_resources_socket);
+  HealthPolicy& h = c.health;
+  h.max_hotspot_c = env.f64_or("max_hotspot_c", h.max_hotspot_c);
+  h.max_mem_c = env.f64_or("max_mem_c", h.max_mem_c);
+  h.max_new_uncorrectable = env.u64_or("max_new_uncorrectable", h.max_new_uncorrectable);
+  h.max_uncorrectable_at_start = env.u64_or("max_uncorrectable_at_start", h.max_uncorrectable_at_start);
+  h.require_all_xgmi_links = env.boolean_or("require_all_xgmi_links", h.require_all_xgmi_links);
+  h.max_retired_pages = env.u64_or("max_retired_pages", h.max_retired_pages);
+  h.max_thermal_violation_pct = env.f64_or("max_thermal_violation_pct", h.max_thermal_violation_pct);
+  h.max_ppt_violation_pct = env.f64_or("max_ppt_violation_pct", h.max_ppt_violation_pct);
+  h.violation_sustain_polls = static_cast<int>(env.u64_or("violation_sustain_polls", static_cast<uint64_t>(h.violation_sustain_polls)));
+  h.fail_threshold = static_cast<int>(env.u64_or("fail_threshold", static_cast<uint64_t>(h.fail_threshold)));
+  h.recover_threshold = static_cast<int>(env.u64_or("recover_threshold", static_cast<uint64_t>(h.recover_threshold)));
+  c.slow_every = static_cast<int>(env.u64_or("slow_every", static_cast<uint64_t>(c.slow_every)));
+  c.ras_every = static_cast<int>(env.u64_or("ras_every", static_cast<uint64_t>(c.ras_every)));
   c.create_node = env.boolean_or("create_node", false);
   c.device_plugin = env.boolean_or("device_plugin", false);
   c.device_plugin_dir = env.str_or("device_plugin_dir", c.device_plugin_dir);
@@ -111,8 +136,17 @@ Value node_labels_patch(const NodeAgentConfig& cfg, const std::vector<GpuInfo>& 
   labels[p + ".diag"] = !diag.ran ? "skipped" : diag.passed ? "passed" : "failed";
   Value topo = Value::array();
   for (const auto& g : gpus) {
+    Value links = Value::array();
+    for (const auto& l : g.links) {
+      links.push_back(Value::object({{"peer", l.peer}, {"type", l.type}, {"hops", static_cast<unsigned long long>(l.hops)},
+                                     {"weight", static_cast<unsigned long long>(l.weight)},
+                                     {"bw_mbps", static_cast<unsigned long long>(l.max_bw_mbps)}}));
+    }
+    int xgmi_up = 0;
+    for (const auto& l : g.phys_links) xgmi_up += (l.type == "xgmi" && l.bit_rate_gbps > 0) ? 1 : 0;
     topo.push_back(Value::object({{"index", g.index}, {"uuid", g.uuid}, {"bdf", g.bdf}, {"hive", hex16(g.xgmi_hive_id)},
-                                  {"node", static_cast<unsigned long long>(g.xgmi_node_id)}, {"numa", g.numa_node}}));
+                                  {"node", static_cast<unsigned long long>(g.xgmi_node_id)}, {"numa", g.numa_node},
+                                  {"render", g.drm_render}, {"xgmi_links_up", xgmi_up}, {"links", links}}));
   }
   Value meta = Value::object({{"name", cfg.node_name}, {"labels", labels},
                               {"annotations", Value::object({{p + ".topology", topo.dump()}})}});
@@ -155,24 +189,15 @@ void NodeAgent::init() {
   LOG_INFO("node_agent") << "discovered " << gpus_.size() << " GPU(s) via " << backend_->name() << ": "
                          << gpus_.front().market_name << " " << gpus_.front().gfx_target << " "
                          << gpus_.front().vram_total_mb << " MB";
-  if (cfg_.run_diag) {
-    diag_.ran = true;
-    Diag& d = Diag::instance();
-    for (const auto& g : gpus_) {
-      int dev = g.hip_id >= 0 ? g.hip_id : g.index;
-      Value hbm = d.hbm(dev, cfg_.diag_hbm_bytes, 2, 0x5eed + static_cast<uint32_t>(dev));
-      Value mfma = d.mfma(dev, 16, 2048, 0x5eed + static_cast<uint32_t>(dev));
-      bool ok = hbm.get("passed").as_bool() && mfma.get("passed").as_bool();
-      diag_.passed = diag_.passed && ok;
-      diag_.per_gpu.push_back(Value::object({{"index", g.index}, {"hbm", hbm}, {"mfma", mfma}, {"passed", ok}}));
-      LOG_INFO("node_agent") << "diag gpu " << g.index << ": " << (ok ? "passed" : "FAILED") << " read "
-                             << hbm.get("read_gbps").as_double() << " GB/s, mfma " << mfma.get("tflops").as_double()
-                             << " TFLOP/s";
-    }
-  }
+  if (cfg_.run_diag) run_diagnostics(true);
   std::vector<int> idx;
-  for (const auto& g : gpus_) idx.push_back(g.index);
-  poller_ = std::make_unique<TelemetryPoller>(*backend_, idx, std::chrono::milliseconds(cfg_.poll_interval_ms));
+  std::vector<uint64_t> page_limits;
+  for (const auto& g : gpus_) {
+    idx.push_back(g.index);
+    page_limits.push_back(g.bad_page_threshold);
+  }
+  poller_ = std::make_unique<TelemetryPoller>(*backend_, idx, std::chrono::milliseconds(cfg_.poll_interval_ms),
+                                              cfg_.health, cfg_.slow_every, cfg_.ras_every, page_limits);
   poller_->poll_once();
   bool exists = client_.get_opt(types::Node, "", cfg_.node_name).has_value();
   if (cfg_.create_node && !exists) {
@@ -195,18 +220,125 @@ bool NodeAgent::node_up_to_date(const Value& node) const {
          st.get("allocatable").get_string(cfg_.resource_name) == std::to_string(healthy);
 }
 
+static bool diag_failed(const DiagOutcome& d, size_t i) {
+  if (!d.ran || i >= d.per_gpu.items().size()) return false;
+  const Value& r = d.per_gpu.items()[i];
+  return r.is_object() && r.get("passed").is_bool() && !r.get("passed").as_bool();
+}
+
 std::vector<bool> NodeAgent::healthy_flags() const {
   auto snap = poller_ ? poller_->snapshot() : nullptr;
+  std::lock_guard<std::mutex> lk(diag_mu_);
   std::vector<bool> out(gpus_.size(), true);
   for (size_t i = 0; i < gpus_.size(); ++i) {
     if (snap && i < snap->health.size() && !snap->health[i].healthy) out[i] = false;
-    if (diag_.ran && i < diag_.per_gpu.size() && !diag_.per_gpu[i].get("passed").as_bool()) out[i] = false;
+    if (diag_failed(diag_, i)) out[i] = false;
   }
   return out;
 }
 
+DiagOutcome NodeAgent::diag_outcome() const {
+  std::lock_guard<std::mutex> lk(diag_mu_);
+  return diag_;
+}
+
+Value NodeAgent::diagnose(const GpuInfo& g) const {
+  const int dev = g.hip_id >= 0 ? g.hip_id : g.index;
+  const uint32_t seed = 0x5eed + static_cast<uint32_t>(dev);
+  Value r = Value::object({{"index", g.index}});
+  try {
+    Diag& d = Diag::instance();
+    r["hbm"] = d.hbm(dev, cfg_.diag_hbm_bytes, 2, seed);
+    r["mfma"] = d.mfma(dev, 16, 2048, seed);
+    r["gemm"] = d.gemm_check(dev, 64, 64, 512, seed);
+  } catch (const std::exception& e) {
+    r["error"] = std::string(e.what());
+  }
+  return judge_diag(r, cfg_.diag_floors);
+}
+
+std::vector<bool> NodeAgent::in_use() const {
+  std::vector<bool> out(gpus_.size(), false);
+  std::set<std::string> held;
+  bool pod_api = false;
+  if (!cfg_.pod_resources_socket.empty() && ::access(cfg_.pod_resources_socket.c_str(), F_OK) == 0) {
+    try {
+      held = allocated_device_ids(cfg_.pod_resources_socket, cfg_.resource_name);
+      pod_api = true;
+    } catch (const std::exception& e) {
+      LOG_WARN("node_agent") << "pod-resources List failed: " << e.what() << "; falling back to amdsmi process lists";
+    }
+  }
+  const std::vector<std::string> ids = plugin_ ? plugin_->ids() : std::vector<std::string>{};
+  for (size_t i = 0; i < gpus_.size(); ++i) {
+    if (pod_api && i < ids.size() && held.count(ids[i])) out[i] = true;
+    if (backend_->busy_processes(gpus_[i].index) > 0) out[i] = true;
+  }
+  return out;
+}
+
+bool NodeAgent::run_diagnostics(bool force) {
+  const std::vector<bool> busy = force ? std::vector<bool>(gpus_.size(), false) : in_use();
+  DiagOutcome prev = diag_outcome();
+  std::vector<Value> results(gpus_.size());
+  uint64_t skipped = 0;
+  for (size_t i = 0; i < gpus_.size(); ++i) {
+    if (busy[i]) {
+      ++skipped;
+      if (i < prev.per_gpu.items().size()) results[i] = prev.per_gpu.items()[i];
+      LOG_INFO("node_agent") << "diag gpu " << gpus_[i].index << ": skipped (in use)";
+      continue;
+    }
+    results[i] = diagnose(gpus_[i]);
+    const Value& r = results[i];
+    auto get = [&](const char* sect, const char* k) {
+      const Value& v = r.get(sect).get(k);
+      return v.is_number() ? v.as_double() : 0.0;
+    };
+    if (r.get("passed").as_bool()) {
+      LOG_INFO("node_agent") << "diag gpu " << gpus_[i].index << ": passed, read " << get("hbm", "read_gbps")
+                             << " GB/s, copy " << get("hbm", "copy_gbps") << " GB/s, mfma " << get("mfma", "tflops")
+                             << " TFLOP/s, xcc balance " << get("mfma", "xcc_balance");
+    } else {
+      LOG_WARN("node_agent") << "diag gpu " << gpus_[i].index << ": FAILED " << r.get("failures").dump();
+    }
+  }
+  bool changed = false;
+  {
+    std::lock_guard<std::mutex> lk(diag_mu_);
+    Value per = Value::array();
+    bool passed = true;
+    for (size_t i = 0; i < gpus_.size(); ++i) {
+      const bool was_bad = diag_failed(diag_, i);
+      per.push_back(results[i]);
+      const bool bad = results[i].is_object() && !results[i].get("passed").as_bool();
+      changed = changed || (was_bad != bad);
+      passed = passed && !bad;
+    }
+    diag_.ran = true;
+    diag_.passed = passed;
+    diag_.per_gpu = per;
+    diag_.runs++;
+    diag_.skipped_in_use += skipped;
+  }
+  auto& reg = metrics::Registry::global();
+  reg.counter("bgc_gpu_diag_runs_total", "Diagnostics passes").inc();
+  if (skipped) reg.counter("bgc_gpu_diag_skipped_in_use_total", "GPUs skipped by a diagnostics pass because a container held them").inc(static_cast<double>(skipped));
+  return changed;
+}
+
+void NodeAgent::on_health_changed() {
+  if (plugin_) plugin_->set_health(healthy_flags());
+  try {
+    publish();
+  } catch (const std::exception& e) {
+    LOG_ERROR("node_agent") << "publish after health change failed: " << e.what();
+  }
+}
+
 int NodeAgent::healthy_count(std::string* reason) const {
   auto snap = poller_ ? poller_->snapshot() : nullptr;
+  std::lock_guard<std::mutex> lk(diag_mu_);
   int healthy = 0;
   std::string why;
   for (size_t i = 0; i < gpus_.size(); ++i) {
@@ -215,9 +347,9 @@ int NodeAgent::healthy_count(std::string* reason) const {
       ok = snap->health[i].healthy;
       if (!ok) why += "gpu" + std::to_string(gpus_[i].index) + ": " + snap->health[i].reason + "; ";
     }
-    if (diag_.ran && i < diag_.per_gpu.size() && !diag_.per_gpu[i].get("passed").as_bool()) {
+    if (diag_failed(diag_, i)) {
       ok = false;
-      why += "gpu" + std::to_string(gpus_[i].index) + ": diagnostics failed; ";
+      why += "gpu" + std::to_string(gpus_[i].index) + ": diagnostics failed " + diag_.per_gpu.items()[i].get("failures").dump() + "; ";
     }
     if (ok) ++healthy;
   }
@@ -230,7 +362,8 @@ void NodeAgent::publish() {
   if (!cfg_.create_node && !node_present_) return;  // the kubelet registers the Node, not us
   std::string reason;
   int healthy = healthy_count(&reason);
-  client_.apply(types::Node, "", cfg_.node_name, node_labels_patch(cfg_, gpus_, healthy, diag_), kNodeAgentManager, true);
+  client_.apply(types::Node, "", cfg_.node_name, node_labels_patch(cfg_, gpus_, healthy, diag_outcome()), kNodeAgentManager,
+                true);
   client_.apply_status(types::Node, "", cfg_.node_name, node_status_patch(cfg_, gpus_, healthy, reason),
                        kNodeAgentManager, true);
   publishes_.fetch_add(1);
@@ -250,15 +383,19 @@ void NodeAgent::start() {
     plugin_->set_health(healthy_flags());
     plugin_->start();
   }
-  poller_->on_health_change([this](const Snapshot&) {
-    if (plugin_) plugin_->set_health(healthy_flags());
-    try {
-      publish();
-    } catch (const std::exception& e) {
-      LOG_ERROR("node_agent") << "publish after health change failed: " << e.what();
-    }
-  });
+  poller_->on_health_change([this](const Snapshot&) { on_health_changed(); });
   poller_->start();
+  if (cfg_.run_diag && cfg_.diag_interval_secs > 0) {
+    diag_thread_ = std::thread([this] {
+      while (!stop_.wait_for(std::chrono::seconds(cfg_.diag_interval_secs))) {
+        try {
+          if (run_diagnostics(false)) on_health_changed();
+        } catch (const std::exception& e) {
+          LOG_ERROR("node_agent") << "periodic diagnostics failed: " << e.what();
+        }
+      }
+    });
+  }
   heartbeat_ = std::thread([this] {
     while (!stop_.wait_for(std::chrono::seconds(cfg_.heartbeat_secs))) {
       try {
@@ -309,6 +446,7 @@ void NodeAgent::stop() {
   if (poller_) poller_->stop();
   if (plugin_) plugin_->stop();
   if (heartbeat_.joinable()) heartbeat_.join();
+  if (diag_thread_.joinable()) diag_thread_.join();
   if (node_watch_.joinable()) node_watch_.join();
 }
 
@@ -327,7 +465,10 @@ Value NodeAgent::describe() const {
   std::string reason;
   out["healthy"] = healthy_count(&reason);
   out["unhealthy_reason"] = reason;
-  out["diag"] = diag_.per_gpu;
+  DiagOutcome d = diag_outcome();
+  out["diag"] = d.per_gpu;
+  out["diag_runs"] = static_cast<unsigned long long>(d.runs);
+  out["diag_skipped_in_use"] = static_cast<unsigned long long>(d.skipped_in_use);
   if (plugin_) out["device_plugin"] = plugin_->describe();
   return out;
 }

@@ -5,7 +5,8 @@
 //   labels       amd.com/gpu.present=true, .family=gfx950, .product=MI355X, .count=8,
 //                .vram-gb=288, .xgmi-hive-id=<hex>, .compute-partition=SPX,
 //                .memory-partition=NPS1, .cu-count=256, .healthy-count=8, .diag=passed
-//   annotation   amd.com/gpu.topology = JSON [{index,uuid,bdf,hive,node,numa}]
+//   annotation   amd.com/gpu.topology = JSON [{index,uuid,bdf,hive,node,numa,render,
+//                links:[{peer,type,hops,weight,bw}]}] (the measured amdsmi link map)
 //   status       capacity/allocatable amd.com/gpu, condition AMDGPUHealthy
 //
 // Labels go through server-side apply on the Node, capacity/condition through SSA on
@@ -27,6 +28,7 @@
 #include "core/json.h"
 #include "gpu/device.h"
 #include "gpu/device_plugin.h"
+#include "gpu/diag.h"
 #include "gpu/telemetry.h"
 #include "kube/client.h"
 
@@ -50,8 +52,19 @@ struct NodeAgentConfig {
   std::string partition_resource_name = "amd.com/gpu-partition";
   std::string label_prefix = "amd.com/gpu";
   int max_gpus = 0;                    // 0 = all discovered
-  bool run_diag = false;               // HIP HBM + MFMA check before advertising
+  // HIP diagnostics (gpu/diag.h): HBM pattern + bandwidth, per-CU MFMA tiles + rate,
+  // per-XCC balance and an MFMA GEMM checked against a host fp32 product.  They run
+  // before the first advertisement and then every `diag_interval_secs` on GPUs that no
+  // container holds (kubelet pod-resources API, else amdsmi's process list); a GPU that
+  // fails a check or a floor is advertised Unhealthy until a later run passes.
+  bool run_diag = false;
   uint64_t diag_hbm_bytes = 1ULL << 30;
+  uint64_t diag_interval_secs = 0;     // 0 = only at start
+  DiagFloors diag_floors = DiagFloors::mi355x_defaults();
+  std::string pod_resources_socket = "/var/lib/kubelet/pod-resources/kubelet.sock";
+  HealthPolicy health;
+  int slow_every = 10;                 // polls between VRAM/ECC-total reads
+  int ras_every = 60;                  // polls between bad-page / per-block ECC / link reads
   bool create_node = false;            // test clusters without a kubelet
   // Kubelet device plugin (gpu/device_plugin.h).  When on, the kubelet owns the
   // amd.com/gpu capacity/allocatable counts, so the Node status patch carries only the
@@ -67,7 +80,9 @@ struct NodeAgentConfig {
 struct DiagOutcome {
   bool ran = false;
   bool passed = true;
-  json::Value per_gpu = json::Value::array();
+  json::Value per_gpu = json::Value::array();  // judged results, one per GPU (null = not run)
+  uint64_t runs = 0;
+  uint64_t skipped_in_use = 0;
 };
 
 std::string sanitize_label_value(const std::string& v);
@@ -100,14 +115,23 @@ class NodeAgent {
   DevicePlugin* device_plugin() { return plugin_.get(); }
   // Per-GPU health: telemetry state machine AND (when run) the HIP diagnostics.
   std::vector<bool> healthy_flags() const;
+  // One diagnostics pass over every GPU not held by a container; returns true when any
+  // GPU's verdict changed (and then re-publishes health).  `force` ignores allocation.
+  bool run_diagnostics(bool force = false);
+  DiagOutcome diag_outcome() const;
 
  private:
   int healthy_count(std::string* reason) const;
+  json::Value diagnose(const GpuInfo& g) const;
+  std::vector<bool> in_use() const;
+  void on_health_changed();
   kube::KubeClient& client_;
   std::unique_ptr<Backend> backend_;
   NodeAgentConfig cfg_;
   std::vector<GpuInfo> gpus_;
+  mutable std::mutex diag_mu_;  // guards diag_ (the diag thread updates it)
   DiagOutcome diag_;
+  std::thread diag_thread_;
   std::unique_ptr<TelemetryPoller> poller_;
   std::unique_ptr<DevicePlugin> plugin_;
   std::mutex publish_mu_;

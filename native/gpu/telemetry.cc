@@ -1,5 +1,6 @@
 #include "gpu/telemetry.h"
 
+#include <algorithm>
 #include <future>
 
 #include "core/log.h"
@@ -9,15 +10,19 @@
 namespace bgc::gpu {
 
 TelemetryPoller::TelemetryPoller(Backend& backend, std::vector<int> indices, std::chrono::milliseconds interval,
-                                 HealthPolicy policy, int slow_every)
+                                 HealthPolicy policy, int slow_every, int ras_every, std::vector<uint64_t> page_limits)
     : backend_(backend), indices_(std::move(indices)), interval_(interval), policy_(policy),
-      slow_every_(std::max(1, slow_every)) {
-  for (int i : indices_) {
+      slow_every_(std::max(1, slow_every)), ras_every_(std::max(1, ras_every)) {
+  for (size_t k = 0; k < indices_.size(); ++k) {
     DeviceHealth h;
-    h.index = i;
+    h.index = indices_[k];
+    h.page_limit = policy_.max_retired_pages;
+    if (k < page_limits.size() && page_limits[k] > 0) h.page_limit = std::min(h.page_limit, page_limits[k]);
     health_.push_back(h);
   }
   slow_cache_.resize(indices_.size());
+  ras_cache_.resize(indices_.size());
+  prev_.resize(indices_.size());
   if (indices_.size() > 1) pool_ = std::make_unique<ThreadPool>(indices_.size());
   auto& reg = metrics::Registry::global();
   for (int i : indices_) {
@@ -32,7 +37,11 @@ TelemetryPoller::TelemetryPoller(Backend& backend, std::vector<int> indices, std
                        &reg.gauge("amd_gpu_gfxclk_mhz", "GFX clock", l),
                        &reg.gauge("amd_gpu_ecc_uncorrectable_total", "Uncorrectable ECC errors", l),
                        &reg.gauge("amd_gpu_xgmi_links_up", "xGMI links up", l),
-                       &reg.gauge("amd_gpu_healthy", "1 when the device passes the health policy", l)});
+                       &reg.gauge("amd_gpu_healthy", "1 when the device passes the health policy", l),
+                       &reg.gauge("amd_gpu_violation_ppt_percent", "Power-cap (PPT) throttle residency, last interval", l),
+                       &reg.gauge("amd_gpu_violation_thermal_percent", "Thermal throttle residency, last interval", l),
+                       &reg.gauge("amd_gpu_retired_pages", "Retired + pending HBM pages", l),
+                       &reg.gauge("amd_gpu_throttle_status", "Independent throttle status bits (-1 = not reported)", l)});
   }
   snap_ = std::make_shared<Snapshot>();
 }
@@ -46,8 +55,26 @@ std::shared_ptr<const Snapshot> TelemetryPoller::snapshot() const {
   return snap_;
 }
 
+void TelemetryPoller::violation_deltas(const Telemetry& prev, Telemetry& cur) {
+  cur.violation_ppt_pct = cur.violation_thermal_pct = -1;
+  if (cur.acc_counter == Telemetry::kNoAcc || prev.acc_counter == Telemetry::kNoAcc) return;
+  if (cur.acc_counter <= prev.acc_counter) return;  // no new accumulation cycle (or a reset)
+  const double span = static_cast<double>(cur.acc_counter - prev.acc_counter);
+  auto pct = [&](uint64_t a, uint64_t b) -> double {
+    if (a == Telemetry::kNoAcc || b == Telemetry::kNoAcc || a < b) return -1;
+    return std::min(100.0, 100.0 * static_cast<double>(a - b) / span);
+  };
+  cur.violation_ppt_pct = pct(cur.acc_ppt, prev.acc_ppt);
+  cur.violation_thermal_pct = pct(cur.acc_thermal, prev.acc_thermal);
+}
+
 void TelemetryPoller::evaluate(const Telemetry& t, const HealthPolicy& p, DeviceHealth& h) {
   std::string problem;
+  if (t.ras_ok) {
+    h.retired_pages = t.retired_pages;
+    h.unreservable_pages = t.unreservable_pages;
+  }
+  if (h.page_limit == 0) h.page_limit = p.max_retired_pages;
   if (!t.ok) {
     problem = "telemetry unavailable: " + t.error;
   } else {
@@ -55,13 +82,27 @@ void TelemetryPoller::evaluate(const Telemetry& t, const HealthPolicy& p, Device
       h.baseline_uncorrectable = t.ecc_uncorrectable;
       h.baseline_set = true;
     }
+    h.consecutive_thermal = t.violation_thermal_pct > p.max_thermal_violation_pct ? h.consecutive_thermal + 1 : 0;
+    h.consecutive_ppt = t.violation_ppt_pct > p.max_ppt_violation_pct ? h.consecutive_ppt + 1 : 0;
     if (t.temp_hotspot_c > p.max_hotspot_c) problem = "hotspot temperature " + std::to_string(t.temp_hotspot_c) + "C";
     else if (t.temp_mem_c > p.max_mem_c) problem = "HBM temperature " + std::to_string(t.temp_mem_c) + "C";
-    else if (t.ecc_uncorrectable > h.baseline_uncorrectable + p.max_new_uncorrectable) {
+    else if (h.baseline_uncorrectable > p.max_uncorrectable_at_start && t.ecc_uncorrectable >= h.baseline_uncorrectable) {
+      problem = std::to_string(h.baseline_uncorrectable) + " uncorrectable ECC errors already present at agent start";
+    } else if (t.ecc_uncorrectable > h.baseline_uncorrectable + p.max_new_uncorrectable) {
       problem = "uncorrectable ECC errors: " + std::to_string(t.ecc_uncorrectable - h.baseline_uncorrectable);
+    } else if (h.unreservable_pages > 0) {
+      problem = std::to_string(h.unreservable_pages) + " bad HBM pages could not be retired";
+    } else if (h.retired_pages > h.page_limit) {
+      problem = "retired HBM pages " + std::to_string(h.retired_pages) + " > " + std::to_string(h.page_limit);
     } else if (p.require_all_xgmi_links && t.xgmi_links_total > 0 && t.xgmi_links_up < t.xgmi_links_total) {
       problem = "xGMI links down: " + std::to_string(t.xgmi_links_total - t.xgmi_links_up) + "/" +
                 std::to_string(t.xgmi_links_total);
+    } else if (h.consecutive_thermal >= p.violation_sustain_polls) {
+      problem = "sustained thermal throttling: " + std::to_string(static_cast<int>(t.violation_thermal_pct)) + "% for " +
+                std::to_string(h.consecutive_thermal) + " polls";
+    } else if (h.consecutive_ppt >= p.violation_sustain_polls) {
+      problem = "sustained power-cap throttling: " + std::to_string(static_cast<int>(t.violation_ppt_pct)) + "% for " +
+                std::to_string(h.consecutive_ppt) + " polls";
     }
   }
   if (problem.empty()) {
@@ -88,16 +129,20 @@ void TelemetryPoller::poll_once() {
   auto snap = std::make_shared<Snapshot>();
   snap->devices.reserve(indices_.size());
   bool changed = false;
-  const bool full = polls_.load() % static_cast<uint64_t>(slow_every_) == 0;
+  const uint64_t seq = polls_.load();
+  const SampleLevel level = seq % static_cast<uint64_t>(ras_every_) == 0    ? SampleLevel::Ras
+                            : seq % static_cast<uint64_t>(slow_every_) == 0 ? SampleLevel::Slow
+                                                                            : SampleLevel::Fast;
+  const bool full = level >= SampleLevel::Slow;
   std::vector<Telemetry> samples(indices_.size());
   if (pool_) {
     std::vector<std::future<void>> futs;
     for (size_t k = 0; k < indices_.size(); ++k) {
-      futs.push_back(pool_->submit([&, k] { samples[k] = backend_.sample(indices_[k], full); }));
+      futs.push_back(pool_->submit([&, k] { samples[k] = backend_.sample(indices_[k], level); }));
     }
     for (auto& f : futs) f.get();
   } else {
-    for (size_t k = 0; k < indices_.size(); ++k) samples[k] = backend_.sample(indices_[k], full);
+    for (size_t k = 0; k < indices_.size(); ++k) samples[k] = backend_.sample(indices_[k], level);
   }
   for (size_t k = 0; k < indices_.size(); ++k) {
     Telemetry t = std::move(samples[k]);
@@ -106,8 +151,24 @@ void TelemetryPoller::poll_once() {
     } else if (t.ok) {
       t.ecc_correctable = slow_cache_[k].ecc_correctable;
       t.ecc_uncorrectable = slow_cache_[k].ecc_uncorrectable;
+      t.ecc_deferred = slow_cache_[k].ecc_deferred;
       t.vram_used_mb = slow_cache_[k].vram_used_mb;
       t.vram_total_mb = slow_cache_[k].vram_total_mb;
+    }
+    if (level == SampleLevel::Ras) {
+      ras_cache_[k] = t;
+    } else if (t.ok && ras_cache_[k].ras_ok) {
+      t.ras_ok = true;
+      t.retired_pages = ras_cache_[k].retired_pages;
+      t.unreservable_pages = ras_cache_[k].unreservable_pages;
+      t.ecc_blocks = ras_cache_[k].ecc_blocks;
+      t.links = ras_cache_[k].links;
+    }
+    if (t.ok) {
+      violation_deltas(prev_[k], t);
+      prev_[k].acc_counter = t.acc_counter;
+      prev_[k].acc_ppt = t.acc_ppt;
+      prev_[k].acc_thermal = t.acc_thermal;
     }
     bool was = health_[k].healthy;
     evaluate(t, policy_, health_[k]);
@@ -131,6 +192,10 @@ void TelemetryPoller::poll_once() {
     g.ecc_ue->set(static_cast<double>(t.ecc_uncorrectable));
     g.xgmi_up->set(t.xgmi_links_up);
     g.healthy->set(health_[k].healthy ? 1 : 0);
+    g.viol_ppt->set(t.violation_ppt_pct);
+    g.viol_thermal->set(t.violation_thermal_pct);
+    g.retired->set(static_cast<double>(health_[k].retired_pages));
+    g.throttle->set(t.throttle_valid ? static_cast<double>(t.throttle_status) : -1.0);
     snap->devices.push_back(std::move(t));
   }
   snap->health = health_;

@@ -1,8 +1,9 @@
 // Side-thread telemetry poller + health evaluation (north-star N2).
 //
 // One background thread samples every managed device each `interval` (amdsmi
-// gpu_metrics: activity, power, temperatures, clocks, throttle, xGMI link status; VRAM
-// usage; ECC totals), publishes an immutable snapshot (readers never block the poll),
+// gpu_metrics: activity, power, temperatures, clocks, throttle, violation residency, xGMI
+// link status; every Nth poll VRAM usage and ECC totals; every Mth poll retired pages,
+// per-block ECC and xGMI link traffic), publishes an immutable snapshot (readers never block the poll),
 // exports `amd_gpu_*` Prometheus gauges, and drives a per-device health state machine
 // with hysteresis.  Each poll is bracketed by a roctx range so rocprofv3 --marker-trace
 // shows its cost; the reconcile/admission paths never touch it.
@@ -28,7 +29,20 @@ struct HealthPolicy {
   double max_hotspot_c = 105.0;      // above -> unhealthy
   double max_mem_c = 95.0;
   uint64_t max_new_uncorrectable = 0;  // new uncorrectable ECC errors tolerated since start
+  // Uncorrectable errors already counted when the agent starts (the counters reset on
+  // driver load, so these happened during this boot): more than this -> unhealthy.
+  uint64_t max_uncorrectable_at_start = 0;
   bool require_all_xgmi_links = true;  // a down xGMI link breaks TP=8 all-reduce placement
+  // Retired (reserved + pending) HBM pages above this -> unhealthy; the driver's own
+  // bad-page threshold, when readable, caps it.  Any page the driver could not retire
+  // (unreservable) is always unhealthy.
+  uint64_t max_retired_pages = 64;
+  // Sustained throttling: thermal (socket/HBM/VR/PROCHOT) residency above this
+  // percentage for `violation_sustain_polls` consecutive polls -> unhealthy.  Power
+  // (PPT) capping is normal for an MI355X at full load, so it is off by default (>100).
+  double max_thermal_violation_pct = 20.0;
+  double max_ppt_violation_pct = 101.0;
+  int violation_sustain_polls = 30;
   int fail_threshold = 3;              // consecutive bad polls before flipping to unhealthy
   int recover_threshold = 3;           // consecutive good polls before flipping back
 };
@@ -41,6 +55,11 @@ struct DeviceHealth {
   int consecutive_good = 0;
   uint64_t baseline_uncorrectable = 0;
   bool baseline_set = false;
+  int consecutive_thermal = 0;  // polls in a row over the thermal violation limit
+  int consecutive_ppt = 0;
+  uint64_t retired_pages = 0;   // last RAS reading (cached between RAS polls)
+  uint64_t unreservable_pages = 0;
+  uint64_t page_limit = 0;      // effective retired-page limit (policy, capped by driver)
 };
 
 struct Snapshot {
@@ -56,8 +75,11 @@ class TelemetryPoller {
   // slow_every: the expensive counters (ECC totals, VRAM usage) are read every Nth poll
   // and cached in between; devices are sampled concurrently (one task per GPU), so a
   // poll over 8 MI355X costs about one device's latency, not eight.
+  // ras_every: bad pages, per-block ECC and xGMI link metrics are read every Nth poll.
+  // page_limits[k] (optional): the driver's bad-page threshold of device k.
   TelemetryPoller(Backend& backend, std::vector<int> indices, std::chrono::milliseconds interval,
-                  HealthPolicy policy = {}, int slow_every = 10);
+                  HealthPolicy policy = {}, int slow_every = 10, int ras_every = 60,
+                  std::vector<uint64_t> page_limits = {});
   ~TelemetryPoller();
   void start();
   void stop();
@@ -70,6 +92,9 @@ class TelemetryPoller {
 
   // Pure health step (exposed for tests).
   static void evaluate(const Telemetry& t, const HealthPolicy& p, DeviceHealth& h);
+  // Violation percentages of `cur` over the interval since `prev` (pure, exposed for tests).
+  static void violation_deltas(const Telemetry& prev, Telemetry& cur);
+  const HealthPolicy& policy() const { return policy_; }
 
  private:
   Backend& backend_;
@@ -78,10 +103,14 @@ class TelemetryPoller {
   HealthPolicy policy_;
   std::vector<DeviceHealth> health_;
   int slow_every_;
+  int ras_every_;
   std::vector<Telemetry> slow_cache_;
+  std::vector<Telemetry> ras_cache_;
+  std::vector<Telemetry> prev_;  // last sample per device (violation deltas)
   std::unique_ptr<ThreadPool> pool_;
   struct Gauges {
-    metrics::Gauge *gfx, *umc, *power, *hotspot, *mem_temp, *vram_used, *vram_total, *gfxclk, *ecc_ue, *xgmi_up, *healthy;
+    metrics::Gauge *gfx, *umc, *power, *hotspot, *mem_temp, *vram_used, *vram_total, *gfxclk, *ecc_ue, *xgmi_up, *healthy,
+        *viol_ppt, *viol_thermal, *retired, *throttle;
   };
   std::vector<Gauges> gauges_;  // resolved once: the poll path does no registry lookups
   mutable std::mutex snap_mu_;

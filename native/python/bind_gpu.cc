@@ -3,6 +3,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
 #include <chrono>
 #include <memory>
 
@@ -44,6 +45,32 @@ std::string snapshot_json(const bgc::gpu::Snapshot& s) {
   return v.dump();
 }
 
+bgc::gpu::HealthPolicy policy_from_json(const std::string& js) {
+  bgc::gpu::HealthPolicy p;
+  Value v = bgc::json::parse(js.empty() ? "{}" : js);
+  auto d = [&](const char* k, double& dst) {
+    if (v.get(k).is_number()) dst = v.get(k).as_double();
+  };
+  auto u = [&](const char* k, uint64_t& dst) {
+    if (v.get(k).is_int()) dst = v.get(k).as_uint();
+  };
+  auto i = [&](const char* k, int& dst) {
+    if (v.get(k).is_int()) dst = static_cast<int>(v.get(k).as_int());
+  };
+  d("max_hotspot_c", p.max_hotspot_c);
+  d("max_mem_c", p.max_mem_c);
+  u("max_new_uncorrectable", p.max_new_uncorrectable);
+  u("max_uncorrectable_at_start", p.max_uncorrectable_at_start);
+  if (v.get("require_all_xgmi_links").is_bool()) p.require_all_xgmi_links = v.get("require_all_xgmi_links").as_bool();
+  u("max_retired_pages", p.max_retired_pages);
+  d("max_thermal_violation_pct", p.max_thermal_violation_pct);
+  d("max_ppt_violation_pct", p.max_ppt_violation_pct);
+  i("violation_sustain_polls", p.violation_sustain_polls);
+  i("fail_threshold", p.fail_threshold);
+  i("recover_threshold", p.recover_threshold);
+  return p;
+}
+
 }  // namespace
 
 void register_gpu(py::module_& m) {
@@ -57,14 +84,15 @@ void register_gpu(py::module_& m) {
         }
         return arr.dump();
       })
-      .def("sample", [](PyBackend& b, int idx, bool full) {
+      .def("sample", [](PyBackend& b, int idx, int level) {
         bgc::gpu::Telemetry t;
         {
           py::gil_scoped_release nogil;
-          t = b.b->sample(idx, full);
+          t = b.b->sample(idx, static_cast<bgc::gpu::SampleLevel>(std::clamp(level, 0, 2)));
         }
         return bgc::gpu::to_json(t).dump();
-      }, py::arg("index"), py::arg("full") = true);
+      }, py::arg("index"), py::arg("level") = 2)
+      .def("busy_processes", [](PyBackend& b, int idx) { return b.b->busy_processes(idx); });
 
   m.def("gpu_backend", [](const std::string& kind, const std::string& fixture_json) {
     auto pb = std::make_shared<PyBackend>();
@@ -82,13 +110,17 @@ void register_gpu(py::module_& m) {
         py::arg("hive_id") = 0x1a2b3c4d5e6f7788ULL);
 
   py::class_<PyPoller>(m, "TelemetryPoller")
-      .def(py::init([](std::shared_ptr<PyBackend> b, std::vector<int> idx, int interval_ms) {
+      .def(py::init([](std::shared_ptr<PyBackend> b, std::vector<int> idx, int interval_ms, const std::string& policy,
+                       int slow_every, int ras_every, std::vector<uint64_t> page_limits) {
              auto p = std::make_unique<PyPoller>();
              p->backend = b;
-             p->poller = std::make_unique<bgc::gpu::TelemetryPoller>(*b->b, idx, std::chrono::milliseconds(interval_ms));
+             p->poller = std::make_unique<bgc::gpu::TelemetryPoller>(
+                 *b->b, idx, std::chrono::milliseconds(interval_ms), policy_from_json(policy), slow_every, ras_every,
+                 std::move(page_limits));
              return p;
            }),
-           py::arg("backend"), py::arg("indices"), py::arg("interval_ms") = 1000)
+           py::arg("backend"), py::arg("indices"), py::arg("interval_ms") = 1000, py::arg("policy") = "{}",
+           py::arg("slow_every") = 10, py::arg("ras_every") = 60, py::arg("page_limits") = std::vector<uint64_t>{})
       .def("start", [](PyPoller& p) { p.poller->start(); })
       .def("stop", [](PyPoller& p) {
         py::gil_scoped_release nogil;
@@ -102,31 +134,30 @@ void register_gpu(py::module_& m) {
       .def("snapshot", [](PyPoller& p) { return snapshot_json(*p.poller->snapshot()); });
 
   m.def("health_step", [](const std::string& telemetry_json, int fail_threshold, int recover_threshold,
-                          std::vector<py::dict> history) {
-    // Runs the health state machine over a sequence of telemetry samples; returns the
-    // (healthy, reason) after each step.
-    bgc::gpu::HealthPolicy pol;
+                          const std::string& policy, uint64_t page_limit) {
+    // Runs the health state machine over a sequence of telemetry samples (violation
+    // percentages are derived from accumulators when a sample carries acc_counter);
+    // returns (healthy, reason) after each step.
+    bgc::gpu::HealthPolicy pol = policy_from_json(policy);
     pol.fail_threshold = fail_threshold;
     pol.recover_threshold = recover_threshold;
     bgc::gpu::DeviceHealth h;
+    h.page_limit = page_limit ? std::min<uint64_t>(page_limit, pol.max_retired_pages) : pol.max_retired_pages;
+    bgc::gpu::Telemetry prev;
     std::vector<py::tuple> out;
     Value seq = bgc::json::parse(telemetry_json);
     for (const auto& tv : seq.items()) {
-      bgc::gpu::Telemetry t;
-      t.ok = tv.get("ok").is_bool() ? tv.get("ok").as_bool() : true;
-      t.error = tv.get_string("error");
-      t.temp_hotspot_c = tv.get("temp_hotspot_c").is_number() ? tv.get("temp_hotspot_c").as_double() : 40;
-      t.temp_mem_c = tv.get("temp_mem_c").is_number() ? tv.get("temp_mem_c").as_double() : 40;
-      t.ecc_uncorrectable = tv.get("ecc_uncorrectable").is_int() ? tv.get("ecc_uncorrectable").as_uint() : 0;
-      t.xgmi_links_up = tv.get("xgmi_links_up").is_int() ? static_cast<int>(tv.get("xgmi_links_up").as_int()) : -1;
-      t.xgmi_links_total = tv.get("xgmi_links_total").is_int() ? static_cast<int>(tv.get("xgmi_links_total").as_int()) : -1;
+      bgc::gpu::Telemetry t = bgc::gpu::telemetry_from_json(tv);
+      if (t.acc_counter != bgc::gpu::Telemetry::kNoAcc) {
+        bgc::gpu::TelemetryPoller::violation_deltas(prev, t);
+        prev = t;
+      }
       bgc::gpu::TelemetryPoller::evaluate(t, pol, h);
       out.push_back(py::make_tuple(h.healthy, h.reason));
     }
-    (void)history;
     return out;
   }, py::arg("telemetry_json"), py::arg("fail_threshold") = 3, py::arg("recover_threshold") = 3,
-     py::arg("history") = std::vector<py::dict>{});
+     py::arg("policy") = "{}", py::arg("page_limit") = 0);
 
   // --- HIP diagnostics ---
   m.def("diag_library_path", [](const std::string& p) { return bgc::gpu::Diag::instance(p).path(); },
@@ -149,6 +180,40 @@ void register_gpu(py::module_& m) {
     }
     return v.dump();
   }, py::arg("device"), py::arg("waves_per_cu") = 32, py::arg("iters") = 4096, py::arg("seed") = 0x5eed);
+  m.def("diag_gemm", [](int device, int mm, int nn, int kk, const std::string& a, const std::string& b) {
+    if (a.size() != static_cast<size_t>(mm) * kk * 2 || b.size() != static_cast<size_t>(kk) * nn * 2) {
+      throw std::invalid_argument("A must be M*K and B K*N bf16 values");
+    }
+    std::string c(static_cast<size_t>(mm) * nn * 4, '\0');
+    {
+      py::gil_scoped_release nogil;
+      bgc::gpu::Diag::instance().gemm(device, mm, nn, kk, reinterpret_cast<const uint16_t*>(a.data()),
+                                      reinterpret_cast<const uint16_t*>(b.data()), reinterpret_cast<float*>(c.data()));
+    }
+    return py::bytes(c);
+  }, py::arg("device"), py::arg("m"), py::arg("n"), py::arg("k"), py::arg("a_bf16"), py::arg("b_bf16"));
+  m.def("diag_gemm_check", [](int device, int mm, int nn, int kk, unsigned seed) {
+    Value v;
+    {
+      py::gil_scoped_release nogil;
+      v = bgc::gpu::Diag::instance().gemm_check(device, mm, nn, kk, seed);
+    }
+    return v.dump();
+  }, py::arg("device"), py::arg("m") = 64, py::arg("n") = 64, py::arg("k") = 512, py::arg("seed") = 0x5eed);
+  m.def("judge_diag", [](const std::string& result, const std::string& floors_json) {
+    bgc::gpu::DiagFloors f = bgc::gpu::DiagFloors::mi355x_defaults();
+    Value fj = bgc::json::parse(floors_json);
+    auto num = [&](const char* k, double& dst) {
+      if (fj.get(k).is_number()) dst = fj.get(k).as_double();
+    };
+    num("min_read_gbps", f.min_read_gbps);
+    num("min_copy_gbps", f.min_copy_gbps);
+    num("min_write_gbps", f.min_write_gbps);
+    num("min_mfma_tflops", f.min_mfma_tflops);
+    num("min_xcc_balance", f.min_xcc_balance);
+    if (fj.get("min_xccs").is_int()) f.min_xccs = static_cast<int>(fj.get("min_xccs").as_int());
+    return bgc::gpu::judge_diag(bgc::json::parse(result), f).dump();
+  }, py::arg("result"), py::arg("floors") = "{}");
   m.def("roctx_available", &bgc::roctx::available);
 
   // Node agent rendering (pure functions).

@@ -193,6 +193,33 @@ void register_grpc(py::module_& m) {
           return bgc::gpu::preferred_allocation(gpus_from_json(gpus_json), ids, available, must_include, size);
         });
 
+  // kubelet pod-resources v1 (List) codec + client
+  m.def("pod_resources_encode", [](const std::string& js) {
+    std::vector<bgc::gpu::PodDevices> v;
+    const bgc::json::Value parsed = bgc::json::parse(js);
+    for (const auto& p : parsed.items()) {
+      bgc::gpu::PodDevices d{p.get_string("pod"), p.get_string("namespace"), p.get_string("container"),
+                             p.get_string("resource"), {}};
+      for (const auto& id : p.get("ids").items()) d.ids.push_back(id.as_string());
+      v.push_back(std::move(d));
+    }
+    return py::bytes(bgc::gpu::encode_pod_resources(v));
+  });
+  m.def("pod_resources_decode", [](const std::string& buf) {
+    bgc::json::Value out = bgc::json::Value::array();
+    for (const auto& d : bgc::gpu::decode_pod_resources(buf)) {
+      bgc::json::Value ids = bgc::json::Value::array();
+      for (const auto& id : d.ids) ids.push_back(id);
+      out.push_back(bgc::json::Value::object({{"pod", d.pod}, {"namespace", d.ns}, {"container", d.container},
+                                              {"resource", d.resource}, {"ids", ids}}));
+    }
+    return out.dump();
+  });
+  m.def("allocated_device_ids", [](const std::string& socket, const std::string& resource) {
+    py::gil_scoped_release nogil;
+    return bgc::gpu::allocated_device_ids(socket, resource);
+  });
+
   py::class_<bgc::grpc::Channel>(m, "GrpcChannel")
       .def(py::init<std::string, int>(), py::arg("target"), py::arg("connect_timeout_ms") = 5000)
       .def("unary",
@@ -248,6 +275,17 @@ void register_grpc(py::module_& m) {
       .def("start", &bgc::gpu::DevicePlugin::start, py::call_guard<py::gil_scoped_release>())
       .def("stop", &bgc::gpu::DevicePlugin::stop, py::call_guard<py::gil_scoped_release>())
       .def("set_health", &bgc::gpu::DevicePlugin::set_health)
+      .def("allocate_json", [](const bgc::gpu::DevicePlugin& p, const std::vector<std::string>& ids) {
+        auto c = p.allocate(ids);
+        bgc::json::Value devs = bgc::json::Value::array();
+        for (const auto& d : c.devices) {
+          devs.push_back(bgc::json::Value::object(
+              {{"container_path", d.container_path}, {"host_path", d.host_path}, {"permissions", d.permissions}}));
+        }
+        bgc::json::Value envs = bgc::json::Value::object();
+        for (const auto& [k, v] : c.envs) envs[k] = v;
+        return bgc::json::Value::object({{"devices", devs}, {"envs", envs}}).dump();
+      })
       .def_property_readonly("ids", &bgc::gpu::DevicePlugin::ids)
       .def_property_readonly("socket_path", &bgc::gpu::DevicePlugin::socket_path)
       .def_property_readonly("registrations", &bgc::gpu::DevicePlugin::registrations)

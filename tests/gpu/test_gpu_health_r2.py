@@ -1,0 +1,151 @@
+"""Round-2 N1/N2/diag depth on a real MI355X:
+
+* amdsmi topology / RAS of the visible device: physical xGMI link metrics, retired-page
+  count, per-block ECC, violation residency (not the 0xFFFFFFFF throttle sentinel);
+* the MFMA GEMM kernel checked against a host torch fp32 matmul;
+* per-XCC balance from the MFMA throughput pass;
+* the diagnostics as a health gate: an unreachable floor marks the GPU Unhealthy in
+  ListAndWatch and drops amd.com/gpu.healthy-count, the default floors pass.
+
+Results are also written to gpurun_out/ for profiles/."""
+import json
+import os
+import time
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+OUT = os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "gpurun_out", "r2_gpu")
+
+
+def _dump(name, obj):
+    os.makedirs(OUT, exist_ok=True)
+    with open(os.path.join(OUT, name), "w") as f:
+        json.dump(obj, f, indent=1, sort_keys=True)
+
+
+def test_amdsmi_topology_ras_and_violations():
+    from bacchus_gpu_controller_amd import native
+
+    b = native().gpu_backend("amdsmi", "")
+    gpus = json.loads(b.discover())
+    g = gpus[0]
+    ras = json.loads(b.sample(0, 2))
+    time.sleep(0.2)
+    ras2 = json.loads(b.sample(0, 2))
+    _dump("amdsmi_topology_ras.json", {"gpu": g, "ras_sample": ras, "busy_processes": b.busy_processes(0)})
+    assert ras["ok"] and "retired_pages" in ras and "unreservable_pages" in ras
+    assert isinstance(ras["ecc_blocks"], dict)
+    # MI355X OAM: 7 xGMI links per GPU even when only one GPU is visible to us
+    xgmi = [l for l in g["phys_links"] if l["type"] == "xgmi"]
+    assert len(xgmi) >= 1, g["phys_links"]
+    assert all(l["peer_bdf"] for l in xgmi)
+    assert g["drm_render"] >= 128, g
+    # the 32-bit legacy throttle word is the all-ones sentinel on MI355X: never exported
+    assert ras["throttle_status"] != 0xFFFFFFFF
+    assert ras2["ok"]
+
+
+def test_poller_violation_percentages_and_own_process():
+    from bacchus_gpu_controller_amd import native, ops
+
+    n = native()
+    b = n.gpu_backend("amdsmi", "")
+    ops.device_count()  # this process now holds a HIP context on the GPU
+    assert b.busy_processes(0) >= 0  # ... which busy_processes() does not count
+    p = n.TelemetryPoller(b, [0], 50)
+    p.poll_once()
+    time.sleep(1.2)  # the SMU accumulation window is ~1 ms; give it many cycles
+    p.poll_once()
+    d = json.loads(p.snapshot())["devices"][0]
+    _dump("poller_violation.json", d)
+    assert d["violation_ppt_pct"] is not None and 0 <= d["violation_ppt_pct"] <= 100, d
+    assert d["violation_thermal_pct"] is not None and d["violation_thermal_pct"] < 50, d
+
+
+def test_sample_level_costs():
+    from bacchus_gpu_controller_amd import native
+
+    b = native().gpu_backend("amdsmi", "")
+    cost = {}
+    for level, name in ((0, "fast"), (1, "slow"), (2, "ras")):
+        samples = []
+        for _ in range(20):
+            t0 = time.perf_counter()
+            b.sample(0, level)
+            samples.append((time.perf_counter() - t0) * 1e6)
+        samples.sort()
+        cost[name] = {"p50_us": samples[len(samples) // 2], "min_us": samples[0], "max_us": samples[-1]}
+    _dump("amdsmi_cost_r2.json", cost)
+    assert cost["fast"]["p50_us"] < cost["ras"]["p50_us"]
+
+
+def test_mfma_gemm_matches_torch_fp32():
+    import torch
+
+    from bacchus_gpu_controller_amd import native
+
+    torch.manual_seed(0)
+    m, n, k = 128, 96, 512
+    a = torch.randn(m, k).to(torch.bfloat16)
+    bm = torch.randn(k, n).to(torch.bfloat16)
+    raw = native().diag_gemm(0, m, n, k, a.view(torch.int16).numpy().tobytes(), bm.view(torch.int16).numpy().tobytes())
+    c = torch.frombuffer(bytearray(raw), dtype=torch.float32).reshape(m, n)
+    ref = a.float() @ bm.float()  # plain PyTorch fp32 reference on the host
+    err = (c - ref).abs().max().item()
+    _dump("mfma_gemm_vs_torch.json", {"m": m, "n": n, "k": k, "max_abs_err": err,
+                                      "ref_abs_max": ref.abs().max().item()})
+    torch.testing.assert_close(c, ref, rtol=1e-4, atol=1e-4)
+    chk = json.loads(native().diag_gemm_check(0, 64, 64, 512, 7))
+    assert chk["passed"], chk
+
+
+def test_mfma_xcc_balance():
+    from bacchus_gpu_controller_amd import ops
+
+    r = ops.mfma(0, waves_per_cu=16, iters=2048)
+    assert r["xccs_seen"] == 8 and sum(r["xcc_waves"]) > 0
+    assert r["xcc_balance"] > 0.8, r
+    _dump("mfma_xcc_balance.json", r)
+
+
+def _agent_with_floors(tmp_path, name, floors_env):
+    from bacchus_gpu_controller_amd.testing.cluster import Cluster
+    from bacchus_gpu_controller_amd.testing.kubeapi import wait_for
+    from bacchus_gpu_controller_amd.testing.kubelet import FakeKubelet
+
+    d = str(tmp_path / f"dp-{name}")
+    kubelet = FakeKubelet(d).start()
+    try:
+        with Cluster(admission=False, controller=False) as c:
+            env = {"CONF_DEVICE_PLUGIN": "true", "CONF_DEVICE_PLUGIN_DIR": d, "CONF_RUN_DIAG": "true",
+                   "CONF_DIAG_HBM_BYTES": str(1 << 30), "CONF_HEARTBEAT_SECS": "1"}
+            env.update(floors_env)
+            c.start_node_agent(node_name=name, backend="amdsmi", max_gpus=1, poll_interval_ms=200, extra_env=env)
+            assert kubelet.wait(lambda: kubelet.device_lists, timeout=60)
+            node = wait_for(lambda: (lambda n: n if n and n["metadata"].get("labels", {}).get("amd.com/gpu.diag") else None)(
+                c.admin.get_or_none("nodes", name)), timeout=30, desc="labels")
+            import requests
+
+            desc = requests.get(f"http://127.0.0.1:{c.node_agent_ports[name]}/gpus", timeout=10).json()
+            return kubelet.device_lists[-1][1], node["metadata"]["labels"], desc
+    finally:
+        kubelet.stop()
+
+
+def test_diag_floor_gates_health(tmp_path):
+    devs, labels, desc = _agent_with_floors(tmp_path, "mi355x-floor", {"CONF_DIAG_MIN_READ_GBPS": "1e9"})
+    _dump("diag_unreachable_floor.json", desc["diag"])
+    assert [x[1] for x in devs] == ["Unhealthy"]
+    assert labels["amd.com/gpu.healthy-count"] == "0" and labels["amd.com/gpu.diag"] == "failed"
+    assert any("HBM read" in f for f in desc["diag"][0]["failures"])
+
+
+def test_diag_default_floors_pass(tmp_path):
+    devs, labels, desc = _agent_with_floors(tmp_path, "mi355x-ok", {})
+    _dump("diag_default_floors.json", desc["diag"])
+    assert desc["diag"][0]["passed"], desc["diag"][0]["failures"]
+    assert desc["diag"][0]["gemm"]["passed"]
+    assert [x[1] for x in devs] == ["Healthy"]
+    assert labels["amd.com/gpu.healthy-count"] == "1" and labels["amd.com/gpu.diag"] == "passed"

@@ -310,3 +310,60 @@ def test_compute_partitions_advertised_as_partition_resource(nat, tmp_path):
             assert ids[0] == fx["gpus"][0]["bdf"] + "-p0" and ids[1] == fx["gpus"][0]["bdf"] + "-p1"
     finally:
         kubelet.stop()
+
+
+def test_pod_resources_client_against_grpcio(nat, tmp_path):
+    from bacchus_gpu_controller_amd.testing.kubelet import FakePodResources
+
+    pr = FakePodResources(str(tmp_path / "pod-resources" / "kubelet.sock")).start()
+    try:
+        pr.assign("train-0", "amd.com/gpu", ["0000:05:00.0", "0000:15:00.0"])
+        pr.assign("other", "example.com/nic", ["eth0"])
+        assert nat.allocated_device_ids(pr.path, "amd.com/gpu") == {"0000:05:00.0", "0000:15:00.0"}
+        pr.release("train-0")
+        assert nat.allocated_device_ids(pr.path, "amd.com/gpu") == set()
+        assert pr.lists == 2
+    finally:
+        pr.stop()
+
+
+def test_periodic_diagnostics_skip_gpus_in_use(tmp_path):
+    """CONF_RUN_DIAG with CONF_DIAG_INTERVAL_SECS: the agent re-runs the HIP diagnostics on
+    GPUs no container holds — GPU 0 is held per the kubelet's pod-resources API, GPU 1 has a
+    compute process per amdsmi — and a failed diagnosis drives ListAndWatch and the
+    healthy-count label.  (On a host without a GPU every diagnosis fails loudly, which is
+    exactly what this test relies on; tests/gpu covers the passing path.)"""
+    from bacchus_gpu_controller_amd.testing.kubelet import FakePodResources
+
+    d = str(tmp_path / "dp")
+    kubelet = FakeKubelet(d).start()
+    pr = FakePodResources(str(tmp_path / "pod-resources" / "kubelet.sock")).start()
+    try:
+        with Cluster(admission=False, controller=False) as c:
+            fx_path = None
+            c.start_node_agent(node_name="mi355x-diag", backend="mock", n_mock_gpus=4, poll_interval_ms=50,
+                               extra_env={"CONF_DEVICE_PLUGIN": "true", "CONF_DEVICE_PLUGIN_DIR": d,
+                                          "CONF_RUN_DIAG": "true", "CONF_DIAG_INTERVAL_SECS": "1",
+                                          "CONF_DIAG_HBM_BYTES": str(64 << 20),
+                                          "CONF_POD_RESOURCES_SOCKET": pr.path, "CONF_HEARTBEAT_SECS": "1"})
+            fx_path = c.fixtures["mi355x-diag"]
+            fx = json.loads(open(fx_path).read())
+            fx["gpus"][1]["telemetry"]["busy_processes"] = 2
+            c.set_gpu_fixture("mi355x-diag", fx)
+            assert kubelet.wait(lambda: kubelet.registrations and kubelet.device_lists, timeout=15)
+            ids = [x[0] for x in kubelet.device_lists[-1][1]]
+            pr.assign("train-0", "amd.com/gpu", [ids[0]])
+            import requests
+
+            port = c.node_agent_ports["mi355x-diag"]
+            desc = wait_for(lambda: (lambda g: g if g["diag_runs"] >= 3 and g["diag_skipped_in_use"] >= 2 else None)(
+                requests.get(f"http://127.0.0.1:{port}/gpus", timeout=5).json()), timeout=30, desc="periodic diag runs")
+            assert pr.lists >= 1
+            assert all(not r["passed"] and r["failures"] for r in desc["diag"])
+            assert kubelet.wait(lambda: all(x[1] == "Unhealthy" for x in kubelet.device_lists[-1][1]), timeout=10)
+            node = c.admin.get_or_none("nodes", "mi355x-diag")
+            assert node["metadata"]["labels"]["amd.com/gpu.diag"] == "failed"
+            assert node["metadata"]["labels"]["amd.com/gpu.healthy-count"] == "0"
+    finally:
+        pr.stop()
+        kubelet.stop()

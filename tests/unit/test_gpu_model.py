@@ -38,7 +38,7 @@ def test_health_hysteresis(nat):
 
 def test_health_ecc_and_xgmi(nat):
     seq = [{"ecc_uncorrectable": 5}, {"ecc_uncorrectable": 6}]  # baseline 5, then +1
-    out = nat.health_step(json.dumps(seq), 1, 1)
+    out = nat.health_step(json.dumps(seq), 1, 1, json.dumps({"max_uncorrectable_at_start": 10}))
     assert out[0][0] is True and out[1][0] is False and "ECC" in out[1][1]
     out = nat.health_step(json.dumps([{"xgmi_links_up": 6, "xgmi_links_total": 7}]), 1, 1)
     assert out[0][0] is False and "xGMI" in out[0][1]

@@ -254,3 +254,15 @@ def test_node_agent_device_plugin_wiring():
     env = {e["name"]: e.get("value") for e in c["env"]}
     assert env["CONF_DEVICE_PLUGIN"] == "false" and "CONF_DEVICE_PLUGIN_DIR" not in env
     assert all(m["name"] != "device-plugins" for m in c["volumeMounts"])
+
+
+def test_node_agent_diag_and_health_policy_env():
+    ds = [m for m in render() if m.get("kind") == "DaemonSet"][0]
+    pod = ds["spec"]["template"]["spec"]
+    env = {e["name"]: e.get("value") for e in pod["containers"][0]["env"]}
+    assert env["CONF_RUN_DIAG"] == "true" and env["CONF_DIAG_HBM_BYTES"] == str(256 << 20)
+    assert env["CONF_DIAG_INTERVAL_SECS"] == "21600" and env["CONF_DIAG_MIN_READ_GBPS"] == "4750"
+    assert env["CONF_DIAG_MIN_XCC_BALANCE"] == "0.85" and env["CONF_MAX_RETIRED_PAGES"] == "64"
+    assert env["CONF_POD_RESOURCES_SOCKET"] == "/var/lib/kubelet/pod-resources/kubelet.sock"
+    mounts = {m["name"]: m["mountPath"] for m in pod["containers"][0]["volumeMounts"]}
+    assert mounts["pod-resources"] == "/var/lib/kubelet/pod-resources"
