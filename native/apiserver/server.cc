@@ -403,6 +403,7 @@ struct FaultRule {
   std::regex path;
   std::string path_src;
   int status = 0;
+  int retry_after_s = -1;  // >= 0: send a Retry-After header (429 / 503 throttling)
   int delay_ms = 0;
   int remaining = -1;  // -1 = unlimited
   bool reset = false;  // drop the connection without a response
@@ -476,6 +477,49 @@ struct ApiServer::Impl {
 
   std::mutex fault_mu;
   std::vector<FaultRule> faults;
+
+  // Paginated LIST snapshots (continue tokens).
+  struct ListSnapshot {
+    uint64_t rv = 0;
+    std::vector<std::shared_ptr<const Value>> items;
+    std::chrono::steady_clock::time_point expires;
+  };
+  std::mutex list_mu;
+  std::map<uint64_t, ListSnapshot> list_snapshots;
+  uint64_t next_list_id = 1;
+  std::atomic<uint64_t> list_pages{0};
+
+  // resourceVersion <-> wire string (decimal, or opaque "kl.<base36>" with --opaque-rv)
+  static constexpr uint64_t kRvMask = 0x5bd1e9955bd1e995ULL;
+  std::string rv_str(uint64_t v) const {
+    if (!opts.opaque_rv) return std::to_string(v);
+    static const char* digits = "0123456789abcdefghijklmnopqrstuvwxyz";
+    uint64_t x = v ^ kRvMask;
+    std::string out;
+    do {
+      out.insert(out.begin(), digits[x % 36]);
+      x /= 36;
+    } while (x);
+    return "kl." + out;
+  }
+  // false when the string is not a resourceVersion this server issued
+  bool parse_rv(const std::string& s, uint64_t* v) const {
+    if (!opts.opaque_rv) {
+      if (s.empty() || s.find_first_not_of("0123456789") != std::string::npos) return false;
+      *v = std::strtoull(s.c_str(), nullptr, 10);
+      return true;
+    }
+    if (s.rfind("kl.", 0) != 0 || s.size() < 4) return false;
+    uint64_t x = 0;
+    for (size_t i = 3; i < s.size(); ++i) {
+      const char c = s[i];
+      int d = c >= '0' && c <= '9' ? c - '0' : c >= 'a' && c <= 'z' ? c - 'a' + 10 : -1;
+      if (d < 0) return false;
+      x = x * 36 + static_cast<uint64_t>(d);
+    }
+    *v = x ^ kRvMask;
+    return true;
+  }
 
   std::mutex hook_mu;
   struct FastHook {
@@ -1105,7 +1149,7 @@ struct ApiServer::Impl {
                                             const PreparedEvent* pe = nullptr, bool* dangling = nullptr,
                                             std::shared_ptr<const std::string>* line_out = nullptr) {
     uint64_t new_rv = ++rv;
-    std::string digits = std::to_string(new_rv);
+    std::string digits = rv_str(new_rv);
     Value& meta = obj["metadata"];
     meta["resourceVersion"] = digits;
     std::string preline;
@@ -1174,10 +1218,10 @@ struct ApiServer::Impl {
       const std::string old_rv = "\"resourceVersion\":" + json::quote(ptr->get("metadata").get_string("resourceVersion"));
       size_t pos = line.find(old_rv, obj_at);
       if (pos != std::string::npos) {
-        line.replace(pos, old_rv.size(), "\"resourceVersion\":\"" + std::to_string(new_rv) + "\"");
+        line.replace(pos, old_rv.size(), "\"resourceVersion\":\"" + rv_str(new_rv) + "\"");
       } else {  // no resourceVersion in the stored object (never for committed objects)
         Value final_obj = *ptr;
-        final_obj["metadata"]["resourceVersion"] = std::to_string(new_rv);
+        final_obj["metadata"]["resourceVersion"] = rv_str(new_rv);
         ptr = std::make_shared<const Value>(std::move(final_obj));
         line = "{\"type\":\"DELETED\",\"object\":";
         ptr->dump_to(line);
@@ -1640,35 +1684,81 @@ struct ApiServer::Impl {
   }
 
   void do_list(ParsedPath& p, const http::Request& req, http::ResponseWriter& w) {
-    auto sel = parse_selector(req.query_param("labelSelector"));
-    auto ff = parse_field_selector(req.query_param("fieldSelector"));
+    const int64_t limit = req.has_query_param("limit") ? std::atoll(req.query_param("limit").c_str()) : 0;
+    const std::string cont = req.query_param("continue");
     std::vector<std::shared_ptr<const Value>> items;
-    uint64_t list_rv;
-    {
-      // no commit of this type is in flight while we hold its shared lock, so every event
-      // of this type with rv <= list_rv is reflected in the items
-      SharedStoreLock lk(p.ti->store->mu, p.ti->store->stats);
-      list_rv = rv.load();
-      for (auto& [k, st] : bucket(*p.ti)) {
-        const Value& meta = st.obj->get("metadata");
-        if (!p.ns.empty() && meta.get_string("namespace") != p.ns) continue;
-        if (!ff.name.empty() && meta.get_string("name") != ff.name) continue;
-        if (!ff.ns.empty() && meta.get_string("namespace") != ff.ns) continue;
-        if (!sel.empty() && !selector_matches(sel, *st.obj)) continue;
-        items.push_back(st.obj);
+    uint64_t list_rv = 0;
+    size_t offset = 0;
+    uint64_t snap_id = 0;
+    if (!cont.empty()) {
+      // "<snapshot id>.<offset>": later pages come from the first page's snapshot, so a
+      // paginated LIST is consistent at one resourceVersion (as etcd serves it)
+      const size_t dot = cont.find('.');
+      snap_id = std::strtoull(cont.c_str(), nullptr, 10);
+      offset = dot == std::string::npos ? 0 : std::strtoull(cont.c_str() + dot + 1, nullptr, 10);
+      std::lock_guard<std::mutex> lk(list_mu);
+      auto it = list_snapshots.find(snap_id);
+      if (it == list_snapshots.end() || std::chrono::steady_clock::now() > it->second.expires) {
+        if (it != list_snapshots.end()) list_snapshots.erase(it);
+        throw StatusError(410, "Expired",
+                          "The provided continue parameter is too old to display a consistent list result. You can "
+                          "start a new list without the continue parameter.");
       }
+      list_rv = it->second.rv;
+      items = it->second.items;  // shared pointers only
+    } else {
+      auto sel = parse_selector(req.query_param("labelSelector"));
+      auto ff = parse_field_selector(req.query_param("fieldSelector"));
+      {
+        // no commit of this type is in flight while we hold its shared lock, so every event
+        // of this type with rv <= list_rv is reflected in the items
+        SharedStoreLock lk(p.ti->store->mu, p.ti->store->stats);
+        list_rv = rv.load();
+        for (auto& [k, st] : bucket(*p.ti)) {
+          const Value& meta = st.obj->get("metadata");
+          if (!p.ns.empty() && meta.get_string("namespace") != p.ns) continue;
+          if (!ff.name.empty() && meta.get_string("name") != ff.name) continue;
+          if (!ff.ns.empty() && meta.get_string("namespace") != ff.ns) continue;
+          if (!sel.empty() && !selector_matches(sel, *st.obj)) continue;
+          items.push_back(st.obj);
+        }
+      }
+      std::sort(items.begin(), items.end(), [](const auto& a, const auto& b) {
+        const Value& ma = a->get("metadata");
+        const Value& mb = b->get("metadata");
+        return std::make_pair(ma.get_string("namespace"), ma.get_string("name")) <
+               std::make_pair(mb.get_string("namespace"), mb.get_string("name"));
+      });
     }
-    std::sort(items.begin(), items.end(), [](const auto& a, const auto& b) {
-      const Value& ma = a->get("metadata");
-      const Value& mb = b->get("metadata");
-      return std::make_pair(ma.get_string("namespace"), ma.get_string("name")) <
-             std::make_pair(mb.get_string("namespace"), mb.get_string("name"));
-    });
+    size_t end = items.size();
+    std::string next;
+    if (limit > 0 && offset + static_cast<size_t>(limit) < items.size()) {
+      end = offset + static_cast<size_t>(limit);
+      std::lock_guard<std::mutex> lk(list_mu);
+      if (snap_id == 0) {
+        const auto now = std::chrono::steady_clock::now();
+        for (auto it = list_snapshots.begin(); it != list_snapshots.end();) {
+          it = now > it->second.expires ? list_snapshots.erase(it) : std::next(it);
+        }
+        snap_id = next_list_id++;
+        list_snapshots[snap_id] = ListSnapshot{list_rv, items, now + std::chrono::milliseconds(opts.continue_ttl_ms)};
+      }
+      next = std::to_string(snap_id) + "." + std::to_string(end);
+    } else if (snap_id != 0) {
+      std::lock_guard<std::mutex> lk(list_mu);
+      list_snapshots.erase(snap_id);  // last page served
+    }
+    if (limit > 0) list_pages.fetch_add(1);
     std::string out = "{\"apiVersion\":" + json::quote(p.ti->rt.api_version()) + ",\"kind\":" +
-                      json::quote(p.ti->rt.kind + "List") + ",\"metadata\":{\"resourceVersion\":\"" +
-                      std::to_string(list_rv) + "\"},\"items\":[";
-    for (size_t i = 0; i < items.size(); ++i) {
-      if (i) out.push_back(',');
+                      json::quote(p.ti->rt.kind + "List") + ",\"metadata\":{\"resourceVersion\":\"" + rv_str(list_rv) +
+                      "\"";
+    if (!next.empty()) {
+      out += ",\"continue\":" + json::quote(next) +
+             ",\"remainingItemCount\":" + std::to_string(items.size() - end);
+    }
+    out += "},\"items\":[";
+    for (size_t i = offset; i < end; ++i) {
+      if (i != offset) out.push_back(',');
       items[i]->dump_to(out);
     }
     out += "]}";
@@ -1687,17 +1777,31 @@ struct ApiServer::Impl {
     int timeout_s = opts.max_watch_seconds;
     if (req.has_query_param("timeoutSeconds")) timeout_s = std::min(timeout_s, std::atoi(req.query_param("timeoutSeconds").c_str()));
     bool bookmarks = req.query_param("allowWatchBookmarks") == "true";
+    // Streaming lists (WatchList): sendInitialEvents=true replays the current state as
+    // ADDED events, then a BOOKMARK annotated k8s.io/initial-events-end marks the point
+    // where the initial state is complete (requires allowWatchBookmarks and
+    // resourceVersionMatch=NotOlderThan, as on a real apiserver).
+    const bool send_initial = req.query_param("sendInitialEvents") == "true";
+    if (send_initial && (!bookmarks || req.query_param("resourceVersionMatch") != "NotOlderThan")) {
+      throw StatusError(422, "Invalid",
+                        "sendInitialEvents requires allowWatchBookmarks=true and resourceVersionMatch=NotOlderThan");
+    }
+    uint64_t from = 0;
+    if (!rv_s.empty() && rv_s != "0" && !parse_rv(rv_s, &from)) {
+      throw StatusError(400, "BadRequest", "invalid resource version: " + rv_s);
+    }
     std::vector<std::shared_ptr<const std::string>> initial;
     bool gone = false;
     TypeStore& ts = *p.ti->store;
     uint64_t compacted = 0;
+    uint64_t initial_rv = 0;
     {
       // shared: no commit of this type can interleave between the snapshot/history scan and
       // the registration below
       SharedStoreLock lk(ts.mu, ts.stats);
       compacted = ts.compacted_rv;
-      uint64_t from = rv_s.empty() ? 0 : std::strtoull(rv_s.c_str(), nullptr, 10);
-      if (rv_s.empty() || rv_s == "0") {
+      initial_rv = rv.load();
+      if (rv_s.empty() || rv_s == "0" || send_initial) {
         for (auto& [k, st] : ts.objs) {
           const Value& meta = st.obj->get("metadata");
           if (!sub.ns.empty() && meta.get_string("namespace") != sub.ns) continue;
@@ -1735,7 +1839,7 @@ struct ApiServer::Impl {
     if (gone) {
       Value ev = Value::object({{"type", "ERROR"},
                                 {"object", status_body(410, "Expired", "too old resource version: " + rv_s + " (" +
-                                                                           std::to_string(compacted) + ")")}});
+                                                                           rv_str(compacted) + ")")}});
       w.write_chunk(ev.dump() + "\n");
       w.end_chunked();
       return;
@@ -1743,6 +1847,15 @@ struct ApiServer::Impl {
     bool ok = true;
     for (auto& l : initial) {
       if (!(ok = w.write_chunk(*l))) break;
+    }
+    if (ok && send_initial) {
+      Value bm = Value::object(
+          {{"type", "BOOKMARK"},
+           {"object", Value::object({{"kind", p.ti->rt.kind},
+                                     {"apiVersion", p.ti->rt.api_version()},
+                                     {"metadata", Value::object({{"resourceVersion", rv_str(initial_rv)},
+                                                                 {"annotations", Value::object({{"k8s.io/initial-events-end", "true"}})}})}})}});
+      ok = w.write_chunk(bm.dump() + "\n");
     }
     auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(timeout_s);
     auto next_bookmark = std::chrono::steady_clock::now() + std::chrono::milliseconds(opts.bookmark_interval_ms);
@@ -1790,7 +1903,7 @@ struct ApiServer::Impl {
         Value bm = Value::object({{"type", "BOOKMARK"},
                                   {"object", Value::object({{"kind", p.ti->rt.kind},
                                                             {"apiVersion", p.ti->rt.api_version()},
-                                                            {"metadata", Value::object({{"resourceVersion", std::to_string(cur_rv)}})}})}});
+                                                            {"metadata", Value::object({{"resourceVersion", rv_str(cur_rv)}})}})}});
         if (!w.write_chunk(bm.dump() + "\n")) break;
         next_bookmark = now + std::chrono::milliseconds(opts.bookmark_interval_ms);
       }
@@ -1864,8 +1977,15 @@ struct ApiServer::Impl {
       return true;
     }
     if (hit.status > 0) {
-      std::string reason = hit.status == 409 ? "Conflict" : hit.status == 410 ? "Expired" : hit.status >= 500 ? "InternalError" : "BadRequest";
-      w.send_json(hit.status, status_body(hit.status, reason, hit.message.empty() ? "injected fault" : hit.message).dump());
+      std::string reason = hit.status == 409   ? "Conflict"
+                           : hit.status == 410 ? "Expired"
+                           : hit.status == 429 ? "TooManyRequests"
+                           : hit.status >= 500 ? "InternalError"
+                                               : "BadRequest";
+      http::Headers extra;
+      if (hit.retry_after_s >= 0) extra.set("Retry-After", std::to_string(hit.retry_after_s));
+      w.send(hit.status, status_body(hit.status, reason, hit.message.empty() ? "injected fault" : hit.message).dump(),
+             "application/json", &extra);
       return true;
     }
     return false;
@@ -1886,6 +2006,7 @@ struct ApiServer::Impl {
         f.remaining = r.get("count").is_int() ? static_cast<int>(r.get("count").as_int()) : -1;
         f.message = r.get_string("message");
         f.reset = r.get("reset").is_bool() && r.get("reset").as_bool();
+        f.retry_after_s = r.get("retry_after").is_int() ? static_cast<int>(r.get("retry_after").as_int()) : -1;
         faults.push_back(std::move(f));
       }
       w.send_json(200, "{}");
@@ -1946,6 +2067,8 @@ struct ApiServer::Impl {
                                       {"watches", static_cast<unsigned long long>(n_watches)},
                                       {"requests", static_cast<unsigned long long>(requests.load())},
                                       {"faults_hit", static_cast<unsigned long long>(faults_hit.load())},
+                                      {"list_pages", static_cast<unsigned long long>(list_pages.load())},
+                                      {"resource_version", rv_str(rv.load())},
                                       {"gc_collected", static_cast<unsigned long long>(gc_collected.load())},
                                       {"gc_pending", static_cast<unsigned long long>([&] {
                                          std::lock_guard<std::mutex> g(gc_mu);

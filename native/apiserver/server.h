@@ -49,6 +49,13 @@ struct Options {
   // applied: a real apiserver answers a write only after etcd's raft commit + fsync
   // (typically 1-10 ms).  0 = in-memory speed.
   int64_t write_latency_us = 0;
+  // Opaque resourceVersions ("kl.<base36>" instead of decimal digits): clients must treat
+  // them as opaque strings, as the Kubernetes API contract says; this catches any that
+  // parse or compare them.
+  bool opaque_rv = false;
+  // Paginated LIST (limit/continue) serves later pages from a snapshot taken at the first
+  // page; continue tokens expire after this long (then 410 Expired, as etcd compaction).
+  int continue_ttl_ms = 60000;
 };
 
 class ApiServer {

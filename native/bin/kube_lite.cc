@@ -25,6 +25,7 @@ static void usage() {
                "usage: kube-lite [--addr A] [--port P] [--port-file F] [--token-file F] [--no-anonymous]\n"
                "                 [--tls-cert F --tls-key F] [--service-override ns/name=host:port]...\n"
                "                 [--bookmark-ms N] [--history N] [--watch-coalesce-us N] [--gc-workers N]\n"
+               "                 [--opaque-rv] [--continue-ttl-ms N]\n"
                "                 [--write-latency-ms F]\n"
                "                 [--manifest file.{json,yaml}]...\n");
 }
@@ -55,6 +56,8 @@ int main(int argc, char** argv) {
     else if (a == "--watch-coalesce-us") o.watch_coalesce_us = std::atoi(next().c_str());
     else if (a == "--gc-workers") o.gc_workers = std::atoi(next().c_str());
     else if (a == "--write-latency-ms") o.write_latency_us = static_cast<int64_t>(std::atof(next().c_str()) * 1000.0);
+    else if (a == "--opaque-rv") o.opaque_rv = true;
+    else if (a == "--continue-ttl-ms") o.continue_ttl_ms = std::atoi(next().c_str());
     else if (a == "--manifest") manifests.push_back(next());
     else if (a == "--service-override") {
       std::string v = next();

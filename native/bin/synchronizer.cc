@@ -5,6 +5,7 @@
 
 #include "core/cancel.h"
 #include "core/env_config.h"
+#include "kube/runtime.h"
 #include "core/http.h"
 #include "core/log.h"
 #include "core/process.h"
@@ -20,6 +21,13 @@ int main() {
   sync::Config cfg;
   try {
     cfg = sync::Config::from_env(EnvConfig("CONF_"));
+    {
+      EnvConfig env("CONF_");
+      kube::Watcher::Defaults wd;
+      wd.page_size = static_cast<int64_t>(env.u64_or("list_page_size", 500));
+      wd.streaming_lists = env.boolean_or("streaming_lists", false);
+      kube::Watcher::set_defaults(wd);
+    }
   } catch (const std::exception& e) {
     std::fprintf(stderr, "Error: %s\n", e.what());
     return 1;

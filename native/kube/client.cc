@@ -1,10 +1,14 @@
 #include "kube/client.h"
 
+#include <algorithm>
+#include <cctype>
 #include <cstdlib>
+#include <thread>
 #include <fstream>
 
 #include "core/crypto.h"
 #include "core/log.h"
+#include "core/metrics.h"
 #include "core/net.h"
 #include "core/yaml.h"
 
@@ -158,11 +162,30 @@ void throw_api_error(const http::Response& r) {
   throw ApiError(r.status, reason, msg, st);
 }
 
+// Seconds to wait before retrying a throttled response, or -1 when it is not one.
+static int retry_after_seconds(const http::Response& r, int cap) {
+  const std::string* ra = r.headers.get("Retry-After");
+  if (r.status != 429 && !(r.status >= 500 && r.status < 600 && ra)) return -1;
+  int secs = 1;
+  if (ra && !ra->empty() && std::isdigit(static_cast<unsigned char>((*ra)[0]))) secs = std::atoi(ra->c_str());
+  return std::clamp(secs, 0, cap);
+}
+
 http::Response KubeClient::raw(const std::string& method, const std::string& path, const std::string& body,
                                const std::string& content_type) {
-  http::Headers h = auth_headers();
-  if (!body.empty() || method == "POST" || method == "PUT" || method == "PATCH") h.set("Content-Type", content_type);
-  return http_->request(method, path, body, &h);
+  static auto& throttled = metrics::Registry::global().counter(
+      "bgc_kube_client_throttled_total", "Requests the apiserver throttled (429 / Retry-After) and that were retried");
+  for (int attempt = 0;; ++attempt) {
+    http::Headers h = auth_headers();
+    if (!body.empty() || method == "POST" || method == "PUT" || method == "PATCH") h.set("Content-Type", content_type);
+    http::Response r = http_->request(method, path, body, &h);
+    const int wait_s = retry_after_seconds(r, cfg_.max_retry_after_s);
+    if (wait_s < 0 || attempt >= cfg_.max_throttle_retries) return r;
+    throttled.inc();
+    throttled_.fetch_add(1);
+    LOG_DEBUG("kube") << method << " " << path << ": " << r.status << ", retrying after " << wait_s << "s";
+    std::this_thread::sleep_for(std::chrono::seconds(wait_s));
+  }
 }
 
 Value KubeClient::call(const std::string& method, const std::string& path, const std::string& body,
@@ -259,7 +282,9 @@ std::unique_ptr<http::StreamingResponse> KubeClient::watch(const ResourceType& r
                                                           {"labelSelector", o.label_selector},
                                                           {"fieldSelector", o.field_selector},
                                                           {"timeoutSeconds", std::to_string(o.timeout_seconds)},
-                                                          {"allowWatchBookmarks", o.allow_bookmarks ? "true" : ""}});
+                                                          {"allowWatchBookmarks", o.allow_bookmarks ? "true" : ""},
+                                                          {"sendInitialEvents", o.send_initial_events ? "true" : ""},
+                                                          {"resourceVersionMatch", o.send_initial_events ? "NotOlderThan" : ""}});
   http::Headers h = auth_headers();
   auto s = http_->stream("GET", path, &h);
   if (s->status < 200 || s->status >= 300) {

@@ -4,6 +4,7 @@
 // `replace_status` at src/synchronizer.rs:302, JSON patch at :323-330).
 #pragma once
 
+#include <atomic>
 #include <chrono>
 #include <memory>
 #include <mutex>
@@ -30,6 +31,11 @@ struct KubeConfig {
   std::string impersonate_user;
   std::vector<std::string> impersonate_groups;
   int timeout_ms = 30000;
+  // Throttling (HTTP 429, or 5xx with Retry-After): wait as the server asks — capped at
+  // max_retry_after_s, 1 s when no header — and retry up to this many times (client-go
+  // retries 429 with Retry-After up to 10 times).  0 = surface the error at once.
+  int max_throttle_retries = 10;
+  int max_retry_after_s = 10;
   std::string source;           // "in-cluster" | "kubeconfig:<path>" | "env"
 
   // Inference order (kube-client `Config::infer`): $BGC_KUBE_SERVER override (tests),
@@ -70,6 +76,9 @@ struct WatchOptions {
   std::string field_selector;
   int timeout_seconds = 290;
   bool allow_bookmarks = true;
+  // Streaming list: replay the current state as ADDED events, ended by a BOOKMARK
+  // annotated k8s.io/initial-events-end (sendInitialEvents + resourceVersionMatch).
+  bool send_initial_events = false;
 };
 
 class KubeClient {
@@ -106,6 +115,7 @@ class KubeClient {
   http::Response raw(const std::string& method, const std::string& path, const std::string& body = "",
                      const std::string& content_type = "application/json");
   const KubeConfig& config() const { return cfg_; }
+  uint64_t throttled() const { return throttled_.load(); }
 
  private:
   http::Headers auth_headers();
@@ -114,6 +124,7 @@ class KubeClient {
   std::mutex token_mu_;
   std::string token_;
   std::chrono::steady_clock::time_point token_read_{};
+  std::atomic<uint64_t> throttled_{0};
 };
 
 // Raises ApiError for a non-2xx response (parsing a metav1.Status body when present).

@@ -16,13 +16,67 @@ std::string meta_rv(const Value& obj) { return obj.get("metadata").get_string("r
 // ---------------------------------------------------------------------------
 // Watcher
 
+namespace {
+std::mutex g_watch_defaults_mu;
+Watcher::Defaults g_watch_defaults;
+}  // namespace
+
+void Watcher::set_defaults(Defaults d) {
+  std::lock_guard<std::mutex> lk(g_watch_defaults_mu);
+  g_watch_defaults = d;
+}
+
+Watcher::Defaults Watcher::defaults() {
+  std::lock_guard<std::mutex> lk(g_watch_defaults_mu);
+  return g_watch_defaults;
+}
+
 Watcher::Watcher(KubeClient& client, ResourceType rt, std::string ns, std::string label_selector,
                  std::string field_selector)
     : client_(client),
       rt_(std::move(rt)),
       ns_(std::move(ns)),
       selector_(std::move(label_selector)),
-      field_selector_(std::move(field_selector)) {}
+      field_selector_(std::move(field_selector)) {
+  const Defaults d = defaults();
+  page_size_ = d.page_size;
+  streaming_ = d.streaming_lists;
+}
+
+ObjPtr Watcher::typed(Value obj) const {
+  if (!obj.contains("apiVersion")) obj["apiVersion"] = rt_.api_version();
+  if (!obj.contains("kind")) obj["kind"] = rt_.kind;
+  return std::make_shared<const Value>(std::move(obj));
+}
+
+std::string Watcher::list_all(std::vector<ObjPtr>& out, CancelToken& stop) {
+  for (int attempt = 0;; ++attempt) {
+    out.clear();
+    ListOptions lo;
+    lo.label_selector = selector_;
+    lo.field_selector = field_selector_;
+    lo.limit = page_size_ > 0 ? page_size_ : 0;
+    std::string rv;
+    try {
+      do {
+        Value list = client_.list(rt_, ns_, lo);
+        list_pages_.fetch_add(1);
+        const Value& meta = list.get("metadata");
+        if (rv.empty()) rv = meta.get_string("resourceVersion");  // the first page's snapshot
+        lo.continue_token = meta.get_string("continue");
+        Value* items = list.find_mut("items");
+        if (items && items->is_array()) {
+          for (auto& item : items->items_mut()) out.push_back(typed(std::move(item)));
+        }
+      } while (!lo.continue_token.empty() && !stop.cancelled());
+      return rv;
+    } catch (const ApiError& e) {
+      // 410 on a continue token: the snapshot expired mid-list; start over
+      if (e.code() != 410 || lo.continue_token.empty() || attempt >= 3) throw;
+      LOG_INFO("kube::watcher") << rt_.plural << ": continue token expired, restarting the list";
+    }
+  }
+}
 
 void Watcher::run(CancelToken& stop, const std::function<void(const WatchEvent&)>& on_event) {
   std::string rv;
@@ -32,38 +86,47 @@ void Watcher::run(CancelToken& stop, const std::function<void(const WatchEvent&)
   auto& errors = metrics::Registry::global().counter("bgc_watch_errors_total", "Watch stream failures",
                                                      {{"resource", rt_.plural}});
   while (!stop.cancelled()) {
+    // Streaming list: the initial state arrives on this watch; objects collect here until
+    // the initial-events-end bookmark.
+    bool initial_phase = false;
+    std::vector<ObjPtr> initial;
     try {
-      if (need_list) {
-        ListOptions lo;
-        lo.label_selector = selector_;
-        lo.field_selector = field_selector_;
-        Value list = client_.list(rt_, ns_, lo);
-        rv = list.get("metadata").get_string("resourceVersion");
+      if (need_list && !streaming_) {
         WatchEvent ev{WatchEvent::Type::Restarted, nullptr, {}};
-        Value* items = list.find_mut("items");
-        std::vector<Value> none;
-        for (auto& item : items && items->is_array() ? items->items_mut() : none) {
-          Value obj = std::move(item);
-          if (!obj.contains("apiVersion")) obj["apiVersion"] = rt_.api_version();
-          if (!obj.contains("kind")) obj["kind"] = rt_.kind;
-          ev.objects.push_back(std::make_shared<const Value>(std::move(obj)));
-        }
+        rv = list_all(ev.objects, stop);
         on_event(ev);
         need_list = false;
         relists_.fetch_add(1);
       }
       WatchOptions wo;
-      wo.resource_version = rv;
       wo.label_selector = selector_;
       wo.field_selector = field_selector_;
-      auto stream = client_.watch(rt_, ns_, wo);
+      if (need_list) {  // streaming
+        wo.send_initial_events = true;
+        initial_phase = true;
+      } else {
+        wo.resource_version = rv;
+      }
+      std::unique_ptr<http::StreamingResponse> stream;
+      try {
+        stream = client_.watch(rt_, ns_, wo);
+      } catch (const ApiError& e) {
+        if (initial_phase && e.code() >= 400 && e.code() < 500 && e.code() != 410 && e.code() != 429) {
+          LOG_WARN("kube::watcher") << rt_.plural << ": streaming lists rejected (" << e.what()
+                                    << "); falling back to LIST";
+          streaming_ = false;
+          continue;
+        }
+        throw;
+      }
       backoff = std::chrono::milliseconds(800);
       std::string line;
       while (stream->next_line(line, &stop, 500)) {
         if (line.empty()) continue;
         // Events the consumer does not want are dropped before JSON parsing; ERROR and
-        // BOOKMARK lines always go through (they drive relists and resumption).
-        if (line_filter_ && !line_filter_(line) && line.find("\"type\":\"ERROR\"") == std::string::npos &&
+        // BOOKMARK lines always go through (they drive relists and resumption).  During
+        // a streaming list nothing is dropped: the initial state must be complete.
+        if (!initial_phase && line_filter_ && !line_filter_(line) && line.find("\"type\":\"ERROR\"") == std::string::npos &&
             line.find("\"type\":\"BOOKMARK\"") == std::string::npos) {
           continue;
         }
@@ -85,7 +148,22 @@ void Watcher::run(CancelToken& stop, const std::function<void(const WatchEvent&)
         }
         std::string new_rv = meta_rv(obj);
         if (!new_rv.empty()) rv = new_rv;
-        if (type == "BOOKMARK") continue;
+        if (type == "BOOKMARK") {
+          if (initial_phase &&
+              obj.get("metadata").get("annotations").get_string("k8s.io/initial-events-end") == "true") {
+            WatchEvent we{WatchEvent::Type::Restarted, nullptr, std::move(initial)};
+            initial.clear();
+            initial_phase = false;
+            need_list = false;
+            on_event(we);
+            relists_.fetch_add(1);
+          }
+          continue;
+        }
+        if (initial_phase) {
+          if (type == "ADDED") initial.push_back(typed(std::move(obj)));
+          continue;
+        }
         WatchEvent we{WatchEvent::Type::Added, std::make_shared<const Value>(std::move(obj)), {}};
         if (type == "MODIFIED") we.type = WatchEvent::Type::Modified;
         else if (type == "DELETED") we.type = WatchEvent::Type::Deleted;

@@ -46,12 +46,31 @@ std::string meta_name(const json::Value& obj);
 std::string meta_namespace(const json::Value& obj);
 std::string meta_rv(const json::Value& obj);
 
-// Runs LIST then WATCH forever (until cancelled), emitting events. 410 Gone / ERROR
-// events trigger a relist; connection failures back off exponentially (0.8s..30s).
+// Runs LIST then WATCH forever (until cancelled), emitting events. 410 Gone (an ERROR
+// event, or the HTTP status at watch start) triggers a relist; connection failures back
+// off exponentially (0.8s..30s).
+//
+// The initial state comes from a paginated LIST (limit=page_size, following continue
+// tokens; an expired token restarts the list — kube-runtime's watcher::Config default
+// of 500), or, with streaming lists on, from one WATCH with sendInitialEvents=true whose
+// initial ADDED events end at a BOOKMARK annotated k8s.io/initial-events-end (the
+// apiserver never materialises the whole list).  A server that rejects streaming lists
+// (4xx) makes the watcher fall back to LIST for good.
 class Watcher {
  public:
+  struct Defaults {
+    int64_t page_size = 500;   // 0 = unpaginated LIST
+    bool streaming_lists = false;
+  };
+  // Process-wide defaults (each binary sets them from CONF_LIST_PAGE_SIZE /
+  // CONF_STREAMING_LISTS before starting its watchers).
+  static void set_defaults(Defaults d);
+  static Defaults defaults();
+
   Watcher(KubeClient& client, ResourceType rt, std::string ns = "", std::string label_selector = "",
           std::string field_selector = "");
+  void set_page_size(int64_t n) { page_size_ = n; }
+  void set_streaming_lists(bool on) { streaming_ = on; }
   void run(CancelToken& stop, const std::function<void(const WatchEvent&)>& on_event);
   // Optional pre-parse filter on raw watch lines (e.g. a name prefix): ADDED/MODIFIED/
   // DELETED lines it rejects are skipped without JSON parsing.  A consumer whose filter
@@ -60,8 +79,15 @@ class Watcher {
   void set_line_filter(std::function<bool(std::string_view)> f) { line_filter_ = std::move(f); }
   uint64_t relists() const { return relists_.load(); }
   uint64_t reconnects() const { return reconnects_.load(); }
+  uint64_t list_pages() const { return list_pages_.load(); }
 
  private:
+  // Paginated LIST; returns the list resourceVersion.
+  std::string list_all(std::vector<ObjPtr>& out, CancelToken& stop);
+  ObjPtr typed(json::Value obj) const;
+  int64_t page_size_;
+  bool streaming_;
+  std::atomic<uint64_t> list_pages_{0};
   KubeClient& client_;
   ResourceType rt_;
   std::string ns_;

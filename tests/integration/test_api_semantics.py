@@ -1,0 +1,174 @@
+"""Real-apiserver semantics the product depends on, each with the
+controller and synchronizer converging through it:
+
+* opaque (non-numeric) resourceVersions;
+* paginated LIST (limit/continue) from a consistent snapshot, expired continue -> 410;
+* HTTP 410 at watch start (not only an ERROR event in the stream);
+* streaming lists: sendInitialEvents + the k8s.io/initial-events-end BOOKMARK;
+* 429 Too Many Requests with Retry-After, honoured by the client;
+* a non-force server-side apply that conflicts with another field manager -> 409.
+
+Reference call sites: watcher/reflector (src/controller.rs:233-246), SSA with force
+(src/controller.rs:67), replace_status + JSON patch (src/synchronizer.rs:217,302-330)."""
+import json
+import time
+
+import pytest
+import requests
+
+from bacchus_gpu_controller_amd.testing.cluster import Cluster
+from bacchus_gpu_controller_amd.testing.fake_google import FakeGoogle
+from bacchus_gpu_controller_amd.testing.kubeapi import ApiError, wait_for
+
+pytestmark = pytest.mark.slow
+
+
+def ub(name, **spec):
+    return {"apiVersion": "bacchus.io/v1", "kind": "UserBootstrap", "metadata": {"name": name},
+            "spec": spec or {"kube_username": name}}
+
+
+def metric(port, name):
+    text = requests.get(f"http://127.0.0.1:{port}/metrics", timeout=5).text
+    total = 0.0
+    for line in text.splitlines():
+        if line.startswith(name) and not line.startswith("#"):
+            total += float(line.rsplit(" ", 1)[1])
+    return total
+
+
+@pytest.fixture()
+def google():
+    g = FakeGoogle().start()
+    yield g
+    g.stop()
+
+
+def test_opaque_resource_versions_onboarding_converges(google):
+    google.set_rows([{"id_username": "opaq", "gpu": 2}])
+    with Cluster(apiserver_args=["--opaque-rv"], controller_env={"CONF_REQUEUE_SECS": "3600"}) as c:
+        c.as_user("oidc:opaq", ["gpu"]).create("userbootstraps", ub("opaq") | {"spec": {}})
+        c.start_synchronizer(google, interval=1, extra_env={"CONF_WATCH": "true"})
+        rb = wait_for(lambda: c.admin.get_or_none("rolebindings", "opaq", "opaq"), timeout=15, desc="rolebinding")
+        assert rb["metadata"]["resourceVersion"].startswith("kl.")
+        rq = c.admin.get("resourcequotas", "opaq", "opaq")
+        assert rq["spec"]["hard"]["requests.amd.com/gpu"] == "2"
+        # resume + relist with opaque versions: compaction forces every watcher to re-list
+        c.compact_and_drop_watches()
+        time.sleep(0.3)
+        c.as_user("oidc:opaq2", ["gpu"]).create("userbootstraps", ub("opaq2") | {"spec": {}})
+        wait_for(lambda: c.admin.get_or_none("namespaces", "opaq2"), timeout=15, desc="after relist")
+        # a numeric resourceVersion was never issued by this server
+        r = requests.get(c.server + "/apis/bacchus.io/v1/userbootstraps?watch=1&resourceVersion=12",
+                         headers={"Authorization": "Bearer admin-token"}, timeout=5)
+        assert r.status_code == 400
+        assert c.procs["controller"].alive() and c.procs["synchronizer"].alive()
+
+
+def test_paginated_list_snapshot_and_expired_continue():
+    with Cluster(admission=False, controller=False, apiserver_args=["--continue-ttl-ms", "1500"]) as c:
+        for i in range(25):
+            c.admin.create("userbootstraps", ub(f"p{i:02d}"))
+        base = c.server + "/apis/bacchus.io/v1/userbootstraps"
+        h = {"Authorization": "Bearer admin-token"}
+        p1 = requests.get(base + "?limit=10", headers=h, timeout=5).json()
+        assert len(p1["items"]) == 10 and p1["metadata"]["remainingItemCount"] == 15
+        rv1 = p1["metadata"]["resourceVersion"]
+        c.admin.create("userbootstraps", ub("p00a"))  # after the snapshot: not in later pages
+        names = [x["metadata"]["name"] for x in p1["items"]]
+        tok = p1["metadata"]["continue"]
+        while tok:
+            pg = requests.get(base + "?limit=10&continue=" + tok, headers=h, timeout=5).json()
+            assert pg["metadata"]["resourceVersion"] == rv1
+            names += [x["metadata"]["name"] for x in pg["items"]]
+            tok = pg["metadata"].get("continue")
+        assert names == [f"p{i:02d}" for i in range(25)]
+        p1 = requests.get(base + "?limit=5", headers=h, timeout=5).json()
+        time.sleep(2.0)
+        r = requests.get(base + "?limit=5&continue=" + p1["metadata"]["continue"], headers=h, timeout=5)
+        assert r.status_code == 410 and r.json()["reason"] == "Expired"
+        # the controller lists in pages of 7 and still provisions everyone
+        pages0 = c.stats()["list_pages"]
+        c.start_controller(extra_env={"CONF_LIST_PAGE_SIZE": "7", "CONF_REQUEUE_SECS": "3600"})
+        wait_for(lambda: all(c.admin.get_or_none("namespaces", f"p{i:02d}") for i in range(25)), timeout=20,
+                 desc="all namespaces")
+        assert c.stats()["list_pages"] - pages0 >= 4  # 26 UBs / 7 per page
+
+
+def test_http_410_at_watch_start_relists():
+    with Cluster(admission=False, controller_env={"CONF_REQUEUE_SECS": "3600"}) as c:
+        c.admin.create("userbootstraps", ub("g1"))
+        wait_for(lambda: c.admin.get_or_none("namespaces", "g1"), desc="g1")
+        # the next 3 watch requests for userbootstraps fail with HTTP 410 (no stream at all)
+        c.fault([{"method": "GET", "path": "userbootstraps.*watch=1", "status": 410, "count": 3}])
+        c.compact_and_drop_watches()
+        c.admin.create("userbootstraps", ub("g2"))
+        wait_for(lambda: c.admin.get_or_none("namespaces", "g2"), timeout=15, desc="g2 after 410s")
+        assert c.stats()["faults_hit"] >= 3
+        assert metric(c.controller_port, 'bgc_watch_errors_total{resource="userbootstraps"}') >= 3
+
+
+def test_streaming_lists_initial_events_end_bookmark():
+    with Cluster(admission=False, controller=False) as c:
+        for i in range(5):
+            c.admin.create("userbootstraps", ub(f"s{i}"))
+        base = c.server + "/apis/bacchus.io/v1/userbootstraps?watch=1&allowWatchBookmarks=true"
+        h = {"Authorization": "Bearer admin-token"}
+        r = requests.get(base + "&sendInitialEvents=true", headers=h, timeout=5)
+        assert r.status_code == 422  # resourceVersionMatch=NotOlderThan is required
+        with requests.get(base + "&sendInitialEvents=true&resourceVersionMatch=NotOlderThan&timeoutSeconds=1",
+                          headers=h, stream=True, timeout=10) as r:
+            events = [json.loads(line) for line in r.iter_lines() if line]
+        added = [e["object"]["metadata"]["name"] for e in events if e["type"] == "ADDED"]
+        bm = [e for e in events if e["type"] == "BOOKMARK"]
+        assert sorted(added) == [f"s{i}" for i in range(5)]
+        assert bm[0]["object"]["metadata"]["annotations"] == {"k8s.io/initial-events-end": "true"}
+        assert events.index(bm[0]) == 5  # after every initial ADDED
+        # the controller gets its initial state from streaming lists: no LIST request at all
+        pages0 = c.stats()["list_pages"]
+        c.start_controller(extra_env={"CONF_STREAMING_LISTS": "true", "CONF_REQUEUE_SECS": "3600"})
+        wait_for(lambda: all(c.admin.get_or_none("namespaces", f"s{i}") for i in range(5)), desc="pre-existing UBs")
+        c.admin.create("userbootstraps", ub("s9"))
+        wait_for(lambda: c.admin.get_or_none("namespaces", "s9"), desc="new UB")
+        assert c.stats()["list_pages"] == pages0
+
+
+def test_429_retry_after_is_honoured(google):
+    google.set_rows([{"id_username": "thr", "gpu": 1}])
+    with Cluster(admission=False, controller_env={"CONF_REQUEUE_SECS": "3600", "CONF_ERROR_REQUEUE_MS": "60000"}) as c:
+        # two throttled answers for the namespace apply, one for the status PUT
+        c.fault([{"method": "PATCH", "path": "/api/v1/namespaces/thr", "status": 429, "retry_after": 1, "count": 2},
+                 {"method": "PUT", "path": "userbootstraps/thr/status", "status": 429, "retry_after": 1, "count": 1}])
+        t0 = time.time()
+        c.admin.create("userbootstraps", ub("thr"))
+        # the error requeue is 60 s: converging within ~2 s proves the client retried itself
+        wait_for(lambda: c.admin.get_or_none("namespaces", "thr"), timeout=10, desc="namespace after 429s")
+        assert time.time() - t0 >= 1.9
+        assert metric(c.controller_port, "bgc_kube_client_throttled_total") == 2
+        assert metric(c.controller_port, 'bgc_reconcile_total{result="error"}') == 0
+        c.start_synchronizer(google, interval=60)
+        wait_for(lambda: c.admin.get("userbootstraps", "thr").get("status", {}).get("synchronized_with_sheet"),
+                 timeout=10, desc="status after 429")
+        assert metric(c.sync_port, "bgc_kube_client_throttled_total") == 1
+        assert c.procs["synchronizer"].alive()
+
+
+def test_non_force_apply_conflict_and_forced_reclaim():
+    with Cluster(admission=False, controller_env={"CONF_REQUEUE_SECS": "3600"}) as c:
+        c.admin.create("userbootstraps", ub("cf", kube_username="cf", quota={"hard": {"requests.cpu": "8"}}))
+        wait_for(lambda: c.admin.get_or_none("resourcequotas", "cf", "cf"), desc="quota")
+        url = c.server + "/api/v1/namespaces/cf/resourcequotas/cf?fieldManager=kubectl"
+        h = {"Authorization": "Bearer admin-token", "Content-Type": "application/apply-patch+yaml"}
+        body = {"apiVersion": "v1", "kind": "ResourceQuota", "metadata": {"name": "cf", "namespace": "cf"},
+                "spec": {"hard": {"requests.cpu": "64"}}}
+        r = requests.patch(url, data=json.dumps(body), headers=h, timeout=5)
+        assert r.status_code == 409 and "conflict with" in r.json()["message"]
+        assert "bacchus-gpu-controller.bacchus.io" in r.json()["message"]
+        r = requests.patch(url + "&force=true", data=json.dumps(body), headers=h, timeout=5)
+        assert r.status_code == 200 and r.json()["spec"]["hard"]["requests.cpu"] == "64"
+        # the foreign change is a child MODIFIED event: the controller re-applies with force
+        # and takes the field back (drift repair without waiting for the 30 s requeue)
+        rq = wait_for(lambda: (lambda q: q if q["spec"]["hard"]["requests.cpu"] == "8" else None)(
+            c.admin.get("resourcequotas", "cf", "cf")), desc="reclaimed")
+        managers = {m["manager"] for m in rq["metadata"]["managedFields"]}
+        assert "bacchus-gpu-controller.bacchus.io" in managers
