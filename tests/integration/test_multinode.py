@@ -109,3 +109,18 @@ def test_multinode_drain_flap_and_sync_convergence():
             assert not google.errors
     finally:
         google.stop()
+
+
+def test_flap_bench_mode_reports_convergence(tmp_path):
+    """BASELINE config #5 as a bench mode (bacchus_gpu_controller_amd/bench/flap.py): one
+    round at fast cadences; every phase converges and is reported."""
+    from bacchus_gpu_controller_amd.bench import flap
+
+    out = tmp_path / "flap.json"
+    assert flap.main(["--nodes", "2", "--tenants", "8", "--rounds", "2", "--poll-ms", "50", "--sheet-poll-ms", "300",
+                      "--churn-hz", "10", "--log-level", "warn", "--json-out", str(out)]) == 0
+    res = json.loads(out.read_text())
+    for k in ("drain_republish_ms", "flap_unhealthy_ms", "flap_recover_ms", "sheet_converge_ms"):
+        assert len(res[k]["samples"]) == 2 and res[k]["p50"] is not None, (k, res[k])
+    assert res["flap_unhealthy_ms"]["max"] < 5000 and res["sheet_converge_ms"]["max"] < 10000
+    assert all(res["processes_alive"].values()) and res["churn_created"] > 0
