@@ -40,7 +40,7 @@ def test_amdsmi_topology_ras_and_violations():
     # MI355X OAM: 7 xGMI links per GPU even when only one GPU is visible to us
     xgmi = [l for l in g["phys_links"] if l["type"] == "xgmi"]
     assert len(xgmi) >= 1, g["phys_links"]
-    assert all(l["peer_bdf"] for l in xgmi)
+    assert sum(1 for l in xgmi if l["peer_bdf"]) >= 1  # an all-ones peer BDF is reported as ""
     assert g["drm_render"] >= 128, g
     # the 32-bit legacy throttle word is the all-ones sentinel on MI355X: never exported
     assert ras["throttle_status"] != 0xFFFFFFFF
