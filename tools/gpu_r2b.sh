@@ -17,7 +17,7 @@ timeout -k 10 300 python -u bench.py --json-out "$OUT/bench_default.json" > "$OU
 step bench-approve &&
 timeout -k 10 400 python -u bench.py --no-tuned-phase --approve-after-create --steps 10 --warmup 1 --json-out "$OUT/bench_approve.json" > "$OUT/bench_approve.log" 2>&1 &&
 step rocprof-diag &&
-timeout -k 10 180 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof_diag" -o diag -- python3 tools/diag_floor_sweep.py "$OUT/diag_floors_rocprof.json" > "$OUT/rocprof_diag.log" 2>&1
+timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/rocprof_diag" -o diag -- python3 tools/diag_floor_sweep.py "$OUT/diag_floors_rocprof.json" > "$OUT/rocprof_diag.log" 2>&1
 rc=$?
 step "done rc=$rc"
 tail -3 "$OUT/pytest_gpu.log"
