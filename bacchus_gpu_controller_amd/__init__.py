@@ -29,6 +29,14 @@ _native_mod = None
 def native():
     """Return the compiled C++ core module, building it first if needed."""
     global _native_mod
+    if _native_mod is None and os.environ.get("BGC_NATIVE_MODULE"):
+        # a sanitizer build of the module (tools/sanitize.sh asan-py): same name, other file
+        from importlib import util as _util
+
+        spec = _util.spec_from_file_location("bacchus_gpu_controller_amd._native",
+                                                      os.environ["BGC_NATIVE_MODULE"])
+        _native_mod = _util.module_from_spec(spec)
+        spec.loader.exec_module(_native_mod)
     if _native_mod is None:
         try:
             _native_mod = importlib.import_module("bacchus_gpu_controller_amd._native")

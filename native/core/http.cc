@@ -1,5 +1,7 @@
 #include "core/http.h"
 
+#include <openssl/crypto.h>
+
 #include <fcntl.h>
 #include <netinet/in.h>
 #include <poll.h>
@@ -412,6 +414,10 @@ void Server::accept_loop() {
     active_.fetch_add(1);
     std::thread([this, fd, remote = std::string(host)] {
       serve_conn(fd, remote);
+      // OpenSSL keeps per-thread state (the thread's public/private DRBGs) that is only
+      // released by OPENSSL_thread_stop(): without it every TLS connection thread leaked
+      // ~0.1 KB (found by LeakSanitizer, tools/sanitize.sh asan).
+      if (opts_.tls) OPENSSL_thread_stop();
       // notify under the lock: once stop() observes active_==0 the Server (and the cv) may be destroyed
       std::lock_guard<std::mutex> lk(conns_mu_);
       active_.fetch_sub(1);

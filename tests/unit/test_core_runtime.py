@@ -252,3 +252,29 @@ def test_workqueue_forget_while_in_flight_drops_the_workers_requeue(nat):
     q.requeue("again", 30000)
     assert q.pending() == 2
     q.shutdown()
+
+
+def test_lsan_filter_keeps_only_native_leaks(tmp_path):
+    """tools/lsan_filter.py (tools/sanitize.sh asan-py): CPython's end-of-life allocations
+    are dropped, a leak with a frame in native/ or the _native module is reported."""
+    import subprocess
+    import sys
+
+    from bacchus_gpu_controller_amd import REPO_ROOT
+
+    log = tmp_path / "asan.1"
+    log.write_text(
+        "==1==ERROR: LeakSanitizer: detected memory leaks\n\n"
+        "Direct leak of 64 byte(s) in 1 object(s) allocated from:\n"
+        "    #0 0x7f in __interceptor_malloc asan_malloc_linux.cpp:145\n"
+        "    #1 0x55 in _PyObject_Malloc (/usr/bin/python3.10+0x1)\n\n"
+        "Direct leak of 32 byte(s) in 1 object(s) allocated from:\n"
+        "    #0 0x7f in operator new(unsigned long) asan_new_delete.cpp:95\n"
+        "    #1 0x7f in bgc::json::parse(std::string_view) /root/repo/native/core/json.cc:400\n"
+        "    #2 0x7f in pybind11::cpp_function::dispatcher (_native.cpython-310-x86_64-linux-gnu.so+0x1)\n\n")
+    tool = os.path.join(REPO_ROOT, "tools", "lsan_filter.py")
+    r = subprocess.run([sys.executable, tool, str(log)], capture_output=True, text=True)
+    assert r.returncode == 1 and "1 leak record(s)" in r.stderr and "json.cc:400" in r.stdout
+    log.write_text(log.read_text().split("Direct leak of 32")[0])
+    r = subprocess.run([sys.executable, tool, str(log)], capture_output=True, text=True)
+    assert r.returncode == 0 and "0 leak record(s)" in r.stderr

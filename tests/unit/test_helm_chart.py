@@ -266,3 +266,43 @@ def test_node_agent_diag_and_health_policy_env():
     assert env["CONF_POD_RESOURCES_SOCKET"] == "/var/lib/kubelet/pod-resources/kubelet.sock"
     mounts = {m["name"]: m["mountPath"] for m in pod["containers"][0]["volumeMounts"]}
     assert mounts["pod-resources"] == "/var/lib/kubelet/pod-resources"
+
+
+def test_each_component_runs_its_own_image():
+    """a slim control-plane image (no ROCm, no kube-lite) for the three
+    reference components, a ROCm runtime image only for the node agent."""
+    images = {}
+    for m in render():
+        if m.get("kind") in ("Deployment", "DaemonSet"):
+            for c in m["spec"]["template"]["spec"]["containers"]:
+                images[m["metadata"]["name"]] = (c["image"], c["command"])
+    cp = "ghcr.io/bacchus-snu/bacchus-gpu-controller:latest"
+    assert images["bgc-bacchus-gpu-controller"] == (cp, ["/app/controller"])
+    assert images["bgc-bacchus-gpu-admission"] == (cp, ["/app/admission"])
+    assert images["bgc-bacchus-gpu-synchronizer"] == (cp, ["/app/synchronizer"])
+    assert images["bgc-bacchus-gpu-node-agent"] == ("ghcr.io/bacchus-snu/bacchus-gpu-controller-node-agent:latest",
+                                                   ["/app/node-agent"])
+    over = {m["metadata"]["name"]: m for m in render({"nodeAgent": {"image": {"repository": "r/na", "tag": "v9"}}})
+            if m.get("kind") == "DaemonSet"}
+    assert over["bgc-bacchus-gpu-node-agent"]["spec"]["template"]["spec"]["containers"][0]["image"] == "r/na:v9"
+
+
+def test_dockerfile_targets_ship_only_production_binaries():
+    text = open(os.path.join(REPO_ROOT, "Dockerfile")).read()
+    stages = {}
+    cur = None
+    for line in text.splitlines():
+        if line.startswith("FROM "):
+            cur = line.split(" AS ")[-1].strip()
+            stages[cur] = []
+        elif cur:
+            stages[cur].append(line)
+    cp = "\n".join(stages["control-plane"])
+    node = "\n".join(stages["node-agent"])
+    assert stages["control-plane"] and "FROM ${CP_BASE} AS control-plane" in text and "CP_BASE=debian:stable-slim" in text
+    for b in ("controller", "admission", "synchronizer"):
+        assert f"/src/bin/{b}" in cp
+    for tool in ("kube-lite", "crdgen", "certgen", "rocm"):
+        assert tool not in cp.lower(), tool
+    assert "/app/node-agent" in node and "libbgc_gpu_diag.so" in node and "kube-lite" not in node
+    assert "-DBGC_PYTHON=OFF" in text
