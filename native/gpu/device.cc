@@ -512,6 +512,7 @@ class AmdSmiBackend : public Backend {
       api_.get_processor_handles(s, &n, ps.data());
       for (auto p : ps) handles_.push_back(p);
     }
+    for (size_t i = 0; i < handles_.size(); ++i) handle_mu_.push_back(std::make_unique<std::mutex>());
   }
   ~AmdSmiBackend() override {
     if (initialized_) api_.shut_down();
@@ -634,6 +635,7 @@ class AmdSmiBackend : public Backend {
   int busy_processes(int index) override {
     if (index < 0 || static_cast<size_t>(index) >= handles_.size() || !api_.process_list) return -1;
     // Processes other than this one (the agent's own diagnostics hold a HIP context).
+    std::lock_guard<std::mutex> hl(*handle_mu_[static_cast<size_t>(index)]);
     std::vector<amdsmi_proc_info_t> procs(64);
     uint32_t n = static_cast<uint32_t>(procs.size());
     amdsmi_status_t st = api_.process_list(handles_[static_cast<size_t>(index)], &n, procs.data());
@@ -677,6 +679,11 @@ class AmdSmiBackend : public Backend {
       return t;
     }
     auto h = handles_[static_cast<size_t>(index)];
+    // One call at a time per handle: the poller samples different handles concurrently
+    // (safe: libamd_smi/rocm_smi lock per device), while the diagnostics thread's
+    // busy_processes() may hit the same handle — serialized here instead of letting the
+    // library's device mutex answer AMDSMI_STATUS_BUSY.
+    std::lock_guard<std::mutex> hl(*handle_mu_[static_cast<size_t>(index)]);
     if (!api_.get_metrics) {
       t.error = "amdsmi_get_gpu_metrics_info unavailable";
       return t;
@@ -785,6 +792,7 @@ class AmdSmiBackend : public Backend {
   AmdSmiApi api_;
   bool initialized_ = false;
   std::vector<amdsmi_processor_handle> handles_;
+  std::vector<std::unique_ptr<std::mutex>> handle_mu_;  // per-handle call serialization
   std::mutex mu_;
 };
 
