@@ -269,12 +269,13 @@ current-context: {name}@kube-lite
         return p
 
     def start_node_agent(self, node_name="mi355x-0", max_gpus=0, backend="auto", n_mock_gpus=8, extra_env=None,
-                         poll_interval_ms=1000, hive_id=None, proc_name=None):
+                         poll_interval_ms=1000, hive_id=None, proc_name=None, fixture_obj=None):
         """Start the native node agent; amdsmi when available, else a mock MI355X hive.
         Several agents (one per synthetic node) may run side by side: each gets its own
         fixture file (`self.fixtures[node_name]`), process name and port."""
         fixture = os.path.join(self.workdir, f"gpus-{node_name}.json")
-        fx = native().default_mi355x_fixture(n_mock_gpus, *([hive_id] if hive_id is not None else []))
+        fx = (json.dumps(fixture_obj) if fixture_obj is not None
+              else native().default_mi355x_fixture(n_mock_gpus, *([hive_id] if hive_id is not None else [])))
         with open(fixture, "w") as f:
             f.write(fx)
         self.fixtures = getattr(self, "fixtures", {})

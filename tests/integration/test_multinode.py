@@ -124,3 +124,16 @@ def test_flap_bench_mode_reports_convergence(tmp_path):
         assert len(res[k]["samples"]) == 2 and res[k]["p50"] is not None, (k, res[k])
     assert res["flap_unhealthy_ms"]["max"] < 5000 and res["sheet_converge_ms"]["max"] < 10000
     assert all(res["processes_alive"].values()) and res["churn_created"] > 0
+
+
+def test_tp8_bench_mode_reports_coscheduling(tmp_path):
+    """BASELINE config #4 as a bench mode (bacchus_gpu_controller_amd/bench/tp8.py)."""
+    from bacchus_gpu_controller_amd.bench import tp8
+
+    out = tmp_path / "tp8.json"
+    assert tp8.main(["--nodes", "2", "--iters", "60", "--log-level", "warn", "--json-out", str(out)]) == 0
+    res = json.loads(out.read_text())
+    assert res["plan_tp8_groups"] == 2 and res["plan_groups_on_distinct_hives"]
+    assert res["churn_single_hive_share"] == 1.0 and res["two_quad_direct_xgmi_share"] == 1.0
+    assert res["preferred_8_us"]["p50"] > 0 and res["allocate_8_us"]["p50"] > 0
+    assert all(res["processes_alive"].values())
