@@ -264,7 +264,10 @@ X509Ptr make_cert(EVP_PKEY* subject_key, const std::string& cn, X509* issuer_cer
     add_ext(x.get(), iss, NID_key_usage, "critical,keyCertSign,cRLSign,digitalSignature");
   } else {
     add_ext(x.get(), iss, NID_basic_constraints, "critical,CA:FALSE");
-    add_ext(x.get(), iss, NID_key_usage, "critical,digitalSignature,keyEncipherment");
+    // keyEncipherment only means something for RSA key transport
+    add_ext(x.get(), iss, NID_key_usage,
+            EVP_PKEY_get_base_id(subject_key) == EVP_PKEY_RSA ? "critical,digitalSignature,keyEncipherment"
+                                                              : "critical,digitalSignature");
     add_ext(x.get(), iss, NID_ext_key_usage, "serverAuth,clientAuth");
     std::string san;
     for (const auto& d : dns) {
@@ -282,10 +285,12 @@ X509Ptr make_cert(EVP_PKEY* subject_key, const std::string& cn, X509* issuer_cer
 }  // namespace
 
 CertBundle make_ca_and_leaf(const std::string& common_name, const std::vector<std::string>& dns_names,
-                            int valid_days) {
-  PkeyPtr ca_key(EVP_RSA_gen(2048));
-  PkeyPtr leaf_key(EVP_RSA_gen(2048));
-  if (!ca_key || !leaf_key) throw std::runtime_error(ssl_error("RSA keygen"));
+                            int valid_days, const std::string& key_type) {
+  if (key_type != "ec" && key_type != "rsa") throw std::invalid_argument("key_type must be ec or rsa");
+  auto gen = [&]() -> EVP_PKEY* { return key_type == "ec" ? EVP_EC_gen("P-256") : EVP_RSA_gen(2048); };
+  PkeyPtr ca_key(gen());
+  PkeyPtr leaf_key(gen());
+  if (!ca_key || !leaf_key) throw std::runtime_error(ssl_error("keygen"));
   X509Ptr ca = make_cert(ca_key.get(), common_name + "-ca", nullptr, ca_key.get(), true, {}, 36500);
   X509Ptr leaf = make_cert(leaf_key.get(), common_name, ca.get(), ca_key.get(), false, dns_names, valid_days);
   CertBundle b;

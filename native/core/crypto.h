@@ -46,8 +46,11 @@ struct CertBundle {
 // Self-signed CA plus a leaf certificate signed by it (what the chart gets from
 // cert-manager, reference charts/.../templates/certificate.yaml:1-51). Used by tests,
 // the bench and `bgc-certgen`.
+// key_type "ec" (P-256, the default: a TLS handshake signs with ECDSA in ~30 us instead of
+// an RSA-2048 private-key operation of ~1 ms — the chart's cert-manager Certificate asks
+// for the same) or "rsa" (2048 bit).
 CertBundle make_ca_and_leaf(const std::string& common_name,
                             const std::vector<std::string>& dns_names,
-                            int valid_days = 90);
+                            int valid_days = 90, const std::string& key_type = "ec");
 
 }  // namespace bgc::crypto

@@ -93,15 +93,16 @@ PYBIND11_MODULE(_native, m) {
     auto k = bgc::crypto::generate_rsa(bits);
     return py::make_tuple(k.private_key_pem, k.public_key_pem);
   }, py::arg("bits") = 2048);
-  m.def("make_ca_and_leaf", [](const std::string& cn, const std::vector<std::string>& dns, int days) {
-    auto b = bgc::crypto::make_ca_and_leaf(cn, dns, days);
+  m.def("make_ca_and_leaf", [](const std::string& cn, const std::vector<std::string>& dns, int days,
+                               const std::string& key_type) {
+    auto b = bgc::crypto::make_ca_and_leaf(cn, dns, days, key_type);
     py::dict d;
     d["ca_cert"] = b.ca_cert_pem;
     d["ca_key"] = b.ca_key_pem;
     d["cert"] = b.cert_pem;
     d["key"] = b.key_pem;
     return d;
-  }, py::arg("common_name"), py::arg("dns_names"), py::arg("valid_days") = 90);
+  }, py::arg("common_name"), py::arg("dns_names"), py::arg("valid_days") = 90, py::arg("key_type") = "ec");
   m.def("uuid_v4", &bgc::crypto::uuid_v4);
 
   m.def("env_config", &env_config, py::arg("env"), py::arg("kind"));

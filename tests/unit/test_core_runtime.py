@@ -278,3 +278,19 @@ def test_lsan_filter_keeps_only_native_leaks(tmp_path):
     log.write_text(log.read_text().split("Direct leak of 32")[0])
     r = subprocess.run([sys.executable, tool, str(log)], capture_output=True, text=True)
     assert r.returncode == 0 and "0 leak record(s)" in r.stderr
+
+
+def test_cert_bundle_key_types(nat, tmp_path):
+    import subprocess
+
+    for kt, want in (("ec", "id-ecPublicKey"), ("rsa", "rsaEncryption")):
+        b = nat.make_ca_and_leaf("svc", ["svc.ns.svc", "127.0.0.1"], 30, kt)
+        (tmp_path / "ca.crt").write_text(b["ca_cert"])
+        (tmp_path / "leaf.crt").write_text(b["cert"])
+        txt = subprocess.run(["openssl", "x509", "-in", str(tmp_path / "leaf.crt"), "-noout", "-text"],
+                             capture_output=True, text=True, check=True).stdout
+        assert want in txt and "DNS:svc.ns.svc" in txt and "IP Address:127.0.0.1" in txt
+        assert ("Key Encipherment" in txt) == (kt == "rsa")
+        v = subprocess.run(["openssl", "verify", "-CAfile", str(tmp_path / "ca.crt"), str(tmp_path / "leaf.crt")],
+                           capture_output=True, text=True)
+        assert v.returncode == 0, v.stdout + v.stderr

@@ -306,3 +306,10 @@ def test_dockerfile_targets_ship_only_production_binaries():
         assert tool not in cp.lower(), tool
     assert "/app/node-agent" in node and "libbgc_gpu_diag.so" in node and "kube-lite" not in node
     assert "-DBGC_PYTHON=OFF" in text
+
+
+def test_webhook_certificates_use_ecdsa_keys():
+    certs = {m["metadata"]["name"]: m for m in render() if m.get("kind") == "Certificate"}
+    assert len(certs) == 2
+    for c in certs.values():
+        assert c["spec"]["privateKey"]["algorithm"] == "ECDSA" and c["spec"]["privateKey"]["size"] == 256
