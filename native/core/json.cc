@@ -1,5 +1,7 @@
 #include "core/json.h"
 
+#include <cctype>
+
 #include <algorithm>
 #include <charconv>
 #include <cmath>
@@ -792,6 +794,62 @@ class Parser {
   std::vector<Value>& vals_;
   std::vector<std::string>& keys_;
 };
+
+namespace {
+// index just past the string that starts at text[i] == '"'
+size_t skip_string(std::string_view t, size_t i) {
+  for (++i; i < t.size(); ++i) {
+    if (t[i] == '\\') ++i;
+    else if (t[i] == '"') return i + 1;
+  }
+  return t.size();
+}
+// index just past the value that starts at text[i]
+size_t skip_value(std::string_view t, size_t i) {
+  if (i >= t.size()) return i;
+  if (t[i] == '"') return skip_string(t, i);
+  if (t[i] == '{' || t[i] == '[') {
+    int depth = 0;
+    for (; i < t.size(); ++i) {
+      const char c = t[i];
+      if (c == '"') {
+        i = skip_string(t, i) - 1;
+      } else if (c == '{' || c == '[') {
+        ++depth;
+      } else if (c == '}' || c == ']') {
+        if (--depth == 0) return i + 1;
+      }
+    }
+    return t.size();
+  }
+  while (i < t.size() && t[i] != ',' && t[i] != '}' && t[i] != ']' && !std::isspace(static_cast<unsigned char>(t[i]))) ++i;
+  return i;
+}
+size_t skip_ws(std::string_view t, size_t i) {
+  while (i < t.size() && std::isspace(static_cast<unsigned char>(t[i]))) ++i;
+  return i;
+}
+}  // namespace
+
+std::string_view raw_member(std::string_view t, std::string_view key) {
+  size_t i = skip_ws(t, 0);
+  if (i >= t.size() || t[i] != '{') return {};
+  ++i;
+  while (true) {
+    i = skip_ws(t, i);
+    if (i >= t.size() || t[i] != '"') return {};
+    const size_t k0 = i + 1, k1 = skip_string(t, i);
+    const std::string_view k = t.substr(k0, k1 - 1 - k0);  // raw (escaped) key text
+    i = skip_ws(t, k1);
+    if (i >= t.size() || t[i] != ':') return {};
+    i = skip_ws(t, i + 1);
+    const size_t v0 = i, v1 = skip_value(t, i);
+    if (k == key) return t.substr(v0, v1 - v0);
+    i = skip_ws(t, v1);
+    if (i >= t.size() || t[i] != ',') return {};
+    ++i;
+  }
+}
 
 Value parse(std::string_view text) { return Parser(text).parse_document(); }
 Value parse(std::string_view text, std::string_view drop_key) { return Parser(text, drop_key).parse_document(); }

@@ -139,6 +139,11 @@ Value parse(std::string_view text);
 Value parse(std::string_view text, std::string_view drop_key);
 // Parses; returns false (and fills err) instead of throwing.
 bool try_parse(std::string_view text, Value& out, std::string* err = nullptr);
+// Raw text of a top-level object member's value (structural scan: no parsing, no
+// allocation), e.g. raw_member(review, "request") for logging a received document
+// without re-serializing it.  Empty when `text` is not an object or has no such key;
+// assumes `text` is valid JSON (run it through parse first).
+std::string_view raw_member(std::string_view text, std::string_view key);
 
 void escape_string(std::string_view s, std::string& out);
 std::string quote(std::string_view s);

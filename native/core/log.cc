@@ -6,8 +6,16 @@
 #include <cstdio>
 #include <cstdlib>
 #include <ctime>
+#include <condition_variable>
+#include <memory>
 #include <mutex>
+#include <thread>
 #include <vector>
+
+#include <cerrno>
+#include <csignal>
+#include <pthread.h>
+#include <unistd.h>
 
 namespace bgc::log {
 
@@ -18,11 +26,92 @@ struct Directive {
   Level level;
 };
 
-std::mutex g_mu;
-std::vector<Directive> g_directives;  // sorted: longest target first
+std::mutex g_mu;  // serializes init()
+// Directive sets are immutable once published: enabled() reads the current one through
+// an atomic pointer with no lock (it runs on every log statement of every thread; the
+// mutex it used to take showed up as lock contention in the control-plane profiles).
+// Replaced sets are kept alive (init() runs once per process outside tests).
+std::atomic<const std::vector<Directive>*> g_directives{nullptr};  // sorted: longest target first
+std::vector<std::unique_ptr<const std::vector<Directive>>> g_retired;  // guarded by g_mu
 std::atomic<int> g_min_level{static_cast<int>(Level::Info)};
 std::atomic<bool> g_initialized{false};
-void (*g_sink)(const std::string&) = nullptr;
+std::atomic<void (*)(const std::string&)> g_sink{nullptr};
+
+// Asynchronous stderr writer: log lines are appended to a buffer and one thread writes
+// them in batches (one write(2) per batch instead of one per line through stdio's stderr
+// lock).  ERROR lines, and everything before them, are written synchronously; the buffer
+// is flushed at exit and by log::flush().  BGC_LOG_SYNC=1 writes every line directly.
+class AsyncWriter {
+ public:
+  static AsyncWriter& instance() {
+    static AsyncWriter* w = new AsyncWriter();  // never destroyed: usable from atexit handlers
+    return *w;
+  }
+  void append(const std::string& line, bool sync) {
+    std::unique_lock<std::mutex> lk(mu_);
+    buf_ += line;
+    if (sync || buf_.size() >= kMaxBuffered) {
+      flush_locked(lk);
+      return;
+    }
+    if (!thread_started_) start_locked();
+    if (!wake_pending_) {
+      wake_pending_ = true;
+      cv_.notify_one();
+    }
+  }
+  void flush() {
+    std::unique_lock<std::mutex> lk(mu_);
+    flush_locked(lk);
+  }
+
+ private:
+  static constexpr size_t kMaxBuffered = 1 << 20;
+  AsyncWriter() { std::atexit([] { AsyncWriter::instance().flush(); }); }
+  void start_locked() {
+    thread_started_ = true;
+    std::thread([this] {
+      // the writer must not take signals meant for the services' shutdown handling
+      sigset_t all;
+      sigfillset(&all);
+      pthread_sigmask(SIG_BLOCK, &all, nullptr);
+      std::unique_lock<std::mutex> lk(mu_);
+      while (true) {
+        cv_.wait(lk, [&] { return wake_pending_; });
+        // let a burst of lines from other threads accumulate into one write
+        lk.unlock();
+        std::this_thread::sleep_for(std::chrono::microseconds(500));
+        lk.lock();
+        wake_pending_ = false;
+        flush_locked(lk);
+      }
+    }).detach();
+  }
+  void flush_locked(std::unique_lock<std::mutex>& lk) {
+    if (buf_.empty()) return;
+    std::string out;
+    out.swap(buf_);
+    // write outside the buffer lock would reorder with a concurrent synchronous flush;
+    // writes are rare (batched), so keep them under it
+    size_t off = 0;
+    while (off < out.size()) {
+      ssize_t n = ::write(2, out.data() + off, out.size() - off);
+      if (n <= 0) {
+        if (n < 0 && errno == EINTR) continue;
+        break;
+      }
+      off += static_cast<size_t>(n);
+    }
+    (void)lk;
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::string buf_;
+  bool wake_pending_ = false;
+  bool thread_started_ = false;
+};
+
+bool g_sync_writes = std::getenv("BGC_LOG_SYNC") && std::string(std::getenv("BGC_LOG_SYNC")) == "1";
 
 bool parse_level(std::string s, Level& out) {
   for (auto& c : s) c = static_cast<char>(std::tolower(static_cast<unsigned char>(c)));
@@ -85,10 +174,14 @@ void init(const std::string& spec) {
   int mn = static_cast<int>(Level::Off);
   for (auto& d : ds) mn = std::min(mn, static_cast<int>(d.level));
   std::lock_guard<std::mutex> lk(g_mu);
-  g_directives = std::move(ds);
+  auto next = std::make_unique<const std::vector<Directive>>(std::move(ds));
+  g_directives.store(next.get(), std::memory_order_release);
+  g_retired.push_back(std::move(next));
   g_min_level.store(mn);
   g_initialized.store(true);
 }
+
+void flush() { AsyncWriter::instance().flush(); }
 
 void init_from_env(const char* var) {
   const char* v = std::getenv(var);
@@ -98,8 +191,9 @@ void init_from_env(const char* var) {
 bool enabled(Level lvl, std::string_view target) {
   if (!g_initialized.load(std::memory_order_relaxed)) init_from_env();
   if (static_cast<int>(lvl) < g_min_level.load(std::memory_order_relaxed)) return false;
-  std::lock_guard<std::mutex> lk(g_mu);
-  for (const auto& d : g_directives) {
+  const std::vector<Directive>* ds = g_directives.load(std::memory_order_acquire);
+  if (!ds) return false;
+  for (const auto& d : *ds) {
     if (d.target.empty() ||
         (target.substr(0, d.target.size()) == d.target &&
          (target.size() == d.target.size() || target.substr(d.target.size(), 2) == "::"))) {
@@ -109,7 +203,10 @@ bool enabled(Level lvl, std::string_view target) {
   return false;
 }
 
-void set_sink(void (*sink)(const std::string&)) { g_sink = sink; }
+void set_sink(void (*sink)(const std::string&)) {
+  flush();
+  g_sink.store(sink);
+}
 
 void write(Level lvl, std::string_view target, std::string_view msg) {
   auto now = std::chrono::system_clock::now();
@@ -125,11 +222,11 @@ void write(Level lvl, std::string_view target, std::string_view msg) {
   line.reserve(msg.size() + target.size() + 48);
   line.append(ts).append(" ").append(level_name(lvl)).append(" ");
   line.append(target).append(": ").append(msg).push_back('\n');
-  if (g_sink) {
-    g_sink(line);
+  if (auto sink = g_sink.load()) {
+    sink(line);
     return;
   }
-  std::fwrite(line.data(), 1, line.size(), stderr);
+  AsyncWriter::instance().append(line, g_sync_writes || lvl >= Level::Error);
 }
 
 }  // namespace bgc::log

@@ -23,6 +23,9 @@ bool enabled(Level lvl, std::string_view target);
 void write(Level lvl, std::string_view target, std::string_view msg);
 // Redirect output (tests); nullptr restores stderr.
 void set_sink(void (*sink)(const std::string& line));
+// Writes buffered lines now (lines go to stderr in batches from a writer thread; ERROR
+// lines and exit flush automatically).
+void flush();
 
 class Line {
  public:

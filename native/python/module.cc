@@ -78,6 +78,9 @@ PYBIND11_MODULE(_native, m) {
   m.def("json_roundtrip", &json_roundtrip, py::arg("text"), py::arg("drop_key") = "");
   m.def("yaml_to_json", &yaml_to_json);
   m.def("json_to_yaml", &json_to_yaml);
+  m.def("json_raw_member", [](const std::string& text, const std::string& key) {
+    return std::string(bgc::json::raw_member(text, key));
+  });
   m.def("apply_json_patch", &apply_json_patch);
   m.def("apply_merge_patch", &apply_merge_patch);
 

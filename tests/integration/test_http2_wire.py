@@ -201,7 +201,9 @@ def test_client_reset_ends_list_and_watch(nat, plugin):
                 break
         c.send(frame(RST, 0, 1, struct.pack(">I", 8)))  # CANCEL
         # a health flip after the reset is not written to the cancelled stream, and the
-        # connection stays usable for new calls
+        # connection stays usable for new calls.  (Give the server a moment to read the
+        # RST_STREAM first: a flip racing it may legally still be in flight.)
+        time.sleep(0.2)
         plugin.set_health([False] + [True] * 7)
         time.sleep(0.3)
         c.send(frame(HEADERS, END_HEADERS, 3, request_headers(nat, "/v1beta1.DevicePlugin/GetDevicePluginOptions")))

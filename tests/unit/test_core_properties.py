@@ -126,3 +126,16 @@ def test_yaml_block_scalars_roundtrip_in_both_parsers(nat, v):
     y = nat.json_to_yaml(json.dumps(v))
     assert json.loads(nat.yaml_to_json(y)) == v
     assert yaml.safe_load(y) == v
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.dictionaries(KEYS, json_values(st.none() | st.booleans() | I64 | TEXT), max_size=6), st.booleans())
+def test_raw_member_matches_parse(nat, obj, pretty):
+    """json::raw_member (admission logs the received request without re-serializing it):
+    the raw slice of every top-level member parses to that member's value."""
+    text = json.dumps(obj, indent=1 if pretty else None, ensure_ascii=False)
+    for k, v in obj.items():
+        raw = nat.json_raw_member(text, json.dumps(k, ensure_ascii=False)[1:-1])
+        assert json.loads(raw) == v
+    assert nat.json_raw_member(text, "\x00missing") == ""
+    assert nat.json_raw_member("[1, 2]", "a") == ""
