@@ -21,6 +21,7 @@ Config Config::from_env(const EnvConfig& env) {
   c.child_delete_delay_ms = static_cast<int64_t>(env.u64_or("child_delete_delay_ms", 50));
   c.requeue_secs = static_cast<int64_t>(env.u64_or("requeue_secs", 30));
   c.error_requeue_ms = static_cast<int64_t>(env.u64_or("error_requeue_ms", 3000));
+  c.error_backoff_base_ms = static_cast<int64_t>(env.u64_or("error_backoff_base_ms", 0));
   c.lease = kube::LeaseSettings::from_env(env, "bacchus-gpu-controller");
   return c;
 }
@@ -112,6 +113,7 @@ void Reconciler::forget(const kube::ResourceType& rt, const Value& child) {
 }
 
 void Reconciler::forget_owner_locked(const std::string& owner) {
+  failures_.erase(owner);
   std::string ns = owner;
   for (auto& ch : ns) ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
   ub_state_.erase(owner);
@@ -236,6 +238,7 @@ kube::Action Reconciler::reconcile(const kube::ObjPtr& ub_ptr) {
   }
   {
     std::lock_guard<std::mutex> lk(mu_);
+    if (!failures_.empty()) failures_.erase(owner_name);
     if (!owner_live(owner_name, owner_uid)) {
       forget_owner_locked(owner_name);
     } else if (cfg_.skip_unchanged) {
@@ -289,7 +292,17 @@ kube::Action Reconciler::error_policy(const kube::ObjPtr& ub, const std::excepti
   const Value& meta = ub->get("metadata");
   LOG_ERROR("controller") << "error reconciling \"" << meta.get_string("namespace", "<unknown>") << "/"
                           << meta.get_string("name", "<unknown>") << "\": " << err.what();
-  return kube::Action::requeue_after(std::chrono::milliseconds(cfg_.error_requeue_ms));
+  int64_t delay = cfg_.error_requeue_ms;
+  if (cfg_.error_backoff_base_ms > 0) {
+    int n;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      n = ++failures_[meta.get_string("name")];
+    }
+    const int shift = std::min(n - 1, 30);
+    delay = std::min<int64_t>(cfg_.error_requeue_ms, cfg_.error_backoff_base_ms << shift);
+  }
+  return kube::Action::requeue_after(std::chrono::milliseconds(delay));
 }
 
 }  // namespace bgc::controller

@@ -43,6 +43,11 @@ struct Config {
   bool parallel_children = true;
   int64_t requeue_secs = 30;
   int64_t error_requeue_ms = 3000;
+  // Optional per-UB exponential backoff on errors: the n-th consecutive
+  // failure requeues after min(error_requeue_ms, base * 2^(n-1)), so a transient apiserver
+  // error is retried in milliseconds while a persistent one settles at the reference's
+  // 3 s.  0 = the reference's fixed error_requeue_ms (controller.rs:174).
+  int64_t error_backoff_base_ms = 0;
   int64_t child_delete_delay_ms = 50;
   kube::LeaseSettings lease;  // optional leader election (CONF_LEADER_ELECTION, ...)
   // reference fields are required (controller.rs:24-28); the rest default
@@ -101,6 +106,7 @@ class Reconciler {
   ThreadPool pool_;
   mutable std::mutex mu_;
   std::unordered_map<std::string, Applied> last_applied_;
+  std::unordered_map<std::string, int> failures_;  // consecutive errors per UB (backoff)
   // Fast path for periodic resyncs: after a fully successful reconcile, the UB's
   // resourceVersion and each child's resourceVersion. A later reconcile of the same UB
   // version whose children are still at those versions in the watch cache does nothing.

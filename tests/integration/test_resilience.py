@@ -166,3 +166,15 @@ def test_graceful_shutdown_exit_codes():
         for name in ("controller", "admission"):
             codes[name] = c.procs[name].stop(timeout=20)
         assert codes == {"controller": 0, "admission": 0}
+
+
+def test_error_backoff_retries_transient_errors_fast():
+    """CONF_ERROR_BACKOFF_BASE_MS: consecutive failures requeue after
+    50, 100, 200 ms ... capped at the reference's 3 s, instead of 3 s each."""
+    with Cluster(admission=False, controller_env={"CONF_ERROR_BACKOFF_BASE_MS": "50"}) as c:
+        c.fault([{"method": "PATCH", "path": "/api/v1/namespaces/bk1", "status": 500, "count": 4}])
+        t0 = time.time()
+        c.admin.create("userbootstraps", ub("bk1"))
+        wait_for(lambda: c.admin.get_or_none("namespaces", "bk1"), timeout=10, desc="bk1 after 4 errors")
+        # 50+100+200+400 ms of backoff (+ the client's own latency); fixed requeues: >= 12 s
+        assert time.time() - t0 < 3.0
