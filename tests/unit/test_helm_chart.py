@@ -313,3 +313,18 @@ def test_webhook_certificates_use_ecdsa_keys():
     assert len(certs) == 2
     for c in certs.values():
         assert c["spec"]["privateKey"]["algorithm"] == "ECDSA" and c["spec"]["privateKey"]["size"] == 256
+
+
+def test_admission_pdb_and_optional_metrics():
+    pdb = [m for m in render() if m.get("kind") == "PodDisruptionBudget"]
+    assert len(pdb) == 1 and pdb[0]["spec"]["minAvailable"] == 1
+    assert pdb[0]["spec"]["selector"]["matchLabels"]["app.kubernetes.io/component"] == "admission"
+    assert not [m for m in render() if m.get("kind") == "ServiceMonitor" or m["metadata"]["name"].endswith("-metrics")]
+    ms = render({"metrics": {"enabled": True, "serviceMonitor": {"enabled": True, "labels": {"release": "prom"}}}})
+    svcs = {m["metadata"]["name"]: m for m in ms if m.get("kind") == "Service" and m["metadata"]["name"].endswith("-metrics")}
+    assert set(svcs) == {"bgc-bacchus-gpu-controller-metrics", "bgc-bacchus-gpu-synchronizer-metrics",
+                         "bgc-bacchus-gpu-node-agent-metrics"}
+    assert svcs["bgc-bacchus-gpu-node-agent-metrics"]["spec"]["ports"][0]["port"] == 12324
+    assert svcs["bgc-bacchus-gpu-controller-metrics"]["spec"]["selector"]["app.kubernetes.io/component"] == "controller"
+    sm = [m for m in ms if m.get("kind") == "ServiceMonitor"][0]
+    assert sm["metadata"]["labels"]["release"] == "prom" and sm["spec"]["endpoints"][0]["path"] == "/metrics"
