@@ -11,6 +11,7 @@
 
 #include "core/log.h"
 #include "core/metrics.h"
+#include "core/net.h"
 #include "core/protobuf.h"
 
 namespace bgc::gpu {
@@ -157,6 +158,11 @@ std::string encode_allocate_response(const std::vector<ContainerAllocation>& con
       cw.message(3, dw);
     }
     for (const auto& [k, v] : c.annotations) cw.map_entry(4, k, v);
+    for (const auto& name : c.cdi_devices) {
+      Writer dw;
+      dw.str(1, name);
+      cw.message(5, dw);
+    }
     w.message(1, cw);
   }
   return w.take();
@@ -173,6 +179,12 @@ std::vector<ContainerAllocation> decode_allocate_response(std::string_view buf) 
       switch (cr.field()) {
         case 1: c.envs.insert(pb::read_map_entry(cr.bytes_value())); break;
         case 4: c.annotations.insert(pb::read_map_entry(cr.bytes_value())); break;
+        case 5: {
+          Reader nr(cr.bytes_value());
+          while (nr.next())
+            if (nr.field() == 1) c.cdi_devices.push_back(nr.string_value());
+          break;
+        }
         case 2: {
           Mount m;
           Reader mr(cr.bytes_value());
@@ -572,9 +584,31 @@ void DevicePlugin::set_health(const std::vector<bool>& healthy) {
   cv_.notify_all();
 }
 
+std::pair<std::string, std::string> DevicePlugin::drm_node_names(size_t gi) const {
+  const GpuInfo& g = gpus_[gi];
+  std::string card, render;
+  if (shared_bdf_[gi]) {
+    // A compute partition: the BDF's DRM nodes belong to partition 0, so only the
+    // minors amdsmi reported for this logical device are correct.
+    if (g.drm_render <= 0) {
+      throw std::invalid_argument(cfg_.resource_name + " device " + ids_[gi] +
+                                  " shares its PCI function with another partition and its render node is unknown");
+    }
+    render = "renderD" + std::to_string(g.drm_render);
+    if (g.drm_card >= 0) card = "card" + std::to_string(g.drm_card);
+  } else {
+    drm_nodes(cfg_.sysfs_root, g.bdf, &card, &render);
+    if (render.empty() && g.drm_render > 0) render = "renderD" + std::to_string(g.drm_render);
+    if (card.empty() && g.drm_card >= 0) card = "card" + std::to_string(g.drm_card);
+  }
+  if (card.empty()) card = "card" + std::to_string(g.index);
+  if (render.empty()) render = "renderD" + std::to_string(128 + g.index);
+  return {card, render};
+}
+
 dp::ContainerAllocation DevicePlugin::allocate(const std::vector<std::string>& req_ids) const {
   dp::ContainerAllocation c;
-  c.devices.push_back({"/dev/kfd", join_path(cfg_.dev_root, "kfd"), "rw"});
+  if (!cfg_.cdi) c.devices.push_back({"/dev/kfd", join_path(cfg_.dev_root, "kfd"), "rw"});
   std::set<uint64_t> hives;
   std::string id_list;
   for (const auto& id : req_ids) {
@@ -582,25 +616,14 @@ dp::ContainerAllocation DevicePlugin::allocate(const std::vector<std::string>& r
     if (it == ids_.end()) throw std::invalid_argument("unknown " + cfg_.resource_name + " device id " + id);
     const size_t gi = static_cast<size_t>(it - ids_.begin());
     const GpuInfo& g = gpus_[gi];
-    std::string card, render;
-    if (shared_bdf_[gi]) {
-      // A compute partition: the BDF's DRM nodes belong to partition 0, so only the
-      // minors amdsmi reported for this logical device are correct.
-      if (g.drm_render <= 0) {
-        throw std::invalid_argument(cfg_.resource_name + " device " + id +
-                                    " shares its PCI function with another partition and its render node is unknown");
-      }
-      render = "renderD" + std::to_string(g.drm_render);
-      if (g.drm_card >= 0) card = "card" + std::to_string(g.drm_card);
+    if (cfg_.cdi) {
+      if (shared_bdf_[gi] && g.drm_render <= 0) (void)drm_node_names(gi);  // same refusal as device specs
+      c.cdi_devices.push_back(cfg_.resource_name + "=" + id);
     } else {
-      drm_nodes(cfg_.sysfs_root, g.bdf, &card, &render);
-      if (render.empty() && g.drm_render > 0) render = "renderD" + std::to_string(g.drm_render);
-      if (card.empty() && g.drm_card >= 0) card = "card" + std::to_string(g.drm_card);
+      const auto [card, render] = drm_node_names(gi);
+      c.devices.push_back({"/dev/dri/" + card, join_path(cfg_.dev_root, "dri/" + card), "rw"});
+      c.devices.push_back({"/dev/dri/" + render, join_path(cfg_.dev_root, "dri/" + render), "rw"});
     }
-    if (card.empty()) card = "card" + std::to_string(g.index);
-    if (render.empty()) render = "renderD" + std::to_string(128 + g.index);
-    c.devices.push_back({"/dev/dri/" + card, join_path(cfg_.dev_root, "dri/" + card), "rw"});
-    c.devices.push_back({"/dev/dri/" + render, join_path(cfg_.dev_root, "dri/" + render), "rw"});
     hives.insert(g.xgmi_hive_id);
     if (!id_list.empty()) id_list += ",";
     id_list += id;
@@ -611,6 +634,48 @@ dp::ContainerAllocation DevicePlugin::allocate(const std::vector<std::string>& r
   c.envs["BGC_AMD_GPU_XGMI_HIVES"] = hive_list;
   c.envs["BGC_AMD_GPU_SINGLE_XGMI_HIVE"] = hives.size() <= 1 ? "true" : "false";
   return c;
+}
+
+json::Value cdi_spec(const std::string& kind, const std::vector<GpuInfo>& gpus, const std::vector<std::string>& ids,
+                     const std::vector<std::pair<std::string, std::string>>& nodes) {
+  json::Value devs = json::Value::array();
+  for (size_t i = 0; i < gpus.size() && i < ids.size() && i < nodes.size(); ++i) {
+    json::Value dn = json::Value::array();
+    dn.push_back(json::Value::object({{"path", "/dev/dri/" + nodes[i].first}}));
+    dn.push_back(json::Value::object({{"path", "/dev/dri/" + nodes[i].second}}));
+    devs.push_back(json::Value::object({{"name", ids[i]},
+                                        {"containerEdits", json::Value::object({{"deviceNodes", dn}})}}));
+  }
+  return json::Value::object(
+      {{"cdiVersion", "0.6.0"},
+       {"kind", kind},
+       {"devices", devs},
+       {"containerEdits",
+        json::Value::object({{"deviceNodes", json::Value::array({json::Value::object({{"path", "/dev/kfd"}})})}})}});
+}
+
+std::string DevicePlugin::write_cdi_spec() const {
+  std::vector<std::pair<std::string, std::string>> nodes;
+  std::vector<GpuInfo> gpus;
+  std::vector<std::string> ids;
+  for (size_t i = 0; i < gpus_.size(); ++i) {
+    try {
+      nodes.push_back(drm_node_names(i));
+      gpus.push_back(gpus_[i]);
+      ids.push_back(ids_[i]);
+    } catch (const std::invalid_argument& e) {
+      LOG_WARN("device_plugin") << "CDI spec: " << e.what();  // left out: Allocate refuses it too
+    }
+  }
+  ::mkdir(cfg_.cdi_dir.c_str(), 0755);
+  std::string kind = cfg_.resource_name;
+  std::string file = kind;
+  std::replace(file.begin(), file.end(), '/', '-');
+  const std::string path = join_path(cfg_.cdi_dir, "bgc-" + file + ".json");
+  const std::string tmp = path + ".tmp";
+  net::write_file(tmp, cdi_spec(kind, gpus, ids, nodes).dump());
+  if (::rename(tmp.c_str(), path.c_str()) != 0) throw std::runtime_error("rename " + tmp + " failed");
+  return path;
 }
 
 grpc::Status DevicePlugin::list_and_watch(grpc::ServerCall& call) {
@@ -729,6 +794,7 @@ void DevicePlugin::watch_loop() {
 
 void DevicePlugin::start() {
   ::mkdir(cfg_.plugin_dir.c_str(), 0755);
+  if (cfg_.cdi) LOG_INFO("device_plugin") << "CDI spec written to " << write_cdi_spec();
   start_server();
   watcher_ = std::thread([this] { watch_loop(); });
 }

@@ -70,6 +70,7 @@ struct ContainerAllocation {
   std::vector<Mount> mounts;
   std::vector<DeviceSpec> devices;
   std::map<std::string, std::string> annotations;
+  std::vector<std::string> cdi_devices;  // fully qualified CDI names, e.g. amd.com/gpu=0000:05:00.0
 };
 
 struct PreferredRequest {
@@ -109,7 +110,17 @@ struct DevicePluginConfig {
   std::string sysfs_root = "/sys";  // bus/pci/devices/<bdf>/drm/{card*,renderD*}
   int watch_interval_ms = 1000;
   bool register_with_kubelet = true;
+  // Container Device Interface (k8s >= 1.28 with a CDI-enabled runtime): the plugin writes
+  // a CDI spec for its devices into cdi_dir and Allocate answers with CDI device names
+  // instead of raw device nodes; the runtime injects /dev/kfd and the DRM nodes.
+  bool cdi = false;
+  std::string cdi_dir = "/var/run/cdi";
 };
+
+// CDI spec (cdiVersion 0.6.0, kind = the resource name) for these devices: per device its
+// render and card nodes, /dev/kfd as a spec-wide edit.  `ids[i]` names gpus[i].
+json::Value cdi_spec(const std::string& kind, const std::vector<GpuInfo>& gpus, const std::vector<std::string>& ids,
+                     const std::vector<std::pair<std::string, std::string>>& nodes);
 
 // Kubelet pod-resources API (k8s.io/kubelet/pkg/apis/podresources/v1,
 // PodResourcesLister/List): the device ids of `resource_name` currently assigned to
@@ -141,6 +152,8 @@ class DevicePlugin {
   // Per-GPU health (same order as the gpus passed in); re-sends ListAndWatch on change.
   void set_health(const std::vector<bool>& healthy);
   dp::ContainerAllocation allocate(const std::vector<std::string>& ids) const;  // throws on unknown ids
+  // Writes the CDI spec (cdi mode); returns its path.
+  std::string write_cdi_spec() const;
   std::vector<dp::Device> devices() const;
   const std::vector<std::string>& ids() const { return ids_; }
   std::string socket_path() const;
@@ -151,6 +164,8 @@ class DevicePlugin {
  private:
   void start_server();
   bool register_once();
+  // card* / renderD* node names of gpus_[i] (throws for a partition with no known render node)
+  std::pair<std::string, std::string> drm_node_names(size_t i) const;
   void watch_loop();
   grpc::Status list_and_watch(grpc::ServerCall& call);
 

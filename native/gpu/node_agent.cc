@@ -59,6 +59,8 @@ NodeAgentConfig NodeAgentConfig::from_env(const EnvConfig& env) {
   c.device_plugin = env.boolean_or("device_plugin", false);
   c.device_plugin_dir = env.str_or("device_plugin_dir", c.device_plugin_dir);
   c.device_plugin_socket = env.str_or("device_plugin_socket", c.device_plugin_socket);
+  c.device_plugin_cdi = env.boolean_or("device_plugin_cdi", false);
+  c.cdi_dir = env.str_or("cdi_dir", c.cdi_dir);
   c.dev_root = env.str_or("dev_root", c.dev_root);
   c.sysfs_root = env.str_or("sysfs_root", c.sysfs_root);
   return c;
@@ -379,6 +381,8 @@ void NodeAgent::start() {
     pc.resource_name = cfg_.resource_name;
     pc.dev_root = cfg_.dev_root;
     pc.sysfs_root = cfg_.sysfs_root;
+    pc.cdi = cfg_.device_plugin_cdi;
+    pc.cdi_dir = cfg_.cdi_dir;
     plugin_ = std::make_unique<DevicePlugin>(gpus_, pc);
     plugin_->set_health(healthy_flags());
     plugin_->start();

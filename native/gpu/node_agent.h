@@ -72,6 +72,8 @@ struct NodeAgentConfig {
   bool device_plugin = false;
   std::string device_plugin_dir = "/var/lib/kubelet/device-plugins";
   std::string device_plugin_socket = "bgc-amd-gpu.sock";
+  bool device_plugin_cdi = false;        // answer Allocate with CDI device names (DevicePluginConfig::cdi)
+  std::string cdi_dir = "/var/run/cdi";
   std::string dev_root = "/dev";
   std::string sysfs_root = "/sys";
   static NodeAgentConfig from_env(const EnvConfig& env);

@@ -269,6 +269,8 @@ void register_grpc(py::module_& m) {
              get("sysfs_root", c.sysfs_root);
              if (cfg.count("watch_interval_ms")) c.watch_interval_ms = std::stoi(cfg.at("watch_interval_ms"));
              if (cfg.count("register")) c.register_with_kubelet = cfg.at("register") == "true";
+             if (cfg.count("cdi")) c.cdi = cfg.at("cdi") == "true";
+             get("cdi_dir", c.cdi_dir);
              return std::make_unique<bgc::gpu::DevicePlugin>(gpus_from_json(gpus_json), c);
            }),
            py::arg("gpus_json"), py::arg("config"))
@@ -284,8 +286,11 @@ void register_grpc(py::module_& m) {
         }
         bgc::json::Value envs = bgc::json::Value::object();
         for (const auto& [k, v] : c.envs) envs[k] = v;
-        return bgc::json::Value::object({{"devices", devs}, {"envs", envs}}).dump();
+        bgc::json::Value cdi = bgc::json::Value::array();
+        for (const auto& n : c.cdi_devices) cdi.push_back(n);
+        return bgc::json::Value::object({{"devices", devs}, {"envs", envs}, {"cdi_devices", cdi}}).dump();
       })
+      .def("write_cdi_spec", &bgc::gpu::DevicePlugin::write_cdi_spec)
       .def_property_readonly("ids", &bgc::gpu::DevicePlugin::ids)
       .def_property_readonly("socket_path", &bgc::gpu::DevicePlugin::socket_path)
       .def_property_readonly("registrations", &bgc::gpu::DevicePlugin::registrations)

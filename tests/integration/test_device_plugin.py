@@ -367,3 +367,38 @@ def test_periodic_diagnostics_skip_gpus_in_use(tmp_path):
     finally:
         pr.stop()
         kubelet.stop()
+
+
+def test_cdi_mode_spec_and_allocate(nat, tmp_path):
+    """CDI mode: the plugin writes a CDI spec (cdiVersion 0.6.0, kind amd.com/gpu, one
+    device per BDF with its DRM nodes, /dev/kfd spec-wide) and Allocate answers with CDI
+    names that a CDI-enabled runtime resolves; decoded by the independent grpcio stack."""
+    d = str(tmp_path / "dp")
+    kubelet = FakeKubelet(d).start()
+    gpus = json.loads(nat.default_mi355x_fixture(4))["gpus"]
+    drm = tmp_path / "sys" / "bus" / "pci" / "devices" / gpus[1]["bdf"] / "drm"
+    os.makedirs(drm / "card9")
+    os.makedirs(drm / "renderD140")
+    plugin = nat.DevicePlugin(json.dumps(gpus), {"plugin_dir": d, "watch_interval_ms": "50", "cdi": "true",
+                                                 "cdi_dir": str(tmp_path / "cdi"), "sysfs_root": str(tmp_path / "sys")})
+    plugin.start()
+    try:
+        spec = json.load(open(tmp_path / "cdi" / "bgc-amd.com-gpu.json"))
+        assert spec["cdiVersion"] == "0.6.0" and spec["kind"] == "amd.com/gpu"
+        assert spec["containerEdits"]["deviceNodes"] == [{"path": "/dev/kfd"}]
+        byname = {x["name"]: [n["path"] for n in x["containerEdits"]["deviceNodes"]] for x in spec["devices"]}
+        assert byname[gpus[1]["bdf"]] == ["/dev/dri/card9", "/dev/dri/renderD140"]
+        assert byname[gpus[0]["bdf"]] == ["/dev/dri/card1", "/dev/dri/renderD128"]  # amdsmi minors
+        assert kubelet.wait(lambda: kubelet.registrations and kubelet.device_lists, timeout=15)
+        c = PluginClient(plugin.socket_path)
+        try:
+            req = pb["AllocateRequest"]()
+            req.container_requests.add().devices_ids.extend([gpus[1]["bdf"], gpus[3]["bdf"]])
+            r = c.allocate(req, timeout=5).container_responses[0]
+        finally:
+            c.close()
+        assert [x.name for x in r.cdi_devices] == [f"amd.com/gpu={gpus[1]['bdf']}", f"amd.com/gpu={gpus[3]['bdf']}"]
+        assert len(r.devices) == 0 and r.envs["BGC_AMD_GPU_SINGLE_XGMI_HIVE"] == "true"
+    finally:
+        plugin.stop()
+        kubelet.stop()
