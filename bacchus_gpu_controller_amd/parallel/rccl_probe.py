@@ -11,7 +11,9 @@ Each rank:
     --require-single-hive, fails);
   * runs bf16 all-reduce over a size sweep with the `nccl` backend (= RCCL on ROCm),
     checks the result exactly, and reports algbw and busbw (busbw = algbw * 2(n-1)/n,
-    the per-link figure comparable to the ~153 GB/s xGMI link rate).
+    the per-link figure comparable to the ~153 GB/s xGMI link rate);
+  * reads its GPU's xGMI link write counters (amdsmi_get_link_metrics) before and after
+    and compares the bytes that crossed xGMI with what the ring must have sent.
 
 A TP=8 group on one hive should show busbw in the hundreds of GB/s; a group that fell
 back to PCIe/NIC shows an order of magnitude less — the co-scheduling signal the node
@@ -41,6 +43,20 @@ def local_hive_id(local_rank):
         return f"unavailable:{type(e).__name__}"
 
 
+def _amdsmi_index(backend, local_rank):
+    gpus = json.loads(backend.discover())
+    for g in gpus:
+        if g.get("hip_id", g["index"]) == local_rank:
+            return g["index"]
+    return local_rank % max(1, len(gpus))
+
+
+def xgmi_write_kb(backend, index):
+    """Cumulative KB this GPU has written over its xGMI links (amdsmi link metrics)."""
+    t = json.loads(backend.sample(index, 2))
+    return sum(l.get("write_kb", 0) for l in t.get("links", []) if l.get("type") == "xgmi")
+
+
 def run(sizes_mb, iters=10, warmup=3, require_single_hive=False, dtype="bf16"):
     import torch
     import torch.distributed as dist
@@ -64,6 +80,20 @@ def run(sizes_mb, iters=10, warmup=3, require_single_hive=False, dtype="bf16"):
     hives = [None] * world
     dist.all_gather_object(hives, hive)
     single_hive = len(set(hives)) == 1
+    # xGMI traffic check: the link counters of this rank's GPU before and after the sweep.
+    # A ring all-reduce writes 2(n-1)/n of the buffer per rank and iteration, so a group
+    # that really runs over xGMI shows about that many bytes on its links.
+    smi, smi_idx, kb0 = None, None, None
+    if cuda:
+        try:
+            from .. import native
+
+            smi = native().gpu_backend("amdsmi", "")
+            smi_idx = _amdsmi_index(smi, local)
+            kb0 = xgmi_write_kb(smi, smi_idx)
+        except Exception:  # noqa: BLE001
+            smi = None
+    expected_bytes = 0
     results = []
     for mb in sizes_mb:
         n = int(mb * (1 << 20) // torch.tensor([], dtype=tdtype).element_size())
@@ -93,10 +123,25 @@ def run(sizes_mb, iters=10, warmup=3, require_single_hive=False, dtype="bf16"):
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         t = float(tmax.item())
         nbytes = n * buf.element_size()
+        expected_bytes += busbw_factor(world) * nbytes * (warmup + iters) if world > 1 else 0
         algbw = nbytes / t / 1e9
         results.append({"size_mb": mb, "time_us": round(t * 1e6, 2), "algbw_gbps": round(algbw, 2),
                         "busbw_gbps": round(algbw * busbw_factor(world), 2), "correct": ok})
+    wrote = None
+    if smi is not None:
+        try:
+            wrote = (xgmi_write_kb(smi, smi_idx) - kb0) * 1024.0
+        except Exception:  # noqa: BLE001
+            wrote = None
+    traffic = [None] * world
+    dist.all_gather_object(traffic, {"xgmi_written_mb": None if wrote is None else round(wrote / 2**20, 1),
+                                     "expected_mb": round(expected_bytes / 2**20, 1)})
     out = {"world_size": world, "backend": backend, "dtype": dtype, "hives": hives, "single_hive": single_hive,
+           "xgmi_traffic": traffic,
+           # every rank's links carried at least half the ring's bytes (other tenants' traffic
+           # only adds to the counters, so this can miss a fallback only on a shared box)
+           "traffic_on_xgmi": world > 1 and all(t["xgmi_written_mb"] is not None and
+                                                t["xgmi_written_mb"] >= 0.5 * t["expected_mb"] for t in traffic),
            "results": results, "max_busbw_gbps": max(r["busbw_gbps"] for r in results) if results else 0.0,
            "all_correct": all(r["correct"] for r in results)}
     dist.barrier()

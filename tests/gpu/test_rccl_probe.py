@@ -19,3 +19,7 @@ def test_rccl_probe_single_gpu():
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out["backend"] == "nccl" and out["all_correct"]
     assert out["hives"][0] not in ("cpu",) and not out["hives"][0].startswith("unavailable")
+    # the link counters were read (world 1 sends nothing over xGMI itself; 8-GPU runs
+    # compare the written bytes with the ring's expected traffic)
+    t = out["xgmi_traffic"][0]
+    assert t["xgmi_written_mb"] is not None and t["expected_mb"] == 0 and out["traffic_on_xgmi"] is False

@@ -60,3 +60,6 @@ def test_rccl_probe_logic_gloo_world2():
     out = json.loads(line)
     assert out["world_size"] == 2 and out["backend"] == "gloo" and out["all_correct"]
     assert out["single_hive"] and len(out["results"]) == 2
+    # no GPU: no link counters, and a CPU group never claims xGMI traffic
+    assert [t["xgmi_written_mb"] for t in out["xgmi_traffic"]] == [None, None] and out["traffic_on_xgmi"] is False
+    assert all(t["expected_mb"] > 0 for t in out["xgmi_traffic"])
