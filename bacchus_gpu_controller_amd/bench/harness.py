@@ -359,7 +359,8 @@ def run(args):
         if semantics in ("reference", "reference-controller"):
             # the reference's controller on this same stack: children applied one after
             # another and re-applied on every reconcile (controller.rs:81-149)
-            ctrl_env.update({"CONF_SKIP_UNCHANGED": "false", "CONF_PARALLEL_CHILDREN": "false"})
+            ctrl_env.update({"CONF_SKIP_UNCHANGED": "false", "CONF_PARALLEL_CHILDREN": "false",
+                             "CONF_LABEL_CHILDREN": "false"})  # .owns() on every object of each kind
         if semantics == "reference":
             # ... and its synchronizer: sheet read only on the periodic tick
             # (synchronizer.rs:192), every tick rewrites every matched tenant

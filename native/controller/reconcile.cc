@@ -22,6 +22,7 @@ Config Config::from_env(const EnvConfig& env) {
   c.requeue_secs = static_cast<int64_t>(env.u64_or("requeue_secs", 30));
   c.error_requeue_ms = static_cast<int64_t>(env.u64_or("error_requeue_ms", 3000));
   c.error_backoff_base_ms = static_cast<int64_t>(env.u64_or("error_backoff_base_ms", 0));
+  c.label_children = env.boolean_or("label_children", true);
   c.lease = kube::LeaseSettings::from_env(env, "bacchus-gpu-controller");
   return c;
 }
@@ -40,14 +41,18 @@ Value controller_owner_ref(const Value& ub) {
                         {"uid", meta.get_string("uid")}});
 }
 
-std::vector<DesiredChild> desired_children(const Value& ub) {
+std::string child_label_selector() { return std::string(kManagedByLabel) + "=" + kManagedByValue; }
+
+std::vector<DesiredChild> desired_children(const Value& ub, bool label) {
   const Value& name_v = ub.get("metadata").get("name");
   if (!name_v.is_string()) throw std::runtime_error("missing object key: .metadata.name");
   std::string name = name_v.as_string();
   for (auto& ch : name) ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
   Value oref = controller_owner_ref(ub);
   auto meta = [&]() {
-    return Value::object({{"name", name}, {"ownerReferences", Value::array({oref})}});
+    Value m = Value::object({{"name", name}, {"ownerReferences", Value::array({oref})}});
+    if (label) m["labels"] = Value::object({{kManagedByLabel, kManagedByValue}});
+    return m;
   };
   std::vector<DesiredChild> out;
   // (1) Namespace (controller.rs:69-87)
@@ -64,6 +69,10 @@ std::vector<DesiredChild> desired_children(const Value& ub) {
     Value role = Value::object({{"apiVersion", "rbac.authorization.k8s.io/v1"}, {"kind", "Role"}});
     Value m = r->get("metadata").is_object() ? r->get("metadata") : Value::object();
     m["ownerReferences"] = Value::array({oref});
+    if (label) {
+      if (!m.get("labels").is_object()) m["labels"] = Value::object();
+      m["labels"][kManagedByLabel] = kManagedByValue;
+    }
     role["metadata"] = m;
     if (const Value* rules = r->find("rules"); rules && !rules->is_null()) role["rules"] = *rules;
     // The URL name is the namespace name; a Role whose metadata.name differs is
@@ -197,7 +206,7 @@ kube::Action Reconciler::reconcile(const kube::ObjPtr& ub_ptr) {
     fast.inc();
     return kube::Action::requeue_after(std::chrono::milliseconds(cfg_.requeue_secs * 1000));
   }
-  std::vector<DesiredChild> children = desired_children(ub);
+  std::vector<DesiredChild> children = desired_children(ub, cfg_.label_children);
   LOG_INFO("controller") << "reconciling " << children.front().name;
 
   std::vector<std::string> hashes;

@@ -34,6 +34,12 @@
 namespace bgc::controller {
 
 constexpr const char* kFieldManager = "bacchus-gpu-controller.bacchus.io";
+// Label put on every child this controller applies (CONF_LABEL_CHILDREN): the owned-kind
+// watches then select only these, so the apiserver filters events server-side instead of
+// streaming every Namespace/ResourceQuota/Role/RoleBinding in the cluster to the
+// controller (the reference's .owns() watches all of them, controller.rs:235-238).
+constexpr const char* kManagedByLabel = "app.kubernetes.io/managed-by";
+constexpr const char* kManagedByValue = "bacchus-gpu-controller";
 
 struct Config {
   std::string listen_addr = "0.0.0.0";
@@ -49,6 +55,7 @@ struct Config {
   // 3 s.  0 = the reference's fixed error_requeue_ms (controller.rs:174).
   int64_t error_backoff_base_ms = 0;
   int64_t child_delete_delay_ms = 50;
+  bool label_children = true;  // see kManagedByLabel
   kube::LeaseSettings lease;  // optional leader election (CONF_LEADER_ELECTION, ...)
   // reference fields are required (controller.rs:24-28); the rest default
   static Config from_env(const EnvConfig& env);
@@ -64,7 +71,10 @@ struct DesiredChild {
 // Pure planning step: the children the reference would apply for `ub`, in its order.
 // Throws std::runtime_error("missing object key: .metadata.name") like
 // ControllerError::MissingObjectKey.
-std::vector<DesiredChild> desired_children(const json::Value& ub);
+// With `label`, every child also carries kManagedByLabel=kManagedByValue.
+std::vector<DesiredChild> desired_children(const json::Value& ub, bool label = false);
+// The owned-kind watch selector matching those labels.
+std::string child_label_selector();
 json::Value controller_owner_ref(const json::Value& ub);
 
 class Reconciler {

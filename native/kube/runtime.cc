@@ -398,9 +398,10 @@ Controller::Controller(KubeClient& client, ResourceType primary, Options opts)
 
 Controller::~Controller() { queue_.shutdown(); }
 
-void Controller::owns(const ResourceType& child, Mapper mapper) {
+void Controller::owns(const ResourceType& child, Mapper mapper, std::string label_selector) {
   auto c = std::make_unique<Child>();
   c->rt = child;
+  c->selector = std::move(label_selector);
   c->mapper = mapper ? std::move(mapper) : owner_mapper(primary_);
   c->store = std::make_unique<Store>(child);
   children_.push_back(std::move(c));
@@ -456,7 +457,7 @@ void Controller::run(CancelToken& stop, Reconciler reconcile, ErrorPolicy error_
   for (auto& cp : children_) {
     Child* c = cp.get();
     threads.emplace_back([&, c] {
-      Watcher w(client_, c->rt);
+      Watcher w(client_, c->rt, "", c->selector);
       w.run(stop, [&, c](const WatchEvent& ev) {
         c->store->apply(ev);
         c->gauge->set(static_cast<double>(c->store->size()));

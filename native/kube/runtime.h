@@ -188,7 +188,9 @@ class Controller {
   ~Controller();
   // Watches `child` and enqueues its owners (by default: ownerReferences whose kind
   // and apiVersion match the primary type, mapped by name).
-  void owns(const ResourceType& child, Mapper mapper = nullptr);
+  // `label_selector` limits the child watch server-side (e.g. to children this controller
+  // labelled); empty = every object of the kind, like kube-runtime's default.
+  void owns(const ResourceType& child, Mapper mapper = nullptr, std::string label_selector = "");
   // Child ADDED/MODIFIED events for which `filter` returns false do not enqueue the owner
   // (e.g. the echo of the reconciler's own apply). DELETED events and relists always do.
   using ChildFilter = std::function<bool(const ResourceType& child_type, const json::Value& child)>;
@@ -212,6 +214,7 @@ class Controller {
   struct Child {
     ResourceType rt;
     Mapper mapper;
+    std::string selector;
     std::unique_ptr<Store> store;
     metrics::Gauge* gauge = nullptr;  // bgc_controller_store_objects{resource=...}
   };

@@ -173,3 +173,31 @@ def test_owner_deleted_mid_reconcile_leaves_no_cache_state():
         wait_for(lambda: all(v == 0 for v in gauges().values()), timeout=20, desc="caches drained")
         time.sleep(2.0)  # the delayed applies have all returned by now
         assert all(v == 0 for v in gauges().values()), gauges()
+
+
+def test_owned_watches_select_only_labelled_children():
+    """Children carry app.kubernetes.io/managed-by=bacchus-gpu-controller and the owned-kind
+    watches select on it: unrelated Namespaces and RoleBindings (most of a real cluster)
+    never reach the controller's caches.  CONF_LABEL_CHILDREN=false restores the
+    reference's watch-everything behaviour."""
+    import requests
+
+    def store(c, res):
+        m = requests.get(f"http://127.0.0.1:{c.controller_port}/metrics", timeout=5).text
+        line = [l for l in m.splitlines() if l.startswith(f'bgc_controller_store_objects{{resource="{res}"}}')][0]
+        return float(line.split()[-1])
+
+    for labelled in (True, False):
+        env = {"CONF_REQUEUE_SECS": "3600", "CONF_LABEL_CHILDREN": "true" if labelled else "false"}
+        with Cluster(admission=False, controller_env=env) as c:
+            for i in range(20):
+                c.admin.create("namespaces", {"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": f"other{i}"}})
+            c.admin.create("userbootstraps", {"apiVersion": "bacchus.io/v1", "kind": "UserBootstrap",
+                                              "metadata": {"name": "lab"}, "spec": {"kube_username": "lab"}})
+            ns = wait_for(lambda: c.admin.get_or_none("namespaces", "lab"), desc="lab namespace")
+            if labelled:
+                assert ns["metadata"]["labels"]["app.kubernetes.io/managed-by"] == "bacchus-gpu-controller"
+                wait_for(lambda: store(c, "namespaces") == 1, desc="only the labelled namespace cached")
+            else:
+                assert "labels" not in ns["metadata"]
+                wait_for(lambda: store(c, "namespaces") >= 21, desc="every namespace cached")
