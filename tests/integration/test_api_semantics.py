@@ -172,3 +172,19 @@ def test_non_force_apply_conflict_and_forced_reclaim():
             c.admin.get("resourcequotas", "cf", "cf")), desc="reclaimed")
         managers = {m["manager"] for m in rq["metadata"]["managedFields"]}
         assert "bacchus-gpu-controller.bacchus.io" in managers
+
+
+def test_streaming_lists_fall_back_to_list_when_rejected():
+    """An apiserver without the WatchList feature rejects sendInitialEvents: the watcher
+    falls back to a (paginated) LIST for good and the controller still converges."""
+    with Cluster(admission=False, controller=False) as c:
+        c.admin.create("userbootstraps", ub("fb1"))
+        c.fault([{"method": "GET", "path": "sendInitialEvents=true", "status": 400,
+                  "message": "sendInitialEvents is forbidden for watch unless the WatchList feature gate is enabled"}])
+        pages0 = c.stats()["list_pages"]
+        c.start_controller(extra_env={"CONF_STREAMING_LISTS": "true", "CONF_REQUEUE_SECS": "3600"})
+        wait_for(lambda: c.admin.get_or_none("namespaces", "fb1"), timeout=15, desc="fb1 via LIST fallback")
+        c.admin.create("userbootstraps", ub("fb2"))
+        wait_for(lambda: c.admin.get_or_none("namespaces", "fb2"), timeout=15, desc="fb2 via watch")
+        assert c.stats()["list_pages"] - pages0 >= 5  # UB + 4 owned kinds listed after the fallback
+        assert c.stats()["faults_hit"] >= 5
