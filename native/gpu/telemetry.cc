@@ -121,7 +121,6 @@ void TelemetryPoller::evaluate(const Telemetry& t, const HealthPolicy& p, Device
 }
 
 void TelemetryPoller::poll_once() {
-  roctx::Range range("bgc.telemetry.poll");
   auto& reg = metrics::Registry::global();
   static auto& poll_hist = reg.histogram("bgc_telemetry_poll_seconds", "Wall time of one telemetry poll over all devices");
   static auto& poll_ring = reg.samples("telemetry_poll");
@@ -134,6 +133,11 @@ void TelemetryPoller::poll_once() {
                             : seq % static_cast<uint64_t>(slow_every_) == 0 ? SampleLevel::Slow
                                                                             : SampleLevel::Fast;
   const bool full = level >= SampleLevel::Slow;
+  // one roctx range per poll, named by cadence, so rocprofv3 --marker-trace separates the
+  // every-poll cost from the slow-counter polls
+  roctx::Range range(level == SampleLevel::Ras    ? "bgc.telemetry.poll.ras"
+                     : level == SampleLevel::Slow ? "bgc.telemetry.poll.slow"
+                                                  : "bgc.telemetry.poll.fast");
   std::vector<Telemetry> samples(indices_.size());
   if (pool_) {
     std::vector<std::future<void>> futs;

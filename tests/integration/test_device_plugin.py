@@ -402,3 +402,62 @@ def test_cdi_mode_spec_and_allocate(nat, tmp_path):
     finally:
         plugin.stop()
         kubelet.stop()
+
+
+def test_each_health_rule_flips_list_and_watch(tmp_path):
+    """every health rule, driven through the node agent's telemetry side
+    thread (mock amdsmi fixture edited while it runs), turns that GPU Unhealthy in the
+    kubelet's ListAndWatch stream and names the reason in /gpus."""
+    import requests
+
+    d = str(tmp_path / "dp")
+    kubelet = FakeKubelet(d).start()
+    env = {"CONF_DEVICE_PLUGIN": "true", "CONF_DEVICE_PLUGIN_DIR": d, "CONF_HEARTBEAT_SECS": "30",
+           "CONF_SLOW_EVERY": "1", "CONF_RAS_EVERY": "1", "CONF_VIOLATION_SUSTAIN_POLLS": "3",
+           "CONF_FAIL_THRESHOLD": "2"}
+    try:
+        with Cluster(admission=False, controller=False) as c:
+            c.start_node_agent(node_name="mi355x-rules", backend="mock", poll_interval_ms=50, extra_env=env)
+            assert kubelet.wait(lambda: kubelet.device_lists and
+                                all(x[1] == "Healthy" for x in kubelet.device_lists[-1][1]), timeout=15)
+            fx = json.loads(open(c.fixtures["mi355x-rules"]).read())
+            t = [g["telemetry"] for g in fx["gpus"]]
+            t[0]["retired_pages"] = 65                 # over MAX_RETIRED_PAGES (64)
+            t[1]["unreservable_pages"] = 1             # a bad page the driver could not retire
+            t[2]["violation_thermal_pct"] = 50         # sustained thermal throttling
+            t[3]["xgmi_links_up"] = 6                  # one of 7 xGMI links down
+            t[4]["ecc_uncorrectable"] = 1              # a new uncorrectable error
+            t[5]["temp_mem_c"] = 99                    # HBM over 95 C
+            c.set_gpu_fixture("mi355x-rules", fx)
+            want = ["Unhealthy"] * 6 + ["Healthy"] * 2
+            assert kubelet.wait(lambda: [x[1] for x in kubelet.device_lists[-1][1]] == want, timeout=15), \
+                kubelet.device_lists[-1][1]
+            desc = requests.get(f"http://127.0.0.1:{c.node_agent_ports['mi355x-rules']}/gpus", timeout=5).json()
+            reasons = desc["unhealthy_reason"]
+            for needle in ("retired HBM pages 65 > 64", "could not be retired", "sustained thermal throttling",
+                           "xGMI links down: 1/7", "uncorrectable ECC errors: 1", "HBM temperature"):
+                assert needle in reasons, (needle, reasons)
+            node = c.admin.get("nodes", "mi355x-rules")
+            assert node["metadata"]["labels"]["amd.com/gpu.healthy-count"] == "2"
+            # a GPU that already has uncorrectable errors when the agent starts is never advertised Healthy
+            fx2 = json.loads(open(c.fixtures["mi355x-rules"]).read())
+            for g in fx2["gpus"]:
+                g["telemetry"] = {k: v for k, v in g["telemetry"].items()
+                                  if k not in ("retired_pages", "unreservable_pages", "violation_thermal_pct")}
+                g["telemetry"].update({"xgmi_links_up": 7, "temp_mem_c": 40, "ecc_uncorrectable": 0})
+            fx2["gpus"][7]["telemetry"]["ecc_uncorrectable"] = 3
+            d2 = str(tmp_path / "dp2")
+            kubelet2 = FakeKubelet(d2).start()
+            try:
+                env2 = dict(env, CONF_DEVICE_PLUGIN_DIR=d2)
+                c.start_node_agent(node_name="mi355x-ue", backend="mock", poll_interval_ms=50, extra_env=env2,
+                                   proc_name="na-ue", fixture_obj=fx2)
+                assert kubelet2.wait(lambda: kubelet2.device_lists and
+                                     [x[1] for x in kubelet2.device_lists[-1][1]] == ["Healthy"] * 7 + ["Unhealthy"],
+                                     timeout=15), kubelet2.device_lists[-1:]
+                desc2 = requests.get(f"http://127.0.0.1:{c.node_agent_ports['mi355x-ue']}/gpus", timeout=5).json()
+                assert "already present at agent start" in desc2["unhealthy_reason"]
+            finally:
+                kubelet2.stop()
+    finally:
+        kubelet.stop()
