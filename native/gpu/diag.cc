@@ -46,9 +46,10 @@ Diag::Diag(const std::string& path) : path_(path) {
   arch_ = reinterpret_cast<int (*)(int, char*, size_t)>(dlsym(lib_, "bgc_diag_device_arch"));
   gemm_ = reinterpret_cast<int (*)(int, int, int, int, const uint16_t*, const uint16_t*, float*)>(
       dlsym(lib_, "bgc_diag_gemm"));
+  burn_ = reinterpret_cast<int (*)(int, int, int, uint32_t, bgc_burn_result*)>(dlsym(lib_, "bgc_diag_burn"));
   last_error_ = reinterpret_cast<const char* (*)()>(dlsym(lib_, "bgc_diag_last_error"));
   auto abi = reinterpret_cast<int (*)()>(dlsym(lib_, "bgc_diag_abi_version"));
-  if (!device_count_ || !hbm_ || !mfma_ || !arch_ || !gemm_ || !last_error_ || !abi || abi() != BGC_DIAG_ABI_VERSION) {
+  if (!device_count_ || !hbm_ || !mfma_ || !arch_ || !gemm_ || !burn_ || !last_error_ || !abi || abi() != BGC_DIAG_ABI_VERSION) {
     throw std::runtime_error(path + " is not a compatible bgc diag library");
   }
 }
@@ -132,6 +133,16 @@ json::Value Diag::mfma(int device, int waves_per_cu, int throughput_iters, uint3
   return v;
 }
 
+json::Value Diag::burn(int device, int duration_ms, int waves_per_cu, uint32_t seed) {
+  bgc_burn_result r{};
+  if (burn_(device, duration_ms, waves_per_cu, seed, &r) != 0) throw std::runtime_error(std::string("burn: ") + last_error_());
+  return json::Value::object({{"launches", r.launches}, {"elapsed_ms", r.elapsed_ms}, {"tflops_mean", r.tflops_mean},
+                              {"tflops_min", r.tflops_min}, {"tflops_first", r.tflops_first},
+                              {"tflops_last", r.tflops_last},
+                              {"sustain", r.tflops_first > 0 ? r.tflops_last / r.tflops_first : 0.0},
+                              {"mismatches", static_cast<unsigned long long>(r.mismatches)}});
+}
+
 void Diag::gemm(int device, int m, int n, int k, const uint16_t* a, const uint16_t* b, float* c) {
   if (gemm_(device, m, n, k, a, b, c) != 0) throw std::runtime_error(std::string("gemm diag: ") + last_error_());
 }
@@ -204,6 +215,11 @@ DiagFloors DiagFloors::mi355x_defaults() {
   f.min_mfma_tflops = 1500;
   f.min_xcc_balance = 0.85;
   f.min_xccs = 8;
+  // burn-in: measured on MI355X in profiles/diag_burn_r2.json
+  f.min_burn_tflops = 1500;
+  f.min_burn_sustain = 0.80;
+  f.max_burn_hotspot_c = 100;
+  f.max_burn_thermal_violation_pct = 20;
   return f;
 }
 
@@ -239,6 +255,30 @@ json::Value judge_diag(const json::Value& result, const DiagFloors& fl) {
     }
     if (fl.min_xccs > 0 && num(mf, "xccs_seen") < fl.min_xccs) {
       failures.push_back("only " + std::to_string(static_cast<int>(num(mf, "xccs_seen"))) + " XCCs ran MFMA work");
+    }
+  }
+  const json::Value& burn = result.get("burn");
+  if (burn.is_object()) {
+    if (num(burn, "mismatches") > 0) failures.push_back("burn-in MFMA accumulators wrong");
+    floor_check(burn, "tflops_mean", fl.min_burn_tflops, "burn-in MFMA TFLOP/s");
+    if (fl.min_burn_sustain > 0 && num(burn, "sustain") < fl.min_burn_sustain) {
+      char buf[160];
+      std::snprintf(buf, sizeof(buf), "MFMA rate sagged to %.2f of its start under sustained load (floor %.2f)",
+                    num(burn, "sustain"), fl.min_burn_sustain);
+      failures.push_back(std::string(buf));
+    }
+    if (fl.max_burn_hotspot_c > 0 && num(burn, "max_hotspot_c") > fl.max_burn_hotspot_c) {
+      char buf[160];
+      std::snprintf(buf, sizeof(buf), "hotspot %.0f C under sustained load (limit %.0f)", num(burn, "max_hotspot_c"),
+                    fl.max_burn_hotspot_c);
+      failures.push_back(std::string(buf));
+    }
+    if (fl.max_burn_thermal_violation_pct > 0 &&
+        num(burn, "thermal_violation_pct") > fl.max_burn_thermal_violation_pct) {
+      char buf[160];
+      std::snprintf(buf, sizeof(buf), "thermal throttling %.0f%% of the burn (limit %.0f%%)",
+                    num(burn, "thermal_violation_pct"), fl.max_burn_thermal_violation_pct);
+      failures.push_back(std::string(buf));
     }
   }
   const json::Value& gm = result.get("gemm");

@@ -20,6 +20,12 @@ struct DiagFloors {
   double min_mfma_tflops = 0;
   double min_xcc_balance = 0;  // slowest XCC mean wave time / fastest, inverted (0..1]
   int min_xccs = 0;            // XCCs that must have run MFMA work
+  // Burn-in (sustained MFMA load, `burn` section): rate floor, the rate may not sag
+  // below this fraction of its first launch, and the thermal limits under load.
+  double min_burn_tflops = 0;
+  double min_burn_sustain = 0;   // tflops_last / tflops_first
+  double max_burn_hotspot_c = 0;
+  double max_burn_thermal_violation_pct = 0;
   static DiagFloors mi355x_defaults();
 };
 
@@ -39,6 +45,8 @@ class Diag {
   // MFMA GEMM on the device vs a host fp32 product of the same bf16 operands
   // (deterministic pseudo-random values in [-1, 1]).  Returns max error and the bound.
   json::Value gemm_check(int device, int m, int n, int k, uint32_t seed);
+  // Sustained MFMA load for duration_ms (see bgc_diag_burn).
+  json::Value burn(int device, int duration_ms, int waves_per_cu, uint32_t seed);
   // Raw GEMM: A/B as bf16 bit patterns, C fp32 (row-major).
   void gemm(int device, int m, int n, int k, const uint16_t* a, const uint16_t* b, float* c);
   const std::string& path() const { return path_; }
@@ -52,6 +60,7 @@ class Diag {
   int (*mfma_)(int, int, int, uint32_t, bgc_mfma_result*) = nullptr;
   int (*arch_)(int, char*, size_t) = nullptr;
   int (*gemm_)(int, int, int, int, const uint16_t*, const uint16_t*, float*) = nullptr;
+  int (*burn_)(int, int, int, uint32_t, bgc_burn_result*) = nullptr;
   const char* (*last_error_)() = nullptr;
 };
 

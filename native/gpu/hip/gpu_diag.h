@@ -15,7 +15,7 @@
 extern "C" {
 #endif
 
-#define BGC_DIAG_ABI_VERSION 2
+#define BGC_DIAG_ABI_VERSION 3
 #define BGC_DIAG_MAX_CU_KEYS 2048
 
 typedef struct {
@@ -49,6 +49,19 @@ int bgc_diag_device_count(void);
 // Returns 0 on success, non-zero on HIP error (message via bgc_diag_last_error()).
 int bgc_diag_hbm(int device, uint64_t bytes, int iters, uint32_t seed, bgc_hbm_result* out);
 int bgc_diag_mfma(int device, int waves_per_cu, int throughput_iters, uint32_t seed, bgc_mfma_result* out);
+typedef struct {
+  int launches;             // throughput kernels run back to back
+  double elapsed_ms;        // wall time of the burn (device events)
+  double tflops_mean;       // dense bf16 MFMA rate over the whole burn
+  double tflops_min;        // slowest launch
+  double tflops_first;      // first / last launch: a drop means the GPU throttled
+  double tflops_last;
+  uint64_t mismatches;      // accumulator errors over all launches
+} bgc_burn_result;
+
+// Sustained MFMA load for `duration_ms` (back-to-back throughput kernels of ~10 ms each):
+// the node agent samples power, clocks, temperatures and throttle residency meanwhile.
+int bgc_diag_burn(int device, int duration_ms, int waves_per_cu, uint32_t seed, bgc_burn_result* out);
 // C[m,n] (fp32) = A[m,k] * B[k,n], A/B bf16 bit patterns, row-major, via MFMA; the host
 // compares C with its own fp32 product (m, n multiples of 16; k a multiple of 32).
 int bgc_diag_gemm(int device, int m, int n, int k, const uint16_t* a_bf16, const uint16_t* b_bf16, float* c);

@@ -456,6 +456,67 @@ int bgc_diag_mfma(int device, int waves_per_cu, int throughput_iters, uint32_t s
   return 0;
 }
 
+int bgc_diag_burn(int device, int duration_ms, int waves_per_cu, uint32_t seed, bgc_burn_result* out) {
+  if (!out || duration_ms <= 0 || duration_ms > 600000 || waves_per_cu <= 0 || waves_per_cu > 64) {
+    g_last_error = "invalid arguments";
+    return 1;
+  }
+  std::memset(out, 0, sizeof(*out));
+  HIP_TRY(hipSetDevice(device));
+  const int cus = cu_count(device);
+  const int blocks = std::max(1, cus * waves_per_cu / (kBlock / 64));
+  DeviceBuffer fails, xticks, xwaves;
+  HIP_TRY(hipMalloc(&fails.p, sizeof(unsigned)));
+  HIP_TRY(hipMalloc(&xticks.p, 8 * sizeof(unsigned long long)));
+  HIP_TRY(hipMalloc(&xwaves.p, 8 * sizeof(unsigned)));
+  HIP_TRY(hipMemset(fails.p, 0, sizeof(unsigned)));
+  auto* xt = static_cast<unsigned long long*>(xticks.p);
+  auto* xw = static_cast<unsigned*>(xwaves.p);
+  Events ev, total;
+  HIP_TRY(hipEventCreate(&ev.a));
+  HIP_TRY(hipEventCreate(&ev.b));
+  HIP_TRY(hipEventCreate(&total.a));
+  HIP_TRY(hipEventCreate(&total.b));
+  // size one launch to ~10 ms at MI355X rates (iters * 4 MFMA per wave), measured below
+  int iters = 2048;
+  const double flops_per_iter = static_cast<double>(blocks) * (kBlock / 64) * 4.0 * (2.0 * 16 * 16 * 32);
+  float ms = 0.f;
+  HIP_TRY(hipEventRecord(total.a, nullptr));
+  double sum_flops = 0;
+  while (true) {
+    HIP_TRY(hipEventRecord(ev.a, nullptr));
+    hipLaunchKernelGGL(mfma_throughput, dim3(blocks), dim3(kBlock), 0, nullptr, seed, iters,
+                       static_cast<unsigned*>(fails.p), xt, xw);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(ev.b, nullptr));
+    HIP_TRY(hipEventSynchronize(ev.b));
+    HIP_TRY(hipEventElapsedTime(&ms, ev.a, ev.b));
+    const double tf = flops_per_iter * iters / (ms * 1e-3) / 1e12;
+    if (out->launches == 0) {
+      out->tflops_first = tf;
+      out->tflops_min = tf;
+      // retune the launch length to ~10 ms now that the rate is known
+      iters = std::max(64, std::min(1 << 18, static_cast<int>(iters * (10.0 / std::max(0.01f, ms)))));
+    } else {
+      out->tflops_min = std::min(out->tflops_min, tf);
+    }
+    out->tflops_last = tf;
+    out->launches++;
+    sum_flops += flops_per_iter * (out->launches == 1 ? 2048 : iters);
+    HIP_TRY(hipEventRecord(total.b, nullptr));
+    HIP_TRY(hipEventSynchronize(total.b));
+    float so_far = 0.f;
+    HIP_TRY(hipEventElapsedTime(&so_far, total.a, total.b));
+    out->elapsed_ms = so_far;
+    if (so_far >= static_cast<float>(duration_ms)) break;
+  }
+  unsigned h_fails = 0;
+  HIP_TRY(hipMemcpy(&h_fails, fails.p, sizeof(unsigned), hipMemcpyDeviceToHost));
+  out->mismatches = h_fails;
+  out->tflops_mean = sum_flops / (out->elapsed_ms * 1e-3) / 1e12;
+  return 0;
+}
+
 int bgc_diag_gemm(int device, int m, int n, int k, const uint16_t* a_bf16, const uint16_t* b_bf16, float* c) {
   if (!a_bf16 || !b_bf16 || !c || m <= 0 || n <= 0 || k <= 0 || m % 16 || n % 16 || k % 32 || m > 4096 ||
       n > 4096 || k > 8192) {

@@ -34,6 +34,12 @@ NodeAgentConfig NodeAgentConfig::from_env(const EnvConfig& env) {
   c.run_diag = env.boolean_or("run_diag", false);
   c.diag_hbm_bytes = env.u64_or("diag_hbm_bytes", 1ULL << 30);
   c.diag_interval_secs = env.u64_or("diag_interval_secs", 0);
+  c.diag_burn_ms = env.u64_or("diag_burn_ms", 0);
+  c.diag_floors.min_burn_tflops = env.f64_or("diag_min_burn_tflops", c.diag_floors.min_burn_tflops);
+  c.diag_floors.min_burn_sustain = env.f64_or("diag_min_burn_sustain", c.diag_floors.min_burn_sustain);
+  c.diag_floors.max_burn_hotspot_c = env.f64_or("diag_max_burn_hotspot_c", c.diag_floors.max_burn_hotspot_c);
+  c.diag_floors.max_burn_thermal_violation_pct =
+      env.f64_or("diag_max_burn_thermal_violation_pct", c.diag_floors.max_burn_thermal_violation_pct);
   c.diag_floors.min_read_gbps = env.f64_or("diag_min_read_gbps", c.diag_floors.min_read_gbps);
   c.diag_floors.min_copy_gbps = env.f64_or("diag_min_copy_gbps", c.diag_floors.min_copy_gbps);
   c.diag_floors.min_write_gbps = env.f64_or("diag_min_write_gbps", c.diag_floors.min_write_gbps);
@@ -253,10 +259,59 @@ Value NodeAgent::diagnose(const GpuInfo& g) const {
     r["hbm"] = d.hbm(dev, cfg_.diag_hbm_bytes, 2, seed);
     r["mfma"] = d.mfma(dev, 16, 2048, seed);
     r["gemm"] = d.gemm_check(dev, 64, 64, 512, seed);
+    if (cfg_.diag_burn_ms > 0) r["burn"] = burn_in(*backend_, g.index, dev, static_cast<int>(cfg_.diag_burn_ms), seed);
   } catch (const std::exception& e) {
     r["error"] = std::string(e.what());
   }
   return judge_diag(r, cfg_.diag_floors);
+}
+
+Value burn_in(Backend& backend, int index, int hip_device, int duration_ms, uint32_t seed) {
+  // amdsmi sampler on a side thread for the duration of the burn
+  std::atomic<bool> done{false};
+  double max_hot = 0, max_mem = 0, power_sum = 0, power_max = 0, clk_sum = 0;
+  uint32_t clk_min = UINT32_MAX;
+  int n = 0;
+  Telemetry first, last;
+  std::thread sampler([&] {
+    while (!done.load()) {
+      Telemetry t = backend.sample(index, SampleLevel::Fast);
+      if (t.ok) {
+        if (n == 0) first = t;
+        last = t;
+        max_hot = std::max(max_hot, t.temp_hotspot_c);
+        max_mem = std::max(max_mem, t.temp_mem_c);
+        power_sum += t.power_w;
+        power_max = std::max(power_max, t.power_w);
+        clk_sum += t.gfxclk_mhz;
+        clk_min = std::min(clk_min, t.gfxclk_mhz);
+        ++n;
+      }
+      for (int i = 0; i < 10 && !done.load(); ++i) std::this_thread::sleep_for(std::chrono::milliseconds(10));
+    }
+  });
+  Value out;
+  try {
+    out = Diag::instance().burn(hip_device, duration_ms, 32, seed);
+  } catch (...) {
+    done = true;
+    sampler.join();
+    throw;
+  }
+  done = true;
+  sampler.join();
+  out["samples"] = n;
+  out["max_hotspot_c"] = max_hot;
+  out["max_mem_c"] = max_mem;
+  out["power_mean_w"] = n ? power_sum / n : 0.0;
+  out["power_max_w"] = power_max;
+  out["gfxclk_mean_mhz"] = n ? clk_sum / n : 0.0;
+  out["gfxclk_min_mhz"] = n ? static_cast<double>(clk_min) : 0.0;
+  Telemetry span = last;
+  TelemetryPoller::violation_deltas(first, span);
+  out["thermal_violation_pct"] = span.violation_thermal_pct < 0 ? Value() : Value(span.violation_thermal_pct);
+  out["ppt_violation_pct"] = span.violation_ppt_pct < 0 ? Value() : Value(span.violation_ppt_pct);
+  return out;
 }
 
 std::vector<bool> NodeAgent::in_use() const {

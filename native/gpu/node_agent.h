@@ -60,6 +60,10 @@ struct NodeAgentConfig {
   bool run_diag = false;
   uint64_t diag_hbm_bytes = 1ULL << 30;
   uint64_t diag_interval_secs = 0;     // 0 = only at start
+  // Burn-in: sustained MFMA load for this long while power, clocks, temperatures and
+  // throttle residency are sampled (catches cooling/power-delivery faults the short
+  // checks do not); 0 = off.
+  uint64_t diag_burn_ms = 0;
   DiagFloors diag_floors = DiagFloors::mi355x_defaults();
   std::string pod_resources_socket = "/var/lib/kubelet/pod-resources/kubelet.sock";
   HealthPolicy health;
@@ -91,6 +95,10 @@ std::string sanitize_label_value(const std::string& v);
 // The extended-resource name for a set of discovered devices (see partition_resource_name).
 std::string advertised_resource(const NodeAgentConfig& cfg, const std::vector<GpuInfo>& gpus);
 std::string product_label(const GpuInfo& g);
+
+// Burn-in of one GPU: Diag::burn() while a side thread samples it through `backend`
+// (hotspot/HBM temperature, power, gfxclk, thermal/PPT violation residency over the burn).
+json::Value burn_in(Backend& backend, int index, int hip_device, int duration_ms, uint32_t seed);
 
 // Pure rendering of the Node patches (unit-tested).
 json::Value node_labels_patch(const NodeAgentConfig& cfg, const std::vector<GpuInfo>& gpus, int healthy,

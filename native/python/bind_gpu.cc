@@ -200,6 +200,14 @@ void register_gpu(py::module_& m) {
     }
     return v.dump();
   }, py::arg("device"), py::arg("m") = 64, py::arg("n") = 64, py::arg("k") = 512, py::arg("seed") = 0x5eed);
+  m.def("diag_burn", [](std::shared_ptr<PyBackend> b, int index, int hip_device, int duration_ms, unsigned seed) {
+    Value v;
+    {
+      py::gil_scoped_release nogil;
+      v = bgc::gpu::burn_in(*b->b, index, hip_device, duration_ms, seed);
+    }
+    return v.dump();
+  }, py::arg("backend"), py::arg("index"), py::arg("hip_device"), py::arg("duration_ms"), py::arg("seed") = 0x5eed);
   m.def("judge_diag", [](const std::string& result, const std::string& floors_json) {
     bgc::gpu::DiagFloors f = bgc::gpu::DiagFloors::mi355x_defaults();
     Value fj = bgc::json::parse(floors_json);
@@ -211,6 +219,10 @@ void register_gpu(py::module_& m) {
     num("min_write_gbps", f.min_write_gbps);
     num("min_mfma_tflops", f.min_mfma_tflops);
     num("min_xcc_balance", f.min_xcc_balance);
+    num("min_burn_tflops", f.min_burn_tflops);
+    num("min_burn_sustain", f.min_burn_sustain);
+    num("max_burn_hotspot_c", f.max_burn_hotspot_c);
+    num("max_burn_thermal_violation_pct", f.max_burn_thermal_violation_pct);
     if (fj.get("min_xccs").is_int()) f.min_xccs = static_cast<int>(fj.get("min_xccs").as_int());
     return bgc::gpu::judge_diag(bgc::json::parse(result), f).dump();
   }, py::arg("result"), py::arg("floors") = "{}");

@@ -149,3 +149,19 @@ def test_diag_default_floors_pass(tmp_path):
     assert desc["diag"][0]["gemm"]["passed"]
     assert [x[1] for x in devs] == ["Healthy"]
     assert labels["amd.com/gpu.healthy-count"] == "1" and labels["amd.com/gpu.diag"] == "passed"
+
+
+def test_burn_in_sustained_mfma_with_amdsmi_sampling():
+    """Burn-in: 3 s of back-to-back MFMA throughput kernels while amdsmi samples power,
+    clocks, temperatures and throttle residency; the default floors pass on a healthy
+    MI355X."""
+    from bacchus_gpu_controller_amd import native
+
+    n = native()
+    b = n.gpu_backend("amdsmi", "")
+    r = json.loads(n.diag_burn(b, 0, 0, 3000))
+    _dump("diag_burn.json", r)
+    assert r["mismatches"] == 0 and r["launches"] >= 100 and r["elapsed_ms"] >= 3000
+    assert r["samples"] >= 10 and r["power_max_w"] > 0
+    judged = json.loads(n.judge_diag(json.dumps({"burn": r}), json.dumps({"min_read_gbps": 0})))
+    assert judged["passed"], judged["failures"]

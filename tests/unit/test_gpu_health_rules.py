@@ -217,3 +217,15 @@ def test_pod_resources_codec_matches_protobuf(nat):
     ]
     back = Resp.FromString(nat.pod_resources_encode(json.dumps(decoded[:1])))
     assert list(back.pod_resources[0].containers[0].devices[0].device_ids) == ["0000:05:00.0", "0000:15:00.0"]
+
+
+def test_judge_diag_burn_in(nat):
+    good = json.loads(json.dumps(MI355X_MEASURED))
+    good["burn"] = {"tflops_mean": 1950.0, "sustain": 0.97, "max_hotspot_c": 78.0, "thermal_violation_pct": 0.0,
+                    "mismatches": 0}
+    assert json.loads(nat.judge_diag(json.dumps(good)))["passed"]
+    bad = json.loads(json.dumps(good))
+    bad["burn"].update({"sustain": 0.6, "max_hotspot_c": 104.0, "thermal_violation_pct": 35.0})
+    r = json.loads(nat.judge_diag(json.dumps(bad)))
+    assert not r["passed"] and len(r["failures"]) == 3
+    assert any("sagged" in f for f in r["failures"]) and any("hotspot 104" in f for f in r["failures"])
