@@ -23,7 +23,7 @@ struct DiagFloors {
   // Burn-in (sustained MFMA load, `burn` section): rate floor, the rate may not sag
   // below this fraction of its first launch, and the thermal limits under load.
   double min_burn_tflops = 0;
-  double min_burn_sustain = 0;   // tflops_last / tflops_first
+  double min_burn_sustain = 0;   // tflops_last / tflops_max
   double max_burn_hotspot_c = 0;
   double max_burn_thermal_violation_pct = 0;
   static DiagFloors mi355x_defaults();

@@ -54,8 +54,9 @@ typedef struct {
   double elapsed_ms;        // wall time of the burn (device events)
   double tflops_mean;       // dense bf16 MFMA rate over the whole burn
   double tflops_min;        // slowest launch
-  double tflops_first;      // first / last launch: a drop means the GPU throttled
-  double tflops_last;
+  double tflops_first;      // first launch (includes the clock ramp from idle)
+  double tflops_last;       // last launch vs the best one: a drop means the GPU throttled
+  double tflops_max;
   uint64_t mismatches;      // accumulator errors over all launches
 } bgc_burn_result;
 

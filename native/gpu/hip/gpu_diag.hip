@@ -492,6 +492,7 @@ int bgc_diag_burn(int device, int duration_ms, int waves_per_cu, uint32_t seed, 
     HIP_TRY(hipEventSynchronize(ev.b));
     HIP_TRY(hipEventElapsedTime(&ms, ev.a, ev.b));
     const double tf = flops_per_iter * iters / (ms * 1e-3) / 1e12;
+    out->tflops_max = std::max(out->tflops_max, tf);
     if (out->launches == 0) {
       out->tflops_first = tf;
       out->tflops_min = tf;
