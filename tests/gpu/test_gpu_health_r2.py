@@ -143,10 +143,11 @@ def test_diag_floor_gates_health(tmp_path):
 
 
 def test_diag_default_floors_pass(tmp_path):
-    devs, labels, desc = _agent_with_floors(tmp_path, "mi355x-ok", {})
+    devs, labels, desc = _agent_with_floors(tmp_path, "mi355x-ok", {"CONF_DIAG_BURN_MS": "2000"})
     _dump("diag_default_floors.json", desc["diag"])
     assert desc["diag"][0]["passed"], desc["diag"][0]["failures"]
     assert desc["diag"][0]["gemm"]["passed"]
+    assert desc["diag"][0]["burn"]["tflops_mean"] > 1800 and desc["diag"][0]["burn"]["samples"] >= 5
     assert [x[1] for x in devs] == ["Healthy"]
     assert labels["amd.com/gpu.healthy-count"] == "1" and labels["amd.com/gpu.diag"] == "passed"
 
