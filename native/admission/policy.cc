@@ -22,6 +22,7 @@ Config Config::from_env(const EnvConfig& env) {
   c.authorized_group_names = env.comma_list("authorized_group_names");
   c.log_full_request = env.boolean_or("log_full_request", true);
   c.cert_reload_interval_secs = env.u64_or("cert_reload_interval_secs", 60);
+  c.http2 = env.boolean_or("http2", true);
   return c;
 }
 

@@ -23,6 +23,7 @@ struct Config {
   // Additions (not in the reference): request logging detail and cert poll period.
   bool log_full_request = true;          // reference logs the full request (admission.rs:199)
   uint64_t cert_reload_interval_secs = 60;  // admission.rs:112
+  bool http2 = true;  // ALPN h2 + http/1.1, as axum-server's rustls acceptor (admission.rs:141)
 
   // envy semantics: every reference field is required (admission.rs:22-39).
   static Config from_env(const EnvConfig& env);

@@ -817,6 +817,7 @@ struct ApiServer::Impl {
     http::ClientOptions o;
     o.base_url = base;
     o.tls_server_name = server_name;
+    o.http2 = opts.webhook_http2;
     if (base.rfind("https", 0) == 0) {
       o.tls = net::TlsContext::client(ca.empty() ? "" : crypto::base64_decode(ca), false);
     }

@@ -56,6 +56,9 @@ struct Options {
   // Paginated LIST (limit/continue) serves later pages from a snapshot taken at the first
   // page; continue tokens expire after this long (then 410 Expired, as etcd compaction).
   int continue_ttl_ms = 60000;
+  // Webhook callouts offer HTTP/2 by ALPN, as the real apiserver's Go client does; the
+  // admission requests of concurrent writes then share one multiplexed connection.
+  bool webhook_http2 = true;
 };
 
 class ApiServer {

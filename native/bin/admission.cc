@@ -51,6 +51,7 @@ int main() {
   so.port = cfg.listen_port;
   so.tls = tls;
   so.name = "admission";
+  so.http2 = cfg.http2;
   http::Server server(so);
   http::add_standard_routes(server);
   server.handle("POST", "/mutate", [&](http::Request& req, http::ResponseWriter& w) {

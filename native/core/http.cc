@@ -13,7 +13,9 @@
 #include <cctype>
 #include <charconv>
 #include <cstring>
+#include <deque>
 
+#include "core/http2.h"
 #include "core/log.h"
 #include "core/metrics.h"
 
@@ -296,8 +298,47 @@ static bool read_chunked(Reader& r, std::string& body, int timeout_ms, size_t ma
 // ---------------------------------------------------------------------------
 // Server
 
+// Cached worker threads for HTTP/2 request streams: a stream is handed to an idle
+// worker, or to a new one when none is idle; a worker exits after 30 s without work.
+// Shared with the workers, so it outlives the Server if a worker is still winding down.
+struct Server::WorkerPool {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::function<void()>> q;
+  size_t idle = 0;
+  bool tls = false;
+
+  static void run(const std::shared_ptr<WorkerPool>& self) {
+    std::unique_lock<std::mutex> lk(self->mu);
+    while (true) {
+      ++self->idle;
+      bool got = self->cv.wait_for(lk, std::chrono::seconds(30), [&] { return !self->q.empty(); });
+      --self->idle;
+      if (!got) break;
+      auto job = std::move(self->q.front());
+      self->q.pop_front();
+      lk.unlock();
+      job();
+      job = nullptr;
+      lk.lock();
+    }
+    lk.unlock();
+    if (self->tls) OPENSSL_thread_stop();
+  }
+  static void submit(const std::shared_ptr<WorkerPool>& self, std::function<void()> job) {
+    bool spawn;
+    {
+      std::lock_guard<std::mutex> lk(self->mu);
+      self->q.push_back(std::move(job));
+      spawn = self->idle < self->q.size();
+    }
+    if (spawn) std::thread([self] { run(self); }).detach();
+    else self->cv.notify_one();
+  }
+};
+
 void ResponseWriter::abort() {
-  s_.shutdown();
+  s_->shutdown();
   sent_ = true;
   keep_alive_ = false;
 }
@@ -317,7 +358,7 @@ void ResponseWriter::send(int status, std::string_view body, const std::string& 
   }
   out.append(keep_alive_ ? "Connection: keep-alive\r\n\r\n" : "Connection: close\r\n\r\n");
   out.append(body);
-  s_.write_all(out);
+  s_->write_all(out);
 }
 
 bool ResponseWriter::start_chunked(int status, const std::string& content_type) {
@@ -328,7 +369,7 @@ bool ResponseWriter::start_chunked(int status, const std::string& content_type) 
   keep_alive_ = false;  // long-lived stream: close afterwards
   std::string out = "HTTP/1.1 " + std::to_string(status) + " " + status_text(status) + "\r\n";
   out += "Content-Type: " + content_type + "\r\nTransfer-Encoding: chunked\r\nConnection: close\r\n\r\n";
-  return s_.write_all(out);
+  return s_->write_all(out);
 }
 
 bool ResponseWriter::write_chunk(const std::string& data) {
@@ -338,23 +379,23 @@ bool ResponseWriter::write_chunk(const std::string& data) {
   std::string out;
   out.reserve(data.size() + 16);
   out.append(hdr, static_cast<size_t>(n)).append(data).append("\r\n");
-  return s_.write_all(out);
+  return s_->write_all(out);
 }
 
 void ResponseWriter::end_chunked() {
-  if (chunked_) s_.write_all("0\r\n\r\n", 5);
+  if (chunked_) s_->write_all("0\r\n\r\n", 5);
 }
 
 bool ResponseWriter::peer_closed() {
   struct pollfd p {};
-  p.fd = s_.fd();
+  p.fd = s_->fd();
   p.events = POLLIN | POLLRDHUP;
   int r = ::poll(&p, 1, 0);
   if (r <= 0) return false;
   if (p.revents & (POLLHUP | POLLERR | POLLRDHUP)) return true;
   if (p.revents & POLLIN) {
     char c;
-    ssize_t n = ::recv(s_.fd(), &c, 1, MSG_PEEK | MSG_DONTWAIT);
+    ssize_t n = ::recv(s_->fd(), &c, 1, MSG_PEEK | MSG_DONTWAIT);
     return n == 0;
   }
   return false;
@@ -377,6 +418,11 @@ void Server::handle_prefix(const std::string& prefix, Handler h) {
 }
 
 void Server::start() {
+  if (opts_.tls && opts_.http2) {
+    opts_.tls->enable_h2();
+    h2_workers_ = std::make_shared<WorkerPool>();
+    h2_workers_->tls = true;
+  }
   listen_fd_ = net::listen_tcp(opts_.addr, opts_.port, 1024, &port_);
   if (::pipe2(wake_pipe_, O_CLOEXEC) != 0) throw net::NetError("pipe2 failed");
   started_ = true;
@@ -442,6 +488,10 @@ void Server::serve_conn(int fd, std::string remote) {
     std::lock_guard<std::mutex> lk(conns_mu_);
     conns_[fd] = s.get();
   }
+  if (opts_.tls && opts_.http2 && static_cast<net::TlsStream&>(*s).alpn() == "h2") {
+    serve_h2(fd, std::move(s), remote);  // unregisters the stream before releasing it
+    return;
+  }
   Reader r(*s);
   while (!stop_.cancelled()) {
     Request req;
@@ -496,27 +546,168 @@ void Server::serve_conn(int fd, std::string remote) {
       size_t n = 0;
       auto res = std::from_chars(cl->data(), cl->data() + cl->size(), n);
       if (res.ec != std::errc() || n > opts_.max_body) {
-        ResponseWriter w(*s, false, stop_);
+        ResponseWriter w(s.get(), false, stop_);
         w.send(413, "request body too large\n");
         break;
       }
       body_ok = r.read_exact(req.body, n, opts_.header_timeout_ms);
     }
     if (!body_ok) break;
-    ResponseWriter w(*s, keep_alive && !stop_.cancelled(), stop_);
-    try {
-      if (!dispatch(req, w)) w.send(404, "404 page not found\n");
-    } catch (const std::exception& e) {
-      LOG_ERROR(opts_.name) << "handler error for " << req.method << " " << req.path << ": " << e.what();
-      if (!w.sent()) w.send(500, std::string("internal error: ") + e.what() + "\n");
-    }
-    if (!w.sent()) w.send(500, "handler produced no response\n");
+    ResponseWriter w(s.get(), keep_alive && !stop_.cancelled(), stop_);
+    handle_request(req, w);
     if (!w.keep_alive()) break;
   }
   {
     std::lock_guard<std::mutex> lk(conns_mu_);
     conns_.erase(fd);
   }
+}
+
+void Server::handle_request(Request& req, ResponseWriter& w) {
+  try {
+    if (!dispatch(req, w)) w.send(404, "404 page not found\n");
+  } catch (const std::exception& e) {
+    LOG_ERROR(opts_.name) << "handler error for " << req.method << " " << req.path << ": " << e.what();
+    if (!w.sent()) w.send(500, std::string("internal error: ") + e.what() + "\n");
+  }
+  if (!w.sent()) w.send(500, "handler produced no response\n");
+}
+
+// ---------------------------------------------------------------------------
+// HTTP/2 (ALPN "h2" over TLS)
+
+namespace {
+
+bool h2_forbidden_header(const std::string& lname) {
+  // connection-specific fields are malformed in HTTP/2 (RFC 9113 section 8.2.2)
+  return lname == "connection" || lname == "keep-alive" || lname == "transfer-encoding" || lname == "upgrade" ||
+         lname == "proxy-connection";
+}
+
+class H2ResponseWriter final : public ResponseWriter {
+ public:
+  H2ResponseWriter(std::shared_ptr<http2::Connection> c, std::shared_ptr<http2::Stream> st, const CancelToken& stop)
+      : ResponseWriter(nullptr, true, stop), c_(std::move(c)), st_(std::move(st)) {}
+
+  void send(int status, std::string_view body, const std::string& content_type, const Headers* extra) override {
+    status_ = status;
+    if (sent_) return;
+    sent_ = true;
+    hpack::HeaderList h = head(status, content_type, extra);
+    h.emplace_back("content-length", std::to_string(body.size()));
+    if (body.empty()) {
+      c_->send_headers(*st_, h, true);
+    } else if (c_->send_headers(*st_, h, false)) {
+      c_->send_data(*st_, body, true);
+    }
+  }
+  bool start_chunked(int status, const std::string& content_type) override {
+    status_ = status;
+    if (sent_) return false;
+    sent_ = chunked_ = true;
+    return c_->send_headers(*st_, head(status, content_type, nullptr), false);
+  }
+  bool write_chunk(const std::string& data) override { return data.empty() || c_->send_data(*st_, data, false); }
+  void end_chunked() override {
+    if (chunked_) c_->send_data(*st_, {}, true);
+  }
+  void abort() override {
+    c_->reset_stream(*st_, http2::kInternalError);
+    sent_ = true;
+  }
+  bool peer_closed() override { return c_->closed() || c_->locked([&] { return st_->reset; }); }
+  const char* protocol() const override { return "HTTP/2"; }
+
+ private:
+  static hpack::HeaderList head(int status, const std::string& content_type, const Headers* extra) {
+    hpack::HeaderList h;
+    h.emplace_back(":status", std::to_string(status));
+    if (!content_type.empty()) h.emplace_back("content-type", content_type);
+    if (extra) {
+      for (auto& kv : extra->items()) {
+        std::string n = lower(kv.first);
+        if (!h2_forbidden_header(n) && n != "content-length") h.emplace_back(std::move(n), kv.second);
+      }
+    }
+    return h;
+  }
+  std::shared_ptr<http2::Connection> c_;
+  std::shared_ptr<http2::Stream> st_;
+};
+
+}  // namespace
+
+void Server::serve_h2(int fd, std::unique_ptr<net::Stream> s, const std::string& remote) {
+  static metrics::Counter& streams = metrics::Registry::global().counter(
+      "bgc_http2_streams_total", "HTTP/2 request streams served (ALPN h2 over TLS)");
+  struct Inflight {
+    std::mutex mu;
+    std::condition_variable cv;
+    int n = 0;
+  };
+  auto inflight = std::make_shared<Inflight>();
+  auto pool = h2_workers_;
+  const size_t max_body = opts_.max_body;
+  auto conn = std::make_shared<http2::Connection>(
+      std::move(s), http2::Connection::Role::kServer,
+      [this, inflight, pool, remote, max_body](std::shared_ptr<http2::Connection> c, std::shared_ptr<http2::Stream> st) {
+        {
+          std::lock_guard<std::mutex> lk(inflight->mu);
+          ++inflight->n;
+        }
+        WorkerPool::submit(pool, [this, inflight, remote, max_body, c = std::move(c), st = std::move(st)] {
+          Request req;
+          req.remote = remote;
+          bool ok = c->locked([&] {
+            for (auto& [k, v] : st->headers) {
+              if (k == ":method") req.method = v;
+              else if (k == ":path") req.target = v;
+              else if (!k.empty() && k[0] != ':') req.headers.add(k, v);
+            }
+            req.body = std::move(st->data);
+            return !st->reset;
+          });
+          streams.inc();
+          H2ResponseWriter h2w(c, st, stop_);
+          ResponseWriter& w = h2w;
+          if (ok) {
+            size_t q = req.target.find('?');
+            req.path = url_decode(req.target.substr(0, q));
+            req.query = q == std::string::npos ? "" : req.target.substr(q + 1);
+            if (req.method.empty() || req.target.empty()) w.send(400, "missing :method or :path\n");
+            else if (req.body.size() > max_body) w.send(413, "request body too large\n");
+            else handle_request(req, w);
+          }
+          std::lock_guard<std::mutex> lk(inflight->mu);
+          --inflight->n;
+          inflight->cv.notify_all();
+        });
+      });
+  conn->start();
+  // Runs until the peer goes away, the server stops, or the connection idles out.
+  uint64_t frames = conn->frames_received();
+  int idle = 0;
+  while (!conn->closed() && !stop_.cancelled()) {
+    conn->wait_until(std::chrono::steady_clock::now() + std::chrono::milliseconds(500), [] { return false; });
+    const uint64_t now = conn->frames_received();
+    bool busy;
+    {
+      std::lock_guard<std::mutex> lk(inflight->mu);
+      busy = inflight->n > 0;
+    }
+    idle = (now != frames || busy) ? 0 : idle + 500;
+    frames = now;
+    if (idle >= opts_.idle_timeout_ms) break;
+  }
+  conn->close();
+  conn->join();  // no stream is dispatched after this
+  {
+    // handlers see their streams reset and return; the server must outlive them
+    std::unique_lock<std::mutex> lk(inflight->mu);
+    inflight->cv.wait(lk, [&] { return inflight->n == 0; });
+  }
+  std::lock_guard<std::mutex> lk(conns_mu_);
+  conns_.erase(fd);
 }
 
 bool Server::dispatch(Request& req, ResponseWriter& w) {
@@ -586,12 +777,12 @@ void add_standard_routes(Server& s) {
 // ---------------------------------------------------------------------------
 // Client
 
+Client::~Client() = default;
+
 Client::Client(ClientOptions opts) : opts_(std::move(opts)) {
   url_ = parse_url(opts_.base_url);
   if (url_.scheme == "https" && !opts_.tls) opts_.tls = net::TlsContext::client("", false);
 }
-
-Client::~Client() = default;
 
 void Client::set_default_header(const std::string& name, const std::string& value) {
   std::lock_guard<std::mutex> lk(mu_);
@@ -644,6 +835,16 @@ std::string Client::build_request(const std::string& method, const std::string& 
     out.append(":").append(std::to_string(url_.port));
   }
   out.append("\r\n");
+  Headers merged = merged_headers(headers);
+  for (auto& kv : merged.items()) out.append(kv.first).append(": ").append(kv.second).append("\r\n");
+  if (!body.empty() || method == "POST" || method == "PUT" || method == "PATCH") {
+    out.append("Content-Length: ").append(std::to_string(body.size())).append("\r\n");
+  }
+  out.append("\r\n").append(body);
+  return out;
+}
+
+Headers Client::merged_headers(const Headers* headers) {
   Headers merged;
   {
     std::lock_guard<std::mutex> lk(mu_);
@@ -653,17 +854,83 @@ std::string Client::build_request(const std::string& method, const std::string& 
     for (auto& kv : headers->items()) merged.set(kv.first, kv.second);
   }
   if (!merged.has("User-Agent")) merged.set("User-Agent", "bgc-amd/0.1");
-  for (auto& kv : merged.items()) out.append(kv.first).append(": ").append(kv.second).append("\r\n");
-  if (!body.empty() || method == "POST" || method == "PUT" || method == "PATCH") {
-    out.append("Content-Length: ").append(std::to_string(body.size())).append("\r\n");
+  return merged;
+}
+
+std::shared_ptr<http2::Connection> Client::h2_connection() {
+  std::lock_guard<std::mutex> lk(h2_mu_);  // concurrent first requests share one handshake
+  if (h2_ && h2_->usable()) return h2_;
+  if (h2_refused_) return nullptr;
+  int fd = net::connect_tcp(url_.host, url_.port, opts_.connect_timeout_ms);
+  std::string host = opts_.tls_server_name.empty() ? url_.host : opts_.tls_server_name;
+  auto ts = std::make_unique<net::TlsStream>(fd, opts_.tls->get(), false, host, !opts_.tls->insecure(),
+                                             opts_.connect_timeout_ms, /*offer_h2=*/true);
+  if (ts->alpn() != "h2") {
+    h2_refused_ = true;
+    give_back(std::move(ts));
+    return nullptr;
   }
-  out.append("\r\n").append(body);
-  return out;
+  h2_ = std::make_shared<http2::Connection>(std::move(ts), http2::Connection::Role::kClient);
+  h2_->start();
+  return h2_;
+}
+
+bool Client::request_h2(const std::string& method, const std::string& path, const std::string& body,
+                        const Headers* headers, int timeout_ms, Response* out) {
+  std::string authority = url_.host;
+  if (!((url_.scheme == "http" && url_.port == 80) || (url_.scheme == "https" && url_.port == 443))) {
+    authority += ":" + std::to_string(url_.port);
+  }
+  hpack::HeaderList h = {{":method", method}, {":scheme", url_.scheme}, {":authority", authority},
+                         {":path", path.empty() ? "/" : path}};
+  const Headers merged = merged_headers(headers);
+  for (auto& kv : merged.items()) {
+    std::string n = lower(kv.first);
+    if (n != "host" && n != "content-length" && !h2_forbidden_header(n)) h.emplace_back(std::move(n), kv.second);
+  }
+  if (!body.empty() || method == "POST" || method == "PUT" || method == "PATCH") {
+    h.emplace_back("content-length", std::to_string(body.size()));
+  }
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    auto c = h2_connection();
+    if (!c) return false;
+    auto st = c->open(h, body, true);
+    if (!st) {
+      if (c->usable()) return false;  // e.g. a header block beyond one frame: use HTTP/1.1
+      continue;                       // the connection died or went away: a fresh one
+    }
+    c->wait_until(deadline, [&] { return st->remote_closed || st->reset; });
+    bool done = false, refused = false, started = false;
+    c->locked([&] {
+      done = st->remote_closed && !st->reset;
+      refused = st->reset && st->reset_code == http2::kRefusedStream;
+      started = st->headers_received;
+      if (done) {
+        for (auto& [k, v] : st->headers) {
+          if (k == ":status") out->status = std::atoi(v.c_str());
+          else if (!k.empty() && k[0] != ':') out->headers.add(k, v);
+        }
+        out->body = std::move(st->data);
+      }
+      return 0;
+    });
+    if (done) return true;
+    if (refused && !started) continue;  // RFC 9113 8.7: not processed, safe to retry
+    if (!st->reset) c->reset_stream(*st, http2::kCancel);
+    throw HttpError(std::string(std::chrono::steady_clock::now() >= deadline ? "timeout" : "stream reset") +
+                    " (HTTP/2): " + method + " " + path);
+  }
+  throw HttpError("request failed after retry (HTTP/2): " + method + " " + path);
 }
 
 Response Client::request(const std::string& method, const std::string& path, const std::string& body,
                          const Headers* headers, int timeout_ms) {
   int to = timeout_ms < 0 ? opts_.timeout_ms : timeout_ms;
+  if (opts_.http2 && url_.scheme == "https") {
+    Response resp;
+    if (request_h2(method, path, body, headers, to, &resp)) return resp;
+  }
   std::string wire = build_request(method, path, body, headers);
   for (int attempt = 0; attempt < 2; ++attempt) {
     auto s = take_idle();

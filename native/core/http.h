@@ -1,9 +1,14 @@
-// HTTP/1.1 server and keep-alive client.
+// HTTP/1.1 + HTTP/2 server and keep-alive client.
 //
 // Server: one thread per connection (blocking I/O, TCP_NODELAY) — latency-optimal for
-// the handful of keep-alive connections the apiserver and kubelet probes open; a
-// request is served on the thread that read it, with no hand-off.  Replaces axum 0.6
-// (`/health`, `/mutate`, reference src/controller.rs:256-263, src/admission.rs:149-177).
+// the handful of keep-alive connections the apiserver and kubelet probes open; an
+// HTTP/1.1 request is served on the thread that read it, with no hand-off.  Over TLS the
+// server also speaks HTTP/2 when the client selects "h2" by ALPN (the apiserver's Go
+// webhook client does; axum-server's rustls acceptor offers h2 + http/1.1 the same way):
+// the connection thread then runs an http2::Connection and every request stream is
+// served on a pooled worker thread, so one connection carries concurrent requests.
+// Replaces axum 0.6 (`/health`, `/mutate`, reference src/controller.rs:256-263,
+// src/admission.rs:149-177).
 //
 // Client: per-endpoint pool of keep-alive connections (plain or TLS) plus streaming
 // responses for WATCH.  Replaces hyper 0.14 inside kube-client / google-drive3.
@@ -94,29 +99,35 @@ class Reader {
 // ---------------------------------------------------------------------------
 // Server
 
+// HTTP/1.1 response on the connection's stream; the HTTP/2 writer (http.cc) overrides
+// every I/O method to emit HEADERS/DATA frames on its stream instead.
 class ResponseWriter {
  public:
-  ResponseWriter(net::Stream& s, bool keep_alive, const CancelToken& server_stop)
+  ResponseWriter(net::Stream* s, bool keep_alive, const CancelToken& server_stop)
       : s_(s), keep_alive_(keep_alive), stop_(server_stop) {}
-  void send(int status, std::string_view body, const std::string& content_type = "text/plain; charset=utf-8",
-            const Headers* extra = nullptr);
+  virtual ~ResponseWriter() = default;
+  virtual void send(int status, std::string_view body, const std::string& content_type = "text/plain; charset=utf-8",
+                    const Headers* extra = nullptr);
   void send_json(int status, std::string_view body) { send(status, body, "application/json"); }
   // Streaming (chunked) responses for WATCH.
-  bool start_chunked(int status, const std::string& content_type);
-  bool write_chunk(const std::string& data);
-  void end_chunked();
-  // Drops the connection without a response (fault injection: connection reset).
-  void abort();
+  virtual bool start_chunked(int status, const std::string& content_type);
+  virtual bool write_chunk(const std::string& data);
+  virtual void end_chunked();
+  // Drops the connection without a response (fault injection: connection reset); over
+  // HTTP/2 only the request's stream is reset.
+  virtual void abort();
   bool sent() const { return sent_; }
   int status_code() const { return status_; }  // 0 until a response (or stream) has started
   bool keep_alive() const { return keep_alive_; }
   // True once the server is shutting down; streaming handlers should return.
   bool stopping() const { return stop_.cancelled(); }
   // Non-blocking peer liveness probe for long-lived streams.
-  bool peer_closed();
+  virtual bool peer_closed();
+  // "HTTP/1.1" or "HTTP/2".
+  virtual const char* protocol() const { return "HTTP/1.1"; }
 
- private:
-  net::Stream& s_;
+ protected:
+  net::Stream* s_;
   bool keep_alive_;
   const CancelToken& stop_;
   bool sent_ = false;
@@ -135,6 +146,8 @@ struct ServerOptions {
   int header_timeout_ms = 10000;
   size_t max_connections = 4096;
   std::string name = "http";
+  // TLS servers: offer HTTP/2 by ALPN (enables it on `tls`); HTTP/1.1 clients unaffected.
+  bool http2 = true;
 };
 
 class Server {
@@ -153,7 +166,9 @@ class Server {
  private:
   void accept_loop();
   void serve_conn(int fd, std::string remote);
+  void serve_h2(int fd, std::unique_ptr<net::Stream> s, const std::string& remote);
   bool dispatch(Request& req, ResponseWriter& w);
+  void handle_request(Request& req, ResponseWriter& w);
 
   ServerOptions opts_;
   std::map<std::pair<std::string, std::string>, Handler> exact_;
@@ -168,6 +183,8 @@ class Server {
   std::condition_variable conns_cv_;
   std::map<int, net::Stream*> conns_;
   bool started_ = false;
+  struct WorkerPool;  // HTTP/2 stream workers (cached threads)
+  std::shared_ptr<WorkerPool> h2_workers_;
 };
 
 // Attaches `/health` (-> "pong"), `/metrics` and `/debug/samples/<name>`.
@@ -184,6 +201,10 @@ struct ClientOptions {
   int timeout_ms = 30000;
   size_t max_idle = 256;
   Headers default_headers;
+  // https: offer h2 by ALPN; when the server selects it, request() calls are multiplexed
+  // as streams on one connection (stream() keeps its own HTTP/1.1 connections).  A
+  // server that answers with HTTP/1.1 gets the keep-alive pool as before.
+  bool http2 = false;
 };
 
 class HttpError : public std::runtime_error {
@@ -192,6 +213,11 @@ class HttpError : public std::runtime_error {
 };
 
 class Client;
+}  // namespace bgc::http
+namespace bgc::http2 {
+class Connection;
+}
+namespace bgc::http {
 
 // A response whose body is consumed incrementally (chunked/line-delimited).
 class StreamingResponse {
@@ -234,11 +260,19 @@ class Client {
   void give_back(std::unique_ptr<net::Stream> s);
   std::string build_request(const std::string& method, const std::string& path, const std::string& body,
                             const Headers* headers);
+  Headers merged_headers(const Headers* headers);
+  std::shared_ptr<http2::Connection> h2_connection();
+  // false: HTTP/2 not available for this request (fall back to HTTP/1.1)
+  bool request_h2(const std::string& method, const std::string& path, const std::string& body,
+                  const Headers* headers, int timeout_ms, Response* out);
 
   ClientOptions opts_;
   Url url_;
   std::mutex mu_;
   std::vector<std::unique_ptr<net::Stream>> idle_;
+  std::mutex h2_mu_;
+  std::shared_ptr<http2::Connection> h2_;
+  bool h2_refused_ = false;  // the server selected HTTP/1.1
 };
 
 // One-shot convenience (no pooling).

@@ -92,6 +92,11 @@ void Connection::close(uint32_t code) {
   cv_.notify_all();
 }
 
+bool Connection::usable() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return !closed_ && !goaway_received_ && next_stream_id_ < 0x7fff0000u;
+}
+
 void Connection::join() {
   if (!reader_.joinable()) return;
   // The last reference can be dropped on the reader thread itself (a request dispatch

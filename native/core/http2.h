@@ -87,6 +87,8 @@ class Connection : public std::enable_shared_from_this<Connection> {
   void close(uint32_t code = kNoError);
   void join();
   bool closed() const { return closed_.load(); }
+  // Client: new streams may still be opened (not closed, no GOAWAY, ids left).
+  bool usable() const;
 
   // Client: allocates the next odd stream id and sends request HEADERS (+ body DATA).
   std::shared_ptr<Stream> open(const hpack::HeaderList& headers, std::string_view body, bool end_stream);

@@ -13,6 +13,7 @@
 #include <sys/un.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <cstring>
 #include <fstream>
@@ -141,7 +142,6 @@ std::shared_ptr<TlsContext> TlsContext::server_from_pem(const std::string& cert_
   auto ctx = wrap_ctx(c);
   SSL_CTX_set_min_proto_version(c, TLS1_2_VERSION);
   SSL_CTX_set_mode(c, SSL_MODE_AUTO_RETRY);
-  // HTTP/1.1 only (axum-server serves h1 for the apiserver's webhook client too).
   load_cert_chain_pem(c, cert_pem, key_pem);
   auto t = std::make_shared<TlsContext>();
   t->ctx_ = ctx;
@@ -155,8 +155,35 @@ std::shared_ptr<TlsContext> TlsContext::server_from_files(const std::string& cer
 
 void TlsContext::reload_from_files(const std::string& cert_path, const std::string& key_path) {
   auto fresh = server_from_files(cert_path, key_path);
+  if (h2_) apply_alpn(fresh->ctx_.get());
   std::lock_guard<std::mutex> lk(mu_);
   ctx_ = fresh->ctx_;
+}
+
+namespace {
+// ALPN wire format, in our order of preference.
+constexpr unsigned char kAlpnH2[] = {2, 'h', '2', 8, 'h', 't', 't', 'p', '/', '1', '.', '1'};
+
+int select_alpn(SSL*, const unsigned char** out, unsigned char* outlen, const unsigned char* in, unsigned int inlen,
+                void*) {
+  unsigned char* sel = nullptr;
+  // first of OUR protocols that the client offered (h2 before http/1.1)
+  if (SSL_select_next_proto(&sel, outlen, kAlpnH2, sizeof(kAlpnH2), in, inlen) == OPENSSL_NPN_NEGOTIATED) {
+    *out = sel;
+    return SSL_TLSEXT_ERR_OK;
+  }
+  return SSL_TLSEXT_ERR_NOACK;  // e.g. a client offering only "acme-tls/1": no ALPN, HTTP/1.1
+}
+}  // namespace
+
+void TlsContext::apply_alpn(SSL_CTX* c) const {
+  if (server_) SSL_CTX_set_alpn_select_cb(c, select_alpn, nullptr);
+}
+
+void TlsContext::enable_h2() {
+  std::lock_guard<std::mutex> lk(mu_);
+  h2_ = true;
+  apply_alpn(ctx_.get());
 }
 
 std::shared_ptr<SSL_CTX> TlsContext::get() const {
@@ -203,7 +230,7 @@ std::shared_ptr<TlsContext> TlsContext::client(const std::string& ca_pem, bool i
 }
 
 TlsStream::TlsStream(int fd, std::shared_ptr<SSL_CTX> ctx, bool server, const std::string& verify_host,
-                     bool verify_peer, int timeout_ms)
+                     bool verify_peer, int timeout_ms, bool offer_h2)
     : fd_(fd), ctx_(std::move(ctx)) {
   ssl_ = SSL_new(ctx_.get());
   if (!ssl_) {
@@ -212,6 +239,7 @@ TlsStream::TlsStream(int fd, std::shared_ptr<SSL_CTX> ctx, bool server, const st
     throw NetError("SSL_new: " + ssl_errors());
   }
   SSL_set_fd(ssl_, fd_);
+  if (!server && offer_h2) SSL_set_alpn_protos(ssl_, kAlpnH2, sizeof(kAlpnH2));
   if (!server) {
     if (!verify_host.empty()) {
       bool is_ip = verify_host.find_first_not_of("0123456789.") == std::string::npos ||
@@ -236,6 +264,7 @@ TlsStream::TlsStream(int fd, std::shared_ptr<SSL_CTX> ctx, bool server, const st
   struct timeval zero {};
   setsockopt(fd_, SOL_SOCKET, SO_RCVTIMEO, &zero, sizeof(zero));
   setsockopt(fd_, SOL_SOCKET, SO_SNDTIMEO, &zero, sizeof(zero));
+  if (rc == 1) fcntl(fd_, F_SETFL, fcntl(fd_, F_GETFL, 0) | O_NONBLOCK);
   if (rc != 1) {
     std::string err = ssl_errors();
     long vr = SSL_get_verify_result(ssl_);
@@ -256,43 +285,71 @@ TlsStream::~TlsStream() {
   if (fd_ >= 0) ::close(fd_);
 }
 
-bool TlsStream::has_buffered() const { return ssl_ && SSL_pending(ssl_) > 0; }
+bool TlsStream::has_buffered() const {
+  std::lock_guard<std::mutex> lk(ssl_mu_);
+  return ssl_ && SSL_pending(ssl_) > 0;
+}
+
+std::string TlsStream::alpn() const {
+  const unsigned char* p = nullptr;
+  unsigned int n = 0;
+  std::lock_guard<std::mutex> lk(ssl_mu_);
+  SSL_get0_alpn_selected(ssl_, &p, &n);
+  return p ? std::string(reinterpret_cast<const char*>(p), n) : std::string();
+}
 
 ssize_t TlsStream::read_some(char* buf, size_t n, int timeout_ms) {
-  if (timeout_ms >= 0 && SSL_pending(ssl_) == 0) {
-    int r = poll_fd(fd_, POLLIN, timeout_ms);
-    if (r == 0) return -2;
-    if (r < 0) return -1;
-  }
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(std::max(timeout_ms, 0));
   while (true) {
-    int r = SSL_read(ssl_, buf, static_cast<int>(n));
-    if (r > 0) return r;
-    int err = SSL_get_error(ssl_, r);
+    int r, err;
+    {
+      std::lock_guard<std::mutex> lk(ssl_mu_);
+      r = SSL_read(ssl_, buf, static_cast<int>(n));
+      if (r > 0) return r;
+      err = SSL_get_error(ssl_, r);
+      if (err != SSL_ERROR_WANT_READ && err != SSL_ERROR_WANT_WRITE) ERR_clear_error();
+    }
     if (err == SSL_ERROR_ZERO_RETURN) return 0;
     if (err == SSL_ERROR_WANT_READ || err == SSL_ERROR_WANT_WRITE) {
-      int pr = poll_fd(fd_, err == SSL_ERROR_WANT_READ ? POLLIN : POLLOUT, timeout_ms < 0 ? -1 : timeout_ms);
+      int wait = -1;
+      if (timeout_ms >= 0) {
+        wait = static_cast<int>(std::chrono::duration_cast<std::chrono::milliseconds>(
+                                    deadline - std::chrono::steady_clock::now()).count());
+        if (wait < 0) return -2;
+      }
+      int pr = poll_fd(fd_, err == SSL_ERROR_WANT_READ ? POLLIN : POLLOUT, wait);
       if (pr == 0) return -2;
       if (pr < 0) return -1;
       continue;
     }
     if (err == SSL_ERROR_SYSCALL && errno == 0) return 0;  // unexpected EOF
-    ERR_clear_error();
     return -1;
   }
 }
 
 bool TlsStream::write_all(const char* buf, size_t n) {
-  std::lock_guard<std::mutex> lk(write_mu_);
+  std::lock_guard<std::mutex> wl(write_mu_);
   while (n > 0) {
-    int r = SSL_write(ssl_, buf, static_cast<int>(n));
-    if (r <= 0) {
-      int err = SSL_get_error(ssl_, r);
-      if (err == SSL_ERROR_WANT_WRITE || err == SSL_ERROR_WANT_READ) continue;
-      ERR_clear_error();
-      return false;
+    int r, err;
+    {
+      std::lock_guard<std::mutex> lk(ssl_mu_);
+      r = SSL_write(ssl_, buf, static_cast<int>(n));
+      if (r <= 0) {
+        err = SSL_get_error(ssl_, r);
+        if (err != SSL_ERROR_WANT_READ && err != SSL_ERROR_WANT_WRITE) ERR_clear_error();
+      }
     }
-    buf += r;
-    n -= static_cast<size_t>(r);
+    if (r > 0) {
+      buf += r;
+      n -= static_cast<size_t>(r);
+      continue;
+    }
+    // retried with the same buffer, as a non-blocking SSL_write requires
+    if (err == SSL_ERROR_WANT_WRITE || err == SSL_ERROR_WANT_READ) {
+      if (poll_fd(fd_, err == SSL_ERROR_WANT_WRITE ? POLLOUT : POLLIN, 30000) <= 0) return false;
+      continue;
+    }
+    return false;
   }
   return true;
 }

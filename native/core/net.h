@@ -64,30 +64,45 @@ class TlsContext {
   std::shared_ptr<SSL_CTX> get() const;
   bool is_server() const { return server_; }
   bool insecure() const { return insecure_; }
+  // ALPN (RFC 7301) for HTTP/2: a server context selects "h2" when the client offers it
+  // and "http/1.1" otherwise.  Survives reloads.  (Clients choose per connection:
+  // TlsStream's offer_h2.)
+  void enable_h2();
+  bool h2() const { return h2_.load(); }
 
  private:
+  void apply_alpn(SSL_CTX* c) const;
   mutable std::mutex mu_;
   std::shared_ptr<SSL_CTX> ctx_;
   bool server_ = false;
   bool insecure_ = false;
+  std::atomic<bool> h2_{false};
 };
 
 class TlsStream : public Stream {
  public:
   // Takes ownership of fd. Performs the handshake; throws NetError on failure.
+  // offer_h2 (client): offer "h2" before "http/1.1" by ALPN on this connection only.
   TlsStream(int fd, std::shared_ptr<SSL_CTX> ctx, bool server, const std::string& verify_host,
-            bool verify_peer, int timeout_ms);
+            bool verify_peer, int timeout_ms, bool offer_h2 = false);
   ~TlsStream() override;
   ssize_t read_some(char* buf, size_t n, int timeout_ms) override;
   bool write_all(const char* buf, size_t n) override;
   void shutdown() override;
   int fd() const override { return fd_; }
   bool has_buffered() const override;
+  // Protocol selected by ALPN during the handshake ("" when none was negotiated).
+  std::string alpn() const;
 
  private:
   int fd_;
   std::shared_ptr<SSL_CTX> ctx_;
   SSL* ssl_ = nullptr;
+  // After the handshake the socket is non-blocking and every SSL call runs under ssl_mu_,
+  // waiting in poll() with the lock released: one thread may read while others write
+  // (an HTTP/2 connection's reader thread and its stream writers share one SSL object,
+  // which OpenSSL does not allow concurrently).  write_mu_ orders whole writes.
+  mutable std::mutex ssl_mu_;
   std::mutex write_mu_;
 };
 

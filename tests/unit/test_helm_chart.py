@@ -328,3 +328,12 @@ def test_admission_pdb_and_optional_metrics():
     assert svcs["bgc-bacchus-gpu-controller-metrics"]["spec"]["selector"]["app.kubernetes.io/component"] == "controller"
     sm = [m for m in ms if m.get("kind") == "ServiceMonitor"][0]
     assert sm["metadata"]["labels"]["release"] == "prom" and sm["spec"]["endpoints"][0]["path"] == "/metrics"
+
+
+def test_admission_http2_toggle():
+    def env_of(values):
+        dep = [m for m in render(values) if m.get("kind") == "Deployment" and m["metadata"]["name"].endswith("admission")][0]
+        return {e["name"]: e.get("value") for e in dep["spec"]["template"]["spec"]["containers"][0]["env"]}
+
+    assert env_of({})["CONF_HTTP2"] == "true"
+    assert env_of({"admission": {"configs": {"http2": False}}})["CONF_HTTP2"] == "false"
