@@ -8,11 +8,12 @@ telemetry side thread, HIP/CDNA4 health diagnostics) and an RCCL/xGMI placement 
 Python is the test/bench surface:
   * ``native()``          -> the pybind11 module over the C++ core (``_native``)
   * ``models``            -> UserBootstrap object builders (CRD data model)
-  * ``ops``               -> HIP/CDNA4 GPU health kernels (``_gpu_ops``)
+  * ``ops``               -> HIP/CDNA4 GPU health kernels (``libbgc_gpu_diag.so``, loaded by ``_native``)
   * ``parallel``          -> RCCL-over-xGMI all-reduce probe and hive topology
   * ``utils``             -> build + process helpers (binaries under ``bin/``)
   * ``testing``           -> fake Google OAuth2/Drive endpoint, cluster harness
-  * ``bench``             -> churn benchmark driver used by ``bench.py``
+  * ``bench``             -> churn benchmark driver used by ``bench.py`` (config #3), plus the
+                             config #4 (``bench.tp8``) and config #5 (``bench.flap``) modes
 """
 import importlib
 import os

@@ -595,11 +595,7 @@ class H2ResponseWriter final : public ResponseWriter {
     sent_ = true;
     hpack::HeaderList h = head(status, content_type, extra);
     h.emplace_back("content-length", std::to_string(body.size()));
-    if (body.empty()) {
-      c_->send_headers(*st_, h, true);
-    } else if (c_->send_headers(*st_, h, false)) {
-      c_->send_data(*st_, body, true);
-    }
+    c_->send_response(*st_, h, body);
   }
   bool start_chunked(int status, const std::string& content_type) override {
     status_ = status;
@@ -687,15 +683,17 @@ void Server::serve_h2(int fd, std::unique_ptr<net::Stream> s, const std::string&
   // Runs until the peer goes away, the server stops, or the connection idles out.
   uint64_t frames = conn->frames_received();
   int idle = 0;
-  while (!conn->closed() && !stop_.cancelled()) {
-    conn->wait_until(std::chrono::steady_clock::now() + std::chrono::milliseconds(500), [] { return false; });
+  // (polled: waiting on the connection's condition variable would wake this thread on
+  // every frame)
+  while (!conn->closed()) {
+    if (stop_.wait_for(std::chrono::milliseconds(250))) break;
     const uint64_t now = conn->frames_received();
     bool busy;
     {
       std::lock_guard<std::mutex> lk(inflight->mu);
       busy = inflight->n > 0;
     }
-    idle = (now != frames || busy) ? 0 : idle + 500;
+    idle = (now != frames || busy) ? 0 : idle + 250;
     frames = now;
     if (idle >= opts_.idle_timeout_ms) break;
   }
@@ -900,7 +898,7 @@ bool Client::request_h2(const std::string& method, const std::string& path, cons
       if (c->usable()) return false;  // e.g. a header block beyond one frame: use HTTP/1.1
       continue;                       // the connection died or went away: a fresh one
     }
-    c->wait_until(deadline, [&] { return st->remote_closed || st->reset; });
+    c->wait_stream(*st, deadline, [&] { return st->remote_closed || st->reset; });
     bool done = false, refused = false, started = false;
     c->locked([&] {
       done = st->remote_closed && !st->reset;

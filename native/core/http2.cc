@@ -25,6 +25,18 @@ void put32(std::string& out, uint32_t v) {
   out.push_back(static_cast<char>(v));
 }
 
+// Appends one frame (9-byte header + payload) to `out`, to coalesce several into one write.
+void append_frame(std::string& out, uint8_t type, uint8_t flags, uint32_t sid, std::string_view payload) {
+  const uint32_t len = static_cast<uint32_t>(payload.size());
+  out.push_back(static_cast<char>(len >> 16));
+  out.push_back(static_cast<char>(len >> 8));
+  out.push_back(static_cast<char>(len));
+  out.push_back(static_cast<char>(type));
+  out.push_back(static_cast<char>(flags));
+  put32(out, sid & 0x7fffffff);
+  out.append(payload.data(), payload.size());
+}
+
 void put_setting(std::string& out, uint16_t id, uint32_t v) {
   out.push_back(static_cast<char>(id >> 8));
   out.push_back(static_cast<char>(id));
@@ -89,6 +101,10 @@ void Connection::close(uint32_t code) {
     write_frame_locked(kGoaway, 0, 0, p);
   }
   if (io_) io_->shutdown();
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (auto& [id, st] : streams_) st->cv.notify_all();
+  }
   cv_.notify_all();
 }
 
@@ -142,6 +158,7 @@ void Connection::maybe_forget(const std::shared_ptr<Stream>& s) {
 std::shared_ptr<Stream> Connection::open(const hpack::HeaderList& headers, std::string_view body, bool end_stream) {
   auto s = std::make_shared<Stream>();
   const std::string block = hpack::encode(headers);
+  bool body_sent = false;
   {
     std::lock_guard<std::mutex> wl(write_mu_);  // ids must hit the wire in increasing order
     {
@@ -152,16 +169,59 @@ std::shared_ptr<Stream> Connection::open(const hpack::HeaderList& headers, std::
       s->send_window = peer_initial_window_;
       if (block.size() > peer_max_frame_) return nullptr;  // never for gRPC request headers
       streams_[s->id] = s;
+      // a small body goes out in the same write as the HEADERS frame
+      const int64_t n = static_cast<int64_t>(body.size());
+      if (!body.empty() && body.size() <= peer_max_frame_ && n <= conn_send_window_ && n <= s->send_window) {
+        conn_send_window_ -= n;
+        s->send_window -= n;
+        body_sent = true;
+      }
     }
     const bool headers_end = end_stream && body.empty();
-    if (!write_frame_locked(kHeaders, kEndHeaders | (headers_end ? kEndStream : 0), s->id, block)) return nullptr;
-    if (headers_end) {
+    std::string out;
+    out.reserve(block.size() + (body_sent ? body.size() + 18 : 9));
+    append_frame(out, kHeaders, kEndHeaders | (headers_end ? kEndStream : 0), s->id, block);
+    if (body_sent) append_frame(out, kData, end_stream ? kEndStream : 0, s->id, body);
+    if (!io_->write_all(out)) return nullptr;
+    if (headers_end || (body_sent && end_stream)) {
       std::lock_guard<std::mutex> lk(mu_);
       s->local_closed = true;
     }
   }
-  if (!body.empty() && !send_data(*s, body, end_stream)) return nullptr;
+  if (!body.empty() && !body_sent && !send_data(*s, body, end_stream)) return nullptr;
   return s;
+}
+
+bool Connection::send_response(Stream& s, const hpack::HeaderList& headers, std::string_view body) {
+  if (body.empty()) return send_headers(s, headers, true);
+  const std::string block = hpack::encode(headers);
+  {
+    std::lock_guard<std::mutex> wl(write_mu_);
+    bool fits = false;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (closed_ || s.reset || s.local_closed) return false;
+      const int64_t n = static_cast<int64_t>(body.size());
+      fits = block.size() <= peer_max_frame_ && body.size() <= peer_max_frame_ && n <= conn_send_window_ &&
+             n <= s.send_window;
+      if (fits) {
+        conn_send_window_ -= n;
+        s.send_window -= n;
+      }
+    }
+    if (fits) {
+      std::string out;
+      out.reserve(block.size() + body.size() + 18);
+      append_frame(out, kHeaders, kEndHeaders, s.id, block);
+      append_frame(out, kData, kEndStream, s.id, body);
+      if (!io_->write_all(out)) return false;
+      std::lock_guard<std::mutex> lk(mu_);
+      s.local_closed = true;
+      if (auto sp = find(s.id)) maybe_forget(sp);
+      return true;
+    }
+  }
+  return send_headers(s, headers, false) && send_data(s, body, true);
 }
 
 bool Connection::send_headers(Stream& s, const hpack::HeaderList& headers, bool end_stream) {
@@ -230,6 +290,7 @@ void Connection::reset_stream(Stream& s, uint32_t code) {
   std::string p;
   put32(p, code);
   write_frame(kRstStream, 0, s.id, p);
+  s.cv.notify_all();
   cv_.notify_all();
 }
 
@@ -261,6 +322,7 @@ void Connection::goaway(uint32_t code, const std::string& why) {
 }
 
 void Connection::fail_all() {
+  std::map<uint32_t, std::shared_ptr<Stream>> dead;
   {
     std::lock_guard<std::mutex> lk(mu_);
     closed_ = true;
@@ -268,8 +330,9 @@ void Connection::fail_all() {
       s->reset = true;
       if (!s->reset_code) s->reset_code = kCancel;
     }
-    streams_.clear();
+    dead.swap(streams_);
   }
+  for (auto& [id, s] : dead) s->cv.notify_all();
   cv_.notify_all();
 }
 
@@ -432,14 +495,17 @@ void Connection::on_window_update(uint32_t sid, std::string_view p) {
 }
 
 void Connection::on_rst(uint32_t sid, std::string_view p) {
+  std::shared_ptr<Stream> s;
   {
     std::lock_guard<std::mutex> lk(mu_);
-    if (auto s = find(sid)) {
+    s = find(sid);
+    if (s) {
       s->reset = true;
       s->reset_code = be32(p.data());
       streams_.erase(sid);
     }
   }
+  if (s) s->cv.notify_all();
   cv_.notify_all();
 }
 
@@ -450,10 +516,10 @@ void Connection::on_headers(uint32_t sid, uint8_t flags, const std::string& bloc
     goaway(kCompressionError, "HPACK: " + err);
     return;
   }
-  std::shared_ptr<Stream> dispatch;
+  std::shared_ptr<Stream> dispatch, s;
   {
     std::lock_guard<std::mutex> lk(mu_);
-    auto s = find(sid);
+    s = find(sid);
     if (!s) {
       if (role_ == Role::kClient || (sid % 2) == 0 || sid <= last_peer_stream_) {
         // trailers for a stream we already forgot, or a bogus id: ignore (decoded for HPACK state)
@@ -480,16 +546,17 @@ void Connection::on_headers(uint32_t sid, uint8_t flags, const std::string& bloc
       maybe_forget(s);
     }
   }
+  s->cv.notify_all();
   cv_.notify_all();
   if (dispatch && on_request_) on_request_(shared_from_this(), dispatch);
 }
 
 void Connection::on_data(uint32_t sid, uint8_t flags, std::string_view payload, size_t flow_len) {
-  std::shared_ptr<Stream> dispatch;
+  std::shared_ptr<Stream> dispatch, s;
   bool stream_open = false;
   {
     std::lock_guard<std::mutex> lk(mu_);
-    auto s = find(sid);
+    s = find(sid);
     if (s && !s->remote_closed) {
       s->data.append(payload.data(), payload.size());
       if (flags & kEndStream) {
@@ -504,14 +571,37 @@ void Connection::on_data(uint32_t sid, uint8_t flags, std::string_view payload, 
       }
     }
   }
-  // Re-open the receive windows right away: data is buffered, not back-pressured.
+  // Re-open the receive windows once half of one is used: data is buffered, not
+  // back-pressured, and a request that fits in a window costs no WINDOW_UPDATE write.
   if (flow_len) {
-    std::string inc;
-    put32(inc, static_cast<uint32_t>(flow_len));
-    std::lock_guard<std::mutex> wl(write_mu_);
-    write_frame_locked(kWindowUpdate, 0, 0, inc);
-    if (stream_open) write_frame_locked(kWindowUpdate, 0, sid, inc);
+    conn_recv_pending_ += flow_len;
+    uint32_t stream_inc = 0;
+    if (stream_open) {
+      std::lock_guard<std::mutex> lk(mu_);
+      s->recv_pending += static_cast<uint32_t>(flow_len);
+      if (s->recv_pending >= kOurWindow / 2) {
+        stream_inc = s->recv_pending;
+        s->recv_pending = 0;
+      }
+    }
+    std::string out;
+    if (conn_recv_pending_ >= kOurWindow / 2) {
+      std::string inc;
+      put32(inc, static_cast<uint32_t>(conn_recv_pending_));
+      append_frame(out, kWindowUpdate, 0, 0, inc);
+      conn_recv_pending_ = 0;
+    }
+    if (stream_inc) {
+      std::string inc;
+      put32(inc, stream_inc);
+      append_frame(out, kWindowUpdate, 0, sid, inc);
+    }
+    if (!out.empty()) {
+      std::lock_guard<std::mutex> wl(write_mu_);
+      io_->write_all(out);
+    }
   }
+  if (s) s->cv.notify_all();
   cv_.notify_all();
   if (dispatch && on_request_) on_request_(shared_from_this(), dispatch);
 }

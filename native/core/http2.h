@@ -66,6 +66,10 @@ struct Stream {
   uint32_t reset_code = 0;
   int64_t send_window = kDefaultWindow;
   bool dispatched = false;
+  uint32_t recv_pending = 0;   // received DATA bytes not yet returned by WINDOW_UPDATE
+  // Waiters for this stream alone (with the connection mutex): a client multiplexing
+  // many requests wakes only the caller whose response arrived, not every caller.
+  std::condition_variable cv;
 };
 
 class Connection : public std::enable_shared_from_this<Connection> {
@@ -94,6 +98,9 @@ class Connection : public std::enable_shared_from_this<Connection> {
   std::shared_ptr<Stream> open(const hpack::HeaderList& headers, std::string_view body, bool end_stream);
 
   bool send_headers(Stream& s, const hpack::HeaderList& headers, bool end_stream);
+  // A complete response: HEADERS + DATA(END_STREAM) in one write when the body fits one
+  // frame and the send windows, else send_headers + send_data.
+  bool send_response(Stream& s, const hpack::HeaderList& headers, std::string_view body);
   // Blocks on flow control; false when the stream or connection died meanwhile.
   bool send_data(Stream& s, std::string_view data, bool end_stream);
   void reset_stream(Stream& s, uint32_t code);
@@ -104,6 +111,13 @@ class Connection : public std::enable_shared_from_this<Connection> {
   bool wait_until(std::chrono::steady_clock::time_point deadline, Pred pred) {
     std::unique_lock<std::mutex> lk(mu_);
     return cv_.wait_until(lk, deadline, [&] { return pred() || closed_.load(); }) && pred();
+  }
+  // As wait_until, on the stream's own condition variable (woken by that stream's frames,
+  // its reset, and the connection closing).
+  template <class Pred>
+  bool wait_stream(Stream& s, std::chrono::steady_clock::time_point deadline, Pred pred) {
+    std::unique_lock<std::mutex> lk(mu_);
+    return s.cv.wait_until(lk, deadline, [&] { return pred() || closed_.load(); }) && pred();
   }
   // Runs fn with the connection mutex held (to read/modify Stream fields).
   template <class Fn>
@@ -147,7 +161,9 @@ class Connection : public std::enable_shared_from_this<Connection> {
   std::atomic<bool> closed_{false};
   std::atomic<uint64_t> frames_in_{0};
   std::thread reader_;
-  // reader-thread-only state: a header block split over CONTINUATION frames
+  // reader-thread-only state: connection-level DATA bytes not yet returned, and a header
+  // block split over CONTINUATION frames
+  uint64_t conn_recv_pending_ = 0;
   std::string hdr_block_;
   uint32_t hdr_sid_ = 0;
   uint8_t hdr_flags_ = 0;

@@ -212,12 +212,22 @@ void write(Level lvl, std::string_view target, std::string_view msg) {
   auto now = std::chrono::system_clock::now();
   auto secs = std::chrono::time_point_cast<std::chrono::seconds>(now);
   auto micros = std::chrono::duration_cast<std::chrono::microseconds>(now - secs).count();
-  std::time_t t = std::chrono::system_clock::to_time_t(now);
-  std::tm tm{};
-  gmtime_r(&t, &tm);
-  char ts[64];
-  std::snprintf(ts, sizeof(ts), "%04d-%02d-%02dT%02d:%02d:%02d.%06ldZ", tm.tm_year + 1900, tm.tm_mon + 1,
-                tm.tm_mday, tm.tm_hour, tm.tm_min, tm.tm_sec, static_cast<long>(micros));
+  // gmtime_r takes glibc's process-wide tz lock on every call: the date part is formatted
+  // once per second per thread and reused (the lock showed up in the services' profiles).
+  thread_local std::time_t cached_sec = -1;
+  thread_local char ts[96];  // "YYYY-MM-DDTHH:MM:SS.uuuuuuZ"
+  thread_local int date_len = 0;
+  const std::time_t t = std::chrono::system_clock::to_time_t(secs);
+  if (t != cached_sec) {
+    std::tm tm{};
+    gmtime_r(&t, &tm);
+    date_len = std::snprintf(ts, 80, "%04d-%02d-%02dT%02d:%02d:%02d.", tm.tm_year + 1900, tm.tm_mon + 1,
+                             tm.tm_mday, tm.tm_hour, tm.tm_min, tm.tm_sec);
+    cached_sec = t;
+  }
+  for (int i = date_len + 5; i >= date_len; --i, micros /= 10) ts[i] = static_cast<char>('0' + micros % 10);
+  ts[date_len + 6] = 'Z';
+  ts[date_len + 7] = '\0';
   std::string line;
   line.reserve(msg.size() + target.size() + 48);
   line.append(ts).append(" ").append(level_name(lvl)).append(" ");
