@@ -192,36 +192,39 @@ std::shared_ptr<Stream> Connection::open(const hpack::HeaderList& headers, std::
   return s;
 }
 
-bool Connection::send_response(Stream& s, const hpack::HeaderList& headers, std::string_view body) {
-  if (body.empty()) return send_headers(s, headers, true);
+Connection::SendResult Connection::try_send_response(Stream& s, const hpack::HeaderList& headers,
+                                                     std::string_view body) {
   const std::string block = hpack::encode(headers);
+  std::lock_guard<std::mutex> wl(write_mu_);
   {
-    std::lock_guard<std::mutex> wl(write_mu_);
-    bool fits = false;
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      if (closed_ || s.reset || s.local_closed) return false;
-      const int64_t n = static_cast<int64_t>(body.size());
-      fits = block.size() <= peer_max_frame_ && body.size() <= peer_max_frame_ && n <= conn_send_window_ &&
-             n <= s.send_window;
-      if (fits) {
-        conn_send_window_ -= n;
-        s.send_window -= n;
-      }
+    std::lock_guard<std::mutex> lk(mu_);
+    if (closed_ || s.reset || s.local_closed) return SendResult::kFailed;
+    const int64_t n = static_cast<int64_t>(body.size());
+    if (block.size() > peer_max_frame_ || body.size() > peer_max_frame_ || n > conn_send_window_ ||
+        n > s.send_window) {
+      return SendResult::kWouldBlock;
     }
-    if (fits) {
-      std::string out;
-      out.reserve(block.size() + body.size() + 18);
-      append_frame(out, kHeaders, kEndHeaders, s.id, block);
-      append_frame(out, kData, kEndStream, s.id, body);
-      if (!io_->write_all(out)) return false;
-      std::lock_guard<std::mutex> lk(mu_);
-      s.local_closed = true;
-      if (auto sp = find(s.id)) maybe_forget(sp);
-      return true;
-    }
+    conn_send_window_ -= n;
+    s.send_window -= n;
   }
-  return send_headers(s, headers, false) && send_data(s, body, true);
+  std::string out;
+  out.reserve(block.size() + body.size() + 18);
+  append_frame(out, kHeaders, kEndHeaders | (body.empty() ? kEndStream : 0), s.id, block);
+  if (!body.empty()) append_frame(out, kData, kEndStream, s.id, body);
+  if (!io_->write_all(out)) return SendResult::kFailed;
+  std::lock_guard<std::mutex> lk(mu_);
+  s.local_closed = true;
+  if (auto sp = find(s.id)) maybe_forget(sp);
+  return SendResult::kSent;
+}
+
+bool Connection::send_response(Stream& s, const hpack::HeaderList& headers, std::string_view body) {
+  switch (try_send_response(s, headers, body)) {
+    case SendResult::kSent: return true;
+    case SendResult::kFailed: return false;
+    case SendResult::kWouldBlock: break;
+  }
+  return send_headers(s, headers, body.empty()) && (body.empty() || send_data(s, body, true));
 }
 
 bool Connection::send_headers(Stream& s, const hpack::HeaderList& headers, bool end_stream) {

@@ -101,6 +101,11 @@ class Connection : public std::enable_shared_from_this<Connection> {
   // A complete response: HEADERS + DATA(END_STREAM) in one write when the body fits one
   // frame and the send windows, else send_headers + send_data.
   bool send_response(Stream& s, const hpack::HeaderList& headers, std::string_view body);
+  // As send_response without ever waiting: kWouldBlock (nothing sent) when the body does
+  // not fit one frame and the current send windows.
+  enum class SendResult { kSent, kFailed, kWouldBlock };
+  SendResult try_send_response(Stream& s, const hpack::HeaderList& headers, std::string_view body);
+
   // Blocks on flow control; false when the stream or connection died meanwhile.
   bool send_data(Stream& s, std::string_view data, bool end_stream);
   void reset_stream(Stream& s, uint32_t code);
