@@ -232,6 +232,7 @@ def _phase(d, nat, info, args, phase, concurrency, total_steps, cluster):
                     _clear(info["controller"] + "/debug/samples/reconcile")
                     _clear(info["server"] + "/debug/samples/webhook", verify=info["apiserver_verify"])
                     _clear(info["admission"] + "/debug/samples/admission", verify=info["ca"])
+                    _clear(info["admission"] + "/debug/samples/h2_server", verify=info["ca"])
                     _clear(info["node_agent"] + "/debug/samples/telemetry_poll")
                     _clear(info["synchronizer"] + "/debug/samples/sync_ub")
                     lock0 = _kl_lock(info)
@@ -272,6 +273,8 @@ def _phase(d, nat, info, args, phase, concurrency, total_steps, cluster):
     rec = _samples(info["controller"] + "/debug/samples/reconcile")
     hook = _samples(info["server"] + "/debug/samples/webhook", verify=info["apiserver_verify"])
     adm = _samples(info["admission"] + "/debug/samples/admission", verify=info["ca"])
+    # HTTP/2 webhook requests: request complete on the server's reader -> response written
+    h2s = _samples(info["admission"] + "/debug/samples/h2_server", verify=info["ca"])
     tel = _samples(info["node_agent"] + "/debug/samples/telemetry_poll")
     syn = _samples(info["synchronizer"] + "/debug/samples/sync_ub")
     total_ready = sum(p["ready"] for p in per_rank)
@@ -298,6 +301,8 @@ def _phase(d, nat, info, args, phase, concurrency, total_steps, cluster):
         "admission_p50_ms": ms(_pct(hook, 0.50)),
         "admission_p99_ms": ms(_pct(hook, 0.99)),
         "admission_handler_p50_ms": ms(_pct(adm, 0.50)),
+        "admission_h2_server_p50_ms": ms(_pct(h2s, 0.50)),
+        "admission_h2_server_p99_ms": ms(_pct(h2s, 0.99)),
         "apply_to_ready_p50_ms": ms(_pct(all_lat, 0.50)),
         "apply_to_ready_p99_ms": ms(_pct(all_lat, 0.99)),
         "create_p50_ms": ms(_pct(all_clat, 0.50)),
@@ -412,7 +417,10 @@ def run(args):
                        "concurrency_per_rank": args.concurrency, "log_level": args.log_level,
                        "apiserver_write_latency_ms": args.write_latency_ms, "control_plane_cpus": cpus,
                        "controller_workers": controller_workers, "sync_workers": sync_workers,
-                       "sheet_poll_ms": args.sheet_poll_ms, "sync_interval_s": args.sync_interval},
+                       "sheet_poll_ms": args.sheet_poll_ms, "sync_interval_s": args.sync_interval,
+                       # API server -> webhook protocol: h2 (one multiplexed connection, as the
+                       # real apiserver's Go client) unless kube-lite runs --webhook-http1
+                       "webhook_protocol": "http/1.1" if "--webhook-http1" in args.apiserver_arg else "h2"},
         }
         out.update(main_r)
         if "t" in results:

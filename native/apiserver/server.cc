@@ -818,6 +818,7 @@ struct ApiServer::Impl {
     o.base_url = base;
     o.tls_server_name = server_name;
     o.http2 = opts.webhook_http2;
+    o.h2_connections = opts.webhook_h2_connections;
     if (base.rfind("https", 0) == 0) {
       o.tls = net::TlsContext::client(ca.empty() ? "" : crypto::base64_decode(ca), false);
     }

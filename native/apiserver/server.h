@@ -59,6 +59,7 @@ struct Options {
   // Webhook callouts offer HTTP/2 by ALPN, as the real apiserver's Go client does; the
   // admission requests of concurrent writes then share one multiplexed connection.
   bool webhook_http2 = true;
+  size_t webhook_h2_connections = 1;
 };
 
 class ApiServer {

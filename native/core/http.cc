@@ -636,6 +636,8 @@ class H2ResponseWriter final : public ResponseWriter {
 void Server::serve_h2(int fd, std::unique_ptr<net::Stream> s, const std::string& remote) {
   static metrics::Counter& streams = metrics::Registry::global().counter(
       "bgc_http2_streams_total", "HTTP/2 request streams served (ALPN h2 over TLS)");
+  // request complete on the reader thread -> handler returned (queueing + handler + write)
+  static auto& server_time = metrics::Registry::global().samples("h2_server");
   struct Inflight {
     std::mutex mu;
     std::condition_variable cv;
@@ -651,7 +653,8 @@ void Server::serve_h2(int fd, std::unique_ptr<net::Stream> s, const std::string&
           std::lock_guard<std::mutex> lk(inflight->mu);
           ++inflight->n;
         }
-        WorkerPool::submit(pool, [this, inflight, remote, max_body, c = std::move(c), st = std::move(st)] {
+        const int64_t t0 = metrics::now_ns();
+        WorkerPool::submit(pool, [this, inflight, remote, max_body, t0, c = std::move(c), st = std::move(st)] {
           Request req;
           req.remote = remote;
           bool ok = c->locked([&] {
@@ -674,6 +677,7 @@ void Server::serve_h2(int fd, std::unique_ptr<net::Stream> s, const std::string&
             else if (req.body.size() > max_body) w.send(413, "request body too large\n");
             else handle_request(req, w);
           }
+          server_time.add(static_cast<double>(metrics::now_ns() - t0) * 1e-9);
           std::lock_guard<std::mutex> lk(inflight->mu);
           --inflight->n;
           inflight->cv.notify_all();
@@ -857,7 +861,9 @@ Headers Client::merged_headers(const Headers* headers) {
 
 std::shared_ptr<http2::Connection> Client::h2_connection() {
   std::lock_guard<std::mutex> lk(h2_mu_);  // concurrent first requests share one handshake
-  if (h2_ && h2_->usable()) return h2_;
+  h2_.resize(std::max<size_t>(1, opts_.h2_connections));
+  auto& slot = h2_[h2_next_++ % h2_.size()];
+  if (slot && slot->usable()) return slot;
   if (h2_refused_) return nullptr;
   int fd = net::connect_tcp(url_.host, url_.port, opts_.connect_timeout_ms);
   std::string host = opts_.tls_server_name.empty() ? url_.host : opts_.tls_server_name;
@@ -868,9 +874,9 @@ std::shared_ptr<http2::Connection> Client::h2_connection() {
     give_back(std::move(ts));
     return nullptr;
   }
-  h2_ = std::make_shared<http2::Connection>(std::move(ts), http2::Connection::Role::kClient);
-  h2_->start();
-  return h2_;
+  slot = std::make_shared<http2::Connection>(std::move(ts), http2::Connection::Role::kClient);
+  slot->start();
+  return slot;
 }
 
 bool Client::request_h2(const std::string& method, const std::string& path, const std::string& body,

@@ -205,6 +205,9 @@ struct ClientOptions {
   // as streams on one connection (stream() keeps its own HTTP/1.1 connections).  A
   // server that answers with HTTP/1.1 gets the keep-alive pool as before.
   bool http2 = false;
+  // HTTP/2 connections request() streams are spread over (round robin); 1 = one
+  // multiplexed connection, as Go's client (and so the apiserver) uses.
+  size_t h2_connections = 1;
 };
 
 class HttpError : public std::runtime_error {
@@ -271,7 +274,8 @@ class Client {
   std::mutex mu_;
   std::vector<std::unique_ptr<net::Stream>> idle_;
   std::mutex h2_mu_;
-  std::shared_ptr<http2::Connection> h2_;
+  std::vector<std::shared_ptr<http2::Connection>> h2_;
+  size_t h2_next_ = 0;
   bool h2_refused_ = false;  // the server selected HTTP/1.1
 };
 

@@ -160,3 +160,19 @@ def test_webhook_http1_flag_keeps_http11():
         assert c.admin.get("userbootstraps", "h1user")["metadata"]["name"] == "h1user"
         after = metric(requests.get(f"{base}/metrics", verify=ca).text, "bgc_http2_streams_total")
         assert after == before
+
+
+def test_webhook_h2_connection_spread():
+    """--webhook-h2-connections N spreads the callouts over N multiplexed connections."""
+    with Cluster(controller=False, apiserver_args=["--webhook-h2-connections", "3"]) as c:
+        ca = os.path.join(c.cert_dir, "ca.crt")
+        base = f"https://127.0.0.1:{c.admission_port}"
+        before = metric(requests.get(f"{base}/metrics", verify=ca).text, "bgc_http2_streams_total")
+        for i in range(6):
+            c.as_user(f"oidc:spread{i}", ["gpu"]).create(
+                "userbootstraps", {"apiVersion": "bacchus.io/v1", "kind": "UserBootstrap",
+                                   "metadata": {"name": f"spread{i}"}, "spec": {}})
+        after = metric(requests.get(f"{base}/metrics", verify=ca).text, "bgc_http2_streams_total")
+        assert after - before >= 6
+        samples = requests.get(f"{base}/debug/samples/h2_server", verify=ca).json()
+        assert samples

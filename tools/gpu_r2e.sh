@@ -1,17 +1,19 @@
 #!/usr/bin/env bash
-# Round-2 GPU pass e: webhook callouts over HTTP/2 (default) vs HTTP/1.1 (--webhook-http1),
-# interleaved A/B of the headline bench on the MI355X box.
+# Round-2 GPU pass e: API server -> webhook over HTTP/2 (default, one multiplexed
+# connection like the real apiserver) vs HTTP/1.1 (--webhook-http1), interleaved A/B of
+# the headline bench on the MI355X box, 3 runs each.
 set -o pipefail
 OUT=gpurun_out/r2e
-mkdir -p "$OUT"
+rm -rf "$OUT" && mkdir -p "$OUT"
 export TMPDIR=/tmp
 step() { echo "[$(date +%T)] $*"; }
 run() {  # name, extra args
   step "$1" && timeout -k 10 300 python -u bench.py --json-out "$OUT/$1.json" "${@:2}" > "$OUT/$1.log" 2>&1
 }
-run h2_a && run h1_a --apiserver-arg=--webhook-http1 && run h2_b && run h1_b --apiserver-arg=--webhook-http1
+run h2_1 && run h1_1 --apiserver-arg=--webhook-http1 && run h2_2 && run h1_2 --apiserver-arg=--webhook-http1 &&
+run h2_3 && run h1_3 --apiserver-arg=--webhook-http1
 rc=$?
 step "done rc=$rc"
 for f in "$OUT"/*.json; do python3 -c "
-import json; d=json.load(open('$f')); print('$f', d['value'], d['reconcile_p99_ms'], d['admission_p50_ms'], d['apply_to_ready_p99_ms'], d['cpu_ms_per_cr'], d['tuned']['value'])"; done
+import json; d=json.load(open('$f')); print('$f', d['config']['webhook_protocol'], d['value'], 'adm_rt_p50', d['admission_p50_ms'], 'adm_handler_p50', d['admission_handler_p50_ms'], 'ready_p99', d['apply_to_ready_p99_ms'], d['cpu_ms_per_cr'], 'tuned', d['tuned']['value'], d['tuned']['admission_p50_ms'])"; done
 exit $rc
