@@ -183,12 +183,12 @@ bool Reconciler::up_to_date(const DesiredChild& c, const std::string& body_hash)
   return it != last_applied_.end() && it->second.body_hash == body_hash && it->second.rv == kube::meta_rv(*cur);
 }
 
-void Reconciler::apply_child(const DesiredChild& c, const std::string& body_hash) {
+void Reconciler::apply_child(const DesiredChild& c, const std::string& body_hash, const std::string& body_json) {
   static auto& applied = metrics::Registry::global().counter("bgc_apply_total", "Server-side applies issued");
-  Value res = client_.apply(*c.rt, c.ns, c.name, c.body, kFieldManager, /*force=*/true);
+  std::string rv = client_.apply_rv(*c.rt, c.ns, c.name, body_json, kFieldManager, /*force=*/true);
   applied.inc();
   std::lock_guard<std::mutex> lk(mu_);
-  last_applied_[child_key(c)] = {body_hash, kube::meta_rv(res)};
+  last_applied_[child_key(c)] = {body_hash, std::move(rv)};
   publish_cache_sizes(last_applied_.size(), ub_state_.size());
   stats_.applied++;
 }
@@ -209,9 +209,13 @@ kube::Action Reconciler::reconcile(const kube::ObjPtr& ub_ptr) {
   std::vector<DesiredChild> children = desired_children(ub, cfg_.label_children);
   LOG_INFO("controller") << "reconciling " << children.front().name;
 
-  std::vector<std::string> hashes;
+  std::vector<std::string> bodies, hashes;
+  bodies.reserve(children.size());
   hashes.reserve(children.size());
-  for (const auto& c : children) hashes.push_back(std::to_string(std::hash<std::string>{}(c.body.dump())));
+  for (const auto& c : children) {
+    bodies.push_back(c.body.dump());
+    hashes.push_back(std::to_string(std::hash<std::string>{}(bodies.back())));
+  }
 
   auto run_one = [&](size_t i) {
     if (up_to_date(children[i], hashes[i])) {
@@ -221,7 +225,7 @@ kube::Action Reconciler::reconcile(const kube::ObjPtr& ub_ptr) {
       return;
     }
     try {
-      apply_child(children[i], hashes[i]);
+      apply_child(children[i], hashes[i], bodies[i]);
     } catch (const std::exception& e) {
       LOG_ERROR("controller") << "failed to patch " << children[i].rt->kind << ": " << e.what();
       throw;

@@ -108,7 +108,7 @@ class Reconciler {
   void apply_all(const std::vector<DesiredChild>& children, const std::function<void(size_t)>& run_one);
   void forget_owner_locked(const std::string& owner);  // mu_ held
   bool owner_live(const std::string& name, const std::string& uid);
-  void apply_child(const DesiredChild& c, const std::string& body_hash);
+  void apply_child(const DesiredChild& c, const std::string& body_hash, const std::string& body_json);
 
   kube::KubeClient& client_;
   kube::Controller& ctrl_;

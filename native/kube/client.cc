@@ -249,6 +249,17 @@ Value KubeClient::apply(const ResourceType& rt, const std::string& ns, const std
   return call("PATCH", path, body.dump(), "application/apply-patch+yaml");
 }
 
+std::string KubeClient::apply_rv(const ResourceType& rt, const std::string& ns, const std::string& name,
+                                 const std::string& body_json, const std::string& field_manager, bool force) {
+  std::string path =
+      with_params(rt.object_path(ns, name), {{"fieldManager", field_manager}, {"force", force ? "true" : ""}});
+  http::Response r = raw("PATCH", path, body_json, "application/apply-patch+yaml");
+  if (r.status < 200 || r.status >= 300) throw_api_error(r);
+  std::string_view md = json::raw_member(r.body, "metadata");
+  if (md.empty()) return "";
+  return json::parse(md, "managedFields").get_string("resourceVersion");
+}
+
 Value KubeClient::apply_status(const ResourceType& rt, const std::string& ns, const std::string& name,
                                const Value& body, const std::string& field_manager, bool force) {
   std::string path = with_params(rt.object_path(ns, name) + "/status",

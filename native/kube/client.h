@@ -99,6 +99,11 @@ class KubeClient {
                     const std::string& field_manager, bool force);
   json::Value apply_status(const ResourceType& rt, const std::string& ns, const std::string& name,
                            const json::Value& body, const std::string& field_manager, bool force);
+  // Server-side apply of an already serialized body, for callers that only need the
+  // result's resourceVersion: only the response's `metadata` (minus managedFields) is
+  // parsed, not the whole object.
+  std::string apply_rv(const ResourceType& rt, const std::string& ns, const std::string& name,
+                       const std::string& body_json, const std::string& field_manager, bool force);
   json::Value patch_json(const ResourceType& rt, const std::string& ns, const std::string& name,
                          const json::Value& ops, const std::string& field_manager = "");
   json::Value patch_merge(const ResourceType& rt, const std::string& ns, const std::string& name,
