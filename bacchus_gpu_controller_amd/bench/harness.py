@@ -208,7 +208,8 @@ def _phase(d, nat, info, args, phase, concurrency, total_steps, cluster):
     from bacchus_gpu_controller_amd.testing.cluster import ADMIN_TOKEN
 
     driver = nat.ChurnDriver(info["server"], ADMIN_TOKEN, f"r{d.rank}-", concurrency,
-                             ca_pem=info["apiserver_ca"], approve_url=info.get("approve_url", ""))
+                             ca_pem=info["apiserver_ca"], approve_url=info.get("approve_url", ""),
+                             http2=args.driver_http2)
     driver.start()
     time.sleep(0.2)
     prev = None
@@ -420,7 +421,8 @@ def run(args):
                        "sheet_poll_ms": args.sheet_poll_ms, "sync_interval_s": args.sync_interval,
                        # API server -> webhook protocol: h2 (one multiplexed connection, as the
                        # real apiserver's Go client) unless kube-lite runs --webhook-http1
-                       "webhook_protocol": "http/1.1" if "--webhook-http1" in args.apiserver_arg else "h2"},
+                       "webhook_protocol": "http/1.1" if "--webhook-http1" in args.apiserver_arg else "h2",
+                       "driver_protocol": "h2" if args.driver_http2 and args.tls_apiserver else "http/1.1"},
         }
         out.update(main_r)
         if "t" in results:
@@ -494,6 +496,9 @@ def main(argv=None):
     ap.add_argument("--sync-interval", type=int, default=60, help="synchronizer tick (s); the reference default is 60")
     ap.add_argument("--apiserver-arg", action="append", default=[], help="extra kube-lite flag (repeatable)")
     ap.add_argument("--report-cpu", action="store_true", help="add RSS, object counts and controller gauges")
+    ap.add_argument("--driver-http2", action=argparse.BooleanOptionalAction, default=False,
+                    help="tenant load over HTTP/2 multiplexed connections (profiles/http2_r2/: no gain at N=1, "
+                         "worse at N=8 on kube-lite)")
     ap.add_argument("--tls-apiserver", action=argparse.BooleanOptionalAction, default=True,
                     help="components reach kube-lite over HTTPS via kubeconfigs, as in a real cluster")
     args = ap.parse_args(argv)

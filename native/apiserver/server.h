@@ -56,10 +56,12 @@ struct Options {
   // Paginated LIST (limit/continue) serves later pages from a snapshot taken at the first
   // page; continue tokens expire after this long (then 410 Expired, as etcd compaction).
   int continue_ttl_ms = 60000;
-  // Webhook callouts offer HTTP/2 by ALPN, as the real apiserver's Go client does; the
-  // admission requests of concurrent writes then share one multiplexed connection.
+  // Webhook callouts offer HTTP/2 by ALPN, as the real apiserver's Go client does, and
+  // concurrent admission requests are multiplexed as streams.  The apiserver keeps one
+  // connection; kube-lite spreads them over 4 (one connection's single reader thread in
+  // this process is the bottleneck at 800 callouts in flight, profiles/http2_r2/).
   bool webhook_http2 = true;
-  size_t webhook_h2_connections = 1;
+  size_t webhook_h2_connections = 4;
 };
 
 class ApiServer {

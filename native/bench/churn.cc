@@ -19,11 +19,13 @@ ChurnDriver::ChurnDriver(ChurnOptions o) : opts_(std::move(o)) {
   kc.token = opts_.admin_token;
   kc.ca_pem = opts_.ca_pem;
   kc.timeout_ms = 60000;
+  kc.http2 = opts_.http2;
   admin_ = std::make_unique<kube::KubeClient>(kc);
   http::ClientOptions ho;
   ho.base_url = opts_.server;
   ho.timeout_ms = 60000;
   ho.max_idle = static_cast<size_t>(opts_.concurrency) * 2;
+  ho.http2 = opts_.http2;
   if (opts_.server.rfind("https", 0) == 0) ho.tls = net::TlsContext::client(opts_.ca_pem, false, "", "");
   http_ = std::make_unique<http::Client>(ho);
   pool_ = std::make_unique<ThreadPool>(static_cast<size_t>(std::max(1, opts_.concurrency)));

@@ -41,6 +41,9 @@ struct ChurnOptions {
   // batch with one sheet edit (POST {"rows":[{"id_username":...}],"append":true} to this
   // URL, the fake Google's operator endpoint), then waits for Ready.
   std::string approve_url;
+  // Tenant creates and admin deletes over HTTP/2 (one multiplexed connection each), as
+  // kubectl/client-go talk to a TLS apiserver; false = HTTP/1.1 keep-alive pools.
+  bool http2 = false;
 };
 
 class ChurnDriver {

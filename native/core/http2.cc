@@ -78,7 +78,7 @@ void Connection::start() {
   else put_setting(settings, 0x3, 1000);                           // MAX_CONCURRENT_STREAMS
   put_setting(settings, 0x4, kOurWindow);                          // INITIAL_WINDOW_SIZE
   std::string wu;
-  put32(wu, kOurWindow - kDefaultWindow);  // connection window: 64 KiB -> 1 MiB
+  put32(wu, kOurConnWindow - kDefaultWindow);  // connection window: 64 KiB -> 64 MiB
   {
     std::lock_guard<std::mutex> lk(write_mu_);
     bool ok = hello.empty() || io_->write_all(hello);
@@ -105,6 +105,7 @@ void Connection::close(uint32_t code) {
     std::lock_guard<std::mutex> lk(mu_);
     for (auto& [id, st] : streams_) st->cv.notify_all();
   }
+  window_cv_.notify_all();
   cv_.notify_all();
 }
 
@@ -261,7 +262,7 @@ bool Connection::send_data(Stream& s, std::string_view data, bool end_stream) {
     {
       std::unique_lock<std::mutex> lk(mu_);
       if (!data.empty()) {
-        cv_.wait(lk, [&] { return closed_ || s.reset || (conn_send_window_ > 0 && s.send_window > 0); });
+        window_cv_.wait(lk, [&] { return closed_ || s.reset || (conn_send_window_ > 0 && s.send_window > 0); });
       }
       if (closed_ || s.reset || s.local_closed) return false;
       n = std::min<size_t>({data.size(), static_cast<size_t>(std::max<int64_t>(0, conn_send_window_)),
@@ -294,6 +295,7 @@ void Connection::reset_stream(Stream& s, uint32_t code) {
   put32(p, code);
   write_frame(kRstStream, 0, s.id, p);
   s.cv.notify_all();
+  window_cv_.notify_all();
   cv_.notify_all();
 }
 
@@ -336,6 +338,7 @@ void Connection::fail_all() {
     dead.swap(streams_);
   }
   for (auto& [id, s] : dead) s->cv.notify_all();
+  window_cv_.notify_all();
   cv_.notify_all();
 }
 
@@ -481,6 +484,7 @@ void Connection::on_settings(uint8_t flags, std::string_view p) {
   }
   write_frame_locked(kSettings, kAck, 0, {});
   wl.unlock();
+  window_cv_.notify_all();
   cv_.notify_all();
 }
 
@@ -494,6 +498,7 @@ void Connection::on_window_update(uint32_t sid, std::string_view p) {
       s->send_window += inc;
     }
   }
+  window_cv_.notify_all();
   cv_.notify_all();
 }
 
@@ -509,6 +514,7 @@ void Connection::on_rst(uint32_t sid, std::string_view p) {
     }
   }
   if (s) s->cv.notify_all();
+  window_cv_.notify_all();
   cv_.notify_all();
 }
 
@@ -588,7 +594,7 @@ void Connection::on_data(uint32_t sid, uint8_t flags, std::string_view payload, 
       }
     }
     std::string out;
-    if (conn_recv_pending_ >= kOurWindow / 2) {
+    if (conn_recv_pending_ >= kOurConnWindow / 2) {
       std::string inc;
       put32(inc, static_cast<uint32_t>(conn_recv_pending_));
       append_frame(out, kWindowUpdate, 0, 0, inc);

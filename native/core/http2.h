@@ -49,7 +49,9 @@ enum ErrorCode : uint32_t {
 
 constexpr const char kPreface[] = "PRI * HTTP/2.0\r\n\r\nSM\r\n\r\n";
 constexpr uint32_t kDefaultWindow = 65535;
-constexpr uint32_t kOurWindow = 1u << 20;  // advertised receive window (stream + connection)
+constexpr uint32_t kOurWindow = 1u << 20;       // advertised receive window per stream
+constexpr uint32_t kOurConnWindow = 64u << 20;  // ... and per connection: hundreds of concurrent
+                                                // requests never wait for a WINDOW_UPDATE
 
 class Connection;
 
@@ -156,6 +158,7 @@ class Connection : public std::enable_shared_from_this<Connection> {
   std::mutex write_mu_;
   mutable std::mutex mu_;
   std::condition_variable cv_;
+  std::condition_variable window_cv_;  // senders blocked on flow control (window changes only)
   std::map<uint32_t, std::shared_ptr<Stream>> streams_;
   uint32_t next_stream_id_ = 1;
   uint32_t last_peer_stream_ = 0;

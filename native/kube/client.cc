@@ -120,6 +120,7 @@ KubeClient::KubeClient(KubeConfig cfg) : cfg_(std::move(cfg)) {
   o.base_url = cfg_.server;
   o.timeout_ms = cfg_.timeout_ms;
   o.tls_server_name = cfg_.tls_server_name;
+  o.http2 = cfg_.http2;
   if (cfg_.server.rfind("https", 0) == 0) {
     o.tls = net::TlsContext::client(cfg_.ca_pem, cfg_.insecure, cfg_.client_cert_pem, cfg_.client_key_pem);
   }

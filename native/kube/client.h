@@ -31,6 +31,9 @@ struct KubeConfig {
   std::string impersonate_user;
   std::vector<std::string> impersonate_groups;
   int timeout_ms = 30000;
+  // https: offer HTTP/2 and multiplex request/response calls on one connection, as
+  // client-go does (watches keep their own HTTP/1.1 streams).
+  bool http2 = false;
   // Throttling (HTTP 429, or 5xx with Retry-After): wait as the server asks — capped at
   // max_retry_after_s, 1 s when no header — and retry up to this many times (client-go
   // retries 429 with Retry-After up to 10 times).  0 = surface the error at once.

@@ -3,7 +3,7 @@
 # connection like the real apiserver) vs HTTP/1.1 (--webhook-http1), interleaved A/B of
 # the headline bench on the MI355X box, 3 runs each.
 set -o pipefail
-OUT=gpurun_out/r2e
+OUT=${OUT:-gpurun_out/r2e}
 rm -rf "$OUT" && mkdir -p "$OUT"
 export TMPDIR=/tmp
 step() { echo "[$(date +%T)] $*"; }
