@@ -701,6 +701,12 @@ void Server::serve_h2(int fd, std::unique_ptr<net::Stream> s, const std::string&
     frames = now;
     if (idle >= opts_.idle_timeout_ms) break;
   }
+  if (stop_.cancelled() && !conn->closed()) {
+    // graceful: GOAWAY, let the streams in flight finish (bounded by stop()'s grace)
+    conn->drain();
+    std::unique_lock<std::mutex> lk(inflight->mu);
+    inflight->cv.wait_for(lk, std::chrono::milliseconds(grace_ms_.load()), [&] { return inflight->n == 0; });
+  }
   conn->close();
   conn->join();  // no stream is dispatched after this
   {
@@ -737,6 +743,7 @@ bool Server::dispatch(Request& req, ResponseWriter& w) {
 
 void Server::stop(std::chrono::milliseconds grace) {
   if (!started_) return;
+  grace_ms_ = grace.count();
   stop_.cancel();
   if (wake_pipe_[1] >= 0) {
     char c = 1;

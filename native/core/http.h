@@ -183,6 +183,7 @@ class Server {
   std::condition_variable conns_cv_;
   std::map<int, net::Stream*> conns_;
   bool started_ = false;
+  std::atomic<int64_t> grace_ms_{10000};  // stop()'s grace, for draining HTTP/2 connections
   struct WorkerPool;  // HTTP/2 stream workers (cached threads)
   std::shared_ptr<WorkerPool> h2_workers_;
 };

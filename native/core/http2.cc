@@ -437,8 +437,11 @@ void Connection::reader_loop() {
         on_rst(sid, p);
         break;
       case kGoaway: {
-        std::lock_guard<std::mutex> lk(mu_);
-        goaway_received_ = true;
+        if (len < 8) {
+          goaway(kFrameSizeError, "bad GOAWAY frame");
+          break;
+        }
+        on_goaway(be32(p.data()) & 0x7fffffff);
         break;
       }
       case kPushPromise:
@@ -534,30 +537,78 @@ void Connection::on_headers(uint32_t sid, uint8_t flags, const std::string& bloc
         // trailers for a stream we already forgot, or a bogus id: ignore (decoded for HPACK state)
         return;
       }
-      last_peer_stream_ = sid;
-      s = std::make_shared<Stream>();
-      s->id = sid;
-      s->send_window = peer_initial_window_;
-      streams_[sid] = s;
-    }
-    if (!s->headers_received) {
-      s->headers = std::move(hl);
-      s->headers_received = true;
-    } else {
-      for (auto& h : hl) s->trailers.push_back(std::move(h));
-    }
-    if (flags & kEndStream) {
-      s->remote_closed = true;
-      if (role_ == Role::kServer && !s->dispatched) {
-        s->dispatched = true;
-        dispatch = s;
+      if (goaway_sent_) {
+        s = nullptr;  // draining: refused below (the peer may retry it elsewhere)
+      } else {
+        last_peer_stream_ = sid;
+        s = std::make_shared<Stream>();
+        s->id = sid;
+        s->send_window = peer_initial_window_;
+        streams_[sid] = s;
       }
-      maybe_forget(s);
     }
+    if (s) {
+      if (!s->headers_received) {
+        s->headers = std::move(hl);
+        s->headers_received = true;
+      } else {
+        for (auto& h : hl) s->trailers.push_back(std::move(h));
+      }
+      if (flags & kEndStream) {
+        s->remote_closed = true;
+        if (role_ == Role::kServer && !s->dispatched) {
+          s->dispatched = true;
+          dispatch = s;
+        }
+        maybe_forget(s);
+      }
+    }
+  }
+  if (!s) {
+    std::string p;
+    put32(p, kRefusedStream);
+    write_frame(kRstStream, 0, sid, p);
+    return;
   }
   s->cv.notify_all();
   cv_.notify_all();
   if (dispatch && on_request_) on_request_(shared_from_this(), dispatch);
+}
+
+void Connection::on_goaway(uint32_t last_stream) {
+  // RFC 9113 6.8: our streams above last_stream were not processed and may be retried
+  std::vector<std::shared_ptr<Stream>> refused;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    goaway_received_ = true;
+    for (auto it = streams_.upper_bound(last_stream); it != streams_.end();) {
+      if ((it->first % 2) == (role_ == Role::kClient ? 1u : 0u)) {
+        it->second->reset = true;
+        it->second->reset_code = kRefusedStream;
+        refused.push_back(it->second);
+        it = streams_.erase(it);
+      } else {
+        ++it;
+      }
+    }
+  }
+  for (auto& st : refused) st->cv.notify_all();
+  window_cv_.notify_all();
+  cv_.notify_all();
+}
+
+void Connection::drain() {
+  uint32_t last;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (goaway_sent_ || closed_) return;
+    goaway_sent_ = true;
+    last = last_peer_stream_;
+  }
+  std::string p;
+  put32(p, last);
+  put32(p, kNoError);
+  write_frame(kGoaway, 0, 0, p);
 }
 
 void Connection::on_data(uint32_t sid, uint8_t flags, std::string_view payload, size_t flow_len) {

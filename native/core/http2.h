@@ -91,6 +91,10 @@ class Connection : public std::enable_shared_from_this<Connection> {
   void start();
   // GOAWAY (best effort) + socket shutdown; the reader thread ends, all streams reset.
   void close(uint32_t code = kNoError);
+  // Server: graceful drain.  Sends GOAWAY(NO_ERROR) naming the last stream accepted; the
+  // streams in flight finish normally and any the peer opens afterwards are refused with
+  // REFUSED_STREAM (which a client retries on a new connection).
+  void drain();
   void join();
   bool closed() const { return closed_.load(); }
   // Client: new streams may still be opened (not closed, no GOAWAY, ids left).
@@ -146,6 +150,7 @@ class Connection : public std::enable_shared_from_this<Connection> {
   void on_settings(uint8_t flags, std::string_view payload);
   void on_window_update(uint32_t sid, std::string_view payload);
   void on_rst(uint32_t sid, std::string_view payload);
+  void on_goaway(uint32_t last_stream);
   void fail_all();
   void goaway(uint32_t code, const std::string& why);
   std::shared_ptr<Stream> find(uint32_t sid);
@@ -166,6 +171,7 @@ class Connection : public std::enable_shared_from_this<Connection> {
   uint32_t peer_initial_window_ = kDefaultWindow;
   uint32_t peer_max_frame_ = 16384;
   bool goaway_received_ = false;
+  bool goaway_sent_ = false;  // drain(): no new peer streams
   std::atomic<bool> closed_{false};
   std::atomic<uint64_t> frames_in_{0};
   std::thread reader_;

@@ -21,6 +21,7 @@ void register_sync(py::module_& m);
 void register_kube(py::module_& m);
 void register_gpu(py::module_& m);
 void register_grpc(py::module_& m);
+void register_http(py::module_& m);
 }  // namespace bgc_py
 
 namespace {
@@ -159,4 +160,5 @@ PYBIND11_MODULE(_native, m) {
   bgc_py::register_kube(m);
   bgc_py::register_gpu(m);
   bgc_py::register_grpc(m);
+  bgc_py::register_http(m);
 }
