@@ -257,6 +257,37 @@ struct Stored {
   Managers managers;
 };
 
+// PartialObjectMetadata (meta.k8s.io/v1): what metadata-only clients ask for with
+// Accept: application/json;as=PartialObjectMetadata[List];g=meta.k8s.io;v=v1.
+bool wants_metadata(const http::Request& req) {
+  const std::string* a = req.headers.get("Accept");
+  return a && a->find("as=PartialObjectMetadata") != std::string::npos;
+}
+
+void dump_partial_metadata(const Value& obj, std::string& out) {
+  out += "{\"kind\":\"PartialObjectMetadata\",\"apiVersion\":\"meta.k8s.io/v1\",\"metadata\":";
+  obj.get("metadata").dump_to(out);
+  out += "}";
+}
+
+// {"type":T,"object":O}\n -> {"type":T,"object":<PartialObjectMetadata of O>}\n, from the
+// serialized line (no re-parse of the object).
+std::string partial_metadata_line(const std::string& line) {
+  std::string_view body(line);
+  while (!body.empty() && (body.back() == '\n' || body.back() == '\r')) body.remove_suffix(1);
+  const std::string_view type = json::raw_member(body, "type");
+  const std::string_view md = json::raw_member(json::raw_member(body, "object"), "metadata");
+  std::string out;
+  out.reserve(md.size() + 128);
+  out += "{\"type\":";
+  out.append(type.data(), type.size());
+  out += ",\"object\":{\"kind\":\"PartialObjectMetadata\",\"apiVersion\":\"meta.k8s.io/v1\",\"metadata\":";
+  if (md.empty()) out += "{}";
+  else out.append(md.data(), md.size());
+  out += "}}\n";
+  return out;
+}
+
 struct EventRec {
   uint64_t rv;
   std::string type_key;
@@ -265,6 +296,15 @@ struct EventRec {
   // object: the watch cache must not pin every old version's full tree in memory.
   std::shared_ptr<const Value> meta;
   std::shared_ptr<const std::string> line;  // {"type":..,"object":..}\n
+  // The PartialObjectMetadata form, built once on first use by a metadata-only watch.
+  const std::string& metadata_line() const {
+    std::call_once(meta_once_, [this] { meta_line_ = partial_metadata_line(*line); });
+    return meta_line_;
+  }
+
+ private:
+  mutable std::once_flag meta_once_;
+  mutable std::string meta_line_;
 };
 
 // {"metadata":{"name":..,"labels":..}} of an object: the fields watch filters read.
@@ -1673,7 +1713,7 @@ struct ApiServer::Impl {
     w.send_json(200, status_body(200, "", "").dump());
   }
 
-  void do_get(ParsedPath& p, http::ResponseWriter& w) {
+  void do_get(ParsedPath& p, http::ResponseWriter& w, bool meta_only = false) {
     std::shared_ptr<const Value> obj;
     {
       SharedStoreLock lk(p.ti->store->mu, p.ti->store->stats);
@@ -1681,6 +1721,12 @@ struct ApiServer::Impl {
       auto it = b.find(obj_key(p.ti->rt, p.ns, p.name));
       if (it == b.end()) throw not_found(p.ti->rt, p.name);
       obj = it->second.obj;
+    }
+    if (meta_only) {
+      std::string out;
+      dump_partial_metadata(*obj, out);
+      w.send_json(200, out);
+      return;
     }
     w.send_json(200, obj->dump());
   }
@@ -1751,9 +1797,11 @@ struct ApiServer::Impl {
       list_snapshots.erase(snap_id);  // last page served
     }
     if (limit > 0) list_pages.fetch_add(1);
-    std::string out = "{\"apiVersion\":" + json::quote(p.ti->rt.api_version()) + ",\"kind\":" +
-                      json::quote(p.ti->rt.kind + "List") + ",\"metadata\":{\"resourceVersion\":\"" + rv_str(list_rv) +
-                      "\"";
+    const bool meta_only = wants_metadata(req);
+    std::string out = meta_only ? std::string("{\"apiVersion\":\"meta.k8s.io/v1\",\"kind\":\"PartialObjectMetadataList\"")
+                                : "{\"apiVersion\":" + json::quote(p.ti->rt.api_version()) + ",\"kind\":" +
+                                      json::quote(p.ti->rt.kind + "List");
+    out += ",\"metadata\":{\"resourceVersion\":\"" + rv_str(list_rv) + "\"";
     if (!next.empty()) {
       out += ",\"continue\":" + json::quote(next) +
              ",\"remainingItemCount\":" + std::to_string(items.size() - end);
@@ -1761,7 +1809,8 @@ struct ApiServer::Impl {
     out += "},\"items\":[";
     for (size_t i = offset; i < end; ++i) {
       if (i != offset) out.push_back(',');
-      items[i]->dump_to(out);
+      if (meta_only) dump_partial_metadata(*items[i], out);
+      else items[i]->dump_to(out);
     }
     out += "]}";
     w.send_json(200, out);
@@ -1776,6 +1825,7 @@ struct ApiServer::Impl {
     sub.fields = parse_field_selector(req.query_param("fieldSelector"));
     if (!sub.fields.ns.empty()) sub.ns = sub.fields.ns;
     std::string rv_s = req.query_param("resourceVersion");
+    const bool meta_only = wants_metadata(req);
     int timeout_s = opts.max_watch_seconds;
     if (req.has_query_param("timeoutSeconds")) timeout_s = std::min(timeout_s, std::atoi(req.query_param("timeoutSeconds").c_str()));
     bool bookmarks = req.query_param("allowWatchBookmarks") == "true";
@@ -1810,7 +1860,8 @@ struct ApiServer::Impl {
           if (!sub.fields.name.empty() && meta.get_string("name") != sub.fields.name) continue;
           if (!sub.sel.empty() && !selector_matches(sub.sel, *st.obj)) continue;
           std::string line = "{\"type\":\"ADDED\",\"object\":";
-          st.obj->dump_to(line);
+          if (meta_only) dump_partial_metadata(*st.obj, line);
+          else st.obj->dump_to(line);
           line += "}\n";
           initial.push_back(std::make_shared<const std::string>(std::move(line)));
         }
@@ -1825,7 +1876,7 @@ struct ApiServer::Impl {
           if (!sub.ns.empty() && e->ns != sub.ns) continue;
           if (!sub.fields.name.empty() && e->meta->get("metadata").get_string("name") != sub.fields.name) continue;
           if (!sub.sel.empty() && !selector_matches(sub.sel, *e->meta)) continue;
-          initial.push_back(e->line);
+          initial.push_back(meta_only ? std::make_shared<const std::string>(e->metadata_line()) : e->line);
         }
       }
       if (!gone) {
@@ -1879,7 +1930,7 @@ struct ApiServer::Impl {
       }
       if (!batch.empty()) {
         std::string buf;
-        for (auto& e : batch) buf += *e->line;
+        for (auto& e : batch) buf += meta_only ? e->metadata_line() : *e->line;
         if (!w.write_chunk(buf)) break;
       }
       if (closed || overflow) break;
@@ -1899,7 +1950,7 @@ struct ApiServer::Impl {
         }
         if (!pending.empty()) {
           std::string buf;
-          for (auto& e : pending) buf += *e->line;
+          for (auto& e : pending) buf += meta_only ? e->metadata_line() : *e->line;
           if (!w.write_chunk(buf)) break;
         }
         Value bm = Value::object({{"type", "BOOKMARK"},
@@ -2153,7 +2204,7 @@ struct ApiServer::Impl {
         }
         return;
       }
-      if (m == "GET") do_get(p, w);
+      if (m == "GET") do_get(p, w, wants_metadata(req));
       else if (m == "PUT") do_update(p, req, user, w);
       else if (m == "PATCH") do_patch(p, req, user, w);
       else if (m == "DELETE") do_delete(p, req, user, w);

@@ -70,10 +70,10 @@ int main() {
   co.child_delete_delay = std::chrono::milliseconds(cfg.child_delete_delay_ms);
   kube::Controller ctrl(*client, kube::types::UserBootstrap, co);
   const std::string sel = cfg.label_children ? controller::child_label_selector() : "";
-  ctrl.owns(kube::types::Namespace, nullptr, sel);
-  ctrl.owns(kube::types::ResourceQuota, nullptr, sel);
-  ctrl.owns(kube::types::Role, nullptr, sel);
-  ctrl.owns(kube::types::RoleBinding, nullptr, sel);
+  ctrl.owns(kube::types::Namespace, nullptr, sel, cfg.metadata_watches);
+  ctrl.owns(kube::types::ResourceQuota, nullptr, sel, cfg.metadata_watches);
+  ctrl.owns(kube::types::Role, nullptr, sel, cfg.metadata_watches);
+  ctrl.owns(kube::types::RoleBinding, nullptr, sel, cfg.metadata_watches);
   controller::Reconciler rec(*client, ctrl, cfg);
   auto& echoes = metrics::Registry::global().counter(
       "bgc_controller_own_write_events_total", "Child watch events dropped as echoes of our own applies");

@@ -23,6 +23,7 @@ Config Config::from_env(const EnvConfig& env) {
   c.error_requeue_ms = static_cast<int64_t>(env.u64_or("error_requeue_ms", 3000));
   c.error_backoff_base_ms = static_cast<int64_t>(env.u64_or("error_backoff_base_ms", 0));
   c.label_children = env.boolean_or("label_children", true);
+  c.metadata_watches = env.boolean_or("metadata_watches", true);
   c.lease = kube::LeaseSettings::from_env(env, "bacchus-gpu-controller");
   return c;
 }

@@ -56,6 +56,9 @@ struct Config {
   int64_t error_backoff_base_ms = 0;
   int64_t child_delete_delay_ms = 50;
   bool label_children = true;  // see kManagedByLabel
+  // Child watches ask for PartialObjectMetadata only: the controller reads a child's
+  // resourceVersion and ownerReferences, never its spec (kube-rs metadata_watcher).
+  bool metadata_watches = true;
   kube::LeaseSettings lease;  // optional leader election (CONF_LEADER_ELECTION, ...)
   // reference fields are required (controller.rs:24-28); the rest default
   static Config from_env(const EnvConfig& env);

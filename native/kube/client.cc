@@ -173,12 +173,13 @@ static int retry_after_seconds(const http::Response& r, int cap) {
 }
 
 http::Response KubeClient::raw(const std::string& method, const std::string& path, const std::string& body,
-                               const std::string& content_type) {
+                               const std::string& content_type, const std::string& accept) {
   static auto& throttled = metrics::Registry::global().counter(
       "bgc_kube_client_throttled_total", "Requests the apiserver throttled (429 / Retry-After) and that were retried");
   for (int attempt = 0;; ++attempt) {
     http::Headers h = auth_headers();
     if (!body.empty() || method == "POST" || method == "PUT" || method == "PATCH") h.set("Content-Type", content_type);
+    if (!accept.empty()) h.set("Accept", accept);
     http::Response r = http_->request(method, path, body, &h);
     const int wait_s = retry_after_seconds(r, cfg_.max_retry_after_s);
     if (wait_s < 0 || attempt >= cfg_.max_throttle_retries) return r;
@@ -190,8 +191,8 @@ http::Response KubeClient::raw(const std::string& method, const std::string& pat
 }
 
 Value KubeClient::call(const std::string& method, const std::string& path, const std::string& body,
-                       const std::string& content_type) {
-  http::Response r = raw(method, path, body, content_type);
+                       const std::string& content_type, const std::string& accept) {
+  http::Response r = raw(method, path, body, content_type, accept);
   if (r.status < 200 || r.status >= 300) throw_api_error(r);
   if (r.body.empty()) return Value();
   return json::parse(r.body);
@@ -225,7 +226,7 @@ Value KubeClient::list(const ResourceType& rt, const std::string& ns, const List
                                                           {"resourceVersion", o.resource_version},
                                                           {"limit", o.limit ? std::to_string(o.limit) : ""},
                                                           {"continue", o.continue_token}});
-  return call("GET", path);
+  return call("GET", path, "", "application/json", o.metadata_only ? kAcceptMetadataList : "");
 }
 
 Value KubeClient::create(const ResourceType& rt, const std::string& ns, const Value& body,
@@ -298,6 +299,7 @@ std::unique_ptr<http::StreamingResponse> KubeClient::watch(const ResourceType& r
                                                           {"sendInitialEvents", o.send_initial_events ? "true" : ""},
                                                           {"resourceVersionMatch", o.send_initial_events ? "NotOlderThan" : ""}});
   http::Headers h = auth_headers();
+  if (o.metadata_only) h.set("Accept", kAcceptMetadata);
   auto s = http_->stream("GET", path, &h);
   if (s->status < 200 || s->status >= 300) {
     http::Response r;

@@ -65,12 +65,16 @@ class ApiError : public std::runtime_error {
   json::Value status_;
 };
 
+// metadata_only: ask for PartialObjectMetadata(List) (meta.k8s.io/v1) instead of the full
+// objects, as client-go's metadata informers and kube-rs' metadata_watcher do: the apiserver
+// sends only each object's metadata.
 struct ListOptions {
   std::string label_selector;
   std::string field_selector;
   std::string resource_version;
   int64_t limit = 0;
   std::string continue_token;
+  bool metadata_only = false;
 };
 
 struct WatchOptions {
@@ -82,7 +86,14 @@ struct WatchOptions {
   // Streaming list: replay the current state as ADDED events, ended by a BOOKMARK
   // annotated k8s.io/initial-events-end (sendInitialEvents + resourceVersionMatch).
   bool send_initial_events = false;
+  bool metadata_only = false;  // events carry PartialObjectMetadata
 };
+
+// Accept headers of metadata-only requests (with a plain-JSON fallback, as client-go sends).
+constexpr const char kAcceptMetadataList[] =
+    "application/json;as=PartialObjectMetadataList;g=meta.k8s.io;v=v1,application/json";
+constexpr const char kAcceptMetadata[] =
+    "application/json;as=PartialObjectMetadata;g=meta.k8s.io;v=v1,application/json";
 
 class KubeClient {
  public:
@@ -119,9 +130,9 @@ class KubeClient {
 
   // Low level: throws ApiError on non-2xx.
   json::Value call(const std::string& method, const std::string& path, const std::string& body = "",
-                   const std::string& content_type = "application/json");
+                   const std::string& content_type = "application/json", const std::string& accept = "");
   http::Response raw(const std::string& method, const std::string& path, const std::string& body = "",
-                     const std::string& content_type = "application/json");
+                     const std::string& content_type = "application/json", const std::string& accept = "");
   const KubeConfig& config() const { return cfg_; }
   uint64_t throttled() const { return throttled_.load(); }
 

@@ -44,6 +44,10 @@ Watcher::Watcher(KubeClient& client, ResourceType rt, std::string ns, std::strin
 }
 
 ObjPtr Watcher::typed(Value obj) const {
+  if (metadata_only_) {  // PartialObjectMetadata -> a metadata view of the watched type
+    obj["apiVersion"] = rt_.api_version();
+    obj["kind"] = rt_.kind;
+  }
   if (!obj.contains("apiVersion")) obj["apiVersion"] = rt_.api_version();
   if (!obj.contains("kind")) obj["kind"] = rt_.kind;
   return std::make_shared<const Value>(std::move(obj));
@@ -56,6 +60,7 @@ std::string Watcher::list_all(std::vector<ObjPtr>& out, CancelToken& stop) {
     lo.label_selector = selector_;
     lo.field_selector = field_selector_;
     lo.limit = page_size_ > 0 ? page_size_ : 0;
+    lo.metadata_only = metadata_only_;
     std::string rv;
     try {
       do {
@@ -101,6 +106,7 @@ void Watcher::run(CancelToken& stop, const std::function<void(const WatchEvent&)
       WatchOptions wo;
       wo.label_selector = selector_;
       wo.field_selector = field_selector_;
+      wo.metadata_only = metadata_only_;
       if (need_list) {  // streaming
         wo.send_initial_events = true;
         initial_phase = true;
@@ -164,7 +170,8 @@ void Watcher::run(CancelToken& stop, const std::function<void(const WatchEvent&)
           if (type == "ADDED") initial.push_back(typed(std::move(obj)));
           continue;
         }
-        WatchEvent we{WatchEvent::Type::Added, std::make_shared<const Value>(std::move(obj)), {}};
+        WatchEvent we{WatchEvent::Type::Added,
+                      metadata_only_ ? typed(std::move(obj)) : std::make_shared<const Value>(std::move(obj)), {}};
         if (type == "MODIFIED") we.type = WatchEvent::Type::Modified;
         else if (type == "DELETED") we.type = WatchEvent::Type::Deleted;
         else if (type != "ADDED") continue;
@@ -398,10 +405,11 @@ Controller::Controller(KubeClient& client, ResourceType primary, Options opts)
 
 Controller::~Controller() { queue_.shutdown(); }
 
-void Controller::owns(const ResourceType& child, Mapper mapper, std::string label_selector) {
+void Controller::owns(const ResourceType& child, Mapper mapper, std::string label_selector, bool metadata_only) {
   auto c = std::make_unique<Child>();
   c->rt = child;
   c->selector = std::move(label_selector);
+  c->metadata_only = metadata_only;
   c->mapper = mapper ? std::move(mapper) : owner_mapper(primary_);
   c->store = std::make_unique<Store>(child);
   children_.push_back(std::move(c));
@@ -458,6 +466,7 @@ void Controller::run(CancelToken& stop, Reconciler reconcile, ErrorPolicy error_
     Child* c = cp.get();
     threads.emplace_back([&, c] {
       Watcher w(client_, c->rt, "", c->selector);
+      w.set_metadata_only(c->metadata_only);
       w.run(stop, [&, c](const WatchEvent& ev) {
         c->store->apply(ev);
         c->gauge->set(static_cast<double>(c->store->size()));

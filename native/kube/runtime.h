@@ -71,6 +71,9 @@ class Watcher {
           std::string field_selector = "");
   void set_page_size(int64_t n) { page_size_ = n; }
   void set_streaming_lists(bool on) { streaming_ = on; }
+  // Only object metadata (PartialObjectMetadata lists and events); cached objects keep
+  // the watched type's kind/apiVersion and carry just "metadata".
+  void set_metadata_only(bool on) { metadata_only_ = on; }
   void run(CancelToken& stop, const std::function<void(const WatchEvent&)>& on_event);
   // Optional pre-parse filter on raw watch lines (e.g. a name prefix): ADDED/MODIFIED/
   // DELETED lines it rejects are skipped without JSON parsing.  A consumer whose filter
@@ -87,6 +90,7 @@ class Watcher {
   ObjPtr typed(json::Value obj) const;
   int64_t page_size_;
   bool streaming_;
+  bool metadata_only_ = false;
   std::atomic<uint64_t> list_pages_{0};
   KubeClient& client_;
   ResourceType rt_;
@@ -190,7 +194,10 @@ class Controller {
   // and apiVersion match the primary type, mapped by name).
   // `label_selector` limits the child watch server-side (e.g. to children this controller
   // labelled); empty = every object of the kind, like kube-runtime's default.
-  void owns(const ResourceType& child, Mapper mapper = nullptr, std::string label_selector = "");
+  // `metadata_only`: watch PartialObjectMetadata (enough for the default mapper and for
+  // resourceVersion checks; the child store then holds metadata only).
+  void owns(const ResourceType& child, Mapper mapper = nullptr, std::string label_selector = "",
+            bool metadata_only = false);
   // Child ADDED/MODIFIED events for which `filter` returns false do not enqueue the owner
   // (e.g. the echo of the reconciler's own apply). DELETED events and relists always do.
   using ChildFilter = std::function<bool(const ResourceType& child_type, const json::Value& child)>;
@@ -215,6 +222,7 @@ class Controller {
     ResourceType rt;
     Mapper mapper;
     std::string selector;
+    bool metadata_only = false;
     std::unique_ptr<Store> store;
     metrics::Gauge* gauge = nullptr;  // bgc_controller_store_objects{resource=...}
   };

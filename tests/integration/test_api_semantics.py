@@ -188,3 +188,58 @@ def test_streaming_lists_fall_back_to_list_when_rejected():
         wait_for(lambda: c.admin.get_or_none("namespaces", "fb2"), timeout=15, desc="fb2 via watch")
         assert c.stats()["list_pages"] - pages0 >= 5  # UB + 4 owned kinds listed after the fallback
         assert c.stats()["faults_hit"] >= 5
+
+
+META = "application/json;as=PartialObjectMetadata;g=meta.k8s.io;v=v1,application/json"
+META_LIST = "application/json;as=PartialObjectMetadataList;g=meta.k8s.io;v=v1,application/json"
+
+
+def test_partial_object_metadata_get_list_watch():
+    """metadata-only clients (client-go metadata informers, kube-rs metadata_watcher): the
+    apiserver answers GET/LIST/WATCH with PartialObjectMetadata(List) when asked by Accept."""
+    with Cluster(admission=False, controller=False) as c:
+        c.admin.create("namespaces", {"apiVersion": "v1", "kind": "Namespace",
+                                      "metadata": {"name": "pm1", "labels": {"a": "b"}}})
+        c.admin.create("resourcequotas", {"apiVersion": "v1", "kind": "ResourceQuota",
+                                          "metadata": {"name": "q", "namespace": "pm1"},
+                                          "spec": {"hard": {"requests.amd.com/gpu": "2"}}}, namespace="pm1")
+        h = {"Authorization": "Bearer admin-token"}
+        url = c.server + "/api/v1/namespaces/pm1/resourcequotas"
+        o = requests.get(url + "/q", headers={**h, "Accept": META}, timeout=5).json()
+        assert (o["kind"], o["apiVersion"]) == ("PartialObjectMetadata", "meta.k8s.io/v1")
+        assert o["metadata"]["name"] == "q" and "spec" not in o
+        full = requests.get(url + "/q", headers=h, timeout=5).json()
+        assert full["spec"]["hard"] == {"requests.amd.com/gpu": "2"}
+        assert o["metadata"]["resourceVersion"] == full["metadata"]["resourceVersion"]
+        lst = requests.get(c.server + "/api/v1/namespaces?labelSelector=a%3Db",
+                           headers={**h, "Accept": META_LIST}, timeout=5).json()
+        assert (lst["kind"], lst["apiVersion"]) == ("PartialObjectMetadataList", "meta.k8s.io/v1")
+        assert [i["metadata"]["name"] for i in lst["items"]] == ["pm1"]
+        assert all(i["kind"] == "PartialObjectMetadata" and set(i) == {"kind", "apiVersion", "metadata"}
+                   for i in lst["items"])
+        rv = lst["metadata"]["resourceVersion"]
+        # a resumed watch (history) and the live stream both carry metadata only
+        c.admin.merge_patch("resourcequotas", "q", {"spec": {"hard": {"requests.amd.com/gpu": "4"}}}, namespace="pm1")
+        with requests.get(url + f"?watch=1&resourceVersion={rv}&timeoutSeconds=1",
+                          headers={**h, "Accept": META}, stream=True, timeout=10) as r:
+            events = [json.loads(line) for line in r.iter_lines() if line]
+        mods = [e for e in events if e["type"] == "MODIFIED"]
+        assert mods and all(set(e["object"]) == {"kind", "apiVersion", "metadata"} for e in mods)
+        assert mods[-1]["object"]["metadata"]["name"] == "q"
+
+
+@pytest.mark.parametrize("metadata_watches", ["true", "false"])
+def test_controller_converges_with_metadata_child_watches(metadata_watches):
+    with Cluster(admission=False, controller_env={"CONF_METADATA_WATCHES": metadata_watches,
+                                                  "CONF_REQUEUE_SECS": "3600"}) as c:
+        c.admin.create("userbootstraps", ub("mw1", quota={"hard": {"requests.amd.com/gpu": "1"}}))
+        wait_for(lambda: c.admin.get_or_none("resourcequotas", "mw1", "mw1"), desc="quota")
+        # drift on a child is repaired (the MODIFIED event of a metadata watch is enough)
+        c.admin.merge_patch("resourcequotas", "mw1", {"spec": {"hard": {"requests.amd.com/gpu": "7"}}}, namespace="mw1")
+        wait_for(lambda: c.admin.get("resourcequotas", "mw1", "mw1")["spec"]["hard"] == {"requests.amd.com/gpu": "1"},
+                 timeout=15, desc="drift repaired")
+        # a deleted child is re-created
+        uid = c.admin.get("resourcequotas", "mw1", "mw1")["metadata"]["uid"]
+        c.admin.delete("resourcequotas", "mw1", namespace="mw1")
+        wait_for(lambda: (c.admin.get_or_none("resourcequotas", "mw1", "mw1") or {"metadata": {"uid": uid}})
+                 ["metadata"]["uid"] != uid, timeout=15, desc="re-created")

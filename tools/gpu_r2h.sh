@@ -3,7 +3,7 @@
 # (default) vs HTTP/1.1 keep-alive pools, at N=1 on the MI355X and N=4/8 gloo ranks
 # (BGC_BENCH_CPU=1, ranks do not touch the card) on the box's 16-CPU share.
 set -o pipefail
-OUT=gpurun_out/r2h
+OUT=${OUT:-gpurun_out/r2h}
 rm -rf "$OUT" && mkdir -p "$OUT"
 export TMPDIR=/tmp
 step() { echo "[$(date +%T)] $*"; }
@@ -15,8 +15,8 @@ nn() {  # n, name, extra args
     --master-addr 127.0.0.1 --master-port $((29600+$1)) bench.py --gpus $1 --steps 20 --warmup 3 --report-cpu \
     --no-tuned-phase --json-out "$OUT/$2.json" "${@:3}" > "$OUT/$2.log" 2>&1
 }
-n1 n1_h2 && n1 n1_h1 --no-driver-http2 && n1 n1_h2b && n1 n1_h1b --no-driver-http2 &&
-nn 4 n4_h2 && nn 4 n4_h1 --no-driver-http2 && nn 8 n8_h2 && nn 8 n8_h1 --no-driver-http2
+n1 n1_h2 --driver-http2 && n1 n1_h1 && n1 n1_h2b --driver-http2 && n1 n1_h1b &&
+nn 4 n4_h2 --driver-http2 && nn 4 n4_h1 && nn 8 n8_h2 --driver-http2 && nn 8 n8_h1
 rc=$?
 step "done rc=$rc"
 for f in "$OUT"/*.json; do python3 -c "
