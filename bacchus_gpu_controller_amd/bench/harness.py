@@ -360,6 +360,7 @@ def run(args):
             google.set_rows([{"id_username": name} for r in range(d.world) for ph, _ in phases
                              for s in range(total_steps) for name in _names(r, ph, s, args.batch)])
         ctrl_env = {"CONF_WORKERS": str(controller_workers)}
+        ctrl_env.update(dict(kv.split("=", 1) for kv in args.controller_env))
         sync_env = {"CONF_WATCH": "true", "CONF_WORKERS": str(sync_workers), "RUST_LOG": args.log_level,
                     "CONF_SHEET_POLL_MS": str(args.sheet_poll_ms)}
         if semantics in ("reference", "reference-controller"):
@@ -495,6 +496,8 @@ def main(argv=None):
                     help="kube-lite storage commit latency per write (etcd model)")
     ap.add_argument("--sync-interval", type=int, default=60, help="synchronizer tick (s); the reference default is 60")
     ap.add_argument("--apiserver-arg", action="append", default=[], help="extra kube-lite flag (repeatable)")
+    ap.add_argument("--controller-env", action="append", default=[], metavar="CONF_X=V",
+                    help="extra controller environment (repeatable), e.g. CONF_METADATA_WATCHES=false")
     ap.add_argument("--report-cpu", action="store_true", help="add RSS, object counts and controller gauges")
     ap.add_argument("--driver-http2", action=argparse.BooleanOptionalAction, default=False,
                     help="tenant load over HTTP/2 multiplexed connections (profiles/http2_r2/: no gain at N=1, "
