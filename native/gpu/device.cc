@@ -50,6 +50,9 @@ Value to_json(const GpuInfo& g) {
   v["drm_render"] = g.drm_render;
   v["drm_card"] = g.drm_card;
   v["bad_page_threshold"] = g.bad_page_threshold;
+  v["pcie_max_width"] = g.pcie_max_width;
+  v["pcie_max_speed_mts"] = g.pcie_max_speed_mts;
+  v["pcie_max_gen"] = g.pcie_max_gen;
   Value links = Value::array();
   for (const auto& l : g.links) links.push_back(to_json(l));
   v["links"] = links;
@@ -130,6 +133,12 @@ Value to_json(const Telemetry& t) {
   v["ecc_deferred"] = static_cast<unsigned long long>(t.ecc_deferred);
   v["xgmi_links_up"] = t.xgmi_links_up;
   v["xgmi_links_total"] = t.xgmi_links_total;
+  if (t.pcie_width >= 0) v["pcie_width"] = t.pcie_width;
+  if (t.pcie_speed_mts >= 0) v["pcie_speed_mts"] = t.pcie_speed_mts;
+  if (t.pcie_replays >= 0) v["pcie_replays"] = t.pcie_replays;
+  if (t.pcie_recoveries >= 0) v["pcie_recoveries"] = t.pcie_recoveries;
+  if (t.pcie_nak_sent >= 0) v["pcie_nak_sent"] = t.pcie_nak_sent;
+  if (t.pcie_nak_received >= 0) v["pcie_nak_received"] = t.pcie_nak_received;
   if (t.ras_ok) {
     v["retired_pages"] = static_cast<unsigned long long>(t.retired_pages);
     v["unreservable_pages"] = static_cast<unsigned long long>(t.unreservable_pages);
@@ -178,6 +187,10 @@ GpuInfo gpu_info_from_json(const Value& v) {
   g.drm_render = v.get("drm_render").is_int() ? static_cast<int>(v.get("drm_render").as_int()) : -1;
   g.drm_card = v.get("drm_card").is_int() ? static_cast<int>(v.get("drm_card").as_int()) : -1;
   g.bad_page_threshold = static_cast<uint32_t>(u64_or(v, "bad_page_threshold", 0));
+  auto int_or = [&](const char* k, int d) { return v.get(k).is_int() ? static_cast<int>(v.get(k).as_int()) : d; };
+  g.pcie_max_width = int_or("pcie_max_width", -1);
+  g.pcie_max_speed_mts = int_or("pcie_max_speed_mts", -1);
+  g.pcie_max_gen = int_or("pcie_max_gen", -1);
   for (const auto& l : v.get("links").items()) g.links.push_back(peer_link_from_json(l));
   for (const auto& l : v.get("phys_links").items()) g.phys_links.push_back(phys_link_from_json(l));
   return g;
@@ -201,6 +214,10 @@ Telemetry telemetry_from_json(const Value& v) {
     t.acc_ppt = v.get("acc_ppt").is_number() ? static_cast<uint64_t>(num("acc_ppt", 0)) : Telemetry::kNoAcc;
     t.acc_thermal = v.get("acc_thermal").is_number() ? static_cast<uint64_t>(num("acc_thermal", 0)) : Telemetry::kNoAcc;
   }
+  t.pcie_width = static_cast<int>(num("pcie_width", -1));
+  t.pcie_speed_mts = static_cast<int>(num("pcie_speed_mts", -1));
+  t.pcie_replays = static_cast<int64_t>(num("pcie_replays", -1));
+  t.pcie_recoveries = static_cast<int64_t>(num("pcie_recoveries", -1));
   if (v.get("retired_pages").is_number() || v.get("unreservable_pages").is_number()) {
     t.ras_ok = true;
     t.retired_pages = static_cast<uint64_t>(num("retired_pages", 0));
@@ -235,6 +252,9 @@ Value default_mi355x_fixture(int n_gpus, uint64_t hive_id) {
     g["power_cap_w"] = 1400;
     g["drm_card"] = 1 + i;
     g["drm_render"] = 128 + i;
+    g["pcie_max_width"] = 16;
+    g["pcie_max_speed_mts"] = 32000;  // Gen5
+    g["pcie_max_gen"] = 5;
     // 8x MI355X UBB: a full xGMI mesh, one link to every peer (7 x ~153 GB/s per GPU).
     Value links = Value::array(), phys = Value::array();
     for (int j = 0; j < n_gpus; ++j) {
@@ -259,6 +279,10 @@ Value default_mi355x_fixture(int n_gpus, uint64_t hive_id) {
     t["uclk_mhz"] = 1900;
     t["xgmi_links_up"] = n_gpus - 1;
     t["xgmi_links_total"] = n_gpus - 1;
+    t["pcie_width"] = 16;
+    t["pcie_speed_mts"] = 32000;
+    t["pcie_replays"] = 0;
+    t["pcie_recoveries"] = 0;
     g["telemetry"] = t;
     gpus.push_back(g);
   }
@@ -357,6 +381,12 @@ class MockBackend : public Backend {
       t.ecc_correctable = static_cast<uint64_t>(num("ecc_correctable", 0));
       t.ecc_uncorrectable = static_cast<uint64_t>(num("ecc_uncorrectable", 0));
       t.ecc_deferred = static_cast<uint64_t>(num("ecc_deferred", 0));
+      t.pcie_width = static_cast<int>(num("pcie_width", -1));
+      t.pcie_speed_mts = static_cast<int>(num("pcie_speed_mts", -1));
+      t.pcie_replays = static_cast<int64_t>(num("pcie_replays", -1));
+      t.pcie_recoveries = static_cast<int64_t>(num("pcie_recoveries", -1));
+      t.pcie_nak_sent = static_cast<int64_t>(num("pcie_nak_sent", -1));
+      t.pcie_nak_received = static_cast<int64_t>(num("pcie_nak_received", -1));
     } else {
       t.vram_used_mb = 0;
     }
@@ -433,6 +463,7 @@ struct AmdSmiApi {
   decltype(&amdsmi_get_gpu_ecc_enabled) ecc_enabled = nullptr;
   decltype(&amdsmi_get_gpu_ecc_count) ecc_count = nullptr;
   decltype(&amdsmi_get_gpu_process_list) process_list = nullptr;
+  decltype(&amdsmi_get_pcie_info) pcie_info = nullptr;
 };
 
 struct BlockName {
@@ -498,6 +529,7 @@ class AmdSmiBackend : public Backend {
     resolve(api_.lib, api_.ecc_enabled, "amdsmi_get_gpu_ecc_enabled", false);
     resolve(api_.lib, api_.ecc_count, "amdsmi_get_gpu_ecc_count", false);
     resolve(api_.lib, api_.process_list, "amdsmi_get_gpu_process_list", false);
+    resolve(api_.lib, api_.pcie_info, "amdsmi_get_pcie_info", false);
     amdsmi_status_t st = api_.init(AMDSMI_INIT_AMD_GPUS);
     if (st != AMDSMI_STATUS_SUCCESS) throw std::runtime_error("amdsmi_init failed: status " + std::to_string(st));
     initialized_ = true;
@@ -597,6 +629,22 @@ class AmdSmiBackend : public Backend {
       if (api_.bad_page_threshold) {
         uint32_t thr = 0;
         if (api_.bad_page_threshold(h, &thr) == AMDSMI_STATUS_SUCCESS && thr != 0xFFFFFFFFu) g.bad_page_threshold = thr;
+      }
+      if (api_.pcie_info) {
+        amdsmi_pcie_info_t pi;
+        std::memset(&pi, 0, sizeof(pi));
+        if (api_.pcie_info(h, &pi) == AMDSMI_STATUS_SUCCESS) {
+          const auto& ps = pi.pcie_static;
+          if (ps.max_pcie_width != 0xFFFF && ps.max_pcie_width != 0) g.pcie_max_width = ps.max_pcie_width;
+          if (ps.max_pcie_speed != 0xFFFFFFFFu && ps.max_pcie_speed != 0) {
+            // documented as GT/s, reported as MT/s by some firmware: normalise to MT/s
+            g.pcie_max_speed_mts = static_cast<int>(ps.max_pcie_speed < 1000 ? ps.max_pcie_speed * 1000 : ps.max_pcie_speed);
+          }
+          const uint32_t gen = ps.max_pcie_interface_version != 0xFFFFFFFFu && ps.max_pcie_interface_version != 0
+                                   ? ps.max_pcie_interface_version
+                                   : ps.pcie_interface_version;
+          if (gen != 0xFFFFFFFFu && gen != 0) g.pcie_max_gen = static_cast<int>(gen);
+        }
       }
       g.phys_links = read_links(h);
       // Peer links: one amdsmi topology query per ordered pair (8 GPUs: 56 pairs, once
@@ -754,6 +802,20 @@ class AmdSmiBackend : public Backend {
         t.ecc_correctable = e.correctable_count;
         t.ecc_uncorrectable = e.uncorrectable_count;
         t.ecc_deferred = e.deferred_count;
+      }
+    }
+    if (full && api_.pcie_info) {
+      amdsmi_pcie_info_t pi;
+      std::memset(&pi, 0, sizeof(pi));
+      if (api_.pcie_info(h, &pi) == AMDSMI_STATUS_SUCCESS) {
+        const auto& pm = pi.pcie_metric;
+        auto cnt = [](uint64_t v) { return v == ~0ULL ? int64_t{-1} : static_cast<int64_t>(v); };
+        if (pm.pcie_width != 0xFFFF) t.pcie_width = pm.pcie_width;
+        if (pm.pcie_speed != 0xFFFFFFFFu) t.pcie_speed_mts = static_cast<int>(pm.pcie_speed);
+        t.pcie_replays = cnt(pm.pcie_replay_count);
+        t.pcie_recoveries = cnt(pm.pcie_l0_to_recovery_count);
+        t.pcie_nak_sent = cnt(pm.pcie_nak_sent_count);
+        t.pcie_nak_received = cnt(pm.pcie_nak_received_count);
       }
     }
     if (level == SampleLevel::Ras) sample_ras(h, t);

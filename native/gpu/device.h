@@ -67,6 +67,10 @@ struct GpuInfo {
   int drm_render = -1;
   int drm_card = -1;
   uint32_t bad_page_threshold = 0;   // driver's retirement limit (0 = unknown / no root)
+  // PCIe link capability (amdsmi_get_pcie_info static part); -1 = unknown
+  int pcie_max_width = -1;       // lanes
+  int pcie_max_speed_mts = -1;   // per-lane rate, MT/s (Gen5 = 32000)
+  int pcie_max_gen = -1;
   std::vector<PeerLink> links;       // to every other discovered GPU
   std::vector<PhysLink> phys_links;  // physical links at discovery time
 };
@@ -100,6 +104,14 @@ struct Telemetry {
   uint64_t ecc_deferred = 0;
   int xgmi_links_up = -1;     // -1 = unknown
   int xgmi_links_total = -1;
+  // PCIe link state (Slow level; amdsmi_get_pcie_info metric part); -1 = unknown.  The
+  // error counters are cumulative since boot: the poller watches their deltas.
+  int pcie_width = -1;
+  int pcie_speed_mts = -1;
+  int64_t pcie_replays = -1;
+  int64_t pcie_recoveries = -1;   // L0 -> recovery transitions
+  int64_t pcie_nak_sent = -1;
+  int64_t pcie_nak_received = -1;
   // RAS level only (SampleLevel::Ras); `ras_ok` says whether they were read.
   bool ras_ok = false;
   uint64_t retired_pages = 0;       // reserved + pending

@@ -47,9 +47,11 @@ Diag::Diag(const std::string& path) : path_(path) {
   gemm_ = reinterpret_cast<int (*)(int, int, int, int, const uint16_t*, const uint16_t*, float*)>(
       dlsym(lib_, "bgc_diag_gemm"));
   burn_ = reinterpret_cast<int (*)(int, int, int, uint32_t, bgc_burn_result*)>(dlsym(lib_, "bgc_diag_burn"));
+  pcie_ = reinterpret_cast<int (*)(int, uint64_t, int, uint32_t, bgc_pcie_result*)>(dlsym(lib_, "bgc_diag_pcie"));
   last_error_ = reinterpret_cast<const char* (*)()>(dlsym(lib_, "bgc_diag_last_error"));
   auto abi = reinterpret_cast<int (*)()>(dlsym(lib_, "bgc_diag_abi_version"));
-  if (!device_count_ || !hbm_ || !mfma_ || !arch_ || !gemm_ || !burn_ || !last_error_ || !abi || abi() != BGC_DIAG_ABI_VERSION) {
+  if (!device_count_ || !hbm_ || !mfma_ || !arch_ || !gemm_ || !burn_ || !pcie_ || !last_error_ || !abi ||
+      abi() != BGC_DIAG_ABI_VERSION) {
     throw std::runtime_error(path + " is not a compatible bgc diag library");
   }
 }
@@ -144,6 +146,15 @@ json::Value Diag::burn(int device, int duration_ms, int waves_per_cu, uint32_t s
                               {"mismatches", static_cast<unsigned long long>(r.mismatches)}});
 }
 
+json::Value Diag::pcie(int device, uint64_t bytes, int iters, uint32_t seed) {
+  bgc_pcie_result r{};
+  if (pcie_(device, bytes, iters, seed, &r) != 0) throw std::runtime_error(std::string("pcie diag: ") + last_error_());
+  return json::Value::object({{"device", device}, {"bytes", static_cast<unsigned long long>(r.bytes)},
+                              {"iters", r.iters}, {"h2d_gbps", r.h2d_gbps}, {"d2h_gbps", r.d2h_gbps},
+                              {"bidir_gbps", r.bidir_gbps}, {"mismatches", static_cast<unsigned long long>(r.mismatches)},
+                              {"elapsed_ms", r.elapsed_ms}, {"passed", r.mismatches == 0}});
+}
+
 void Diag::gemm(int device, int m, int n, int k, const uint16_t* a, const uint16_t* b, float* c) {
   if (gemm_(device, m, n, k, a, b, c) != 0) throw std::runtime_error(std::string("gemm diag: ") + last_error_());
 }
@@ -222,6 +233,13 @@ DiagFloors DiagFloors::mi355x_defaults() {
   f.min_burn_sustain = 0.80;
   f.max_burn_hotspot_c = 100;
   f.max_burn_thermal_violation_pct = 20;
+  // PCIe Gen5 x16 host link (profiles/pcie_r2/probe.json): 57.1 GB/s host-to-device and
+  // 56.7 GB/s device-to-host with 64 MiB - 1 GiB pinned copies, 97 GB/s both ways at
+  // once; a Gen4-trained or x8 link delivers half of that.
+  f.min_pcie_h2d_gbps = 45;
+  f.min_pcie_d2h_gbps = 45;
+  f.require_full_pcie_width = true;
+  f.min_pcie_speed_fraction = 0.5;
   return f;
 }
 
@@ -280,6 +298,23 @@ json::Value judge_diag(const json::Value& result, const DiagFloors& fl) {
       char buf[160];
       std::snprintf(buf, sizeof(buf), "thermal throttling %.0f%% of the burn (limit %.0f%%)",
                     num(burn, "thermal_violation_pct"), fl.max_burn_thermal_violation_pct);
+      failures.push_back(std::string(buf));
+    }
+  }
+  const json::Value& pc = result.get("pcie");
+  if (pc.is_object()) {
+    if (num(pc, "mismatches") > 0) failures.push_back("PCIe round-trip mismatches: " + std::to_string(static_cast<uint64_t>(num(pc, "mismatches"))));
+    floor_check(pc, "h2d_gbps", fl.min_pcie_h2d_gbps, "PCIe host-to-device GB/s");
+    floor_check(pc, "d2h_gbps", fl.min_pcie_d2h_gbps, "PCIe device-to-host GB/s");
+    // link state read right after the copies (amdsmi; absent when unknown)
+    const double w = num(pc, "link_width"), mw = num(pc, "max_width");
+    if (fl.require_full_pcie_width && w > 0 && mw > 0 && w < mw) {
+      failures.push_back("PCIe link x" + std::to_string(static_cast<int>(w)) + " of x" + std::to_string(static_cast<int>(mw)));
+    }
+    const double sp = num(pc, "link_speed_mts"), msp = num(pc, "max_speed_mts");
+    if (fl.min_pcie_speed_fraction > 0 && sp > 0 && msp > 0 && sp < fl.min_pcie_speed_fraction * msp) {
+      char buf[160];
+      std::snprintf(buf, sizeof(buf), "PCIe link at %.0f of %.0f MT/s under load", sp, msp);
       failures.push_back(std::string(buf));
     }
   }

@@ -26,6 +26,12 @@ struct DiagFloors {
   double min_burn_sustain = 0;   // tflops_last / tflops_max
   double max_burn_hotspot_c = 0;
   double max_burn_thermal_violation_pct = 0;
+  // PCIe (`pcie` section): host<->device DMA rates, and the link must run at its full
+  // width (and at least this fraction of its top speed) while the copies run.
+  double min_pcie_h2d_gbps = 0;
+  double min_pcie_d2h_gbps = 0;
+  bool require_full_pcie_width = false;
+  double min_pcie_speed_fraction = 0;
   static DiagFloors mi355x_defaults();
 };
 
@@ -47,6 +53,8 @@ class Diag {
   json::Value gemm_check(int device, int m, int n, int k, uint32_t seed);
   // Sustained MFMA load for duration_ms (see bgc_diag_burn).
   json::Value burn(int device, int duration_ms, int waves_per_cu, uint32_t seed);
+  // Pinned host <-> device copies (see bgc_diag_pcie).
+  json::Value pcie(int device, uint64_t bytes, int iters, uint32_t seed);
   // Raw GEMM: A/B as bf16 bit patterns, C fp32 (row-major).
   void gemm(int device, int m, int n, int k, const uint16_t* a, const uint16_t* b, float* c);
   const std::string& path() const { return path_; }
@@ -61,6 +69,7 @@ class Diag {
   int (*arch_)(int, char*, size_t) = nullptr;
   int (*gemm_)(int, int, int, int, const uint16_t*, const uint16_t*, float*) = nullptr;
   int (*burn_)(int, int, int, uint32_t, bgc_burn_result*) = nullptr;
+  int (*pcie_)(int, uint64_t, int, uint32_t, bgc_pcie_result*) = nullptr;
   const char* (*last_error_)() = nullptr;
 };
 

@@ -15,7 +15,7 @@
 extern "C" {
 #endif
 
-#define BGC_DIAG_ABI_VERSION 3
+#define BGC_DIAG_ABI_VERSION 4
 #define BGC_DIAG_MAX_CU_KEYS 2048
 
 typedef struct {
@@ -66,6 +66,19 @@ int bgc_diag_burn(int device, int duration_ms, int waves_per_cu, uint32_t seed, 
 // C[m,n] (fp32) = A[m,k] * B[k,n], A/B bf16 bit patterns, row-major, via MFMA; the host
 // compares C with its own fp32 product (m, n multiples of 16; k a multiple of 32).
 int bgc_diag_gemm(int device, int m, int n, int k, const uint16_t* a_bf16, const uint16_t* b_bf16, float* c);
+typedef struct {
+  uint64_t bytes;           // transfer size (pinned host buffers)
+  int iters;
+  double h2d_gbps;          // best host -> device rate
+  double d2h_gbps;          // best device -> host rate
+  double bidir_gbps;        // both directions at once on two streams (sum of the two)
+  uint64_t mismatches;      // 64-bit words that did not survive the H2D + D2H round trip
+  double elapsed_ms;
+} bgc_pcie_result;
+
+// Host <-> device DMA over the GPU's PCIe link: a link that trained narrow or slow, or
+// that replays, shows up here before a training job's data loader notices.
+int bgc_diag_pcie(int device, uint64_t bytes, int iters, uint32_t seed, bgc_pcie_result* out);
 // Device name / gfx arch string, e.g. "gfx950".
 int bgc_diag_device_arch(int device, char* buf, size_t len);
 const char* bgc_diag_last_error(void);

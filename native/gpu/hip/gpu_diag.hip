@@ -281,6 +281,21 @@ struct Events {
   }
 };
 
+struct HostBuffer {  // pinned: DMA straight from/to it, no staging copy
+  void* p = nullptr;
+  ~HostBuffer() {
+    if (p) (void)hipHostFree(p);
+  }
+};
+
+struct Streams {
+  hipStream_t a = nullptr, b = nullptr;
+  ~Streams() {
+    if (a) (void)hipStreamDestroy(a);
+    if (b) (void)hipStreamDestroy(b);
+  }
+};
+
 }  // namespace
 
 extern "C" {
@@ -537,6 +552,87 @@ int bgc_diag_gemm(int device, int m, int n, int k, const uint16_t* a_bf16, const
                      static_cast<const __bf16*>(db.p), static_cast<float*>(dc.p), m, n, k);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpy(c, dc.p, c_bytes, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int bgc_diag_pcie(int device, uint64_t bytes, int iters, uint32_t seed, bgc_pcie_result* out) {
+  if (!out || iters <= 0 || bytes < (1u << 20) || bytes > (uint64_t{16} << 30)) {
+    g_last_error = "invalid arguments";
+    return 1;
+  }
+  std::memset(out, 0, sizeof(*out));
+  bytes &= ~static_cast<uint64_t>(7);
+  const uint64_t words = bytes / 8;
+  HIP_TRY(hipSetDevice(device));
+  HostBuffer src, dst, src2;
+  DeviceBuffer d1, d2;
+  HIP_TRY(hipHostMalloc(&src.p, bytes, hipHostMallocDefault));
+  HIP_TRY(hipHostMalloc(&dst.p, bytes, hipHostMallocDefault));
+  HIP_TRY(hipHostMalloc(&src2.p, bytes, hipHostMallocDefault));
+  HIP_TRY(hipMalloc(&d1.p, bytes));
+  HIP_TRY(hipMalloc(&d2.p, bytes));
+  auto* s64 = static_cast<uint64_t*>(src.p);
+  for (uint64_t i = 0; i < words; ++i) s64[i] = (static_cast<uint64_t>(mix32(static_cast<uint32_t>(i) ^ seed)) << 32) | mix32(static_cast<uint32_t>(i >> 32) + seed + 1);
+  std::memset(dst.p, 0, bytes);
+  std::memset(src2.p, 0x5a, bytes);
+  Streams st;
+  HIP_TRY(hipStreamCreateWithFlags(&st.a, hipStreamNonBlocking));
+  HIP_TRY(hipStreamCreateWithFlags(&st.b, hipStreamNonBlocking));
+  Events ev, ev2;
+  HIP_TRY(hipEventCreate(&ev.a));
+  HIP_TRY(hipEventCreate(&ev.b));
+  HIP_TRY(hipEventCreate(&ev2.a));
+  HIP_TRY(hipEventCreate(&ev2.b));
+  // warm-up both directions (page tables, DMA engine clocks)
+  HIP_TRY(hipMemcpyAsync(d1.p, src.p, bytes, hipMemcpyHostToDevice, st.a));
+  HIP_TRY(hipMemcpyAsync(d2.p, d1.p, bytes, hipMemcpyDeviceToDevice, st.a));
+  HIP_TRY(hipMemcpyAsync(dst.p, d2.p, bytes, hipMemcpyDeviceToHost, st.a));
+  HIP_TRY(hipStreamSynchronize(st.a));
+  // round trip check: the pattern went host -> device -> device -> host
+  const auto* d64 = static_cast<const uint64_t*>(dst.p);
+  uint64_t bad = 0;
+  for (uint64_t i = 0; i < words; ++i) bad += d64[i] != s64[i];
+  float best_h2d = 1e30f, best_d2h = 1e30f, ms = 0.f, total = 0.f;
+  double best_bidir = 0;
+  for (int it = 0; it < iters; ++it) {
+    HIP_TRY(hipEventRecord(ev.a, st.a));
+    HIP_TRY(hipMemcpyAsync(d1.p, src.p, bytes, hipMemcpyHostToDevice, st.a));
+    HIP_TRY(hipEventRecord(ev.b, st.a));
+    HIP_TRY(hipEventSynchronize(ev.b));
+    HIP_TRY(hipEventElapsedTime(&ms, ev.a, ev.b));
+    best_h2d = std::min(best_h2d, ms);
+    total += ms;
+    HIP_TRY(hipEventRecord(ev.a, st.a));
+    HIP_TRY(hipMemcpyAsync(dst.p, d1.p, bytes, hipMemcpyDeviceToHost, st.a));
+    HIP_TRY(hipEventRecord(ev.b, st.a));
+    HIP_TRY(hipEventSynchronize(ev.b));
+    HIP_TRY(hipEventElapsedTime(&ms, ev.a, ev.b));
+    best_d2h = std::min(best_d2h, ms);
+    total += ms;
+    // both directions at once: H2D on one stream, D2H on the other
+    HIP_TRY(hipEventRecord(ev.a, st.a));
+    HIP_TRY(hipEventRecord(ev2.a, st.b));
+    HIP_TRY(hipMemcpyAsync(d2.p, src2.p, bytes, hipMemcpyHostToDevice, st.a));
+    HIP_TRY(hipMemcpyAsync(dst.p, d1.p, bytes, hipMemcpyDeviceToHost, st.b));
+    HIP_TRY(hipEventRecord(ev.b, st.a));
+    HIP_TRY(hipEventRecord(ev2.b, st.b));
+    HIP_TRY(hipEventSynchronize(ev.b));
+    HIP_TRY(hipEventSynchronize(ev2.b));
+    float ms_a = 0.f, ms_b = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms_a, ev.a, ev.b));
+    HIP_TRY(hipEventElapsedTime(&ms_b, ev2.a, ev2.b));
+    const double span = std::max(ms_a, ms_b);
+    best_bidir = std::max(best_bidir, 2.0 * static_cast<double>(bytes) / (span * 1e-3) / 1e9);
+    total += static_cast<float>(span);
+  }
+  HIP_TRY(hipGetLastError());
+  out->bytes = bytes;
+  out->iters = iters;
+  out->h2d_gbps = static_cast<double>(bytes) / (best_h2d * 1e-3) / 1e9;
+  out->d2h_gbps = static_cast<double>(bytes) / (best_d2h * 1e-3) / 1e9;
+  out->bidir_gbps = best_bidir;
+  out->mismatches = bad;
+  out->elapsed_ms = total;
   return 0;
 }
 

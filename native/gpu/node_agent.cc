@@ -35,6 +35,11 @@ NodeAgentConfig NodeAgentConfig::from_env(const EnvConfig& env) {
   c.diag_hbm_bytes = env.u64_or("diag_hbm_bytes", 1ULL << 30);
   c.diag_interval_secs = env.u64_or("diag_interval_secs", 0);
   c.diag_burn_ms = env.u64_or("diag_burn_ms", 0);
+  c.diag_pcie_bytes = env.u64_or("diag_pcie_bytes", c.diag_pcie_bytes);
+  c.diag_floors.min_pcie_h2d_gbps = env.f64_or("diag_min_pcie_h2d_gbps", c.diag_floors.min_pcie_h2d_gbps);
+  c.diag_floors.min_pcie_d2h_gbps = env.f64_or("diag_min_pcie_d2h_gbps", c.diag_floors.min_pcie_d2h_gbps);
+  c.diag_floors.require_full_pcie_width = env.boolean_or("diag_require_full_pcie_width", c.diag_floors.require_full_pcie_width);
+  c.diag_floors.min_pcie_speed_fraction = env.f64_or("diag_min_pcie_speed_fraction", c.diag_floors.min_pcie_speed_fraction);
   c.diag_floors.min_burn_tflops = env.f64_or("diag_min_burn_tflops", c.diag_floors.min_burn_tflops);
   c.diag_floors.min_burn_sustain = env.f64_or("diag_min_burn_sustain", c.diag_floors.min_burn_sustain);
   c.diag_floors.max_burn_hotspot_c = env.f64_or("diag_max_burn_hotspot_c", c.diag_floors.max_burn_hotspot_c);
@@ -57,6 +62,8 @@ NodeAgentConfig NodeAgentConfig::from_env(const EnvConfig& env) {
   h.max_thermal_violation_pct = env.f64_or("max_thermal_violation_pct", h.max_thermal_violation_pct);
   h.max_ppt_violation_pct = env.f64_or("max_ppt_violation_pct", h.max_ppt_violation_pct);
   h.violation_sustain_polls = static_cast<int>(env.u64_or("violation_sustain_polls", static_cast<uint64_t>(h.violation_sustain_polls)));
+  h.require_full_pcie_width = env.boolean_or("require_full_pcie_width", h.require_full_pcie_width);
+  h.max_pcie_replays_per_poll = static_cast<int64_t>(env.u64_or("max_pcie_replays_per_poll", static_cast<uint64_t>(h.max_pcie_replays_per_poll)));
   h.fail_threshold = static_cast<int>(env.u64_or("fail_threshold", static_cast<uint64_t>(h.fail_threshold)));
   h.recover_threshold = static_cast<int>(env.u64_or("recover_threshold", static_cast<uint64_t>(h.recover_threshold)));
   c.slow_every = static_cast<int>(env.u64_or("slow_every", static_cast<uint64_t>(c.slow_every)));
@@ -206,6 +213,7 @@ void NodeAgent::init() {
   }
   poller_ = std::make_unique<TelemetryPoller>(*backend_, idx, std::chrono::milliseconds(cfg_.poll_interval_ms),
                                               cfg_.health, cfg_.slow_every, cfg_.ras_every, page_limits);
+  for (size_t k = 0; k < gpus_.size(); ++k) poller_->set_pcie_max_width(k, gpus_[k].pcie_max_width);
   poller_->poll_once();
   bool exists = client_.get_opt(types::Node, "", cfg_.node_name).has_value();
   if (cfg_.create_node && !exists) {
@@ -259,6 +267,7 @@ Value NodeAgent::diagnose(const GpuInfo& g) const {
     r["hbm"] = d.hbm(dev, cfg_.diag_hbm_bytes, 2, seed);
     r["mfma"] = d.mfma(dev, 16, 2048, seed);
     r["gemm"] = d.gemm_check(dev, 64, 64, 512, seed);
+    if (cfg_.diag_pcie_bytes > 0) r["pcie"] = pcie_check(*backend_, g, dev, cfg_.diag_pcie_bytes, seed);
     if (cfg_.diag_burn_ms > 0) r["burn"] = burn_in(*backend_, g.index, dev, static_cast<int>(cfg_.diag_burn_ms), seed);
   } catch (const std::exception& e) {
     r["error"] = std::string(e.what());
@@ -311,6 +320,42 @@ Value burn_in(Backend& backend, int index, int hip_device, int duration_ms, uint
   TelemetryPoller::violation_deltas(first, span);
   out["thermal_violation_pct"] = span.violation_thermal_pct < 0 ? Value() : Value(span.violation_thermal_pct);
   out["ppt_violation_pct"] = span.violation_ppt_pct < 0 ? Value() : Value(span.violation_ppt_pct);
+  return out;
+}
+
+Value pcie_check(Backend& backend, const GpuInfo& g, int hip_device, uint64_t bytes, uint32_t seed) {
+  const Telemetry before = backend.sample(g.index, SampleLevel::Slow);
+  std::atomic<bool> done{false};
+  int width = -1, speed = -1;  // highest seen while copying
+  std::thread sampler([&] {
+    while (!done.load()) {
+      Telemetry t = backend.sample(g.index, SampleLevel::Slow);
+      if (t.ok) {
+        width = std::max(width, t.pcie_width);
+        speed = std::max(speed, t.pcie_speed_mts);
+      }
+      for (int i = 0; i < 5 && !done.load(); ++i) std::this_thread::sleep_for(std::chrono::milliseconds(10));
+    }
+  });
+  Value out;
+  try {
+    out = Diag::instance().pcie(hip_device, bytes, 5, seed);
+  } catch (...) {
+    done = true;
+    sampler.join();
+    throw;
+  }
+  done = true;
+  sampler.join();
+  const Telemetry after = backend.sample(g.index, SampleLevel::Slow);
+  if (width > 0) out["link_width"] = width;
+  if (speed > 0) out["link_speed_mts"] = speed;
+  if (g.pcie_max_width > 0) out["max_width"] = g.pcie_max_width;
+  if (g.pcie_max_speed_mts > 0) out["max_speed_mts"] = g.pcie_max_speed_mts;
+  if (g.pcie_max_gen > 0) out["max_gen"] = g.pcie_max_gen;
+  auto delta = [&](int64_t a, int64_t b) { return a >= 0 && b >= a ? Value(static_cast<long long>(b - a)) : Value(); };
+  out["replays"] = delta(before.pcie_replays, after.pcie_replays);
+  out["recoveries"] = delta(before.pcie_recoveries, after.pcie_recoveries);
   return out;
 }
 

@@ -64,6 +64,9 @@ struct NodeAgentConfig {
   // throttle residency are sampled (catches cooling/power-delivery faults the short
   // checks do not); 0 = off.
   uint64_t diag_burn_ms = 0;
+  // PCIe check: pinned host<->device copies of this size (0 = off) with the link's
+  // width/speed read while they run.
+  uint64_t diag_pcie_bytes = 256ULL << 20;
   DiagFloors diag_floors = DiagFloors::mi355x_defaults();
   std::string pod_resources_socket = "/var/lib/kubelet/pod-resources/kubelet.sock";
   HealthPolicy health;
@@ -99,6 +102,10 @@ std::string product_label(const GpuInfo& g);
 // Burn-in of one GPU: Diag::burn() while a side thread samples it through `backend`
 // (hotspot/HBM temperature, power, gfxclk, thermal/PPT violation residency over the burn).
 json::Value burn_in(Backend& backend, int index, int hip_device, int duration_ms, uint32_t seed);
+// Host<->device copy rates (Diag::pcie) plus the PCIe link width/speed sampled through
+// `backend` while the copies run (links drop to a low-power rate when idle), and the
+// link's replay/recovery counter deltas over the test.
+json::Value pcie_check(Backend& backend, const GpuInfo& g, int hip_device, uint64_t bytes, uint32_t seed);
 
 // Pure rendering of the Node patches (unit-tested).
 json::Value node_labels_patch(const NodeAgentConfig& cfg, const std::vector<GpuInfo>& gpus, int healthy,

@@ -41,7 +41,10 @@ TelemetryPoller::TelemetryPoller(Backend& backend, std::vector<int> indices, std
                        &reg.gauge("amd_gpu_violation_ppt_percent", "Power-cap (PPT) throttle residency, last interval", l),
                        &reg.gauge("amd_gpu_violation_thermal_percent", "Thermal throttle residency, last interval", l),
                        &reg.gauge("amd_gpu_retired_pages", "Retired + pending HBM pages", l),
-                       &reg.gauge("amd_gpu_throttle_status", "Independent throttle status bits (-1 = not reported)", l)});
+                       &reg.gauge("amd_gpu_throttle_status", "Independent throttle status bits (-1 = not reported)", l),
+                       &reg.gauge("amd_gpu_pcie_link_width", "PCIe link width (lanes)", l),
+                       &reg.gauge("amd_gpu_pcie_link_speed_mts", "PCIe link rate per lane (MT/s)", l),
+                       &reg.gauge("amd_gpu_pcie_replays_total", "PCIe replays since boot", l)});
   }
   snap_ = std::make_shared<Snapshot>();
 }
@@ -82,6 +85,12 @@ void TelemetryPoller::evaluate(const Telemetry& t, const HealthPolicy& p, Device
       h.baseline_uncorrectable = t.ecc_uncorrectable;
       h.baseline_set = true;
     }
+    if (t.pcie_replays >= 0) {  // fresh only on slow polls: the verdict holds until the next one
+      h.pcie_replay_delta = h.pcie_last_replays >= 0 && t.pcie_replays >= h.pcie_last_replays
+                                ? t.pcie_replays - h.pcie_last_replays
+                                : 0;
+      h.pcie_last_replays = t.pcie_replays;
+    }
     h.consecutive_thermal = t.violation_thermal_pct > p.max_thermal_violation_pct ? h.consecutive_thermal + 1 : 0;
     h.consecutive_ppt = t.violation_ppt_pct > p.max_ppt_violation_pct ? h.consecutive_ppt + 1 : 0;
     if (t.temp_hotspot_c > p.max_hotspot_c) problem = "hotspot temperature " + std::to_string(t.temp_hotspot_c) + "C";
@@ -103,6 +112,10 @@ void TelemetryPoller::evaluate(const Telemetry& t, const HealthPolicy& p, Device
     } else if (h.consecutive_ppt >= p.violation_sustain_polls) {
       problem = "sustained power-cap throttling: " + std::to_string(static_cast<int>(t.violation_ppt_pct)) + "% for " +
                 std::to_string(h.consecutive_ppt) + " polls";
+    } else if (p.require_full_pcie_width && h.pcie_max_width > 0 && t.pcie_width > 0 && t.pcie_width < h.pcie_max_width) {
+      problem = "PCIe link x" + std::to_string(t.pcie_width) + " of x" + std::to_string(h.pcie_max_width);
+    } else if (p.max_pcie_replays_per_poll >= 0 && h.pcie_replay_delta > p.max_pcie_replays_per_poll) {
+      problem = "PCIe link replays: " + std::to_string(h.pcie_replay_delta) + " since the previous slow poll";
     }
   }
   if (problem.empty()) {
@@ -158,6 +171,9 @@ void TelemetryPoller::poll_once() {
       t.ecc_deferred = slow_cache_[k].ecc_deferred;
       t.vram_used_mb = slow_cache_[k].vram_used_mb;
       t.vram_total_mb = slow_cache_[k].vram_total_mb;
+      t.pcie_width = slow_cache_[k].pcie_width;
+      t.pcie_speed_mts = slow_cache_[k].pcie_speed_mts;
+      // the error counters stay -1 on fast polls: evaluate() diffs fresh readings only
     }
     if (level == SampleLevel::Ras) {
       ras_cache_[k] = t;
@@ -200,6 +216,9 @@ void TelemetryPoller::poll_once() {
     g.viol_thermal->set(t.violation_thermal_pct);
     g.retired->set(static_cast<double>(health_[k].retired_pages));
     g.throttle->set(t.throttle_valid ? static_cast<double>(t.throttle_status) : -1.0);
+    g.pcie_width->set(t.pcie_width);
+    g.pcie_speed->set(t.pcie_speed_mts);
+    if (t.pcie_replays >= 0) g.pcie_replays->set(static_cast<double>(t.pcie_replays));
     snap->devices.push_back(std::move(t));
   }
   snap->health = health_;

@@ -43,6 +43,11 @@ struct HealthPolicy {
   double max_thermal_violation_pct = 20.0;
   double max_ppt_violation_pct = 101.0;
   int violation_sustain_polls = 30;
+  // PCIe: the link must run at its full width (a link that trained x8 on an x16 slot
+  // halves host bandwidth), and more than this many replays between two slow polls
+  // (a marginal link retrying packets) is a fault until a later slow poll is clean.
+  bool require_full_pcie_width = true;
+  int64_t max_pcie_replays_per_poll = 100;
   int fail_threshold = 3;              // consecutive bad polls before flipping to unhealthy
   int recover_threshold = 3;           // consecutive good polls before flipping back
 };
@@ -60,6 +65,9 @@ struct DeviceHealth {
   uint64_t retired_pages = 0;   // last RAS reading (cached between RAS polls)
   uint64_t unreservable_pages = 0;
   uint64_t page_limit = 0;      // effective retired-page limit (policy, capped by driver)
+  int pcie_max_width = -1;      // from discovery (-1 = unknown: width rule off)
+  int64_t pcie_last_replays = -1;
+  int64_t pcie_replay_delta = 0;  // over the last slow-poll interval
 };
 
 struct Snapshot {
@@ -81,6 +89,11 @@ class TelemetryPoller {
                   HealthPolicy policy = {}, int slow_every = 10, int ras_every = 60,
                   std::vector<uint64_t> page_limits = {});
   ~TelemetryPoller();
+  // Link capability of device k (GpuInfo::pcie_max_width), for the PCIe width rule;
+  // call before start().
+  void set_pcie_max_width(size_t k, int width) {
+    if (k < health_.size()) health_[k].pcie_max_width = width;
+  }
   void start();
   void stop();
   // Runs one poll synchronously (tests, and the first poll before start()).
@@ -110,7 +123,7 @@ class TelemetryPoller {
   std::unique_ptr<ThreadPool> pool_;
   struct Gauges {
     metrics::Gauge *gfx, *umc, *power, *hotspot, *mem_temp, *vram_used, *vram_total, *gfxclk, *ecc_ue, *xgmi_up, *healthy,
-        *viol_ppt, *viol_thermal, *retired, *throttle;
+        *viol_ppt, *viol_thermal, *retired, *throttle, *pcie_width, *pcie_speed, *pcie_replays;
   };
   std::vector<Gauges> gauges_;  // resolved once: the poll path does no registry lookups
   mutable std::mutex snap_mu_;

@@ -68,6 +68,8 @@ bgc::gpu::HealthPolicy policy_from_json(const std::string& js) {
   i("violation_sustain_polls", p.violation_sustain_polls);
   i("fail_threshold", p.fail_threshold);
   i("recover_threshold", p.recover_threshold);
+  if (v.get("require_full_pcie_width").is_bool()) p.require_full_pcie_width = v.get("require_full_pcie_width").as_bool();
+  if (v.get("max_pcie_replays_per_poll").is_int()) p.max_pcie_replays_per_poll = v.get("max_pcie_replays_per_poll").as_int();
   return p;
 }
 
@@ -143,6 +145,10 @@ void register_gpu(py::module_& m) {
     pol.recover_threshold = recover_threshold;
     bgc::gpu::DeviceHealth h;
     h.page_limit = page_limit ? std::min<uint64_t>(page_limit, pol.max_retired_pages) : pol.max_retired_pages;
+    const Value pol_json = bgc::json::parse(policy.empty() ? "{}" : policy);
+    if (pol_json.get("pcie_max_width").is_int()) {
+      h.pcie_max_width = static_cast<int>(pol_json.get("pcie_max_width").as_int());  // capability (discovery)
+    }
     bgc::gpu::Telemetry prev;
     std::vector<py::tuple> out;
     Value seq = bgc::json::parse(telemetry_json);
@@ -208,6 +214,24 @@ void register_gpu(py::module_& m) {
     }
     return v.dump();
   }, py::arg("backend"), py::arg("index"), py::arg("hip_device"), py::arg("duration_ms"), py::arg("seed") = 0x5eed);
+  m.def("diag_pcie", [](int device, unsigned long long bytes, int iters, unsigned seed) {
+    Value v;
+    {
+      py::gil_scoped_release nogil;
+      v = bgc::gpu::Diag::instance().pcie(device, bytes, iters, seed);
+    }
+    return v.dump();
+  }, py::arg("device"), py::arg("bytes") = 256ULL << 20, py::arg("iters") = 5, py::arg("seed") = 0x5eed);
+  m.def("pcie_check", [](std::shared_ptr<PyBackend> b, int index, int hip_device, unsigned long long bytes, unsigned seed) {
+    Value v;
+    {
+      py::gil_scoped_release nogil;
+      auto gpus = b->b->discover();
+      if (index < 0 || static_cast<size_t>(index) >= gpus.size()) throw std::out_of_range("no such GPU");
+      v = bgc::gpu::pcie_check(*b->b, gpus[static_cast<size_t>(index)], hip_device, bytes, seed);
+    }
+    return v.dump();
+  }, py::arg("backend"), py::arg("index"), py::arg("hip_device"), py::arg("bytes") = 256ULL << 20, py::arg("seed") = 0x5eed);
   m.def("judge_diag", [](const std::string& result, const std::string& floors_json) {
     bgc::gpu::DiagFloors f = bgc::gpu::DiagFloors::mi355x_defaults();
     Value fj = bgc::json::parse(floors_json);
@@ -223,6 +247,10 @@ void register_gpu(py::module_& m) {
     num("min_burn_sustain", f.min_burn_sustain);
     num("max_burn_hotspot_c", f.max_burn_hotspot_c);
     num("max_burn_thermal_violation_pct", f.max_burn_thermal_violation_pct);
+    num("min_pcie_h2d_gbps", f.min_pcie_h2d_gbps);
+    num("min_pcie_d2h_gbps", f.min_pcie_d2h_gbps);
+    num("min_pcie_speed_fraction", f.min_pcie_speed_fraction);
+    if (fj.get("require_full_pcie_width").is_bool()) f.require_full_pcie_width = fj.get("require_full_pcie_width").as_bool();
     if (fj.get("min_xccs").is_int()) f.min_xccs = static_cast<int>(fj.get("min_xccs").as_int());
     return bgc::gpu::judge_diag(bgc::json::parse(result), f).dump();
   }, py::arg("result"), py::arg("floors") = "{}");

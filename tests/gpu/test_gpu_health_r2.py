@@ -147,6 +147,7 @@ def test_diag_default_floors_pass(tmp_path):
     _dump("diag_default_floors.json", desc["diag"])
     assert desc["diag"][0]["passed"], desc["diag"][0]["failures"]
     assert desc["diag"][0]["gemm"]["passed"]
+    assert desc["diag"][0]["pcie"]["h2d_gbps"] > 45 and desc["diag"][0]["pcie"]["link_width"] == 16
     assert desc["diag"][0]["burn"]["tflops_mean"] > 1800 and desc["diag"][0]["burn"]["samples"] >= 5
     assert [x[1] for x in devs] == ["Healthy"]
     assert labels["amd.com/gpu.healthy-count"] == "1" and labels["amd.com/gpu.diag"] == "passed"
@@ -165,4 +166,25 @@ def test_burn_in_sustained_mfma_with_amdsmi_sampling():
     assert r["mismatches"] == 0 and r["launches"] >= 100 and r["elapsed_ms"] >= 3000
     assert r["samples"] >= 10 and r["power_max_w"] > 0
     judged = json.loads(n.judge_diag(json.dumps({"burn": r}), json.dumps({"min_read_gbps": 0})))
+    assert judged["passed"], judged["failures"]
+
+
+def test_pcie_link_and_host_device_copies():
+    """PCIe: amdsmi link capability and state of the MI355X (Gen5 x16), then pinned
+    host<->device copies with the link sampled while they run; the default floors pass
+    and the data survives the round trip."""
+    from bacchus_gpu_controller_amd import native
+
+    n = native()
+    b = n.gpu_backend("amdsmi", "")
+    g = json.loads(b.discover())[0]
+    slow = json.loads(b.sample(0, 1))
+    r = json.loads(n.pcie_check(b, 0, 0, 256 << 20))
+    _dump("pcie_check.json", {"gpu": {k: g[k] for k in ("pcie_max_width", "pcie_max_speed_mts", "pcie_max_gen")},
+                              "slow_sample": {k: v for k, v in slow.items() if k.startswith("pcie")}, "check": r})
+    assert g["pcie_max_width"] == 16 and g["pcie_max_speed_mts"] >= 32000
+    assert slow["pcie_width"] > 0 and slow["pcie_replays"] >= 0
+    assert r["mismatches"] == 0 and r["h2d_gbps"] > 45 and r["d2h_gbps"] > 45 and r["bidir_gbps"] > r["h2d_gbps"]
+    assert r["link_width"] == 16 and r["link_speed_mts"] >= 32000
+    judged = json.loads(n.judge_diag(json.dumps({"pcie": r})))
     assert judged["passed"], judged["failures"]

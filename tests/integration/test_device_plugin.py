@@ -428,23 +428,25 @@ def test_each_health_rule_flips_list_and_watch(tmp_path):
             t[3]["xgmi_links_up"] = 6                  # one of 7 xGMI links down
             t[4]["ecc_uncorrectable"] = 1              # a new uncorrectable error
             t[5]["temp_mem_c"] = 99                    # HBM over 95 C
+            t[6]["pcie_width"] = 8                     # PCIe link trained x8 of x16
             c.set_gpu_fixture("mi355x-rules", fx)
-            want = ["Unhealthy"] * 6 + ["Healthy"] * 2
+            want = ["Unhealthy"] * 7 + ["Healthy"]
             assert kubelet.wait(lambda: [x[1] for x in kubelet.device_lists[-1][1]] == want, timeout=15), \
                 kubelet.device_lists[-1][1]
             desc = requests.get(f"http://127.0.0.1:{c.node_agent_ports['mi355x-rules']}/gpus", timeout=5).json()
             reasons = desc["unhealthy_reason"]
             for needle in ("retired HBM pages 65 > 64", "could not be retired", "sustained thermal throttling",
-                           "xGMI links down: 1/7", "uncorrectable ECC errors: 1", "HBM temperature"):
+                           "xGMI links down: 1/7", "uncorrectable ECC errors: 1", "HBM temperature",
+                           "PCIe link x8 of x16"):
                 assert needle in reasons, (needle, reasons)
             node = c.admin.get("nodes", "mi355x-rules")
-            assert node["metadata"]["labels"]["amd.com/gpu.healthy-count"] == "2"
+            assert node["metadata"]["labels"]["amd.com/gpu.healthy-count"] == "1"
             # a GPU that already has uncorrectable errors when the agent starts is never advertised Healthy
             fx2 = json.loads(open(c.fixtures["mi355x-rules"]).read())
             for g in fx2["gpus"]:
                 g["telemetry"] = {k: v for k, v in g["telemetry"].items()
                                   if k not in ("retired_pages", "unreservable_pages", "violation_thermal_pct")}
-                g["telemetry"].update({"xgmi_links_up": 7, "temp_mem_c": 40, "ecc_uncorrectable": 0})
+                g["telemetry"].update({"xgmi_links_up": 7, "temp_mem_c": 40, "ecc_uncorrectable": 0, "pcie_width": 16})
             fx2["gpus"][7]["telemetry"]["ecc_uncorrectable"] = 3
             d2 = str(tmp_path / "dp2")
             kubelet2 = FakeKubelet(d2).start()

@@ -229,3 +229,58 @@ def test_judge_diag_burn_in(nat):
     r = json.loads(nat.judge_diag(json.dumps(bad)))
     assert not r["passed"] and len(r["failures"]) == 3
     assert any("sagged" in f for f in r["failures"]) and any("hotspot 104" in f for f in r["failures"])
+
+
+MI355X_PCIE = {"device": 0, "bytes": 268435456, "iters": 5, "h2d_gbps": 57.14, "d2h_gbps": 56.69,
+               "bidir_gbps": 97.02, "mismatches": 0, "passed": True, "link_width": 16, "link_speed_mts": 32000,
+               "max_width": 16, "max_speed_mts": 32000, "max_gen": 5, "replays": 0, "recoveries": 0}
+
+
+def test_judge_diag_pcie(nat):
+    """Host<->device copy floors and the link state read while the copies ran
+    (values measured on the MI355X box, profiles/pcie_r2/probe.json)."""
+    assert json.loads(nat.judge_diag(json.dumps({"pcie": MI355X_PCIE})))["passed"]
+    x8 = dict(MI355X_PCIE, link_width=8, h2d_gbps=28.5, d2h_gbps=28.3)
+    r = json.loads(nat.judge_diag(json.dumps({"pcie": x8})))
+    assert not r["passed"] and "PCIe link x8 of x16" in r["failures"]
+    assert any("host-to-device" in f for f in r["failures"]) and any("device-to-host" in f for f in r["failures"])
+    gen3 = dict(MI355X_PCIE, link_speed_mts=8000)
+    r = json.loads(nat.judge_diag(json.dumps({"pcie": gen3})))
+    assert r["failures"] == ["PCIe link at 8000 of 32000 MT/s under load"]
+    # a Gen4 link (half speed) passes the speed rule at the default fraction, and the
+    # operator can relax the rates for Gen4 hosts
+    gen4 = dict(MI355X_PCIE, link_speed_mts=16000, h2d_gbps=27.0, d2h_gbps=26.5)
+    r = json.loads(nat.judge_diag(json.dumps({"pcie": gen4}), json.dumps({"min_pcie_h2d_gbps": 20,
+                                                                          "min_pcie_d2h_gbps": 20})))
+    assert r["passed"]
+    bad = dict(MI355X_PCIE, mismatches=12)
+    r = json.loads(nat.judge_diag(json.dumps({"pcie": bad})))
+    assert r["failures"] == ["PCIe round-trip mismatches: 12"]
+
+
+def test_pcie_width_and_replay_health_rules(nat):
+    full = {"pcie_width": 16, "pcie_speed_mts": 32000, "pcie_replays": 0}
+    out = _steps(nat, [full, dict(full, pcie_width=8), dict(full, pcie_width=8)], {"pcie_max_width": 16}, fail=2)
+    assert [h for h, _ in out] == [True, True, False] and "PCIe link x8 of x16" in out[2][1]
+    assert all(h for h, _ in _steps(nat, [dict(full, pcie_width=8)] * 3,
+                                    {"pcie_max_width": 16, "require_full_pcie_width": False}))
+    # width unknown at discovery: the rule is off
+    assert all(h for h, _ in _steps(nat, [dict(full, pcie_width=8)] * 3))
+    # replays: the delta between slow readings; fast polls (-1) keep the last verdict
+    seq = [dict(full, pcie_replays=10), dict(full, pcie_replays=15), dict(full, pcie_replays=900),
+           {"pcie_width": 16}, {"pcie_width": 16}, dict(full, pcie_replays=905)]
+    out = _steps(nat, seq, {"max_pcie_replays_per_poll": 100})
+    assert [h for h, _ in out] == [True, True, False, False, False, True]
+    assert "PCIe link replays: 885" in out[2][1]
+
+
+def test_mock_pcie_link_state(nat):
+    f = json.loads(nat.default_mi355x_fixture(2))
+    f["gpus"][1]["telemetry"]["pcie_width"] = 4
+    b = nat.gpu_backend("mock", json.dumps(f))
+    g = json.loads(b.discover())[0]
+    assert (g["pcie_max_width"], g["pcie_max_speed_mts"], g["pcie_max_gen"]) == (16, 32000, 5)
+    slow = json.loads(b.sample(0, 1))
+    assert (slow["pcie_width"], slow["pcie_speed_mts"], slow["pcie_replays"]) == (16, 32000, 0)
+    assert "pcie_width" not in json.loads(b.sample(0, 0))  # fast level: not read
+    assert json.loads(b.sample(1, 1))["pcie_width"] == 4
