@@ -48,9 +48,10 @@ Diag::Diag(const std::string& path) : path_(path) {
       dlsym(lib_, "bgc_diag_gemm"));
   burn_ = reinterpret_cast<int (*)(int, int, int, uint32_t, bgc_burn_result*)>(dlsym(lib_, "bgc_diag_burn"));
   pcie_ = reinterpret_cast<int (*)(int, uint64_t, int, uint32_t, bgc_pcie_result*)>(dlsym(lib_, "bgc_diag_pcie"));
+  soak_ = reinterpret_cast<int (*)(int, int, int, int, int, uint32_t, bgc_soak_result*)>(dlsym(lib_, "bgc_diag_gemm_soak"));
   last_error_ = reinterpret_cast<const char* (*)()>(dlsym(lib_, "bgc_diag_last_error"));
   auto abi = reinterpret_cast<int (*)()>(dlsym(lib_, "bgc_diag_abi_version"));
-  if (!device_count_ || !hbm_ || !mfma_ || !arch_ || !gemm_ || !burn_ || !pcie_ || !last_error_ || !abi ||
+  if (!device_count_ || !hbm_ || !mfma_ || !arch_ || !gemm_ || !burn_ || !pcie_ || !soak_ || !last_error_ || !abi ||
       abi() != BGC_DIAG_ABI_VERSION) {
     throw std::runtime_error(path + " is not a compatible bgc diag library");
   }
@@ -155,6 +156,17 @@ json::Value Diag::pcie(int device, uint64_t bytes, int iters, uint32_t seed) {
                               {"elapsed_ms", r.elapsed_ms}, {"passed", r.mismatches == 0}});
 }
 
+json::Value Diag::gemm_soak(int device, int m, int n, int k, int launches, uint32_t seed) {
+  bgc_soak_result r{};
+  if (soak_(device, m, n, k, launches, seed, &r) != 0) throw std::runtime_error(std::string("gemm soak: ") + last_error_());
+  return json::Value::object({{"device", device}, {"m", r.m}, {"n", r.n}, {"k", r.k}, {"launches", r.launches},
+                              {"tile", r.tile}, {"elapsed_ms", r.elapsed_ms}, {"tflops_mean", r.tflops_mean},
+                              {"tflops_best", r.tflops_best},
+                              {"row_mismatches", static_cast<unsigned long long>(r.row_mismatches)},
+                              {"col_mismatches", static_cast<unsigned long long>(r.col_mismatches)},
+                              {"passed", r.row_mismatches == 0 && r.col_mismatches == 0}});
+}
+
 void Diag::gemm(int device, int m, int n, int k, const uint16_t* a, const uint16_t* b, float* c) {
   if (gemm_(device, m, n, k, a, b, c) != 0) throw std::runtime_error(std::string("gemm diag: ") + last_error_());
 }
@@ -240,6 +252,9 @@ DiagFloors DiagFloors::mi355x_defaults() {
   f.min_pcie_d2h_gbps = 45;
   f.require_full_pcie_width = true;
   f.min_pcie_speed_fraction = 0.5;
+  // GEMM soak (LDS-tiled bf16 MFMA, 256x256 tiles): 1253-1288 TF/s at 8192^3 and
+  // 1164-1193 at 4096^3 on MI355X (profiles/gemm_soak_r2/)
+  f.min_soak_tflops = 950;
   return f;
 }
 
@@ -317,6 +332,15 @@ json::Value judge_diag(const json::Value& result, const DiagFloors& fl) {
       std::snprintf(buf, sizeof(buf), "PCIe link at %.0f of %.0f MT/s under load", sp, msp);
       failures.push_back(std::string(buf));
     }
+  }
+  const json::Value& sk = result.get("soak");
+  if (sk.is_object()) {
+    const double bad = num(sk, "row_mismatches") + num(sk, "col_mismatches");
+    if (bad > 0) {
+      failures.push_back("GEMM soak checksums wrong: " + std::to_string(static_cast<uint64_t>(num(sk, "row_mismatches"))) +
+                         " rows, " + std::to_string(static_cast<uint64_t>(num(sk, "col_mismatches"))) + " columns");
+    }
+    floor_check(sk, "tflops_mean", fl.min_soak_tflops, "GEMM soak TFLOP/s");
   }
   const json::Value& gm = result.get("gemm");
   if (gm.is_object() && gm.get("passed").is_bool() && !gm.get("passed").as_bool()) {

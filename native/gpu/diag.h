@@ -32,6 +32,8 @@ struct DiagFloors {
   double min_pcie_d2h_gbps = 0;
   bool require_full_pcie_width = false;
   double min_pcie_speed_fraction = 0;
+  // GEMM soak (`soak` section): every checksum must match; rate floor on the mean.
+  double min_soak_tflops = 0;
   static DiagFloors mi355x_defaults();
 };
 
@@ -55,6 +57,8 @@ class Diag {
   json::Value burn(int device, int duration_ms, int waves_per_cu, uint32_t seed);
   // Pinned host <-> device copies (see bgc_diag_pcie).
   json::Value pcie(int device, uint64_t bytes, int iters, uint32_t seed);
+  // LDS-tiled MFMA GEMM run back to back, checked by exact checksums (bgc_diag_gemm_soak).
+  json::Value gemm_soak(int device, int m, int n, int k, int launches, uint32_t seed);
   // Raw GEMM: A/B as bf16 bit patterns, C fp32 (row-major).
   void gemm(int device, int m, int n, int k, const uint16_t* a, const uint16_t* b, float* c);
   const std::string& path() const { return path_; }
@@ -70,6 +74,7 @@ class Diag {
   int (*gemm_)(int, int, int, int, const uint16_t*, const uint16_t*, float*) = nullptr;
   int (*burn_)(int, int, int, uint32_t, bgc_burn_result*) = nullptr;
   int (*pcie_)(int, uint64_t, int, uint32_t, bgc_pcie_result*) = nullptr;
+  int (*soak_)(int, int, int, int, int, uint32_t, bgc_soak_result*) = nullptr;
   const char* (*last_error_)() = nullptr;
 };
 

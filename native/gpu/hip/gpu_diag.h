@@ -15,7 +15,7 @@
 extern "C" {
 #endif
 
-#define BGC_DIAG_ABI_VERSION 4
+#define BGC_DIAG_ABI_VERSION 5
 #define BGC_DIAG_MAX_CU_KEYS 2048
 
 typedef struct {
@@ -79,6 +79,21 @@ typedef struct {
 // Host <-> device DMA over the GPU's PCIe link: a link that trained narrow or slow, or
 // that replays, shows up here before a training job's data loader notices.
 int bgc_diag_pcie(int device, uint64_t bytes, int iters, uint32_t seed, bgc_pcie_result* out);
+typedef struct {
+  int m, n, k;              // C[m,n] = A[m,k] * B[k,n], bf16 in, fp32 out
+  int launches;             // back-to-back GEMMs
+  double elapsed_ms;        // sum of the launches (device events)
+  double tflops_mean;       // over all launches
+  double tflops_best;
+  uint64_t row_mismatches;  // C row sums that differ from A (B 1)  (after the first and the last launch)
+  uint64_t col_mismatches;  // C column sums that differ from (1^T A) B
+  int tile;                 // 256 (256x256 tile, 8 waves) or 128 (128x128, 4 waves)
+} bgc_soak_result;
+
+// GEMM soak: an LDS-tiled (global_load_lds double buffering, XOR-swizzled LDS) bf16 MFMA
+// GEMM run `launches` times back to back on operands in {-1, 0, 1}, checked by exact
+// row/column checksums (ABFT).  m, n multiples of 128; k a multiple of 64.
+int bgc_diag_gemm_soak(int device, int m, int n, int k, int launches, uint32_t seed, bgc_soak_result* out);
 // Device name / gfx arch string, e.g. "gfx950".
 int bgc_diag_device_arch(int device, char* buf, size_t len);
 const char* bgc_diag_last_error(void);

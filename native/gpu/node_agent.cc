@@ -36,6 +36,9 @@ NodeAgentConfig NodeAgentConfig::from_env(const EnvConfig& env) {
   c.diag_interval_secs = env.u64_or("diag_interval_secs", 0);
   c.diag_burn_ms = env.u64_or("diag_burn_ms", 0);
   c.diag_pcie_bytes = env.u64_or("diag_pcie_bytes", c.diag_pcie_bytes);
+  c.diag_soak_size = static_cast<int>(env.u64_or("diag_soak_size", static_cast<uint64_t>(c.diag_soak_size)));
+  c.diag_soak_launches = static_cast<int>(env.u64_or("diag_soak_launches", static_cast<uint64_t>(c.diag_soak_launches)));
+  c.diag_floors.min_soak_tflops = env.f64_or("diag_min_soak_tflops", c.diag_floors.min_soak_tflops);
   c.diag_floors.min_pcie_h2d_gbps = env.f64_or("diag_min_pcie_h2d_gbps", c.diag_floors.min_pcie_h2d_gbps);
   c.diag_floors.min_pcie_d2h_gbps = env.f64_or("diag_min_pcie_d2h_gbps", c.diag_floors.min_pcie_d2h_gbps);
   c.diag_floors.require_full_pcie_width = env.boolean_or("diag_require_full_pcie_width", c.diag_floors.require_full_pcie_width);
@@ -268,6 +271,9 @@ Value NodeAgent::diagnose(const GpuInfo& g) const {
     r["mfma"] = d.mfma(dev, 16, 2048, seed);
     r["gemm"] = d.gemm_check(dev, 64, 64, 512, seed);
     if (cfg_.diag_pcie_bytes > 0) r["pcie"] = pcie_check(*backend_, g, dev, cfg_.diag_pcie_bytes, seed);
+    if (cfg_.diag_soak_launches > 0) {
+      r["soak"] = d.gemm_soak(dev, cfg_.diag_soak_size, cfg_.diag_soak_size, cfg_.diag_soak_size, cfg_.diag_soak_launches, seed);
+    }
     if (cfg_.diag_burn_ms > 0) r["burn"] = burn_in(*backend_, g.index, dev, static_cast<int>(cfg_.diag_burn_ms), seed);
   } catch (const std::exception& e) {
     r["error"] = std::string(e.what());

@@ -67,6 +67,10 @@ struct NodeAgentConfig {
   // PCIe check: pinned host<->device copies of this size (0 = off) with the link's
   // width/speed read while they run.
   uint64_t diag_pcie_bytes = 256ULL << 20;
+  // GEMM soak: `diag_soak_launches` back-to-back LDS-tiled MFMA GEMMs of size^3 (bf16),
+  // checked by exact checksums (0 launches = off).
+  int diag_soak_size = 8192;
+  int diag_soak_launches = 20;
   DiagFloors diag_floors = DiagFloors::mi355x_defaults();
   std::string pod_resources_socket = "/var/lib/kubelet/pod-resources/kubelet.sock";
   HealthPolicy health;

@@ -222,6 +222,15 @@ void register_gpu(py::module_& m) {
     }
     return v.dump();
   }, py::arg("device"), py::arg("bytes") = 256ULL << 20, py::arg("iters") = 5, py::arg("seed") = 0x5eed);
+  m.def("diag_gemm_soak", [](int device, int mm, int nn, int kk, int launches, unsigned seed) {
+    Value v;
+    {
+      py::gil_scoped_release nogil;
+      v = bgc::gpu::Diag::instance().gemm_soak(device, mm, nn, kk, launches, seed);
+    }
+    return v.dump();
+  }, py::arg("device"), py::arg("m") = 8192, py::arg("n") = 8192, py::arg("k") = 8192, py::arg("launches") = 10,
+     py::arg("seed") = 0x5eed);
   m.def("pcie_check", [](std::shared_ptr<PyBackend> b, int index, int hip_device, unsigned long long bytes, unsigned seed) {
     Value v;
     {
@@ -250,6 +259,7 @@ void register_gpu(py::module_& m) {
     num("min_pcie_h2d_gbps", f.min_pcie_h2d_gbps);
     num("min_pcie_d2h_gbps", f.min_pcie_d2h_gbps);
     num("min_pcie_speed_fraction", f.min_pcie_speed_fraction);
+    num("min_soak_tflops", f.min_soak_tflops);
     if (fj.get("require_full_pcie_width").is_bool()) f.require_full_pcie_width = fj.get("require_full_pcie_width").as_bool();
     if (fj.get("min_xccs").is_int()) f.min_xccs = static_cast<int>(fj.get("min_xccs").as_int());
     return bgc::gpu::judge_diag(bgc::json::parse(result), f).dump();

@@ -148,6 +148,7 @@ def test_diag_default_floors_pass(tmp_path):
     assert desc["diag"][0]["passed"], desc["diag"][0]["failures"]
     assert desc["diag"][0]["gemm"]["passed"]
     assert desc["diag"][0]["pcie"]["h2d_gbps"] > 45 and desc["diag"][0]["pcie"]["link_width"] == 16
+    assert desc["diag"][0]["soak"]["passed"] and desc["diag"][0]["soak"]["tflops_mean"] > 950
     assert desc["diag"][0]["burn"]["tflops_mean"] > 1800 and desc["diag"][0]["burn"]["samples"] >= 5
     assert [x[1] for x in devs] == ["Healthy"]
     assert labels["amd.com/gpu.healthy-count"] == "1" and labels["amd.com/gpu.diag"] == "passed"
@@ -187,4 +188,20 @@ def test_pcie_link_and_host_device_copies():
     assert r["mismatches"] == 0 and r["h2d_gbps"] > 45 and r["d2h_gbps"] > 45 and r["bidir_gbps"] > r["h2d_gbps"]
     assert r["link_width"] == 16 and r["link_speed_mts"] >= 32000
     judged = json.loads(n.judge_diag(json.dumps({"pcie": r})))
+    assert judged["passed"], judged["failures"]
+
+
+def test_gemm_soak_lds_tiled_mfma_checksums():
+    """GEMM soak: the LDS-tiled bf16 MFMA GEMM (global_load_lds double buffering, swizzled
+    LDS, XCD-aware tile order) on both tile shapes, verified by exact row/column checksums;
+    the 256x256 tile at 8192^3 clears the default rate floor."""
+    from bacchus_gpu_controller_amd import native
+
+    n = native()
+    small = [json.loads(n.diag_gemm_soak(0, m, nn, k, 2)) for m, nn, k in ((128, 384, 64), (384, 128, 192), (512, 768, 1024))]
+    big = json.loads(n.diag_gemm_soak(0, 8192, 8192, 8192, 10))
+    _dump("gemm_soak.json", {"small": small, "8192": big})
+    assert all(r["passed"] for r in small) and [r["tile"] for r in small] == [128, 128, 256]
+    assert big["passed"] and big["tile"] == 256 and big["tflops_mean"] > 950
+    judged = json.loads(n.judge_diag(json.dumps({"soak": big})))
     assert judged["passed"], judged["failures"]

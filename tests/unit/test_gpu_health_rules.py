@@ -284,3 +284,13 @@ def test_mock_pcie_link_state(nat):
     assert (slow["pcie_width"], slow["pcie_speed_mts"], slow["pcie_replays"]) == (16, 32000, 0)
     assert "pcie_width" not in json.loads(b.sample(0, 0))  # fast level: not read
     assert json.loads(b.sample(1, 1))["pcie_width"] == 4
+
+
+def test_judge_diag_gemm_soak(nat):
+    ok = {"m": 8192, "n": 8192, "k": 8192, "launches": 10, "tile": 256, "tflops_mean": 1253.0, "tflops_best": 1288.0,
+          "row_mismatches": 0, "col_mismatches": 0, "passed": True}
+    assert json.loads(nat.judge_diag(json.dumps({"soak": ok})))["passed"]
+    r = json.loads(nat.judge_diag(json.dumps({"soak": dict(ok, row_mismatches=1, col_mismatches=1)})))
+    assert r["failures"] == ["GEMM soak checksums wrong: 1 rows, 1 columns"]
+    r = json.loads(nat.judge_diag(json.dumps({"soak": dict(ok, tflops_mean=600.0)})))
+    assert r["failures"] == ["GEMM soak TFLOP/s 600 below floor 950"]
