@@ -403,10 +403,35 @@ bool NodeAgent::run_diagnostics(bool force) {
       const Value& v = r.get(sect).get(k);
       return v.is_number() ? v.as_double() : 0.0;
     };
+    // per-GPU results as gauges (Prometheus), so fleet dashboards see a slow GPU before it fails a floor
+    auto& reg = metrics::Registry::global();
+    const metrics::Labels gl{{"gpu", std::to_string(gpus_[i].index)}};
+    struct G {
+      const char *name, *help, *sect, *key;
+    };
+    static const G kGauges[] = {
+        {"amd_gpu_diag_hbm_read_gbps", "Diagnostics: HBM read GB/s", "hbm", "read_gbps"},
+        {"amd_gpu_diag_hbm_write_gbps", "Diagnostics: HBM write GB/s", "hbm", "write_gbps"},
+        {"amd_gpu_diag_hbm_copy_gbps", "Diagnostics: HBM copy GB/s", "hbm", "copy_gbps"},
+        {"amd_gpu_diag_mfma_tflops", "Diagnostics: bf16 MFMA TFLOP/s (register operands)", "mfma", "tflops"},
+        {"amd_gpu_diag_xcc_balance", "Diagnostics: fastest/slowest XCC wave time", "mfma", "xcc_balance"},
+        {"amd_gpu_diag_soak_tflops", "Diagnostics: LDS-tiled MFMA GEMM soak TFLOP/s", "soak", "tflops_mean"},
+        {"amd_gpu_diag_pcie_h2d_gbps", "Diagnostics: PCIe host-to-device GB/s", "pcie", "h2d_gbps"},
+        {"amd_gpu_diag_pcie_d2h_gbps", "Diagnostics: PCIe device-to-host GB/s", "pcie", "d2h_gbps"},
+        {"amd_gpu_diag_burn_tflops", "Diagnostics: burn-in mean MFMA TFLOP/s", "burn", "tflops_mean"},
+        {"amd_gpu_diag_burn_max_hotspot_celsius", "Diagnostics: burn-in peak hotspot temperature", "burn", "max_hotspot_c"},
+    };
+    for (const auto& g : kGauges) {
+      if (r.get(g.sect).get(g.key).is_number()) reg.gauge(g.name, g.help, gl).set(get(g.sect, g.key));
+    }
+    reg.gauge("amd_gpu_diag_passed", "1 when the last diagnostics pass of the GPU succeeded", gl)
+        .set(r.get("passed").as_bool() ? 1 : 0);
     if (r.get("passed").as_bool()) {
       LOG_INFO("node_agent") << "diag gpu " << gpus_[i].index << ": passed, read " << get("hbm", "read_gbps")
                              << " GB/s, copy " << get("hbm", "copy_gbps") << " GB/s, mfma " << get("mfma", "tflops")
-                             << " TFLOP/s, xcc balance " << get("mfma", "xcc_balance");
+                             << " TFLOP/s, xcc balance " << get("mfma", "xcc_balance") << ", soak "
+                             << get("soak", "tflops_mean") << " TFLOP/s, pcie " << get("pcie", "h2d_gbps") << "/"
+                             << get("pcie", "d2h_gbps") << " GB/s";
     } else {
       LOG_WARN("node_agent") << "diag gpu " << gpus_[i].index << ": FAILED " << r.get("failures").dump();
     }

@@ -129,6 +129,7 @@ def _agent_with_floors(tmp_path, name, floors_env):
             import requests
 
             desc = requests.get(f"http://127.0.0.1:{c.node_agent_ports[name]}/gpus", timeout=10).json()
+            desc["_metrics"] = requests.get(f"http://127.0.0.1:{c.node_agent_ports[name]}/metrics", timeout=10).text
             return kubelet.device_lists[-1][1], node["metadata"]["labels"], desc
     finally:
         kubelet.stop()
@@ -145,10 +146,15 @@ def test_diag_floor_gates_health(tmp_path):
 def test_diag_default_floors_pass(tmp_path):
     devs, labels, desc = _agent_with_floors(tmp_path, "mi355x-ok", {"CONF_DIAG_BURN_MS": "2000"})
     _dump("diag_default_floors.json", desc["diag"])
+    _dump("diag_gauges.txt", {"metrics": [l for l in desc["_metrics"].splitlines() if l.startswith("amd_gpu_diag_")]})
     assert desc["diag"][0]["passed"], desc["diag"][0]["failures"]
     assert desc["diag"][0]["gemm"]["passed"]
     assert desc["diag"][0]["pcie"]["h2d_gbps"] > 45 and desc["diag"][0]["pcie"]["link_width"] == 16
     assert desc["diag"][0]["soak"]["passed"] and desc["diag"][0]["soak"]["tflops_mean"] > 950
+    gauges = {l.split("{")[0]: float(l.rsplit(" ", 1)[1]) for l in desc["_metrics"].splitlines()
+              if l.startswith("amd_gpu_diag_")}
+    assert gauges["amd_gpu_diag_passed"] == 1 and gauges["amd_gpu_diag_soak_tflops"] > 950
+    assert gauges["amd_gpu_diag_pcie_h2d_gbps"] > 45 and gauges["amd_gpu_diag_hbm_read_gbps"] > 4750
     assert desc["diag"][0]["burn"]["tflops_mean"] > 1800 and desc["diag"][0]["burn"]["samples"] >= 5
     assert [x[1] for x in devs] == ["Healthy"]
     assert labels["amd.com/gpu.healthy-count"] == "1" and labels["amd.com/gpu.diag"] == "passed"
