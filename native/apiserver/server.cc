@@ -337,15 +337,19 @@ struct WatchSub {
   }
 };
 
-// Store lock: a writer-preferring reader/writer lock (glibc's default rwlock prefers
-// readers, which starves commits under a steady GET/LIST load). Reads (path parsing, GET,
-// LIST, the optimistic pre-read of a write) share it; commits are exclusive.
+// Store lock.  Default: one mutex (futex wake-one) for reads and commits alike.  The
+// reader/writer lock used before (writer-preferring, since glibc's default starves commits
+// under a steady GET/LIST load) woke every waiting reader at each commit's unlock: at 800
+// creates in flight its wake-up herd cost more than the read parallelism gained
+// (profiles/kl_store_lock_r2/: N=8 +63 % CR/s, kube-lite CPU per CR 4.2 -> 2.2 ms with the
+// mutex; N=1 +17 %).  BGC_KL_RWLOCK=writer|reader selects the rwlock variants.
 class RwLock {
  public:
   RwLock() {
+    const char* kind = std::getenv("BGC_KL_RWLOCK");  // unset/"mutex": one mutex; "writer" / "reader": rwlock
+    mutex_only_ = !kind || (std::string(kind) != "writer" && std::string(kind) != "reader");
     pthread_rwlockattr_t a;
     pthread_rwlockattr_init(&a);
-    const char* kind = std::getenv("BGC_KL_RWLOCK");  // "reader" switches to reader preference
     pthread_rwlockattr_setkind_np(&a, kind && std::string(kind) == "reader" ? PTHREAD_RWLOCK_PREFER_READER_NP
                                                                            : PTHREAD_RWLOCK_PREFER_WRITER_NONRECURSIVE_NP);
     pthread_rwlock_init(&l_, &a);
@@ -354,15 +358,26 @@ class RwLock {
   ~RwLock() { pthread_rwlock_destroy(&l_); }
   RwLock(const RwLock&) = delete;
   RwLock& operator=(const RwLock&) = delete;
-  void lock() { pthread_rwlock_wrlock(&l_); }
-  bool try_lock() { return pthread_rwlock_trywrlock(&l_) == 0; }
-  void unlock() { pthread_rwlock_unlock(&l_); }
-  void lock_shared() { pthread_rwlock_rdlock(&l_); }
-  bool try_lock_shared() { return pthread_rwlock_tryrdlock(&l_) == 0; }
-  void unlock_shared() { pthread_rwlock_unlock(&l_); }
+  void lock() {
+    if (mutex_only_) m_.lock();
+    else pthread_rwlock_wrlock(&l_);
+  }
+  bool try_lock() { return mutex_only_ ? m_.try_lock() : pthread_rwlock_trywrlock(&l_) == 0; }
+  void unlock() {
+    if (mutex_only_) m_.unlock();
+    else pthread_rwlock_unlock(&l_);
+  }
+  void lock_shared() {
+    if (mutex_only_) m_.lock();
+    else pthread_rwlock_rdlock(&l_);
+  }
+  bool try_lock_shared() { return mutex_only_ ? m_.try_lock() : pthread_rwlock_tryrdlock(&l_) == 0; }
+  void unlock_shared() { unlock(); }
 
  private:
   pthread_rwlock_t l_;
+  std::mutex m_;
+  bool mutex_only_ = false;
 };
 
 // Watch wake-ups are deferred until the exclusive store lock is released (a futex wake per
