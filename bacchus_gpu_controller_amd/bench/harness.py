@@ -420,9 +420,9 @@ def run(args):
                        "apiserver_write_latency_ms": args.write_latency_ms, "control_plane_cpus": cpus,
                        "controller_workers": controller_workers, "sync_workers": sync_workers,
                        "sheet_poll_ms": args.sheet_poll_ms, "sync_interval_s": args.sync_interval,
-                       # API server -> webhook protocol: h2 (one multiplexed connection, as the
-                       # real apiserver's Go client) unless kube-lite runs --webhook-http1
-                       "webhook_protocol": "http/1.1" if "--webhook-http1" in args.apiserver_arg else "h2",
+                       # API server -> webhook protocol: kube-lite's HTTP/1.1 pool unless it runs
+                       # --webhook-http2 (multiplexed h2 streams)
+                       "webhook_protocol": "h2" if "--webhook-http2" in args.apiserver_arg else "http/1.1",
                        "driver_protocol": "h2" if args.driver_http2 and args.tls_apiserver else "http/1.1"},
         }
         out.update(main_r)

@@ -56,11 +56,11 @@ struct Options {
   // Paginated LIST (limit/continue) serves later pages from a snapshot taken at the first
   // page; continue tokens expire after this long (then 410 Expired, as etcd compaction).
   int continue_ttl_ms = 60000;
-  // Webhook callouts offer HTTP/2 by ALPN, as the real apiserver's Go client does, and
-  // concurrent admission requests are multiplexed as streams.  The apiserver keeps one
-  // connection; kube-lite spreads them over 4 (one connection's single reader thread in
-  // this process is the bottleneck at 800 callouts in flight, profiles/http2_r2/).
-  bool webhook_http2 = true;
+  // Webhook callouts: HTTP/1.1 keep-alive pool by default; webhook_http2 offers h2 by ALPN
+  // and multiplexes the callouts as streams over webhook_h2_connections connections (as
+  // the real apiserver's Go client does over one).  With kube-lite's mutex store lock the
+  // HTTP/1.1 pool measured equal or better at N=1..8 (profiles/http2_r2/after_store_lock/).
+  bool webhook_http2 = false;
   size_t webhook_h2_connections = 4;
 };
 

@@ -37,7 +37,9 @@ def review(uid, username="oidc:alice", groups=("gpu",), name="alice"):
 
 @pytest.fixture(scope="module")
 def cluster():
-    with Cluster(controller=False, tls_apiserver=True) as c:
+    # kube-lite's webhook client speaks HTTP/1.1 by default; --webhook-http2 makes it call
+    # the webhook the way the real apiserver does (h2 streams)
+    with Cluster(controller=False, tls_apiserver=True, apiserver_args=["--webhook-http2"]) as c:
         yield c
 
 
@@ -149,8 +151,9 @@ def test_webhook_callouts_use_h2_like_the_real_apiserver(cluster):
     assert after - before >= 5
 
 
-def test_webhook_http1_flag_keeps_http11():
-    with Cluster(controller=False, apiserver_args=["--webhook-http1"]) as c:
+@pytest.mark.parametrize("args", [[], ["--webhook-http1"]])
+def test_webhook_http1_default_keeps_http11(args):
+    with Cluster(controller=False, apiserver_args=args) as c:
         ca = os.path.join(c.cert_dir, "ca.crt")
         base = f"https://127.0.0.1:{c.admission_port}"
         before = metric(requests.get(f"{base}/metrics", verify=ca).text, "bgc_http2_streams_total")
@@ -164,7 +167,7 @@ def test_webhook_http1_flag_keeps_http11():
 
 def test_webhook_h2_connection_spread():
     """--webhook-h2-connections N spreads the callouts over N multiplexed connections."""
-    with Cluster(controller=False, apiserver_args=["--webhook-h2-connections", "3"]) as c:
+    with Cluster(controller=False, apiserver_args=["--webhook-http2", "--webhook-h2-connections", "3"]) as c:
         ca = os.path.join(c.cert_dir, "ca.crt")
         base = f"https://127.0.0.1:{c.admission_port}"
         before = metric(requests.get(f"{base}/metrics", verify=ca).text, "bgc_http2_streams_total")
