@@ -7,7 +7,7 @@
 # Each run has its own time limit; runs are chained with && so the first failure ends
 # the call.  JSON lines land in gpurun_out/matrix/.
 set -o pipefail
-OUT=gpurun_out/matrix
+OUT=${OUT:-gpurun_out/matrix}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 run() {  # name, timeout, bench args...
