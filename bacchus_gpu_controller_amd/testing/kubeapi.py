@@ -19,6 +19,7 @@ RESOURCES = {
     "leases": ("coordination.k8s.io", "v1", True),
     "secrets": ("", "v1", True),
     "serviceaccounts": ("", "v1", True),
+    "events": ("", "v1", True),
     "roles": ("rbac.authorization.k8s.io", "v1", True),
     "rolebindings": ("rbac.authorization.k8s.io", "v1", True),
     "clusterroles": ("rbac.authorization.k8s.io", "v1", False),

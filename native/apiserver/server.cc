@@ -597,6 +597,22 @@ struct ApiServer::Impl {
       types[ti.key()] = ti;
     }
     if (!opts.token_file.empty()) load_tokens(opts.token_file);
+    // the namespaces every cluster starts with (the apiserver's system namespace controller)
+    const TypeInfo& ns_ti = types.at(kube::types::Namespace.group + "/" + kube::types::Namespace.version + "/" +
+                                     kube::types::Namespace.plural);
+    for (const char* name : {"default", "kube-system", "kube-public", "kube-node-lease"}) {
+      const uint64_t v = ++rv;
+      Value ns = Value::object(
+          {{"apiVersion", "v1"}, {"kind", "Namespace"},
+           {"metadata", Value::object({{"name", name}, {"uid", crypto::uuid_v4()}, {"creationTimestamp", now_rfc3339()},
+                                       {"resourceVersion", rv_str(v)}})},
+           {"spec", Value::object({{"finalizers", Value::array({Value("kubernetes")})}})},
+           {"status", Value::object({{"phase", "Active"}})}});
+      Stored st;
+      st.obj = std::make_shared<const Value>(std::move(ns));
+      st.rv = v;
+      ns_ti.store->objs[name] = std::move(st);
+    }
     for (int i = 0; i < std::max(1, opts.gc_workers); ++i) gc_threads.emplace_back([this] { gc_loop(); });
   }
 

@@ -2,6 +2,7 @@
 // RoleBindings) and reconciles them; serves /health, /metrics on CONF_LISTEN_ADDR:PORT.
 // Reference: src/controller.rs:215-287.
 #include <cstdio>
+#include <unistd.h>
 #include <memory>
 
 #include "controller/reconcile.h"
@@ -75,6 +76,16 @@ int main() {
   ctrl.owns(kube::types::Role, nullptr, sel, cfg.metadata_watches);
   ctrl.owns(kube::types::RoleBinding, nullptr, sel, cfg.metadata_watches);
   controller::Reconciler rec(*client, ctrl, cfg);
+  std::unique_ptr<kube::EventRecorder> events;
+  if (cfg.events) {
+    kube::EventOptions eo;
+    eo.component = "bacchus-gpu-controller";
+    char host[256] = {0};
+    ::gethostname(host, sizeof(host) - 1);
+    eo.host = host;
+    events = std::make_unique<kube::EventRecorder>(*client, eo);
+    rec.set_event_recorder(events.get());
+  }
   auto& echoes = metrics::Registry::global().counter(
       "bgc_controller_own_write_events_total", "Child watch events dropped as echoes of our own applies");
   ctrl.set_child_filter([&](const kube::ResourceType& rt, const json::Value& child) {

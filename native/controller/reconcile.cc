@@ -24,6 +24,7 @@ Config Config::from_env(const EnvConfig& env) {
   c.error_backoff_base_ms = static_cast<int64_t>(env.u64_or("error_backoff_base_ms", 0));
   c.label_children = env.boolean_or("label_children", true);
   c.metadata_watches = env.boolean_or("metadata_watches", true);
+  c.events = env.boolean_or("events", true);
   c.lease = kube::LeaseSettings::from_env(env, "bacchus-gpu-controller");
   return c;
 }
@@ -306,6 +307,7 @@ kube::Action Reconciler::error_policy(const kube::ObjPtr& ub, const std::excepti
   const Value& meta = ub->get("metadata");
   LOG_ERROR("controller") << "error reconciling \"" << meta.get_string("namespace", "<unknown>") << "/"
                           << meta.get_string("name", "<unknown>") << "\": " << err.what();
+  if (events_) events_->record(kube::types::UserBootstrap, *ub, "Warning", "ReconcileFailed", err.what());
   int64_t delay = cfg_.error_requeue_ms;
   if (cfg_.error_backoff_base_ms > 0) {
     int n;

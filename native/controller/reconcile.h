@@ -29,6 +29,7 @@
 #include "core/threadpool.h"
 #include "kube/client.h"
 #include "kube/leader.h"
+#include "kube/events.h"
 #include "kube/runtime.h"
 
 namespace bgc::controller {
@@ -59,6 +60,8 @@ struct Config {
   // Child watches ask for PartialObjectMetadata only: the controller reads a child's
   // resourceVersion and ownerReferences, never its spec (kube-rs metadata_watcher).
   bool metadata_watches = true;
+  // Warning Events (kubectl describe userbootstrap) for failed reconciles.
+  bool events = true;
   kube::LeaseSettings lease;  // optional leader election (CONF_LEADER_ELECTION, ...)
   // reference fields are required (controller.rs:24-28); the rest default
   static Config from_env(const EnvConfig& env);
@@ -94,6 +97,8 @@ class Reconciler {
   // records (their DELETED events may be missed across a watch relist).
   void forget_owner(const std::string& owner);
   size_t cached_children() const;
+  // Optional (null = no Events): failed reconciles are recorded on the UserBootstrap.
+  void set_event_recorder(kube::EventRecorder* r) { events_ = r; }
 
   struct Stats {
     uint64_t applied = 0;
@@ -111,6 +116,7 @@ class Reconciler {
   void apply_all(const std::vector<DesiredChild>& children, const std::function<void(size_t)>& run_one);
   void forget_owner_locked(const std::string& owner);  // mu_ held
   bool owner_live(const std::string& name, const std::string& uid);
+  kube::EventRecorder* events_ = nullptr;
   void apply_child(const DesiredChild& c, const std::string& body_hash, const std::string& body_json);
 
   kube::KubeClient& client_;

@@ -72,6 +72,7 @@ NodeAgentConfig NodeAgentConfig::from_env(const EnvConfig& env) {
   c.slow_every = static_cast<int>(env.u64_or("slow_every", static_cast<uint64_t>(c.slow_every)));
   c.ras_every = static_cast<int>(env.u64_or("ras_every", static_cast<uint64_t>(c.ras_every)));
   c.create_node = env.boolean_or("create_node", false);
+  c.events = env.boolean_or("events", true);
   c.device_plugin = env.boolean_or("device_plugin", false);
   c.device_plugin_dir = env.str_or("device_plugin_dir", c.device_plugin_dir);
   c.device_plugin_socket = env.str_or("device_plugin_socket", c.device_plugin_socket);
@@ -190,7 +191,50 @@ Value node_status_patch(const NodeAgentConfig& cfg, const std::vector<GpuInfo>& 
 }
 
 NodeAgent::NodeAgent(kube::KubeClient& client, std::unique_ptr<Backend> backend, NodeAgentConfig cfg)
-    : client_(client), backend_(std::move(backend)), cfg_(std::move(cfg)) {}
+    : client_(client), backend_(std::move(backend)), cfg_(std::move(cfg)) {
+  if (cfg_.events) {
+    kube::EventOptions eo;
+    eo.component = "bgc-node-agent";
+    eo.host = cfg_.node_name;
+    events_ = std::make_unique<kube::EventRecorder>(client_, eo);
+  }
+}
+
+static bool diag_failed(const DiagOutcome& d, size_t i);
+
+void NodeAgent::node_event(const std::string& type, const std::string& reason, const std::string& message) {
+  if (!events_) return;
+  events_->record(types::Node, Value::object({{"metadata", Value::object({{"name", cfg_.node_name}})}}), type, reason,
+                  message);
+}
+
+std::string NodeAgent::gpu_reason(size_t i) const {
+  auto snap = poller_ ? poller_->snapshot() : nullptr;
+  std::string why;
+  if (snap && i < snap->health.size() && !snap->health[i].healthy) why = snap->health[i].reason;
+  std::lock_guard<std::mutex> lk(diag_mu_);
+  if (diag_failed(diag_, i)) {
+    if (!why.empty()) why += "; ";
+    why += "diagnostics failed " + diag_.per_gpu.items()[i].get("failures").dump();
+  }
+  return why;
+}
+
+void NodeAgent::emit_health_events() {
+  if (!events_) return;
+  const std::vector<bool> flags = healthy_flags();
+  std::lock_guard<std::mutex> lk(event_mu_);
+  event_state_.resize(gpus_.size(), -1);
+  for (size_t i = 0; i < gpus_.size() && i < flags.size(); ++i) {
+    const int now = flags[i] ? 1 : 0;
+    const int was = event_state_[i];
+    event_state_[i] = now;
+    if (now == was || (was == -1 && now == 1)) continue;  // healthy at start is not news
+    const std::string id = "gpu " + std::to_string(gpus_[i].index) + " (" + gpus_[i].bdf + ")";
+    if (now == 0) node_event("Warning", "GPUUnhealthy", id + " unhealthy: " + gpu_reason(i));
+    else node_event("Normal", "GPUHealthy", id + " healthy again");
+  }
+}
 
 NodeAgent::~NodeAgent() { stop(); }
 
@@ -434,6 +478,8 @@ bool NodeAgent::run_diagnostics(bool force) {
                              << get("pcie", "d2h_gbps") << " GB/s";
     } else {
       LOG_WARN("node_agent") << "diag gpu " << gpus_[i].index << ": FAILED " << r.get("failures").dump();
+      node_event("Warning", "GPUDiagnosticsFailed",
+                 "gpu " + std::to_string(gpus_[i].index) + " (" + gpus_[i].bdf + "): " + r.get("failures").dump());
     }
   }
   bool changed = false;
@@ -462,6 +508,7 @@ bool NodeAgent::run_diagnostics(bool force) {
 
 void NodeAgent::on_health_changed() {
   if (plugin_) plugin_->set_health(healthy_flags());
+  emit_health_events();
   try {
     publish();
   } catch (const std::exception& e) {
@@ -520,6 +567,7 @@ void NodeAgent::start() {
   }
   poller_->on_health_change([this](const Snapshot&) { on_health_changed(); });
   poller_->start();
+  emit_health_events();  // GPUs already unhealthy at start (pre-existing UEs, failed diagnostics)
   if (cfg_.run_diag && cfg_.diag_interval_secs > 0) {
     diag_thread_ = std::thread([this] {
       while (!stop_.wait_for(std::chrono::seconds(cfg_.diag_interval_secs))) {

@@ -31,6 +31,7 @@
 #include "gpu/diag.h"
 #include "gpu/telemetry.h"
 #include "kube/client.h"
+#include "kube/events.h"
 
 namespace bgc::gpu {
 
@@ -77,6 +78,9 @@ struct NodeAgentConfig {
   int slow_every = 10;                 // polls between VRAM/ECC-total reads
   int ras_every = 60;                  // polls between bad-page / per-block ECC / link reads
   bool create_node = false;            // test clusters without a kubelet
+  // Events on the Node (kubectl describe node): GPUUnhealthy / GPUHealthy transitions and
+  // GPUDiagnosticsFailed, aggregated and rate limited (kube/events.h).
+  bool events = true;
   // Kubelet device plugin (gpu/device_plugin.h).  When on, the kubelet owns the
   // amd.com/gpu capacity/allocatable counts, so the Node status patch carries only the
   // AMDGPUHealthy condition; labels and topology are published as before.
@@ -161,6 +165,12 @@ class NodeAgent {
   std::thread node_watch_;
   std::atomic<bool> node_present_{true};
   std::atomic<uint64_t> publishes_{0};
+  std::unique_ptr<kube::EventRecorder> events_;
+  std::mutex event_mu_;
+  std::vector<int> event_state_;  // per GPU: -1 not reported yet, 1 healthy, 0 unhealthy
+  void emit_health_events();
+  void node_event(const std::string& type, const std::string& reason, const std::string& message);
+  std::string gpu_reason(size_t i) const;  // why GPU i is unhealthy ("" when healthy)
 };
 
 }  // namespace bgc::gpu

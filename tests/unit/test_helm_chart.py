@@ -111,12 +111,13 @@ NEEDED = {
     + [("", r, v) for r in ("namespaces", "resourcequotas") for v in ("get", "list", "watch", "create", "patch")]
     + [("rbac.authorization.k8s.io", r, v) for r in ("roles", "rolebindings") for v in ("get", "list", "watch", "create", "patch")]
     + [("rbac.authorization.k8s.io", "roles", "bind"), ("rbac.authorization.k8s.io", "roles", "escalate")]
-    + [("coordination.k8s.io", "leases", v) for v in ("get", "create", "update")],
+    + [("coordination.k8s.io", "leases", v) for v in ("get", "create", "update")]
+    + [("", "events", v) for v in ("create", "patch")],  # ReconcileFailed events
     "synchronizer": [("bacchus.io", "userbootstraps", v) for v in ("get", "list", "watch", "patch")]
     + [("bacchus.io", "userbootstraps/status", "update")]
     + [("coordination.k8s.io", "leases", v) for v in ("get", "create", "update")],
     "node-agent": [("", "nodes", v) for v in ("get", "list", "watch", "patch")]
-    + [("", "nodes/status", "patch")],
+    + [("", "nodes/status", "patch")] + [("", "events", v) for v in ("create", "patch")],  # GPU health events
 }
 
 
