@@ -53,6 +53,10 @@ Value to_json(const GpuInfo& g) {
   v["pcie_max_width"] = g.pcie_max_width;
   v["pcie_max_speed_mts"] = g.pcie_max_speed_mts;
   v["pcie_max_gen"] = g.pcie_max_gen;
+  v["driver_name"] = g.driver_name;
+  v["driver_version"] = g.driver_version;
+  v["vbios_version"] = g.vbios_version;
+  v["vbios_part_number"] = g.vbios_part_number;
   Value links = Value::array();
   for (const auto& l : g.links) links.push_back(to_json(l));
   v["links"] = links;
@@ -191,6 +195,10 @@ GpuInfo gpu_info_from_json(const Value& v) {
   g.pcie_max_width = int_or("pcie_max_width", -1);
   g.pcie_max_speed_mts = int_or("pcie_max_speed_mts", -1);
   g.pcie_max_gen = int_or("pcie_max_gen", -1);
+  g.driver_name = v.get_string("driver_name");
+  g.driver_version = v.get_string("driver_version");
+  g.vbios_version = v.get_string("vbios_version");
+  g.vbios_part_number = v.get_string("vbios_part_number");
   for (const auto& l : v.get("links").items()) g.links.push_back(peer_link_from_json(l));
   for (const auto& l : v.get("phys_links").items()) g.phys_links.push_back(phys_link_from_json(l));
   return g;
@@ -255,6 +263,10 @@ Value default_mi355x_fixture(int n_gpus, uint64_t hive_id) {
     g["pcie_max_width"] = 16;
     g["pcie_max_speed_mts"] = 32000;  // Gen5
     g["pcie_max_gen"] = 5;
+    g["driver_name"] = "amdgpu";
+    g["driver_version"] = "6.16.6";
+    g["vbios_version"] = "022.040.003.043.000001";
+    g["vbios_part_number"] = "113-M3550101-100";
     // 8x MI355X UBB: a full xGMI mesh, one link to every peer (7 x ~153 GB/s per GPU).
     Value links = Value::array(), phys = Value::array();
     for (int j = 0; j < n_gpus; ++j) {
@@ -464,6 +476,8 @@ struct AmdSmiApi {
   decltype(&amdsmi_get_gpu_ecc_count) ecc_count = nullptr;
   decltype(&amdsmi_get_gpu_process_list) process_list = nullptr;
   decltype(&amdsmi_get_pcie_info) pcie_info = nullptr;
+  decltype(&amdsmi_get_gpu_driver_info) driver_info = nullptr;
+  decltype(&amdsmi_get_gpu_vbios_info) vbios_info = nullptr;
 };
 
 struct BlockName {
@@ -487,6 +501,9 @@ std::string bdf_string(const amdsmi_bdf_t& bdf) {
                 static_cast<unsigned>(bdf.function_number));
   return buf;
 }
+
+// amdsmi string fields are fixed arrays that may lack a terminator when full
+std::string cstr(const char* p, size_t cap) { return std::string(p, strnlen(p, cap)); }
 
 template <typename F>
 void resolve(void* lib, F& fn, const char* sym, bool required) {
@@ -530,6 +547,8 @@ class AmdSmiBackend : public Backend {
     resolve(api_.lib, api_.ecc_count, "amdsmi_get_gpu_ecc_count", false);
     resolve(api_.lib, api_.process_list, "amdsmi_get_gpu_process_list", false);
     resolve(api_.lib, api_.pcie_info, "amdsmi_get_pcie_info", false);
+    resolve(api_.lib, api_.driver_info, "amdsmi_get_gpu_driver_info", false);
+    resolve(api_.lib, api_.vbios_info, "amdsmi_get_gpu_vbios_info", false);
     amdsmi_status_t st = api_.init(AMDSMI_INIT_AMD_GPUS);
     if (st != AMDSMI_STATUS_SUCCESS) throw std::runtime_error("amdsmi_init failed: status " + std::to_string(st));
     initialized_ = true;
@@ -644,6 +663,22 @@ class AmdSmiBackend : public Backend {
                                    ? ps.max_pcie_interface_version
                                    : ps.pcie_interface_version;
           if (gen != 0xFFFFFFFFu && gen != 0) g.pcie_max_gen = static_cast<int>(gen);
+        }
+      }
+      if (api_.driver_info) {
+        amdsmi_driver_info_t d;
+        std::memset(&d, 0, sizeof(d));
+        if (api_.driver_info(h, &d) == AMDSMI_STATUS_SUCCESS) {
+          g.driver_name = cstr(d.driver_name, sizeof(d.driver_name));
+          g.driver_version = cstr(d.driver_version, sizeof(d.driver_version));
+        }
+      }
+      if (api_.vbios_info) {
+        amdsmi_vbios_info_t vb;
+        std::memset(&vb, 0, sizeof(vb));
+        if (api_.vbios_info(h, &vb) == AMDSMI_STATUS_SUCCESS) {
+          g.vbios_version = cstr(vb.version, sizeof(vb.version));
+          g.vbios_part_number = cstr(vb.part_number, sizeof(vb.part_number));
         }
       }
       g.phys_links = read_links(h);

@@ -71,6 +71,12 @@ struct GpuInfo {
   int pcie_max_width = -1;       // lanes
   int pcie_max_speed_mts = -1;   // per-lane rate, MT/s (Gen5 = 32000)
   int pcie_max_gen = -1;
+  // Software/firmware identity (amdsmi_get_gpu_driver_info, amdsmi_get_gpu_vbios_info):
+  // published as node labels so a driver or VBIOS rollout can be tracked per node.
+  std::string driver_name;      // "amdgpu"
+  std::string driver_version;   // "6.16.6" (empty = unknown)
+  std::string vbios_version;
+  std::string vbios_part_number;
   std::vector<PeerLink> links;       // to every other discovered GPU
   std::vector<PhysLink> phys_links;  // physical links at discovery time
 };

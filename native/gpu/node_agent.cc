@@ -151,6 +151,17 @@ Value node_labels_patch(const NodeAgentConfig& cfg, const std::vector<GpuInfo>& 
     labels[p + ".compute-partition"] = sanitize_label_value(g.compute_partition.empty() ? "unknown" : g.compute_partition);
     labels[p + ".memory-partition"] = sanitize_label_value(g.memory_partition.empty() ? "unknown" : g.memory_partition);
     if (g.num_cus) labels[p + ".cu-count"] = std::to_string(g.num_cus);
+    // Driver / VBIOS identity; "mixed" flags a node caught mid-way through a firmware
+    // rollout (one value per node, as every GPU of a UBB should match).
+    auto common = [&](auto field) {
+      std::set<std::string> vals;
+      for (const auto& x : gpus) vals.insert(x.*field);
+      if (vals.size() > 1) return std::string("mixed");
+      std::string v = sanitize_label_value(*vals.begin());
+      return v.empty() ? std::string("unknown") : v;
+    };
+    labels[p + ".driver-version"] = common(&GpuInfo::driver_version);
+    labels[p + ".vbios-version"] = common(&GpuInfo::vbios_version);
   }
   labels[p + ".diag"] = !diag.ran ? "skipped" : diag.passed ? "passed" : "failed";
   Value topo = Value::array();

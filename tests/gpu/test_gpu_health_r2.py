@@ -45,6 +45,11 @@ def test_amdsmi_topology_ras_and_violations():
     # the 32-bit legacy throttle word is the all-ones sentinel on MI355X: never exported
     assert ras["throttle_status"] != 0xFFFFFFFF
     assert ras2["ok"]
+    # driver / VBIOS identity feeds the amd.com/gpu.driver-version and .vbios-version labels
+    assert g["driver_name"] == "amdgpu" and g["driver_version"], g
+    assert g["vbios_version"] or g["vbios_part_number"], g
+    labels = json.loads(native().node_patches(json.dumps(gpus), len(gpus))[0])["metadata"]["labels"]
+    assert labels["amd.com/gpu.driver-version"] not in ("", "unknown", "mixed"), labels
 
 
 def test_poller_violation_percentages_and_own_process():

@@ -57,6 +57,8 @@ def test_node_patches(nat):
     assert l["amd.com/gpu.vram-gb"] == "288"
     assert l["amd.com/gpu.xgmi-hive-id"] == "1a2b3c4d5e6f7788" and l["amd.com/gpu.xgmi-hives"] == "1"
     assert l["amd.com/gpu.diag"] == "passed"
+    assert l["amd.com/gpu.driver-version"] == "6.16.6"
+    assert l["amd.com/gpu.vbios-version"] == "022.040.003.043.000001"
     topo = json.loads(labels["metadata"]["annotations"]["amd.com/gpu.topology"])
     assert len(topo) == 8 and topo[3]["node"] == 3
     st = status["status"]
@@ -70,6 +72,18 @@ def test_mixed_hives_label(nat):
     gpus = json.loads(nat.gpu_backend("mock", json.dumps(f)).discover())
     labels = json.loads(nat.node_patches(json.dumps(gpus), 4)[0])["metadata"]["labels"]
     assert labels["amd.com/gpu.xgmi-hive-id"] == "mixed" and labels["amd.com/gpu.xgmi-hives"] == "2"
+
+
+def test_driver_and_vbios_labels(nat):
+    f = json.loads(nat.default_mi355x_fixture(4))
+    f["gpus"][1]["vbios_version"] = "022.040.003.044.000001"  # one board mid-rollout
+    for g in f["gpus"]:
+        g["driver_version"] = ""
+    gpus = json.loads(nat.gpu_backend("mock", json.dumps(f)).discover())
+    assert gpus[0]["vbios_part_number"] == "113-M3550101-100" and gpus[0]["driver_name"] == "amdgpu"
+    labels = json.loads(nat.node_patches(json.dumps(gpus), 4)[0])["metadata"]["labels"]
+    assert labels["amd.com/gpu.vbios-version"] == "mixed"
+    assert labels["amd.com/gpu.driver-version"] == "unknown"
 
 
 def test_sanitize_label_value(nat):
