@@ -873,6 +873,8 @@ int bgc_diag_gemm_soak(int device, int m, int n, int k, int launches, uint32_t s
   const double flop = 2.0 * m * n * static_cast<double>(k);
   float ms = 0.f, best = 1e30f, total = 0.f;
   for (int it = 0; it < launches; ++it) {
+    // poison C before the last checked launch, so its checksums cover that launch's writes
+    if (it > 0 && it == launches - 1) HIP_TRY(hipMemsetAsync(c.p, 0xFF, nc * 4, nullptr));
     HIP_TRY(hipEventRecord(ev.a, nullptr));
     if (big) {
       hipLaunchKernelGGL((gemm_soak<256, 256, 2, 4>), dim3(grid), dim3(512), 0, nullptr, static_cast<const __bf16*>(a.p),
