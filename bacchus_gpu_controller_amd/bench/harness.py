@@ -345,8 +345,11 @@ def run(args):
     total_steps = args.warmup + args.steps
     cpus = effective_cpus()
     tuned = args.tuned_concurrency if args.tuned_concurrency > 0 else auto_concurrency(d.world, cpus)
-    phases = [("m", args.concurrency)]
-    if args.tuned_phase and tuned != args.concurrency:
+    # BASELINE config #3 is 100 concurrent CRs on the node: by default that total is split
+    # over the ranks (ceil), so N load generators offer the same in-flight load as one
+    conc = args.concurrency if args.concurrency_scope == "rank" else max(1, -(-args.concurrency // d.world))
+    phases = [("m", conc)]
+    if args.tuned_phase and tuned != conc:
         phases.append(("t", tuned))
     semantics = "reference" if args.reference_semantics else args.semantics
     # Reconcile/sync workers spend most of their time waiting on API round trips, so they
@@ -416,7 +419,8 @@ def run(args):
             "data": "synthetic tenants (UserBootstrap CRs), fake Google sheet",
             "config": {"model": model, "global_batch": args.batch * d.world, "seq_len": None,
                        "parallelism": f"dp{d.world}", "semantics": semantics, "flow": flow,
-                       "concurrency_per_rank": args.concurrency, "log_level": args.log_level,
+                       "concurrency_per_rank": conc, "concurrency_total": conc * d.world,
+                       "concurrency_scope": args.concurrency_scope, "log_level": args.log_level,
                        "apiserver_write_latency_ms": args.write_latency_ms, "control_plane_cpus": cpus,
                        "controller_workers": controller_workers, "sync_workers": sync_workers,
                        "sheet_poll_ms": args.sheet_poll_ms, "sync_interval_s": args.sync_interval,
@@ -472,7 +476,9 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=100, help="UserBootstraps applied per rank per step")
     ap.add_argument("--concurrency", type=int, default=100,
-                    help="in-flight creates per rank (BASELINE config #3: 100 concurrent CRs)")
+                    help="in-flight creates (BASELINE config #3: 100 concurrent CRs on the node)")
+    ap.add_argument("--concurrency-scope", choices=("total", "rank"), default="total",
+                    help="total: --concurrency is split over the ranks; rank: every rank keeps that many in flight")
     ap.add_argument("--tuned-phase", action=argparse.BooleanOptionalAction, default=True,
                     help="also measure a secondary phase with the offered load sized to the CPU share")
     ap.add_argument("--tuned-concurrency", type=int, default=0, help="0 = auto_concurrency()")

@@ -28,14 +28,16 @@ def test_bench_two_ranks_gloo():
     assert d["config"]["global_batch"] == 40 and d["config"]["parallelism"] == "dp2"
     assert d["ready_crs"] == 2 * 2 * 20 and d["failed_crs"] == 0
     assert d["value"] > 0 and d["scaling"] == "weak"
-    assert d["config"]["concurrency_per_rank"] == 100 and d["config"]["control_plane_cpus"] >= 1
+    # config #3's 100 concurrent CRs are split over the ranks
+    assert d["config"]["concurrency_per_rank"] == 50 and d["config"]["concurrency_total"] == 100
+    assert d["config"]["concurrency_scope"] == "total" and d["config"]["control_plane_cpus"] >= 1
     assert d["config"]["log_level"] == "info" and d["dtype"] == "none"
     # per-component CPU cost of the timed region, split product vs test scaffolding
     cpu = d["cpu_ms_per_cr"]
     for k in ("controller", "admission", "synchronizer", "node_agent", "kube_lite", "load_driver", "product_total"):
         assert k in cpu and cpu[k] >= 0
     assert d["apiserver_requests_per_cr"] > 0
-    assert d["tuned"]["concurrency_per_rank"] < 100 and d["tuned"]["failed_crs"] == 0
+    assert d["tuned"]["concurrency_per_rank"] < 50 and d["tuned"]["failed_crs"] == 0
 
 
 def test_bench_approve_after_create():
