@@ -332,6 +332,23 @@ def _phase(d, nat, info, args, phase, concurrency, total_steps, cluster):
     return out
 
 
+def _xgmi_probe(d, args):
+    """RCCL all-reduce over the ranks' GPUs (N5, parallel/rccl_probe.py), after the timed
+    region: busbw per size, exact results, hive placement and the bytes amdsmi saw on each
+    GPU's xGMI links. Only with N>1 ranks on GPUs; a failure is reported, not raised."""
+    sizes = [float(x) for x in args.xgmi_probe_mb.split(",") if x]
+    if d.world < 2 or not d.cuda or not sizes:
+        return None
+    try:
+        from ..parallel.rccl_probe import sweep
+
+        r = sweep(sizes, iters=5, warmup=2)
+        return {k: r[k] for k in ("world_size", "single_hive", "traffic_on_xgmi", "all_correct",
+                                  "max_busbw_gbps", "results", "hives", "xgmi_traffic")}
+    except Exception as e:  # noqa: BLE001
+        return {"error": f"{type(e).__name__}: {e}"}
+
+
 def run(args):
     d = Dist()
     n = args.gpus if args.gpus else d.world
@@ -395,6 +412,7 @@ def run(args):
     info = d.broadcast_obj(info)
     try:
         results = {ph: _phase(d, nat, info, args, ph, conc, total_steps, cluster) for ph, conc in phases}
+        xgmi = _xgmi_probe(d, args)
         if d.rank != 0:
             return None
         main_r = results["m"]
@@ -438,6 +456,8 @@ def run(args):
                                                   "apply_to_ready_p99_ms", "cpu_ms_per_cr", "failed_crs")}
         # amdsmi counters of the advertised GPUs at the end of the timed region (node agent)
         out["gpu_telemetry"] = gpu_tel
+        if xgmi is not None:
+            out["rccl_xgmi"] = xgmi
         out["reference_structural"] = {"apply_to_ready_p50_s": 30.0, "apply_to_ready_p99_s": 59.4,
                                        "note": "reference gates readiness on a 60 s sheet poll (synchronizer.rs:192)"}
         if args.report_cpu and cluster is not None:
@@ -488,6 +508,8 @@ def main(argv=None):
     ap.add_argument("--poll-ms", type=int, default=250)
     ap.add_argument("--log-level", default="info", help="RUST_LOG of every service (chart default: info)")
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--xgmi-probe-mb", default="16,256",
+                    help="N>1 GPUs: all-reduce sizes (MiB) for the RCCL/xGMI probe after the timed region ('' = off)")
     ap.add_argument("--semantics", choices=("this", "reference", "reference-controller"), default="this",
                     help="reference: the reference's controller and synchronizer behaviour on this stack "
                          "(periodic sheet sync only, sequential unconditional child applies); "

@@ -74,8 +74,33 @@ def run(sizes_mb, iters=10, warmup=3, require_single_hive=False, dtype="bf16"):
         os.environ.setdefault("RANK", str(rank))
         os.environ.setdefault("WORLD_SIZE", str(world))
         dist.init_process_group(backend=backend)
+    out = sweep(sizes_mb, iters, warmup, dtype)
+    dist.barrier()
+    dist.destroy_process_group()
+    if require_single_hive and not out["single_hive"]:
+        raise SystemExit(f"TP group spans multiple xGMI hives: {out['hives']}")
+    return out if rank == 0 else None
+
+
+def sweep(sizes_mb, iters=10, warmup=3, dtype="bf16"):
+    """The probe over an already initialised process group (every rank calls it; every
+    rank gets the result). bench.py runs it after its timed region on N>1 GPUs."""
+    import torch
+    import torch.distributed as dist
+
+    rank, world = dist.get_rank(), dist.get_world_size()
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    backend = dist.get_backend()
+    cuda = backend == "nccl"
     dev = torch.device("cuda", torch.cuda.current_device()) if cuda else torch.device("cpu")
     tdtype = {"bf16": torch.bfloat16, "fp32": torch.float32}[dtype]
+
+    def barrier():
+        if cuda:
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()
+
     hive = local_hive_id(local) if cuda else "cpu"
     hives = [None] * world
     dist.all_gather_object(hives, hive)
@@ -111,7 +136,7 @@ def run(sizes_mb, iters=10, warmup=3, require_single_hive=False, dtype="bf16"):
             buf.fill_(float(rank + 1))
             if cuda:
                 torch.cuda.synchronize()
-            dist.barrier()
+            barrier()
             t0 = time.perf_counter()
             dist.all_reduce(buf)
             if cuda:
@@ -144,11 +169,7 @@ def run(sizes_mb, iters=10, warmup=3, require_single_hive=False, dtype="bf16"):
                                                 t["xgmi_written_mb"] >= 0.5 * t["expected_mb"] for t in traffic),
            "results": results, "max_busbw_gbps": max(r["busbw_gbps"] for r in results) if results else 0.0,
            "all_correct": all(r["correct"] for r in results)}
-    dist.barrier()
-    dist.destroy_process_group()
-    if require_single_hive and not single_hive:
-        raise SystemExit(f"TP group spans multiple xGMI hives: {hives}")
-    return out if rank == 0 else None
+    return out
 
 
 def main(argv=None):
