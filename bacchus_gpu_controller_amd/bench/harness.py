@@ -209,7 +209,7 @@ def _phase(d, nat, info, args, phase, concurrency, total_steps, cluster):
 
     driver = nat.ChurnDriver(info["server"], ADMIN_TOKEN, f"r{d.rank}-", concurrency,
                              ca_pem=info["apiserver_ca"], approve_url=info.get("approve_url", ""),
-                             http2=args.driver_http2)
+                             http2=args.driver_http2, server_filter=args.driver_server_filter)
     driver.start()
     time.sleep(0.2)
     prev = None
@@ -445,7 +445,10 @@ def run(args):
                        # API server -> webhook protocol: kube-lite's HTTP/1.1 pool unless it runs
                        # --webhook-http2 (multiplexed h2 streams)
                        "webhook_protocol": "h2" if "--webhook-http2" in args.apiserver_arg else "http/1.1",
-                       "driver_protocol": "h2" if args.driver_http2 and args.tls_apiserver else "http/1.1"},
+                       "driver_protocol": "h2" if args.driver_http2 and args.tls_apiserver else "http/1.1",
+                       # each rank's load driver watches only its own tenants' children
+                       # (kube-lite name-prefix field selector); the product is unaffected
+                       "driver_server_filter": args.driver_server_filter},
         }
         out.update(main_r)
         if "t" in results:
@@ -508,6 +511,9 @@ def main(argv=None):
     ap.add_argument("--poll-ms", type=int, default=250)
     ap.add_argument("--log-level", default="info", help="RUST_LOG of every service (chart default: info)")
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--driver-server-filter", action=argparse.BooleanOptionalAction, default=True,
+                    help="per-rank load drivers ask kube-lite to filter their child watches by tenant-name "
+                         "prefix (no N-fold watch fan-out from the load generators themselves)")
     ap.add_argument("--xgmi-probe-mb", default="16,256",
                     help="N>1 GPUs: all-reduce sizes (MiB) for the RCCL/xGMI probe after the timed region ('' = off)")
     ap.add_argument("--semantics", choices=("this", "reference", "reference-controller"), default="this",

@@ -109,8 +109,8 @@ class KubeApi:
                 return None
             raise
 
-    def list(self, plural, namespace=None, label_selector=None):
-        params = {"labelSelector": label_selector} if label_selector else None
+    def list(self, plural, namespace=None, label_selector=None, field_selector=None):
+        params = {k: v for k, v in (("labelSelector", label_selector), ("fieldSelector", field_selector)) if v} or None
         return self._req("GET", path_for(plural, None, namespace), params=params)
 
     def create(self, plural, obj, namespace=None, field_manager=None):

@@ -195,6 +195,13 @@ bool selector_matches(const std::vector<Requirement>& reqs, const Value& obj) {
 
 struct FieldFilter {
   std::string name, ns;
+  // kube-lite test extension (a real apiserver rejects the key): only objects whose name
+  // starts with this prefix. Used by the bench's per-rank load drivers, so N drivers do not
+  // multiply the child-watch fan-out N times; the product binaries never send it.
+  std::string name_prefix;
+  bool name_ok(std::string_view n) const {
+    return (name.empty() || n == name) && (name_prefix.empty() || n.substr(0, name_prefix.size()) == name_prefix);
+  }
 };
 
 FieldFilter parse_field_selector(const std::string& s) {
@@ -208,6 +215,7 @@ FieldFilter parse_field_selector(const std::string& s) {
     std::string v = trim(part.substr(part[eq + 1] == '=' ? eq + 2 : eq + 1));
     if (k == "metadata.name") f.name = v;
     else if (k == "metadata.namespace") f.ns = v;
+    else if (k == "kube-lite.test/name-prefix") f.name_prefix = v;
   }
   return f;
 }
@@ -792,7 +800,7 @@ struct ApiServer::Impl {
     std::lock_guard<std::mutex> wg(st.watches_mu);
     for (const auto& w : st.watches) {
       if (!w->ns.empty() && w->ns != ns) continue;
-      if (!w->fields.name.empty() && obj->get("metadata").get_string("name") != w->fields.name) continue;
+      if (!w->fields.name_ok(obj->get("metadata").get_string("name"))) continue;
       if (!w->sel.empty() && !selector_matches(w->sel, *obj)) continue;
       {
         std::lock_guard<std::mutex> g(w->m);
@@ -1796,7 +1804,7 @@ struct ApiServer::Impl {
         for (auto& [k, st] : bucket(*p.ti)) {
           const Value& meta = st.obj->get("metadata");
           if (!p.ns.empty() && meta.get_string("namespace") != p.ns) continue;
-          if (!ff.name.empty() && meta.get_string("name") != ff.name) continue;
+          if (!ff.name_ok(meta.get_string("name"))) continue;
           if (!ff.ns.empty() && meta.get_string("namespace") != ff.ns) continue;
           if (!sel.empty() && !selector_matches(sel, *st.obj)) continue;
           items.push_back(st.obj);
@@ -1888,7 +1896,7 @@ struct ApiServer::Impl {
         for (auto& [k, st] : ts.objs) {
           const Value& meta = st.obj->get("metadata");
           if (!sub.ns.empty() && meta.get_string("namespace") != sub.ns) continue;
-          if (!sub.fields.name.empty() && meta.get_string("name") != sub.fields.name) continue;
+          if (!sub.fields.name_ok(meta.get_string("name"))) continue;
           if (!sub.sel.empty() && !selector_matches(sub.sel, *st.obj)) continue;
           std::string line = "{\"type\":\"ADDED\",\"object\":";
           if (meta_only) dump_partial_metadata(*st.obj, line);
@@ -1905,7 +1913,7 @@ struct ApiServer::Impl {
           const auto& e = *it;
           if (e->type_key != sub.type_key) continue;
           if (!sub.ns.empty() && e->ns != sub.ns) continue;
-          if (!sub.fields.name.empty() && e->meta->get("metadata").get_string("name") != sub.fields.name) continue;
+          if (!sub.fields.name_ok(e->meta->get("metadata").get_string("name"))) continue;
           if (!sub.sel.empty() && !selector_matches(sub.sel, *e->meta)) continue;
           initial.push_back(meta_only ? std::make_shared<const std::string>(e->metadata_line()) : e->line);
         }

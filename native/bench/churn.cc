@@ -83,7 +83,8 @@ void ChurnDriver::start() {
   };
   for (W w : {W{&types::Namespace, 0}, W{&types::ResourceQuota, 1}, W{&types::RoleBinding, 2}}) {
     watchers_.emplace_back([this, w] {
-      kube::Watcher watcher(*admin_, *w.rt);
+      const bool filter = opts_.server_filter && !opts_.name_prefix.empty();
+      kube::Watcher watcher(*admin_, *w.rt, "", "", filter ? "kube-lite.test/name-prefix=" + opts_.name_prefix : "");
       if (!opts_.name_prefix.empty()) {
         // one driver per rank: skip other ranks' tenants without parsing their events
         // (each child's name, and its owner reference, carry the tenant name)

@@ -36,6 +36,10 @@ struct ChurnOptions {
   std::string gpu_quota_key = "requests.amd.com/gpu";
   int concurrency = 32;
   std::string name_prefix;  // only names with this prefix are tracked (one driver per rank)
+  // Ask kube-lite to filter the child watches by name_prefix on the server (its
+  // kube-lite.test/name-prefix field selector), so N per-rank drivers do not receive, and
+  // the server does not encrypt and write, every other rank's child events.
+  bool server_filter = false;
   // Approve-after-create (the reference's real onboarding order):
   // when set, a step first waits for every tenant's Namespace, then approves the whole
   // batch with one sheet edit (POST {"rows":[{"id_username":...}],"append":true} to this

@@ -16,7 +16,8 @@ void register_kube(py::module_& m) {
   py::class_<bgc::bench::ChurnDriver>(m, "ChurnDriver")
       .def(py::init([](const std::string& server, const std::string& token, const std::string& prefix,
                        int concurrency, const std::string& gpu_key, const std::string& group,
-                       const std::string& ca_pem, const std::string& approve_url, bool http2) {
+                       const std::string& ca_pem, const std::string& approve_url, bool http2,
+                       bool server_filter) {
              bgc::bench::ChurnOptions o;
              o.server = server;
              o.admin_token = token;
@@ -27,11 +28,13 @@ void register_kube(py::module_& m) {
              o.group = group;
              o.approve_url = approve_url;
              o.http2 = http2;
+             o.server_filter = server_filter;
              return std::make_unique<bgc::bench::ChurnDriver>(o);
            }),
            py::arg("server"), py::arg("admin_token"), py::arg("name_prefix"), py::arg("concurrency") = 32,
            py::arg("gpu_quota_key") = "requests.amd.com/gpu", py::arg("group") = "gpu", py::arg("ca_pem") = "",
-           py::arg("approve_url") = "", py::arg("http2") = false)
+           py::arg("approve_url") = "", py::arg("http2") = false,
+           py::arg("server_filter") = false)
       .def("start", &bgc::bench::ChurnDriver::start)
       .def("step", [](bgc::bench::ChurnDriver& d, const std::vector<std::string>& names, double timeout) {
         bgc::json::Value v;

@@ -142,6 +142,33 @@ def test_label_and_field_selectors(c):
     assert [i["metadata"]["name"] for i in notgold["items"]] == ["s1"]
 
 
+def test_name_prefix_test_extension_filters_list_and_watch(c):
+    """kube-lite.test/name-prefix (the bench's per-rank driver filter) on LIST, on a watch's
+    history replay and on live events."""
+    sel = "kube-lite.test/name-prefix=pfa-"
+    rv = c.admin.list("namespaces")["metadata"]["resourceVersion"]
+    for n in ("pfa-1", "pfb-1", "pfa-2"):
+        ns(c, n)
+    names = [i["metadata"]["name"] for i in c.admin.list("namespaces", field_selector=sel)["items"]]
+    assert names == ["pfa-1", "pfa-2"]
+    events = []
+
+    def watch():  # starts at rv: the three creates are replayed from history, then live
+        with requests.get(c.server + f"/api/v1/namespaces?watch=1&resourceVersion={rv}&timeoutSeconds=3"
+                                     f"&fieldSelector={sel}", headers={"Authorization": "Bearer admin-token"},
+                          stream=True, timeout=10) as r:
+            for line in r.iter_lines():
+                if line:
+                    events.append(json.loads(line))
+
+    t = threading.Thread(target=watch)
+    t.start()
+    ns(c, "pfb-2")
+    ns(c, "pfa-3")
+    t.join(10)
+    assert [e["object"]["metadata"]["name"] for e in events if e["type"] == "ADDED"] == ["pfa-1", "pfa-2", "pfa-3"]
+
+
 def _watch_lines(c, path, rv, seconds):
     out = []
     with requests.get(c.server + f"{path}?watch=1&resourceVersion={rv}&timeoutSeconds={seconds}",
