@@ -32,6 +32,9 @@ def test_bench_two_ranks_gloo():
     assert d["config"]["concurrency_per_rank"] == 50 and d["config"]["concurrency_total"] == 100
     assert d["config"]["concurrency_scope"] == "total" and d["config"]["control_plane_cpus"] >= 1
     assert d["config"]["log_level"] == "info" and d["dtype"] == "none"
+    # per-rank drivers filter their child watches server-side; the RCCL/xGMI probe runs only
+    # on GPU ranks (gloo here)
+    assert d["config"]["driver_server_filter"] is True and "rccl_xgmi" not in d
     # per-component CPU cost of the timed region, split product vs test scaffolding
     cpu = d["cpu_ms_per_cr"]
     for k in ("controller", "admission", "synchronizer", "node_agent", "kube_lite", "load_driver", "product_total"):
