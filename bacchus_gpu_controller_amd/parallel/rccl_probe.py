@@ -30,25 +30,77 @@ def busbw_factor(world):
     return 2.0 * (world - 1) / world if world > 1 else 1.0
 
 
+def _bdf_key(bdf):
+    """domain:bus:device of a PCI address, lower-case (torch reports no function number)."""
+    b = (bdf or "").strip().lower()
+    if b.count(":") == 1:  # "bb:dd.f" without a domain
+        b = "0000:" + b
+    return b.rsplit(".", 1)[0]
+
+
+def device_bdf(local_device):
+    """PCI address of a torch (HIP) device, e.g. "0000:05:00.0"."""
+    import torch
+
+    p = torch.cuda.get_device_properties(local_device)
+    return f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+
+
+def match_gpu(gpus, bdf=None, local_rank=0, allocated=None):
+    """The amdsmi discovery entry of this rank's GPU.
+
+    HIP renumbers the visible devices from 0 inside a container (HIP_VISIBLE_DEVICES or
+    the device plugin's allocation), while amdsmi's ``hip_id`` is host-wide, so the match
+    is by PCI address: ``bdf`` is this rank's device (``device_bdf``).  ``allocated`` is
+    the device plugin's ``BGC_AMD_GPU_IDS`` (BDFs, or ``<bdf>-p<index>`` for compute
+    partitions that share one); it narrows the candidates and tells partitions apart.
+    ``hip_id == local_rank`` is the last resort, for hosts where neither is known."""
+    cands = list(gpus)
+    if allocated:
+        keys = {_bdf_key(a.split("-p")[0]) for a in allocated}
+        parts = {int(a.rsplit("-p", 1)[1]) for a in allocated if "-p" in a and a.rsplit("-p", 1)[1].isdigit()}
+        narrowed = [g for g in cands if _bdf_key(g.get("bdf")) in keys and (not parts or g.get("index") in parts)]
+        cands = narrowed or cands
+    if bdf:
+        same = [g for g in cands if _bdf_key(g.get("bdf")) == _bdf_key(bdf)]
+        if len(same) == 1:
+            return same[0]
+        if len(same) > 1:  # partitions of one GPU: the hip ordinal among them
+            cands = same
+    for g in cands:
+        if g.get("hip_id", g.get("index")) == local_rank:
+            return g
+    return cands[local_rank % len(cands)] if cands else None
+
+
+def _allocated_ids():
+    v = os.environ.get("BGC_AMD_GPU_IDS", "")
+    return [x for x in v.split(",") if x] or None
+
+
+def _rank_gpu(gpus, local_rank):
+    try:
+        bdf = device_bdf(local_rank)
+    except Exception:  # noqa: BLE001 - no torch device (CPU rank)
+        bdf = None
+    return match_gpu(gpus, bdf, local_rank, _allocated_ids()), bdf
+
+
 def local_hive_id(local_rank):
     try:
         from .. import native
 
         gpus = json.loads(native().gpu_backend("amdsmi", "").discover())
-        for g in gpus:
-            if g.get("hip_id", g["index"]) == local_rank:
-                return g["xgmi_hive_id"]
-        return gpus[local_rank % len(gpus)]["xgmi_hive_id"] if gpus else "unknown"
+        g, _ = _rank_gpu(gpus, local_rank)
+        return g["xgmi_hive_id"] if g else "unknown"
     except Exception as e:  # noqa: BLE001
         return f"unavailable:{type(e).__name__}"
 
 
 def _amdsmi_index(backend, local_rank):
     gpus = json.loads(backend.discover())
-    for g in gpus:
-        if g.get("hip_id", g["index"]) == local_rank:
-            return g["index"]
-    return local_rank % max(1, len(gpus))
+    g, _ = _rank_gpu(gpus, local_rank)
+    return g["index"] if g else local_rank % max(1, len(gpus))
 
 
 def xgmi_write_kb(backend, index):
@@ -101,9 +153,19 @@ def sweep(sizes_mb, iters=10, warmup=3, dtype="bf16"):
         else:
             dist.barrier()
 
-    hive = local_hive_id(local) if cuda else "cpu"
-    hives = [None] * world
-    dist.all_gather_object(hives, hive)
+    dev_index = torch.cuda.current_device() if cuda else local
+    ident = {"hive": "cpu", "bdf": None, "amdsmi_bdf": None}
+    if cuda:
+        try:
+            from .. import native
+
+            g, bdf = _rank_gpu(json.loads(native().gpu_backend("amdsmi", "").discover()), dev_index)
+            ident = {"hive": g["xgmi_hive_id"] if g else "unknown", "bdf": bdf, "amdsmi_bdf": g and g.get("bdf")}
+        except Exception as e:  # noqa: BLE001
+            ident["hive"] = f"unavailable:{type(e).__name__}"
+    idents = [None] * world
+    dist.all_gather_object(idents, ident)
+    hives = [i["hive"] for i in idents]
     single_hive = len(set(hives)) == 1
     # xGMI traffic check: the link counters of this rank's GPU before and after the sweep.
     # A ring all-reduce writes 2(n-1)/n of the buffer per rank and iteration, so a group
@@ -114,7 +176,7 @@ def sweep(sizes_mb, iters=10, warmup=3, dtype="bf16"):
             from .. import native
 
             smi = native().gpu_backend("amdsmi", "")
-            smi_idx = _amdsmi_index(smi, local)
+            smi_idx = _amdsmi_index(smi, dev_index)
             kb0 = xgmi_write_kb(smi, smi_idx)
         except Exception:  # noqa: BLE001
             smi = None
@@ -162,6 +224,7 @@ def sweep(sizes_mb, iters=10, warmup=3, dtype="bf16"):
     dist.all_gather_object(traffic, {"xgmi_written_mb": None if wrote is None else round(wrote / 2**20, 1),
                                      "expected_mb": round(expected_bytes / 2**20, 1)})
     out = {"world_size": world, "backend": backend, "dtype": dtype, "hives": hives, "single_hive": single_hive,
+           "devices": [{"bdf": i["bdf"], "amdsmi_bdf": i["amdsmi_bdf"]} for i in idents],
            "xgmi_traffic": traffic,
            # every rank's links carried at least half the ring's bytes (other tenants' traffic
            # only adds to the counters, so this can miss a fallback only on a shared box)

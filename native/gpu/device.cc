@@ -434,6 +434,11 @@ class MockBackend : public Backend {
     const Value& b = gpus[static_cast<size_t>(index)].get("telemetry").get("busy_processes");
     return b.is_int() ? static_cast<int>(b.as_int()) : 0;
   }
+  Value diag_script() override {
+    reload();
+    std::lock_guard<std::mutex> lk(mu_);
+    return fixture_.get("diag_script");
+  }
 
  private:
   Value fixture_;

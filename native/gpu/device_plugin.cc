@@ -536,7 +536,11 @@ void drm_nodes(const std::string& sysfs_root, const std::string& bdf, std::strin
 }  // namespace
 
 DevicePlugin::DevicePlugin(std::vector<GpuInfo> gpus, DevicePluginConfig cfg)
-    : gpus_(std::move(gpus)), cfg_(std::move(cfg)), healthy_(gpus_.size(), true) {
+    : gpus_(std::move(gpus)),
+      cfg_(std::move(cfg)),
+      healthy_(gpus_.size(), true),
+      fenced_(gpus_.size(), false),
+      alloc_counts_(gpus_.size(), 0) {
   // ID = PCI BDF; compute partitions of one GPU can share a BDF, so duplicates get the
   // logical device index appended.
   std::map<std::string, int> seen;
@@ -559,7 +563,7 @@ std::vector<dp::Device> DevicePlugin::devices() const {
   for (size_t i = 0; i < gpus_.size(); ++i) {
     dp::Device d;
     d.id = ids_[i];
-    d.healthy = healthy_[i];
+    d.healthy = healthy_[i] && !fenced_[i];
     if (gpus_[i].numa_node >= 0) d.numa_nodes.push_back(gpus_[i].numa_node);
     out.push_back(std::move(d));
   }
@@ -584,6 +588,33 @@ void DevicePlugin::set_health(const std::vector<bool>& healthy) {
   cv_.notify_all();
 }
 
+void DevicePlugin::set_fenced(const std::vector<size_t>& which, bool fenced) {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    bool changed = false;
+    for (size_t i : which) {
+      if (i >= fenced_.size() || fenced_[i] == fenced) continue;
+      fenced_[i] = fenced;
+      changed = true;
+      LOG_INFO("device_plugin") << cfg_.resource_name << " " << ids_[i]
+                                << (fenced ? " fenced for diagnostics" : " released from diagnostics");
+    }
+    if (!changed) return;
+    ++version_;
+  }
+  cv_.notify_all();
+}
+
+std::vector<bool> DevicePlugin::fenced() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return fenced_;
+}
+
+std::vector<uint64_t> DevicePlugin::allocation_counts() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return alloc_counts_;
+}
+
 std::pair<std::string, std::string> DevicePlugin::drm_node_names(size_t gi) const {
   const GpuInfo& g = gpus_[gi];
   std::string card, render;
@@ -606,7 +637,18 @@ std::pair<std::string, std::string> DevicePlugin::drm_node_names(size_t gi) cons
   return {card, render};
 }
 
-dp::ContainerAllocation DevicePlugin::allocate(const std::vector<std::string>& req_ids) const {
+dp::ContainerAllocation DevicePlugin::allocate(const std::vector<std::string>& req_ids) {
+  std::lock_guard<std::mutex> lk(mu_);
+  std::vector<size_t> idx;
+  for (const auto& id : req_ids) {
+    auto it = std::find(ids_.begin(), ids_.end(), id);
+    if (it == ids_.end()) throw std::invalid_argument("unknown " + cfg_.resource_name + " device id " + id);
+    idx.push_back(static_cast<size_t>(it - ids_.begin()));
+    if (fenced_[idx.back()]) {
+      refused_fenced_.fetch_add(1);
+      throw std::invalid_argument(cfg_.resource_name + " device " + id + " is under node diagnostics");
+    }
+  }
   dp::ContainerAllocation c;
   if (!cfg_.cdi) c.devices.push_back({"/dev/kfd", join_path(cfg_.dev_root, "kfd"), "rw"});
   std::set<uint64_t> hives;
@@ -633,6 +675,7 @@ dp::ContainerAllocation DevicePlugin::allocate(const std::vector<std::string>& r
   c.envs["BGC_AMD_GPU_IDS"] = id_list;
   c.envs["BGC_AMD_GPU_XGMI_HIVES"] = hive_list;
   c.envs["BGC_AMD_GPU_SINGLE_XGMI_HIVE"] = hives.size() <= 1 ? "true" : "false";
+  for (size_t i : idx) alloc_counts_[i]++;
   return c;
 }
 
@@ -705,8 +748,17 @@ void DevicePlugin::start_server() {
   srv->add("/v1beta1.DevicePlugin/ListAndWatch", [this](grpc::ServerCall& call) { return list_and_watch(call); });
   srv->add("/v1beta1.DevicePlugin/GetPreferredAllocation", [this](grpc::ServerCall& call) {
     std::vector<std::vector<std::string>> resp;
-    for (const auto& q : dp::decode_preferred_request(call.request()))
-      resp.push_back(preferred_allocation(gpus_, ids_, q.available, q.must_include, q.size));
+    const std::vector<bool> fenced = this->fenced();
+    for (auto q : dp::decode_preferred_request(call.request())) {
+      // a fenced GPU is not offered (the kubelet's list may predate the fence)
+      std::vector<std::string> avail;
+      for (const auto& id : q.available) {
+        auto it = std::find(ids_.begin(), ids_.end(), id);
+        if (it == ids_.end() || !fenced[static_cast<size_t>(it - ids_.begin())]) avail.push_back(id);
+      }
+      if (static_cast<int32_t>(avail.size()) < q.size) avail = q.available;  // cannot satisfy otherwise
+      resp.push_back(preferred_allocation(gpus_, ids_, avail, q.must_include, q.size));
+    }
     call.send_message(dp::encode_preferred_response(resp));
     return grpc::Status::Ok();
   });
@@ -816,12 +868,20 @@ json::Value DevicePlugin::describe() const {
   for (const auto& d : devices()) {
     devs.push_back(json::Value::object({{"id", d.id}, {"health", d.healthy ? dp::kHealthy : dp::kUnhealthy}}));
   }
+  json::Value fenced = json::Value::array();
+  {
+    const std::vector<bool> f = this->fenced();
+    for (size_t i = 0; i < f.size(); ++i)
+      if (f[i]) fenced.push_back(ids_[i]);
+  }
   return json::Value::object({{"resource", cfg_.resource_name},
                               {"socket", socket_path()},
                               {"registrations", static_cast<unsigned long long>(registrations_.load())},
                               {"server_restarts", static_cast<unsigned long long>(server_restarts_.load())},
                               {"allocations", static_cast<unsigned long long>(allocations_.load())},
-                              {"devices", devs}});
+                              {"refused_fenced", static_cast<unsigned long long>(refused_fenced_.load())},
+                              {"devices", devs},
+                              {"fenced", fenced}});
 }
 
 }  // namespace bgc::gpu

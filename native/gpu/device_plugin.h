@@ -151,7 +151,17 @@ class DevicePlugin {
   void stop();
   // Per-GPU health (same order as the gpus passed in); re-sends ListAndWatch on change.
   void set_health(const std::vector<bool>& healthy);
-  dp::ContainerAllocation allocate(const std::vector<std::string>& ids) const;  // throws on unknown ids
+  // Diagnostics fence: a fenced GPU is listed Unhealthy, left out of preferred
+  // allocations and refused by Allocate until it is unfenced, so the kubelet cannot hand
+  // a tenant a GPU that is under a burn-in.  Re-sends ListAndWatch on change.
+  void set_fenced(const std::vector<size_t>& which, bool fenced);
+  std::vector<bool> fenced() const;
+  // Per GPU: Allocate calls that handed it out (the fence re-checks these for an
+  // allocation that raced the fence).
+  std::vector<uint64_t> allocation_counts() const;
+  // Throws std::invalid_argument on unknown or fenced ids.  Holds the plugin lock
+  // throughout, so an allocation either completes before a fence or is refused by it.
+  dp::ContainerAllocation allocate(const std::vector<std::string>& ids);
   // Writes the CDI spec (cdi mode); returns its path.
   std::string write_cdi_spec() const;
   std::vector<dp::Device> devices() const;
@@ -176,6 +186,8 @@ class DevicePlugin {
   mutable std::mutex mu_;
   std::condition_variable cv_;
   std::vector<bool> healthy_;
+  std::vector<bool> fenced_;
+  std::vector<uint64_t> alloc_counts_;
   uint64_t version_ = 1;
   std::unique_ptr<grpc::Server> server_;
   std::mutex server_mu_;
@@ -186,6 +198,7 @@ class DevicePlugin {
   std::atomic<uint64_t> registrations_{0};
   std::atomic<uint64_t> server_restarts_{0};
   std::atomic<uint64_t> allocations_{0};
+  std::atomic<uint64_t> refused_fenced_{0};
 };
 
 }  // namespace bgc::gpu

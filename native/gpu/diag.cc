@@ -49,9 +49,15 @@ Diag::Diag(const std::string& path) : path_(path) {
   burn_ = reinterpret_cast<int (*)(int, int, int, uint32_t, bgc_burn_result*)>(dlsym(lib_, "bgc_diag_burn"));
   pcie_ = reinterpret_cast<int (*)(int, uint64_t, int, uint32_t, bgc_pcie_result*)>(dlsym(lib_, "bgc_diag_pcie"));
   soak_ = reinterpret_cast<int (*)(int, int, int, int, int, uint32_t, bgc_soak_result*)>(dlsym(lib_, "bgc_diag_gemm_soak"));
+  tiled_ = reinterpret_cast<int (*)(int, int, int, int, const uint16_t*, const uint16_t*, float*)>(
+      dlsym(lib_, "bgc_diag_gemm_tiled"));
+  walk_ = reinterpret_cast<int (*)(int, double, uint64_t, int, uint32_t, bgc_hbm_walk_result*)>(
+      dlsym(lib_, "bgc_diag_hbm_walk"));
+  bdf_ = reinterpret_cast<int (*)(int, char*, size_t)>(dlsym(lib_, "bgc_diag_device_bdf"));
   last_error_ = reinterpret_cast<const char* (*)()>(dlsym(lib_, "bgc_diag_last_error"));
   auto abi = reinterpret_cast<int (*)()>(dlsym(lib_, "bgc_diag_abi_version"));
-  if (!device_count_ || !hbm_ || !mfma_ || !arch_ || !gemm_ || !burn_ || !pcie_ || !soak_ || !last_error_ || !abi ||
+  if (!device_count_ || !hbm_ || !mfma_ || !arch_ || !gemm_ || !burn_ || !pcie_ || !soak_ || !tiled_ ||
+      !walk_ || !bdf_ || !last_error_ || !abi ||
       abi() != BGC_DIAG_ABI_VERSION) {
     throw std::runtime_error(path + " is not a compatible bgc diag library");
   }
@@ -171,6 +177,43 @@ void Diag::gemm(int device, int m, int n, int k, const uint16_t* a, const uint16
   if (gemm_(device, m, n, k, a, b, c) != 0) throw std::runtime_error(std::string("gemm diag: ") + last_error_());
 }
 
+void Diag::gemm_tiled(int device, int m, int n, int k, const uint16_t* a, const uint16_t* bt, float* c) {
+  if (tiled_(device, m, n, k, a, bt, c) != 0) throw std::runtime_error(std::string("tiled gemm: ") + last_error_());
+}
+
+json::Value Diag::hbm_walk(int device, double fraction, uint64_t chunk_bytes, int budget_ms, uint32_t seed) {
+  bgc_hbm_walk_result r{};
+  if (walk_(device, fraction, chunk_bytes, budget_ms, seed, &r) != 0) {
+    throw std::runtime_error(std::string("hbm walk: ") + last_error_());
+  }
+  char addr[32], flips[32];
+  std::snprintf(addr, sizeof(addr), "0x%llx", static_cast<unsigned long long>(r.first_bad_addr));
+  std::snprintf(flips, sizeof(flips), "0x%016llx", static_cast<unsigned long long>(r.first_bad_xor));
+  const double cov = r.free_bytes ? static_cast<double>(r.bytes_covered) / static_cast<double>(r.free_bytes) : 0.0;
+  return json::Value::object({{"device", device},
+                              {"free_bytes", static_cast<unsigned long long>(r.free_bytes)},
+                              {"total_bytes", static_cast<unsigned long long>(r.total_bytes)},
+                              {"target_bytes", static_cast<unsigned long long>(r.target_bytes)},
+                              {"bytes_covered", static_cast<unsigned long long>(r.bytes_covered)},
+                              {"coverage_of_free", cov},
+                              {"chunks", r.chunks},
+                              {"passes", r.passes},
+                              {"mismatches", static_cast<unsigned long long>(r.mismatches)},
+                              {"first_bad_addr", r.mismatches ? json::Value(std::string(addr)) : json::Value()},
+                              {"first_bad_bits", r.mismatches ? json::Value(std::string(flips)) : json::Value()},
+                              {"write_gbps", r.write_gbps},
+                              {"read_gbps", r.read_gbps},
+                              {"elapsed_ms", r.elapsed_ms},
+                              {"budget_hit", r.budget_hit != 0},
+                              {"passed", r.mismatches == 0 && r.passes == 2}});
+}
+
+std::string Diag::device_bdf(int device) {
+  char buf[64] = {0};
+  if (bdf_(device, buf, sizeof(buf)) != 0) throw std::runtime_error(std::string("device bdf: ") + last_error_());
+  return buf;
+}
+
 namespace {
 
 uint32_t mix(uint32_t x) {
@@ -255,6 +298,13 @@ DiagFloors DiagFloors::mi355x_defaults() {
   // GEMM soak (LDS-tiled bf16 MFMA, 256x256 tiles): 1253-1288 TF/s at 8192^3 and
   // 1164-1193 at 4096^3 on MI355X (profiles/gemm_soak_r2/)
   f.min_soak_tflops = 950;
+  // HBM walk: 0.9 of free VRAM is requested; 0.8 leaves room for allocator granularity
+  f.min_hbm_walk_coverage = 0.8;
+  // node-level burn: one GPU 15 % behind the node's fastest under the shared load is a
+  // cooling or power-delivery outlier (healthy MI355X burns agree within ~1 %,
+  // profiles/diag_burn_r2.json); the node power limit is site-specific (0 = off)
+  f.min_node_burn_balance = 0.85;
+  f.max_node_power_w = 0;
   return f;
 }
 
@@ -277,6 +327,22 @@ json::Value judge_diag(const json::Value& result, const DiagFloors& fl) {
     floor_check(hbm, "read_gbps", fl.min_read_gbps, "HBM read GB/s");
     floor_check(hbm, "copy_gbps", fl.min_copy_gbps, "HBM copy GB/s");
     floor_check(hbm, "write_gbps", fl.min_write_gbps, "HBM write GB/s");
+  }
+  const json::Value& hw = result.get("hbm_walk");
+  if (hw.is_object()) {
+    if (num(hw, "mismatches") > 0) {
+      std::string msg = "HBM walk mismatches: " + std::to_string(static_cast<uint64_t>(num(hw, "mismatches")));
+      if (hw.get("first_bad_addr").is_string()) {
+        msg += " (first at " + hw.get_string("first_bad_addr") + ", bits " + hw.get_string("first_bad_bits") + ")";
+      }
+      failures.push_back(msg);
+    }
+    if (fl.min_hbm_walk_coverage > 0 && num(hw, "coverage_of_free") < fl.min_hbm_walk_coverage) {
+      char buf[160];
+      std::snprintf(buf, sizeof(buf), "HBM walk covered %.2f of free VRAM (floor %.2f)", num(hw, "coverage_of_free"),
+                    fl.min_hbm_walk_coverage);
+      failures.push_back(std::string(buf));
+    }
   }
   const json::Value& mf = result.get("mfma");
   if (mf.is_object()) {

@@ -34,6 +34,14 @@ struct DiagFloors {
   double min_pcie_speed_fraction = 0;
   // GEMM soak (`soak` section): every checksum must match; rate floor on the mean.
   double min_soak_tflops = 0;
+  // HBM walk (`hbm_walk` section): any mismatch fails; the walk must cover at least this
+  // share of the free VRAM (a failed allocation on an idle, fenced GPU means something
+  // else holds its memory).
+  double min_hbm_walk_coverage = 0;
+  // Node-level burn (diag_runner.h): under the shared load every GPU must reach this
+  // fraction of the node's fastest GPU, and the summed draw must stay under the limit.
+  double min_node_burn_balance = 0;
+  double max_node_power_w = 0;
   static DiagFloors mi355x_defaults();
 };
 
@@ -61,6 +69,12 @@ class Diag {
   json::Value gemm_soak(int device, int m, int n, int k, int launches, uint32_t seed);
   // Raw GEMM: A/B as bf16 bit patterns, C fp32 (row-major).
   void gemm(int device, int m, int n, int k, const uint16_t* a, const uint16_t* b, float* c);
+  // The soak's LDS-tiled GEMM on caller operands (Bt = B transposed, [n][k]).
+  void gemm_tiled(int device, int m, int n, int k, const uint16_t* a, const uint16_t* bt, float* c);
+  // Address-pattern walk of `fraction` of the free VRAM (see bgc_diag_hbm_walk).
+  json::Value hbm_walk(int device, double fraction, uint64_t chunk_bytes, int budget_ms, uint32_t seed);
+  // PCI bus id of a HIP device, lower-case ("0000:05:00.0").
+  std::string device_bdf(int device);
   const std::string& path() const { return path_; }
 
  private:
@@ -75,6 +89,9 @@ class Diag {
   int (*burn_)(int, int, int, uint32_t, bgc_burn_result*) = nullptr;
   int (*pcie_)(int, uint64_t, int, uint32_t, bgc_pcie_result*) = nullptr;
   int (*soak_)(int, int, int, int, int, uint32_t, bgc_soak_result*) = nullptr;
+  int (*tiled_)(int, int, int, int, const uint16_t*, const uint16_t*, float*) = nullptr;
+  int (*walk_)(int, double, uint64_t, int, uint32_t, bgc_hbm_walk_result*) = nullptr;
+  int (*bdf_)(int, char*, size_t) = nullptr;
   const char* (*last_error_)() = nullptr;
 };
 

@@ -1,0 +1,353 @@
+#include "gpu/diag_runner.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cctype>
+#include <chrono>
+#include <climits>
+#include <condition_variable>
+#include <cstdio>
+#include <map>
+#include <mutex>
+#include <thread>
+
+#include "gpu/telemetry.h"
+
+namespace bgc::gpu {
+
+using json::Value;
+
+namespace {
+
+// Per-GPU sampler statistics over a burn.
+struct BurnStats {
+  double max_hot = 0, max_mem = 0, power_sum = 0, power_max = 0, clk_sum = 0;
+  uint32_t clk_min = UINT32_MAX;
+  int n = 0;
+  Telemetry first, last;
+  void add(const Telemetry& t) {
+    if (!t.ok) return;
+    if (n == 0) first = t;
+    last = t;
+    max_hot = std::max(max_hot, t.temp_hotspot_c);
+    max_mem = std::max(max_mem, t.temp_mem_c);
+    power_sum += t.power_w;
+    power_max = std::max(power_max, t.power_w);
+    clk_sum += t.gfxclk_mhz;
+    clk_min = std::min(clk_min, t.gfxclk_mhz);
+    ++n;
+  }
+  void fill(Value& out) const {
+    out["samples"] = n;
+    out["max_hotspot_c"] = max_hot;
+    out["max_mem_c"] = max_mem;
+    out["power_mean_w"] = n ? power_sum / n : 0.0;
+    out["power_max_w"] = power_max;
+    out["gfxclk_mean_mhz"] = n ? clk_sum / n : 0.0;
+    out["gfxclk_min_mhz"] = n ? static_cast<double>(clk_min) : 0.0;
+    Telemetry span = last;
+    TelemetryPoller::violation_deltas(first, span);
+    out["thermal_violation_pct"] = span.violation_thermal_pct < 0 ? Value() : Value(span.violation_thermal_pct);
+    out["ppt_violation_pct"] = span.violation_ppt_pct < 0 ? Value() : Value(span.violation_ppt_pct);
+  }
+};
+
+// Sleeps in short slices so a sampler notices `done` quickly.
+void nap(const std::atomic<bool>& done, int ms) {
+  for (int i = 0; i < ms / 10 && !done.load(); ++i) std::this_thread::sleep_for(std::chrono::milliseconds(10));
+}
+
+class HipDiagEngine : public DiagEngine {
+ public:
+  std::string name() const override { return "hip"; }
+  Value checks(Backend& backend, const GpuInfo& g, int dev, const DiagPlan& plan, uint32_t seed) override {
+    Diag& d = Diag::instance();
+    Value r = Value::object();
+    r["hbm"] = d.hbm(dev, plan.hbm_bytes, 2, seed);
+    if (plan.hbm_walk_fraction > 0) {
+      r["hbm_walk"] = d.hbm_walk(dev, plan.hbm_walk_fraction, plan.hbm_walk_chunk_bytes, plan.hbm_walk_budget_ms, seed);
+    }
+    r["mfma"] = d.mfma(dev, 16, 2048, seed);
+    r["gemm"] = d.gemm_check(dev, 64, 64, 512, seed);
+    if (plan.pcie_bytes > 0) {
+      // One GPU at a time: eight concurrent pinned-copy streams share the host's memory
+      // bandwidth and root complexes, so concurrent rates would measure the host, not
+      // the GPU's link.  ~50 ms per GPU.
+      static std::mutex pcie_mu;
+      std::lock_guard<std::mutex> lk(pcie_mu);
+      r["pcie"] = pcie_check(backend, g, dev, plan.pcie_bytes, seed);
+    }
+    if (plan.soak_launches > 0) {
+      r["soak"] = d.gemm_soak(dev, plan.soak_size, plan.soak_size, plan.soak_size, plan.soak_launches, seed);
+    }
+    return r;
+  }
+  Value burn(int dev, int duration_ms, uint32_t seed) override { return Diag::instance().burn(dev, duration_ms, 32, seed); }
+};
+
+// Re-reads the script from the backend on every call, so a test can change a running
+// agent's diagnostics by rewriting the mock fixture.
+class ScriptedDiagEngine : public DiagEngine {
+ public:
+  explicit ScriptedDiagEngine(Backend& backend) : backend_(backend) {}
+  std::string name() const override { return "scripted"; }
+  Value checks(Backend&, const GpuInfo& g, int dev, const DiagPlan& plan, uint32_t) override {
+    const Value script = backend_.diag_script();
+    const Value& e = script.get("gpus").get(std::to_string(g.index));
+    std::this_thread::sleep_for(std::chrono::milliseconds(static_cast<int64_t>(num(e, "checks_ms", num(script, "checks_ms", 100)))));
+    Value r = Value::object();
+    r["hbm"] = Value::object({{"device", dev}, {"bytes", static_cast<unsigned long long>(plan.hbm_bytes)}, {"read_gbps", 6400.0},
+                              {"write_gbps", 5200.0}, {"copy_gbps", 5400.0}, {"mismatches", 0}, {"passed", true}});
+    if (plan.hbm_walk_fraction > 0) {
+      const uint64_t free_b = g.vram_total_mb * (1ULL << 20);
+      const uint64_t covered = static_cast<uint64_t>(static_cast<double>(free_b) * plan.hbm_walk_fraction);
+      const uint64_t bad = static_cast<uint64_t>(num(e, "walk_mismatches", 0));
+      r["hbm_walk"] = Value::object({{"device", dev}, {"free_bytes", static_cast<unsigned long long>(free_b)},
+                                     {"bytes_covered", static_cast<unsigned long long>(covered)},
+                                     {"coverage_of_free", plan.hbm_walk_fraction}, {"passes", 2},
+                                     {"mismatches", static_cast<unsigned long long>(bad)}, {"passed", bad == 0}});
+    }
+    r["mfma"] = Value::object({{"device", dev}, {"tflops", 2000.0}, {"xcc_balance", 0.96}, {"xccs_seen", 8},
+                               {"mismatches", 0}, {"bad_cus", 0}, {"throughput_ok", true}, {"passed", true}});
+    r["gemm"] = Value::object({{"passed", true}});
+    if (plan.soak_launches > 0) {
+      r["soak"] = Value::object({{"tflops_mean", 1300.0}, {"row_mismatches", 0}, {"col_mismatches", 0}, {"passed", true}});
+    }
+    if (e.get("fail").is_string()) r["error"] = e.get_string("fail");
+    return r;
+  }
+  Value burn(int dev, int duration_ms, uint32_t) override {
+    std::this_thread::sleep_for(std::chrono::milliseconds(duration_ms));
+    const Value script = backend_.diag_script();
+    const double tf = num(script.get("gpus").get(std::to_string(dev)), "burn_tflops", num(script, "burn_tflops", 2400));
+    return Value::object({{"launches", std::max(1, duration_ms / 10)}, {"elapsed_ms", static_cast<double>(duration_ms)},
+                          {"tflops_mean", tf}, {"tflops_min", tf}, {"tflops_first", tf}, {"tflops_last", tf},
+                          {"tflops_max", tf}, {"sustain", 1.0}, {"mismatches", 0}});
+  }
+
+ private:
+  static double num(const Value& v, const char* k, double d) { return v.get(k).is_number() ? v.get(k).as_double() : d; }
+  Backend& backend_;
+};
+
+}  // namespace
+
+std::unique_ptr<DiagEngine> make_hip_diag_engine() { return std::make_unique<HipDiagEngine>(); }
+
+std::unique_ptr<DiagEngine> make_scripted_diag_engine(Backend& backend) {
+  return std::make_unique<ScriptedDiagEngine>(backend);
+}
+
+Value pcie_check(Backend& backend, const GpuInfo& g, int hip_device, uint64_t bytes, uint32_t seed) {
+  const Telemetry before = backend.sample(g.index, SampleLevel::Slow);
+  std::atomic<bool> done{false};
+  int width = -1, speed = -1;  // highest seen while copying
+  std::thread sampler([&] {
+    while (!done.load()) {
+      Telemetry t = backend.sample(g.index, SampleLevel::Slow);
+      if (t.ok) {
+        width = std::max(width, t.pcie_width);
+        speed = std::max(speed, t.pcie_speed_mts);
+      }
+      for (int i = 0; i < 5 && !done.load(); ++i) std::this_thread::sleep_for(std::chrono::milliseconds(10));
+    }
+  });
+  Value out;
+  try {
+    out = Diag::instance().pcie(hip_device, bytes, 5, seed);
+  } catch (...) {
+    done = true;
+    sampler.join();
+    throw;
+  }
+  done = true;
+  sampler.join();
+  const Telemetry after = backend.sample(g.index, SampleLevel::Slow);
+  if (width > 0) out["link_width"] = width;
+  if (speed > 0) out["link_speed_mts"] = speed;
+  if (g.pcie_max_width > 0) out["max_width"] = g.pcie_max_width;
+  if (g.pcie_max_speed_mts > 0) out["max_speed_mts"] = g.pcie_max_speed_mts;
+  if (g.pcie_max_gen > 0) out["max_gen"] = g.pcie_max_gen;
+  auto delta = [&](int64_t a, int64_t b) { return a >= 0 && b >= a ? Value(static_cast<long long>(b - a)) : Value(); };
+  out["replays"] = delta(before.pcie_replays, after.pcie_replays);
+  out["recoveries"] = delta(before.pcie_recoveries, after.pcie_recoveries);
+  return out;
+}
+
+Value burn_in(Backend& backend, int index, int hip_device, int duration_ms, uint32_t seed, DiagEngine* engine) {
+  std::unique_ptr<DiagEngine> own;
+  if (!engine) {
+    own = make_hip_diag_engine();
+    engine = own.get();
+  }
+  std::atomic<bool> done{false};
+  BurnStats st;
+  std::thread sampler([&] {
+    while (!done.load()) {
+      st.add(backend.sample(index, SampleLevel::Fast));
+      nap(done, 100);
+    }
+  });
+  Value out;
+  try {
+    out = engine->burn(hip_device, duration_ms, seed);
+  } catch (...) {
+    done = true;
+    sampler.join();
+    throw;
+  }
+  done = true;
+  sampler.join();
+  st.fill(out);
+  return out;
+}
+
+NodeBurnResult node_burn(Backend& backend, DiagEngine& engine, const std::vector<GpuInfo>& gpus,
+                         const std::vector<int>& hip_devs, const std::vector<size_t>& which, int duration_ms,
+                         uint32_t seed) {
+  const size_t n = which.size();
+  NodeBurnResult res;
+  res.per_gpu.assign(n, Value());
+  std::vector<BurnStats> st(n);
+  std::vector<std::string> err(n);
+  std::mutex mu;
+  std::condition_variable cv;
+  size_t ready = 0;
+  bool go = false;
+  std::atomic<bool> done{false};
+  double sum_max = 0, sum_acc = 0, peak_hot = 0;
+  int sweeps = 0;
+  // One sampler for the whole node: each sweep reads every GPU under load, so the summed
+  // power is the node's draw at one moment rather than a sum of separate peaks.
+  std::thread sampler([&] {
+    while (!done.load()) {
+      double sum = 0;
+      int ok = 0;
+      for (size_t k = 0; k < n; ++k) {
+        const Telemetry t = backend.sample(gpus[which[k]].index, SampleLevel::Fast);
+        if (!t.ok) continue;
+        st[k].add(t);
+        sum += t.power_w;
+        peak_hot = std::max(peak_hot, t.temp_hotspot_c);
+        ++ok;
+      }
+      if (ok) {
+        sum_max = std::max(sum_max, sum);
+        sum_acc += sum;
+        ++sweeps;
+      }
+      nap(done, 100);
+    }
+  });
+  std::vector<std::thread> workers;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (size_t k = 0; k < n; ++k) {
+    workers.emplace_back([&, k] {
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        if (++ready == n) {
+          go = true;
+          cv.notify_all();
+        }
+        cv.wait(lk, [&] { return go; });
+      }
+      try {
+        res.per_gpu[k] = engine.burn(hip_devs[which[k]], duration_ms, seed + static_cast<uint32_t>(which[k]));
+      } catch (const std::exception& e) {
+        err[k] = e.what();
+      }
+    });
+  }
+  for (auto& w : workers) w.join();
+  const double wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  done = true;
+  sampler.join();
+  Value per = Value::array();
+  for (size_t k = 0; k < n; ++k) {
+    if (!err[k].empty()) {
+      res.per_gpu[k] = Value::object({{"error", err[k]}});
+      continue;
+    }
+    st[k].fill(res.per_gpu[k]);
+  }
+  res.node = Value::object({{"gpus", static_cast<unsigned long long>(n)},
+                            {"duration_ms", duration_ms},
+                            {"wall_ms", wall_ms},
+                            {"sweeps", sweeps},
+                            {"power_sum_max_w", sum_max},
+                            {"power_sum_mean_w", sweeps ? sum_acc / sweeps : 0.0},
+                            {"peak_hotspot_c", peak_hot}});
+  return res;
+}
+
+std::vector<std::vector<std::string>> judge_node_burn(NodeBurnResult& r, const DiagFloors& fl) {
+  const size_t n = r.per_gpu.size();
+  std::vector<std::vector<std::string>> per(n);
+  std::vector<std::string> node_fail;
+  double best = 0, worst = 0;
+  bool any = false;
+  for (const auto& b : r.per_gpu) {
+    if (!b.get("tflops_mean").is_number()) continue;
+    const double tf = b.get("tflops_mean").as_double();
+    best = any ? std::max(best, tf) : tf;
+    worst = any ? std::min(worst, tf) : tf;
+    any = true;
+  }
+  const double balance = any && best > 0 ? worst / best : 0.0;
+  r.node["tflops_best"] = best;
+  r.node["tflops_worst"] = worst;
+  r.node["balance"] = balance;
+  char buf[200];
+  if (fl.min_node_burn_balance > 0 && any && n > 1) {
+    for (size_t k = 0; k < n; ++k) {
+      const Value& b = r.per_gpu[k];
+      if (!b.get("tflops_mean").is_number()) continue;
+      const double frac = best > 0 ? b.get("tflops_mean").as_double() / best : 0.0;
+      if (frac < fl.min_node_burn_balance) {
+        std::snprintf(buf, sizeof(buf), "node burn-in: %.0f TF/s is %.2f of the node's fastest GPU under shared load (floor %.2f)",
+                      b.get("tflops_mean").as_double(), frac, fl.min_node_burn_balance);
+        per[k].push_back(buf);
+      }
+    }
+  }
+  const double psum = r.node.get("power_sum_max_w").is_number() ? r.node.get("power_sum_max_w").as_double() : 0.0;
+  if (fl.max_node_power_w > 0 && psum > fl.max_node_power_w) {
+    std::snprintf(buf, sizeof(buf), "node drew %.0f W with %zu GPUs under burn (limit %.0f W)", psum, n, fl.max_node_power_w);
+    node_fail.push_back(buf);
+  }
+  const double hot = r.node.get("peak_hotspot_c").is_number() ? r.node.get("peak_hotspot_c").as_double() : 0.0;
+  if (fl.max_burn_hotspot_c > 0 && hot > fl.max_burn_hotspot_c) {
+    std::snprintf(buf, sizeof(buf), "node peak hotspot %.0f C under the node-level burn (limit %.0f C)", hot,
+                  fl.max_burn_hotspot_c);
+    node_fail.push_back(buf);
+  }
+  Value nf = Value::array();
+  for (const auto& f : node_fail) {
+    nf.push_back(f);
+    for (auto& p : per) p.push_back(f);  // a node-wide limit: no GPU of the node is trusted
+  }
+  r.node["failures"] = nf;
+  r.node["passed"] = node_fail.empty();
+  return per;
+}
+
+std::vector<int> hip_devices_for(const std::vector<GpuInfo>& gpus, const std::vector<std::string>& hip_bdfs) {
+  auto lower = [](std::string s) {
+    for (auto& c : s) c = static_cast<char>(std::tolower(static_cast<unsigned char>(c)));
+    return s;
+  };
+  std::map<std::string, int> bdf_count, hip_by_bdf;
+  for (const auto& g : gpus) bdf_count[lower(g.bdf)]++;
+  for (size_t d = 0; d < hip_bdfs.size(); ++d) hip_by_bdf.emplace(lower(hip_bdfs[d]), static_cast<int>(d));
+  std::vector<int> out;
+  for (const auto& g : gpus) {
+    const std::string b = lower(g.bdf);
+    auto it = hip_by_bdf.find(b);
+    // partitions share a BDF: only amdsmi's own enumeration can tell them apart
+    if (!b.empty() && bdf_count[b] == 1 && it != hip_by_bdf.end()) out.push_back(it->second);
+    else out.push_back(g.hip_id >= 0 ? g.hip_id : g.index);
+  }
+  return out;
+}
+
+}  // namespace bgc::gpu

@@ -15,7 +15,7 @@
 extern "C" {
 #endif
 
-#define BGC_DIAG_ABI_VERSION 5
+#define BGC_DIAG_ABI_VERSION 6
 #define BGC_DIAG_MAX_CU_KEYS 2048
 
 typedef struct {
@@ -94,6 +94,38 @@ typedef struct {
 // GEMM run `launches` times back to back on operands in {-1, 0, 1}, checked by exact
 // row/column checksums (ABFT).  m, n multiples of 128; k a multiple of 64.
 int bgc_diag_gemm_soak(int device, int m, int n, int k, int launches, uint32_t seed, bgc_soak_result* out);
+// The soak's GEMM kernel on caller operands: C[m,n] (fp32) = A[m,k] * Bt[n,k]^T, A/Bt bf16
+// bit patterns, row-major (so both are K-contiguous, as the kernel reads them); same shape
+// rules as bgc_diag_gemm_soak.  Lets a test compare the LDS-tiled kernel on random data
+// with an independent fp32 product.
+int bgc_diag_gemm_tiled(int device, int m, int n, int k, const uint16_t* a_bf16, const uint16_t* bt_bf16, float* c);
+
+typedef struct {
+  uint64_t free_bytes;        // hipMemGetInfo before the walk
+  uint64_t total_bytes;
+  uint64_t target_bytes;      // fraction * free_bytes
+  uint64_t bytes_covered;     // allocated and written + verified with both patterns
+  int chunks;                 // device allocations the walk spans
+  int passes;                 // completed passes (2 = address pattern, then its inverse)
+  uint64_t mismatches;        // 64-bit words that read back wrong
+  uint64_t first_bad_addr;    // device address of the lowest failing word (0 = none)
+  uint64_t first_bad_xor;     // expected ^ found at that word: the flipped bits
+  double write_gbps;          // fill rate over the covered bytes
+  double read_gbps;           // verify rate
+  double elapsed_ms;          // wall time of the walk (allocation included)
+  int budget_hit;             // 1 when the time budget ended the walk before both passes
+} bgc_hbm_walk_result;
+
+// Pattern walk of (nearly) all free HBM: allocates `fraction` of the free VRAM in chunks of
+// `chunk_bytes`, writes every 64-bit word with its own device address XOR a seed-derived
+// key, verifies all of it only after every chunk was written (a write that lands on the
+// wrong row or stack shows up as a wrong address elsewhere), then repeats with the inverse
+// so every cell is checked holding both 0 and 1.  Stops early after `budget_ms`.
+int bgc_diag_hbm_walk(int device, double fraction, uint64_t chunk_bytes, int budget_ms, uint32_t seed,
+                      bgc_hbm_walk_result* out);
+// PCI bus id of a HIP device ("0000:05:00.0", lower-case hex) — the key the node agent and
+// the RCCL probe use to match a HIP device (renumbered inside a container) to amdsmi.
+int bgc_diag_device_bdf(int device, char* buf, size_t len);
 // Device name / gfx arch string, e.g. "gfx950".
 int bgc_diag_device_arch(int device, char* buf, size_t len);
 const char* bgc_diag_last_error(void);

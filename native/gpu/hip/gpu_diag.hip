@@ -5,8 +5,10 @@
 //  * HBM phases are pure streams: 16 B per lane (global_load/store_dwordx4), 256-thread
 //    blocks, 8 blocks per CU (2048 WGs >> 256 CUs) each owning one contiguous slab, 4
 //    independent 16 B accesses in flight per lane so each CU keeps ~128 KiB outstanding;
-//    nontemporal hints since every byte is touched exactly once per pass.  Buffers default to 2 GiB each, far
-//    past the 256 MiB Infinity Cache, so the numbers are HBM numbers.
+//    nontemporal hints since every byte is touched exactly once per pass.  The bandwidth
+//    phases run on two buffers of `bytes` each (the node agent uses 1 GiB, 4x the 256 MiB
+//    Infinity Cache, so the rates are HBM rates); coverage of the whole HBM is the job of
+//    the separate address-pattern walk over ~all free VRAM (walk_fill / walk_check).
 //  * The MFMA test runs one v_mfma_f32_16x16x32_bf16 tile per wave per round with
 //    operands in {-1,0,1} generated from a hash in registers (no memory traffic), so
 //    every product sum is an exact fp32 integer and is checked element-wise against a
@@ -17,6 +19,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cctype>
+#include <chrono>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
@@ -124,6 +128,68 @@ __global__ __launch_bounds__(kBlock) void hbm_check(const u32x4* __restrict__ bu
   if (local_bad) {
     atomicAdd(bad, local_bad);
     atomicMin(first_bad, local_first);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// HBM walk (bgc_diag_hbm_walk): every 64-bit word holds its own device address ^ key.
+// A stuck bit, a weak cell or a write that decodes to the wrong row/bank/stack shows up
+// at verify time as a word whose content is not its address.  The inverse pass is the
+// same kernel with ~key, so every bit is checked at 0 and at 1.
+
+__device__ __forceinline__ u32x4 walk_value(const u32x4* p, uint64_t key) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  const uint64_t w0 = a ^ key, w1 = (a + 8) ^ key;
+  u32x4 v;
+  v.x = static_cast<uint32_t>(w0);
+  v.y = static_cast<uint32_t>(w0 >> 32);
+  v.z = static_cast<uint32_t>(w1);
+  v.w = static_cast<uint32_t>(w1 >> 32);
+  return v;
+}
+
+__global__ __launch_bounds__(kBlock) void walk_fill(u32x4* __restrict__ buf, uint64_t n16, uint64_t key) {
+  uint64_t beg, end;
+  block_range(n16, beg, end);
+  for (uint64_t b = beg + threadIdx.x; b < end; b += kBlock * kUnroll) {
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const uint64_t i = b + u * kBlock;
+      if (i < end) __builtin_nontemporal_store(walk_value(&buf[i], key), &buf[i]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void walk_check(const u32x4* __restrict__ buf, uint64_t n16, uint64_t key,
+                                                     unsigned long long* __restrict__ bad,
+                                                     unsigned long long* __restrict__ first_bad_addr) {
+  uint64_t beg, end;
+  block_range(n16, beg, end);
+  unsigned long long local_bad = 0, local_first = ~0ULL;
+  for (uint64_t b = beg + threadIdx.x; b < end; b += kBlock * kUnroll) {
+    u32x4 v[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const uint64_t i = b + u * kBlock;
+      if (i < end) v[u] = __builtin_nontemporal_load(&buf[i]);
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const uint64_t i = b + u * kBlock;
+      if (i < end) {
+        const u32x4 e = walk_value(&buf[i], key);
+        const bool b0 = v[u].x != e.x || v[u].y != e.y, b1 = v[u].z != e.z || v[u].w != e.w;
+        if (b0 || b1) {
+          local_bad += static_cast<unsigned long long>(b0) + static_cast<unsigned long long>(b1);
+          const uint64_t a = reinterpret_cast<uint64_t>(&buf[i]) + (b0 ? 0 : 8);
+          local_first = std::min<unsigned long long>(local_first, a);
+        }
+      }
+    }
+  }
+  if (local_bad) {
+    atomicAdd(bad, local_bad);
+    atomicMin(first_bad_addr, local_first);
   }
 }
 
@@ -471,6 +537,43 @@ struct Streams {
   }
 };
 
+struct Chunks {  // the HBM walk's allocations, freed on every exit path
+  std::vector<std::pair<void*, uint64_t>> v;
+  ~Chunks() {
+    for (auto& c : v) (void)hipFree(c.first);
+  }
+};
+
+// 256x256 tiles (8 waves, 128 KiB LDS, 1 block/CU) when the shape divides; else 128x128
+bool soak_big_tile(int m, int n) {
+  const char* tile_env = std::getenv("BGC_SOAK_TILE");
+  return (m % 256 == 0 && n % 256 == 0) && !(tile_env && std::string(tile_env) == "128");
+}
+
+void launch_soak_gemm(bool big, const void* a, const void* bt, void* c, int m, int n, int k, hipStream_t s) {
+  if (big) {
+    hipLaunchKernelGGL((gemm_soak<256, 256, 2, 4>), dim3((m / 256) * (n / 256)), dim3(512), 0, s,
+                       static_cast<const __bf16*>(a), static_cast<const __bf16*>(bt), static_cast<float*>(c), m, n, k);
+  } else {
+    hipLaunchKernelGGL((gemm_soak<128, 128, 2, 2>), dim3((m / 128) * (n / 128)), dim3(256), 0, s,
+                       static_cast<const __bf16*>(a), static_cast<const __bf16*>(bt), static_cast<float*>(c), m, n, k);
+  }
+}
+
+bool soak_shape_ok(int m, int n, int k) {
+  return m >= 128 && n >= 128 && k >= kSoakBK && m % 128 == 0 && n % 128 == 0 && k % kSoakBK == 0 && m <= 32768 &&
+         n <= 32768 && k <= 32768;
+}
+
+uint64_t mix64(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return x;
+}
+
 }  // namespace
 
 extern "C" {
@@ -812,14 +915,11 @@ int bgc_diag_pcie(int device, uint64_t bytes, int iters, uint32_t seed, bgc_pcie
 }
 
 int bgc_diag_gemm_soak(int device, int m, int n, int k, int launches, uint32_t seed, bgc_soak_result* out) {
-  if (!out || launches <= 0 || m < 128 || n < 128 || k < kSoakBK || m % 128 || n % 128 || k % kSoakBK || m > 32768 ||
-      n > 32768 || k > 32768) {
+  if (!out || launches <= 0 || !soak_shape_ok(m, n, k)) {
     g_last_error = "invalid arguments: m, n multiples of 128 and k of 64 (each <= 32768)";
     return 1;
   }
-  // 256x256 tiles (8 waves, 128 KiB LDS, 1 block/CU) when the shape divides; else 128x128
-  const char* tile_env = std::getenv("BGC_SOAK_TILE");
-  const bool big = (m % 256 == 0 && n % 256 == 0) && !(tile_env && std::string(tile_env) == "128");
+  const bool big = soak_big_tile(m, n);
   std::memset(out, 0, sizeof(*out));
   HIP_TRY(hipSetDevice(device));
   const size_t na = static_cast<size_t>(m) * k, nb = static_cast<size_t>(n) * k, nc = static_cast<size_t>(m) * n;
@@ -866,7 +966,6 @@ int bgc_diag_gemm_soak(int device, int m, int n, int k, int launches, uint32_t s
     for (int j = 0; j < n; ++j) *col_bad += cg[static_cast<size_t>(j)] != cr[static_cast<size_t>(j)];
     return 0;
   };
-  const int grid = big ? (m / 256) * (n / 256) : (m / 128) * (n / 128);
   Events ev;
   HIP_TRY(hipEventCreate(&ev.a));
   HIP_TRY(hipEventCreate(&ev.b));
@@ -876,13 +975,7 @@ int bgc_diag_gemm_soak(int device, int m, int n, int k, int launches, uint32_t s
     // poison C before the last checked launch, so its checksums cover that launch's writes
     if (it > 0 && it == launches - 1) HIP_TRY(hipMemsetAsync(c.p, 0xFF, nc * 4, nullptr));
     HIP_TRY(hipEventRecord(ev.a, nullptr));
-    if (big) {
-      hipLaunchKernelGGL((gemm_soak<256, 256, 2, 4>), dim3(grid), dim3(512), 0, nullptr, static_cast<const __bf16*>(a.p),
-                         static_cast<const __bf16*>(bt.p), static_cast<float*>(c.p), m, n, k);
-    } else {
-      hipLaunchKernelGGL((gemm_soak<128, 128, 2, 2>), dim3(grid), dim3(256), 0, nullptr, static_cast<const __bf16*>(a.p),
-                         static_cast<const __bf16*>(bt.p), static_cast<float*>(c.p), m, n, k);
-    }
+    launch_soak_gemm(big, a.p, bt.p, c.p, m, n, k, nullptr);
     HIP_TRY(hipEventRecord(ev.b, nullptr));
     HIP_TRY(hipEventSynchronize(ev.b));
     HIP_TRY(hipGetLastError());
@@ -900,6 +993,133 @@ int bgc_diag_gemm_soak(int device, int m, int n, int k, int launches, uint32_t s
   out->elapsed_ms = total;
   out->tflops_best = flop / (best * 1e-3) / 1e12;
   out->tflops_mean = flop * launches / (total * 1e-3) / 1e12;
+  return 0;
+}
+
+int bgc_diag_gemm_tiled(int device, int m, int n, int k, const uint16_t* a_bf16, const uint16_t* bt_bf16, float* c) {
+  if (!a_bf16 || !bt_bf16 || !c || !soak_shape_ok(m, n, k)) {
+    g_last_error = "invalid arguments: m, n multiples of 128 and k of 64 (each <= 32768)";
+    return 1;
+  }
+  HIP_TRY(hipSetDevice(device));
+  const size_t na = static_cast<size_t>(m) * k, nb = static_cast<size_t>(n) * k, nc = static_cast<size_t>(m) * n;
+  DeviceBuffer da, db, dc;
+  HIP_TRY(hipMalloc(&da.p, na * 2));
+  HIP_TRY(hipMalloc(&db.p, nb * 2));
+  HIP_TRY(hipMalloc(&dc.p, nc * 4));
+  HIP_TRY(hipMemcpy(da.p, a_bf16, na * 2, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(db.p, bt_bf16, nb * 2, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemset(dc.p, 0xFF, nc * 4));  // NaN: an element the kernel never writes cannot pass
+  launch_soak_gemm(soak_big_tile(m, n), da.p, db.p, dc.p, m, n, k, nullptr);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpy(c, dc.p, nc * 4, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int bgc_diag_hbm_walk(int device, double fraction, uint64_t chunk_bytes, int budget_ms, uint32_t seed,
+                      bgc_hbm_walk_result* out) {
+  constexpr uint64_t kMinChunk = 64ULL << 20;
+  if (!out || !(fraction > 0.0 && fraction <= 0.99) || chunk_bytes < kMinChunk || budget_ms <= 0) {
+    g_last_error = "invalid arguments: 0 < fraction <= 0.99, chunk_bytes >= 64 MiB, budget_ms > 0";
+    return 1;
+  }
+  std::memset(out, 0, sizeof(*out));
+  const auto t0 = std::chrono::steady_clock::now();
+  auto elapsed_ms = [&] {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  };
+  HIP_TRY(hipSetDevice(device));
+  DeviceBuffer counters;  // before the walk takes the memory
+  HIP_TRY(hipMalloc(&counters.p, 2 * sizeof(unsigned long long)));
+  size_t free_b = 0, total_b = 0;
+  HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+  out->free_bytes = free_b;
+  out->total_bytes = total_b;
+  const uint64_t align = 2ULL << 20;
+  const uint64_t target = static_cast<uint64_t>(fraction * static_cast<double>(free_b)) & ~(align - 1);
+  out->target_bytes = target;
+  Chunks chunks;
+  uint64_t got = 0, cb = chunk_bytes & ~(align - 1);
+  while (got < target) {
+    const uint64_t want = std::min(cb, target - got);
+    void* p = nullptr;
+    if (hipMalloc(&p, want) != hipSuccess || !p) {
+      (void)hipGetLastError();  // clear the sticky allocation error
+      if (cb <= kMinChunk) break;
+      cb = std::max(kMinChunk, (cb / 2) & ~(align - 1));
+      continue;
+    }
+    chunks.v.emplace_back(p, want);
+    got += want;
+  }
+  if (chunks.v.empty()) {
+    g_last_error = "hbm walk: no device memory could be allocated";
+    return 1;
+  }
+  out->chunks = static_cast<int>(chunks.v.size());
+  auto* bad = static_cast<unsigned long long*>(counters.p);
+  const int grid = cu_count(device) * 8;
+  Events ev;
+  HIP_TRY(hipEventCreate(&ev.a));
+  HIP_TRY(hipEventCreate(&ev.b));
+  const uint64_t key0 = mix64(0x9e3779b97f4a7c15ULL ^ seed);
+  double fill_ms = 0, check_ms = 0;
+  for (int pass = 0; pass < 2; ++pass) {
+    if (pass > 0 && elapsed_ms() > budget_ms) {
+      out->budget_hit = 1;
+      break;
+    }
+    const uint64_t key = pass == 0 ? key0 : ~key0;
+    const unsigned long long init[2] = {0ULL, ~0ULL};
+    HIP_TRY(hipMemcpy(bad, init, sizeof(init), hipMemcpyHostToDevice));
+    float ms = 0.f;
+    HIP_TRY(hipEventRecord(ev.a, nullptr));
+    for (const auto& c : chunks.v) {
+      hipLaunchKernelGGL(walk_fill, dim3(grid), dim3(kBlock), 0, nullptr, static_cast<u32x4*>(c.first), c.second / 16, key);
+    }
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(ev.b, nullptr));
+    HIP_TRY(hipEventSynchronize(ev.b));
+    HIP_TRY(hipEventElapsedTime(&ms, ev.a, ev.b));
+    fill_ms += ms;
+    HIP_TRY(hipEventRecord(ev.a, nullptr));
+    for (const auto& c : chunks.v) {
+      hipLaunchKernelGGL(walk_check, dim3(grid), dim3(kBlock), 0, nullptr, static_cast<const u32x4*>(c.first),
+                         c.second / 16, key, bad, bad + 1);
+    }
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(ev.b, nullptr));
+    HIP_TRY(hipEventSynchronize(ev.b));
+    HIP_TRY(hipEventElapsedTime(&ms, ev.a, ev.b));
+    check_ms += ms;
+    unsigned long long res[2];
+    HIP_TRY(hipMemcpy(res, bad, sizeof(res), hipMemcpyDeviceToHost));
+    if (res[0] && !out->mismatches) {  // the first failing pass names the first bad word
+      out->first_bad_addr = res[1];
+      uint64_t found = 0;
+      HIP_TRY(hipMemcpy(&found, reinterpret_cast<void*>(static_cast<uintptr_t>(res[1])), 8, hipMemcpyDeviceToHost));
+      out->first_bad_xor = found ^ (static_cast<uint64_t>(res[1]) ^ key);
+    }
+    out->mismatches += res[0];
+    out->passes = pass + 1;
+  }
+  out->bytes_covered = got;
+  const double moved = static_cast<double>(got) * out->passes;
+  out->write_gbps = fill_ms > 0 ? moved / (fill_ms * 1e-3) / 1e9 : 0.0;
+  out->read_gbps = check_ms > 0 ? moved / (check_ms * 1e-3) / 1e9 : 0.0;
+  out->elapsed_ms = elapsed_ms();
+  return 0;
+}
+
+int bgc_diag_device_bdf(int device, char* buf, size_t len) {
+  if (!buf || len < 13) {
+    g_last_error = "invalid arguments";
+    return 1;
+  }
+  char tmp[64] = {0};
+  HIP_TRY(hipDeviceGetPCIBusId(tmp, static_cast<int>(sizeof(tmp)), device));
+  for (char* p = tmp; *p; ++p) *p = static_cast<char>(std::tolower(static_cast<unsigned char>(*p)));
+  std::snprintf(buf, len, "%s", tmp);
   return 0;
 }
 

@@ -34,6 +34,13 @@ NodeAgentConfig NodeAgentConfig::from_env(const EnvConfig& env) {
   c.run_diag = env.boolean_or("run_diag", false);
   c.diag_hbm_bytes = env.u64_or("diag_hbm_bytes", 1ULL << 30);
   c.diag_interval_secs = env.u64_or("diag_interval_secs", 0);
+  c.diag_hbm_walk_fraction = env.f64_or("diag_hbm_walk_fraction", c.diag_hbm_walk_fraction);
+  c.diag_hbm_walk_chunk_mb = env.u64_or("diag_hbm_walk_chunk_mb", c.diag_hbm_walk_chunk_mb);
+  c.diag_hbm_walk_budget_ms = env.u64_or("diag_hbm_walk_budget_ms", c.diag_hbm_walk_budget_ms);
+  c.diag_fence_settle_ms = env.u64_or("diag_fence_settle_ms", c.diag_fence_settle_ms);
+  c.diag_floors.min_hbm_walk_coverage = env.f64_or("diag_min_hbm_walk_coverage", c.diag_floors.min_hbm_walk_coverage);
+  c.diag_floors.min_node_burn_balance = env.f64_or("diag_min_node_burn_balance", c.diag_floors.min_node_burn_balance);
+  c.diag_floors.max_node_power_w = env.f64_or("diag_max_node_power_w", c.diag_floors.max_node_power_w);
   c.diag_burn_ms = env.u64_or("diag_burn_ms", 0);
   c.diag_pcie_bytes = env.u64_or("diag_pcie_bytes", c.diag_pcie_bytes);
   c.diag_soak_size = static_cast<int>(env.u64_or("diag_soak_size", static_cast<uint64_t>(c.diag_soak_size)));
@@ -249,8 +256,18 @@ void NodeAgent::emit_health_events() {
 
 NodeAgent::~NodeAgent() { stop(); }
 
+static double ms_since(std::chrono::steady_clock::time_point t) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+}
+
+void NodeAgent::mark_advertised() {
+  double zero = 0;
+  first_advertise_ms_.compare_exchange_strong(zero, ms_since(t_created_));
+}
+
 void NodeAgent::init() {
   gpus_ = backend_->discover();
+  discover_ms_ = ms_since(t_created_);
   if (cfg_.max_gpus > 0 && static_cast<int>(gpus_.size()) > cfg_.max_gpus) gpus_.resize(static_cast<size_t>(cfg_.max_gpus));
   if (gpus_.empty()) throw std::runtime_error("no GPUs discovered via " + backend_->name());
   const std::string res = advertised_resource(cfg_, gpus_);
@@ -262,7 +279,11 @@ void NodeAgent::init() {
   LOG_INFO("node_agent") << "discovered " << gpus_.size() << " GPU(s) via " << backend_->name() << ": "
                          << gpus_.front().market_name << " " << gpus_.front().gfx_target << " "
                          << gpus_.front().vram_total_mb << " MB";
-  if (cfg_.run_diag) run_diagnostics(true);
+  if (cfg_.run_diag) {
+    const auto t0 = std::chrono::steady_clock::now();
+    run_diagnostics(true);
+    startup_diag_ms_ = ms_since(t0);
+  }
   std::vector<int> idx;
   std::vector<uint64_t> page_limits;
   for (const auto& g : gpus_) {
@@ -316,108 +337,34 @@ DiagOutcome NodeAgent::diag_outcome() const {
   return diag_;
 }
 
-Value NodeAgent::diagnose(const GpuInfo& g) const {
-  const int dev = g.hip_id >= 0 ? g.hip_id : g.index;
-  const uint32_t seed = 0x5eed + static_cast<uint32_t>(dev);
-  Value r = Value::object({{"index", g.index}});
-  try {
-    Diag& d = Diag::instance();
-    r["hbm"] = d.hbm(dev, cfg_.diag_hbm_bytes, 2, seed);
-    r["mfma"] = d.mfma(dev, 16, 2048, seed);
-    r["gemm"] = d.gemm_check(dev, 64, 64, 512, seed);
-    if (cfg_.diag_pcie_bytes > 0) r["pcie"] = pcie_check(*backend_, g, dev, cfg_.diag_pcie_bytes, seed);
-    if (cfg_.diag_soak_launches > 0) {
-      r["soak"] = d.gemm_soak(dev, cfg_.diag_soak_size, cfg_.diag_soak_size, cfg_.diag_soak_size, cfg_.diag_soak_launches, seed);
-    }
-    if (cfg_.diag_burn_ms > 0) r["burn"] = burn_in(*backend_, g.index, dev, static_cast<int>(cfg_.diag_burn_ms), seed);
-  } catch (const std::exception& e) {
-    r["error"] = std::string(e.what());
-  }
-  return judge_diag(r, cfg_.diag_floors);
+DiagPlan NodeAgent::diag_plan() const {
+  DiagPlan p;
+  p.hbm_bytes = cfg_.diag_hbm_bytes;
+  p.hbm_walk_fraction = cfg_.diag_hbm_walk_fraction;
+  p.hbm_walk_chunk_bytes = cfg_.diag_hbm_walk_chunk_mb << 20;
+  p.hbm_walk_budget_ms = static_cast<int>(cfg_.diag_hbm_walk_budget_ms);
+  p.pcie_bytes = cfg_.diag_pcie_bytes;
+  p.soak_size = cfg_.diag_soak_size;
+  p.soak_launches = cfg_.diag_soak_launches;
+  p.burn_ms = static_cast<int>(cfg_.diag_burn_ms);
+  return p;
 }
 
-Value burn_in(Backend& backend, int index, int hip_device, int duration_ms, uint32_t seed) {
-  // amdsmi sampler on a side thread for the duration of the burn
-  std::atomic<bool> done{false};
-  double max_hot = 0, max_mem = 0, power_sum = 0, power_max = 0, clk_sum = 0;
-  uint32_t clk_min = UINT32_MAX;
-  int n = 0;
-  Telemetry first, last;
-  std::thread sampler([&] {
-    while (!done.load()) {
-      Telemetry t = backend.sample(index, SampleLevel::Fast);
-      if (t.ok) {
-        if (n == 0) first = t;
-        last = t;
-        max_hot = std::max(max_hot, t.temp_hotspot_c);
-        max_mem = std::max(max_mem, t.temp_mem_c);
-        power_sum += t.power_w;
-        power_max = std::max(power_max, t.power_w);
-        clk_sum += t.gfxclk_mhz;
-        clk_min = std::min(clk_min, t.gfxclk_mhz);
-        ++n;
-      }
-      for (int i = 0; i < 10 && !done.load(); ++i) std::this_thread::sleep_for(std::chrono::milliseconds(10));
+void NodeAgent::setup_diag() {
+  if (engine_) return;
+  const Value script = backend_->diag_script();
+  engine_ = script.is_object() ? make_scripted_diag_engine(*backend_) : make_hip_diag_engine();
+  std::vector<std::string> bdfs;
+  if (engine_->name() == "hip") {
+    try {
+      Diag& d = Diag::instance();
+      for (int i = 0, n = d.device_count(); i < n; ++i) bdfs.push_back(d.device_bdf(i));
+    } catch (const std::exception& e) {
+      LOG_WARN("node_agent") << "HIP device BDFs unavailable (" << e.what() << "); using amdsmi hip ids";
     }
-  });
-  Value out;
-  try {
-    out = Diag::instance().burn(hip_device, duration_ms, 32, seed);
-  } catch (...) {
-    done = true;
-    sampler.join();
-    throw;
   }
-  done = true;
-  sampler.join();
-  out["samples"] = n;
-  out["max_hotspot_c"] = max_hot;
-  out["max_mem_c"] = max_mem;
-  out["power_mean_w"] = n ? power_sum / n : 0.0;
-  out["power_max_w"] = power_max;
-  out["gfxclk_mean_mhz"] = n ? clk_sum / n : 0.0;
-  out["gfxclk_min_mhz"] = n ? static_cast<double>(clk_min) : 0.0;
-  Telemetry span = last;
-  TelemetryPoller::violation_deltas(first, span);
-  out["thermal_violation_pct"] = span.violation_thermal_pct < 0 ? Value() : Value(span.violation_thermal_pct);
-  out["ppt_violation_pct"] = span.violation_ppt_pct < 0 ? Value() : Value(span.violation_ppt_pct);
-  return out;
-}
-
-Value pcie_check(Backend& backend, const GpuInfo& g, int hip_device, uint64_t bytes, uint32_t seed) {
-  const Telemetry before = backend.sample(g.index, SampleLevel::Slow);
-  std::atomic<bool> done{false};
-  int width = -1, speed = -1;  // highest seen while copying
-  std::thread sampler([&] {
-    while (!done.load()) {
-      Telemetry t = backend.sample(g.index, SampleLevel::Slow);
-      if (t.ok) {
-        width = std::max(width, t.pcie_width);
-        speed = std::max(speed, t.pcie_speed_mts);
-      }
-      for (int i = 0; i < 5 && !done.load(); ++i) std::this_thread::sleep_for(std::chrono::milliseconds(10));
-    }
-  });
-  Value out;
-  try {
-    out = Diag::instance().pcie(hip_device, bytes, 5, seed);
-  } catch (...) {
-    done = true;
-    sampler.join();
-    throw;
-  }
-  done = true;
-  sampler.join();
-  const Telemetry after = backend.sample(g.index, SampleLevel::Slow);
-  if (width > 0) out["link_width"] = width;
-  if (speed > 0) out["link_speed_mts"] = speed;
-  if (g.pcie_max_width > 0) out["max_width"] = g.pcie_max_width;
-  if (g.pcie_max_speed_mts > 0) out["max_speed_mts"] = g.pcie_max_speed_mts;
-  if (g.pcie_max_gen > 0) out["max_gen"] = g.pcie_max_gen;
-  auto delta = [&](int64_t a, int64_t b) { return a >= 0 && b >= a ? Value(static_cast<long long>(b - a)) : Value(); };
-  out["replays"] = delta(before.pcie_replays, after.pcie_replays);
-  out["recoveries"] = delta(before.pcie_recoveries, after.pcie_recoveries);
-  return out;
+  hip_devs_ = hip_devices_for(gpus_, bdfs);
+  LOG_INFO("node_agent") << "diagnostics engine " << engine_->name() << ", " << bdfs.size() << " HIP devices named by BDF";
 }
 
 std::vector<bool> NodeAgent::in_use() const {
@@ -440,59 +387,147 @@ std::vector<bool> NodeAgent::in_use() const {
   return out;
 }
 
+void NodeAgent::record_diag_gauges(size_t i, const Value& r) {
+  auto get = [&](const char* sect, const char* k) {
+    const Value& v = r.get(sect).get(k);
+    return v.is_number() ? v.as_double() : 0.0;
+  };
+  // per-GPU results as gauges (Prometheus), so fleet dashboards see a slow GPU before it fails a floor
+  auto& reg = metrics::Registry::global();
+  const metrics::Labels gl{{"gpu", std::to_string(gpus_[i].index)}};
+  struct G {
+    const char *name, *help, *sect, *key;
+  };
+  static const G kGauges[] = {
+      {"amd_gpu_diag_hbm_read_gbps", "Diagnostics: HBM read GB/s", "hbm", "read_gbps"},
+      {"amd_gpu_diag_hbm_write_gbps", "Diagnostics: HBM write GB/s", "hbm", "write_gbps"},
+      {"amd_gpu_diag_hbm_copy_gbps", "Diagnostics: HBM copy GB/s", "hbm", "copy_gbps"},
+      {"amd_gpu_diag_hbm_walk_covered_bytes", "Diagnostics: HBM bytes pattern-walked", "hbm_walk", "bytes_covered"},
+      {"amd_gpu_diag_hbm_walk_mismatches", "Diagnostics: HBM walk words read back wrong", "hbm_walk", "mismatches"},
+      {"amd_gpu_diag_mfma_tflops", "Diagnostics: bf16 MFMA TFLOP/s (register operands)", "mfma", "tflops"},
+      {"amd_gpu_diag_xcc_balance", "Diagnostics: fastest/slowest XCC wave time", "mfma", "xcc_balance"},
+      {"amd_gpu_diag_soak_tflops", "Diagnostics: LDS-tiled MFMA GEMM soak TFLOP/s", "soak", "tflops_mean"},
+      {"amd_gpu_diag_pcie_h2d_gbps", "Diagnostics: PCIe host-to-device GB/s", "pcie", "h2d_gbps"},
+      {"amd_gpu_diag_pcie_d2h_gbps", "Diagnostics: PCIe device-to-host GB/s", "pcie", "d2h_gbps"},
+      {"amd_gpu_diag_burn_tflops", "Diagnostics: burn-in mean MFMA TFLOP/s", "burn", "tflops_mean"},
+      {"amd_gpu_diag_burn_max_hotspot_celsius", "Diagnostics: burn-in peak hotspot temperature", "burn", "max_hotspot_c"},
+  };
+  for (const auto& g : kGauges) {
+    if (r.get(g.sect).get(g.key).is_number()) reg.gauge(g.name, g.help, gl).set(get(g.sect, g.key));
+  }
+  reg.gauge("amd_gpu_diag_passed", "1 when the last diagnostics pass of the GPU succeeded", gl)
+      .set(r.get("passed").as_bool() ? 1 : 0);
+  if (r.get("passed").as_bool()) {
+    LOG_INFO("node_agent") << "diag gpu " << gpus_[i].index << ": passed in " << r.get("checks_ms").dump()
+                           << " ms, read " << get("hbm", "read_gbps") << " GB/s, walk "
+                           << get("hbm_walk", "bytes_covered") / 1e9 << " GB, mfma " << get("mfma", "tflops")
+                           << " TFLOP/s, xcc balance " << get("mfma", "xcc_balance") << ", soak "
+                           << get("soak", "tflops_mean") << " TFLOP/s, pcie " << get("pcie", "h2d_gbps") << "/"
+                           << get("pcie", "d2h_gbps") << " GB/s, burn " << get("burn", "tflops_mean") << " TFLOP/s";
+  } else {
+    LOG_WARN("node_agent") << "diag gpu " << gpus_[i].index << ": FAILED " << r.get("failures").dump();
+    node_event("Warning", "GPUDiagnosticsFailed",
+               "gpu " + std::to_string(gpus_[i].index) + " (" + gpus_[i].bdf + "): " + r.get("failures").dump());
+  }
+}
+
 bool NodeAgent::run_diagnostics(bool force) {
-  const std::vector<bool> busy = force ? std::vector<bool>(gpus_.size(), false) : in_use();
+  setup_diag();
+  using clock = std::chrono::steady_clock;
+  const auto t_pass = clock::now();
+  auto since = [&](clock::time_point t) { return std::chrono::duration<double, std::milli>(t - t_pass).count(); };
   DiagOutcome prev = diag_outcome();
   std::vector<Value> results(gpus_.size());
   uint64_t skipped = 0;
+  auto keep_previous = [&](size_t i, const char* why) {
+    ++skipped;
+    if (i < prev.per_gpu.items().size()) results[i] = prev.per_gpu.items()[i];
+    LOG_INFO("node_agent") << "diag gpu " << gpus_[i].index << ": skipped (" << why << ")";
+  };
+  // Allocation counters first: an Allocate that lands between the in_use() snapshot and
+  // the fence shows up as a changed counter.
+  const std::vector<uint64_t> allocs0 = plugin_ ? plugin_->allocation_counts() : std::vector<uint64_t>{};
+  const std::vector<bool> busy = force ? std::vector<bool>(gpus_.size(), false) : in_use();
+  std::vector<size_t> todo;
   for (size_t i = 0; i < gpus_.size(); ++i) {
-    if (busy[i]) {
-      ++skipped;
-      if (i < prev.per_gpu.items().size()) results[i] = prev.per_gpu.items()[i];
-      LOG_INFO("node_agent") << "diag gpu " << gpus_[i].index << ": skipped (in use)";
-      continue;
-    }
-    results[i] = diagnose(gpus_[i]);
-    const Value& r = results[i];
-    auto get = [&](const char* sect, const char* k) {
-      const Value& v = r.get(sect).get(k);
-      return v.is_number() ? v.as_double() : 0.0;
-    };
-    // per-GPU results as gauges (Prometheus), so fleet dashboards see a slow GPU before it fails a floor
-    auto& reg = metrics::Registry::global();
-    const metrics::Labels gl{{"gpu", std::to_string(gpus_[i].index)}};
-    struct G {
-      const char *name, *help, *sect, *key;
-    };
-    static const G kGauges[] = {
-        {"amd_gpu_diag_hbm_read_gbps", "Diagnostics: HBM read GB/s", "hbm", "read_gbps"},
-        {"amd_gpu_diag_hbm_write_gbps", "Diagnostics: HBM write GB/s", "hbm", "write_gbps"},
-        {"amd_gpu_diag_hbm_copy_gbps", "Diagnostics: HBM copy GB/s", "hbm", "copy_gbps"},
-        {"amd_gpu_diag_mfma_tflops", "Diagnostics: bf16 MFMA TFLOP/s (register operands)", "mfma", "tflops"},
-        {"amd_gpu_diag_xcc_balance", "Diagnostics: fastest/slowest XCC wave time", "mfma", "xcc_balance"},
-        {"amd_gpu_diag_soak_tflops", "Diagnostics: LDS-tiled MFMA GEMM soak TFLOP/s", "soak", "tflops_mean"},
-        {"amd_gpu_diag_pcie_h2d_gbps", "Diagnostics: PCIe host-to-device GB/s", "pcie", "h2d_gbps"},
-        {"amd_gpu_diag_pcie_d2h_gbps", "Diagnostics: PCIe device-to-host GB/s", "pcie", "d2h_gbps"},
-        {"amd_gpu_diag_burn_tflops", "Diagnostics: burn-in mean MFMA TFLOP/s", "burn", "tflops_mean"},
-        {"amd_gpu_diag_burn_max_hotspot_celsius", "Diagnostics: burn-in peak hotspot temperature", "burn", "max_hotspot_c"},
-    };
-    for (const auto& g : kGauges) {
-      if (r.get(g.sect).get(g.key).is_number()) reg.gauge(g.name, g.help, gl).set(get(g.sect, g.key));
-    }
-    reg.gauge("amd_gpu_diag_passed", "1 when the last diagnostics pass of the GPU succeeded", gl)
-        .set(r.get("passed").as_bool() ? 1 : 0);
-    if (r.get("passed").as_bool()) {
-      LOG_INFO("node_agent") << "diag gpu " << gpus_[i].index << ": passed, read " << get("hbm", "read_gbps")
-                             << " GB/s, copy " << get("hbm", "copy_gbps") << " GB/s, mfma " << get("mfma", "tflops")
-                             << " TFLOP/s, xcc balance " << get("mfma", "xcc_balance") << ", soak "
-                             << get("soak", "tflops_mean") << " TFLOP/s, pcie " << get("pcie", "h2d_gbps") << "/"
-                             << get("pcie", "d2h_gbps") << " GB/s";
-    } else {
-      LOG_WARN("node_agent") << "diag gpu " << gpus_[i].index << ": FAILED " << r.get("failures").dump();
-      node_event("Warning", "GPUDiagnosticsFailed",
-                 "gpu " + std::to_string(gpus_[i].index) + " (" + gpus_[i].bdf + "): " + r.get("failures").dump());
-    }
+    if (busy[i]) keep_previous(i, "in use");
+    else todo.push_back(i);
   }
+  // Fence: withdraw the candidates from the kubelet (Unhealthy in ListAndWatch, refused
+  // by Allocate), give an in-flight admission time to land, then re-check. Only GPUs
+  // still free are diagnosed; the rest are released untouched.
+  const bool fence = !force && plugin_ && !todo.empty();
+  if (fence) {
+    plugin_->set_fenced(todo, true);
+    if (stop_.wait_for(std::chrono::milliseconds(cfg_.diag_fence_settle_ms))) {
+      plugin_->set_fenced(todo, false);
+      return false;
+    }
+    const std::vector<bool> busy2 = in_use();
+    const std::vector<uint64_t> allocs1 = plugin_->allocation_counts();
+    std::vector<size_t> still, released;
+    for (size_t i : todo) {
+      const bool raced = busy2[i] || (i < allocs0.size() && i < allocs1.size() && allocs1[i] != allocs0[i]);
+      (raced ? released : still).push_back(i);
+    }
+    for (size_t i : released) keep_previous(i, "allocated while being fenced");
+    if (!released.empty()) plugin_->set_fenced(released, false);
+    fence_races_ += released.size();
+    todo = still;
+  }
+  const DiagPlan plan = diag_plan();
+  // Phase 1: every GPU's checks at once, one thread per GPU.
+  {
+    std::vector<std::thread> threads;
+    for (size_t i : todo) {
+      threads.emplace_back([&, i] {
+        const int dev = hip_devs_[i];
+        const auto t0 = clock::now();
+        Value r;
+        try {
+          r = engine_->checks(*backend_, gpus_[i], dev, plan, 0x5eed + static_cast<uint32_t>(dev));
+        } catch (const std::exception& e) {
+          r = Value::object({{"error", std::string(e.what())}});
+        }
+        r["index"] = gpus_[i].index;
+        r["hip_device"] = dev;
+        r["checks_started_ms"] = since(t0);
+        r["checks_ms"] = std::chrono::duration<double, std::milli>(clock::now() - t0).count();
+        results[i] = std::move(r);
+      });
+    }
+    for (auto& t : threads) t.join();
+  }
+  // Phase 2: the node-level burn — every GPU under diagnosis at full MFMA load together.
+  Value node = Value();
+  std::vector<std::vector<std::string>> node_failures(todo.size());
+  if (cfg_.diag_burn_ms > 0 && !todo.empty()) {
+    NodeBurnResult nb = node_burn(*backend_, *engine_, gpus_, hip_devs_, todo, static_cast<int>(cfg_.diag_burn_ms), 0xb0c4);
+    node_failures = judge_node_burn(nb, cfg_.diag_floors);
+    for (size_t k = 0; k < todo.size(); ++k) results[todo[k]]["burn"] = nb.per_gpu[k];
+    node = nb.node;
+    auto& reg = metrics::Registry::global();
+    reg.gauge("amd_gpu_diag_node_burn_power_watts", "Diagnostics: peak summed GPU power during the node-level burn")
+        .set(node.get("power_sum_max_w").as_double());
+    reg.gauge("amd_gpu_diag_node_burn_balance", "Diagnostics: slowest/fastest GPU burn rate under shared load")
+        .set(node.get("balance").as_double());
+    LOG_INFO("node_agent") << "node burn: " << todo.size() << " GPUs, peak " << node.get("power_sum_max_w").as_double()
+                           << " W summed, peak hotspot " << node.get("peak_hotspot_c").as_double() << " C, balance "
+                           << node.get("balance").as_double();
+  }
+  for (size_t k = 0; k < todo.size(); ++k) {
+    const size_t i = todo[k];
+    Value r = judge_diag(results[i], cfg_.diag_floors);
+    if (!node_failures[k].empty()) {
+      Value f = r.get("failures");
+      for (const auto& s : node_failures[k]) f.push_back(s);
+      r["failures"] = f;
+      r["passed"] = false;
+    }
+    results[i] = std::move(r);
+    record_diag_gauges(i, results[i]);
+  }
+  const double pass_ms = since(clock::now());
   bool changed = false;
   {
     std::lock_guard<std::mutex> lk(diag_mu_);
@@ -510,10 +545,20 @@ bool NodeAgent::run_diagnostics(bool force) {
     diag_.per_gpu = per;
     diag_.runs++;
     diag_.skipped_in_use += skipped;
+    diag_.last_pass_ms = pass_ms;
+    diag_.last_diagnosed = todo.size();
+    if (!node.is_null()) diag_.node_burn = node;
+  }
+  if (fence) {  // verdicts first, so a failed GPU never flashes Healthy on release
+    plugin_->set_health(healthy_flags());
+    plugin_->set_fenced(todo, false);
   }
   auto& reg = metrics::Registry::global();
   reg.counter("bgc_gpu_diag_runs_total", "Diagnostics passes").inc();
+  reg.gauge("bgc_gpu_diag_pass_seconds", "Wall time of the last diagnostics pass").set(pass_ms / 1e3);
   if (skipped) reg.counter("bgc_gpu_diag_skipped_in_use_total", "GPUs skipped by a diagnostics pass because a container held them").inc(static_cast<double>(skipped));
+  LOG_INFO("node_agent") << "diagnostics pass: " << todo.size() << " GPU(s) in " << pass_ms << " ms, " << skipped
+                         << " skipped";
   return changed;
 }
 
@@ -558,6 +603,7 @@ void NodeAgent::publish() {
   client_.apply_status(types::Node, "", cfg_.node_name, node_status_patch(cfg_, gpus_, healthy, reason),
                        kNodeAgentManager, true);
   publishes_.fetch_add(1);
+  if (!cfg_.device_plugin) mark_advertised();  // capacity/allocatable is the advertisement
   LOG_INFO("node_agent") << "published node " << cfg_.node_name << ": " << cfg_.resource_name << " capacity "
                          << gpus_.size() << ", allocatable " << healthy;
 }
@@ -575,6 +621,7 @@ void NodeAgent::start() {
     plugin_ = std::make_unique<DevicePlugin>(gpus_, pc);
     plugin_->set_health(healthy_flags());
     plugin_->start();
+    mark_advertised();  // ListAndWatch serves from here on
   }
   poller_->on_health_change([this](const Snapshot&) { on_health_changed(); });
   poller_->start();
@@ -663,6 +710,17 @@ Value NodeAgent::describe() const {
   out["diag"] = d.per_gpu;
   out["diag_runs"] = static_cast<unsigned long long>(d.runs);
   out["diag_skipped_in_use"] = static_cast<unsigned long long>(d.skipped_in_use);
+  out["diag_last_pass_ms"] = d.last_pass_ms;
+  out["diag_last_diagnosed"] = static_cast<unsigned long long>(d.last_diagnosed);
+  out["diag_node_burn"] = d.node_burn;
+  out["diag_fence_races"] = static_cast<unsigned long long>(fence_races_.load());
+  out["diag_engine"] = engine_ ? Value(engine_->name()) : Value();
+  Value hd = Value::array();
+  for (int h : hip_devs_) hd.push_back(h);
+  out["hip_devices"] = hd;
+  out["startup_ms"] = Value::object({{"discover", discover_ms_},
+                                     {"diagnostics", startup_diag_ms_},
+                                     {"first_advertise", first_advertise_ms_.load()}});
   if (plugin_) out["device_plugin"] = plugin_->describe();
   return out;
 }

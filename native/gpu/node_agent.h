@@ -19,6 +19,7 @@
 #pragma once
 
 #include <atomic>
+#include <chrono>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -29,6 +30,7 @@
 #include "gpu/device.h"
 #include "gpu/device_plugin.h"
 #include "gpu/diag.h"
+#include "gpu/diag_runner.h"
 #include "gpu/telemetry.h"
 #include "kube/client.h"
 #include "kube/events.h"
@@ -58,9 +60,20 @@ struct NodeAgentConfig {
   // before the first advertisement and then every `diag_interval_secs` on GPUs that no
   // container holds (kubelet pod-resources API, else amdsmi's process list); a GPU that
   // fails a check or a floor is advertised Unhealthy until a later run passes.
+  //
+  // Every GPU is diagnosed on its own thread and the burn-in is one node-level phase
+  // (gpu/diag_runner.h).  A periodic pass first fences its GPUs in the device plugin
+  // (listed Unhealthy, refused by Allocate), waits `diag_fence_settle_ms` for an
+  // in-flight admission to land, re-checks that they are still free and only then runs.
   bool run_diag = false;
-  uint64_t diag_hbm_bytes = 1ULL << 30;
+  uint64_t diag_hbm_bytes = 1ULL << 30;  // bandwidth phases (two buffers)
   uint64_t diag_interval_secs = 0;     // 0 = only at start
+  // Address-pattern walk of this share of each GPU's free VRAM (0 = off), in chunks, with
+  // a time budget after which the second (inverse) pass is skipped.
+  double diag_hbm_walk_fraction = 0.9;
+  uint64_t diag_hbm_walk_chunk_mb = 4096;
+  uint64_t diag_hbm_walk_budget_ms = 20000;
+  uint64_t diag_fence_settle_ms = 2000;
   // Burn-in: sustained MFMA load for this long while power, clocks, temperatures and
   // throttle residency are sampled (catches cooling/power-delivery faults the short
   // checks do not); 0 = off.
@@ -100,20 +113,15 @@ struct DiagOutcome {
   json::Value per_gpu = json::Value::array();  // judged results, one per GPU (null = not run)
   uint64_t runs = 0;
   uint64_t skipped_in_use = 0;
+  double last_pass_ms = 0;             // wall time of the last pass
+  uint64_t last_diagnosed = 0;         // GPUs the last pass ran on
+  json::Value node_burn;               // node-level burn summary of the last pass (null = none)
 };
 
 std::string sanitize_label_value(const std::string& v);
 // The extended-resource name for a set of discovered devices (see partition_resource_name).
 std::string advertised_resource(const NodeAgentConfig& cfg, const std::vector<GpuInfo>& gpus);
 std::string product_label(const GpuInfo& g);
-
-// Burn-in of one GPU: Diag::burn() while a side thread samples it through `backend`
-// (hotspot/HBM temperature, power, gfxclk, thermal/PPT violation residency over the burn).
-json::Value burn_in(Backend& backend, int index, int hip_device, int duration_ms, uint32_t seed);
-// Host<->device copy rates (Diag::pcie) plus the PCIe link width/speed sampled through
-// `backend` while the copies run (links drop to a low-power rate when idle), and the
-// link's replay/recovery counter deltas over the test.
-json::Value pcie_check(Backend& backend, const GpuInfo& g, int hip_device, uint64_t bytes, uint32_t seed);
 
 // Pure rendering of the Node patches (unit-tested).
 json::Value node_labels_patch(const NodeAgentConfig& cfg, const std::vector<GpuInfo>& gpus, int healthy,
@@ -147,8 +155,18 @@ class NodeAgent {
 
  private:
   int healthy_count(std::string* reason) const;
-  json::Value diagnose(const GpuInfo& g) const;
+  DiagPlan diag_plan() const;
+  void setup_diag();  // engine + HIP device ids (by BDF); idempotent
+  void record_diag_gauges(size_t i, const json::Value& judged);
   std::vector<bool> in_use() const;
+  std::unique_ptr<DiagEngine> engine_;
+  std::vector<int> hip_devs_;          // HIP device id per GPU (diag_runner.h hip_devices_for)
+  std::atomic<uint64_t> fence_races_{0};  // GPUs released because an allocation raced the fence
+  // start-up timeline (ms since the agent was constructed)
+  std::chrono::steady_clock::time_point t_created_ = std::chrono::steady_clock::now();
+  double discover_ms_ = 0, startup_diag_ms_ = 0;
+  std::atomic<double> first_advertise_ms_{0};
+  void mark_advertised();
   void on_health_changed();
   kube::KubeClient& client_;
   std::unique_ptr<Backend> backend_;

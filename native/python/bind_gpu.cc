@@ -198,6 +198,28 @@ void register_gpu(py::module_& m) {
     }
     return py::bytes(c);
   }, py::arg("device"), py::arg("m"), py::arg("n"), py::arg("k"), py::arg("a_bf16"), py::arg("b_bf16"));
+  m.def("diag_gemm_tiled", [](int device, int mm, int nn, int kk, const std::string& a, const std::string& bt) {
+    if (a.size() != static_cast<size_t>(mm) * kk * 2 || bt.size() != static_cast<size_t>(nn) * kk * 2) {
+      throw std::invalid_argument("A must be M*K and Bt N*K bf16 values");
+    }
+    std::string c(static_cast<size_t>(mm) * nn * 4, '\0');
+    {
+      py::gil_scoped_release nogil;
+      bgc::gpu::Diag::instance().gemm_tiled(device, mm, nn, kk, reinterpret_cast<const uint16_t*>(a.data()),
+                                            reinterpret_cast<const uint16_t*>(bt.data()), reinterpret_cast<float*>(c.data()));
+    }
+    return py::bytes(c);
+  }, py::arg("device"), py::arg("m"), py::arg("n"), py::arg("k"), py::arg("a_bf16"), py::arg("bt_bf16"));
+  m.def("diag_hbm_walk", [](int device, double fraction, unsigned long long chunk_bytes, int budget_ms, unsigned seed) {
+    Value v;
+    {
+      py::gil_scoped_release nogil;
+      v = bgc::gpu::Diag::instance().hbm_walk(device, fraction, chunk_bytes, budget_ms, seed);
+    }
+    return v.dump();
+  }, py::arg("device"), py::arg("fraction") = 0.9, py::arg("chunk_bytes") = 4ULL << 30, py::arg("budget_ms") = 20000,
+     py::arg("seed") = 0x5eed);
+  m.def("diag_device_bdf", [](int d) { return bgc::gpu::Diag::instance().device_bdf(d); });
   m.def("diag_gemm_check", [](int device, int mm, int nn, int kk, unsigned seed) {
     Value v;
     {
@@ -260,6 +282,9 @@ void register_gpu(py::module_& m) {
     num("min_pcie_d2h_gbps", f.min_pcie_d2h_gbps);
     num("min_pcie_speed_fraction", f.min_pcie_speed_fraction);
     num("min_soak_tflops", f.min_soak_tflops);
+    num("min_hbm_walk_coverage", f.min_hbm_walk_coverage);
+    num("min_node_burn_balance", f.min_node_burn_balance);
+    num("max_node_power_w", f.max_node_power_w);
     if (fj.get("require_full_pcie_width").is_bool()) f.require_full_pcie_width = fj.get("require_full_pcie_width").as_bool();
     if (fj.get("min_xccs").is_int()) f.min_xccs = static_cast<int>(fj.get("min_xccs").as_int());
     return bgc::gpu::judge_diag(bgc::json::parse(result), f).dump();

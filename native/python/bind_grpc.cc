@@ -277,7 +277,10 @@ void register_grpc(py::module_& m) {
       .def("start", &bgc::gpu::DevicePlugin::start, py::call_guard<py::gil_scoped_release>())
       .def("stop", &bgc::gpu::DevicePlugin::stop, py::call_guard<py::gil_scoped_release>())
       .def("set_health", &bgc::gpu::DevicePlugin::set_health)
-      .def("allocate_json", [](const bgc::gpu::DevicePlugin& p, const std::vector<std::string>& ids) {
+      .def("set_fenced", &bgc::gpu::DevicePlugin::set_fenced)
+      .def("fenced", &bgc::gpu::DevicePlugin::fenced)
+      .def("allocation_counts", &bgc::gpu::DevicePlugin::allocation_counts)
+      .def("allocate_json", [](bgc::gpu::DevicePlugin& p, const std::vector<std::string>& ids) {
         auto c = p.allocate(ids);
         bgc::json::Value devs = bgc::json::Value::array();
         for (const auto& d : c.devices) {

@@ -344,7 +344,7 @@ def test_periodic_diagnostics_skip_gpus_in_use(tmp_path):
             c.start_node_agent(node_name="mi355x-diag", backend="mock", n_mock_gpus=4, poll_interval_ms=50,
                                extra_env={"CONF_DEVICE_PLUGIN": "true", "CONF_DEVICE_PLUGIN_DIR": d,
                                           "CONF_RUN_DIAG": "true", "CONF_DIAG_INTERVAL_SECS": "1",
-                                          "CONF_DIAG_HBM_BYTES": str(64 << 20),
+                                          "CONF_DIAG_HBM_BYTES": str(64 << 20), "CONF_DIAG_FENCE_SETTLE_MS": "200",
                                           "CONF_POD_RESOURCES_SOCKET": pr.path, "CONF_HEARTBEAT_SECS": "1"})
             fx_path = c.fixtures["mi355x-diag"]
             fx = json.loads(open(fx_path).read())

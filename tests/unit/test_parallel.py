@@ -63,3 +63,40 @@ def test_rccl_probe_logic_gloo_world2():
     # no GPU: no link counters, and a CPU group never claims xGMI traffic
     assert [t["xgmi_written_mb"] for t in out["xgmi_traffic"]] == [None, None] and out["traffic_on_xgmi"] is False
     assert all(t["expected_mb"] > 0 for t in out["xgmi_traffic"])
+
+
+def _hive_fixture():
+    # two 4-GPU hives; amdsmi hip_id is the host-wide ordinal
+    return [{"index": i, "hip_id": i, "bdf": f"0000:{0x05 + 0x10 * i:02x}:00.0",
+             "xgmi_hive_id": "aaaa" if i < 4 else "bbbb"} for i in range(8)]
+
+
+def test_probe_maps_rank_gpu_by_bdf_not_hip_id():
+    """Inside a container with HIP_VISIBLE_DEVICES=6,2 HIP calls the GPUs 0 and 1, but
+    amdsmi's hip_id 0/1 are other GPUs on the host: the BDF decides."""
+    from bacchus_gpu_controller_amd.parallel import rccl_probe
+
+    gpus = _hive_fixture()
+    visible = [6, 2]  # HIP ordinal -> host GPU
+    for local, host in enumerate(visible):
+        bdf = gpus[host]["bdf"]
+        g = rccl_probe.match_gpu(gpus, bdf=bdf, local_rank=local)
+        assert g["index"] == host and g["xgmi_hive_id"] == gpus[host]["xgmi_hive_id"]
+    # torch reports no function number and may use upper-case hex
+    assert rccl_probe.match_gpu(gpus, bdf="0000:65:00.0".upper(), local_rank=0)["index"] == 6
+    # without a BDF the old hip_id rule is the last resort
+    assert rccl_probe.match_gpu(gpus, bdf=None, local_rank=1)["index"] == 1
+
+
+def test_probe_uses_device_plugin_allocation_for_partitions():
+    from bacchus_gpu_controller_amd.parallel import rccl_probe
+
+    # CPX: 4 logical devices share each BDF; the plugin names them <bdf>-p<index>
+    gpus = [{"index": i, "hip_id": i, "bdf": "0000:05:00.0" if i < 4 else "0000:15:00.0",
+             "xgmi_hive_id": "h" + str(i // 4)} for i in range(8)]
+    alloc = ["0000:15:00.0-p6"]
+    g = rccl_probe.match_gpu(gpus, bdf="0000:15:00.0", local_rank=0, allocated=alloc)
+    assert g["index"] == 6
+    # allocation without partitions narrows to the allocated BDFs
+    g = rccl_probe.match_gpu(_hive_fixture(), bdf=None, local_rank=0, allocated=["0000:45:00.0"])
+    assert g["index"] == 4
