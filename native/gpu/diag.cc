@@ -203,6 +203,7 @@ json::Value Diag::hbm_walk(int device, double fraction, uint64_t chunk_bytes, in
                               {"first_bad_bits", r.mismatches ? json::Value(std::string(flips)) : json::Value()},
                               {"write_gbps", r.write_gbps},
                               {"read_gbps", r.read_gbps},
+                              {"alloc_ms", r.alloc_ms},
                               {"elapsed_ms", r.elapsed_ms},
                               {"budget_hit", r.budget_hit != 0},
                               {"passed", r.mismatches == 0 && r.passes == 2}});

@@ -63,12 +63,23 @@ class HipDiagEngine : public DiagEngine {
   Value checks(Backend& backend, const GpuInfo& g, int dev, const DiagPlan& plan, uint32_t seed) override {
     Diag& d = Diag::instance();
     Value r = Value::object();
+    Value timing = Value::object();  // wall ms per section, to see where a pass spends its time
+    auto t = std::chrono::steady_clock::now();
+    auto lap = [&](const char* name) {
+      const auto now = std::chrono::steady_clock::now();
+      timing[name] = std::chrono::duration<double, std::milli>(now - t).count();
+      t = now;
+    };
     r["hbm"] = d.hbm(dev, plan.hbm_bytes, 2, seed);
+    lap("hbm");
     if (plan.hbm_walk_fraction > 0) {
       r["hbm_walk"] = d.hbm_walk(dev, plan.hbm_walk_fraction, plan.hbm_walk_chunk_bytes, plan.hbm_walk_budget_ms, seed);
+      lap("hbm_walk");
     }
     r["mfma"] = d.mfma(dev, 16, 2048, seed);
+    lap("mfma");
     r["gemm"] = d.gemm_check(dev, 64, 64, 512, seed);
+    lap("gemm");
     if (plan.pcie_bytes > 0) {
       // One GPU at a time: eight concurrent pinned-copy streams share the host's memory
       // bandwidth and root complexes, so concurrent rates would measure the host, not
@@ -76,10 +87,13 @@ class HipDiagEngine : public DiagEngine {
       static std::mutex pcie_mu;
       std::lock_guard<std::mutex> lk(pcie_mu);
       r["pcie"] = pcie_check(backend, g, dev, plan.pcie_bytes, seed);
+      lap("pcie");
     }
     if (plan.soak_launches > 0) {
       r["soak"] = d.gemm_soak(dev, plan.soak_size, plan.soak_size, plan.soak_size, plan.soak_launches, seed);
+      lap("soak");
     }
+    r["timing_ms"] = timing;
     return r;
   }
   Value burn(int dev, int duration_ms, uint32_t seed) override { return Diag::instance().burn(dev, duration_ms, 32, seed); }

@@ -15,7 +15,7 @@
 extern "C" {
 #endif
 
-#define BGC_DIAG_ABI_VERSION 6
+#define BGC_DIAG_ABI_VERSION 7
 #define BGC_DIAG_MAX_CU_KEYS 2048
 
 typedef struct {
@@ -112,6 +112,7 @@ typedef struct {
   uint64_t first_bad_xor;     // expected ^ found at that word: the flipped bits
   double write_gbps;          // fill rate over the covered bytes
   double read_gbps;           // verify rate
+  double alloc_ms;            // of which: allocating the chunks
   double elapsed_ms;          // wall time of the walk (allocation included)
   int budget_hit;             // 1 when the time budget ended the walk before both passes
 } bgc_hbm_walk_result;

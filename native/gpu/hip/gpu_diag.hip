@@ -1057,6 +1057,7 @@ int bgc_diag_hbm_walk(int device, double fraction, uint64_t chunk_bytes, int bud
     return 1;
   }
   out->chunks = static_cast<int>(chunks.v.size());
+  out->alloc_ms = elapsed_ms();
   auto* bad = static_cast<unsigned long long*>(counters.p);
   const int grid = cu_count(device) * 8;
   Events ev;
