@@ -599,6 +599,12 @@ class Renderer:
             "print": lambda *a: "".join(_go_str(x) for x in a),
             "join": lambda sep, lst: sep.join(_go_str(x) for x in (lst or [])),
             "list": lambda *a: list(a), "dict": dict_, "index": index,
+            "kindIs": lambda kind, v: {"float64": isinstance(v, float), "int64": isinstance(v, int) and not isinstance(v, bool),
+                                       "int": isinstance(v, int) and not isinstance(v, bool), "string": isinstance(v, str),
+                                       "bool": isinstance(v, bool), "map": isinstance(v, dict),
+                                       "slice": isinstance(v, list), "invalid": v is None}.get(kind, False),
+            # sprig get: a missing key is "" (not nil)
+            "get": lambda d, k: d.get(_go_str(k), "") if isinstance(d, dict) else "",
             "eq": eq, "ne": lambda a, b: a != b, "lt": lambda a, b: a < b, "le": lambda a, b: a <= b,
             "gt": lambda a, b: a > b, "ge": lambda a, b: a >= b,
             "and": and_, "or": or_, "not": lambda a: not _truthy(a),

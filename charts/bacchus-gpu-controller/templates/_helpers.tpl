@@ -1,12 +1,16 @@
-{{/* Chart name, truncated to the 63-char DNS label limit. */}}
+{{/* Chart name, truncated to the 63-char DNS label limit.  The top-level nameOverride /
+     fullnameOverride are the keys the reference helpers read (reference
+     templates/_helpers.tpl:5,14-17), so a release installed with --set fullnameOverride=X keeps
+     every object name; the per-component keys of values.yaml are a fallback. */}}
 {{- define "bgc.name" -}}
-{{- default .Chart.Name .Values.controller.nameOverride | trunc 63 | trimSuffix "-" }}
+{{- default .Chart.Name (.Values.nameOverride | default .Values.controller.nameOverride) | trunc 63 | trimSuffix "-" }}
 {{- end }}
 
 {{/* Release-qualified name; the release name alone when it already contains the chart name. */}}
 {{- define "bgc.fullname" -}}
-{{- if .Values.controller.fullnameOverride }}
-{{- .Values.controller.fullnameOverride | trunc 63 | trimSuffix "-" }}
+{{- $override := .Values.fullnameOverride | default .Values.controller.fullnameOverride }}
+{{- if $override }}
+{{- $override | trunc 63 | trimSuffix "-" }}
 {{- else }}
 {{- $name := include "bgc.name" . }}
 {{- if contains $name .Release.Name }}
@@ -21,9 +25,18 @@
 {{- printf "%s-%s" .Chart.Name .Chart.Version | replace "+" "_" | trunc 63 | trimSuffix "-" }}
 {{- end }}
 
-{{/* Selector labels. `component` keeps each Deployment/Service selecting only its own
-     pods (the reference shared one selector, so its webhook Service also routed to the
-     plain-HTTP controller/synchronizer pods). Call with (dict "root" $ "component" "x"). */}}
+{{/* Deployment spec.selector: exactly the reference's (name + instance; reference
+     templates/deployment.yaml:12-14).  spec.selector is immutable, so anything else would make
+     an in-place `helm upgrade` from a reference release fail.  Call with the root context. */}}
+{{- define "bgc.deploymentSelector" -}}
+app.kubernetes.io/name: {{ include "bgc.name" . }}
+app.kubernetes.io/instance: {{ .Release.Name }}
+{{- end }}
+
+{{/* Pod labels and the selector of the Service, PDB and DaemonSet. `component` keeps the
+     webhook Service on the admission pods only (the reference shared one selector, so its
+     Service also routed to the plain-HTTP controller/synchronizer pods: SURVEY Q1).
+     Call with (dict "root" $ "component" "x"). */}}
 {{- define "bgc.selectorLabels" -}}
 app.kubernetes.io/name: {{ include "bgc.name" .root }}
 app.kubernetes.io/instance: {{ .root.Release.Name }}

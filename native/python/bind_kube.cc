@@ -6,6 +6,7 @@
 
 #include "apiserver/server.h"
 #include "bench/churn.h"
+#include "kube/ratelimit.h"
 #include "kube/runtime.h"
 
 namespace py = pybind11;
@@ -63,6 +64,15 @@ void register_kube(py::module_& m) {
       });
 
   // WorkQueue (unit tests of dedup / delay / exclusivity semantics)
+  py::class_<bgc::kube::RetryLimiter>(m, "RetryLimiter")
+      .def(py::init([](int64_t base_ms, int64_t cap_ms, double qps, int burst) {
+             return std::make_unique<bgc::kube::RetryLimiter>(std::chrono::milliseconds(base_ms),
+                                                              std::chrono::milliseconds(cap_ms), qps, burst);
+           }),
+           py::arg("base_ms") = 5, py::arg("cap_ms") = 60000, py::arg("qps") = 10.0, py::arg("burst") = 100)
+      .def("when", [](bgc::kube::RetryLimiter& r, const std::string& k) { return r.when(k).count(); })
+      .def("forget", &bgc::kube::RetryLimiter::forget)
+      .def("failures", &bgc::kube::RetryLimiter::failures);
   py::class_<bgc::kube::WorkQueue>(m, "WorkQueue")
       .def(py::init<>())
       .def("add", [](bgc::kube::WorkQueue& q, const std::string& k) { q.add(k); })

@@ -7,6 +7,7 @@
 #include "core/json_patch.h"
 #include "core/log.h"
 #include "core/metrics.h"
+#include "kube/ratelimit.h"
 
 namespace bgc::sync {
 
@@ -29,6 +30,10 @@ Config Config::from_env(const EnvConfig& env) {
   c.exit_on_error = env.boolean_or("exit_on_error", true);
   c.skip_unchanged = env.boolean_or("skip_unchanged", true);
   c.workers = static_cast<int>(env.u64_or("workers", 8));
+  c.retry_base_ms = env.u64_or("retry_base_ms", c.retry_base_ms);
+  c.retry_max_ms = env.u64_or("retry_max_ms", c.retry_max_ms);
+  c.retry_qps = env.f64_or("retry_qps", c.retry_qps);
+  c.retry_burst = static_cast<int>(env.u64_or("retry_burst", static_cast<uint64_t>(c.retry_burst)));
   c.lease = kube::LeaseSettings::from_env(env, "bacchus-gpu-synchronizer");
   if (c.sync_interval_secs == 0) throw ConfigError("invalid value for field sync_interval_secs: must be > 0");
   return c;
@@ -73,6 +78,17 @@ bool Synchronizer::refresh_if_stale() {
 }
 
 void Synchronizer::refresh_locked() {
+  // The sheet's Drive version goes with the export it describes, so the version poller's
+  // baseline is the version this export read — not whatever its own first poll, one
+  // sheet_poll_ms later, finds (an edit in between would otherwise wait for the next tick).
+  std::string version;
+  if (version_source_) {
+    try {
+      version = version_source_();
+    } catch (const std::exception& e) {
+      LOG_WARN("synchronizer") << "sheet version read failed: " << e.what();
+    }
+  }
   std::string csv = source_();
   LOG_INFO("synchronizer") << "downloaded csv file";
   std::vector<std::string> warnings;
@@ -87,6 +103,13 @@ void Synchronizer::refresh_locked() {
   }
   last_refresh_ns_.store(metrics::now_ns());
   index_gen_.fetch_add(1);
+  std::lock_guard<std::mutex> lk(mu_);
+  known_version_ = version;
+}
+
+std::string Synchronizer::known_version() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return known_version_;
 }
 
 bool Synchronizer::sync_one(const Value& ub, std::vector<std::string>* produced) {
@@ -172,6 +195,12 @@ int Synchronizer::run(CancelToken& stop) {
     std::vector<std::string> versions;  // UB versions acted on or produced by our writes
   };
   std::unordered_map<std::string, Acted> acted;
+  // CONF_EXIT_ON_ERROR=false only: per-UserBootstrap exponential backoff plus an overall
+  // retry budget (client-go's controller rate limiter) instead of a fixed delay
+  kube::RetryLimiter retries(std::chrono::milliseconds(cfg_.retry_base_ms), std::chrono::milliseconds(cfg_.retry_max_ms),
+                             cfg_.retry_qps, cfg_.retry_burst);
+  static auto& retried = metrics::Registry::global().counter("bgc_sync_retries_total",
+                                                             "UserBootstrap syncs re-queued after a failure");
 
   if (cfg_.watch) {
     watch_thread = std::make_unique<std::thread>([&] {
@@ -216,9 +245,22 @@ int Synchronizer::run(CancelToken& stop) {
                 std::lock_guard<std::mutex> g(acted_mu);
                 acted[key] = Acted{gen, std::move(produced)};
               }
+              retries.forget(key);
             } catch (const std::exception& e) {
-              LOG_ERROR("synchronizer") << "sync of " << key << " failed (retrying): " << e.what();
-              queue.add_after(key, std::chrono::milliseconds(1000));
+              if (cfg_.exit_on_error) {
+                // Q7, as the reference: a failed status PUT or spec PATCH returns Err out of
+                // synchronize_loop and try_join! ends the process (synchronizer.rs:302-330,
+                // 426-430); the kubelet restarts it with crash-loop backoff.
+                LOG_ERROR("synchronizer") << "synchronization of " << key << " failed: " << e.what();
+                fatal = true;
+                stop.cancel();
+              } else {
+                const auto delay = retries.when(key);
+                retried.inc();
+                LOG_ERROR("synchronizer") << "sync of " << key << " failed (retry " << retries.failures(key) << " in "
+                                          << delay.count() << " ms): " << e.what();
+                queue.add_after(key, delay);
+              }
             }
           }
           queue.done(key);
@@ -236,17 +278,13 @@ int Synchronizer::run(CancelToken& stop) {
       static auto& polls = metrics::Registry::global().counter("bgc_drive_version_polls_total",
                                                                "Drive file-version metadata requests");
       static auto& changed = drive_exports("changed");
-      std::string last;
       while (!stop.wait_for(std::chrono::milliseconds(cfg_.sheet_poll_ms))) {
         try {
           polls.inc();
           std::string v = version_source_();
-          if (last.empty()) {
-            last = v;  // the first tick's export already covers this version
-            continue;
-          }
-          if (v == last) continue;
-          last = v;
+          // known_version(): what the last export read ("" when that read failed: then
+          // any version re-reads, at the cost of one possibly redundant export)
+          if (v == known_version()) continue;
           LOG_INFO("synchronizer") << "sheet changed (version " << v << "); re-reading";
           {
             std::lock_guard<std::mutex> rl(refresh_mu_);
@@ -287,6 +325,7 @@ int Synchronizer::run(CancelToken& stop) {
   queue.shutdown();
   for (auto& t : workers) t.join();
   if (watch_thread) watch_thread->join();
+  if (fatal) rc = 1;
   return rc;
 }
 

@@ -3,8 +3,11 @@
 // Reference semantics kept: every `sync_interval_secs` (first tick immediate) export the
 // sheet as CSV, keep rows whose gpu_server contains `gpu_server_name`, and for each
 // UserBootstrap with an authorized row (last match wins) write spec.quota (JSON Patch:
-// add {} if absent, then replace) and status.synchronized_with_sheet=true.  A tick-level
-// error ends the process (kubelet restarts it) unless CONF_EXIT_ON_ERROR=false.
+// add {} if absent, then replace) and status.synchronized_with_sheet=true.  Any error — a
+// sheet export, the LIST, a status PUT or a quota PATCH, in the periodic tick or in a watch
+// worker — ends the process (kubelet restarts it; SURVEY Q7, reference
+// src/synchronizer.rs:302-330,426-430) unless CONF_EXIT_ON_ERROR=false, which retries a
+// failed UserBootstrap with per-key exponential backoff under a global retry budget.
 //
 // Changes (end state identical):
 //  * Q5: quota is written BEFORE status, closing the window in which the controller could
@@ -51,6 +54,12 @@ struct Config {
   // poll instead of one sync tick (reference: export every 60 s tick only).  0 = off.
   uint64_t sheet_poll_ms = 5000;
   bool exit_on_error = true;
+  // exit_on_error=false: retry a failed UserBootstrap after base * 2^(n-1) ms (capped),
+  // all retries together at most retry_qps with retry_burst (client-go's defaults)
+  uint64_t retry_base_ms = 5;
+  uint64_t retry_max_ms = 60000;
+  double retry_qps = 10;
+  int retry_burst = 100;
   bool skip_unchanged = true;
   int workers = 8;
   // Lease-based leader election (reference: none; two synchronizer replicas would both
@@ -92,12 +101,14 @@ class Synchronizer {
  private:
   std::shared_ptr<const RowIndex> index() const;
   void refresh_locked();  // refresh_mu_ held
+  std::string known_version() const;  // Drive version read with the last export
   kube::KubeClient& client_;
   SheetSource source_;
   std::function<std::string()> version_source_;
   Config cfg_;
   mutable std::mutex mu_;
   std::shared_ptr<const RowIndex> index_;
+  std::string known_version_;  // guarded by mu_
   std::atomic<int64_t> last_refresh_ns_{0};
   std::atomic<uint64_t> index_gen_{0};  // bumped by every refresh()
   std::mutex refresh_mu_;

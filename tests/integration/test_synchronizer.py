@@ -204,3 +204,52 @@ def test_approval_after_create_is_picked_up_by_version_poll(google):
         assert rq["spec"]["hard"]["requests.amd.com/gpu"] == "4"
         assert google.export_requests - exports_before == 1  # one export for one sheet edit
         assert google.metadata_requests >= 3
+
+
+def _patch_failures(c):
+    return sum(v for k, v in c.stats()["requests_by_kind"].items()
+               if k.startswith("PATCH userbootstraps ") and not k.endswith(" 200"))
+
+
+def test_webhook_down_default_synchronizer_exits(google):
+    """Q7 in the default (watch) mode too: the quota PATCH re-enters the webhook (C16);
+    with the webhook down (failurePolicy Fail) the PATCH fails and — as the reference's
+    synchronize_loop returns Err and try_join! ends the process — the synchronizer exits
+    non-zero for the kubelet to restart (synchronizer.rs:323-330,426-430)."""
+    google.set_rows([{"id_username": "frank", "gpu": 1}])
+    with Cluster(controller=False) as c:
+        c.as_user("oidc:frank", ["gpu"]).create("userbootstraps", ub("frank"))
+        c.procs["admission"].stop()
+        p = c.start_synchronizer(google, interval=60, wait_healthy=False)
+        wait_for(lambda: p.p.poll() is not None, timeout=15, desc="synchronizer exit")
+        assert p.p.returncode != 0
+        assert "synchronization of frank failed" in p.output()
+        assert _patch_failures(c) == 1  # it did not keep hammering the dead webhook
+        assert not c.admin.get("userbootstraps", "frank").get("status")  # Q5: quota first, so no status
+
+
+def test_webhook_down_retries_back_off_then_converge(google):
+    """CONF_EXIT_ON_ERROR=false: a failing UserBootstrap is retried with per-key exponential
+    backoff (base 100 ms, cap 800 ms here; 5 ms / 60 s by default) instead of a fixed
+    interval, and converges once the webhook is back."""
+    google.set_rows([{"id_username": "gina", "gpu": 3}])
+    with Cluster(controller=False) as c:
+        c.as_user("oidc:gina", ["gpu"]).create("userbootstraps", ub("gina"))
+        c.procs["admission"].stop()
+        c.start_synchronizer(google, interval=60, extra_env={"CONF_EXIT_ON_ERROR": "false", "CONF_RETRY_BASE_MS": "100",
+                                                              "CONF_RETRY_MAX_MS": "800"})
+        wait_for(lambda: _patch_failures(c) >= 1, timeout=10, desc="first failure")
+        t0 = time.time()
+        time.sleep(4.0)
+        n = _patch_failures(c) - 1
+        # after the first failure: retries at +0.1, +0.3, +0.7, +1.5, +2.3, +3.1, +3.9 s
+        elapsed = time.time() - t0
+        schedule = [0.1, 0.3, 0.7, 1.5, 2.3, 3.1, 3.9, 4.7]
+        allowed = sum(1 for t in schedule if t <= elapsed) + 1
+        assert 4 <= n <= allowed, (n, allowed)
+        m = requests.get(f"http://127.0.0.1:{c.sync_port}/metrics", timeout=5).text
+        assert "bgc_sync_retries_total" in m
+        c.start_admission()
+        obj = wait_for(lambda: (lambda o: o if o.get("status", {}).get("synchronized_with_sheet") else None)(
+            c.admin.get("userbootstraps", "gina")), timeout=5, desc="gina converged")
+        assert obj["spec"]["quota"] == {"hard": expected_hard(3)}

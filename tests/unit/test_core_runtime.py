@@ -294,3 +294,20 @@ def test_cert_bundle_key_types(nat, tmp_path):
         v = subprocess.run(["openssl", "verify", "-CAfile", str(tmp_path / "ca.crt"), str(tmp_path / "leaf.crt")],
                            capture_output=True, text=True)
         assert v.returncode == 0, v.stdout + v.stderr
+
+
+def test_retry_limiter_exponential_cap_and_bucket(nat):
+    """client-go's controller rate limiter: base * 2^(n-1) per key, capped, max'd with an
+    overall token bucket; forget() restarts a key's backoff."""
+    r = nat.RetryLimiter(5, 60000, 1e6, 1000)
+    assert [r.when("a") for _ in range(6)] == [5, 10, 20, 40, 80, 160]
+    assert r.failures("a") == 6 and r.when("b") == 5  # keys are independent
+    for _ in range(20):
+        r.when("a")
+    assert r.when("a") == 60000  # capped
+    r.forget("a")
+    assert r.failures("a") == 0 and r.when("a") == 5
+    # the bucket: 10 qps with burst 2 -> the third immediate retry waits ~100 ms
+    b = nat.RetryLimiter(1, 1, 10.0, 2)
+    d = [b.when(f"k{i}") for i in range(4)]
+    assert d[:2] == [1, 1] and 90 <= d[2] <= 101 and 190 <= d[3] <= 201
