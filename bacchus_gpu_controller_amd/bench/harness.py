@@ -241,20 +241,23 @@ def _phase(d, nat, info, args, phase, concurrency, total_steps, cluster):
                 d.barrier()
                 t_start = time.perf_counter()
                 ru0 = resource.getrusage(resource.RUSAGE_SELF)
-            names = _names(d.rank, phase, s, args.batch)
-            res = json.loads(driver.step_with_delete(names, prev or [], args.timeout))
-            prev = names
-            if s >= args.warmup:
-                lat += res["ready_latency_s"]
-                clat += res["create_latency_s"]
-                ap_lat += res.get("approve_latency_s", [])
-                ap_ready += res.get("approve_to_ready_latency_s", [])
-                for k in stage:
-                    stage[k] += res[f"{k}_latency_s"]
-                ready += res["ready"]
-                failed += res["failed"]
-                timeouts += res["timeouts"]
-                errors += res["errors"]
+            for r in range(args.rounds):
+                # one round: `batch` tenants applied `concurrency` at a time and waited to
+                # Ready, deleting the previous round's tenants (GC churn) meanwhile
+                names = _names(d.rank, phase, s * args.rounds + r, args.batch)
+                res = json.loads(driver.step_with_delete(names, prev or [], args.timeout))
+                prev = names
+                if s >= args.warmup:
+                    lat += res["ready_latency_s"]
+                    clat += res["create_latency_s"]
+                    ap_lat += res.get("approve_latency_s", [])
+                    ap_ready += res.get("approve_to_ready_latency_s", [])
+                    for k in stage:
+                        stage[k] += res[f"{k}_latency_s"]
+                    ready += res["ready"]
+                    failed += res["failed"]
+                    timeouts += res["timeouts"]
+                    errors += res["errors"]
         d.sync()
         d.barrier()
         elapsed = time.perf_counter() - t_start
@@ -365,9 +368,13 @@ def run(args):
     # BASELINE config #3 is 100 concurrent CRs on the node: by default that total is split
     # over the ranks (ceil), so N load generators offer the same in-flight load as one
     conc = args.concurrency if args.concurrency_scope == "rank" else max(1, -(-args.concurrency // d.world))
-    phases = [("m", conc)]
+    # (phase, in-flight creates per rank, API server -> webhook protocol)
+    phases = [("m", conc, args.webhook_protocol)]
     if args.tuned_phase and tuned != conc:
-        phases.append(("t", tuned))
+        phases.append(("t", tuned, args.webhook_protocol))
+    if args.http1_phase and args.webhook_protocol == "h2":
+        # secondary: the same load with the webhook called over HTTP/1.1 (keep-alive pool)
+        phases.append(("w", conc, "http/1.1"))
     semantics = "reference" if args.reference_semantics else args.semantics
     # Reconcile/sync workers spend most of their time waiting on API round trips, so they
     # are not sized to the CPU share like the offered load is (16 = the binaries' default).
@@ -377,8 +384,8 @@ def run(args):
         google = FakeGoogle().start()
         if not args.approve_after_create:
             # pre-approved sheet: every tenant's row is marked O before it applies
-            google.set_rows([{"id_username": name} for r in range(d.world) for ph, _ in phases
-                             for s in range(total_steps) for name in _names(r, ph, s, args.batch)])
+            google.set_rows([{"id_username": name} for r in range(d.world) for ph, _, _ in phases
+                             for s in range(total_steps * args.rounds) for name in _names(r, ph, s, args.batch)])
         ctrl_env = {"CONF_WORKERS": str(controller_workers)}
         ctrl_env.update(dict(kv.split("=", 1) for kv in args.controller_env))
         sync_env = {"CONF_WATCH": "true", "CONF_WORKERS": str(sync_workers), "RUST_LOG": args.log_level,
@@ -393,6 +400,10 @@ def run(args):
             # (synchronizer.rs:192), every tick rewrites every matched tenant
             sync_env.update({"CONF_WATCH": "false", "CONF_SKIP_UNCHANGED": "false"})
         apiserver_args = list(args.apiserver_arg)
+        if args.webhook_protocol == "h2" and "--webhook-http2" not in apiserver_args:
+            # what a real apiserver negotiates with the admission server (ALPN h2, one
+            # multiplexed connection): the production webhook transport
+            apiserver_args.append("--webhook-http2")
         if args.write_latency_ms > 0:
             apiserver_args += ["--write-latency-ms", str(args.write_latency_ms)]
         cluster = Cluster(controller_env=ctrl_env, log_level=args.log_level, tls_apiserver=args.tls_apiserver,
@@ -411,7 +422,15 @@ def run(args):
                 "approve_url": google.base + "/_fake/rows" if args.approve_after_create else ""}
     info = d.broadcast_obj(info)
     try:
-        results = {ph: _phase(d, nat, info, args, ph, conc, total_steps, cluster) for ph, conc in phases}
+        results = {}
+        for ph, pconc, proto in phases:
+            if d.rank == 0:
+                import requests
+
+                requests.post(info["server"] + "/_kl/webhook-protocol", data=proto, timeout=10,
+                              verify=info["apiserver_verify"]).raise_for_status()
+            d.barrier()
+            results[ph] = _phase(d, nat, info, args, ph, pconc, total_steps, cluster)
         xgmi = _xgmi_probe(d, args)
         if d.rank != 0:
             return None
@@ -435,16 +454,17 @@ def run(args):
             # a control plane: no tensor math, so no compute dtype (BASELINE names none)
             "dtype": "none",
             "data": "synthetic tenants (UserBootstrap CRs), fake Google sheet",
-            "config": {"model": model, "global_batch": args.batch * d.world, "seq_len": None,
+            "config": {"model": model, "global_batch": args.batch * args.rounds * d.world, "seq_len": None,
+                       "rounds_per_step": args.rounds, "tenants_per_round": args.batch,
                        "parallelism": f"dp{d.world}", "semantics": semantics, "flow": flow,
                        "concurrency_per_rank": conc, "concurrency_total": conc * d.world,
                        "concurrency_scope": args.concurrency_scope, "log_level": args.log_level,
                        "apiserver_write_latency_ms": args.write_latency_ms, "control_plane_cpus": cpus,
                        "controller_workers": controller_workers, "sync_workers": sync_workers,
                        "sheet_poll_ms": args.sheet_poll_ms, "sync_interval_s": args.sync_interval,
-                       # API server -> webhook protocol: kube-lite's HTTP/1.1 pool unless it runs
-                       # --webhook-http2 (multiplexed h2 streams)
-                       "webhook_protocol": "h2" if "--webhook-http2" in args.apiserver_arg else "http/1.1",
+                       # API server -> webhook protocol of the headline phase: h2 (what the
+                       # admission server's ALPN gives a real apiserver) unless --webhook-protocol
+                       "webhook_protocol": args.webhook_protocol,
                        "driver_protocol": "h2" if args.driver_http2 and args.tls_apiserver else "http/1.1",
                        # each rank's load driver watches only its own tenants' children
                        # (kube-lite name-prefix field selector); the product is unaffected
@@ -457,6 +477,11 @@ def run(args):
             out["tuned"] = {k: t.get(k) for k in ("value", "concurrency_per_rank", "reconcile_p99_ms",
                                                   "admission_p50_ms", "apply_to_ready_p50_ms",
                                                   "apply_to_ready_p99_ms", "cpu_ms_per_cr", "failed_crs")}
+        if "w" in results:
+            w = results["w"]
+            out["webhook_http1"] = {k: w.get(k) for k in ("value", "admission_p50_ms", "admission_p99_ms",
+                                                          "admission_handler_p50_ms", "reconcile_p99_ms",
+                                                          "apply_to_ready_p50_ms", "failed_crs")}
         # amdsmi counters of the advertised GPUs at the end of the timed region (node agent)
         out["gpu_telemetry"] = gpu_tel
         if xgmi is not None:
@@ -494,10 +519,13 @@ def run(args):
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
-    # a step is ~10 ms at N=1: 50 timed steps keep the measured window around half a second
-    ap.add_argument("--steps", type=int, default=50)
+    # a step is 10 rounds of 100 tenants per rank, ~120 ms at N=1: the driver's 20 timed
+    # steps span ~2.5 s, long enough for a stable rate and p99, while no more than 100
+    # tenants per rank are ever on their way to Ready at once (BASELINE config #3)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=100, help="UserBootstraps applied per rank per step")
+    ap.add_argument("--batch", type=int, default=100, help="UserBootstraps applied per rank per round")
+    ap.add_argument("--rounds", type=int, default=10, help="rounds of --batch tenants per step")
     ap.add_argument("--concurrency", type=int, default=100,
                     help="in-flight creates (BASELINE config #3: 100 concurrent CRs on the node)")
     ap.add_argument("--concurrency-scope", choices=("total", "rank"), default="total",
@@ -505,6 +533,10 @@ def main(argv=None):
     ap.add_argument("--tuned-phase", action=argparse.BooleanOptionalAction, default=True,
                     help="also measure a secondary phase with the offered load sized to the CPU share")
     ap.add_argument("--tuned-concurrency", type=int, default=0, help="0 = auto_concurrency()")
+    ap.add_argument("--webhook-protocol", choices=("h2", "http/1.1"), default="h2",
+                    help="API server -> admission webhook transport of the headline phase")
+    ap.add_argument("--http1-phase", action=argparse.BooleanOptionalAction, default=True,
+                    help="with --webhook-protocol h2: also time the webhook over HTTP/1.1 (secondary field)")
     ap.add_argument("--timeout", type=float, default=120.0)
     ap.add_argument("--controller-workers", type=int, default=0, help="0 = 16")
     ap.add_argument("--sync-workers", type=int, default=0, help="0 = 16")

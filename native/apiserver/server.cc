@@ -592,12 +592,16 @@ struct ApiServer::Impl {
   };
   std::map<const Value*, FastHook> hook_fast;  // guarded by hook_mu
   std::map<std::string, std::shared_ptr<http::Client>> hook_clients;
+  // webhook transport for new clients (--webhook-http2; switchable at run time through
+  // POST /_kl/webhook-protocol so one bench run can time both)
+  std::atomic<bool> webhook_h2{false};
 
   std::atomic<uint64_t> requests{0};
   std::atomic<uint64_t> faults_hit{0};
   LockStats types_stats;  // types_mu accounting
 
   explicit Impl(Options o) : opts(std::move(o)) {
+    webhook_h2 = opts.webhook_http2;
     for (const ResourceType* rt : kube::types::builtin()) {
       TypeInfo ti;
       ti.rt = *rt;
@@ -896,7 +900,7 @@ struct ApiServer::Impl {
     http::ClientOptions o;
     o.base_url = base;
     o.tls_server_name = server_name;
-    o.http2 = opts.webhook_http2;
+    o.http2 = webhook_h2.load();
     o.h2_connections = opts.webhook_h2_connections;
     if (base.rfind("https", 0) == 0) {
       o.tls = net::TlsContext::client(ca.empty() ? "" : crypto::base64_decode(ca), false);
@@ -2108,6 +2112,22 @@ struct ApiServer::Impl {
       std::lock_guard<std::mutex> lk(fault_mu);
       faults.clear();
       w.send_json(200, "{}");
+      return;
+    }
+    if (req.path == "/_kl/webhook-protocol" && req.method == "POST") {
+      // body "h2" or "http/1.1": later webhook calls use fresh clients of that protocol
+      const bool h2 = req.body == "h2";
+      if (!h2 && req.body != "http/1.1") {
+        w.send(400, "body must be h2 or http/1.1\n");
+        return;
+      }
+      {
+        std::lock_guard<std::mutex> lk(hook_mu);
+        webhook_h2 = h2;
+        hook_fast.clear();
+        hook_clients.clear();
+      }
+      w.send(200, h2 ? "h2\n" : "http/1.1\n");
       return;
     }
     if (req.path == "/_kl/compact" && req.method == "POST") {
