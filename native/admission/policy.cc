@@ -1,6 +1,7 @@
 #include "admission/policy.h"
 
 #include <algorithm>
+#include <iterator>
 
 #include "core/crypto.h"
 #include "core/json_patch.h"
@@ -120,9 +121,9 @@ Decision mutate(const Value& req, const Config& cfg) {
   }
 
   // rule 12: must parse as UserBootstrap
-  crd::UserBootstrap ub;
+  crd::UserBootstrapShape ub;
   try {
-    ub = crd::parse_userbootstrap(obj);
+    ub = crd::inspect_userbootstrap(obj);
   } catch (const std::exception& e) {
     LOG_ERROR("admission") << "Request is not UserBootstrap resource: " << e.what();
     return invalid(uid, e.what(), 12);
@@ -132,7 +133,7 @@ Decision mutate(const Value& req, const Config& cfg) {
   if (username.kind == UserKind::Normal) {
     // rule 13: always (over)write kube_username for normal users
     patches.add("/spec/kube_username", Value(username.kube_username));
-  } else if (!ub.has_kube_username || ub.kube_username.empty()) {
+  } else if (!ub.kube_username || ub.kube_username->empty()) {
     // rule 14
     return deny(uid, "kube_username field is empty. you are an admin, so fill it", 14);
   }
@@ -146,7 +147,7 @@ Decision mutate(const Value& req, const Config& cfg) {
     // rule 16: default RoleBinding (two ops, exactly as the reference emits them)
     patches.add("/spec/rolebinding", Value::object());
     const std::string subject_name =
-        username.kind == UserKind::Normal ? username.original_username : ub.kube_username;
+        username.kind == UserKind::Normal ? username.original_username : *ub.kube_username;
     Value rb = Value::object();
     rb["role_ref"] = Value::object({{"apiGroup", "rbac.authorization.k8s.io"},
                                     {"kind", "ClusterRole"},
@@ -190,6 +191,26 @@ Value review_response(const Decision& d, const std::string& api_version) {
   return review;
 }
 
+namespace {
+
+// What handle_review and mutate() read from an AdmissionReview (reference
+// src/admission.rs:184-431): the request's identity and user, the object's name and the
+// parts of a UserBootstrap (spec, status), and only the shape of everything else — the
+// request's oldObject and both objects' managedFields are the bulk of an UPDATE review
+// and are never looked at.
+using P = json::Projection;
+const P kObjectMeta[] = {{"name", P::Keep}, {"uid", P::Keep}, {"resourceVersion", P::Keep}};
+const P kObject[] = {{"apiVersion", P::Keep}, {"kind", P::Keep}, {"spec", P::Keep}, {"status", P::Keep},
+                     {"metadata", P::Descend, kObjectMeta, std::size(kObjectMeta)}};
+const P kOldObject[] = {{"metadata", P::Shape}};
+const P kRequest[] = {{"uid", P::Keep}, {"operation", P::Keep}, {"userInfo", P::Keep},
+                      {"object", P::Descend, kObject, std::size(kObject)},
+                      {"oldObject", P::Descend, kOldObject, std::size(kOldObject)}};
+const P kReview[] = {{"apiVersion", P::Keep}, {"kind", P::Keep}, {"request", P::Descend, kRequest, std::size(kRequest)}};
+const P kReviewRoot{"", P::Descend, kReview, std::size(kReview)};
+
+}  // namespace
+
 HttpResult handle_review(const std::string& body, const std::string& content_type, const Config& cfg) {
   HttpResult r;
   if (content_type.find("application/json") == std::string::npos) {
@@ -200,7 +221,7 @@ HttpResult handle_review(const std::string& body, const std::string& content_typ
   }
   Value review;
   std::string err;
-  if (!json::try_parse(body, review, &err)) {
+  if (!json::try_parse_projected(body, kReviewRoot, review, &err)) {
     r.status = 400;
     r.content_type = "text/plain; charset=utf-8";
     r.body = "Failed to parse the request body as JSON: " + err;

@@ -5,6 +5,7 @@
 #include <sys/time.h>
 #include <ucontext.h>
 #include <unistd.h>
+#include <unwind.h>
 
 #include <atomic>
 #include <cerrno>
@@ -35,6 +36,32 @@ std::atomic<size_t> g_next{0};
 std::atomic<bool> g_on{false};
 std::atomic<uint64_t> g_dropped{0};
 int g_probe[2] = {-1, -1};
+// BGC_CPU_PROFILE_UNWIND=eh: walk with the .eh_frame unwinder (libgcc) instead of frame
+// pointers.  OpenSSL and glibc are built without frame pointers (they use %rbp as a
+// general register), so a frame-pointer walk that starts inside them ends at once and the
+// sample cannot be charged to the bgc code that called them; the unwinder follows the CFI
+// those libraries ship.  _Unwind_Backtrace is not formally async-signal-safe; glibc's
+// dl_iterate_phdr lock it takes is recursive, and the profiler is a diagnostics mode only.
+bool g_eh = false;
+
+struct EhWalk {
+  Sample* s;
+  int skip;  // frames of the signal handler itself
+};
+
+_Unwind_Reason_Code eh_frame(struct _Unwind_Context* ctx, void* arg) {
+  auto* w = static_cast<EhWalk*>(arg);
+  const uintptr_t ip = _Unwind_GetIP(ctx);
+  if (ip == 0) return _URC_END_OF_STACK;
+  if (w->skip > 0) {
+    --w->skip;
+    return _URC_NO_REASON;
+  }
+  if (w->s->n >= kMaxFrames) return _URC_END_OF_STACK;
+  w->s->pc[w->s->n] = ip - 1;  // return addresses: attribute to the call instruction
+  w->s->n++;
+  return _URC_NO_REASON;
+}
 std::string g_path;
 std::mutex g_mu;
 bool g_started = false;
@@ -60,6 +87,30 @@ void on_sigprof(int, siginfo_t*, void* ucv) {
   }
   auto* uc = static_cast<ucontext_t*>(ucv);
   Sample& s = g_buf[i];
+  if (g_eh) {
+    // frames: eh_frame's caller chain starts in this handler, then the kernel's signal
+    // trampoline (__restore_rt), then the interrupted function
+    s.n = 0;
+    EhWalk w{&s, 0};
+    _Unwind_Backtrace(eh_frame, &w);
+    // drop the handler's own frames and the signal trampoline: the unwinder reports the
+    // interrupted pc itself (not a return address) right after the trampoline
+    const uintptr_t rip = static_cast<uintptr_t>(uc->uc_mcontext.gregs[REG_RIP]);
+    uint32_t start = 0;
+    for (uint32_t k = 0; k < s.n; ++k) {
+      if (s.pc[k] + 1 == rip || s.pc[k] == rip) {
+        start = k;
+        break;
+      }
+    }
+    if (start > 0) {
+      for (uint32_t k = start; k < s.n; ++k) s.pc[k - start] = s.pc[k];
+      s.n -= start;
+    }
+    if (s.n > 0) s.pc[0] = rip;
+    errno = saved_errno;
+    return;
+  }
   uint32_t n = 0;
   s.pc[n++] = static_cast<uintptr_t>(uc->uc_mcontext.gregs[REG_RIP]);
   uintptr_t sp = static_cast<uintptr_t>(uc->uc_mcontext.gregs[REG_RSP]);
@@ -109,6 +160,12 @@ bool start(const std::string& path, int hz) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (g_started) return true;
   if (::pipe2(g_probe, O_CLOEXEC | O_NONBLOCK) != 0) return false;
+  if (const char* u = std::getenv("BGC_CPU_PROFILE_UNWIND"); u && std::string(u) == "eh") {
+    g_eh = true;
+    Sample warm{};
+    EhWalk w{&warm, 0};
+    _Unwind_Backtrace(eh_frame, &w);  // first use outside a signal handler: lazy setup
+  }
   g_buf = static_cast<Sample*>(std::calloc(kMaxSamples, sizeof(Sample)));
   if (!g_buf) return false;
   g_path = path;

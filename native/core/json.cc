@@ -436,6 +436,15 @@ class Parser {
     return v;
   }
 
+  Value parse_document(const Projection& root) {
+    Value v;
+    skip_ws();
+    parse_projected(v, 0, &root);
+    skip_ws();
+    if (p_ != s_.size()) fail("trailing characters");
+    return v;
+  }
+
  private:
   [[noreturn]] void fail(const std::string& msg) const {
     size_t line = 1, col = 1;
@@ -578,6 +587,127 @@ class Parser {
         }
         fail("expected value");
     }
+  }
+
+  // Projection-driven parse (see json::Projection).  `p` null = not named: Shape.
+  void parse_projected(Value& out, int depth, const Projection* p) {
+    if (p && p->mode == Projection::Keep) {
+      parse_value(out, depth);
+      return;
+    }
+    if (!p || p->mode == Projection::Shape || p_ >= s_.size() || s_[p_] != '{') {
+      if (p && p->mode == Projection::Descend) {  // not an object: keep it whole (type errors stay visible)
+        parse_value(out, depth);
+        return;
+      }
+      shape_value(out, depth);
+      return;
+    }
+    if (depth > 512) fail("recursion limit exceeded");
+    ++p_;
+    out.type_ = Type::Object;
+    skip_ws();
+    if (p_ < s_.size() && s_[p_] == '}') {
+      ++p_;
+      return;
+    }
+    const size_t base = vals_.size();
+    const size_t kbase = keys_.size();
+    while (true) {
+      skip_ws();
+      if (p_ >= s_.size() || s_[p_] != '"') fail("key must be a string");
+      std::string key;
+      parse_string(key);
+      skip_ws();
+      if (p_ >= s_.size() || s_[p_] != ':') fail("expected `:`");
+      ++p_;
+      skip_ws();
+      const Projection* child = nullptr;
+      for (size_t i = 0; i < p->n_children; ++i) {
+        if (p->children[i].key == key) {
+          child = &p->children[i];
+          break;
+        }
+      }
+      Value v;
+      parse_projected(v, depth + 1, child);
+      bool dup = false;
+      for (size_t i = kbase; i < keys_.size(); ++i) {
+        if (keys_[i] == key) {
+          vals_[base + (i - kbase)] = std::move(v);
+          dup = true;
+          break;
+        }
+      }
+      if (!dup) {
+        keys_.push_back(std::move(key));
+        vals_.push_back(std::move(v));
+      }
+      skip_ws();
+      if (p_ >= s_.size()) fail("EOF while parsing an object");
+      if (s_[p_] == ',') {
+        ++p_;
+        continue;
+      }
+      if (s_[p_] == '}') {
+        ++p_;
+        finish_object(out, base, kbase);
+        return;
+      }
+      fail("expected `,` or `}`");
+    }
+  }
+
+  // Validates one value exactly as parse_value would, building nothing but an empty value
+  // of the same type.
+  void shape_value(Value& out, int depth) {
+    if (depth > 512) fail("recursion limit exceeded");
+    if (p_ >= s_.size()) fail("EOF while parsing a value");
+    const char c = s_[p_];
+    if (c == '"') {
+      static thread_local std::string scratch;
+      parse_string(scratch);
+      out = Value(std::string());
+      return;
+    }
+    if (c == '[' || c == '{') {
+      const bool obj = c == '{';
+      ++p_;
+      out = obj ? Value::object() : Value::array();
+      skip_ws();
+      if (p_ < s_.size() && s_[p_] == (obj ? '}' : ']')) {
+        ++p_;
+        return;
+      }
+      while (true) {
+        skip_ws();
+        if (obj) {
+          if (p_ >= s_.size() || s_[p_] != '"') fail("key must be a string");
+          static thread_local std::string key;
+          parse_string(key);
+          skip_ws();
+          if (p_ >= s_.size() || s_[p_] != ':') fail("expected `:`");
+          ++p_;
+          skip_ws();
+        }
+        Value child;
+        shape_value(child, depth + 1);
+        skip_ws();
+        if (p_ >= s_.size()) fail(obj ? "EOF while parsing an object" : "EOF while parsing a list");
+        if (s_[p_] == ',') {
+          ++p_;
+          continue;
+        }
+        if (s_[p_] == (obj ? '}' : ']')) {
+          ++p_;
+          return;
+        }
+        fail(obj ? "expected `,` or `}`" : "expected `,` or `]`");
+      }
+    }
+    parse_value(out, depth);  // literal or number: nothing to save
+    if (out.is_number()) out = Value(0);
+    else if (out.is_bool()) out = Value(false);
   }
 
   static int hexval(char c) {
@@ -853,6 +983,18 @@ std::string_view raw_member(std::string_view t, std::string_view key) {
 
 Value parse(std::string_view text) { return Parser(text).parse_document(); }
 Value parse(std::string_view text, std::string_view drop_key) { return Parser(text, drop_key).parse_document(); }
+
+Value parse_projected(std::string_view text, const Projection& root) { return Parser(text).parse_document(root); }
+
+bool try_parse_projected(std::string_view text, const Projection& root, Value& out, std::string* err) {
+  try {
+    out = parse_projected(text, root);
+    return true;
+  } catch (const ParseError& e) {
+    if (err) *err = e.what();
+    return false;
+  }
+}
 
 bool try_parse(std::string_view text, Value& out, std::string* err) {
   try {

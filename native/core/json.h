@@ -139,6 +139,25 @@ Value parse(std::string_view text);
 Value parse(std::string_view text, std::string_view drop_key);
 // Parses; returns false (and fills err) instead of throwing.
 bool try_parse(std::string_view text, Value& out, std::string* err = nullptr);
+
+// Selective parsing: only the members a projection names are built.  Every other value is
+// still fully validated (the same syntax errors as parse) but stands in the result as an
+// empty value of its own type ("", 0, false, {}, []), so a caller that only tests the
+// type or presence of those members sees the same answers without the allocations of
+// big subtrees (an AdmissionReview's oldObject and managedFields).
+struct Projection {
+  enum Mode : uint8_t {
+    Keep,     // build the whole value
+    Shape,    // validate; keep only its type
+    Descend,  // an object: `children` name the members to build, the rest is Shape
+  };
+  std::string_view key;
+  Mode mode = Keep;
+  const Projection* children = nullptr;
+  size_t n_children = 0;
+};
+Value parse_projected(std::string_view text, const Projection& root);
+bool try_parse_projected(std::string_view text, const Projection& root, Value& out, std::string* err = nullptr);
 // Raw text of a top-level object member's value (structural scan: no parsing, no
 // allocation), e.g. raw_member(review, "request") for logging a received document
 // without re-serializing it.  Empty when `text` is not an object or has no such key;

@@ -168,9 +168,36 @@ bool type_matches(const Value& v, const std::string& t) {
   return true;
 }
 
-std::string join_path(const std::string& base, const std::string& key) { return base.empty() ? key : base + "." + key; }
+// The path of the node being validated, kept as segments and rendered only when an error
+// is recorded: building "spec.role.rules[3].verbs" strings for every visited node made the
+// walk allocation-bound (admission runs it on every review, reference admission.rs:341-347).
+struct PathStack {
+  struct Seg {
+    std::string_view key;
+    size_t index;  // SIZE_MAX: a key segment
+  };
+  std::vector<Seg> segs;
+  std::string render() const {
+    std::string out;
+    for (const auto& g : segs) {
+      if (g.index != SIZE_MAX) {
+        out += "[" + std::to_string(g.index) + "]";
+      } else {
+        if (!out.empty()) out += ".";
+        out.append(g.key);
+      }
+    }
+    return out;
+  }
+  std::string render_with(std::string_view key) const {
+    std::string out = render();
+    if (!out.empty()) out += ".";
+    out.append(key);
+    return out;
+  }
+};
 
-void validate_rec(const Value& v, const Value& s, const std::string& path, const ValidateOptions& opts,
+void validate_rec(const Value& v, const Value& s, PathStack& path, const ValidateOptions& opts,
                   std::vector<ValidationError>& errs) {
   if (!s.is_object()) return;
   if (v.is_null()) {
@@ -178,16 +205,16 @@ void validate_rec(const Value& v, const Value& s, const std::string& path, const
     // Absent-vs-null: for serde Option<T> fields null is fine; a non-nullable null is
     // a type error.
     const Value& t = s.get("type");
-    if (t.is_string()) errs.push_back({path, "null", "expected " + t.as_string()});
+    if (t.is_string()) errs.push_back({path.render(), "null", "expected " + t.as_string()});
     return;
   }
   const Value& t = s.get("type");
   if (t.is_string() && !type_matches(v, t.as_string())) {
-    errs.push_back({path, "type", "expected " + t.as_string()});
+    errs.push_back({path.render(), "type", "expected " + t.as_string()});
     return;
   }
   if (const Value* fmt = s.find("format"); fmt && fmt->is_string() && fmt->as_string() == "date-time") {
-    if (v.is_string() && !is_rfc3339(v.as_string())) errs.push_back({path, "format", "expected RFC 3339 date-time"});
+    if (v.is_string() && !is_rfc3339(v.as_string())) errs.push_back({path.render(), "format", "expected RFC 3339 date-time"});
   }
   if (v.is_object()) {
     const Value& props = s.get("properties");
@@ -195,25 +222,35 @@ void validate_rec(const Value& v, const Value& s, const std::string& path, const
       const auto& keys = props.keys();
       const auto& vals = props.values();
       for (size_t i = 0; i < keys.size(); ++i) {
-        if (const Value* child = v.find(keys[i])) validate_rec(*child, vals[i], join_path(path, keys[i]), opts, errs);
+        if (const Value* child = v.find(keys[i])) {
+          path.segs.push_back({keys[i], SIZE_MAX});
+          validate_rec(*child, vals[i], path, opts, errs);
+          path.segs.pop_back();
+        }
       }
     }
     if (const Value* req = s.find("required"); req && req->is_array()) {
       for (const auto& r : req->items()) {
         const std::string& k = r.as_string();
         if (opts.serde && k == "metadata") continue;
-        if (!v.contains(k)) errs.push_back({join_path(path, k), "required", "missing field `" + k + "`"});
+        if (!v.contains(k)) errs.push_back({path.render_with(k), "required", "missing field `" + k + "`"});
       }
     }
     if (const Value* ap = s.find("additionalProperties"); ap && ap->is_object()) {
       const auto& keys = v.keys();
       const auto& vals = v.values();
-      for (size_t i = 0; i < keys.size(); ++i) validate_rec(vals[i], *ap, join_path(path, keys[i]), opts, errs);
+      for (size_t i = 0; i < keys.size(); ++i) {
+        path.segs.push_back({keys[i], SIZE_MAX});
+        validate_rec(vals[i], *ap, path, opts, errs);
+        path.segs.pop_back();
+      }
     }
   } else if (v.is_array()) {
     if (const Value* items = s.find("items")) {
       for (size_t i = 0; i < v.size(); ++i) {
-        validate_rec(v[i], *items, path + "[" + std::to_string(i) + "]", opts, errs);
+        path.segs.push_back({{}, i});
+        validate_rec(v[i], *items, path, opts, errs);
+        path.segs.pop_back();
       }
     }
   }
@@ -273,7 +310,8 @@ std::string serde_expected(const std::string& detail) {
 
 std::vector<ValidationError> validate(const Value& value, const Value& schema, const ValidateOptions& opts) {
   std::vector<ValidationError> errs;
-  validate_rec(value, schema, "", opts, errs);
+  PathStack path;
+  validate_rec(value, schema, path, opts, errs);
   return errs;
 }
 
@@ -285,13 +323,24 @@ std::string serde_error_message(const Value& value, const ValidationError& e) {
   return "invalid type: " + got + ", expected " + serde_expected(e.detail) + " at " + e.path;
 }
 
-UserBootstrap parse_userbootstrap(const Value& obj) {
+UserBootstrapShape inspect_userbootstrap(const Value& obj) {
   if (!obj.is_object()) throw std::runtime_error("invalid type: " + serde_unexpected(obj) + ", expected struct UserBootstrap");
   ValidateOptions o;
   o.serde = true;
   auto errs = validate(obj, userbootstrap_schema(), o);
   if (!errs.empty()) throw std::runtime_error(serde_error_message(obj, errs.front()));
   if (!obj.contains("metadata")) throw std::runtime_error("missing field `metadata`");
+  UserBootstrapShape sh;
+  const Value& spec = obj.get("spec");
+  if (const Value* ku = spec.find("kube_username"); ku && !ku->is_null()) sh.kube_username = &ku->as_string();
+  if (const Value* q = spec.find("quota"); q && !q->is_null()) sh.has_quota = true;
+  if (const Value* r = spec.find("role"); r && !r->is_null()) sh.has_role = true;
+  if (const Value* rb = spec.find("rolebinding"); rb && !rb->is_null()) sh.has_rolebinding = true;
+  return sh;
+}
+
+UserBootstrap parse_userbootstrap(const Value& obj) {
+  (void)inspect_userbootstrap(obj);  // validation (throws)
   UserBootstrap ub;
   ub.raw = obj;
   const Value& meta = obj.get("metadata");

@@ -84,6 +84,16 @@ struct UserBootstrap {
 // Throws std::runtime_error with a serde-style message on type errors.
 UserBootstrap parse_userbootstrap(const json::Value& obj);
 
+// The same validation as parse_userbootstrap, returning only which spec fields are set (no
+// copies): what the admission policy needs on every review.  Pointers alias `obj`.
+struct UserBootstrapShape {
+  const std::string* kube_username = nullptr;  // null when absent or null
+  bool has_quota = false;
+  bool has_role = false;
+  bool has_rolebinding = false;
+};
+UserBootstrapShape inspect_userbootstrap(const json::Value& obj);
+
 bool is_rfc3339(const std::string& s);
 
 }  // namespace bgc::crd

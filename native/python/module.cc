@@ -7,6 +7,8 @@
 #include "core/env_config.h"
 #include "core/json.h"
 #include "core/json_patch.h"
+#include <memory>
+#include <vector>
 #include "core/yaml.h"
 #include "crd/schema.h"
 #include "core/log.h"
@@ -32,6 +34,58 @@ std::string json_to_yaml(const std::string& j) { return bgc::yaml::emit(bgc::jso
 
 std::string json_roundtrip(const std::string& j, const std::string& drop_key) {
   return (drop_key.empty() ? bgc::json::parse(j) : bgc::json::parse(j, drop_key)).dump();
+}
+
+// A json::Projection built from dotted paths ("request.object.spec"): every path is
+// Descend along the way and Keep at its end.  Nodes live in `store`.
+struct ProjectionTree {
+  std::vector<std::string> keys;  // backing storage for the string_views
+  struct Node {
+    std::string key;
+    bool keep = false;
+    std::vector<Node> kids;
+  };
+  Node root;
+  std::vector<std::unique_ptr<std::vector<bgc::json::Projection>>> store;
+  bgc::json::Projection build(const Node& n) {
+    bgc::json::Projection p;
+    p.key = n.key;
+    if (n.keep) {
+      p.mode = bgc::json::Projection::Keep;
+      return p;
+    }
+    p.mode = bgc::json::Projection::Descend;
+    auto v = std::make_unique<std::vector<bgc::json::Projection>>();
+    for (const auto& k : n.kids) v->push_back(build(k));
+    p.children = v->data();
+    p.n_children = v->size();
+    store.push_back(std::move(v));
+    return p;
+  }
+};
+
+std::string json_parse_projected(const std::string& text, const std::vector<std::string>& keep) {
+  ProjectionTree t;
+  for (const auto& path : keep) {
+    ProjectionTree::Node* n = &t.root;
+    size_t start = 0;
+    while (true) {
+      size_t dot = path.find('.', start);
+      std::string k = path.substr(start, dot == std::string::npos ? std::string::npos : dot - start);
+      ProjectionTree::Node* next = nullptr;
+      for (auto& c : n->kids)
+        if (c.key == k) next = &c;
+      if (!next) {
+        n->kids.push_back({k, false, {}});
+        next = &n->kids.back();
+      }
+      n = next;
+      if (dot == std::string::npos) break;
+      start = dot + 1;
+    }
+    n->keep = true;
+  }
+  return bgc::json::parse_projected(text, t.build(t.root)).dump();
 }
 
 std::string apply_json_patch(const std::string& doc, const std::string& patch) {
@@ -79,6 +133,7 @@ PYBIND11_MODULE(_native, m) {
   m.def("json_roundtrip", &json_roundtrip, py::arg("text"), py::arg("drop_key") = "");
   m.def("yaml_to_json", &yaml_to_json);
   m.def("json_to_yaml", &json_to_yaml);
+  m.def("json_parse_projected", &json_parse_projected, py::arg("text"), py::arg("keep"));
   m.def("json_raw_member", [](const std::string& text, const std::string& key) {
     return std::string(bgc::json::raw_member(text, key));
   });

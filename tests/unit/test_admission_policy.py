@@ -253,3 +253,35 @@ def test_property_matches_oracle(nat, cfg, op, username, grp, name, spec, has_ob
     assert invalid == (kind == "invalid")
     assert msg == omsg
     assert patch == opatch
+
+
+MANAGED = [{"manager": "kubectl", "operation": "Update", "apiVersion": "bacchus.io/v1", "time": "2024-01-01T00:00:00Z",
+            "fieldsType": "FieldsV1", "fieldsV1": {"f:spec": {"f:quota": {".": {}, "f:hard": {"f:requests.cpu": {}}}}}}]
+
+
+@settings(max_examples=300, deadline=None)
+@given(op=st.sampled_from(["CREATE", "UPDATE", "DELETE", "CONNECT"]), username=usernames, grp=groups,
+       name=st.one_of(st.none(), names), spec=specs, has_obj=st.booleans(), old=st.booleans(),
+       status=st.one_of(st.none(), st.booleans()))
+def test_http_review_projection_matches_full_parse(nat, cfg, op, username, grp, name, spec, has_obj, old, status):
+    """handle_review parses only what mutate() reads (json::Projection: uid, operation,
+    userInfo, object name/spec/status; the shape of the rest).  Its decision equals mutate()
+    on the fully parsed request, with managedFields, labels and oldObject present."""
+    req = request(op=op, username=username, groups=grp, name=name, spec=spec, obj=has_obj)
+    if has_obj:
+        req["object"]["metadata"].update({"managedFields": MANAGED, "labels": {"a": "b"}, "resourceVersion": "7",
+                                          "uid": "0-1", "annotations": {"x": "y" * 200}})
+        if status is not None:
+            req["object"]["status"] = {"synchronized_with_sheet": status}
+    if old:
+        req["oldObject"] = {"apiVersion": "bacchus.io/v1", "kind": "UserBootstrap",
+                            "metadata": {"name": "alice", "managedFields": MANAGED}, "spec": {"quota": {"hard": {}}}}
+    review = {"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview", "request": req}
+    status_code, body, _ = nat.admission_handle_review(json.dumps(review), "application/json", cfg)
+    assert status_code == 200
+    resp = json.loads(body)["response"]
+    allowed, invalid, msg, patch, _ = run(nat, cfg, req)
+    assert resp["uid"] == "u-1" and resp["allowed"] == allowed
+    assert resp.get("status", {}).get("message") == (msg or None if not allowed else None)
+    got = json.loads(base64.b64decode(resp["patch"])) if "patch" in resp else None
+    assert got == patch

@@ -139,3 +139,62 @@ def test_raw_member_matches_parse(nat, obj, pretty):
         assert json.loads(raw) == v
     assert nat.json_raw_member(text, "\x00missing") == ""
     assert nat.json_raw_member("[1, 2]", "a") == ""
+
+
+def _shape(v):
+    return {dict: {}, list: [], str: "", bool: False, type(None): None}.get(type(v), 0)
+
+
+def _project(v, tree):
+    """Python model of json::parse_projected: kept paths whole, the rest empty-of-type."""
+    if tree is True:
+        return v
+    if not isinstance(v, dict):
+        return v if tree else _shape(v)  # a Descend node that is not an object is kept whole
+    return {k: (_project(x, tree[k]) if k in tree else _shape(x)) for k, x in v.items()}
+
+
+def _tree(paths):
+    t = {}
+    for p in paths:
+        node = t
+        parts = p.split(".")
+        for k in parts[:-1]:
+            node = node.setdefault(k, {})
+            if node is True:
+                break
+        else:
+            node[parts[-1]] = True
+    return t
+
+
+@settings(max_examples=300, deadline=None)
+@given(json_values(st.none() | st.booleans() | I64 | FLOATS | st.text(alphabet="ab.", max_size=3)),
+       st.lists(st.sampled_from(["a", "b", "a.a", "a.b", "b.a.a", "a.b.a"]), max_size=3))
+def test_projected_parse_matches_model(nat, v, keep):
+    """parse_projected keeps the named paths and only the type of everything else (the
+    AdmissionReview fast path of admission/policy.cc)."""
+    doc = {"a": v, "b": {"a": v, "b": [v]}} if not isinstance(v, dict) else v
+    text = json.dumps(doc)
+    assert json.loads(nat.json_parse_projected(text, keep)) == _project(doc, _tree(keep) or {})
+
+
+@settings(max_examples=300, deadline=None)
+@given(json_values(st.none() | st.booleans() | I64 | TEXT), st.integers(min_value=0, max_value=200),
+       st.sampled_from(["", "x", "{", "]", "\\", "\"", ",", "1e", "tru", "\u0001"]))
+def test_projected_parse_rejects_what_parse_rejects(nat, v, pos, junk):
+    """Skipped subtrees are still validated: a corrupted document fails the projected parse
+    with the same error as the full parse."""
+    text = json.dumps({"keep": v, "skip": [v, {"deep": v}]})
+    pos = min(pos, len(text))
+    bad = text[:pos] + junk + text[pos:]
+    full = proj = None
+    try:
+        nat.json_roundtrip(bad)
+    except Exception as e:  # noqa: BLE001
+        full = str(e)
+    try:
+        nat.json_parse_projected(bad, ["keep"])
+    except Exception as e:  # noqa: BLE001
+        proj = str(e)
+    assert full == proj
