@@ -22,6 +22,7 @@
 #include <string>
 #include <thread>
 #include <unordered_map>
+#include <unordered_set>
 
 #include "core/metrics.h"
 #include <vector>
@@ -157,11 +158,13 @@ class WorkQueue {
   int idle_ = 0;                  // workers waiting on cv_
   bool timer_waiter_ = false;     // a worker is waiting on timer_cv_
   Clock::time_point timer_target_{};
-  std::map<std::string, Clock::time_point> due_;           // key -> due time
-  std::multimap<Clock::time_point, std::string> timeline_;  // due time -> key (may hold stale entries)
-  std::set<std::string> processing_;
-  std::map<std::string, Clock::time_point> deferred_;      // re-added while processing
-  std::set<std::string> forgotten_;                        // forgotten while processing
+  // Hash containers: under churn the queue holds a pending 30 s requeue for every live
+  // UserBootstrap, and ordered maps paid a chain of string compares per operation.
+  std::unordered_map<std::string, Clock::time_point> due_;       // key -> due time
+  std::multimap<Clock::time_point, std::string> timeline_;        // due time -> key (may hold stale entries)
+  std::unordered_set<std::string> processing_;
+  std::unordered_map<std::string, Clock::time_point> deferred_;  // re-added while processing
+  std::unordered_set<std::string> forgotten_;                    // forgotten while processing
   void add_after_locked(const std::string& key, Clock::time_point t);
   bool shutdown_ = false;
 };
