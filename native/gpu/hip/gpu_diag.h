@@ -15,7 +15,7 @@
 extern "C" {
 #endif
 
-#define BGC_DIAG_ABI_VERSION 7
+#define BGC_DIAG_ABI_VERSION 8
 #define BGC_DIAG_MAX_CU_KEYS 2048
 
 typedef struct {
@@ -88,6 +88,7 @@ typedef struct {
   uint64_t row_mismatches;  // C row sums that differ from A (B 1)  (after the first and the last launch)
   uint64_t col_mismatches;  // C column sums that differ from (1^T A) B
   int tile;                 // 256 (256x256 tile, 8 waves) or 128 (128x128, 4 waves)
+  int kernel;               // 2: 8-phase ping-pong (K % 128 == 0), 1: double-buffered
 } bgc_soak_result;
 
 // GEMM soak: an LDS-tiled (global_load_lds double buffering, XOR-swizzled LDS) bf16 MFMA

@@ -432,6 +432,164 @@ __global__ __launch_bounds__(64 * WM * WN, (BM * BN >= 256 * 256) ? 1 : 2) void 
       }
 }
 
+// ---------------------------------------------------------------------------
+// 256x256 ping-pong GEMM: the soak's kernel whenever K is a multiple of 128.
+//
+// The 2-buffer kernel above drains every K-tile's loads (vmcnt(0) + barrier) one tile
+// after issuing them; with one 512-thread block per CU a tile's 64 MFMAs per wave
+// (~0.9 us per SIMD) do not cover an HBM/L2 fetch under full load, and the matrix pipe
+// sat idle 42 % of the time (profiles/gemm_soak_r2/pmc_soak_8192.json).  This kernel
+// keeps the same LDS budget (two K-tiles, 128 KiB) but manages it in eight 16 KiB
+// half-tiles (A rows 0-127 / 128-255, Bt rows 0-127 / 128-255 of each K-tile):
+//
+//  * Two wave groups, waves 0-3 (output rows 0-127) and 4-7 (rows 128-255): each SIMD
+//    hosts one wave of each.  Group 1 runs one s_barrier behind group 0, so between any
+//    two barriers one wave of a SIMD issues its 16 MFMAs while its partner issues LDS
+//    fragment reads and global->LDS loads — matrix beside memory, never matrix beside
+//    matrix.
+//  * A phase is one C quadrant of the wave's 128x64 output (4x2 tiles of 16x16, K=64):
+//    16 v_mfma_f32_16x16x32_bf16.  Eight phases = two K-tiles per loop iteration.
+//    Fragments: all of the wave's B (64 columns) and half its A at phase 0, the other A
+//    half at phase 2 (192 VGPRs: 128 accumulator, 32 A, 32 B).
+//  * One half-tile load per phase, placed where the half it overwrites was last read
+//    (B halves are read only in the first phase of a K-tile, A halves in the first and
+//    third), so every load has 4-11 phases to land before it is read.  Waits are
+//    counted, vmcnt(4) at phases 3 and 7 (each half-tile is 2 glds per thread), and a
+//    half is first read one phase after the wait that retires it; loads stay in flight
+//    across the barriers.
+//  * Staging past the last K-tile re-reads the last tile into a buffer nobody reads
+//    again, so the vmcnt counts never change; the block drains (vmcnt(0)) before its
+//    epilogue.
+constexpr int kPPHalf = 128 * 128;  // one half-tile image: 128 rows x 64 k x 2 B
+
+__device__ __forceinline__ void pp_stage(char* lds, int half, const __bf16* __restrict__ src, int K, int row_base, int k0,
+                                         int wid, int lane) {
+  char* dst = lds + half * kPPHalf;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row0 = (i * 8 + wid) * 8;  // 8 rows of 128 B per wave-instruction
+    const int row = row0 + (lane >> 3);
+    const int chunk = (lane & 7) ^ (row & 7);  // LDS slot (lane & 7) holds source chunk ^ swizzle
+    const __bf16* g = src + static_cast<size_t>(row_base + row) * K + k0 + chunk * 8;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                     (__attribute__((address_space(3))) void*)(dst + row0 * 128), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void pp_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+__global__ __launch_bounds__(512, 1) void gemm_pingpong(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
+                                                        float* __restrict__ C, int M, int N, int K) {
+  __shared__ __attribute__((aligned(16))) char lds[8 * kPPHalf];  // [buf][A_top, A_bot, B_left, B_right]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;  // wave group = output row half
+  // XCD-aware bijective remap + 8 tile-rows grouped per B column tile (as gemm_soak)
+  const int nwg = static_cast<int>(gridDim.x), orig = static_cast<int>(blockIdx.x);
+  const int xcd = orig % 8, q = nwg / 8, r = nwg % 8;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+  const int tiles_m = M / 256, tiles_n = N / 256, group = 8;
+  const int per_group = group * tiles_n;
+  const int first_m = (wgid / per_group) * group;
+  const int gsize = min(tiles_m - first_m, group);
+  const int tm = first_m + (wgid % per_group) % gsize;
+  const int tn = (wgid % per_group) / gsize;
+  const int kt_n = K / kSoakBK;
+  const int a_row = tm * 256, b_row = tn * 256;
+  auto kofs = [&](int t) { return min(t, kt_n - 1) * kSoakBK; };
+  // half-tile images of buffer b: A_top 4b, A_bot 4b+1, B_left 4b+2, B_right 4b+3
+  auto stage = [&](int half, int t) {
+    const int h = half & 3;
+    if (h < 2) pp_stage(lds, half, A, K, a_row + h * 128, kofs(t), wid, lane);
+    else pp_stage(lds, half, Bt, K, b_row + (h - 2) * 128, kofs(t), wid, lane);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[4][2], bfr[4][2];
+
+  // prologue: K-tile 0 into buffer 0, K-tile 1's B halves into buffer 1
+  stage(0, 0);
+  stage(1, 0);
+  stage(2, 0);
+  stage(3, 0);
+  stage(6, 1);
+  stage(7, 1);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  pp_barrier();
+  if (wr == 1) pp_barrier();  // the stagger: group 1 runs one barrier behind
+
+  const int a_half = wr;            // A image this wave reads (per buffer)
+  const int b_half = 2 + (wc >> 1);  // Bt image
+  const int b_row0 = (wc & 1) * 64;  // first of the wave's 64 Bt rows inside that image
+
+  for (int it = 0; it < kt_n / 2; ++it) {
+    const int t_odd = 2 * it + 1, t_next = 2 * it + 2, t_next_odd = 2 * it + 3;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const char* buf = lds + (p >> 2) * 4 * kPPHalf;
+      if ((p & 3) == 0) {  // all of B, rows 0-63 of A
+        const char* bi = buf + b_half * kPPHalf;
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) bfr[ni][ks] = soak_frag(bi, b_row0 + ni * 16 + (lane & 15), ks * 4 + (lane >> 4));
+      }
+      if ((p & 1) == 0) {  // phases 0/2 (4/6): the A half this quadrant pair needs
+        const char* ai = buf + a_half * kPPHalf;
+        const int m0 = (p & 2) ? 64 : 0;
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) af[mi][ks] = soak_frag(ai, m0 + mi * 16 + (lane & 15), ks * 4 + (lane >> 4));
+      }
+      switch (p) {  // one half-tile per phase, each into a half nobody reads any more
+        case 0: stage(4, t_odd); break;      // buffer 1 A_top (read at phase 4)
+        case 1: stage(5, t_odd); break;      // buffer 1 A_bot
+        case 2: stage(2, t_next); break;     // buffer 0 B_left (last read at phase 0)
+        case 3: stage(3, t_next); break;     // buffer 0 B_right
+        case 4: stage(0, t_next); break;     // buffer 0 A_top (last read at phase 2)
+        case 5: stage(1, t_next); break;     // buffer 0 A_bot
+        case 6: stage(6, t_next_odd); break; // buffer 1 B_left (last read at phase 4)
+        default: stage(7, t_next_odd); break;
+      }
+      if ((p & 3) == 3) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // retires everything through phase p-2
+      pp_barrier();
+      __builtin_amdgcn_s_setprio(1);
+      const int mh = (p >> 1) & 1, nh = p & 1;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni)
+            acc[mh * 4 + mi][nh * 2 + ni] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi][ks], bfr[nh * 2 + ni][ks], acc[mh * 4 + mi][nh * 2 + ni], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      pp_barrier();
+    }
+  }
+  if (wr == 0) pp_barrier();  // matches group 1's extra barrier
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the block
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const size_t row = static_cast<size_t>(a_row + wr * 128 + mi * 16 + (lane >> 4) * 4 + j);
+        C[row * N + b_row + wc * 64 + ni * 16 + (lane & 15)] = acc[mi][ni][j];
+      }
+}
+
 // X[rows][cols] = hash-derived values in {-1, 0, 1} (exact in bf16)
 __global__ __launch_bounds__(kBlock) void soak_fill(__bf16* __restrict__ X, uint64_t n, uint32_t seed) {
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n;
@@ -550,8 +708,17 @@ bool soak_big_tile(int m, int n) {
   return (m % 256 == 0 && n % 256 == 0) && !(tile_env && std::string(tile_env) == "128");
 }
 
+// BGC_SOAK_KERNEL=2buf keeps the double-buffered kernel for A/B runs
+bool soak_pingpong(bool big, int k) {
+  const char* kern = std::getenv("BGC_SOAK_KERNEL");
+  return big && k % (2 * kSoakBK) == 0 && !(kern && std::string(kern) == "2buf");
+}
+
 void launch_soak_gemm(bool big, const void* a, const void* bt, void* c, int m, int n, int k, hipStream_t s) {
-  if (big) {
+  if (soak_pingpong(big, k)) {
+    hipLaunchKernelGGL(gemm_pingpong, dim3((m / 256) * (n / 256)), dim3(512), 0, s, static_cast<const __bf16*>(a),
+                       static_cast<const __bf16*>(bt), static_cast<float*>(c), m, n, k);
+  } else if (big) {
     hipLaunchKernelGGL((gemm_soak<256, 256, 2, 4>), dim3((m / 256) * (n / 256)), dim3(512), 0, s,
                        static_cast<const __bf16*>(a), static_cast<const __bf16*>(bt), static_cast<float*>(c), m, n, k);
   } else {
@@ -989,6 +1156,7 @@ int bgc_diag_gemm_soak(int device, int m, int n, int k, int launches, uint32_t s
   out->n = n;
   out->k = k;
   out->tile = big ? 256 : 128;
+  out->kernel = soak_pingpong(big, k) ? 2 : 1;
   out->launches = launches;
   out->elapsed_ms = total;
   out->tflops_best = flop / (best * 1e-3) / 1e12;

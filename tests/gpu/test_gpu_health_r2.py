@@ -213,6 +213,8 @@ def test_gemm_soak_lds_tiled_mfma_checksums():
     big = json.loads(n.diag_gemm_soak(0, 8192, 8192, 8192, 10))
     _dump("gemm_soak.json", {"small": small, "8192": big})
     assert all(r["passed"] for r in small) and [r["tile"] for r in small] == [128, 128, 256]
-    assert big["passed"] and big["tile"] == 256 and big["tflops_mean"] > 950
+    # 256x256 tiles with K % 128 == 0 run the 8-phase ping-pong kernel (profiles/gemm_soak_r3/)
+    assert [r["kernel"] for r in small] == ["2buf", "2buf", "pingpong"]
+    assert big["passed"] and big["tile"] == 256 and big["kernel"] == "pingpong" and big["tflops_mean"] > 950
     judged = json.loads(n.judge_diag(json.dumps({"soak": big})))
     assert judged["passed"], judged["failures"]
