@@ -1,0 +1,23 @@
+// Run a helper program as a child process and collect its output (kubeconfig exec
+// credential plugins, gcp auth-provider commands).  posix_spawn: the calling process is
+// never replaced, and no shell is involved.
+#pragma once
+
+#include <string>
+#include <utility>
+#include <vector>
+
+namespace bgc {
+
+struct RunResult {
+  int exit_code = -1;      // -1: did not exit normally (signal, timeout, spawn failure)
+  bool timed_out = false;
+  std::string out, err;
+};
+
+// argv[0] is looked up on PATH when it has no '/'.  `env` entries are added to (and
+// override) the parent's environment.  The child is killed after timeout_ms.
+RunResult run_command(const std::vector<std::string>& argv, const std::vector<std::pair<std::string, std::string>>& env,
+                      int timeout_ms);
+
+}  // namespace bgc

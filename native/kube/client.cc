@@ -10,7 +10,10 @@
 #include "core/log.h"
 #include "core/metrics.h"
 #include "core/net.h"
+#include "core/subprocess.h"
 #include "core/yaml.h"
+
+#include <ctime>
 
 namespace bgc::kube {
 
@@ -52,30 +55,83 @@ static std::string data_or_file(const Value& obj, const std::string& key, const 
   return net::read_file(f);
 }
 
-KubeConfig KubeConfig::from_kubeconfig(const std::string& path, const std::string& context) {
-  Value kc = yaml::parse(net::read_file(path));
-  std::string base_dir = path.substr(0, path.rfind('/'));
-  std::string ctx_name = context.empty() ? kc.get_string("current-context") : context;
-  const Value* ctx = nullptr;
-  for (const auto& c : kc.get("contexts").items()) {
-    if (c.get_string("name") == ctx_name) ctx = &c.get("context");
+namespace {
+
+std::string dir_of(const std::string& path) {
+  const size_t slash = path.rfind('/');
+  return slash == std::string::npos ? "." : path.substr(0, slash);
+}
+
+// Merges kubeconfig files: named entries of clusters/contexts/users keep the first
+// definition, each tagged with the directory of its file ("__dir").
+Value merge_kubeconfigs(const std::vector<std::string>& paths, std::vector<std::string>* loaded) {
+  Value merged = Value::object();
+  merged["clusters"] = Value::array();
+  merged["contexts"] = Value::array();
+  merged["users"] = Value::array();
+  for (const auto& path : paths) {
+    if (path.empty() || !file_exists(path)) continue;
+    Value kc = yaml::parse(net::read_file(path));
+    if (!kc.is_object()) continue;
+    loaded->push_back(path);
+    const std::string dir = dir_of(path);
+    if (merged.get_string("current-context").empty() && !kc.get_string("current-context").empty()) {
+      merged["current-context"] = kc.get_string("current-context");
+    }
+    for (const char* section : {"clusters", "contexts", "users"}) {
+      Value& dst = merged[section];
+      for (const auto& e : kc.get(section).items()) {
+        const std::string name = e.get_string("name");
+        bool seen = false;
+        for (const auto& d : dst.items()) seen = seen || d.get_string("name") == name;
+        if (seen) continue;
+        Value copy = e;
+        copy["__dir"] = dir;
+        dst.push_back(std::move(copy));
+      }
+    }
   }
-  if (!ctx) throw std::runtime_error("kubeconfig: context not found: " + ctx_name);
-  std::string cluster_name = ctx->get_string("cluster");
-  std::string user_name = ctx->get_string("user");
+  return merged;
+}
+
+const Value* named(const Value& list, const std::string& name, const char* field) {
+  for (const auto& e : list.items()) {
+    if (e.get_string("name") == name) return &e;
+  }
+  (void)field;
+  return nullptr;
+}
+
+}  // namespace
+
+KubeConfig KubeConfig::from_kubeconfig(const std::string& path, const std::string& context) {
+  if (!file_exists(path)) throw std::runtime_error("kubeconfig: cannot read " + path);
+  return from_kubeconfigs({path}, context);
+}
+
+KubeConfig KubeConfig::from_kubeconfigs(const std::vector<std::string>& paths, const std::string& context) {
+  std::vector<std::string> loaded;
+  Value kc = merge_kubeconfigs(paths, &loaded);
+  if (loaded.empty()) throw std::runtime_error("kubeconfig: none of the files exists");
+  std::string ctx_name = context.empty() ? kc.get_string("current-context") : context;
+  const Value* ctx_entry = named(kc.get("contexts"), ctx_name, "context");
+  if (!ctx_entry) throw std::runtime_error("kubeconfig: context not found: " + ctx_name);
+  const Value& ctx = ctx_entry->get("context");
+  std::string cluster_name = ctx.get_string("cluster");
+  std::string user_name = ctx.get_string("user");
   KubeConfig c;
-  for (const auto& cl : kc.get("clusters").items()) {
-    if (cl.get_string("name") != cluster_name) continue;
-    const Value& cv = cl.get("cluster");
+  if (const Value* cl = named(kc.get("clusters"), cluster_name, "cluster")) {
+    const Value& cv = cl->get("cluster");
+    const std::string dir = cl->get_string("__dir");
     c.server = cv.get_string("server");
-    c.ca_pem = data_or_file(cv, "certificate-authority", base_dir);
+    c.ca_pem = data_or_file(cv, "certificate-authority", dir);
     c.insecure = cv.get("insecure-skip-tls-verify").is_bool() && cv.get("insecure-skip-tls-verify").as_bool();
     c.tls_server_name = cv.get_string("tls-server-name");
   }
   if (c.server.empty()) throw std::runtime_error("kubeconfig: cluster not found: " + cluster_name);
-  for (const auto& u : kc.get("users").items()) {
-    if (u.get_string("name") != user_name) continue;
-    const Value& uv = u.get("user");
+  if (const Value* u = named(kc.get("users"), user_name, "user")) {
+    const Value& uv = u->get("user");
+    const std::string base_dir = u->get_string("__dir");
     c.token = uv.get_string("token");
     c.token_file = uv.get_string("tokenFile");
     // relative paths in a kubeconfig are relative to the kubeconfig file (client-go)
@@ -85,8 +141,42 @@ KubeConfig KubeConfig::from_kubeconfig(const std::string& path, const std::strin
     c.client_key_pem = data_or_file(uv, "client-key", base_dir);
     c.impersonate_user = uv.get_string("as");
     for (const auto& g : uv.get("as-groups").items()) c.impersonate_groups.push_back(g.as_string());
+    if (!uv.get_string("username").empty()) c.basic_auth = uv.get_string("username") + ":" + uv.get_string("password");
+    const Value& ex = uv.get("exec");
+    if (ex.is_object()) {
+      ExecPlugin e;
+      e.api_version = ex.get_string("apiVersion");
+      e.command = ex.get_string("command");
+      // a command with a path separator is relative to the kubeconfig (client-go); a bare
+      // name is looked up on PATH
+      if (e.command.find('/') != std::string::npos && e.command[0] != '/') {
+        while (e.command.rfind("./", 0) == 0) e.command.erase(0, 2);
+        e.command = base_dir + "/" + e.command;
+      }
+      for (const auto& a : ex.get("args").items()) e.args.push_back(a.as_string());
+      for (const auto& kv : ex.get("env").items()) e.env.emplace_back(kv.get_string("name"), kv.get_string("value"));
+      e.provide_cluster_info = ex.get("provideClusterInfo").is_bool() && ex.get("provideClusterInfo").as_bool();
+      if (e.command.empty()) throw std::runtime_error("kubeconfig: exec plugin of user " + user_name + " has no command");
+      if (e.api_version != "client.authentication.k8s.io/v1" && e.api_version != "client.authentication.k8s.io/v1beta1") {
+        throw std::runtime_error("kubeconfig: exec plugin apiVersion " + e.api_version + " is not supported");
+      }
+      c.exec = std::move(e);
+    }
+    const Value& ap = uv.get("auth-provider");
+    if (ap.is_object()) {
+      c.auth_provider = ap.get_string("name");
+      c.auth_provider_config = ap.get("config");
+      if (c.auth_provider == "oidc") {
+        // kube-client 0.84 without its `oidc` feature: the stored id-token, no refresh
+        c.token = c.auth_provider_config.get_string("id-token");
+        if (c.token.empty()) throw std::runtime_error("kubeconfig: no id-token for the oidc auth-provider");
+      } else if (c.auth_provider != "gcp") {
+        throw std::runtime_error("kubeconfig: auth-provider " + c.auth_provider + " is not supported");
+      }
+    }
   }
-  c.source = "kubeconfig:" + path;
+  c.source = "kubeconfig:";
+  for (size_t i = 0; i < loaded.size(); ++i) c.source += (i ? ":" : "") + loaded[i];
   return c;
 }
 
@@ -100,16 +190,22 @@ KubeConfig KubeConfig::infer() {
     c.source = "env";
     return c;
   }
-  std::string path;
-  if (const char* k = std::getenv("KUBECONFIG")) {
-    path = k;
-    size_t colon = path.find(':');
-    if (colon != std::string::npos) path = path.substr(0, colon);
-  } else if (const char* home = std::getenv("HOME")) {
-    std::string p = std::string(home) + "/.kube/config";
-    if (file_exists(p)) path = p;
+  if (const char* k = std::getenv("KUBECONFIG"); k && *k) {
+    std::vector<std::string> paths;
+    std::string v = k;
+    size_t start = 0;
+    while (true) {
+      size_t colon = v.find(':', start);
+      paths.push_back(v.substr(start, colon == std::string::npos ? std::string::npos : colon - start));
+      if (colon == std::string::npos) break;
+      start = colon + 1;
+    }
+    return from_kubeconfigs(paths);
   }
-  if (!path.empty()) return from_kubeconfig(path);
+  if (const char* home = std::getenv("HOME")) {
+    std::string p = std::string(home) + "/.kube/config";
+    if (file_exists(p)) return from_kubeconfig(p);
+  }
   return in_cluster();
 }
 
@@ -124,15 +220,159 @@ KubeClient::KubeClient(KubeConfig cfg) : cfg_(std::move(cfg)) {
   if (cfg_.server.rfind("https", 0) == 0) {
     o.tls = net::TlsContext::client(cfg_.ca_pem, cfg_.insecure, cfg_.client_cert_pem, cfg_.client_key_pem);
   }
+  if (cfg_.exec && cfg_.client_cert_pem.empty()) {
+    // an exec plugin may hand out a client certificate instead of (or with) a token: it
+    // has to be known before the TLS context is built
+    plugin_token(true);
+    if (!cfg_.client_cert_pem.empty() && o.tls) {
+      o.tls = net::TlsContext::client(cfg_.ca_pem, cfg_.insecure, cfg_.client_cert_pem, cfg_.client_key_pem);
+    }
+  }
   http_ = std::make_unique<http::Client>(o);
-  token_ = cfg_.token;
+  if (!has_plugin()) token_ = cfg_.token;
   token_read_ = std::chrono::steady_clock::now();
+}
+
+namespace {
+
+// RFC 3339 timestamp -> system_clock (false when malformed)
+bool parse_rfc3339(const std::string& s, std::chrono::system_clock::time_point* out) {
+  int Y, M, D, h, m, sec;
+  if (std::sscanf(s.c_str(), "%d-%d-%dT%d:%d:%d", &Y, &M, &D, &h, &m, &sec) != 6) return false;
+  std::tm tm{};
+  tm.tm_year = Y - 1900;
+  tm.tm_mon = M - 1;
+  tm.tm_mday = D;
+  tm.tm_hour = h;
+  tm.tm_min = m;
+  tm.tm_sec = sec;
+  time_t t = timegm(&tm);
+  size_t i = 19;
+  if (i < s.size() && s[i] == '.') {
+    ++i;
+    while (i < s.size() && std::isdigit(static_cast<unsigned char>(s[i]))) ++i;
+  }
+  if (i < s.size() && (s[i] == '+' || s[i] == '-') && i + 5 < s.size() + 1) {
+    int oh = 0, om = 0;
+    if (std::sscanf(s.c_str() + i + 1, "%d:%d", &oh, &om) == 2) {
+      const long off = (oh * 3600L + om * 60L) * (s[i] == '+' ? 1 : -1);
+      t -= off;
+    }
+  }
+  *out = std::chrono::system_clock::from_time_t(t);
+  return true;
+}
+
+// "{.credential.access_token}" -> value at that path of `v` (gcp auth-provider keys)
+std::string json_path_string(const Value& v, std::string key) {
+  if (!key.empty() && key.front() == '{') key = key.substr(1);
+  if (!key.empty() && key.back() == '}') key.pop_back();
+  const Value* cur = &v;
+  size_t start = key.empty() || key[0] != '.' ? 0 : 1;
+  while (cur && start <= key.size()) {
+    size_t dot = key.find('.', start);
+    std::string part = key.substr(start, dot == std::string::npos ? std::string::npos : dot - start);
+    if (!part.empty()) cur = cur->find(part);
+    if (dot == std::string::npos) break;
+    start = dot + 1;
+  }
+  return cur && cur->is_string() ? cur->as_string() : "";
+}
+
+}  // namespace
+
+std::string KubeClient::plugin_token(bool force) {
+  std::lock_guard<std::mutex> lk(token_mu_);
+  const auto now = std::chrono::system_clock::now();
+  if (!force && plugin_fetched_ && now + std::chrono::seconds(10) < token_expiry_) return token_;
+  static auto& refreshes = metrics::Registry::global().counter(
+      "bgc_kube_client_credential_refreshes_total", "Credentials fetched from a kubeconfig exec plugin or auth-provider");
+  if (cfg_.exec) {
+    const auto& e = *cfg_.exec;
+    Value info = Value::object({{"apiVersion", e.api_version}, {"kind", "ExecCredential"}});
+    Value spec = Value::object({{"interactive", false}});
+    if (e.provide_cluster_info) {
+      Value cluster = Value::object({{"server", cfg_.server}});
+      if (!cfg_.ca_pem.empty()) cluster["certificate-authority-data"] = crypto::base64_encode(cfg_.ca_pem);
+      if (cfg_.insecure) cluster["insecure-skip-tls-verify"] = true;
+      if (!cfg_.tls_server_name.empty()) cluster["tls-server-name"] = cfg_.tls_server_name;
+      spec["cluster"] = cluster;
+    }
+    info["spec"] = spec;
+    std::vector<std::string> argv{e.command};
+    argv.insert(argv.end(), e.args.begin(), e.args.end());
+    auto env = e.env;
+    env.emplace_back("KUBERNETES_EXEC_INFO", info.dump());
+    RunResult r = run_command(argv, env, cfg_.exec_timeout_ms);
+    if (r.exit_code != 0) {
+      throw std::runtime_error("exec credential plugin " + e.command + " failed (" +
+                               (r.timed_out ? std::string("timed out") : "exit " + std::to_string(r.exit_code)) +
+                               "): " + r.err.substr(0, 500));
+    }
+    Value cred;
+    std::string perr;
+    if (!json::try_parse(r.out, cred, &perr)) throw std::runtime_error("exec credential plugin output: " + perr);
+    if (cred.get_string("kind") != "ExecCredential" || cred.get_string("apiVersion") != e.api_version) {
+      throw std::runtime_error("exec credential plugin returned " + cred.get_string("apiVersion") + " " +
+                               cred.get_string("kind") + ", expected " + e.api_version + " ExecCredential");
+    }
+    const Value& st = cred.get("status");
+    token_ = st.get_string("token");
+    if (!st.get_string("clientCertificateData").empty()) {
+      cfg_.client_cert_pem = st.get_string("clientCertificateData");
+      cfg_.client_key_pem = st.get_string("clientKeyData");
+    }
+    if (token_.empty() && cfg_.client_cert_pem.empty()) {
+      throw std::runtime_error("exec credential plugin returned neither a token nor a client certificate");
+    }
+    token_expiry_ = std::chrono::system_clock::time_point::max();
+    if (!st.get_string("expirationTimestamp").empty() && !parse_rfc3339(st.get_string("expirationTimestamp"), &token_expiry_)) {
+      throw std::runtime_error("exec credential plugin: bad expirationTimestamp " + st.get_string("expirationTimestamp"));
+    }
+  } else {  // gcp auth-provider
+    const Value& pc = cfg_.auth_provider_config;
+    std::chrono::system_clock::time_point exp = std::chrono::system_clock::time_point::max();
+    const bool has_exp = !pc.get_string("expiry").empty() && parse_rfc3339(pc.get_string("expiry"), &exp);
+    const std::string cached = pc.get_string("access-token");
+    if (!force && !plugin_fetched_ && !cached.empty() && (!has_exp || now + std::chrono::seconds(10) < exp)) {
+      token_ = cached;
+      token_expiry_ = exp;
+    } else {
+      const std::string cmd = pc.get_string("cmd-path");
+      if (cmd.empty()) throw std::runtime_error("gcp auth-provider: token expired and no cmd-path to refresh it");
+      std::vector<std::string> argv{cmd};
+      std::string args = pc.get_string("cmd-args");
+      size_t start = 0;
+      while (start < args.size()) {
+        size_t sp = args.find(' ', start);
+        std::string a = args.substr(start, sp == std::string::npos ? std::string::npos : sp - start);
+        if (!a.empty()) argv.push_back(a);
+        if (sp == std::string::npos) break;
+        start = sp + 1;
+      }
+      RunResult r = run_command(argv, {}, cfg_.exec_timeout_ms);
+      if (r.exit_code != 0) throw std::runtime_error("gcp auth-provider command failed: " + r.err.substr(0, 500));
+      Value out = json::parse(r.out);
+      const std::string tk = pc.get_string("token-key").empty() ? "{.access_token}" : pc.get_string("token-key");
+      token_ = json_path_string(out, tk);
+      if (token_.empty()) throw std::runtime_error("gcp auth-provider: no token at " + tk);
+      token_expiry_ = std::chrono::system_clock::time_point::max();
+      const std::string ek = pc.get_string("expiry-key");
+      if (!ek.empty()) parse_rfc3339(json_path_string(out, ek), &token_expiry_);
+    }
+  }
+  plugin_fetched_ = true;
+  credential_refreshes_.fetch_add(1);
+  refreshes.inc();
+  return token_;
 }
 
 http::Headers KubeClient::auth_headers() {
   http::Headers h;
   std::string tok;
-  {
+  if (has_plugin()) {
+    tok = plugin_token(false);
+  } else {
     std::lock_guard<std::mutex> lk(token_mu_);
     auto now = std::chrono::steady_clock::now();
     if (!cfg_.token_file.empty() && now - token_read_ > std::chrono::seconds(60)) {
@@ -146,6 +386,7 @@ http::Headers KubeClient::auth_headers() {
     tok = token_;
   }
   if (!tok.empty()) h.set("Authorization", "Bearer " + tok);
+  else if (!cfg_.basic_auth.empty()) h.set("Authorization", "Basic " + crypto::base64_encode(cfg_.basic_auth));
   if (!cfg_.impersonate_user.empty()) h.set("Impersonate-User", cfg_.impersonate_user);
   for (const auto& g : cfg_.impersonate_groups) h.add("Impersonate-Group", g);
   h.set("Accept", "application/json");
@@ -181,6 +422,12 @@ http::Response KubeClient::raw(const std::string& method, const std::string& pat
     if (!body.empty() || method == "POST" || method == "PUT" || method == "PATCH") h.set("Content-Type", content_type);
     if (!accept.empty()) h.set("Accept", accept);
     http::Response r = http_->request(method, path, body, &h);
+    if (r.status == 401 && has_plugin() && attempt == 0) {
+      // the plugin's credential was revoked or rotated early: fetch a fresh one, retry once
+      LOG_INFO("kube") << method << " " << path << ": 401, refreshing the plugin credential";
+      plugin_token(true);
+      continue;
+    }
     const int wait_s = retry_after_seconds(r, cfg_.max_retry_after_s);
     if (wait_s < 0 || attempt >= cfg_.max_throttle_retries) return r;
     throttled.inc();

@@ -30,6 +30,23 @@ struct KubeConfig {
   std::string tls_server_name;
   std::string impersonate_user;
   std::vector<std::string> impersonate_groups;
+  // users[].user.exec: a credential plugin (client.authentication.k8s.io ExecCredential
+  // v1 / v1beta1) run as a child process; its token is cached until its
+  // expirationTimestamp and re-fetched on a 401 (client-go / kube-client behaviour).
+  struct ExecPlugin {
+    std::string api_version;
+    std::string command;
+    std::vector<std::string> args;
+    std::vector<std::pair<std::string, std::string>> env;
+    bool provide_cluster_info = false;
+  };
+  std::optional<ExecPlugin> exec;
+  // users[].user.auth-provider (kube-client 0.84 without its oidc feature): "oidc" uses the
+  // stored id-token; "gcp" uses access-token until expiry, then runs cmd-path.
+  std::string auth_provider;
+  json::Value auth_provider_config;
+  std::string basic_auth;       // users[].user.username:password
+  int exec_timeout_ms = 30000;
   int timeout_ms = 30000;
   // https: offer HTTP/2 and multiplex request/response calls on one connection, as
   // client-go does (watches keep their own HTTP/1.1 streams).
@@ -46,6 +63,10 @@ struct KubeConfig {
   static KubeConfig infer();
   static KubeConfig in_cluster();
   static KubeConfig from_kubeconfig(const std::string& path, const std::string& context = "");
+  // $KUBECONFIG with several files: merged as client-go merges them — the first file that
+  // defines a cluster, context or user name wins, and so does the first current-context;
+  // relative paths stay relative to the file that defined the entry.
+  static KubeConfig from_kubeconfigs(const std::vector<std::string>& paths, const std::string& context = "");
 };
 
 class ApiError : public std::runtime_error {
@@ -135,15 +156,22 @@ class KubeClient {
                      const std::string& content_type = "application/json", const std::string& accept = "");
   const KubeConfig& config() const { return cfg_; }
   uint64_t throttled() const { return throttled_.load(); }
+  uint64_t credential_refreshes() const { return credential_refreshes_.load(); }
 
  private:
   http::Headers auth_headers();
+  // Token from the exec plugin / gcp auth-provider, refreshed when expired or `force`d.
+  std::string plugin_token(bool force);
+  bool has_plugin() const { return cfg_.exec.has_value() || cfg_.auth_provider == "gcp"; }
   KubeConfig cfg_;
   std::unique_ptr<http::Client> http_;
   std::mutex token_mu_;
   std::string token_;
   std::chrono::steady_clock::time_point token_read_{};
+  std::chrono::system_clock::time_point token_expiry_ = std::chrono::system_clock::time_point::max();
+  bool plugin_fetched_ = false;
   std::atomic<uint64_t> throttled_{0};
+  std::atomic<uint64_t> credential_refreshes_{0};
 };
 
 // Raises ApiError for a non-2xx response (parsing a metav1.Status body when present).

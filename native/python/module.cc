@@ -3,12 +3,13 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <memory>
+#include <vector>
+
 #include "core/crypto.h"
 #include "core/env_config.h"
 #include "core/json.h"
 #include "core/json_patch.h"
-#include <memory>
-#include <vector>
 #include "core/yaml.h"
 #include "crd/schema.h"
 #include "core/log.h"
@@ -175,6 +176,27 @@ PYBIND11_MODULE(_native, m) {
     bgc::log::init_from_env();
     return r;
   });
+  // A KubeClient built from a $KUBECONFIG-style path list, one request per call (tests of
+  // credential plugins and multi-file merging).  Returns (status, body, credential refreshes).
+  m.def("kube_request", [](const std::string& kubeconfig_list, const std::string& method, const std::string& path,
+                           int repeat) {
+    std::vector<std::string> paths;
+    size_t start = 0;
+    while (true) {
+      size_t colon = kubeconfig_list.find(':', start);
+      paths.push_back(kubeconfig_list.substr(start, colon == std::string::npos ? std::string::npos : colon - start));
+      if (colon == std::string::npos) break;
+      start = colon + 1;
+    }
+    py::gil_scoped_release nogil;
+    bgc::kube::KubeClient client(bgc::kube::KubeConfig::from_kubeconfigs(paths));
+    std::vector<std::pair<int, std::string>> out;
+    for (int i = 0; i < std::max(1, repeat); ++i) {
+      auto r = client.raw(method, path);
+      out.emplace_back(r.status, r.body);
+    }
+    return std::make_tuple(out, client.credential_refreshes(), client.config().source);
+  }, py::arg("kubeconfig"), py::arg("method"), py::arg("path"), py::arg("repeat") = 1);
   m.def("kubeconfig_parse", [](const std::string& path, const std::string& context) {
     auto c = bgc::kube::KubeConfig::from_kubeconfig(path, context);
     py::dict d;
@@ -185,6 +207,16 @@ PYBIND11_MODULE(_native, m) {
     d["insecure"] = c.insecure;
     d["impersonate_user"] = c.impersonate_user;
     d["impersonate_groups"] = c.impersonate_groups;
+    d["auth_provider"] = c.auth_provider;
+    d["basic_auth"] = c.basic_auth;
+    if (c.exec) {
+      py::dict e;
+      e["api_version"] = c.exec->api_version;
+      e["command"] = c.exec->command;
+      e["args"] = c.exec->args;
+      e["provide_cluster_info"] = c.exec->provide_cluster_info;
+      d["exec"] = e;
+    }
     return d;
   }, py::arg("path"), py::arg("context") = "");
 
