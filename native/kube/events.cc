@@ -50,8 +50,24 @@ bool EventRecorder::allow(const std::string& key, std::chrono::steady_clock::tim
   }
   if (b.tokens < 1.0) return false;
   b.tokens -= 1.0;
-  if (buckets_.size() > 4096) buckets_.erase(buckets_.begin());  // bound memory on huge clusters
+  if (buckets_.size() > 4096) evict(now);  // bound memory on huge clusters
   return true;
+}
+
+// Drops buckets that have refilled to the burst (a fresh bucket is identical, so this
+// loses nothing); if every bucket is still draining, drops the one refilled longest ago.
+void EventRecorder::evict(std::chrono::steady_clock::time_point now) {
+  auto oldest = buckets_.end();
+  for (auto it = buckets_.begin(); it != buckets_.end();) {
+    const double mins = std::chrono::duration<double>(now - it->second.refilled).count() / 60.0;
+    if (it->second.tokens + mins * opts_.refill_per_minute >= opts_.burst) {
+      it = buckets_.erase(it);
+      continue;
+    }
+    if (oldest == buckets_.end() || it->second.refilled < oldest->second.refilled) oldest = it;
+    ++it;
+  }
+  if (buckets_.size() > 4096 && oldest != buckets_.end()) buckets_.erase(oldest);
 }
 
 void EventRecorder::record(const ResourceType& rt, const Value& obj, const std::string& type, const std::string& reason,

@@ -73,6 +73,7 @@ class EventRecorder {
   void run();
   void write(const Item& it);
   bool allow(const std::string& object_key, std::chrono::steady_clock::time_point now);
+  void evict(std::chrono::steady_clock::time_point now);
 
   KubeClient& client_;
   EventOptions opts_;

@@ -2,6 +2,7 @@
 
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <ctime>
@@ -77,6 +78,10 @@ LeaseSettings LeaseSettings::from_env(const EnvConfig& env, const std::string& d
 
 LeaderElector::LeaderElector(KubeClient& client, LeaseSettings s, std::string identity)
     : client_(client), s_(std::move(s)), identity_(std::move(identity)) {
+  KubeConfig lc = client_.config();
+  lc.timeout_ms = std::max(1, s_.renew_deadline_seconds - s_.retry_seconds) * 1000;
+  lc.max_throttle_retries = 0;  // a throttled renew is a failed renew: retried on the next period
+  lease_client_ = std::make_unique<KubeClient>(lc);
   if (identity_.empty()) {
     char host[256] = {0};
     gethostname(host, sizeof(host) - 1);
@@ -86,12 +91,13 @@ LeaderElector::LeaderElector(KubeClient& client, LeaseSettings s, std::string id
 
 LeaderElector::~LeaderElector() {
   stop_renew_.cancel();
+  if (watchdog_.joinable()) watchdog_.join();
   if (renew_thread_.joinable()) renew_thread_.join();
 }
 
 LeaderElector::Attempt LeaderElector::try_acquire_or_renew() {
   std::string now = rfc3339_micro_now();
-  auto cur = client_.get_opt(types::Lease, s_.ns, s_.name);
+  auto cur = lease_client_->get_opt(types::Lease, s_.ns, s_.name);
   if (!cur) {
     Value lease = Value::object({{"apiVersion", "coordination.k8s.io/v1"}, {"kind", "Lease"}});
     lease["metadata"] = Value::object({{"name", s_.name}, {"namespace", s_.ns}});
@@ -101,7 +107,7 @@ LeaderElector::Attempt LeaderElector::try_acquire_or_renew() {
                                    {"renewTime", now},
                                    {"leaseTransitions", 0}});
     try {
-      client_.create(types::Lease, s_.ns, lease);
+      lease_client_->create(types::Lease, s_.ns, lease);
       return Attempt::Held;
     } catch (const ApiError& e) {
       if (e.code() == 409) return Attempt::HeldByOther;  // somebody else created it first
@@ -124,7 +130,7 @@ LeaderElector::Attempt LeaderElector::try_acquire_or_renew() {
   spec["leaseDurationSeconds"] = s_.lease_seconds;
   spec["renewTime"] = now;
   try {
-    client_.replace(types::Lease, s_.ns, s_.name, lease);  // resourceVersion precondition
+    lease_client_->replace(types::Lease, s_.ns, s_.name, lease);  // resourceVersion precondition
     return Attempt::Held;
   } catch (const ApiError& e) {
     if (e.code() == 409) return Attempt::HeldByOther;  // lost a write race: re-read next time
@@ -149,35 +155,47 @@ bool LeaderElector::acquire(CancelToken& stop) {
 }
 
 void LeaderElector::keep_renewing(std::shared_ptr<CancelToken> stop_on_loss) {
-  renew_thread_ = std::thread([this, stop_on_loss] {
-    // the deadline runs from when the last successful renew was *sent*: the lease's
-    // renewTime is at or after that instant, so a standby (waiting lease_seconds from
-    // renewTime by its own clock) cannot take over before we stop.
-    auto last_ok_sent = std::chrono::steady_clock::now();
-    const auto deadline = std::chrono::seconds(s_.renew_deadline_seconds);
+  using clock = std::chrono::steady_clock;
+  auto ns_now = [] { return clock::now().time_since_epoch().count(); };
+  // the deadline runs from when the last successful renew was *sent*: the lease's
+  // renewTime is at or after that instant, so a standby (waiting lease_seconds from
+  // renewTime by its own clock) cannot take over before we stop.
+  last_ok_sent_ns_ = ns_now();
+  const int64_t deadline_ns = std::chrono::nanoseconds(std::chrono::seconds(s_.renew_deadline_seconds)).count();
+  renew_thread_ = std::thread([this, stop_on_loss, ns_now] {
     while (!stop_renew_.wait_for(std::chrono::seconds(s_.retry_seconds))) {
       if (stop_on_loss->cancelled()) return;
-      auto sent = std::chrono::steady_clock::now();
+      const int64_t sent = ns_now();
       Attempt a = Attempt::Failed;
       try {
         a = try_acquire_or_renew();
       } catch (const std::exception& e) {
         LOG_WARN("leader") << "lease renew failed: " << e.what();
       }
+      if (stop_on_loss->cancelled()) return;  // the watchdog already stepped down
       if (a == Attempt::Held) {
-        last_ok_sent = sent;
+        last_ok_sent_ns_ = sent;
         continue;
       }
       if (a == Attempt::HeldByOther) {
         LOG_ERROR("leader") << "lease " << s_.ns << "/" << s_.name << " is held by another replica; stepping down";
-      } else if (std::chrono::steady_clock::now() - last_ok_sent < deadline) {
-        continue;  // transient failure: retry until the renew deadline
-      } else {
+        stop_on_loss->cancel();
+        return;
+      }
+      // transient failure: retried every period; the watchdog enforces the deadline
+    }
+  });
+  // Watchdog: steps down at last_ok_sent + renew_deadline even when a renew request is
+  // still hanging on a stalled API server.
+  watchdog_ = std::thread([this, stop_on_loss, ns_now, deadline_ns] {
+    while (!stop_renew_.wait_for(std::chrono::milliseconds(100))) {
+      if (stop_on_loss->cancelled()) return;
+      if (ns_now() - last_ok_sent_ns_.load() >= deadline_ns) {
         LOG_ERROR("leader") << "lost lease " << s_.ns << "/" << s_.name << " (renew deadline " << s_.renew_deadline_seconds
                             << " s passed); shutting down";
+        stop_on_loss->cancel();
+        return;
       }
-      stop_on_loss->cancel();
-      return;
     }
   });
 }

@@ -8,8 +8,13 @@
 // within `renew_deadline_seconds` (10) of the last successful renew's *send* time, so it
 // stops acting before a standby (which waits the full lease duration by its own clock)
 // can take over.  It also steps down at once when the lease names another holder.
+// The deadline holds even while a renew request hangs: Lease calls go through their own
+// client (request timeout renew_deadline - retry_period, no 429 retries), and a watchdog
+// thread cancels the guarded work at last_ok_sent + renew_deadline regardless of any
+// request in flight.
 #pragma once
 
+#include <atomic>
 #include <chrono>
 #include <memory>
 #include <string>
@@ -52,11 +57,14 @@ class LeaderElector {
   const std::string& identity() const { return identity_; }
 
  private:
-  KubeClient& client_;
+  KubeClient& client_;  // the caller's client (kept for identity of the API server)
+  std::unique_ptr<KubeClient> lease_client_;  // bounded timeout, no throttle retries
   LeaseSettings s_;
   std::string identity_;
   std::thread renew_thread_;
+  std::thread watchdog_;
   CancelToken stop_renew_;
+  std::atomic<int64_t> last_ok_sent_ns_{0};  // steady clock
 };
 
 // Acquires leadership when `s.enabled` (blocking until acquired or stopped) and keeps it

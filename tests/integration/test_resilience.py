@@ -160,6 +160,32 @@ def test_leader_steps_down_when_lease_taken():
         assert "held by another replica; stepping down" in leader.output()
 
 
+def test_leader_steps_down_at_renew_deadline_while_renew_hangs():
+    """the deadline used to be checked only after a renew request
+    returned, so a stalled apiserver (here: Lease requests held for 8 s, longer than the
+    4 s lease) kept the leader acting past the point a standby may take over.  The
+    watchdog must stop it within renew_deadline (3 s) of the last successful renew."""
+    with Cluster(admission=False, controller=False) as c:
+        c.start_controller(extra_env=FAST_LEASE)
+        leader = c.procs["controller"]
+        wait_for(lambda: "acquired lease" in leader.output(), desc="leader acquires")
+        last = c.admin.get("leases", "bacchus-gpu-controller", "bgc")["spec"]["renewTime"]
+        wait_for(lambda: c.admin.get("leases", "bacchus-gpu-controller", "bgc")["spec"]["renewTime"] != last,
+                 timeout=5, desc="a renew lands")
+        t0 = time.monotonic()  # the last successful renew was sent at most ~0.1 s ago
+        c.fault([{"path": "/leases/bacchus-gpu-controller", "delay_ms": 8000, "count": 6}])
+        wait_for(lambda: "gracefully shutted down" in leader.output(), timeout=15, interval=0.05,
+                 desc="leader stops reconciling")
+        elapsed = time.monotonic() - t0
+        out = leader.output()
+        assert "renew deadline 3 s passed" in out, out[-2000:]
+        # deadline 3 s after the last good renew (renews land every 1 s, so t0 is at most
+        # ~1 s after it), + the 100 ms watchdog tick and the controller's shutdown
+        assert elapsed < 3.6, f"leader acted for {elapsed:.1f} s after the apiserver stalled"
+        # the hung renew is bounded by the Lease client's own timeout (deadline - retry = 2 s)
+        wait_for(lambda: not leader.alive(), timeout=5, desc="leader exits")
+
+
 def test_graceful_shutdown_exit_codes():
     with Cluster() as c:
         codes = {}
