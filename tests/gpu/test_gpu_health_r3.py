@@ -52,19 +52,21 @@ def test_hip_device_bdf_matches_amdsmi():
     assert g is not None and g["bdf"].lower() == bdf, (bdf, [x["bdf"] for x in gpus])
 
 
-@pytest.mark.parametrize("size", [1024, 4096])
-def test_tiled_gemm_matches_torch_fp32(size):
+@pytest.mark.parametrize("m,n,k", [(1024, 1024, 1024), (4096, 4096, 4096), (384, 640, 192), (512, 256, 1152)])
+def test_tiled_gemm_matches_torch_fp32(m, n, k):
+    """The soak's kernels on N(0,1) operands against a PyTorch fp32 product: square
+    sizes run the 8-phase ping-pong kernel, 384x640x192 the double-buffered one (M, N not
+    multiples of 256), 512x256x1152 the ping-pong kernel on a rectangular grid with an odd
+    number of 8-phase iterations (18 K-tiles)."""
     import torch
 
-    from bacchus_gpu_controller_amd import native
+    from bacchus_gpu_controller_amd import ops
 
-    torch.manual_seed(size)
-    m = n = k = size
+    torch.manual_seed(m * 7 + n * 3 + k)
     a = torch.randn(m, k).to(torch.bfloat16)
     bt = torch.randn(n, k).to(torch.bfloat16)
-    raw = native().diag_gemm_tiled(0, m, n, k, a.view(torch.int16).numpy().tobytes(),
-                                   bt.view(torch.int16).numpy().tobytes())
-    c = torch.frombuffer(bytearray(raw), dtype=torch.float32).reshape(m, n)
+    c = torch.from_numpy(ops.gemm_tiled(a, bt).copy())
+    size = f"{m}x{n}x{k}" if not m == n == k else m
     af, bf = a.float(), bt.float()
     ref = af @ bf.T
     mag = af.abs() @ bf.abs().T
