@@ -407,7 +407,8 @@ def run(args):
         if args.write_latency_ms > 0:
             apiserver_args += ["--write-latency-ms", str(args.write_latency_ms)]
         cluster = Cluster(controller_env=ctrl_env, log_level=args.log_level, tls_apiserver=args.tls_apiserver,
-                          apiserver_args=apiserver_args)
+                          apiserver_args=apiserver_args,
+                          admission_env=dict(kv.split("=", 1) for kv in args.admission_env))
         cluster.start()
         cluster.start_synchronizer(google, interval=args.sync_interval, extra_env=sync_env)
         cluster.start_node_agent(max_gpus=n, n_mock_gpus=n, poll_interval_ms=args.poll_ms,
@@ -564,6 +565,8 @@ def main(argv=None):
     ap.add_argument("--apiserver-arg", action="append", default=[], help="extra kube-lite flag (repeatable)")
     ap.add_argument("--controller-env", action="append", default=[], metavar="CONF_X=V",
                     help="extra controller environment (repeatable), e.g. CONF_METADATA_WATCHES=false")
+    ap.add_argument("--admission-env", action="append", default=[], metavar="CONF_X=V",
+                    help="extra admission environment (repeatable), e.g. CONF_HTTP2_INLINE=false")
     ap.add_argument("--report-cpu", action="store_true", help="add RSS, object counts and controller gauges")
     ap.add_argument("--driver-http2", action=argparse.BooleanOptionalAction, default=False,
                     help="tenant load over HTTP/2 multiplexed connections (profiles/http2_r2/: no gain at N=1, "

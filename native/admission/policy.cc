@@ -24,6 +24,7 @@ Config Config::from_env(const EnvConfig& env) {
   c.log_full_request = env.boolean_or("log_full_request", true);
   c.cert_reload_interval_secs = env.u64_or("cert_reload_interval_secs", 60);
   c.http2 = env.boolean_or("http2", true);
+  c.http2_inline = env.boolean_or("http2_inline", true);
   return c;
 }
 

@@ -24,6 +24,9 @@ struct Config {
   bool log_full_request = true;          // reference logs the full request (admission.rs:199)
   uint64_t cert_reload_interval_secs = 60;  // admission.rs:112
   bool http2 = true;  // ALPN h2 + http/1.1, as axum-server's rustls acceptor (admission.rs:141)
+  // h2: run /mutate on the connection reader when the connection has nothing else in
+  // flight (no worker hand-off; profiles/admission_h2_inline_r3/)
+  bool http2_inline = true;
 
   // envy semantics: every reference field is required (admission.rs:22-39).
   static Config from_env(const EnvConfig& env);

@@ -52,6 +52,7 @@ int main() {
   so.tls = tls;
   so.name = "admission";
   so.http2 = cfg.http2;
+  if (cfg.http2_inline) so.h2_inline_paths = {"/mutate"};
   http::Server server(so);
   http::add_standard_routes(server);
   server.handle("POST", "/mutate", [&](http::Request& req, http::ResponseWriter& w) {

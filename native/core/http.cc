@@ -586,8 +586,13 @@ bool h2_forbidden_header(const std::string& lname) {
 
 class H2ResponseWriter final : public ResponseWriter {
  public:
-  H2ResponseWriter(std::shared_ptr<http2::Connection> c, std::shared_ptr<http2::Stream> st, const CancelToken& stop)
-      : ResponseWriter(nullptr, true, stop), c_(std::move(c)), st_(std::move(st)) {}
+  // `blocked_send`: set when the handler runs on the connection's reader thread, which
+  // must never wait for a WINDOW_UPDATE it alone can read; a response that does not fit
+  // the peer's window is handed to it (a worker finishes the send).
+  using BlockedSend = std::function<void(hpack::HeaderList, std::string)>;
+  H2ResponseWriter(std::shared_ptr<http2::Connection> c, std::shared_ptr<http2::Stream> st, const CancelToken& stop,
+                   BlockedSend blocked_send = nullptr)
+      : ResponseWriter(nullptr, true, stop), c_(std::move(c)), st_(std::move(st)), blocked_send_(std::move(blocked_send)) {}
 
   void send(int status, std::string_view body, const std::string& content_type, const Headers* extra) override {
     status_ = status;
@@ -595,11 +600,16 @@ class H2ResponseWriter final : public ResponseWriter {
     sent_ = true;
     hpack::HeaderList h = head(status, content_type, extra);
     h.emplace_back("content-length", std::to_string(body.size()));
-    c_->send_response(*st_, h, body);
+    if (!blocked_send_) {
+      c_->send_response(*st_, h, body);
+    } else if (c_->try_send_response(*st_, h, body) == http2::Connection::SendResult::kWouldBlock) {
+      blocked_send_(std::move(h), std::string(body));
+    }
   }
   bool start_chunked(int status, const std::string& content_type) override {
     status_ = status;
     if (sent_) return false;
+    if (blocked_send_) throw std::logic_error("streaming response from an inline HTTP/2 handler");
     sent_ = chunked_ = true;
     return c_->send_headers(*st_, head(status, content_type, nullptr), false);
   }
@@ -629,6 +639,7 @@ class H2ResponseWriter final : public ResponseWriter {
   }
   std::shared_ptr<http2::Connection> c_;
   std::shared_ptr<http2::Stream> st_;
+  BlockedSend blocked_send_;
 };
 
 }  // namespace
@@ -646,38 +657,89 @@ void Server::serve_h2(int fd, std::unique_ptr<net::Stream> s, const std::string&
   auto inflight = std::make_shared<Inflight>();
   auto pool = h2_workers_;
   const size_t max_body = opts_.max_body;
-  auto conn = std::make_shared<http2::Connection>(
-      std::move(s), http2::Connection::Role::kServer,
-      [this, inflight, pool, remote, max_body](std::shared_ptr<http2::Connection> c, std::shared_ptr<http2::Stream> st) {
+  // one stream, start to finish: on a worker, or inline on the reader thread
+  auto serve_stream = [this, inflight, pool, remote, max_body](const std::shared_ptr<http2::Connection>& c,
+                                                                const std::shared_ptr<http2::Stream>& st, int64_t t0,
+                                                                Request& req, bool ok, bool on_reader) {
+    streams.inc();
+    H2ResponseWriter::BlockedSend blocked;
+    if (on_reader) {
+      blocked = [inflight, pool, c, st](hpack::HeaderList h, std::string body) {
         {
           std::lock_guard<std::mutex> lk(inflight->mu);
           ++inflight->n;
         }
+        WorkerPool::submit(pool, [inflight, c, st, h = std::move(h), body = std::move(body)] {
+          c->send_response(*st, h, body);
+          std::lock_guard<std::mutex> lk(inflight->mu);
+          --inflight->n;
+          inflight->cv.notify_all();
+        });
+      };
+    }
+    H2ResponseWriter h2w(c, st, stop_, std::move(blocked));
+    ResponseWriter& w = h2w;
+    if (ok) {
+      if (req.method.empty() || req.target.empty()) w.send(400, "missing :method or :path\n");
+      else if (req.body.size() > max_body) w.send(413, "request body too large\n");
+      else handle_request(req, w);
+    }
+    server_time.add(static_cast<double>(metrics::now_ns() - t0) * 1e-9);
+  };
+  auto take_request = [remote](const std::shared_ptr<http2::Connection>& c, const std::shared_ptr<http2::Stream>& st,
+                               Request& req) {
+    req.remote = remote;
+    bool ok = c->locked([&] {
+      for (auto& [k, v] : st->headers) {
+        if (k == ":method") req.method = v;
+        else if (k == ":path") req.target = v;
+        else if (!k.empty() && k[0] != ':') req.headers.add(k, v);
+      }
+      req.body = std::move(st->data);
+      return !st->reset;
+    });
+    size_t q = req.target.find('?');
+    req.path = url_decode(req.target.substr(0, q));
+    req.query = q == std::string::npos ? "" : req.target.substr(q + 1);
+    return ok;
+  };
+  const bool any_inline = !opts_.h2_inline_paths.empty();
+  auto conn = std::make_shared<http2::Connection>(
+      std::move(s), http2::Connection::Role::kServer,
+      [this, inflight, pool, serve_stream, take_request, any_inline](std::shared_ptr<http2::Connection> c,
+                                                                     std::shared_ptr<http2::Stream> st) {
         const int64_t t0 = metrics::now_ns();
-        WorkerPool::submit(pool, [this, inflight, remote, max_body, t0, c = std::move(c), st = std::move(st)] {
-          Request req;
-          req.remote = remote;
-          bool ok = c->locked([&] {
-            for (auto& [k, v] : st->headers) {
-              if (k == ":method") req.method = v;
-              else if (k == ":path") req.target = v;
-              else if (!k.empty() && k[0] != ':') req.headers.add(k, v);
-            }
-            req.body = std::move(st->data);
-            return !st->reset;
-          });
-          streams.inc();
-          H2ResponseWriter h2w(c, st, stop_);
-          ResponseWriter& w = h2w;
-          if (ok) {
-            size_t q = req.target.find('?');
-            req.path = url_decode(req.target.substr(0, q));
-            req.query = q == std::string::npos ? "" : req.target.substr(q + 1);
-            if (req.method.empty() || req.target.empty()) w.send(400, "missing :method or :path\n");
-            else if (req.body.size() > max_body) w.send(413, "request body too large\n");
-            else handle_request(req, w);
+        bool idle;
+        {
+          std::lock_guard<std::mutex> lk(inflight->mu);
+          idle = inflight->n == 0;
+          ++inflight->n;
+        }
+        if (idle && any_inline) {
+          auto req = std::make_shared<Request>();
+          const bool ok = take_request(c, st, *req);
+          const auto& paths = opts_.h2_inline_paths;
+          if (std::find(paths.begin(), paths.end(), req->path) != paths.end()) {
+            h2_inline_.fetch_add(1, std::memory_order_relaxed);
+            serve_stream(c, st, t0, *req, ok, /*on_reader=*/true);
+            std::lock_guard<std::mutex> lk(inflight->mu);
+            --inflight->n;
+            inflight->cv.notify_all();
+            return;
           }
-          server_time.add(static_cast<double>(metrics::now_ns() - t0) * 1e-9);
+          WorkerPool::submit(pool, [inflight, serve_stream, t0, ok, c = std::move(c), st = std::move(st),
+                                    req = std::move(req)] {
+            serve_stream(c, st, t0, *req, ok, false);
+            std::lock_guard<std::mutex> lk(inflight->mu);
+            --inflight->n;
+            inflight->cv.notify_all();
+          });
+          return;
+        }
+        WorkerPool::submit(pool, [inflight, serve_stream, take_request, t0, c = std::move(c), st = std::move(st)] {
+          Request req;
+          const bool ok = take_request(c, st, req);
+          serve_stream(c, st, t0, req, ok, false);
           std::lock_guard<std::mutex> lk(inflight->mu);
           --inflight->n;
           inflight->cv.notify_all();

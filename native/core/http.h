@@ -148,6 +148,11 @@ struct ServerOptions {
   std::string name = "http";
   // TLS servers: offer HTTP/2 by ALPN (enables it on `tls`); HTTP/1.1 clients unaffected.
   bool http2 = true;
+  // HTTP/2: exact paths whose handlers may run on the connection's reader thread when no
+  // other stream of that connection is in flight (saves the hand-off to a worker thread).
+  // Only for short handlers that answer with one send(); a response the peer's flow-control
+  // window cannot take at once is finished on a worker.
+  std::vector<std::string> h2_inline_paths;
 };
 
 class Server {
@@ -162,6 +167,8 @@ class Server {
   // Stops accepting, waits up to `grace` for in-flight requests, then force-closes.
   void stop(std::chrono::milliseconds grace = std::chrono::milliseconds(10000));
   size_t active_connections() const { return active_.load(); }
+  // HTTP/2 streams whose handler ran on the connection's reader thread (h2_inline_paths)
+  uint64_t h2_inline_served() const { return h2_inline_.load(); }
 
  private:
   void accept_loop();
@@ -186,6 +193,7 @@ class Server {
   std::atomic<int64_t> grace_ms_{10000};  // stop()'s grace, for draining HTTP/2 connections
   struct WorkerPool;  // HTTP/2 stream workers (cached threads)
   std::shared_ptr<WorkerPool> h2_workers_;
+  std::atomic<uint64_t> h2_inline_{0};
 };
 
 // Attaches `/health` (-> "pong"), `/metrics` and `/debug/samples/<name>`.

@@ -21,12 +21,14 @@ namespace {
 
 class TestServer {
  public:
-  TestServer(const std::string& cert_pem, const std::string& key_pem, bool http2, int idle_timeout_ms) {
+  TestServer(const std::string& cert_pem, const std::string& key_pem, bool http2, int idle_timeout_ms,
+             std::vector<std::string> inline_paths) {
     bgc::http::ServerOptions so;
     so.addr = "127.0.0.1";
     so.port = 0;
     so.name = "http-test";
     so.http2 = http2;
+    so.h2_inline_paths = std::move(inline_paths);
     if (idle_timeout_ms > 0) so.idle_timeout_ms = idle_timeout_ms;
     if (!cert_pem.empty()) so.tls = bgc::net::TlsContext::server_from_pem(cert_pem, key_pem);
     srv_ = std::make_unique<bgc::http::Server>(so);
@@ -63,6 +65,7 @@ class TestServer {
   }
   uint16_t port() const { return srv_->port(); }
   uint64_t served() const { return served_.load(); }
+  uint64_t inline_served() const { return srv_->h2_inline_served(); }
   void stop(int grace_ms) { srv_->stop(std::chrono::milliseconds(grace_ms)); }
 
  private:
@@ -74,9 +77,11 @@ class TestServer {
 
 void register_http(py::module_& m) {
   py::class_<TestServer>(m, "HttpTestServer")
-      .def(py::init<const std::string&, const std::string&, bool, int>(), py::arg("cert_pem"), py::arg("key_pem"),
-           py::arg("http2") = true, py::arg("idle_timeout_ms") = 0)
+      .def(py::init<const std::string&, const std::string&, bool, int, std::vector<std::string>>(), py::arg("cert_pem"),
+           py::arg("key_pem"), py::arg("http2") = true, py::arg("idle_timeout_ms") = 0,
+           py::arg("inline_paths") = std::vector<std::string>{})
       .def_property_readonly("port", &TestServer::port)
+      .def_property_readonly("inline_served", &TestServer::inline_served)
       .def_property_readonly("served", &TestServer::served)
       .def("stop", &TestServer::stop, py::arg("grace_ms") = 10000, py::call_guard<py::gil_scoped_release>());
 

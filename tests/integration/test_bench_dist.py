@@ -18,15 +18,17 @@ def test_bench_two_ranks_gloo():
     env = dict(os.environ, BGC_BENCH_CPU="1", OMP_NUM_THREADS="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(REPO_ROOT, "bench.py"),
-           "--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "20"]
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "20", "--rounds", "2"]
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=REPO_ROOT)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, p.stdout  # only rank 0 prints
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 1
-    assert d["config"]["global_batch"] == 40 and d["config"]["parallelism"] == "dp2"
-    assert d["ready_crs"] == 2 * 2 * 20 and d["failed_crs"] == 0
+    # a step is `rounds` rounds of `batch` tenants per rank
+    assert d["config"]["global_batch"] == 2 * 20 * 2 and d["config"]["parallelism"] == "dp2"
+    assert d["config"]["rounds_per_step"] == 2 and d["config"]["tenants_per_round"] == 20
+    assert d["ready_crs"] == 2 * 2 * 20 * 2 and d["failed_crs"] == 0
     assert d["value"] > 0 and d["scaling"] == "weak"
     # config #3's 100 concurrent CRs are split over the ranks
     assert d["config"]["concurrency_per_rank"] == 50 and d["config"]["concurrency_total"] == 100
@@ -47,7 +49,7 @@ def test_bench_approve_after_create():
     """--approve-after-create: tenants apply, then one sheet edit per step approves them
     (the reference's onboarding order); the JSON times approve -> Ready."""
     cmd = [sys.executable, os.path.join(REPO_ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--batch", "20",
-           "--approve-after-create", "--sheet-poll-ms", "300", "--no-tuned-phase", "--write-latency-ms", "1"]
+           "--rounds", "1", "--approve-after-create", "--sheet-poll-ms", "300", "--no-tuned-phase", "--write-latency-ms", "1"]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=REPO_ROOT,
                        env=dict(os.environ, BGC_BENCH_CPU="1"))
     assert p.returncode == 0, p.stderr[-3000:]

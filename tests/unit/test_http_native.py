@@ -138,3 +138,57 @@ def test_h2_spreads_over_several_connections(nat, pki, server):
     for i in range(9):
         assert c.request("POST", "/echo", str(i).encode())[1] == str(i).encode()
     assert server.served >= 9
+
+
+def test_h2_inline_handlers(nat, pki):
+    """h2_inline_paths: a stream that arrives on an idle connection runs on the reader
+    thread.  Streams that arrive while another is in flight still go to workers, and a
+    response larger than the client's 64 KiB window is finished on a worker: the reader
+    thread cannot wait for a WINDOW_UPDATE that only it can read."""
+    s = nat.HttpTestServer(pki["cert"], pki["key"], inline_paths=["/echo", "/big", "/slow"])
+    try:
+        c = client(nat, pki, s.port)
+        for i in range(5):
+            assert c.request("POST", "/echo", str(i).encode())[1] == str(i).encode()
+        assert s.inline_served == 5
+        # 3 MiB down through the blocked-send hand-off, twice (the connection stays good)
+        for _ in range(2):
+            status, body, _ = c.request("GET", f"/big?n={3 << 20}")
+            assert status == 200 and len(body) == 3 << 20 and body[4096:4097] == b"b"
+        # a slow inline handler holds the reader; a concurrent stream waits for it and is
+        # then served (on a worker or inline), never lost
+        out = {}
+        t = threading.Thread(target=lambda: out.setdefault("slow", c.request("GET", "/slow?ms=300")))
+        t.start()
+        time.sleep(0.05)
+        assert c.request("POST", "/echo", b"during")[1] == b"during"
+        t.join(10)
+        assert out["slow"][:2] == (200, b"done")
+    finally:
+        s.stop(0)
+
+
+def test_h2_inline_concurrent_streams_one_connection(nat, pki):
+    s = nat.HttpTestServer(pki["cert"], pki["key"], inline_paths=["/echo"])
+    try:
+        c = client(nat, pki, s.port)
+        errors = []
+
+        def worker(k):
+            try:
+                for i in range(30):
+                    payload = f"{k}-{i}".encode() * 40
+                    status, body, _ = c.request("POST", "/echo", payload)
+                    assert status == 200 and body == payload
+            except Exception as e:  # noqa: BLE001
+                errors.append(repr(e))
+
+        ts = [threading.Thread(target=worker, args=(k,)) for k in range(16)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(60)
+        assert not errors
+        assert s.served == 16 * 30 and 0 < s.inline_served <= s.served
+    finally:
+        s.stop(0)
