@@ -136,12 +136,28 @@ static void load_cert_chain_pem(SSL_CTX* ctx, const std::string& cert_pem, const
   }
 }
 
+namespace {
+// Read-ahead: SSL_read pulls everything the socket holds into OpenSSL's buffer with one
+// read(2), instead of one read for each record header and one for its body (2 syscalls
+// per record).  Every reader here calls SSL_read before it polls, and has_buffered()
+// counts read-ahead bytes, so buffered records are never missed.  BGC_TLS_READ_AHEAD=0
+// turns it off (A/B).
+void tune_ctx(SSL_CTX* c) {
+  SSL_CTX_set_min_proto_version(c, TLS1_2_VERSION);
+  SSL_CTX_set_mode(c, SSL_MODE_AUTO_RETRY);
+  static const bool read_ahead = [] {
+    const char* e = std::getenv("BGC_TLS_READ_AHEAD");
+    return !(e && std::string(e) == "0");
+  }();
+  if (read_ahead) SSL_CTX_set_read_ahead(c, 1);
+}
+}  // namespace
+
 std::shared_ptr<TlsContext> TlsContext::server_from_pem(const std::string& cert_pem, const std::string& key_pem) {
   SSL_CTX* c = SSL_CTX_new(TLS_server_method());
   if (!c) throw NetError("SSL_CTX_new: " + ssl_errors());
   auto ctx = wrap_ctx(c);
-  SSL_CTX_set_min_proto_version(c, TLS1_2_VERSION);
-  SSL_CTX_set_mode(c, SSL_MODE_AUTO_RETRY);
+  tune_ctx(c);
   load_cert_chain_pem(c, cert_pem, key_pem);
   auto t = std::make_shared<TlsContext>();
   t->ctx_ = ctx;
@@ -197,8 +213,7 @@ std::shared_ptr<TlsContext> TlsContext::client(const std::string& ca_pem, bool i
   SSL_CTX* c = SSL_CTX_new(TLS_client_method());
   if (!c) throw NetError("SSL_CTX_new: " + ssl_errors());
   auto ctx = wrap_ctx(c);
-  SSL_CTX_set_min_proto_version(c, TLS1_2_VERSION);
-  SSL_CTX_set_mode(c, SSL_MODE_AUTO_RETRY);
+  tune_ctx(c);
   // Session resumption keeps reconnect cost low for the webhook/apiserver clients.
   SSL_CTX_set_session_cache_mode(c, SSL_SESS_CACHE_CLIENT);
   if (!insecure) {
@@ -287,7 +302,7 @@ TlsStream::~TlsStream() {
 
 bool TlsStream::has_buffered() const {
   std::lock_guard<std::mutex> lk(ssl_mu_);
-  return ssl_ && SSL_pending(ssl_) > 0;
+  return ssl_ && SSL_has_pending(ssl_) == 1;  // decrypted or read-ahead (unprocessed) bytes
 }
 
 std::string TlsStream::alpn() const {
