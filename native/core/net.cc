@@ -137,17 +137,17 @@ static void load_cert_chain_pem(SSL_CTX* ctx, const std::string& cert_pem, const
 }
 
 namespace {
-// Read-ahead: SSL_read pulls everything the socket holds into OpenSSL's buffer with one
-// read(2), instead of one read for each record header and one for its body (2 syscalls
-// per record).  Every reader here calls SSL_read before it polls, and has_buffered()
-// counts read-ahead bytes, so buffered records are never missed.  BGC_TLS_READ_AHEAD=0
-// turns it off (A/B).
+// Read-ahead (BGC_TLS_READ_AHEAD=1): SSL_read pulls everything the socket holds into
+// OpenSSL's buffer with one read(2), instead of one read for each record header and one
+// for its body.  Every reader here calls SSL_read before it polls, and has_buffered()
+// counts read-ahead bytes, so it is safe; but on the MI355X box it did not pay (no CPU
+// or rate gain in an interleaved A/B, profiles/admission_h2_inline_r3/), so it is off.
 void tune_ctx(SSL_CTX* c) {
   SSL_CTX_set_min_proto_version(c, TLS1_2_VERSION);
   SSL_CTX_set_mode(c, SSL_MODE_AUTO_RETRY);
   static const bool read_ahead = [] {
     const char* e = std::getenv("BGC_TLS_READ_AHEAD");
-    return !(e && std::string(e) == "0");
+    return e && std::string(e) == "1";
   }();
   if (read_ahead) SSL_CTX_set_read_ahead(c, 1);
 }
