@@ -45,24 +45,18 @@ RUN cmake -S . -B build -G Ninja -DCMAKE_BUILD_TYPE=Release -DBGC_PYTHON=OFF && 
       -mllvm -amdgpu-mfma-vgpr-form=1 -Inative/gpu/hip native/gpu/hip/gpu_diag.hip \
       -o bin/libbgc_gpu_diag.so
 # The agent dlopen()s libamd_smi and the diagnostics library (which links the HIP
-# runtime): collect exactly those plus their ROCm dependencies.
-RUN mkdir -p /rt && \
-    for f in /opt/rocm/lib/libamd_smi.so /src/bin/libbgc_gpu_diag.so; do \
-      cp -L "$f" /rt/; \
-      ldd "$f" | awk '$3 ~ /^\/opt\/rocm/ {print $3}' | xargs -r -I{} cp -L {} /rt/; \
-    done && \
-    for f in /rt/*.so*; do \
-      ldd "$f" | awk '$3 ~ /^\/opt\/rocm/ {print $3}' | xargs -r -I{} cp -nL {} /rt/; \
-    done && \
-    cp -L /opt/rocm/lib/libamd_comgr.so* /rt/ 2>/dev/null || true
+# runtime): collect exactly those plus, to a fixpoint, their ROCm dependencies.  The same
+# script runs in tests/gpu/test_node_image_closure.py, which runs the agent's diagnostics
+# on an MI355X with only these libraries and checks nothing else came from /opt/rocm.
+COPY tools/node_image_closure.sh ./tools/
+RUN bash tools/node_image_closure.sh /rt /src/bin/libbgc_gpu_diag.so
 
 FROM ${NODE_BASE} AS node-agent
 RUN apt-get update && apt-get install -y --no-install-recommends ca-certificates libssl3 libdrm2 libdrm-amdgpu1 \
       libnuma1 libelf1 && rm -rf /var/lib/apt/lists/*
 COPY --from=build-node /rt/ /opt/bgc/lib/
 COPY --from=build-node /src/bin/node-agent /app/node-agent
-COPY --from=build-node /src/bin/libbgc_gpu_diag.so /app/libbgc_gpu_diag.so
-ENV BGC_GPU_DIAG_LIB=/app/libbgc_gpu_diag.so \
+ENV BGC_GPU_DIAG_LIB=/opt/bgc/lib/libbgc_gpu_diag.so \
     LD_LIBRARY_PATH=/opt/bgc/lib \
     GLIBC_TUNABLES=glibc.malloc.tcache_count=64:glibc.malloc.tcache_max=16384
 # root: amdsmi reads /sys and the render/kfd nodes, the device plugin writes its socket
