@@ -484,22 +484,6 @@ __device__ __forceinline__ void pp_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// kSched 1 (default) balances the LDS work of the phases; kSched 0 is the first schedule
-// (BGC_SOAK_KERNEL=pingpong0, A/B).  Per wave and K-tile, fragment reads / LDS-DMA pieces:
-//
-//   phase            0      1      2      3
-//   kSched 0 reads  16      0      8      0     pieces 2 2 2 2
-//   kSched 1 reads  12      4      8      0     pieces 0 2 0 6
-//
-// With four waves reading per interval, 16 ds_read_b128 take the LDS array's whole
-// 256-cycle MFMA interval (1 KiB per wave-read at 256 B/clk), so in kSched 0 phase 0's
-// reads alone are as long as the partner's MFMAs, plus two LDS-DMA pieces.  kSched 1
-// reads B's second column pair in phase 1 (where it is first used) and moves every
-// load out of the read-heavy phases.  A later last read of the B halves moves their
-// reload from phases 2/3 to 3; every reload still comes at least two barriers after the
-// half's last read (B 2,3: read p1, staged p3; A 0: read p2, staged p3; A 1: p2 -> p5;
-// B 6,7: p5 -> p7; A 4: p6 -> p7; A 5: p6 -> next p1), and waits become vmcnt(6).
-template <int kSched>
 __global__ __launch_bounds__(512, 1) void gemm_pingpong(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
                                                         float* __restrict__ C, int M, int N, int K) {
   __shared__ __attribute__((aligned(16))) char lds[8 * kPPHalf];  // [buf][A_top, A_bot, B_left, B_right]
@@ -532,20 +516,14 @@ __global__ __launch_bounds__(512, 1) void gemm_pingpong(const __bf16* __restrict
     for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 af[4][2], bfr[4][2];
 
-  // prologue: K-tile 0 into buffer 0, K-tile 1's B halves (and, kSched 1, A_top) into
-  // buffer 1; everything but those last loads must land before phase 0's reads
+  // prologue: K-tile 0 into buffer 0, K-tile 1's B halves into buffer 1
   stage(0, 0);
   stage(1, 0);
   stage(2, 0);
   stage(3, 0);
   stage(6, 1);
   stage(7, 1);
-  if constexpr (kSched == 1) {
-    stage(4, 1);
-    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  }
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   pp_barrier();
   if (wr == 1) pp_barrier();  // the stagger: group 1 runs one barrier behind
 
@@ -558,25 +536,12 @@ __global__ __launch_bounds__(512, 1) void gemm_pingpong(const __bf16* __restrict
 #pragma unroll
     for (int p = 0; p < 8; ++p) {
       const char* buf = lds + (p >> 2) * 4 * kPPHalf;
-      if constexpr (kSched == 0) {
-        if ((p & 3) == 0) {  // all of B, rows 0-63 of A
-          const char* bi = buf + b_half * kPPHalf;
+      if ((p & 3) == 0) {  // all of B, rows 0-63 of A
+        const char* bi = buf + b_half * kPPHalf;
 #pragma unroll
-          for (int ni = 0; ni < 4; ++ni)
+        for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
-            for (int ks = 0; ks < 2; ++ks)
-              bfr[ni][ks] = soak_frag(bi, b_row0 + ni * 16 + (lane & 15), ks * 4 + (lane >> 4));
-        }
-      } else {
-        if ((p & 3) < 2) {  // B columns 0-31 at phase 0, 32-63 at phase 1 (each where first used)
-          const char* bi = buf + b_half * kPPHalf;
-          const int n0 = (p & 1) * 2;
-#pragma unroll
-          for (int ni = n0; ni < n0 + 2; ++ni)
-#pragma unroll
-            for (int ks = 0; ks < 2; ++ks)
-              bfr[ni][ks] = soak_frag(bi, b_row0 + ni * 16 + (lane & 15), ks * 4 + (lane >> 4));
-        }
+          for (int ks = 0; ks < 2; ++ks) bfr[ni][ks] = soak_frag(bi, b_row0 + ni * 16 + (lane & 15), ks * 4 + (lane >> 4));
       }
       if ((p & 1) == 0) {  // phases 0/2 (4/6): the A half this quadrant pair needs
         const char* ai = buf + a_half * kPPHalf;
@@ -586,42 +551,17 @@ __global__ __launch_bounds__(512, 1) void gemm_pingpong(const __bf16* __restrict
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks) af[mi][ks] = soak_frag(ai, m0 + mi * 16 + (lane & 15), ks * 4 + (lane >> 4));
       }
-      if constexpr (kSched == 0) {
-        switch (p) {  // one half-tile per phase, each into a half nobody reads any more
-          case 0: stage(4, t_odd); break;      // buffer 1 A_top (read at phase 4)
-          case 1: stage(5, t_odd); break;      // buffer 1 A_bot
-          case 2: stage(2, t_next); break;     // buffer 0 B_left (last read at phase 0)
-          case 3: stage(3, t_next); break;     // buffer 0 B_right
-          case 4: stage(0, t_next); break;     // buffer 0 A_top (last read at phase 2)
-          case 5: stage(1, t_next); break;     // buffer 0 A_bot
-          case 6: stage(6, t_next_odd); break; // buffer 1 B_left (last read at phase 4)
-          default: stage(7, t_next_odd); break;
-        }
-        if ((p & 3) == 3) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // retires everything through phase p-2
-      } else {
-        // Reloads, each >= 2 barriers after the half's last read (group 1 reads one
-        // interval after group 0) and retired by the next vmcnt(6) at phase 3 or 7:
-        //   p1: buffer 1 A_bot  (last read p6 of the previous iteration; read again p4)
-        //   p3: buffer 0 B_left, B_right (last read p1), A_top (last read p2); read next p0-p2
-        //   p5: buffer 0 A_bot  (last read p2; read next p0)
-        //   p7: buffer 1 B_left, B_right (last read p5), A_top (last read p6); read next p4-p6
-        switch (p) {
-          case 1: stage(5, t_odd); break;
-          case 3:
-            stage(2, t_next);
-            stage(3, t_next);
-            stage(0, t_next);
-            break;
-          case 5: stage(1, t_next); break;
-          case 7:
-            stage(6, t_next_odd);
-            stage(7, t_next_odd);
-            stage(4, t_next_odd);
-            break;
-          default: break;
-        }
-        if ((p & 3) == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // all but this phase's 3 half-tiles
+      switch (p) {  // one half-tile per phase, each into a half nobody reads any more
+        case 0: stage(4, t_odd); break;      // buffer 1 A_top (read at phase 4)
+        case 1: stage(5, t_odd); break;      // buffer 1 A_bot
+        case 2: stage(2, t_next); break;     // buffer 0 B_left (last read at phase 0)
+        case 3: stage(3, t_next); break;     // buffer 0 B_right
+        case 4: stage(0, t_next); break;     // buffer 0 A_top (last read at phase 2)
+        case 5: stage(1, t_next); break;     // buffer 0 A_bot
+        case 6: stage(6, t_next_odd); break; // buffer 1 B_left (last read at phase 4)
+        default: stage(7, t_next_odd); break;
       }
+      if ((p & 3) == 3) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // retires everything through phase p-2
       pp_barrier();
       __builtin_amdgcn_s_setprio(1);
       const int mh = (p >> 1) & 1, nh = p & 1;
@@ -768,30 +708,16 @@ bool soak_big_tile(int m, int n) {
   return (m % 256 == 0 && n % 256 == 0) && !(tile_env && std::string(tile_env) == "128");
 }
 
-// BGC_SOAK_KERNEL=2buf keeps the double-buffered kernel and =pingpong0 the first
-// ping-pong schedule, for A/B runs
+// BGC_SOAK_KERNEL=2buf keeps the double-buffered kernel for A/B runs
 bool soak_pingpong(bool big, int k) {
   const char* kern = std::getenv("BGC_SOAK_KERNEL");
   return big && k % (2 * kSoakBK) == 0 && !(kern && std::string(kern) == "2buf");
 }
 
-int soak_pingpong_sched() {
-  const char* kern = std::getenv("BGC_SOAK_KERNEL");
-  return kern && std::string(kern) == "pingpong0" ? 0 : 1;
-}
-
-// bgc_soak_result.kernel: 1 = 2buf, 2 = pingpong, 3 = pingpong0
-int soak_kernel_id(bool big, int k) { return soak_pingpong(big, k) ? (soak_pingpong_sched() == 1 ? 2 : 3) : 1; }
-
 void launch_soak_gemm(bool big, const void* a, const void* bt, void* c, int m, int n, int k, hipStream_t s) {
   if (soak_pingpong(big, k)) {
-    if (soak_pingpong_sched() == 1) {
-      hipLaunchKernelGGL(gemm_pingpong<1>, dim3((m / 256) * (n / 256)), dim3(512), 0, s, static_cast<const __bf16*>(a),
-                         static_cast<const __bf16*>(bt), static_cast<float*>(c), m, n, k);
-    } else {
-      hipLaunchKernelGGL(gemm_pingpong<0>, dim3((m / 256) * (n / 256)), dim3(512), 0, s, static_cast<const __bf16*>(a),
-                         static_cast<const __bf16*>(bt), static_cast<float*>(c), m, n, k);
-    }
+    hipLaunchKernelGGL(gemm_pingpong, dim3((m / 256) * (n / 256)), dim3(512), 0, s, static_cast<const __bf16*>(a),
+                       static_cast<const __bf16*>(bt), static_cast<float*>(c), m, n, k);
   } else if (big) {
     hipLaunchKernelGGL((gemm_soak<256, 256, 2, 4>), dim3((m / 256) * (n / 256)), dim3(512), 0, s,
                        static_cast<const __bf16*>(a), static_cast<const __bf16*>(bt), static_cast<float*>(c), m, n, k);
@@ -1230,7 +1156,7 @@ int bgc_diag_gemm_soak(int device, int m, int n, int k, int launches, uint32_t s
   out->n = n;
   out->k = k;
   out->tile = big ? 256 : 128;
-  out->kernel = soak_kernel_id(big, k);
+  out->kernel = soak_pingpong(big, k) ? 2 : 1;
   out->launches = launches;
   out->elapsed_ms = total;
   out->tflops_best = flop / (best * 1e-3) / 1e12;

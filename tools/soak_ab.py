@@ -1,7 +1,8 @@
 """GEMM soak kernels A/B in one process (cdna guide §5.4 rule 24: interleaved rounds):
 the kernels named in $KERNELS (BGC_SOAK_KERNEL values: 2buf = double-buffered, round 2;
-pingpong0 = the first 8-phase schedule; pingpong = the default), on the soak's {-1,0,1}
-operands, plus an ABFT race screen over several shapes.  Writes gpurun_out/soak_ab.json."""
+pingpong = the 8-phase kernel; a variant under test gets its own value), on the soak's
+{-1,0,1} operands, plus an ABFT race screen over several shapes.  Writes
+gpurun_out/soak_ab.json."""
 import json
 import os
 import statistics
