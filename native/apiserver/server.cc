@@ -2067,7 +2067,11 @@ struct ApiServer::Impl {
     }
     if (!found) return false;
     faults_hit.fetch_add(1);
-    if (hit.delay_ms > 0) std::this_thread::sleep_for(std::chrono::milliseconds(hit.delay_ms));
+    // a delay ends early when the server stops, so no handler outlives it
+    if (hit.delay_ms > 0 && w.wait_stopping(std::chrono::milliseconds(hit.delay_ms))) {
+      w.abort();
+      return true;
+    }
     if (hit.reset) {
       w.abort();
       return true;

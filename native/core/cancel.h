@@ -28,11 +28,11 @@ class CancelToken {
 
   // Sleeps up to `d`; returns true if cancelled (early or already).
   template <typename Rep, typename Period>
-  bool wait_for(std::chrono::duration<Rep, Period> d) {
+  bool wait_for(std::chrono::duration<Rep, Period> d) const {
     std::unique_lock<std::mutex> lk(mu_);
     return cv_.wait_for(lk, d, [&] { return cancelled_.load(); });
   }
-  void wait() {
+  void wait() const {
     std::unique_lock<std::mutex> lk(mu_);
     cv_.wait(lk, [&] { return cancelled_.load(); });
   }
@@ -49,8 +49,8 @@ class CancelToken {
   }
 
  private:
-  std::mutex mu_;
-  std::condition_variable cv_;
+  mutable std::mutex mu_;
+  mutable std::condition_variable cv_;
   std::atomic<bool> cancelled_{false};
   std::vector<std::function<void()>> callbacks_;
 };

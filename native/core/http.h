@@ -121,6 +121,8 @@ class ResponseWriter {
   bool keep_alive() const { return keep_alive_; }
   // True once the server is shutting down; streaming handlers should return.
   bool stopping() const { return stop_.cancelled(); }
+  // Sleeps up to `d`; true (early) once the server is shutting down.
+  bool wait_stopping(std::chrono::milliseconds d) const { return stop_.wait_for(d); }
   // Non-blocking peer liveness probe for long-lived streams.
   virtual bool peer_closed();
   // "HTTP/1.1" or "HTTP/2".
