@@ -13,9 +13,16 @@ set -euo pipefail
 out=${1:?out dir}; diag=${2:?diagnostics library}; rocm=${3:-/opt/rocm}
 mkdir -p "$out"
 cp -L "$rocm/lib/libamd_smi.so" "$diag" "$out/"
-# the code-object manager is dlopen'd by the HIP runtime by its soname (libamd_comgr.so.N),
-# not linked: one copy of that file (the library is ~160 MB)
-for f in "$rocm"/lib/libamd_comgr.so.[0-9]; do [ -e "$f" ] && cp -L "$f" "$out/"; done
+# Libraries loaded with dlopen, by their sonames, so ldd does not list them (found by
+# the loader trace in tests/gpu/test_node_image_closure.py):
+#   libamd_comgr.so.N              the HIP runtime's code-object manager (~160 MB: one copy)
+#   libhsa-amd-aqlprofile64.so     the HSA runtime's profiling extension (opened by its
+#                                  unversioned name)
+#   librocprofiler-sdk-roctx.so.1  the agent's own roctx ranges (native/core/roctx.cc)
+for f in "$rocm"/lib/libamd_comgr.so.[0-9] "$rocm"/lib/libhsa-amd-aqlprofile64.so \
+         "$rocm"/lib/librocprofiler-sdk-roctx.so.[0-9]; do
+  [ -e "$f" ] && cp -L "$f" "$out/"
+done
 while :; do
   added=0
   for f in "$out"/*.so*; do
