@@ -166,7 +166,7 @@ json::Value Diag::gemm_soak(int device, int m, int n, int k, int launches, uint3
   bgc_soak_result r{};
   if (soak_(device, m, n, k, launches, seed, &r) != 0) throw std::runtime_error(std::string("gemm soak: ") + last_error_());
   return json::Value::object({{"device", device}, {"m", r.m}, {"n", r.n}, {"k", r.k}, {"launches", r.launches},
-                              {"tile", r.tile}, {"kernel", r.kernel == 2 ? "pingpong" : r.kernel == 3 ? "pingpongk" : "2buf"},
+                              {"tile", r.tile}, {"kernel", r.kernel == 2 ? "pingpong" : "2buf"},
                               {"elapsed_ms", r.elapsed_ms}, {"tflops_mean", r.tflops_mean},
                               {"tflops_best", r.tflops_best},
                               {"row_mismatches", static_cast<unsigned long long>(r.row_mismatches)},

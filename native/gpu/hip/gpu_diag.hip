@@ -590,141 +590,6 @@ __global__ __launch_bounds__(512, 1) void gemm_pingpong(const __bf16* __restrict
       }
 }
 
-// ---------------------------------------------------------------------------
-// K-split ping-pong (BGC_SOAK_KERNEL=pingpongk, under evaluation against gemm_pingpong).
-//
-// Same block (256x256, 512 threads, two wave groups one barrier apart, 128 KiB of LDS in
-// eight 16 KiB regions), but a region holds one K-HALF of a tile (256 rows x 32 k)
-// instead of one row half, and a phase is one K-half: all 32 of the wave's 16x16 tiles,
-// 32 MFMAs.  Every phase then reads the same 12 fragments (A 8, B 4: 3/8 of the LDS
-// array's time beside the partner's MFMAs), stages the same two regions (4 LDS-DMA
-// pieces per wave), and a K-tile takes 4 barriers instead of 8.
-//
-//   phase (per iteration = 2 K-tiles)    p0        p1        p2        p3
-//   reads (buffer, k-half)               0,k0      0,k1      1,k0      1,k1
-//   stages regions (tile)                4,6 (t+1) 5,7 (t+1) 0,2 (t+2) 1,3 (t+2)
-//   region last read (group 1 interval)  1         3         5         7
-//
-// A region is restaged >= 2 barrier intervals after its last read (buffer 0 k0: read
-// interval 1, staged at 4; k1: 3 -> 6; buffer 1 k0: 5 -> next 8; k1: 7 -> next 10), and
-// each phase's vmcnt(4) retires the previous phase's loads, which are first read one
-// phase later (after the barrier that follows every wave's wait).
-//
-// Region image: row r (64 B = 4 chunks of 8 bf16) keeps chunk c in slot c ^ g(r>>2 & 3),
-// g = {0, 3, 2, 1}: each 16-lane group of a ds_read_b128 (rows l&15, chunk l>>4) then
-// covers all 64 banks once.
-__device__ __forceinline__ int pk_swz(int row) { return (4 - ((row >> 2) & 3)) & 3; }
-
-__device__ __forceinline__ bf16x8 pk_frag(const char* base, int row, int chunk) {
-  return *reinterpret_cast<const bf16x8*>(base + row * 64 + ((chunk ^ pk_swz(row)) << 4));
-}
-
-__device__ __forceinline__ void pk_stage(char* region, const __bf16* __restrict__ src, int K, int row_base, int k0,
-                                         int wid, int lane) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row0 = (i * 8 + wid) * 16;  // 16 rows of 64 B per wave-instruction
-    const int row = row0 + (lane >> 2);
-    const int chunk = (lane & 3) ^ pk_swz(row);  // LDS slot (lane & 3) holds this source chunk
-    const __bf16* g = src + static_cast<size_t>(row_base + row) * K + k0 + chunk * 8;
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                     (__attribute__((address_space(3))) void*)(region + row0 * 64), 16, 0, 0);
-  }
-}
-
-__global__ __launch_bounds__(512, 1) void gemm_pingpong_k(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
-                                                          float* __restrict__ C, int M, int N, int K) {
-  __shared__ __attribute__((aligned(16))) char lds[8 * kPPHalf];  // [buf][A_k0, A_k1, B_k0, B_k1]
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 2, wc = wid & 3;
-  const int nwg = static_cast<int>(gridDim.x), orig = static_cast<int>(blockIdx.x);
-  const int xcd = orig % 8, q = nwg / 8, r = nwg % 8;
-  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
-  const int tiles_m = M / 256, tiles_n = N / 256, group = 8;
-  const int per_group = group * tiles_n;
-  const int first_m = (wgid / per_group) * group;
-  const int gsize = min(tiles_m - first_m, group);
-  const int tm = first_m + (wgid % per_group) % gsize;
-  const int tn = (wgid % per_group) / gsize;
-  const int kt_n = K / kSoakBK;
-  const int a_row = tm * 256, b_row = tn * 256;
-  // region = buf*4 + {0: A k0, 1: A k1, 2: B k0, 3: B k1}
-  auto stage = [&](int region, int t) {
-    const int k0 = min(t, kt_n - 1) * kSoakBK + (region & 1) * 32;
-    char* dst = lds + region * kPPHalf;
-    if ((region & 2) == 0) pk_stage(dst, A, K, a_row, k0, wid, lane);
-    else pk_stage(dst, Bt, K, b_row, k0, wid, lane);
-  };
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 af[8], bfr[4];
-
-  stage(0, 0);
-  stage(2, 0);
-  stage(1, 0);
-  stage(3, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  pp_barrier();
-  if (wr == 1) pp_barrier();  // the stagger
-
-  const int a_r0 = wr * 128, b_r0 = wc * 64;
-  for (int it = 0; it < kt_n / 2; ++it) {
-    const int t_odd = 2 * it + 1, t_next = 2 * it + 2;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const char* ra = lds + ((p >> 1) * 4 + (p & 1)) * kPPHalf;
-      const char* rb = ra + 2 * kPPHalf;
-#pragma unroll
-      for (int mi = 0; mi < 8; ++mi) af[mi] = pk_frag(ra, a_r0 + mi * 16 + (lane & 15), lane >> 4);
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) bfr[ni] = pk_frag(rb, b_r0 + ni * 16 + (lane & 15), lane >> 4);
-      switch (p) {
-        case 0:
-          stage(4, t_odd);
-          stage(6, t_odd);
-          break;
-        case 1:
-          stage(5, t_odd);
-          stage(7, t_odd);
-          break;
-        case 2:
-          stage(0, t_next);
-          stage(2, t_next);
-          break;
-        default:
-          stage(1, t_next);
-          stage(3, t_next);
-          break;
-      }
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // the previous phase's regions have landed
-      pp_barrier();
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-      pp_barrier();
-    }
-  }
-  if (wr == 0) pp_barrier();
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const size_t row = static_cast<size_t>(a_row + wr * 128 + mi * 16 + (lane >> 4) * 4 + j);
-        C[row * N + b_row + wc * 64 + ni * 16 + (lane & 15)] = acc[mi][ni][j];
-      }
-}
-
 // X[rows][cols] = hash-derived values in {-1, 0, 1} (exact in bf16)
 __global__ __launch_bounds__(kBlock) void soak_fill(__bf16* __restrict__ X, uint64_t n, uint32_t seed) {
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n;
@@ -843,26 +708,14 @@ bool soak_big_tile(int m, int n) {
   return (m % 256 == 0 && n % 256 == 0) && !(tile_env && std::string(tile_env) == "128");
 }
 
-// BGC_SOAK_KERNEL=2buf keeps the double-buffered kernel for A/B runs; =pingpongk selects
-// the K-split ping-pong variant under evaluation
+// BGC_SOAK_KERNEL=2buf keeps the double-buffered kernel for A/B runs
 bool soak_pingpong(bool big, int k) {
   const char* kern = std::getenv("BGC_SOAK_KERNEL");
   return big && k % (2 * kSoakBK) == 0 && !(kern && std::string(kern) == "2buf");
 }
 
-bool soak_ksplit() {
-  const char* kern = std::getenv("BGC_SOAK_KERNEL");
-  return kern && std::string(kern) == "pingpongk";
-}
-
-// bgc_soak_result.kernel: 1 = 2buf, 2 = pingpong, 3 = pingpongk
-int soak_kernel_id(bool big, int k) { return soak_pingpong(big, k) ? (soak_ksplit() ? 3 : 2) : 1; }
-
 void launch_soak_gemm(bool big, const void* a, const void* bt, void* c, int m, int n, int k, hipStream_t s) {
-  if (soak_pingpong(big, k) && soak_ksplit()) {
-    hipLaunchKernelGGL(gemm_pingpong_k, dim3((m / 256) * (n / 256)), dim3(512), 0, s, static_cast<const __bf16*>(a),
-                       static_cast<const __bf16*>(bt), static_cast<float*>(c), m, n, k);
-  } else if (soak_pingpong(big, k)) {
+  if (soak_pingpong(big, k)) {
     hipLaunchKernelGGL(gemm_pingpong, dim3((m / 256) * (n / 256)), dim3(512), 0, s, static_cast<const __bf16*>(a),
                        static_cast<const __bf16*>(bt), static_cast<float*>(c), m, n, k);
   } else if (big) {
@@ -1303,7 +1156,7 @@ int bgc_diag_gemm_soak(int device, int m, int n, int k, int launches, uint32_t s
   out->n = n;
   out->k = k;
   out->tile = big ? 256 : 128;
-  out->kernel = soak_kernel_id(big, k);
+  out->kernel = soak_pingpong(big, k) ? 2 : 1;
   out->launches = launches;
   out->elapsed_ms = total;
   out->tflops_best = flop / (best * 1e-3) / 1e12;
