@@ -457,12 +457,22 @@ bool NodeAgent::run_diagnostics(bool force) {
   // by Allocate), give an in-flight admission time to land, then re-check. Only GPUs
   // still free are diagnosed; the rest are released untouched.
   const bool fence = !force && plugin_ && !todo.empty();
+  // whatever happens below (an engine or judge exception), fenced GPUs are released
+  struct Unfence {
+    DevicePlugin* plugin;
+    std::vector<size_t>* gpus;
+    bool armed;
+    ~Unfence() {
+      if (!armed) return;
+      try {
+        plugin->set_fenced(*gpus, false);
+      } catch (...) {
+      }
+    }
+  } unfence{plugin_.get(), &todo, fence};
   if (fence) {
     plugin_->set_fenced(todo, true);
-    if (stop_.wait_for(std::chrono::milliseconds(cfg_.diag_fence_settle_ms))) {
-      plugin_->set_fenced(todo, false);
-      return false;
-    }
+    if (stop_.wait_for(std::chrono::milliseconds(cfg_.diag_fence_settle_ms))) return false;  // unfenced on return
     const std::vector<bool> busy2 = in_use();
     const std::vector<uint64_t> allocs1 = plugin_->allocation_counts();
     std::vector<size_t> still, released;
@@ -552,6 +562,7 @@ bool NodeAgent::run_diagnostics(bool force) {
   if (fence) {  // verdicts first, so a failed GPU never flashes Healthy on release
     plugin_->set_health(healthy_flags());
     plugin_->set_fenced(todo, false);
+    unfence.armed = false;
   }
   auto& reg = metrics::Registry::global();
   reg.counter("bgc_gpu_diag_runs_total", "Diagnostics passes").inc();
