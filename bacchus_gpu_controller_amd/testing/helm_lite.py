@@ -161,20 +161,60 @@ def _go_sprintf(fmt, args):
 
 # ----------------------------------------------------------------------------- lexing
 
-_ACTION = re.compile(r"\{\{(-[ \t\r\n])?(.*?)([ \t\r\n]-)?\}\}", re.S)
+def _actions(src):
+    """(start, end, left_trim, body, right_trim) of every {{ ... }} action, as Go's lexer
+    finds them: a "}}" inside a quoted or raw (backquoted) string does not end the action
+    (e.g. {{`{{ $labels.gpu }}`}}, how a chart emits Prometheus template text)."""
+    pos = 0
+    while True:
+        start = src.find("{{", pos)
+        if start < 0:
+            return
+        i = start + 2
+        left = src.startswith("-", i) and i + 1 < len(src) and src[i + 1] in " \t\r\n"
+        if left:
+            i += 1
+        body_start = i
+        while True:
+            if i >= len(src):
+                raise TemplateError("unclosed action")
+            c = src[i]
+            if src.startswith("/*", i):
+                j = src.find("*/", i + 2)
+                if j < 0:
+                    raise TemplateError("unclosed comment")
+                i = j + 2
+            elif c == '"':
+                i += 1
+                while i < len(src) and src[i] != '"':
+                    i += 2 if src[i] == "\\" else 1
+                i += 1
+            elif c == "`":
+                j = src.find("`", i + 1)
+                if j < 0:
+                    raise TemplateError("unclosed raw string")
+                i = j + 1
+            elif src.startswith("}}", i):
+                break
+            else:
+                i += 1
+        body, right = src[body_start:i], False
+        if len(body) >= 2 and body[-1] == "-" and body[-2] in " \t\r\n":
+            body, right = body[:-1], True
+        yield start, i + 2, left, body, right
+        pos = i + 2
 
 
 def _lex(src):
     """-> list of ("text", s) / ("action", s) with trim markers applied."""
     items, pos = [], 0
-    for m in _ACTION.finditer(src):
-        text = src[pos:m.start()]
-        if m.group(1):
+    for start, end, left, body, right in _actions(src):
+        text = src[pos:start]
+        if left:
             text = text.rstrip(" \t\r\n")
         items.append(["text", text])
-        body = m.group(2).strip()
-        items.append(["action", body, bool(m.group(3))])
-        pos = m.end()
+        items.append(["action", body.strip(), right])
+        pos = end
     items.append(["text", src[pos:]])
     # right-trim markers eat leading whitespace of the following text
     out = []

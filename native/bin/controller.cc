@@ -103,5 +103,5 @@ int main() {
       [&](const kube::ObjPtr& o, const std::exception& e) { return rec.error_policy(o, e); });
   health.stop(std::chrono::milliseconds(1000));
   LOG_INFO("controller") << "controller gracefully shutted down";
-  return 0;
+  return leader && leader->lost() ? 1 : 0;  // a lost lease is a failure: restart as a standby
 }

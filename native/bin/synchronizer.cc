@@ -83,6 +83,7 @@ int main() {
   sync::Synchronizer s(*client, [&] { return drive->export_file(file_id, "text/csv"); }, cfg);
   s.set_version_source([&] { return drive->file_version(file_id); });
   int rc = s.run(*stop);
+  if (rc == 0 && leader && leader->lost()) rc = 1;  // a lost lease is a failure: restart as a standby
   health.stop(std::chrono::milliseconds(1000));
   if (rc == 0) {
     LOG_INFO("synchronizer") << "synchronizer gracefully shutted down";

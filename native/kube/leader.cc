@@ -179,6 +179,7 @@ void LeaderElector::keep_renewing(std::shared_ptr<CancelToken> stop_on_loss) {
       }
       if (a == Attempt::HeldByOther) {
         LOG_ERROR("leader") << "lease " << s_.ns << "/" << s_.name << " is held by another replica; stepping down";
+        lost_ = true;
         stop_on_loss->cancel();
         return;
       }
@@ -193,6 +194,7 @@ void LeaderElector::keep_renewing(std::shared_ptr<CancelToken> stop_on_loss) {
       if (ns_now() - last_ok_sent_ns_.load() >= deadline_ns) {
         LOG_ERROR("leader") << "lost lease " << s_.ns << "/" << s_.name << " (renew deadline " << s_.renew_deadline_seconds
                             << " s passed); shutting down";
+        lost_ = true;
         stop_on_loss->cancel();
         return;
       }

@@ -54,6 +54,9 @@ class LeaderElector {
   // Renews in the background until destroyed; on loss of the lease cancels `stop_on_loss`.
   // The elector must outlive the work it guards (keep it in main's scope).
   void keep_renewing(std::shared_ptr<CancelToken> stop_on_loss);
+  // True once keep_renewing() stepped down (renew deadline passed or another holder):
+  // the process should exit non-zero, as client-go's OnStoppedLeading does.
+  bool lost() const { return lost_.load(); }
   const std::string& identity() const { return identity_; }
 
  private:
@@ -65,6 +68,7 @@ class LeaderElector {
   std::thread watchdog_;
   CancelToken stop_renew_;
   std::atomic<int64_t> last_ok_sent_ns_{0};  // steady clock
+  std::atomic<bool> lost_{false};
 };
 
 // Acquires leadership when `s.enabled` (blocking until acquired or stopped) and keeps it

@@ -158,6 +158,7 @@ def test_leader_steps_down_when_lease_taken():
                     raise
         wait_for(lambda: not leader.alive(), timeout=10, desc="leader exits")
         assert "held by another replica; stepping down" in leader.output()
+        assert leader.p.returncode == 1  # a lost lease is a failure (client-go: OnStoppedLeading)
 
 
 def test_leader_steps_down_at_renew_deadline_while_renew_hangs():
@@ -184,6 +185,7 @@ def test_leader_steps_down_at_renew_deadline_while_renew_hangs():
         assert elapsed < 3.6, f"leader acted for {elapsed:.1f} s after the apiserver stalled"
         # the hung renew is bounded by the Lease client's own timeout (deadline - retry = 2 s)
         wait_for(lambda: not leader.alive(), timeout=5, desc="leader exits")
+        assert leader.p.returncode == 1
 
 
 def test_graceful_shutdown_exit_codes():

@@ -399,3 +399,29 @@ def test_admission_http2_toggle():
 
     assert env_of({})["CONF_HTTP2"] == "true"
     assert env_of({"admission": {"configs": {"http2": False}}})["CONF_HTTP2"] == "false"
+
+
+def test_prometheus_rule_alerts_reference_exported_series():
+    """The optional PrometheusRule: off by default; when on, every series its alerts use
+    is one the services really export (registered in native/)."""
+    import glob
+    import re
+
+    assert not [m for m in render({"metrics": {"enabled": True}}) if m.get("kind") == "PrometheusRule"]
+    ms = render({"metrics": {"enabled": True, "prometheusRule": {"enabled": True, "labels": {"release": "prom"},
+                                                                  "xgmiLinksExpected": 6}}})
+    rule = [m for m in ms if m.get("kind") == "PrometheusRule"]
+    assert len(rule) == 1 and rule[0]["metadata"]["labels"]["release"] == "prom"
+    alerts = {r["alert"]: r for g in rule[0]["spec"]["groups"] for r in g["rules"]}
+    assert {"AMDGPUUnhealthy", "AMDGPUDiagnosticsFailed", "AMDGPUUncorrectableECC", "AMDGPUXGMILinkDown",
+            "BGCReconcileErrors", "BGCAdmissionSlow"} <= set(alerts)
+    assert alerts["AMDGPUXGMILinkDown"]["expr"] == "amd_gpu_xgmi_links_up < 6"
+    assert "{{ $labels.gpu }}" in alerts["AMDGPUUnhealthy"]["annotations"]["summary"]  # escaped for Prometheus
+    exported = set()
+    for f in glob.glob(os.path.join(REPO_ROOT, "native", "**", "*.cc"), recursive=True):
+        exported |= set(re.findall(r'"((?:amd_gpu|bgc)_[a-z0-9_]+)"', open(f).read()))
+    used = set()
+    for a in alerts.values():
+        for name in re.findall(r"\b((?:amd_gpu|bgc)_[a-z0-9_]+)", a["expr"]):
+            used.add(re.sub(r"_bucket$", "", name))
+    assert used and used <= exported, used - exported
