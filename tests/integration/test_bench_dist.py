@@ -68,3 +68,16 @@ def test_auto_concurrency_follows_cpu_share():
     # a bigger share keeps more tenants in flight, capped at 32 per rank
     assert [auto_concurrency(n, 128) for n in (1, 2, 4, 8)] == [32, 32, 32, 23]
     assert 1 <= effective_cpus() <= (os.cpu_count() or 1)
+
+
+def test_single_tenant_bench_config1():
+    """BASELINE config #1 as a bench mode: crdgen byte-identical to the chart, and tenants
+    onboarded one at a time through the whole stack with per-stage latencies."""
+    cmd = [sys.executable, "-m", "bacchus_gpu_controller_amd.bench.single", "--tenants", "4"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=REPO_ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["config"] == 1 and d["crdgen"]["byte_identical"] and d["tenants"] == 4
+    st = d["apply_to_stage_ms"]
+    assert 0 < st["namespace"]["p50"] <= st["quota"]["p50"] <= st["rolebinding"]["p50"] < 5000
+    assert d["reconcile_ms"]["p50"] > 0
