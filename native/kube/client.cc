@@ -156,6 +156,8 @@ KubeConfig KubeConfig::from_kubeconfigs(const std::vector<std::string>& paths, c
       for (const auto& a : ex.get("args").items()) e.args.push_back(a.as_string());
       for (const auto& kv : ex.get("env").items()) e.env.emplace_back(kv.get_string("name"), kv.get_string("value"));
       e.provide_cluster_info = ex.get("provideClusterInfo").is_bool() && ex.get("provideClusterInfo").as_bool();
+      e.interactive_mode = ex.get_string("interactiveMode");
+      e.install_hint = ex.get_string("installHint");
       if (e.command.empty()) throw std::runtime_error("kubeconfig: exec plugin of user " + user_name + " has no command");
       if (e.api_version != "client.authentication.k8s.io/v1" && e.api_version != "client.authentication.k8s.io/v1beta1") {
         throw std::runtime_error("kubeconfig: exec plugin apiVersion " + e.api_version + " is not supported");
@@ -289,6 +291,12 @@ std::string KubeClient::plugin_token(bool force) {
       "bgc_kube_client_credential_refreshes_total", "Credentials fetched from a kubeconfig exec plugin or auth-provider");
   if (cfg_.exec) {
     const auto& e = *cfg_.exec;
+    // services run without a terminal: a plugin that must prompt cannot run (client-go
+    // refuses the same way when stdin is not a terminal)
+    if (e.interactive_mode == "Always") {
+      throw std::runtime_error("exec credential plugin " + e.command +
+                               " requires interactive mode (interactiveMode: Always), but standard input is not a terminal");
+    }
     Value info = Value::object({{"apiVersion", e.api_version}, {"kind", "ExecCredential"}});
     Value spec = Value::object({{"interactive", false}});
     if (e.provide_cluster_info) {
@@ -305,9 +313,11 @@ std::string KubeClient::plugin_token(bool force) {
     env.emplace_back("KUBERNETES_EXEC_INFO", info.dump());
     RunResult r = run_command(argv, env, cfg_.exec_timeout_ms);
     if (r.exit_code != 0) {
-      throw std::runtime_error("exec credential plugin " + e.command + " failed (" +
-                               (r.timed_out ? std::string("timed out") : "exit " + std::to_string(r.exit_code)) +
-                               "): " + r.err.substr(0, 500));
+      std::string msg = "exec credential plugin " + e.command + " failed (" +
+                        (r.timed_out ? std::string("timed out") : "exit " + std::to_string(r.exit_code)) +
+                        "): " + r.err.substr(0, 500);
+      if (r.err.rfind("cannot run ", 0) == 0 && !e.install_hint.empty()) msg += "\n" + e.install_hint;
+      throw std::runtime_error(msg);
     }
     Value cred;
     std::string perr;

@@ -39,6 +39,8 @@ struct KubeConfig {
     std::vector<std::string> args;
     std::vector<std::pair<std::string, std::string>> env;
     bool provide_cluster_info = false;
+    std::string interactive_mode;  // Never | IfAvailable | Always ("" = IfAvailable)
+    std::string install_hint;      // shown when the command cannot be run
   };
   std::optional<ExecPlugin> exec;
   // users[].user.auth-provider (kube-client 0.84 without its oidc feature): "oidc" uses the

@@ -215,6 +215,8 @@ PYBIND11_MODULE(_native, m) {
       e["command"] = c.exec->command;
       e["args"] = c.exec->args;
       e["provide_cluster_info"] = c.exec->provide_cluster_info;
+      e["interactive_mode"] = c.exec->interactive_mode;
+      e["install_hint"] = c.exec->install_hint;
       d["exec"] = e;
     }
     return d;

@@ -222,3 +222,27 @@ def test_controller_binary_runs_on_an_exec_plugin_kubeconfig(tmp_path):
                                           "metadata": {"name": "exec-user"}, "spec": {"kube_username": "exec-user"}})
         wait_for(lambda: c.admin.get_or_none("namespaces", "exec-user"), timeout=15, desc="namespace via exec creds")
         assert _calls(pd)  # the plugin really ran
+
+
+def test_exec_plugin_install_hint_and_interactive_mode(nat, tmp_path):
+    """client-go parity: a missing command reports the kubeconfig's installHint, and a
+    plugin that insists on a terminal (interactiveMode: Always) is refused, since the
+    services never have one."""
+    with Cluster(admission=False, controller=False, tls_apiserver=True) as c:
+        d = tmp_path / "hint"
+        d.mkdir()
+        kc = _cluster_kubeconfig(c, str(d / "missing"), """exec:
+  apiVersion: client.authentication.k8s.io/v1
+  command: bgc-no-such-credential-helper
+  installHint: "install it with: apt install bgc-credential-helper\"""")
+        assert nat.kubeconfig_parse(kc)["exec"]["install_hint"].startswith("install it with")
+        with pytest.raises(Exception, match="(?s)cannot run.*install it with: apt install"):
+            nat.kube_request(kc, "GET", "/api/v1/namespaces", 1)
+        pd = _plugin_dir(tmp_path, [ADMIN_TOKEN])
+        kc = _cluster_kubeconfig(c, str(pd / "config"), """exec:
+  apiVersion: client.authentication.k8s.io/v1
+  command: ./plugin.py
+  interactiveMode: Always""")
+        with pytest.raises(Exception, match="interactive mode"):
+            nat.kube_request(kc, "GET", "/api/v1/namespaces", 1)
+        assert not _calls(pd)  # refused before running it
