@@ -3,6 +3,7 @@
 // and keeps a telemetry side thread (amdsmi gpu_metrics) feeding health + /metrics.
 #include <cstdio>
 #include <memory>
+#include <string>
 
 #include "core/cancel.h"
 #include "core/env_config.h"
@@ -11,12 +12,15 @@
 #include "core/log.h"
 #include "core/process.h"
 #include "gpu/device.h"
+#include "gpu/diag_runner.h"
 #include "gpu/node_agent.h"
 #include "kube/client.h"
 
 using namespace bgc;
 
-int main() {
+int main(int argc, char** argv) {
+  // a diagnostics worker (gpu/diag_runner.h): one request, then exit
+  if (argc > 1 && std::string(argv[1]) == "--diag-worker") return gpu::diag_worker_main();
   process_init();
   gpu::NodeAgentConfig cfg;
   try {

@@ -11,6 +11,14 @@
 #include <mutex>
 #include <thread>
 
+#include <fcntl.h>
+#include <sys/file.h>
+#include <unistd.h>
+
+#include <cstdlib>
+
+#include "core/log.h"
+#include "core/subprocess.h"
 #include "gpu/telemetry.h"
 
 namespace bgc::gpu {
@@ -57,8 +65,34 @@ void nap(const std::atomic<bool>& done, int ms) {
   for (int i = 0; i < ms / 10 && !done.load(); ++i) std::this_thread::sleep_for(std::chrono::milliseconds(10));
 }
 
+void sleep_until(std::chrono::steady_clock::time_point t) {
+  if (t > std::chrono::steady_clock::now()) std::this_thread::sleep_until(t);
+}
+
+// flock(2) on a file: PCIe sections of concurrent worker processes take turns.
+class FileLock {
+ public:
+  explicit FileLock(const std::string& path) {
+    if (path.empty()) return;
+    fd_ = ::open(path.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0600);
+    if (fd_ >= 0) {
+      while (::flock(fd_, LOCK_EX) != 0 && errno == EINTR) {
+      }
+    }
+  }
+  ~FileLock() {
+    if (fd_ >= 0) ::close(fd_);  // releases the lock
+  }
+  FileLock(const FileLock&) = delete;
+  FileLock& operator=(const FileLock&) = delete;
+
+ private:
+  int fd_ = -1;
+};
+
 class HipDiagEngine : public DiagEngine {
  public:
+  explicit HipDiagEngine(std::string pcie_lock_path = "") : pcie_lock_path_(std::move(pcie_lock_path)) {}
   std::string name() const override { return "hip"; }
   Value checks(Backend& backend, const GpuInfo& g, int dev, const DiagPlan& plan, uint32_t seed) override {
     Diag& d = Diag::instance();
@@ -86,6 +120,7 @@ class HipDiagEngine : public DiagEngine {
       // the GPU's link.  ~50 ms per GPU.
       static std::mutex pcie_mu;
       std::lock_guard<std::mutex> lk(pcie_mu);
+      FileLock across_processes(pcie_lock_path_);
       r["pcie"] = pcie_check(backend, g, dev, plan.pcie_bytes, seed);
       lap("pcie");
     }
@@ -96,7 +131,68 @@ class HipDiagEngine : public DiagEngine {
     r["timing_ms"] = timing;
     return r;
   }
-  Value burn(int dev, int duration_ms, uint32_t seed) override { return Diag::instance().burn(dev, duration_ms, 32, seed); }
+  Value burn(int dev, int duration_ms, uint32_t seed, std::chrono::steady_clock::time_point start_at) override {
+    Diag& d = Diag::instance();  // HIP initialised before the wait, not inside the burn window
+    sleep_until(start_at);
+    return d.burn(dev, duration_ms, 32, seed);
+  }
+
+ private:
+  std::string pcie_lock_path_;
+};
+
+std::string self_exe() {
+  char buf[4096];
+  const ssize_t n = ::readlink("/proc/self/exe", buf, sizeof(buf) - 1);
+  return n > 0 ? std::string(buf, static_cast<size_t>(n)) : std::string();
+}
+
+// Runs one worker request; the result JSON, or throws with the worker's error.
+Value run_worker(const std::string& exe, const Value& request, int visible_device, int timeout_ms) {
+  std::vector<std::pair<std::string, std::string>> env{{"BGC_DIAG_REQUEST", request.dump()}};
+  // only its own GPU: HSA opens no other device, so the worker leaves no footprint there
+  if (visible_device >= 0) env.emplace_back("ROCR_VISIBLE_DEVICES", std::to_string(visible_device));
+  RunResult r = run_command({exe, "--diag-worker"}, env, timeout_ms);
+  if (r.exit_code != 0) {
+    throw std::runtime_error("diagnostics worker " +
+                             (r.timed_out ? std::string("timed out") : "failed (exit " + std::to_string(r.exit_code) + ")") +
+                             (r.err.empty() ? "" : ": " + r.err.substr(r.err.size() > 800 ? r.err.size() - 800 : 0)));
+  }
+  Value out;
+  std::string perr;
+  const size_t brace = r.out.find('{');
+  if (brace == std::string::npos || !json::try_parse(std::string_view(r.out).substr(brace), out, &perr)) {
+    throw std::runtime_error("diagnostics worker printed no result: " + perr);
+  }
+  if (out.get("error").is_string()) throw std::runtime_error(out.get_string("error"));
+  return out;
+}
+
+class ProcessDiagEngine : public DiagEngine {
+ public:
+  ProcessDiagEngine(std::string exe, std::string kind, std::string fixture, std::string lock)
+      : exe_(std::move(exe)), kind_(std::move(kind)), fixture_(std::move(fixture)), lock_(std::move(lock)) {}
+  std::string name() const override { return "hip"; }
+  int start_lead_ms() const override { return 2000; }  // a worker's HIP start-up on one visible GPU
+  Value checks(Backend&, const GpuInfo& g, int dev, const DiagPlan& plan, uint32_t seed) override {
+    Value req = Value::object({{"op", "checks"}, {"backend", kind_}, {"fixture", fixture_}, {"gpu", to_json(g)},
+                               {"plan", to_json(plan)}, {"seed", static_cast<unsigned long long>(seed)},
+                               {"pcie_lock", lock_}});
+    const auto t0 = std::chrono::steady_clock::now();
+    // the walk's budget, the soak and the PCIe copies (waiting for the other GPUs' turns)
+    Value r = run_worker(exe_, req, dev, 600000);
+    r["worker_ms"] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return r;
+  }
+  Value burn(int dev, int duration_ms, uint32_t seed, std::chrono::steady_clock::time_point start_at) override {
+    const int64_t at = std::chrono::duration_cast<std::chrono::nanoseconds>(start_at.time_since_epoch()).count();
+    Value req = Value::object({{"op", "burn"}, {"duration_ms", duration_ms}, {"seed", static_cast<unsigned long long>(seed)},
+                               {"start_at_ns", static_cast<long long>(at)}});
+    return run_worker(exe_, req, dev, duration_ms + 120000);
+  }
+
+ private:
+  std::string exe_, kind_, fixture_, lock_;
 };
 
 // Re-reads the script from the backend on every call, so a test can change a running
@@ -130,7 +226,8 @@ class ScriptedDiagEngine : public DiagEngine {
     if (e.get("fail").is_string()) r["error"] = e.get_string("fail");
     return r;
   }
-  Value burn(int dev, int duration_ms, uint32_t) override {
+  Value burn(int dev, int duration_ms, uint32_t, std::chrono::steady_clock::time_point start_at) override {
+    sleep_until(start_at);
     std::this_thread::sleep_for(std::chrono::milliseconds(duration_ms));
     const Value script = backend_.diag_script();
     const double tf = num(script.get("gpus").get(std::to_string(dev)), "burn_tflops", num(script, "burn_tflops", 2400));
@@ -147,6 +244,83 @@ class ScriptedDiagEngine : public DiagEngine {
 }  // namespace
 
 std::unique_ptr<DiagEngine> make_hip_diag_engine() { return std::make_unique<HipDiagEngine>(); }
+
+std::unique_ptr<DiagEngine> make_process_diag_engine(std::string exe, std::string backend_kind,
+                                                     std::string mock_fixture_path, std::string pcie_lock_path) {
+  if (exe.empty()) exe = self_exe();
+  return std::make_unique<ProcessDiagEngine>(std::move(exe), std::move(backend_kind), std::move(mock_fixture_path),
+                                             std::move(pcie_lock_path));
+}
+
+std::vector<std::string> worker_device_bdfs(const std::string& exe) {
+  const Value r = run_worker(exe.empty() ? self_exe() : exe, Value::object({{"op", "devices"}}), -1, 120000);
+  std::vector<std::string> out;
+  for (const auto& b : r.get("bdfs").items()) out.push_back(b.as_string());
+  return out;
+}
+
+Value to_json(const DiagPlan& p) {
+  return Value::object({{"hbm_bytes", static_cast<unsigned long long>(p.hbm_bytes)},
+                        {"hbm_walk_fraction", p.hbm_walk_fraction},
+                        {"hbm_walk_chunk_bytes", static_cast<unsigned long long>(p.hbm_walk_chunk_bytes)},
+                        {"hbm_walk_budget_ms", p.hbm_walk_budget_ms},
+                        {"pcie_bytes", static_cast<unsigned long long>(p.pcie_bytes)},
+                        {"soak_size", p.soak_size},
+                        {"soak_launches", p.soak_launches},
+                        {"burn_ms", p.burn_ms}});
+}
+
+DiagPlan diag_plan_from_json(const Value& v) {
+  DiagPlan p;
+  auto u64 = [&](const char* k, uint64_t d) { return v.get(k).is_int() ? v.get(k).as_uint() : d; };
+  auto i32 = [&](const char* k, int d) { return v.get(k).is_int() ? static_cast<int>(v.get(k).as_int()) : d; };
+  p.hbm_bytes = u64("hbm_bytes", p.hbm_bytes);
+  p.hbm_walk_fraction = v.get("hbm_walk_fraction").is_number() ? v.get("hbm_walk_fraction").as_double() : p.hbm_walk_fraction;
+  p.hbm_walk_chunk_bytes = u64("hbm_walk_chunk_bytes", p.hbm_walk_chunk_bytes);
+  p.hbm_walk_budget_ms = i32("hbm_walk_budget_ms", p.hbm_walk_budget_ms);
+  p.pcie_bytes = u64("pcie_bytes", p.pcie_bytes);
+  p.soak_size = i32("soak_size", p.soak_size);
+  p.soak_launches = i32("soak_launches", p.soak_launches);
+  p.burn_ms = i32("burn_ms", p.burn_ms);
+  return p;
+}
+
+int diag_worker_main() {
+  Value out;
+  try {
+    const char* req_text = std::getenv("BGC_DIAG_REQUEST");
+    if (!req_text) throw std::runtime_error("BGC_DIAG_REQUEST is not set");
+    const Value req = json::parse(req_text);
+    const std::string op = req.get_string("op");
+    // the parent made this worker's GPU the only visible one (ROCR_VISIBLE_DEVICES)
+    const int dev = std::getenv("ROCR_VISIBLE_DEVICES") || !req.get("hip_device").is_int()
+                        ? 0
+                        : static_cast<int>(req.get("hip_device").as_int());
+    const uint32_t seed = static_cast<uint32_t>(req.get("seed").is_int() ? req.get("seed").as_uint() : 0x5eed);
+    if (op == "devices") {
+      Diag& d = Diag::instance();
+      Value b = Value::array();
+      for (int i = 0, n = d.device_count(); i < n; ++i) b.push_back(d.device_bdf(i));
+      out = Value::object({{"bdfs", b}});
+    } else if (op == "checks") {
+      auto backend = make_backend(req.get_string("backend", "amdsmi"), req.get_string("fixture"));
+      HipDiagEngine engine(req.get_string("pcie_lock"));
+      out = engine.checks(*backend, gpu_info_from_json(req.get("gpu")), dev, diag_plan_from_json(req.get("plan")), seed);
+    } else if (op == "burn") {
+      HipDiagEngine engine;
+      const auto at = std::chrono::steady_clock::time_point(std::chrono::nanoseconds(req.get("start_at_ns").as_int()));
+      out = engine.burn(dev, static_cast<int>(req.get("duration_ms").as_int()), seed, at);
+    } else {
+      throw std::runtime_error("unknown diagnostics worker op '" + op + "'");
+    }
+  } catch (const std::exception& e) {
+    out = Value::object({{"error", std::string(e.what())}});
+  }
+  const std::string text = out.dump() + "\n";
+  std::fwrite(text.data(), 1, text.size(), stdout);
+  std::fflush(stdout);
+  return 0;
+}
 
 std::unique_ptr<DiagEngine> make_scripted_diag_engine(Backend& backend) {
   return std::make_unique<ScriptedDiagEngine>(backend);
@@ -204,7 +378,7 @@ Value burn_in(Backend& backend, int index, int hip_device, int duration_ms, uint
   });
   Value out;
   try {
-    out = engine->burn(hip_device, duration_ms, seed);
+    out = engine->burn(hip_device, duration_ms, seed, std::chrono::steady_clock::time_point());
   } catch (...) {
     done = true;
     sampler.join();
@@ -231,9 +405,13 @@ NodeBurnResult node_burn(Backend& backend, DiagEngine& engine, const std::vector
   std::atomic<bool> done{false};
   double sum_max = 0, sum_acc = 0, peak_hot = 0;
   int sweeps = 0;
+  // Every GPU starts at the same instant: after the engine's start-up lead (a worker
+  // process initialises HIP first), not when its thread happens to get there.
+  const auto start_at = std::chrono::steady_clock::now() + std::chrono::milliseconds(engine.start_lead_ms());
   // One sampler for the whole node: each sweep reads every GPU under load, so the summed
   // power is the node's draw at one moment rather than a sum of separate peaks.
   std::thread sampler([&] {
+    while (!done.load() && std::chrono::steady_clock::now() < start_at) nap(done, 20);
     while (!done.load()) {
       double sum = 0;
       int ok = 0;
@@ -266,7 +444,7 @@ NodeBurnResult node_burn(Backend& backend, DiagEngine& engine, const std::vector
         cv.wait(lk, [&] { return go; });
       }
       try {
-        res.per_gpu[k] = engine.burn(hip_devs[which[k]], duration_ms, seed + static_cast<uint32_t>(which[k]));
+        res.per_gpu[k] = engine.burn(hip_devs[which[k]], duration_ms, seed + static_cast<uint32_t>(which[k]), start_at);
       } catch (const std::exception& e) {
         err[k] = e.what();
       }
@@ -274,6 +452,7 @@ NodeBurnResult node_burn(Backend& backend, DiagEngine& engine, const std::vector
   }
   for (auto& w : workers) w.join();
   const double wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  const double start_lead_ms = std::chrono::duration<double, std::milli>(start_at - t0).count();
   done = true;
   sampler.join();
   Value per = Value::array();
@@ -287,6 +466,7 @@ NodeBurnResult node_burn(Backend& backend, DiagEngine& engine, const std::vector
   res.node = Value::object({{"gpus", static_cast<unsigned long long>(n)},
                             {"duration_ms", duration_ms},
                             {"wall_ms", wall_ms},
+                            {"start_lead_ms", start_lead_ms},
                             {"sweeps", sweeps},
                             {"power_sum_max_w", sum_max},
                             {"power_sum_mean_w", sweeps ? sum_acc / sweeps : 0.0},

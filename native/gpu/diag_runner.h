@@ -18,6 +18,7 @@
 // durations and outcomes) so fencing and concurrency are tested on CPU hosts.
 #pragma once
 
+#include <chrono>
 #include <cstdint>
 #include <memory>
 #include <string>
@@ -44,15 +45,37 @@ class DiagEngine {
  public:
   virtual ~DiagEngine() = default;
   virtual std::string name() const = 0;
+  // How far ahead node_burn schedules a common start (time a burn needs to get ready).
+  virtual int start_lead_ms() const { return 0; }
   // Everything but the burn for one GPU: {"hbm","hbm_walk","mfma","gemm","pcie","soak"}.
   // Throws on a HIP/library error.
   virtual json::Value checks(Backend& backend, const GpuInfo& g, int hip_device, const DiagPlan& plan,
                              uint32_t seed) = 0;
-  // Sustained MFMA load on one GPU (Diag::burn's result shape).
-  virtual json::Value burn(int hip_device, int duration_ms, uint32_t seed) = 0;
+  // Sustained MFMA load on one GPU (Diag::burn's result shape), starting at start_at
+  // (steady clock; the epoch = now) so that GPUs burning together start together.
+  virtual json::Value burn(int hip_device, int duration_ms, uint32_t seed,
+                           std::chrono::steady_clock::time_point start_at) = 0;
 };
 
+// In this process (the python bindings, tools): the first call initialises HIP here.
 std::unique_ptr<DiagEngine> make_hip_diag_engine();
+// The node agent's engine: every check and burn runs in a child process (`exe
+// --diag-worker`, see diag_worker_main) that sees only its own GPU
+// (ROCR_VISIBLE_DEVICES).  The agent itself never initialises HIP, so between passes it
+// holds no GPU context and no VRAM, a GPU fault in a kernel ends the worker rather than
+// the agent, and amdsmi's process list shows only tenants' processes (a container's
+// getpid() is not the host PID KFD reports, so the agent could not recognise itself).
+// PCIe sections of concurrent workers take turns on an flock(2) of pcie_lock_path.
+std::unique_ptr<DiagEngine> make_process_diag_engine(std::string exe, std::string backend_kind,
+                                                     std::string mock_fixture_path, std::string pcie_lock_path);
+// PCI addresses of the HIP devices, in HIP order, read by a worker process.
+std::vector<std::string> worker_device_bdfs(const std::string& exe);
+// `node-agent --diag-worker`: the request JSON in $BGC_DIAG_REQUEST ({"op": "devices" |
+// "checks" | "burn", ...}), the result JSON (or {"error": ...}) on stdout.
+int diag_worker_main();
+
+json::Value to_json(const DiagPlan& p);
+DiagPlan diag_plan_from_json(const json::Value& v);
 // Replays backend.diag_script() (re-read on every call):
 //   {"checks_ms": 200, "burn_tflops": 2400,
 //    "gpus": {"<index>": {"checks_ms": .., "burn_tflops": .., "walk_mismatches": .., "fail": "<text>"}}}

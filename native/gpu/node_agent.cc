@@ -353,18 +353,34 @@ DiagPlan NodeAgent::diag_plan() const {
 void NodeAgent::setup_diag() {
   if (engine_) return;
   const Value script = backend_->diag_script();
-  engine_ = script.is_object() ? make_scripted_diag_engine(*backend_) : make_hip_diag_engine();
+  // HIP work runs in worker processes (make_process_diag_engine); BGC_DIAG_IN_PROCESS=1
+  // keeps it in the agent, which then holds a GPU context on every GPU from the first pass
+  const char* inproc = std::getenv("BGC_DIAG_IN_PROCESS");
+  diag_in_process_ = inproc && std::string(inproc) == "1";
+  if (script.is_object()) {
+    engine_ = make_scripted_diag_engine(*backend_);
+  } else if (diag_in_process_) {
+    engine_ = make_hip_diag_engine();
+  } else {
+    pcie_lock_path_ = "/tmp/bgc-node-agent-" + std::to_string(::getpid()) + ".pcie.lock";
+    engine_ = make_process_diag_engine("", cfg_.backend, cfg_.mock_fixture_path, pcie_lock_path_);
+  }
   std::vector<std::string> bdfs;
   if (engine_->name() == "hip") {
     try {
-      Diag& d = Diag::instance();
-      for (int i = 0, n = d.device_count(); i < n; ++i) bdfs.push_back(d.device_bdf(i));
+      if (diag_in_process_) {
+        Diag& d = Diag::instance();
+        for (int i = 0, n = d.device_count(); i < n; ++i) bdfs.push_back(d.device_bdf(i));
+      } else {
+        bdfs = worker_device_bdfs("");
+      }
     } catch (const std::exception& e) {
       LOG_WARN("node_agent") << "HIP device BDFs unavailable (" << e.what() << "); using amdsmi hip ids";
     }
   }
   hip_devs_ = hip_devices_for(gpus_, bdfs);
-  LOG_INFO("node_agent") << "diagnostics engine " << engine_->name() << ", " << bdfs.size() << " HIP devices named by BDF";
+  LOG_INFO("node_agent") << "diagnostics engine " << engine_->name() << (diag_in_process_ ? " (in process)" : " (worker processes)")
+                         << ", " << bdfs.size() << " HIP devices named by BDF";
 }
 
 std::vector<bool> NodeAgent::in_use() const {
@@ -695,6 +711,7 @@ void NodeAgent::start() {
 
 void NodeAgent::stop() {
   stop_.cancel();
+  if (!pcie_lock_path_.empty()) ::unlink(pcie_lock_path_.c_str());
   if (poller_) poller_->stop();
   if (plugin_) plugin_->stop();
   if (heartbeat_.joinable()) heartbeat_.join();
@@ -726,6 +743,7 @@ Value NodeAgent::describe() const {
   out["diag_node_burn"] = d.node_burn;
   out["diag_fence_races"] = static_cast<unsigned long long>(fence_races_.load());
   out["diag_engine"] = engine_ ? Value(engine_->name()) : Value();
+  out["diag_isolation"] = !engine_ ? Value() : Value(engine_->name() != "hip" ? "none" : diag_in_process_ ? "in-process" : "worker-process");
   Value hd = Value::array();
   for (int h : hip_devs_) hd.push_back(h);
   out["hip_devices"] = hd;

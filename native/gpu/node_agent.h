@@ -177,6 +177,8 @@ class NodeAgent {
   std::thread diag_thread_;
   std::unique_ptr<TelemetryPoller> poller_;
   std::unique_ptr<DevicePlugin> plugin_;
+  bool diag_in_process_ = false;
+  std::string pcie_lock_path_;
   std::mutex publish_mu_;
   CancelToken stop_;
   std::thread heartbeat_;
