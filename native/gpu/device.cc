@@ -722,7 +722,12 @@ class AmdSmiBackend : public Backend {
 
   int busy_processes(int index) override {
     if (index < 0 || static_cast<size_t>(index) >= handles_.size() || !api_.process_list) return -1;
-    // Processes other than this one (the agent's own diagnostics hold a HIP context).
+    // Processes other than this one that hold memory on the GPU or have run work on it.
+    // A process that merely opened the device (a monitoring daemon's KFD context: no
+    // VRAM, no GTT, no engine time; on the MI355X box one such host process is always
+    // listed) is not a tenant.  A container's getpid() is not the host PID KFD reports,
+    // so the agent keeps HIP out of its own process (gpu/diag_runner.h) rather than rely
+    // on recognising itself here.
     std::lock_guard<std::mutex> hl(*handle_mu_[static_cast<size_t>(index)]);
     std::vector<amdsmi_proc_info_t> procs(64);
     uint32_t n = static_cast<uint32_t>(procs.size());
@@ -730,7 +735,11 @@ class AmdSmiBackend : public Backend {
     if (st != AMDSMI_STATUS_SUCCESS && st != AMDSMI_STATUS_OUT_OF_RESOURCES) return -1;
     const uint32_t self = static_cast<uint32_t>(::getpid());
     int others = 0;
-    for (uint32_t k = 0; k < n && k < procs.size(); ++k) others += procs[k].pid != self ? 1 : 0;
+    for (uint32_t k = 0; k < n && k < procs.size(); ++k) {
+      const auto& p = procs[k];
+      const bool holds = p.mem > 0 || p.memory_usage.vram_mem > 0 || p.memory_usage.gtt_mem > 0 || p.engine_usage.gfx > 0;
+      others += p.pid != self && holds ? 1 : 0;
+    }
     if (n > procs.size()) others += static_cast<int>(n - procs.size());
     return others;
   }

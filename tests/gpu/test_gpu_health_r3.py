@@ -108,3 +108,33 @@ def test_node_agent_startup_pass_and_first_advertise(tmp_path):
             assert desc["startup_ms"]["first_advertise"] >= desc["startup_ms"]["diagnostics"] > 3000
     finally:
         kubelet.stop()
+
+
+def test_periodic_pass_diagnoses_idle_gpu_in_worker_processes(tmp_path):
+    """Periodic passes really run on an idle MI355X: the HIP work happens in worker
+    processes, so the agent holds no GPU context between passes (small RSS, VRAM back to
+    the idle level) and amdsmi never lists the agent as the GPU's user.  Before, every
+    pass after the first was skipped as "in use" (the agent's own context, reported under
+    its host PID, which the container's getpid() cannot match)."""
+    from bacchus_gpu_controller_amd.testing.cluster import Cluster
+    from bacchus_gpu_controller_amd.testing.kubeapi import wait_for
+
+    import requests
+
+    with Cluster(admission=False, controller=False) as c:
+        c.start_node_agent(node_name="mi355x-periodic", backend="amdsmi", max_gpus=1, poll_interval_ms=500,
+                           extra_env={"CONF_RUN_DIAG": "true", "CONF_DIAG_BURN_MS": "500", "CONF_DIAG_INTERVAL_SECS": "3",
+                                      "CONF_DIAG_HBM_WALK_FRACTION": "0.2"})
+        url = f"http://127.0.0.1:{c.node_agent_ports['mi355x-periodic']}/gpus"
+        wait_for(lambda: requests.get(url, timeout=5).json().get("diag_runs", 0) >= 3, timeout=110, interval=0.5,
+                 desc="three diagnostics passes")
+        desc = requests.get(url, timeout=5).json()
+        pid = c.procs["node-agent"].p.pid
+        rss_mb = int(open(f"/proc/{pid}/status").read().split("VmRSS:")[1].split()[0]) / 1024
+        _dump("periodic_pass.json", {"diag_runs": desc["diag_runs"], "skipped_in_use": desc["diag_skipped_in_use"],
+                                     "last_pass_ms": desc["diag_last_pass_ms"], "isolation": desc["diag_isolation"],
+                                     "agent_rss_mb": rss_mb, "vram_used_mb": desc["telemetry"][0]["vram_used_mb"]})
+        assert desc["diag_isolation"] == "worker-process"
+        assert desc["diag_skipped_in_use"] == 0 and desc["diag_last_pass_ms"] > 1000, desc["diag_last_pass_ms"]
+        assert desc["diag"][0]["passed"], desc["diag"][0]["failures"]
+        assert rss_mb < 200  # the HIP runtime in the agent itself took ~1.2 GB
