@@ -74,3 +74,25 @@ def test_node_agent_waits_for_kubelet_registration():
         labels = node["metadata"]["labels"]
         assert labels["kubernetes.io/hostname"] == "mi355x-9" and labels["amd.com/gpu.count"] == "8"
         assert c.procs["na"].alive()
+
+
+def test_diag_worker_protocol():
+    """`node-agent --diag-worker` (gpu/diag_runner.h): one JSON request from
+    $BGC_DIAG_REQUEST, one JSON result on stdout, exit 0 even on errors (the agent reads
+    the error from the result).  On a CPU host HIP sees no devices."""
+    import subprocess
+
+    from bacchus_gpu_controller_amd import binary
+
+    def worker(req):
+        env = dict(os.environ, BGC_DIAG_REQUEST=json.dumps(req))
+        p = subprocess.run([binary("node-agent"), "--diag-worker"], env=env, capture_output=True, text=True, timeout=60)
+        assert p.returncode == 0, p.stderr
+        return json.loads(p.stdout)
+
+    assert "bdfs" in worker({"op": "devices"})
+    assert "unknown diagnostics worker op" in worker({"op": "bogus"})["error"]
+    p = subprocess.run([binary("node-agent"), "--diag-worker"], env={k: v for k, v in os.environ.items()
+                                                                      if k != "BGC_DIAG_REQUEST"},
+                       capture_output=True, text=True, timeout=60)
+    assert "BGC_DIAG_REQUEST is not set" in json.loads(p.stdout)["error"]
