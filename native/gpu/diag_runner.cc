@@ -158,10 +158,14 @@ Value run_worker(const std::string& exe, const Value& request, int visible_devic
                              (r.timed_out ? std::string("timed out") : "failed (exit " + std::to_string(r.exit_code) + ")") +
                              (r.err.empty() ? "" : ": " + r.err.substr(r.err.size() > 800 ? r.err.size() - 800 : 0)));
   }
+  // the result is the last line (anything a library prints to stdout comes before it)
+  std::string_view text(r.out);
+  while (!text.empty() && (text.back() == '\n' || text.back() == '\r')) text.remove_suffix(1);
+  const size_t nl = text.rfind('\n');
+  if (nl != std::string_view::npos) text.remove_prefix(nl + 1);
   Value out;
   std::string perr;
-  const size_t brace = r.out.find('{');
-  if (brace == std::string::npos || !json::try_parse(std::string_view(r.out).substr(brace), out, &perr)) {
+  if (text.empty() || !json::try_parse(text, out, &perr)) {
     throw std::runtime_error("diagnostics worker printed no result: " + perr);
   }
   if (out.get("error").is_string()) throw std::runtime_error(out.get_string("error"));
