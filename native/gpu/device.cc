@@ -744,6 +744,27 @@ class AmdSmiBackend : public Backend {
     return others;
   }
 
+  Value processes(int index) override {
+    Value out = Value::array();
+    if (index < 0 || static_cast<size_t>(index) >= handles_.size() || !api_.process_list) return out;
+    std::lock_guard<std::mutex> hl(*handle_mu_[static_cast<size_t>(index)]);
+    std::vector<amdsmi_proc_info_t> procs(64);
+    uint32_t n = static_cast<uint32_t>(procs.size());
+    amdsmi_status_t st = api_.process_list(handles_[static_cast<size_t>(index)], &n, procs.data());
+    if (st != AMDSMI_STATUS_SUCCESS && st != AMDSMI_STATUS_OUT_OF_RESOURCES) return out;
+    for (uint32_t k = 0; k < n && k < procs.size(); ++k) {
+      const auto& p = procs[k];
+      const bool holds = p.mem > 0 || p.memory_usage.vram_mem > 0 || p.memory_usage.gtt_mem > 0 || p.engine_usage.gfx > 0;
+      out.push_back(Value::object({{"pid", static_cast<unsigned long long>(p.pid)},
+                                   {"name", std::string(p.name, strnlen(p.name, sizeof(p.name)))},
+                                   {"vram_bytes", static_cast<unsigned long long>(p.memory_usage.vram_mem)},
+                                   {"gtt_bytes", static_cast<unsigned long long>(p.memory_usage.gtt_mem)},
+                                   {"gfx_ns", static_cast<unsigned long long>(p.engine_usage.gfx)},
+                                   {"holds", holds}}));
+    }
+    return out;
+  }
+
   std::vector<PhysLink> read_links(amdsmi_processor_handle h) {
     std::vector<PhysLink> out;
     if (!api_.link_metrics) return out;

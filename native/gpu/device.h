@@ -147,6 +147,9 @@ class Backend {
   virtual Telemetry sample(int index, SampleLevel level = SampleLevel::Ras) = 0;
   // Compute processes currently holding the device (-1 = unknown).
   virtual int busy_processes(int index) { (void)index; return -1; }
+  // Every process the driver lists on the device: [{pid, name, vram_bytes, gtt_bytes,
+  // gfx_ns, holds}] (holds = counted by busy_processes); empty when unknown.
+  virtual json::Value processes(int index) { (void)index; return json::Value::array(); }
   // Mock backends only: a scripted diagnostics engine (diag_runner.h) instead of the HIP
   // kernels; null = run the real diagnostics.
   virtual json::Value diag_script() { return json::Value(); }

@@ -742,6 +742,9 @@ Value NodeAgent::describe() const {
   out["diag_last_diagnosed"] = static_cast<unsigned long long>(d.last_diagnosed);
   out["diag_node_burn"] = d.node_burn;
   out["diag_fence_races"] = static_cast<unsigned long long>(fence_races_.load());
+  Value procs = Value::array();  // what the driver lists on each GPU (why a pass skipped it)
+  for (const auto& g : gpus_) procs.push_back(backend_->processes(g.index));
+  out["processes"] = procs;
   out["diag_engine"] = engine_ ? Value(engine_->name()) : Value();
   out["diag_isolation"] = !engine_ ? Value() : Value(engine_->name() != "hip" ? "none" : diag_in_process_ ? "in-process" : "worker-process");
   Value hd = Value::array();
