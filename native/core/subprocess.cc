@@ -7,6 +7,7 @@
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <map>
@@ -16,7 +17,7 @@ extern char** environ;
 namespace bgc {
 
 RunResult run_command(const std::vector<std::string>& argv, const std::vector<std::pair<std::string, std::string>>& env,
-                      int timeout_ms) {
+                      int timeout_ms, const CancelToken* cancel) {
   RunResult res;
   if (argv.empty()) {
     res.err = "empty command";
@@ -76,7 +77,12 @@ RunResult run_command(const std::vector<std::string>& argv, const std::vector<st
       ::kill(pid, SIGKILL);
       break;
     }
-    const int n = ::poll(fds, 2, static_cast<int>(left.count()));
+    if (cancel && cancel->cancelled()) {
+      res.cancelled = true;
+      ::kill(pid, SIGKILL);
+      break;
+    }
+    const int n = ::poll(fds, 2, static_cast<int>(std::min<int64_t>(left.count(), cancel ? 100 : left.count())));
     if (n < 0) {
       if (errno == EINTR) continue;
       break;

@@ -12,7 +12,9 @@
 #include <thread>
 
 #include <fcntl.h>
+#include <signal.h>
 #include <sys/file.h>
+#include <sys/prctl.h>
 #include <unistd.h>
 
 #include <cstdlib>
@@ -148,11 +150,13 @@ std::string self_exe() {
 }
 
 // Runs one worker request; the result JSON, or throws with the worker's error.
-Value run_worker(const std::string& exe, const Value& request, int visible_device, int timeout_ms) {
+Value run_worker(const std::string& exe, const Value& request, int visible_device, int timeout_ms,
+                 const CancelToken* cancel = nullptr) {
   std::vector<std::pair<std::string, std::string>> env{{"BGC_DIAG_REQUEST", request.dump()}};
   // only its own GPU: HSA opens no other device, so the worker leaves no footprint there
   if (visible_device >= 0) env.emplace_back("ROCR_VISIBLE_DEVICES", std::to_string(visible_device));
-  RunResult r = run_command({exe, "--diag-worker"}, env, timeout_ms);
+  RunResult r = run_command({exe, "--diag-worker"}, env, timeout_ms, cancel);
+  if (r.cancelled) throw std::runtime_error("diagnostics worker stopped: the agent is shutting down");
   if (r.exit_code != 0) {
     throw std::runtime_error("diagnostics worker " +
                              (r.timed_out ? std::string("timed out") : "failed (exit " + std::to_string(r.exit_code) + ")") +
@@ -174,8 +178,9 @@ Value run_worker(const std::string& exe, const Value& request, int visible_devic
 
 class ProcessDiagEngine : public DiagEngine {
  public:
-  ProcessDiagEngine(std::string exe, std::string kind, std::string fixture, std::string lock)
-      : exe_(std::move(exe)), kind_(std::move(kind)), fixture_(std::move(fixture)), lock_(std::move(lock)) {}
+  ProcessDiagEngine(std::string exe, std::string kind, std::string fixture, std::string lock, const CancelToken* cancel)
+      : exe_(std::move(exe)), kind_(std::move(kind)), fixture_(std::move(fixture)), lock_(std::move(lock)),
+        cancel_(cancel) {}
   std::string name() const override { return "hip"; }
   int start_lead_ms() const override { return 2000; }  // a worker's HIP start-up on one visible GPU
   Value checks(Backend&, const GpuInfo& g, int dev, const DiagPlan& plan, uint32_t seed) override {
@@ -184,7 +189,7 @@ class ProcessDiagEngine : public DiagEngine {
                                {"pcie_lock", lock_}});
     const auto t0 = std::chrono::steady_clock::now();
     // the walk's budget, the soak and the PCIe copies (waiting for the other GPUs' turns)
-    Value r = run_worker(exe_, req, dev, 600000);
+    Value r = run_worker(exe_, req, dev, 600000, cancel_);
     r["worker_ms"] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return r;
   }
@@ -192,11 +197,12 @@ class ProcessDiagEngine : public DiagEngine {
     const int64_t at = std::chrono::duration_cast<std::chrono::nanoseconds>(start_at.time_since_epoch()).count();
     Value req = Value::object({{"op", "burn"}, {"duration_ms", duration_ms}, {"seed", static_cast<unsigned long long>(seed)},
                                {"start_at_ns", static_cast<long long>(at)}});
-    return run_worker(exe_, req, dev, duration_ms + 120000);
+    return run_worker(exe_, req, dev, duration_ms + 120000, cancel_);
   }
 
  private:
   std::string exe_, kind_, fixture_, lock_;
+  const CancelToken* cancel_;
 };
 
 // Re-reads the script from the backend on every call, so a test can change a running
@@ -250,10 +256,11 @@ class ScriptedDiagEngine : public DiagEngine {
 std::unique_ptr<DiagEngine> make_hip_diag_engine() { return std::make_unique<HipDiagEngine>(); }
 
 std::unique_ptr<DiagEngine> make_process_diag_engine(std::string exe, std::string backend_kind,
-                                                     std::string mock_fixture_path, std::string pcie_lock_path) {
+                                                     std::string mock_fixture_path, std::string pcie_lock_path,
+                                                     const CancelToken* cancel) {
   if (exe.empty()) exe = self_exe();
   return std::make_unique<ProcessDiagEngine>(std::move(exe), std::move(backend_kind), std::move(mock_fixture_path),
-                                             std::move(pcie_lock_path));
+                                             std::move(pcie_lock_path), cancel);
 }
 
 std::vector<std::string> worker_device_bdfs(const std::string& exe) {
@@ -290,6 +297,12 @@ DiagPlan diag_plan_from_json(const Value& v) {
 }
 
 int diag_worker_main() {
+  // The worker must not outlive the agent (a burn or a walk left running on a GPU the
+  // restarted agent is about to diagnose): die with the thread that spawned it, which
+  // waits for this process to finish.
+  const pid_t parent = ::getppid();
+  ::prctl(PR_SET_PDEATHSIG, SIGKILL);
+  if (::getppid() != parent) return 1;  // the parent died before the line above
   Value out;
   try {
     const char* req_text = std::getenv("BGC_DIAG_REQUEST");

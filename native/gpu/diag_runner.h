@@ -24,6 +24,7 @@
 #include <string>
 #include <vector>
 
+#include "core/cancel.h"
 #include "core/json.h"
 #include "gpu/device.h"
 #include "gpu/diag.h"
@@ -66,8 +67,10 @@ std::unique_ptr<DiagEngine> make_hip_diag_engine();
 // the agent, and amdsmi's process list shows only tenants' processes (a container's
 // getpid() is not the host PID KFD reports, so the agent could not recognise itself).
 // PCIe sections of concurrent workers take turns on an flock(2) of pcie_lock_path.
+// A running worker is killed as soon as `cancel` is cancelled (the agent stopping).
 std::unique_ptr<DiagEngine> make_process_diag_engine(std::string exe, std::string backend_kind,
-                                                     std::string mock_fixture_path, std::string pcie_lock_path);
+                                                     std::string mock_fixture_path, std::string pcie_lock_path,
+                                                     const CancelToken* cancel = nullptr);
 // PCI addresses of the HIP devices, in HIP order, read by a worker process.
 std::vector<std::string> worker_device_bdfs(const std::string& exe);
 // `node-agent --diag-worker`: the request JSON in $BGC_DIAG_REQUEST ({"op": "devices" |

@@ -363,7 +363,7 @@ void NodeAgent::setup_diag() {
     engine_ = make_hip_diag_engine();
   } else {
     pcie_lock_path_ = "/tmp/bgc-node-agent-" + std::to_string(::getpid()) + ".pcie.lock";
-    engine_ = make_process_diag_engine("", cfg_.backend, cfg_.mock_fixture_path, pcie_lock_path_);
+    engine_ = make_process_diag_engine("", cfg_.backend, cfg_.mock_fixture_path, pcie_lock_path_, &stop_);
   }
   std::vector<std::string> bdfs;
   if (engine_->name() == "hip") {

@@ -111,7 +111,8 @@ def test_node_agent_startup_pass_and_first_advertise(tmp_path):
 
 
 def test_periodic_pass_diagnoses_idle_gpu_in_worker_processes(tmp_path):
-    """Periodic passes really run on an idle MI355X: the HIP work happens in worker
+    """Periodic passes really run on an idle MI355X (and are skipped while another process
+    holds it): the HIP work happens in worker
     processes, so the agent holds no GPU context between passes (small RSS, VRAM back to
     the idle level) and amdsmi never lists the agent as the GPU's user.  Before, every
     pass after the first was skipped as "in use" (the agent's own context, reported under
@@ -135,6 +136,13 @@ def test_periodic_pass_diagnoses_idle_gpu_in_worker_processes(tmp_path):
                                      "last_pass_ms": desc["diag_last_pass_ms"], "isolation": desc["diag_isolation"],
                                      "agent_rss_mb": rss_mb, "vram_used_mb": desc["telemetry"][0]["vram_used_mb"]})
         assert desc["diag_isolation"] == "worker-process"
-        assert desc["diag_skipped_in_use"] == 0 and desc["diag_last_pass_ms"] > 1000, desc["diag_last_pass_ms"]
-        assert desc["diag"][0]["passed"], desc["diag"][0]["failures"]
         assert rss_mb < 200  # the HIP runtime in the agent itself took ~1.2 GB
+        holders = [p for p in desc["processes"][0] if p["holds"]]
+        _dump("periodic_pass_processes.json", desc["processes"])
+        if holders:
+            # another process holds the GPU (in a full `pytest -m gpu` run: this test
+            # process, whose earlier tests created a torch context): skipping is right
+            assert desc["diag_skipped_in_use"] >= 1, desc
+        else:
+            assert desc["diag_skipped_in_use"] == 0 and desc["diag_last_pass_ms"] > 1000, desc["diag_last_pass_ms"]
+        assert desc["diag"][0]["passed"], desc["diag"][0]["failures"]
