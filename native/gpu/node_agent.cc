@@ -38,6 +38,10 @@ NodeAgentConfig NodeAgentConfig::from_env(const EnvConfig& env) {
   c.diag_hbm_walk_chunk_mb = env.u64_or("diag_hbm_walk_chunk_mb", c.diag_hbm_walk_chunk_mb);
   c.diag_hbm_walk_budget_ms = env.u64_or("diag_hbm_walk_budget_ms", c.diag_hbm_walk_budget_ms);
   c.diag_fence_settle_ms = env.u64_or("diag_fence_settle_ms", c.diag_fence_settle_ms);
+  c.diag_start_busy = env.str_or("diag_start_busy", c.diag_start_busy);
+  if (c.diag_start_busy != "skip" && c.diag_start_busy != "diagnose") {
+    throw std::runtime_error("CONF_DIAG_START_BUSY must be skip or diagnose, not " + c.diag_start_busy);
+  }
   c.diag_floors.min_hbm_walk_coverage = env.f64_or("diag_min_hbm_walk_coverage", c.diag_floors.min_hbm_walk_coverage);
   c.diag_floors.min_node_burn_balance = env.f64_or("diag_min_node_burn_balance", c.diag_floors.min_node_burn_balance);
   c.diag_floors.max_node_power_w = env.f64_or("diag_max_node_power_w", c.diag_floors.max_node_power_w);
@@ -447,7 +451,7 @@ void NodeAgent::record_diag_gauges(size_t i, const Value& r) {
   }
 }
 
-bool NodeAgent::run_diagnostics(bool force) {
+bool NodeAgent::run_diagnostics(bool at_start) {
   setup_diag();
   using clock = std::chrono::steady_clock;
   const auto t_pass = clock::now();
@@ -463,7 +467,11 @@ bool NodeAgent::run_diagnostics(bool force) {
   // Allocation counters first: an Allocate that lands between the in_use() snapshot and
   // the fence shows up as a changed counter.
   const std::vector<uint64_t> allocs0 = plugin_ ? plugin_->allocation_counts() : std::vector<uint64_t>{};
-  const std::vector<bool> busy = force ? std::vector<bool>(gpus_.size(), false) : in_use();
+  // Busy GPUs are left alone at start as well: an agent restarted (an upgrade, a crash) on
+  // a node whose GPUs run tenants' jobs must not burn or walk them.  They keep no verdict
+  // (not failed) until a periodic pass finds them free.
+  const std::vector<bool> busy =
+      at_start && cfg_.diag_start_busy == "diagnose" ? std::vector<bool>(gpus_.size(), false) : in_use();
   std::vector<size_t> todo;
   for (size_t i = 0; i < gpus_.size(); ++i) {
     if (busy[i]) keep_previous(i, "in use");
@@ -472,7 +480,7 @@ bool NodeAgent::run_diagnostics(bool force) {
   // Fence: withdraw the candidates from the kubelet (Unhealthy in ListAndWatch, refused
   // by Allocate), give an in-flight admission time to land, then re-check. Only GPUs
   // still free are diagnosed; the rest are released untouched.
-  const bool fence = !force && plugin_ && !todo.empty();
+  const bool fence = !at_start && plugin_ && !todo.empty();  // at start nothing is advertised yet
   // whatever happens below (an engine or judge exception), fenced GPUs are released
   struct Unfence {
     DevicePlugin* plugin;

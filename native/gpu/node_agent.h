@@ -64,6 +64,11 @@ struct NodeAgentConfig {
   // Every GPU is diagnosed on its own thread and the burn-in is one node-level phase
   // (gpu/diag_runner.h).  A periodic pass first fences its GPUs in the device plugin
   // (listed Unhealthy, refused by Allocate), waits `diag_fence_settle_ms` for an
+  // GPUs that a container (pod-resources) or a process (amdsmi) holds when the agent
+  // starts: "skip" leaves them without a verdict until a periodic pass finds them free;
+  // "diagnose" runs the start-up pass on them anyway (a fresh node, or a test whose own
+  // process holds the GPU)
+  std::string diag_start_busy = "skip";
   // in-flight admission to land, re-checks that they are still free and only then runs.
   bool run_diag = false;
   uint64_t diag_hbm_bytes = 1ULL << 30;  // bandwidth phases (two buffers)
@@ -150,7 +155,7 @@ class NodeAgent {
   std::vector<bool> healthy_flags() const;
   // One diagnostics pass over every GPU not held by a container; returns true when any
   // GPU's verdict changed (and then re-publishes health).  `force` ignores allocation.
-  bool run_diagnostics(bool force = false);
+  bool run_diagnostics(bool at_start = false);
   DiagOutcome diag_outcome() const;
 
  private:

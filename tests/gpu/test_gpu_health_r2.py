@@ -125,6 +125,7 @@ def _agent_with_floors(tmp_path, name, floors_env):
     try:
         with Cluster(admission=False, controller=False) as c:
             env = {"CONF_DEVICE_PLUGIN": "true", "CONF_DEVICE_PLUGIN_DIR": d, "CONF_RUN_DIAG": "true",
+                   "CONF_DIAG_START_BUSY": "diagnose",  # this test process may hold the GPU
                    "CONF_DIAG_HBM_BYTES": str(1 << 30), "CONF_HEARTBEAT_SECS": "1"}
             env.update(floors_env)
             c.start_node_agent(node_name=name, backend="amdsmi", max_gpus=1, poll_interval_ms=200, extra_env=env)

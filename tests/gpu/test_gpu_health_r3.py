@@ -93,6 +93,7 @@ def test_node_agent_startup_pass_and_first_advertise(tmp_path):
             c.start_node_agent(node_name="mi355x-r3", backend="amdsmi", max_gpus=1, poll_interval_ms=200,
                                extra_env={"CONF_DEVICE_PLUGIN": "true", "CONF_DEVICE_PLUGIN_DIR": d,
                                           "CONF_RUN_DIAG": "true", "CONF_DIAG_BURN_MS": "3000",
+                                          "CONF_DIAG_START_BUSY": "diagnose",  # this process may hold the GPU
                                           "CONF_HEARTBEAT_SECS": "1"})
             assert kubelet.wait(lambda: kubelet.device_lists, timeout=90)
             wall = time.time() - t0
@@ -125,6 +126,7 @@ def test_periodic_pass_diagnoses_idle_gpu_in_worker_processes(tmp_path):
     with Cluster(admission=False, controller=False) as c:
         c.start_node_agent(node_name="mi355x-periodic", backend="amdsmi", max_gpus=1, poll_interval_ms=500,
                            extra_env={"CONF_RUN_DIAG": "true", "CONF_DIAG_BURN_MS": "500", "CONF_DIAG_INTERVAL_SECS": "3",
+                                      "CONF_DIAG_START_BUSY": "diagnose",
                                       "CONF_DIAG_HBM_WALK_FRACTION": "0.2", "CONF_DIAG_MIN_HBM_WALK_COVERAGE": "0.15"})
         url = f"http://127.0.0.1:{c.node_agent_ports['mi355x-periodic']}/gpus"
         wait_for(lambda: requests.get(url, timeout=5).json().get("diag_runs", 0) >= 3, timeout=110, interval=0.5,

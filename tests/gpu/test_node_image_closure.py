@@ -46,7 +46,8 @@ def test_node_agent_runs_on_the_image_closure(tmp_path):
         c.start_node_agent(node_name="mi355x-img", backend="amdsmi", max_gpus=1, poll_interval_ms=200,
                            extra_env={"LD_LIBRARY_PATH": str(rt), "BGC_GPU_DIAG_LIB": str(rt / "libbgc_gpu_diag.so"),
                                       "LD_DEBUG": "files", "LD_DEBUG_OUTPUT": str(ld_dir / "ld"),
-                                      "CONF_RUN_DIAG": "true", "CONF_DIAG_BURN_MS": "1000"})
+                                      "CONF_RUN_DIAG": "true", "CONF_DIAG_BURN_MS": "1000",
+                                      "CONF_DIAG_START_BUSY": "diagnose"})  # this test process may hold the GPU
         port = c.node_agent_ports["mi355x-img"]
         wait_for(lambda: requests.get(f"http://127.0.0.1:{port}/gpus", timeout=5).json().get("diag"), timeout=90,
                  desc="diagnostics pass")

@@ -159,3 +159,31 @@ def test_node_burn_gates_on_summed_power_and_balance(nat):
         node = wait_for(lambda: (lambda n: n if n and n["metadata"]["labels"].get("amd.com/gpu.diag") == "failed" else None)(
             c.admin.get_or_none("nodes", "mi355x-pw")), timeout=15, desc="diag label")
         assert node["metadata"]["labels"]["amd.com/gpu.healthy-count"] == "0"
+
+
+def test_restart_leaves_busy_gpus_alone(nat, tmp_path):
+    """An agent (re)started on a node whose GPUs already run jobs must not burn or walk
+    them: the start-up pass diagnoses only free GPUs, a busy one stays advertised without
+    a verdict, and a later periodic pass diagnoses it once its job is gone."""
+    d = str(tmp_path / "dp")
+    kubelet = FakeKubelet(d).start()
+    fx = _fixture(nat, 4, {"checks_ms": 50})
+    fx["gpus"][2]["telemetry"]["busy_processes"] = 1  # a tenant process holds GPU 2 (amdsmi)
+    try:
+        with Cluster(admission=False, controller=False) as c:
+            c.start_node_agent(node_name="mi355x-restart", backend="mock", poll_interval_ms=100, fixture_obj=fx,
+                               extra_env={"CONF_DEVICE_PLUGIN": "true", "CONF_DEVICE_PLUGIN_DIR": d,
+                                          "CONF_RUN_DIAG": "true", "CONF_DIAG_INTERVAL_SECS": "1",
+                                          "CONF_DIAG_FENCE_SETTLE_MS": "100", "CONF_DIAG_BURN_MS": "100",
+                                          "CONF_HEARTBEAT_SECS": "1"})
+            assert kubelet.wait(lambda: kubelet.registrations and kubelet.device_lists, timeout=15)
+            assert all(x[1] == "Healthy" for x in kubelet.device_lists[-1][1])  # the busy GPU is still offered
+            desc = _describe(c, "mi355x-restart")
+            assert desc["diag"][2] is None and desc["diag_skipped_in_use"] >= 1
+            assert all(desc["diag"][i]["passed"] for i in (0, 1, 3))
+            fx["gpus"][2]["telemetry"]["busy_processes"] = 0  # the job ends
+            c.set_gpu_fixture("mi355x-restart", fx)
+            wait_for(lambda: (_describe(c, "mi355x-restart")["diag"][2] or {}).get("passed"), timeout=20,
+                     desc="GPU 2 diagnosed once free")
+    finally:
+        kubelet.stop()
