@@ -188,8 +188,11 @@ class ProcessDiagEngine : public DiagEngine {
                                {"plan", to_json(plan)}, {"seed", static_cast<unsigned long long>(seed)},
                                {"pcie_lock", lock_}});
     const auto t0 = std::chrono::steady_clock::now();
-    // the walk's budget, the soak and the PCIe copies (waiting for the other GPUs' turns)
-    Value r = run_worker(exe_, req, dev, 600000, cancel_);
+    // a healthy pass takes ~3 s (8 s with the VRAM clear of a reused GPU); the bound
+    // covers the walk's budget, the PCIe copies waiting for the other GPUs' turns and a
+    // slow HIP start, so a hung kernel costs the pass at most this long
+    const int timeout_ms = std::max(60000, plan.hbm_walk_budget_ms + 90000);
+    Value r = run_worker(exe_, req, dev, timeout_ms, cancel_);
     r["worker_ms"] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return r;
   }
@@ -197,7 +200,7 @@ class ProcessDiagEngine : public DiagEngine {
     const int64_t at = std::chrono::duration_cast<std::chrono::nanoseconds>(start_at.time_since_epoch()).count();
     Value req = Value::object({{"op", "burn"}, {"duration_ms", duration_ms}, {"seed", static_cast<unsigned long long>(seed)},
                                {"start_at_ns", static_cast<long long>(at)}});
-    return run_worker(exe_, req, dev, duration_ms + 120000, cancel_);
+    return run_worker(exe_, req, dev, duration_ms + start_lead_ms() + 60000, cancel_);
   }
 
  private:
