@@ -3,12 +3,15 @@ telemetry poller and the kubelet device plugin running, to show that repeated pa
 not leak (agent RSS, VRAM in use after each pass) and that their verdicts and rates are
 stable.
 
-    python3 tools/node_agent_soak.py OUT.json [minutes=8] [interval_s=20]
+    python3 tools/node_agent_soak.py OUT.json [minutes=8] [interval_s=20] [tenant_from_min tenant_to_min]
 
-Prints one progress line per sample (every 10 s).
+With a tenant window, a "tenant" process (torch: 16 GiB resident and a matmul loop)
+holds the GPU in that window: passes then must skip the GPU as in use, and resume once
+the tenant exits.  Prints one progress line per sample (every 10 s).
 """
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -28,10 +31,25 @@ def rss_mb(pid):
     return None
 
 
+TENANT = """
+import time, torch
+x = torch.empty(16 << 30, dtype=torch.uint8, device="cuda")
+a = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+print("tenant up", flush=True)
+while True:
+    for _ in range(50):
+        a = (a @ a).clamp_(-1, 1)
+    torch.cuda.synchronize()
+    time.sleep(0.05)
+"""
+
+
 def main():
     out_path = sys.argv[1]
     minutes = float(sys.argv[2]) if len(sys.argv) > 2 else 8.0
     interval = int(sys.argv[3]) if len(sys.argv) > 3 else 20
+    window = (float(sys.argv[4]) * 60, float(sys.argv[5]) * 60) if len(sys.argv) > 5 else None
+    tenant = None
     d = "/tmp/bgc-soak-dp"
     os.makedirs(d, exist_ok=True)
     kubelet = FakeKubelet(d).start()
@@ -49,17 +67,27 @@ def main():
             seen_runs = 0
             while time.time() - t0 < minutes * 60:
                 time.sleep(10)
+                now = time.time() - t0
+                if window and tenant is None and window[0] <= now < window[1]:
+                    tenant = subprocess.Popen([sys.executable, "-c", TENANT], stdout=subprocess.DEVNULL)
+                if window and tenant is not None and now >= window[1] and tenant.poll() is None:
+                    tenant.kill()
+                    tenant.wait(30)
                 g = requests.get(url, timeout=10).json()
                 tele = (g.get("telemetry") or [{}])[0] if isinstance(g.get("telemetry"), list) else {}
                 runs = g.get("diag_runs", 0)
                 s = {"t_s": round(time.time() - t0, 1), "rss_mb": rss_mb(pid), "diag_runs": runs,
+                     "tenant": tenant is not None and tenant.poll() is None,
+                     "skipped_in_use": g.get("diag_skipped_in_use"),
                      "vram_used_mb": tele.get("vram_used_mb"), "healthy": g.get("healthy"),
                      "last_pass_ms": g.get("diag_last_pass_ms")}
                 samples.append(s)
                 if runs != seen_runs:
                     seen_runs = runs
                     r = (g.get("diag") or [{}])[0]
-                    passes.append({"run": runs, "passed": r.get("passed"), "failures": r.get("failures"),
+                    passes.append({"run": runs, "t_s": s["t_s"], "tenant": s["tenant"],
+                                   "skipped_in_use": g.get("diag_skipped_in_use"),
+                                   "passed": r.get("passed"), "failures": r.get("failures"),
                                    "pass_ms": g.get("diag_last_pass_ms"),
                                    "soak_tflops": (r.get("soak") or {}).get("tflops_mean"),
                                    "burn_tflops": (r.get("burn") or {}).get("tflops_mean"),
@@ -69,6 +97,8 @@ def main():
             out = {"minutes": minutes, "interval_s": interval, "samples": samples, "passes": passes,
                    "fence_races": g.get("diag_fence_races"), "agent_alive": c.procs["node-agent"].alive()}
     finally:
+        if tenant is not None and tenant.poll() is None:
+            tenant.kill()
         kubelet.stop()
     with open(out_path, "w") as f:
         json.dump(out, f, indent=1)
