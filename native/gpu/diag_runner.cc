@@ -198,8 +198,9 @@ class ProcessDiagEngine : public DiagEngine {
   }
   Value burn(int dev, int duration_ms, uint32_t seed, std::chrono::steady_clock::time_point start_at) override {
     const int64_t at = std::chrono::duration_cast<std::chrono::nanoseconds>(start_at.time_since_epoch()).count();
-    Value req = Value::object({{"op", "burn"}, {"duration_ms", duration_ms}, {"seed", static_cast<unsigned long long>(seed)},
-                               {"start_at_ns", static_cast<long long>(at)}});
+    Value req = Value::object({{"op", "burn"}, {"backend", kind_}, {"fixture", fixture_}, {"gpu_hip_device", dev},
+                               {"duration_ms", duration_ms},
+                               {"seed", static_cast<unsigned long long>(seed)}, {"start_at_ns", static_cast<long long>(at)}});
     return run_worker(exe_, req, dev, duration_ms + start_lead_ms() + 60000, cancel_);
   }
 
@@ -322,14 +323,22 @@ int diag_worker_main() {
       Value b = Value::array();
       for (int i = 0, n = d.device_count(); i < n; ++i) b.push_back(d.device_bdf(i));
       out = Value::object({{"bdfs", b}});
-    } else if (op == "checks") {
+    } else if (op == "checks" || op == "burn") {
       auto backend = make_backend(req.get_string("backend", "amdsmi"), req.get_string("fixture"));
-      HipDiagEngine engine(req.get_string("pcie_lock"));
-      out = engine.checks(*backend, gpu_info_from_json(req.get("gpu")), dev, diag_plan_from_json(req.get("plan")), seed);
-    } else if (op == "burn") {
-      HipDiagEngine engine;
-      const auto at = std::chrono::steady_clock::time_point(std::chrono::nanoseconds(req.get("start_at_ns").as_int()));
-      out = engine.burn(dev, static_cast<int>(req.get("duration_ms").as_int()), seed, at);
+      // a mock backend with a diagnostics script (CPU tests of the worker plumbing)
+      const bool scripted = backend->diag_script().is_object();
+      std::unique_ptr<DiagEngine> engine = scripted ? make_scripted_diag_engine(*backend)
+                                                    : std::make_unique<HipDiagEngine>(req.get_string("pcie_lock"));
+      // a script names GPUs by the agent's device number, not the worker's only device 0
+      const int script_dev = scripted && req.get("gpu_hip_device").is_int()
+                                 ? static_cast<int>(req.get("gpu_hip_device").as_int())
+                                 : dev;
+      if (op == "checks") {
+        out = engine->checks(*backend, gpu_info_from_json(req.get("gpu")), dev, diag_plan_from_json(req.get("plan")), seed);
+      } else {
+        const auto at = std::chrono::steady_clock::time_point(std::chrono::nanoseconds(req.get("start_at_ns").as_int()));
+        out = engine->burn(script_dev, static_cast<int>(req.get("duration_ms").as_int()), seed, at);
+      }
     } else {
       throw std::runtime_error("unknown diagnostics worker op '" + op + "'");
     }

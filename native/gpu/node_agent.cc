@@ -361,7 +361,11 @@ void NodeAgent::setup_diag() {
   // keeps it in the agent, which then holds a GPU context on every GPU from the first pass
   const char* inproc = std::getenv("BGC_DIAG_IN_PROCESS");
   diag_in_process_ = inproc && std::string(inproc) == "1";
-  if (script.is_object()) {
+  // BGC_DIAG_WORKERS=1 with a scripted mock: the script runs inside worker processes, so
+  // CPU tests cover the worker plumbing (spawn, results, common burn start, cancellation)
+  const char* workers = std::getenv("BGC_DIAG_WORKERS");
+  const bool scripted_workers = script.is_object() && workers && std::string(workers) == "1";
+  if (script.is_object() && !scripted_workers) {
     engine_ = make_scripted_diag_engine(*backend_);
   } else if (diag_in_process_) {
     engine_ = make_hip_diag_engine();
@@ -370,7 +374,7 @@ void NodeAgent::setup_diag() {
     engine_ = make_process_diag_engine("", cfg_.backend, cfg_.mock_fixture_path, pcie_lock_path_, &stop_);
   }
   std::vector<std::string> bdfs;
-  if (engine_->name() == "hip") {
+  if (engine_->name() == "hip" && !scripted_workers) {
     try {
       if (diag_in_process_) {
         Diag& d = Diag::instance();

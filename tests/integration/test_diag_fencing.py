@@ -187,3 +187,58 @@ def test_restart_leaves_busy_gpus_alone(nat, tmp_path):
                      desc="GPU 2 diagnosed once free")
     finally:
         kubelet.stop()
+
+
+def _children(pid):
+    """Child processes of any thread of `pid` (workers are spawned from the diag threads)."""
+    out = []
+    try:
+        tasks = os.listdir(f"/proc/{pid}/task")
+    except OSError:
+        return out
+    for t in tasks:
+        try:
+            with open(f"/proc/{pid}/task/{t}/children") as f:
+                out += [int(x) for x in f.read().split()]
+        except OSError:
+            pass
+    return out
+
+
+def test_worker_processes_run_the_pass_and_stop_with_the_agent(nat, tmp_path):
+    """The production engine runs every check and burn in `node-agent --diag-worker`
+    processes (BGC_DIAG_WORKERS=1 puts the mock's diagnostics script inside them on a CPU
+    host).  A pass's results come back through the workers, the burn starts after the
+    common lead, and an agent stopped mid-pass kills its worker instead of waiting for it."""
+    d = str(tmp_path / "dp")
+    kubelet = FakeKubelet(d).start()
+    try:
+        with Cluster(admission=False, controller=False) as c:
+            os.environ["BGC_DIAG_WORKERS"] = "1"
+            try:
+                c.start_node_agent(node_name="mi355x-workers", backend="mock", n_mock_gpus=2, poll_interval_ms=100,
+                                   fixture_obj=_fixture(nat, 2, {"checks_ms": 100, "burn_tflops": 2400}),
+                                   extra_env={"CONF_DEVICE_PLUGIN": "true", "CONF_DEVICE_PLUGIN_DIR": d,
+                                              "CONF_RUN_DIAG": "true", "CONF_DIAG_BURN_MS": "300",
+                                              "CONF_DIAG_INTERVAL_SECS": "1", "CONF_DIAG_FENCE_SETTLE_MS": "100"})
+            finally:
+                del os.environ["BGC_DIAG_WORKERS"]
+            assert kubelet.wait(lambda: kubelet.device_lists, timeout=30)
+            desc = _describe(c, "mi355x-workers")
+            assert desc["diag_isolation"] == "worker-process"
+            assert all(r["passed"] and r["worker_ms"] > 100 for r in desc["diag"]), desc["diag"]
+            assert desc["diag_node_burn"]["start_lead_ms"] >= 1900 and desc["diag_node_burn"]["gpus"] == 2
+            agent = c.procs["node-agent"]
+            # periodic passes now take 30 s each: stop the agent while a worker runs
+            c.set_gpu_fixture("mi355x-workers", _fixture(nat, 2, {"checks_ms": 30000}))
+            wait_for(lambda: _children(agent.p.pid), timeout=20, interval=0.05, desc="a worker running")
+            workers = _children(agent.p.pid)
+            t0 = time.time()
+            agent.p.terminate()
+            agent.p.wait(15)
+            assert time.time() - t0 < 5, "the agent waited for its worker"
+            time.sleep(0.3)
+            assert not [w for w in workers if os.path.exists(f"/proc/{w}") and
+                        open(f"/proc/{w}/stat").read().split()[2] != "Z"], "a worker outlived the agent"
+    finally:
+        kubelet.stop()
