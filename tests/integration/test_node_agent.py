@@ -84,8 +84,13 @@ def test_diag_worker_protocol():
 
     from bacchus_gpu_controller_amd import binary
 
+    from bacchus_gpu_controller_amd import REPO_ROOT
+
+    lib = os.path.join(REPO_ROOT, "bacchus_gpu_controller_amd", "libbgc_gpu_diag.so")
+
     def worker(req):
-        env = dict(os.environ, BGC_DIAG_REQUEST=json.dumps(req))
+        # the in-tree library, wherever the binary under test was built (sanitizer trees)
+        env = dict(os.environ, BGC_DIAG_REQUEST=json.dumps(req), BGC_GPU_DIAG_LIB=lib)
         p = subprocess.run([binary("node-agent"), "--diag-worker"], env=env, capture_output=True, text=True, timeout=60)
         assert p.returncode == 0, p.stderr
         return json.loads(p.stdout)
