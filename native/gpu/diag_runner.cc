@@ -134,9 +134,14 @@ class HipDiagEngine : public DiagEngine {
     return r;
   }
   Value burn(int dev, int duration_ms, uint32_t seed, std::chrono::steady_clock::time_point start_at) override {
-    Diag& d = Diag::instance();  // HIP initialised before the wait, not inside the burn window
+    Diag& d = Diag::instance();
+    (void)d.device_arch(dev);  // the HIP runtime and the device's context, before the wait
+    const auto ready = std::chrono::steady_clock::now();
     sleep_until(start_at);
-    return d.burn(dev, duration_ms, 32, seed);
+    Value r = d.burn(dev, duration_ms, 32, seed);
+    r["ready_at_ns"] = static_cast<long long>(std::chrono::duration_cast<std::chrono::nanoseconds>(ready.time_since_epoch()).count());
+    r["late_ms"] = ready > start_at ? std::chrono::duration<double, std::milli>(ready - start_at).count() : 0.0;
+    return r;
   }
 
  private:
@@ -182,7 +187,13 @@ class ProcessDiagEngine : public DiagEngine {
       : exe_(std::move(exe)), kind_(std::move(kind)), fixture_(std::move(fixture)), lock_(std::move(lock)),
         cancel_(cancel) {}
   std::string name() const override { return "hip"; }
-  int start_lead_ms() const override { return 2000; }  // a worker's HIP start-up on one visible GPU
+  // A worker's HIP start-up on one visible GPU: 3 s before any burn has been measured,
+  // then 1.5x the slowest start-up seen so far (concurrent start-ups on a full node are
+  // slower than one alone), at least 1 s.
+  int start_lead_ms() const override {
+    const int seen = slowest_ready_ms_.load();
+    return seen <= 0 ? 3000 : std::max(1000, seen * 3 / 2 + 200);
+  }
   Value checks(Backend&, const GpuInfo& g, int dev, const DiagPlan& plan, uint32_t seed) override {
     Value req = Value::object({{"op", "checks"}, {"backend", kind_}, {"fixture", fixture_}, {"gpu", to_json(g)},
                                {"plan", to_json(plan)}, {"seed", static_cast<unsigned long long>(seed)},
@@ -201,12 +212,23 @@ class ProcessDiagEngine : public DiagEngine {
     Value req = Value::object({{"op", "burn"}, {"backend", kind_}, {"fixture", fixture_}, {"gpu_hip_device", dev},
                                {"duration_ms", duration_ms},
                                {"seed", static_cast<unsigned long long>(seed)}, {"start_at_ns", static_cast<long long>(at)}});
-    return run_worker(exe_, req, dev, duration_ms + start_lead_ms() + 60000, cancel_);
+    const auto spawned = std::chrono::steady_clock::now();
+    Value r = run_worker(exe_, req, dev, duration_ms + start_lead_ms() + 60000, cancel_);
+    if (r.get("ready_at_ns").is_int()) {
+      const auto ready = std::chrono::steady_clock::time_point(std::chrono::nanoseconds(r.get("ready_at_ns").as_int()));
+      const int ms = static_cast<int>(std::chrono::duration<double, std::milli>(ready - spawned).count());
+      r["worker_ready_ms"] = ms;
+      int prev = slowest_ready_ms_.load();
+      while (ms > prev && !slowest_ready_ms_.compare_exchange_weak(prev, ms)) {
+      }
+    }
+    return r;
   }
 
  private:
   std::string exe_, kind_, fixture_, lock_;
   const CancelToken* cancel_;
+  std::atomic<int> slowest_ready_ms_{0};
 };
 
 // Re-reads the script from the backend on every call, so a test can change a running
@@ -482,6 +504,10 @@ NodeBurnResult node_burn(Backend& backend, DiagEngine& engine, const std::vector
   for (auto& w : workers) w.join();
   const double wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   const double start_lead_ms = std::chrono::duration<double, std::milli>(start_at - t0).count();
+  double late_max = 0;  // how long after the common start the slowest GPU began
+  for (const auto& r : res.per_gpu) {
+    if (r.get("late_ms").is_number()) late_max = std::max(late_max, r.get("late_ms").as_double());
+  }
   done = true;
   sampler.join();
   Value per = Value::array();
@@ -496,6 +522,7 @@ NodeBurnResult node_burn(Backend& backend, DiagEngine& engine, const std::vector
                             {"duration_ms", duration_ms},
                             {"wall_ms", wall_ms},
                             {"start_lead_ms", start_lead_ms},
+                            {"start_late_max_ms", late_max},
                             {"sweeps", sweeps},
                             {"power_sum_max_w", sum_max},
                             {"power_sum_mean_w", sweeps ? sum_acc / sweeps : 0.0},
