@@ -552,6 +552,13 @@ class Renderer:
                 args.append(piped)
             return self._call(head[1], args, dot, scope)
         if len(cmd) > 1 or piped is not _NOARG:
+            # a method on an object, as .Files.Get "path"
+            fn = self._operand(head, dot, scope) if head[0] in ("field", "chain", "var") else None
+            if callable(fn):
+                args = [self._operand(a, dot, scope) for a in cmd[1:]]
+                if piped is not _NOARG:
+                    args.append(piped)
+                return fn(*args)
             raise TemplateError(f"can't give argument to non-function {head[1]}")
         return self._operand(head, dot, scope)
 
@@ -685,8 +692,16 @@ def render_chart(chart_dir, values=None, release=None):
     for fn in sorted(os.listdir(tdir)):
         with open(os.path.join(tdir, fn)) as f:
             parsed[fn] = r.load(fn, f.read())
+    def files_get(path):
+        """Helm's .Files.Get: a chart file's text ("" when missing), never from templates/."""
+        full = os.path.normpath(os.path.join(chart_dir, path))
+        if not full.startswith(os.path.normpath(chart_dir) + os.sep) or not os.path.isfile(full):
+            return ""
+        with open(full) as f:
+            return f.read()
+
     root = {"Values": vals, "Release": rel, "Chart": chart_obj, "Capabilities": {"KubeVersion": {"Version": "v1.30.0"}},
-            "Template": {"BasePath": f"{chart['name']}/templates"}}
+            "Template": {"BasePath": f"{chart['name']}/templates"}, "Files": {"Get": files_get}}
     out = {}
     for fn, nodes in parsed.items():
         if fn.startswith("_") or not fn.endswith((".yaml", ".yml", ".tpl")) or fn.endswith(".tpl"):

@@ -425,3 +425,25 @@ def test_prometheus_rule_alerts_reference_exported_series():
         for name in re.findall(r"\b((?:amd_gpu|bgc)_[a-z0-9_]+)", a["expr"]):
             used.add(re.sub(r"_bucket$", "", name))
     assert used and used <= exported, used - exported
+
+
+def test_grafana_dashboard_configmap():
+    """metrics.grafanaDashboard: a ConfigMap with the sidecar label carrying the chart's
+    dashboard JSON (read with .Files.Get); every series its panels query is exported."""
+    import re
+
+    assert not [m for m in render({"metrics": {"enabled": True}}) if m.get("kind") == "ConfigMap"
+                and m["metadata"]["name"].endswith("-dashboard")]
+    ms = render({"metrics": {"enabled": True, "grafanaDashboard": {"enabled": True}}})
+    cm = [m for m in ms if m.get("kind") == "ConfigMap" and m["metadata"]["name"].endswith("-dashboard")]
+    assert len(cm) == 1 and cm[0]["metadata"]["labels"]["grafana_dashboard"] == "1"
+    dash = json.loads(cm[0]["data"]["bgc-overview.json"])
+    assert dash["uid"] == "bgc-mi355x" and len(dash["panels"]) >= 12
+    exported = set()
+    for root, _, files in os.walk(os.path.join(REPO_ROOT, "native")):
+        for f in files:
+            if f.endswith(".cc"):
+                exported |= set(re.findall(r'"((?:amd_gpu|bgc)_[a-z0-9_]+)"', open(os.path.join(root, f)).read()))
+    used = {re.sub(r"_bucket$", "", n) for p in dash["panels"] for t in p["targets"]
+            for n in re.findall(r"\b((?:amd_gpu|bgc)_[a-z0-9_]+)", t["expr"])}
+    assert used and used <= exported, used - exported
