@@ -484,6 +484,7 @@ __device__ __forceinline__ void pp_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+template <bool kLoadsOffReadPhases>
 __global__ __launch_bounds__(512, 1) void gemm_pingpong(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
                                                         float* __restrict__ C, int M, int N, int K) {
   __shared__ __attribute__((aligned(16))) char lds[8 * kPPHalf];  // [buf][A_top, A_bot, B_left, B_right]
@@ -551,15 +552,28 @@ __global__ __launch_bounds__(512, 1) void gemm_pingpong(const __bf16* __restrict
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks) af[mi][ks] = soak_frag(ai, m0 + mi * 16 + (lane & 15), ks * 4 + (lane >> 4));
       }
-      switch (p) {  // one half-tile per phase, each into a half nobody reads any more
-        case 0: stage(4, t_odd); break;      // buffer 1 A_top (read at phase 4)
-        case 1: stage(5, t_odd); break;      // buffer 1 A_bot
-        case 2: stage(2, t_next); break;     // buffer 0 B_left (last read at phase 0)
-        case 3: stage(3, t_next); break;     // buffer 0 B_right
-        case 4: stage(0, t_next); break;     // buffer 0 A_top (last read at phase 2)
-        case 5: stage(1, t_next); break;     // buffer 0 A_bot
-        case 6: stage(6, t_next_odd); break; // buffer 1 B_left (last read at phase 4)
-        default: stage(7, t_next_odd); break;
+      if constexpr (kLoadsOffReadPhases) {
+        // variant under test: phases 0/4 (16 fragment reads) issue no loads; 1/5 take two
+        switch (p) {
+          case 1: stage(4, t_odd); stage(5, t_odd); break;
+          case 2: stage(2, t_next); break;
+          case 3: stage(3, t_next); break;
+          case 5: stage(0, t_next); stage(1, t_next); break;
+          case 6: stage(6, t_next_odd); break;
+          case 7: stage(7, t_next_odd); break;
+          default: break;
+        }
+      } else {
+        switch (p) {  // one half-tile per phase, each into a half nobody reads any more
+          case 0: stage(4, t_odd); break;      // buffer 1 A_top (read at phase 4)
+          case 1: stage(5, t_odd); break;      // buffer 1 A_bot
+          case 2: stage(2, t_next); break;     // buffer 0 B_left (last read at phase 0)
+          case 3: stage(3, t_next); break;     // buffer 0 B_right
+          case 4: stage(0, t_next); break;     // buffer 0 A_top (last read at phase 2)
+          case 5: stage(1, t_next); break;     // buffer 0 A_bot
+          case 6: stage(6, t_next_odd); break; // buffer 1 B_left (last read at phase 4)
+          default: stage(7, t_next_odd); break;
+        }
       }
       if ((p & 3) == 3) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // retires everything through phase p-2
       pp_barrier();
@@ -716,8 +730,14 @@ bool soak_pingpong(bool big, int k) {
 
 void launch_soak_gemm(bool big, const void* a, const void* bt, void* c, int m, int n, int k, hipStream_t s) {
   if (soak_pingpong(big, k)) {
-    hipLaunchKernelGGL(gemm_pingpong, dim3((m / 256) * (n / 256)), dim3(512), 0, s, static_cast<const __bf16*>(a),
-                       static_cast<const __bf16*>(bt), static_cast<float*>(c), m, n, k);
+    const char* kern = std::getenv("BGC_SOAK_KERNEL");
+    if (kern && std::string(kern) == "pingpong-lo") {
+      hipLaunchKernelGGL(gemm_pingpong<true>, dim3((m / 256) * (n / 256)), dim3(512), 0, s,
+                         static_cast<const __bf16*>(a), static_cast<const __bf16*>(bt), static_cast<float*>(c), m, n, k);
+    } else {
+      hipLaunchKernelGGL(gemm_pingpong<false>, dim3((m / 256) * (n / 256)), dim3(512), 0, s,
+                         static_cast<const __bf16*>(a), static_cast<const __bf16*>(bt), static_cast<float*>(c), m, n, k);
+    }
   } else if (big) {
     hipLaunchKernelGGL((gemm_soak<256, 256, 2, 4>), dim3((m / 256) * (n / 256)), dim3(512), 0, s,
                        static_cast<const __bf16*>(a), static_cast<const __bf16*>(bt), static_cast<float*>(c), m, n, k);

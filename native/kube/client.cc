@@ -501,6 +501,29 @@ Value KubeClient::replace_status(const ResourceType& rt, const std::string& ns, 
   return call("PUT", rt.object_path(ns, name) + "/status", body.dump());
 }
 
+namespace {
+std::string response_rv(const http::Response& r) {
+  std::string_view md = json::raw_member(r.body, "metadata");
+  if (md.empty()) return "";
+  return json::parse(md, "managedFields").get_string("resourceVersion");
+}
+}  // namespace
+
+std::string KubeClient::replace_status_rv(const ResourceType& rt, const std::string& ns, const std::string& name,
+                                          const Value& body) {
+  http::Response r = raw("PUT", rt.object_path(ns, name) + "/status", body.dump(), "application/json");
+  if (r.status < 200 || r.status >= 300) throw_api_error(r);
+  return response_rv(r);
+}
+
+std::string KubeClient::patch_json_rv(const ResourceType& rt, const std::string& ns, const std::string& name,
+                                      const Value& ops, const std::string& field_manager) {
+  http::Response r = raw("PATCH", with_params(rt.object_path(ns, name), {{"fieldManager", field_manager}}), ops.dump(),
+                         "application/json-patch+json");
+  if (r.status < 200 || r.status >= 300) throw_api_error(r);
+  return response_rv(r);
+}
+
 Value KubeClient::apply(const ResourceType& rt, const std::string& ns, const std::string& name, const Value& body,
                         const std::string& field_manager, bool force) {
   std::string path =

@@ -129,6 +129,12 @@ class KubeClient {
                      const std::string& field_manager = "");
   json::Value replace(const ResourceType& rt, const std::string& ns, const std::string& name, const json::Value& body,
                       const std::string& field_manager = "");
+  // The same writes returning only the written object's resourceVersion: the response is
+  // not parsed beyond metadata (managedFields skipped), for callers that need nothing else.
+  std::string replace_status_rv(const ResourceType& rt, const std::string& ns, const std::string& name,
+                                const json::Value& body);
+  std::string patch_json_rv(const ResourceType& rt, const std::string& ns, const std::string& name,
+                            const json::Value& ops, const std::string& field_manager = "");
   json::Value replace_status(const ResourceType& rt, const std::string& ns, const std::string& name,
                              const json::Value& body);
   // Server-side apply (application/apply-patch+yaml; JSON is valid YAML).

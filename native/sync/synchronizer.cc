@@ -135,8 +135,7 @@ bool Synchronizer::sync_one(const Value& ub, std::vector<std::string>* produced)
     json::PatchBuilder ops;
     if (!has_quota) ops.add("/spec/quota", Value::object());
     ops.replace("/spec/quota", desired);
-    Value res = client_.patch_json(types::UserBootstrap, "", name, ops.ops(), kPatchManager);
-    rv = res.get("metadata").get_string("resourceVersion");
+    rv = client_.patch_json_rv(types::UserBootstrap, "", name, ops.ops(), kPatchManager);
     if (produced) produced->push_back(rv);
     LOG_INFO("synchronizer") << "quota updated";
   }
@@ -147,8 +146,8 @@ bool Synchronizer::sync_one(const Value& ub, std::vector<std::string>* produced)
       body["status"] = Value::object({{"synchronized_with_sheet", true}});
       try {
         LOG_INFO("synchronizer") << "updating status";
-        Value res = client_.replace_status(types::UserBootstrap, "", name, body);
-        if (produced) produced->push_back(res.get("metadata").get_string("resourceVersion"));
+        const std::string written_rv = client_.replace_status_rv(types::UserBootstrap, "", name, body);
+        if (produced) produced->push_back(written_rv);
         break;
       } catch (const kube::ApiError& e) {
         if (e.code() != 409 || attempt == 2) throw;
