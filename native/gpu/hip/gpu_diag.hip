@@ -553,7 +553,10 @@ __global__ __launch_bounds__(512, 1) void gemm_pingpong(const __bf16* __restrict
           for (int ks = 0; ks < 2; ++ks) af[mi][ks] = soak_frag(ai, m0 + mi * 16 + (lane & 15), ks * 4 + (lane >> 4));
       }
       if constexpr (kLoadsOffReadPhases) {
-        // variant under test: phases 0/4 (16 fragment reads) issue no loads; 1/5 take two
+        // Phases 0/4 issue 16 fragment reads, as long as the partner's 16 MFMAs at four
+        // reading waves per CU: no loads there; phases 1/5 (no reads) issue two half-tiles.
+        // Same halves, each still staged >= 2 barriers after its last read, and vmcnt(4)
+        // at phases 3/7 still retires phases 1/5 (profiles/gemm_soak_r3/: +4 % at 4096^3)
         switch (p) {
           case 1: stage(4, t_odd); stage(5, t_odd); break;
           case 2: stage(2, t_next); break;
@@ -730,12 +733,13 @@ bool soak_pingpong(bool big, int k) {
 
 void launch_soak_gemm(bool big, const void* a, const void* bt, void* c, int m, int n, int k, hipStream_t s) {
   if (soak_pingpong(big, k)) {
+    // BGC_SOAK_KERNEL=pingpong0: the first schedule (one half-tile load in every phase)
     const char* kern = std::getenv("BGC_SOAK_KERNEL");
-    if (kern && std::string(kern) == "pingpong-lo") {
-      hipLaunchKernelGGL(gemm_pingpong<true>, dim3((m / 256) * (n / 256)), dim3(512), 0, s,
+    if (kern && std::string(kern) == "pingpong0") {
+      hipLaunchKernelGGL(gemm_pingpong<false>, dim3((m / 256) * (n / 256)), dim3(512), 0, s,
                          static_cast<const __bf16*>(a), static_cast<const __bf16*>(bt), static_cast<float*>(c), m, n, k);
     } else {
-      hipLaunchKernelGGL(gemm_pingpong<false>, dim3((m / 256) * (n / 256)), dim3(512), 0, s,
+      hipLaunchKernelGGL(gemm_pingpong<true>, dim3((m / 256) * (n / 256)), dim3(512), 0, s,
                          static_cast<const __bf16*>(a), static_cast<const __bf16*>(bt), static_cast<float*>(c), m, n, k);
     }
   } else if (big) {
