@@ -1,13 +1,13 @@
 #!/usr/bin/env bash
 # PMC counters (counters only, no trace domains) of the 256x256 soak kernels at 8192^3:
-# BGC_SOAK_KERNEL=2buf vs the default 8-phase ping-pong, one rocprofv3 pass per kernel.
-#   OUT=gpurun_out/pmc_soak bash tools/pmc_soak.sh
+# BGC_SOAK_KERNEL values in $KERNELS (default "2buf pingpong"), one rocprofv3 pass each.
+#   OUT=gpurun_out/pmc_soak [KERNELS="pingpong0 pingpong"] bash tools/pmc_soak.sh
 set -o pipefail
 OUT=${OUT:-gpurun_out/pmc_soak}
 rm -rf "$OUT" && mkdir -p "$OUT"
 export TMPDIR=/tmp
 SQ="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS GRBM_GUI_ACTIVE"
-for kern in 2buf pingpong; do
+for kern in ${KERNELS:-2buf pingpong}; do
   export BGC_SOAK_KERNEL=$kern
   echo "pmc $kern"
   timeout -s KILL 90 rocprofv3 --pmc $SQ --kernel-trace --output-format csv -d "$OUT/$kern" -o sq -- python3 tools/soak_one.py 8192 8192 8192 5 > "$OUT/$kern.log" 2>&1 || { tail -20 "$OUT/$kern.log"; exit 1; }
