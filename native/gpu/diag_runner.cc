@@ -85,6 +85,7 @@ class FileLock {
   ~FileLock() {
     if (fd_ >= 0) ::close(fd_);  // releases the lock
   }
+  bool held() const { return fd_ >= 0; }
   FileLock(const FileLock&) = delete;
   FileLock& operator=(const FileLock&) = delete;
 
@@ -124,6 +125,8 @@ class HipDiagEngine : public DiagEngine {
       std::lock_guard<std::mutex> lk(pcie_mu);
       FileLock across_processes(pcie_lock_path_);
       r["pcie"] = pcie_check(backend, g, dev, plan.pcie_bytes, seed);
+      // false: the lock file could not be opened, so other GPUs' copies may have overlapped
+      if (!pcie_lock_path_.empty()) r["pcie"]["serialized"] = across_processes.held();
       lap("pcie");
     }
     if (plan.soak_launches > 0) {
@@ -218,8 +221,10 @@ class ProcessDiagEngine : public DiagEngine {
       const auto ready = std::chrono::steady_clock::time_point(std::chrono::nanoseconds(r.get("ready_at_ns").as_int()));
       const int ms = static_cast<int>(std::chrono::duration<double, std::milli>(ready - spawned).count());
       r["worker_ready_ms"] = ms;
+      // the slowest recent start-up: a new maximum at once, an old one fades by a quarter
+      // per burn, so one cold start does not lengthen every later pass
       int prev = slowest_ready_ms_.load();
-      while (ms > prev && !slowest_ready_ms_.compare_exchange_weak(prev, ms)) {
+      while (!slowest_ready_ms_.compare_exchange_weak(prev, std::max(ms, prev * 3 / 4))) {
       }
     }
     return r;
