@@ -451,12 +451,13 @@ __global__ __launch_bounds__(64 * WM * WN, (BM * BN >= 256 * 256) ? 1 : 2) void 
 //    16 v_mfma_f32_16x16x32_bf16.  Eight phases = two K-tiles per loop iteration.
 //    Fragments: all of the wave's B (64 columns) and half its A at phase 0, the other A
 //    half at phase 2 (192 VGPRs: 128 accumulator, 32 A, 32 B).
-//  * One half-tile load per phase, placed where the half it overwrites was last read
-//    (B halves are read only in the first phase of a K-tile, A halves in the first and
-//    third), so every load has 4-11 phases to land before it is read.  Waits are
+//  * Two half-tile loads in every odd phase (the even phases carry all the fragment
+//    reads), each into a half last read at least two barriers earlier (B halves are read
+//    only in the first phase of a K-tile, A halves in the first and third).  Waits are
 //    counted, vmcnt(4) at phases 3 and 7 (each half-tile is 2 glds per thread), and a
 //    half is first read one phase after the wait that retires it; loads stay in flight
-//    across the barriers.
+//    across the barriers.  (kSched 0, BGC_SOAK_KERNEL=pingpong0: the first schedule, one
+//    half-tile in every phase.)
 //  * Staging past the last K-tile re-reads the last tile into a buffer nobody reads
 //    again, so the vmcnt counts never change; the block drains (vmcnt(0)) before its
 //    epilogue.
@@ -484,7 +485,7 @@ __device__ __forceinline__ void pp_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <bool kLoadsOffReadPhases>
+template <int kSched>  // 0: a half-tile load in every phase; 2: two in every odd phase
 __global__ __launch_bounds__(512, 1) void gemm_pingpong(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
                                                         float* __restrict__ C, int M, int N, int K) {
   __shared__ __attribute__((aligned(16))) char lds[8 * kPPHalf];  // [buf][A_top, A_bot, B_left, B_right]
@@ -552,18 +553,17 @@ __global__ __launch_bounds__(512, 1) void gemm_pingpong(const __bf16* __restrict
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks) af[mi][ks] = soak_frag(ai, m0 + mi * 16 + (lane & 15), ks * 4 + (lane >> 4));
       }
-      if constexpr (kLoadsOffReadPhases) {
-        // Phases 0/4 issue 16 fragment reads, as long as the partner's 16 MFMAs at four
-        // reading waves per CU: no loads there; phases 1/5 (no reads) issue two half-tiles.
-        // Same halves, each still staged >= 2 barriers after its last read, and vmcnt(4)
-        // at phases 3/7 still retires phases 1/5 (profiles/gemm_soak_r3/: +4 % at 4096^3)
+      if constexpr (kSched == 2) {
+        // All fragment reads happen in the even phases (16 at 0/4, 8 at 2/6; at four
+        // reading waves per CU, 16 take the partner's whole MFMA interval), so the loads
+        // go to the odd phases, two half-tiles each.  Same halves; each is still reloaded
+        // >= 2 barriers after its last read, and vmcnt(4) at phases 3/7 retires phases
+        // 1/5 (profiles/gemm_soak_r3/: +3-7 % at 4096^3, +0.5 % at 8192^3)
         switch (p) {
-          case 1: stage(4, t_odd); stage(5, t_odd); break;
-          case 2: stage(2, t_next); break;
-          case 3: stage(3, t_next); break;
-          case 5: stage(0, t_next); stage(1, t_next); break;
-          case 6: stage(6, t_next_odd); break;
-          case 7: stage(7, t_next_odd); break;
+          case 1: stage(4, t_odd); stage(5, t_odd); break;           // buffer 1 A (read at phase 4)
+          case 3: stage(2, t_next); stage(3, t_next); break;         // buffer 0 B (last read at phase 0)
+          case 5: stage(0, t_next); stage(1, t_next); break;         // buffer 0 A (last read at phase 2)
+          case 7: stage(6, t_next_odd); stage(7, t_next_odd); break; // buffer 1 B (last read at phase 4)
           default: break;
         }
       } else {
@@ -736,10 +736,10 @@ void launch_soak_gemm(bool big, const void* a, const void* bt, void* c, int m, i
     // BGC_SOAK_KERNEL=pingpong0: the first schedule (one half-tile load in every phase)
     const char* kern = std::getenv("BGC_SOAK_KERNEL");
     if (kern && std::string(kern) == "pingpong0") {
-      hipLaunchKernelGGL(gemm_pingpong<false>, dim3((m / 256) * (n / 256)), dim3(512), 0, s,
+      hipLaunchKernelGGL(gemm_pingpong<0>, dim3((m / 256) * (n / 256)), dim3(512), 0, s,
                          static_cast<const __bf16*>(a), static_cast<const __bf16*>(bt), static_cast<float*>(c), m, n, k);
     } else {
-      hipLaunchKernelGGL(gemm_pingpong<true>, dim3((m / 256) * (n / 256)), dim3(512), 0, s,
+      hipLaunchKernelGGL(gemm_pingpong<2>, dim3((m / 256) * (n / 256)), dim3(512), 0, s,
                          static_cast<const __bf16*>(a), static_cast<const __bf16*>(bt), static_cast<float*>(c), m, n, k);
     }
   } else if (big) {
