@@ -99,7 +99,10 @@ class HipDiagEngine : public DiagEngine {
   std::string name() const override { return "hip"; }
   Value checks(Backend& backend, const GpuInfo& g, int dev, const DiagPlan& plan, uint32_t seed) override {
     Diag& d = Diag::instance();
+    (void)d.device_arch(dev);  // HIP up: when this happened tells the agent a worker's start-up time
     Value r = Value::object();
+    r["ready_at_ns"] = static_cast<long long>(
+        std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count());
     Value timing = Value::object();  // wall ms per section, to see where a pass spends its time
     auto t = std::chrono::steady_clock::now();
     auto lap = [&](const char* name) {
@@ -190,9 +193,9 @@ class ProcessDiagEngine : public DiagEngine {
       : exe_(std::move(exe)), kind_(std::move(kind)), fixture_(std::move(fixture)), lock_(std::move(lock)),
         cancel_(cancel) {}
   std::string name() const override { return "hip"; }
-  // A worker's HIP start-up on one visible GPU: 3 s before any burn has been measured,
-  // then 1.5x the slowest start-up seen so far (concurrent start-ups on a full node are
-  // slower than one alone), at least 1 s.
+  // A worker's HIP start-up on one visible GPU: 3 s before any worker has been measured,
+  // then 1.5x the slowest recent start-up (concurrent start-ups on a full node are slower
+  // than one alone), at least 1 s.  The checks workers measure it before the first burn.
   int start_lead_ms() const override {
     const int seen = slowest_ready_ms_.load();
     return seen <= 0 ? 3000 : std::max(1000, seen * 3 / 2 + 200);
@@ -208,6 +211,7 @@ class ProcessDiagEngine : public DiagEngine {
     const int timeout_ms = std::max(60000, plan.hbm_walk_budget_ms + 90000);
     Value r = run_worker(exe_, req, dev, timeout_ms, cancel_);
     r["worker_ms"] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    note_ready(r, t0);  // so the start-up burn's lead is measured, not guessed
     return r;
   }
   Value burn(int dev, int duration_ms, uint32_t seed, std::chrono::steady_clock::time_point start_at) override {
@@ -217,18 +221,25 @@ class ProcessDiagEngine : public DiagEngine {
                                {"seed", static_cast<unsigned long long>(seed)}, {"start_at_ns", static_cast<long long>(at)}});
     const auto spawned = std::chrono::steady_clock::now();
     Value r = run_worker(exe_, req, dev, duration_ms + start_lead_ms() + 60000, cancel_);
-    if (r.get("ready_at_ns").is_int()) {
-      const auto ready = std::chrono::steady_clock::time_point(std::chrono::nanoseconds(r.get("ready_at_ns").as_int()));
-      const int ms = static_cast<int>(std::chrono::duration<double, std::milli>(ready - spawned).count());
-      r["worker_ready_ms"] = ms;
-      // the slowest recent start-up: a new maximum at once, an old one fades by a quarter
-      // per burn, so one cold start does not lengthen every later pass
-      int prev = slowest_ready_ms_.load();
-      while (!slowest_ready_ms_.compare_exchange_weak(prev, std::max(ms, prev * 3 / 4))) {
-      }
-    }
+    note_ready(r, spawned);
     return r;
   }
+
+ private:
+  // A worker's start-up (spawn to HIP ready) from its result's ready_at_ns: the slowest
+  // recent one sets the burn lead.  A new maximum counts at once, an old one fades by a
+  // quarter per worker, so one cold start does not lengthen every later pass.
+  void note_ready(Value& r, std::chrono::steady_clock::time_point spawned) {
+    if (!r.get("ready_at_ns").is_int()) return;
+    const auto ready = std::chrono::steady_clock::time_point(std::chrono::nanoseconds(r.get("ready_at_ns").as_int()));
+    const int ms = static_cast<int>(std::chrono::duration<double, std::milli>(ready - spawned).count());
+    r["worker_ready_ms"] = ms;
+    int prev = slowest_ready_ms_.load();
+    while (!slowest_ready_ms_.compare_exchange_weak(prev, std::max(ms, prev * 3 / 4))) {
+    }
+  }
+
+ public:
 
  private:
   std::string exe_, kind_, fixture_, lock_;
