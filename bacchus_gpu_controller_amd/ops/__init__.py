@@ -8,6 +8,8 @@ These are the only compute kernels in the framework: the reference controller ha
 * ``hbm_walk(device)``  — address-in-data walk over most of the free HBM (stuck bits,
   aliased addresses), reporting the first bad address
 * ``mfma(device)``      — exact-integer bf16 MFMA tiles on every CU + a throughput pass
+* ``mfma_lowp(device)`` — the same for the MX block-scaled fp8 / fp4 matrix-core path
+  (``v_mfma_scale_f32_16x16x128_f8f6f4``), with and without E8M0 block scales
 * ``gemm_check(device)``— a bf16 GEMM on the matrix cores checked against exact row and
   column checksums (ABFT)
 * ``gemm_soak(device)`` — the sustained-throughput soak: the 8-phase ping-pong GEMM
@@ -53,6 +55,12 @@ def hbm_walk(device=0, fraction=0.9, chunk_bytes=4 << 30, budget_ms=20000, seed=
 
 def mfma(device=0, waves_per_cu=32, iters=4096, seed=0x5EED):
     return json.loads(native().diag_mfma(device, waves_per_cu, iters, seed))
+
+
+def mfma_lowp(device=0, waves_per_cu=32, iters=4096, seed=0x5EED):
+    """MX block-scaled fp8 (e4m3) and fp4 (e2m1) matrix-core tiles on every CU, with unit
+    and random E8M0 block scales, checked exactly; then the dense fp8 and fp4 rates."""
+    return json.loads(native().diag_mfma_lowp(device, waves_per_cu, iters, seed))
 
 
 def gemm_check(device=0, m=4096, n=4096, k=4096, seed=0x5EED):

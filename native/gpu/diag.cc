@@ -43,6 +43,7 @@ Diag::Diag(const std::string& path) : path_(path) {
   device_count_ = reinterpret_cast<int (*)()>(dlsym(lib_, "bgc_diag_device_count"));
   hbm_ = reinterpret_cast<int (*)(int, uint64_t, int, uint32_t, bgc_hbm_result*)>(dlsym(lib_, "bgc_diag_hbm"));
   mfma_ = reinterpret_cast<int (*)(int, int, int, uint32_t, bgc_mfma_result*)>(dlsym(lib_, "bgc_diag_mfma"));
+  lowp_ = reinterpret_cast<int (*)(int, int, int, uint32_t, bgc_lowp_result*)>(dlsym(lib_, "bgc_diag_mfma_lowp"));
   arch_ = reinterpret_cast<int (*)(int, char*, size_t)>(dlsym(lib_, "bgc_diag_device_arch"));
   gemm_ = reinterpret_cast<int (*)(int, int, int, int, const uint16_t*, const uint16_t*, float*)>(
       dlsym(lib_, "bgc_diag_gemm"));
@@ -56,7 +57,7 @@ Diag::Diag(const std::string& path) : path_(path) {
   bdf_ = reinterpret_cast<int (*)(int, char*, size_t)>(dlsym(lib_, "bgc_diag_device_bdf"));
   last_error_ = reinterpret_cast<const char* (*)()>(dlsym(lib_, "bgc_diag_last_error"));
   auto abi = reinterpret_cast<int (*)()>(dlsym(lib_, "bgc_diag_abi_version"));
-  if (!device_count_ || !hbm_ || !mfma_ || !arch_ || !gemm_ || !burn_ || !pcie_ || !soak_ || !tiled_ ||
+  if (!device_count_ || !hbm_ || !mfma_ || !lowp_ || !arch_ || !gemm_ || !burn_ || !pcie_ || !soak_ || !tiled_ ||
       !walk_ || !bdf_ || !last_error_ || !abi ||
       abi() != BGC_DIAG_ABI_VERSION) {
     throw std::runtime_error(path + " is not a compatible bgc diag library");
@@ -140,6 +141,31 @@ json::Value Diag::mfma(int device, int waves_per_cu, int throughput_iters, uint3
   v["elapsed_ms"] = r.elapsed_ms;
   v["passed"] = r.mismatches == 0 && r.throughput_ok != 0;
   return v;
+}
+
+json::Value Diag::mfma_lowp(int device, int waves_per_cu, int throughput_iters, uint32_t seed) {
+  bgc_lowp_result r{};
+  if (lowp_(device, waves_per_cu, throughput_iters, seed, &r) != 0) {
+    throw std::runtime_error(std::string("low-precision mfma diag: ") + last_error_());
+  }
+  json::Value bad = json::Value::array();
+  for (int i = 0; i < r.bad_cus && i < 64; ++i) bad.push_back(r.bad_cu_keys[i]);
+  const uint64_t mism = r.fp8_mismatches + r.fp8_scaled_mismatches + r.fp4_mismatches + r.fp4_scaled_mismatches;
+  return json::Value::object({{"device", device},
+                              {"tiles_checked", static_cast<unsigned long long>(r.tiles_checked)},
+                              {"fp8_mismatches", static_cast<unsigned long long>(r.fp8_mismatches)},
+                              {"fp8_scaled_mismatches", static_cast<unsigned long long>(r.fp8_scaled_mismatches)},
+                              {"fp4_mismatches", static_cast<unsigned long long>(r.fp4_mismatches)},
+                              {"fp4_scaled_mismatches", static_cast<unsigned long long>(r.fp4_scaled_mismatches)},
+                              {"mismatches", static_cast<unsigned long long>(mism)},
+                              {"cus_seen", r.cus_seen},
+                              {"bad_cus", r.bad_cus},
+                              {"bad_cu_keys", bad},
+                              {"fp8_tflops", r.fp8_tflops},
+                              {"fp4_tflops", r.fp4_tflops},
+                              {"throughput_ok", r.throughput_ok != 0},
+                              {"elapsed_ms", r.elapsed_ms},
+                              {"passed", mism == 0 && r.throughput_ok != 0}});
 }
 
 json::Value Diag::burn(int device, int duration_ms, int waves_per_cu, uint32_t seed) {
@@ -284,6 +310,11 @@ DiagFloors DiagFloors::mi355x_defaults() {
   f.min_mfma_tflops = 1500;
   f.min_xcc_balance = 0.85;
   f.min_xccs = 8;
+  // MX fp8 / fp4 (v_mfma_scale_f32_16x16x128_f8f6f4, 32 waves per CU x 4096 iterations,
+  // profiles/mx_lowp_r3/): 4.1-4.7 PF/s fp8 and 7.3-8.1 PF/s fp4 depending on how warm
+  // the clocks are, against ~5 and ~10 PF/s dense peaks
+  f.min_fp8_tflops = 3000;
+  f.min_fp4_tflops = 5000;
   // burn-in: measured on MI355X in profiles/diag_burn_r2.json (sustained bf16 MFMA at
   // 97 % of the 2.5 PF/s dense peak once clocks settle)
   f.min_burn_tflops = 1800;  // measured 2409-2421 PF/s mean over 10 s at 1.17-1.22 kW, 2.34-2.39 GHz
@@ -360,6 +391,21 @@ json::Value judge_diag(const json::Value& result, const DiagFloors& fl) {
     if (fl.min_xccs > 0 && num(mf, "xccs_seen") < fl.min_xccs) {
       failures.push_back("only " + std::to_string(static_cast<int>(num(mf, "xccs_seen"))) + " XCCs ran MFMA work");
     }
+  }
+  const json::Value& lp = result.get("lowp");
+  if (lp.is_object()) {
+    if (num(lp, "mismatches") > 0) {
+      char buf[200];
+      std::snprintf(buf, sizeof(buf), "MX fp8/fp4 MFMA tile mismatches on %d CU(s): fp8 %.0f, fp8 scaled %.0f, fp4 %.0f, fp4 scaled %.0f",
+                    static_cast<int>(num(lp, "bad_cus")), num(lp, "fp8_mismatches"), num(lp, "fp8_scaled_mismatches"),
+                    num(lp, "fp4_mismatches"), num(lp, "fp4_scaled_mismatches"));
+      failures.push_back(std::string(buf));
+    }
+    if (lp.get("throughput_ok").is_bool() && !lp.get("throughput_ok").as_bool()) {
+      failures.push_back("MX fp8/fp4 MFMA throughput accumulators wrong");
+    }
+    floor_check(lp, "fp8_tflops", fl.min_fp8_tflops, "MX fp8 MFMA TFLOP/s");
+    floor_check(lp, "fp4_tflops", fl.min_fp4_tflops, "MX fp4 MFMA TFLOP/s");
   }
   const json::Value& burn = result.get("burn");
   if (burn.is_object()) {

@@ -19,6 +19,10 @@ struct DiagFloors {
   double min_write_gbps = 0;
   double min_mfma_tflops = 0;
   double min_xcc_balance = 0;  // slowest XCC mean wave time / fastest, inverted (0..1]
+  // MX block-scaled low-precision matrix cores (`lowp` section): any wrong tile fails;
+  // rate floors for the dense fp8 and fp4 phases.
+  double min_fp8_tflops = 0;
+  double min_fp4_tflops = 0;
   int min_xccs = 0;            // XCCs that must have run MFMA work
   // Burn-in (sustained MFMA load, `burn` section): rate floor, the rate may not sag
   // below this fraction of its first launch, and the thermal limits under load.
@@ -58,6 +62,8 @@ class Diag {
   std::string device_arch(int device);
   json::Value hbm(int device, uint64_t bytes, int iters, uint32_t seed);
   json::Value mfma(int device, int waves_per_cu, int throughput_iters, uint32_t seed);
+  // MX block-scaled fp8 / fp4 matrix-core tiles and rates (see bgc_diag_mfma_lowp).
+  json::Value mfma_lowp(int device, int waves_per_cu, int throughput_iters, uint32_t seed);
   // MFMA GEMM on the device vs a host fp32 product of the same bf16 operands
   // (deterministic pseudo-random values in [-1, 1]).  Returns max error and the bound.
   json::Value gemm_check(int device, int m, int n, int k, uint32_t seed);
@@ -84,6 +90,7 @@ class Diag {
   int (*device_count_)() = nullptr;
   int (*hbm_)(int, uint64_t, int, uint32_t, bgc_hbm_result*) = nullptr;
   int (*mfma_)(int, int, int, uint32_t, bgc_mfma_result*) = nullptr;
+  int (*lowp_)(int, int, int, uint32_t, bgc_lowp_result*) = nullptr;
   int (*arch_)(int, char*, size_t) = nullptr;
   int (*gemm_)(int, int, int, int, const uint16_t*, const uint16_t*, float*) = nullptr;
   int (*burn_)(int, int, int, uint32_t, bgc_burn_result*) = nullptr;

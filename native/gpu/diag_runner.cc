@@ -118,6 +118,10 @@ class HipDiagEngine : public DiagEngine {
     }
     r["mfma"] = d.mfma(dev, 16, 2048, seed);
     lap("mfma");
+    if (plan.lowp) {
+      r["lowp"] = d.mfma_lowp(dev, 32, 4096, seed);  // ~5 ms
+      lap("lowp");
+    }
     r["gemm"] = d.gemm_check(dev, 64, 64, 512, seed);
     lap("gemm");
     if (plan.pcie_bytes > 0) {
@@ -271,6 +275,10 @@ class ScriptedDiagEngine : public DiagEngine {
     }
     r["mfma"] = Value::object({{"device", dev}, {"tflops", 2000.0}, {"xcc_balance", 0.96}, {"xccs_seen", 8},
                                {"mismatches", 0}, {"bad_cus", 0}, {"throughput_ok", true}, {"passed", true}});
+    if (plan.lowp) {
+      r["lowp"] = Value::object({{"device", dev}, {"fp8_tflops", 4000.0}, {"fp4_tflops", 7000.0}, {"mismatches", 0},
+                                 {"bad_cus", 0}, {"throughput_ok", true}, {"passed", true}});
+    }
     r["gemm"] = Value::object({{"passed", true}});
     if (plan.soak_launches > 0) {
       r["soak"] = Value::object({{"tflops_mean", 1300.0}, {"row_mismatches", 0}, {"col_mismatches", 0}, {"passed", true}});
@@ -320,6 +328,7 @@ Value to_json(const DiagPlan& p) {
                         {"pcie_bytes", static_cast<unsigned long long>(p.pcie_bytes)},
                         {"soak_size", p.soak_size},
                         {"soak_launches", p.soak_launches},
+                        {"lowp", p.lowp},
                         {"burn_ms", p.burn_ms}});
 }
 
@@ -334,6 +343,7 @@ DiagPlan diag_plan_from_json(const Value& v) {
   p.pcie_bytes = u64("pcie_bytes", p.pcie_bytes);
   p.soak_size = i32("soak_size", p.soak_size);
   p.soak_launches = i32("soak_launches", p.soak_launches);
+  p.lowp = v.get("lowp").is_bool() ? v.get("lowp").as_bool() : p.lowp;
   p.burn_ms = i32("burn_ms", p.burn_ms);
   return p;
 }

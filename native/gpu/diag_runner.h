@@ -39,6 +39,7 @@ struct DiagPlan {
   uint64_t pcie_bytes = 256ULL << 20;    // 0 = off
   int soak_size = 8192;
   int soak_launches = 20;                // 0 = off
+  bool lowp = true;                      // MX fp8 / fp4 matrix-core tiles and rates
   int burn_ms = 0;                       // node-level burn phase (0 = off)
 };
 
@@ -48,7 +49,7 @@ class DiagEngine {
   virtual std::string name() const = 0;
   // How far ahead node_burn schedules a common start (time a burn needs to get ready).
   virtual int start_lead_ms() const { return 0; }
-  // Everything but the burn for one GPU: {"hbm","hbm_walk","mfma","gemm","pcie","soak"}.
+  // Everything but the burn for one GPU: {"hbm","hbm_walk","mfma","lowp","gemm","pcie","soak"}.
   // Throws on a HIP/library error.
   virtual json::Value checks(Backend& backend, const GpuInfo& g, int hip_device, const DiagPlan& plan,
                              uint32_t seed) = 0;

@@ -15,7 +15,7 @@
 extern "C" {
 #endif
 
-#define BGC_DIAG_ABI_VERSION 8
+#define BGC_DIAG_ABI_VERSION 9
 #define BGC_DIAG_MAX_CU_KEYS 2048
 
 typedef struct {
@@ -49,6 +49,25 @@ int bgc_diag_device_count(void);
 // Returns 0 on success, non-zero on HIP error (message via bgc_diag_last_error()).
 int bgc_diag_hbm(int device, uint64_t bytes, int iters, uint32_t seed, bgc_hbm_result* out);
 int bgc_diag_mfma(int device, int waves_per_cu, int throughput_iters, uint32_t seed, bgc_mfma_result* out);
+typedef struct {
+  uint64_t tiles_checked;         // 16x16x128 MX tiles verified element-wise (all four variants)
+  uint64_t fp8_mismatches;        // e4m3 operands, unit E8M0 scales
+  uint64_t fp8_scaled_mismatches; // e4m3 operands, per-32-element-block scales in {1/2, 1, 2}
+  uint64_t fp4_mismatches;        // e2m1 operands, unit scales
+  uint64_t fp4_scaled_mismatches; // e2m1 operands, block scales
+  int cus_seen;
+  int bad_cus;                    // CUs with >= 1 mismatch in any variant
+  double fp8_tflops;              // dense MX-fp8 rate (v_mfma_scale_f32_16x16x128_f8f6f4)
+  double fp4_tflops;              // dense MX-fp4 rate, same instruction
+  int throughput_ok;              // both rate phases' accumulators matched exactly
+  double elapsed_ms;
+  int bad_cu_keys[64];
+} bgc_lowp_result;
+
+// The block-scaled low-precision matrix-core path (the one fp8/fp4 inference uses), which
+// the bf16 checks above never exercise: exact-integer fp8 and fp4 tiles with and without
+// E8M0 block scales on every CU, then the dense fp8 and fp4 rates.
+int bgc_diag_mfma_lowp(int device, int waves_per_cu, int throughput_iters, uint32_t seed, bgc_lowp_result* out);
 typedef struct {
   int launches;             // throughput kernels run back to back
   double elapsed_ms;        // wall time of the burn (device events)

@@ -293,6 +293,128 @@ __global__ __launch_bounds__(kBlock) void mfma_throughput(uint32_t seed, int ite
   }
 }
 
+// ---------------------------------------------------------------------------
+// Low-precision (MX block-scaled) matrix cores: v_mfma_scale_f32_16x16x128_f8f6f4.
+// Lane l holds 32 K-elements of A row (l & 15) and of B column (l & 15) from lane group
+// g = l >> 4, plus one E8M0 scale byte for (its row or column, block g) of the 4 K-blocks
+// of 32.  A and B are laid out alike, so A element (g, j) always meets B element (g, j);
+// which block, hence which scale, an element belongs to is lowp_block().  The exact
+// result is sum_blk 2^(sa(r, blk) + sb(c, blk)) * sum_{(g, j) in blk} a(r, g, j) b(c, g, j).
+// Operands in {-1, 0, 1} and scales in {1/2, 1, 2} keep every product and sum exact.
+// kFmt: 0 = fp8 e4m3 (OCP), 4 = fp4 e2m1 (two per byte; 16 of the 32 operand bytes).
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+template <int kFmt>
+__device__ __forceinline__ uint32_t lowp_code(int v) {
+  if (kFmt == 0) return v > 0 ? 0x38u : (v < 0 ? 0xB8u : 0u);  // e4m3: +-1.0 = 0 0111 000
+  return v > 0 ? 0x2u : (v < 0 ? 0xAu : 0u);                  // e2m1: +-1.0 = 0 01 0
+}
+
+// 32 operands of one lane (row or column `rc`, block `g`) packed for the MFMA
+template <int kFmt>
+__device__ __forceinline__ i32x8 lowp_pack(uint32_t seed, uint32_t tile, int rc, int g, uint32_t which) {
+  i32x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    const uint32_t c = lowp_code<kFmt>(operand(seed, tile, rc, 32 * g + j, which));
+    if (kFmt == 0) {
+      v[j >> 2] |= static_cast<int>(c << (8 * (j & 3)));
+    } else {
+      v[j >> 3] |= static_cast<int>(c << (4 * (j & 7)));
+    }
+  }
+  return v;
+}
+
+// The scale block (= the lane group whose scale byte applies) of element j of lane group g,
+// measured on the MI355X with tools/mx_scale_layout.hip (profiles/mx_lowp_r3/):
+//  * fp4: a lane group's 32 elements are K 32g..32g+31, one block, its own scale;
+//  * fp8: elements 0-15 are K 16g..16g+15 and 16-31 are K 64+16g.., so they fall in
+//    blocks g/2 and 2+g/2, scaled by lane groups g/2 and 2+g/2.
+template <int kFmt>
+__device__ __forceinline__ int lowp_block(int g, int j) {
+  return kFmt == 0 ? (g >> 1) + 2 * (j >> 4) : g;
+}
+
+// scale exponent in {-1, 0, 1} for (row or column, block); 0 when unscaled
+__device__ __forceinline__ int lowp_exp(uint32_t seed, uint32_t tile, int rc, int g, uint32_t which, bool scaled) {
+  return scaled ? operand(seed ^ 0x5ca1e, tile, rc, g, which) : 0;
+}
+
+template <int kFmt>
+__device__ __forceinline__ f32x4 lowp_mfma(i32x8 a, i32x8 b, f32x4 acc, int sa, int sb) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, acc, kFmt, kFmt, 0, 127 + sa, 0, 127 + sb);
+}
+
+template <int kFmt>
+__global__ __launch_bounds__(kBlock) void mfma_lowp_check(uint32_t seed, int rounds, int scaled,
+                                                          unsigned* __restrict__ cu_tiles,
+                                                          unsigned* __restrict__ cu_bad) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = (blockIdx.x * (kBlock / 64)) + (threadIdx.x >> 6);
+  const uint32_t key = cu_key();
+  const int rc = lane & 15, g = lane >> 4;
+  unsigned bad = 0;
+  for (int r = 0; r < rounds; ++r) {
+    const uint32_t tile = wave * static_cast<uint32_t>(rounds) + static_cast<uint32_t>(r);
+    const i32x8 a = lowp_pack<kFmt>(seed, tile, rc, g, 0xA);
+    const i32x8 b = lowp_pack<kFmt>(seed, tile, rc, g, 0xB);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    acc = lowp_mfma<kFmt>(a, b, acc, lowp_exp(seed, tile, rc, g, 0xA, scaled), lowp_exp(seed, tile, rc, g, 0xB, scaled));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int orow = 4 * g + i;  // the C/D map of every 16x16 MFMA: column lane & 15, row 4 (lane >> 4) + i
+      int dot[4] = {0, 0, 0, 0};  // per scale block
+      for (int gg = 0; gg < 4; ++gg) {
+        for (int j = 0; j < 32; ++j) {
+          dot[lowp_block<kFmt>(gg, j)] +=
+              operand(seed, tile, orow, 32 * gg + j, 0xA) * operand(seed, tile, rc, 32 * gg + j, 0xB);
+        }
+      }
+      float expect = 0.f;
+      for (int blk = 0; blk < 4; ++blk) {
+        const int e = lowp_exp(seed, tile, orow, blk, 0xA, scaled) + lowp_exp(seed, tile, rc, blk, 0xB, scaled);
+        expect += ldexpf(static_cast<float>(dot[blk]), e);
+      }
+      bad += (acc[i] != expect);
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) bad += __shfl_down(bad, off, 64);
+  if (lane == 0) {
+    atomicAdd(&cu_tiles[key], static_cast<unsigned>(rounds));
+    if (bad) atomicAdd(&cu_bad[key], bad);
+  }
+}
+
+// Rate: 4 independent accumulator chains per wave, unit scales, acc == iters * tile + c
+template <int kFmt>
+__global__ __launch_bounds__(kBlock) void mfma_lowp_throughput(uint32_t seed, int iters, unsigned* __restrict__ fails) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t tile = (blockIdx.x * (kBlock / 64)) + (threadIdx.x >> 6);
+  const int rc = lane & 15, g = lane >> 4;
+  const i32x8 a = lowp_pack<kFmt>(seed, tile, rc, g, 0xA);
+  const i32x8 b = lowp_pack<kFmt>(seed, tile, rc, g, 0xB);
+  f32x4 acc[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) acc[c] = f32x4{float(c), float(c), float(c), float(c)};
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[c] = lowp_mfma<kFmt>(a, b, acc[c], 0, 0);
+  }
+  unsigned bad = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int orow = 4 * g + i;
+    int expect = 0;
+    for (int k = 0; k < 128; ++k) expect += operand(seed, tile, orow, k, 0xA) * operand(seed, tile, rc, k, 0xB);
+    const float e = static_cast<float>(expect) * static_cast<float>(iters);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) bad += (acc[c][i] != e + float(c));
+  }
+  for (int off = 32; off > 0; off >>= 1) bad += __shfl_down(bad, off, 64);
+  if (lane == 0 && bad) atomicAdd(fails, bad);
+}
+
 // Plain MFMA GEMM for the host cross-check: C[M,N] (fp32) = A[M,K] * B[K,N] (bf16,
 // row-major).  One wave per 16x16 output tile, K consumed 32 at a time by
 // v_mfma_f32_16x16x32_bf16 with the same operand layout as the tests above: lane l
@@ -937,6 +1059,91 @@ int bgc_diag_mfma(int device, int waves_per_cu, int throughput_iters, uint32_t s
   out->tflops = flops / (ms_tp * 1e-3) / 1e12;
   out->throughput_ok = h_fails == 0;
   out->elapsed_ms = ms_check + ms_tp;
+  return 0;
+}
+
+int bgc_diag_mfma_lowp(int device, int waves_per_cu, int throughput_iters, uint32_t seed, bgc_lowp_result* out) {
+  if (!out || waves_per_cu <= 0 || waves_per_cu > 64 || throughput_iters <= 0 || throughput_iters > (1 << 16)) {
+    g_last_error = "invalid arguments";
+    return 1;
+  }
+  std::memset(out, 0, sizeof(*out));
+  HIP_TRY(hipSetDevice(device));
+  const int cus = cu_count(device);
+  const int blocks = std::max(1, cus * waves_per_cu / (kBlock / 64));
+  const int rounds = 2;
+  // bins: [fmt][scaled] tiles and mismatches per CU key
+  DeviceBuffer tiles, bad, fails;
+  const size_t bins = 4 * static_cast<size_t>(BGC_DIAG_MAX_CU_KEYS);
+  HIP_TRY(hipMalloc(&tiles.p, bins * sizeof(unsigned)));
+  HIP_TRY(hipMalloc(&bad.p, bins * sizeof(unsigned)));
+  HIP_TRY(hipMalloc(&fails.p, 2 * sizeof(unsigned)));
+  HIP_TRY(hipMemset(tiles.p, 0, bins * sizeof(unsigned)));
+  HIP_TRY(hipMemset(bad.p, 0, bins * sizeof(unsigned)));
+  auto* t = static_cast<unsigned*>(tiles.p);
+  auto* b = static_cast<unsigned*>(bad.p);
+  auto* f = static_cast<unsigned*>(fails.p);
+  Events ev;
+  HIP_TRY(hipEventCreate(&ev.a));
+  HIP_TRY(hipEventCreate(&ev.b));
+  float ms = 0.f, total = 0.f;
+  HIP_TRY(hipEventRecord(ev.a, nullptr));
+  for (int sc = 0; sc < 2; ++sc) {
+    const size_t o8 = static_cast<size_t>(sc) * BGC_DIAG_MAX_CU_KEYS, o4 = (2 + static_cast<size_t>(sc)) * BGC_DIAG_MAX_CU_KEYS;
+    hipLaunchKernelGGL(mfma_lowp_check<0>, dim3(blocks), dim3(kBlock), 0, nullptr, seed, rounds, sc, t + o8, b + o8);
+    hipLaunchKernelGGL(mfma_lowp_check<4>, dim3(blocks), dim3(kBlock), 0, nullptr, seed, rounds, sc, t + o4, b + o4);
+  }
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(ev.b, nullptr));
+  HIP_TRY(hipEventSynchronize(ev.b));
+  HIP_TRY(hipEventElapsedTime(&ms, ev.a, ev.b));
+  total += ms;
+  // warm-up, then one timed launch per format
+  hipLaunchKernelGGL(mfma_lowp_throughput<0>, dim3(blocks), dim3(kBlock), 0, nullptr, seed, 64, f);
+  HIP_TRY(hipMemset(f, 0, 2 * sizeof(unsigned)));
+  float ms_fmt[2] = {0.f, 0.f};
+  for (int i = 0; i < 2; ++i) {
+    HIP_TRY(hipEventRecord(ev.a, nullptr));
+    if (i == 0) {
+      hipLaunchKernelGGL(mfma_lowp_throughput<0>, dim3(blocks), dim3(kBlock), 0, nullptr, seed, throughput_iters, f);
+    } else {
+      hipLaunchKernelGGL(mfma_lowp_throughput<4>, dim3(blocks), dim3(kBlock), 0, nullptr, seed, throughput_iters, f + 1);
+    }
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(ev.b, nullptr));
+    HIP_TRY(hipEventSynchronize(ev.b));
+    HIP_TRY(hipEventElapsedTime(&ms_fmt[i], ev.a, ev.b));
+    total += ms_fmt[i];
+  }
+  std::vector<unsigned> h_t(bins), h_b(bins);
+  unsigned h_f[2] = {0, 0};
+  HIP_TRY(hipMemcpy(h_t.data(), t, bins * sizeof(unsigned), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(h_b.data(), b, bins * sizeof(unsigned), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(h_f, f, sizeof(h_f), hipMemcpyDeviceToHost));
+  uint64_t* mism[4] = {&out->fp8_mismatches, &out->fp8_scaled_mismatches, &out->fp4_mismatches,
+                       &out->fp4_scaled_mismatches};
+  for (int k = 0; k < BGC_DIAG_MAX_CU_KEYS; ++k) {
+    unsigned seen = 0, bad_here = 0;
+    for (int v = 0; v < 4; ++v) {
+      const size_t i = static_cast<size_t>(v) * BGC_DIAG_MAX_CU_KEYS + static_cast<size_t>(k);
+      seen += h_t[i];
+      bad_here += h_b[i];
+      *mism[v] += h_b[i];
+      out->tiles_checked += h_t[i];
+    }
+    if (!seen) continue;
+    out->cus_seen++;
+    if (bad_here) {
+      if (out->bad_cus < 64) out->bad_cu_keys[out->bad_cus] = k;
+      out->bad_cus++;
+    }
+  }
+  const double waves = static_cast<double>(blocks) * (kBlock / 64);
+  const double flops = waves * throughput_iters * 4.0 * (2.0 * 16 * 16 * 128);
+  out->fp8_tflops = ms_fmt[0] > 0 ? flops / (ms_fmt[0] * 1e-3) / 1e12 : 0.0;
+  out->fp4_tflops = ms_fmt[1] > 0 ? flops / (ms_fmt[1] * 1e-3) / 1e12 : 0.0;
+  out->throughput_ok = h_f[0] == 0 && h_f[1] == 0;
+  out->elapsed_ms = total;
   return 0;
 }
 

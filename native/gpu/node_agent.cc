@@ -50,6 +50,9 @@ NodeAgentConfig NodeAgentConfig::from_env(const EnvConfig& env) {
   c.diag_soak_size = static_cast<int>(env.u64_or("diag_soak_size", static_cast<uint64_t>(c.diag_soak_size)));
   c.diag_soak_launches = static_cast<int>(env.u64_or("diag_soak_launches", static_cast<uint64_t>(c.diag_soak_launches)));
   c.diag_floors.min_soak_tflops = env.f64_or("diag_min_soak_tflops", c.diag_floors.min_soak_tflops);
+  c.diag_lowp = env.boolean_or("diag_lowp", c.diag_lowp);
+  c.diag_floors.min_fp8_tflops = env.f64_or("diag_min_fp8_tflops", c.diag_floors.min_fp8_tflops);
+  c.diag_floors.min_fp4_tflops = env.f64_or("diag_min_fp4_tflops", c.diag_floors.min_fp4_tflops);
   c.diag_floors.min_pcie_h2d_gbps = env.f64_or("diag_min_pcie_h2d_gbps", c.diag_floors.min_pcie_h2d_gbps);
   c.diag_floors.min_pcie_d2h_gbps = env.f64_or("diag_min_pcie_d2h_gbps", c.diag_floors.min_pcie_d2h_gbps);
   c.diag_floors.require_full_pcie_width = env.boolean_or("diag_require_full_pcie_width", c.diag_floors.require_full_pcie_width);
@@ -350,6 +353,7 @@ DiagPlan NodeAgent::diag_plan() const {
   p.pcie_bytes = cfg_.diag_pcie_bytes;
   p.soak_size = cfg_.diag_soak_size;
   p.soak_launches = cfg_.diag_soak_launches;
+  p.lowp = cfg_.diag_lowp;
   p.burn_ms = static_cast<int>(cfg_.diag_burn_ms);
   return p;
 }
@@ -430,6 +434,8 @@ void NodeAgent::record_diag_gauges(size_t i, const Value& r) {
       {"amd_gpu_diag_hbm_walk_mismatches", "Diagnostics: HBM walk words read back wrong", "hbm_walk", "mismatches"},
       {"amd_gpu_diag_mfma_tflops", "Diagnostics: bf16 MFMA TFLOP/s (register operands)", "mfma", "tflops"},
       {"amd_gpu_diag_xcc_balance", "Diagnostics: fastest/slowest XCC wave time", "mfma", "xcc_balance"},
+      {"amd_gpu_diag_fp8_tflops", "Diagnostics: MX fp8 MFMA TFLOP/s (register operands)", "lowp", "fp8_tflops"},
+      {"amd_gpu_diag_fp4_tflops", "Diagnostics: MX fp4 MFMA TFLOP/s (register operands)", "lowp", "fp4_tflops"},
       {"amd_gpu_diag_soak_tflops", "Diagnostics: LDS-tiled MFMA GEMM soak TFLOP/s", "soak", "tflops_mean"},
       {"amd_gpu_diag_pcie_h2d_gbps", "Diagnostics: PCIe host-to-device GB/s", "pcie", "h2d_gbps"},
       {"amd_gpu_diag_pcie_d2h_gbps", "Diagnostics: PCIe device-to-host GB/s", "pcie", "d2h_gbps"},
@@ -445,7 +451,8 @@ void NodeAgent::record_diag_gauges(size_t i, const Value& r) {
     LOG_INFO("node_agent") << "diag gpu " << gpus_[i].index << ": passed in " << r.get("checks_ms").dump()
                            << " ms, read " << get("hbm", "read_gbps") << " GB/s, walk "
                            << get("hbm_walk", "bytes_covered") / 1e9 << " GB, mfma " << get("mfma", "tflops")
-                           << " TFLOP/s, xcc balance " << get("mfma", "xcc_balance") << ", soak "
+                           << " TFLOP/s, xcc balance " << get("mfma", "xcc_balance") << ", mx fp8/fp4 "
+                           << get("lowp", "fp8_tflops") << "/" << get("lowp", "fp4_tflops") << " TFLOP/s, soak "
                            << get("soak", "tflops_mean") << " TFLOP/s, pcie " << get("pcie", "h2d_gbps") << "/"
                            << get("pcie", "d2h_gbps") << " GB/s, burn " << get("burn", "tflops_mean") << " TFLOP/s";
   } else {

@@ -64,13 +64,13 @@ struct NodeAgentConfig {
   // Every GPU is diagnosed on its own thread and the burn-in is one node-level phase
   // (gpu/diag_runner.h).  A periodic pass first fences its GPUs in the device plugin
   // (listed Unhealthy, refused by Allocate), waits `diag_fence_settle_ms` for an
+  // in-flight admission to land, re-checks that they are still free and only then runs.
+  bool run_diag = false;
   // GPUs that a container (pod-resources) or a process (amdsmi) holds when the agent
   // starts: "skip" leaves them without a verdict until a periodic pass finds them free;
   // "diagnose" runs the start-up pass on them anyway (a fresh node, or a test whose own
   // process holds the GPU)
   std::string diag_start_busy = "skip";
-  // in-flight admission to land, re-checks that they are still free and only then runs.
-  bool run_diag = false;
   uint64_t diag_hbm_bytes = 1ULL << 30;  // bandwidth phases (two buffers)
   uint64_t diag_interval_secs = 0;     // 0 = only at start
   // Address-pattern walk of this share of each GPU's free VRAM (0 = off), in chunks, with
@@ -90,6 +90,8 @@ struct NodeAgentConfig {
   // checked by exact checksums (0 launches = off).
   int diag_soak_size = 8192;
   int diag_soak_launches = 20;
+  // MX block-scaled fp8 / fp4 matrix-core tiles (with and without E8M0 scales) and rates
+  bool diag_lowp = true;
   DiagFloors diag_floors = DiagFloors::mi355x_defaults();
   std::string pod_resources_socket = "/var/lib/kubelet/pod-resources/kubelet.sock";
   HealthPolicy health;

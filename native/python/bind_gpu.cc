@@ -186,6 +186,14 @@ void register_gpu(py::module_& m) {
     }
     return v.dump();
   }, py::arg("device"), py::arg("waves_per_cu") = 32, py::arg("iters") = 4096, py::arg("seed") = 0x5eed);
+  m.def("diag_mfma_lowp", [](int device, int waves_per_cu, int iters, unsigned seed) {
+    Value v;
+    {
+      py::gil_scoped_release nogil;
+      v = bgc::gpu::Diag::instance().mfma_lowp(device, waves_per_cu, iters, seed);
+    }
+    return v.dump();
+  }, py::arg("device"), py::arg("waves_per_cu") = 32, py::arg("iters") = 4096, py::arg("seed") = 0x5eed);
   m.def("diag_gemm", [](int device, int mm, int nn, int kk, const std::string& a, const std::string& b) {
     if (a.size() != static_cast<size_t>(mm) * kk * 2 || b.size() != static_cast<size_t>(kk) * nn * 2) {
       throw std::invalid_argument("A must be M*K and B K*N bf16 values");
@@ -274,6 +282,8 @@ void register_gpu(py::module_& m) {
     num("min_write_gbps", f.min_write_gbps);
     num("min_mfma_tflops", f.min_mfma_tflops);
     num("min_xcc_balance", f.min_xcc_balance);
+    num("min_fp8_tflops", f.min_fp8_tflops);
+    num("min_fp4_tflops", f.min_fp4_tflops);
     num("min_burn_tflops", f.min_burn_tflops);
     num("min_burn_sustain", f.min_burn_sustain);
     num("max_burn_hotspot_c", f.max_burn_hotspot_c);

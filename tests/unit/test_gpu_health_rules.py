@@ -174,6 +174,23 @@ def test_judge_diag_floors(nat):
     assert not r["passed"] and len(r["failures"]) == 2
 
 
+def test_judge_diag_mx_lowp_section(nat):
+    """The MX fp8/fp4 matrix-core check: any wrong tile, wrong accumulators or a rate under
+    its floor fails the GPU, and the failure names the variant."""
+    lowp = {"fp8_tflops": 4000.0, "fp4_tflops": 7000.0, "fp8_mismatches": 0, "fp8_scaled_mismatches": 0,
+            "fp4_mismatches": 0, "fp4_scaled_mismatches": 0, "mismatches": 0, "bad_cus": 0, "throughput_ok": True}
+    ok = json.loads(nat.judge_diag(json.dumps(dict(MI355X_MEASURED, lowp=lowp))))
+    assert ok["passed"], ok["failures"]
+    bad = dict(lowp, fp4_scaled_mismatches=12, mismatches=12, bad_cus=1)
+    r = json.loads(nat.judge_diag(json.dumps(dict(MI355X_MEASURED, lowp=bad))))
+    assert not r["passed"] and "fp4 scaled 12" in r["failures"][0] and "1 CU(s)" in r["failures"][0]
+    r = json.loads(nat.judge_diag(json.dumps(dict(MI355X_MEASURED, lowp=dict(lowp, throughput_ok=False)))))
+    assert r["failures"] == ["MX fp8/fp4 MFMA throughput accumulators wrong"]
+    r = json.loads(nat.judge_diag(json.dumps(dict(MI355X_MEASURED, lowp=lowp)),
+                                  json.dumps({"min_fp8_tflops": 5000, "min_fp4_tflops": 6000})))
+    assert r["failures"] == ["MX fp8 MFMA TFLOP/s 4000 below floor 5000"]
+
+
 def test_pod_resources_codec_matches_protobuf(nat):
     from google.protobuf import descriptor_pb2, descriptor_pool, message_factory
 
