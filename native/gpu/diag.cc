@@ -47,7 +47,7 @@ Diag::Diag(const std::string& path) : path_(path) {
   arch_ = reinterpret_cast<int (*)(int, char*, size_t)>(dlsym(lib_, "bgc_diag_device_arch"));
   gemm_ = reinterpret_cast<int (*)(int, int, int, int, const uint16_t*, const uint16_t*, float*)>(
       dlsym(lib_, "bgc_diag_gemm"));
-  burn_ = reinterpret_cast<int (*)(int, int, int, uint32_t, bgc_burn_result*)>(dlsym(lib_, "bgc_diag_burn"));
+  burn_ = reinterpret_cast<int (*)(int, int, int, uint32_t, int, bgc_burn_result*)>(dlsym(lib_, "bgc_diag_burn_dtype"));
   pcie_ = reinterpret_cast<int (*)(int, uint64_t, int, uint32_t, bgc_pcie_result*)>(dlsym(lib_, "bgc_diag_pcie"));
   soak_ = reinterpret_cast<int (*)(int, int, int, int, int, uint32_t, bgc_soak_result*)>(dlsym(lib_, "bgc_diag_gemm_soak"));
   tiled_ = reinterpret_cast<int (*)(int, int, int, int, const uint16_t*, const uint16_t*, float*)>(
@@ -168,10 +168,12 @@ json::Value Diag::mfma_lowp(int device, int waves_per_cu, int throughput_iters, 
                               {"passed", mism == 0 && r.throughput_ok != 0}});
 }
 
-json::Value Diag::burn(int device, int duration_ms, int waves_per_cu, uint32_t seed) {
+json::Value Diag::burn(int device, int duration_ms, int waves_per_cu, uint32_t seed, int dtype) {
   bgc_burn_result r{};
-  if (burn_(device, duration_ms, waves_per_cu, seed, &r) != 0) throw std::runtime_error(std::string("burn: ") + last_error_());
-  return json::Value::object({{"launches", r.launches}, {"elapsed_ms", r.elapsed_ms}, {"tflops_mean", r.tflops_mean},
+  if (burn_(device, duration_ms, waves_per_cu, seed, dtype, &r) != 0) {
+    throw std::runtime_error(std::string("burn: ") + last_error_());
+  }
+  return json::Value::object({{"dtype", burn_dtype_name(dtype)}, {"launches", r.launches}, {"elapsed_ms", r.elapsed_ms}, {"tflops_mean", r.tflops_mean},
                               {"tflops_min", r.tflops_min}, {"tflops_first", r.tflops_first},
                               {"tflops_last", r.tflops_last}, {"tflops_max", r.tflops_max},
                               // the last launch against the best: < 1 when the GPU throttled
@@ -298,6 +300,22 @@ json::Value Diag::gemm_check(int device, int m, int n, int k, uint32_t seed) {
                               {"passed", bad == 0}});
 }
 
+int burn_dtype_code(const std::string& name) {
+  if (name == "bf16") return BGC_BURN_BF16;
+  if (name == "fp8") return BGC_BURN_FP8;
+  if (name == "fp4") return BGC_BURN_FP4;
+  throw std::runtime_error("burn dtype must be bf16, fp8 or fp4, not '" + name + "'");
+}
+
+const char* burn_dtype_name(int code) {
+  return code == BGC_BURN_FP8 ? "fp8" : code == BGC_BURN_FP4 ? "fp4" : "bf16";
+}
+
+double burn_dtype_rate_ratio(int code) {
+  // sustained on MI355X: bf16 2.40, MX fp8 4.79, MX fp4 8.47 PF/s (profiles/mx_lowp_r3/)
+  return code == BGC_BURN_FP8 ? 2.0 : code == BGC_BURN_FP4 ? 3.5 : 1.0;
+}
+
 DiagFloors DiagFloors::mi355x_defaults() {
   DiagFloors f;
   // MI355X, ROCm 7.2, 1 GiB buffers / 16 waves per CU x 2048 MFMA iterations
@@ -410,7 +428,11 @@ json::Value judge_diag(const json::Value& result, const DiagFloors& fl) {
   const json::Value& burn = result.get("burn");
   if (burn.is_object()) {
     if (num(burn, "mismatches") > 0) failures.push_back("burn-in MFMA accumulators wrong");
-    floor_check(burn, "tflops_mean", fl.min_burn_tflops, "burn-in MFMA TFLOP/s");
+    // the floor is for bf16; an fp8 / fp4 burn is held to it scaled by that path's rate
+    const std::string dt = burn.get("dtype").is_string() ? burn.get_string("dtype") : "bf16";
+    const int code = dt == "fp8" ? BGC_BURN_FP8 : dt == "fp4" ? BGC_BURN_FP4 : BGC_BURN_BF16;
+    const std::string what = "burn-in MFMA " + (code == BGC_BURN_BF16 ? std::string() : "MX " + dt + " ") + "TFLOP/s";
+    floor_check(burn, "tflops_mean", fl.min_burn_tflops * burn_dtype_rate_ratio(code), what.c_str());
     if (fl.min_burn_sustain > 0 && num(burn, "sustain") < fl.min_burn_sustain) {
       char buf[160];
       std::snprintf(buf, sizeof(buf), "MFMA rate sagged to %.2f of its start under sustained load (floor %.2f)",

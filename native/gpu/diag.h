@@ -49,6 +49,13 @@ struct DiagFloors {
   static DiagFloors mi355x_defaults();
 };
 
+// Burn dtype names ("bf16", "fp8", "fp4") <-> BGC_BURN_*; the name throws on anything else.
+int burn_dtype_code(const std::string& name);
+const char* burn_dtype_name(int code);
+// Dense-rate ratio of a burn dtype to bf16 on MI355X, as the burn kernels measure it (fp8
+// 2.0x, fp4 3.5x; profiles/mx_lowp_r3/): the bf16 burn floor scales by it.
+double burn_dtype_rate_ratio(int code);
+
 // Pure verdict over one GPU's results ({"hbm":…, "mfma":…, "gemm":…}): adds "passed" and
 // "failures" (one string per violated check) to a copy of `result`.
 json::Value judge_diag(const json::Value& result, const DiagFloors& floors);
@@ -67,8 +74,8 @@ class Diag {
   // MFMA GEMM on the device vs a host fp32 product of the same bf16 operands
   // (deterministic pseudo-random values in [-1, 1]).  Returns max error and the bound.
   json::Value gemm_check(int device, int m, int n, int k, uint32_t seed);
-  // Sustained MFMA load for duration_ms (see bgc_diag_burn).
-  json::Value burn(int device, int duration_ms, int waves_per_cu, uint32_t seed);
+  // Sustained MFMA load for duration_ms (see bgc_diag_burn_dtype; dtype BGC_BURN_*).
+  json::Value burn(int device, int duration_ms, int waves_per_cu, uint32_t seed, int dtype = BGC_BURN_BF16);
   // Pinned host <-> device copies (see bgc_diag_pcie).
   json::Value pcie(int device, uint64_t bytes, int iters, uint32_t seed);
   // LDS-tiled MFMA GEMM run back to back, checked by exact checksums (bgc_diag_gemm_soak).
@@ -93,7 +100,7 @@ class Diag {
   int (*lowp_)(int, int, int, uint32_t, bgc_lowp_result*) = nullptr;
   int (*arch_)(int, char*, size_t) = nullptr;
   int (*gemm_)(int, int, int, int, const uint16_t*, const uint16_t*, float*) = nullptr;
-  int (*burn_)(int, int, int, uint32_t, bgc_burn_result*) = nullptr;
+  int (*burn_)(int, int, int, uint32_t, int, bgc_burn_result*) = nullptr;
   int (*pcie_)(int, uint64_t, int, uint32_t, bgc_pcie_result*) = nullptr;
   int (*soak_)(int, int, int, int, int, uint32_t, bgc_soak_result*) = nullptr;
   int (*tiled_)(int, int, int, int, const uint16_t*, const uint16_t*, float*) = nullptr;

@@ -143,12 +143,12 @@ class HipDiagEngine : public DiagEngine {
     r["timing_ms"] = timing;
     return r;
   }
-  Value burn(int dev, int duration_ms, uint32_t seed, std::chrono::steady_clock::time_point start_at) override {
+  Value burn(int dev, int duration_ms, uint32_t seed, int dtype, std::chrono::steady_clock::time_point start_at) override {
     Diag& d = Diag::instance();
     (void)d.device_arch(dev);  // the HIP runtime and the device's context, before the wait
     const auto ready = std::chrono::steady_clock::now();
     sleep_until(start_at);
-    Value r = d.burn(dev, duration_ms, 32, seed);
+    Value r = d.burn(dev, duration_ms, 32, seed, dtype);
     r["ready_at_ns"] = static_cast<long long>(std::chrono::duration_cast<std::chrono::nanoseconds>(ready.time_since_epoch()).count());
     r["late_ms"] = ready > start_at ? std::chrono::duration<double, std::milli>(ready - start_at).count() : 0.0;
     return r;
@@ -218,10 +218,10 @@ class ProcessDiagEngine : public DiagEngine {
     note_ready(r, t0);  // so the start-up burn's lead is measured, not guessed
     return r;
   }
-  Value burn(int dev, int duration_ms, uint32_t seed, std::chrono::steady_clock::time_point start_at) override {
+  Value burn(int dev, int duration_ms, uint32_t seed, int dtype, std::chrono::steady_clock::time_point start_at) override {
     const int64_t at = std::chrono::duration_cast<std::chrono::nanoseconds>(start_at.time_since_epoch()).count();
     Value req = Value::object({{"op", "burn"}, {"backend", kind_}, {"fixture", fixture_}, {"gpu_hip_device", dev},
-                               {"duration_ms", duration_ms},
+                               {"duration_ms", duration_ms}, {"dtype", burn_dtype_name(dtype)},
                                {"seed", static_cast<unsigned long long>(seed)}, {"start_at_ns", static_cast<long long>(at)}});
     const auto spawned = std::chrono::steady_clock::now();
     Value r = run_worker(exe_, req, dev, duration_ms + start_lead_ms() + 60000, cancel_);
@@ -286,12 +286,14 @@ class ScriptedDiagEngine : public DiagEngine {
     if (e.get("fail").is_string()) r["error"] = e.get_string("fail");
     return r;
   }
-  Value burn(int dev, int duration_ms, uint32_t, std::chrono::steady_clock::time_point start_at) override {
+  Value burn(int dev, int duration_ms, uint32_t, int dtype, std::chrono::steady_clock::time_point start_at) override {
     sleep_until(start_at);
     std::this_thread::sleep_for(std::chrono::milliseconds(duration_ms));
     const Value script = backend_.diag_script();
-    const double tf = num(script.get("gpus").get(std::to_string(dev)), "burn_tflops", num(script, "burn_tflops", 2400));
-    return Value::object({{"launches", std::max(1, duration_ms / 10)}, {"elapsed_ms", static_cast<double>(duration_ms)},
+    // the script's rate is a bf16 rate; an MX burn scales it like the hardware does
+    const double tf = num(script.get("gpus").get(std::to_string(dev)), "burn_tflops", num(script, "burn_tflops", 2400)) *
+                      burn_dtype_rate_ratio(dtype);
+    return Value::object({{"dtype", burn_dtype_name(dtype)}, {"launches", std::max(1, duration_ms / 10)}, {"elapsed_ms", static_cast<double>(duration_ms)},
                           {"tflops_mean", tf}, {"tflops_min", tf}, {"tflops_first", tf}, {"tflops_last", tf},
                           {"tflops_max", tf}, {"sustain", 1.0}, {"mismatches", 0}});
   }
@@ -329,7 +331,8 @@ Value to_json(const DiagPlan& p) {
                         {"soak_size", p.soak_size},
                         {"soak_launches", p.soak_launches},
                         {"lowp", p.lowp},
-                        {"burn_ms", p.burn_ms}});
+                        {"burn_ms", p.burn_ms},
+                        {"burn_dtype", burn_dtype_name(p.burn_dtype)}});
 }
 
 DiagPlan diag_plan_from_json(const Value& v) {
@@ -345,6 +348,7 @@ DiagPlan diag_plan_from_json(const Value& v) {
   p.soak_launches = i32("soak_launches", p.soak_launches);
   p.lowp = v.get("lowp").is_bool() ? v.get("lowp").as_bool() : p.lowp;
   p.burn_ms = i32("burn_ms", p.burn_ms);
+  if (v.get("burn_dtype").is_string()) p.burn_dtype = burn_dtype_code(v.get_string("burn_dtype"));
   return p;
 }
 
@@ -385,7 +389,8 @@ int diag_worker_main() {
         out = engine->checks(*backend, gpu_info_from_json(req.get("gpu")), dev, diag_plan_from_json(req.get("plan")), seed);
       } else {
         const auto at = std::chrono::steady_clock::time_point(std::chrono::nanoseconds(req.get("start_at_ns").as_int()));
-        out = engine->burn(script_dev, static_cast<int>(req.get("duration_ms").as_int()), seed, at);
+        out = engine->burn(script_dev, static_cast<int>(req.get("duration_ms").as_int()), seed,
+                           burn_dtype_code(req.get_string("dtype", "bf16")), at);
       }
     } else {
       throw std::runtime_error("unknown diagnostics worker op '" + op + "'");
@@ -439,7 +444,8 @@ Value pcie_check(Backend& backend, const GpuInfo& g, int hip_device, uint64_t by
   return out;
 }
 
-Value burn_in(Backend& backend, int index, int hip_device, int duration_ms, uint32_t seed, DiagEngine* engine) {
+Value burn_in(Backend& backend, int index, int hip_device, int duration_ms, uint32_t seed, DiagEngine* engine,
+              int dtype) {
   std::unique_ptr<DiagEngine> own;
   if (!engine) {
     own = make_hip_diag_engine();
@@ -455,7 +461,7 @@ Value burn_in(Backend& backend, int index, int hip_device, int duration_ms, uint
   });
   Value out;
   try {
-    out = engine->burn(hip_device, duration_ms, seed, std::chrono::steady_clock::time_point());
+    out = engine->burn(hip_device, duration_ms, seed, dtype, std::chrono::steady_clock::time_point());
   } catch (...) {
     done = true;
     sampler.join();
@@ -469,7 +475,7 @@ Value burn_in(Backend& backend, int index, int hip_device, int duration_ms, uint
 
 NodeBurnResult node_burn(Backend& backend, DiagEngine& engine, const std::vector<GpuInfo>& gpus,
                          const std::vector<int>& hip_devs, const std::vector<size_t>& which, int duration_ms,
-                         uint32_t seed) {
+                         uint32_t seed, int dtype) {
   const size_t n = which.size();
   NodeBurnResult res;
   res.per_gpu.assign(n, Value());
@@ -521,7 +527,7 @@ NodeBurnResult node_burn(Backend& backend, DiagEngine& engine, const std::vector
         cv.wait(lk, [&] { return go; });
       }
       try {
-        res.per_gpu[k] = engine.burn(hip_devs[which[k]], duration_ms, seed + static_cast<uint32_t>(which[k]), start_at);
+        res.per_gpu[k] = engine.burn(hip_devs[which[k]], duration_ms, seed + static_cast<uint32_t>(which[k]), dtype, start_at);
       } catch (const std::exception& e) {
         err[k] = e.what();
       }
@@ -545,6 +551,7 @@ NodeBurnResult node_burn(Backend& backend, DiagEngine& engine, const std::vector
     st[k].fill(res.per_gpu[k]);
   }
   res.node = Value::object({{"gpus", static_cast<unsigned long long>(n)},
+                            {"dtype", burn_dtype_name(dtype)},
                             {"duration_ms", duration_ms},
                             {"wall_ms", wall_ms},
                             {"start_lead_ms", start_lead_ms},

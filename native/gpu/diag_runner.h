@@ -41,6 +41,7 @@ struct DiagPlan {
   int soak_launches = 20;                // 0 = off
   bool lowp = true;                      // MX fp8 / fp4 matrix-core tiles and rates
   int burn_ms = 0;                       // node-level burn phase (0 = off)
+  int burn_dtype = BGC_BURN_BF16;         // its matrix-core path (bf16, MX fp8, MX fp4)
 };
 
 class DiagEngine {
@@ -53,9 +54,9 @@ class DiagEngine {
   // Throws on a HIP/library error.
   virtual json::Value checks(Backend& backend, const GpuInfo& g, int hip_device, const DiagPlan& plan,
                              uint32_t seed) = 0;
-  // Sustained MFMA load on one GPU (Diag::burn's result shape), starting at start_at
+  // Sustained MFMA load on one GPU (Diag::burn's result shape; dtype BGC_BURN_*), starting at start_at
   // (steady clock; the epoch = now) so that GPUs burning together start together.
-  virtual json::Value burn(int hip_device, int duration_ms, uint32_t seed,
+  virtual json::Value burn(int hip_device, int duration_ms, uint32_t seed, int dtype,
                            std::chrono::steady_clock::time_point start_at) = 0;
 };
 
@@ -93,7 +94,7 @@ json::Value pcie_check(Backend& backend, const GpuInfo& g, int hip_device, uint6
 // One GPU's burn while a side thread samples it (power, clocks, temperatures, throttle
 // residency); the single-GPU form of node_burn.
 json::Value burn_in(Backend& backend, int index, int hip_device, int duration_ms, uint32_t seed,
-                    DiagEngine* engine = nullptr);
+                    DiagEngine* engine = nullptr, int dtype = BGC_BURN_BF16);
 
 struct NodeBurnResult {
   std::vector<json::Value> per_gpu;   // burn section per entry of `which` (burn_in's shape)
@@ -104,7 +105,7 @@ struct NodeBurnResult {
 // for duration_ms behind a start barrier.
 NodeBurnResult node_burn(Backend& backend, DiagEngine& engine, const std::vector<GpuInfo>& gpus,
                          const std::vector<int>& hip_devs, const std::vector<size_t>& which, int duration_ms,
-                         uint32_t seed);
+                         uint32_t seed, int dtype = BGC_BURN_BF16);
 
 // Node-level verdict over a node_burn: adds "failures"/"passed" to the node summary and
 // returns, per GPU in the burn, the failures that name it (a GPU far below the node's

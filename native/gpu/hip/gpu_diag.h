@@ -15,7 +15,7 @@
 extern "C" {
 #endif
 
-#define BGC_DIAG_ABI_VERSION 9
+#define BGC_DIAG_ABI_VERSION 10
 #define BGC_DIAG_MAX_CU_KEYS 2048
 
 typedef struct {
@@ -82,6 +82,12 @@ typedef struct {
 // Sustained MFMA load for `duration_ms` (back-to-back throughput kernels of ~10 ms each):
 // the node agent samples power, clocks, temperatures and throttle residency meanwhile.
 int bgc_diag_burn(int device, int duration_ms, int waves_per_cu, uint32_t seed, bgc_burn_result* out);
+// The same load on another matrix-core path: BGC_BURN_FP8 / BGC_BURN_FP4 run the MX
+// block-scaled v_mfma_scale_f32_16x16x128_f8f6f4 rate kernel (rates in that dtype's FLOP/s).
+#define BGC_BURN_BF16 0
+#define BGC_BURN_FP8 1
+#define BGC_BURN_FP4 2
+int bgc_diag_burn_dtype(int device, int duration_ms, int waves_per_cu, uint32_t seed, int dtype, bgc_burn_result* out);
 // C[m,n] (fp32) = A[m,k] * B[k,n], A/B bf16 bit patterns, row-major, via MFMA; the host
 // compares C with its own fp32 product (m, n multiples of 16; k a multiple of 32).
 int bgc_diag_gemm(int device, int m, int n, int k, const uint16_t* a_bf16, const uint16_t* b_bf16, float* c);

@@ -1148,7 +1148,12 @@ int bgc_diag_mfma_lowp(int device, int waves_per_cu, int throughput_iters, uint3
 }
 
 int bgc_diag_burn(int device, int duration_ms, int waves_per_cu, uint32_t seed, bgc_burn_result* out) {
-  if (!out || duration_ms <= 0 || duration_ms > 600000 || waves_per_cu <= 0 || waves_per_cu > 64) {
+  return bgc_diag_burn_dtype(device, duration_ms, waves_per_cu, seed, BGC_BURN_BF16, out);
+}
+
+int bgc_diag_burn_dtype(int device, int duration_ms, int waves_per_cu, uint32_t seed, int dtype, bgc_burn_result* out) {
+  if (!out || duration_ms <= 0 || duration_ms > 600000 || waves_per_cu <= 0 || waves_per_cu > 64 ||
+      dtype < BGC_BURN_BF16 || dtype > BGC_BURN_FP4) {
     g_last_error = "invalid arguments";
     return 1;
   }
@@ -1170,14 +1175,21 @@ int bgc_diag_burn(int device, int duration_ms, int waves_per_cu, uint32_t seed, 
   HIP_TRY(hipEventCreate(&total.b));
   // size one launch to ~10 ms at MI355X rates (iters * 4 MFMA per wave), measured below
   int iters = 2048;
-  const double flops_per_iter = static_cast<double>(blocks) * (kBlock / 64) * 4.0 * (2.0 * 16 * 16 * 32);
+  const double mfma_k = dtype == BGC_BURN_BF16 ? 32.0 : 128.0;  // 16x16x32 bf16, 16x16x128 MX
+  const double flops_per_iter = static_cast<double>(blocks) * (kBlock / 64) * 4.0 * (2.0 * 16 * 16 * mfma_k);
+  auto* fp = static_cast<unsigned*>(fails.p);
   float ms = 0.f;
   HIP_TRY(hipEventRecord(total.a, nullptr));
   double sum_flops = 0;
   while (true) {
     HIP_TRY(hipEventRecord(ev.a, nullptr));
-    hipLaunchKernelGGL(mfma_throughput, dim3(blocks), dim3(kBlock), 0, nullptr, seed, iters,
-                       static_cast<unsigned*>(fails.p), xt, xw);
+    if (dtype == BGC_BURN_FP8) {
+      hipLaunchKernelGGL(mfma_lowp_throughput<0>, dim3(blocks), dim3(kBlock), 0, nullptr, seed, iters, fp);
+    } else if (dtype == BGC_BURN_FP4) {
+      hipLaunchKernelGGL(mfma_lowp_throughput<4>, dim3(blocks), dim3(kBlock), 0, nullptr, seed, iters, fp);
+    } else {
+      hipLaunchKernelGGL(mfma_throughput, dim3(blocks), dim3(kBlock), 0, nullptr, seed, iters, fp, xt, xw);
+    }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ev.b, nullptr));
     HIP_TRY(hipEventSynchronize(ev.b));

@@ -46,6 +46,8 @@ NodeAgentConfig NodeAgentConfig::from_env(const EnvConfig& env) {
   c.diag_floors.min_node_burn_balance = env.f64_or("diag_min_node_burn_balance", c.diag_floors.min_node_burn_balance);
   c.diag_floors.max_node_power_w = env.f64_or("diag_max_node_power_w", c.diag_floors.max_node_power_w);
   c.diag_burn_ms = env.u64_or("diag_burn_ms", 0);
+  c.diag_burn_dtype = env.str_or("diag_burn_dtype", c.diag_burn_dtype);
+  (void)burn_dtype_code(c.diag_burn_dtype);  // bf16 | fp8 | fp4, else the agent does not start
   c.diag_pcie_bytes = env.u64_or("diag_pcie_bytes", c.diag_pcie_bytes);
   c.diag_soak_size = static_cast<int>(env.u64_or("diag_soak_size", static_cast<uint64_t>(c.diag_soak_size)));
   c.diag_soak_launches = static_cast<int>(env.u64_or("diag_soak_launches", static_cast<uint64_t>(c.diag_soak_launches)));
@@ -547,7 +549,8 @@ bool NodeAgent::run_diagnostics(bool at_start) {
   Value node = Value();
   std::vector<std::vector<std::string>> node_failures(todo.size());
   if (cfg_.diag_burn_ms > 0 && !todo.empty()) {
-    NodeBurnResult nb = node_burn(*backend_, *engine_, gpus_, hip_devs_, todo, static_cast<int>(cfg_.diag_burn_ms), 0xb0c4);
+    NodeBurnResult nb = node_burn(*backend_, *engine_, gpus_, hip_devs_, todo, static_cast<int>(cfg_.diag_burn_ms), 0xb0c4,
+                                  burn_dtype_code(cfg_.diag_burn_dtype));
     node_failures = judge_node_burn(nb, cfg_.diag_floors);
     for (size_t k = 0; k < todo.size(); ++k) results[todo[k]]["burn"] = nb.per_gpu[k];
     node = nb.node;

@@ -83,6 +83,11 @@ struct NodeAgentConfig {
   // throttle residency are sampled (catches cooling/power-delivery faults the short
   // checks do not); 0 = off.
   uint64_t diag_burn_ms = 0;
+  // its matrix-core path.  "fp4" (MX block-scaled) drives an MI355X to its power cap:
+  // 1.30 kW mean, power-limited 71 % of the time, against 1.08-1.17 kW for "bf16" and
+  // 1.21 kW for "fp8" (profiles/mx_lowp_r3/burn_dtype.json), so it is the hardest
+  // power-delivery and cooling stress.  The bf16 rate floor scales with the dtype.
+  std::string diag_burn_dtype = "fp4";
   // PCIe check: pinned host<->device copies of this size (0 = off) with the link's
   // width/speed read while they run.
   uint64_t diag_pcie_bytes = 256ULL << 20;

@@ -236,14 +236,17 @@ void register_gpu(py::module_& m) {
     }
     return v.dump();
   }, py::arg("device"), py::arg("m") = 64, py::arg("n") = 64, py::arg("k") = 512, py::arg("seed") = 0x5eed);
-  m.def("diag_burn", [](std::shared_ptr<PyBackend> b, int index, int hip_device, int duration_ms, unsigned seed) {
+  m.def("diag_burn", [](std::shared_ptr<PyBackend> b, int index, int hip_device, int duration_ms, unsigned seed,
+                        const std::string& dtype) {
+    const int code = bgc::gpu::burn_dtype_code(dtype);
     Value v;
     {
       py::gil_scoped_release nogil;
-      v = bgc::gpu::burn_in(*b->b, index, hip_device, duration_ms, seed);
+      v = bgc::gpu::burn_in(*b->b, index, hip_device, duration_ms, seed, nullptr, code);
     }
     return v.dump();
-  }, py::arg("backend"), py::arg("index"), py::arg("hip_device"), py::arg("duration_ms"), py::arg("seed") = 0x5eed);
+  }, py::arg("backend"), py::arg("index"), py::arg("hip_device"), py::arg("duration_ms"), py::arg("seed") = 0x5eed,
+     py::arg("dtype") = "bf16");
   m.def("diag_pcie", [](int device, unsigned long long bytes, int iters, unsigned seed) {
     Value v;
     {

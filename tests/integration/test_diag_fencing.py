@@ -14,6 +14,7 @@ The fake kubelet is python grpcio (an independent gRPC stack, as grpc-go in a re
 """
 import json
 import os
+import subprocess
 import time
 
 import grpc
@@ -159,6 +160,34 @@ def test_node_burn_gates_on_summed_power_and_balance(nat):
         node = wait_for(lambda: (lambda n: n if n and n["metadata"]["labels"].get("amd.com/gpu.diag") == "failed" else None)(
             c.admin.get_or_none("nodes", "mi355x-pw")), timeout=15, desc="diag label")
         assert node["metadata"]["labels"]["amd.com/gpu.healthy-count"] == "0"
+
+
+def test_mx_burn_dtype_scales_the_burn_floor(nat):
+    """DIAG_BURN_DTYPE=fp4 runs the node burn on the MX fp4 path: its rate is held to the
+    bf16 floor scaled 3.5x, so a GPU at fp4 speed passes and one at only twice the bf16
+    rate fails with a message naming the dtype."""
+    script = {"checks_ms": 50, "gpus": {"1": {"burn_tflops": 1000}}}  # scripted rates are bf16 rates
+    with Cluster(admission=False, controller=False) as c:
+        c.start_node_agent(node_name="mi355x-mx", backend="mock", poll_interval_ms=200,
+                           fixture_obj=_fixture(nat, 2, script),
+                           extra_env={"CONF_RUN_DIAG": "true", "CONF_DIAG_BURN_MS": "300",
+                                      "CONF_DIAG_BURN_DTYPE": "fp4", "CONF_DIAG_MIN_NODE_BURN_BALANCE": "0"})
+        desc = _describe(c, "mi355x-mx")
+        assert desc["diag_node_burn"]["dtype"] == "fp4"
+        ok, slow = desc["diag"]
+        assert ok["burn"]["dtype"] == "fp4" and ok["burn"]["tflops_mean"] == pytest.approx(2400 * 3.5)
+        assert ok["passed"], ok["failures"]
+        assert not slow["passed"] and slow["failures"] == ["burn-in MFMA MX fp4 TFLOP/s 3500 below floor 6300"]
+
+
+def test_unknown_burn_dtype_stops_the_agent(tmp_path):
+    from bacchus_gpu_controller_amd import REPO_ROOT
+
+    env = dict(os.environ, CONF_GPU_BACKEND="mock", CONF_NODE_NAME="n", CONF_DIAG_BURN_DTYPE="int8",
+               CONF_LISTEN_ADDR="127.0.0.1", CONF_LISTEN_PORT="0", KUBE_API_URL="http://127.0.0.1:9")
+    p = subprocess.run([os.path.join(REPO_ROOT, "bin", "node-agent")], env=env, capture_output=True, text=True,
+                       timeout=30)
+    assert p.returncode != 0 and "burn dtype must be bf16, fp8 or fp4, not 'int8'" in p.stderr
 
 
 def test_restart_leaves_busy_gpus_alone(nat, tmp_path):
