@@ -2,9 +2,9 @@
 
 One tiny end-to-end pass of the flagship path on a real MI355X:
   1. HIP/CDNA4 diagnostics on device 0 (64 MiB HBM pattern test, MFMA tile check, an MFMA
-     GEMM compared with a host fp32 product, two launches of the 8-phase ping-pong soak GEMM
-     at 1024^3 under its ABFT checksums) — the native kernels in libbgc_gpu_diag.so, no
-     fallback;
+     GEMM compared with a host fp32 product, MX fp8 / fp4 block-scaled MFMA tiles, two
+     launches of the 8-phase ping-pong soak GEMM at 1024^3 under its ABFT checksums) — the
+     native kernels in libbgc_gpu_diag.so, no fallback;
   2. amdsmi discovery of device 0 (gfx950, HBM3E capacity);
   3. a one-tenant onboarding through kube-lite -> TLS webhook -> controller ->
      synchronizer, with the node agent advertising the GPU, until Ready.
@@ -28,8 +28,9 @@ def run_smoke(device=0):
     mfma = ops.mfma(device, waves_per_cu=4, iters=256)
     gemm = json.loads(nat.diag_gemm_check(device, 64, 64, 256, 0x5eed))  # MFMA GEMM vs a host fp32 product
     soak = ops.gemm_soak(device, 1024, 1024, 1024, launches=2)
-    if not (hbm["passed"] and mfma["passed"] and gemm["passed"] and soak["passed"]):
-        raise RuntimeError(f"GPU diagnostics failed: hbm={hbm} mfma={mfma} gemm={gemm} soak={soak}")
+    lowp = ops.mfma_lowp(device, waves_per_cu=4, iters=256)
+    if not (hbm["passed"] and mfma["passed"] and gemm["passed"] and soak["passed"] and lowp["passed"]):
+        raise RuntimeError(f"GPU diagnostics failed: hbm={hbm} mfma={mfma} gemm={gemm} soak={soak} mx={lowp}")
     if soak.get("kernel") != "pingpong":
         raise RuntimeError(f"soak ran {soak.get('kernel')}, expected the ping-pong kernel")
     gpus = json.loads(nat.gpu_backend("amdsmi", "").discover())
@@ -58,7 +59,7 @@ def run_smoke(device=0):
         raise RuntimeError(f"node not advertised: {node['status']}")
     print(json.dumps({"smoke": "ok", "arch": arch, "hbm_read_gbps": round(hbm["read_gbps"], 1),
                       "mfma_tflops": round(mfma["tflops"], 1), "gemm_max_abs_err": gemm["max_abs_err"],
-                      "soak_kernel": soak["kernel"],
+                      "soak_kernel": soak["kernel"], "mx_tiles_checked": lowp["tiles_checked"],
                       "apply_to_ready_ms": round(ready_ms, 2),
                       "node_labels": {k: v for k, v in node["metadata"]["labels"].items() if "product" in k or "vram" in k}}))
 
