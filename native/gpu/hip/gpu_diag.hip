@@ -1,5 +1,9 @@
-// MI355X (gfx950 / CDNA4) GPU health diagnostics: HBM3E pattern + bandwidth test and a
-// per-CU MFMA functional/throughput test.  See gpu_diag.h for the C ABI.
+// MI355X (gfx950 / CDNA4) GPU health diagnostics.  See gpu_diag.h for the C ABI.  Kernels:
+// HBM3E bandwidth (fill/copy/check) and the address-in-data walk over free VRAM; per-CU
+// bf16 MFMA check and throughput; the MX fp8/fp4 block-scaled matrix-core check and
+// throughput; the ABFT-checked GEMMs (one-wave mfma_gemm, the LDS-tiled gemm_soak and the
+// 8-phase gemm_pingpong soak kernel); the burn-in loop (bf16/fp8/fp4 throughput kernels
+// back to back) and pinned host<->device copies for PCIe.
 //
 // Design notes (CDNA4, see /opt/skills/guides):
 //  * HBM phases are pure streams: 16 B per lane (global_load/store_dwordx4), 256-thread
