@@ -19,12 +19,17 @@ def _ensure_built():
     if rank == 0:
         from bacchus_gpu_controller_amd.utils.build import ensure_built
 
-        import contextlib
-        import io
-
-        buf = io.StringIO()
-        with contextlib.redirect_stdout(buf):
+        # stdout carries exactly one JSON line: build chatter (ninja/hipcc are child
+        # processes writing to fd 1) goes to stderr
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
             ensure_built()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     else:
         import time
 
