@@ -16,6 +16,9 @@ These are the only compute kernels in the framework: the reference controller ha
   (256x256 tiles) for ``launches`` launches, every result checksummed
 * ``gemm_tiled(a, bt)`` — the soak's kernel on caller operands (A: MxK, Bt: NxK bf16),
   fp32 result; used to check the kernel against a PyTorch fp32 product
+* ``mx_gemm(a, sa, bt, sbt, fmt)`` — the MX block-scaled matrix-core path on caller
+  codes (fp8 e4m3 bytes or packed fp4 e2m1) and E8M0 scales; used to check the hardware's
+  operand/scale layout against an independent PyTorch decode
 * ``pcie(device)``      — host<->device copy bandwidth, pinned
 * ``device_bdf(device)``— the HIP device's PCI address, to match it to amdsmi / kubelet
 
@@ -96,4 +99,19 @@ def gemm_tiled(a, bt, device=0):
     if k != k2:
         raise ValueError(f"inner dimensions differ: A is {m}x{k}, Bt is {n}x{k2}")
     c = native().diag_gemm_tiled(device, m, n, k, _bf16_bytes(a), _bf16_bytes(bt))
+    return np.frombuffer(c, dtype=np.float32).reshape(m, n)
+
+
+def mx_gemm(a, a_scales, bt, bt_scales, fmt="fp8", device=0):
+    """C = sum_k a[m,k] 2^(sa[m,k/32]-127) * bt[n,k] 2^(sbt[n,k/32]-127) on the MX matrix
+    cores (v_mfma_scale_f32_16x16x128_f8f6f4).  fp8: `a` M x K and `bt` N x K uint8 e4m3
+    codes; fp4: M x K/2 and N x K/2 bytes of packed e2m1 codes (element 2i in the low
+    nibble).  Scales: uint8 E8M0, M x K/32 and N x K/32.  M, N multiples of 16, K of 128.
+    Returns an fp32 numpy array M x N."""
+    code = {"fp8": 0, "fp4": 4}[fmt]
+    a, bt = np.ascontiguousarray(a, dtype=np.uint8), np.ascontiguousarray(bt, dtype=np.uint8)
+    sa, sb = np.ascontiguousarray(a_scales, dtype=np.uint8), np.ascontiguousarray(bt_scales, dtype=np.uint8)
+    m, n = a.shape[0], bt.shape[0]
+    k = sa.shape[1] * 32
+    c = native().diag_mx_gemm(device, code, m, n, k, a.tobytes(), sa.tobytes(), bt.tobytes(), sb.tobytes())
     return np.frombuffer(c, dtype=np.float32).reshape(m, n)

@@ -52,13 +52,15 @@ Diag::Diag(const std::string& path) : path_(path) {
   soak_ = reinterpret_cast<int (*)(int, int, int, int, int, uint32_t, bgc_soak_result*)>(dlsym(lib_, "bgc_diag_gemm_soak"));
   tiled_ = reinterpret_cast<int (*)(int, int, int, int, const uint16_t*, const uint16_t*, float*)>(
       dlsym(lib_, "bgc_diag_gemm_tiled"));
+  mx_gemm_ = reinterpret_cast<int (*)(int, int, int, int, int, const uint8_t*, const uint8_t*, const uint8_t*,
+                                      const uint8_t*, float*)>(dlsym(lib_, "bgc_diag_mx_gemm"));
   walk_ = reinterpret_cast<int (*)(int, double, uint64_t, int, uint32_t, bgc_hbm_walk_result*)>(
       dlsym(lib_, "bgc_diag_hbm_walk"));
   bdf_ = reinterpret_cast<int (*)(int, char*, size_t)>(dlsym(lib_, "bgc_diag_device_bdf"));
   last_error_ = reinterpret_cast<const char* (*)()>(dlsym(lib_, "bgc_diag_last_error"));
   auto abi = reinterpret_cast<int (*)()>(dlsym(lib_, "bgc_diag_abi_version"));
   if (!device_count_ || !hbm_ || !mfma_ || !lowp_ || !arch_ || !gemm_ || !burn_ || !pcie_ || !soak_ || !tiled_ ||
-      !walk_ || !bdf_ || !last_error_ || !abi ||
+      !mx_gemm_ || !walk_ || !bdf_ || !last_error_ || !abi ||
       abi() != BGC_DIAG_ABI_VERSION) {
     throw std::runtime_error(path + " is not a compatible bgc diag library");
   }
@@ -208,6 +210,13 @@ void Diag::gemm(int device, int m, int n, int k, const uint16_t* a, const uint16
 
 void Diag::gemm_tiled(int device, int m, int n, int k, const uint16_t* a, const uint16_t* bt, float* c) {
   if (tiled_(device, m, n, k, a, bt, c) != 0) throw std::runtime_error(std::string("tiled gemm: ") + last_error_());
+}
+
+void Diag::mx_gemm(int device, int fmt, int m, int n, int k, const uint8_t* a, const uint8_t* a_scales,
+                   const uint8_t* bt, const uint8_t* bt_scales, float* c) {
+  if (mx_gemm_(device, fmt, m, n, k, a, a_scales, bt, bt_scales, c) != 0) {
+    throw std::runtime_error(std::string("mx gemm: ") + last_error_());
+  }
 }
 
 json::Value Diag::hbm_walk(int device, double fraction, uint64_t chunk_bytes, int budget_ms, uint32_t seed) {

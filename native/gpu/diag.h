@@ -84,6 +84,9 @@ class Diag {
   void gemm(int device, int m, int n, int k, const uint16_t* a, const uint16_t* b, float* c);
   // The soak's LDS-tiled GEMM on caller operands (Bt = B transposed, [n][k]).
   void gemm_tiled(int device, int m, int n, int k, const uint16_t* a, const uint16_t* bt, float* c);
+  // MX fp8 (fmt 0) / fp4 (fmt 4) block-scaled GEMM on caller codes and E8M0 scales
+  void mx_gemm(int device, int fmt, int m, int n, int k, const uint8_t* a, const uint8_t* a_scales, const uint8_t* bt,
+               const uint8_t* bt_scales, float* c);
   // Address-pattern walk of `fraction` of the free VRAM (see bgc_diag_hbm_walk).
   json::Value hbm_walk(int device, double fraction, uint64_t chunk_bytes, int budget_ms, uint32_t seed);
   // PCI bus id of a HIP device, lower-case ("0000:05:00.0").
@@ -104,6 +107,8 @@ class Diag {
   int (*pcie_)(int, uint64_t, int, uint32_t, bgc_pcie_result*) = nullptr;
   int (*soak_)(int, int, int, int, int, uint32_t, bgc_soak_result*) = nullptr;
   int (*tiled_)(int, int, int, int, const uint16_t*, const uint16_t*, float*) = nullptr;
+  int (*mx_gemm_)(int, int, int, int, int, const uint8_t*, const uint8_t*, const uint8_t*, const uint8_t*,
+                  float*) = nullptr;
   int (*walk_)(int, double, uint64_t, int, uint32_t, bgc_hbm_walk_result*) = nullptr;
   int (*bdf_)(int, char*, size_t) = nullptr;
   const char* (*last_error_)() = nullptr;

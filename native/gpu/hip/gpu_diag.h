@@ -15,7 +15,7 @@
 extern "C" {
 #endif
 
-#define BGC_DIAG_ABI_VERSION 10
+#define BGC_DIAG_ABI_VERSION 11
 #define BGC_DIAG_MAX_CU_KEYS 2048
 
 typedef struct {
@@ -125,6 +125,14 @@ int bgc_diag_gemm_soak(int device, int m, int n, int k, int launches, uint32_t s
 // rules as bgc_diag_gemm_soak.  Lets a test compare the LDS-tiled kernel on random data
 // with an independent fp32 product.
 int bgc_diag_gemm_tiled(int device, int m, int n, int k, const uint16_t* a_bf16, const uint16_t* bt_bf16, float* c);
+// The MX block-scaled matrix-core path (v_mfma_scale_f32_16x16x128_f8f6f4) on caller
+// operands: C[m,n] (fp32) = sum_k a(m,k) 2^(sa(m,k/32)-127) * bt(n,k) 2^(sb(n,k/32)-127).
+// fmt 0: fp8 e4m3 (OCP), one byte per element; fmt 4: fp4 e2m1, two per byte (element 2i in
+// the low nibble).  a is m x k, bt is n x k (row-major, K-contiguous), the E8M0 scales are
+// m x k/32 and n x k/32 bytes.  m, n multiples of 16; k a multiple of 128.  Lets a test
+// check the hardware's operand and scale layout against an independent decode.
+int bgc_diag_mx_gemm(int device, int fmt, int m, int n, int k, const uint8_t* a, const uint8_t* a_scales,
+                     const uint8_t* bt, const uint8_t* bt_scales, float* c);
 
 typedef struct {
   uint64_t free_bytes;        // hipMemGetInfo before the walk

@@ -419,6 +419,49 @@ __global__ __launch_bounds__(kBlock) void mfma_lowp_throughput(uint32_t seed, in
   if (lane == 0 && bad) atomicAdd(fails, bad);
 }
 
+// MX GEMM on caller operands, for the host cross-check of the block-scaled path against an
+// independent decode (PyTorch): C[m, n] = sum_k a(m, k) 2^(sa(m, k/32) - 127) *
+// b(n, k) 2^(sb(n, k/32) - 127).  A is M x K codes (fp8: one byte each; fp4: two per byte,
+// element 2i in the low nibble), Bt is N x K alike, the E8M0 scales are M x K/32 and
+// N x K/32 bytes.  One wave per 16x16 output tile, K consumed 128 at a time; each lane loads
+// its operands straight from memory in the MFMA's own layout (lowp_block above): fp8 lane
+// group g holds K 16g..16g+15 then 64+16g..64+16g+15, fp4 lane group g holds K 32g..32g+31.
+template <int kFmt>
+__device__ __forceinline__ i32x8 lowp_load(const uint8_t* __restrict__ X, int row, int K, int k0, int g) {
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  i32x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (kFmt == 0) {
+    const uint8_t* p = X + static_cast<size_t>(row) * K + k0 + 16 * g;
+    const i32x4 lo = *reinterpret_cast<const i32x4*>(p);
+    const i32x4 hi = *reinterpret_cast<const i32x4*>(p + 64);
+    v = i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  } else {
+    const i32x4 q = *reinterpret_cast<const i32x4*>(X + static_cast<size_t>(row) * (K / 2) + (k0 + 32 * g) / 2);
+    v = i32x8{q[0], q[1], q[2], q[3], 0, 0, 0, 0};
+  }
+  return v;
+}
+
+template <int kFmt>
+__global__ __launch_bounds__(64) void mx_gemm(const uint8_t* __restrict__ A, const uint8_t* __restrict__ sA,
+                                              const uint8_t* __restrict__ Bt, const uint8_t* __restrict__ sB,
+                                              float* __restrict__ C, int M, int N, int K) {
+  const int lane = threadIdx.x, rc = lane & 15, g = lane >> 4;
+  const int tiles_n = N / 16;
+  const int m0 = (static_cast<int>(blockIdx.x) / tiles_n) * 16, n0 = (static_cast<int>(blockIdx.x) % tiles_n) * 16;
+  const int kb = K / 32;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < K; k0 += 128) {
+    const i32x8 a = lowp_load<kFmt>(A, m0 + rc, K, k0, g);
+    const i32x8 b = lowp_load<kFmt>(Bt, n0 + rc, K, k0, g);
+    const int sa = sA[static_cast<size_t>(m0 + rc) * kb + k0 / 32 + g];  // this lane's (row, block g) scale
+    const int sb = sB[static_cast<size_t>(n0 + rc) * kb + k0 / 32 + g];
+    acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, acc, kFmt, kFmt, 0, sa, 0, sb);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) C[static_cast<size_t>(m0 + 4 * g + i) * N + n0 + rc] = acc[i];
+}
+
 // Plain MFMA GEMM for the host cross-check: C[M,N] (fp32) = A[M,K] * B[K,N] (bf16,
 // row-major).  One wave per 16x16 output tile, K consumed 32 at a time by
 // v_mfma_f32_16x16x32_bf16 with the same operand layout as the tests above: lane l
@@ -1426,6 +1469,44 @@ int bgc_diag_gemm_tiled(int device, int m, int n, int k, const uint16_t* a_bf16,
   HIP_TRY(hipMemcpy(db.p, bt_bf16, nb * 2, hipMemcpyHostToDevice));
   HIP_TRY(hipMemset(dc.p, 0xFF, nc * 4));  // NaN: an element the kernel never writes cannot pass
   launch_soak_gemm(soak_big_tile(m, n), da.p, db.p, dc.p, m, n, k, nullptr);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpy(c, dc.p, nc * 4, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int bgc_diag_mx_gemm(int device, int fmt, int m, int n, int k, const uint8_t* a, const uint8_t* a_scales,
+                     const uint8_t* bt, const uint8_t* bt_scales, float* c) {
+  if (!a || !a_scales || !bt || !bt_scales || !c || (fmt != 0 && fmt != 4) || m <= 0 || n <= 0 || k <= 0 ||
+      m % 16 || n % 16 || k % 128 || m > 16384 || n > 16384 || k > 65536) {
+    g_last_error = "invalid arguments: fmt 0 (fp8 e4m3) or 4 (fp4 e2m1); m, n multiples of 16 (<= 16384), k of 128 (<= 65536)";
+    return 1;
+  }
+  HIP_TRY(hipSetDevice(device));
+  const size_t code_bytes_a = fmt == 0 ? static_cast<size_t>(m) * k : static_cast<size_t>(m) * k / 2;
+  const size_t code_bytes_b = fmt == 0 ? static_cast<size_t>(n) * k : static_cast<size_t>(n) * k / 2;
+  const size_t sa_bytes = static_cast<size_t>(m) * (k / 32), sb_bytes = static_cast<size_t>(n) * (k / 32);
+  const size_t nc = static_cast<size_t>(m) * n;
+  DeviceBuffer da, dsa, db, dsb, dc;
+  HIP_TRY(hipMalloc(&da.p, code_bytes_a));
+  HIP_TRY(hipMalloc(&dsa.p, sa_bytes));
+  HIP_TRY(hipMalloc(&db.p, code_bytes_b));
+  HIP_TRY(hipMalloc(&dsb.p, sb_bytes));
+  HIP_TRY(hipMalloc(&dc.p, nc * 4));
+  HIP_TRY(hipMemcpy(da.p, a, code_bytes_a, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dsa.p, a_scales, sa_bytes, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(db.p, bt, code_bytes_b, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dsb.p, bt_scales, sb_bytes, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemset(dc.p, 0xFF, nc * 4));  // NaN: an element the kernel never writes cannot pass
+  const dim3 grid(static_cast<unsigned>((m / 16) * (n / 16)));
+  const auto* pa = static_cast<const uint8_t*>(da.p);
+  const auto* psa = static_cast<const uint8_t*>(dsa.p);
+  const auto* pb = static_cast<const uint8_t*>(db.p);
+  const auto* psb = static_cast<const uint8_t*>(dsb.p);
+  if (fmt == 0) {
+    hipLaunchKernelGGL(mx_gemm<0>, grid, dim3(64), 0, nullptr, pa, psa, pb, psb, static_cast<float*>(dc.p), m, n, k);
+  } else {
+    hipLaunchKernelGGL(mx_gemm<4>, grid, dim3(64), 0, nullptr, pa, psa, pb, psb, static_cast<float*>(dc.p), m, n, k);
+  }
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpy(c, dc.p, nc * 4, hipMemcpyDeviceToHost));
   return 0;

@@ -218,6 +218,24 @@ void register_gpu(py::module_& m) {
     }
     return py::bytes(c);
   }, py::arg("device"), py::arg("m"), py::arg("n"), py::arg("k"), py::arg("a_bf16"), py::arg("bt_bf16"));
+  m.def("diag_mx_gemm", [](int device, int fmt, int mm, int nn, int kk, const std::string& a, const std::string& sa,
+                           const std::string& bt, const std::string& sb) {
+    const size_t per = fmt == 0 ? static_cast<size_t>(kk) : static_cast<size_t>(kk) / 2;
+    if ((fmt != 0 && fmt != 4) || kk % 128 || a.size() != static_cast<size_t>(mm) * per ||
+        bt.size() != static_cast<size_t>(nn) * per || sa.size() != static_cast<size_t>(mm) * (kk / 32) ||
+        sb.size() != static_cast<size_t>(nn) * (kk / 32)) {
+      throw std::invalid_argument("fmt 0: A M*K, Bt N*K bytes; fmt 4: M*K/2, N*K/2; scales M*K/32 and N*K/32 bytes");
+    }
+    std::string c(static_cast<size_t>(mm) * nn * 4, '\0');
+    {
+      py::gil_scoped_release nogil;
+      auto u8 = [](const std::string& x) { return reinterpret_cast<const uint8_t*>(x.data()); };
+      bgc::gpu::Diag::instance().mx_gemm(device, fmt, mm, nn, kk, u8(a), u8(sa), u8(bt), u8(sb),
+                                         reinterpret_cast<float*>(c.data()));
+    }
+    return py::bytes(c);
+  }, py::arg("device"), py::arg("fmt"), py::arg("m"), py::arg("n"), py::arg("k"), py::arg("a"), py::arg("a_scales"),
+     py::arg("bt"), py::arg("bt_scales"));
   m.def("diag_hbm_walk", [](int device, double fraction, unsigned long long chunk_bytes, int budget_ms, unsigned seed) {
     Value v;
     {

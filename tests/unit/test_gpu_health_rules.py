@@ -311,3 +311,24 @@ def test_judge_diag_gemm_soak(nat):
     assert r["failures"] == ["GEMM soak checksums wrong: 1 rows, 1 columns"]
     r = json.loads(nat.judge_diag(json.dumps({"soak": dict(ok, tflops_mean=600.0)})))
     assert r["failures"] == ["GEMM soak TFLOP/s 600 below floor 950"]
+
+
+def test_mx_gemm_binding_checks_operand_sizes(nat):
+    """diag_mx_gemm rejects mismatched code/scale buffers before it touches the library or
+    a GPU (fp8: one byte per element, fp4: two per byte; scales one byte per 32 K)."""
+    m, n, k = 16, 32, 128
+    ok = dict(a=b"\0" * (m * k), a_scales=b"\x7f" * (m * k // 32), bt=b"\0" * (n * k), bt_scales=b"\x7f" * (n * k // 32))
+    bad_cases = [
+        dict(ok, a=b"\0" * (m * k - 1)),                      # fp8 A one byte short
+        dict(ok, bt_scales=b"\x7f" * (n * k // 32 + 1)),      # scale rows too long
+    ]
+    for kw in bad_cases:
+        with pytest.raises(ValueError):
+            nat.diag_mx_gemm(0, 0, m, n, k, **kw)
+    with pytest.raises(ValueError):  # fp4 wants packed nibbles: half the fp8 size
+        nat.diag_mx_gemm(0, 4, m, n, k, **ok)
+    with pytest.raises(ValueError):  # K must be a multiple of 128
+        nat.diag_mx_gemm(0, 0, m, n, 96, a=b"\0" * (m * 96), a_scales=b"\x7f" * (m * 3), bt=b"\0" * (n * 96),
+                         bt_scales=b"\x7f" * (n * 3))
+    with pytest.raises(ValueError):  # only fp8 (0) and fp4 (4)
+        nat.diag_mx_gemm(0, 2, m, n, k, **ok)
