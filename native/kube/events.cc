@@ -24,7 +24,8 @@ std::string rfc3339_now() {  // Event timestamps are whole seconds (metav1.Time)
 
 }  // namespace
 
-EventRecorder::EventRecorder(KubeClient& client, EventOptions opts) : client_(client), opts_(std::move(opts)) {
+EventRecorder::EventRecorder(KubeClient& client, EventOptions opts)
+    : client_(client), opts_(std::move(opts)), limiter_(opts_.burst, opts_.refill_per_minute) {
   worker_ = std::thread([this] { run(); });
 }
 
@@ -37,37 +38,42 @@ EventRecorder::~EventRecorder() {
   if (worker_.joinable()) worker_.join();
 }
 
-bool EventRecorder::allow(const std::string& key, std::chrono::steady_clock::time_point now) {
+bool EventRateLimiter::allow(const std::string& key, std::chrono::steady_clock::time_point now) {
   auto [it, fresh] = buckets_.try_emplace(key);
   Bucket& b = it->second;
   if (fresh) {
-    b.tokens = opts_.burst;
+    b.tokens = burst_;
     b.refilled = now;
   } else {
     const double mins = std::chrono::duration<double>(now - b.refilled).count() / 60.0;
-    b.tokens = std::min(opts_.burst, b.tokens + mins * opts_.refill_per_minute);
+    b.tokens = std::min(burst_, b.tokens + mins * refill_per_minute_);
     b.refilled = now;
   }
   if (b.tokens < 1.0) return false;
   b.tokens -= 1.0;
-  if (buckets_.size() > 4096) evict(now);  // bound memory on huge clusters
+  if (buckets_.size() > max_keys_) evict(now, key);  // bound memory on huge clusters
   return true;
 }
 
 // Drops buckets that have refilled to the burst (a fresh bucket is identical, so this
 // loses nothing); if every bucket is still draining, drops the one refilled longest ago.
-void EventRecorder::evict(std::chrono::steady_clock::time_point now) {
+// `keep` (the key just charged) is never dropped.
+void EventRateLimiter::evict(std::chrono::steady_clock::time_point now, const std::string& keep) {
   auto oldest = buckets_.end();
   for (auto it = buckets_.begin(); it != buckets_.end();) {
+    if (it->first == keep) {
+      ++it;
+      continue;
+    }
     const double mins = std::chrono::duration<double>(now - it->second.refilled).count() / 60.0;
-    if (it->second.tokens + mins * opts_.refill_per_minute >= opts_.burst) {
+    if (it->second.tokens + mins * refill_per_minute_ >= burst_) {
       it = buckets_.erase(it);
       continue;
     }
     if (oldest == buckets_.end() || it->second.refilled < oldest->second.refilled) oldest = it;
     ++it;
   }
-  if (buckets_.size() > 4096 && oldest != buckets_.end()) buckets_.erase(oldest);
+  if (buckets_.size() > max_keys_ && oldest != buckets_.end()) buckets_.erase(oldest);
 }
 
 void EventRecorder::record(const ResourceType& rt, const Value& obj, const std::string& type, const std::string& reason,
@@ -88,7 +94,7 @@ void EventRecorder::record(const ResourceType& rt, const Value& obj, const std::
   const std::string object_key = rt.plural + "/" + it.ns + "/" + meta.get_string("name");
   {
     std::lock_guard<std::mutex> lk(mu_);
-    if (stop_ || q_.size() >= opts_.max_queue || !allow(object_key, it.at)) {
+    if (stop_ || q_.size() >= opts_.max_queue || !limiter_.allow(object_key, it.at)) {
       dropped_.fetch_add(1);
       dropped.inc();
       return;

@@ -36,6 +36,28 @@ struct EventOptions {
   size_t max_queue = 1024;
 };
 
+// Per-object token bucket of the recorder (client-go's EventSourceObjectSpamFilter): `burst`
+// events, refilled at `refill_per_minute`.  Past `max_keys` objects it evicts buckets that
+// have refilled to the burst (a fresh bucket is identical), else the one refilled longest
+// ago, so an object that floods events keeps its drained bucket.  Not thread-safe.
+class EventRateLimiter {
+ public:
+  EventRateLimiter(double burst, double refill_per_minute, size_t max_keys = 4096)
+      : burst_(burst), refill_per_minute_(refill_per_minute), max_keys_(max_keys) {}
+  bool allow(const std::string& object_key, std::chrono::steady_clock::time_point now);
+  size_t size() const { return buckets_.size(); }
+
+ private:
+  struct Bucket {
+    double tokens = 0;
+    std::chrono::steady_clock::time_point refilled;
+  };
+  void evict(std::chrono::steady_clock::time_point now, const std::string& keep);
+  double burst_, refill_per_minute_;
+  size_t max_keys_;
+  std::map<std::string, Bucket> buckets_;
+};
+
 class EventRecorder {
  public:
   EventRecorder(KubeClient& client, EventOptions opts);
@@ -66,14 +88,8 @@ class EventRecorder {
     std::string first;  // firstTimestamp
     std::chrono::steady_clock::time_point last;
   };
-  struct Bucket {
-    double tokens = 0;
-    std::chrono::steady_clock::time_point refilled;
-  };
   void run();
   void write(const Item& it);
-  bool allow(const std::string& object_key, std::chrono::steady_clock::time_point now);
-  void evict(std::chrono::steady_clock::time_point now);
 
   KubeClient& client_;
   EventOptions opts_;
@@ -84,7 +100,7 @@ class EventRecorder {
   bool busy_ = false;
   bool stop_ = false;
   std::map<std::string, Seen> seen_;      // correlation key -> existing Event (worker only)
-  std::map<std::string, Bucket> buckets_; // object key -> tokens (under mu_)
+  EventRateLimiter limiter_;              // object key -> tokens (under mu_)
   std::atomic<uint64_t> created_{0}, aggregated_{0}, dropped_{0};
   std::thread worker_;
 };

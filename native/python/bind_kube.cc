@@ -6,6 +6,7 @@
 
 #include "apiserver/server.h"
 #include "bench/churn.h"
+#include "kube/events.h"
 #include "kube/ratelimit.h"
 #include "kube/runtime.h"
 
@@ -73,6 +74,16 @@ void register_kube(py::module_& m) {
       .def("when", [](bgc::kube::RetryLimiter& r, const std::string& k) { return r.when(k).count(); })
       .def("forget", &bgc::kube::RetryLimiter::forget)
       .def("failures", &bgc::kube::RetryLimiter::failures);
+  // Event recorder's per-object token bucket; `at_s` is a synthetic clock in seconds
+  py::class_<bgc::kube::EventRateLimiter>(m, "EventRateLimiter")
+      .def(py::init<double, double, size_t>(), py::arg("burst") = 10.0, py::arg("refill_per_minute") = 6.0,
+           py::arg("max_keys") = 4096)
+      .def("allow", [](bgc::kube::EventRateLimiter& l, const std::string& key, double at_s) {
+        return l.allow(key, std::chrono::steady_clock::time_point(
+                                std::chrono::duration_cast<std::chrono::steady_clock::duration>(
+                                    std::chrono::duration<double>(at_s))));
+      })
+      .def("size", &bgc::kube::EventRateLimiter::size);
   py::class_<bgc::kube::WorkQueue>(m, "WorkQueue")
       .def(py::init<>())
       .def("add", [](bgc::kube::WorkQueue& q, const std::string& k) { q.add(k); })

@@ -311,3 +311,31 @@ def test_retry_limiter_exponential_cap_and_bucket(nat):
     b = nat.RetryLimiter(1, 1, 10.0, 2)
     d = [b.when(f"k{i}") for i in range(4)]
     assert d[:2] == [1, 1] and 90 <= d[2] <= 101 and 190 <= d[3] <= 201
+
+
+def test_event_rate_limiter_keeps_a_flooding_objects_bucket(nat):
+    """The recorder's per-object bucket (client-go EventSourceObjectSpamFilter): `burst`
+    events, then refill_per_minute.  Past max_keys objects, buckets that refilled to the
+    burst are dropped first (identical to a fresh one), else the longest-idle one, and never
+    the object just charged, so an object flooding events stays limited however many other
+    objects come and go (eviction used to drop the lexicographically first key)."""
+    lim = nat.EventRateLimiter(burst=3, refill_per_minute=6, max_keys=4)
+    t = 0.0
+    # "a-flood" sorts first: the old eviction (buckets_.begin()) would have reset it
+    assert [lim.allow("a-flood", t) for _ in range(5)] == [True, True, True, False, False]
+    for i in range(50):  # many one-off objects over 5 s, each charged once
+        t += 0.1
+        assert lim.allow(f"obj-{i:03d}", t)
+        assert lim.size() <= 5
+        assert not lim.allow("a-flood", t)  # 5 s at 6/min refills half a token: still drained
+    # 5.5 s more completes one token (denied events cost nothing) -> exactly one more event
+    t += 5.5
+    assert lim.allow("a-flood", t)
+    assert not lim.allow("a-flood", t)
+    # a bucket that refilled to the burst is evicted before a draining one
+    lim2 = nat.EventRateLimiter(burst=2, refill_per_minute=60, max_keys=2)
+    assert lim2.allow("idle", 0.0)
+    assert lim2.allow("busy", 10.0) and lim2.allow("busy", 10.0)  # drained at t=10
+    assert lim2.allow("new", 10.5)  # 3 keys > 2: "idle" refilled (60/min) -> evicted
+    assert lim2.size() == 2
+    assert not lim2.allow("busy", 10.5)  # "busy" kept its drained bucket
