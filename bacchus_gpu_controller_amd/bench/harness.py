@@ -150,16 +150,60 @@ def _names(rank, phase, step, batch):
     return [f"r{rank}-{phase}{step}-u{i}" for i in range(batch)]
 
 
-def _samples(url, verify=None):
+class TruncatedWindow(RuntimeError):
+    """A latency window lost samples: no percentile may be reported over it."""
+
+
+def _get_json(url, method="GET", verify=None):
+    """GET/DELETE a /debug/samples/<name> document; None when the process has no such log."""
     import requests
 
-    return requests.get(url, timeout=10, verify=verify).json()["samples"]
+    r = requests.request(method, url, timeout=10, verify=verify)
+    if r.status_code == 404:
+        return None
+    r.raise_for_status()
+    return r.json()
+
+
+def _samples(url, verify=None):
+    return _get_json(url, verify=verify)
 
 
 def _clear(url, verify=None):
-    import requests
+    """Starts a window: clears the log and returns its counts at that instant."""
+    return _get_json(url, method="DELETE", verify=verify)
 
-    requests.delete(url, timeout=10, verify=verify)
+
+def linked_delta(doc, start):
+    """Increments of the log's linked counters (e.g. bgc_reconcile_total) over the window.
+    They are counted inside the log's lock together with each sample (SampleLog::add), so
+    for a complete window this equals the number of samples exactly."""
+    if not doc or not doc.get("linked"):
+        return None
+    base = (start or {}).get("linked", {})
+    return int(round(sum(v - base.get(k, 0.0) for k, v in doc["linked"].items())))
+
+
+def window_samples(doc, start=None, required=True):
+    """The samples of one measurement window, checked complete.
+
+    `doc` is GET /debug/samples/<name> at the end of the window, `start` the DELETE response
+    at its start.  Raises TruncatedWindow when the log dropped samples (capacity reached or
+    recording off) or when its linked counters moved by other than the number of samples,
+    so a truncated window can never turn into a reported percentile."""
+    if doc is None:
+        if required:
+            raise TruncatedWindow("sample log missing (is CONF_DEBUG_ENDPOINTS on?)")
+        return []
+    name, samples = doc.get("name"), doc["samples"]
+    if doc.get("dropped", 0) or len(samples) != doc["total"]:
+        raise TruncatedWindow(f"{name}: {len(samples)} of {doc['total']} samples kept (capacity "
+                              f"{doc.get('capacity')}, dropped {doc.get('dropped')}): refusing a percentile "
+                              "over a truncated window")
+    delta = linked_delta(doc, start)
+    if delta is not None and start is not None and delta != len(samples):
+        raise TruncatedWindow(f"{name}: {len(samples)} samples but linked counters moved by {delta}")
+    return samples
 
 
 def _lock_report(l0, l1, elapsed):
@@ -202,9 +246,20 @@ def _cpu_snapshot(cluster):
     return {name: _cpu_seconds(p.p.pid) for name, p in cluster.procs.items()}
 
 
-def _phase(d, nat, info, args, phase, concurrency, total_steps, cluster):
-    """One measured phase: W warmup + K timed steps at `concurrency` creates in flight per
-    rank.  Returns the per-phase record on rank 0 (None elsewhere)."""
+def _sample_logs(info):
+    """The latency logs a phase reads: key -> (URL, TLS verify)."""
+    return {"reconcile": (info["controller"] + "/debug/samples/reconcile", None),
+            "webhook": (info["server"] + "/debug/samples/webhook", info["apiserver_verify"]),
+            "admission": (info["admission"] + "/debug/samples/admission", info["ca"]),
+            "h2_server": (info["admission"] + "/debug/samples/h2_server", info["ca"]),
+            "telemetry_poll": (info["node_agent"] + "/debug/samples/telemetry_poll", None),
+            "sync_ub": (info["synchronizer"] + "/debug/samples/sync_ub", None)}
+
+
+def _phase(d, nat, info, args, phase, concurrency, warmup, steps, cluster):
+    """One measured phase: `warmup` untimed + `steps` timed steps at `concurrency` creates in
+    flight per rank.  Returns the per-phase record on rank 0 (None elsewhere)."""
+    total_steps = warmup + steps
     from bacchus_gpu_controller_amd.testing.cluster import ADMIN_TOKEN
 
     driver = nat.ChurnDriver(info["server"], ADMIN_TOKEN, f"r{d.rank}-", concurrency,
@@ -217,6 +272,7 @@ def _phase(d, nat, info, args, phase, concurrency, total_steps, cluster):
     stage = {"ns": [], "rq": [], "rb": []}
     ready = failed = timeouts = 0
     lock0 = cpu0 = None
+    starts = {}
     t_start = None
     errors = []
     last_note = time.perf_counter()
@@ -226,16 +282,11 @@ def _phase(d, nat, info, args, phase, concurrency, total_steps, cluster):
                 # slow modes (the reference's 60 s sheet tick) must still show progress
                 print(f"[bench] phase {phase} step {s}/{total_steps}", file=sys.stderr, flush=True)
                 last_note = time.perf_counter()
-            if s == args.warmup:
+            if s == warmup:
                 d.barrier()
                 d.sync()
                 if d.rank == 0:
-                    _clear(info["controller"] + "/debug/samples/reconcile")
-                    _clear(info["server"] + "/debug/samples/webhook", verify=info["apiserver_verify"])
-                    _clear(info["admission"] + "/debug/samples/admission", verify=info["ca"])
-                    _clear(info["admission"] + "/debug/samples/h2_server", verify=info["ca"])
-                    _clear(info["node_agent"] + "/debug/samples/telemetry_poll")
-                    _clear(info["synchronizer"] + "/debug/samples/sync_ub")
+                    starts = {key: _clear(url, verify) for key, (url, verify) in _sample_logs(info).items()}
                     lock0 = _kl_lock(info)
                     cpu0 = _cpu_snapshot(cluster)
                 d.barrier()
@@ -247,7 +298,7 @@ def _phase(d, nat, info, args, phase, concurrency, total_steps, cluster):
                 names = _names(d.rank, phase, s * args.rounds + r, args.batch)
                 res = json.loads(driver.step_with_delete(names, prev or [], args.timeout))
                 prev = names
-                if s >= args.warmup:
+                if s >= warmup:
                     lat += res["ready_latency_s"]
                     clat += res["create_latency_s"]
                     ap_lat += res.get("approve_latency_s", [])
@@ -274,13 +325,13 @@ def _phase(d, nat, info, args, phase, concurrency, total_steps, cluster):
     if d.rank != 0:
         return None
     lock1 = _kl_lock(info)
-    rec = _samples(info["controller"] + "/debug/samples/reconcile")
-    hook = _samples(info["server"] + "/debug/samples/webhook", verify=info["apiserver_verify"])
-    adm = _samples(info["admission"] + "/debug/samples/admission", verify=info["ca"])
+    docs = {key: _samples(url, verify) for key, (url, verify) in _sample_logs(info).items()}
+    # every log is checked complete over the window; the headline two must exist
+    win = {key: window_samples(docs[key], starts.get(key), required=key in ("reconcile", "webhook"))
+           for key in docs}
+    rec, hook, adm = win["reconcile"], win["webhook"], win["admission"]
     # HTTP/2 webhook requests: request complete on the server's reader -> response written
-    h2s = _samples(info["admission"] + "/debug/samples/h2_server", verify=info["ca"])
-    tel = _samples(info["node_agent"] + "/debug/samples/telemetry_poll")
-    syn = _samples(info["synchronizer"] + "/debug/samples/sync_ub")
+    h2s, tel, syn = win["h2_server"], win["telemetry_poll"], win["sync_ub"]
     total_ready = sum(p["ready"] for p in per_rank)
     total_failed = sum(p["failed"] + p["timeouts"] for p in per_rank)
     flat = lambda key: [x for p in per_rank for x in p[key]]  # noqa: E731
@@ -297,10 +348,18 @@ def _phase(d, nat, info, args, phase, concurrency, total_steps, cluster):
     out = {
         "value": round(total_ready / elapsed if elapsed > 0 else 0.0, 3),
         "elapsed_s": elapsed,
+        "steps": steps,
+        "warmup": warmup,
         "concurrency_per_rank": concurrency,
         "reconcile_p99_ms": ms(_pct(rec, 0.99)),
         "reconcile_p50_ms": ms(_pct(rec, 0.50)),
+        # every reconcile of the window: len(samples) == the increase of the controller's
+        # bgc_reconcile_total (counted with each sample, under the log's lock)
         "reconciles": len(rec),
+        "reconcile_total_delta": linked_delta(docs["reconcile"], starts.get("reconcile")),
+        "webhook_calls": len(hook),
+        "webhook_calls_total_delta": linked_delta(docs["webhook"], starts.get("webhook")),
+        "samples_complete": True,
         # webhook round trip as the API server measures it (TLS + handler + response)
         "admission_p50_ms": ms(_pct(hook, 0.50)),
         "admission_p99_ms": ms(_pct(hook, 0.99)),
@@ -352,6 +411,15 @@ def _xgmi_probe(d, args):
         return {"error": f"{type(e).__name__}: {e}"}
 
 
+class _Phase:
+    """One timed phase: key (tenant-name prefix), in-flight creates per rank, API server ->
+    webhook protocol, controller semantics, kube-lite write latency, warmup and timed steps."""
+
+    def __init__(self, key, concurrency, protocol, semantics, write_latency_ms, warmup, steps):
+        self.key, self.concurrency, self.protocol, self.semantics = key, concurrency, protocol, semantics
+        self.write_latency_ms, self.warmup, self.steps = write_latency_ms, warmup, steps
+
+
 def run(args):
     d = Dist()
     n = args.gpus if args.gpus else d.world
@@ -362,39 +430,56 @@ def run(args):
     nat = native()
     cluster = google = None
     info = None
-    total_steps = args.warmup + args.steps
     cpus = effective_cpus()
     tuned = args.tuned_concurrency if args.tuned_concurrency > 0 else auto_concurrency(d.world, cpus)
     # BASELINE config #3 is 100 concurrent CRs on the node: by default that total is split
     # over the ranks (ceil), so N load generators offer the same in-flight load as one
     conc = args.concurrency if args.concurrency_scope == "rank" else max(1, -(-args.concurrency // d.world))
-    # (phase, in-flight creates per rank, API server -> webhook protocol)
-    phases = [("m", conc, args.webhook_protocol)]
+    semantics0 = "reference" if args.reference_semantics else args.semantics
+    phases = [_Phase("m", conc, args.webhook_protocol, semantics0, args.write_latency_ms, args.warmup, args.steps)]
     if args.tuned_phase and tuned != conc:
-        phases.append(("t", tuned, args.webhook_protocol))
+        phases.append(_Phase("t", tuned, args.webhook_protocol, semantics0, args.write_latency_ms,
+                             args.warmup, args.steps))
     if args.http1_phase and args.webhook_protocol == "h2":
         # secondary: the same load with the webhook called over HTTP/1.1 (keep-alive pool)
-        phases.append(("w", conc, "http/1.1"))
+        phases.append(_Phase("w", conc, "http/1.1", semantics0, args.write_latency_ms, args.warmup, args.steps))
     semantics = "reference" if args.reference_semantics else args.semantics
+    if args.reference_arms and semantics == "this":
+        # same-stack comparison, timed like the headline: the reference's controller
+        # behaviour (controller.rs:81-154: sequential, unconditional applies) on this stack,
+        # at the headline's storage latency and with a write-latency (etcd commit) model
+        phases.append(_Phase("rc", conc, args.webhook_protocol, "reference-controller", args.write_latency_ms,
+                             args.warmup, args.steps))
+        if args.arm_write_latency_ms > 0:
+            phases.append(_Phase("rl", conc, args.webhook_protocol, "reference-controller",
+                                 args.arm_write_latency_ms, args.arm_warmup, args.arm_steps))
+            phases.append(_Phase("ml", conc, args.webhook_protocol, "this", args.arm_write_latency_ms,
+                                 args.arm_warmup, args.arm_steps))
     # Reconcile/sync workers spend most of their time waiting on API round trips, so they
     # are not sized to the CPU share like the offered load is (16 = the binaries' default).
     controller_workers = args.controller_workers or 16
     sync_workers = args.sync_workers or 16
+
+    def controller_env(sem):
+        env = {"CONF_WORKERS": str(controller_workers)}
+        env.update(dict(kv.split("=", 1) for kv in args.controller_env))
+        if sem in ("reference", "reference-controller"):
+            # the reference's controller on this same stack: children applied one after
+            # another and re-applied on every reconcile (controller.rs:81-149)
+            env.update({"CONF_SKIP_UNCHANGED": "false", "CONF_PARALLEL_CHILDREN": "false",
+                        "CONF_LABEL_CHILDREN": "false"})  # .owns() on every object of each kind
+        return env
+
     if d.rank == 0:
         google = FakeGoogle().start()
         if not args.approve_after_create:
             # pre-approved sheet: every tenant's row is marked O before it applies
-            google.set_rows([{"id_username": name} for r in range(d.world) for ph, _, _ in phases
-                             for s in range(total_steps * args.rounds) for name in _names(r, ph, s, args.batch)])
-        ctrl_env = {"CONF_WORKERS": str(controller_workers)}
-        ctrl_env.update(dict(kv.split("=", 1) for kv in args.controller_env))
+            google.set_rows([{"id_username": name} for r in range(d.world) for p in phases
+                             for s in range((p.warmup + p.steps) * args.rounds)
+                             for name in _names(r, p.key, s, args.batch)])
+        ctrl_env = controller_env(semantics)
         sync_env = {"CONF_WATCH": "true", "CONF_WORKERS": str(sync_workers), "RUST_LOG": args.log_level,
                     "CONF_SHEET_POLL_MS": str(args.sheet_poll_ms)}
-        if semantics in ("reference", "reference-controller"):
-            # the reference's controller on this same stack: children applied one after
-            # another and re-applied on every reconcile (controller.rs:81-149)
-            ctrl_env.update({"CONF_SKIP_UNCHANGED": "false", "CONF_PARALLEL_CHILDREN": "false",
-                             "CONF_LABEL_CHILDREN": "false"})  # .owns() on every object of each kind
         if semantics == "reference":
             # ... and its synchronizer: sheet read only on the periodic tick
             # (synchronizer.rs:192), every tick rewrites every matched tenant
@@ -404,8 +489,6 @@ def run(args):
             # what a real apiserver negotiates with the admission server (ALPN h2, one
             # multiplexed connection): the production webhook transport
             apiserver_args.append("--webhook-http2")
-        if args.write_latency_ms > 0:
-            apiserver_args += ["--write-latency-ms", str(args.write_latency_ms)]
         cluster = Cluster(controller_env=ctrl_env, log_level=args.log_level, tls_apiserver=args.tls_apiserver,
                           apiserver_args=apiserver_args,
                           admission_env=dict(kv.split("=", 1) for kv in args.admission_env))
@@ -424,20 +507,36 @@ def run(args):
     info = d.broadcast_obj(info)
     try:
         results = {}
-        for ph, pconc, proto in phases:
+        running = semantics  # controller semantics of the running controller
+        for p in phases:
             if d.rank == 0:
                 import requests
 
-                requests.post(info["server"] + "/_kl/webhook-protocol", data=proto, timeout=10,
+                requests.post(info["server"] + "/_kl/webhook-protocol", data=p.protocol, timeout=10,
                               verify=info["apiserver_verify"]).raise_for_status()
+                requests.post(info["server"] + "/_kl/write-latency-us", data=str(int(p.write_latency_ms * 1000)),
+                              timeout=10, verify=info["apiserver_verify"]).raise_for_status()
+                if controller_env(p.semantics) != controller_env(running):
+                    # the other controller behaviour: a fresh controller process, which
+                    # re-lists every object like any controller start
+                    cluster.procs["controller"].stop()
+                    cluster.controller_env = controller_env(p.semantics)
+                    cluster.start_controller()
+                    info["controller"] = f"http://127.0.0.1:{cluster.controller_port}"
+                    running = p.semantics
             d.barrier()
-            results[ph] = _phase(d, nat, info, args, ph, pconc, total_steps, cluster)
+            results[p.key] = _phase(d, nat, info, args, p.key, p.concurrency, p.warmup, p.steps, cluster)
+            if results[p.key] is not None:
+                results[p.key]["semantics"] = p.semantics
+                results[p.key]["apiserver_write_latency_ms"] = p.write_latency_ms
         xgmi = _xgmi_probe(d, args)
         if d.rank != 0:
             return None
         main_r = results["m"]
         gpu_tel = _gpu_telemetry(info["node_agent"])
         elapsed = main_r.pop("elapsed_s")
+        for k in ("steps", "warmup", "semantics", "apiserver_write_latency_ms"):
+            main_r.pop(k, None)  # in the top-level fields and config already
         model = ("UserBootstrap onboarding churn (kube-lite" + (" over HTTPS" if args.tls_apiserver else "")
                  + " + TLS admission + controller + synchronizer + MI355X node-agent)")
         flow = "create->approve->Ready" if args.approve_after_create else "pre-approved sheet"
@@ -483,6 +582,23 @@ def run(args):
             out["webhook_http1"] = {k: w.get(k) for k in ("value", "admission_p50_ms", "admission_p99_ms",
                                                           "admission_handler_p50_ms", "reconcile_p99_ms",
                                                           "apply_to_ready_p50_ms", "failed_crs")}
+        arm_keys = ("value", "steps", "warmup", "semantics", "apiserver_write_latency_ms", "reconcile_p99_ms",
+                    "reconcile_p50_ms", "reconciles", "reconcile_total_delta", "admission_p50_ms",
+                    "apply_to_ready_p50_ms", "apply_to_ready_p99_ms", "apiserver_requests_per_cr", "cpu_ms_per_cr",
+                    "ready_crs", "failed_crs")
+        arm = lambda r: {k: r.get(k) for k in arm_keys}  # noqa: E731
+        ratio = lambda a, b: round(a / b, 3) if a and b else None  # noqa: E731
+        if "rc" in results:
+            # same stack, the reference's controller behaviour (an emulation, not a published
+            # number: vs_baseline stays null)
+            rc = arm(results["rc"])
+            rc["this_over_reference_cr_per_s"] = ratio(out["value"], rc["value"])
+            out["reference_controller"] = rc
+        if "rl" in results and "ml" in results:
+            this_l, ref_l = arm(results["ml"]), arm(results["rl"])
+            out[f"write_latency_{args.arm_write_latency_ms:g}ms"] = {
+                "this": this_l, "reference_controller": ref_l,
+                "this_over_reference_cr_per_s": ratio(this_l["value"], ref_l["value"])}
         # amdsmi counters of the advertised GPUs at the end of the timed region (node agent)
         out["gpu_telemetry"] = gpu_tel
         if xgmi is not None:
@@ -555,6 +671,13 @@ def main(argv=None):
                          "(periodic sheet sync only, sequential unconditional child applies); "
                          "reference-controller: only the controller side")
     ap.add_argument("--reference-semantics", action="store_true", help="alias for --semantics reference")
+    ap.add_argument("--reference-arms", action=argparse.BooleanOptionalAction, default=True,
+                    help="also time the reference's controller behaviour on this stack (reference_controller) "
+                         "and both controllers at --arm-write-latency-ms (secondary fields)")
+    ap.add_argument("--arm-write-latency-ms", type=float, default=2.0,
+                    help="kube-lite storage commit latency of the write-latency arms (0 = no such arms)")
+    ap.add_argument("--arm-steps", type=int, default=6, help="timed steps of each write-latency arm")
+    ap.add_argument("--arm-warmup", type=int, default=2, help="warmup steps of each write-latency arm")
     ap.add_argument("--approve-after-create", action="store_true",
                     help="tenants apply first; each step's batch is approved by one sheet edit once its "
                          "Namespaces exist (the reference's onboarding order); times create->approve->Ready")

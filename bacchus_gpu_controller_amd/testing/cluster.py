@@ -55,6 +55,9 @@ class Proc:
         self.log = open(self.log_path, "wb")
         full_env = dict(os.environ)
         full_env.setdefault("GLIBC_TUNABLES", SERVICE_GLIBC_TUNABLES)
+        # tests and the bench read exact latency samples (/debug/samples/<name>); the
+        # binaries and the chart leave them off
+        full_env.setdefault("CONF_DEBUG_ENDPOINTS", "true")
         full_env.update(env)
         self.p = subprocess.Popen(cmd, env=full_env, stdout=self.log, stderr=subprocess.STDOUT,
                                   start_new_session=True)

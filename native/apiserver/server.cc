@@ -595,6 +595,9 @@ struct ApiServer::Impl {
   // webhook transport for new clients (--webhook-http2; switchable at run time through
   // POST /_kl/webhook-protocol so one bench run can time both)
   std::atomic<bool> webhook_h2{false};
+  // storage commit latency (Options::write_latency_us), switchable at run time through
+  // POST /_kl/write-latency-us so one bench run can time several etcd models
+  std::atomic<int64_t> write_latency_us{0};
 
   std::atomic<uint64_t> requests{0};
   std::atomic<uint64_t> faults_hit{0};
@@ -602,6 +605,7 @@ struct ApiServer::Impl {
 
   explicit Impl(Options o) : opts(std::move(o)) {
     webhook_h2 = opts.webhook_http2;
+    write_latency_us = opts.write_latency_us;
     for (const ResourceType* rt : kube::types::builtin()) {
       TypeInfo ti;
       ti.rt = *rt;
@@ -915,8 +919,13 @@ struct ApiServer::Impl {
                      const std::string& name, Value* obj, const Value* old, const UserInfo& user) {
     auto hooks = matching_webhooks(ti, sub, op);
     if (hooks.empty()) return;
-    static auto& ring = metrics::Registry::global().samples("webhook");
     static auto& hist = metrics::Registry::global().histogram("kl_webhook_duration_seconds", "Webhook callout latency");
+    static auto& calls = metrics::Registry::global().counter("kl_webhook_calls_total", "Webhook callouts (any outcome)");
+    static auto& ring = [] () -> metrics::SampleLog& {
+      auto& r = metrics::Registry::global().samples("webhook");
+      r.link("kl_webhook_calls_total", &calls);  // counted with the sample, under its lock
+      return r;
+    }();
     for (const auto& hm : hooks) {
       const Value& hook = *hm.hook;
       std::string fail_policy = hook.get_string("failurePolicy", "Fail");
@@ -970,8 +979,8 @@ struct ApiServer::Impl {
         err = e.what();
       }
       double secs = static_cast<double>(metrics::now_ns() - t0) * 1e-9;
-      ring.add(secs);
       hist.observe(secs);
+      ring.add(secs, &calls);
       const Value& resp = resp_review.get("response");
       if (err.empty() && !resp.is_object()) err = "webhook response was absent";
       if (err.empty() && resp.get_string("uid") != uid) {
@@ -2118,6 +2127,20 @@ struct ApiServer::Impl {
       w.send_json(200, "{}");
       return;
     }
+    if (req.path == "/_kl/write-latency-us" && req.method == "POST") {
+      // body: microseconds of storage commit latency for later writes
+      try {
+        size_t used = 0;
+        const long long us = std::stoll(req.body, &used);
+        if (us < 0 || us > 10000000) throw std::out_of_range("write latency");
+        write_latency_us = us;
+      } catch (const std::exception&) {
+        w.send(400, "body must be 0..10000000 microseconds\n");
+        return;
+      }
+      w.send(200, std::to_string(write_latency_us.load()) + "\n");
+      return;
+    }
     if (req.path == "/_kl/webhook-protocol" && req.method == "POST") {
       // body "h2" or "http/1.1": later webhook calls use fresh clients of that protocol
       const bool h2 = req.body == "h2";
@@ -2252,8 +2275,8 @@ struct ApiServer::Impl {
       const std::string& m = req.method;
       // etcd model: a write is visible (response, watch event) only after a storage
       // commit round trip.  Writes wait concurrently, as they pipeline through raft.
-      if (opts.write_latency_us > 0 && m != "GET") {
-        std::this_thread::sleep_for(std::chrono::microseconds(opts.write_latency_us));
+      if (const int64_t lat = write_latency_us.load(std::memory_order_relaxed); lat > 0 && m != "GET") {
+        std::this_thread::sleep_for(std::chrono::microseconds(lat));
       }
       if (p.collection) {
         if (m == "GET") {
@@ -2294,6 +2317,7 @@ void ApiServer::start() {
   }
   impl_->server = std::make_unique<http::Server>(so);
   Impl* im = impl_.get();
+  metrics::set_debug_endpoints(true);  // a test fixture: the bench reads its webhook samples
   http::add_standard_routes(*impl_->server);
   impl_->server->handle("GET", "/healthz", [](http::Request&, http::ResponseWriter& w) { w.send(200, "ok"); });
   impl_->server->handle("GET", "/readyz", [](http::Request&, http::ResponseWriter& w) { w.send(200, "ok"); });

@@ -26,6 +26,7 @@ int main() {
   admission::Config cfg;
   try {
     cfg = admission::Config::from_env(EnvConfig("CONF_"));
+    metrics::configure_debug(EnvConfig("CONF_"));  // /debug/samples: off unless CONF_DEBUG_ENDPOINTS
   } catch (const std::exception& e) {
     std::fprintf(stderr, "Error: %s\n", e.what());
     return 1;

@@ -22,6 +22,7 @@ int main() {
   controller::Config cfg;
   try {
     cfg = controller::Config::from_env(EnvConfig("CONF_"));
+    metrics::configure_debug(EnvConfig("CONF_"));  // /debug/samples: off unless CONF_DEBUG_ENDPOINTS
     {
       EnvConfig env("CONF_");
       kube::Watcher::Defaults wd;

@@ -10,6 +10,7 @@
 #include "kube/runtime.h"
 #include "core/http.h"
 #include "core/log.h"
+#include "core/metrics.h"
 #include "core/process.h"
 #include "gpu/device.h"
 #include "gpu/diag_runner.h"
@@ -25,6 +26,7 @@ int main(int argc, char** argv) {
   gpu::NodeAgentConfig cfg;
   try {
     cfg = gpu::NodeAgentConfig::from_env(EnvConfig("CONF_"));
+    metrics::configure_debug(EnvConfig("CONF_"));  // /debug/samples: off unless CONF_DEBUG_ENDPOINTS
     {
       EnvConfig env("CONF_");
       kube::Watcher::Defaults wd;

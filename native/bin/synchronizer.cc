@@ -8,6 +8,7 @@
 #include "kube/runtime.h"
 #include "core/http.h"
 #include "core/log.h"
+#include "core/metrics.h"
 #include "core/process.h"
 #include "kube/client.h"
 #include "kube/leader.h"
@@ -21,6 +22,7 @@ int main() {
   sync::Config cfg;
   try {
     cfg = sync::Config::from_env(EnvConfig("CONF_"));
+    metrics::configure_debug(EnvConfig("CONF_"));  // /debug/samples: off unless CONF_DEBUG_ENDPOINTS
     {
       EnvConfig env("CONF_");
       kube::Watcher::Defaults wd;

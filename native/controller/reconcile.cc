@@ -1,6 +1,7 @@
 #include "controller/reconcile.h"
 
 #include <cctype>
+#include <exception>
 #include <future>
 
 #include "core/log.h"
@@ -198,9 +199,26 @@ void Reconciler::apply_child(const DesiredChild& c, const std::string& body_hash
 kube::Action Reconciler::reconcile(const kube::ObjPtr& ub_ptr) {
   auto& reg = metrics::Registry::global();
   static auto& hist = reg.histogram("bgc_reconcile_duration_seconds", "Wall time of one reconcile");
-  static auto& ring = reg.samples("reconcile");
+  static auto& ok = reg.counter("bgc_reconcile_total", "Reconciles", {{"result", "ok"}});
+  static auto& failed = reg.counter("bgc_reconcile_total", "Reconciles", {{"result", "error"}});
+  // bgc_reconcile_total is counted in the sample log's critical section (SampleLog::add), so
+  // the samples of a bench window are exactly that counter's increments over the window.
+  static auto& ring = [&]() -> metrics::SampleLog& {
+    auto& r = reg.samples("reconcile");
+    r.link("bgc_reconcile_total{result=\"ok\"}", &ok);
+    r.link("bgc_reconcile_total{result=\"error\"}", &failed);
+    return r;
+  }();
   static auto& skipped = reg.counter("bgc_apply_skipped_total", "Applies skipped: child already as last written");
-  metrics::Timer timer(&hist, &ring);
+  struct Timed {
+    const int64_t t0 = metrics::now_ns();
+    const int exceptions = std::uncaught_exceptions();
+    ~Timed() {
+      const double e = static_cast<double>(metrics::now_ns() - t0) * 1e-9;
+      hist.observe(e);
+      ring.add(e, std::uncaught_exceptions() > exceptions ? &failed : &ok);  // thrown: error_policy runs next
+    }
+  } timed;
   const Value& ub = *ub_ptr;
   const std::string owner_name = kube::meta_name(ub), owner_rv = kube::meta_rv(ub);
   if (cfg_.skip_unchanged && fresh(owner_name, owner_rv)) {
@@ -272,8 +290,6 @@ kube::Action Reconciler::reconcile(const kube::ObjPtr& ub_ptr) {
       publish_cache_sizes(last_applied_.size(), ub_state_.size());
     }
   }
-  static auto& ok = reg.counter("bgc_reconcile_total", "Reconciles", {{"result", "ok"}});
-  ok.inc();
   return kube::Action::requeue_after(std::chrono::milliseconds(cfg_.requeue_secs * 1000));
 }
 
@@ -302,8 +318,6 @@ void Reconciler::apply_all(const std::vector<DesiredChild>& children, const std:
 }
 
 kube::Action Reconciler::error_policy(const kube::ObjPtr& ub, const std::exception& err) {
-  static auto& fail = metrics::Registry::global().counter("bgc_reconcile_total", "Reconciles", {{"result", "error"}});
-  fail.inc();
   const Value& meta = ub->get("metadata");
   LOG_ERROR("controller") << "error reconciling \"" << meta.get_string("namespace", "<unknown>") << "/"
                           << meta.get_string("name", "<unknown>") << "\": " << err.what();

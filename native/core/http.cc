@@ -834,14 +834,18 @@ void add_standard_routes(Server& s) {
   s.handle("GET", "/metrics", [](Request&, ResponseWriter& w) {
     w.send(200, metrics::Registry::global().render(), "text/plain; version=0.0.4");
   });
+  // Raw latency samples are a test/bench surface: off unless CONF_DEBUG_ENDPOINTS=true (the
+  // reference serves only /mutate and /health, admission.rs:149-152).  A request never
+  // creates a log: unknown names are 404.
+  if (!metrics::debug_endpoints_enabled()) return;
   s.handle_prefix("/debug/samples/", [](Request& r, ResponseWriter& w) {
     std::string name = r.path.substr(std::strlen("/debug/samples/"));
-    if (r.method == "DELETE") {
-      metrics::Registry::global().samples(name).clear();
-      w.send(200, "{}", "application/json");
-      return;
-    }
-    w.send(200, metrics::Registry::global().render_samples_json(name), "application/json");
+    std::string body;
+    if (r.method == "DELETE") body = metrics::Registry::global().clear_samples_json(name);
+    else if (r.method == "GET") body = metrics::Registry::global().render_samples_json(name);
+    else return w.send(405, "method not allowed\n");
+    if (body.empty()) return w.send(404, "no such sample log\n");
+    w.send(200, body, "application/json");
   });
 }
 

@@ -198,7 +198,8 @@ class Server {
   std::atomic<uint64_t> h2_inline_{0};
 };
 
-// Attaches `/health` (-> "pong"), `/metrics` and `/debug/samples/<name>`.
+// Attaches `/health` (-> "pong"), `/metrics` and, only when metrics::debug_endpoints_enabled()
+// (CONF_DEBUG_ENDPOINTS=true), GET/DELETE `/debug/samples/<name>`.
 void add_standard_routes(Server& s);
 
 // ---------------------------------------------------------------------------

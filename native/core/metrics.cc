@@ -9,6 +9,7 @@
 #include <unistd.h>
 #include <sstream>
 
+#include "core/env_config.h"
 #include "core/json.h"
 
 namespace bgc::metrics {
@@ -70,32 +71,83 @@ std::vector<uint64_t> Histogram::bucket_counts() const {
 double Histogram::sum() const { return from_bits(sum_bits_.load(std::memory_order_relaxed)); }
 uint64_t Histogram::count() const { return count_.load(std::memory_order_relaxed); }
 
-SampleRing::SampleRing(size_t capacity) : cap_(capacity ? capacity : 1) {}
+namespace {
+std::atomic<bool> g_samples_enabled{false};
+std::atomic<size_t> g_sample_capacity{size_t{1} << 22};
+std::atomic<bool> g_debug_endpoints{false};
+}  // namespace
 
-void SampleRing::add(double v) {
+void configure_samples(bool enabled, size_t capacity) {
+  g_sample_capacity.store(capacity ? capacity : 1);
+  g_samples_enabled.store(enabled);
+}
+bool samples_enabled() { return g_samples_enabled.load(std::memory_order_relaxed); }
+size_t sample_capacity() { return g_sample_capacity.load(std::memory_order_relaxed); }
+
+void configure_debug(const EnvConfig& env) {
+  const bool on = env.boolean_or("debug_endpoints", false);
+  g_debug_endpoints.store(on);
+  configure_samples(on, static_cast<size_t>(env.u64_or("debug_sample_capacity", uint64_t{1} << 22)));
+}
+void set_debug_endpoints(bool on) {
+  g_debug_endpoints.store(on);
+  configure_samples(on, sample_capacity());
+}
+bool debug_endpoints_enabled() { return g_debug_endpoints.load(std::memory_order_relaxed); }
+
+// capacity 0: the process-wide setting, read when a sample arrives
+SampleLog::SampleLog(size_t capacity) : cap_(capacity) {}
+
+void SampleLog::add(double v, Counter* linked) {
+  const bool keep = samples_enabled();
+  const size_t cap = cap_ ? cap_ : sample_capacity();
   std::lock_guard<std::mutex> lk(mu_);
+  ++lifetime_;
   ++total_;
-  if (buf_.size() < cap_) {
-    buf_.push_back(v);
-  } else {
-    buf_[next_] = v;
-    next_ = (next_ + 1) % buf_.size();
-  }
+  if (linked) linked->inc();
+  if (keep && buf_.size() < cap) buf_.push_back(v);
+  else ++dropped_;
 }
 
-std::vector<double> SampleRing::snapshot() const {
+void SampleLog::link(const std::string& key, Counter* c) {
   std::lock_guard<std::mutex> lk(mu_);
-  return buf_;
+  for (auto& kv : linked_) {
+    if (kv.first == key) {
+      kv.second = c;
+      return;
+    }
+  }
+  linked_.emplace_back(key, c);
 }
 
-void SampleRing::clear() {
+void SampleLog::fill_counts(Snapshot& s) const {
+  s.total = total_;
+  s.dropped = dropped_;
+  s.lifetime = lifetime_;
+  s.capacity = cap_ ? cap_ : sample_capacity();
+  for (const auto& kv : linked_) s.linked.emplace_back(kv.first, kv.second->value());
+}
+
+SampleLog::Snapshot SampleLog::snapshot() const {
+  Snapshot s;
+  std::lock_guard<std::mutex> lk(mu_);
+  s.samples = buf_;
+  fill_counts(s);
+  return s;
+}
+
+SampleLog::Snapshot SampleLog::clear() {
+  Snapshot s;
   std::lock_guard<std::mutex> lk(mu_);
   buf_.clear();
-  next_ = 0;
+  buf_.shrink_to_fit();
   total_ = 0;
+  dropped_ = 0;
+  fill_counts(s);
+  return s;
 }
 
-uint64_t SampleRing::total() const {
+uint64_t SampleLog::total() const {
   std::lock_guard<std::mutex> lk(mu_);
   return total_;
 }
@@ -180,11 +232,17 @@ Histogram& Registry::histogram(const std::string& name, const std::string& help,
   return *slot;
 }
 
-SampleRing& Registry::samples(const std::string& name) {
+SampleLog& Registry::samples(const std::string& name) {
   std::lock_guard<std::mutex> lk(mu_);
   auto& slot = samples_[name];
-  if (!slot) slot = std::make_unique<SampleRing>();
+  if (!slot) slot = std::make_unique<SampleLog>(0);
   return *slot;
+}
+
+SampleLog* Registry::find_samples(const std::string& name) const {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = samples_.find(name);
+  return it == samples_.end() ? nullptr : it->second.get();
 }
 
 void append_process_memory(std::string& out);
@@ -213,6 +271,8 @@ std::string Registry::render() const {
       out += name + "_count" + lbl + " " + std::to_string(h->count()) + "\n";
     }
   }
+  out += "# HELP bgc_debug_sample_logs Latency sample logs in this process (fixed at start-up)\n"
+         "# TYPE bgc_debug_sample_logs gauge\nbgc_debug_sample_logs " + std::to_string(samples_.size()) + "\n";
   append_process_memory(out);
   return out;
 }
@@ -245,27 +305,40 @@ std::vector<std::string> Registry::sample_names() const {
   return out;
 }
 
-std::string Registry::render_samples_json(const std::string& name) const {
-  const SampleRing* ring = nullptr;
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    auto it = samples_.find(name);
-    if (it != samples_.end()) ring = it->second.get();
-  }
+namespace {
+json::Value snapshot_json(const std::string& name, const SampleLog::Snapshot& s) {
   json::Value out = json::Value::object();
   out["name"] = name;
+  out["total"] = static_cast<unsigned long long>(s.total);
+  out["dropped"] = static_cast<unsigned long long>(s.dropped);
+  out["lifetime"] = static_cast<unsigned long long>(s.lifetime);
+  out["capacity"] = static_cast<unsigned long long>(s.capacity);
+  out["complete"] = s.dropped == 0;
+  json::Value linked = json::Value::object();
+  for (const auto& kv : s.linked) linked[kv.first] = kv.second;
+  out["linked"] = std::move(linked);
+  return out;
+}
+}  // namespace
+
+std::string Registry::render_samples_json(const std::string& name) const {
+  const SampleLog* log = find_samples(name);
+  if (!log) return "";
+  SampleLog::Snapshot s = log->snapshot();
+  json::Value out = snapshot_json(name, s);
   json::Value arr = json::Value::array();
-  uint64_t total = 0;
-  if (ring) {
-    for (double d : ring->snapshot()) arr.push_back(d);
-    total = ring->total();
-  }
-  out["total"] = static_cast<unsigned long long>(total);
+  for (double d : s.samples) arr.push_back(d);
   out["samples"] = std::move(arr);
   return out.dump();
 }
 
-Timer::Timer(Histogram* h, SampleRing* s) : h_(h), s_(s), start_ns_(now_ns()) {}
+std::string Registry::clear_samples_json(const std::string& name) const {
+  SampleLog* log = find_samples(name);
+  if (!log) return "";
+  return snapshot_json(name, log->clear()).dump();
+}
+
+Timer::Timer(Histogram* h, SampleLog* s) : h_(h), s_(s), start_ns_(now_ns()) {}
 Timer::~Timer() {
   double e = elapsed();
   if (h_) h_->observe(e);

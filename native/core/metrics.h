@@ -1,8 +1,10 @@
 // Prometheus text-format metrics plus an exact-latency sample recorder.
 //
 // The reference exposes no metrics at all; every binary here serves
-// `/metrics` on its health listener and `/debug/samples` with raw latencies, which the
-// bench harness turns into exact p50/p99 values.
+// `/metrics` on its health listener.  With CONF_DEBUG_ENDPOINTS=true (tests and the bench
+// harness only; off in the binaries and the chart) it also keeps every latency sample of
+// a window and serves them on `/debug/samples/<name>`, which the harness turns into exact
+// p50/p99 values.
 #pragma once
 
 #include <atomic>
@@ -12,6 +14,10 @@
 #include <mutex>
 #include <string>
 #include <vector>
+
+namespace bgc {
+class EnvConfig;
+}
 
 namespace bgc::metrics {
 
@@ -51,22 +57,54 @@ class Histogram {
   std::atomic<uint64_t> count_{0};
 };
 
-// Keeps the last `capacity` observations (seconds) for exact quantiles.
-class SampleRing {
+// Every observation of a measurement window (seconds), for exact quantiles.
+//
+// Nothing is overwritten: once `capacity` samples are held, further ones are counted as
+// dropped, so a reader can tell a complete window from a truncated one (the bench refuses
+// to report a percentile over a truncated window).  Samples are only kept while sample
+// recording is enabled (configure_samples); otherwise add() just counts.
+//
+// Linked counters: a Prometheus counter passed to add() is incremented inside the same
+// critical section that records the sample, and snapshot()/clear() read every linked
+// counter under that lock.  The samples of a window are then exactly the increments of
+// its linked counters between clear() and snapshot(), by construction.
+class SampleLog {
  public:
-  explicit SampleRing(size_t capacity = 1 << 16);
-  void add(double v);
-  std::vector<double> snapshot() const;
-  void clear();
+  explicit SampleLog(size_t capacity);
+  void add(double v, Counter* linked = nullptr);
+  // Registers `c` under `key` (its exposition name + labels) for snapshots.
+  void link(const std::string& key, Counter* c);
+
+  struct Snapshot {
+    std::vector<double> samples;
+    uint64_t total = 0;     // add() calls since the last clear (kept + dropped)
+    uint64_t dropped = 0;   // not kept: capacity reached or recording disabled
+    uint64_t lifetime = 0;  // add() calls since start
+    uint64_t capacity = 0;
+    std::vector<std::pair<std::string, double>> linked;  // linked counter values
+  };
+  Snapshot snapshot() const;
+  Snapshot clear();  // returns the counts at the instant of clearing (no samples)
   uint64_t total() const;
 
  private:
   mutable std::mutex mu_;
   size_t cap_;
   std::vector<double> buf_;
-  size_t next_ = 0;
-  uint64_t total_ = 0;
+  uint64_t total_ = 0, dropped_ = 0, lifetime_ = 0;
+  std::vector<std::pair<std::string, Counter*>> linked_;
+  void fill_counts(Snapshot& s) const;  // mu_ held
 };
+
+// Sample recording (off by default: production binaries keep no raw samples).
+void configure_samples(bool enabled, size_t capacity = size_t{1} << 22);
+bool samples_enabled();
+size_t sample_capacity();
+// Reads CONF_DEBUG_ENDPOINTS (bool, default false) and CONF_DEBUG_SAMPLE_CAPACITY
+// (default 4,194,304 samples per log): the /debug/samples routes and sample recording.
+void configure_debug(const EnvConfig& env);
+void set_debug_endpoints(bool on);  // routes + recording (kube-lite, a test fixture)
+bool debug_endpoints_enabled();
 
 double quantile(std::vector<double> v, double q);
 
@@ -80,10 +118,15 @@ class Registry {
   Gauge& gauge(const std::string& name, const std::string& help, const Labels& labels = {});
   Histogram& histogram(const std::string& name, const std::string& help, const Labels& labels = {},
                        std::vector<double> buckets = default_latency_buckets());
-  SampleRing& samples(const std::string& name);
+  SampleLog& samples(const std::string& name);             // creates the log
+  SampleLog* find_samples(const std::string& name) const;  // nullptr if absent
 
   std::string render() const;  // Prometheus exposition format 0.0.4
+  // JSON of one log: {"name","total","dropped","lifetime","capacity","complete",
+  // "linked":{...},"samples":[...]}; clear_samples_json() clears it and returns the same
+  // fields without samples.  Both return "" for an unknown name (never create one).
   std::string render_samples_json(const std::string& name) const;
+  std::string clear_samples_json(const std::string& name) const;
   std::vector<std::string> sample_names() const;
 
  private:
@@ -95,23 +138,23 @@ class Registry {
   };
   mutable std::mutex mu_;
   std::map<std::string, Family> families_;
-  std::map<std::string, std::unique_ptr<SampleRing>> samples_;
+  std::map<std::string, std::unique_ptr<SampleLog>> samples_;
 };
 
 std::string render_labels(const Labels& labels, const std::string& extra_key = "",
                           const std::string& extra_val = "");
 
-// RAII timer: observes elapsed seconds into histogram (and optional sample ring).
+// RAII timer: observes elapsed seconds into histogram (and optional sample log).
 class Timer {
  public:
-  Timer(Histogram* h, SampleRing* s = nullptr);
+  Timer(Histogram* h, SampleLog* s = nullptr);
   ~Timer();
   double elapsed() const;
   void cancel() { h_ = nullptr; s_ = nullptr; }
 
  private:
   Histogram* h_;
-  SampleRing* s_;
+  SampleLog* s_;
   int64_t start_ns_;
 };
 
