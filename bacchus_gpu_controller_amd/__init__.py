@@ -50,7 +50,12 @@ def native():
 
 
 def binary(name):
-    """Absolute path of a native binary (controller, admission, kube-lite, ...)."""
+    """Absolute path of a native binary (controller, admission, kube-lite, ...).
+    BGC_BIN_<NAME> (e.g. BGC_BIN_CONTROLLER) substitutes one binary: A/B runs of one
+    component's older build against the rest of this tree (tools/gpu_ab.sh)."""
+    override = os.environ.get("BGC_BIN_" + name.upper().replace("-", "_"))
+    if override:
+        return override
     path = os.path.join(BIN_DIR, name)
     if not os.path.exists(path):
         from .utils.build import ensure_built

@@ -485,6 +485,8 @@ def run(args):
             # (synchronizer.rs:192), every tick rewrites every matched tenant
             sync_env.update({"CONF_WATCH": "false", "CONF_SKIP_UNCHANGED": "false"})
         apiserver_args = list(args.apiserver_arg)
+        if args.write_latency_ms > 0:
+            apiserver_args += ["--write-latency-ms", str(args.write_latency_ms)]
         if args.webhook_protocol == "h2" and "--webhook-http2" not in apiserver_args:
             # what a real apiserver negotiates with the admission server (ALPN h2, one
             # multiplexed connection): the production webhook transport
@@ -508,14 +510,17 @@ def run(args):
     try:
         results = {}
         running = semantics  # controller semantics of the running controller
+        latency = args.write_latency_ms  # kube-lite's current storage latency
         for p in phases:
             if d.rank == 0:
                 import requests
 
                 requests.post(info["server"] + "/_kl/webhook-protocol", data=p.protocol, timeout=10,
                               verify=info["apiserver_verify"]).raise_for_status()
-                requests.post(info["server"] + "/_kl/write-latency-us", data=str(int(p.write_latency_ms * 1000)),
-                              timeout=10, verify=info["apiserver_verify"]).raise_for_status()
+                if p.write_latency_ms != latency:
+                    requests.post(info["server"] + "/_kl/write-latency-us", data=str(int(p.write_latency_ms * 1000)),
+                                  timeout=10, verify=info["apiserver_verify"]).raise_for_status()
+                    latency = p.write_latency_ms
                 if controller_env(p.semantics) != controller_env(running):
                     # the other controller behaviour: a fresh controller process, which
                     # re-lists every object like any controller start

@@ -2,6 +2,7 @@
 
 #include <cctype>
 #include <exception>
+#include <iterator>
 #include <future>
 
 #include "core/log.h"
@@ -26,6 +27,7 @@ Config Config::from_env(const EnvConfig& env) {
   c.label_children = env.boolean_or("label_children", true);
   c.metadata_watches = env.boolean_or("metadata_watches", true);
   c.events = env.boolean_or("events", true);
+  c.projected_watch = env.boolean_or("projected_watch", true);
   c.lease = kube::LeaseSettings::from_env(env, "bacchus-gpu-controller");
   return c;
 }
@@ -44,34 +46,71 @@ Value controller_owner_ref(const Value& ub) {
                         {"uid", meta.get_string("uid")}});
 }
 
+const json::Projection& user_bootstrap_event_projection() {
+  using P = json::Projection;
+  static const P kMeta[] = {{"name", P::Keep},          {"namespace", P::Keep},  {"uid", P::Keep},
+                            {"resourceVersion", P::Keep}, {"generation", P::Keep}, {"deletionTimestamp", P::Keep}};
+  static const P kObject[] = {{"apiVersion", P::Keep}, {"kind", P::Keep},  {"metadata", P::Descend, kMeta, std::size(kMeta)},
+                              {"spec", P::Keep},       {"status", P::Keep}};
+  static const P kEvent[] = {{"type", P::Keep}, {"object", P::Descend, kObject, std::size(kObject)}};
+  static const P kRoot{"", P::Descend, kEvent, std::size(kEvent)};
+  return kRoot;
+}
+
 std::string child_label_selector() { return std::string(kManagedByLabel) + "=" + kManagedByValue; }
 
+// The bodies are written straight into JSON text: a reconcile plans up to four children
+// and the only trees it needs are the user's own subtrees (quota, role, rolebinding),
+// which are already parsed.  Member order matches what a json::Value build would emit.
 std::vector<DesiredChild> desired_children(const Value& ub, bool label) {
-  const Value& name_v = ub.get("metadata").get("name");
+  const Value& meta_v = ub.get("metadata");
+  const Value& name_v = meta_v.get("name");
   if (!name_v.is_string()) throw std::runtime_error("missing object key: .metadata.name");
+  if (!meta_v.get("uid").is_string()) throw std::runtime_error("missing object key: .metadata.uid");
   std::string name = name_v.as_string();
   for (auto& ch : name) ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
-  Value oref = controller_owner_ref(ub);
-  auto meta = [&]() {
-    Value m = Value::object({{"name", name}, {"ownerReferences", Value::array({oref})}});
-    if (label) m["labels"] = Value::object({{kManagedByLabel, kManagedByValue}});
-    return m;
+  // kube `controller_owner_ref` (see controller_owner_ref above), as text
+  std::string oref = "{\"apiVersion\":\"bacchus.io/v1\",\"controller\":true,\"kind\":\"UserBootstrap\",\"name\":";
+  json::escape_string(name_v.as_string(), oref);
+  oref += ",\"uid\":";
+  json::escape_string(meta_v.get("uid").as_string(), oref);
+  oref += "}";
+  std::string qname;
+  json::escape_string(name, qname);
+  const std::string label_json =
+      std::string("{") + json::quote(kManagedByLabel) + ":" + json::quote(kManagedByValue) + "}";
+  // {"name":..,"ownerReferences":[..](,"labels":{..})}
+  std::string meta = "{\"name\":" + qname + ",\"ownerReferences\":[" + oref + "]";
+  if (label) meta += ",\"labels\":" + label_json;
+  meta += "}";
+  auto head = [&](const char* api_version, const char* kind) {
+    std::string b;
+    b.reserve(256 + meta.size());
+    b += "{\"apiVersion\":\"";
+    b += api_version;
+    b += "\",\"kind\":\"";
+    b += kind;
+    b += "\",\"metadata\":";
+    b += meta;
+    return b;
   };
   std::vector<DesiredChild> out;
   // (1) Namespace (controller.rs:69-87)
-  out.push_back({&types::Namespace, "", name,
-                 Value::object({{"apiVersion", "v1"}, {"kind", "Namespace"}, {"metadata", meta()}})});
+  out.push_back({&types::Namespace, "", name, head("v1", "Namespace") + "}"});
   const Value& spec = ub.get("spec");
   // (2) ResourceQuota (controller.rs:89-110)
   if (const Value* q = spec.find("quota"); q && !q->is_null()) {
-    out.push_back({&types::ResourceQuota, name, name,
-                   Value::object({{"apiVersion", "v1"}, {"kind", "ResourceQuota"}, {"metadata", meta()}, {"spec", *q}})});
+    std::string b = head("v1", "ResourceQuota");
+    b += ",\"spec\":";
+    q->dump_to(b);
+    b += "}";
+    out.push_back({&types::ResourceQuota, name, name, std::move(b)});
   }
   // (3) Role: the user's object with ownerReferences overwritten (controller.rs:112-124)
   if (const Value* r = spec.find("role"); r && !r->is_null()) {
     Value role = Value::object({{"apiVersion", "rbac.authorization.k8s.io/v1"}, {"kind", "Role"}});
     Value m = r->get("metadata").is_object() ? r->get("metadata") : Value::object();
-    m["ownerReferences"] = Value::array({oref});
+    m["ownerReferences"] = Value::array({controller_owner_ref(ub)});
     if (label) {
       if (!m.get("labels").is_object()) m["labels"] = Value::object();
       m["labels"][kManagedByLabel] = kManagedByValue;
@@ -80,16 +119,21 @@ std::vector<DesiredChild> desired_children(const Value& ub, bool label) {
     if (const Value* rules = r->find("rules"); rules && !rules->is_null()) role["rules"] = *rules;
     // The URL name is the namespace name; a Role whose metadata.name differs is
     // rejected by the apiserver on every reconcile, exactly like the reference (Q9).
-    out.push_back({&types::Role, name, name, role});
+    out.push_back({&types::Role, name, name, role.dump()});
   }
   // (4) RoleBinding, gated on status.synchronized_with_sheet (controller.rs:126-152)
   if (const Value* rb = spec.find("rolebinding"); rb && !rb->is_null()) {
     const Value& st = ub.get("status");
     if (st.is_object() && st.get("synchronized_with_sheet").is_bool() && st.get("synchronized_with_sheet").as_bool()) {
-      Value body = Value::object({{"apiVersion", "rbac.authorization.k8s.io/v1"}, {"kind", "RoleBinding"}, {"metadata", meta()}});
-      body["roleRef"] = rb->get("role_ref");
-      if (const Value* s = rb->find("subjects"); s && !s->is_null()) body["subjects"] = *s;
-      out.push_back({&types::RoleBinding, name, name, body});
+      std::string b = head("rbac.authorization.k8s.io/v1", "RoleBinding");
+      b += ",\"roleRef\":";
+      rb->get("role_ref").dump_to(b);
+      if (const Value* sub = rb->find("subjects"); sub && !sub->is_null()) {
+        b += ",\"subjects\":";
+        sub->dump_to(b);
+      }
+      b += "}";
+      out.push_back({&types::RoleBinding, name, name, std::move(b)});
     }
   }
   return out;
@@ -229,13 +273,9 @@ kube::Action Reconciler::reconcile(const kube::ObjPtr& ub_ptr) {
   std::vector<DesiredChild> children = desired_children(ub, cfg_.label_children);
   LOG_INFO("controller") << "reconciling " << children.front().name;
 
-  std::vector<std::string> bodies, hashes;
-  bodies.reserve(children.size());
+  std::vector<std::string> hashes;
   hashes.reserve(children.size());
-  for (const auto& c : children) {
-    bodies.push_back(c.body.dump());
-    hashes.push_back(std::to_string(std::hash<std::string>{}(bodies.back())));
-  }
+  for (const auto& c : children) hashes.push_back(std::to_string(std::hash<std::string>{}(c.body)));
 
   auto run_one = [&](size_t i) {
     if (up_to_date(children[i], hashes[i])) {
@@ -245,7 +285,7 @@ kube::Action Reconciler::reconcile(const kube::ObjPtr& ub_ptr) {
       return;
     }
     try {
-      apply_child(children[i], hashes[i], bodies[i]);
+      apply_child(children[i], hashes[i], children[i].body);
     } catch (const std::exception& e) {
       LOG_ERROR("controller") << "failed to patch " << children[i].rt->kind << ": " << e.what();
       throw;

@@ -62,6 +62,8 @@ struct Config {
   bool metadata_watches = true;
   // Warning Events (kubectl describe userbootstrap) for failed reconciles.
   bool events = true;
+  // UserBootstrap watch events parsed through user_bootstrap_event_projection().
+  bool projected_watch = true;
   kube::LeaseSettings lease;  // optional leader election (CONF_LEADER_ELECTION, ...)
   // reference fields are required (controller.rs:24-28); the rest default
   static Config from_env(const EnvConfig& env);
@@ -71,7 +73,7 @@ struct DesiredChild {
   const kube::ResourceType* rt;
   std::string ns;
   std::string name;
-  json::Value body;
+  std::string body;  // the apply body, JSON text
 };
 
 // Pure planning step: the children the reference would apply for `ub`, in its order.
@@ -81,6 +83,11 @@ struct DesiredChild {
 std::vector<DesiredChild> desired_children(const json::Value& ub, bool label = false);
 // The owned-kind watch selector matching those labels.
 std::string child_label_selector();
+// What a reconcile reads from a UserBootstrap watch event: type, apiVersion, kind,
+// metadata.{name,namespace,uid,resourceVersion,generation,deletionTimestamp}, spec and
+// status (reference controller.rs:50-155).  Everything else, annotations and labels
+// included, is scanned but not built.
+const json::Projection& user_bootstrap_event_projection();
 json::Value controller_owner_ref(const json::Value& ub);
 
 class Reconciler {

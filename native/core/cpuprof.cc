@@ -1,13 +1,18 @@
 #include "core/cpuprof.h"
 
+#include <dirent.h>
 #include <fcntl.h>
+#include <pthread.h>
 #include <signal.h>
+#include <sys/syscall.h>
 #include <sys/time.h>
+#include <time.h>
 #include <ucontext.h>
 #include <unistd.h>
 #include <unwind.h>
 
 #include <atomic>
+#include <chrono>
 #include <cerrno>
 #include <cstdint>
 #include <cstdio>
@@ -16,7 +21,9 @@
 #include <fstream>
 #include <map>
 #include <mutex>
+#include <set>
 #include <sstream>
+#include <thread>
 #include <vector>
 
 namespace bgc::cpuprof {
@@ -65,6 +72,58 @@ _Unwind_Reason_Code eh_frame(struct _Unwind_Context* ctx, void* arg) {
 std::string g_path;
 std::mutex g_mu;
 bool g_started = false;
+
+// Per-thread CPU timers.  A process-wide ITIMER_PROF fires at most once per scheduler
+// tick for the whole process (250-1000 Hz however many threads are busy), so a 16-thread
+// service is sampled at a fraction of `hz`.  Instead every thread gets its own
+// CLOCK_THREAD_CPUTIME timer delivering SIGPROF to that thread (SIGEV_THREAD_ID); a
+// helper thread arms one for each new thread it finds in /proc/self/task every 50 ms.
+bool g_per_thread = false;
+long g_interval_ns = 0;
+std::thread g_arm;
+std::atomic<bool> g_arm_stop{false};
+std::map<pid_t, timer_t> g_timers;  // under g_timers_mu
+std::mutex g_timers_mu;
+
+clockid_t thread_cpu_clock(pid_t tid) {
+  // MAKE_THREAD_CPUCLOCK(tid, CPUCLOCK_SCHED): ((~tid) << 3) | CPUCLOCK_PERTHREAD_MASK | CPUCLOCK_SCHED
+  return static_cast<clockid_t>((~static_cast<unsigned>(tid) << 3) | 4 | 2);
+}
+
+void arm_new_threads() {
+  std::set<pid_t> live;
+  if (DIR* d = ::opendir("/proc/self/task")) {
+    while (dirent* e = ::readdir(d)) {
+      if (e->d_name[0] >= '0' && e->d_name[0] <= '9') live.insert(static_cast<pid_t>(std::atoi(e->d_name)));
+    }
+    ::closedir(d);
+  }
+  const pid_t self = static_cast<pid_t>(::syscall(SYS_gettid));
+  std::lock_guard<std::mutex> lk(g_timers_mu);
+  for (auto it = g_timers.begin(); it != g_timers.end();) {
+    if (!live.count(it->first)) {
+      ::timer_delete(it->second);
+      it = g_timers.erase(it);
+    } else {
+      ++it;
+    }
+  }
+  for (pid_t tid : live) {
+    if (tid == self || g_timers.count(tid)) continue;
+    struct sigevent sev {};
+    sev.sigev_notify = SIGEV_THREAD_ID;
+    sev.sigev_signo = SIGPROF;
+    sev._sigev_un._tid = tid;
+    timer_t t;
+    if (::timer_create(thread_cpu_clock(tid), &sev, &t) != 0) continue;  // the thread just exited
+    struct itimerspec its {};
+    its.it_interval.tv_sec = g_interval_ns / 1000000000L;
+    its.it_interval.tv_nsec = g_interval_ns % 1000000000L;
+    its.it_value = its.it_interval;
+    ::timer_settime(t, 0, &its, nullptr);
+    g_timers[tid] = t;
+  }
+}
 
 // True when [p, p+16) is readable: write() reports EFAULT instead of faulting.
 bool readable(uintptr_t p) {
@@ -175,12 +234,32 @@ bool start(const std::string& path, int hz) {
   sigemptyset(&sa.sa_mask);
   if (sigaction(SIGPROF, &sa, nullptr) != 0) return false;
   g_on = true;
-  struct itimerval it {};
-  long us = 1000000L / std::max(1, hz);
-  it.it_interval.tv_sec = us / 1000000L;
-  it.it_interval.tv_usec = us % 1000000L;
-  it.it_value = it.it_interval;
-  if (setitimer(ITIMER_PROF, &it, nullptr) != 0) return false;
+  const char* mode = std::getenv("BGC_CPU_PROFILE_TIMER");  // "thread" (default) | "process"
+  g_per_thread = !(mode && std::string(mode) == "process");
+  if (g_per_thread) {
+    g_interval_ns = 1000000000L / std::max(1, hz);
+    g_arm_stop = false;
+    arm_new_threads();
+    // The helper never takes process signals (SIGTERM belongs to the service's sigwait
+    // thread): it is created with every signal blocked and inherits that mask.
+    sigset_t all, old;
+    sigfillset(&all);
+    pthread_sigmask(SIG_BLOCK, &all, &old);
+    g_arm = std::thread([] {
+      while (!g_arm_stop.load()) {
+        arm_new_threads();
+        std::this_thread::sleep_for(std::chrono::milliseconds(50));
+      }
+    });
+    pthread_sigmask(SIG_SETMASK, &old, nullptr);
+  } else {
+    struct itimerval it {};
+    long us = 1000000L / std::max(1, hz);
+    it.it_interval.tv_sec = us / 1000000L;
+    it.it_interval.tv_usec = us % 1000000L;
+    it.it_value = it.it_interval;
+    if (setitimer(ITIMER_PROF, &it, nullptr) != 0) return false;
+  }
   g_started = true;
   std::atexit([] { stop(); });
   return true;
@@ -201,8 +280,16 @@ void start_from_env() {
 void stop() {
   std::lock_guard<std::mutex> lk(g_mu);
   if (!g_started) return;
-  struct itimerval it {};
-  setitimer(ITIMER_PROF, &it, nullptr);
+  if (g_per_thread) {
+    g_arm_stop = true;
+    if (g_arm.joinable()) g_arm.join();
+    std::lock_guard<std::mutex> tl(g_timers_mu);
+    for (auto& kv : g_timers) ::timer_delete(kv.second);
+    g_timers.clear();
+  } else {
+    struct itimerval it {};
+    setitimer(ITIMER_PROF, &it, nullptr);
+  }
   g_on = false;
   write_profile();
   g_started = false;

@@ -313,8 +313,32 @@ std::string TlsStream::alpn() const {
   return p ? std::string(reinterpret_cast<const char*>(p), n) : std::string();
 }
 
+// BGC_TLS_POLL_FIRST=1: when OpenSSL holds no buffered bytes, wait in poll() before the
+// first SSL_read instead of after it fails: a reader that has consumed everything (a
+// client waiting for its response, a watch stream between events) saves the EAGAIN
+// recv() of every read.
+static bool tls_poll_first() {
+  static const bool on = [] {
+    const char* e = std::getenv("BGC_TLS_POLL_FIRST");
+    return e && std::string(e) == "1";
+  }();
+  return on;
+}
+
 ssize_t TlsStream::read_some(char* buf, size_t n, int timeout_ms) {
   const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(std::max(timeout_ms, 0));
+  if (timeout_ms != 0 && tls_poll_first()) {
+    bool pending;
+    {
+      std::lock_guard<std::mutex> lk(ssl_mu_);
+      pending = SSL_has_pending(ssl_) == 1;
+    }
+    if (!pending) {
+      const int pr = poll_fd(fd_, POLLIN, timeout_ms);
+      if (pr == 0) return -2;
+      if (pr < 0) return -1;
+    }
+  }
   while (true) {
     int r, err;
     {

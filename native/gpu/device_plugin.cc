@@ -541,16 +541,96 @@ DevicePlugin::DevicePlugin(std::vector<GpuInfo> gpus, DevicePluginConfig cfg)
       healthy_(gpus_.size(), true),
       fenced_(gpus_.size(), false),
       alloc_counts_(gpus_.size(), 0) {
+  ids_ = device_ids_for(gpus_);
+  std::map<std::string, int> seen;
+  for (const auto& g : gpus_) seen[g.bdf]++;
+  for (const auto& g : gpus_) shared_bdf_.push_back(!g.bdf.empty() && seen[g.bdf] > 1);
+}
+
+std::vector<std::string> device_ids_for(const std::vector<GpuInfo>& gpus) {
   // ID = PCI BDF; compute partitions of one GPU can share a BDF, so duplicates get the
   // logical device index appended.
   std::map<std::string, int> seen;
-  for (const auto& g : gpus_) seen[g.bdf]++;
-  for (const auto& g : gpus_) {
-    shared_bdf_.push_back(!g.bdf.empty() && seen[g.bdf] > 1);
-    if (g.bdf.empty()) ids_.push_back("gpu-" + std::to_string(g.index));
-    else if (seen[g.bdf] > 1) ids_.push_back(g.bdf + "-p" + std::to_string(g.index));
-    else ids_.push_back(g.bdf);
+  for (const auto& g : gpus) seen[g.bdf]++;
+  std::vector<std::string> ids;
+  for (const auto& g : gpus) {
+    if (g.bdf.empty()) ids.push_back("gpu-" + std::to_string(g.index));
+    else if (seen[g.bdf] > 1) ids.push_back(g.bdf + "-p" + std::to_string(g.index));
+    else ids.push_back(g.bdf);
   }
+  return ids;
+}
+
+std::set<std::string> checkpoint_devices(const std::string& plugin_dir, const std::string& resource, bool* readable) {
+  std::set<std::string> out;
+  if (readable) *readable = false;
+  std::string text;
+  try {
+    text = net::read_file(join_path(plugin_dir, "kubelet_internal_checkpoint"));
+  } catch (const std::exception&) {
+    return out;
+  }
+  json::Value cp;
+  if (!json::try_parse(text, cp)) return out;
+  if (readable) *readable = true;
+  // {"Data":{"PodDeviceEntries":[...],"RegisteredDevices":{"<resource>":["id",...]}},"Checksum":N}
+  for (const auto& id : cp.get("Data").get("RegisteredDevices").get(resource).items()) {
+    if (id.is_string()) out.insert(id.as_string());
+  }
+  return out;
+}
+
+std::vector<ForeignPlugin> foreign_plugins_for(const std::string& plugin_dir, const std::string& kubelet_socket,
+                                               const std::string& own_socket, const std::string& resource,
+                                               const std::vector<std::string>& own_ids, int timeout_ms) {
+  std::vector<ForeignPlugin> out;
+  DIR* d = ::opendir(plugin_dir.c_str());
+  if (!d) return out;
+  std::vector<std::string> sockets;
+  while (dirent* e = ::readdir(d)) {
+    const std::string name = e->d_name;
+    if (name == "." || name == ".." || name == kubelet_socket || name == own_socket) continue;
+    struct stat st{};
+    if (::stat(join_path(plugin_dir, name).c_str(), &st) == 0 && S_ISSOCK(st.st_mode)) sockets.push_back(name);
+  }
+  ::closedir(d);
+  std::sort(sockets.begin(), sockets.end());
+  if (sockets.empty()) return out;
+  bool cp_ok = false;
+  const std::set<std::string> registered = checkpoint_devices(plugin_dir, resource, &cp_ok);
+  const std::set<std::string> ours(own_ids.begin(), own_ids.end());
+  for (const auto& name : sockets) {
+    ForeignPlugin fp;
+    fp.socket = name;
+    bool answered = false;
+    try {
+      grpc::Channel ch(join_path(plugin_dir, name), timeout_ms);
+      grpc::Status st = ch.server_stream(
+          "/v1beta1.DevicePlugin/ListAndWatch", "",
+          [&](const std::string& msg) {
+            for (const auto& dev : dp::decode_list_and_watch(msg)) fp.ids.push_back(dev.id);
+            answered = true;
+            return false;  // the first list is enough
+          },
+          std::chrono::milliseconds(timeout_ms));
+      (void)st;  // cancelled by us after the first message, or a stale socket / not a device plugin
+      ch.close();
+    } catch (const std::exception&) {
+      continue;  // stale socket: nobody listening
+    }
+    if (!answered) continue;
+    bool serves = false;
+    for (const auto& id : fp.ids) {
+      if (cp_ok ? registered.count(id) > 0 : ours.count(id) > 0) {
+        serves = true;
+        break;
+      }
+    }
+    if (!serves) continue;
+    fp.via_checkpoint = cp_ok;
+    out.push_back(std::move(fp));
+  }
+  return out;
 }
 
 DevicePlugin::~DevicePlugin() { stop(); }

@@ -143,6 +143,29 @@ std::vector<std::string> preferred_allocation(const std::vector<GpuInfo>& gpus, 
                                               const std::vector<std::string>& available,
                                               const std::vector<std::string>& must_include, int size);
 
+// Device ids a DevicePlugin advertises for `gpus` (PCI BDF; "-p<index>" for partitions
+// sharing one, "gpu-<index>" without a BDF).
+std::vector<std::string> device_ids_for(const std::vector<GpuInfo>& gpus);
+
+// Coexistence with another advertiser of the same resource (an MI355X node commonly runs
+// AMD's GPU Operator, whose device plugin registers amd.com/gpu too).  A foreign plugin
+// is any live socket in `plugin_dir` other than the kubelet's and ours that answers
+// v1beta1.DevicePlugin/ListAndWatch; it serves `resource` when one of its device ids is
+// registered for `resource` in the kubelet's checkpoint (kubelet_internal_checkpoint,
+// RegisteredDevices), or, without a readable checkpoint, when it lists one of our ids.
+struct ForeignPlugin {
+  std::string socket;              // file name in plugin_dir
+  std::vector<std::string> ids;    // what its ListAndWatch listed
+  bool via_checkpoint = false;     // matched through the kubelet checkpoint
+};
+std::vector<ForeignPlugin> foreign_plugins_for(const std::string& plugin_dir, const std::string& kubelet_socket,
+                                               const std::string& own_socket, const std::string& resource,
+                                               const std::vector<std::string>& own_ids, int timeout_ms = 2000);
+// RegisteredDevices[resource] of the kubelet checkpoint in `plugin_dir` (empty set when the
+// file is missing; `readable` says whether it parsed).
+std::set<std::string> checkpoint_devices(const std::string& plugin_dir, const std::string& resource,
+                                         bool* readable = nullptr);
+
 class DevicePlugin {
  public:
   DevicePlugin(std::vector<GpuInfo> gpus, DevicePluginConfig cfg);

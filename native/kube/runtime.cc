@@ -132,13 +132,13 @@ void Watcher::run(CancelToken& stop, const std::function<void(const WatchEvent&)
         // Events the consumer does not want are dropped before JSON parsing; ERROR and
         // BOOKMARK lines always go through (they drive relists and resumption).  During
         // a streaming list nothing is dropped: the initial state must be complete.
-        if (!initial_phase && line_filter_ && !line_filter_(line) && line.find("\"type\":\"ERROR\"") == std::string::npos &&
-            line.find("\"type\":\"BOOKMARK\"") == std::string::npos) {
-          continue;
-        }
+        const bool control = line.find("\"type\":\"ERROR\"") != std::string::npos ||
+                             line.find("\"type\":\"BOOKMARK\"") != std::string::npos;
+        if (!initial_phase && line_filter_ && !control && !line_filter_(line)) continue;
         // metadata.managedFields is never read from the cache; skipping it while parsing
         // saves most of the allocations of an SSA-managed child's event.
-        Value ev = json::parse(line, "managedFields");
+        Value ev = projection_ && !initial_phase && !control ? json::parse_projected(line, *projection_)
+                                                            : json::parse(line, "managedFields");
         const std::string type = ev.get_string("type");
         Value* objp = ev.find_mut("object");
         Value obj = objp ? std::move(*objp) : Value();  // no deep copy of the event object
@@ -447,6 +447,7 @@ void Controller::run(CancelToken& stop, Reconciler reconcile, ErrorPolicy error_
   // primary watcher: trigger_self
   threads.emplace_back([&] {
     Watcher w(client_, primary_);
+    w.set_projection(opts_.primary_projection);
     w.run(stop, [&](const WatchEvent& ev) {
       primary_store_->apply(ev);
       primary_gauge.set(static_cast<double>(primary_store_->size()));

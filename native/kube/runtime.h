@@ -81,6 +81,12 @@ class Watcher {
   // drops events must not rely on them (the resume resourceVersion may lag; a resumed
   // watch replays them, and they are filtered again).
   void set_line_filter(std::function<bool(std::string_view)> f) { line_filter_ = std::move(f); }
+  // Optional selective parse of ADDED/MODIFIED/DELETED events (json::parse_projected over
+  // the whole event line, so the root projection names "type" and "object"): members the
+  // consumer never reads (annotations such as kubectl's last-applied copy of the spec,
+  // managedFields) are scanned, not built.  ERROR and BOOKMARK lines and the initial
+  // events of a streaming list are always parsed in full.  `p` must outlive the watcher.
+  void set_projection(const json::Projection* p) { projection_ = p; }
   uint64_t relists() const { return relists_.load(); }
   uint64_t reconnects() const { return reconnects_.load(); }
   uint64_t list_pages() const { return list_pages_.load(); }
@@ -99,6 +105,7 @@ class Watcher {
   std::string selector_;
   std::string field_selector_;
   std::function<bool(std::string_view)> line_filter_;
+  const json::Projection* projection_ = nullptr;
   std::atomic<uint64_t> relists_{0};
   std::atomic<uint64_t> reconnects_{0};
 };
@@ -189,6 +196,8 @@ class Controller {
     // children's DELETED events can overtake the owner's own DELETED event, and reconciling
     // the stale owner would re-create children the garbage collector is removing.
     std::chrono::milliseconds child_delete_delay{50};
+    // Selective parse of the primary watch's events (Watcher::set_projection).
+    const json::Projection* primary_projection = nullptr;
   };
 
   Controller(KubeClient& client, ResourceType primary, Options opts);

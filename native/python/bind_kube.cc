@@ -6,6 +6,7 @@
 
 #include "apiserver/server.h"
 #include "bench/churn.h"
+#include "controller/reconcile.h"
 #include "kube/events.h"
 #include "kube/ratelimit.h"
 #include "kube/runtime.h"
@@ -15,6 +16,13 @@ namespace py = pybind11;
 namespace bgc_py {
 
 void register_kube(py::module_& m) {
+  // The reconciler's pure planning step (controller/reconcile.h): [(plural, ns, name, body)]
+  m.def("desired_children", [](const std::string& ub_json, bool label) {
+    std::vector<std::tuple<std::string, std::string, std::string, std::string>> out;
+    for (auto& c : bgc::controller::desired_children(bgc::json::parse(ub_json), label))
+      out.emplace_back(c.rt->plural, c.ns, c.name, std::move(c.body));
+    return out;
+  }, py::arg("ub_json"), py::arg("label") = false);
   py::class_<bgc::bench::ChurnDriver>(m, "ChurnDriver")
       .def(py::init([](const std::string& server, const std::string& token, const std::string& prefix,
                        int concurrency, const std::string& gpu_key, const std::string& group,
