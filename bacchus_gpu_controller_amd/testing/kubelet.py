@@ -12,6 +12,7 @@ FakeKubelet:
   * restart() mimics a kubelet restart: stops, wipes the plugin directory (the real
     kubelet deletes every socket there), and serves a fresh kubelet.sock.
 """
+import json
 import os
 import threading
 import time
@@ -118,6 +119,16 @@ class FakeKubelet:
         self.server = None
         self._watchers = []
         self._stopping = False
+        self.registered_devices = {}  # resource -> device ids (the kubelet checkpoint's RegisteredDevices)
+
+    def _write_checkpoint(self):
+        """The kubelet's device-manager checkpoint (<dir>/kubelet_internal_checkpoint), which
+        records the device ids each registered resource listed."""
+        doc = {"Data": {"PodDeviceEntries": None, "RegisteredDevices": self.registered_devices}, "Checksum": 0}
+        tmp = os.path.join(self.dir, ".checkpoint.tmp")
+        with open(tmp, "w") as f:
+            json.dump(doc, f)
+        os.replace(tmp, os.path.join(self.dir, "kubelet_internal_checkpoint"))
 
     # -- Registration service
     def _register(self, req, ctx):
@@ -137,6 +148,11 @@ class FakeKubelet:
                 devs = [(d.ID, d.health, [n.ID for n in d.topology.nodes]) for d in resp.devices]
                 with self.cv:
                     self.device_lists.append((endpoint, devs))
+                    resource = next((r.resource_name for r in reversed(self.registrations) if r.endpoint == endpoint),
+                                    None)
+                    if resource:
+                        self.registered_devices[resource] = [d[0] for d in devs]
+                        self._write_checkpoint()
                     self.cv.notify_all()
                 if self._stopping:
                     break
@@ -184,6 +200,60 @@ class FakeKubelet:
                     return False
                 self.cv.wait(left)
         return True
+
+
+class FakeDevicePlugin:
+    """Another vendor's device plugin (e.g. the GPU Operator's): serves ListAndWatch and
+    GetDevicePluginOptions on <dir>/<socket> with fixed device ids, and registers
+    `resource` with the kubelet when asked to."""
+
+    def __init__(self, plugin_dir, socket_name, device_ids):
+        self.dir, self.socket, self.ids = plugin_dir, socket_name, list(device_ids)
+        self.server = None
+        self._stop = threading.Event()
+
+    def _list_and_watch(self, req, ctx):
+        resp = pb["ListAndWatchResponse"]()
+        for i in self.ids:
+            resp.devices.add(ID=i, health="Healthy")
+        yield resp
+        while not self._stop.is_set() and ctx.is_active():
+            self._stop.wait(0.2)
+
+    def _options(self, req, ctx):
+        return pb["DevicePluginOptions"]()
+
+    def start(self):
+        self.server = grpc.server(futures.ThreadPoolExecutor(max_workers=8))
+        handler = grpc.method_handlers_generic_handler("v1beta1.DevicePlugin", {
+            "ListAndWatch": grpc.unary_stream_rpc_method_handler(
+                self._list_and_watch, request_deserializer=pb["Empty"].FromString,
+                response_serializer=pb["ListAndWatchResponse"].SerializeToString),
+            "GetDevicePluginOptions": grpc.unary_unary_rpc_method_handler(
+                self._options, request_deserializer=pb["Empty"].FromString,
+                response_serializer=pb["DevicePluginOptions"].SerializeToString)})
+        self.server.add_generic_rpc_handlers((handler,))
+        self.server.add_insecure_port("unix://" + os.path.join(self.dir, self.socket))
+        self.server.start()
+        return self
+
+    def register(self, resource):
+        ch = grpc.insecure_channel("unix://" + os.path.join(self.dir, "kubelet.sock"))
+        try:
+            reg = _unary(ch, "/v1beta1.Registration/Register", pb["RegisterRequest"], pb["Empty"])
+            reg(pb["RegisterRequest"](version="v1beta1", endpoint=self.socket, resource_name=resource), timeout=5)
+        finally:
+            ch.close()
+
+    def stop(self):
+        self._stop.set()
+        if self.server is not None:
+            self.server.stop(grace=None)
+            self.server = None
+        try:
+            os.unlink(os.path.join(self.dir, self.socket))
+        except OSError:
+            pass
 
 
 def _build_podresources():

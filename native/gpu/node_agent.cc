@@ -96,6 +96,8 @@ NodeAgentConfig NodeAgentConfig::from_env(const EnvConfig& env) {
   c.cdi_dir = env.str_or("cdi_dir", c.cdi_dir);
   c.dev_root = env.str_or("dev_root", c.dev_root);
   c.sysfs_root = env.str_or("sysfs_root", c.sysfs_root);
+  c.advertiser_check = env.boolean_or("advertiser_check", c.advertiser_check);
+  c.take_over = env.boolean_or("take_over", c.take_over);
   return c;
 }
 
@@ -217,6 +219,41 @@ Value node_status_patch(const NodeAgentConfig& cfg, const std::vector<GpuInfo>& 
                         {"status", status}});
 }
 
+Value foreign_field_owners(const NodeAgentConfig& cfg, const Value& node) {
+  Value out = Value::array();
+  const std::string label_key = "f:" + cfg.label_prefix + ".";
+  const std::string res_key = "f:" + cfg.resource_name;
+  for (const auto& mf : node.get("metadata").get("managedFields").items()) {
+    const std::string manager = mf.get_string("manager");
+    if (manager == kNodeAgentManager) continue;
+    const Value& f = mf.get("fieldsV1");
+    Value labels = Value::array();
+    const Value& lf = f.get("f:metadata").get("f:labels");
+    if (lf.is_object()) {
+      for (const auto& k : lf.keys()) {
+        if (k.rfind(label_key, 0) == 0) labels.push_back(k.substr(2));
+      }
+    }
+    if (!labels.empty()) {
+      out.push_back(Value::object({{"kind", "labels"}, {"manager", manager}, {"operation", mf.get_string("operation")},
+                                   {"fields", labels}}));
+    }
+    // the kubelet writes a device plugin's counts: that is this agent's own plugin unless
+    // the agent advertises through the Node status itself
+    if (manager == "kubelet" && cfg.device_plugin) continue;
+    Value res = Value::array();
+    for (const char* sect : {"f:capacity", "f:allocatable"}) {
+      const Value& sf = f.get("f:status").get(sect);
+      if (sf.is_object() && sf.contains(res_key)) res.push_back(std::string("status.") + (sect + 2) + "." + cfg.resource_name);
+    }
+    if (!res.empty()) {
+      out.push_back(Value::object({{"kind", "capacity"}, {"manager", manager}, {"operation", mf.get_string("operation")},
+                                   {"fields", res}}));
+    }
+  }
+  return out;
+}
+
 NodeAgent::NodeAgent(kube::KubeClient& client, std::unique_ptr<Backend> backend, NodeAgentConfig cfg)
     : client_(client), backend_(std::move(backend)), cfg_(std::move(cfg)) {
   if (cfg_.events) {
@@ -311,6 +348,68 @@ void NodeAgent::init() {
   }
   node_present_ = exists;
   if (!exists) LOG_WARN("node_agent") << "node " << cfg_.node_name << " is not registered yet; waiting for the kubelet";
+  check_advertisers();
+}
+
+Value NodeAgent::advertiser_conflicts() const {
+  std::lock_guard<std::mutex> lk(conflict_mu_);
+  return conflicts_;
+}
+
+bool NodeAgent::check_advertisers() {
+  if (!cfg_.advertiser_check) return false;
+  Value found = Value::array();
+  for (const auto& fp : foreign_plugins_for(cfg_.device_plugin_dir, "kubelet.sock", cfg_.device_plugin_socket,
+                                            cfg_.resource_name, device_ids_for(gpus_))) {
+    Value ids = Value::array();
+    for (size_t k = 0; k < fp.ids.size() && k < 8; ++k) ids.push_back(fp.ids[k]);
+    found.push_back(Value::object({{"kind", "device-plugin"},
+                                   {"socket", cfg_.device_plugin_dir + "/" + fp.socket},
+                                   {"resource", cfg_.resource_name},
+                                   {"devices", static_cast<unsigned long long>(fp.ids.size())},
+                                   {"device_ids", ids},
+                                   {"evidence", fp.via_checkpoint ? "kubelet checkpoint" : "device ids"}}));
+  }
+  try {
+    if (auto node = client_.get_opt(types::Node, "", cfg_.node_name)) {
+      const Value owners = foreign_field_owners(cfg_, *node);
+      for (const auto& o : owners.items()) found.push_back(o);
+    }
+  } catch (const std::exception& e) {
+    LOG_WARN("node_agent") << "advertiser check: reading node " << cfg_.node_name << " failed: " << e.what();
+  }
+  const bool conflict = !found.empty();
+  const bool down = conflict && !cfg_.take_over;
+  const std::string sig = found.dump();
+  bool report;
+  {
+    std::lock_guard<std::mutex> lk(conflict_mu_);
+    report = sig != conflict_sig_;
+    conflict_sig_ = sig;
+    conflicts_ = found;
+  }
+  const bool was_down = standing_down_.exchange(down);
+  auto& reg = metrics::Registry::global();
+  reg.gauge("bgc_node_agent_advertiser_conflicts", "Other advertisers of this node's GPUs found by the last check")
+      .set(static_cast<double>(found.size()));
+  reg.gauge("bgc_node_agent_standing_down", "1 while the agent leaves the GPUs to another advertiser").set(down ? 1 : 0);
+  if (report && conflict) {
+    const std::string what = "another advertiser of " + cfg_.resource_name + " on node " + cfg_.node_name + ": " + sig;
+    if (down) {
+      LOG_ERROR("node_agent") << what << "; standing down: no device-plugin registration and no label or status "
+                              << "writes. Disable the other advertiser (e.g. the GPU Operator's device plugin and "
+                              << "labeller), give this agent another resource_name/label_prefix, or set "
+                              << "CONF_TAKE_OVER=true";
+      node_event("Warning", "GPUAdvertiserConflict", what + "; bgc node agent standing down");
+    } else {
+      LOG_WARN("node_agent") << what << "; CONF_TAKE_OVER=true: advertising anyway";
+      node_event("Warning", "GPUAdvertiserTakeOver", what + "; bgc node agent advertising anyway (take_over)");
+    }
+  } else if (!conflict && was_down) {
+    LOG_INFO("node_agent") << "no other advertiser of " << cfg_.resource_name << " any more; advertising";
+    node_event("Normal", "GPUAdvertiserConflictResolved", "no other advertiser of " + cfg_.resource_name);
+  }
+  return down;
 }
 
 bool NodeAgent::node_up_to_date(const Value& node) const {
@@ -645,6 +744,7 @@ int NodeAgent::healthy_count(std::string* reason) const {
 void NodeAgent::publish() {
   std::lock_guard<std::mutex> lk(publish_mu_);
   if (!cfg_.create_node && !node_present_) return;  // the kubelet registers the Node, not us
+  if (standing_down_) return;                        // another advertiser owns these fields
   std::string reason;
   int healthy = healthy_count(&reason);
   client_.apply(types::Node, "", cfg_.node_name, node_labels_patch(cfg_, gpus_, healthy, diag_outcome()), kNodeAgentManager,
@@ -655,6 +755,15 @@ void NodeAgent::publish() {
   if (!cfg_.device_plugin) mark_advertised();  // capacity/allocatable is the advertisement
   LOG_INFO("node_agent") << "published node " << cfg_.node_name << ": " << cfg_.resource_name << " capacity "
                          << gpus_.size() << ", allocatable " << healthy;
+}
+
+// The plugin object exists from start() on (diagnostics fence it, health flips reach it);
+// its server and kubelet registration start only while no other advertiser is found.
+void NodeAgent::start_plugin() {
+  if (!plugin_ || plugin_started_.exchange(true)) return;
+  plugin_->set_health(healthy_flags());
+  plugin_->start();
+  mark_advertised();  // ListAndWatch serves from here on
 }
 
 void NodeAgent::start() {
@@ -669,8 +778,7 @@ void NodeAgent::start() {
     pc.cdi_dir = cfg_.cdi_dir;
     plugin_ = std::make_unique<DevicePlugin>(gpus_, pc);
     plugin_->set_health(healthy_flags());
-    plugin_->start();
-    mark_advertised();  // ListAndWatch serves from here on
+    if (!standing_down_) start_plugin();
   }
   poller_->on_health_change([this](const Snapshot&) { on_health_changed(); });
   poller_->start();
@@ -689,6 +797,15 @@ void NodeAgent::start() {
   heartbeat_ = std::thread([this] {
     while (!stop_.wait_for(std::chrono::seconds(cfg_.heartbeat_secs))) {
       try {
+        const bool was_down = standing_down_.load();
+        const bool down = check_advertisers();
+        if (down && !was_down && plugin_started_ && !plugin_stopped_.exchange(true)) {
+          // found while advertising: unregister from the kubelet (a stopped plugin is not
+          // restarted; the agent resumes the plugin after a restart once the conflict is gone)
+          plugin_->stop();
+          LOG_ERROR("node_agent") << "device plugin stopped: another advertiser appeared; restart the agent once it is gone";
+        }
+        if (!down && was_down && !plugin_stopped_ && !stop_.cancelled()) start_plugin();
         publish();
       } catch (const std::exception& e) {
         LOG_ERROR("node_agent") << "heartbeat publish failed: " << e.what();
@@ -707,8 +824,11 @@ void NodeAgent::start() {
         LOG_WARN("node_agent") << "node " << cfg_.node_name << " deleted; re-creating";
       } else {
         node_present_ = true;
+        if (standing_down_) return;  // the heartbeat re-checks the other advertiser
         if (node_up_to_date(*obj)) return;
         LOG_INFO("node_agent") << "node " << cfg_.node_name << " (re)registered or drifted; re-publishing";
+        // drift may be another manager writing the same labels: look before forcing ours back
+        check_advertisers();
       }
       try {
         publish();
@@ -776,6 +896,12 @@ Value NodeAgent::describe() const {
                                      {"diagnostics", startup_diag_ms_},
                                      {"first_advertise", first_advertise_ms_.load()}});
   if (plugin_) out["device_plugin"] = plugin_->describe();
+  out["advertiser"] = Value::object({{"standing_down", standing_down_.load()},
+                                     {"take_over", cfg_.take_over},
+                                     {"check", cfg_.advertiser_check},
+                                     {"plugin_started", plugin_started_.load()},
+                                     {"plugin_stopped", plugin_stopped_.load()},
+                                     {"conflicts", advertiser_conflicts()}});
   return out;
 }
 

@@ -116,6 +116,18 @@ struct NodeAgentConfig {
   std::string cdi_dir = "/var/run/cdi";
   std::string dev_root = "/dev";
   std::string sysfs_root = "/sys";
+  // Coexistence with another advertiser of the same GPUs (an MI355X node commonly runs
+  // AMD's GPU Operator: its device plugin registers amd.com/gpu and its labeller owns
+  // amd.com/gpu.* labels).  At start and on every heartbeat the agent looks for
+  //   * another live device plugin in device_plugin_dir serving resource_name
+  //     (foreign_plugins_for), and
+  //   * another field manager on the Node owning label_prefix.* labels or
+  //     status.capacity/allocatable[resource_name] (foreign_field_owners);
+  // on a finding it logs an error, records a Warning Event (GPUAdvertiserConflict) and
+  // stands down: no device-plugin registration, no label or status writes.  take_over
+  // (CONF_TAKE_OVER) advertises anyway (Event GPUAdvertiserTakeOver).
+  bool advertiser_check = true;
+  bool take_over = false;
   static NodeAgentConfig from_env(const EnvConfig& env);
 };
 
@@ -140,6 +152,11 @@ json::Value node_labels_patch(const NodeAgentConfig& cfg, const std::vector<GpuI
                               const DiagOutcome& diag);
 json::Value node_status_patch(const NodeAgentConfig& cfg, const std::vector<GpuInfo>& gpus, int healthy,
                               const std::string& unhealthy_reason);
+// Field managers of `node` other than this agent that own what it advertises:
+// [{"kind":"labels"|"capacity","manager":..,"operation":..,"fields":[..]}].  The kubelet's
+// capacity/allocatable entries are its device-plugin bookkeeping and count only when the
+// agent itself advertises through the Node status (no device plugin of its own).
+json::Value foreign_field_owners(const NodeAgentConfig& cfg, const json::Value& node);
 
 class NodeAgent {
  public:
@@ -164,6 +181,11 @@ class NodeAgent {
   // GPU's verdict changed (and then re-publishes health).  `force` ignores allocation.
   bool run_diagnostics(bool at_start = false);
   DiagOutcome diag_outcome() const;
+  // Another advertiser found by the last check (see NodeAgentConfig::advertiser_check).
+  bool standing_down() const { return standing_down_.load(); }
+  json::Value advertiser_conflicts() const;
+  // Runs the coexistence check now; returns true when the agent stands down.
+  bool check_advertisers();
 
  private:
   int healthy_count(std::string* reason) const;
@@ -198,6 +220,13 @@ class NodeAgent {
   std::atomic<bool> node_present_{true};
   std::atomic<uint64_t> publishes_{0};
   std::unique_ptr<kube::EventRecorder> events_;
+  std::atomic<bool> standing_down_{false};
+  std::atomic<bool> plugin_started_{false};
+  std::atomic<bool> plugin_stopped_{false};  // stopped for a conflict found while advertising
+  mutable std::mutex conflict_mu_;
+  json::Value conflicts_ = json::Value::array();
+  std::string conflict_sig_;  // last conflict set reported (one Event per change)
+  void start_plugin();
   std::mutex event_mu_;
   std::vector<int> event_state_;  // per GPU: -1 not reported yet, 1 healthy, 0 unhealthy
   void emit_health_events();
