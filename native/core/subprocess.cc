@@ -17,10 +17,14 @@ extern char** environ;
 namespace bgc {
 
 RunResult run_command(const std::vector<std::string>& argv, const std::vector<std::pair<std::string, std::string>>& env,
-                      int timeout_ms, const CancelToken* cancel) {
+                      int timeout_ms, const CancelToken* cancel, const std::vector<std::string>& unset) {
   RunResult res;
   if (argv.empty()) {
     res.err = "empty command";
+    return res;
+  }
+  if (cancel && cancel->cancelled()) {  // shutting down: start nothing
+    res.cancelled = true;
     return res;
   }
   int out_pipe[2], err_pipe[2];
@@ -41,6 +45,7 @@ RunResult run_command(const std::vector<std::string>& argv, const std::vector<st
     if (eq) merged[std::string(*e, static_cast<size_t>(eq - *e))] = eq + 1;
   }
   for (const auto& [k, v] : env) merged[k] = v;
+  for (const auto& k : unset) merged.erase(k);
   std::vector<std::string> env_strs;
   for (const auto& [k, v] : merged) env_strs.push_back(k + "=" + v);
   std::vector<char*> envp, args;

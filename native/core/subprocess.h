@@ -20,8 +20,9 @@ struct RunResult {
 
 // argv[0] is looked up on PATH when it has no '/'.  `env` entries are added to (and
 // override) the parent's environment.  The child is killed after timeout_ms, or as soon
-// as `cancel` is cancelled (checked every 100 ms).
+// as `cancel` is cancelled (checked every 100 ms); nothing is started when it already is.
+// `unset` names parent variables the child must not inherit.
 RunResult run_command(const std::vector<std::string>& argv, const std::vector<std::pair<std::string, std::string>>& env,
-                      int timeout_ms, const CancelToken* cancel = nullptr);
+                      int timeout_ms, const CancelToken* cancel = nullptr, const std::vector<std::string>& unset = {});
 
 }  // namespace bgc

@@ -493,6 +493,13 @@ json::Value judge_diag(const json::Value& result, const DiagFloors& fl) {
     failures.push_back("MFMA GEMM differs from the host fp32 product");
   }
   if (result.get("error").is_string()) failures.push_back(result.get_string("error"));
+  // a section that failed to run (a HIP fault, a worker that timed out) carries the cause
+  // as {"error": ...}: that is a failure in its own right, whatever the floors say
+  static const char* const kSections[] = {"hbm", "hbm_walk", "mfma", "lowp", "burn", "pcie", "soak", "gemm"};
+  for (const char* sect : kSections) {
+    const json::Value& v = result.get(sect);
+    if (v.is_object() && v.get("error").is_string()) failures.push_back(std::string(sect) + ": " + v.get_string("error"));
+  }
   out["failures"] = failures;
   out["passed"] = failures.items().empty();
   return out;

@@ -168,9 +168,15 @@ std::string self_exe() {
 Value run_worker(const std::string& exe, const Value& request, int visible_device, int timeout_ms,
                  const CancelToken* cancel = nullptr) {
   std::vector<std::pair<std::string, std::string>> env{{"BGC_DIAG_REQUEST", request.dump()}};
-  // only its own GPU: HSA opens no other device, so the worker leaves no footprint there
+  // Device numbering: `visible_device` is a ROCr index over ALL of the node's GPUs (the
+  // "devices" enumeration below runs with nothing hidden, so its HIP order is ROCr's).
+  // Visibility variables the agent itself may carry would renumber or hide devices in the
+  // worker, so none is inherited; the worker then sees exactly its own GPU (HSA opens no
+  // other device, so it leaves no footprint there) and checks its BDF against the request.
+  std::vector<std::string> unset{"HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "GPU_DEVICE_ORDINAL"};
   if (visible_device >= 0) env.emplace_back("ROCR_VISIBLE_DEVICES", std::to_string(visible_device));
-  RunResult r = run_command({exe, "--diag-worker"}, env, timeout_ms, cancel);
+  else unset.push_back("ROCR_VISIBLE_DEVICES");
+  RunResult r = run_command({exe, "--diag-worker"}, env, timeout_ms, cancel, unset);
   if (r.cancelled) throw std::runtime_error("diagnostics worker stopped: the agent is shutting down");
   if (r.exit_code != 0) {
     throw std::runtime_error("diagnostics worker " +
@@ -223,6 +229,7 @@ class ProcessDiagEngine : public DiagEngine {
     Value req = Value::object({{"op", "burn"}, {"backend", kind_}, {"fixture", fixture_}, {"gpu_hip_device", dev},
                                {"duration_ms", duration_ms}, {"dtype", burn_dtype_name(dtype)},
                                {"seed", static_cast<unsigned long long>(seed)}, {"start_at_ns", static_cast<long long>(at)}});
+    if (auto it = bdfs_.find(dev); it != bdfs_.end()) req["expect_bdf"] = it->second;
     const auto spawned = std::chrono::steady_clock::now();
     Value r = run_worker(exe_, req, dev, duration_ms + start_lead_ms() + 60000, cancel_);
     note_ready(r, spawned);
@@ -246,7 +253,11 @@ class ProcessDiagEngine : public DiagEngine {
  public:
 
  private:
+  void set_device_bdfs(std::map<int, std::string> bdfs) override { bdfs_ = std::move(bdfs); }
+
+ private:
   std::string exe_, kind_, fixture_, lock_;
+  std::map<int, std::string> bdfs_;  // ROCr device -> the BDF its worker must find
   const CancelToken* cancel_;
   std::atomic<int> slowest_ready_ms_{0};
 };
@@ -379,6 +390,22 @@ int diag_worker_main() {
       auto backend = make_backend(req.get_string("backend", "amdsmi"), req.get_string("fixture"));
       // a mock backend with a diagnostics script (CPU tests of the worker plumbing)
       const bool scripted = backend->diag_script().is_object();
+      // the one GPU this worker sees must be the one the agent means (a renumbered or
+      // hidden device would put a burn or a verdict on another GPU, maybe a tenant's)
+      const std::string expect = op == "checks" ? req.get("gpu").get_string("bdf") : req.get_string("expect_bdf");
+      if (!scripted && !expect.empty()) {
+        auto lower = [](std::string v) {
+          for (auto& c : v) c = static_cast<char>(std::tolower(static_cast<unsigned char>(c)));
+          return v;
+        };
+        Diag& d = Diag::instance();
+        const std::string got = d.device_count() > 0 ? d.device_bdf(dev) : std::string("no device");
+        if (lower(got) != lower(expect)) {
+          throw std::runtime_error("diagnostics worker opened GPU " + got + " (ROCR_VISIBLE_DEVICES=" +
+                                   (std::getenv("ROCR_VISIBLE_DEVICES") ? std::getenv("ROCR_VISIBLE_DEVICES") : "") +
+                                   "), expected " + expect + ": not diagnosing another GPU");
+        }
+      }
       std::unique_ptr<DiagEngine> engine = scripted ? make_scripted_diag_engine(*backend)
                                                     : std::make_unique<HipDiagEngine>(req.get_string("pcie_lock"));
       // a script names GPUs by the agent's device number, not the worker's only device 0

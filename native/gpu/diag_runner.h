@@ -20,6 +20,7 @@
 
 #include <chrono>
 #include <cstdint>
+#include <map>
 #include <memory>
 #include <string>
 #include <vector>
@@ -58,6 +59,8 @@ class DiagEngine {
   // (steady clock; the epoch = now) so that GPUs burning together start together.
   virtual json::Value burn(int hip_device, int duration_ms, uint32_t seed, int dtype,
                            std::chrono::steady_clock::time_point start_at) = 0;
+  // device -> PCI BDF of the GPU it must be (worker engines verify it before running).
+  virtual void set_device_bdfs(std::map<int, std::string>) {}
 };
 
 // In this process (the python bindings, tools): the first call initialises HIP here.

@@ -492,6 +492,17 @@ void NodeAgent::setup_diag() {
     }
   }
   hip_devs_ = hip_devices_for(gpus_, bdfs);
+  {
+    // workers verify that the one GPU they see is the one meant (BDF); partitions share a
+    // BDF and are told apart by amdsmi's numbering only
+    std::map<std::string, int> count;
+    for (const auto& g : gpus_) count[g.bdf]++;
+    std::map<int, std::string> by_dev;
+    for (size_t i = 0; i < gpus_.size(); ++i) {
+      if (!gpus_[i].bdf.empty() && count[gpus_[i].bdf] == 1) by_dev[hip_devs_[i]] = gpus_[i].bdf;
+    }
+    engine_->set_device_bdfs(std::move(by_dev));
+  }
   LOG_INFO("node_agent") << "diagnostics engine " << engine_->name() << (diag_in_process_ ? " (in process)" : " (worker processes)")
                          << ", " << bdfs.size() << " HIP devices named by BDF";
 }
@@ -644,6 +655,15 @@ bool NodeAgent::run_diagnostics(bool at_start) {
     }
     for (auto& t : threads) t.join();
   }
+  // The agent is stopping (a DaemonSet rolling update): its workers were killed, so these
+  // results say nothing about the GPUs.  Drop the pass — no verdicts, gauges, Events or
+  // health change; the Unfence guard releases fenced GPUs.
+  auto abandoned = [&](const char* phase) {
+    if (!stop_.cancelled()) return false;
+    LOG_WARN("node_agent") << "diagnostics pass abandoned " << phase << ": the agent is shutting down";
+    return true;
+  };
+  if (abandoned("after the checks")) return false;
   // Phase 2: the node-level burn — every GPU under diagnosis at full MFMA load together.
   Value node = Value();
   std::vector<std::vector<std::string>> node_failures(todo.size());
@@ -653,6 +673,7 @@ bool NodeAgent::run_diagnostics(bool at_start) {
     node_failures = judge_node_burn(nb, cfg_.diag_floors);
     for (size_t k = 0; k < todo.size(); ++k) results[todo[k]]["burn"] = nb.per_gpu[k];
     node = nb.node;
+    if (abandoned("after the burn")) return false;
     auto& reg = metrics::Registry::global();
     reg.gauge("amd_gpu_diag_node_burn_power_watts", "Diagnostics: peak summed GPU power during the node-level burn")
         .set(node.get("power_sum_max_w").as_double());

@@ -269,5 +269,13 @@ def test_worker_processes_run_the_pass_and_stop_with_the_agent(nat, tmp_path):
             time.sleep(0.3)
             assert not [w for w in workers if os.path.exists(f"/proc/{w}") and
                         open(f"/proc/{w}/stat").read().split()[2] != "Z"], "a worker outlived the agent"
+            # a routine shutdown is not a GPU failure: the killed pass is dropped, with no
+            # verdict, Event or health change published on the way out
+            assert "diagnostics pass abandoned" in agent.output()
+            evs = [e for e in c.admin.list("events", namespace="default")["items"]
+                   if e["involvedObject"]["name"] == "mi355x-workers"]
+            assert not [e for e in evs if e["reason"] in ("GPUDiagnosticsFailed", "GPUUnhealthy")], evs
+            labels = c.admin.get("nodes", "mi355x-workers")["metadata"]["labels"]
+            assert labels["amd.com/gpu.diag"] == "passed" and labels["amd.com/gpu.healthy-count"] == "2"
     finally:
         kubelet.stop()

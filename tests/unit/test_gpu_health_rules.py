@@ -174,6 +174,18 @@ def test_judge_diag_floors(nat):
     assert not r["passed"] and len(r["failures"]) == 2
 
 
+def test_judge_diag_section_errors_are_failures(nat):
+    """A section that could not run (a HIP fault, a worker timeout) reports {"error": ...};
+    the cause must reach the failures list even when every floor is off."""
+    floors_off = json.dumps({k: 0 for k in ("min_burn_tflops", "min_burn_sustain", "max_burn_hotspot_c",
+                                            "max_burn_thermal_violation_pct")})
+    crashed = dict(MI355X_MEASURED, burn={"error": "diagnostics worker timed out"})
+    r = json.loads(nat.judge_diag(json.dumps(crashed), floors_off))
+    assert not r["passed"] and r["failures"] == ["burn: diagnostics worker timed out"]
+    r = json.loads(nat.judge_diag(json.dumps(dict(MI355X_MEASURED, pcie={"error": "hipMemcpy: fault"}))))
+    assert "pcie: hipMemcpy: fault" in r["failures"]
+
+
 def test_judge_diag_mx_lowp_section(nat):
     """The MX fp8/fp4 matrix-core check: any wrong tile, wrong accumulators or a rate under
     its floor fails the GPU, and the failure names the variant."""
