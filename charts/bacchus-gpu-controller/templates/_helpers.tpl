@@ -38,7 +38,13 @@ app.kubernetes.io/instance: {{ .Release.Name }}
      Service also routed to the plain-HTTP controller/synchronizer pods: SURVEY Q1).
      Call with (dict "root" $ "component" "x"). */}}
 {{- define "bgc.selectorLabels" -}}
+{{- if eq .component "node-agent" }}
+{{- /* the DaemonSet's pods carry their own name, so the reference-shaped Deployment
+       selectors (name + instance only) never match a node-agent pod */}}
+app.kubernetes.io/name: {{ printf "%s-node-agent" (include "bgc.name" .root) | trunc 63 | trimSuffix "-" }}
+{{- else }}
 app.kubernetes.io/name: {{ include "bgc.name" .root }}
+{{- end }}
 app.kubernetes.io/instance: {{ .root.Release.Name }}
 app.kubernetes.io/component: {{ .component }}
 {{- end }}

@@ -700,6 +700,11 @@ struct ApiServer::Impl {
       auto it = tokens.find(auth.substr(7));
       if (it == tokens.end()) throw StatusError(401, "Unauthorized", "Unauthorized");
       u = it->second;
+    } else if (!req.peer_cn.empty()) {
+      // x509 authenticator: CN is the user name, each O a group
+      u.username = req.peer_cn;
+      u.groups = req.peer_orgs;
+      u.groups.push_back("system:authenticated");
     } else if (opts.anonymous_admin) {
       u.username = "system:admin";
       u.groups = {"system:masters", "system:authenticated"};
@@ -2254,6 +2259,19 @@ struct ApiServer::Impl {
     try {
       if (inject_fault(req, w)) return;
       UserInfo user = authenticate(req);
+      if (req.path == "/apis/authentication.k8s.io/v1/selfsubjectreviews" && req.method == "POST") {
+        // `kubectl auth whoami`: who the request authenticated as
+        Value ui = Value::object({{"username", user.username}});
+        if (!user.uid.empty()) ui["uid"] = user.uid;
+        Value groups = Value::array();
+        for (const auto& g : user.groups) groups.push_back(g);
+        ui["groups"] = groups;
+        w.send_json(201, Value::object({{"kind", "SelfSubjectReview"},
+                                        {"apiVersion", "authentication.k8s.io/v1"},
+                                        {"metadata", Value::object({{"creationTimestamp", Value()}})},
+                                        {"status", Value::object({{"userInfo", ui}})}}).dump());
+        return;
+      }
       if (req.path == "/api" || req.path == "/apis") {
         discovery(req.path, w);
         return;
@@ -2313,7 +2331,9 @@ void ApiServer::start() {
   so.name = "apiserver";
   so.idle_timeout_ms = 300000;
   if (!impl_->opts.tls_cert_file.empty()) {
-    so.tls = net::TlsContext::server_from_files(impl_->opts.tls_cert_file, impl_->opts.tls_key_file);
+    so.tls = net::TlsContext::server_from_files(
+        impl_->opts.tls_cert_file, impl_->opts.tls_key_file,
+        impl_->opts.client_ca_file.empty() ? "" : net::read_file(impl_->opts.client_ca_file));
   }
   impl_->server = std::make_unique<http::Server>(so);
   Impl* im = impl_.get();

@@ -30,6 +30,9 @@ struct Options {
   std::string token_file;         // CSV: token,user,uid,"group1,group2"
   bool anonymous_admin = true;    // no token => system:admin in system:masters
   std::string tls_cert_file;      // serve HTTPS when set
+  // x509 client-certificate authentication (kube-apiserver --client-ca-file): a verified
+  // client certificate authenticates as user CN with groups O when no bearer token is sent
+  std::string client_ca_file;
   std::string tls_key_file;
   // "namespace/service" -> "host:port": where a webhook's clientConfig.service is reachable.
   std::map<std::string, std::string> service_overrides;

@@ -51,6 +51,7 @@ int main(int argc, char** argv) {
     else if (a == "--no-anonymous") o.anonymous_admin = false;
     else if (a == "--tls-cert") o.tls_cert_file = next();
     else if (a == "--tls-key") o.tls_key_file = next();
+    else if (a == "--client-ca-file") o.client_ca_file = next();
     else if (a == "--bookmark-ms") o.bookmark_interval_ms = std::atoi(next().c_str());
     else if (a == "--history") o.history_limit = static_cast<size_t>(std::atol(next().c_str()));
     else if (a == "--watch-coalesce-us") o.watch_coalesce_us = std::atoi(next().c_str());

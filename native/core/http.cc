@@ -488,6 +488,9 @@ void Server::serve_conn(int fd, std::string remote) {
     std::lock_guard<std::mutex> lk(conns_mu_);
     conns_[fd] = s.get();
   }
+  std::string peer_cn;
+  std::vector<std::string> peer_orgs;
+  s->peer_identity(&peer_cn, &peer_orgs);
   if (opts_.tls && opts_.http2 && static_cast<net::TlsStream&>(*s).alpn() == "h2") {
     serve_h2(fd, std::move(s), remote);  // unregisters the stream before releasing it
     return;
@@ -496,6 +499,8 @@ void Server::serve_conn(int fd, std::string remote) {
   while (!stop_.cancelled()) {
     Request req;
     req.remote = remote;
+    req.peer_cn = peer_cn;
+    req.peer_orgs = peer_orgs;
     std::string line;
     // wait for the request line, waking periodically to observe shutdown
     int idle = 0;
@@ -686,9 +691,14 @@ void Server::serve_h2(int fd, std::unique_ptr<net::Stream> s, const std::string&
     }
     server_time.add(static_cast<double>(metrics::now_ns() - t0) * 1e-9);
   };
-  auto take_request = [remote](const std::shared_ptr<http2::Connection>& c, const std::shared_ptr<http2::Stream>& st,
-                               Request& req) {
+  std::string peer_cn;
+  std::vector<std::string> peer_orgs;
+  s->peer_identity(&peer_cn, &peer_orgs);
+  auto take_request = [remote, peer_cn, peer_orgs](const std::shared_ptr<http2::Connection>& c,
+                                                  const std::shared_ptr<http2::Stream>& st, Request& req) {
     req.remote = remote;
+    req.peer_cn = peer_cn;
+    req.peer_orgs = peer_orgs;
     bool ok = c->locked([&] {
       for (auto& [k, v] : st->headers) {
         if (k == ":method") req.method = v;

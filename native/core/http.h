@@ -53,6 +53,9 @@ struct Request {
   Headers headers;
   std::string body;
   std::string remote;
+  // verified TLS client certificate (net::Stream::peer_identity): CN and O values
+  std::string peer_cn;
+  std::vector<std::string> peer_orgs;
   std::string query_param(const std::string& name, const std::string& dflt = "") const;
   bool has_query_param(const std::string& name) const;
   std::map<std::string, std::string> query_params() const;

@@ -153,24 +153,50 @@ void tune_ctx(SSL_CTX* c) {
 }
 }  // namespace
 
-std::shared_ptr<TlsContext> TlsContext::server_from_pem(const std::string& cert_pem, const std::string& key_pem) {
+// Every certificate in a PEM bundle into the context's verification store; the count.
+static int add_ca_pem(SSL_CTX* c, const std::string& ca_pem) {
+  X509_STORE* store = SSL_CTX_get_cert_store(c);
+  BIO* b = BIO_new_mem_buf(ca_pem.data(), static_cast<int>(ca_pem.size()));
+  int added = 0;
+  while (X509* x = PEM_read_bio_X509(b, nullptr, nullptr, nullptr)) {
+    X509_STORE_add_cert(store, x);
+    X509_free(x);
+    ++added;
+  }
+  BIO_free(b);
+  ERR_clear_error();
+  return added;
+}
+
+std::shared_ptr<TlsContext> TlsContext::server_from_pem(const std::string& cert_pem, const std::string& key_pem,
+                                                        const std::string& client_ca_pem) {
   SSL_CTX* c = SSL_CTX_new(TLS_server_method());
   if (!c) throw NetError("SSL_CTX_new: " + ssl_errors());
   auto ctx = wrap_ctx(c);
   tune_ctx(c);
   load_cert_chain_pem(c, cert_pem, key_pem);
+  if (!client_ca_pem.empty()) {
+    // the kube-apiserver's --client-ca-file: a client certificate is requested and, when
+    // one is sent, must verify; clients with bearer tokens send none
+    if (!add_ca_pem(c, client_ca_pem)) throw NetError("no certificates found in the client CA bundle");
+    SSL_CTX_set_verify(c, SSL_VERIFY_PEER | SSL_VERIFY_CLIENT_ONCE, nullptr);
+    static const unsigned char kSid[] = "bgc-x509";
+    SSL_CTX_set_session_id_context(c, kSid, sizeof(kSid) - 1);
+  }
   auto t = std::make_shared<TlsContext>();
   t->ctx_ = ctx;
+  t->client_ca_pem_ = client_ca_pem;
   t->server_ = true;
   return t;
 }
 
-std::shared_ptr<TlsContext> TlsContext::server_from_files(const std::string& cert_path, const std::string& key_path) {
-  return server_from_pem(read_file(cert_path), read_file(key_path));
+std::shared_ptr<TlsContext> TlsContext::server_from_files(const std::string& cert_path, const std::string& key_path,
+                                                          const std::string& client_ca_pem) {
+  return server_from_pem(read_file(cert_path), read_file(key_path), client_ca_pem);
 }
 
 void TlsContext::reload_from_files(const std::string& cert_path, const std::string& key_path) {
-  auto fresh = server_from_files(cert_path, key_path);
+  auto fresh = server_from_files(cert_path, key_path, client_ca_pem_);
   if (h2_) apply_alpn(fresh->ctx_.get());
   std::lock_guard<std::mutex> lk(mu_);
   ctx_ = fresh->ctx_;
@@ -220,17 +246,7 @@ std::shared_ptr<TlsContext> TlsContext::client(const std::string& ca_pem, bool i
     if (ca_pem.empty()) {
       SSL_CTX_set_default_verify_paths(c);
     } else {
-      X509_STORE* store = SSL_CTX_get_cert_store(c);
-      BIO* b = BIO_new_mem_buf(ca_pem.data(), static_cast<int>(ca_pem.size()));
-      int added = 0;
-      while (X509* x = PEM_read_bio_X509(b, nullptr, nullptr, nullptr)) {
-        X509_STORE_add_cert(store, x);
-        X509_free(x);
-        ++added;
-      }
-      BIO_free(b);
-      ERR_clear_error();
-      if (!added) throw NetError("no certificates found in CA bundle");
+      if (!add_ca_pem(c, ca_pem)) throw NetError("no certificates found in CA bundle");
     }
     SSL_CTX_set_verify(c, SSL_VERIFY_PEER, nullptr);
   } else {
@@ -303,6 +319,34 @@ TlsStream::~TlsStream() {
 bool TlsStream::has_buffered() const {
   std::lock_guard<std::mutex> lk(ssl_mu_);
   return ssl_ && SSL_has_pending(ssl_) == 1;  // decrypted or read-ahead (unprocessed) bytes
+}
+
+bool TlsStream::peer_identity(std::string* cn, std::vector<std::string>* orgs) const {
+  std::lock_guard<std::mutex> lk(ssl_mu_);
+  if (!ssl_) return false;
+  X509* peer = SSL_get0_peer_certificate(ssl_);
+  if (!peer || SSL_get_verify_result(ssl_) != X509_V_OK) return false;
+  const X509_NAME* subj = X509_get_subject_name(peer);
+  auto text = [](const X509_NAME_ENTRY* e) {
+    const ASN1_STRING* d = X509_NAME_ENTRY_get_data(e);
+    unsigned char* utf8 = nullptr;
+    const int n = ASN1_STRING_to_UTF8(&utf8, d);
+    std::string v = n > 0 ? std::string(reinterpret_cast<char*>(utf8), static_cast<size_t>(n)) : std::string();
+    OPENSSL_free(utf8);
+    return v;
+  };
+  std::string name;
+  std::vector<std::string> groups;
+  for (int i = 0, n = X509_NAME_entry_count(subj); i < n; ++i) {
+    const X509_NAME_ENTRY* e = X509_NAME_get_entry(subj, i);
+    const int nid = OBJ_obj2nid(X509_NAME_ENTRY_get_object(e));
+    if (nid == NID_commonName) name = text(e);
+    else if (nid == NID_organizationName) groups.push_back(text(e));
+  }
+  if (name.empty()) return false;
+  if (cn) *cn = name;
+  if (orgs) *orgs = groups;
+  return true;
 }
 
 std::string TlsStream::alpn() const {

@@ -13,6 +13,7 @@
 #include <stdexcept>
 #include <string>
 #include <sys/types.h>
+#include <vector>
 
 namespace bgc::net {
 
@@ -31,6 +32,14 @@ class Stream {
   virtual void shutdown() = 0;
   virtual int fd() const = 0;
   virtual bool has_buffered() const { return false; }
+  // A TLS server connection whose client presented a certificate that verified against
+  // the server's client CA: its subject CN and O values (the Kubernetes x509
+  // authenticator's username and groups).  false otherwise.
+  virtual bool peer_identity(std::string* cn, std::vector<std::string>* orgs) const {
+    (void)cn;
+    (void)orgs;
+    return false;
+  }
   bool write_all(const std::string& s) { return write_all(s.data(), s.size()); }
 };
 
@@ -51,10 +60,14 @@ class TcpStream : public Stream {
 // connections pick up the new certificate, established ones keep the old context.
 class TlsContext {
  public:
+  // client_ca_pem: also ask clients for a certificate and verify it against this CA
+  // (optional: clients without one still connect; see TlsStream::peer_identity).
   static std::shared_ptr<TlsContext> server_from_files(const std::string& cert_path,
-                                                       const std::string& key_path);
+                                                       const std::string& key_path,
+                                                       const std::string& client_ca_pem = "");
   static std::shared_ptr<TlsContext> server_from_pem(const std::string& cert_pem,
-                                                     const std::string& key_pem);
+                                                     const std::string& key_pem,
+                                                     const std::string& client_ca_pem = "");
   // ca_pem empty + insecure=false => system roots (with_native_roots).
   static std::shared_ptr<TlsContext> client(const std::string& ca_pem, bool insecure,
                                             const std::string& client_cert_pem = "",
@@ -74,6 +87,7 @@ class TlsContext {
   void apply_alpn(SSL_CTX* c) const;
   mutable std::mutex mu_;
   std::shared_ptr<SSL_CTX> ctx_;
+  std::string client_ca_pem_;  // kept for reloads
   bool server_ = false;
   bool insecure_ = false;
   std::atomic<bool> h2_{false};
@@ -91,6 +105,7 @@ class TlsStream : public Stream {
   void shutdown() override;
   int fd() const override { return fd_; }
   bool has_buffered() const override;
+  bool peer_identity(std::string* cn, std::vector<std::string>* orgs) const override;
   // Protocol selected by ALPN during the handshake ("" when none was negotiated).
   std::string alpn() const;
 

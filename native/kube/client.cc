@@ -213,26 +213,37 @@ KubeConfig KubeConfig::infer() {
 
 // ---------------------------------------------------------------------------
 
-KubeClient::KubeClient(KubeConfig cfg) : cfg_(std::move(cfg)) {
+std::shared_ptr<http::Client> KubeClient::make_http(const KubeConfig& cfg) {
   http::ClientOptions o;
-  o.base_url = cfg_.server;
-  o.timeout_ms = cfg_.timeout_ms;
-  o.tls_server_name = cfg_.tls_server_name;
-  o.http2 = cfg_.http2;
-  if (cfg_.server.rfind("https", 0) == 0) {
-    o.tls = net::TlsContext::client(cfg_.ca_pem, cfg_.insecure, cfg_.client_cert_pem, cfg_.client_key_pem);
+  o.base_url = cfg.server;
+  o.timeout_ms = cfg.timeout_ms;
+  o.tls_server_name = cfg.tls_server_name;
+  // BGC_KUBE_HTTP2=1: request/response calls multiplexed over one HTTP/2 connection
+  const char* h2 = std::getenv("BGC_KUBE_HTTP2");
+  o.http2 = cfg.http2 || (h2 && std::string(h2) == "1");
+  if (cfg.server.rfind("https", 0) == 0) {
+    o.tls = net::TlsContext::client(cfg.ca_pem, cfg.insecure, cfg.client_cert_pem, cfg.client_key_pem);
   }
-  if (cfg_.exec && cfg_.client_cert_pem.empty()) {
-    // an exec plugin may hand out a client certificate instead of (or with) a token: it
-    // has to be known before the TLS context is built
-    plugin_token(true);
-    if (!cfg_.client_cert_pem.empty() && o.tls) {
-      o.tls = net::TlsContext::client(cfg_.ca_pem, cfg_.insecure, cfg_.client_cert_pem, cfg_.client_key_pem);
-    }
-  }
-  http_ = std::make_unique<http::Client>(o);
+  return std::make_shared<http::Client>(o);
+}
+
+KubeClient::KubeClient(KubeConfig cfg) : cfg_(std::move(cfg)) {
+  // an exec plugin may hand out a client certificate instead of (or with) a token: it has
+  // to be known before the first TLS context is built
+  if (cfg_.exec && cfg_.client_cert_pem.empty()) plugin_token(true);
+  http_ = make_http(cfg_);
   if (!has_plugin()) token_ = cfg_.token;
   token_read_ = std::chrono::steady_clock::now();
+}
+
+KubeConfig KubeClient::config() const {
+  std::lock_guard<std::mutex> lk(token_mu_);
+  return cfg_;
+}
+
+std::shared_ptr<http::Client> KubeClient::http() const {
+  std::lock_guard<std::mutex> lk(http_mu_);
+  return http_;
 }
 
 namespace {
@@ -328,9 +339,18 @@ std::string KubeClient::plugin_token(bool force) {
     }
     const Value& st = cred.get("status");
     token_ = st.get_string("token");
-    if (!st.get_string("clientCertificateData").empty()) {
-      cfg_.client_cert_pem = st.get_string("clientCertificateData");
-      cfg_.client_key_pem = st.get_string("clientKeyData");
+    const std::string cert = st.get_string("clientCertificateData"), key = st.get_string("clientKeyData");
+    if (!cert.empty() && (cert != cfg_.client_cert_pem || key != cfg_.client_key_pem)) {
+      cfg_.client_cert_pem = cert;
+      cfg_.client_key_pem = key;
+      // a new client certificate: new connections must present it, so the TLS context
+      // and the connection pool are rebuilt (not at construction: no client exists yet)
+      std::lock_guard<std::mutex> hl(http_mu_);
+      if (http_) {
+        http_ = make_http(cfg_);
+        tls_rebuilds_.fetch_add(1);
+        LOG_INFO("kube") << "exec credential plugin rotated the client certificate; TLS context rebuilt";
+      }
     }
     if (token_.empty() && cfg_.client_cert_pem.empty()) {
       throw std::runtime_error("exec credential plugin returned neither a token nor a client certificate");
@@ -431,7 +451,7 @@ http::Response KubeClient::raw(const std::string& method, const std::string& pat
     http::Headers h = auth_headers();
     if (!body.empty() || method == "POST" || method == "PUT" || method == "PATCH") h.set("Content-Type", content_type);
     if (!accept.empty()) h.set("Accept", accept);
-    http::Response r = http_->request(method, path, body, &h);
+    http::Response r = http()->request(method, path, body, &h);
     if (r.status == 401 && has_plugin() && attempt == 0) {
       // the plugin's credential was revoked or rotated early: fetch a fresh one, retry once
       LOG_INFO("kube") << method << " " << path << ": 401, refreshing the plugin credential";
@@ -580,7 +600,7 @@ std::unique_ptr<http::StreamingResponse> KubeClient::watch(const ResourceType& r
                                                           {"resourceVersionMatch", o.send_initial_events ? "NotOlderThan" : ""}});
   http::Headers h = auth_headers();
   if (o.metadata_only) h.set("Accept", kAcceptMetadata);
-  auto s = http_->stream("GET", path, &h);
+  auto s = http()->stream("GET", path, &h);
   if (s->status < 200 || s->status >= 300) {
     http::Response r;
     r.status = s->status;

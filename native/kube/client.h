@@ -162,7 +162,9 @@ class KubeClient {
                    const std::string& content_type = "application/json", const std::string& accept = "");
   http::Response raw(const std::string& method, const std::string& path, const std::string& body = "",
                      const std::string& content_type = "application/json", const std::string& accept = "");
-  const KubeConfig& config() const { return cfg_; }
+  // A snapshot: an exec plugin's refresh may replace the client certificate at any time.
+  KubeConfig config() const;
+  uint64_t tls_rebuilds() const { return tls_rebuilds_.load(); }
   uint64_t throttled() const { return throttled_.load(); }
   uint64_t credential_refreshes() const { return credential_refreshes_.load(); }
 
@@ -171,9 +173,16 @@ class KubeClient {
   // Token from the exec plugin / gcp auth-provider, refreshed when expired or `force`d.
   std::string plugin_token(bool force);
   bool has_plugin() const { return cfg_.exec.has_value() || cfg_.auth_provider == "gcp"; }
-  KubeConfig cfg_;
-  std::unique_ptr<http::Client> http_;
-  std::mutex token_mu_;
+  // An HTTP client for the current credentials (TLS client certificate included).
+  static std::shared_ptr<http::Client> make_http(const KubeConfig& cfg);
+  std::shared_ptr<http::Client> http() const;
+  KubeConfig cfg_;  // client_cert/key under token_mu_ (exec plugin refreshes)
+  // Replaced when an exec plugin hands out a new client certificate (client-go rotates
+  // its TLS certificate the same way): requests in flight finish on the old client.
+  std::shared_ptr<http::Client> http_;
+  mutable std::mutex http_mu_;
+  std::atomic<uint64_t> tls_rebuilds_{0};
+  mutable std::mutex token_mu_;
   std::string token_;
   std::chrono::steady_clock::time_point token_read_{};
   std::chrono::system_clock::time_point token_expiry_ = std::chrono::system_clock::time_point::max();

@@ -246,3 +246,76 @@ def test_exec_plugin_install_hint_and_interactive_mode(nat, tmp_path):
         with pytest.raises(Exception, match="interactive mode"):
             nat.kube_request(kc, "GET", "/api/v1/namespaces", 1)
         assert not _calls(pd)  # refused before running it
+
+
+CERT_PLUGIN = textwrap.dedent("""\
+    #!{python}
+    # fake exec plugin that hands out client certificates: the n-th call returns cert<n>
+    # (the last one from then on), each valid for PLUGIN_TTL seconds
+    import datetime, json, os
+    d = os.path.dirname(os.path.abspath(__file__))
+    info = json.loads(os.environ["KUBERNETES_EXEC_INFO"])
+    with open(os.path.join(d, "calls.jsonl"), "a") as f:
+        f.write("{{}}\\n")
+    n = sum(1 for _ in open(os.path.join(d, "calls.jsonl")))
+    k = min(n, int(open(os.path.join(d, "count")).read()))
+    exp = (datetime.datetime.now(datetime.timezone.utc)
+           + datetime.timedelta(seconds=float(os.environ.get("PLUGIN_TTL", "3600")))).strftime("%Y-%m-%dT%H:%M:%SZ")
+    print(json.dumps({{"apiVersion": info["apiVersion"], "kind": "ExecCredential",
+                      "status": {{"clientCertificateData": open(os.path.join(d, f"cert{{k}}.pem")).read(),
+                                  "clientKeyData": open(os.path.join(d, f"key{{k}}.pem")).read(),
+                                  "expirationTimestamp": exp}}}}))
+    """)
+
+
+def _openssl(*args, cwd):
+    import subprocess
+
+    subprocess.run(["openssl", *args], cwd=cwd, check=True, capture_output=True)
+
+
+def _client_pki(d, users):
+    """A client CA (the apiserver's --client-ca-file) and one certificate per (CN, O)."""
+    _openssl("req", "-x509", "-newkey", "ec", "-pkeyopt", "ec_paramgen_curve:P-256", "-nodes", "-keyout", "ca.key",
+             "-out", "ca.crt", "-days", "1", "-subj", "/CN=bgc-test-client-ca", cwd=d)
+    for i, (cn, org) in enumerate(users, 1):
+        _openssl("req", "-newkey", "ec", "-pkeyopt", "ec_paramgen_curve:P-256", "-nodes", "-keyout", f"key{i}.pem",
+                 "-out", f"c{i}.csr", "-subj", f"/O={org}/CN={cn}", cwd=d)
+        _openssl("x509", "-req", "-in", f"c{i}.csr", "-CA", "ca.crt", "-CAkey", "ca.key", "-CAcreateserial",
+                 "-out", f"cert{i}.pem", "-days", "1", cwd=d)
+    _write(os.path.join(d, "count"), str(len(users)))
+    return os.path.join(d, "ca.crt")
+
+
+def test_exec_plugin_client_certificate_rotation(nat, tmp_path, monkeypatch):
+    """An exec plugin that issues short-lived client certificates: when a
+    refresh returns a new certificate, the client rebuilds its TLS context, so the next
+    requests present the new certificate instead of failing on the expired one.  kube-lite
+    authenticates x509 client certificates (--client-ca-file: CN = user, O = groups) and
+    answers SelfSubjectReview, which shows which certificate each request carried."""
+    d = tmp_path / "certplugin"
+    d.mkdir()
+    ca = _client_pki(str(d), [("cert-admin-a", "system:masters"), ("cert-admin-b", "system:masters")])
+    with Cluster(admission=False, controller=False, tls_apiserver=True,
+                 apiserver_args=["--client-ca-file", ca]) as c:
+        _write(str(d / "plugin.py"), CERT_PLUGIN.format(python=sys.executable), exe=True)
+        kc = _cluster_kubeconfig(c, str(d / "config"), """exec:
+  apiVersion: client.authentication.k8s.io/v1
+  command: ./plugin.py""")
+        review = "/apis/authentication.k8s.io/v1/selfsubjectreviews"
+        # a long-lived certificate: fetched once, then cached
+        results, refreshes, _ = nat.kube_request(kc, "POST", review, 2)
+        users = [json.loads(b)["status"]["userInfo"]["username"] for _, b in results]
+        assert [s for s, _ in results] == [201, 201] and users == ["cert-admin-a"] * 2 and refreshes == 1
+        assert "system:masters" in json.loads(results[0][1])["status"]["userInfo"]["groups"]
+        # certificates that expire within the client's 10 s margin: every request refreshes,
+        # the second fetch hands out certificate b, and the requests carry b from then on
+        os.unlink(d / "calls.jsonl")
+        monkeypatch.setenv("PLUGIN_TTL", "5")
+        results, refreshes, _ = nat.kube_request(kc, "POST", review, 3)
+        users = [json.loads(b)["status"]["userInfo"]["username"] for _, b in results]
+        assert [s for s, _ in results] == [201] * 3 and users == ["cert-admin-b"] * 3, users
+        assert refreshes == 4
+        # the cert user is an admin like any other: it can list
+        results, _, _ = nat.kube_request(kc, "GET", "/api/v1/namespaces", 1)
+        assert results[0][0] == 200

@@ -69,6 +69,31 @@ def test_selectors_and_service_accounts(objs):
     assert comps == {"controller", "admission", "synchronizer"}
 
 
+def _matches(selector, labels):
+    return all(labels.get(k) == v for k, v in selector.items())
+
+
+@pytest.mark.parametrize("values", [None, {"fullnameOverride": "x"}, {"nameOverride": "n"}])
+def test_no_workload_selector_matches_another_workloads_pods(values):
+    """Deployments keep the reference's bare name+instance selector (upgrade parity), so
+    the node-agent DaemonSet's pods carry another app.kubernetes.io/name: no Deployment
+    selects them (kubectl logs deploy/..., rollout status) and the DaemonSet selects no
+    Deployment pod."""
+    objs = render(values)
+    deps = list(by_kind(objs, "Deployment").values())
+    [na] = by_kind(objs, "DaemonSet").values()
+    na_pods = na["spec"]["template"]["metadata"]["labels"]
+    for dep in deps:
+        assert not _matches(dep["spec"]["selector"]["matchLabels"], na_pods), dep["metadata"]["name"]
+        assert not _matches(na["spec"]["selector"]["matchLabels"], dep["spec"]["template"]["metadata"]["labels"])
+    # (the three Deployments share the reference's selector among themselves: an in-place
+    # upgrade needs it unchanged; see test_in_place_upgrade_from_a_reference_release)
+    # the metrics Service (when enabled) still selects exactly the node-agent pods
+    svcs = [o for o in render(dict(values or {}, metrics={"enabled": True})) if o["kind"] == "Service"
+            and o["metadata"]["name"].endswith("node-agent-metrics")]
+    assert _matches(svcs[0]["spec"]["selector"], na["spec"]["template"]["metadata"]["labels"])
+
+
 def test_webhook_service_deployment_certificate_wiring(objs):
     svc = by_kind(objs, "Service")["bgc-bacchus-gpu-admission"]
     adm = by_kind(objs, "Deployment")["bgc-bacchus-gpu-admission"]
