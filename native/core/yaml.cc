@@ -45,7 +45,10 @@ struct Analysis {
   bool block_allowed = false;
 };
 
-// Port of the decision logic of libyaml's yaml_emitter_analyze_scalar.
+// Port of the decision logic of libyaml's yaml_emitter_analyze_scalar (libyaml, MIT
+// License, Copyright (c) 2017-2020 Ingy döt Net, (c) 2006-2016 Kirill Simonov): the
+// scalar-style rules serde_yaml 0.9 inherits, re-implemented here so that crdgen's output
+// is byte-identical to the reference's crd.yaml.
 Analysis analyze(std::string_view s) {
   Analysis a;
   if (s.empty()) {

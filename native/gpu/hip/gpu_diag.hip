@@ -65,7 +65,7 @@ __device__ __forceinline__ u32x4 pattern16(uint64_t i, uint32_t seed) {
 
 // Each block streams one contiguous slab (per-block chunking keeps DRAM pages open and
 // measured 5.57 TB/s copy / 6.19 TB/s read on MI355X vs 5.08 / 5.61 for a grid-stride
-// interleave — tools/hbm_sweep.hip, profiles/hbm_sweep_r1.jsonl).
+// interleave — tools/probes/hbm_sweep.hip, profiles/hbm_sweep_r1.jsonl).
 __device__ __forceinline__ void block_range(uint64_t n16, uint64_t& beg, uint64_t& end) {
   const uint64_t per = (n16 + gridDim.x - 1) / gridDim.x;
   beg = static_cast<uint64_t>(blockIdx.x) * per;
@@ -331,7 +331,7 @@ __device__ __forceinline__ i32x8 lowp_pack(uint32_t seed, uint32_t tile, int rc,
 }
 
 // The scale block (= the lane group whose scale byte applies) of element j of lane group g,
-// measured on the MI355X with tools/mx_scale_layout.hip (profiles/mx_lowp_r3/):
+// measured on the MI355X with tools/probes/mx_scale_layout.hip (profiles/mx_lowp_r3/):
 //  * fp4: a lane group's 32 elements are K 32g..32g+31, one block, its own scale;
 //  * fp8: elements 0-15 are K 16g..16g+15 and 16-31 are K 64+16g.., so they fall in
 //    blocks g/2 and 2+g/2, scaled by lane groups g/2 and 2+g/2.

@@ -10,7 +10,7 @@ SQ="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_
 for kern in ${KERNELS:-2buf pingpong}; do
   export BGC_SOAK_KERNEL=$kern
   echo "pmc $kern"
-  timeout -s KILL 90 rocprofv3 --pmc $SQ --kernel-trace --output-format csv -d "$OUT/$kern" -o sq -- python3 tools/soak_one.py 8192 8192 8192 5 > "$OUT/$kern.log" 2>&1 || { tail -20 "$OUT/$kern.log"; exit 1; }
+  timeout -s KILL 90 rocprofv3 --pmc $SQ --kernel-trace --output-format csv -d "$OUT/$kern" -o sq -- python3 tools/probes/soak_one.py 8192 8192 8192 5 > "$OUT/$kern.log" 2>&1 || { tail -20 "$OUT/$kern.log"; exit 1; }
 done
 python3 - "$OUT" <<'PY'
 import collections, csv, glob, json, os, re, sys

@@ -54,7 +54,7 @@ def main(d):
             e["hbm_read_plus_write_tbps"] = round((rd / t_fe[k] + wb / t_wr[k]) * 1e-12, 3)  # concurrent in one kernel
         e["waves"] = int(sq[k]["SQ_WAVES"])
         out[k] = e
-    print(json.dumps({"source": "rocprofv3 --pmc (counters only) on 1x MI355X, workload tools/gpu_probe.py",
+    print(json.dumps({"source": "rocprofv3 --pmc (counters only) on 1x MI355X, workload tools/probes/gpu_probe.py",
                       "kernels": out}, indent=1))
 
 

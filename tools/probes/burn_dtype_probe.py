@@ -1,7 +1,7 @@
 """Power, clocks and rate of the burn-in on each matrix-core path of one MI355X (bf16, MX
 fp8, MX fp4): which one is the harder power/thermal stress?
 
-    python3 tools/burn_dtype_probe.py [seconds=4]
+    python3 tools/probes/burn_dtype_probe.py [seconds=4]
 
 Writes gpurun_out/burn_dtype_probe.json; one line per dtype on stdout."""
 import json

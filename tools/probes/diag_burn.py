@@ -1,7 +1,7 @@
 """Burn-in measurement on cuda:0: sustained MFMA load for N seconds with amdsmi sampling
 (power, gfxclk, temperatures, throttle residency).  Sets the DiagFloors burn defaults.
 
-    python3 tools/diag_burn.py 10 gpurun_out/diag_burn.json"""
+    python3 tools/probes/diag_burn.py 10 gpurun_out/diag_burn.json"""
 import json
 import os
 import sys

@@ -1,5 +1,5 @@
 // HBM streaming micro-benchmark sweep for the diag kernels (gfx950).
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/hbm_sweep.hip -o bin/hbm_sweep
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/probes/hbm_sweep.hip -o bin/hbm_sweep
 // Prints one JSON object per variant: {"kernel","nt","unroll","bpc","gbps"}.
 #include <hip/hip_runtime.h>
 

@@ -1,7 +1,7 @@
 """MX fp8 / fp4 matrix-core check on the MI355X: tiles, scaled tiles and dense rates at a
 few occupancies.  Writes gpurun_out/lowp_probe.json.
 
-    python3 tools/lowp_probe.py
+    python3 tools/probes/lowp_probe.py
 """
 import json
 import os

@@ -3,7 +3,7 @@
 // element position p = 32 g + j: only A row 0's element j of lane group g is 1.0, B is all
 // ones with unit scales, and lane group g' supplies scale 2^(g' + 1).  C[0][0] is then the
 // scale that hit that element; log2 - 1 names the lane group it came from.
-//   hipcc --offload-arch=gfx950 -O2 tools/mx_scale_layout.hip -o tools/mx_scale_layout
+//   hipcc --offload-arch=gfx950 -O2 tools/probes/mx_scale_layout.hip -o tools/probes/mx_scale_layout
 #include <hip/hip_runtime.h>
 
 #include <cmath>

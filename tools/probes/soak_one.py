@@ -1,4 +1,4 @@
-"""One GEMM soak on the GPU box (for rocprofv3 runs): python3 tools/soak_one.py M N K LAUNCHES."""
+"""One GEMM soak on the GPU box (for rocprofv3 runs): python3 tools/probes/soak_one.py M N K LAUNCHES."""
 import json
 import os
 import sys
