@@ -626,7 +626,10 @@ def run(args):
                                             if l.startswith(("bgc_controller_apply_cache_entries",
                                                              "bgc_controller_queue_depth", "bgc_heap_",
                                                              "bgc_controller_owner_state_entries",
-                                                             "bgc_controller_store_objects"))}
+                                                             "bgc_controller_store_objects",
+                                                             "bgc_reconcile_total", "bgc_reconcile_fast_total",
+                                                             "bgc_apply_total", "bgc_apply_skipped_total",
+                                                             "bgc_controller_own_write_events_total"))}
             except Exception:  # noqa: BLE001
                 pass
         return out

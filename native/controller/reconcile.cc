@@ -143,45 +143,69 @@ Reconciler::Reconciler(kube::KubeClient& client, kube::Controller& ctrl, Config 
     : client_(client), ctrl_(ctrl), cfg_(cfg), pool_(static_cast<size_t>(std::max(4, cfg.workers * 3))) {}
 
 Reconciler::Stats Reconciler::stats() const {
-  std::lock_guard<std::mutex> lk(mu_);
-  return stats_;
+  return {stats_applied_.load(std::memory_order_relaxed), stats_skipped_.load(std::memory_order_relaxed)};
+}
+
+static std::string lower(std::string s) {
+  for (auto& ch : s) ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
+  return s;
+}
+
+// Every record of one tenant (its children's applies, its fast-path state, its failure
+// count) lives in the shard of its namespace name: the lower-cased UserBootstrap name,
+// which is also each child's name (the Namespace) or namespace (the rest).
+Reconciler::Shard& Reconciler::shard(const std::string& ns_name) const {
+  return shards_[std::hash<std::string>{}(ns_name) % kShards];
 }
 
 static std::string child_key(const DesiredChild& c) { return c.rt->plural + "/" + c.ns + "/" + c.name; }
 
 // Publishes the sizes of the two per-tenant caches (bounded-memory check under churn).
-static void publish_cache_sizes(size_t applied, size_t owners) {
+void Reconciler::publish_cache_sizes() {
   static auto& reg = metrics::Registry::global();
   static auto& a = reg.gauge("bgc_controller_apply_cache_entries", "Children with a remembered last apply");
   static auto& o = reg.gauge("bgc_controller_owner_state_entries", "UserBootstraps with fast-path state");
-  a.set(static_cast<double>(applied));
-  o.set(static_cast<double>(owners));
+  a.set(static_cast<double>(applied_entries_.load(std::memory_order_relaxed)));
+  o.set(static_cast<double>(owner_entries_.load(std::memory_order_relaxed)));
+}
+
+void Reconciler::erase_applied_locked(Shard& sh, const std::string& key) {
+  if (sh.last_applied.erase(key)) applied_entries_.fetch_sub(1, std::memory_order_relaxed);
+}
+
+void Reconciler::erase_owner_state_locked(Shard& sh, const std::string& owner) {
+  if (sh.ub_state.erase(owner)) owner_entries_.fetch_sub(1, std::memory_order_relaxed);
 }
 
 void Reconciler::forget(const kube::ResourceType& rt, const Value& child) {
-  std::string key = rt.plural + "/" + kube::meta_namespace(child) + "/" + kube::meta_name(child);
-  std::lock_guard<std::mutex> lk(mu_);
-  last_applied_.erase(key);
-  for (const auto& ref : child.get("metadata").get("ownerReferences").items()) {
-    if (ref.get_string("kind") == types::UserBootstrap.kind) ub_state_.erase(ref.get_string("name"));
+  const std::string ns = kube::meta_namespace(child), name = kube::meta_name(child);
+  Shard& sh = shard(ns.empty() ? name : ns);
+  {
+    std::lock_guard<std::mutex> lk(sh.mu);
+    erase_applied_locked(sh, rt.plural + "/" + ns + "/" + name);
+    for (const auto& ref : child.get("metadata").get("ownerReferences").items()) {
+      if (ref.get_string("kind") == types::UserBootstrap.kind) erase_owner_state_locked(sh, ref.get_string("name"));
+    }
   }
-  publish_cache_sizes(last_applied_.size(), ub_state_.size());
+  publish_cache_sizes();
 }
 
-void Reconciler::forget_owner_locked(const std::string& owner) {
-  failures_.erase(owner);
-  std::string ns = owner;
-  for (auto& ch : ns) ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
-  ub_state_.erase(owner);
-  last_applied_.erase(types::Namespace.plural + "//" + ns);
+void Reconciler::forget_owner_locked(Shard& sh, const std::string& owner) {
+  sh.failures.erase(owner);
+  const std::string ns = lower(owner);
+  erase_owner_state_locked(sh, owner);
+  erase_applied_locked(sh, types::Namespace.plural + "//" + ns);
   for (const auto* rt : {&types::ResourceQuota, &types::Role, &types::RoleBinding})
-    last_applied_.erase(rt->plural + "/" + ns + "/" + ns);
-  publish_cache_sizes(last_applied_.size(), ub_state_.size());
+    erase_applied_locked(sh, rt->plural + "/" + ns + "/" + ns);
 }
 
 void Reconciler::forget_owner(const std::string& owner) {
-  std::lock_guard<std::mutex> lk(mu_);
-  forget_owner_locked(owner);
+  Shard& sh = shard(lower(owner));
+  {
+    std::lock_guard<std::mutex> lk(sh.mu);
+    forget_owner_locked(sh, owner);
+  }
+  publish_cache_sizes();
 }
 
 bool Reconciler::owner_live(const std::string& name, const std::string& uid) {
@@ -192,9 +216,10 @@ bool Reconciler::owner_live(const std::string& name, const std::string& uid) {
 bool Reconciler::fresh(const std::string& owner_name, const std::string& owner_rv) {
   std::vector<ChildRef> children;
   {
-    std::lock_guard<std::mutex> lk(mu_);
-    auto it = ub_state_.find(owner_name);
-    if (it == ub_state_.end() || it->second.owner_rv != owner_rv) return false;
+    Shard& sh = shard(lower(owner_name));
+    std::lock_guard<std::mutex> lk(sh.mu);
+    auto it = sh.ub_state.find(owner_name);
+    if (it == sh.ub_state.end() || it->second.owner_rv != owner_rv) return false;
     children = it->second.children;
   }
   for (const auto& c : children) {
@@ -206,38 +231,54 @@ bool Reconciler::fresh(const std::string& owner_name, const std::string& owner_r
   return true;
 }
 
-size_t Reconciler::cached_children() const {
-  std::lock_guard<std::mutex> lk(mu_);
-  return last_applied_.size();
-}
+size_t Reconciler::cached_children() const { return applied_entries_.load(std::memory_order_relaxed); }
 
 bool Reconciler::is_own_write(const kube::ResourceType& rt, const Value& child) const {
   if (!cfg_.skip_unchanged) return false;
-  std::string key = rt.plural + "/" + kube::meta_namespace(child) + "/" + kube::meta_name(child);
-  std::lock_guard<std::mutex> lk(mu_);
-  auto it = last_applied_.find(key);
-  return it != last_applied_.end() && it->second.rv == kube::meta_rv(child);
+  const std::string ns = kube::meta_namespace(child), name = kube::meta_name(child);
+  const std::string key = rt.plural + "/" + ns + "/" + name;
+  Shard& sh = shard(ns.empty() ? name : ns);
+  std::lock_guard<std::mutex> lk(sh.mu);
+  auto it = sh.last_applied.find(key);
+  return it != sh.last_applied.end() && it->second.rv == kube::meta_rv(child);
 }
 
+// Up to date: the same body as our last apply, and the watch cache shows that apply's
+// result — or still shows exactly what it showed when we applied (absent, or the version
+// before), i.e. our write's watch echo is on its way.  Watch events arrive in order, so
+// anything another writer did after our apply reaches the cache after that echo and is
+// seen by a later reconcile; without this a reconcile that overtakes the echo (the status
+// write right after the quota apply) re-applies an unchanged ResourceQuota.
 bool Reconciler::up_to_date(const DesiredChild& c, const std::string& body_hash) {
   if (!cfg_.skip_unchanged) return false;
   kube::Store* store = ctrl_.child_store(c.rt->plural);
   if (!store) return false;
   kube::ObjPtr cur = store->get(c.ns, c.name);
-  if (!cur) return false;
-  std::lock_guard<std::mutex> lk(mu_);
-  auto it = last_applied_.find(child_key(c));
-  return it != last_applied_.end() && it->second.body_hash == body_hash && it->second.rv == kube::meta_rv(*cur);
+  Shard& sh = shard(c.name);
+  std::lock_guard<std::mutex> lk(sh.mu);
+  auto it = sh.last_applied.find(child_key(c));
+  if (it == sh.last_applied.end() || it->second.body_hash != body_hash) return false;
+  const Applied& a = it->second;
+  if (!cur) return !a.prev_present;
+  const std::string rv = kube::meta_rv(*cur);
+  return rv == a.rv || (a.prev_present && rv == a.prev_rv);
 }
 
 void Reconciler::apply_child(const DesiredChild& c, const std::string& body_hash, const std::string& body_json) {
   static auto& applied = metrics::Registry::global().counter("bgc_apply_total", "Server-side applies issued");
+  kube::Store* store = ctrl_.child_store(c.rt->plural);
+  const kube::ObjPtr before = store ? store->get(c.ns, c.name) : nullptr;
   std::string rv = client_.apply_rv(*c.rt, c.ns, c.name, body_json, kFieldManager, /*force=*/true);
   applied.inc();
-  std::lock_guard<std::mutex> lk(mu_);
-  last_applied_[child_key(c)] = {body_hash, std::move(rv)};
-  publish_cache_sizes(last_applied_.size(), ub_state_.size());
-  stats_.applied++;
+  {
+    Shard& sh = shard(c.name);
+    std::lock_guard<std::mutex> lk(sh.mu);
+    auto [it, inserted] = sh.last_applied.try_emplace(child_key(c));
+    it->second = {body_hash, std::move(rv), before ? kube::meta_rv(*before) : std::string(), before != nullptr};
+    if (inserted) applied_entries_.fetch_add(1, std::memory_order_relaxed);
+  }
+  publish_cache_sizes();
+  stats_applied_.fetch_add(1, std::memory_order_relaxed);
 }
 
 kube::Action Reconciler::reconcile(const kube::ObjPtr& ub_ptr) {
@@ -280,8 +321,7 @@ kube::Action Reconciler::reconcile(const kube::ObjPtr& ub_ptr) {
   auto run_one = [&](size_t i) {
     if (up_to_date(children[i], hashes[i])) {
       skipped.inc();
-      std::lock_guard<std::mutex> lk(mu_);
-      stats_.skipped++;
+      stats_skipped_.fetch_add(1, std::memory_order_relaxed);
       return;
     }
     try {
@@ -302,34 +342,42 @@ kube::Action Reconciler::reconcile(const kube::ObjPtr& ub_ptr) {
   // entries that nothing removes.  Every exit re-checks the watch cache under mu_ and
   // drops the owner's entries when the UB (this uid) is gone.
   const std::string owner_uid = ub.get("metadata").get_string("uid");
+  Shard& sh = shard(children.front().name);
   try {
     apply_all(children, run_one);
   } catch (...) {
-    std::lock_guard<std::mutex> lk(mu_);
-    if (!owner_live(owner_name, owner_uid)) forget_owner_locked(owner_name);
+    {
+      std::lock_guard<std::mutex> lk(sh.mu);
+      if (!owner_live(owner_name, owner_uid)) forget_owner_locked(sh, owner_name);
+    }
+    publish_cache_sizes();
     throw;
   }
   {
-    std::lock_guard<std::mutex> lk(mu_);
-    if (!failures_.empty()) failures_.erase(owner_name);
+    std::lock_guard<std::mutex> lk(sh.mu);
+    if (!sh.failures.empty()) sh.failures.erase(owner_name);
     if (!owner_live(owner_name, owner_uid)) {
-      forget_owner_locked(owner_name);
+      forget_owner_locked(sh, owner_name);
     } else if (cfg_.skip_unchanged) {
       UbState st;
       st.owner_rv = owner_rv;
       bool complete = true;
       for (const auto& c : children) {
-        auto it = last_applied_.find(child_key(c));
-        if (it == last_applied_.end()) {
+        auto it = sh.last_applied.find(child_key(c));
+        if (it == sh.last_applied.end()) {
           complete = false;
           break;
         }
         st.children.push_back({c.rt, c.ns, c.name, it->second.rv});
       }
-      if (complete) ub_state_[owner_name] = std::move(st);
-      publish_cache_sizes(last_applied_.size(), ub_state_.size());
+      if (complete) {
+        auto [it, inserted] = sh.ub_state.try_emplace(owner_name);
+        it->second = std::move(st);
+        if (inserted) owner_entries_.fetch_add(1, std::memory_order_relaxed);
+      }
     }
   }
+  publish_cache_sizes();
   return kube::Action::requeue_after(std::chrono::milliseconds(cfg_.requeue_secs * 1000));
 }
 
@@ -366,8 +414,10 @@ kube::Action Reconciler::error_policy(const kube::ObjPtr& ub, const std::excepti
   if (cfg_.error_backoff_base_ms > 0) {
     int n;
     {
-      std::lock_guard<std::mutex> lk(mu_);
-      n = ++failures_[meta.get_string("name")];
+      const std::string owner = meta.get_string("name");
+      Shard& sh = shard(lower(owner));
+      std::lock_guard<std::mutex> lk(sh.mu);
+      n = ++sh.failures[owner];
     }
     const int shift = std::min(n - 1, 30);
     delay = std::min<int64_t>(cfg_.error_requeue_ms, cfg_.error_backoff_base_ms << shift);

@@ -17,6 +17,8 @@
 //    drift-repair pass costs zero API writes unless something actually drifted.
 #pragma once
 
+#include <array>
+#include <atomic>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -116,23 +118,10 @@ class Reconciler {
  private:
   struct Applied {
     std::string body_hash;
-    std::string rv;
+    std::string rv;       // what our apply returned
+    std::string prev_rv;  // what the watch cache showed just before it (prev_present)
+    bool prev_present = false;
   };
-  bool up_to_date(const DesiredChild& c, const std::string& body_hash);
-  // Stage order: Namespace, then ResourceQuota ‖ Role, then RoleBinding.
-  void apply_all(const std::vector<DesiredChild>& children, const std::function<void(size_t)>& run_one);
-  void forget_owner_locked(const std::string& owner);  // mu_ held
-  bool owner_live(const std::string& name, const std::string& uid);
-  kube::EventRecorder* events_ = nullptr;
-  void apply_child(const DesiredChild& c, const std::string& body_hash, const std::string& body_json);
-
-  kube::KubeClient& client_;
-  kube::Controller& ctrl_;
-  Config cfg_;
-  ThreadPool pool_;
-  mutable std::mutex mu_;
-  std::unordered_map<std::string, Applied> last_applied_;
-  std::unordered_map<std::string, int> failures_;  // consecutive errors per UB (backoff)
   // Fast path for periodic resyncs: after a fully successful reconcile, the UB's
   // resourceVersion and each child's resourceVersion. A later reconcile of the same UB
   // version whose children are still at those versions in the watch cache does nothing.
@@ -144,9 +133,36 @@ class Reconciler {
     std::string owner_rv;
     std::vector<ChildRef> children;
   };
-  std::unordered_map<std::string, UbState> ub_state_;
+  // The per-tenant records, split into lock shards by namespace name: a child watch event
+  // (is_own_write), a reconcile's checks and applies and a deletion (forget) touch one
+  // tenant's shard only, so 16 workers and 5 watch threads rarely meet on a lock.
+  struct Shard {
+    std::mutex mu;
+    std::unordered_map<std::string, Applied> last_applied;  // "plural/ns/name"
+    std::unordered_map<std::string, UbState> ub_state;      // owner name
+    std::unordered_map<std::string, int> failures;          // consecutive errors per UB (backoff)
+  };
+  static constexpr size_t kShards = 64;
+  Shard& shard(const std::string& ns_name) const;
+  void erase_applied_locked(Shard& sh, const std::string& key);
+  void erase_owner_state_locked(Shard& sh, const std::string& owner);
+  void forget_owner_locked(Shard& sh, const std::string& owner);  // sh.mu held
+  void publish_cache_sizes();
+  bool up_to_date(const DesiredChild& c, const std::string& body_hash);
+  // Stage order: Namespace, then ResourceQuota ‖ Role, then RoleBinding.
+  void apply_all(const std::vector<DesiredChild>& children, const std::function<void(size_t)>& run_one);
+  bool owner_live(const std::string& name, const std::string& uid);
   bool fresh(const std::string& owner_name, const std::string& owner_rv);
-  Stats stats_;
+  kube::EventRecorder* events_ = nullptr;
+  void apply_child(const DesiredChild& c, const std::string& body_hash, const std::string& body_json);
+
+  kube::KubeClient& client_;
+  kube::Controller& ctrl_;
+  Config cfg_;
+  ThreadPool pool_;
+  mutable std::array<Shard, kShards> shards_;
+  std::atomic<size_t> applied_entries_{0}, owner_entries_{0};
+  std::atomic<uint64_t> stats_applied_{0}, stats_skipped_{0};
 };
 
 }  // namespace bgc::controller

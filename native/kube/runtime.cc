@@ -202,7 +202,12 @@ void Watcher::run(CancelToken& stop, const std::function<void(const WatchEvent&)
 // Store
 
 void Store::apply(const WatchEvent& ev) {
+  ObjPtr replaced;  // the previous object is freed after the lock is released
   std::lock_guard<std::mutex> lk(mu_);
+  struct Count {
+    Store* s;
+    ~Count() { s->size_.store(s->items_.size(), std::memory_order_relaxed); }
+  } count{this};
   switch (ev.type) {
     case WatchEvent::Type::Restarted:
       items_.clear();
@@ -211,12 +216,20 @@ void Store::apply(const WatchEvent& ev) {
       cv_.notify_all();
       break;
     case WatchEvent::Type::Added:
-    case WatchEvent::Type::Modified:
-      items_[rt_.key(meta_namespace(*ev.object), meta_name(*ev.object))] = ev.object;
+    case WatchEvent::Type::Modified: {
+      ObjPtr& slot = items_[rt_.key(meta_namespace(*ev.object), meta_name(*ev.object))];
+      replaced = std::move(slot);
+      slot = ev.object;
       break;
-    case WatchEvent::Type::Deleted:
-      items_.erase(rt_.key(meta_namespace(*ev.object), meta_name(*ev.object)));
+    }
+    case WatchEvent::Type::Deleted: {
+      auto it = items_.find(rt_.key(meta_namespace(*ev.object), meta_name(*ev.object)));
+      if (it != items_.end()) {
+        replaced = std::move(it->second);
+        items_.erase(it);
+      }
       break;
+    }
   }
 }
 
@@ -232,11 +245,6 @@ std::vector<ObjPtr> Store::list() const {
   out.reserve(items_.size());
   for (auto& kv : items_) out.push_back(kv.second);
   return out;
-}
-
-size_t Store::size() const {
-  std::lock_guard<std::mutex> lk(mu_);
-  return items_.size();
 }
 
 bool Store::wait_synced(std::chrono::milliseconds timeout) const {
@@ -280,6 +288,7 @@ void WorkQueue::add_after(const std::string& key, std::chrono::milliseconds dela
   std::lock_guard<std::mutex> lk(mu_);
   if (!forgotten_.empty()) forgotten_.erase(key);
   add_after_locked(key, t);
+  count_locked();
 }
 
 void WorkQueue::requeue(const std::string& key, std::chrono::milliseconds delay) {
@@ -287,6 +296,15 @@ void WorkQueue::requeue(const std::string& key, std::chrono::milliseconds delay)
   std::lock_guard<std::mutex> lk(mu_);
   if (!forgotten_.empty() && forgotten_.count(key)) return;
   add_after_locked(key, t);
+  count_locked();
+}
+
+void WorkQueue::finish(const std::string& key, bool requeue, std::chrono::milliseconds delay) {
+  const auto t = Clock::now() + delay;
+  std::lock_guard<std::mutex> lk(mu_);
+  if (requeue && (forgotten_.empty() || !forgotten_.count(key))) add_after_locked(key, t);
+  done_locked(key);
+  count_locked();
 }
 
 void WorkQueue::add_after_locked(const std::string& key, Clock::time_point t) {
@@ -306,7 +324,10 @@ void WorkQueue::forget(const std::string& key) {
   deferred_.erase(key);
   if (processing_.count(key)) forgotten_.insert(key);
   auto d = due_.find(key);
-  if (d == due_.end()) return;
+  if (d == due_.end()) {
+    count_locked();
+    return;
+  }
   auto range = timeline_.equal_range(d->second);
   for (auto it = range.first; it != range.second; ++it) {
     if (it->second == key) {
@@ -315,6 +336,7 @@ void WorkQueue::forget(const std::string& key) {
     }
   }
   due_.erase(d);
+  count_locked();
 }
 
 bool WorkQueue::get(std::string& key) {
@@ -334,6 +356,7 @@ bool WorkQueue::get(std::string& key) {
       timeline_.erase(it);
       due_.erase(d);
       processing_.insert(key);
+      count_locked();
       // hand the timer role on if more work is waiting and nobody is timing it
       if (!timeline_.empty() && !timer_waiter_ && idle_ > 0) cv_.notify_one();
       return true;
@@ -355,6 +378,11 @@ bool WorkQueue::get(std::string& key) {
 
 void WorkQueue::done(const std::string& key) {
   std::lock_guard<std::mutex> lk(mu_);
+  done_locked(key);
+  count_locked();
+}
+
+void WorkQueue::done_locked(const std::string& key) {
   processing_.erase(key);
   if (!forgotten_.empty()) forgotten_.erase(key);
   auto it = deferred_.find(key);
@@ -371,11 +399,6 @@ void WorkQueue::shutdown() {
   shutdown_ = true;
   cv_.notify_all();
   timer_cv_.notify_all();
-}
-
-size_t WorkQueue::pending() const {
-  std::lock_guard<std::mutex> lk(mu_);
-  return due_.size() + deferred_.size();
 }
 
 size_t WorkQueue::in_flight() const {
@@ -513,8 +536,7 @@ void Controller::run(CancelToken& stop, Reconciler reconcile, ErrorPolicy error_
         } catch (const std::exception& e) {
           a = error_policy(obj, e);
         }
-        if (a.requeue) queue_.requeue(key, a.after);
-        queue_.done(key);
+        queue_.finish(key, a.requeue, a.after);
         q_depth.set(static_cast<double>(queue_.pending()));
       }
     });

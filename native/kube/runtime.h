@@ -118,7 +118,7 @@ class Store {
   ObjPtr get(const std::string& key) const;
   ObjPtr get(const std::string& ns, const std::string& name) const { return get(rt_.key(ns, name)); }
   std::vector<ObjPtr> list() const;
-  size_t size() const;
+  size_t size() const { return size_.load(std::memory_order_relaxed); }  // lock-free (gauges)
   bool synced() const { return synced_.load(); }
   // Blocks until the first full list has been applied (or timeout).
   bool wait_synced(std::chrono::milliseconds timeout) const;
@@ -129,6 +129,7 @@ class Store {
   mutable std::mutex mu_;
   mutable std::condition_variable cv_;
   std::unordered_map<std::string, ObjPtr> items_;
+  std::atomic<size_t> size_{0};
   std::atomic<bool> synced_{false};
 };
 
@@ -151,8 +152,10 @@ class WorkQueue {
   void forget(const std::string& key);
   // The worker's periodic/error requeue of the key it is processing.
   void requeue(const std::string& key, std::chrono::milliseconds delay);
+  // A worker is done with `key`: requeue (when `requeue`) and done() under one lock.
+  void finish(const std::string& key, bool requeue, std::chrono::milliseconds delay);
   void shutdown();
-  size_t pending() const;
+  size_t pending() const { return pending_.load(std::memory_order_relaxed); }  // lock-free (gauges)
   size_t in_flight() const;
 
  private:
@@ -173,6 +176,9 @@ class WorkQueue {
   std::unordered_map<std::string, Clock::time_point> deferred_;  // re-added while processing
   std::unordered_set<std::string> forgotten_;                    // forgotten while processing
   void add_after_locked(const std::string& key, Clock::time_point t);
+  void done_locked(const std::string& key);
+  void count_locked() { pending_.store(due_.size() + deferred_.size(), std::memory_order_relaxed); }
+  std::atomic<size_t> pending_{0};
   bool shutdown_ = false;
 };
 
