@@ -70,7 +70,10 @@ int main() {
   kube::Controller::Options co;
   co.workers = cfg.workers;
   co.child_delete_delay = std::chrono::milliseconds(cfg.child_delete_delay_ms);
-  if (cfg.projected_watch) co.primary_projection = &controller::user_bootstrap_event_projection();
+  if (cfg.projected_watch) {
+    co.primary_projection = &controller::user_bootstrap_event_projection();
+    co.child_projection = &controller::child_event_projection();
+  }
   kube::Controller ctrl(*client, kube::types::UserBootstrap, co);
   const std::string sel = cfg.label_children ? controller::child_label_selector() : "";
   ctrl.owns(kube::types::Namespace, nullptr, sel, cfg.metadata_watches);

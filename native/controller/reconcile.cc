@@ -50,10 +50,28 @@ const json::Projection& user_bootstrap_event_projection() {
   using P = json::Projection;
   static const P kMeta[] = {{"name", P::Keep},          {"namespace", P::Keep},  {"uid", P::Keep},
                             {"resourceVersion", P::Keep}, {"generation", P::Keep}, {"deletionTimestamp", P::Keep}};
-  static const P kObject[] = {{"apiVersion", P::Keep}, {"kind", P::Keep},  {"metadata", P::Descend, kMeta, std::size(kMeta)},
-                              {"spec", P::Keep},       {"status", P::Keep}};
-  static const P kEvent[] = {{"type", P::Keep}, {"object", P::Descend, kObject, std::size(kObject)}};
-  static const P kRoot{"", P::Descend, kEvent, std::size(kEvent)};
+  // the apiserver's own output: unnamed members are skipped structurally and left out
+  static const P kObject[] = {{"apiVersion", P::Keep},
+                              {"kind", P::Keep},
+                              {"metadata", P::Descend, kMeta, std::size(kMeta), true},
+                              {"spec", P::Keep},
+                              {"status", P::Keep}};
+  static const P kEvent[] = {{"type", P::Keep}, {"object", P::Descend, kObject, std::size(kObject), true}};
+  static const P kRoot{"", P::Descend, kEvent, std::size(kEvent), true};
+  return kRoot;
+}
+
+const json::Projection& child_event_projection() {
+  using P = json::Projection;
+  static const P kMeta[] = {{"name", P::Keep},
+                            {"namespace", P::Keep},
+                            {"resourceVersion", P::Keep},
+                            {"ownerReferences", P::Keep},
+                            {"deletionTimestamp", P::Keep}};
+  static const P kObject[] = {{"apiVersion", P::Keep}, {"kind", P::Keep},
+                              {"metadata", P::Descend, kMeta, std::size(kMeta), true}};
+  static const P kEvent[] = {{"type", P::Keep}, {"object", P::Descend, kObject, std::size(kObject), true}};
+  static const P kRoot{"", P::Descend, kEvent, std::size(kEvent), true};
   return kRoot;
 }
 

@@ -87,9 +87,12 @@ std::vector<DesiredChild> desired_children(const json::Value& ub, bool label = f
 std::string child_label_selector();
 // What a reconcile reads from a UserBootstrap watch event: type, apiVersion, kind,
 // metadata.{name,namespace,uid,resourceVersion,generation,deletionTimestamp}, spec and
-// status (reference controller.rs:50-155).  Everything else, annotations and labels
-// included, is scanned but not built.
+// status (reference controller.rs:50-155).  Everything else (managedFields, annotations,
+// labels) is stepped over and left out of the cached object.
 const json::Projection& user_bootstrap_event_projection();
+// What the controller reads from a child's watch event: type and the child's
+// metadata.{name,namespace,resourceVersion,ownerReferences,deletionTimestamp}.
+const json::Projection& child_event_projection();
 json::Value controller_owner_ref(const json::Value& ub);
 
 class Reconciler {

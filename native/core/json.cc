@@ -629,6 +629,21 @@ class Parser {
           break;
         }
       }
+      if (!child && p->omit_unnamed) {
+        skip_value();
+        skip_ws();
+        if (p_ >= s_.size()) fail("EOF while parsing an object");
+        if (s_[p_] == ',') {
+          ++p_;
+          continue;
+        }
+        if (s_[p_] == '}') {
+          ++p_;
+          finish_object(out, base, kbase);
+          return;
+        }
+        fail("expected `,` or `}`");
+      }
       Value v;
       parse_projected(v, depth + 1, child);
       bool dup = false;

@@ -155,6 +155,11 @@ struct Projection {
   Mode mode = Keep;
   const Projection* children = nullptr;
   size_t n_children = 0;
+  // Descend only: members `children` do not name are stepped over with a structural scan
+  // (balanced brackets, closed strings; not validated) and left out of the result, instead
+  // of standing in as empty values.  For trusted input whose extra members are large (a
+  // watch event's managedFields and annotations).
+  bool omit_unnamed = false;
 };
 Value parse_projected(std::string_view text, const Projection& root);
 bool try_parse_projected(std::string_view text, const Projection& root, Value& out, std::string* err = nullptr);

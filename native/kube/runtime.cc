@@ -83,6 +83,19 @@ std::string Watcher::list_all(std::vector<ObjPtr>& out, CancelToken& stop) {
   }
 }
 
+// ERROR and BOOKMARK watch lines.  The apiserver writes "type" first ({"type":"ADDED",...}),
+// so the prefix answers without scanning a multi-kilobyte object; a line in another member
+// order falls back to a search of the whole line.
+static bool is_control_event(std::string_view line) {
+  constexpr std::string_view kPrefix = "{\"type\":\"";
+  if (line.substr(0, kPrefix.size()) == kPrefix) {
+    const std::string_view t = line.substr(kPrefix.size(), 9);
+    return t.substr(0, 6) == "ERROR\"" || t == "BOOKMARK\"";
+  }
+  return line.find("\"type\":\"ERROR\"") != std::string_view::npos ||
+         line.find("\"type\":\"BOOKMARK\"") != std::string_view::npos;
+}
+
 void Watcher::run(CancelToken& stop, const std::function<void(const WatchEvent&)>& on_event) {
   std::string rv;
   bool need_list = true;
@@ -132,8 +145,7 @@ void Watcher::run(CancelToken& stop, const std::function<void(const WatchEvent&)
         // Events the consumer does not want are dropped before JSON parsing; ERROR and
         // BOOKMARK lines always go through (they drive relists and resumption).  During
         // a streaming list nothing is dropped: the initial state must be complete.
-        const bool control = line.find("\"type\":\"ERROR\"") != std::string::npos ||
-                             line.find("\"type\":\"BOOKMARK\"") != std::string::npos;
+        const bool control = is_control_event(line);
         if (!initial_phase && line_filter_ && !control && !line_filter_(line)) continue;
         // metadata.managedFields is never read from the cache; skipping it while parsing
         // saves most of the allocations of an SSA-managed child's event.
@@ -491,6 +503,7 @@ void Controller::run(CancelToken& stop, Reconciler reconcile, ErrorPolicy error_
     threads.emplace_back([&, c] {
       Watcher w(client_, c->rt, "", c->selector);
       w.set_metadata_only(c->metadata_only);
+      w.set_projection(opts_.child_projection);
       w.run(stop, [&, c](const WatchEvent& ev) {
         c->store->apply(ev);
         c->gauge->set(static_cast<double>(c->store->size()));

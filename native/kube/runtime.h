@@ -202,8 +202,10 @@ class Controller {
     // children's DELETED events can overtake the owner's own DELETED event, and reconciling
     // the stale owner would re-create children the garbage collector is removing.
     std::chrono::milliseconds child_delete_delay{50};
-    // Selective parse of the primary watch's events (Watcher::set_projection).
+    // Selective parse of the primary watch's and the owned-kind watches' events
+    // (Watcher::set_projection).
     const json::Projection* primary_projection = nullptr;
+    const json::Projection* child_projection = nullptr;
   };
 
   Controller(KubeClient& client, ResourceType primary, Options opts);

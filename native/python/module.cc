@@ -48,6 +48,7 @@ struct ProjectionTree {
   };
   Node root;
   std::vector<std::unique_ptr<std::vector<bgc::json::Projection>>> store;
+  bool omit_unnamed = false;
   bgc::json::Projection build(const Node& n) {
     bgc::json::Projection p;
     p.key = n.key;
@@ -56,6 +57,7 @@ struct ProjectionTree {
       return p;
     }
     p.mode = bgc::json::Projection::Descend;
+    p.omit_unnamed = omit_unnamed;
     auto v = std::make_unique<std::vector<bgc::json::Projection>>();
     for (const auto& k : n.kids) v->push_back(build(k));
     p.children = v->data();
@@ -65,8 +67,9 @@ struct ProjectionTree {
   }
 };
 
-std::string json_parse_projected(const std::string& text, const std::vector<std::string>& keep) {
+std::string json_parse_projected(const std::string& text, const std::vector<std::string>& keep, bool omit_unnamed) {
   ProjectionTree t;
+  t.omit_unnamed = omit_unnamed;
   for (const auto& path : keep) {
     ProjectionTree::Node* n = &t.root;
     size_t start = 0;
@@ -134,7 +137,8 @@ PYBIND11_MODULE(_native, m) {
   m.def("json_roundtrip", &json_roundtrip, py::arg("text"), py::arg("drop_key") = "");
   m.def("yaml_to_json", &yaml_to_json);
   m.def("json_to_yaml", &json_to_yaml);
-  m.def("json_parse_projected", &json_parse_projected, py::arg("text"), py::arg("keep"));
+  m.def("json_parse_projected", &json_parse_projected, py::arg("text"), py::arg("keep"),
+        py::arg("omit_unnamed") = false);
   m.def("json_raw_member", [](const std::string& text, const std::string& key) {
     return std::string(bgc::json::raw_member(text, key));
   });

@@ -179,6 +179,26 @@ def test_projected_parse_matches_model(nat, v, keep):
     assert json.loads(nat.json_parse_projected(text, keep)) == _project(doc, _tree(keep) or {})
 
 
+def _omit(v, tree):
+    if tree is True:
+        return v
+    if not isinstance(v, dict):
+        return v  # a Descend node that is not an object is kept whole
+    return {k: _omit(x, tree[k]) for k, x in v.items() if k in tree}
+
+
+@settings(max_examples=300, deadline=None)
+@given(json_values(st.none() | st.booleans() | I64 | FLOATS | st.text(alphabet="ab.\"\\{}[],:", max_size=4)),
+       st.lists(st.sampled_from(["a", "b", "a.a", "a.b", "b.a.a", "a.b.a"]), max_size=3))
+def test_projected_parse_omit_unnamed_matches_model(nat, v, keep):
+    """omit_unnamed (the controller's UserBootstrap watch events): members no projection
+    names are stepped over structurally and left out, whatever brackets or quotes their
+    strings hold."""
+    doc = {"a": v, "b": {"a": v, "b": [v]}, "c": {"x": [v, {"y": v}]}} if not isinstance(v, dict) else v
+    text = json.dumps(doc)
+    assert json.loads(nat.json_parse_projected(text, keep, True)) == _omit(doc, _tree(keep) or {})
+
+
 @settings(max_examples=300, deadline=None)
 @given(json_values(st.none() | st.booleans() | I64 | TEXT), st.integers(min_value=0, max_value=200),
        st.sampled_from(["", "x", "{", "]", "\\", "\"", ",", "1e", "tru", "\u0001"]))
