@@ -259,10 +259,17 @@ struct ManagerEntry {
 };
 using Managers = std::map<std::string, ManagerEntry>;
 
+inline const std::shared_ptr<const Managers>& no_managers() {
+  static const std::shared_ptr<const Managers> empty = std::make_shared<const Managers>();
+  return empty;
+}
+
 struct Stored {
   std::shared_ptr<const Value> obj;
   uint64_t rv = 0;
-  Managers managers;
+  // Shared and immutable, like obj: a writer's snapshot of the stored object (taken under
+  // the store lock) copies two pointers instead of every manager's field set.
+  std::shared_ptr<const Managers> managers = no_managers();
 };
 
 // PartialObjectMetadata (meta.k8s.io/v1): what metadata-only clients ask for with
@@ -789,15 +796,25 @@ struct ApiServer::Impl {
 
   // ---------------------------------------------------------------- events
   // Caller holds ti.store->mu exclusively.
+  // Work moved out of the exclusive section (see prepare_commit).
+  struct PreparedEvent {
+    std::string head, tail;  // event line = head + rv digits + tail
+    bool ok = false;
+    // built before the exclusive section: the resuming-watch filter view and the event
+    // record (its line is filled in under the lock)
+    std::shared_ptr<const Value> filter;
+    std::shared_ptr<EventRec> rec;
+  };
+
   std::shared_ptr<const std::string> emit_locked(const std::string& type, const TypeInfo& ti, const std::string& ns,
                                                  const std::shared_ptr<const Value>& obj, uint64_t ev_rv,
-                                                 std::string preline = {}) {
+                                                 std::string preline = {}, const PreparedEvent* pe = nullptr) {
     TypeStore& st = *ti.store;
-    auto rec = std::make_shared<EventRec>();
+    auto rec = pe && pe->rec ? pe->rec : std::make_shared<EventRec>();
     rec->rv = ev_rv;
     rec->type_key = ti.key();
     rec->ns = ns;
-    rec->meta = filter_view(*obj);
+    rec->meta = pe && pe->filter ? pe->filter : filter_view(*obj);
     std::string line = std::move(preline);
     if (line.empty()) {
       line = "{\"type\":\"" + type + "\",\"object\":";
@@ -1215,10 +1232,6 @@ struct ApiServer::Impl {
 
   // Work moved out of the exclusive section: managedFields are rendered and the watch event
   // is serialized around a resourceVersion placeholder; commit_locked splices in the digits.
-  struct PreparedEvent {
-    std::string head, tail;  // event line = head + rv digits + tail
-    bool ok = false;
-  };
   static const std::string& rv_placeholder() {
     static const std::string p = "\x01rv\x01";
     return p;
@@ -1232,6 +1245,8 @@ struct ApiServer::Impl {
     line += "}\n";
     static const std::string needle = "\"resourceVersion\":" + Value(rv_placeholder()).dump();
     PreparedEvent pe;
+    pe.filter = filter_view(obj);
+    pe.rec = std::make_shared<EventRec>();
     size_t pos = line.find(needle);
     if (pos == std::string::npos) return pe;
     pe.head.assign(line, 0, pos);
@@ -1265,7 +1280,7 @@ struct ApiServer::Impl {
     Stored s;
     s.obj = ptr;
     s.rv = new_rv;
-    s.managers = std::move(managers);
+    s.managers = std::make_shared<const Managers>(std::move(managers));
     std::string key = obj_key(ti.rt, ns, name);
     Ref ref{ti.key(), key};
     {
@@ -1284,7 +1299,7 @@ struct ApiServer::Impl {
       }
     }
     b[key] = std::move(s);
-    auto line = emit_locked(prev ? "MODIFIED" : "ADDED", ti, ns, ptr, new_rv, std::move(preline));
+    auto line = emit_locked(prev ? "MODIFIED" : "ADDED", ti, ns, ptr, new_rv, std::move(preline), pe);
     if (line_out) *line_out = std::move(line);
     return ptr;
   }
@@ -1424,7 +1439,7 @@ struct ApiServer::Impl {
         }
       }
       // no-op short-circuit (before admission, like the apiserver's update path)
-      if (exists && same_content(obj, *cur_copy.obj) && managers == cur_copy.managers) {
+      if (exists && same_content(obj, *cur_copy.obj) && managers == *cur_copy.managers) {
         return {cur_copy.obj, 200, nullptr};
       }
       call_webhooks(ti, sub, op, ns, name, &obj, exists ? cur_copy.obj.get() : nullptr, user);
@@ -1434,7 +1449,7 @@ struct ApiServer::Impl {
       else obj["metadata"].erase("namespace");
       validate_object(ti, name, ns, obj);
       // everything below up to the lock depends only on cur_copy, which the commit re-checks
-      if (exists && same_content(obj, *cur_copy.obj) && managers == cur_copy.managers) {
+      if (exists && same_content(obj, *cur_copy.obj) && managers == *cur_copy.managers) {
         return {cur_copy.obj, 200, nullptr};  // mutation turned it into a no-op
       }
       if (exists && spec_changed(*cur_copy.obj, obj)) {
@@ -1592,7 +1607,7 @@ struct ApiServer::Impl {
                            else obj.erase("status");
                          }
                        }
-                       Managers m = cur->managers;
+                       Managers m = *cur->managers;
                        attribute_update(m, manager, *cur->obj, obj, is_status, p.ti->rt.api_version());
                        return {std::move(obj), std::move(m)};
                      },
@@ -1620,7 +1635,7 @@ struct ApiServer::Impl {
     Managers m;
     if (cur) {
       live = *cur->obj;
-      m = cur->managers;
+      m = *cur->managers;
     } else {
       live = Value::object();
       init_new(ti, live, ns, name);
@@ -1726,7 +1741,7 @@ struct ApiServer::Impl {
                            else obj.erase("status");
                          }
                        }
-                       Managers m = cur->managers;
+                       Managers m = *cur->managers;
                        attribute_update(m, manager, *cur->obj, obj, is_status, p.ti->rt.api_version());
                        return {std::move(obj), std::move(m)};
                      },
@@ -1758,7 +1773,7 @@ struct ApiServer::Impl {
         Value obj = *it->second.obj;
         obj["metadata"]["deletionTimestamp"] = now_rfc3339();
         obj["metadata"]["deletionGracePeriodSeconds"] = 0;
-        auto ptr = commit_locked(*p.ti, p.ns, p.name, std::move(obj), it->second.managers, &it->second);
+        auto ptr = commit_locked(*p.ti, p.ns, p.name, std::move(obj), *it->second.managers, &it->second);
         w.send_json(202, ptr->dump());
         return;
       }
