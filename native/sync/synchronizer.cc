@@ -1,6 +1,7 @@
 #include "sync/synchronizer.h"
 
 #include <algorithm>
+#include <iterator>
 #include <thread>
 #include <unordered_map>
 
@@ -179,6 +180,23 @@ TickStats Synchronizer::tick() {
   return ts;
 }
 
+// What sync_one reads from a UserBootstrap watch event (reference synchronizer.rs:218-330:
+// the name, the resourceVersion for the status PUT, spec.quota to compare, status): the rest
+// of the object (managedFields, annotations, the rest of the spec) is stepped over.
+static const json::Projection& ub_watch_projection() {
+  using P = json::Projection;
+  static const P kMeta[] = {{"name", P::Keep}, {"namespace", P::Keep}, {"uid", P::Keep}, {"resourceVersion", P::Keep}};
+  static const P kSpec[] = {{"quota", P::Keep}};
+  static const P kObject[] = {{"apiVersion", P::Keep},
+                              {"kind", P::Keep},
+                              {"metadata", P::Descend, kMeta, std::size(kMeta), true},
+                              {"spec", P::Descend, kSpec, std::size(kSpec), true},
+                              {"status", P::Keep}};
+  static const P kEvent[] = {{"type", P::Keep}, {"object", P::Descend, kObject, std::size(kObject), true}};
+  static const P kRoot{"", P::Descend, kEvent, std::size(kEvent), true};
+  return kRoot;
+}
+
 int Synchronizer::run(CancelToken& stop) {
   std::unique_ptr<std::thread> watch_thread;
   std::vector<std::thread> workers;
@@ -204,6 +222,7 @@ int Synchronizer::run(CancelToken& stop) {
   if (cfg_.watch) {
     watch_thread = std::make_unique<std::thread>([&] {
       kube::Watcher w(client_, types::UserBootstrap);
+      w.set_projection(&ub_watch_projection());
       w.run(stop, [&](const kube::WatchEvent& ev) {
         store.apply(ev);
         if (ev.type == kube::WatchEvent::Type::Restarted) {
