@@ -70,6 +70,7 @@ int main() {
   kube::Controller::Options co;
   co.workers = cfg.workers;
   co.child_delete_delay = std::chrono::milliseconds(cfg.child_delete_delay_ms);
+  co.debounce = std::chrono::milliseconds(cfg.debounce_ms);
   if (cfg.projected_watch) {
     co.primary_projection = &controller::user_bootstrap_event_projection();
     co.child_projection = &controller::child_event_projection();

@@ -58,6 +58,7 @@ struct Config {
   // 3 s.  0 = the reference's fixed error_requeue_ms (controller.rs:174).
   int64_t error_backoff_base_ms = 0;
   int64_t child_delete_delay_ms = 50;
+  int64_t debounce_ms = 0;  // kube::Controller::Options::debounce (CONF_DEBOUNCE_MS)
   bool label_children = true;  // see kManagedByLabel
   // Child watches ask for PartialObjectMetadata only: the controller reads a child's
   // resourceVersion and ownerReferences, never its spec (kube-rs metadata_watcher).

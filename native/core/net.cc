@@ -150,6 +150,10 @@ void tune_ctx(SSL_CTX* c) {
     return e && std::string(e) == "1";
   }();
   if (read_ahead) SSL_CTX_set_read_ahead(c, 1);
+  // BGC_TLS13_CIPHERSUITES (A/B knob): the TLS 1.3 suites offered/accepted, e.g.
+  // TLS_AES_128_GCM_SHA256 (OpenSSL's default list leads with AES-256-GCM)
+  static const char* suites = std::getenv("BGC_TLS13_CIPHERSUITES");
+  if (suites && *suites && SSL_CTX_set_ciphersuites(c, suites) != 1) ERR_clear_error();
 }
 }  // namespace
 

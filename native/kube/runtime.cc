@@ -489,7 +489,7 @@ void Controller::run(CancelToken& stop, Reconciler reconcile, ErrorPolicy error_
       if (ev.type == WatchEvent::Type::Restarted) {
         for (const auto& o : ev.objects) queue_.add(primary_.key(meta_namespace(*o), meta_name(*o)));
       } else if (ev.type != WatchEvent::Type::Deleted) {
-        queue_.add(primary_.key(meta_namespace(*ev.object), meta_name(*ev.object)));
+        queue_.add_after(primary_.key(meta_namespace(*ev.object), meta_name(*ev.object)), opts_.debounce);
       } else {
         // the object is gone: its periodic requeue would only find nothing
         queue_.forget(primary_.key(meta_namespace(*ev.object), meta_name(*ev.object)));
@@ -525,7 +525,7 @@ void Controller::run(CancelToken& stop, Reconciler reconcile, ErrorPolicy error_
             filtered_.fetch_add(1, std::memory_order_relaxed);
             return;
           }
-          for (const auto& k : c->mapper(*ev.object)) queue_.add(k);
+          for (const auto& k : c->mapper(*ev.object)) queue_.add_after(k, opts_.debounce);
         }
       });
     });

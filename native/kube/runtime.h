@@ -202,6 +202,10 @@ class Controller {
     // children's DELETED events can overtake the owner's own DELETED event, and reconciling
     // the stale owner would re-create children the garbage collector is removing.
     std::chrono::milliseconds child_delete_delay{50};
+    // kube-runtime's controller::Config::debounce: a watch event schedules its object's
+    // reconcile this much later, and further events for the object meanwhile merge into
+    // that one reconcile (the earliest due time wins, so a burst is delayed by at most this).
+    std::chrono::milliseconds debounce{0};
     // Selective parse of the primary watch's and the owned-kind watches' events
     // (Watcher::set_projection).
     const json::Projection* primary_projection = nullptr;

@@ -201,3 +201,25 @@ def test_owned_watches_select_only_labelled_children():
             else:
                 assert "labels" not in ns["metadata"]
                 wait_for(lambda: store(c, "namespaces") >= 21, desc="every namespace cached")
+
+
+def test_debounce_merges_a_burst_of_events_into_one_reconcile():
+    """CONF_DEBOUNCE_MS (kube-runtime's controller::Config::debounce): events for one
+    UserBootstrap within the window merge into one reconcile, which sees the last version."""
+
+    def reconciles(c):
+        m = requests.get(f"http://127.0.0.1:{c.controller_port}/metrics", timeout=5).text
+        hit = re.search(r'^bgc_reconcile_total\{result="ok"\} (\S+)$', m, re.M)
+        return float(hit.group(1)) if hit else 0.0
+
+    with Cluster(admission=False, controller_env={"CONF_DEBOUNCE_MS": "400", "CONF_REQUEUE_SECS": "3600"}) as c:
+        c.admin.create("userbootstraps", {"apiVersion": "bacchus.io/v1", "kind": "UserBootstrap",
+                                          "metadata": {"name": "burst"}, "spec": {"kube_username": "burst"}})
+        for gpus in ("1", "2", "3"):
+            c.admin.merge_patch("userbootstraps", "burst", {"spec": {"quota": {"hard": {"requests.amd.com/gpu": gpus}}}})
+        rq = wait_for(lambda: c.admin.get_or_none("resourcequotas", "burst", "burst"), timeout=10, desc="quota")
+        assert rq["spec"]["hard"]["requests.amd.com/gpu"] == "3"  # the merged reconcile saw the last version
+        time.sleep(1.0)
+        # one reconcile for the four writes (plus at most one for an apply echo that beat
+        # the apply's response), not one per write
+        assert reconciles(c) <= 2, reconciles(c)
