@@ -467,7 +467,8 @@ def run(args):
             # the reference's controller on this same stack: children applied one after
             # another and re-applied on every reconcile (controller.rs:81-149)
             env.update({"CONF_SKIP_UNCHANGED": "false", "CONF_PARALLEL_CHILDREN": "false",
-                        "CONF_LABEL_CHILDREN": "false"})  # .owns() on every object of each kind
+                        "CONF_LABEL_CHILDREN": "false",  # .owns() on every object of each kind
+                        "CONF_DEBOUNCE_MS": "0"})  # every event reconciles at once
         return env
 
     if d.rank == 0:
