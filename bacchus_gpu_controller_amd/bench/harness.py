@@ -207,16 +207,25 @@ def window_samples(doc, start=None, required=True):
 
 
 def _lock_report(l0, l1, elapsed):
+    """kube-lite's store locks over the window: every acquisition of a per-object shard lock
+    and of a type's commit-order lock (seq), how many had to wait and for how long; the
+    busiest type is the one whose seq section (the serialized part of its commits) was held
+    the largest share of the window."""
     t0, t1 = l0["total"], l1["total"]
     busiest, util = None, 0.0
     for k, v in l1["by_type"].items():
         h = v["hold_ms"] - l0["by_type"].get(k, {}).get("hold_ms", 0.0)
         if h / (elapsed * 1e3) > util:
             busiest, util = k, h / (elapsed * 1e3)
-    return {"acquisitions": t1["acquisitions"] - t0["acquisitions"],
-            "contended": t1["contended"] - t0["contended"],
+    acq = t1["acquisitions"] - t0["acquisitions"]
+    contended = t1["contended"] - t0["contended"]
+    wait_ms = t1["wait_ms"] - t0["wait_ms"]
+    return {"acquisitions": acq,
+            "contended": contended,
+            "contended_pct": round(100.0 * contended / acq, 2) if acq else 0.0,
             "hold_ms": round(t1["hold_ms"] - t0["hold_ms"], 3),
-            "wait_ms": round(t1["wait_ms"] - t0["wait_ms"], 3),
+            "wait_ms": round(wait_ms, 3),
+            "wait_s_per_s": round(wait_ms / 1e3 / elapsed, 3) if elapsed > 0 else None,
             "busiest_type": busiest, "busiest_utilisation": round(util, 4)}
 
 

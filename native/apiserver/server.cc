@@ -1,12 +1,14 @@
 #include "apiserver/server.h"
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <functional>
 #include <mutex>
+#include <optional>
 #include <regex>
 #include <set>
 #include <sstream>
@@ -398,10 +400,13 @@ class RwLock {
 // Watch wake-ups are deferred until the exclusive store lock is released (a futex wake per
 // subscriber inside the critical section would stretch every commit).
 thread_local std::vector<std::shared_ptr<WatchSub>> t_pending_wakeups;
+// History records compacted away under a lock: their lines are freed after it is released.
+thread_local std::vector<std::shared_ptr<const EventRec>> t_retired_events;
 
 inline void flush_watch_wakeups() {
   for (auto& w : t_pending_wakeups) w->cv.notify_one();
   t_pending_wakeups.clear();
+  t_retired_events.clear();
 }
 
 // Store-lock accounting (exported in /_kl/stats): exclusive hold time bounds kube-lite's
@@ -412,18 +417,30 @@ struct LockStats {
 
 class StoreLock {  // exclusive
  public:
-  StoreLock(RwLock& m, LockStats& st) : m_(m), st_(st) {
+  // `also`: a second account of the same acquisition (a type's seq lock: its own stats
+  // and the type's total)
+  StoreLock(RwLock& m, LockStats& st, LockStats* also = nullptr) : m_(m), st_(st), also_(also) {
     if (!m_.try_lock()) {
       int64_t t0 = metrics::now_ns();
       m_.lock();
+      const auto waited = static_cast<uint64_t>(metrics::now_ns() - t0);
       st_.contended.fetch_add(1, std::memory_order_relaxed);
-      st_.wait_ns.fetch_add(static_cast<uint64_t>(metrics::now_ns() - t0), std::memory_order_relaxed);
+      st_.wait_ns.fetch_add(waited, std::memory_order_relaxed);
+      if (also_) {
+        also_->contended.fetch_add(1, std::memory_order_relaxed);
+        also_->wait_ns.fetch_add(waited, std::memory_order_relaxed);
+      }
     }
     t_acq_ = metrics::now_ns();
   }
   ~StoreLock() {
+    const auto held = static_cast<uint64_t>(metrics::now_ns() - t_acq_);
     st_.acquisitions.fetch_add(1, std::memory_order_relaxed);
-    st_.hold_ns.fetch_add(static_cast<uint64_t>(metrics::now_ns() - t_acq_), std::memory_order_relaxed);
+    st_.hold_ns.fetch_add(held, std::memory_order_relaxed);
+    if (also_) {
+      also_->acquisitions.fetch_add(1, std::memory_order_relaxed);
+      also_->hold_ns.fetch_add(held, std::memory_order_relaxed);
+    }
     m_.unlock();
     flush_watch_wakeups();
   }
@@ -433,6 +450,7 @@ class StoreLock {  // exclusive
  private:
   RwLock& m_;
   LockStats& st_;
+  LockStats* also_;
   int64_t t_acq_ = 0;
 };
 
@@ -455,17 +473,70 @@ class SharedStoreLock {
   RwLock& m_;
 };
 
-// Per-resource-type storage shard (like the apiserver's per-resource storage and watch
-// cache): its own lock, objects, event history and watchers, so commits to different
-// types never serialize on each other.
+// Per-resource-type storage (like the apiserver's per-resource storage and watch cache):
+// its objects, event history and watchers, so commits to different types never serialize
+// on each other.  Within a type:
+//  * objects live in kShards key-hashed shards, each with its own lock: reads and commits
+//    of different objects proceed in parallel (the whole write path — webhook, merge,
+//    validation, the stored-version check — runs under one object's shard at most);
+//  * `seq` orders the type's events: a commit, holding its object's shard exclusively,
+//    takes seq only to assign the resourceVersion and append the event to the history
+//    and to the watchers' queues.  Lock order: shard -> seq -> watches_mu -> WatchSub::m.
+//  * a whole-type read (LIST, a watch's initial snapshot) holds every shard (AllShards),
+//    so no commit of the type is in flight while it reads; a watch resuming from a
+//    resourceVersion holds seq while it replays the history and registers.
 struct TypeStore {
-  RwLock mu;
-  LockStats stats;
-  std::unordered_map<std::string, Stored> objs;              // obj key -> stored (guarded by mu)
-  std::deque<std::shared_ptr<const EventRec>> history;       // rv-ordered (appended under exclusive mu)
+  static constexpr size_t kShards = 16;
+  struct Shard {
+    RwLock mu;
+    std::unordered_map<std::string, Stored> objs;  // obj key -> stored (guarded by mu)
+  };
+  std::array<Shard, kShards> shards;
+  Shard& shard(const std::string& key) { return shards[std::hash<std::string>{}(key) % kShards]; }
+  RwLock seq;
+  std::atomic<uint64_t> version{0};                          // bumped by every commit/erase (under seq)
+  LockStats stats;                                           // the shard locks
+  LockStats seq_stats;                                       // seq (the type's commit order)
+  std::deque<std::shared_ptr<const EventRec>> history;       // rv-ordered (appended under seq)
   uint64_t compacted_rv = 0;                                 // resumes from rv < compacted_rv get 410
-  std::mutex watches_mu;                                     // lock order: mu -> watches_mu -> WatchSub::m
+  std::mutex watches_mu;                                     // lock order: seq -> watches_mu -> WatchSub::m
   std::set<std::shared_ptr<WatchSub>> watches;
+};
+
+// Every shard of a type, in index order (the same order commits can never hold two of).
+class AllShards {
+ public:
+  AllShards(TypeStore& ts, bool exclusive) : ts_(ts), exclusive_(exclusive) {
+    for (auto& sh : ts_.shards) {
+      if (exclusive_) {
+        if (!sh.mu.try_lock()) {
+          const int64_t t0 = metrics::now_ns();
+          sh.mu.lock();
+          ts_.stats.contended.fetch_add(1, std::memory_order_relaxed);
+          ts_.stats.wait_ns.fetch_add(static_cast<uint64_t>(metrics::now_ns() - t0), std::memory_order_relaxed);
+        }
+      } else if (!sh.mu.try_lock_shared()) {
+        const int64_t t0 = metrics::now_ns();
+        sh.mu.lock_shared();
+        ts_.stats.contended.fetch_add(1, std::memory_order_relaxed);
+        ts_.stats.wait_ns.fetch_add(static_cast<uint64_t>(metrics::now_ns() - t0), std::memory_order_relaxed);
+      }
+    }
+    ts_.stats.acquisitions.fetch_add(1, std::memory_order_relaxed);
+  }
+  ~AllShards() {
+    for (auto it = ts_.shards.rbegin(); it != ts_.shards.rend(); ++it) {
+      if (exclusive_) it->mu.unlock();
+      else it->mu.unlock_shared();
+    }
+    flush_watch_wakeups();
+  }
+  AllShards(const AllShards&) = delete;
+  AllShards& operator=(const AllShards&) = delete;
+
+ private:
+  TypeStore& ts_;
+  bool exclusive_;
 };
 
 struct FaultRule {
@@ -634,7 +705,7 @@ struct ApiServer::Impl {
       Stored st;
       st.obj = std::make_shared<const Value>(std::move(ns));
       st.rv = v;
-      ns_ti.store->objs[name] = std::move(st);
+      ns_ti.store->shard(obj_key(ns_ti.rt, "", name)).objs[obj_key(ns_ti.rt, "", name)] = std::move(st);
     }
     for (int i = 0; i < std::max(1, opts.gc_workers); ++i) gc_threads.emplace_back([this] { gc_loop(); });
   }
@@ -795,7 +866,6 @@ struct ApiServer::Impl {
   }
 
   // ---------------------------------------------------------------- events
-  // Caller holds ti.store->mu exclusively.
   // Work moved out of the exclusive section (see prepare_commit).
   struct PreparedEvent {
     std::string head, tail;  // event line = head + rv digits + tail
@@ -806,32 +876,32 @@ struct ApiServer::Impl {
     std::shared_ptr<EventRec> rec;
   };
 
-  std::shared_ptr<const std::string> emit_locked(const std::string& type, const TypeInfo& ti, const std::string& ns,
-                                                 const std::shared_ptr<const Value>& obj, uint64_t ev_rv,
-                                                 std::string preline = {}, const PreparedEvent* pe = nullptr) {
+  // Appends one event to the type's history and to its watchers' queues.  Caller holds
+  // ti.store->seq.  `filter` is the event object's {"metadata":{"name","labels"}} view,
+  // which is all a watch filters on.
+  std::shared_ptr<const std::string> emit_locked(const TypeInfo& ti, const std::string& ns, uint64_t ev_rv,
+                                                 std::string line, std::shared_ptr<const Value> filter,
+                                                 std::shared_ptr<EventRec> rec) {
     TypeStore& st = *ti.store;
-    auto rec = pe && pe->rec ? pe->rec : std::make_shared<EventRec>();
+    st.version.fetch_add(1, std::memory_order_release);
+    if (!rec) rec = std::make_shared<EventRec>();
     rec->rv = ev_rv;
     rec->type_key = ti.key();
     rec->ns = ns;
-    rec->meta = pe && pe->filter ? pe->filter : filter_view(*obj);
-    std::string line = std::move(preline);
-    if (line.empty()) {
-      line = "{\"type\":\"" + type + "\",\"object\":";
-      obj->dump_to(line);
-      line += "}\n";
-    }
+    rec->meta = std::move(filter);
     rec->line = std::make_shared<const std::string>(std::move(line));
     st.history.push_back(rec);
     while (st.history.size() > opts.history_limit) {
       st.compacted_rv = st.history.front()->rv;
+      t_retired_events.push_back(std::move(st.history.front()));  // freed after the lock
       st.history.pop_front();
     }
+    const std::string& name = rec->meta->get("metadata").get_string("name");
     std::lock_guard<std::mutex> wg(st.watches_mu);
     for (const auto& w : st.watches) {
       if (!w->ns.empty() && w->ns != ns) continue;
-      if (!w->fields.name_ok(obj->get("metadata").get_string("name"))) continue;
-      if (!w->sel.empty() && !selector_matches(w->sel, *obj)) continue;
+      if (!w->fields.name_ok(name)) continue;
+      if (!w->sel.empty() && !selector_matches(w->sel, *rec->meta)) continue;
       {
         std::lock_guard<std::mutex> g(w->m);
         if (w->q.size() > 100000) w->overflow = true;
@@ -848,14 +918,30 @@ struct ApiServer::Impl {
     std::shared_ptr<const Value> cfg;  // keeps `hook` alive (stored objects are immutable)
     const Value* hook;
   };
+  std::mutex hook_match_mu;                    // matching_webhooks' cache
+  uint64_t hook_match_version = ~uint64_t{0};  // MWC store version the cache is for
+  std::unordered_map<std::string, std::vector<HookMatch>> hook_match_cache;
 
+  // The hooks a request triggers, cached per (type, subresource, operation) for one version
+  // of the MutatingWebhookConfigurations: every UserBootstrap write asks, and scanning the
+  // configurations under all their shard locks each time serialized the writers.
   std::vector<HookMatch> matching_webhooks(const TypeInfo& ti, const std::string& sub, const std::string& op) {
-    std::vector<HookMatch> out;
     TypeInfo* mwc = type_by_key(kube::types::MutatingWebhookConfiguration.group + "/v1/mutatingwebhookconfigurations");
-    if (!mwc) return out;
-    SharedStoreLock lk(mwc->store->mu, mwc->store->stats);
+    if (!mwc) return {};
+    const std::string cache_key = ti.key() + "|" + sub + "|" + op;
+    {
+      std::lock_guard<std::mutex> g(hook_match_mu);
+      if (hook_match_version == mwc->store->version.load(std::memory_order_acquire)) {
+        auto it = hook_match_cache.find(cache_key);
+        if (it != hook_match_cache.end()) return it->second;
+      }
+    }
+    std::vector<HookMatch> out;
+    AllShards lk(*mwc->store, false);
+    const uint64_t version = mwc->store->version.load(std::memory_order_acquire);  // no commit in flight
     std::string res = ti.rt.plural + (sub.empty() ? "" : "/" + sub);
-    for (auto& kv : mwc->store->objs) {
+    for (auto& sh : mwc->store->shards)
+    for (auto& kv : sh.objs) {
       for (const auto& hook : kv.second.obj->get("webhooks").items()) {
         for (const auto& rule : hook.get("rules").items()) {
           auto contains = [](const Value& arr, const std::string& v) {
@@ -879,6 +965,14 @@ struct ApiServer::Impl {
           }
         }
       }
+    }
+    {
+      std::lock_guard<std::mutex> g(hook_match_mu);
+      if (hook_match_version != version) {
+        hook_match_cache.clear();
+        hook_match_version = version;
+      }
+      hook_match_cache[cache_key] = out;
     }
     return out;
   }
@@ -1118,14 +1212,14 @@ struct ApiServer::Impl {
   }
 
   // ---------------------------------------------------------------- storage helpers
-  static std::unordered_map<std::string, Stored>& bucket(const TypeInfo& ti) { return ti.store->objs; }
-
   bool namespace_exists(const std::string& ns) {
     TypeInfo* nti = type_by_key(kube::types::Namespace.group + "/v1/namespaces");
     if (!nti) return false;
-    SharedStoreLock lk(nti->store->mu, nti->store->stats);
-    auto it = nti->store->objs.find(ns);
-    return it != nti->store->objs.end() && !it->second.obj->get("metadata").contains("deletionTimestamp");
+    const std::string key = obj_key(nti->rt, "", ns);
+    auto& sh = nti->store->shard(key);
+    SharedStoreLock lk(sh.mu, nti->store->stats);
+    auto it = sh.objs.find(key);
+    return it != sh.objs.end() && !it->second.obj->get("metadata").contains("deletionTimestamp");
   }
 
   static void render_managed(Value& obj, const Managers& m, const std::string& api_version) {
@@ -1256,50 +1350,67 @@ struct ApiServer::Impl {
     return pe;
   }
 
-  // Commits `obj` (already validated) under the type's exclusive lock. Returns the stored
-  // object; *dangling is set when every owner reference points at a deleted object.
+  // Commits `obj` (already validated).  Caller holds the object's shard exclusively; the
+  // type's seq lock is taken here only to assign the resourceVersion and emit the event.
+  // Returns the stored object; *dangling is set when every owner reference points at a
+  // deleted object.
   std::shared_ptr<const Value> commit_locked(const TypeInfo& ti, const std::string& ns, const std::string& name,
                                             Value obj, Managers managers, const Stored* prev,
                                             const PreparedEvent* pe = nullptr, bool* dangling = nullptr,
                                             std::shared_ptr<const std::string>* line_out = nullptr) {
-    uint64_t new_rv = ++rv;
-    std::string digits = rv_str(new_rv);
-    Value& meta = obj["metadata"];
-    meta["resourceVersion"] = digits;
-    std::string preline;
-    if (pe && pe->ok) {
-      preline.reserve(pe->head.size() + digits.size() + pe->tail.size());
-      preline += pe->head;
-      preline += digits;
-      preline += pe->tail;
-    } else {
-      render_managed(obj, managers, ti.rt.api_version());
+    TypeStore& ts = *ti.store;
+    PreparedEvent local;
+    if (!pe || !pe->ok) {
+      local = prepare_commit(obj, managers, ti.rt.api_version(), prev ? "MODIFIED" : "ADDED");
+      pe = &local;
     }
-    auto ptr = std::make_shared<const Value>(std::move(obj));
-    auto& b = bucket(ti);
-    Stored s;
-    s.obj = ptr;
-    s.rv = new_rv;
-    s.managers = std::make_shared<const Managers>(std::move(managers));
     std::string key = obj_key(ti.rt, ns, name);
     Ref ref{ti.key(), key};
     {
+      // Indexed before the event is out: a client that reacts to it (creating a dependent
+      // of this object) must find the owner in by_uid.  Indexed and checked in one critical
+      // section: either the owner's deletion sees this dependent in by_owner (and the GC
+      // removes it) or this check sees the owner gone.
       std::lock_guard<std::mutex> ig(index_mu);
       if (prev) unindex_owners_locked(*prev->obj, ref);
-      by_uid[ptr->get("metadata").get_string("uid")] = ref;
-      const Value& owners = ptr->get("metadata").get("ownerReferences");
+      by_uid[obj.get("metadata").get_string("uid")] = ref;
+      const Value& owners = obj.get("metadata").get("ownerReferences");
       for (const auto& r : owners.items()) by_owner[r.get_string("uid")].insert(ref);
       if (ti.rt.namespaced) by_namespace[ns].insert(ref);
-      // indexed and checked in one critical section: either the owner's deletion sees this
-      // dependent in by_owner (and the GC removes it) or this check sees the owner gone
       if (dangling && !prev && !owners.empty()) {
         bool alive = false;
         for (const auto& r : owners.items()) alive = alive || by_uid.count(r.get_string("uid")) > 0;
         *dangling = !alive;
       }
     }
-    b[key] = std::move(s);
-    auto line = emit_locked(prev ? "MODIFIED" : "ADDED", ti, ns, ptr, new_rv, std::move(preline), pe);
+    uint64_t new_rv;
+    std::string digits;
+    std::shared_ptr<const std::string> line;
+    {
+      StoreLock sl(ts.seq, ts.seq_stats);
+      new_rv = ++rv;
+      digits = rv_str(new_rv);
+      std::string preline;
+      if (pe->ok) {
+        preline.reserve(pe->head.size() + digits.size() + pe->tail.size());
+        preline += pe->head;
+        preline += digits;
+        preline += pe->tail;
+      } else {  // no resourceVersion placeholder found (never for a prepared object)
+        obj["metadata"]["resourceVersion"] = digits;
+        preline = std::string("{\"type\":\"") + (prev ? "MODIFIED" : "ADDED") + "\",\"object\":";
+        obj.dump_to(preline);
+        preline += "}\n";
+      }
+      line = emit_locked(ti, ns, new_rv, std::move(preline), pe->filter ? pe->filter : filter_view(obj), pe->rec);
+    }
+    obj["metadata"]["resourceVersion"] = digits;
+    auto ptr = std::make_shared<const Value>(std::move(obj));
+    Stored s;
+    s.obj = ptr;
+    s.rv = new_rv;
+    s.managers = std::make_shared<const Managers>(std::move(managers));
+    ts.shard(key).objs[key] = std::move(s);
     if (line_out) *line_out = std::move(line);
     return ptr;
   }
@@ -1313,35 +1424,24 @@ struct ApiServer::Impl {
     }
   }
 
-  // Removes an object under its type's exclusive lock and hands its dependents (and, for a
-  // Namespace, its contents) to the garbage collector.
+  // Removes an object and hands its dependents (and, for a Namespace, its contents) to the
+  // garbage collector.  Caller holds the object's shard exclusively.
   void erase_locked(const TypeInfo& ti, const std::string& ns, const std::string& name) {
-    auto& b = bucket(ti);
+    TypeStore& ts = *ti.store;
     std::string key = obj_key(ti.rt, ns, name);
+    auto& b = ts.shard(key).objs;
     auto it = b.find(key);
     if (it == b.end()) return;
-    uint64_t new_rv = ++rv;
-    // The DELETED event carries the object at the new resourceVersion: splice the digits
-    // into its serialization instead of deep-copying the tree under the exclusive lock.
+    // The DELETED event carries the object at the new resourceVersion: its serialization is
+    // split around the stored resourceVersion and the new digits are spliced in under seq.
     std::shared_ptr<const Value> ptr = it->second.obj;
     std::string line = "{\"type\":\"DELETED\",\"object\":";
     const size_t obj_at = line.size();
     ptr->dump_to(line);
     line += "}\n";
-    {
-      const std::string old_rv = "\"resourceVersion\":" + json::quote(ptr->get("metadata").get_string("resourceVersion"));
-      size_t pos = line.find(old_rv, obj_at);
-      if (pos != std::string::npos) {
-        line.replace(pos, old_rv.size(), "\"resourceVersion\":\"" + rv_str(new_rv) + "\"");
-      } else {  // no resourceVersion in the stored object (never for committed objects)
-        Value final_obj = *ptr;
-        final_obj["metadata"]["resourceVersion"] = rv_str(new_rv);
-        ptr = std::make_shared<const Value>(std::move(final_obj));
-        line = "{\"type\":\"DELETED\",\"object\":";
-        ptr->dump_to(line);
-        line += "}\n";
-      }
-    }
+    const std::string old_rv = "\"resourceVersion\":" + json::quote(ptr->get("metadata").get_string("resourceVersion"));
+    const size_t pos = line.find(old_rv, obj_at);
+    auto filter = filter_view(*ptr);
     std::string uid = ptr->get("metadata").get_string("uid");
     Ref ref{ti.key(), key};
     bool has_dependents;
@@ -1358,8 +1458,23 @@ struct ApiServer::Impl {
       }
       has_dependents = by_owner.count(uid) > 0;
     }
+    uint64_t new_rv;
+    {
+      StoreLock sl(ts.seq, ts.seq_stats);
+      new_rv = ++rv;
+      const std::string digits = rv_str(new_rv);
+      if (pos != std::string::npos) {
+        line.replace(pos, old_rv.size(), "\"resourceVersion\":\"" + digits + "\"");
+      } else {  // no resourceVersion in the stored object (never for committed objects)
+        Value final_obj = *ptr;
+        final_obj["metadata"]["resourceVersion"] = digits;
+        line = "{\"type\":\"DELETED\",\"object\":";
+        final_obj.dump_to(line);
+        line += "}\n";
+      }
+      emit_locked(ti, ns, new_rv, std::move(line), std::move(filter), nullptr);
+    }
     b.erase(it);
-    emit_locked("DELETED", ti, ns, ptr, new_rv, std::move(line));
     bool is_ns = ti.rt.plural == "namespaces" && ti.rt.group.empty();
     if (has_dependents || is_ns) {
       std::lock_guard<std::mutex> g(gc_mu);
@@ -1391,9 +1506,10 @@ struct ApiServer::Impl {
       for (const auto& v : victims) {
         TypeInfo* vti = type_by_key(v.first);
         if (!vti) continue;
-        StoreLock lk(vti->store->mu, vti->store->stats);
-        auto it = vti->store->objs.find(v.second);
-        if (it == vti->store->objs.end()) continue;
+        auto& vsh = vti->store->shard(v.second);
+        StoreLock lk(vsh.mu, vti->store->stats);
+        auto it = vsh.objs.find(v.second);
+        if (it == vsh.objs.end()) continue;
         const Value& meta = it->second.obj->get("metadata");
         if (!item.is_namespace) {
           bool alive = false;
@@ -1420,11 +1536,12 @@ struct ApiServer::Impl {
     for (int attempt = 0; attempt < 8; ++attempt) {
       Stored cur_copy;
       bool exists = false;
+      const std::string key = obj_key(ti.rt, ns, name);
+      auto& sh = ti.store->shard(key);
       {
-        SharedStoreLock lk(ti.store->mu, ti.store->stats);
-        auto& b = bucket(ti);
-        auto it = b.find(obj_key(ti.rt, ns, name));
-        if (it != b.end()) {
+        SharedStoreLock lk(sh.mu, ti.store->stats);
+        auto it = sh.objs.find(key);
+        if (it != sh.objs.end()) {
           cur_copy = it->second;
           exists = true;
         }
@@ -1459,10 +1576,9 @@ struct ApiServer::Impl {
         obj["metadata"]["generation"] = gen + 1;
       }
       PreparedEvent pe = prepare_commit(obj, managers, ti.rt.api_version(), exists ? "MODIFIED" : "ADDED");
-      StoreLock lk(ti.store->mu, ti.store->stats);
-      auto& b = bucket(ti);
-      auto it = b.find(obj_key(ti.rt, ns, name));
-      bool now_exists = it != b.end();
+      StoreLock lk(sh.mu, ti.store->stats);
+      auto it = sh.objs.find(key);
+      bool now_exists = it != sh.objs.end();
       if (now_exists != exists || (exists && it->second.rv != cur_copy.rv)) continue;  // raced: retry
       if (exists) {
         // finalizer-gated deletion completes when the last finalizer is removed
@@ -1755,18 +1871,18 @@ struct ApiServer::Impl {
 
   void do_delete(ParsedPath& p, const http::Request& req, const UserInfo& user, http::ResponseWriter& w) {
     std::shared_ptr<const Value> cur;
+    const std::string key = obj_key(p.ti->rt, p.ns, p.name);
+    auto& sh = p.ti->store->shard(key);
     {
-      SharedStoreLock lk(p.ti->store->mu, p.ti->store->stats);
-      auto& b = bucket(*p.ti);
-      auto it = b.find(obj_key(p.ti->rt, p.ns, p.name));
-      if (it == b.end()) throw not_found(p.ti->rt, p.name);
+      SharedStoreLock lk(sh.mu, p.ti->store->stats);
+      auto it = sh.objs.find(key);
+      if (it == sh.objs.end()) throw not_found(p.ti->rt, p.name);
       cur = it->second.obj;
     }
     call_webhooks(*p.ti, "", "DELETE", p.ns, p.name, nullptr, cur.get(), user);
-    StoreLock lk(p.ti->store->mu, p.ti->store->stats);
-    auto& b = bucket(*p.ti);
-    auto it = b.find(obj_key(p.ti->rt, p.ns, p.name));
-    if (it == b.end()) throw not_found(p.ti->rt, p.name);
+    StoreLock lk(sh.mu, p.ti->store->stats);
+    auto it = sh.objs.find(key);
+    if (it == sh.objs.end()) throw not_found(p.ti->rt, p.name);
     const Value& meta = it->second.obj->get("metadata");
     if (!meta.get("finalizers").empty()) {
       if (!meta.contains("deletionTimestamp")) {
@@ -1788,10 +1904,11 @@ struct ApiServer::Impl {
   void do_get(ParsedPath& p, http::ResponseWriter& w, bool meta_only = false) {
     std::shared_ptr<const Value> obj;
     {
-      SharedStoreLock lk(p.ti->store->mu, p.ti->store->stats);
-      auto& b = bucket(*p.ti);
-      auto it = b.find(obj_key(p.ti->rt, p.ns, p.name));
-      if (it == b.end()) throw not_found(p.ti->rt, p.name);
+      const std::string key = obj_key(p.ti->rt, p.ns, p.name);
+      auto& sh = p.ti->store->shard(key);
+      SharedStoreLock lk(sh.mu, p.ti->store->stats);
+      auto it = sh.objs.find(key);
+      if (it == sh.objs.end()) throw not_found(p.ti->rt, p.name);
       obj = it->second.obj;
     }
     if (meta_only) {
@@ -1830,11 +1947,12 @@ struct ApiServer::Impl {
       auto sel = parse_selector(req.query_param("labelSelector"));
       auto ff = parse_field_selector(req.query_param("fieldSelector"));
       {
-        // no commit of this type is in flight while we hold its shared lock, so every event
+        // no commit of this type is in flight while we hold all its shards, so every event
         // of this type with rv <= list_rv is reflected in the items
-        SharedStoreLock lk(p.ti->store->mu, p.ti->store->stats);
+        AllShards lk(*p.ti->store, false);
         list_rv = rv.load();
-        for (auto& [k, st] : bucket(*p.ti)) {
+        for (auto& sh : p.ti->store->shards)
+        for (auto& [k, st] : sh.objs) {
           const Value& meta = st.obj->get("metadata");
           if (!p.ns.empty() && meta.get_string("namespace") != p.ns) continue;
           if (!ff.name_ok(meta.get_string("name"))) continue;
@@ -1920,13 +2038,18 @@ struct ApiServer::Impl {
     uint64_t compacted = 0;
     uint64_t initial_rv = 0;
     {
-      // shared: no commit of this type can interleave between the snapshot/history scan and
-      // the registration below
-      SharedStoreLock lk(ts.mu, ts.stats);
+      // No event of this type can interleave between the snapshot / history scan and the
+      // registration below: a snapshot holds every shard (no commit of the type in flight),
+      // a history replay holds seq (where commits append their events).
+      const bool snapshot = rv_s.empty() || rv_s == "0" || send_initial;
+      std::optional<AllShards> shards_lk;
+      if (snapshot) shards_lk.emplace(ts, false);
+      SharedStoreLock lk(ts.seq, ts.seq_stats);
       compacted = ts.compacted_rv;
       initial_rv = rv.load();
-      if (rv_s.empty() || rv_s == "0" || send_initial) {
-        for (auto& [k, st] : ts.objs) {
+      if (snapshot) {
+        for (auto& sh : ts.shards)
+        for (auto& [k, st] : sh.objs) {
           const Value& meta = st.obj->get("metadata");
           if (!sub.ns.empty() && meta.get_string("namespace") != sub.ns) continue;
           if (!sub.fields.name_ok(meta.get_string("name"))) continue;
@@ -2014,7 +2137,7 @@ struct ApiServer::Impl {
         uint64_t cur_rv;
         std::vector<std::shared_ptr<const EventRec>> pending;
         {
-          SharedStoreLock lk(ts.mu, ts.stats);
+          SharedStoreLock lk(ts.seq, ts.seq_stats);  // every event of the type up to cur_rv is queued
           cur_rv = rv.load();
           std::lock_guard<std::mutex> g(sub.m);
           pending.assign(sub.q.begin(), sub.q.end());
@@ -2180,7 +2303,7 @@ struct ApiServer::Impl {
     if (req.path == "/_kl/compact" && req.method == "POST") {
       uint64_t at = 0;
       for_each_store([&](const std::string&, TypeStore& ts) {
-        StoreLock lk(ts.mu, ts.stats);
+        StoreLock lk(ts.seq, ts.seq_stats);
         at = rv.load();
         ts.compacted_rv = at;
         ts.history.clear();
@@ -2205,21 +2328,38 @@ struct ApiServer::Impl {
       uint64_t acq = 0, contended = 0, wait_ns = 0, hold_ns = 0;
       for_each_store([&](const std::string& key, TypeStore& ts) {
         {
-          SharedStoreLock lk(ts.mu, ts.stats);
-          counts[key] = static_cast<unsigned long long>(ts.objs.size());
-          total += ts.objs.size();
+          AllShards lk(ts, false);
+          size_t n = 0;
+          for (auto& sh : ts.shards) n += sh.objs.size();
+          counts[key] = static_cast<unsigned long long>(n);
+          total += n;
         }
         {
           std::lock_guard<std::mutex> wg(ts.watches_mu);
           n_watches += ts.watches.size();
         }
-        uint64_t a = ts.stats.acquisitions.load(), h = ts.stats.hold_ns.load();
-        acq += a;
-        hold_ns += h;
-        contended += ts.stats.contended.load();
-        wait_ns += ts.stats.wait_ns.load();
-        if (a) locks[key] = Value::object({{"acquisitions", static_cast<unsigned long long>(a)},
-                                           {"hold_ms", static_cast<double>(h) * 1e-6}});
+        // shard locks and the commit-order lock (seq) together; by type, each on its own
+        auto account = [](const LockStats& st) {
+          return Value::object({{"acquisitions", static_cast<unsigned long long>(st.acquisitions.load())},
+                                {"contended", static_cast<unsigned long long>(st.contended.load())},
+                                {"wait_ms", static_cast<double>(st.wait_ns.load()) * 1e-6},
+                                {"hold_ms", static_cast<double>(st.hold_ns.load()) * 1e-6}});
+        };
+        for (const LockStats* st : {&ts.stats, &ts.seq_stats}) {
+          acq += st->acquisitions.load();
+          hold_ns += st->hold_ns.load();
+          contended += st->contended.load();
+          wait_ns += st->wait_ns.load();
+        }
+        const uint64_t a = ts.stats.acquisitions.load() + ts.seq_stats.acquisitions.load();
+        if (a) {
+          // "hold_ms": the serialized part, the commit-order section (what bounds a type's
+          // commit rate); "shards": the per-object locks
+          locks[key] = Value::object({{"acquisitions", static_cast<unsigned long long>(a)},
+                                      {"hold_ms", static_cast<double>(ts.seq_stats.hold_ns.load()) * 1e-6},
+                                      {"seq", account(ts.seq_stats)},
+                                      {"shards", account(ts.stats)}});
+        }
       });
       w.send_json(200, Value::object({{"resourceVersion", static_cast<unsigned long long>(rv.load())},
                                       {"objects", static_cast<unsigned long long>(total)},

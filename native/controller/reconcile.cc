@@ -278,9 +278,13 @@ bool Reconciler::up_to_date(const DesiredChild& c, const std::string& body_hash)
   auto it = sh.last_applied.find(child_key(c));
   if (it == sh.last_applied.end() || it->second.body_hash != body_hash) return false;
   const Applied& a = it->second;
-  if (!cur) return !a.prev_present;
-  const std::string rv = kube::meta_rv(*cur);
-  return rv == a.rv || (a.prev_present && rv == a.prev_rv);
+  const std::string rv = cur ? kube::meta_rv(*cur) : std::string();
+  if (cur && rv == a.rv) return true;
+  // The echo is in flight only briefly (milliseconds): past that, a cache that still shows
+  // the old state means the object changed or went away in a way whose events arrived
+  // before our record of the apply (e.g. created and deleted again meanwhile).
+  if (std::chrono::steady_clock::now() - a.at > std::chrono::seconds(2)) return false;
+  return cur ? (a.prev_present && rv == a.prev_rv) : !a.prev_present;
 }
 
 void Reconciler::apply_child(const DesiredChild& c, const std::string& body_hash, const std::string& body_json) {
@@ -293,7 +297,8 @@ void Reconciler::apply_child(const DesiredChild& c, const std::string& body_hash
     Shard& sh = shard(c.name);
     std::lock_guard<std::mutex> lk(sh.mu);
     auto [it, inserted] = sh.last_applied.try_emplace(child_key(c));
-    it->second = {body_hash, std::move(rv), before ? kube::meta_rv(*before) : std::string(), before != nullptr};
+    it->second = {body_hash, std::move(rv), before ? kube::meta_rv(*before) : std::string(), before != nullptr,
+                  std::chrono::steady_clock::now()};
     if (inserted) applied_entries_.fetch_add(1, std::memory_order_relaxed);
   }
   publish_cache_sizes();
@@ -366,8 +371,12 @@ kube::Action Reconciler::reconcile(const kube::ObjPtr& ub_ptr) {
     apply_all(children, run_one);
   } catch (...) {
     {
+      // A failed apply invalidates what we remember of this tenant's children (e.g. a
+      // ResourceQuota refused because its Namespace is gone): the retry re-applies them all.
       std::lock_guard<std::mutex> lk(sh.mu);
-      if (!owner_live(owner_name, owner_uid)) forget_owner_locked(sh, owner_name);
+      const int failures = sh.failures.count(owner_name) ? sh.failures[owner_name] : 0;
+      forget_owner_locked(sh, owner_name);
+      if (failures && owner_live(owner_name, owner_uid)) sh.failures[owner_name] = failures;  // keep the backoff
     }
     publish_cache_sizes();
     throw;

@@ -18,6 +18,7 @@
 #pragma once
 
 #include <array>
+#include <chrono>
 #include <atomic>
 #include <functional>
 #include <memory>
@@ -129,6 +130,7 @@ class Reconciler {
     std::string rv;       // what our apply returned
     std::string prev_rv;  // what the watch cache showed just before it (prev_present)
     bool prev_present = false;
+    std::chrono::steady_clock::time_point at{};  // when the apply returned
   };
   // Fast path for periodic resyncs: after a fully successful reconcile, the UB's
   // resourceVersion and each child's resourceVersion. A later reconcile of the same UB
