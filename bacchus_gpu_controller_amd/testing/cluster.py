@@ -8,6 +8,7 @@ Used by tests/integration and by bench.py.
 import base64
 import json
 import os
+import re
 import socket
 import subprocess
 import tempfile
@@ -116,7 +117,11 @@ class Cluster:
         keep = os.environ.get("BGC_CLUSTER_LOGDIR")  # keep component logs (sanitizer runs)
         if workdir is None and keep:
             os.makedirs(keep, exist_ok=True)
-            workdir = tempfile.mkdtemp(prefix="cluster-", dir=keep)
+            # named after the running test (truncated: unix socket paths go under it), so a
+            # sanitizer report leads back to it
+            test = os.environ.get("PYTEST_CURRENT_TEST", "").split(" ")[0].rsplit("::", 1)[-1]
+            prefix = "cluster-" + re.sub(r"[^A-Za-z0-9_.-]", "_", test)[:32] + "-" if test else "cluster-"
+            workdir = tempfile.mkdtemp(prefix=prefix, dir=keep)
         if workdir is None:
             self._tmp = tempfile.TemporaryDirectory(prefix="bgc-cluster-")
             workdir = self._tmp.name

@@ -268,23 +268,12 @@ bool Store::wait_synced(std::chrono::milliseconds timeout) const {
 // WorkQueue
 
 void WorkQueue::schedule_locked(const std::string& key, Clock::time_point t) {
-  auto d = due_.find(key);
-  if (d != due_.end()) {
-    // Moving a key earlier (an event arriving for a key with a pending 30 s requeue):
-    // drop its old timeline node now rather than leaving a stale one for up to the
-    // requeue period, which under churn piles up by the hundreds of thousands.
-    auto range = timeline_.equal_range(d->second);
-    for (auto it = range.first; it != range.second; ++it) {
-      if (it->second == key) {
-        timeline_.erase(it);
-        break;
-      }
-    }
-    d->second = t;
-  } else {
-    due_.emplace(key, t);
-  }
-  timeline_.emplace(t, key);
+  auto [d, fresh] = due_.try_emplace(key);
+  // Moving a key earlier (an event for a key with a pending 30 s requeue) drops its old node.
+  if (!fresh) timeline_.erase(d->second.node);
+  d->second.t = t;
+  d->second.node = (timeline_.empty() || !(t < timeline_.rbegin()->first)) ? timeline_.emplace_hint(timeline_.end(), t, key)
+                                                                           : timeline_.emplace(t, key);
   if (t <= Clock::now()) {
     if (idle_ > 0) cv_.notify_one();
     else if (timer_waiter_) timer_cv_.notify_one();
@@ -327,7 +316,7 @@ void WorkQueue::add_after_locked(const std::string& key, Clock::time_point t) {
     return;
   }
   auto it = due_.find(key);
-  if (it != due_.end() && it->second <= t) return;
+  if (it != due_.end() && it->second.t <= t) return;
   schedule_locked(key, t);
 }
 
@@ -340,13 +329,7 @@ void WorkQueue::forget(const std::string& key) {
     count_locked();
     return;
   }
-  auto range = timeline_.equal_range(d->second);
-  for (auto it = range.first; it != range.second; ++it) {
-    if (it->second == key) {
-      timeline_.erase(it);
-      break;
-    }
-  }
+  timeline_.erase(d->second.node);
   due_.erase(d);
   count_locked();
 }
@@ -356,17 +339,11 @@ bool WorkQueue::get(std::string& key) {
   while (true) {
     if (shutdown_) return false;
     auto now = Clock::now();
-    while (!timeline_.empty()) {
+    if (!timeline_.empty() && !(timeline_.begin()->first > now)) {
       auto it = timeline_.begin();
-      auto d = due_.find(it->second);
-      if (d == due_.end() || d->second != it->first) {
-        timeline_.erase(it);  // stale entry (superseded by an earlier due time)
-        continue;
-      }
-      if (it->first > now) break;
-      key = it->second;
+      key = std::move(it->second);
       timeline_.erase(it);
-      due_.erase(d);
+      due_.erase(key);
       processing_.insert(key);
       count_locked();
       // hand the timer role on if more work is waiting and nobody is timing it
@@ -402,7 +379,7 @@ void WorkQueue::done_locked(const std::string& key) {
     auto t = it->second;
     deferred_.erase(it);
     auto d = due_.find(key);
-    if (d == due_.end() || t < d->second) schedule_locked(key, t);
+    if (d == due_.end() || t < d->second.t) schedule_locked(key, t);
   }
 }
 

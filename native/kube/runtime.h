@@ -170,8 +170,17 @@ class WorkQueue {
   Clock::time_point timer_target_{};
   // Hash containers: under churn the queue holds a pending 30 s requeue for every live
   // UserBootstrap, and ordered maps paid a chain of string compares per operation.
-  std::unordered_map<std::string, Clock::time_point> due_;       // key -> due time
-  std::multimap<Clock::time_point, std::string> timeline_;        // due time -> key (may hold stale entries)
+  // due_ and timeline_ index each other one to one: a key's entry holds its timeline node,
+  // so moving or dropping a key erases that node directly (no equal_range walk, no stale
+  // nodes left behind), and the common insert, a periodic requeue later than everything
+  // queued, goes in at the end with a hint instead of a search from the root.
+  using Timeline = std::multimap<Clock::time_point, std::string>;
+  struct Due {
+    Clock::time_point t;
+    Timeline::iterator node;
+  };
+  std::unordered_map<std::string, Due> due_;  // key -> due time and its timeline node
+  Timeline timeline_;                         // due time -> key
   std::unordered_set<std::string> processing_;
   std::unordered_map<std::string, Clock::time_point> deferred_;  // re-added while processing
   std::unordered_set<std::string> forgotten_;                    // forgotten while processing

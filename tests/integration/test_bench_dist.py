@@ -60,6 +60,28 @@ def test_bench_approve_after_create():
     assert d["create_to_approve_p50_ms"] > 0
 
 
+def test_default_run_carries_the_reference_arms():
+    """The default single-GPU run also times the reference's controller behaviour on the same
+    stack and both controllers at an etcd-like write latency; every
+    arm's percentiles come from whole windows."""
+    cmd = [sys.executable, os.path.join(REPO_ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--batch", "20",
+           "--rounds", "1", "--no-tuned-phase", "--no-http1-phase", "--arm-steps", "2", "--arm-warmup", "1"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=REPO_ROOT,
+                       env=dict(os.environ, BGC_BENCH_CPU="1"))
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["vs_baseline"] is None and d["samples_complete"] is True
+    assert d["reconciles"] == d["reconcile_total_delta"] and d["webhook_calls"] == d["webhook_calls_total_delta"]
+    rc = d["reference_controller"]
+    assert rc["semantics"] == "reference-controller" and rc["failed_crs"] == 0 and rc["value"] > 0
+    assert rc["reconciles"] == rc["reconcile_total_delta"] and rc["this_over_reference_cr_per_s"] > 0
+    wl = d["write_latency_2ms"]
+    for side in ("this", "reference_controller"):
+        assert wl[side]["apiserver_write_latency_ms"] == 2 and wl[side]["failed_crs"] == 0
+        assert wl[side]["steps"] == 2 and wl[side]["reconciles"] == wl[side]["reconcile_total_delta"]
+    assert wl["this_over_reference_cr_per_s"] > 0
+
+
 def test_auto_concurrency_follows_cpu_share():
     from bacchus_gpu_controller_amd.bench.harness import auto_concurrency, effective_cpus
 

@@ -74,6 +74,8 @@ for name in names:
     arm = {k: [d.get(k) for d in rows] for k in keys}
     for k in cpu_keys:
         arm[f"cpu_ms_per_cr.{k}"] = [(d.get("cpu_ms_per_cr") or {}).get(k) for d in rows]
+    for k in ("contended_pct", "wait_s_per_s"):
+        arm[f"store_lock.{k}"] = [(d.get("apiserver_store_lock") or {}).get(k) for d in rows]
     summary[name] = {k: {"median": statistics.median(v) if all(x is not None for x in v) else None, "all": v}
                      for k, v in arm.items()}
 json.dump(summary, open(f"{out}/summary.json", "w"), indent=1)

@@ -37,11 +37,11 @@ if [ "$mode" = asan-py ]; then
   python3 tools/lsan_filter.py "$logs"/asan* || exit 1
   exit $rc
 fi
-ninja -C "build-$preset" -j "${JOBS:-8}" controller admission synchronizer node-agent kube-lite || exit 1
+ninja -C "build-$preset" -j "${JOBS:-8}" controller admission synchronizer node-agent kube-lite crdgen || exit 1
 logs="$PWD/build-$preset/logs"
 rm -rf "$logs"
 export BGC_BIN_DIR="$PWD/build-$preset/bin" BGC_CLUSTER_LOGDIR="$logs"
-export ASAN_OPTIONS=detect_leaks=1:abort_on_error=1
+export ASAN_OPTIONS=${ASAN_OPTIONS:-detect_leaks=1:abort_on_error=1}
 export TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1 suppressions=$PWD/tools/tsan.supp"
 python3 -m pytest tests/integration -q -p no:cacheprovider "${@:2}"
 rc=$?
