@@ -220,7 +220,8 @@ def _lock_report(l0, l1, elapsed):
     acq = t1["acquisitions"] - t0["acquisitions"]
     contended = t1["contended"] - t0["contended"]
     wait_ms = t1["wait_ms"] - t0["wait_ms"]
-    return {"acquisitions": acq,
+    return {"store_shards": l1.get("store_shards"),
+            "acquisitions": acq,
             "contended": contended,
             "contended_pct": round(100.0 * contended / acq, 2) if acq else 0.0,
             "hold_ms": round(t1["hold_ms"] - t0["hold_ms"], 3),
@@ -245,21 +246,7 @@ def _kl_lock(info):
 
     st = requests.get(info["server"] + "/_kl/stats", timeout=10, verify=info["apiserver_verify"]).json()
     return {"total": st["store_lock"], "by_type": st.get("by_type_lock", {}), "requests": st["requests"],
-            "by_kind": st.get("requests_by_kind", {}), "procs": st.get("procs")}
-
-
-def _procs_report(l0, l1, elapsed):
-    """kube-lite's processor slots (its GOMAXPROCS model) over the window: how many handler
-    runs had to wait for a slot, and the wait per second of the window."""
-    p0, p1 = l0.get("procs"), l1.get("procs")
-    if not p0 or not p1:
-        return None
-    acq = p1["acquisitions"] - p0["acquisitions"]
-    waited = p1["waited"] - p0["waited"]
-    wait_ms = p1["wait_ms"] - p0["wait_ms"]
-    return {"slots": p1["slots"], "acquisitions": acq,
-            "waited_pct": round(100.0 * waited / acq, 2) if acq else 0.0,
-            "wait_s_per_s": round(wait_ms / 1e3 / elapsed, 3) if elapsed > 0 else None}
+            "by_kind": st.get("requests_by_kind", {}), "store_shards": st.get("store_shards")}
 
 
 PRODUCT = ("controller", "admission", "synchronizer", "node-agent")
@@ -401,7 +388,6 @@ def _phase(d, nat, info, args, phase, concurrency, warmup, steps, cluster):
         # test API server and load_driver the tenant simulator: neither ships.
         "cpu_ms_per_cr": cpu_ms,
         "apiserver_store_lock": _lock_report(lock0, lock1, elapsed),
-        "apiserver_procs": _procs_report(lock0, lock1, elapsed),
         "apiserver_requests_per_cr": round((lock1["requests"] - lock0["requests"]) / per_cr, 2),
         "apiserver_requests_per_cr_by_kind": {
             k: round((v - lock0["by_kind"].get(k, 0)) / per_cr, 3)

@@ -6,8 +6,8 @@
 #include <chrono>
 #include <condition_variable>
 #include <deque>
-#include <fstream>
 #include <functional>
+#include <iterator>
 #include <mutex>
 #include <optional>
 #include <regex>
@@ -17,10 +17,7 @@
 #include <unordered_map>
 #include <unordered_set>
 
-#include <errno.h>
 #include <openssl/crypto.h>
-#include <sched.h>
-#include <semaphore.h>
 
 #include "apiserver/fieldset.h"
 #include "core/crypto.h"
@@ -403,86 +400,6 @@ class RwLock {
   bool mutex_only_ = false;
 };
 
-// Processor slots: the GOMAXPROCS model of Options::procs.  A handler thread holds a slot
-// while it computes (thread-local t_holds_proc) and yields it around blocking waits, so at
-// most `procs` handlers are runnable at once and the rest sleep instead of time-slicing
-// the CPUs (a thread per connection with every one runnable is not how the apiserver
-// schedules, and it starves the threads that complete I/O: webhook responses, watch
-// writers).  A POSIX semaphore: its uncontended path is one atomic op, no mutex.
-class Procs {
- public:
-  void init(int n) {
-    n_ = n;
-    if (n_ > 0) sem_init(&sem_, 0, static_cast<unsigned>(n_));
-  }
-  ~Procs() {
-    if (n_ > 0) sem_destroy(&sem_);
-  }
-  int slots() const { return n_; }
-  void acquire() {
-    if (sem_trywait(&sem_) != 0) {
-      const int64_t t0 = metrics::now_ns();
-      while (sem_wait(&sem_) != 0 && errno == EINTR) {
-      }
-      waited.fetch_add(1, std::memory_order_relaxed);
-      wait_ns.fetch_add(static_cast<uint64_t>(metrics::now_ns() - t0), std::memory_order_relaxed);
-    }
-    acquisitions.fetch_add(1, std::memory_order_relaxed);
-  }
-  void release() { sem_post(&sem_); }
-  std::atomic<uint64_t> acquisitions{0}, waited{0}, wait_ns{0};
-
- private:
-  int n_ = 0;
-  sem_t sem_;
-};
-
-// The CPUs this process may run on, capped by a cgroup v2 CPU quota (cpu.max).
-int default_procs() {
-  cpu_set_t set;
-  int n = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : 0;
-  if (n <= 0) n = static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
-  std::ifstream f("/sys/fs/cgroup/cpu.max");
-  std::string quota;
-  long long period = 0;
-  if (f >> quota >> period && quota != "max" && period > 0) {
-    const long long q = std::atoll(quota.c_str());
-    if (q > 0) n = std::min<int>(n, static_cast<int>(std::max(1LL, (q + period - 1) / period)));
-  }
-  return n;
-}
-
-thread_local Procs* t_procs = nullptr;  // the slots of the server whose handler runs here
-thread_local bool t_holds_proc = false;
-
-// Gives this thread's slot up (if it holds one); true if it did.
-inline bool yield_proc() {
-  if (!t_holds_proc) return false;
-  t_holds_proc = false;
-  t_procs->release();
-  return true;
-}
-inline void resume_proc(bool yielded) {
-  if (!yielded) return;
-  t_procs->acquire();
-  t_holds_proc = true;
-}
-struct ProcGuard {  // a request handler's slot, for the whole handler
-  explicit ProcGuard(Procs& p) {
-    if (p.slots() > 0) {
-      p.acquire();
-      t_procs = &p;
-      t_holds_proc = true;
-    }
-  }
-  ~ProcGuard() { yield_proc(); }
-};
-struct ProcYield {  // gives the slot up for a blocking wait
-  ProcYield() : y(yield_proc()) {}
-  ~ProcYield() { resume_proc(y); }
-  bool y;
-};
-
 // Watch wake-ups are deferred until the exclusive store lock is released (a futex wake per
 // subscriber inside the critical section would stretch every commit).
 thread_local std::vector<std::shared_ptr<WatchSub>> t_pending_wakeups;
@@ -508,9 +425,6 @@ class StoreLock {  // exclusive
   StoreLock(RwLock& m, LockStats& st, LockStats* also = nullptr) : m_(m), st_(st), also_(also) {
     if (!m_.try_lock()) {
       int64_t t0 = metrics::now_ns();
-      // the processor slot is given up for the wait and taken back after the unlock (not
-      // before the critical section: a lock holder must never wait for a slot)
-      yielded_ = yield_proc();
       m_.lock();
       const auto waited = static_cast<uint64_t>(metrics::now_ns() - t0);
       st_.contended.fetch_add(1, std::memory_order_relaxed);
@@ -532,7 +446,6 @@ class StoreLock {  // exclusive
     }
     m_.unlock();
     flush_watch_wakeups();
-    resume_proc(yielded_);
   }
   StoreLock(const StoreLock&) = delete;
   StoreLock& operator=(const StoreLock&) = delete;
@@ -542,7 +455,6 @@ class StoreLock {  // exclusive
   LockStats& st_;
   LockStats* also_;
   int64_t t_acq_ = 0;
-  bool yielded_ = false;
 };
 
 class SharedStoreLock {
@@ -550,31 +462,27 @@ class SharedStoreLock {
   SharedStoreLock(RwLock& m, LockStats& st) : m_(m) {
     if (!m_.try_lock_shared()) {
       int64_t t0 = metrics::now_ns();
-      yielded_ = yield_proc();
       m_.lock_shared();
       st.contended.fetch_add(1, std::memory_order_relaxed);
       st.wait_ns.fetch_add(static_cast<uint64_t>(metrics::now_ns() - t0), std::memory_order_relaxed);
     }
     st.shared.fetch_add(1, std::memory_order_relaxed);
   }
-  ~SharedStoreLock() {
-    m_.unlock_shared();
-    resume_proc(yielded_);
-  }
+  ~SharedStoreLock() { m_.unlock_shared(); }
   SharedStoreLock(const SharedStoreLock&) = delete;
   SharedStoreLock& operator=(const SharedStoreLock&) = delete;
 
  private:
   RwLock& m_;
-  bool yielded_ = false;
 };
 
 // Per-resource-type storage (like the apiserver's per-resource storage and watch cache):
 // its objects, event history and watchers, so commits to different types never serialize
 // on each other.  Within a type:
-//  * objects live in kShards key-hashed shards, each with its own lock: reads and commits
-//    of different objects proceed in parallel (the whole write path — webhook, merge,
-//    validation, the stored-version check — runs under one object's shard at most);
+//  * objects live in Options::store_shards key-hashed shards, each with its own lock:
+//    reads and commits of different objects proceed in parallel (a commit's stored-version
+//    check and its map update run under its object's shard only; the webhook, merge and
+//    validation before it under no lock).  One shard is a single lock per type;
 //  * `seq` orders the type's events: a commit, holding its object's shard exclusively,
 //    takes seq only to assign the resourceVersion and append the event to the history
 //    and to the watchers' queues.  Lock order: shard -> seq -> watches_mu -> WatchSub::m.
@@ -582,13 +490,30 @@ class SharedStoreLock {
 //    so no commit of the type is in flight while it reads; a watch resuming from a
 //    resourceVersion holds seq while it replays the history and registers.
 struct TypeStore {
-  static constexpr size_t kShards = 16;
   struct Shard {
     RwLock mu;
     std::unordered_map<std::string, Stored> objs;  // obj key -> stored (guarded by mu)
   };
-  std::array<Shard, kShards> shards;
-  Shard& shard(const std::string& key) { return shards[std::hash<std::string>{}(key) % kShards]; }
+  // A fixed array of n shards (RwLock is neither movable nor copyable), iterable.
+  class Shards {
+   public:
+    explicit Shards(size_t n) : n_(std::max<size_t>(1, n)), p_(new Shard[n_]) {}
+    Shard* begin() { return p_.get(); }
+    Shard* end() { return p_.get() + n_; }
+    std::reverse_iterator<Shard*> rbegin() { return std::reverse_iterator<Shard*>(end()); }
+    std::reverse_iterator<Shard*> rend() { return std::reverse_iterator<Shard*>(begin()); }
+    size_t size() const { return n_; }
+    Shard& operator[](size_t i) { return p_[i]; }
+
+   private:
+    size_t n_;
+    std::unique_ptr<Shard[]> p_;
+  };
+  explicit TypeStore(size_t n_shards) : shards(n_shards) {}
+  Shards shards;
+  Shard& shard(const std::string& key) {
+    return shards.size() == 1 ? shards[0] : shards[std::hash<std::string>{}(key) % shards.size()];
+  }
   RwLock seq;
   std::atomic<uint64_t> version{0};                          // bumped by every commit/erase (under seq)
   LockStats stats;                                           // the shard locks
@@ -607,14 +532,12 @@ class AllShards {
       if (exclusive_) {
         if (!sh.mu.try_lock()) {
           const int64_t t0 = metrics::now_ns();
-          if (!yielded_) yielded_ = yield_proc();
           sh.mu.lock();
           ts_.stats.contended.fetch_add(1, std::memory_order_relaxed);
           ts_.stats.wait_ns.fetch_add(static_cast<uint64_t>(metrics::now_ns() - t0), std::memory_order_relaxed);
         }
       } else if (!sh.mu.try_lock_shared()) {
         const int64_t t0 = metrics::now_ns();
-        if (!yielded_) yielded_ = yield_proc();
         sh.mu.lock_shared();
         ts_.stats.contended.fetch_add(1, std::memory_order_relaxed);
         ts_.stats.wait_ns.fetch_add(static_cast<uint64_t>(metrics::now_ns() - t0), std::memory_order_relaxed);
@@ -628,7 +551,6 @@ class AllShards {
       else it->mu.unlock_shared();
     }
     flush_watch_wakeups();
-    resume_proc(yielded_);
   }
   AllShards(const AllShards&) = delete;
   AllShards& operator=(const AllShards&) = delete;
@@ -636,7 +558,6 @@ class AllShards {
  private:
   TypeStore& ts_;
   bool exclusive_;
-  bool yielded_ = false;
 };
 
 struct FaultRule {
@@ -780,18 +701,15 @@ struct ApiServer::Impl {
   std::atomic<uint64_t> requests{0};
   std::atomic<uint64_t> faults_hit{0};
   LockStats types_stats;  // types_mu accounting
-  Procs procs;            // Options::procs
 
   explicit Impl(Options o) : opts(std::move(o)) {
-    int np = opts.procs;
-    if (const char* e = std::getenv("BGC_KL_PROCS"); e && *e) np = std::atoi(e);
-    procs.init(np < 0 ? default_procs() : np);
+    if (const char* e = std::getenv("BGC_KL_STORE_SHARDS"); e && *e) opts.store_shards = std::max(1, std::atoi(e));
     webhook_h2 = opts.webhook_http2;
     write_latency_us = opts.write_latency_us;
     for (const ResourceType* rt : kube::types::builtin()) {
       TypeInfo ti;
       ti.rt = *rt;
-      ti.store = std::make_shared<TypeStore>();
+      ti.store = std::make_shared<TypeStore>(opts.store_shards);
       types[ti.key()] = ti;
     }
     if (!opts.token_file.empty()) load_tokens(opts.token_file);
@@ -1184,7 +1102,6 @@ struct ApiServer::Impl {
               ",\"apiVersion\":\"meta.k8s.io/v1\"}}}";
       std::string err;
       Value resp_review;
-      ProcYield waiting_on_the_webhook;
       int64_t t0 = metrics::now_ns();
       try {
         std::string path;
@@ -1205,7 +1122,6 @@ struct ApiServer::Impl {
       double secs = static_cast<double>(metrics::now_ns() - t0) * 1e-9;
       hist.observe(secs);
       ring.add(secs, &calls);
-      resume_proc(std::exchange(waiting_on_the_webhook.y, false));
       const Value& resp = resp_review.get("response");
       if (err.empty() && !resp.is_object()) err = "webhook response was absent";
       if (err.empty() && resp.get_string("uid") != uid) {
@@ -1315,7 +1231,7 @@ struct ApiServer::Impl {
         continue;
       }
       ti.schema = schema;
-      ti.store = std::make_shared<TypeStore>();
+      ti.store = std::make_shared<TypeStore>(opts.store_shards);
       types[ti.key()] = ti;
     }
   }
@@ -2478,11 +2394,7 @@ struct ApiServer::Impl {
                                       {"list_pages", static_cast<unsigned long long>(list_pages.load())},
                                       {"resource_version", rv_str(rv.load())},
                                       {"gc_collected", static_cast<unsigned long long>(gc_collected.load())},
-                                      {"procs", Value::object({
-                                          {"slots", procs.slots()},
-                                          {"acquisitions", static_cast<unsigned long long>(procs.acquisitions.load())},
-                                          {"waited", static_cast<unsigned long long>(procs.waited.load())},
-                                          {"wait_ms", static_cast<double>(procs.wait_ns.load()) * 1e-6}})},
+                                      {"store_shards", static_cast<unsigned long long>(opts.store_shards)},
                                       {"gc_pending", static_cast<unsigned long long>([&] {
                                          std::lock_guard<std::mutex> g(gc_mu);
                                          return gc_queue.size();
@@ -2525,7 +2437,6 @@ struct ApiServer::Impl {
         im->req_counts[k]++;
       }
     } count{this, req, w, res_key};
-    ProcGuard proc(procs);
     try {
       if (inject_fault(req, w)) return;
       UserInfo user = authenticate(req);
@@ -2564,16 +2475,12 @@ struct ApiServer::Impl {
       // etcd model: a write is visible (response, watch event) only after a storage
       // commit round trip.  Writes wait concurrently, as they pipeline through raft.
       if (const int64_t lat = write_latency_us.load(std::memory_order_relaxed); lat > 0 && m != "GET") {
-        ProcYield commit_wait;
         std::this_thread::sleep_for(std::chrono::microseconds(lat));
       }
       if (p.collection) {
         if (m == "GET") {
           std::string wq = req.query_param("watch");
-          if (wq == "1" || wq == "true") {
-            yield_proc();  // a watch stream is I/O-bound for its lifetime
-            do_watch(p, req, w);
-          }
+          if (wq == "1" || wq == "true") do_watch(p, req, w);
           else do_list(p, req, w);
         } else if (m == "POST") {
           do_create(p, req, user, w);

@@ -65,14 +65,11 @@ struct Options {
   // HTTP/1.1 pool measured equal or better at N=1..8 (profiles/http2_r2/after_store_lock/).
   bool webhook_http2 = false;
   size_t webhook_h2_connections = 4;
-  // Request handlers running at once (the Go runtime's GOMAXPROCS: the real apiserver runs
-  // at most that many goroutines at a time, and one blocked in network I/O, a sleep or a
-  // contended mutex gives its processor up).  A handler holds a slot while it computes and
-  // gives it up while it waits on a webhook, the storage commit latency or a contended
-  // store lock; watch streams hold none.  -1: the CPUs this process may use (affinity,
-  // capped by the cgroup CPU quota, as GOMAXPROCS since Go 1.25); 0: unlimited (a thread
-  // per connection, all runnable).  BGC_KL_PROCS overrides.
-  int procs = 0;
+  // Key-hashed shards of each type's object store, each with its own lock (commits of
+  // different objects run in parallel; a commit-order lock per type assigns resourceVersions
+  // and queues events).  1 = one lock per type, the round-3 store.  BGC_KL_STORE_SHARDS
+  // overrides.
+  size_t store_shards = 16;
 };
 
 class ApiServer {

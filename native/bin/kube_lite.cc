@@ -26,7 +26,7 @@ static void usage() {
                "                 [--tls-cert F --tls-key F] [--service-override ns/name=host:port]...\n"
                "                 [--bookmark-ms N] [--history N] [--watch-coalesce-us N] [--gc-workers N]\n"
                "                 [--opaque-rv] [--continue-ttl-ms N] [--webhook-http1|--webhook-http2] [--webhook-h2-connections N]\n"
-               "                 [--write-latency-ms F] [--procs N]\n"
+               "                 [--write-latency-ms F] [--store-shards N]\n"
                "                 [--manifest file.{json,yaml}]...\n");
 }
 
@@ -61,7 +61,7 @@ int main(int argc, char** argv) {
     else if (a == "--webhook-http1") o.webhook_http2 = false;
     else if (a == "--webhook-http2") o.webhook_http2 = true;
     else if (a == "--webhook-h2-connections") o.webhook_h2_connections = static_cast<size_t>(std::atoi(next().c_str()));
-    else if (a == "--procs") o.procs = std::atoi(next().c_str());
+    else if (a == "--store-shards") o.store_shards = static_cast<size_t>(std::max(1, std::atoi(next().c_str())));
     else if (a == "--continue-ttl-ms") o.continue_ttl_ms = std::atoi(next().c_str());
     else if (a == "--manifest") manifests.push_back(next());
     else if (a == "--service-override") {
