@@ -16,6 +16,7 @@ Weak scaling: per-rank work (B CRs/step) is fixed; the whole-job value is
 total Ready CRs / wall time of the K timed steps (max over ranks).
 """
 import argparse
+import glob
 import json
 import os
 import resource
@@ -124,6 +125,74 @@ def effective_cpus():
     except (OSError, ValueError):
         pass
     return max(1, n)
+
+
+def _cpulist(text):
+    cpus = set()
+    for part in text.strip().split(","):
+        if part:
+            a, _, b = part.partition("-")
+            cpus.update(range(int(a), int(b or a) + 1))
+    return cpus
+
+
+def _cpulist_text(cpus):
+    out, run = [], []
+    for c in sorted(cpus):
+        if run and c == run[-1] + 1:
+            run.append(c)
+        else:
+            if run:
+                out.append(f"{run[0]}-{run[-1]}" if len(run) > 1 else str(run[0]))
+            run = [c]
+    if run:
+        out.append(f"{run[0]}-{run[-1]}" if len(run) > 1 else str(run[0]))
+    return ",".join(out)
+
+
+def quota_cpuset():
+    """The CPUs to run the control plane on when the cgroup's CPU quota is smaller than the
+    affinity mask (the MI355X boxes: a 16-CPU quota per GPU over 256 visible CPUs), or None.
+
+    Unpinned, the job's threads spread over every visible CPU, spend the quota in a fraction
+    of each 100 ms CFS period and are then frozen for the rest of it: tail latencies of the
+    whole stack jump to 40-50 ms whenever the load outruns the quota (measured on the box:
+    33 of 97 periods throttled in a headline run, profiles/kl_shard_r4/).  Pinned to as many
+    CPUs as the quota grants, the same CPU time is shared instead (what a Kubernetes pod gets
+    from the static CPU manager, or a Go service from a quota-sized GOMAXPROCS).  Prefers the
+    CPUs local to the first GPU's NUMA node, leaving CPU 0 (interrupts) out when it can."""
+    if not hasattr(os, "sched_getaffinity"):
+        return None
+    aff = sorted(os.sched_getaffinity(0))
+    n = effective_cpus()
+    if n >= len(aff):
+        return None
+    local = set()
+    for dev in sorted(glob.glob("/sys/class/drm/renderD*/device")):
+        try:
+            with open(os.path.join(dev, "vendor")) as f:
+                if f.read().strip() != "0x1002":
+                    continue
+            with open(os.path.join(dev, "local_cpulist")) as f:
+                local = _cpulist(f.read()) & set(aff)
+            break
+        except (OSError, ValueError):
+            continue
+    pool = [c for c in aff if c in local and c != 0] or [c for c in aff if c != 0] or aff
+    if len(pool) < n:
+        pool += [c for c in aff if c not in pool]
+    return sorted(pool[:n])
+
+
+def cgroup_throttling():
+    """cgroup v2 cpu.stat: CFS bandwidth periods and throttled time so far (None if absent)."""
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            st = dict(line.split() for line in f if line.strip())
+        return {"periods": int(st["nr_periods"]), "throttled": int(st["nr_throttled"]),
+                "throttled_ms": int(st["throttled_usec"]) / 1e3}
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def auto_concurrency(world, cpus):
@@ -281,7 +350,7 @@ def _phase(d, nat, info, args, phase, concurrency, warmup, steps, cluster):
     lat, clat, ap_lat, ap_ready = [], [], [], []
     stage = {"ns": [], "rq": [], "rb": []}
     ready = failed = timeouts = 0
-    lock0 = cpu0 = None
+    lock0 = cpu0 = thr0 = thr1 = None
     starts = {}
     t_start = None
     errors = []
@@ -299,6 +368,7 @@ def _phase(d, nat, info, args, phase, concurrency, warmup, steps, cluster):
                     starts = {key: _clear(url, verify) for key, (url, verify) in _sample_logs(info).items()}
                     lock0 = _kl_lock(info)
                     cpu0 = _cpu_snapshot(cluster)
+                    thr0 = cgroup_throttling()
                 d.barrier()
                 t_start = time.perf_counter()
                 ru0 = resource.getrusage(resource.RUSAGE_SELF)
@@ -324,6 +394,7 @@ def _phase(d, nat, info, args, phase, concurrency, warmup, steps, cluster):
         elapsed = time.perf_counter() - t_start
         ru1 = resource.getrusage(resource.RUSAGE_SELF)
         cpu1 = _cpu_snapshot(cluster) if d.rank == 0 else None
+        thr1 = cgroup_throttling() if d.rank == 0 else None
         driver_cpu = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
         elapsed = d.max_scalar(elapsed)
         driver.remove(prev)
@@ -395,6 +466,12 @@ def _phase(d, nat, info, args, phase, concurrency, warmup, steps, cluster):
         "ready_crs": total_ready,
         "failed_crs": total_failed,
     }
+    if thr0 and thr1:
+        # CFS bandwidth control over the window: periods in which the job's cgroup ran out
+        # of its CPU quota and was frozen until the next period (see quota_cpuset)
+        periods = thr1["periods"] - thr0["periods"]
+        out["cgroup_throttled"] = {"periods": periods, "throttled_periods": thr1["throttled"] - thr0["throttled"],
+                                   "throttled_ms": round(thr1["throttled_ms"] - thr0["throttled_ms"], 1)}
     if info.get("approve_url"):
         out["approve_to_ready_p50_ms"] = ms(_pct(flat("ap_ready"), 0.50))
         out["approve_to_ready_p99_ms"] = ms(_pct(flat("ap_ready"), 0.99))
@@ -430,9 +507,24 @@ class _Phase:
         self.write_latency_ms, self.warmup, self.steps = write_latency_ms, warmup, steps
 
 
+def pin_to_quota():
+    """Pins every thread of this process (and so the control plane it starts) to
+    quota_cpuset(); the CPU list, or None when no pinning is needed."""
+    cs = quota_cpuset()
+    if cs:
+        for tid in os.listdir("/proc/self/task"):
+            try:
+                os.sched_setaffinity(int(tid), cs)
+            except OSError:
+                pass
+    return cs
+
+
 def run(args):
     d = Dist()
     n = args.gpus if args.gpus else d.world
+    # every rank pins itself to the same CPUs: the quota covers the whole job
+    cpuset = pin_to_quota() if args.pin_to_quota else None
     from bacchus_gpu_controller_amd import native
     from bacchus_gpu_controller_amd.testing.cluster import Cluster
     from bacchus_gpu_controller_amd.testing.fake_google import FakeGoogle
@@ -584,7 +676,9 @@ def run(args):
                        "driver_protocol": "h2" if args.driver_http2 and args.tls_apiserver else "http/1.1",
                        # each rank's load driver watches only its own tenants' children
                        # (kube-lite name-prefix field selector); the product is unaffected
-                       "driver_server_filter": args.driver_server_filter},
+                       "driver_server_filter": args.driver_server_filter,
+                       # CPUs the job was pinned to (quota_cpuset), or null when not pinned
+                       "cpuset": _cpulist_text(cpuset) if cpuset else None},
         }
         out.update(main_r)
         if "t" in results:
@@ -690,6 +784,9 @@ def main(argv=None):
                          "(periodic sheet sync only, sequential unconditional child applies); "
                          "reference-controller: only the controller side")
     ap.add_argument("--reference-semantics", action="store_true", help="alias for --semantics reference")
+    ap.add_argument("--pin-to-quota", action=argparse.BooleanOptionalAction, default=True,
+                    help="when the cgroup CPU quota grants fewer CPUs than are visible, run the job on that "
+                         "many CPUs (quota_cpuset) instead of bursting over all of them and being throttled")
     ap.add_argument("--reference-arms", action=argparse.BooleanOptionalAction, default=True,
                     help="also time the reference's controller behaviour on this stack (reference_controller) "
                          "and both controllers at --arm-write-latency-ms (secondary fields)")

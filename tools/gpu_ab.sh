@@ -76,6 +76,9 @@ for name in names:
         arm[f"cpu_ms_per_cr.{k}"] = [(d.get("cpu_ms_per_cr") or {}).get(k) for d in rows]
     for k in ("contended_pct", "wait_s_per_s"):
         arm[f"store_lock.{k}"] = [(d.get("apiserver_store_lock") or {}).get(k) for d in rows]
+    arm["admission_p99_ms"] = [d.get("admission_p99_ms") for d in rows]
+    arm["apply_to_ready_p50_ms"] = [d.get("apply_to_ready_p50_ms") for d in rows]
+    arm["cgroup_throttled_periods"] = [(d.get("cgroup_throttled") or {}).get("throttled_periods", 0) for d in rows]
     summary[name] = {k: {"median": statistics.median(v) if all(x is not None for x in v) else None, "all": v}
                      for k, v in arm.items()}
 json.dump(summary, open(f"{out}/summary.json", "w"), indent=1)
