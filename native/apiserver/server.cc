@@ -704,6 +704,7 @@ struct ApiServer::Impl {
 
   explicit Impl(Options o) : opts(std::move(o)) {
     if (const char* e = std::getenv("BGC_KL_STORE_SHARDS"); e && *e) opts.store_shards = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("BGC_KL_H2_CALLER_READS"); e && *e) opts.webhook_h2_caller_reads = std::string(e) != "0";
     webhook_h2 = opts.webhook_http2;
     write_latency_us = opts.write_latency_us;
     for (const ResourceType* rt : kube::types::builtin()) {
@@ -1047,6 +1048,7 @@ struct ApiServer::Impl {
     o.tls_server_name = server_name;
     o.http2 = webhook_h2.load();
     o.h2_connections = opts.webhook_h2_connections;
+    o.h2_caller_reads = opts.webhook_h2_caller_reads;
     if (base.rfind("https", 0) == 0) {
       o.tls = net::TlsContext::client(ca.empty() ? "" : crypto::base64_decode(ca), false);
     }

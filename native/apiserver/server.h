@@ -65,6 +65,11 @@ struct Options {
   // HTTP/1.1 pool measured equal or better at N=1..8 (profiles/http2_r2/after_store_lock/).
   bool webhook_http2 = false;
   size_t webhook_h2_connections = 4;
+  // HTTP/2 webhook callouts: the calling handler threads read their responses themselves
+  // (http::ClientOptions::h2_caller_reads) instead of a reader thread per connection that
+  // then wakes them: one wake-up per callout instead of two.  BGC_KL_H2_CALLER_READS=0
+  // turns it off.
+  bool webhook_h2_caller_reads = true;
   // Key-hashed shards of each type's object store, each with its own lock (commits of
   // different objects run in parallel; a commit-order lock per type assigns resourceVersions
   // and queues events).  1 = one lock per type, the round-3 store.  BGC_KL_STORE_SHARDS

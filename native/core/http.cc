@@ -946,7 +946,7 @@ std::shared_ptr<http2::Connection> Client::h2_connection() {
   std::lock_guard<std::mutex> lk(h2_mu_);  // concurrent first requests share one handshake
   h2_.resize(std::max<size_t>(1, opts_.h2_connections));
   auto& slot = h2_[h2_next_++ % h2_.size()];
-  if (slot && slot->usable()) return slot;
+  if (slot && slot->usable() && (!opts_.h2_caller_reads || slot->poll_idle()) && slot->usable()) return slot;
   if (h2_refused_) return nullptr;
   int fd = net::connect_tcp(url_.host, url_.port, opts_.connect_timeout_ms);
   std::string host = opts_.tls_server_name.empty() ? url_.host : opts_.tls_server_name;
@@ -958,6 +958,7 @@ std::shared_ptr<http2::Connection> Client::h2_connection() {
     return nullptr;
   }
   slot = std::make_shared<http2::Connection>(std::move(ts), http2::Connection::Role::kClient);
+  if (opts_.h2_caller_reads) slot->set_caller_reads();
   slot->start();
   return slot;
 }

@@ -223,6 +223,9 @@ struct ClientOptions {
   // HTTP/2 connections request() streams are spread over (round robin); 1 = one
   // multiplexed connection, as Go's client (and so the apiserver) uses.
   size_t h2_connections = 1;
+  // HTTP/2: no reader thread per connection; the callers waiting for responses read the
+  // frames themselves (http2::Connection::set_caller_reads).
+  bool h2_caller_reads = false;
 };
 
 class HttpError : public std::runtime_error {

@@ -89,6 +89,7 @@ void Connection::start() {
   // The reader owns a reference for its whole run, so the Connection is never destroyed
   // under it; if that reference is the last one, the destructor runs at thread exit and
   // join() detaches instead of joining itself.
+  if (caller_reads_) return;  // the callers waiting for responses read the frames
   reader_ = std::thread([self = shared_from_this()] {
     self->reader_loop();
     // OpenSSL's per-thread state (the error queue an SSL_read failure at close fills, the
@@ -268,7 +269,9 @@ bool Connection::send_data(Stream& s, std::string_view data, bool end_stream) {
     {
       std::unique_lock<std::mutex> lk(mu_);
       if (!data.empty()) {
-        window_cv_.wait(lk, [&] { return closed_ || s.reset || (conn_send_window_ > 0 && s.send_window > 0); });
+        auto can_send = [&] { return closed_ || s.reset || (conn_send_window_ > 0 && s.send_window > 0); };
+        if (caller_reads_) wait_reading(lk, window_cv_, std::chrono::steady_clock::time_point::max(), can_send);
+        else window_cv_.wait(lk, can_send);
       }
       if (closed_ || s.reset || s.local_closed) return false;
       n = std::min<size_t>({data.size(), static_cast<size_t>(std::max<int64_t>(0, conn_send_window_)),
@@ -305,28 +308,6 @@ void Connection::reset_stream(Stream& s, uint32_t code) {
   cv_.notify_all();
 }
 
-bool Connection::read_exact(char* buf, size_t n) {
-  while (n > 0) {
-    if (rpos_ < rbuf_.size()) {
-      size_t k = std::min(n, rbuf_.size() - rpos_);
-      std::memcpy(buf, rbuf_.data() + rpos_, k);
-      rpos_ += k;
-      buf += k;
-      n -= k;
-      continue;
-    }
-    rbuf_.resize(64 * 1024);
-    rpos_ = 0;
-    ssize_t r = io_->read_some(rbuf_.data(), rbuf_.size(), -1);
-    if (r <= 0) {
-      rbuf_.clear();
-      return false;
-    }
-    rbuf_.resize(static_cast<size_t>(r));
-  }
-  return true;
-}
-
 void Connection::goaway(uint32_t code, const std::string& why) {
   LOG_WARN("http2") << "connection error: " << why;
   close(code);
@@ -348,117 +329,195 @@ void Connection::fail_all() {
   cv_.notify_all();
 }
 
+// Ensures rbuf_ holds at least n unread bytes (from rpos_).  1: yes; 0: EOF or error;
+// -2: timeout (what was read so far stays buffered for the next reader).
+int Connection::fill(size_t n, int timeout_ms) {
+  while (rbuf_.size() - rpos_ < n) {
+    if (rpos_ == rbuf_.size()) {
+      rbuf_.clear();
+      rpos_ = 0;
+    } else if (rpos_ >= 32 * 1024) {
+      rbuf_.erase(0, rpos_);
+      rpos_ = 0;
+    }
+    const size_t old = rbuf_.size();
+    rbuf_.resize(old + 64 * 1024);
+    const ssize_t r = io_->read_some(&rbuf_[old], 64 * 1024, timeout_ms);
+    if (r <= 0) {
+      rbuf_.resize(old);
+      return r == -2 ? -2 : 0;
+    }
+    rbuf_.resize(old + static_cast<size_t>(r));
+  }
+  return 1;
+}
+
+Connection::ReadResult Connection::read_frame(int timeout_ms) {
+  const int h = fill(9, timeout_ms);
+  if (h != 1) return h == -2 ? ReadResult::kTimeout : ReadResult::kClosed;
+  const char* hdr = rbuf_.data() + rpos_;
+  const uint32_t len = (uint32_t(static_cast<uint8_t>(hdr[0])) << 16) |
+                       (uint32_t(static_cast<uint8_t>(hdr[1])) << 8) | uint32_t(static_cast<uint8_t>(hdr[2]));
+  if (len > 16384) {  // we never raise SETTINGS_MAX_FRAME_SIZE
+    goaway(kFrameSizeError, "frame larger than 16384");
+    return ReadResult::kClosed;
+  }
+  const int b = fill(9 + len, timeout_ms);
+  if (b != 1) return b == -2 ? ReadResult::kTimeout : ReadResult::kClosed;
+  hdr = rbuf_.data() + rpos_;
+  const uint8_t type = static_cast<uint8_t>(hdr[3]);
+  const uint8_t flags = static_cast<uint8_t>(hdr[4]);
+  const uint32_t sid = be32(hdr + 5) & 0x7fffffff;
+  std::string payload(hdr + 9, len);
+  rpos_ += 9 + len;
+  frames_in_.fetch_add(1, std::memory_order_relaxed);
+  handle_frame(type, flags, sid, payload, len);
+  return closed_ ? ReadResult::kClosed : ReadResult::kFrame;
+}
+
+void Connection::handle_frame(uint8_t type, uint8_t flags, uint32_t sid, const std::string& payload, uint32_t len) {
+  if (hdr_sid_ && type != kContinuation) {
+    goaway(kProtocolError, "header block interrupted");
+    return;
+  }
+  std::string_view p(payload);
+  switch (type) {
+    case kData: {
+      if (sid == 0 || !strip_padding(flags, false, p)) {
+        goaway(kProtocolError, "bad DATA frame");
+        break;
+      }
+      on_data(sid, flags, p, len);
+      break;
+    }
+    case kHeaders: {
+      if (sid == 0 || !strip_padding(flags, true, p)) {
+        goaway(kProtocolError, "bad HEADERS frame");
+        break;
+      }
+      hdr_block_.assign(p.data(), p.size());
+      hdr_flags_ = flags;
+      if (flags & kEndHeaders) {
+        on_headers(sid, flags, hdr_block_);
+      } else {
+        hdr_sid_ = sid;
+      }
+      break;
+    }
+    case kContinuation: {
+      if (!hdr_sid_ || sid != hdr_sid_) {
+        goaway(kProtocolError, "unexpected CONTINUATION");
+        break;
+      }
+      hdr_block_.append(p.data(), p.size());
+      if (flags & kEndHeaders) {
+        uint32_t s = hdr_sid_;
+        hdr_sid_ = 0;
+        on_headers(s, hdr_flags_, hdr_block_);
+      }
+      break;
+    }
+    case kSettings:
+      if (sid != 0 || (!(flags & kAck) && len % 6 != 0)) {
+        goaway(kProtocolError, "bad SETTINGS frame");
+        break;
+      }
+      on_settings(flags, p);
+      break;
+    case kPing:
+      if (len != 8) {
+        goaway(kFrameSizeError, "bad PING frame");
+        break;
+      }
+      if (!(flags & kAck)) write_frame(kPing, kAck, 0, p);
+      break;
+    case kWindowUpdate:
+      if (len != 4) {
+        goaway(kFrameSizeError, "bad WINDOW_UPDATE frame");
+        break;
+      }
+      on_window_update(sid, p);
+      break;
+    case kRstStream:
+      if (len != 4) {
+        goaway(kFrameSizeError, "bad RST_STREAM frame");
+        break;
+      }
+      on_rst(sid, p);
+      break;
+    case kGoaway: {
+      if (len < 8) {
+        goaway(kFrameSizeError, "bad GOAWAY frame");
+        break;
+      }
+      on_goaway(be32(p.data()) & 0x7fffffff);
+      break;
+    }
+    case kPushPromise:
+      goaway(kProtocolError, "PUSH_PROMISE with push disabled");
+      break;
+    default:  // PRIORITY and unknown extension frames are ignored
+      break;
+  }
+}
+
 void Connection::reader_loop() {
   if (role_ == Role::kServer) {
-    char pre[sizeof(kPreface) - 1];
-    if (!read_exact(pre, sizeof(pre)) || std::memcmp(pre, kPreface, sizeof(pre)) != 0) {
+    if (fill(sizeof(kPreface) - 1, -1) != 1 ||
+        std::memcmp(rbuf_.data() + rpos_, kPreface, sizeof(kPreface) - 1) != 0) {
       fail_all();
       close(kProtocolError);
       return;
     }
+    rpos_ += sizeof(kPreface) - 1;
   }
-  char hdr[9];
-  std::string payload;
-  while (!closed_) {
-    if (!read_exact(hdr, 9)) break;
-    const uint32_t len = (uint32_t(static_cast<uint8_t>(hdr[0])) << 16) |
-                         (uint32_t(static_cast<uint8_t>(hdr[1])) << 8) | uint32_t(static_cast<uint8_t>(hdr[2]));
-    const uint8_t type = static_cast<uint8_t>(hdr[3]);
-    const uint8_t flags = static_cast<uint8_t>(hdr[4]);
-    const uint32_t sid = be32(hdr + 5) & 0x7fffffff;
-    if (len > 16384) {  // we never raise SETTINGS_MAX_FRAME_SIZE
-      goaway(kFrameSizeError, "frame larger than 16384");
-      break;
-    }
-    payload.resize(len);
-    if (len && !read_exact(payload.data(), len)) break;
-    frames_in_.fetch_add(1, std::memory_order_relaxed);
-    if (hdr_sid_ && type != kContinuation) {
-      goaway(kProtocolError, "header block interrupted");
-      break;
-    }
-    std::string_view p(payload);
-    switch (type) {
-      case kData: {
-        if (sid == 0 || !strip_padding(flags, false, p)) {
-          goaway(kProtocolError, "bad DATA frame");
-          break;
-        }
-        on_data(sid, flags, p, len);
-        break;
-      }
-      case kHeaders: {
-        if (sid == 0 || !strip_padding(flags, true, p)) {
-          goaway(kProtocolError, "bad HEADERS frame");
-          break;
-        }
-        hdr_block_.assign(p.data(), p.size());
-        hdr_flags_ = flags;
-        if (flags & kEndHeaders) {
-          on_headers(sid, flags, hdr_block_);
-        } else {
-          hdr_sid_ = sid;
-        }
-        break;
-      }
-      case kContinuation: {
-        if (!hdr_sid_ || sid != hdr_sid_) {
-          goaway(kProtocolError, "unexpected CONTINUATION");
-          break;
-        }
-        hdr_block_.append(p.data(), p.size());
-        if (flags & kEndHeaders) {
-          uint32_t s = hdr_sid_;
-          hdr_sid_ = 0;
-          on_headers(s, hdr_flags_, hdr_block_);
-        }
-        break;
-      }
-      case kSettings:
-        if (sid != 0 || (!(flags & kAck) && len % 6 != 0)) {
-          goaway(kProtocolError, "bad SETTINGS frame");
-          break;
-        }
-        on_settings(flags, p);
-        break;
-      case kPing:
-        if (len != 8) {
-          goaway(kFrameSizeError, "bad PING frame");
-          break;
-        }
-        if (!(flags & kAck)) write_frame(kPing, kAck, 0, p);
-        break;
-      case kWindowUpdate:
-        if (len != 4) {
-          goaway(kFrameSizeError, "bad WINDOW_UPDATE frame");
-          break;
-        }
-        on_window_update(sid, p);
-        break;
-      case kRstStream:
-        if (len != 4) {
-          goaway(kFrameSizeError, "bad RST_STREAM frame");
-          break;
-        }
-        on_rst(sid, p);
-        break;
-      case kGoaway: {
-        if (len < 8) {
-          goaway(kFrameSizeError, "bad GOAWAY frame");
-          break;
-        }
-        on_goaway(be32(p.data()) & 0x7fffffff);
-        break;
-      }
-      case kPushPromise:
-        goaway(kProtocolError, "PUSH_PROMISE with push disabled");
-        break;
-      default:  // PRIORITY and unknown extension frames are ignored
-        break;
-    }
+  while (!closed_ && read_frame(-1) == ReadResult::kFrame) {
   }
   fail_all();
   if (io_) io_->shutdown();
+}
+
+bool Connection::read_step_locked(std::unique_lock<std::mutex>& lk, std::chrono::steady_clock::time_point deadline) {
+  const auto now = std::chrono::steady_clock::now();
+  if (deadline <= now) return false;
+  const auto left = std::chrono::ceil<std::chrono::milliseconds>(deadline - now);
+  reading_ = true;
+  lk.unlock();
+  const ReadResult r = read_frame(static_cast<int>(std::min<int64_t>(left.count(), 1 << 30)));
+  if (r == ReadResult::kClosed) {
+    fail_all();
+    if (io_) io_->shutdown();
+  }
+  lk.lock();
+  reading_ = false;
+  return r == ReadResult::kFrame || (r == ReadResult::kTimeout && std::chrono::steady_clock::now() < deadline);
+}
+
+void Connection::hand_off_locked() {
+  // the reader role is free and callers still wait: wake one, it reads next
+  if (!reading_ && !waiting_cvs_.empty()) waiting_cvs_.front()->notify_one();
+}
+
+bool Connection::poll_idle() {
+  if (!caller_reads_) return !closed_;
+  std::unique_lock<std::mutex> lk(mu_);
+  if (reading_ || closed_) return !closed_;
+  // frames that arrived while nobody waited: SETTINGS, PING, WINDOW_UPDATE, a GOAWAY or
+  // the peer closing an idle connection
+  reading_ = true;
+  lk.unlock();
+  ReadResult r;
+  do {
+    r = read_frame(0);
+  } while (r == ReadResult::kFrame && !closed_);
+  if (r == ReadResult::kClosed) {
+    fail_all();
+    if (io_) io_->shutdown();
+  }
+  lk.lock();
+  reading_ = false;
+  hand_off_locked();
+  return !closed_;
 }
 
 void Connection::on_settings(uint8_t flags, std::string_view p) {

@@ -4,7 +4,8 @@
 // sockets (k8s.io/kubelet/pkg/apis/deviceplugin/v1beta1).  The image has no gRPC C++,
 // protoc or nghttp2 headers, so the node agent carries its own small h2c stack:
 //
-//   Connection  one socket, one reader thread; HPACK decoder state lives on that thread,
+//   Connection  one socket, one reader thread (or, for a client in caller-reads mode, the
+//               waiting callers take turns reading); HPACK decoder state lives with the reader,
 //               writes are serialised by a mutex (a frame, or a HEADERS+CONTINUATION
 //               run, is written atomically).  Send-side flow control is honoured per
 //               stream and per connection (senders block until WINDOW_UPDATE); the
@@ -128,8 +129,20 @@ class Connection : public std::enable_shared_from_this<Connection> {
   template <class Pred>
   bool wait_stream(Stream& s, std::chrono::steady_clock::time_point deadline, Pred pred) {
     std::unique_lock<std::mutex> lk(mu_);
+    if (caller_reads_) return wait_reading(lk, s.cv, deadline, pred);
     return s.cv.wait_until(lk, deadline, [&] { return pred() || closed_.load(); }) && pred();
   }
+
+  // Client, before start(): no reader thread.  A caller waiting for its stream reads the
+  // connection's frames itself while no other caller does (one at a time; frames for other
+  // streams wake their callers), and hands the reader role on when its own stream is done.
+  // A response then costs one wake-up on this side (the caller's) instead of two (the
+  // reader thread's, then the caller's), which is what matters on a saturated CPU set.
+  void set_caller_reads() { caller_reads_ = true; }
+  // Caller-reads client about to reuse an idle connection: processes the frames that
+  // arrived while nobody waited (SETTINGS, PING, a GOAWAY, the peer closing); false if the
+  // connection is closed.
+  bool poll_idle();
   // Runs fn with the connection mutex held (to read/modify Stream fields).
   template <class Fn>
   auto locked(Fn fn) {
@@ -142,7 +155,46 @@ class Connection : public std::enable_shared_from_this<Connection> {
 
  private:
   void reader_loop();
-  bool read_exact(char* buf, size_t n);
+  enum class ReadResult { kFrame, kTimeout, kClosed };
+  int fill(size_t n, int timeout_ms);
+  ReadResult read_frame(int timeout_ms);  // reads and handles one frame (one reader at a time)
+  void handle_frame(uint8_t type, uint8_t flags, uint32_t sid, const std::string& payload, uint32_t len);
+  // caller-reads mode (mu_ held through lk): read one frame as the reader, up to deadline;
+  // false when the connection closed or the deadline passed
+  bool read_step_locked(std::unique_lock<std::mutex>& lk, std::chrono::steady_clock::time_point deadline);
+  void hand_off_locked();
+  template <class Pred>
+  bool wait_reading(std::unique_lock<std::mutex>& lk, std::condition_variable& cv,
+                    std::chrono::steady_clock::time_point deadline, Pred pred) {
+    waiting_cvs_.push_back(&cv);
+    bool ok = false;
+    while (true) {
+      if (pred()) {
+        ok = true;
+        break;
+      }
+      if (closed_) break;
+      if (!reading_) {
+        if (!read_step_locked(lk, deadline)) {
+          ok = pred();
+          break;
+        }
+        continue;
+      }
+      if (cv.wait_until(lk, deadline) == std::cv_status::timeout) {
+        ok = pred();
+        break;
+      }
+    }
+    for (auto it = waiting_cvs_.begin(); it != waiting_cvs_.end(); ++it) {
+      if (*it == &cv) {
+        waiting_cvs_.erase(it);
+        break;
+      }
+    }
+    hand_off_locked();
+    return ok;
+  }
   bool write_frame(uint8_t type, uint8_t flags, uint32_t sid, std::string_view payload);
   bool write_frame_locked(uint8_t type, uint8_t flags, uint32_t sid, std::string_view payload);
   void on_headers(uint32_t sid, uint8_t flags, const std::string& block);
@@ -184,6 +236,11 @@ class Connection : public std::enable_shared_from_this<Connection> {
   // read buffer
   std::string rbuf_;
   size_t rpos_ = 0;
+  // caller-reads mode (set_caller_reads): whether a caller holds the reader role, and the
+  // condition variables of the callers waiting (guarded by mu_)
+  bool caller_reads_ = false;
+  bool reading_ = false;
+  std::vector<std::condition_variable*> waiting_cvs_;
 };
 
 }  // namespace bgc::http2

@@ -316,6 +316,10 @@ TlsStream::~TlsStream() {
   if (ssl_) {
     SSL_shutdown(ssl_);
     SSL_free(ssl_);
+    // SSL_shutdown on a connection that already failed queues an error on this thread;
+    // left there, it would make the next SSL_get_error on another connection read
+    // SSL_ERROR_SSL instead of WANT_READ
+    ERR_clear_error();
   }
   if (fd_ >= 0) ::close(fd_);
 }
@@ -391,6 +395,7 @@ ssize_t TlsStream::read_some(char* buf, size_t n, int timeout_ms) {
     int r, err;
     {
       std::lock_guard<std::mutex> lk(ssl_mu_);
+      ERR_clear_error();  // SSL_get_error reads this thread's queue first: start it empty
       r = SSL_read(ssl_, buf, static_cast<int>(n));
       if (r > 0) return r;
       err = SSL_get_error(ssl_, r);
@@ -420,6 +425,7 @@ bool TlsStream::write_all(const char* buf, size_t n) {
     int r, err;
     {
       std::lock_guard<std::mutex> lk(ssl_mu_);
+      ERR_clear_error();
       r = SSL_write(ssl_, buf, static_cast<int>(n));
       if (r <= 0) {
         err = SSL_get_error(ssl_, r);

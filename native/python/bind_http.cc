@@ -87,17 +87,18 @@ void register_http(py::module_& m) {
 
   py::class_<bgc::http::Client>(m, "HttpClient")
       .def(py::init([](const std::string& base_url, const std::string& ca_pem, bool http2, size_t h2_connections,
-                       int timeout_ms) {
+                       int timeout_ms, bool h2_caller_reads) {
              bgc::http::ClientOptions o;
              o.base_url = base_url;
              o.http2 = http2;
              o.h2_connections = h2_connections;
              o.timeout_ms = timeout_ms;
+             o.h2_caller_reads = h2_caller_reads;
              if (base_url.rfind("https", 0) == 0) o.tls = bgc::net::TlsContext::client(ca_pem, false);
              return std::make_unique<bgc::http::Client>(o);
            }),
            py::arg("base_url"), py::arg("ca_pem") = "", py::arg("http2") = true, py::arg("h2_connections") = 1,
-           py::arg("timeout_ms") = 10000)
+           py::arg("timeout_ms") = 10000, py::arg("h2_caller_reads") = false)
       // (status, body bytes, {lowercased header: value}); raises RuntimeError (HttpError) on
       // transport failures and timeouts
       .def("request",

@@ -5,6 +5,7 @@ What the services rely on: multiplexed concurrent requests; flow control both wa
 bodies larger than a window; streamed responses; graceful drain on stop (GOAWAY, requests
 in flight finish); reconnect after the server idles a connection out; a timed-out stream
 reset without losing the connection; and HTTP/1.1 fallback when the server does not offer h2.
+The client side runs in both HTTP/2 modes: a reader thread per connection, and caller-reads.
 """
 import threading
 import time
@@ -24,7 +25,19 @@ def server(nat, pki):
     s.stop(0)
 
 
+_MODE = {"caller_reads": False}
+
+
+@pytest.fixture(autouse=True, params=[False, True], ids=["reader-thread", "caller-reads"])
+def h2_client_mode(request):
+    """Every test runs twice: HTTP/2 client connections with their own reader thread, and
+    in caller-reads mode (the waiting callers read the frames; kube-lite's webhook client)."""
+    _MODE["caller_reads"] = request.param
+    yield request.param
+
+
 def client(nat, pki, port, **kw):
+    kw.setdefault("h2_caller_reads", _MODE["caller_reads"])
     return nat.HttpClient(f"https://127.0.0.1:{port}", pki["ca_cert"], **kw)
 
 
