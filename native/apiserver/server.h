@@ -67,9 +67,10 @@ struct Options {
   size_t webhook_h2_connections = 4;
   // HTTP/2 webhook callouts: the calling handler threads read their responses themselves
   // (http::ClientOptions::h2_caller_reads) instead of a reader thread per connection that
-  // then wakes them: one wake-up per callout instead of two.  BGC_KL_H2_CALLER_READS=0
-  // turns it off.
-  bool webhook_h2_caller_reads = true;
+  // then wakes them.  Off: on the MI355X box it raised the webhook p50 0.57 -> 0.71 ms (the
+  // reader-role hand-offs cost more wake-ups than they save, profiles/kl_shard_r4/
+  // caller_reads/).  BGC_KL_H2_CALLER_READS=1 turns it on.
+  bool webhook_h2_caller_reads = false;
   // Key-hashed shards of each type's object store, each with its own lock (commits of
   // different objects run in parallel; a commit-order lock per type assigns resourceVersions
   // and queues events).  1 = one lock per type, the round-3 store.  BGC_KL_STORE_SHARDS
