@@ -42,6 +42,7 @@ Sample* g_buf = nullptr;
 std::atomic<size_t> g_next{0};
 std::atomic<bool> g_on{false};
 std::atomic<uint64_t> g_dropped{0};
+std::atomic<uint64_t> g_overruns{0};  // timer expirations folded into one signal (si_overrun)
 int g_probe[2] = {-1, -1};
 // BGC_CPU_PROFILE_UNWIND=eh: walk with the .eh_frame unwinder (libgcc) instead of frame
 // pointers.  OpenSSL and glibc are built without frame pointers (they use %rbp as a
@@ -135,9 +136,15 @@ bool readable(uintptr_t p) {
   return true;
 }
 
-void on_sigprof(int, siginfo_t*, void* ucv) {
+void on_sigprof(int, siginfo_t* si, void* ucv) {
   if (!g_on.load(std::memory_order_relaxed)) return;
   int saved_errno = errno;
+  // A per-thread CPU timer is checked on scheduler ticks: expirations between two checks
+  // arrive as one signal with si_overrun counting the rest (coverage = samples /
+  // (samples + overruns) of the CPU time at the requested rate).
+  if (si && si->si_code == SI_TIMER && si->si_overrun > 0) {
+    g_overruns.fetch_add(static_cast<uint64_t>(si->si_overrun), std::memory_order_relaxed);
+  }
   size_t i = g_next.fetch_add(1, std::memory_order_relaxed);
   if (i >= kMaxSamples) {
     g_dropped.fetch_add(1, std::memory_order_relaxed);
@@ -200,7 +207,8 @@ void write_profile() {
   std::ofstream out(g_path);
   if (!out) return;
   std::ifstream maps("/proc/self/maps");
-  out << "# bgc cpuprof v1 samples=" << n << " dropped=" << g_dropped.load() << "\n";
+  out << "# bgc cpuprof v1 samples=" << n << " dropped=" << g_dropped.load() << " overruns=" << g_overruns.load()
+      << "\n";
   out << "maps\n" << maps.rdbuf() << "end maps\n";
   char buf[32];
   for (const auto& [st, cnt] : stacks) {
