@@ -150,7 +150,59 @@ def _cpulist_text(cpus):
     return ",".join(out)
 
 
-def quota_cpuset():
+def _gpu_local_cpus():
+    """CPUs of the NUMA node of this job's GPU: the container's own /dev/dri render node
+    names its sysfs device (every GPU of the host shows in /sys); else the first AMD GPU."""
+    devs = [f"/sys/class/drm/{os.path.basename(n)}/device" for n in sorted(glob.glob("/dev/dri/renderD*"))]
+    devs += sorted(glob.glob("/sys/class/drm/renderD*/device"))
+    for dev in devs:
+        try:
+            with open(os.path.join(dev, "vendor")) as f:
+                if f.read().strip() != "0x1002":
+                    continue
+            with open(os.path.join(dev, "local_cpulist")) as f:
+                return _cpulist(f.read())
+        except (OSError, ValueError):
+            continue
+    return set()
+
+
+def _cpu_busy(cpus, interval=0.3):
+    """Share of the last `interval` seconds each CPU spent busy (other tenants' work too)."""
+    def snap():
+        out = {}
+        try:
+            with open("/proc/stat") as f:
+                for line in f:
+                    if line.startswith("cpu") and line[3:4].isdigit():
+                        p = line.split()
+                        v = [int(x) for x in p[1:]]
+                        out[int(p[0][3:])] = (sum(v), v[3] + (v[4] if len(v) > 4 else 0))
+        except (OSError, ValueError):
+            pass
+        return out
+    a = snap()
+    time.sleep(interval)
+    b = snap()
+    busy = {}
+    for c in cpus:
+        if c in a and c in b and b[c][0] > a[c][0]:
+            busy[c] = 1.0 - (b[c][1] - a[c][1]) / (b[c][0] - a[c][0])
+        else:
+            busy[c] = 0.0
+    return busy
+
+
+def _core_of(c):
+    """The physical core a CPU belongs to (its SMT siblings share it)."""
+    try:
+        with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
+            return min(_cpulist(f.read()))
+    except (OSError, ValueError):
+        return c
+
+
+def quota_cpuset(measure=True):
     """The CPUs to run the control plane on when the cgroup's CPU quota is smaller than the
     affinity mask (the MI355X boxes: a 16-CPU quota per GPU over 256 visible CPUs), or None.
 
@@ -159,29 +211,40 @@ def quota_cpuset():
     whole stack jump to 40-50 ms whenever the load outruns the quota (measured on the box:
     33 of 97 periods throttled in a headline run, profiles/kl_shard_r4/).  Pinned to as many
     CPUs as the quota grants, the same CPU time is shared instead (what a Kubernetes pod gets
-    from the static CPU manager, or a Go service from a quota-sized GOMAXPROCS).  Prefers the
-    CPUs local to the first GPU's NUMA node, leaving CPU 0 (interrupts) out when it can."""
+    from the static CPU manager, or a Go service from a quota-sized GOMAXPROCS).
+
+    Which CPUs: those of the GPU's NUMA node, CPU 0 (interrupts) left out, the idlest first
+    (the host runs other tenants: one of them held a CPU at 100 % in a sample on the box),
+    one per physical core before any SMT sibling."""
     if not hasattr(os, "sched_getaffinity"):
         return None
     aff = sorted(os.sched_getaffinity(0))
     n = effective_cpus()
     if n >= len(aff):
         return None
-    local = set()
-    for dev in sorted(glob.glob("/sys/class/drm/renderD*/device")):
-        try:
-            with open(os.path.join(dev, "vendor")) as f:
-                if f.read().strip() != "0x1002":
-                    continue
-            with open(os.path.join(dev, "local_cpulist")) as f:
-                local = _cpulist(f.read()) & set(aff)
-            break
-        except (OSError, ValueError):
-            continue
+    local = _gpu_local_cpus() & set(aff)
     pool = [c for c in aff if c in local and c != 0] or [c for c in aff if c != 0] or aff
     if len(pool) < n:
         pool += [c for c in aff if c not in pool]
-    return sorted(pool[:n])
+    if measure:
+        busy = _cpu_busy(pool)
+        # 5 % steps: CPUs equally idle keep their index order
+        order = {c: i for i, c in enumerate(pool)}
+        pool.sort(key=lambda c: (round(busy.get(c, 0.0) * 20), order[c]))
+    chosen, cores = [], set()
+    for c in pool:  # one CPU per physical core first
+        core = _core_of(c)
+        if core not in cores:
+            chosen.append(c)
+            cores.add(core)
+        if len(chosen) == n:
+            break
+    for c in pool:  # then SMT siblings, if the node has fewer idle cores than the quota
+        if len(chosen) == n:
+            break
+        if c not in chosen:
+            chosen.append(c)
+    return sorted(chosen)
 
 
 def cgroup_throttling():
@@ -507,10 +570,13 @@ class _Phase:
         self.write_latency_ms, self.warmup, self.steps = write_latency_ms, warmup, steps
 
 
-def pin_to_quota():
+def pin_to_quota(d=None):
     """Pins every thread of this process (and so the control plane it starts) to
-    quota_cpuset(); the CPU list, or None when no pinning is needed."""
-    cs = quota_cpuset()
+    quota_cpuset(), chosen on rank 0 and shared with every rank (the quota covers the whole
+    job); the CPU list, or None when no pinning is needed."""
+    cs = quota_cpuset() if d is None or d.rank == 0 else None
+    if d is not None:
+        cs = d.broadcast_obj(cs)
     if cs:
         for tid in os.listdir("/proc/self/task"):
             try:
@@ -524,7 +590,7 @@ def run(args):
     d = Dist()
     n = args.gpus if args.gpus else d.world
     # every rank pins itself to the same CPUs: the quota covers the whole job
-    cpuset = pin_to_quota() if args.pin_to_quota else None
+    cpuset = pin_to_quota(d) if args.pin_to_quota else None
     from bacchus_gpu_controller_amd import native
     from bacchus_gpu_controller_amd.testing.cluster import Cluster
     from bacchus_gpu_controller_amd.testing.fake_google import FakeGoogle

@@ -16,16 +16,36 @@ def test_no_pinning_when_the_quota_covers_the_mask(monkeypatch):
     assert harness.quota_cpuset() is None
 
 
-def test_quota_sized_set_prefers_the_gpus_numa_cpus_and_skips_cpu0(monkeypatch, tmp_path):
+def _box(monkeypatch, local, busy=None):
+    # 2 x 64 cores with SMT: CPU c and c + 128 are siblings (the MI355X box's topology)
     monkeypatch.setattr(harness.os, "sched_getaffinity", lambda pid: set(range(256)))
     monkeypatch.setattr(harness, "effective_cpus", lambda: 16)
-    # no AMD GPU visible: the first CPUs of the mask, CPU 0 left out
-    monkeypatch.setattr(harness.glob, "glob", lambda pattern: [])
+    monkeypatch.setattr(harness, "_gpu_local_cpus", lambda: set(local))
+    monkeypatch.setattr(harness, "_core_of", lambda c: c % 128)
+    monkeypatch.setattr(harness, "_cpu_busy", lambda cpus, interval=0.3: {c: (busy or {}).get(c, 0.0) for c in cpus})
+
+
+def test_quota_sized_set_prefers_the_gpus_numa_node_and_skips_cpu0(monkeypatch):
+    _box(monkeypatch, local=[])  # GPU node unknown: the first CPUs of the mask, not CPU 0
     assert harness.quota_cpuset() == list(range(1, 17))
-    # an AMD GPU whose NUMA node holds CPUs 64-127
-    dev = tmp_path / "renderD128" / "device"
-    dev.mkdir(parents=True)
-    (dev / "vendor").write_text("0x1002\n")
-    (dev / "local_cpulist").write_text("64-127\n")
-    monkeypatch.setattr(harness.glob, "glob", lambda pattern: [str(dev)])
+    _box(monkeypatch, local=list(range(64, 128)) + list(range(192, 256)))
     assert harness.quota_cpuset() == list(range(64, 80))
+
+
+def test_busy_cpus_and_smt_siblings_come_last(monkeypatch):
+    # another tenant holds CPUs 8 and 70 at 100 %: they are skipped for idle ones
+    _box(monkeypatch, local=list(range(0, 64)) + list(range(128, 192)), busy={8: 1.0, 12: 0.5})
+    cs = harness.quota_cpuset()
+    assert len(cs) == 16 and 8 not in cs and 12 not in cs and 0 not in cs
+    assert cs == [c for c in range(1, 19) if c not in (8, 12)]
+    # one CPU per physical core: never a CPU and its sibling while idle cores remain
+    assert len({c % 128 for c in cs}) == 16
+    # a node with fewer idle cores than the quota falls back to siblings
+    _box(monkeypatch, local=list(range(1, 9)) + list(range(129, 137)))
+    cs = harness.quota_cpuset()
+    assert sorted(cs) == list(range(1, 9)) + list(range(129, 137))
+
+
+def test_measured_busy_share_from_proc_stat():
+    busy = harness._cpu_busy([0], interval=0.05)
+    assert 0.0 <= busy[0] <= 1.0
