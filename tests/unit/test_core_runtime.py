@@ -132,6 +132,35 @@ def test_crypto_against_stdlib(nat):
     assert re.fullmatch(r"[0-9a-f]{8}-[0-9a-f]{4}-4[0-9a-f]{3}-[89ab][0-9a-f]{3}-[0-9a-f]{12}", nat.uuid_v4())
 
 
+def test_uuids_unique_across_threads_and_forks(nat):
+    """uuid_v4 draws from a per-thread CSPRNG pool: unique across pool refills and
+    threads, and a forked child never repeats the parent's pending pool."""
+    import os
+    import threading
+    pat = re.compile(r"[0-9a-f]{8}-[0-9a-f]{4}-4[0-9a-f]{3}-[89ab][0-9a-f]{3}-[0-9a-f]{12}")
+    seen = [nat.uuid_v4() for _ in range(1000)]  # several 4 KiB pool refills
+    out = []
+    ts = [threading.Thread(target=lambda: out.extend(nat.uuid_v4() for _ in range(600))) for _ in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    seen += out
+    assert all(pat.fullmatch(u) for u in seen) and len(set(seen)) == len(seen) == 3400
+    r, w = os.pipe()
+    pid = os.fork()
+    if pid == 0:  # child: the next UUIDs of the inherited pool must not be the parent's
+        os.close(r)
+        os.write(w, "".join(nat.uuid_v4() for _ in range(4)).encode())
+        os._exit(0)
+    os.close(w)
+    child = os.read(r, 4096).decode()
+    os.close(r)
+    os.waitpid(pid, 0)
+    parent = "".join(nat.uuid_v4() for _ in range(4))
+    assert len(child) == len(parent) == 144 and child != parent
+
+
 def test_certificates_verify_with_openssl(nat, tmp_path):
     b = nat.make_ca_and_leaf("bgc-admission", ["bgc-admission.bgc.svc", "127.0.0.1"], 90)
     (tmp_path / "ca.crt").write_text(b["ca_cert"])
