@@ -272,6 +272,10 @@ inline const std::shared_ptr<const Managers>& no_managers() {
 struct Stored {
   std::shared_ptr<const Value> obj;
   uint64_t rv = 0;
+  // The event line of the commit that stored obj ({"type":"ADDED|MODIFIED","object":<obj>}),
+  // shared with the history: a DELETED event reuses its serialization instead of dumping obj
+  // again.  Null for objects stored outside commit_locked.
+  std::shared_ptr<const std::string> line;
   // Shared and immutable, like obj: a writer's snapshot of the stored object (taken under
   // the store lock) copies two pointers instead of every manager's field set.
   std::shared_ptr<const Managers> managers = no_managers();
@@ -1437,6 +1441,7 @@ struct ApiServer::Impl {
     s.obj = ptr;
     s.rv = new_rv;
     s.managers = std::make_shared<const Managers>(std::move(managers));
+    s.line = line;
     ts.shard(key).objs[key] = std::move(s);
     if (line_out) *line_out = std::move(line);
     return ptr;
@@ -1464,7 +1469,15 @@ struct ApiServer::Impl {
     std::shared_ptr<const Value> ptr = it->second.obj;
     std::string line = "{\"type\":\"DELETED\",\"object\":";
     const size_t obj_at = line.size();
-    ptr->dump_to(line);
+    static const std::string kObjectKey = ",\"object\":";
+    const std::string* committed = it->second.line.get();
+    const size_t at = committed ? committed->find(kObjectKey) : std::string::npos;
+    if (at != std::string::npos && committed->size() >= at + kObjectKey.size() + 2) {
+      // the object as its last commit serialized it (same tree, same rv digits)
+      line.append(*committed, at + kObjectKey.size(), committed->size() - (at + kObjectKey.size()) - 2);
+    } else {
+      ptr->dump_to(line);
+    }
     line += "}\n";
     const std::string old_rv = "\"resourceVersion\":" + json::quote(ptr->get("metadata").get_string("resourceVersion"));
     const size_t pos = line.find(old_rv, obj_at);

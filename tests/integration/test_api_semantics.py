@@ -243,3 +243,37 @@ def test_controller_converges_with_metadata_child_watches(metadata_watches):
         c.admin.delete("resourcequotas", "mw1", namespace="mw1")
         wait_for(lambda: (c.admin.get_or_none("resourcequotas", "mw1", "mw1") or {"metadata": {"uid": uid}})
                  ["metadata"]["uid"] != uid, timeout=15, desc="re-created")
+
+
+def test_deleted_event_carries_the_last_object_at_the_deletion_version():
+    """A DELETED watch event carries the object as last stored (managedFields and all) at
+    the deletion's resourceVersion; kube-lite reuses the last commit's serialization for it."""
+    with Cluster(admission=False, controller=False) as c:
+        c.admin.create("namespaces", {"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "dw"}})
+        rq = {"apiVersion": "v1", "kind": "ResourceQuota", "metadata": {"name": "q", "namespace": "dw",
+                                                                        "labels": {"a": "b"}},
+              "spec": {"hard": {"requests.amd.com/gpu": "1"}}}
+        c.admin.apply("resourcequotas", "q", rq, "mgr-1", namespace="dw")
+        rq["spec"]["hard"]["requests.amd.com/gpu"] = "2"
+        last = c.admin.apply("resourcequotas", "q", rq, "mgr-1", namespace="dw")
+        c.admin.merge_patch("resourcequotas", "q", {"metadata": {"annotations": {"x": "y"}}}, namespace="dw",
+                            field_manager="mgr-2")
+        last = c.admin.get("resourcequotas", "q", "dw")
+        start = last["metadata"]["resourceVersion"]
+        with requests.get(f"{c.server}/api/v1/namespaces/dw/resourcequotas",
+                          params={"watch": "true", "resourceVersion": start, "timeoutSeconds": "10"},
+                          headers={"Authorization": c.admin.s.headers["Authorization"]}, stream=True,
+                          timeout=15, verify=c.verify) as r:
+            time.sleep(0.2)
+            c.admin.delete("resourcequotas", "q", "dw")
+            ev = None
+            for line in r.iter_lines():
+                if line:
+                    ev = json.loads(line)
+                    if ev["type"] == "DELETED":
+                        break
+        assert ev and ev["type"] == "DELETED"
+        got = ev["object"]
+        assert int(got["metadata"].pop("resourceVersion")) > int(last["metadata"].pop("resourceVersion"))
+        assert got == last
+        assert {m["manager"] for m in got["metadata"]["managedFields"]} == {"mgr-1", "mgr-2"}
