@@ -523,9 +523,16 @@ Value KubeClient::replace_status(const ResourceType& rt, const std::string& ns, 
 
 namespace {
 std::string response_rv(const http::Response& r) {
+  // only metadata.resourceVersion is needed: located by scanning, no tree built
   std::string_view md = json::raw_member(r.body, "metadata");
   if (md.empty()) return "";
-  return json::parse(md, "managedFields").get_string("resourceVersion");
+  std::string_view rv = json::raw_member(md, "resourceVersion");
+  if (rv.size() >= 2 && rv.front() == '"' && rv.back() == '"' && rv.find('\\') == std::string_view::npos) {
+    return std::string(rv.substr(1, rv.size() - 2));
+  }
+  if (rv.empty()) return "";
+  const Value v = json::parse(rv);
+  return v.is_string() ? v.as_string() : "";
 }
 }  // namespace
 
@@ -557,9 +564,16 @@ std::string KubeClient::apply_rv(const ResourceType& rt, const std::string& ns, 
       with_params(rt.object_path(ns, name), {{"fieldManager", field_manager}, {"force", force ? "true" : ""}});
   http::Response r = raw("PATCH", path, body_json, "application/apply-patch+yaml");
   if (r.status < 200 || r.status >= 300) throw_api_error(r);
+  // only metadata.resourceVersion is needed: located by scanning, no tree built
   std::string_view md = json::raw_member(r.body, "metadata");
   if (md.empty()) return "";
-  return json::parse(md, "managedFields").get_string("resourceVersion");
+  std::string_view rv = json::raw_member(md, "resourceVersion");
+  if (rv.size() >= 2 && rv.front() == '"' && rv.back() == '"' && rv.find('\\') == std::string_view::npos) {
+    return std::string(rv.substr(1, rv.size() - 2));
+  }
+  if (rv.empty()) return "";
+  const Value v = json::parse(rv);
+  return v.is_string() ? v.as_string() : "";
 }
 
 Value KubeClient::apply_status(const ResourceType& rt, const std::string& ns, const std::string& name,
