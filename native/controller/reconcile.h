@@ -59,11 +59,12 @@ struct Config {
   // 3 s.  0 = the reference's fixed error_requeue_ms (controller.rs:174).
   int64_t error_backoff_base_ms = 0;
   int64_t child_delete_delay_ms = 50;
-  // kube::Controller::Options::debounce (CONF_DEBOUNCE_MS).  1 ms merges the
-  // synchronizer's back-to-back quota and status writes into one reconcile: 3.0 -> 2.1
-  // reconciles and -23 % controller CPU per CR at an unchanged apply->Ready p50
-  // (profiles/controller_cpu_r4/); 0 = every event reconciles at once, as kube-runtime 0.84.
-  int64_t debounce_ms = 1;
+  // kube::Controller::Options::debounce (CONF_DEBOUNCE_MS).  0 (kube-runtime's default):
+  // every event reconciles at once.  1 ms merges the synchronizer's back-to-back quota and
+  // status writes into one reconcile (3.0 -> 2.1 reconciles, controller CPU -15-23 % per CR)
+  // at the price of a higher reconcile p99, since the merged reconcile applies the
+  // ResourceQuota and then the RoleBinding (profiles/controller_cpu_r4/ab_applyrv/).
+  int64_t debounce_ms = 0;
   bool label_children = true;  // see kManagedByLabel
   // Child watches ask for PartialObjectMetadata only: the controller reads a child's
   // resourceVersion and ownerReferences, never its spec (kube-rs metadata_watcher).
