@@ -21,7 +21,7 @@ Config Config::from_env(const EnvConfig& env) {
   c.skip_unchanged = env.boolean_or("skip_unchanged", true);
   c.parallel_children = env.boolean_or("parallel_children", true);
   c.child_delete_delay_ms = static_cast<int64_t>(env.u64_or("child_delete_delay_ms", 50));
-  c.debounce_ms = static_cast<int64_t>(env.u64_or("debounce_ms", 1));
+  c.debounce_ms = static_cast<int64_t>(env.u64_or("debounce_ms", 0));
   c.requeue_secs = static_cast<int64_t>(env.u64_or("requeue_secs", 30));
   c.error_requeue_ms = static_cast<int64_t>(env.u64_or("error_requeue_ms", 3000));
   c.error_backoff_base_ms = static_cast<int64_t>(env.u64_or("error_backoff_base_ms", 0));
