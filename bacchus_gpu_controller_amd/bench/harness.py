@@ -570,6 +570,24 @@ class _Phase:
         self.write_latency_ms, self.warmup, self.steps = write_latency_ms, warmup, steps
 
 
+def _dump_components(cluster):
+    """On a failed run: every component's state and the errors in its log, on stderr (a
+    synchronizer that exits on a write error, as the reference's does, shows up here)."""
+    for name, proc in cluster.procs.items():
+        try:
+            rc = proc.p.poll()
+            text = proc.output()
+            lines = text.splitlines()
+            errors = [l for l in lines if " ERROR " in l or " WARN " in l][-15:]
+            tail = lines[-5:] if rc is not None else []
+            print(f"[bench] component {name}: pid {proc.p.pid}, {'running' if rc is None else f'exited {rc}'}",
+                  file=sys.stderr)
+            for l in errors + [t for t in tail if t not in errors]:
+                print(f"[bench]   {name}: {l[:400]}", file=sys.stderr)
+        except Exception as e:  # noqa: BLE001
+            print(f"[bench] component {name}: state unavailable ({e})", file=sys.stderr)
+
+
 def pin_to_quota(d=None):
     """Pins every thread of this process (and so the control plane it starts) to
     quota_cpuset(), chosen on rank 0 and shared with every rank (the quota covers the whole
@@ -804,6 +822,10 @@ def run(args):
             except Exception:  # noqa: BLE001
                 pass
         return out
+    except BaseException:
+        if cluster is not None:
+            _dump_components(cluster)
+        raise
     finally:
         if cluster is not None:
             cluster.stop()
