@@ -29,12 +29,21 @@ SYNC_TOKEN = "synchronizer-token"
 NODE_AGENT_TOKEN = "node-agent-token"
 
 
+_issued_ports = set()
+
+
 def free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    """A port nothing listens on, never one this process handed out before: the OS may
+    return a just-released port again, and two components told to listen on the same port
+    would have one fail to bind while the other answers its health checks."""
+    while True:
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        p = s.getsockname()[1]
+        s.close()
+        if p not in _issued_ports:
+            _issued_ports.add(p)
+            return p
 
 
 # glibc malloc: a deeper per-thread cache (default 7 chunks per size class) keeps the
@@ -251,8 +260,9 @@ current-context: {name}@kube-lite
         env.update(self.admission_env)
         self.procs["admission"] = Proc("admission", [binary("admission")], env, self.workdir)
         ca = os.path.join(self.cert_dir, "ca.crt")
-        wait_for(lambda: requests.get(f"https://127.0.0.1:{self.admission_port}/health", verify=ca, timeout=1).text == "pong",
-                 20, desc="admission /health")
+        adm = self.procs["admission"]
+        wait_for(lambda: adm.alive() and requests.get(f"https://127.0.0.1:{self.admission_port}/health", verify=ca,
+                                                      timeout=1).text == "pong", 20, desc="admission /health")
 
     def start_controller(self, extra_env=None):
         self.controller_port = free_port()
@@ -260,8 +270,9 @@ current-context: {name}@kube-lite
         env.update(self.controller_env)
         env.update(extra_env or {})
         self.procs["controller"] = Proc("controller", [binary("controller")], env, self.workdir)
-        wait_for(lambda: requests.get(f"http://127.0.0.1:{self.controller_port}/health", timeout=1).text == "pong",
-                 20, desc="controller /health")
+        proc = self.procs["controller"]
+        wait_for(lambda: proc.alive() and requests.get(f"http://127.0.0.1:{self.controller_port}/health",
+                                                       timeout=1).text == "pong", 20, desc="controller /health")
 
     def start_synchronizer(self, google, interval=60, server_name="mi355x-01", extra_env=None, wait_healthy=True):
         """Start the native synchronizer against a FakeGoogle (testing/fake_google.py)."""
@@ -276,8 +287,8 @@ current-context: {name}@kube-lite
         env.update(extra_env or {})
         p = self.start_process("synchronizer", "synchronizer", env)
         if wait_healthy:
-            wait_for(lambda: requests.get(f"http://127.0.0.1:{self.sync_port}/health", timeout=1).text == "pong",
-                     20, desc="synchronizer /health")
+            wait_for(lambda: p.alive() and requests.get(f"http://127.0.0.1:{self.sync_port}/health",
+                                                        timeout=1).text == "pong", 20, desc="synchronizer /health")
         return p
 
     def start_node_agent(self, node_name="mi355x-0", max_gpus=0, backend="auto", n_mock_gpus=8, extra_env=None,
