@@ -132,29 +132,41 @@ bool Synchronizer::sync_one(const Value& ub, std::vector<std::string>* produced)
                            << " storage_request=" << row->storage_request << " mig_request=" << row->mig_request;
   LOG_DEBUG("synchronizer") << "row name=" << row->name << " department=" << row->department;
   std::string rv = ub.get("metadata").get_string("resourceVersion");
-  if (!quota_same || !cfg_.skip_unchanged) {
-    json::PatchBuilder ops;
-    if (!has_quota) ops.add("/spec/quota", Value::object());
-    ops.replace("/spec/quota", desired);
-    rv = client_.patch_json_rv(types::UserBootstrap, "", name, ops.ops(), kPatchManager);
-    if (produced) produced->push_back(rv);
-    LOG_INFO("synchronizer") << "quota updated";
-  }
-  if (!synced || !cfg_.skip_unchanged) {
-    for (int attempt = 0; attempt < 3; ++attempt) {
-      Value body = Value::object({{"apiVersion", "bacchus.io/v1"}, {"kind", "UserBootstrap"}});
-      body["metadata"] = Value::object({{"name", name}, {"resourceVersion", rv}});
-      body["status"] = Value::object({{"synchronized_with_sheet", true}});
-      try {
-        LOG_INFO("synchronizer") << "updating status";
-        const std::string written_rv = client_.replace_status_rv(types::UserBootstrap, "", name, body);
-        if (produced) produced->push_back(written_rv);
-        break;
-      } catch (const kube::ApiError& e) {
-        if (e.code() != 409 || attempt == 2) throw;
-        rv = client_.get(types::UserBootstrap, "", name).get("metadata").get_string("resourceVersion");
+  // A UserBootstrap deleted while it is being synchronized (its owner onboarded and left,
+  // or the cache still showed it) has nothing left to synchronize: NotFound ends this sync
+  // without failing it.  Every other error keeps the reference's exit-on-error (Q7).
+  try {
+    if (!quota_same || !cfg_.skip_unchanged) {
+      json::PatchBuilder ops;
+      if (!has_quota) ops.add("/spec/quota", Value::object());
+      ops.replace("/spec/quota", desired);
+      rv = client_.patch_json_rv(types::UserBootstrap, "", name, ops.ops(), kPatchManager);
+      if (produced) produced->push_back(rv);
+      LOG_INFO("synchronizer") << "quota updated";
+    }
+    if (!synced || !cfg_.skip_unchanged) {
+      for (int attempt = 0; attempt < 3; ++attempt) {
+        Value body = Value::object({{"apiVersion", "bacchus.io/v1"}, {"kind", "UserBootstrap"}});
+        body["metadata"] = Value::object({{"name", name}, {"resourceVersion", rv}});
+        body["status"] = Value::object({{"synchronized_with_sheet", true}});
+        try {
+          LOG_INFO("synchronizer") << "updating status";
+          const std::string written_rv = client_.replace_status_rv(types::UserBootstrap, "", name, body);
+          if (produced) produced->push_back(written_rv);
+          break;
+        } catch (const kube::ApiError& e) {
+          if (e.code() != 409 || attempt == 2) throw;
+          rv = client_.get(types::UserBootstrap, "", name).get("metadata").get_string("resourceVersion");
+        }
       }
     }
+  } catch (const kube::ApiError& e) {
+    if (e.code() != 404) throw;
+    static auto& gone = metrics::Registry::global().counter(
+        "bgc_sync_deleted_during_sync_total", "UserBootstraps deleted while their synchronization was in flight");
+    gone.inc();
+    LOG_INFO("synchronizer") << "userbootstrap " << name << " was deleted during synchronization";
+    return false;
   }
   static auto& written = metrics::Registry::global().counter("bgc_sync_writes_total", "UserBootstraps written by the synchronizer");
   written.inc();

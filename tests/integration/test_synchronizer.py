@@ -228,6 +228,29 @@ def test_webhook_down_default_synchronizer_exits(google):
         assert not c.admin.get("userbootstraps", "frank").get("status")  # Q5: quota first, so no status
 
 
+def test_userbootstrap_deleted_during_sync_is_not_a_failure(google):
+    """A UserBootstrap that is gone when the synchronizer writes it (deleted after the watch
+    offered it) answers NotFound: nothing is left to synchronize, so the synchronizer keeps
+    running and serves the next tenant.  Any other write error still ends it (Q7, above)."""
+    google.set_rows([{"id_username": "hank", "gpu": 1}, {"id_username": "ivy", "gpu": 2}])
+    with Cluster(controller=False) as c:
+        c.as_user("oidc:hank", ["gpu"]).create("userbootstraps", ub("hank"))
+        # hank's quota PATCH answers 404, as if hank had been deleted in between
+        c.fault([{"method": "PATCH", "path": "/apis/bacchus.io/v1/userbootstraps/hank(\\?|$)", "status": 404}])
+        p = c.start_synchronizer(google, interval=60)
+
+        def deleted_during_sync():
+            m = requests.get(f"http://127.0.0.1:{c.sync_port}/metrics", timeout=5).text
+            return "bgc_sync_deleted_during_sync_total 1" in m
+
+        wait_for(deleted_during_sync, timeout=15, desc="NotFound handled")
+        assert p.alive() and c.stats()["faults_hit"] == 1
+        c.as_user("oidc:ivy", ["gpu"]).create("userbootstraps", ub("ivy"))
+        st = wait_for(lambda: (c.admin.get("userbootstraps", "ivy").get("status") or {}).get("synchronized_with_sheet"),
+                      timeout=15, desc="ivy synchronized")
+        assert st is True and p.alive()
+
+
 def test_webhook_down_retries_back_off_then_converge(google):
     """CONF_EXIT_ON_ERROR=false: a failing UserBootstrap is retried with per-key exponential
     backoff (base 100 ms, cap 800 ms here; 5 ms / 60 s by default) instead of a fixed
