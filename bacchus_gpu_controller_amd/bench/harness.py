@@ -441,6 +441,12 @@ def _phase(d, nat, info, args, phase, concurrency, warmup, steps, cluster):
                 names = _names(d.rank, phase, s * args.rounds + r, args.batch)
                 res = json.loads(driver.step_with_delete(names, prev or [], args.timeout))
                 prev = names
+                if cluster is not None and res.get("timeouts"):
+                    # a component that died stalls every later tenant: fail now, not after
+                    # a timeout per round
+                    dead = [n for n, pr in cluster.procs.items() if not pr.alive()]
+                    if dead:
+                        raise RuntimeError(f"control-plane process(es) exited during the run: {', '.join(dead)}")
                 if s >= warmup:
                     lat += res["ready_latency_s"]
                     clat += res["create_latency_s"]
