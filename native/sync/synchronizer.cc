@@ -103,7 +103,11 @@ void Synchronizer::refresh_locked() {
     index_ = idx;
   }
   last_refresh_ns_.store(metrics::now_ns());
-  index_gen_.fetch_add(1);
+  // A new generation re-evaluates every UserBootstrap (the echo filter's decisions were made
+  // against the old rows); an unchanged sheet (the periodic tick's re-read) keeps them, so
+  // a tenant whose own writes have not echoed yet is not written a second time.
+  const size_t digest = std::hash<std::string>{}(csv);
+  if (digest != csv_digest_.exchange(digest) || index_gen_.load() == 0) index_gen_.fetch_add(1);
   std::lock_guard<std::mutex> lk(mu_);
   known_version_ = version;
 }

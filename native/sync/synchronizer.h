@@ -110,7 +110,8 @@ class Synchronizer {
   std::shared_ptr<const RowIndex> index_;
   std::string known_version_;  // guarded by mu_
   std::atomic<int64_t> last_refresh_ns_{0};
-  std::atomic<uint64_t> index_gen_{0};  // bumped by every refresh()
+  std::atomic<uint64_t> index_gen_{0};  // bumped by every refresh() that read a changed sheet
+  std::atomic<size_t> csv_digest_{0};   // hash of the last sheet export read
   std::mutex refresh_mu_;
 };
 
