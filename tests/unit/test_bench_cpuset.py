@@ -49,3 +49,24 @@ def test_busy_cpus_and_smt_siblings_come_last(monkeypatch):
 def test_measured_busy_share_from_proc_stat():
     busy = harness._cpu_busy([0], interval=0.05)
     assert 0.0 <= busy[0] <= 1.0
+
+
+def test_every_rank_pins_to_rank0s_choice(monkeypatch):
+    """The quota covers the whole job: rank 0 chooses the CPU set and every rank applies
+    that same set (a rank choosing on its own could pick other CPUs)."""
+    chosen = [3, 4, 5]
+    pinned = []
+
+    class D:
+        def __init__(self, rank):
+            self.rank = rank
+
+        def broadcast_obj(self, obj):
+            return chosen if self.rank else obj
+
+    monkeypatch.setattr(harness, "quota_cpuset", lambda: chosen)
+    monkeypatch.setattr(harness.os, "sched_setaffinity", lambda tid, cs: pinned.append(tuple(cs)))
+    assert harness.pin_to_quota(D(0)) == chosen
+    monkeypatch.setattr(harness, "quota_cpuset", lambda: (_ for _ in ()).throw(AssertionError("rank 1 chose")))
+    assert harness.pin_to_quota(D(1)) == chosen
+    assert pinned and set(pinned) == {tuple(chosen)}
