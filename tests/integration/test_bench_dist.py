@@ -101,5 +101,7 @@ def test_single_tenant_bench_config1():
     d = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
     assert d["config"] == 1 and d["crdgen"]["byte_identical"] and d["tenants"] == 4
     st = d["apply_to_stage_ms"]
-    assert 0 < st["namespace"]["p50"] <= st["quota"]["p50"] <= st["rolebinding"]["p50"] < 5000
+    # each stage is seen on its own watch stream, so their order is not asserted: under load
+    # one stream's delivery can lag another's by more than the gap between the writes
+    assert all(0 < st[k]["p50"] < 5000 for k in ("namespace", "quota", "rolebinding"))
     assert d["reconcile_ms"]["p50"] > 0
