@@ -201,6 +201,22 @@ void diff_leaves(const Value& before, const Value& after, FieldSet& changed, Fie
   }
 }
 
+void diff_member_leaves(const Value& before, const Value& after, const std::string& key, FieldSet& changed,
+                        FieldSet& removed) {
+  const std::string base = "/" + json::escape_pointer_token(key);
+  FieldSet b, a;
+  if (const Value* v = before.find(key)) collect(*v, base, b, true);
+  if (const Value* v = after.find(key)) collect(*v, base, a, true);
+  for (const auto& p : a) {
+    const Value* bv = b.count(p) ? get_path(before, p) : nullptr;
+    const Value* av = get_path(after, p);
+    if (!bv || !av || !(*bv == *av)) changed.insert(p);
+  }
+  for (const auto& p : b) {
+    if (!a.count(p)) removed.insert(p);
+  }
+}
+
 std::string display_path(const std::string& path) {
   std::string out;
   Tokens ts(path);

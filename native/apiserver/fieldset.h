@@ -27,6 +27,10 @@ void set_path(json::Value& root, const std::string& path, const json::Value& v);
 // those removed.
 void diff_leaves(const json::Value& before, const json::Value& after, FieldSet& changed, FieldSet& removed,
                  bool include_status = false);
+// diff_leaves restricted to the top-level member `key` (paths keep their "/key" prefix),
+// for writes that can change nothing else, such as a status subresource write.
+void diff_member_leaves(const json::Value& before, const json::Value& after, const std::string& key,
+                        FieldSet& changed, FieldSet& removed);
 // Human-readable ".spec.hard.cpu" form for conflict messages.
 std::string display_path(const std::string& path);
 // metadata.managedFields[].fieldsV1 rendering of a set.

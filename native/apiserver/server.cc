@@ -1322,14 +1322,10 @@ struct ApiServer::Impl {
   static void attribute_update(Managers& m, const std::string& manager, const Value& before, const Value& after,
                                bool status_write, const std::string& api_version) {
     FieldSet changed, removed;
-    diff_leaves(before, after, changed, removed, /*include_status=*/status_write);
-    if (status_write) {
-      FieldSet keep;
-      for (const auto& p : changed) {
-        if (p == "/status" || p.rfind("/status/", 0) == 0) keep.insert(p);
-      }
-      changed.swap(keep);
-    }
+    // a status write replaces status alone (do_update / do_patch copy everything else
+    // from the stored object), so only that subtree is diffed
+    if (status_write) diff_member_leaves(before, after, "status", changed, removed);
+    else diff_leaves(before, after, changed, removed);
     for (auto& [name, e] : m) {
       for (const auto& p : changed) e.fields.erase(p);
       for (const auto& p : removed) e.fields.erase(p);

@@ -74,6 +74,22 @@ def test_optimistic_concurrency_and_status_subresource(c):
     assert p["status"]["synchronized_with_sheet"] is True and p["metadata"]["generation"] == 2
 
 
+def test_status_writes_own_only_status_fields(c):
+    c.admin.create("userbootstraps", {"apiVersion": "bacchus.io/v1", "kind": "UserBootstrap",
+                                      "metadata": {"name": "stown"}, "spec": {"kube_username": "stown"}},
+                   field_manager="creator")
+    c.admin.merge_patch("userbootstraps", "stown", {"status": {"synchronized_with_sheet": True, "note": "x"}},
+                        sub="status", field_manager="st-mgr")
+    o = c.admin.merge_patch("userbootstraps", "stown", {"status": {"note": None}}, sub="status",
+                            field_manager="st-mgr2")
+    by = {(m["manager"], m.get("subresource", "")): m for m in o["metadata"]["managedFields"]}
+    assert by[("creator", "")]["fieldsV1"] == {"f:spec": {"f:kube_username": {}}}
+    st = by[("st-mgr", "status")]
+    assert st["operation"] == "Update" and st["fieldsV1"] == {"f:status": {"f:synchronized_with_sheet": {}}}
+    # removing a status leaf drops it from its owner; a write that changes nothing owns nothing
+    assert ("st-mgr2", "status") not in by
+
+
 def test_namespaced_create_requires_namespace(c):
     with pytest.raises(ApiError) as e:
         c.admin.create("configmaps", {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "x"}},
