@@ -27,13 +27,7 @@ int main(int argc, char** argv) {
   try {
     cfg = gpu::NodeAgentConfig::from_env(EnvConfig("CONF_"));
     metrics::configure_debug(EnvConfig("CONF_"));  // /debug/samples: off unless CONF_DEBUG_ENDPOINTS
-    {
-      EnvConfig env("CONF_");
-      kube::Watcher::Defaults wd;
-      wd.page_size = static_cast<int64_t>(env.u64_or("list_page_size", 500));
-      wd.streaming_lists = env.boolean_or("streaming_lists", false);
-      kube::Watcher::set_defaults(wd);
-    }
+    kube::Watcher::configure_from_env(EnvConfig("CONF_"));  // list paging, watch idle deadline, TCP keepalive
   } catch (const std::exception& e) {
     std::fprintf(stderr, "Error: %s\n", e.what());
     return 1;

@@ -209,6 +209,7 @@ ssize_t Reader::fill(int timeout_ms) {
   }
   char tmp[16384];
   ssize_t r = s_.read_some(tmp, sizeof(tmp), timeout_ms);
+  last_ = r;
   if (r > 0) {
     buf_.append(tmp, static_cast<size_t>(r));
     consumed_any_ = true;
@@ -839,8 +840,50 @@ void Server::stop(std::chrono::milliseconds grace) {
   started_ = false;
 }
 
+namespace {
+std::mutex g_ready_mu;
+std::vector<std::pair<std::string, ReadinessCheck>> g_ready_checks;
+}  // namespace
+
+void add_readiness_check(const std::string& name, ReadinessCheck check) {
+  std::lock_guard<std::mutex> lk(g_ready_mu);
+  for (auto& [n, c] : g_ready_checks) {
+    if (n == name) {
+      c = std::move(check);
+      return;
+    }
+  }
+  g_ready_checks.emplace_back(name, std::move(check));
+}
+
+bool readiness(std::string* report) {
+  std::vector<std::pair<std::string, ReadinessCheck>> checks;
+  {
+    std::lock_guard<std::mutex> lk(g_ready_mu);
+    checks = g_ready_checks;
+  }
+  bool ok = true;
+  std::string out;
+  for (const auto& [name, check] : checks) {
+    std::string why;
+    const bool pass = check(&why);
+    ok = ok && pass;
+    out += std::string(pass ? "[+]" : "[-]") + name + (pass ? " ok" : " failed: " + why) + "\n";
+  }
+  if (report) *report = out + (ok ? "readyz check passed\n" : "readyz check failed\n");
+  return ok;
+}
+
 void add_standard_routes(Server& s) {
+  // /health stays the reference's unconditional "pong" (liveness; controller.rs:256,
+  // admission.rs:151); /readyz reports the registered readiness checks, in the
+  // kube-apiserver's /readyz text format.
   s.handle("GET", "/health", [](Request&, ResponseWriter& w) { w.send(200, "pong"); });
+  s.handle("GET", "/readyz", [](Request&, ResponseWriter& w) {
+    std::string report;
+    const bool ok = readiness(&report);
+    w.send(ok ? 200 : 503, report);
+  });
   s.handle("GET", "/metrics", [](Request&, ResponseWriter& w) {
     w.send(200, metrics::Registry::global().render(), "text/plain; version=0.0.4");
   });
@@ -1031,8 +1074,19 @@ Response Client::request(const std::string& method, const std::string& path, con
     Reader r(*s);
     std::string line;
     if (!r.read_line(line, to)) {
+      if (r.timed_out()) {
+        // No answer within the timeout: the path to the server may be dead (a wedged proxy,
+        // a crashed host behind a stale NAT entry), and every pooled connection with it.
+        // Drop them so the next request dials afresh; the request itself is not retried
+        // (the server may have acted on it, and a retry would double the wait).
+        close_idle();
+        static auto& timeouts = metrics::Registry::global().counter(
+            "bgc_http_client_timeouts_total", "Client requests that got no response within their timeout");
+        timeouts.inc();
+        throw HttpError("timeout (" + std::to_string(to) + " ms) waiting for the response: " + method + " " + path);
+      }
       if (reused && !r.consumed_any()) continue;
-      throw HttpError("no response (timeout or connection closed): " + method + " " + path);
+      throw HttpError("no response (connection closed): " + method + " " + path);
     }
     Response resp;
     if (line.size() < 12 || line.compare(0, 5, "HTTP/") != 0) throw HttpError("malformed status line: " + line);
@@ -1083,6 +1137,7 @@ std::unique_ptr<StreamingResponse> Client::stream(const std::string& method, con
     sr->remaining_ = static_cast<int64_t>(std::stoll(*cl));
   }
   sr->stream_ = std::move(s);
+  sr->last_data_ns_ = metrics::now_ns();
   return sr;
 }
 
@@ -1113,8 +1168,10 @@ bool StreamingResponse::pull(const CancelToken* cancel, int poll_ms) {
             }
           }
         }
+        if (idle_expired()) return false;
         continue;  // timeout: re-check cancel
       }
+      last_data_ns_ = metrics::now_ns();
       size_t n = 0;
       size_t semi = line.find(';');
       std::string hex = line.substr(0, semi);
@@ -1140,10 +1197,12 @@ bool StreamingResponse::pull(const CancelToken* cancel, int poll_ms) {
             return false;
           }
         }
+        if (idle_expired()) return false;
       }
       pending_ += data;
       std::string crlf;
       reader_->read_line(crlf, 10000);
+      last_data_ns_ = metrics::now_ns();
       return true;
     }
     if (remaining_ == 0) {
@@ -1152,7 +1211,10 @@ bool StreamingResponse::pull(const CancelToken* cancel, int poll_ms) {
     }
     std::string data;
     ssize_t r = reader_->read_available(data, poll_ms);
-    if (r == -2) continue;
+    if (r == -2) {
+      if (idle_expired()) return false;
+      continue;
+    }
     if (r <= 0) {
       done_ = true;
       return false;
@@ -1162,9 +1224,20 @@ bool StreamingResponse::pull(const CancelToken* cancel, int poll_ms) {
       remaining_ -= static_cast<int64_t>(data.size());
     }
     pending_ += data;
+    last_data_ns_ = metrics::now_ns();
     return true;
   }
   return false;
+}
+
+bool StreamingResponse::idle_expired() {
+  if (idle_ms_ <= 0) return false;
+  const int64_t now = metrics::now_ns();
+  if (last_data_ns_ == 0) last_data_ns_ = now;
+  if (now - last_data_ns_ < static_cast<int64_t>(idle_ms_) * 1000000) return false;
+  idle_timed_out_ = true;
+  done_ = true;
+  return true;
 }
 
 bool StreamingResponse::next_line(std::string& line, const CancelToken* cancel, int poll_ms) {

@@ -90,6 +90,8 @@ class Reader {
   ssize_t read_available(std::string& out, int timeout_ms);
   bool buffered() const { return pos_ < buf_.size() || s_.has_buffered(); }
   bool consumed_any() const { return consumed_any_; }
+  // The last read from the socket waited out its timeout (as opposed to EOF or an error).
+  bool timed_out() const { return last_ == -2; }
 
  private:
   ssize_t fill(int timeout_ms);
@@ -97,6 +99,7 @@ class Reader {
   std::string buf_;
   size_t pos_ = 0;
   bool consumed_any_ = false;
+  ssize_t last_ = 1;
 };
 
 // ---------------------------------------------------------------------------
@@ -201,7 +204,16 @@ class Server {
   std::atomic<uint64_t> h2_inline_{0};
 };
 
-// Attaches `/health` (-> "pong"), `/metrics` and, only when metrics::debug_endpoints_enabled()
+// Process-wide readiness checks served on /readyz: each returns false (with a reason in
+// *why) while its subsystem cannot do its job, e.g. a watch that has gone silent
+// (kube::Watcher).  Registering a name twice replaces the check.
+using ReadinessCheck = std::function<bool(std::string* why)>;
+void add_readiness_check(const std::string& name, ReadinessCheck check);
+// Runs every check; *report gets one "[+]name ok" / "[-]name failed: why" line per check.
+bool readiness(std::string* report = nullptr);
+
+// Attaches `/health` (-> "pong"), `/readyz` (200 when every readiness check passes, 503
+// otherwise), `/metrics` and, only when metrics::debug_endpoints_enabled()
 // (CONF_DEBUG_ENDPOINTS=true), GET/DELETE `/debug/samples/<name>`.
 void add_standard_routes(Server& s);
 
@@ -250,17 +262,27 @@ class StreamingResponse {
   // Reads the whole remaining body (non-2xx error bodies).
   std::string read_all(int timeout_ms = 10000);
   void close();
+  // Idle deadline: no body byte for `ms` ends the stream (next_line returns false and
+  // idle_timed_out() turns true), so a peer or path that silently stops sending cannot hold
+  // the reader forever.  0 (the default) = wait indefinitely.
+  void set_idle_timeout(int ms) { idle_ms_ = ms; }
+  bool idle_timed_out() const { return idle_timed_out_; }
   ~StreamingResponse();
 
  private:
   friend class Client;
   bool pull(const CancelToken* cancel, int poll_ms);
+  // true (and the stream ends) once the idle deadline has passed
+  bool idle_expired();
   std::unique_ptr<net::Stream> stream_;
   std::unique_ptr<Reader> reader_;
   bool chunked_ = false;
   int64_t remaining_ = -1;  // content-length mode
   bool done_ = false;
   std::string pending_;
+  int idle_ms_ = 0;
+  int64_t last_data_ns_ = 0;
+  bool idle_timed_out_ = false;
 };
 
 class Client {

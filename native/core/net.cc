@@ -451,6 +451,38 @@ void TlsStream::shutdown() { ::shutdown(fd_, SHUT_RDWR); }
 
 // ---------------------------------------------------------------------------
 
+namespace {
+std::mutex g_keepalive_mu;
+TcpKeepalive g_keepalive;
+}  // namespace
+
+void set_tcp_keepalive(TcpKeepalive k) {
+  std::lock_guard<std::mutex> lk(g_keepalive_mu);
+  g_keepalive = k;
+}
+
+TcpKeepalive tcp_keepalive() {
+  std::lock_guard<std::mutex> lk(g_keepalive_mu);
+  return g_keepalive;
+}
+
+bool apply_tcp_keepalive(int fd, const TcpKeepalive& k) {
+  bool ok = true;
+  if (k.idle_s > 0) {
+    int one = 1;
+    ok &= setsockopt(fd, SOL_SOCKET, SO_KEEPALIVE, &one, sizeof(one)) == 0;
+    ok &= setsockopt(fd, IPPROTO_TCP, TCP_KEEPIDLE, &k.idle_s, sizeof(k.idle_s)) == 0;
+    const int intvl = std::max(1, k.interval_s), cnt = std::max(1, k.count);
+    ok &= setsockopt(fd, IPPROTO_TCP, TCP_KEEPINTVL, &intvl, sizeof(intvl)) == 0;
+    ok &= setsockopt(fd, IPPROTO_TCP, TCP_KEEPCNT, &cnt, sizeof(cnt)) == 0;
+  }
+  if (k.user_timeout_ms > 0) {
+    const unsigned int ut = static_cast<unsigned int>(k.user_timeout_ms);
+    ok &= setsockopt(fd, IPPROTO_TCP, TCP_USER_TIMEOUT, &ut, sizeof(ut)) == 0;
+  }
+  return ok;
+}
+
 int connect_tcp(const std::string& host_in, uint16_t port, int timeout_ms) {
   std::string host = host_in;
   if (host.size() > 2 && host.front() == '[' && host.back() == ']') host = host.substr(1, host.size() - 2);
@@ -490,6 +522,7 @@ int connect_tcp(const std::string& host_in, uint16_t port, int timeout_ms) {
     }
     fcntl(fd, F_SETFL, flags);
     set_nodelay(fd);
+    apply_tcp_keepalive(fd, tcp_keepalive());
     freeaddrinfo(res);
     return fd;
   }

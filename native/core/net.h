@@ -121,7 +121,27 @@ class TlsStream : public Stream {
   std::mutex write_mu_;
 };
 
-// Resolves and connects (IPv4/IPv6); throws NetError.
+// TCP liveness of outgoing connections (connect_tcp): kernel keepalive probes after
+// `idle_s` without traffic, every `interval_s`, `count` unanswered probes closing the
+// socket; and TCP_USER_TIMEOUT, the longest written data may stay unacknowledged before
+// the kernel drops the connection.  A peer host that crashes or a NAT/conntrack entry that
+// expires then fails the socket instead of leaving it open forever.  (A path that still
+// answers probes but forwards nothing, e.g. a wedged proxy, is caught one level up by the
+// watch idle deadline, kube::Watcher::Defaults::idle_timeout_ms.)  Go's net.Dialer under
+// client-go starts probing after 15-30 s; these defaults are in that range.  idle_s = 0
+// disables keepalive; user_timeout_ms = 0 keeps the kernel default.
+struct TcpKeepalive {
+  int idle_s = 30;
+  int interval_s = 10;
+  int count = 3;
+  int user_timeout_ms = 60000;
+};
+void set_tcp_keepalive(TcpKeepalive k);  // process-wide, for connections opened afterwards
+TcpKeepalive tcp_keepalive();
+// Applies `k` to a connected socket (false if the kernel refused an option).
+bool apply_tcp_keepalive(int fd, const TcpKeepalive& k);
+
+// Resolves and connects (IPv4/IPv6) with the process's TcpKeepalive; throws NetError.
 int connect_tcp(const std::string& host, uint16_t port, int timeout_ms);
 // Listens; port 0 picks an ephemeral port (returned through bound_port).
 int listen_tcp(const std::string& addr, uint16_t port, int backlog, uint16_t* bound_port);

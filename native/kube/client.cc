@@ -602,6 +602,10 @@ Value KubeClient::remove(const ResourceType& rt, const std::string& ns, const st
   return call("DELETE", rt.object_path(ns, name), opts.dump());
 }
 
+void KubeClient::reset_connections() {
+  if (auto h = http()) h->close_idle();
+}
+
 std::unique_ptr<http::StreamingResponse> KubeClient::watch(const ResourceType& rt, const std::string& ns,
                                                            const WatchOptions& o) {
   std::string path = with_params(rt.collection_path(ns), {{"watch", "1"},

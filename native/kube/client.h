@@ -164,6 +164,8 @@ class KubeClient {
                      const std::string& content_type = "application/json", const std::string& accept = "");
   // A snapshot: an exec plugin's refresh may replace the client certificate at any time.
   KubeConfig config() const;
+  // Drops every pooled idle connection (a watch found the path to the apiserver dead).
+  void reset_connections();
   uint64_t tls_rebuilds() const { return tls_rebuilds_.load(); }
   uint64_t throttled() const { return throttled_.load(); }
   uint64_t credential_refreshes() const { return credential_refreshes_.load(); }

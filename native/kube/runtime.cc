@@ -2,8 +2,10 @@
 
 #include <algorithm>
 
+#include "core/http.h"
 #include "core/log.h"
 #include "core/metrics.h"
+#include "core/net.h"
 
 namespace bgc::kube {
 
@@ -19,6 +21,70 @@ std::string meta_rv(const Value& obj) { return obj.get("metadata").get_string("r
 namespace {
 std::mutex g_watch_defaults_mu;
 Watcher::Defaults g_watch_defaults;
+
+// Liveness of the running watchers, read by the "watches" readiness check.
+struct WatchSlot {
+  std::string resource;
+  int64_t deadline_ms = 0;
+  std::atomic<int64_t> last_ns{0};  // last event, bookmark, list or (re)started stream
+  std::atomic<bool> synced{false};  // the initial list has been delivered
+  // Gap between the last two BOOKMARKs of one stream: the server's heartbeat, once seen
+  // (a real apiserver sends one about every minute, kube-lite every --bookmark-ms).
+  std::atomic<int64_t> heartbeat_ns{0};
+};
+
+// How long a watch may be silent before it counts as stale for readiness: three missed
+// heartbeats once the server's bookmark cadence is known (so a stall shows on /readyz well
+// before the idle deadline reconnects it), the idle deadline otherwise.
+int64_t stale_after_ms(const WatchSlot& s) {
+  const int64_t hb_ms = s.heartbeat_ns.load() / 1000000;
+  if (hb_ms <= 0) return s.deadline_ms;
+  return std::min(s.deadline_ms, std::max<int64_t>(3 * hb_ms, 2000));
+}
+std::mutex g_slots_mu;
+std::vector<std::shared_ptr<WatchSlot>> g_slots;
+
+bool watches_ready(std::string* why) {
+  std::vector<std::shared_ptr<WatchSlot>> slots;
+  {
+    std::lock_guard<std::mutex> lk(g_slots_mu);
+    slots = g_slots;
+  }
+  const int64_t now = metrics::now_ns();
+  bool ok = true;
+  for (const auto& s : slots) {
+    std::string problem;
+    const int64_t age_ms = (now - s->last_ns.load()) / 1000000;
+    if (!s->synced.load()) {
+      problem = s->resource + ": initial list not complete";
+    } else if (s->deadline_ms > 0 && age_ms > stale_after_ms(*s)) {
+      problem = s->resource + ": no event or bookmark for " + std::to_string(age_ms) + " ms (stale after " +
+                std::to_string(stale_after_ms(*s)) + " ms)";
+    }
+    if (problem.empty()) continue;
+    if (why) *why += (ok ? "" : "; ") + problem;
+    ok = false;
+  }
+  return ok;
+}
+
+// Registers a running watcher's slot (and, once per process, the readiness check).
+std::shared_ptr<WatchSlot> open_slot(const std::string& resource, int64_t deadline_ms) {
+  static std::once_flag registered;
+  std::call_once(registered, [] { http::add_readiness_check("watches", watches_ready); });
+  auto s = std::make_shared<WatchSlot>();
+  s->resource = resource;
+  s->deadline_ms = deadline_ms;
+  s->last_ns = metrics::now_ns();
+  std::lock_guard<std::mutex> lk(g_slots_mu);
+  g_slots.push_back(s);
+  return s;
+}
+
+void close_slot(const std::shared_ptr<WatchSlot>& s) {
+  std::lock_guard<std::mutex> lk(g_slots_mu);
+  g_slots.erase(std::remove(g_slots.begin(), g_slots.end(), s), g_slots.end());
+}
 }  // namespace
 
 void Watcher::set_defaults(Defaults d) {
@@ -31,6 +97,18 @@ Watcher::Defaults Watcher::defaults() {
   return g_watch_defaults;
 }
 
+void Watcher::configure_from_env(const EnvConfig& env) {
+  Defaults wd;
+  wd.page_size = static_cast<int64_t>(env.u64_or("list_page_size", 500));
+  wd.streaming_lists = env.boolean_or("streaming_lists", false);
+  wd.idle_timeout_ms = static_cast<int64_t>(env.u64_or("watch_idle_timeout_secs", 295)) * 1000;
+  set_defaults(wd);
+  net::TcpKeepalive k;
+  k.idle_s = static_cast<int>(env.u64_or("tcp_keepalive_secs", static_cast<uint64_t>(k.idle_s)));
+  k.user_timeout_ms = static_cast<int>(env.u64_or("tcp_user_timeout_secs", 60)) * 1000;
+  net::set_tcp_keepalive(k);
+}
+
 Watcher::Watcher(KubeClient& client, ResourceType rt, std::string ns, std::string label_selector,
                  std::string field_selector)
     : client_(client),
@@ -41,6 +119,7 @@ Watcher::Watcher(KubeClient& client, ResourceType rt, std::string ns, std::strin
   const Defaults d = defaults();
   page_size_ = d.page_size;
   streaming_ = d.streaming_lists;
+  idle_timeout_ms_ = d.idle_timeout_ms;
 }
 
 ObjPtr Watcher::typed(Value obj) const {
@@ -103,6 +182,16 @@ void Watcher::run(CancelToken& stop, const std::function<void(const WatchEvent&)
   const auto max_backoff = std::chrono::milliseconds(30000);
   auto& errors = metrics::Registry::global().counter("bgc_watch_errors_total", "Watch stream failures",
                                                      {{"resource", rt_.plural}});
+  auto& idle_expired = metrics::Registry::global().counter(
+      "bgc_watch_idle_timeouts_total", "Watch streams closed after their idle deadline passed with no byte received",
+      {{"resource", rt_.plural}});
+  const std::shared_ptr<WatchSlot> slot = open_slot(rt_.plural + (selector_.empty() ? "" : "{" + selector_ + "}"),
+                                                    idle_timeout_ms_);
+  struct SlotGuard {
+    std::shared_ptr<WatchSlot> s;
+    ~SlotGuard() { close_slot(s); }
+  } slot_guard{slot};
+  auto alive = [&] { slot->last_ns.store(metrics::now_ns(), std::memory_order_relaxed); };
   while (!stop.cancelled()) {
     // Streaming list: the initial state arrives on this watch; objects collect here until
     // the initial-events-end bookmark.
@@ -115,11 +204,20 @@ void Watcher::run(CancelToken& stop, const std::function<void(const WatchEvent&)
         on_event(ev);
         need_list = false;
         relists_.fetch_add(1);
+        alive();
+        slot->synced.store(true);
       }
       WatchOptions wo;
       wo.label_selector = selector_;
       wo.field_selector = field_selector_;
       wo.metadata_only = metadata_only_;
+      if (idle_timeout_ms_ > 0) {
+        // the server ends a quiet healthy watch before the client's deadline would (295 s ->
+        // the usual 290 s; a short test deadline keeps most of its length)
+        const int64_t idle_s = idle_timeout_ms_ / 1000;
+        const int64_t margin = std::max<int64_t>(1, std::min<int64_t>(5, idle_s / 10));
+        wo.timeout_seconds = static_cast<int>(std::clamp<int64_t>(idle_s - margin, 1, wo.timeout_seconds));
+      }
       if (need_list) {  // streaming
         wo.send_initial_events = true;
         initial_phase = true;
@@ -139,8 +237,12 @@ void Watcher::run(CancelToken& stop, const std::function<void(const WatchEvent&)
         throw;
       }
       backoff = std::chrono::milliseconds(800);
+      if (idle_timeout_ms_ > 0) stream->set_idle_timeout(static_cast<int>(idle_timeout_ms_));
+      alive();
+      int64_t last_bookmark_ns = 0;
       std::string line;
       while (stream->next_line(line, &stop, 500)) {
+        alive();
         if (line.empty()) continue;
         // Events the consumer does not want are dropped before JSON parsing; ERROR and
         // BOOKMARK lines always go through (they drive relists and resumption).  During
@@ -167,6 +269,9 @@ void Watcher::run(CancelToken& stop, const std::function<void(const WatchEvent&)
         std::string new_rv = meta_rv(obj);
         if (!new_rv.empty()) rv = new_rv;
         if (type == "BOOKMARK") {
+          const int64_t now = metrics::now_ns();
+          if (last_bookmark_ns) slot->heartbeat_ns.store(now - last_bookmark_ns, std::memory_order_relaxed);
+          last_bookmark_ns = now;
           if (initial_phase &&
               obj.get("metadata").get("annotations").get_string("k8s.io/initial-events-end") == "true") {
             WatchEvent we{WatchEvent::Type::Restarted, nullptr, std::move(initial)};
@@ -175,6 +280,7 @@ void Watcher::run(CancelToken& stop, const std::function<void(const WatchEvent&)
             need_list = false;
             on_event(we);
             relists_.fetch_add(1);
+            slot->synced.store(true);
           }
           continue;
         }
@@ -190,6 +296,16 @@ void Watcher::run(CancelToken& stop, const std::function<void(const WatchEvent&)
         on_event(we);
       }
       stream->close();
+      if (stream->idle_timed_out() && !stop.cancelled()) {
+        // Nothing arrived for the whole deadline, not even a bookmark: the connection (or the
+        // path to the apiserver) is presumed dead.  Pooled request connections share that
+        // path, so they go too; the watch resumes from rv on a fresh connection.
+        idle_timeouts_.fetch_add(1);
+        idle_expired.inc();
+        LOG_WARN("kube::watcher") << rt_.plural << ": no event or bookmark for " << idle_timeout_ms_ / 1000
+                                  << " s; reconnecting";
+        client_.reset_connections();
+      }
       if (!stop.cancelled()) reconnects_.fetch_add(1);
     } catch (const ApiError& e) {
       errors.inc();

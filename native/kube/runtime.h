@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "core/cancel.h"
+#include "core/env_config.h"
 #include "core/json.h"
 #include "kube/client.h"
 #include "kube/resource.h"
@@ -57,16 +58,36 @@ std::string meta_rv(const json::Value& obj);
 // initial ADDED events end at a BOOKMARK annotated k8s.io/initial-events-end (the
 // apiserver never materialises the whole list).  A server that rejects streaming lists
 // (4xx) makes the watcher fall back to LIST for good.
+//
+// Liveness: a watch stream that delivers no byte (no event, no BOOKMARK) for
+// idle_timeout_ms is closed and resumed from the last resourceVersion on a new connection,
+// and the client's pooled connections are dropped with it (kube-client puts a 295 s read
+// timeout on its watch connections, hyper-timeout in the reference's Cargo.lock:982-997;
+// kube-runtime's watcher then restarts the stream).  The server-side timeoutSeconds is kept
+// below that deadline, so a healthy quiet watch ends cleanly first.  Every running watcher
+// also feeds the "watches" readiness check (/readyz): it fails while any watcher has not
+// completed its initial list, or has seen no event, bookmark or (re)started stream for
+// three of the server's bookmark intervals (once two bookmarks have shown the cadence;
+// at least 2 s) or, before that, for its idle deadline.  So a silent stall reads as
+// not-ready on /readyz before the deadline reconnects the watch.
 class Watcher {
  public:
   struct Defaults {
     int64_t page_size = 500;   // 0 = unpaginated LIST
     bool streaming_lists = false;
+    int64_t idle_timeout_ms = 295000;  // 0 = no client-side deadline (and no readiness check)
   };
   // Process-wide defaults (each binary sets them from CONF_LIST_PAGE_SIZE /
-  // CONF_STREAMING_LISTS before starting its watchers).
+  // CONF_STREAMING_LISTS / CONF_WATCH_IDLE_TIMEOUT_SECS before starting its watchers;
+  // configure_from_env below).
   static void set_defaults(Defaults d);
   static Defaults defaults();
+  // CONF_LIST_PAGE_SIZE, CONF_STREAMING_LISTS, CONF_WATCH_IDLE_TIMEOUT_SECS (default 295)
+  // and the TCP keepalive of API connections, CONF_TCP_KEEPALIVE_SECS (30, 0 = off) and
+  // CONF_TCP_USER_TIMEOUT_SECS (60, 0 = kernel default).  Throws ConfigError.
+  static void configure_from_env(const EnvConfig& env);
+  void set_idle_timeout_ms(int64_t ms) { idle_timeout_ms_ = ms; }
+  uint64_t idle_timeouts() const { return idle_timeouts_.load(); }
 
   Watcher(KubeClient& client, ResourceType rt, std::string ns = "", std::string label_selector = "",
           std::string field_selector = "");
@@ -97,6 +118,8 @@ class Watcher {
   ObjPtr typed(json::Value obj) const;
   int64_t page_size_;
   bool streaming_;
+  int64_t idle_timeout_ms_;
+  std::atomic<uint64_t> idle_timeouts_{0};
   bool metadata_only_ = false;
   std::atomic<uint64_t> list_pages_{0};
   KubeClient& client_;

@@ -263,9 +263,15 @@ def test_values_and_name_parity_with_reference():
             o = o[k]
         return o
 
+    # deliberate value changes: readiness of the watching components is /readyz (watch
+    # liveness); the reference's /health stays their liveness probe
+    changed = {("controller", "readinessProbe", "httpGet", "path"): "/readyz",
+               ("synchronizer", "readinessProbe", "httpGet", "path"): "/readyz"}
     for p in paths(ref):
         get(ours, p)  # every reference key exists
-        if p[-1] != "repository":
+        if p in changed:
+            assert get(ref, p) == "/health" and get(ours, p) == changed[p], ".".join(p)
+        elif p[-1] != "repository":
             assert get(ours, p) == get(ref, p), ".".join(p)
     with open(os.path.join(REF_CHART, "Chart.yaml")) as f:
         ref_chart = yaml.safe_load(f)
@@ -311,7 +317,7 @@ def test_every_node_agent_config_key_reaches_the_binary():
     ds = by_kind(render(), "DaemonSet")["bgc-bacchus-gpu-node-agent"]
     env = {e["name"]: e.get("value") for e in ds["spec"]["template"]["spec"]["containers"][0]["env"]}
     src = ""
-    for fn in ("native/gpu/node_agent.cc", "native/bin/node_agent.cc"):
+    for fn in ("native/gpu/node_agent.cc", "native/bin/node_agent.cc", "native/kube/runtime.cc"):
         with open(os.path.join(REPO_ROOT, fn)) as f:
             src += f.read()
     for k, v in keys.items():
