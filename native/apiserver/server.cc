@@ -312,6 +312,12 @@ std::string partial_metadata_line(const std::string& line) {
   return out;
 }
 
+// How one watch sees one event (EventRec::line_as).  A label-selector watch sees an update
+// that moves the object into its selector as ADDED and one that moves it out as DELETED
+// (carrying the previous object at the event's resourceVersion), as the kube-apiserver's
+// watch cache does (cacheWatcher.convertToWatchEvent); every other event as it is.
+enum class View : uint8_t { AsIs, Added, Deleted };
+
 struct EventRec {
   uint64_t rv;
   std::string type_key;
@@ -320,15 +326,71 @@ struct EventRec {
   // object: the watch cache must not pin every old version's full tree in memory.
   std::shared_ptr<const Value> meta;
   std::shared_ptr<const std::string> line;  // {"type":..,"object":..}\n
+  // Updates that changed the object's labels (selector transitions possible): the previous
+  // version's filter view and its committed event line.  Null otherwise.
+  std::shared_ptr<const Value> prev_meta;
+  std::shared_ptr<const std::string> prev_line;
   // The PartialObjectMetadata form, built once on first use by a metadata-only watch.
   const std::string& metadata_line() const {
     std::call_once(meta_once_, [this] { meta_line_ = partial_metadata_line(*line); });
     return meta_line_;
   }
+  // The line a watch with this view receives (transition forms built once, on first use).
+  const std::string& line_as(View v, bool meta_only) const {
+    if (v == View::AsIs) return meta_only ? metadata_line() : *line;
+    Transition& t = v == View::Added ? added_ : deleted_;
+    std::call_once(t.once, [&] {
+      t.full = v == View::Added ? retyped_line(*line, "ADDED") : deleted_from_prev();
+      t.meta = partial_metadata_line(t.full);
+    });
+    return meta_only ? t.meta : t.full;
+  }
 
  private:
+  struct Transition {
+    std::once_flag once;
+    std::string full, meta;
+  };
+  // {"type":T,...} -> {"type":<type>,...}
+  static std::string retyped_line(const std::string& l, const char* type) {
+    const std::string_view t = json::raw_member(l, "type");
+    std::string out;
+    if (t.empty()) return l;
+    out.reserve(l.size() + 8);
+    out.append(l, 0, static_cast<size_t>(t.data() - l.data()));
+    out += '"';
+    out += type;
+    out += '"';
+    out.append(t.data() + t.size(), l.data() + l.size());
+    return out;
+  }
+  // DELETED with the previous object, its resourceVersion replaced by this event's
+  std::string deleted_from_prev() const {
+    std::string_view prev(*prev_line);
+    while (!prev.empty() && (prev.back() == '\n' || prev.back() == '\r')) prev.remove_suffix(1);
+    const std::string_view obj = json::raw_member(prev, "object");
+    const std::string_view old_rv = json::raw_member(json::raw_member(obj, "metadata"), "resourceVersion");
+    const std::string_view new_rv =
+        json::raw_member(json::raw_member(json::raw_member(*line, "object"), "metadata"), "resourceVersion");
+    std::string out = "{\"type\":\"DELETED\",\"object\":";
+    if (old_rv.empty()) {
+      out.append(obj.data(), obj.size());
+    } else {
+      out.append(obj.data(), static_cast<size_t>(old_rv.data() - obj.data()));
+      out.append(new_rv.data(), new_rv.size());
+      out.append(old_rv.data() + old_rv.size(), obj.data() + obj.size());
+    }
+    out += "}\n";
+    return out;
+  }
   mutable std::once_flag meta_once_;
   mutable std::string meta_line_;
+  mutable Transition added_, deleted_;
+};
+
+struct QueuedEvent {
+  std::shared_ptr<const EventRec> e;
+  View view = View::AsIs;
 };
 
 // {"metadata":{"name":..,"labels":..}} of an object: the fields watch filters read.
@@ -348,7 +410,7 @@ struct WatchSub {
   // an event never contends with writers. Lock order: store mutex -> m.
   std::mutex m;
   std::condition_variable cv;
-  std::deque<std::shared_ptr<const EventRec>> q;
+  std::deque<QueuedEvent> q;
   bool closed = false;
   bool overflow = false;
 
@@ -571,6 +633,9 @@ struct FaultRule {
   int status = 0;
   int retry_after_s = -1;  // >= 0: send a Retry-After header (429 / 503 throttling)
   int delay_ms = 0;
+  // served as usual, then the response is held this long ("delay_response_ms"): the write
+  // is committed and its watch event delivered before the client has its answer
+  int hold_ms = 0;
   int remaining = -1;  // -1 = unlimited
   bool reset = false;  // drop the connection without a response
   std::string message;
@@ -931,15 +996,28 @@ struct ApiServer::Impl {
     for (const auto& w : st.watches) {
       if (!w->ns.empty() && w->ns != ns) continue;
       if (!w->fields.name_ok(name)) continue;
-      if (!w->sel.empty() && !selector_matches(w->sel, *rec->meta)) continue;
+      View view;
+      if (!view_for(w->sel, *rec, &view)) continue;
       {
         std::lock_guard<std::mutex> g(w->m);
         if (w->q.size() > 100000) w->overflow = true;
-        else w->q.push_back(rec);
+        else w->q.push_back({rec, view});
       }
       t_pending_wakeups.push_back(w);
     }
     return rec->line;
+  }
+
+  // Whether a watch with label selector `sel` receives `e`, and as what.
+  static bool view_for(const std::vector<Requirement>& sel, const EventRec& e, View* view) {
+    *view = View::AsIs;
+    if (sel.empty()) return true;
+    const bool now_in = selector_matches(sel, *e.meta);
+    if (!e.prev_meta) return now_in;
+    const bool was_in = selector_matches(sel, *e.prev_meta);
+    if (now_in && !was_in) *view = View::Added;
+    else if (!now_in && was_in) *view = View::Deleted;
+    return now_in || was_in;
   }
 
   // ---------------------------------------------------------------- webhooks
@@ -1410,6 +1488,24 @@ struct ApiServer::Impl {
         *dangling = !alive;
       }
     }
+    // An update that changes the labels may move the object into or out of a label-selector
+    // watch: the event remembers the previous version for those watches (view_for).
+    std::shared_ptr<EventRec> rec = pe->rec ? pe->rec : std::make_shared<EventRec>();
+    if (prev && opts.selector_transitions) {
+      std::shared_ptr<const Value> now_filter = pe->filter ? pe->filter : filter_view(obj);
+      std::shared_ptr<const Value> prev_filter = filter_view(*prev->obj);
+      if (prev_filter->get("metadata").get("labels") != now_filter->get("metadata").get("labels")) {
+        rec->prev_meta = std::move(prev_filter);
+        if (prev->line) {
+          rec->prev_line = prev->line;
+        } else {
+          std::string l = "{\"type\":\"MODIFIED\",\"object\":";
+          prev->obj->dump_to(l);
+          l += "}\n";
+          rec->prev_line = std::make_shared<const std::string>(std::move(l));
+        }
+      }
+    }
     uint64_t new_rv;
     std::string digits;
     std::shared_ptr<const std::string> line;
@@ -1429,7 +1525,7 @@ struct ApiServer::Impl {
         obj.dump_to(preline);
         preline += "}\n";
       }
-      line = emit_locked(ti, ns, new_rv, std::move(preline), pe->filter ? pe->filter : filter_view(obj), pe->rec);
+      line = emit_locked(ti, ns, new_rv, std::move(preline), pe->filter ? pe->filter : filter_view(obj), std::move(rec));
     }
     obj["metadata"]["resourceVersion"] = digits;
     auto ptr = std::make_shared<const Value>(std::move(obj));
@@ -2106,8 +2202,10 @@ struct ApiServer::Impl {
           if (e->type_key != sub.type_key) continue;
           if (!sub.ns.empty() && e->ns != sub.ns) continue;
           if (!sub.fields.name_ok(e->meta->get("metadata").get_string("name"))) continue;
-          if (!sub.sel.empty() && !selector_matches(sub.sel, *e->meta)) continue;
-          initial.push_back(meta_only ? std::make_shared<const std::string>(e->metadata_line()) : e->line);
+          View view;
+          if (!view_for(sub.sel, *e, &view)) continue;
+          if (view == View::AsIs && !meta_only) initial.push_back(e->line);
+          else initial.push_back(std::make_shared<const std::string>(e->line_as(view, meta_only)));
         }
       }
       if (!gone) {
@@ -2144,7 +2242,7 @@ struct ApiServer::Impl {
     auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(timeout_s);
     auto next_bookmark = std::chrono::steady_clock::now() + std::chrono::milliseconds(opts.bookmark_interval_ms);
     while (ok && !w.stopping()) {
-      std::vector<std::shared_ptr<const EventRec>> batch;
+      std::vector<QueuedEvent> batch;
       bool closed = false, overflow = false;
       {
         std::unique_lock<std::mutex> lk(sub.m);
@@ -2161,7 +2259,7 @@ struct ApiServer::Impl {
       }
       if (!batch.empty()) {
         std::string buf;
-        for (auto& e : batch) buf += meta_only ? e->metadata_line() : *e->line;
+        for (auto& q : batch) buf += q.e->line_as(q.view, meta_only);
         if (!w.write_chunk(buf)) break;
       }
       if (closed || overflow) break;
@@ -2171,7 +2269,7 @@ struct ApiServer::Impl {
         // Under the type's shared lock every event of this type with rv <= cur_rv is already
         // in sub.q; flush those before the bookmark so it never skips an undelivered event.
         uint64_t cur_rv;
-        std::vector<std::shared_ptr<const EventRec>> pending;
+        std::vector<QueuedEvent> pending;
         {
           SharedStoreLock lk(ts.seq, ts.seq_stats);  // every event of the type up to cur_rv is queued
           cur_rv = rv.load();
@@ -2181,7 +2279,7 @@ struct ApiServer::Impl {
         }
         if (!pending.empty()) {
           std::string buf;
-          for (auto& e : pending) buf += meta_only ? e->metadata_line() : *e->line;
+          for (auto& q : pending) buf += q.e->line_as(q.view, meta_only);
           if (!w.write_chunk(buf)) break;
         }
         Value bm = Value::object({{"type", "BOOKMARK"},
@@ -2237,7 +2335,40 @@ struct ApiServer::Impl {
   }
 
   // ---------------------------------------------------------------- faults
-  bool inject_fault(const http::Request& req, http::ResponseWriter& w) {
+  // Fault injection's response hold (FaultRule::hold_ms): every writer call is forwarded to
+  // the connection's writer, send() after waiting out the hold.  Not used for watches.
+  class HoldingWriter : public http::ResponseWriter {
+   public:
+    HoldingWriter(http::ResponseWriter& inner, int hold_ms)
+        : ResponseWriter(nullptr, inner.keep_alive(), never_stops()), inner_(inner), hold_ms_(hold_ms) {}
+    void send(int status, std::string_view body, const std::string& content_type,
+              const http::Headers* extra) override {
+      inner_.wait_stopping(std::chrono::milliseconds(hold_ms_));
+      inner_.send(status, body, content_type, extra);
+      sent_ = true;
+      status_ = status;
+    }
+    bool start_chunked(int status, const std::string& content_type) override {
+      sent_ = true;
+      status_ = status;
+      return inner_.start_chunked(status, content_type);
+    }
+    bool write_chunk(const std::string& data) override { return inner_.write_chunk(data); }
+    void end_chunked() override { inner_.end_chunked(); }
+    void abort() override { inner_.abort(); }
+    bool peer_closed() override { return inner_.peer_closed(); }
+    const char* protocol() const override { return inner_.protocol(); }
+
+   private:
+    static const CancelToken& never_stops() {
+      static const CancelToken t;
+      return t;
+    }
+    http::ResponseWriter& inner_;
+    int hold_ms_;
+  };
+
+  bool inject_fault(const http::Request& req, http::ResponseWriter& w, int* hold_ms) {
     FaultRule hit;
     bool found = false;
     {
@@ -2263,6 +2394,10 @@ struct ApiServer::Impl {
     if (hit.reset) {
       w.abort();
       return true;
+    }
+    if (hit.hold_ms > 0 && hit.status <= 0) {
+      *hold_ms = hit.hold_ms;
+      return false;
     }
     if (hit.status > 0) {
       std::string reason = hit.status == 409   ? "Conflict"
@@ -2291,6 +2426,7 @@ struct ApiServer::Impl {
         f.path = std::regex(f.path_src);
         f.status = r.get("status").is_int() ? static_cast<int>(r.get("status").as_int()) : 0;
         f.delay_ms = r.get("delay_ms").is_int() ? static_cast<int>(r.get("delay_ms").as_int()) : 0;
+        f.hold_ms = r.get("delay_response_ms").is_int() ? static_cast<int>(r.get("delay_response_ms").as_int()) : 0;
         f.remaining = r.get("count").is_int() ? static_cast<int>(r.get("count").as_int()) : -1;
         f.message = r.get_string("message");
         f.reset = r.get("reset").is_bool() && r.get("reset").as_bool();
@@ -2434,7 +2570,10 @@ struct ApiServer::Impl {
   std::mutex req_count_mu;
   std::map<std::string, uint64_t> req_counts;
 
-  void handle(http::Request& req, http::ResponseWriter& w) {
+  void handle(http::Request& req, http::ResponseWriter& w_conn) {
+    http::ResponseWriter* wp = &w_conn;  // the response hold's writer, when a fault asks for one
+    std::optional<HoldingWriter> holder;
+    http::ResponseWriter& w_count = w_conn;
     requests.fetch_add(1, std::memory_order_relaxed);
     std::string res_key = "-";
     struct Count {
@@ -2447,9 +2586,12 @@ struct ApiServer::Impl {
         std::lock_guard<std::mutex> g(im->req_count_mu);
         im->req_counts[k]++;
       }
-    } count{this, req, w, res_key};
+    } count{this, req, w_count, res_key};
     try {
-      if (inject_fault(req, w)) return;
+      int hold_ms = 0;
+      if (inject_fault(req, w_conn, &hold_ms)) return;
+      if (hold_ms > 0 && req.method != "GET") wp = &holder.emplace(w_conn, hold_ms);
+      http::ResponseWriter& w = *wp;
       UserInfo user = authenticate(req);
       if (req.path == "/apis/authentication.k8s.io/v1/selfsubjectreviews" && req.method == "POST") {
         // `kubectl auth whoami`: who the request authenticated as
@@ -2506,9 +2648,9 @@ struct ApiServer::Impl {
       else if (m == "DELETE") do_delete(p, req, user, w);
       else throw StatusError(405, "MethodNotAllowed", "method not allowed");
     } catch (const StatusError& e) {
-      if (!w.sent()) w.send_json(e.code, status_body(e.code, e.reason, e.what(), e.details).dump());
+      if (!wp->sent()) wp->send_json(e.code, status_body(e.code, e.reason, e.what(), e.details).dump());
     } catch (const std::exception& e) {
-      if (!w.sent()) w.send_json(500, status_body(500, "InternalError", e.what()).dump());
+      if (!wp->sent()) wp->send_json(500, status_body(500, "InternalError", e.what()).dump());
     }
   }
 };

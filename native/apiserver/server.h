@@ -39,6 +39,10 @@ struct Options {
   size_t history_limit = 50000;  // watch-cache events kept per type for resume (k8s keeps ~100)
   int bookmark_interval_ms = 60000;
   bool validate_schema = true;
+  // Label-selector watches see an update that moves an object into their selector as ADDED
+  // and one that moves it out as DELETED, as on a real apiserver.  false (kube-lite
+  // --no-selector-transitions) drops such events instead: a lost-event scenario.
+  bool selector_transitions = true;
   int max_watch_seconds = 1800;
   // Watch write coalescing: after a wake-up with few events queued, wait this long for
   // more before writing (fewer wake-ups/syscalls per event at high event rates, at the

@@ -1,7 +1,10 @@
 #include "controller/reconcile.h"
 
+#include <algorithm>
 #include <cctype>
 #include <exception>
+#include <optional>
+#include <random>
 #include <iterator>
 #include <future>
 
@@ -23,6 +26,7 @@ Config Config::from_env(const EnvConfig& env) {
   c.child_delete_delay_ms = static_cast<int64_t>(env.u64_or("child_delete_delay_ms", 50));
   c.debounce_ms = static_cast<int64_t>(env.u64_or("debounce_ms", 0));
   c.requeue_secs = static_cast<int64_t>(env.u64_or("requeue_secs", 30));
+  c.resync_secs = static_cast<int64_t>(env.u64_or("resync_secs", 300));
   c.error_requeue_ms = static_cast<int64_t>(env.u64_or("error_requeue_ms", 3000));
   c.error_backoff_base_ms = static_cast<int64_t>(env.u64_or("error_backoff_base_ms", 0));
   c.label_children = env.boolean_or("label_children", true);
@@ -162,7 +166,8 @@ Reconciler::Reconciler(kube::KubeClient& client, kube::Controller& ctrl, Config 
     : client_(client), ctrl_(ctrl), cfg_(cfg), pool_(static_cast<size_t>(std::max(4, cfg.workers * 3))) {}
 
 Reconciler::Stats Reconciler::stats() const {
-  return {stats_applied_.load(std::memory_order_relaxed), stats_skipped_.load(std::memory_order_relaxed)};
+  return {stats_applied_.load(std::memory_order_relaxed), stats_skipped_.load(std::memory_order_relaxed),
+          stats_verified_.load(std::memory_order_relaxed), stats_repaired_.load(std::memory_order_relaxed)};
 }
 
 static std::string lower(std::string s) {
@@ -201,7 +206,9 @@ void Reconciler::forget(const kube::ResourceType& rt, const Value& child) {
   Shard& sh = shard(ns.empty() ? name : ns);
   {
     std::lock_guard<std::mutex> lk(sh.mu);
-    erase_applied_locked(sh, rt.plural + "/" + ns + "/" + name);
+    const std::string key = rt.plural + "/" + ns + "/" + name;
+    erase_applied_locked(sh, key);
+    if (auto a = sh.applying.find(key); a != sh.applying.end()) a->second = true;
     for (const auto& ref : child.get("metadata").get("ownerReferences").items()) {
       if (ref.get_string("kind") == types::UserBootstrap.kind) erase_owner_state_locked(sh, ref.get_string("name"));
     }
@@ -213,9 +220,12 @@ void Reconciler::forget_owner_locked(Shard& sh, const std::string& owner) {
   sh.failures.erase(owner);
   const std::string ns = lower(owner);
   erase_owner_state_locked(sh, owner);
-  erase_applied_locked(sh, types::Namespace.plural + "//" + ns);
-  for (const auto* rt : {&types::ResourceQuota, &types::Role, &types::RoleBinding})
-    erase_applied_locked(sh, rt->plural + "/" + ns + "/" + ns);
+  auto drop = [&](const std::string& key) {
+    erase_applied_locked(sh, key);
+    if (auto a = sh.applying.find(key); a != sh.applying.end()) a->second = true;
+  };
+  drop(types::Namespace.plural + "//" + ns);
+  for (const auto* rt : {&types::ResourceQuota, &types::Role, &types::RoleBinding}) drop(rt->plural + "/" + ns + "/" + ns);
 }
 
 void Reconciler::forget_owner(const std::string& owner) {
@@ -289,20 +299,124 @@ bool Reconciler::up_to_date(const DesiredChild& c, const std::string& body_hash)
 
 void Reconciler::apply_child(const DesiredChild& c, const std::string& body_hash, const std::string& body_json) {
   static auto& applied = metrics::Registry::global().counter("bgc_apply_total", "Server-side applies issued");
+  static auto& dropped = metrics::Registry::global().counter(
+      "bgc_apply_records_dropped_total", "Applies whose result was not recorded: the child was deleted while in flight");
   kube::Store* store = ctrl_.child_store(c.rt->plural);
+  const std::string key = child_key(c);
+  Shard& sh = shard(c.name);
+  {
+    std::lock_guard<std::mutex> lk(sh.mu);
+    sh.applying[key] = false;
+  }
+  // A watch event of this child can be processed at any point from here on (the apply's
+  // own ADDED, then a DELETED when someone removes it at once).  The cache state read now
+  // is what the "echo pending" rule of up_to_date compares against, so a forget() of the
+  // child before the result is recorded must void the record (Shard::applying).
+  struct Unmark {
+    Shard& sh;
+    const std::string& key;
+    bool armed = true;
+    ~Unmark() {
+      if (!armed) return;
+      std::lock_guard<std::mutex> lk(sh.mu);
+      sh.applying.erase(key);
+    }
+  } unmark{sh, key};
   const kube::ObjPtr before = store ? store->get(c.ns, c.name) : nullptr;
   std::string rv = client_.apply_rv(*c.rt, c.ns, c.name, body_json, kFieldManager, /*force=*/true);
   applied.inc();
+  if (after_apply_) after_apply_(c);
   {
-    Shard& sh = shard(c.name);
     std::lock_guard<std::mutex> lk(sh.mu);
-    auto [it, inserted] = sh.last_applied.try_emplace(child_key(c));
-    it->second = {body_hash, std::move(rv), before ? kube::meta_rv(*before) : std::string(), before != nullptr,
-                  std::chrono::steady_clock::now()};
-    if (inserted) applied_entries_.fetch_add(1, std::memory_order_relaxed);
+    unmark.armed = false;
+    auto a = sh.applying.find(key);
+    const bool forgotten = a != sh.applying.end() && a->second;
+    if (a != sh.applying.end()) sh.applying.erase(a);
+    if (forgotten) {
+      dropped.inc();  // the next reconcile (queued by that DELETED event) applies again
+    } else {
+      auto [it, inserted] = sh.last_applied.try_emplace(key);
+      it->second = {body_hash, std::move(rv), before ? kube::meta_rv(*before) : std::string(), before != nullptr,
+                    std::chrono::steady_clock::now()};
+      if (inserted) applied_entries_.fetch_add(1, std::memory_order_relaxed);
+    }
   }
   publish_cache_sizes();
   stats_applied_.fetch_add(1, std::memory_order_relaxed);
+}
+
+// SSA-shaped coverage: every member `want` sets is in `have` with a covered value.  Maps
+// may hold more (other managers' fields survive a forced apply); ownerReferences is keyed
+// by uid (each wanted reference must be present); other lists are atomic (same length,
+// element by element), as a forced apply replaces them.
+static bool covers(const Value& want, const Value& have, std::string_view key = {}) {
+  if (want.is_object()) {
+    if (!have.is_object()) return false;
+    const auto& keys = want.keys();
+    const auto& vals = want.values();
+    for (size_t i = 0; i < keys.size(); ++i) {
+      const Value* h = have.find(keys[i]);
+      if (!h || !covers(vals[i], *h, keys[i])) return false;
+    }
+    return true;
+  }
+  if (want.is_array()) {
+    if (!have.is_array()) return false;
+    const auto& w = want.items();
+    const auto& h = have.items();
+    if (key == "ownerReferences") {
+      for (const auto& x : w) {
+        if (std::none_of(h.begin(), h.end(), [&](const Value& y) { return covers(x, y); })) return false;
+      }
+      return true;
+    }
+    if (w.size() != h.size()) return false;
+    for (size_t i = 0; i < w.size(); ++i) {
+      if (!covers(w[i], h[i])) return false;
+    }
+    return true;
+  }
+  return want == have;
+}
+
+bool Reconciler::verified_in_sync(const DesiredChild& c, const std::string& body_hash) {
+  static auto& reg = metrics::Registry::global();
+  static auto& checked = reg.counter("bgc_resync_checks_total", "Children read back from the apiserver by a resync");
+  static auto& drifted = reg.counter("bgc_resync_repairs_total", "Children a resync found drifted or missing (re-applied)");
+  checked.inc();
+  stats_verified_.fetch_add(1, std::memory_order_relaxed);
+  std::optional<Value> live = client_.get_opt(*c.rt, c.ns, c.name);
+  if (live && covers(json::parse(c.body), *live)) {
+    const std::string rv = kube::meta_rv(*live);
+    Shard& sh = shard(c.name);
+    std::lock_guard<std::mutex> lk(sh.mu);
+    auto [it, inserted] = sh.last_applied.try_emplace(child_key(c));
+    it->second = {body_hash, rv, rv, true, std::chrono::steady_clock::now()};
+    if (inserted) applied_entries_.fetch_add(1, std::memory_order_relaxed);
+    return true;
+  }
+  drifted.inc();
+  stats_repaired_.fetch_add(1, std::memory_order_relaxed);
+  LOG_INFO("controller") << "resync: " << c.rt->kind << " " << (c.ns.empty() ? "" : c.ns + "/") << c.name
+                         << (live ? " drifted" : " missing") << "; re-applying";
+  return false;
+}
+
+bool Reconciler::resync_due(const std::string& owner_name) {
+  if (!cfg_.skip_unchanged || cfg_.resync_secs <= 0) return false;
+  Shard& sh = shard(lower(owner_name));
+  std::lock_guard<std::mutex> lk(sh.mu);
+  auto it = sh.ub_state.find(owner_name);
+  return it != sh.ub_state.end() && std::chrono::steady_clock::now() >= it->second.next_resync;
+}
+
+std::chrono::steady_clock::time_point Reconciler::next_resync_time() {
+  // spread over [0.75, 1] of the period: UserBootstraps reconciled together (a restart, a
+  // bulk import) do not all come due in the same second
+  thread_local std::minstd_rand rng{std::random_device{}()};
+  const int64_t period_ms = cfg_.resync_secs * 1000;
+  const int64_t ms = period_ms - static_cast<int64_t>(rng() % static_cast<uint64_t>(period_ms / 4 + 1));
+  return std::chrono::steady_clock::now() + std::chrono::milliseconds(ms);
 }
 
 kube::Action Reconciler::reconcile(const kube::ObjPtr& ub_ptr) {
@@ -330,7 +444,10 @@ kube::Action Reconciler::reconcile(const kube::ObjPtr& ub_ptr) {
   } timed;
   const Value& ub = *ub_ptr;
   const std::string owner_name = kube::meta_name(ub), owner_rv = kube::meta_rv(ub);
-  if (cfg_.skip_unchanged && fresh(owner_name, owner_rv)) {
+  // The periodic requeue normally trusts the watch cache; once per resync period it reads
+  // the children back from the apiserver instead.
+  const bool verify = resync_due(owner_name);
+  if (!verify && cfg_.skip_unchanged && fresh(owner_name, owner_rv)) {
     static auto& fast = reg.counter("bgc_reconcile_fast_total", "Reconciles with UB and children unchanged since the last one");
     fast.inc();
     return kube::Action::requeue_after(std::chrono::milliseconds(cfg_.requeue_secs * 1000));
@@ -343,7 +460,7 @@ kube::Action Reconciler::reconcile(const kube::ObjPtr& ub_ptr) {
   for (const auto& c : children) hashes.push_back(std::to_string(std::hash<std::string>{}(c.body)));
 
   auto run_one = [&](size_t i) {
-    if (up_to_date(children[i], hashes[i])) {
+    if (verify ? verified_in_sync(children[i], hashes[i]) : up_to_date(children[i], hashes[i])) {
       skipped.inc();
       stats_skipped_.fetch_add(1, std::memory_order_relaxed);
       return;
@@ -400,6 +517,8 @@ kube::Action Reconciler::reconcile(const kube::ObjPtr& ub_ptr) {
       }
       if (complete) {
         auto [it, inserted] = sh.ub_state.try_emplace(owner_name);
+        // a verification pass restarts the period; otherwise the pending one carries over
+        st.next_resync = verify || inserted ? next_resync_time() : it->second.next_resync;
         it->second = std::move(st);
         if (inserted) owner_entries_.fetch_add(1, std::memory_order_relaxed);
       }

@@ -14,7 +14,13 @@
 //    the RoleBinding last (at most 3 round trips instead of 4 sequential ones);
 //  * an apply is skipped when the watch cache shows the child exactly as this
 //    controller last wrote it (same body hash AND same resourceVersion), so the 30 s
-//    drift-repair pass costs zero API writes unless something actually drifted.
+//    drift-repair pass costs zero API writes unless something actually drifted;
+//  * the watch cache is not the only source of truth: every resync_secs (300 s) a
+//    UserBootstrap's reconcile re-reads each child from the apiserver (one GET) and
+//    re-applies the ones that no longer carry what this controller applies.  A missed
+//    watch event, a stalled watch or a cache bug is healed within one resync period; the
+//    reference heals within its 30 s requeue by re-applying everything unconditionally
+//    (controller.rs:67-154), at 1-4 writes per UserBootstrap per 30 s.
 #pragma once
 
 #include <array>
@@ -52,6 +58,10 @@ struct Config {
   bool skip_unchanged = true;
   bool parallel_children = true;
   int64_t requeue_secs = 30;
+  // Server-side verification period of each UserBootstrap's children (CONF_RESYNC_SECS;
+  // 0 = trust the watch cache for good).  The first one after a UserBootstrap's first
+  // reconcile is spread over [0.75, 1] of the period.
+  int64_t resync_secs = 300;
   int64_t error_requeue_ms = 3000;
   // Optional per-UB exponential backoff on errors: the n-th consecutive
   // failure requeues after min(error_requeue_ms, base * 2^(n-1)), so a transient apiserver
@@ -110,6 +120,9 @@ class Reconciler {
   // True when `child` is exactly the object our last apply returned (same resourceVersion):
   // the watch echo of our own write, which needs no reconcile.
   bool is_own_write(const kube::ResourceType& rt, const json::Value& child) const;
+  // Test hook: runs after an apply returns and before its result is recorded (the window in
+  // which a watch event of the same child can overtake the record).
+  void set_after_apply_hook(std::function<void(const DesiredChild&)> h) { after_apply_ = std::move(h); }
   // Drops the last-applied record of a deleted child (keeps the cache bounded under churn).
   void forget(const kube::ResourceType& rt, const json::Value& child);
   // The UserBootstrap itself is gone: drop its fast-path state and its children's apply
@@ -122,6 +135,8 @@ class Reconciler {
   struct Stats {
     uint64_t applied = 0;
     uint64_t skipped = 0;
+    uint64_t verified = 0;  // children read back from the apiserver by a resync
+    uint64_t repaired = 0;  // of those, re-applied because they had drifted or were gone
   };
   Stats stats() const;
 
@@ -143,6 +158,7 @@ class Reconciler {
   struct UbState {
     std::string owner_rv;
     std::vector<ChildRef> children;
+    std::chrono::steady_clock::time_point next_resync{};  // next server-side verification
   };
   // The per-tenant records, split into lock shards by namespace name: a child watch event
   // (is_own_write), a reconcile's checks and applies and a deletion (forget) touch one
@@ -152,6 +168,9 @@ class Reconciler {
     std::unordered_map<std::string, Applied> last_applied;  // "plural/ns/name"
     std::unordered_map<std::string, UbState> ub_state;      // owner name
     std::unordered_map<std::string, int> failures;          // consecutive errors per UB (backoff)
+    // Applies in flight, by child key: true once a forget() of that child ran meanwhile (its
+    // DELETED event overtook the apply's response), so the apply's result is not recorded.
+    std::unordered_map<std::string, bool> applying;
   };
   static constexpr size_t kShards = 64;
   Shard& shard(const std::string& ns_name) const;
@@ -164,6 +183,13 @@ class Reconciler {
   void apply_all(const std::vector<DesiredChild>& children, const std::function<void(size_t)>& run_one);
   bool owner_live(const std::string& name, const std::string& uid);
   bool fresh(const std::string& owner_name, const std::string& owner_rv);
+  // The owner has fast-path state and its server-side verification is due.
+  bool resync_due(const std::string& owner_name);
+  std::chrono::steady_clock::time_point next_resync_time();
+  // Resync: reads the child from the apiserver; true (and records it as applied) when it
+  // still carries everything `c.body` applies, false when it must be re-applied.
+  bool verified_in_sync(const DesiredChild& c, const std::string& body_hash);
+  std::function<void(const DesiredChild&)> after_apply_;
   kube::EventRecorder* events_ = nullptr;
   void apply_child(const DesiredChild& c, const std::string& body_hash, const std::string& body_json);
 
@@ -173,7 +199,7 @@ class Reconciler {
   ThreadPool pool_;
   mutable std::array<Shard, kShards> shards_;
   std::atomic<size_t> applied_entries_{0}, owner_entries_{0};
-  std::atomic<uint64_t> stats_applied_{0}, stats_skipped_{0};
+  std::atomic<uint64_t> stats_applied_{0}, stats_skipped_{0}, stats_verified_{0}, stats_repaired_{0};
 };
 
 }  // namespace bgc::controller
