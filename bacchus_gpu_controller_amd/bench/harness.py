@@ -550,6 +550,90 @@ def _phase(d, nat, info, args, phase, concurrency, warmup, steps, cluster):
     return out
 
 
+def _rate_names(rank, key, rate, part, n):
+    return [f"r{rank}-{key}{int(rate)}{part}-u{i}" for i in range(n)]
+
+
+def _rate_phase(d, nat, info, args, key, rate, cluster):
+    """Open-loop latency at a fixed offered rate: tenants arrive as a Poisson
+    process of `rate` CR/s over the whole job (each rank offers rate/world), whatever the
+    system's progress, and each leaves once Ready.  Unlike the closed-loop phases, whose
+    latencies grow with the CR/s they reach (a faster controller queues more work on the
+    same CPUs), every arm here carries the same load, so reconcile p99 and admission p50
+    compare like for like.  `--latency-window-s` timed after `--latency-warmup-s` untimed."""
+    from bacchus_gpu_controller_amd.testing.cluster import ADMIN_TOKEN
+
+    per_rank = rate / d.world
+    n_warm = max(1, int(round(per_rank * args.latency_warmup_s)))
+    n_timed = max(1, int(round(per_rank * args.latency_window_s)))
+    driver = nat.ChurnDriver(info["server"], ADMIN_TOKEN, f"r{d.rank}-", args.latency_workers,
+                             ca_pem=info["apiserver_ca"], http2=args.driver_http2,
+                             server_filter=args.driver_server_filter)
+    driver.start()
+    time.sleep(0.2)
+    try:
+        driver.open_loop(_rate_names(d.rank, key, rate, "w", n_warm), args.latency_warmup_s, args.timeout, 7 + d.rank)
+        d.barrier()
+        starts = thr0 = None
+        if d.rank == 0:
+            starts = {k: _clear(url, verify) for k, (url, verify) in _sample_logs(info).items()}
+            thr0 = cgroup_throttling()
+        d.barrier()
+        res = json.loads(driver.open_loop(_rate_names(d.rank, key, rate, "t", n_timed), args.latency_window_s,
+                                          args.timeout, 1000 + d.rank))
+        d.barrier()
+        thr1 = cgroup_throttling() if d.rank == 0 else None
+    finally:
+        driver.stop()
+    per = d.gather_obj({k: res[k] for k in ("ready", "failed", "timeouts", "offered_rate", "achieved_rate",
+                                            "issue_lag_p99_s", "ready_latency_s", "errors")})
+    if d.rank != 0:
+        return None
+    docs = {k: _samples(url, verify) for k, (url, verify) in _sample_logs(info).items()}
+    rec = window_samples(docs["reconcile"], starts.get("reconcile"))
+    hook = window_samples(docs["webhook"], starts.get("webhook"))
+    adm = window_samples(docs["admission"], starts.get("admission"), required=False)
+    lat = [x for p in per for x in p["ready_latency_s"]]
+    ms = lambda v: None if v is None else round(v * 1e3, 4)  # noqa: E731
+    offered = sum(p["offered_rate"] for p in per)
+    achieved = sum(p["achieved_rate"] for p in per)
+    out = {"offered_rate": round(offered, 1), "achieved_rate": round(achieved, 1),
+           "achieved_within_2pct": bool(offered and abs(achieved - offered) <= 0.02 * offered),
+           "reconcile_p99_ms": ms(_pct(rec, 0.99)), "reconcile_p50_ms": ms(_pct(rec, 0.50)),
+           "reconciles": len(rec),
+           "admission_p50_ms": ms(_pct(hook, 0.50)), "admission_p99_ms": ms(_pct(hook, 0.99)),
+           "admission_handler_p50_ms": ms(_pct(adm, 0.50)),
+           "apply_to_ready_p50_ms": ms(_pct(lat, 0.50)), "apply_to_ready_p99_ms": ms(_pct(lat, 0.99)),
+           "issue_lag_p99_ms": ms(max(p["issue_lag_p99_s"] for p in per)),
+           "ready_crs": sum(p["ready"] for p in per),
+           "failed_crs": sum(p["failed"] + p["timeouts"] for p in per)}
+    if thr0 and thr1:
+        out["cgroup_throttled_periods"] = thr1["throttled"] - thr0["throttled"]
+    errs = [e for p in per for e in p["errors"]]
+    if errs:
+        out["errors"] = errs[:3]
+    return out
+
+
+def _compare_at_rate(this, ref):
+    """Per rate: this build's latency over the reference arm's (< 1 = this build lower)."""
+    out = {}
+    for rate, t in this.items():
+        r = ref.get(rate)
+        if not r:
+            continue
+        row = {}
+        for k in ("reconcile_p99_ms", "admission_p50_ms", "apply_to_ready_p99_ms"):
+            if t.get(k) and r.get(k):
+                row[k.replace("_ms", "_ratio")] = round(t[k] / r[k], 3)
+        row["this_lower_reconcile_p99"] = bool(t.get("reconcile_p99_ms") is not None and r.get("reconcile_p99_ms")
+                                               and t["reconcile_p99_ms"] < r["reconcile_p99_ms"])
+        row["this_lower_admission_p50"] = bool(t.get("admission_p50_ms") is not None and r.get("admission_p50_ms")
+                                               and t["admission_p50_ms"] < r["admission_p50_ms"])
+        out[rate] = row
+    return out
+
+
 def _xgmi_probe(d, args):
     """RCCL all-reduce over the ranks' GPUs (N5, parallel/rccl_probe.py), after the timed
     region: busbw per size, exact results, hive placement and the bytes amdsmi saw on each
@@ -569,11 +653,14 @@ def _xgmi_probe(d, args):
 
 class _Phase:
     """One timed phase: key (tenant-name prefix), in-flight creates per rank, API server ->
-    webhook protocol, controller semantics, kube-lite write latency, warmup and timed steps."""
+    webhook protocol, controller semantics, kube-lite write latency, warmup and timed steps.
+    With `rate`, an open-loop phase at that offered rate instead (_rate_phase)."""
 
-    def __init__(self, key, concurrency, protocol, semantics, write_latency_ms, warmup, steps):
+    def __init__(self, key, concurrency, protocol, semantics, write_latency_ms, warmup, steps, rate=None,
+                 isolated=False):
         self.key, self.concurrency, self.protocol, self.semantics = key, concurrency, protocol, semantics
         self.write_latency_ms, self.warmup, self.steps = write_latency_ms, warmup, steps
+        self.rate, self.isolated = rate, isolated
 
 
 def _dump_components(cluster):
@@ -592,6 +679,49 @@ def _dump_components(cluster):
                 print(f"[bench]   {name}: {l[:400]}", file=sys.stderr)
         except Exception as e:  # noqa: BLE001
             print(f"[bench] component {name}: state unavailable ({e})", file=sys.stderr)
+
+
+FIXTURES = ("apiserver",)  # kube-lite; the load driver and the fake Google run in the bench process
+
+
+def _pin_process(pid, cpus):
+    """Every thread of `pid` onto `cpus` (threads it starts later inherit their creator's)."""
+    for tid in os.listdir(f"/proc/{pid}/task"):
+        try:
+            os.sched_setaffinity(int(tid), cpus)
+        except OSError:
+            pass
+
+
+def isolation_split(cpus, cpu_ms):
+    """(fixture CPUs, product CPUs): `cpus` split in proportion to the CPU time per CR the
+    fixtures (kube-lite + load driver) and the shipped binaries spent in the headline phase."""
+    cpus = sorted(cpus)
+    fixture = (cpu_ms.get("kube_lite") or 0.0) + (cpu_ms.get("load_driver") or 0.0)
+    product = cpu_ms.get("product_total") or 0.0
+    share = fixture / (fixture + product) if fixture + product > 0 else 0.5
+    n_fix = min(len(cpus) - 1, max(1, int(round(len(cpus) * share))))
+    return cpus[:n_fix], cpus[n_fix:]
+
+
+class _Isolated:
+    """Context: kube-lite and this process (load driver, fake Google) on the fixture CPUs,
+    the four shipped binaries on the rest; every process back on `cpus` afterwards."""
+
+    def __init__(self, cluster, cpus, cpu_ms):
+        self.cluster, self.cpus = cluster, sorted(cpus)
+        self.fixture, self.product = isolation_split(self.cpus, cpu_ms)
+
+    def __enter__(self):
+        for name, proc in self.cluster.procs.items():
+            _pin_process(proc.p.pid, self.fixture if name in FIXTURES else self.product)
+        _pin_process(os.getpid(), self.fixture)
+        return self
+
+    def __exit__(self, *exc):
+        for proc in self.cluster.procs.values():
+            _pin_process(proc.p.pid, self.cpus)
+        _pin_process(os.getpid(), self.cpus)
 
 
 def pin_to_quota(d=None):
@@ -632,16 +762,29 @@ def run(args):
     if args.tuned_phase and tuned != conc:
         phases.append(_Phase("t", tuned, args.webhook_protocol, semantics0, args.write_latency_ms,
                              args.warmup, args.steps))
+    if args.isolated_phase and d.world == 1:
+        # the headline again, with the fixtures (kube-lite, load driver) and the product on
+        # disjoint CPUs: how much of the headline latencies is queueing behind the fixtures
+        phases.append(_Phase("pi", conc, args.webhook_protocol, semantics0, args.write_latency_ms,
+                             args.warmup, args.steps, isolated=True))
     if args.http1_phase and args.webhook_protocol == "h2":
         # secondary: the same load with the webhook called over HTTP/1.1 (keep-alive pool)
         phases.append(_Phase("w", conc, "http/1.1", semantics0, args.write_latency_ms, args.warmup, args.steps))
     semantics = "reference" if args.reference_semantics else args.semantics
+    rates = [float(x) for x in args.latency_rates.split(",") if x.strip()]
+    if rates:
+        # open loop at equal offered load: this build first (its controller is running) ...
+        phases += [_Phase(f"q{i}", 0, args.webhook_protocol, semantics0, args.write_latency_ms, 0, 0, rate=r)
+                   for i, r in enumerate(rates)]
     if args.reference_arms and semantics == "this":
         # same-stack comparison, timed like the headline: the reference's controller
         # behaviour (controller.rs:81-154: sequential, unconditional applies) on this stack,
         # at the headline's storage latency and with a write-latency (etcd commit) model
         phases.append(_Phase("rc", conc, args.webhook_protocol, "reference-controller", args.write_latency_ms,
                              args.warmup, args.steps))
+        # ... then the reference controller at the same rates, while it runs
+        phases += [_Phase(f"qr{i}", 0, args.webhook_protocol, "reference-controller", args.write_latency_ms, 0, 0,
+                          rate=r) for i, r in enumerate(rates)]
         if args.arm_write_latency_ms > 0:
             phases.append(_Phase("rl", conc, args.webhook_protocol, "reference-controller",
                                  args.arm_write_latency_ms, args.arm_warmup, args.arm_steps))
@@ -665,11 +808,22 @@ def run(args):
 
     if d.rank == 0:
         google = FakeGoogle().start()
+        rows = []
         if not args.approve_after_create:
             # pre-approved sheet: every tenant's row is marked O before it applies
-            google.set_rows([{"id_username": name} for r in range(d.world) for p in phases
-                             for s in range((p.warmup + p.steps) * args.rounds)
-                             for name in _names(r, p.key, s, args.batch)])
+            rows = [{"id_username": name} for r in range(d.world) for p in phases if p.rate is None
+                    for s in range((p.warmup + p.steps) * args.rounds)
+                    for name in _names(r, p.key, s, args.batch)]
+        # the open-loop phases' tenants are pre-approved in either flow
+        for p in phases:
+            if p.rate is not None:
+                per_rank = p.rate / d.world
+                for r in range(d.world):
+                    for part, secs in (("w", args.latency_warmup_s), ("t", args.latency_window_s)):
+                        rows += [{"id_username": name} for name in
+                                 _rate_names(r, p.key, p.rate, part, max(1, int(round(per_rank * secs))))]
+        if rows:
+            google.set_rows(rows)
         ctrl_env = controller_env(semantics)
         sync_env = {"CONF_WATCH": "true", "CONF_WORKERS": str(sync_workers), "RUST_LOG": args.log_level,
                     "CONF_SHEET_POLL_MS": str(args.sheet_poll_ms)}
@@ -723,7 +877,18 @@ def run(args):
                     info["controller"] = f"http://127.0.0.1:{cluster.controller_port}"
                     running = p.semantics
             d.barrier()
-            results[p.key] = _phase(d, nat, info, args, p.key, p.concurrency, p.warmup, p.steps, cluster)
+            if p.rate is not None:
+                results[p.key] = _rate_phase(d, nat, info, args, p.key, p.rate, cluster)
+                if results[p.key] is not None:
+                    results[p.key]["semantics"] = p.semantics
+                continue
+            if p.isolated:
+                cpus = cpuset or sorted(os.sched_getaffinity(0))
+                with _Isolated(cluster, cpus, results["m"]["cpu_ms_per_cr"]) as iso:
+                    results[p.key] = _phase(d, nat, info, args, p.key, p.concurrency, p.warmup, p.steps, cluster)
+                results[p.key]["cpus"] = {"fixtures": _cpulist_text(iso.fixture), "product": _cpulist_text(iso.product)}
+            else:
+                results[p.key] = _phase(d, nat, info, args, p.key, p.concurrency, p.warmup, p.steps, cluster)
             if results[p.key] is not None:
                 results[p.key]["semantics"] = p.semantics
                 results[p.key]["apiserver_write_latency_ms"] = p.write_latency_ms
@@ -777,6 +942,12 @@ def run(args):
             out["tuned"] = {k: t.get(k) for k in ("value", "concurrency_per_rank", "reconcile_p99_ms",
                                                   "admission_p50_ms", "apply_to_ready_p50_ms",
                                                   "apply_to_ready_p99_ms", "cpu_ms_per_cr", "failed_crs")}
+        if "pi" in results:
+            pi = results["pi"]
+            out["product_isolated"] = {k: pi.get(k) for k in (
+                "value", "cpus", "reconcile_p99_ms", "reconcile_p50_ms", "admission_p50_ms", "admission_p99_ms",
+                "admission_handler_p50_ms", "admission_h2_server_p50_ms", "apply_to_ready_p50_ms",
+                "apply_to_ready_p99_ms", "cpu_ms_per_cr", "cgroup_throttled", "failed_crs")}
         if "w" in results:
             w = results["w"]
             out["webhook_http1"] = {k: w.get(k) for k in ("value", "admission_p50_ms", "admission_p99_ms",
@@ -799,6 +970,17 @@ def run(args):
             out[f"write_latency_{args.arm_write_latency_ms:g}ms"] = {
                 "this": this_l, "reference_controller": ref_l,
                 "this_over_reference_cr_per_s": ratio(this_l["value"], ref_l["value"])}
+        if rates:
+            this_q = {f"{r:g}": results[f"q{i}"] for i, r in enumerate(rates) if results.get(f"q{i}")}
+            ref_q = {f"{r:g}": results[f"qr{i}"] for i, r in enumerate(rates) if results.get(f"qr{i}")}
+            for v in list(this_q.values()) + list(ref_q.values()):
+                v.pop("semantics", None)
+            out["latency_at_rate"] = {"rates_cr_per_s": [float(f"{r:g}") for r in rates],
+                                      "window_s": args.latency_window_s, "arrivals": "poisson (open loop)",
+                                      "this": this_q}
+            if ref_q:
+                out["latency_at_rate"]["reference_controller"] = ref_q
+                out["latency_at_rate"]["this_over_reference"] = _compare_at_rate(this_q, ref_q)
         # amdsmi counters of the advertised GPUs at the end of the timed region (node agent)
         out["gpu_telemetry"] = gpu_tel
         if xgmi is not None:
@@ -860,6 +1042,9 @@ def main(argv=None):
     ap.add_argument("--tuned-concurrency", type=int, default=0, help="0 = auto_concurrency()")
     ap.add_argument("--webhook-protocol", choices=("h2", "http/1.1"), default="h2",
                     help="API server -> admission webhook transport of the headline phase")
+    ap.add_argument("--isolated-phase", action=argparse.BooleanOptionalAction, default=True,
+                    help="N=1: also time the headline with kube-lite and the load driver on CPUs of their own, "
+                         "apart from the shipped binaries (product_isolated; split by the headline's CPU per CR)")
     ap.add_argument("--http1-phase", action=argparse.BooleanOptionalAction, default=True,
                     help="with --webhook-protocol h2: also time the webhook over HTTP/1.1 (secondary field)")
     ap.add_argument("--timeout", type=float, default=120.0)
@@ -888,6 +1073,14 @@ def main(argv=None):
                     help="kube-lite storage commit latency of the write-latency arms (0 = no such arms)")
     ap.add_argument("--arm-steps", type=int, default=6, help="timed steps of each write-latency arm")
     ap.add_argument("--arm-warmup", type=int, default=2, help="warmup steps of each write-latency arm")
+    ap.add_argument("--latency-rates", default="2000,6000",
+                    help="open-loop offered rates (CR/s, whole job) at which this build and the reference-controller "
+                         "arm are both timed (latency_at_rate; '' = none)")
+    ap.add_argument("--latency-window-s", type=float, default=2.0, help="timed window of each open-loop phase")
+    ap.add_argument("--latency-warmup-s", type=float, default=0.5, help="untimed lead-in of each open-loop phase")
+    ap.add_argument("--latency-workers", type=int, default=128,
+                    help="open loop: threads issuing creates per rank (arrivals never wait for one below ~that "
+                         "many in flight)")
     ap.add_argument("--approve-after-create", action="store_true",
                     help="tenants apply first; each step's batch is approved by one sheet edit once its "
                          "Namespaces exist (the reference's onboarding order); times create->approve->Ready")

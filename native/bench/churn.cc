@@ -1,7 +1,10 @@
 #include "bench/churn.h"
 
+#include <algorithm>
 #include <array>
 #include <future>
+#include <random>
+#include <thread>
 
 #include "core/log.h"
 #include "core/metrics.h"
@@ -71,9 +74,23 @@ void ChurnDriver::mark(const std::string& name, int which, int64_t t) {
   }
   Track& tr = it->second;
   int64_t* slot = which == 0 ? &tr.t_ns : which == 1 ? &tr.t_rq : &tr.t_rb;
-  if (!*slot) *slot = t;
+  if (*slot) return;
+  *slot = t;
+  if (tr.delete_when_ready && ready_locked(tr)) issue_delete(name);
   // approve-after-create waits on Namespaces alone; otherwise only Ready matters
   if (ready_locked(tr) || (which == 0 && !opts_.approve_url.empty())) cv_.notify_all();
+}
+
+void ChurnDriver::issue_delete(const std::string& name) {
+  delete_pool_->submit([this, name] {
+    try {
+      admin_->remove(types::UserBootstrap, "", name);
+    } catch (const kube::ApiError& e) {
+      if (e.code() != 404) delete_failures_.fetch_add(1);
+    } catch (const std::exception&) {
+      delete_failures_.fetch_add(1);
+    }
+  });
 }
 
 void ChurnDriver::start() {
@@ -212,6 +229,115 @@ json::Value ChurnDriver::step(const std::vector<std::string>& names, double time
     out["approve_latency_s"] = ap_lat;
     out["approve_to_ready_latency_s"] = ap_ready;
   }
+  return out;
+}
+
+json::Value ChurnDriver::open_loop(const std::vector<std::string>& names, double duration_s, double timeout_s,
+                                   uint64_t seed) {
+  const size_t n = names.size();
+  std::vector<int64_t> offset(n);
+  {
+    std::mt19937_64 rng(seed);
+    std::uniform_real_distribution<double> u(0.0, duration_s * 1e9);
+    for (auto& o : offset) o = static_cast<int64_t>(u(rng));
+    std::sort(offset.begin(), offset.end());
+  }
+  delete_failures_.store(0);
+  const int64_t t0 = metrics::now_ns() + 2000000;  // 2 ms to register the tracks first
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (size_t i = 0; i < n; ++i) {
+      Track t;
+      t.t_start = t0 + offset[i];
+      t.delete_when_ready = opts_.approve_url.empty();
+      tracks_[names[i]] = t;
+    }
+  }
+  std::vector<int64_t> lag(n);
+  std::vector<std::future<void>> futs;
+  futs.reserve(n);
+  const auto base = std::chrono::steady_clock::now() + std::chrono::nanoseconds(t0 - metrics::now_ns());
+  for (size_t i = 0; i < n; ++i) {
+    std::this_thread::sleep_until(base + std::chrono::nanoseconds(offset[i]));
+    lag[i] = metrics::now_ns() - (t0 + offset[i]);
+    const std::string& name = names[i];
+    futs.push_back(pool_->submit([this, name] {
+      Value body = Value::object({{"apiVersion", "bacchus.io/v1"}, {"kind", "UserBootstrap"},
+                                  {"metadata", Value::object({{"name", name}})}, {"spec", Value::object()}});
+      http::Headers h;
+      h.set("Authorization", "Bearer " + opts_.admin_token);
+      h.set("Impersonate-User", opts_.user_prefix + name);
+      h.set("Impersonate-Group", opts_.group);
+      h.set("Content-Type", "application/json");
+      std::string err;
+      try {
+        http::Response r = http_->request("POST", types::UserBootstrap.collection_path(), body.dump(), &h);
+        if (r.status != 201 && r.status != 200) err = std::to_string(r.status) + " " + r.body;
+      } catch (const std::exception& e) {
+        err = e.what();
+      }
+      std::lock_guard<std::mutex> lk(mu_);
+      Track& t = tracks_[name];
+      t.t_created = metrics::now_ns();
+      if (!err.empty()) {
+        t.failed = true;
+        t.error = err;
+      }
+      cv_.notify_all();
+    }));
+  }
+  for (auto& f : futs) f.get();
+  const auto deadline = std::chrono::steady_clock::now() +
+                        std::chrono::duration_cast<std::chrono::steady_clock::duration>(std::chrono::duration<double>(timeout_s));
+  Value out = Value::object();
+  std::unique_lock<std::mutex> lk(mu_);
+  cv_.wait_until(lk, deadline, [&] {
+    for (const auto& nm : names) {
+      const Track& t = tracks_[nm];
+      if (!t.failed && !ready_locked(t)) return false;
+    }
+    return true;
+  });
+  Value lat = Value::array(), clat = Value::array(), errs = Value::array();
+  Value ns_lat = Value::array(), rq_lat = Value::array(), rb_lat = Value::array();
+  int ready = 0, failed = 0, timeouts = 0;
+  int64_t last_ready = t0;
+  for (const auto& nm : names) {
+    const Track& t = tracks_[nm];
+    if (t.failed) {
+      ++failed;
+      if (errs.size() < 5) errs.push_back(nm + ": " + t.error);
+    } else if (ready_locked(t)) {
+      ++ready;
+      const int64_t tr = std::max({t.t_ns, t.t_rq, t.t_rb});
+      last_ready = std::max(last_ready, tr);
+      lat.push_back(static_cast<double>(tr - t.t_start) * 1e-9);
+      clat.push_back(static_cast<double>(t.t_created - t.t_start) * 1e-9);
+      ns_lat.push_back(static_cast<double>(t.t_ns - t.t_start) * 1e-9);
+      rq_lat.push_back(static_cast<double>(t.t_rq - t.t_start) * 1e-9);
+      rb_lat.push_back(static_cast<double>(t.t_rb - t.t_start) * 1e-9);
+    } else {
+      ++timeouts;
+    }
+    tracks_.erase(nm);
+    early_.erase(nm);
+  }
+  lk.unlock();
+  std::sort(lag.begin(), lag.end());
+  const double span = static_cast<double>(last_ready - (t0 + (n ? offset.front() : 0))) * 1e-9;
+  out["ready"] = ready;
+  out["failed"] = failed;
+  out["timeouts"] = timeouts;
+  out["offered_rate"] = duration_s > 0 ? static_cast<double>(n) / duration_s : 0.0;
+  out["achieved_rate"] = span > 0 ? static_cast<double>(ready) / span : 0.0;
+  out["issue_lag_p99_s"] = n ? static_cast<double>(lag[std::min(n - 1, n * 99 / 100)]) * 1e-9 : 0.0;
+  out["ready_latency_s"] = lat;
+  out["create_latency_s"] = clat;
+  out["ns_latency_s"] = ns_lat;
+  out["rq_latency_s"] = rq_lat;
+  out["rb_latency_s"] = rb_lat;
+  out["errors"] = errs;
+  out["delete_failures"] = delete_failures_.load();
   return out;
 }
 

@@ -65,6 +65,15 @@ class ChurnDriver {
   // leave while the next ones arrive); the step ends when both are done.
   json::Value step_with_delete(const std::vector<std::string>& names, const std::vector<std::string>& previous,
                                double timeout_s);
+  // Open loop: the creates arrive as a Poisson process of rate names.size() / duration_s,
+  // whatever the system's progress (arrival times: sorted uniforms over the window, i.e.
+  // a Poisson process conditioned on that many arrivals), each tenant is deleted once
+  // Ready, and latencies count from the scheduled arrival, so a lagging system shows up as
+  // latency instead of as a lower offered rate (no coordinated omission).  Waits for every
+  // tenant (or timeout).  Returns step()'s fields plus "offered_rate", "achieved_rate"
+  // (Ready tenants / first arrival to last Ready) and "issue_lag_p99_s" (how late the
+  // dispatcher issued creates).
+  json::Value open_loop(const std::vector<std::string>& names, double duration_s, double timeout_s, uint64_t seed);
   // Deletes (as cluster admin) concurrently; returns number of failures.
   int remove(const std::vector<std::string>& names);
   void stop();
@@ -76,9 +85,11 @@ class ChurnDriver {
     int64_t t_approved = 0;
     int64_t t_ns = 0, t_rq = 0, t_rb = 0;
     bool failed = false;
+    bool delete_when_ready = false;  // open loop: the tenant leaves once Ready
     std::string error;
   };
   void mark(const std::string& name, int which, int64_t t);
+  void issue_delete(const std::string& name);  // asynchronous, on delete_pool_
   // Approve-after-create: waits for the batch's Namespaces, then edits the sheet once.
   void approve_batch(const std::vector<std::string>& names, std::chrono::steady_clock::time_point deadline);
   bool ready_locked(const Track& t) const { return t.t_ns && t.t_rq && t.t_rb; }
@@ -95,6 +106,7 @@ class ChurnDriver {
   std::unordered_map<std::string, Track> tracks_;
   // events that arrived before the step registered the name
   std::unordered_map<std::string, std::array<int64_t, 3>> early_;
+  std::atomic<int> delete_failures_{0};
 };
 
 }  // namespace bgc::bench

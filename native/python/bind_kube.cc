@@ -63,6 +63,15 @@ void register_kube(py::module_& m) {
         }
         return v.dump();
       })
+      .def("open_loop", [](bgc::bench::ChurnDriver& d, const std::vector<std::string>& names, double duration_s,
+                           double timeout, uint64_t seed) {
+        bgc::json::Value v;
+        {
+          py::gil_scoped_release nogil;
+          v = d.open_loop(names, duration_s, timeout, seed);
+        }
+        return v.dump();
+      }, py::arg("names"), py::arg("duration_s"), py::arg("timeout") = 60.0, py::arg("seed") = 1)
       .def("remove", [](bgc::bench::ChurnDriver& d, const std::vector<std::string>& names) {
         py::gil_scoped_release nogil;
         return d.remove(names);
