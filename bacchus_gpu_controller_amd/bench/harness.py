@@ -550,6 +550,23 @@ def _phase(d, nat, info, args, phase, concurrency, warmup, steps, cluster):
     return out
 
 
+def _settle(info, timeout=10.0):
+    """Waits until kube-lite's garbage collector has caught up (the cascades of the previous
+    phase's deletions), so a phase does not start on the tail of another one's work."""
+    import requests
+
+    deadline = time.monotonic() + timeout
+    while time.monotonic() < deadline:
+        try:
+            st = requests.get(info["server"] + "/_kl/stats", timeout=5, verify=info["apiserver_verify"]).json()
+            if not st.get("gc_pending"):
+                break
+        except Exception:  # noqa: BLE001
+            break
+        time.sleep(0.05)
+    time.sleep(0.2)
+
+
 def _rate_names(rank, key, rate, part, n):
     return [f"r{rank}-{key}{int(rate)}{part}-u{i}" for i in range(n)]
 
@@ -570,7 +587,9 @@ def _rate_phase(d, nat, info, args, key, rate, cluster):
                              ca_pem=info["apiserver_ca"], http2=args.driver_http2,
                              server_filter=args.driver_server_filter)
     driver.start()
-    time.sleep(0.2)
+    if d.rank == 0:
+        _settle(info)
+    d.barrier()
     try:
         driver.open_loop(_rate_names(d.rank, key, rate, "w", n_warm), args.latency_warmup_s, args.timeout, 7 + d.rank)
         d.barrier()
@@ -883,6 +902,7 @@ def run(args):
                     results[p.key]["semantics"] = p.semantics
                 continue
             if p.isolated:
+                _settle(info)
                 cpus = cpuset or sorted(os.sched_getaffinity(0))
                 with _Isolated(cluster, cpus, results["m"]["cpu_ms_per_cr"]) as iso:
                     results[p.key] = _phase(d, nat, info, args, p.key, p.concurrency, p.warmup, p.steps, cluster)
@@ -1077,7 +1097,7 @@ def main(argv=None):
                     help="open-loop offered rates (CR/s, whole job) at which this build and the reference-controller "
                          "arm are both timed (latency_at_rate; '' = none)")
     ap.add_argument("--latency-window-s", type=float, default=2.0, help="timed window of each open-loop phase")
-    ap.add_argument("--latency-warmup-s", type=float, default=0.5, help="untimed lead-in of each open-loop phase")
+    ap.add_argument("--latency-warmup-s", type=float, default=1.0, help="untimed lead-in of each open-loop phase")
     ap.add_argument("--latency-workers", type=int, default=128,
                     help="open loop: threads issuing creates per rank (arrivals never wait for one below ~that "
                          "many in flight)")

@@ -3,6 +3,7 @@
 #include <pybind11/stl.h>
 
 #include "core/json.h"
+#include "core/unicode.h"
 #include "sync/google.h"
 #include "sync/sheet.h"
 
@@ -64,6 +65,9 @@ void register_sync(py::module_& m) {
     r.authorized = a;
     return bgc::sync::is_authorized(r);
   });
+  // Rust str::trim / str::to_lowercase slices (core/unicode.h), on UTF-8 bytes
+  m.def("unicode_trim", [](const py::bytes& b) { return py::bytes(std::string(bgc::unicode::trim(std::string(b)))); });
+  m.def("unicode_lower", [](const py::bytes& b) { return py::bytes(bgc::unicode::to_lower(std::string(b))); });
   m.def("quota_spec", [](const py::dict& row, const std::string& gpu, const std::string& part) {
     bgc::sync::QuotaKeys k;
     k.gpu_resource = gpu;

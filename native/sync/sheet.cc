@@ -4,6 +4,8 @@
 #include <charconv>
 #include <map>
 
+#include "core/unicode.h"
+
 namespace bgc::sync {
 
 using json::Value;
@@ -163,12 +165,10 @@ std::vector<Row> parse_csv(std::string_view text, std::vector<std::string>* warn
 }
 
 bool is_authorized(const Row& r) {
-  std::string a = r.authorized;
-  size_t b = a.find_first_not_of(" \t\r\n");
-  size_t e = a.find_last_not_of(" \t\r\n");
-  a = b == std::string::npos ? "" : a.substr(b, e - b + 1);
-  for (auto& c : a) c = static_cast<char>(std::tolower(static_cast<unsigned char>(c)));
-  return a == "o";
+  // `authorized.trim().to_lowercase() == "o"` with Rust's Unicode semantics
+  // (synchronizer.rs:225-236): "\u00a0O" (a Google Form's non-breaking space) is approved,
+  // the fullwidth "Ｏ" is not.
+  return unicode::to_lower(unicode::trim(r.authorized)) == "o";
 }
 
 Value quota_spec(const Row& r, const QuotaKeys& keys) {

@@ -5,6 +5,8 @@ import shutil
 import subprocess
 
 import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
 
 from bacchus_gpu_controller_amd.testing.fake_google import FORM_HEADERS, make_csv
 
@@ -57,10 +59,57 @@ def test_missing_column_skips_every_row(nat):
     assert rows == [] and "missing field `mig_request`" in warnings[0]
 
 
-@pytest.mark.parametrize("value,ok", [("O", True), ("o", True), ("  O \t", True), ("X", False), ("", False),
-                                      ("OO", False), ("0", False)])
+@pytest.mark.parametrize("value,ok", [
+    ("O", True), ("o", True), ("  O \t", True), ("o\t", True), ("X", False), ("", False), ("OO", False), ("0", False),
+    # Rust's str::trim strips Unicode White_Space (synchronizer.rs:225-236)
+    ("\u00a0O", True), (" O\u00a0", True), ("\u3000o\u2003", True), ("\u0085O\u2029", True),
+    ("\u200bO", False),  # zero-width space is not White_Space
+    ("\ufeffO", False),  # nor is a byte-order mark
+    # to_lowercase maps only O to o: fullwidth and look-alike letters stay unauthorized
+    ("\uff4f", False), ("\uff2f", False), ("\u039f", False), ("\u041e", False), ("\u00d8", False),
+])
 def test_authorized(nat, value, ok):
     assert nat.is_authorized(value) is ok
+
+
+# Unicode PropList.txt White_Space (what Rust's char::is_whitespace / str::trim use)
+WHITE_SPACE = set(map(chr, [*range(0x09, 0x0E), 0x20, 0x85, 0xA0, 0x1680, *range(0x2000, 0x200B), 0x2028, 0x2029,
+                            0x202F, 0x205F, 0x3000]))
+
+
+def rust_trim(s):
+    b, e = 0, len(s)
+    while b < e and s[b] in WHITE_SPACE:
+        b += 1
+    while e > b and s[e - 1] in WHITE_SPACE:
+        e -= 1
+    return s[b:e]
+
+
+ALPHABET = sorted(WHITE_SPACE) + list("oO0aZ\u00c0\u00de\u00d7\u0130\u0178\u0391\u03a3\u0410\u0401\uff21\uff2f"
+                                      "\u200b\ufeff\u001c\u4e00\U0001F600")
+
+
+@settings(max_examples=400, deadline=None)
+@given(st.text(alphabet=ALPHABET, max_size=12))
+def test_unicode_trim_matches_rust_semantics(nat, s):
+    assert nat.unicode_trim(s.encode()).decode() == rust_trim(s)
+
+
+@settings(max_examples=400, deadline=None)
+@given(st.text(alphabet=ALPHABET, max_size=12))
+def test_unicode_lower_matches_full_lowercase_on_covered_scripts(nat, s):
+    # Python's str.lower is the full Unicode mapping, like Rust's to_lowercase (final-sigma
+    # context aside: Σ is only lowered to σ here, so it is left out of the comparison)
+    if "\u03a3" in s:
+        return
+    assert nat.unicode_lower(s.encode()).decode() == s.lower()
+
+
+def test_unicode_helpers_keep_invalid_utf8(nat):
+    raw = b"\xa0O\xff\xc3"
+    assert nat.unicode_lower(raw) == b"\xa0o\xff\xc3"
+    assert nat.unicode_trim(b"\xff \xc2\xa0") == b"\xff"
 
 
 def test_last_authorized_match_and_server_substring(nat):
