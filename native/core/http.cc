@@ -307,7 +307,6 @@ struct Server::WorkerPool {
   std::condition_variable cv;
   std::deque<std::function<void()>> q;
   size_t idle = 0;
-  bool tls = false;
 
   static void run(const std::shared_ptr<WorkerPool>& self) {
     std::unique_lock<std::mutex> lk(self->mu);
@@ -324,7 +323,7 @@ struct Server::WorkerPool {
       lk.lock();
     }
     lk.unlock();
-    if (self->tls) OPENSSL_thread_stop();
+    OPENSSL_thread_stop();  // handlers may have made TLS calls of their own (see below)
   }
   static void submit(const std::shared_ptr<WorkerPool>& self, std::function<void()> job) {
     bool spawn;
@@ -422,7 +421,6 @@ void Server::start() {
   if (opts_.tls && opts_.http2) {
     opts_.tls->enable_h2();
     h2_workers_ = std::make_shared<WorkerPool>();
-    h2_workers_->tls = true;
   }
   listen_fd_ = net::listen_tcp(opts_.addr, opts_.port, 1024, &port_);
   if (::pipe2(wake_pipe_, O_CLOEXEC) != 0) throw net::NetError("pipe2 failed");
@@ -461,10 +459,11 @@ void Server::accept_loop() {
     active_.fetch_add(1);
     std::thread([this, fd, remote = std::string(host)] {
       serve_conn(fd, remote);
-      // OpenSSL keeps per-thread state (the thread's public/private DRBGs) that is only
-      // released by OPENSSL_thread_stop(): without it every TLS connection thread leaked
-      // ~0.1 KB (found by LeakSanitizer, tools/sanitize.sh asan).
-      if (opts_.tls) OPENSSL_thread_stop();
+      // OpenSSL keeps per-thread state (the thread's public/private DRBGs, its error queue)
+      // that OPENSSL_thread_stop() releases at once (found by LeakSanitizer, tools/sanitize.sh
+      // asan).  Also on a plain-HTTP server: a handler may have used TLS as a client (kube-lite's
+      // webhook callouts).
+      OPENSSL_thread_stop();
       // notify under the lock: once stop() observes active_==0 the Server (and the cv) may be destroyed
       std::lock_guard<std::mutex> lk(conns_mu_);
       active_.fetch_sub(1);

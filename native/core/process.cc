@@ -1,6 +1,7 @@
 #include "core/process.h"
 
 #include <malloc.h>
+#include <openssl/crypto.h>
 #include <pthread.h>
 #include <signal.h>
 
@@ -43,7 +44,17 @@ void start_malloc_trimmer() {
   }).detach();
 }
 
+// OpenSSL's default atexit handler (OPENSSL_cleanup) frees its global state and deletes
+// the thread-local key whose destructor frees each thread's state (DRBGs, error queue).
+// A detached thread that is still finishing while the process exits (an HTTP connection
+// thread after Server::stop's grace, an idle HTTP/2 worker) then ends after that cleanup,
+// and its state can never be freed: LeakSanitizer's intermittent kube-lite report of round
+// 4 (tools/probes/lsan_openssl_exit_race.cc reproduces it).  Without the handler, exit
+// leaves OpenSSL's memory to the kernel, like any other process memory.
+void init_openssl() { OPENSSL_init_crypto(OPENSSL_INIT_NO_ATEXIT, nullptr); }
+
 void process_init() {
+  init_openssl();
   tune_malloc();
   start_malloc_trimmer();
   log::init_from_env();

@@ -1,11 +1,14 @@
 // Common process start-up for the native services: RUST_LOG-style logging, glibc malloc
-// tuning and the optional sampling profiler (core/cpuprof.h).
+// tuning, OpenSSL's exit behaviour and the optional sampling profiler (core/cpuprof.h).
 #pragma once
 
 namespace bgc {
 
 // Call first thing in main().
 void process_init();
+
+// OpenSSL without its atexit cleanup (see process.cc); part of process_init().
+void init_openssl();
 
 // glibc malloc tuning for many short-lived JSON allocations across thread-per-connection
 // servers: no heap trimming (the sbrk grow/trim cycle cost ~10% of kube-lite CPU), heap
