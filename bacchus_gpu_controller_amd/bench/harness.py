@@ -261,7 +261,7 @@ def cgroup_throttling():
 def auto_concurrency(world, cpus):
     """In-flight creates per rank.  The control plane is CPU-bound, so the total in flight
     is sized to its CPU share rather than fixed per rank: measured on the MI355X box
-    (16 CPUs, profiles/concurrency_sweep_r1/), 32 per rank costs 20-45 % throughput and
+    (16 CPUs, profiles/archive/concurrency_sweep_r1/), 32 per rank costs 20-45 % throughput and
     2x apply->Ready latency at every N against ~cpus/(2*sqrt(N)) per rank."""
     return int(min(32, max(4, round(cpus / (2.0 * world ** 0.5)))))
 
@@ -1116,7 +1116,7 @@ def main(argv=None):
                     help="extra admission environment (repeatable), e.g. CONF_HTTP2_INLINE=false")
     ap.add_argument("--report-cpu", action="store_true", help="add RSS, object counts and controller gauges")
     ap.add_argument("--driver-http2", action=argparse.BooleanOptionalAction, default=False,
-                    help="tenant load over HTTP/2 multiplexed connections (profiles/http2_r2/: no gain at N=1, "
+                    help="tenant load over HTTP/2 multiplexed connections (profiles/archive/http2_r2/: no gain at N=1, "
                          "worse at N=8 on kube-lite)")
     ap.add_argument("--tls-apiserver", action=argparse.BooleanOptionalAction, default=True,
                     help="components reach kube-lite over HTTPS via kubeconfigs, as in a real cluster")

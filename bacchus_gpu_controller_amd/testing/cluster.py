@@ -48,8 +48,8 @@ def free_port():
 
 # glibc malloc: a deeper per-thread cache (default 7 chunks per size class) keeps the
 # services' many short-lived JSON allocations off the shared arenas.  Measured on the
-# MI355X box: +14% CR/s, -12% control-plane CPU per CR (profiles/malloc_tunables_r1/);
-# 64 per class keeps that at half the cached memory of 1024 (profiles/tcache_ab_r1/).
+# MI355X box: +14% CR/s, -12% control-plane CPU per CR (profiles/archive/malloc_tunables_r1/);
+# 64 per class keeps that at half the cached memory of 1024 (profiles/archive/tcache_ab_r1/).
 # The container image sets the same value (Dockerfile ENV).
 # trim_threshold / top_pad / mmap_threshold: no sbrk shrink-and-grow churn in the main
 # arena under bursts (profiles/malloc_trim_r3/: product CPU -3.5 %, reconcile p99 -12 %)

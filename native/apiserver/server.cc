@@ -427,7 +427,7 @@ struct WatchSub {
 // reader/writer lock used before (writer-preferring, since glibc's default starves commits
 // under a steady GET/LIST load) woke every waiting reader at each commit's unlock: at 800
 // creates in flight its wake-up herd cost more than the read parallelism gained
-// (profiles/kl_store_lock_r2/: N=8 +63 % CR/s, kube-lite CPU per CR 4.2 -> 2.2 ms with the
+// (profiles/archive/kl_store_lock_r2/: N=8 +63 % CR/s, kube-lite CPU per CR 4.2 -> 2.2 ms with the
 // mutex; N=1 +17 %).  BGC_KL_RWLOCK=writer|reader selects the rwlock variants.
 class RwLock {
  public:

@@ -47,10 +47,10 @@ struct Options {
   // Watch write coalescing: after a wake-up with few events queued, wait this long for
   // more before writing (fewer wake-ups/syscalls per event at high event rates, at the
   // cost of up to this much added delivery latency).  0 = write immediately.
-  int watch_coalesce_us = 50;  // measured on MI355X: +7 % CR/s, -6 % CPU/CR, lower p50 (profiles/watch_coalesce_r1/)
+  int watch_coalesce_us = 50;  // measured on MI355X: +7 % CR/s, -6 % CPU/CR, lower p50 (profiles/archive/watch_coalesce_r1/)
   // Garbage-collector threads (cascading deletion of dependents and namespace contents).
   // One thread fell 10-14k deletions behind over 100k tenants at ~10k CR/s on the MI355X
-  // box; two keep the backlog at 0 with unchanged CR/s (profiles/gc_workers_r1/).
+  // box; two keep the backlog at 0 with unchanged CR/s (profiles/archive/gc_workers_r1/).
   int gc_workers = 2;
   // Storage commit latency added to every write (POST/PUT/PATCH/DELETE) before it is
   // applied: a real apiserver answers a write only after etcd's raft commit + fsync
@@ -66,7 +66,7 @@ struct Options {
   // Webhook callouts: HTTP/1.1 keep-alive pool by default; webhook_http2 offers h2 by ALPN
   // and multiplexes the callouts as streams over webhook_h2_connections connections (as
   // the real apiserver's Go client does over one).  With kube-lite's mutex store lock the
-  // HTTP/1.1 pool measured equal or better at N=1..8 (profiles/http2_r2/after_store_lock/).
+  // HTTP/1.1 pool measured equal or better at N=1..8 (profiles/archive/http2_r2/after_store_lock/).
   bool webhook_http2 = false;
   size_t webhook_h2_connections = 4;
   // HTTP/2 webhook callouts: the calling handler threads read their responses themselves

@@ -130,7 +130,7 @@ struct Telemetry {
 };
 
 // What one sample() reads.  Costs per device on MI355X / ROCm 7.2
-// (profiles/amdsmi_cost_r1.json, profiles/amdsmi_cost_r2.json):
+// (profiles/archive/amdsmi_cost_r1.json, profiles/archive/amdsmi_cost_r2.json):
 //   Fast : the gpu_metrics blob (activity, power, temps, clocks, throttle, violation
 //          accumulators, xGMI link status)                              ~280 us
 //   Slow : + VRAM usage and total ECC counts                           ~+750 us

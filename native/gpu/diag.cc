@@ -328,7 +328,7 @@ double burn_dtype_rate_ratio(int code) {
 DiagFloors DiagFloors::mi355x_defaults() {
   DiagFloors f;
   // MI355X, ROCm 7.2, 1 GiB buffers / 16 waves per CU x 2048 MFMA iterations
-  // (profiles/diag_floors_r2.json): read 6.33-6.57 TB/s, copy 5.36-5.42, write 5.11-5.25,
+  // (profiles/archive/diag_floors_r2.json): read 6.33-6.57 TB/s, copy 5.36-5.42, write 5.11-5.25,
   // MFMA bf16 1.92-2.06 PF/s, XCC balance 0.96.  At 256 MiB (Infinity-Cache-sized, the
   // smallest sensible buffer) read is still 5.56 TB/s, so these floors hold down to it.
   f.min_read_gbps = 4750;
@@ -342,13 +342,13 @@ DiagFloors DiagFloors::mi355x_defaults() {
   // the clocks are, against ~5 and ~10 PF/s dense peaks
   f.min_fp8_tflops = 3000;
   f.min_fp4_tflops = 5000;
-  // burn-in: measured on MI355X in profiles/diag_burn_r2.json (sustained bf16 MFMA at
+  // burn-in: measured on MI355X in profiles/archive/diag_burn_r2.json (sustained bf16 MFMA at
   // 97 % of the 2.5 PF/s dense peak once clocks settle)
   f.min_burn_tflops = 1800;  // measured 2409-2421 PF/s mean over 10 s at 1.17-1.22 kW, 2.34-2.39 GHz
   f.min_burn_sustain = 0.80;
   f.max_burn_hotspot_c = 100;
   f.max_burn_thermal_violation_pct = 20;
-  // PCIe Gen5 x16 host link (profiles/pcie_r2/probe.json): 57.1 GB/s host-to-device and
+  // PCIe Gen5 x16 host link (profiles/archive/pcie_r2/probe.json): 57.1 GB/s host-to-device and
   // 56.7 GB/s device-to-host with 64 MiB - 1 GiB pinned copies, 97 GB/s both ways at
   // once; a Gen4-trained or x8 link delivers half of that.
   f.min_pcie_h2d_gbps = 45;
@@ -363,7 +363,7 @@ DiagFloors DiagFloors::mi355x_defaults() {
   f.min_hbm_walk_coverage = 0.8;
   // node-level burn: one GPU 15 % behind the node's fastest under the shared load is a
   // cooling or power-delivery outlier (healthy MI355X burns agree within ~1 %,
-  // profiles/diag_burn_r2.json); the node power limit is site-specific (0 = off)
+  // profiles/archive/diag_burn_r2.json); the node power limit is site-specific (0 = off)
   f.min_node_burn_balance = 0.85;
   f.max_node_power_w = 0;
   return f;

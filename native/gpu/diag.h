@@ -12,7 +12,7 @@ namespace bgc::gpu {
 // Performance floors that turn the diagnostics into a health gate: a GPU whose HBM or
 // matrix cores run well below what an MI355X delivers is not advertised, even when every
 // pattern and tile checks out.  Defaults sit ~25 % under the rates measured on MI355X at
-// the node agent's default sizes (profiles/diag_floors_r2.json); 0 disables a floor.
+// the node agent's default sizes (profiles/archive/diag_floors_r2.json); 0 disables a floor.
 struct DiagFloors {
   double min_read_gbps = 0;
   double min_copy_gbps = 0;

@@ -65,7 +65,7 @@ __device__ __forceinline__ u32x4 pattern16(uint64_t i, uint32_t seed) {
 
 // Each block streams one contiguous slab (per-block chunking keeps DRAM pages open and
 // measured 5.57 TB/s copy / 6.19 TB/s read on MI355X vs 5.08 / 5.61 for a grid-stride
-// interleave — tools/probes/hbm_sweep.hip, profiles/hbm_sweep_r1.jsonl).
+// interleave — tools/probes/hbm_sweep.hip, profiles/archive/hbm_sweep_r1.jsonl).
 __device__ __forceinline__ void block_range(uint64_t n16, uint64_t& beg, uint64_t& end) {
   const uint64_t per = (n16 + gridDim.x - 1) / gridDim.x;
   beg = static_cast<uint64_t>(blockIdx.x) * per;
@@ -607,7 +607,7 @@ __global__ __launch_bounds__(64 * WM * WN, (BM * BN >= 256 * 256) ? 1 : 2) void 
 // The 2-buffer kernel above drains every K-tile's loads (vmcnt(0) + barrier) one tile
 // after issuing them; with one 512-thread block per CU a tile's 64 MFMAs per wave
 // (~0.9 us per SIMD) do not cover an HBM/L2 fetch under full load, and the matrix pipe
-// sat idle 42 % of the time (profiles/gemm_soak_r2/pmc_soak_8192.json).  This kernel
+// sat idle 42 % of the time (profiles/archive/gemm_soak_r2/pmc_soak_8192.json).  This kernel
 // keeps the same LDS budget (two K-tiles, 128 KiB) but manages it in eight 16 KiB
 // half-tiles (A rows 0-127 / 128-255, Bt rows 0-127 / 128-255 of each K-tile):
 //

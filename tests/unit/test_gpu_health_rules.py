@@ -267,7 +267,7 @@ MI355X_PCIE = {"device": 0, "bytes": 268435456, "iters": 5, "h2d_gbps": 57.14, "
 
 def test_judge_diag_pcie(nat):
     """Host<->device copy floors and the link state read while the copies ran
-    (values measured on the MI355X box, profiles/pcie_r2/probe.json)."""
+    (values measured on the MI355X box, profiles/archive/pcie_r2/probe.json)."""
     assert json.loads(nat.judge_diag(json.dumps({"pcie": MI355X_PCIE})))["passed"]
     x8 = dict(MI355X_PCIE, link_width=8, h2d_gbps=28.5, d2h_gbps=28.3)
     r = json.loads(nat.judge_diag(json.dumps({"pcie": x8})))

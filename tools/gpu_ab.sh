@@ -9,13 +9,13 @@
 # NPROC > 1 runs torch.distributed.run with that many ranks (the control plane on CPU
 # ranks: BGC_BENCH_CPU=1, never more than the box's GPUs).  Examples (the rounds' studies):
 #
-#   # webhook h2 vs HTTP/1.1 at 8 ranks (profiles/http2_r2)
+#   # webhook h2 vs HTTP/1.1 at 8 ranks (profiles/archive/http2_r2)
 #   tools/gpu_ab.sh -n 8 -r 2 -- h2 '--no-tuned-phase' h1 '--no-tuned-phase --apiserver-arg=--webhook-http1'
-#   # metadata-only watches vs full objects (profiles/metadata_watches_r2)
+#   # metadata-only watches vs full objects (profiles/archive/metadata_watches_r2)
 #   tools/gpu_ab.sh -r 3 -- meta '' full '--controller-env=CONF_METADATA_WATCHES=false'
-#   # kube-lite store lock (profiles/kl_store_lock_r2)
+#   # kube-lite store lock (profiles/archive/kl_store_lock_r2)
 #   tools/gpu_ab.sh -n 8 -r 2 -- rw 'BGC_KL_RWLOCK=writer --no-tuned-phase' mx 'BGC_KL_RWLOCK=mutex --no-tuned-phase'
-#   # glibc tcache depth (profiles/tcache_ab_r1)
+#   # glibc tcache depth (profiles/archive/tcache_ab_r1)
 #   tools/gpu_ab.sh -r 2 -- t64 'GLIBC_TUNABLES=glibc.malloc.tcache_count=64 --steps 300' t7 'GLIBC_TUNABLES=glibc.malloc.tcache_count=7 --steps 300'
 #   # an older build's binaries against this one (profiles/cpuprof_r3)
 #   tools/gpu_ab.sh -r 3 -- base "BGC_BIN_DIR=$PWD/ab/base" cur ''

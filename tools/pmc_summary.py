@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarize rocprofv3 --pmc CSV runs of the diagnostic kernels into derived metrics.
 
-    python3 tools/pmc_summary.py gpurun_out/pmc > profiles/pmc_diag_r1.json
+    python3 tools/pmc_summary.py gpurun_out/pmc > profiles/archive/pmc_diag_r1.json
 
 Expects sub-runs sq/ (SQ_* + GRBM_*), fetch/ (FETCH_SIZE) and write/ (WRITE_SIZE), each with
 <name>_counter_collection.csv and <name>_kernel_trace.csv.

@@ -1,6 +1,6 @@
 """Telemetry poll cost vs device count: a TelemetryPoller over N mock
 MI355X whose backend sleeps the per-call latency measured for amdsmi on MI355X
-(profiles/amdsmi_cost_r2.json: Fast 141 us, Slow 960 us, Ras 1836 us p50 per device).
+(profiles/archive/amdsmi_cost_r2.json: Fast 141 us, Slow 960 us, Ras 1836 us p50 per device).
 Devices are sampled concurrently (one task per GPU), so a poll should cost about one
 device's latency at every N, not N of them.  Writes a JSON summary."""
 import json
@@ -42,4 +42,4 @@ def main(out):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "profiles/telemetry_scaling_r2.json")
+    main(sys.argv[1] if len(sys.argv) > 1 else "profiles/archive/telemetry_scaling_r2.json")

@@ -7,7 +7,7 @@ controller CPU are measured over a window, first with the reference behaviour (e
 re-applies; CONF_SKIP_UNCHANGED=false) and then with this build's default (children already
 as last written are skipped). The requeue period is compressed to make the window short.
 
-    python3 tools/steady_state.py --tenants 2000 --requeue-secs 2 --window 10 > profiles/steady_state_r1.json
+    python3 tools/steady_state.py --tenants 2000 --requeue-secs 2 --window 10 > profiles/archive/steady_state_r1.json
 """
 import argparse
 import json

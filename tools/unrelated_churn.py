@@ -9,7 +9,7 @@ A few tenants are onboarded, then unrelated Namespaces and RoleBindings are crea
 deleted at a steady rate for a window; controller CPU and watch-cache sizes are measured
 with the label selector on and off.
 
-    python3 tools/unrelated_churn.py --rate 400 --window 10 > profiles/unrelated_churn_r2.json
+    python3 tools/unrelated_churn.py --rate 400 --window 10 > profiles/archive/unrelated_churn_r2.json
 """
 import argparse
 import json
