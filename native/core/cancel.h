@@ -25,6 +25,13 @@ class CancelToken {
     for (auto& cb : cbs) cb();
   }
   bool cancelled() const { return cancelled_.load(std::memory_order_acquire); }
+  // Re-arms a cancelled token for another run of what it stops (e.g. a restarted server).
+  // Only once every thread that waited on it has returned.
+  void reset() {
+    std::lock_guard<std::mutex> lk(mu_);
+    cancelled_.store(false, std::memory_order_release);
+    callbacks_.clear();
+  }
 
   // Sleeps up to `d`; returns true if cancelled (early or already).
   template <typename Rep, typename Period>

@@ -925,6 +925,10 @@ void DevicePlugin::watch_loop() {
 }
 
 void DevicePlugin::start() {
+  // after a stop() (an advertiser conflict that has cleared) the plugin serves and registers anew
+  stop_.reset();
+  registered_ = false;
+  kubelet_inode_ = 0;
   ::mkdir(cfg_.plugin_dir.c_str(), 0755);
   if (cfg_.cdi) LOG_INFO("device_plugin") << "CDI spec written to " << write_cdi_spec();
   start_server();

@@ -98,6 +98,7 @@ NodeAgentConfig NodeAgentConfig::from_env(const EnvConfig& env) {
   c.sysfs_root = env.str_or("sysfs_root", c.sysfs_root);
   c.advertiser_check = env.boolean_or("advertiser_check", c.advertiser_check);
   c.take_over = env.boolean_or("take_over", c.take_over);
+  if (env.raw("known_labellers")) c.known_labellers = env.comma_list("known_labellers");
   return c;
 }
 
@@ -219,6 +220,13 @@ Value node_status_patch(const NodeAgentConfig& cfg, const std::vector<GpuInfo>& 
                         {"status", status}});
 }
 
+bool label_owner_conflicts(const NodeAgentConfig& cfg, const std::string& manager, const std::string& operation) {
+  for (const auto& k : cfg.known_labellers) {
+    if (!k.empty() && manager == k) return true;
+  }
+  return operation == "Apply" && manager.rfind("kubectl", 0) != 0;
+}
+
 Value foreign_field_owners(const NodeAgentConfig& cfg, const Value& node) {
   Value out = Value::array();
   const std::string label_key = "f:" + cfg.label_prefix + ".";
@@ -235,8 +243,9 @@ Value foreign_field_owners(const NodeAgentConfig& cfg, const Value& node) {
       }
     }
     if (!labels.empty()) {
-      out.push_back(Value::object({{"kind", "labels"}, {"manager", manager}, {"operation", mf.get_string("operation")},
-                                   {"fields", labels}}));
+      const std::string op = mf.get_string("operation");
+      out.push_back(Value::object({{"kind", "labels"}, {"manager", manager}, {"operation", op}, {"fields", labels},
+                                   {"conflict", label_owner_conflicts(cfg, manager, op)}}));
     }
     // the kubelet writes a device plugin's counts: that is this agent's own plugin unless
     // the agent advertises through the Node status itself
@@ -248,7 +257,7 @@ Value foreign_field_owners(const NodeAgentConfig& cfg, const Value& node) {
     }
     if (!res.empty()) {
       out.push_back(Value::object({{"kind", "capacity"}, {"manager", manager}, {"operation", mf.get_string("operation")},
-                                   {"fields", res}}));
+                                   {"fields", res}, {"conflict", true}}));
     }
   }
   return out;
@@ -378,7 +387,11 @@ bool NodeAgent::check_advertisers() {
   } catch (const std::exception& e) {
     LOG_WARN("node_agent") << "advertiser check: reading node " << cfg_.node_name << " failed: " << e.what();
   }
-  const bool conflict = !found.empty();
+  // Foreign label owners that are no labelling controller (an admin's `kubectl label`) are
+  // reported in /gpus but do not make the agent stand down.
+  const bool conflict = std::any_of(found.items().begin(), found.items().end(), [](const Value& f) {
+    return !f.get("conflict").is_bool() || f.get("conflict").as_bool();
+  });
   const bool down = conflict && !cfg_.take_over;
   const std::string sig = found.dump();
   bool report;
@@ -821,12 +834,20 @@ void NodeAgent::start() {
         const bool was_down = standing_down_.load();
         const bool down = check_advertisers();
         if (down && !was_down && plugin_started_ && !plugin_stopped_.exchange(true)) {
-          // found while advertising: unregister from the kubelet (a stopped plugin is not
-          // restarted; the agent resumes the plugin after a restart once the conflict is gone)
+          // found while advertising: unregister from the kubelet until the conflict clears
           plugin_->stop();
-          LOG_ERROR("node_agent") << "device plugin stopped: another advertiser appeared; restart the agent once it is gone";
+          LOG_ERROR("node_agent") << "device plugin stopped: another advertiser appeared; it starts again once that "
+                                  << "advertiser is gone";
         }
-        if (!down && was_down && !plugin_stopped_ && !stop_.cancelled()) start_plugin();
+        if (!down && was_down && !stop_.cancelled()) {
+          if (plugin_stopped_.exchange(false)) {
+            plugin_->set_health(healthy_flags());
+            plugin_->start();  // registers with the kubelet again
+            LOG_INFO("node_agent") << "device plugin restarted: the other advertiser is gone";
+          } else {
+            start_plugin();
+          }
+        }
         publish();
       } catch (const std::exception& e) {
         LOG_ERROR("node_agent") << "heartbeat publish failed: " << e.what();

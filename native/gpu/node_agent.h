@@ -121,13 +121,21 @@ struct NodeAgentConfig {
   // amd.com/gpu.* labels).  At start and on every heartbeat the agent looks for
   //   * another live device plugin in device_plugin_dir serving resource_name
   //     (foreign_plugins_for), and
-  //   * another field manager on the Node owning label_prefix.* labels or
-  //     status.capacity/allocatable[resource_name] (foreign_field_owners);
+  //   * another field manager on the Node owning status.capacity/allocatable[resource_name],
+  //     or owning label_prefix.* labels as a labelling controller: a server-side apply
+  //     (not kubectl's) or one of known_labellers (foreign_field_owners).  A one-off
+  //     `kubectl label` by an admin is reported but is no conflict;
   // on a finding it logs an error, records a Warning Event (GPUAdvertiserConflict) and
-  // stands down: no device-plugin registration, no label or status writes.  take_over
-  // (CONF_TAKE_OVER) advertises anyway (Event GPUAdvertiserTakeOver).
+  // stands down: no device-plugin registration, no label or status writes.  A plugin
+  // stopped for a conflict found while advertising starts again once a heartbeat finds
+  // the conflict gone.  take_over (CONF_TAKE_OVER) advertises anyway (Event
+  // GPUAdvertiserTakeOver).
   bool advertiser_check = true;
   bool take_over = false;
+  // Field managers that label GPU nodes (CONF_KNOWN_LABELLERS, comma list): AMD's node
+  // labeller, node-feature-discovery.
+  std::vector<std::string> known_labellers = {"amdgpu-node-labeller", "amd-gpu-node-labeller", "node-labeller",
+                                              "nfd-master", "nfd-worker"};
   static NodeAgentConfig from_env(const EnvConfig& env);
 };
 
@@ -153,10 +161,15 @@ json::Value node_labels_patch(const NodeAgentConfig& cfg, const std::vector<GpuI
 json::Value node_status_patch(const NodeAgentConfig& cfg, const std::vector<GpuInfo>& gpus, int healthy,
                               const std::string& unhealthy_reason);
 // Field managers of `node` other than this agent that own what it advertises:
-// [{"kind":"labels"|"capacity","manager":..,"operation":..,"fields":[..]}].  The kubelet's
-// capacity/allocatable entries are its device-plugin bookkeeping and count only when the
-// agent itself advertises through the Node status (no device plugin of its own).
+// [{"kind":"labels"|"capacity","manager":..,"operation":..,"fields":[..],"conflict":bool}].
+// The kubelet's capacity/allocatable entries are its device-plugin bookkeeping and count
+// only when the agent itself advertises through the Node status (no device plugin of its
+// own).  Label owners are a conflict only as labelling controllers (label_owner_conflicts).
 json::Value foreign_field_owners(const NodeAgentConfig& cfg, const json::Value& node);
+// A foreign owner of label_prefix.* labels is another labeller, not an admin's one-off
+// edit: it server-side applies them (kubectl's own managers excepted) or is a known
+// labeller.
+bool label_owner_conflicts(const NodeAgentConfig& cfg, const std::string& manager, const std::string& operation);
 
 class NodeAgent {
  public:

@@ -151,3 +151,48 @@ def test_stands_down_for_fields_owned_by_another_manager(owned):
             c.admin.get("nodes", node)), timeout=10, desc="take-over publish")
         assert got["metadata"]["labels"]["amd.com/gpu.family"] == "gfx950"
         assert got["status"]["capacity"]["amd.com/gpu"] == "8"
+
+
+def test_plugin_stopped_for_a_conflict_restarts_once_it_clears(tmp_path):
+    """a conflict found while advertising used to stop the device plugin
+    until the agent restarted.  Now the plugin serves and registers again once a heartbeat
+    finds the other advertiser gone."""
+    d = str(tmp_path / "dp")
+    kubelet = FakeKubelet(d).start()
+    try:
+        with Cluster(admission=False, controller=False) as c:
+            _agent(c, "mi355x-rs", d, RUST_LOG="info")
+            assert kubelet.wait(lambda: len(_ours(kubelet)) == 1, timeout=10)
+            other = FakeDevicePlugin(d, "amd.com_gpu", OPERATOR_IDS).start()
+            other.register("amd.com/gpu")
+            try:
+                wait_for(lambda: _gpus(c, "mi355x-rs")["advertiser"]["plugin_stopped"], timeout=10, desc="plugin stopped")
+                assert "it starts again once that advertiser is gone" in c.procs["na-mi355x-rs"].output()
+            finally:
+                other.stop()
+            assert kubelet.wait(lambda: len(_ours(kubelet)) == 2, timeout=10), "re-registered after the conflict"
+            g = _gpus(c, "mi355x-rs")["advertiser"]
+            assert not g["plugin_stopped"] and not g["standing_down"]
+            assert "device plugin restarted" in c.procs["na-mi355x-rs"].output()
+    finally:
+        kubelet.stop()
+
+
+def test_an_admins_kubectl_label_is_not_a_conflict():
+    """a one-off `kubectl label` of an amd.com/gpu.* label (an Update by a
+    kubectl manager) is reported, but the agent keeps advertising; a labeller that
+    server-side applies the labels still makes it stand down (test above)."""
+    with Cluster(admission=False, controller=False) as c:
+        node = "mi355x-kl"
+        c.admin.create("nodes", {"apiVersion": "v1", "kind": "Node", "metadata": {"name": node}})
+        c.admin.merge_patch("nodes", node, {"metadata": {"labels": {"amd.com/gpu.note": "reserved-for-lab"}}},
+                            field_manager="kubectl-label")
+        c.start_node_agent(node_name=node, backend="mock", proc_name="na-kl", extra_env={"CONF_HEARTBEAT_SECS": "1"})
+        got = wait_for(lambda: (lambda n: n if n["metadata"].get("labels", {}).get("amd.com/gpu.count") == "8" else None)(
+            c.admin.get("nodes", node)), timeout=10, desc="published despite the admin's label")
+        assert got["metadata"]["labels"]["amd.com/gpu.note"] == "reserved-for-lab"
+        g = _gpus(c, node)["advertiser"]
+        assert not g["standing_down"]
+        [conf] = g["conflicts"]
+        assert conf["manager"] == "kubectl-label" and conf["conflict"] is False
+        assert not _events(c, "GPUAdvertiserConflict", node)
