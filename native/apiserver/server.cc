@@ -273,9 +273,11 @@ struct Stored {
   std::shared_ptr<const Value> obj;
   uint64_t rv = 0;
   // The event line of the commit that stored obj ({"type":"ADDED|MODIFIED","object":<obj>}),
-  // shared with the history: a DELETED event reuses its serialization instead of dumping obj
-  // again.  Null for objects stored outside commit_locked.
-  std::shared_ptr<const std::string> line;
+  // while the watch history still holds it: a DELETED event (or a selector transition)
+  // reuses that serialization instead of dumping obj again.  Weak, so the store never pins
+  // a serialized copy of every live object beyond what history_limit bounds (an object
+  // whose commit has been compacted away is serialized anew when deleted).
+  std::weak_ptr<const std::string> line;
   // Shared and immutable, like obj: a writer's snapshot of the stored object (taken under
   // the store lock) copies two pointers instead of every manager's field set.
   std::shared_ptr<const Managers> managers = no_managers();
@@ -327,9 +329,15 @@ struct EventRec {
   std::shared_ptr<const Value> meta;
   std::shared_ptr<const std::string> line;  // {"type":..,"object":..}\n
   // Updates that changed the object's labels (selector transitions possible): the previous
-  // version's filter view and its committed event line.  Null otherwise.
-  std::shared_ptr<const Value> prev_meta;
-  std::shared_ptr<const std::string> prev_line;
+  // version's filter view and its committed event line, and the transition lines built from
+  // them on first use.  Null for every other event (most of them).
+  struct Transitions {
+    std::shared_ptr<const Value> prev_meta;
+    std::shared_ptr<const std::string> prev_line;
+    std::once_flag added_once, deleted_once;
+    std::string added, added_meta, deleted, deleted_meta;
+  };
+  std::unique_ptr<Transitions> tr;
   // The PartialObjectMetadata form, built once on first use by a metadata-only watch.
   const std::string& metadata_line() const {
     std::call_once(meta_once_, [this] { meta_line_ = partial_metadata_line(*line); });
@@ -337,20 +345,23 @@ struct EventRec {
   }
   // The line a watch with this view receives (transition forms built once, on first use).
   const std::string& line_as(View v, bool meta_only) const {
-    if (v == View::AsIs) return meta_only ? metadata_line() : *line;
-    Transition& t = v == View::Added ? added_ : deleted_;
-    std::call_once(t.once, [&] {
-      t.full = v == View::Added ? retyped_line(*line, "ADDED") : deleted_from_prev();
-      t.meta = partial_metadata_line(t.full);
+    if (v == View::AsIs || !tr) return meta_only ? metadata_line() : *line;
+    Transitions& t = *tr;
+    if (v == View::Added) {
+      std::call_once(t.added_once, [&] {
+        t.added = retyped_line(*line, "ADDED");
+        t.added_meta = partial_metadata_line(t.added);
+      });
+      return meta_only ? t.added_meta : t.added;
+    }
+    std::call_once(t.deleted_once, [&] {
+      t.deleted = deleted_from_prev();
+      t.deleted_meta = partial_metadata_line(t.deleted);
     });
-    return meta_only ? t.meta : t.full;
+    return meta_only ? t.deleted_meta : t.deleted;
   }
 
  private:
-  struct Transition {
-    std::once_flag once;
-    std::string full, meta;
-  };
   // {"type":T,...} -> {"type":<type>,...}
   static std::string retyped_line(const std::string& l, const char* type) {
     const std::string_view t = json::raw_member(l, "type");
@@ -366,7 +377,7 @@ struct EventRec {
   }
   // DELETED with the previous object, its resourceVersion replaced by this event's
   std::string deleted_from_prev() const {
-    std::string_view prev(*prev_line);
+    std::string_view prev(*tr->prev_line);
     while (!prev.empty() && (prev.back() == '\n' || prev.back() == '\r')) prev.remove_suffix(1);
     const std::string_view obj = json::raw_member(prev, "object");
     const std::string_view old_rv = json::raw_member(json::raw_member(obj, "metadata"), "resourceVersion");
@@ -385,7 +396,6 @@ struct EventRec {
   }
   mutable std::once_flag meta_once_;
   mutable std::string meta_line_;
-  mutable Transition added_, deleted_;
 };
 
 struct QueuedEvent {
@@ -1013,8 +1023,8 @@ struct ApiServer::Impl {
     *view = View::AsIs;
     if (sel.empty()) return true;
     const bool now_in = selector_matches(sel, *e.meta);
-    if (!e.prev_meta) return now_in;
-    const bool was_in = selector_matches(sel, *e.prev_meta);
+    if (!e.tr) return now_in;
+    const bool was_in = selector_matches(sel, *e.tr->prev_meta);
     if (now_in && !was_in) *view = View::Added;
     else if (!now_in && was_in) *view = View::Deleted;
     return now_in || was_in;
@@ -1491,20 +1501,19 @@ struct ApiServer::Impl {
     // An update that changes the labels may move the object into or out of a label-selector
     // watch: the event remembers the previous version for those watches (view_for).
     std::shared_ptr<EventRec> rec = pe->rec ? pe->rec : std::make_shared<EventRec>();
-    if (prev && opts.selector_transitions) {
-      std::shared_ptr<const Value> now_filter = pe->filter ? pe->filter : filter_view(obj);
-      std::shared_ptr<const Value> prev_filter = filter_view(*prev->obj);
-      if (prev_filter->get("metadata").get("labels") != now_filter->get("metadata").get("labels")) {
-        rec->prev_meta = std::move(prev_filter);
-        if (prev->line) {
-          rec->prev_line = prev->line;
-        } else {
-          std::string l = "{\"type\":\"MODIFIED\",\"object\":";
-          prev->obj->dump_to(l);
-          l += "}\n";
-          rec->prev_line = std::make_shared<const std::string>(std::move(l));
-        }
+    if (prev && opts.selector_transitions &&
+        prev->obj->get("metadata").get("labels") != obj.get("metadata").get("labels")) {
+      auto t = std::make_unique<EventRec::Transitions>();
+      t->prev_meta = filter_view(*prev->obj);
+      if (auto held = prev->line.lock()) {
+        t->prev_line = std::move(held);
+      } else {
+        std::string l = "{\"type\":\"MODIFIED\",\"object\":";
+        prev->obj->dump_to(l);
+        l += "}\n";
+        t->prev_line = std::make_shared<const std::string>(std::move(l));
       }
+      rec->tr = std::move(t);
     }
     uint64_t new_rv;
     std::string digits;
@@ -1562,7 +1571,8 @@ struct ApiServer::Impl {
     std::string line = "{\"type\":\"DELETED\",\"object\":";
     const size_t obj_at = line.size();
     static const std::string kObjectKey = ",\"object\":";
-    const std::string* committed = it->second.line.get();
+    const std::shared_ptr<const std::string> held = it->second.line.lock();
+    const std::string* committed = held.get();
     const size_t at = committed ? committed->find(kObjectKey) : std::string::npos;
     if (at != std::string::npos && committed->size() >= at + kObjectKey.size() + 2) {
       // the object as its last commit serialized it (same tree, same rv digits)

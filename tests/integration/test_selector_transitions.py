@@ -119,3 +119,24 @@ def test_lossy_mode_drops_transition_events(lossy):
     types = [e["type"] for e in _watch(lossy, base, rv0, 1) if e["type"] != "BOOKMARK"]
     # leaving the selector is never delivered; re-entering is a MODIFIED of an unknown object
     assert types == ["ADDED", "MODIFIED", "MODIFIED", "DELETED"], types
+
+
+def test_events_after_compaction_serialize_the_object_anew(c):
+    """the store no longer pins each live object's last event line; once
+    the history has dropped it, a DELETED event and a selector transition are serialized
+    from the stored object instead, with the same content."""
+    ns = "compacted"
+    c.admin.create("namespaces", {"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": ns}})
+    for n in ("a", "b"):
+        c.admin.create("configmaps", {"apiVersion": "v1", "kind": "ConfigMap",
+                                      "metadata": {"name": n, "labels": {"team": "a"}}, "data": {"v": n}}, namespace=ns)
+    requests.post(c.server + "/_kl/compact", timeout=5).raise_for_status()
+    rv0 = c.admin.list("configmaps", namespace=ns)["metadata"]["resourceVersion"]
+    out = c.admin.merge_patch("configmaps", "a", {"metadata": {"labels": {"team": None}}}, namespace=ns)
+    c.admin.delete("configmaps", "b", namespace=ns)
+    ev = [e for e in _watch(c, f"/api/v1/namespaces/{ns}/configmaps", rv0, 1) if e["type"] != "BOOKMARK"]
+    assert [e["type"] for e in ev] == ["DELETED", "DELETED"]
+    assert ev[0]["object"]["metadata"]["name"] == "a" and ev[0]["object"]["data"] == {"v": "a"}
+    assert ev[0]["object"]["metadata"]["labels"] == {"team": "a"}
+    assert ev[0]["object"]["metadata"]["resourceVersion"] == out["metadata"]["resourceVersion"]
+    assert ev[1]["object"]["metadata"]["name"] == "b" and ev[1]["object"]["data"] == {"v": "b"}
