@@ -872,10 +872,16 @@ void NodeAgent::start() {
         // drift may be another manager writing the same labels: look before forcing ours back
         check_advertisers();
       }
-      try {
-        publish();
-      } catch (const std::exception& e) {
-        LOG_ERROR("node_agent") << "publish after node change failed: " << e.what();
+      // A failed publish (e.g. the first request on a path that was just found dead) is
+      // retried a few times rather than left to the next heartbeat.
+      for (int attempt = 0;; ++attempt) {
+        try {
+          publish();
+          break;
+        } catch (const std::exception& e) {
+          LOG_ERROR("node_agent") << "publish after node change failed: " << e.what();
+          if (attempt == 3 || stop_.wait_for(std::chrono::milliseconds(200 << attempt))) break;
+        }
       }
     };
     w.run(stop_, [&](const kube::WatchEvent& ev) {

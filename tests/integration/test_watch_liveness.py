@@ -156,9 +156,10 @@ def test_node_agent_recovers_from_a_blackholed_apiserver_connection():
             proxy.freeze()
             t_freeze = time.monotonic()
             c.admin.delete("nodes", node)
-            n = wait_for(labelled, timeout=DEADLINE_S + 10, desc="node re-published after the stall")
+            published = lambda: (lambda n: n if n and n.get("status", {}).get("capacity", {}).get("amd.com/gpu") == "8"
+                                 else None)(labelled())
+            wait_for(published, timeout=DEADLINE_S + 10, desc="node re-published after the stall")
             assert time.monotonic() - t_freeze < DEADLINE_S + 10
-            assert n["status"]["capacity"]["amd.com/gpu"] == "8"
             wait_for(lambda: readyz(c.node_agent_port)[0] == 200, timeout=DEADLINE_S + 5, desc="ready again")
             assert c.procs["na-stall"].alive()
         finally:
