@@ -1015,6 +1015,24 @@ def run(args):
                                             "gc_pending": st.get("gc_pending")}
             except Exception:  # noqa: BLE001
                 pass
+            try:  # the periodic malloc_trim pass of each shipped binary (core/process.cc)
+                import requests
+
+                trims = {}
+                for comp, url, verify in (("controller", info["controller"], None),
+                                          ("admission", info["admission"], info["ca"]),
+                                          ("synchronizer", info["synchronizer"], None),
+                                          ("node_agent", info["node_agent"], None)):
+                    txt = requests.get(url + "/metrics", timeout=10, verify=verify).text
+                    vals = {l.split()[0]: float(l.split()[1]) for l in txt.splitlines()
+                            if l.startswith(("bgc_malloc_trim_seconds_sum", "bgc_malloc_trim_seconds_count",
+                                             "bgc_malloc_trim_last_seconds"))}
+                    trims[comp] = {"passes": int(vals.get("bgc_malloc_trim_seconds_count", 0)),
+                                   "total_ms": round(vals.get("bgc_malloc_trim_seconds_sum", 0.0) * 1e3, 3),
+                                   "last_ms": round(vals.get("bgc_malloc_trim_last_seconds", 0.0) * 1e3, 3)}
+                out["malloc_trim"] = trims
+            except Exception:  # noqa: BLE001
+                pass
             try:  # controller cache sizes (bounded-memory check under churn)
                 import requests
 

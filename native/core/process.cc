@@ -12,6 +12,7 @@
 
 #include "core/cpuprof.h"
 #include "core/log.h"
+#include "core/metrics.h"
 
 namespace bgc {
 
@@ -37,9 +38,17 @@ void start_malloc_trimmer() {
     sigset_t all;
     sigfillset(&all);
     pthread_sigmask(SIG_BLOCK, &all, nullptr);
+    // Every trim is timed: it walks the arenas under their locks, so a long one stalls
+    // every allocating thread of the process for that long.
+    auto& hist = metrics::Registry::global().histogram("bgc_malloc_trim_seconds", "Wall time of one malloc_trim pass");
+    auto& last = metrics::Registry::global().gauge("bgc_malloc_trim_last_seconds", "Wall time of the last malloc_trim pass");
     while (true) {
       std::this_thread::sleep_for(std::chrono::seconds(secs));
+      const int64_t t0 = metrics::now_ns();
       malloc_trim(0);
+      const double dt = static_cast<double>(metrics::now_ns() - t0) * 1e-9;
+      hist.observe(dt);
+      last.set(dt);
     }
   }).detach();
 }
