@@ -1015,14 +1015,15 @@ def run(args):
                                             "gc_pending": st.get("gc_pending")}
             except Exception:  # noqa: BLE001
                 pass
-            try:  # the periodic malloc_trim pass of each shipped binary (core/process.cc)
+            try:  # the periodic malloc_trim pass of each process (core/process.cc), kube-lite included
                 import requests
 
                 trims = {}
                 for comp, url, verify in (("controller", info["controller"], None),
                                           ("admission", info["admission"], info["ca"]),
                                           ("synchronizer", info["synchronizer"], None),
-                                          ("node_agent", info["node_agent"], None)):
+                                          ("node_agent", info["node_agent"], None),
+                                          ("kube_lite", info["server"], info["apiserver_verify"])):
                     txt = requests.get(url + "/metrics", timeout=10, verify=verify).text
                     vals = {l.split()[0]: float(l.split()[1]) for l in txt.splitlines()
                             if l.startswith(("bgc_malloc_trim_seconds_sum", "bgc_malloc_trim_seconds_count",

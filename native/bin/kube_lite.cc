@@ -31,6 +31,9 @@ static void usage() {
 }
 
 int main(int argc, char** argv) {
+  // A test server: no malloc_trim passes (one stalls kube-lite for 110-130 ms on the bench's
+  // heap, which would show up in the measured latencies).  BGC_MALLOC_TRIM_SECS still wins.
+  setenv("BGC_MALLOC_TRIM_SECS", "0", /*overwrite=*/0);
   process_init();
   apiserver::Options o;
   std::string port_file;

@@ -41,6 +41,12 @@ std::atomic<void (*)(const std::string&)> g_sink{nullptr};
 // them in batches (one write(2) per batch instead of one per line through stdio's stderr
 // lock).  ERROR lines, and everything before them, are written synchronously; the buffer
 // is flushed at exit and by log::flush().  BGC_LOG_SYNC=1 writes every line directly.
+//
+// The write(2) itself runs outside the buffer lock (under io_mu_, taken before the buffer
+// lock is released, so batches keep their order): a stderr that blocks — a container
+// runtime's pipe that is read slowly, a log file under dirty-page writeback throttling —
+// must not stall every thread that logs a line (the admission server logs each review, the
+// controller each reconcile).
 class AsyncWriter {
  public:
   static AsyncWriter& instance() {
@@ -83,16 +89,22 @@ class AsyncWriter {
         std::this_thread::sleep_for(std::chrono::microseconds(500));
         lk.lock();
         wake_pending_ = false;
-        flush_locked(lk);
+        flush_locked(lk);  // unlocks
+        lk.lock();
       }
     }).detach();
   }
+  // Takes the batch, then writes it with only io_mu_ held.  Returns with `lk` unlocked.
   void flush_locked(std::unique_lock<std::mutex>& lk) {
-    if (buf_.empty()) return;
+    if (buf_.empty()) {
+      lk.unlock();
+      return;
+    }
     std::string out;
     out.swap(buf_);
-    // write outside the buffer lock would reorder with a concurrent synchronous flush;
-    // writes are rare (batched), so keep them under it
+    if (buf_.capacity() == 0) buf_.reserve(out.capacity());
+    std::unique_lock<std::mutex> io(io_mu_);  // the previous batch is out before this one
+    lk.unlock();
     size_t off = 0;
     while (off < out.size()) {
       ssize_t n = ::write(2, out.data() + off, out.size() - off);
@@ -102,9 +114,9 @@ class AsyncWriter {
       }
       off += static_cast<size_t>(n);
     }
-    (void)lk;
   }
-  std::mutex mu_;
+  std::mutex mu_;     // buf_ and the writer's wake-up state
+  std::mutex io_mu_;  // one batch written at a time, in order; taken after mu_
   std::condition_variable cv_;
   std::string buf_;
   bool wake_pending_ = false;

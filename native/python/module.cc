@@ -3,7 +3,10 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <atomic>
+#include <chrono>
 #include <memory>
+#include <thread>
 #include <vector>
 
 #include "core/crypto.h"
@@ -179,6 +182,29 @@ PYBIND11_MODULE(_native, m) {
     bool r = bgc::log::enabled(lv.at(level), target);
     bgc::log::init_from_env();
     return r;
+  });
+  // `threads` threads each log `lines` INFO lines of `width` bytes; returns the slowest single
+  // LOG_INFO call in ms (tests of the asynchronous log writer against a blocked stderr).
+  m.def("log_burst", [](int threads, int lines, int width) {
+    py::gil_scoped_release nogil;
+    bgc::log::init("info");
+    std::atomic<int64_t> worst{0};
+    std::vector<std::thread> ts;
+    const std::string pad(static_cast<size_t>(width), 'x');
+    for (int t = 0; t < threads; ++t) {
+      ts.emplace_back([&, t] {
+        for (int i = 0; i < lines; ++i) {
+          const auto t0 = std::chrono::steady_clock::now();
+          LOG_INFO("burst") << t << " " << i << " " << pad;
+          const int64_t ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+          int64_t cur = worst.load();
+          while (ns > cur && !worst.compare_exchange_weak(cur, ns)) {
+          }
+        }
+      });
+    }
+    for (auto& th : ts) th.join();
+    return static_cast<double>(worst.load()) * 1e-6;
   });
   // A KubeClient built from a $KUBECONFIG-style path list, one request per call (tests of
   // credential plugins and multi-file merging).  Returns (status, body, credential refreshes).
