@@ -212,7 +212,9 @@ def test_debounce_merges_a_burst_of_events_into_one_reconcile():
         hit = re.search(r'^bgc_reconcile_total\{result="ok"\} (\S+)$', m, re.M)
         return float(hit.group(1)) if hit else 0.0
 
-    with Cluster(admission=False, controller_env={"CONF_DEBOUNCE_MS": "400", "CONF_REQUEUE_SECS": "3600"}) as c:
+    # the window is wide enough for the four writes to land in it on a sanitizer build too
+    # (a 400 ms window closed between the writes under ASan, round-5 run 4)
+    with Cluster(admission=False, controller_env={"CONF_DEBOUNCE_MS": "1500", "CONF_REQUEUE_SECS": "3600"}) as c:
         c.admin.create("userbootstraps", {"apiVersion": "bacchus.io/v1", "kind": "UserBootstrap",
                                           "metadata": {"name": "burst"}, "spec": {"kube_username": "burst"}})
         for gpus in ("1", "2", "3"):
