@@ -917,8 +917,14 @@ void Client::set_default_header(const std::string& name, const std::string& valu
 }
 
 void Client::close_idle() {
-  std::lock_guard<std::mutex> lk(mu_);
-  idle_.clear();
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    idle_.clear();
+  }
+  // multiplexed HTTP/2 connections too: the next request dials afresh (streams in flight
+  // keep their connection alive until they end)
+  std::lock_guard<std::mutex> lk(h2_mu_);
+  h2_.clear();
 }
 
 std::unique_ptr<net::Stream> Client::connect() {
@@ -1048,8 +1054,9 @@ bool Client::request_h2(const std::string& method, const std::string& path, cons
     if (done) return true;
     if (refused && !started) continue;  // RFC 9113 8.7: not processed, safe to retry
     if (!st->reset) c->reset_stream(*st, http2::kCancel);
-    throw HttpError(std::string(std::chrono::steady_clock::now() >= deadline ? "timeout" : "stream reset") +
-                    " (HTTP/2): " + method + " " + path);
+    const bool timed_out = std::chrono::steady_clock::now() >= deadline;
+    if (timed_out) close_idle();  // as over HTTP/1.1: the path may be dead
+    throw HttpError(std::string(timed_out ? "timeout" : "stream reset") + " (HTTP/2): " + method + " " + path);
   }
   throw HttpError("request failed after retry (HTTP/2): " + method + " " + path);
 }

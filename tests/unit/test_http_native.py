@@ -205,3 +205,53 @@ def test_h2_inline_concurrent_streams_one_connection(nat, pki):
         assert s.served == 16 * 30 and 0 < s.inline_served <= s.served
     finally:
         s.stop(0)
+
+
+def test_a_timed_out_request_drops_the_pooled_connections():
+    """Round 5: a request that gets no answer within its timeout means the path to the
+    server may be dead, and every pooled connection with it (a wedged proxy, an expired NAT
+    entry).  The client drops them all instead of trying the next one, so the request after
+    the failure dials afresh and succeeds at once."""
+    import http.server
+    import threading
+    import time
+
+    from bacchus_gpu_controller_amd import native
+    from bacchus_gpu_controller_amd.testing.stall_proxy import StallProxy
+
+    class H(http.server.BaseHTTPRequestHandler):
+        protocol_version = "HTTP/1.1"
+
+        def do_GET(self):
+            time.sleep(0.05)  # keeps concurrent requests on separate connections
+            self.send_response(200)
+            self.send_header("Content-Length", "2")
+            self.end_headers()
+            self.wfile.write(b"ok")
+
+        def log_message(self, *a):
+            pass
+
+    srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), H)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    proxy = StallProxy("127.0.0.1", srv.server_address[1]).start()
+    try:
+        c = native().HttpClient(proxy.url, http2=False, timeout_ms=300)
+        ts = [threading.Thread(target=lambda: c.request("GET", "/")) for _ in range(4)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert proxy.accepted >= 3  # several keep-alive connections in the pool
+        proxy.freeze()
+        t0 = time.monotonic()
+        with pytest.raises(RuntimeError, match="timeout"):
+            c.request("GET", "/")
+        assert time.monotonic() - t0 < 0.6  # one timeout, not one per pooled connection
+        before = proxy.accepted
+        t0 = time.monotonic()
+        assert c.request("GET", "/")[0] == 200
+        assert time.monotonic() - t0 < 0.25 and proxy.accepted == before + 1
+    finally:
+        proxy.stop()
+        srv.shutdown()
