@@ -10,6 +10,7 @@
 
 #include "core/log.h"
 #include "core/metrics.h"
+#include "kube/quantity.h"
 
 namespace bgc::controller {
 
@@ -348,17 +349,21 @@ void Reconciler::apply_child(const DesiredChild& c, const std::string& body_hash
 // SSA-shaped coverage: every member `want` sets is in `have` with a covered value.  Maps
 // may hold more (other managers' fields survive a forced apply); ownerReferences is keyed
 // by uid (each wanted reference must be present); other lists are atomic (same length,
-// element by element), as a forced apply replaces them.
-static bool covers(const Value& want, const Value& have, std::string_view key = {}) {
+// element by element), as a forced apply replaces them.  A ResourceQuota's `hard` values
+// are quantities, compared by value: the apiserver stores them canonical ("1000m" -> "1").
+static bool covers(const Value& want, const Value& have, std::string_view key = {}, bool quantities = false) {
   if (want.is_object()) {
     if (!have.is_object()) return false;
     const auto& keys = want.keys();
     const auto& vals = want.values();
     for (size_t i = 0; i < keys.size(); ++i) {
       const Value* h = have.find(keys[i]);
-      if (!h || !covers(vals[i], *h, keys[i])) return false;
+      if (!h || !covers(vals[i], *h, keys[i], key == "hard")) return false;
     }
     return true;
+  }
+  if (quantities && want.is_string() && have.is_string() && want.as_string() != have.as_string()) {
+    return kube::same_quantity(want.as_string(), have.as_string());
   }
   if (want.is_array()) {
     if (!have.is_array()) return false;

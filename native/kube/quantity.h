@@ -1,0 +1,18 @@
+// Kubernetes resource quantities (k8s.io/apimachinery/pkg/api/resource): the apiserver
+// stores a quantity in canonical form ("1000m" comes back as "1", "1024Mi" as "1Gi"), so
+// comparing what the controller applied with what the server holds needs their values.
+#pragma once
+
+#include <optional>
+#include <string_view>
+
+namespace bgc::kube {
+
+// Value of a quantity string: <signed decimal number><suffix>, the suffix one of the binary
+// SI (Ki Mi Gi Ti Pi Ei), the decimal SI (n u m "" k M G T P E) or a decimal exponent
+// (e3, E-2).  nullopt when `s` is not a quantity.
+std::optional<long double> parse_quantity(std::string_view s);
+// Both parse and have the same value (relative tolerance 1e-12).
+bool same_quantity(std::string_view a, std::string_view b);
+
+}  // namespace bgc::kube

@@ -8,6 +8,7 @@
 #include "bench/churn.h"
 #include "controller/reconcile.h"
 #include "kube/events.h"
+#include "kube/quantity.h"
 #include "kube/ratelimit.h"
 #include "kube/runtime.h"
 
@@ -23,6 +24,12 @@ void register_kube(py::module_& m) {
       out.emplace_back(c.rt->plural, c.ns, c.name, std::move(c.body));
     return out;
   }, py::arg("ub_json"), py::arg("label") = false);
+  // Kubernetes quantity value (kube/quantity.h): float, or None when not a quantity
+  m.def("quantity_value", [](const std::string& s) -> py::object {
+    auto v = bgc::kube::parse_quantity(s);
+    return v ? py::object(py::float_(static_cast<double>(*v))) : py::none();
+  });
+  m.def("same_quantity", [](const std::string& a, const std::string& b) { return bgc::kube::same_quantity(a, b); });
   py::class_<bgc::bench::ChurnDriver>(m, "ChurnDriver")
       .def(py::init([](const std::string& server, const std::string& token, const std::string& prefix,
                        int concurrency, const std::string& gpu_key, const std::string& group,

@@ -73,3 +73,24 @@ def test_missing_keys_raise(nat):
         nat.desired_children(json.dumps({"metadata": {"uid": "u"}}), False)
     with pytest.raises(Exception, match="metadata.uid"):
         nat.desired_children(json.dumps({"metadata": {"name": "a"}}), False)
+
+
+@pytest.mark.parametrize("text,value", [
+    ("1", 1), ("0", 0), ("1000m", 1), ("1.5", 1.5), ("-2", -2), ("100u", 1e-4), ("5n", 5e-9),
+    ("1k", 1e3), ("2M", 2e6), ("3G", 3e9), ("1T", 1e12), ("1P", 1e15), ("1E", 1e18),
+    ("1Ki", 1024), ("64Gi", 64 * 2**30), ("0.5Gi", 2**29), ("1Ei", 2**60), ("1e3", 1e3), ("25E-1", 2.5),
+])
+def test_quantity_values(nat, text, value):
+    assert nat.quantity_value(text) == pytest.approx(value, rel=1e-12)
+
+
+@pytest.mark.parametrize("text", ["", "Gi", "1Xi", "1.2.3", "1e", "edit", "1 Gi", "1gi", "ki"])
+def test_not_quantities(nat, text):
+    assert nat.quantity_value(text) is None
+
+
+def test_resync_compares_quota_values_not_spellings(nat):
+    """The apiserver stores quantities canonical ("1000m" comes back as "1"): the resync's
+    coverage check must not call that drift (it would re-apply every such quota forever)."""
+    assert nat.same_quantity("1000m", "1") and nat.same_quantity("1024Mi", "1Gi") and nat.same_quantity("1e3", "1k")
+    assert not nat.same_quantity("1", "2") and not nat.same_quantity("1Gi", "1G") and not nat.same_quantity("x", "x")
