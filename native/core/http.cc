@@ -1070,7 +1070,9 @@ Response Client::request(const std::string& method, const std::string& path, con
   }
   std::string wire = build_request(method, path, body, headers);
   for (int attempt = 0; attempt < 2; ++attempt) {
-    auto s = take_idle();
+    // the retry dials afresh: when the server closed one pooled connection (its idle
+    // timeout), it usually closed the ones opened with it too
+    auto s = attempt == 0 ? take_idle() : nullptr;
     bool reused = s != nullptr;
     if (!s) s = connect();
     if (!s->write_all(wire)) {

@@ -346,6 +346,16 @@ class MockBackend : public Backend {
   Telemetry sample(int index, SampleLevel level) override {
     reload();
     std::unique_lock<std::mutex> lk(mu_);
+    // "sample_hang_ms": every reading blocks this long, as amdsmi does while the driver
+    // resets a wedged GPU; rewriting the fixture without it ends the hang early.
+    for (int64_t hang_start = metrics::now_ns();;) {
+      const Value& hang = fixture_.get("sample_hang_ms");
+      if (!hang.is_number() || static_cast<double>(metrics::now_ns() - hang_start) / 1e6 >= hang.as_double()) break;
+      lk.unlock();
+      std::this_thread::sleep_for(std::chrono::milliseconds(50));
+      reload();
+      lk.lock();
+    }
     int64_t t0 = metrics::now_ns();
     Telemetry t;
     t.index = index;

@@ -27,6 +27,7 @@ NodeAgentConfig NodeAgentConfig::from_env(const EnvConfig& env) {
   c.mock_fixture_path = env.str_or("mock_fixture_path", "");
   c.poll_interval_ms = env.u64_or("poll_interval_ms", 1000);
   c.heartbeat_secs = env.u64_or("heartbeat_secs", 30);
+  c.telemetry_stall_ms = env.u64_or("telemetry_stall_ms", c.telemetry_stall_ms);
   c.resource_name = env.str_or("resource_name", "amd.com/gpu");
   c.partition_resource_name = env.str_or("partition_resource_name", c.partition_resource_name);
   c.label_prefix = env.str_or("label_prefix", "amd.com/gpu");
@@ -348,6 +349,7 @@ void NodeAgent::init() {
   poller_ = std::make_unique<TelemetryPoller>(*backend_, idx, std::chrono::milliseconds(cfg_.poll_interval_ms),
                                               cfg_.health, cfg_.slow_every, cfg_.ras_every, page_limits);
   for (size_t k = 0; k < gpus_.size(); ++k) poller_->set_pcie_max_width(k, gpus_[k].pcie_max_width);
+  poller_->set_stall_timeout(std::chrono::milliseconds(cfg_.telemetry_stall_ms));
   poller_->poll_once();
   bool exists = client_.get_opt(types::Node, "", cfg_.node_name).has_value();
   if (cfg_.create_node && !exists) {
@@ -920,6 +922,7 @@ Value NodeAgent::describe() const {
     out["telemetry"] = tel;
     out["poll_us"] = snap->poll_us;
     out["polls"] = static_cast<unsigned long long>(poller_->polls());
+    out["telemetry_stalled"] = snap->stalled;
   }
   std::string reason;
   out["healthy"] = healthy_count(&reason);

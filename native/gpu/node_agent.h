@@ -47,6 +47,8 @@ struct NodeAgentConfig {
   std::string mock_fixture_path;
   uint64_t poll_interval_ms = 1000;
   uint64_t heartbeat_secs = 30;
+  // a telemetry poll stuck this long marks every GPU unhealthy until one completes (0 = off)
+  uint64_t telemetry_stall_ms = 30000;
   std::string resource_name = "amd.com/gpu";
   // When every GPU runs a sub-device compute partition (DPX/QPX/CPX: one logical device
   // per partition), the devices are advertised under this name instead — the key the

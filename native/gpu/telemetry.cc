@@ -138,6 +138,12 @@ void TelemetryPoller::poll_once() {
   static auto& poll_hist = reg.histogram("bgc_telemetry_poll_seconds", "Wall time of one telemetry poll over all devices");
   static auto& poll_ring = reg.samples("telemetry_poll");
   int64_t t0 = metrics::now_ns();
+  poll_started_ns_.store(t0);
+  // a poll that throws has not stalled: the watchdog only watches polls in progress
+  struct Finished {
+    std::atomic<int64_t>& started;
+    ~Finished() { started.store(0); }
+  } finished{poll_started_ns_};
   auto snap = std::make_shared<Snapshot>();
   snap->devices.reserve(indices_.size());
   bool changed = false;
@@ -227,11 +233,62 @@ void TelemetryPoller::poll_once() {
   snap->poll_seq = polls_.fetch_add(1) + 1;
   poll_hist.observe(snap->poll_us * 1e-6);
   poll_ring.add(snap->poll_us * 1e-6);
+  bool resumed = false;
   {
+    std::lock_guard<std::mutex> sl(stall_mu_);
+    poll_started_ns_.store(0);
+    resumed = stalled_.exchange(false);
     std::lock_guard<std::mutex> lk(snap_mu_);
     snap_ = snap;
   }
-  if (changed && cb_) cb_(*snap);
+  if (resumed) {
+    reg.gauge("bgc_telemetry_stalled", "1 while a telemetry poll has been stuck past the stall timeout").set(0);
+    LOG_WARN("gpu") << "telemetry polls resumed; device health is read from telemetry again";
+  }
+  if (changed || resumed) notify(*snap);
+}
+
+void TelemetryPoller::notify(const Snapshot& s) {
+  std::lock_guard<std::mutex> lk(cb_mu_);
+  if (cb_) cb_(s);
+}
+
+void TelemetryPoller::check_stall() {
+  std::shared_ptr<Snapshot> snap;
+  double stuck_s = 0;
+  {
+    std::lock_guard<std::mutex> sl(stall_mu_);
+    const int64_t started = poll_started_ns_.load();
+    if (started == 0 || stalled_.load()) return;
+    stuck_s = static_cast<double>(metrics::now_ns() - started) / 1e9;
+    if (stuck_s * 1e3 < static_cast<double>(stall_timeout_.count())) return;
+    std::shared_ptr<const Snapshot> last = snapshot();
+    snap = std::make_shared<Snapshot>(*last);
+    snap->stalled = true;
+    if (snap->health.size() < indices_.size()) {
+      for (size_t k = snap->health.size(); k < indices_.size(); ++k) {
+        DeviceHealth h;
+        h.index = indices_[k];
+        snap->health.push_back(h);
+      }
+    }
+    const std::string why = "telemetry stalled: no reading from the " + backend_.name() + " backend for " +
+                            std::to_string(static_cast<long long>(stuck_s)) + " s";
+    for (auto& h : snap->health) {
+      h.healthy = false;
+      h.reason = why;
+    }
+    for (const auto& g : gauges_) g.healthy->set(0);
+    stalled_.store(true);
+    std::lock_guard<std::mutex> lk(snap_mu_);
+    snap_ = snap;
+  }
+  auto& reg = metrics::Registry::global();
+  reg.gauge("bgc_telemetry_stalled", "1 while a telemetry poll has been stuck past the stall timeout").set(1);
+  reg.counter("bgc_telemetry_stalls_total", "Telemetry polls that got stuck past the stall timeout").inc();
+  LOG_ERROR("gpu") << "telemetry poll stuck for " << stuck_s << " s in the " << backend_.name()
+                   << " backend: advertising every GPU unhealthy until a poll completes";
+  notify(*snap);
 }
 
 void TelemetryPoller::start() {
@@ -246,10 +303,17 @@ void TelemetryPoller::start() {
       if (stop_.wait_for(interval_)) break;
     }
   });
+  if (stall_timeout_.count() > 0) {
+    const auto tick = std::clamp(stall_timeout_ / 4, std::chrono::milliseconds(10), std::chrono::milliseconds(1000));
+    watchdog_ = std::thread([this, tick] {
+      while (!stop_.wait_for(tick)) check_stall();
+    });
+  }
 }
 
 void TelemetryPoller::stop() {
   stop_.cancel();
+  if (watchdog_.joinable()) watchdog_.join();
   if (thread_.joinable()) thread_.join();
 }
 

@@ -76,6 +76,9 @@ struct Snapshot {
   double poll_us = 0;  // wall time of the whole poll
   std::vector<Telemetry> devices;
   std::vector<DeviceHealth> health;
+  // Published by the stall watchdog: a poll has been stuck in the backend for longer than
+  // the stall timeout, so every device reads unhealthy until a poll completes again.
+  bool stalled = false;
 };
 
 class TelemetryPoller {
@@ -94,6 +97,10 @@ class TelemetryPoller {
   void set_pcie_max_width(size_t k, int width) {
     if (k < health_.size()) health_[k].pcie_max_width = width;
   }
+  // A poll stuck in the backend (amdsmi blocks while the driver resets a wedged GPU)
+  // longer than this publishes every device unhealthy until a poll completes (0 = off).
+  // Call before start().
+  void set_stall_timeout(std::chrono::milliseconds t) { stall_timeout_ = t; }
   void start();
   void stop();
   // Runs one poll synchronously (tests, and the first poll before start()).
@@ -102,6 +109,7 @@ class TelemetryPoller {
   // Invoked (on the poller thread) whenever any device's health flips.
   void on_health_change(std::function<void(const Snapshot&)> cb);
   uint64_t polls() const { return polls_.load(); }
+  bool stalled() const { return stalled_.load(); }
 
   // Pure health step (exposed for tests).
   static void evaluate(const Telemetry& t, const HealthPolicy& p, DeviceHealth& h);
@@ -129,9 +137,19 @@ class TelemetryPoller {
   mutable std::mutex snap_mu_;
   std::shared_ptr<const Snapshot> snap_;
   std::function<void(const Snapshot&)> cb_;
+  std::mutex cb_mu_;  // the poll thread and the watchdog both report changes
   std::atomic<uint64_t> polls_{0};
+  // Stall watchdog: poll_started_ns_ is the start of the poll in progress (0 = none);
+  // stall_mu_ orders "the poll finished" against "the watchdog declared it stalled".
+  std::chrono::milliseconds stall_timeout_{0};
+  std::mutex stall_mu_;
+  std::atomic<int64_t> poll_started_ns_{0};
+  std::atomic<bool> stalled_{false};
+  void check_stall();
+  void notify(const Snapshot& s);
   CancelToken stop_;
   std::thread thread_;
+  std::thread watchdog_;
 };
 
 }  // namespace bgc::gpu

@@ -444,7 +444,7 @@ def test_prometheus_rule_alerts_reference_exported_series():
     rule = [m for m in ms if m.get("kind") == "PrometheusRule"]
     assert len(rule) == 1 and rule[0]["metadata"]["labels"]["release"] == "prom"
     alerts = {r["alert"]: r for g in rule[0]["spec"]["groups"] for r in g["rules"]}
-    assert {"AMDGPUUnhealthy", "AMDGPUDiagnosticsFailed", "AMDGPUUncorrectableECC", "AMDGPUXGMILinkDown",
+    assert {"AMDGPUUnhealthy", "AMDGPUDiagnosticsFailed", "AMDGPUUncorrectableECC", "AMDGPUXGMILinkDown", "AMDGPUTelemetryStalled",
             "BGCReconcileErrors", "BGCAdmissionSlow"} <= set(alerts)
     assert alerts["AMDGPUXGMILinkDown"]["expr"] == "amd_gpu_xgmi_links_up < 6"
     assert "{{ $labels.gpu }}" in alerts["AMDGPUUnhealthy"]["annotations"]["summary"]  # escaped for Prometheus

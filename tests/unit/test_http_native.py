@@ -255,3 +255,60 @@ def test_a_timed_out_request_drops_the_pooled_connections():
     finally:
         proxy.stop()
         srv.shutdown()
+
+
+def test_a_stale_pooled_connection_is_retried_on_a_fresh_one():
+    """A server that closes idle connections (an idle timeout) may close a pooled one just
+    as the client sends on it, and usually closes the connections opened with it too.  The
+    client's one retry of an unanswered request therefore dials afresh instead of taking the
+    next pooled connection (which would fail the same way)."""
+    import socket
+    import threading
+    import time
+
+    from bacchus_gpu_controller_amd import native
+
+    lsock = socket.socket()
+    lsock.bind(("127.0.0.1", 0))
+    lsock.listen(16)
+    accepted = []
+
+    def serve(conn):
+        buf, served = b"", 0
+        while True:
+            while b"\r\n\r\n" not in buf:
+                d = conn.recv(4096)
+                if not d:
+                    conn.close()
+                    return
+                buf += d
+            buf = buf.split(b"\r\n\r\n", 1)[1]
+            if served == 1:  # the server's idle close, racing the client's second request
+                conn.close()
+                return
+            time.sleep(0.05)  # keeps the first, concurrent requests on separate connections
+            conn.sendall(b"HTTP/1.1 200 OK\r\nContent-Length: 2\r\n\r\nok")
+            served += 1
+
+    def accept_loop():
+        while True:
+            try:
+                conn, _ = lsock.accept()
+            except OSError:
+                return
+            accepted.append(conn)
+            threading.Thread(target=serve, args=(conn,), daemon=True).start()
+
+    threading.Thread(target=accept_loop, daemon=True).start()
+    try:
+        c = native().HttpClient(f"http://127.0.0.1:{lsock.getsockname()[1]}", http2=False, timeout_ms=2000)
+        ts = [threading.Thread(target=lambda: c.request("GET", "/")) for _ in range(2)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert len(accepted) == 2  # two pooled keep-alive connections, both about to fail
+        assert c.request("GET", "/")[0] == 200
+        assert len(accepted) == 3  # the retry dialled a new connection
+    finally:
+        lsock.close()

@@ -13,6 +13,7 @@
 #include <openssl/err.h>
 #include <openssl/rand.h>
 
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -25,12 +26,16 @@ static void slow_exit_work() { std::this_thread::sleep_for(std::chrono::millisec
 int main(int argc, char** argv) {
   std::atexit(slow_exit_work);
   if (argc > 1 && std::strcmp(argv[1], "no-atexit") == 0) OPENSSL_init_crypto(OPENSSL_INIT_NO_ATEXIT, nullptr);
+  static std::atomic<bool> used{false};
   std::thread([] {
     unsigned char b[16];
     RAND_bytes(b, sizeof b);                               // the thread's DRBGs
     ERR_put_error(ERR_LIB_SSL, 0, 1, __FILE__, __LINE__);  // its error queue
+    used.store(true);
     std::this_thread::sleep_for(std::chrono::milliseconds(100));  // ends while the process exits
   }).detach();
-  std::this_thread::sleep_for(std::chrono::milliseconds(20));
+  // exit only once the thread holds its OpenSSL state: on a loaded machine a thread that
+  // first runs after OPENSSL_cleanup crashes in RAND_bytes instead of leaking
+  while (!used.load()) std::this_thread::sleep_for(std::chrono::milliseconds(1));
   return 0;
 }
