@@ -29,6 +29,7 @@
 #include "core/yaml.h"
 #include "crd/schema.h"
 #include "kube/leader.h"
+#include "kube/quantity.h"
 #include "kube/resource.h"
 
 namespace bgc::apiserver {
@@ -1668,6 +1669,39 @@ struct ApiServer::Impl {
     }
   }
 
+  // The apiserver decodes quantities into resource.Quantity and stores their canonical
+  // form ("1000m" -> "1", "2048Mi" -> "2Gi"; a JSON number becomes a string).  kube-lite
+  // does it for the quantity maps the product writes and reads back: ResourceQuota
+  // spec.hard / status.hard / status.used and Node status.capacity / allocatable.
+  static void canonicalize_quantities(const TypeInfo& ti, Value& obj) {
+    if (ti.custom || (ti.rt.plural != "resourcequotas" && ti.rt.plural != "nodes")) return;
+    auto fix = [](Value* m) {
+      if (!m || !m->is_object()) return;
+      for (Value& v : m->items_mut()) {
+        std::string text;
+        if (v.is_string()) text = v.as_string();
+        else if (v.is_int()) text = v.dump();
+        else continue;
+        if (auto c = kube::canonical_quantity(text)) {
+          if (!v.is_string() || *c != text) v = Value(std::move(*c));
+        }
+      }
+    };
+    auto sub = [](Value& o, const char* k) { return o.is_object() ? o.find_mut(k) : nullptr; };
+    Value* spec = sub(obj, "spec");
+    Value* status = sub(obj, "status");
+    if (ti.rt.plural == "resourcequotas") {
+      if (spec) fix(sub(*spec, "hard"));
+      if (status) {
+        fix(sub(*status, "hard"));
+        fix(sub(*status, "used"));
+      }
+    } else if (status) {
+      fix(sub(*status, "capacity"));
+      fix(sub(*status, "allocatable"));
+    }
+  }
+
   // ---------------------------------------------------------------- write path
   using Compute = std::function<std::pair<Value, Managers>(const Stored* cur)>;
 
@@ -1690,6 +1724,7 @@ struct ApiServer::Impl {
       }
       if (!exists && !allow_create) throw not_found(ti.rt, name);
       auto [obj, managers] = compute(exists ? &cur_copy : nullptr);
+      canonicalize_quantities(ti, obj);
       std::string op = exists ? "UPDATE" : "CREATE";
       if (!exists && ti.rt.namespaced) {
         if (!namespace_exists(ns)) {
@@ -1706,6 +1741,7 @@ struct ApiServer::Impl {
       obj["metadata"]["name"] = name;
       if (ti.rt.namespaced) obj["metadata"]["namespace"] = ns;
       else obj["metadata"].erase("namespace");
+      canonicalize_quantities(ti, obj);  // a mutating webhook may have written quantities
       validate_object(ti, name, ns, obj);
       // everything below up to the lock depends only on cur_copy, which the commit re-checks
       if (exists && same_content(obj, *cur_copy.obj) && managers == *cur_copy.managers) {

@@ -30,6 +30,10 @@ void register_kube(py::module_& m) {
     return v ? py::object(py::float_(static_cast<double>(*v))) : py::none();
   });
   m.def("same_quantity", [](const std::string& a, const std::string& b) { return bgc::kube::same_quantity(a, b); });
+  m.def("canonical_quantity", [](const std::string& s) -> py::object {
+    auto c = bgc::kube::canonical_quantity(s);
+    return c ? py::object(py::str(*c)) : py::object(py::none());
+  });
   py::class_<bgc::bench::ChurnDriver>(m, "ChurnDriver")
       .def(py::init([](const std::string& server, const std::string& token, const std::string& prefix,
                        int concurrency, const std::string& gpu_key, const std::string& group,

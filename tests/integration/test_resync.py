@@ -140,3 +140,25 @@ def test_child_deleted_while_its_apply_is_in_flight_is_reapplied():
             c.admin.get_or_none("namespaces", "race1")), timeout=5, desc="namespace re-applied")
         assert again["metadata"]["ownerReferences"][0]["name"] == "race1"
         assert metric(c.controller_port, "bgc_apply_records_dropped_total") >= 1
+
+
+def test_canonicalised_quantities_are_not_drift():
+    """The apiserver stores quantities in canonical form (kube-lite too, since round 5):
+    a quota written as "2048Mi" / "1000m" / "0.5" reads back as "2Gi" / "1" / "500m".  The
+    verification compares values, so the steady state still writes nothing."""
+    env = {"CONF_REQUEUE_SECS": "1", "CONF_RESYNC_SECS": "1"}
+    hard = {"requests.amd.com/gpu": "4", "requests.memory": "2048Mi", "limits.cpu": "1000m",
+            "requests.cpu": "0.5", "requests.storage": "2000"}
+    with Cluster(admission=False, controller_env=env) as c:
+        c.admin.create("userbootstraps", {"apiVersion": "bacchus.io/v1", "kind": "UserBootstrap",
+                                          "metadata": {"name": "canon"},
+                                          "spec": {"kube_username": "canon", "quota": {"hard": hard}}})
+        got = wait_for(lambda: rq(c, "canon"), desc="quota applied")
+        assert got["spec"]["hard"] == {"requests.amd.com/gpu": "4", "requests.memory": "2Gi", "limits.cpu": "1",
+                                       "requests.cpu": "500m", "requests.storage": "2k"}
+        time.sleep(1.5)
+        w0, g0 = writes(c), gets(c, "resourcequotas")
+        time.sleep(3.5)
+        assert writes(c) - w0 == 0
+        assert gets(c, "resourcequotas") - g0 >= 2
+        assert metric(c.controller_port, "bgc_resync_repairs_total") == 0

@@ -94,3 +94,22 @@ def test_resync_compares_quota_values_not_spellings(nat):
     coverage check must not call that drift (it would re-apply every such quota forever)."""
     assert nat.same_quantity("1000m", "1") and nat.same_quantity("1024Mi", "1Gi") and nat.same_quantity("1e3", "1k")
     assert not nat.same_quantity("1", "2") and not nat.same_quantity("1Gi", "1G") and not nat.same_quantity("x", "x")
+
+
+# apimachinery's canonical forms (resource.Quantity.String): parity unpinned against a real
+# apiserver (none on this build's boxes); the cases follow CanonicalizeBytes' rules.
+@pytest.mark.parametrize("text,canon", [
+    ("1000m", "1"), ("0.5", "500m"), ("2000", "2k"), ("1500", "1500"), ("0.1", "100m"), ("0.0001", "100u"),
+    ("12000k", "12M"), ("100m", "100m"), ("1n", "1n"), ("1.1n", "2n"), ("0", "0"), ("0Gi", "0"), ("-1", "-1"),
+    ("1024Mi", "1Gi"), ("2048Mi", "2Gi"), ("1536Mi", "1536Mi"), ("1.5Gi", "1536Mi"), ("0.5Gi", "512Mi"),
+    ("1023Ki", "1023Ki"), ("0.5Ki", "512"), ("1024", "1024"), ("1E", "1E"), ("1000E", "1e21"),
+    ("1e3", "1e3"), ("1.5e3", "1500"), ("12e6", "12e6"), ("1e-10", "1e-9"), ("8", "8"),
+])
+def test_canonical_quantities(nat, text, canon):
+    assert nat.canonical_quantity(text) == canon
+    assert nat.same_quantity(text, canon) or text in ("1.1n", "1e-10")  # rounded up to 1n
+
+
+@pytest.mark.parametrize("text", ["", "abc", "1Xi", ".", "1e", "1 Gi", "1" * 40])
+def test_canonical_rejects_non_quantities(nat, text):
+    assert nat.canonical_quantity(text) is None
