@@ -707,6 +707,7 @@ struct ApiServer::Impl {
   struct GcItem {
     bool is_namespace = false;
     std::string id;  // owner uid or namespace name
+    bool finish_namespace = false;  // then remove the (Terminating) namespace itself
   };
   std::mutex gc_mu;
   std::condition_variable gc_cv;
@@ -1332,14 +1333,54 @@ struct ApiServer::Impl {
   }
 
   // ---------------------------------------------------------------- storage helpers
-  bool namespace_exists(const std::string& ns) {
+  enum class NsPhase { Missing, Active, Terminating };
+  NsPhase namespace_phase(const std::string& ns) {
     TypeInfo* nti = type_by_key(kube::types::Namespace.group + "/v1/namespaces");
-    if (!nti) return false;
+    if (!nti) return NsPhase::Missing;
     const std::string key = obj_key(nti->rt, "", ns);
     auto& sh = nti->store->shard(key);
     SharedStoreLock lk(sh.mu, nti->store->stats);
     auto it = sh.objs.find(key);
-    return it != sh.objs.end() && !it->second.obj->get("metadata").contains("deletionTimestamp");
+    if (it == sh.objs.end()) return NsPhase::Missing;
+    if (!it->second.obj->get("metadata").contains("deletionTimestamp")) return NsPhase::Active;
+    return opts.namespace_termination ? NsPhase::Terminating : NsPhase::Missing;
+  }
+
+  static bool is_core_namespaces(const TypeInfo& ti) { return ti.rt.plural == "namespaces" && ti.rt.group.empty(); }
+
+  // The namespace controller's deletion (k8s.io/kubernetes pkg/controller/namespace): mark
+  // the namespace Terminating and queue its contents; the garbage collector deletes them and
+  // then the namespace (its "kubernetes" spec finalizer).  Caller holds the shard lock.
+  std::shared_ptr<const Value> terminate_namespace_locked(const TypeInfo& ti, const std::string& name, Stored& cur) {
+    Value obj = *cur.obj;
+    obj["metadata"]["deletionTimestamp"] = now_rfc3339();
+    obj["metadata"]["deletionGracePeriodSeconds"] = 0;
+    obj["status"]["phase"] = "Terminating";
+    auto ptr = commit_locked(ti, "", name, std::move(obj), *cur.managers, &cur);
+    std::lock_guard<std::mutex> g(gc_mu);
+    gc_queue.push_back({true, name, true});
+    gc_cv.notify_one();
+    return ptr;
+  }
+
+  // Last step of a namespace's termination: its contents are gone; drop the spec finalizer
+  // and remove it (unless metadata finalizers still hold it).
+  void finish_namespace(const std::string& name) {
+    TypeInfo* nti = type_by_key(kube::types::Namespace.group + "/v1/namespaces");
+    if (!nti) return;
+    const std::string key = obj_key(nti->rt, "", name);
+    auto& sh = nti->store->shard(key);
+    StoreLock lk(sh.mu, nti->store->stats);
+    auto it = sh.objs.find(key);
+    if (it == sh.objs.end() || !it->second.obj->get("metadata").contains("deletionTimestamp")) return;
+    if (it->second.obj->get("metadata").get("finalizers").empty()) {
+      erase_locked(*nti, "", name);
+      return;
+    }
+    Value obj = *it->second.obj;
+    if (obj.get("spec").get("finalizers").empty()) return;
+    obj["spec"]["finalizers"] = Value::array();
+    commit_locked(*nti, "", name, std::move(obj), *it->second.managers, &it->second);
   }
 
   static void render_managed(Value& obj, const Managers& m, const std::string& api_version) {
@@ -1663,9 +1704,14 @@ struct ApiServer::Impl {
           if (alive) continue;
         }
         std::string vns = meta.get_string("namespace"), vname = meta.get_string("name");
+        if (is_core_namespaces(*vti) && opts.namespace_termination) {
+          if (!meta.contains("deletionTimestamp")) terminate_namespace_locked(*vti, vname, it->second);
+          continue;
+        }
         erase_locked(*vti, vns, vname);
         gc_collected.fetch_add(1, std::memory_order_relaxed);
       }
+      if (item.finish_namespace) finish_namespace(item.id);
     }
   }
 
@@ -1727,9 +1773,20 @@ struct ApiServer::Impl {
       canonicalize_quantities(ti, obj);
       std::string op = exists ? "UPDATE" : "CREATE";
       if (!exists && ti.rt.namespaced) {
-        if (!namespace_exists(ns)) {
+        const NsPhase phase = namespace_phase(ns);
+        if (phase == NsPhase::Missing) {
           throw StatusError(404, "NotFound", "namespaces \"" + ns + "\" not found",
                             Value::object({{"name", ns}, {"kind", "namespaces"}}));
+        }
+        if (phase == NsPhase::Terminating) {
+          throw StatusError(
+              403, "Forbidden",
+              ti.rt.plural + " \"" + name + "\" is forbidden: unable to create new content in namespace " + ns +
+                  " because it is being terminated",
+              Value::object({{"name", name}, {"kind", ti.rt.plural},
+                             {"causes", Value::array({Value::object({{"reason", "NamespaceTerminating"},
+                                                                     {"message", "namespace " + ns + " is being terminated"},
+                                                                     {"field", "metadata.namespace"}})})}}));
         }
       }
       // no-op short-circuit (before admission, like the apiserver's update path)
@@ -1760,7 +1817,9 @@ struct ApiServer::Impl {
       if (now_exists != exists || (exists && it->second.rv != cur_copy.rv)) continue;  // raced: retry
       if (exists) {
         // finalizer-gated deletion completes when the last finalizer is removed
-        if (obj.get("metadata").contains("deletionTimestamp") && obj.get("metadata").get("finalizers").empty()) {
+        // (a Terminating namespace waits for its contents: the spec finalizer)
+        if (obj.get("metadata").contains("deletionTimestamp") && obj.get("metadata").get("finalizers").empty() &&
+            !(is_core_namespaces(ti) && opts.namespace_termination && !obj.get("spec").get("finalizers").empty())) {
           erase_locked(ti, ns, name);
           return {cur_copy.obj, 200, nullptr};
         }
@@ -2062,6 +2121,12 @@ struct ApiServer::Impl {
     auto it = sh.objs.find(key);
     if (it == sh.objs.end()) throw not_found(p.ti->rt, p.name);
     const Value& meta = it->second.obj->get("metadata");
+    if (is_core_namespaces(*p.ti) && opts.namespace_termination) {
+      auto ptr = meta.contains("deletionTimestamp") ? it->second.obj
+                                                    : terminate_namespace_locked(*p.ti, p.name, it->second);
+      w.send_json(200, ptr->dump());
+      return;
+    }
     if (!meta.get("finalizers").empty()) {
       if (!meta.contains("deletionTimestamp")) {
         Value obj = *it->second.obj;

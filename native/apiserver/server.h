@@ -43,6 +43,10 @@ struct Options {
   // and one that moves it out as DELETED, as on a real apiserver.  false (kube-lite
   // --no-selector-transitions) drops such events instead: a lost-event scenario.
   bool selector_transitions = true;
+  // Namespace deletion as the namespace controller does it: DELETE marks the namespace
+  // Terminating, creates in it are refused (403, NamespaceLifecycle), its contents are
+  // deleted, then the namespace.  false (--instant-namespace-deletion): removed at once.
+  bool namespace_termination = true;
   int max_watch_seconds = 1800;
   // Watch write coalescing: after a wake-up with few events queued, wait this long for
   // more before writing (fewer wake-ups/syscalls per event at high event rates, at the

@@ -27,6 +27,7 @@ static void usage() {
                "                 [--bookmark-ms N] [--history N] [--watch-coalesce-us N] [--gc-workers N]\n"
                "                 [--opaque-rv] [--continue-ttl-ms N] [--webhook-http1|--webhook-http2] [--webhook-h2-connections N]\n"
                "                 [--write-latency-ms F] [--store-shards N] [--no-selector-transitions]\n"
+               "                 [--instant-namespace-deletion]\n"
                "                 [--manifest file.{json,yaml}]...\n");
 }
 
@@ -62,6 +63,7 @@ int main(int argc, char** argv) {
     else if (a == "--write-latency-ms") o.write_latency_us = static_cast<int64_t>(std::atof(next().c_str()) * 1000.0);
     else if (a == "--opaque-rv") o.opaque_rv = true;
     else if (a == "--no-selector-transitions") o.selector_transitions = false;
+    else if (a == "--instant-namespace-deletion") o.namespace_termination = false;
     else if (a == "--webhook-http1") o.webhook_http2 = false;
     else if (a == "--webhook-http2") o.webhook_http2 = true;
     else if (a == "--webhook-h2-connections") o.webhook_h2_connections = static_cast<size_t>(std::atoi(next().c_str()));

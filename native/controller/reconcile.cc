@@ -14,6 +14,18 @@
 
 namespace bgc::controller {
 
+// A create refused because the tenant's old Namespace is still terminating (a UserBootstrap
+// deleted and created again before the namespace controller finished): expected, and over
+// once the Namespace's DELETED event re-queues the tenant, so not reported as a failure.
+static bool namespace_terminating(const std::exception& err) {
+  const auto* api = dynamic_cast<const kube::ApiError*>(&err);
+  if (!api || api->code() != 403) return false;
+  for (const auto& c : api->status().get("details").get("causes").items()) {
+    if (c.get_string("reason") == "NamespaceTerminating") return true;
+  }
+  return api->message().find("because it is being terminated") != std::string::npos;
+}
+
 using json::Value;
 namespace types = kube::types;
 
@@ -473,7 +485,9 @@ kube::Action Reconciler::reconcile(const kube::ObjPtr& ub_ptr) {
     try {
       apply_child(children[i], hashes[i], children[i].body);
     } catch (const std::exception& e) {
-      LOG_ERROR("controller") << "failed to patch " << children[i].rt->kind << ": " << e.what();
+      if (!namespace_terminating(e)) {
+        LOG_ERROR("controller") << "failed to patch " << children[i].rt->kind << ": " << e.what();
+      }
       throw;
     }
   };
@@ -559,6 +573,14 @@ void Reconciler::apply_all(const std::vector<DesiredChild>& children, const std:
 
 kube::Action Reconciler::error_policy(const kube::ObjPtr& ub, const std::exception& err) {
   const Value& meta = ub->get("metadata");
+  if (namespace_terminating(err)) {
+    static auto& waits = metrics::Registry::global().counter(
+        "bgc_reconcile_namespace_terminating_total", "Reconciles that waited for the tenant's old Namespace to terminate");
+    waits.inc();
+    LOG_INFO("controller") << "\"" << meta.get_string("name", "<unknown>")
+                           << "\": its namespace is still terminating; retrying once it is gone";
+    return kube::Action::requeue_after(std::chrono::milliseconds(cfg_.error_requeue_ms));
+  }
   LOG_ERROR("controller") << "error reconciling \"" << meta.get_string("namespace", "<unknown>") << "/"
                           << meta.get_string("name", "<unknown>") << "\": " << err.what();
   if (events_) events_->record(kube::types::UserBootstrap, *ub, "Warning", "ReconcileFailed", err.what());
