@@ -61,6 +61,7 @@ int main(int argc, char** argv) {
   LOG_INFO("node_agent") << "serving on " << cfg.listen_addr << ":" << server.port();
   agent->start();
   stop->wait();
+  arm_shutdown_deadline(std::chrono::seconds(cfg.shutdown_timeout_secs));
   agent->stop();
   server.stop(std::chrono::milliseconds(1000));
   return 0;

@@ -96,4 +96,15 @@ void process_init() {
   cpuprof::start_from_env();
 }
 
+void arm_shutdown_deadline(std::chrono::milliseconds limit, int code) {
+  if (limit.count() <= 0) return;
+  std::thread([limit, code] {
+    std::this_thread::sleep_for(limit);
+    LOG_ERROR("process") << "shutdown did not finish within " << limit.count()
+                         << " ms (a thread is stuck, e.g. in a driver call); exiting";
+    log::flush();
+    std::_Exit(code);
+  }).detach();
+}
+
 }  // namespace bgc

@@ -2,6 +2,8 @@
 // tuning, OpenSSL's exit behaviour and the optional sampling profiler (core/cpuprof.h).
 #pragma once
 
+#include <chrono>
+
 namespace bgc {
 
 // Call first thing in main().
@@ -14,5 +16,10 @@ void init_openssl();
 // servers: no heap trimming (the sbrk grow/trim cycle cost ~10% of kube-lite CPU), heap
 // growth in 64 MiB steps and a fixed 4 MiB mmap threshold. BGC_MALLOC_TUNE=0 disables it.
 void tune_malloc();
+// Bounds a graceful shutdown once it has started: after `limit` the process logs, flushes
+// the log and exits with `code`.  A thread stuck in a driver call (amdsmi while the driver
+// resets a GPU) would otherwise hold the process until the kubelet's SIGKILL, after its
+// grace period, with nothing in the log.  limit <= 0: no deadline.
+void arm_shutdown_deadline(std::chrono::milliseconds limit, int code = 1);
 
 }  // namespace bgc

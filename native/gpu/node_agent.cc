@@ -28,6 +28,7 @@ NodeAgentConfig NodeAgentConfig::from_env(const EnvConfig& env) {
   c.poll_interval_ms = env.u64_or("poll_interval_ms", 1000);
   c.heartbeat_secs = env.u64_or("heartbeat_secs", 30);
   c.telemetry_stall_ms = env.u64_or("telemetry_stall_ms", c.telemetry_stall_ms);
+  c.shutdown_timeout_secs = env.u64_or("shutdown_timeout_secs", c.shutdown_timeout_secs);
   c.resource_name = env.str_or("resource_name", "amd.com/gpu");
   c.partition_resource_name = env.str_or("partition_resource_name", c.partition_resource_name);
   c.label_prefix = env.str_or("label_prefix", "amd.com/gpu");
@@ -904,11 +905,13 @@ void NodeAgent::start() {
 void NodeAgent::stop() {
   stop_.cancel();
   if (!pcie_lock_path_.empty()) ::unlink(pcie_lock_path_.c_str());
-  if (poller_) poller_->stop();
+  // the device plugin first (unregistered, socket removed), the telemetry poller last: a
+  // poll stuck in amdsmi must not keep the kubelet allocating from a stopping agent
   if (plugin_) plugin_->stop();
   if (heartbeat_.joinable()) heartbeat_.join();
   if (diag_thread_.joinable()) diag_thread_.join();
   if (node_watch_.joinable()) node_watch_.join();
+  if (poller_) poller_->stop();
 }
 
 Value NodeAgent::describe() const {

@@ -49,6 +49,8 @@ struct NodeAgentConfig {
   uint64_t heartbeat_secs = 30;
   // a telemetry poll stuck this long marks every GPU unhealthy until one completes (0 = off)
   uint64_t telemetry_stall_ms = 30000;
+  // a shutdown still running after this long exits anyway (under the kubelet's 30 s grace)
+  uint64_t shutdown_timeout_secs = 20;
   std::string resource_name = "amd.com/gpu";
   // When every GPU runs a sub-device compute partition (DPX/QPX/CPX: one logical device
   // per partition), the devices are advertised under this name instead — the key the

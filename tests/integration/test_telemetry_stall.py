@@ -96,3 +96,22 @@ def test_watchdog_off_keeps_last_readings():
         assert describe(c)["telemetry_stalled"] is False
         c.set_gpu_fixture(NODE, fx)  # let the hung sample return before the agent stops
         time.sleep(0.3)
+
+
+def test_shutdown_is_bounded_while_a_poll_hangs():
+    """SIGTERM while a poll is stuck: the agent stops its device plugin and other threads,
+    and exits after CONF_SHUTDOWN_TIMEOUT_SECS even though the poll thread never returns."""
+    with Cluster(admission=False, controller=False) as c:
+        p = c.start_node_agent(node_name=NODE, backend="mock", poll_interval_ms=50,
+                               extra_env={"CONF_TELEMETRY_STALL_MS": "500", "CONF_SHUTDOWN_TIMEOUT_SECS": "2"})
+        wait_for(lambda: alloc(c) == "8", timeout=10, desc="advertised")
+        hung = copy.deepcopy(json.load(open(c.fixtures[NODE])))
+        hung["sample_hang_ms"] = 600000
+        c.set_gpu_fixture(NODE, hung)
+        wait_for(lambda: alloc(c) == "0", timeout=10, desc="stalled")
+        t0 = time.monotonic()
+        rc = p.stop(timeout=10)
+        took = time.monotonic() - t0
+        assert 1.5 < took < 6, took
+        assert rc == 1
+        assert "shutdown did not finish within 2000 ms" in p.output()
