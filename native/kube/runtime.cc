@@ -591,6 +591,12 @@ void Controller::run(CancelToken& stop, Reconciler reconcile, ErrorPolicy error_
     });
   });
   // owned watchers: trigger_owners
+  auto ignored = [](const char* why) -> metrics::Counter& {
+    return metrics::Registry::global().counter("bgc_controller_child_events_ignored_total",
+                                               "Child watch events that queue no reconcile", {{"reason", why}});
+  };
+  auto& terminating = ignored("terminating");
+  auto& ownerless = ignored("owner_not_cached");
   for (auto& cp : children_) {
     Child* c = cp.get();
     threads.emplace_back([&, c] {
@@ -614,11 +620,22 @@ void Controller::run(CancelToken& stop, Reconciler reconcile, ErrorPolicy error_
             }
             return;
           }
+          // A child on its way out (deletionTimestamp: a Namespace turning Terminating after
+          // its owner was deleted) queues nothing until its DELETED event.
+          if (ev.object->get("metadata").contains("deletionTimestamp")) {
+            terminating.inc();
+            return;
+          }
           if (child_filter_ && !child_filter_(c->rt, *ev.object)) {
             filtered_.fetch_add(1, std::memory_order_relaxed);
             return;
           }
-          for (const auto& k : c->mapper(*ev.object)) queue_.add_after(k, opts_.debounce);
+          // Nor does one whose owner is not in the cache: already deleted (the cascade), or
+          // not seen yet, in which case the owner's own event queues it.
+          for (const auto& k : c->mapper(*ev.object)) {
+            if (primary_store_->get(k)) queue_.add_after(k, opts_.debounce);
+            else ownerless.inc();
+          }
         }
       });
     });

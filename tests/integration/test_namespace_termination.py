@@ -147,3 +147,24 @@ def test_userbootstrap_recreated_while_its_namespace_terminates():
         assert rq["metadata"]["uid"] != first["metadata"]["uid"]
         new_ub = c.admin.get("userbootstraps", "again")
         assert ns["metadata"]["ownerReferences"][0]["uid"] == new_ub["metadata"]["uid"]
+
+
+def test_cascade_after_a_tenant_deletion_queues_no_reconciles():
+    """Deleting a UserBootstrap turns its Namespace Terminating before the children go.  The
+    controller ignores child events that cannot need a reconcile: a child with a
+    deletionTimestamp (until its DELETED event) and one whose owner is no longer cached."""
+    env = {"CONF_REQUEUE_SECS": "3600"}
+    with Cluster(admission=False, controller_env=env) as c:
+        for i in range(3):
+            c.admin.create("userbootstraps", {"apiVersion": "bacchus.io/v1", "kind": "UserBootstrap",
+                                              "metadata": {"name": f"gone{i}"}, "spec": {"kube_username": f"gone{i}"}})
+        for i in range(3):
+            wait_for(lambda: c.admin.get_or_none("namespaces", f"gone{i}"), desc="tenant namespace")
+        r0 = metric(c.controller_port, 'bgc_reconcile_total{result="ok"}')
+        for i in range(3):
+            c.admin.delete("userbootstraps", f"gone{i}")
+        for i in range(3):
+            wait_for(lambda: c.admin.get_or_none("namespaces", f"gone{i}") is None, timeout=10, desc="namespace gone")
+        time.sleep(0.3)
+        assert metric(c.controller_port, 'bgc_controller_child_events_ignored_total{reason="terminating"}') >= 3
+        assert metric(c.controller_port, 'bgc_reconcile_total{result="ok"}') == r0
