@@ -47,6 +47,8 @@ TelemetryPoller::TelemetryPoller(Backend& backend, std::vector<int> indices, std
                        &reg.gauge("amd_gpu_pcie_replays_total", "PCIe replays since boot", l)});
   }
   snap_ = std::make_shared<Snapshot>();
+  // exported from the start (0), so a dashboard or alert sees the series before any stall
+  reg.gauge("bgc_telemetry_stalled", "1 while a telemetry poll has been stuck past the stall timeout");
 }
 
 TelemetryPoller::~TelemetryPoller() { stop(); }
