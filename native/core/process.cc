@@ -4,8 +4,10 @@
 #include <openssl/crypto.h>
 #include <pthread.h>
 #include <signal.h>
+#include <sys/resource.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -35,7 +37,24 @@ void tune_malloc() {
 // pass stalled the synchronizer (85 MB RSS) for 13-15 ms and kube-lite (1.5 GB) for
 // 110-130 ms, every 30 s, which showed up as apply->Ready tails.  Trimming on growth keeps
 // the RSS of a long-running service near its live data after a burst without stalling a
-// steady one.
+// steady one.  A pass also waits for a quiet interval: the process used at most
+// BGC_MALLOC_TRIM_IDLE_PCT (default 5) % of one CPU since the last check, so the stall
+// lands between bursts of work, not inside one (the synchronizer's one pass per bench run
+// fell into a latency window: a 13-15 ms stall of the path to Ready).  A process that is
+// never quiet still trims once its RSS has passed 4x the previous trim's (and 4x the minimum).
+TrimDecision malloc_trim_decision(long rss, long baseline, long min_bytes, double busy_pct, double idle_pct) {
+  if (rss <= min_bytes || rss * 2 <= baseline * 3) return TrimDecision::Skip;
+  if (busy_pct > idle_pct && rss < std::max(baseline, min_bytes) * 4) return TrimDecision::Defer;
+  return TrimDecision::Trim;
+}
+
+static double cpu_seconds() {
+  struct rusage ru {};
+  if (getrusage(RUSAGE_SELF, &ru) != 0) return 0;
+  return static_cast<double>(ru.ru_utime.tv_sec + ru.ru_stime.tv_sec) +
+         static_cast<double>(ru.ru_utime.tv_usec + ru.ru_stime.tv_usec) * 1e-6;
+}
+
 static long rss_bytes() {
   long pages_total = 0, pages_rss = 0;
   if (FILE* f = std::fopen("/proc/self/statm", "r")) {
@@ -51,7 +70,9 @@ void start_malloc_trimmer() {
   if (secs <= 0) return;
   const char* m = std::getenv("BGC_MALLOC_TRIM_MIN_MB");
   const long min_bytes = (m ? std::atol(m) : 64) << 20;
-  std::thread([secs, min_bytes] {
+  const char* ip = std::getenv("BGC_MALLOC_TRIM_IDLE_PCT");
+  const double idle_pct = ip ? std::atof(ip) : 5.0;
+  std::thread([secs, min_bytes, idle_pct] {
     // Never take process signals here: SIGTERM/SIGINT are collected by the sigwait thread
     // that install_shutdown_signals starts (this thread exists before that mask is set).
     sigset_t all;
@@ -61,12 +82,19 @@ void start_malloc_trimmer() {
     auto& hist = reg.histogram("bgc_malloc_trim_seconds", "Wall time of one malloc_trim pass");
     auto& last = reg.gauge("bgc_malloc_trim_last_seconds", "Wall time of the last malloc_trim pass");
     auto& skipped = reg.counter("bgc_malloc_trim_skipped_total", "Trim checks that found the RSS below the trigger");
+    auto& deferred = reg.counter("bgc_malloc_trim_deferred_total",
+                                 "Trim checks that found the RSS grown but the process busy");
     long baseline = rss_bytes();
+    double cpu0 = cpu_seconds();
     while (true) {
       std::this_thread::sleep_for(std::chrono::seconds(secs));
       const long rss = rss_bytes();
-      if (rss <= min_bytes || rss * 2 <= baseline * 3) {
-        skipped.inc();
+      const double cpu = cpu_seconds();
+      const double busy_pct = (cpu - cpu0) * 100.0 / static_cast<double>(secs);
+      cpu0 = cpu;
+      const TrimDecision d = malloc_trim_decision(rss, baseline, min_bytes, busy_pct, idle_pct);
+      if (d != TrimDecision::Trim) {
+        (d == TrimDecision::Skip ? skipped : deferred).inc();
         continue;
       }
       const int64_t t0 = metrics::now_ns();

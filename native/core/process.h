@@ -16,6 +16,11 @@ void init_openssl();
 // servers: no heap trimming (the sbrk grow/trim cycle cost ~10% of kube-lite CPU), heap
 // growth in 64 MiB steps and a fixed 4 MiB mmap threshold. BGC_MALLOC_TUNE=0 disables it.
 void tune_malloc();
+// The periodic trimmer's rule (process.cc): Skip while the RSS is under the minimum or under
+// 1.5x the RSS the previous pass left; Defer while the process used more than idle_pct % of
+// one CPU since the last check, unless the RSS passed 4x max(previous, minimum); else Trim.
+enum class TrimDecision { Skip, Defer, Trim };
+TrimDecision malloc_trim_decision(long rss, long baseline, long min_bytes, double busy_pct, double idle_pct);
 // Bounds a graceful shutdown once it has started: after `limit` the process logs, flushes
 // the log and exits with `code`.  A thread stuck in a driver call (amdsmi while the driver
 // resets a GPU) would otherwise hold the process until the kubelet's SIGKILL, after its

@@ -16,6 +16,7 @@
 #include "core/yaml.h"
 #include "crd/schema.h"
 #include "core/log.h"
+#include "core/process.h"
 #include "kube/client.h"
 
 namespace py = pybind11;
@@ -182,6 +183,13 @@ PYBIND11_MODULE(_native, m) {
     bool r = bgc::log::enabled(lv.at(level), target);
     bgc::log::init_from_env();
     return r;
+  });
+  m.def("malloc_trim_decision", [](long rss, long baseline, long min_bytes, double busy_pct, double idle_pct) {
+    switch (bgc::malloc_trim_decision(rss, baseline, min_bytes, busy_pct, idle_pct)) {
+      case bgc::TrimDecision::Skip: return "skip";
+      case bgc::TrimDecision::Defer: return "defer";
+      default: return "trim";
+    }
   });
   // `threads` threads each log `lines` INFO lines of `width` bytes; returns the slowest single
   // LOG_INFO call in ms (tests of the asynchronous log writer against a blocked stderr).
