@@ -128,9 +128,14 @@ void arm_shutdown_deadline(std::chrono::milliseconds limit, int code) {
   if (limit.count() <= 0) return;
   std::thread([limit, code] {
     std::this_thread::sleep_for(limit);
-    LOG_ERROR("process") << "shutdown did not finish within " << limit.count()
-                         << " ms (a thread is stuck, e.g. in a driver call); exiting";
-    log::flush();
+    // the line is written from a thread of its own: a blocked stderr must not keep the
+    // process alive past the deadline
+    std::thread([limit] {
+      LOG_ERROR("process") << "shutdown did not finish within " << limit.count()
+                           << " ms (a thread is stuck, e.g. in a driver call); exiting";
+      log::flush();
+    }).detach();
+    std::this_thread::sleep_for(std::chrono::milliseconds(500));
     std::_Exit(code);
   }).detach();
 }
