@@ -228,6 +228,8 @@ int Synchronizer::run(CancelToken& stop) {
     std::vector<std::string> versions;  // UB versions acted on or produced by our writes
   };
   std::unordered_map<std::string, Acted> acted;
+  static auto& tracked = metrics::Registry::global().gauge(
+      "bgc_sync_tracked_userbootstraps", "UserBootstraps with a remembered sync (dropped when one is deleted)");
   // CONF_EXIT_ON_ERROR=false only: per-UserBootstrap exponential backoff plus an overall
   // retry budget (client-go's controller rate limiter) instead of a fixed delay
   kube::RetryLimiter retries(std::chrono::milliseconds(cfg_.retry_base_ms), std::chrono::milliseconds(cfg_.retry_max_ms),
@@ -248,6 +250,7 @@ int Synchronizer::run(CancelToken& stop) {
         } else {
           std::lock_guard<std::mutex> g(acted_mu);
           acted.erase(kube::meta_name(*ev.object));
+          tracked.set(static_cast<double>(acted.size()));
         }
       });
     });
@@ -277,7 +280,10 @@ int Synchronizer::run(CancelToken& stop) {
               if (sync_one(*ub, &produced)) {
                 ub_latency.add(static_cast<double>(metrics::now_ns() - t0) * 1e-9);
                 std::lock_guard<std::mutex> g(acted_mu);
-                acted[key] = Acted{gen, std::move(produced)};
+                // not for a UB deleted meanwhile: its DELETED event (store first, then
+                // this map, under acted_mu) may already have run, and the entry would stay
+                if (store.get(key)) acted[key] = Acted{gen, std::move(produced)};
+                tracked.set(static_cast<double>(acted.size()));
               }
               retries.forget(key);
             } catch (const std::exception& e) {

@@ -276,3 +276,32 @@ def test_webhook_down_retries_back_off_then_converge(google):
         obj = wait_for(lambda: (lambda o: o if o.get("status", {}).get("synchronized_with_sheet") else None)(
             c.admin.get("userbootstraps", "gina")), timeout=5, desc="gina converged")
         assert obj["spec"]["quota"] == {"hard": expected_hard(3)}
+
+
+def test_deleted_userbootstraps_leave_no_sync_state(google):
+    """Watch mode remembers, per UserBootstrap, which version it last synced (so its own
+    writes' echoes are not synced again).  The entry goes with the UserBootstrap, also for
+    one deleted while its sync was in flight: bgc_sync_tracked_userbootstraps returns to 0."""
+    users = [f"churn{i:02d}" for i in range(40)]
+    google.set_rows([{"id_username": u} for u in users])
+    with Cluster() as c:
+        c.start_synchronizer(google, interval=3600, extra_env={"CONF_WATCH": "true", "CONF_WORKERS": "8"})
+
+        def tracked():
+            for line in requests.get(f"http://127.0.0.1:{c.sync_port}/metrics", timeout=5).text.splitlines():
+                if line.startswith("bgc_sync_tracked_userbootstraps "):
+                    return float(line.split()[1])
+            return None
+
+        for u in users:
+            c.as_user(f"oidc:{u}", ["gpu"]).create("userbootstraps", ub(u))
+        # delete half right away (their syncs may be in flight), the rest once synced
+        for u in users[::2]:
+            c.admin.delete("userbootstraps", u)
+        for u in users[1::2]:
+            wait_for(lambda: c.admin.get("userbootstraps", u).get("status", {}).get("synchronized_with_sheet"),
+                     timeout=15, desc=f"{u} synced")
+        assert tracked() >= 1
+        for u in users[1::2]:
+            c.admin.delete("userbootstraps", u)
+        wait_for(lambda: tracked() == 0, timeout=10, desc="no sync state left")
