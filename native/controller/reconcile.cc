@@ -592,6 +592,8 @@ kube::Action Reconciler::error_policy(const kube::ObjPtr& ub, const std::excepti
       Shard& sh = shard(lower(owner));
       std::lock_guard<std::mutex> lk(sh.mu);
       n = ++sh.failures[owner];
+      // a UserBootstrap deleted meanwhile (forget_owner may have run already) keeps no count
+      if (!owner_live(owner, meta.get_string("uid"))) sh.failures.erase(owner);
     }
     const int shift = std::min(n - 1, 30);
     delay = std::min<int64_t>(cfg_.error_requeue_ms, cfg_.error_backoff_base_ms << shift);
