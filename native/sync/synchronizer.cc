@@ -248,6 +248,7 @@ int Synchronizer::run(CancelToken& stop) {
         } else if (ev.type != kube::WatchEvent::Type::Deleted) {
           queue.add(kube::meta_name(*ev.object));
         } else {
+          retries.forget(kube::meta_name(*ev.object));  // a failing UB that is gone retries no more
           std::lock_guard<std::mutex> g(acted_mu);
           acted.erase(kube::meta_name(*ev.object));
           tracked.set(static_cast<double>(acted.size()));
