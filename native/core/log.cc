@@ -124,6 +124,32 @@ class AsyncWriter {
 };
 
 bool g_sync_writes = std::getenv("BGC_LOG_SYNC") && std::string(std::getenv("BGC_LOG_SYNC")) == "1";
+// BGC_LOG_FORMAT=json: one JSON object per line in tracing-subscriber's `fmt().json()` layout
+// ({"timestamp","level","fields":{"message"},"target"}), for log pipelines that parse it.
+bool g_json = std::getenv("BGC_LOG_FORMAT") && std::string(std::getenv("BGC_LOG_FORMAT")) == "json";
+
+void append_json_string(std::string& out, std::string_view s) {
+  static const char kHex[] = "0123456789abcdef";
+  out.push_back('"');
+  for (unsigned char c : s) {
+    switch (c) {
+      case '"': out.append("\\\""); break;
+      case '\\': out.append("\\\\"); break;
+      case '\n': out.append("\\n"); break;
+      case '\r': out.append("\\r"); break;
+      case '\t': out.append("\\t"); break;
+      default:
+        if (c < 0x20) {
+          out.append("\\u00");
+          out.push_back(kHex[c >> 4]);
+          out.push_back(kHex[c & 15]);
+        } else {
+          out.push_back(static_cast<char>(c));
+        }
+    }
+  }
+  out.push_back('"');
+}
 
 bool parse_level(std::string s, Level& out) {
   for (auto& c : s) c = static_cast<char>(std::tolower(static_cast<unsigned char>(c)));
@@ -241,9 +267,20 @@ void write(Level lvl, std::string_view target, std::string_view msg) {
   ts[date_len + 6] = 'Z';
   ts[date_len + 7] = '\0';
   std::string line;
-  line.reserve(msg.size() + target.size() + 48);
-  line.append(ts).append(" ").append(level_name(lvl)).append(" ");
-  line.append(target).append(": ").append(msg).push_back('\n');
+  line.reserve(msg.size() + target.size() + 80);
+  if (g_json) {
+    std::string_view lv = level_name(lvl);
+    while (!lv.empty() && lv.front() == ' ') lv.remove_prefix(1);
+    line.append("{\"timestamp\":\"").append(ts).append("\",\"level\":\"").append(lv);
+    line.append("\",\"fields\":{\"message\":");
+    append_json_string(line, msg);
+    line.append("},\"target\":");
+    append_json_string(line, target);
+    line.append("}\n");
+  } else {
+    line.append(ts).append(" ").append(level_name(lvl)).append(" ");
+    line.append(target).append(": ").append(msg).push_back('\n');
+  }
   if (auto sink = g_sink.load()) {
     sink(line);
     return;

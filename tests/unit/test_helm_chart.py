@@ -478,3 +478,18 @@ def test_grafana_dashboard_configmap():
     used = {re.sub(r"_bucket$", "", n) for p in dash["panels"] for t in p["targets"]
             for n in re.findall(r"\b((?:amd_gpu|bgc)_[a-z0-9_]+)", t["expr"])}
     assert used and used <= exported, used - exported
+
+
+def test_log_format_json_reaches_every_service():
+    def envs(ms):
+        out = {}
+        for o in ms:
+            if o.get("kind") in ("Deployment", "DaemonSet"):
+                c = o["spec"]["template"]["spec"]["containers"][0]
+                out[o["metadata"]["name"]] = {e["name"]: e.get("value") for e in c.get("env", [])}
+        return out
+
+    default = envs(render({"nodeAgent": {"enabled": True}}))
+    assert all("BGC_LOG_FORMAT" not in e for e in default.values())
+    js = envs(render({"logFormat": "json", "nodeAgent": {"enabled": True}}))
+    assert len(js) == 4 and all(e.get("BGC_LOG_FORMAT") == "json" for e in js.values()), js
