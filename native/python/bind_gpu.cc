@@ -42,6 +42,7 @@ std::string snapshot_json(const bgc::gpu::Snapshot& s) {
     hs.push_back(Value::object({{"index", h.index}, {"healthy", h.healthy}, {"reason", h.reason}}));
   }
   v["health"] = hs;
+  v["stalled"] = s.stalled;
   return v.dump();
 }
 
@@ -113,16 +114,19 @@ void register_gpu(py::module_& m) {
 
   py::class_<PyPoller>(m, "TelemetryPoller")
       .def(py::init([](std::shared_ptr<PyBackend> b, std::vector<int> idx, int interval_ms, const std::string& policy,
-                       int slow_every, int ras_every, std::vector<uint64_t> page_limits) {
+                       int slow_every, int ras_every, std::vector<uint64_t> page_limits, int stall_ms) {
              auto p = std::make_unique<PyPoller>();
              p->backend = b;
              p->poller = std::make_unique<bgc::gpu::TelemetryPoller>(
                  *b->b, idx, std::chrono::milliseconds(interval_ms), policy_from_json(policy), slow_every, ras_every,
                  std::move(page_limits));
+             p->poller->set_stall_timeout(std::chrono::milliseconds(stall_ms));
              return p;
            }),
            py::arg("backend"), py::arg("indices"), py::arg("interval_ms") = 1000, py::arg("policy") = "{}",
-           py::arg("slow_every") = 10, py::arg("ras_every") = 60, py::arg("page_limits") = std::vector<uint64_t>{})
+           py::arg("slow_every") = 10, py::arg("ras_every") = 60, py::arg("page_limits") = std::vector<uint64_t>{},
+           py::arg("stall_ms") = 0)
+      .def("stalled", [](PyPoller& p) { return p.poller->stalled(); })
       .def("start", [](PyPoller& p) { p.poller->start(); })
       .def("stop", [](PyPoller& p) {
         py::gil_scoped_release nogil;

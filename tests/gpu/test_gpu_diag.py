@@ -65,3 +65,22 @@ def test_telemetry_poller_real_device():
     assert p.polls() >= 3
     assert snap["devices"][0]["ok"]
     assert snap["health"][0]["healthy"]
+
+
+def test_telemetry_watchdog_quiet_on_real_device():
+    """The stall watchdog (CONF_TELEMETRY_STALL_MS) must not fire on a healthy MI355X: real
+    amdsmi polls finish far inside even a 250 ms stall timeout."""
+    import time
+
+    from bacchus_gpu_controller_amd import native
+
+    n = native()
+    p = n.TelemetryPoller(n.gpu_backend("amdsmi", ""), [0], 20, stall_ms=250)
+    p.poll_once()
+    p.start()
+    time.sleep(1.5)
+    p.stop()
+    snap = json.loads(p.snapshot())
+    assert p.polls() >= 20
+    assert not p.stalled() and not snap["stalled"]
+    assert snap["health"][0]["healthy"], snap["health"]

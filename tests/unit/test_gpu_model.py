@@ -25,6 +25,38 @@ def test_poller_side_thread(nat):
     assert all(h["healthy"] for h in snap["health"])
 
 
+def test_poller_stall_watchdog(nat):
+    """A poll stuck in the backend past stall_ms publishes every device unhealthy; the poll
+    that finally completes publishes the real readings again (native/gpu/telemetry.cc)."""
+    fx = json.loads(nat.default_mi355x_fixture(2))
+    fx["sample_hang_ms"] = 600  # every reading blocks this long
+    b = nat.gpu_backend("mock", json.dumps(fx))
+    p = nat.TelemetryPoller(b, [0, 1], 5000, stall_ms=150)
+    p.start()  # the first poll hangs for 600 ms
+    time.sleep(0.4)
+    snap = json.loads(p.snapshot())
+    assert p.stalled() and snap["stalled"]
+    assert [h["healthy"] for h in snap["health"]] == [False, False]
+    assert all("telemetry stalled" in h["reason"] for h in snap["health"])
+    deadline = time.time() + 3
+    while p.polls() < 1 and time.time() < deadline:
+        time.sleep(0.02)
+    snap = json.loads(p.snapshot())
+    p.stop()
+    assert not snap["stalled"] and all(h["healthy"] for h in snap["health"])
+    assert all(d["ok"] for d in snap["devices"])
+
+
+def test_poller_without_stall_timeout_never_stalls(nat):
+    fx = json.loads(nat.default_mi355x_fixture(1))
+    fx["sample_hang_ms"] = 300
+    p = nat.TelemetryPoller(nat.gpu_backend("mock", json.dumps(fx)), [0], 5000)
+    p.start()
+    time.sleep(0.2)
+    assert not p.stalled() and not json.loads(p.snapshot())["stalled"]
+    p.stop()
+
+
 def test_health_hysteresis(nat):
     hot = {"temp_hotspot_c": 120}
     ok = {"temp_hotspot_c": 50}
