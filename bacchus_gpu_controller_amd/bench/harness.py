@@ -778,7 +778,11 @@ def run(args):
     conc = args.concurrency if args.concurrency_scope == "rank" else max(1, -(-args.concurrency // d.world))
     semantics0 = "reference" if args.reference_semantics else args.semantics
     phases = [_Phase("m", conc, args.webhook_protocol, semantics0, args.write_latency_ms, args.warmup, args.steps)]
-    if args.tuned_phase and tuned != conc:
+    # The secondary closed-loop phases (tuned concurrency, HTTP/1.1 webhook, the 2 ms
+    # write-latency arms) run at N=1 only: at N ranks each does N times the work (weak
+    # scaling) and the scaling runs report the headline alone.
+    secondary = d.world == 1
+    if args.tuned_phase and tuned != conc and secondary:
         phases.append(_Phase("t", tuned, args.webhook_protocol, semantics0, args.write_latency_ms,
                              args.warmup, args.steps))
     if args.isolated_phase and d.world == 1:
@@ -786,7 +790,7 @@ def run(args):
         # disjoint CPUs: how much of the headline latencies is queueing behind the fixtures
         phases.append(_Phase("pi", conc, args.webhook_protocol, semantics0, args.write_latency_ms,
                              args.warmup, args.steps, isolated=True))
-    if args.http1_phase and args.webhook_protocol == "h2":
+    if args.http1_phase and args.webhook_protocol == "h2" and secondary:
         # secondary: the same load with the webhook called over HTTP/1.1 (keep-alive pool)
         phases.append(_Phase("w", conc, "http/1.1", semantics0, args.write_latency_ms, args.warmup, args.steps))
     semantics = "reference" if args.reference_semantics else args.semantics
@@ -804,7 +808,7 @@ def run(args):
         # ... then the reference controller at the same rates, while it runs
         phases += [_Phase(f"qr{i}", 0, args.webhook_protocol, "reference-controller", args.write_latency_ms, 0, 0,
                           rate=r) for i, r in enumerate(rates)]
-        if args.arm_write_latency_ms > 0:
+        if args.arm_write_latency_ms > 0 and secondary:
             phases.append(_Phase("rl", conc, args.webhook_protocol, "reference-controller",
                                  args.arm_write_latency_ms, args.arm_warmup, args.arm_steps))
             phases.append(_Phase("ml", conc, args.webhook_protocol, "this", args.arm_write_latency_ms,

@@ -43,7 +43,8 @@ def test_bench_two_ranks_gloo():
     for k in ("controller", "admission", "synchronizer", "node_agent", "kube_lite", "load_driver", "product_total"):
         assert k in cpu and cpu[k] >= 0
     assert d["apiserver_requests_per_cr"] > 0
-    assert d["tuned"]["concurrency_per_rank"] < 50 and d["tuned"]["failed_crs"] == 0
+    # N>1: the secondary closed-loop phases are N=1 only (they would do N times the work)
+    assert "tuned" not in d and "webhook_http1" not in d and "write_latency_2ms" not in d
     # the open-loop phase splits its offered rate over the ranks
     q = d["latency_at_rate"]["this"]["200"]
     assert q["offered_rate"] == 200 and q["ready_crs"] == 200 and q["failed_crs"] == 0
