@@ -1,10 +1,12 @@
 #include "sync/synchronizer.h"
 
 #include <algorithm>
+#include <atomic>
 #include <iterator>
 #include <thread>
 #include <unordered_map>
 
+#include "core/http.h"
 #include "core/json_patch.h"
 #include "core/log.h"
 #include "core/metrics.h"
@@ -51,6 +53,25 @@ std::shared_ptr<const RowIndex> Synchronizer::index() const {
 static metrics::Counter& drive_exports(const char* reason) {
   return metrics::Registry::global().counter("bgc_drive_exports_total", "Google Drive sheet exports issued",
                                              {{"reason", reason}});
+}
+
+// Readiness ("sheet" check behind /readyz): the last sheet export that succeeded, and how old
+// it may get.  Process-wide, like the registry the check lives in.
+static std::atomic<int64_t> g_sheet_ok_ns{0};
+static std::atomic<int64_t> g_sheet_stale_ms{0};
+
+static bool sheet_ready(std::string* why) {
+  const int64_t ok = g_sheet_ok_ns.load();
+  if (ok == 0) {
+    if (why) *why = "the sheet has not been read yet";
+    return false;
+  }
+  const int64_t age_ms = (metrics::now_ns() - ok) / 1000000;
+  if (age_ms > g_sheet_stale_ms.load()) {
+    if (why) *why = "last successful sheet read " + std::to_string(age_ms / 1000) + " s ago";
+    return false;
+  }
+  return true;
 }
 
 void Synchronizer::refresh() {
@@ -103,6 +124,7 @@ void Synchronizer::refresh_locked() {
     index_ = idx;
   }
   last_refresh_ns_.store(metrics::now_ns());
+  g_sheet_ok_ns.store(last_refresh_ns_.load());
   // A new generation re-evaluates every UserBootstrap (the echo filter's decisions were made
   // against the old rows); an unchanged sheet (the periodic tick's re-read) keeps them, so
   // a tenant whose own writes have not echoed yet is not written a second time.
@@ -214,6 +236,10 @@ static const json::Projection& ub_watch_projection() {
 }
 
 int Synchronizer::run(CancelToken& stop) {
+  // Not ready until a sheet read succeeded, nor after three sync intervals without one (with
+  // CONF_EXIT_ON_ERROR=false a synchronizer that cannot reach Google stays up, retrying).
+  g_sheet_stale_ms.store(std::max<int64_t>(3000, 3000 * static_cast<int64_t>(cfg_.sync_interval_secs)));
+  http::add_readiness_check("sheet", sheet_ready);
   std::unique_ptr<std::thread> watch_thread;
   std::vector<std::thread> workers;
   kube::WorkQueue queue;

@@ -305,3 +305,27 @@ def test_deleted_userbootstraps_leave_no_sync_state(google):
         for u in users[1::2]:
             c.admin.delete("userbootstraps", u)
         wait_for(lambda: tracked() == 0, timeout=10, desc="no sync state left")
+
+
+def test_readyz_reports_a_stale_sheet(google):
+    """/readyz's `sheet` check: not ready before the first successful sheet read, nor after
+    three sync intervals without one (a synchronizer with CONF_EXIT_ON_ERROR=false keeps
+    running while Google fails); ready again after the next good read."""
+    google.set_rows([{"id_username": "frank"}])
+    with Cluster(controller=False) as c:
+        c.start_synchronizer(google, interval=1, extra_env={"CONF_EXIT_ON_ERROR": "false"})
+
+        def readyz():
+            r = requests.get(f"http://127.0.0.1:{c.sync_port}/readyz", timeout=5)
+            return r.status_code, r.text
+
+        wait_for(lambda: readyz()[0] == 200, timeout=10, desc="ready")
+        assert "[+]sheet ok" in readyz()[1]
+        google.fail_export = 500
+        t0 = time.monotonic()
+        wait_for(lambda: readyz()[0] == 503, timeout=10, interval=0.1, desc="stale sheet")
+        assert time.monotonic() - t0 > 1.5  # not before the stale window (3 s after the last read)
+        assert "[-]sheet failed: last successful sheet read" in readyz()[1]
+        assert c.procs["synchronizer"].alive()
+        google.fail_export = 0
+        wait_for(lambda: readyz()[0] == 200, timeout=10, desc="ready again")
