@@ -760,6 +760,7 @@ def pin_to_quota(d=None):
 
 
 def run(args):
+    t_run = time.monotonic()
     d = Dist()
     n = args.gpus if args.gpus else d.world
     # every rank pins itself to the same CPUs: the quota covers the whole job
@@ -881,7 +882,9 @@ def run(args):
         results = {}
         running = semantics  # controller semantics of the running controller
         latency = args.write_latency_ms  # kube-lite's current storage latency
+        phase_wall = {"setup": round(time.monotonic() - t_run, 2)}  # wall seconds per phase (rank 0's view)
         for p in phases:
+            t_phase = time.monotonic()
             if d.rank == 0:
                 import requests
 
@@ -904,6 +907,7 @@ def run(args):
                 results[p.key] = _rate_phase(d, nat, info, args, p.key, p.rate, cluster)
                 if results[p.key] is not None:
                     results[p.key]["semantics"] = p.semantics
+                phase_wall[p.key] = round(time.monotonic() - t_phase, 2)
                 continue
             if p.isolated:
                 _settle(info)
@@ -916,6 +920,7 @@ def run(args):
             if results[p.key] is not None:
                 results[p.key]["semantics"] = p.semantics
                 results[p.key]["apiserver_write_latency_ms"] = p.write_latency_ms
+            phase_wall[p.key] = round(time.monotonic() - t_phase, 2)
         xgmi = _xgmi_probe(d, args)
         if d.rank != 0:
             return None
@@ -1007,6 +1012,8 @@ def run(args):
                 out["latency_at_rate"]["this_over_reference"] = _compare_at_rate(this_q, ref_q)
         # amdsmi counters of the advertised GPUs at the end of the timed region (node agent)
         out["gpu_telemetry"] = gpu_tel
+        phase_wall["total"] = round(time.monotonic() - t_run, 2)
+        out["phase_wall_s"] = phase_wall
         if xgmi is not None:
             out["rccl_xgmi"] = xgmi
         out["reference_structural"] = {"apply_to_ready_p50_s": 30.0, "apply_to_ready_p99_s": 59.4,
