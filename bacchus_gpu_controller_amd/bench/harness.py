@@ -781,19 +781,14 @@ def run(args):
     phases = [_Phase("m", conc, args.webhook_protocol, semantics0, args.write_latency_ms, args.warmup, args.steps)]
     # The secondary closed-loop phases (tuned concurrency, HTTP/1.1 webhook, the 2 ms
     # write-latency arms) run at N=1 only: at N ranks each does N times the work (weak
-    # scaling) and the scaling runs report the headline alone.
+    # scaling) and the scaling runs report the headline alone.  They run last, and only
+    # while the run's wall time stays inside --time-budget-s.
     secondary = d.world == 1
-    if args.tuned_phase and tuned != conc and secondary:
-        phases.append(_Phase("t", tuned, args.webhook_protocol, semantics0, args.write_latency_ms,
-                             args.warmup, args.steps))
     if args.isolated_phase and d.world == 1:
         # the headline again, with the fixtures (kube-lite, load driver) and the product on
         # disjoint CPUs: how much of the headline latencies is queueing behind the fixtures
         phases.append(_Phase("pi", conc, args.webhook_protocol, semantics0, args.write_latency_ms,
                              args.warmup, args.steps, isolated=True))
-    if args.http1_phase and args.webhook_protocol == "h2" and secondary:
-        # secondary: the same load with the webhook called over HTTP/1.1 (keep-alive pool)
-        phases.append(_Phase("w", conc, "http/1.1", semantics0, args.write_latency_ms, args.warmup, args.steps))
     semantics = "reference" if args.reference_semantics else args.semantics
     rates = [float(x) for x in args.latency_rates.split(",") if x.strip()]
     if rates:
@@ -814,6 +809,13 @@ def run(args):
                                  args.arm_write_latency_ms, args.arm_warmup, args.arm_steps))
             phases.append(_Phase("ml", conc, args.webhook_protocol, "this", args.arm_write_latency_ms,
                                  args.arm_warmup, args.arm_steps))
+    if args.tuned_phase and tuned != conc and secondary:
+        phases.append(_Phase("t", tuned, args.webhook_protocol, semantics0, args.write_latency_ms,
+                             args.warmup, args.steps))
+    if args.http1_phase and args.webhook_protocol == "h2" and secondary:
+        # secondary: the same load with the webhook called over HTTP/1.1 (keep-alive pool)
+        phases.append(_Phase("w", conc, "http/1.1", semantics0, args.write_latency_ms, args.warmup, args.steps))
+    optional = {"rl", "ml", "t", "w"}
     # Reconcile/sync workers spend most of their time waiting on API round trips, so they
     # are not sized to the CPU share like the offered load is (16 = the binaries' default).
     controller_workers = args.controller_workers or 16
@@ -883,8 +885,18 @@ def run(args):
         running = semantics  # controller semantics of the running controller
         latency = args.write_latency_ms  # kube-lite's current storage latency
         phase_wall = {"setup": round(time.monotonic() - t_run, 2)}  # wall seconds per phase (rank 0's view)
+        skipped = []
         for p in phases:
             t_phase = time.monotonic()
+            if p.key in optional and args.time_budget_s > 0:
+                # an estimate from the headline's pace: a closed-loop step at the 2 ms write
+                # latency takes about 6x a headline step
+                per_step = phase_wall["m"] / max(1, args.warmup + args.steps)
+                est = per_step * (p.warmup + p.steps) * (6 if p.write_latency_ms > 0 else 1)
+                over = d.max_scalar(time.monotonic() - t_run + est) > args.time_budget_s
+                if over or (p.key == "ml" and "rl" in skipped):  # the write-latency pair goes together
+                    skipped.append(p.key)
+                    continue
             if d.rank == 0:
                 import requests
 
@@ -1014,6 +1026,8 @@ def run(args):
         out["gpu_telemetry"] = gpu_tel
         phase_wall["total"] = round(time.monotonic() - t_run, 2)
         out["phase_wall_s"] = phase_wall
+        if skipped:  # secondary phases left out to keep the run inside --time-budget-s
+            out["skipped_phases"] = skipped
         if xgmi is not None:
             out["rccl_xgmi"] = xgmi
         out["reference_structural"] = {"apply_to_ready_p50_s": 30.0, "apply_to_ready_p99_s": 59.4,
@@ -1121,8 +1135,11 @@ def main(argv=None):
                          "and both controllers at --arm-write-latency-ms (secondary fields)")
     ap.add_argument("--arm-write-latency-ms", type=float, default=2.0,
                     help="kube-lite storage commit latency of the write-latency arms (0 = no such arms)")
-    ap.add_argument("--arm-steps", type=int, default=6, help="timed steps of each write-latency arm")
-    ap.add_argument("--arm-warmup", type=int, default=2, help="warmup steps of each write-latency arm")
+    ap.add_argument("--arm-steps", type=int, default=5, help="timed steps of each write-latency arm")
+    ap.add_argument("--arm-warmup", type=int, default=1, help="warmup steps of each write-latency arm")
+    ap.add_argument("--time-budget-s", type=float, default=50.0,
+                    help="wall seconds of the run after which the secondary phases (write-latency arms, tuned, "
+                         "HTTP/1.1 webhook) are skipped (listed in skipped_phases); 0 = no budget")
     ap.add_argument("--latency-rates", default="2000,6000",
                     help="open-loop offered rates (CR/s, whole job) at which this build and the reference-controller "
                          "arm are both timed (latency_at_rate; '' = none)")

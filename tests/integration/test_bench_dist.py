@@ -73,12 +73,13 @@ def test_default_run_carries_the_reference_arms():
     arm's percentiles come from whole windows."""
     cmd = [sys.executable, os.path.join(REPO_ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--batch", "20",
            "--rounds", "1", "--no-tuned-phase", "--no-http1-phase", "--arm-steps", "2", "--arm-warmup", "1",
-           "--latency-rates", "100,200", "--latency-window-s", "1"]
+           "--latency-rates", "100,200", "--latency-window-s", "1", "--time-budget-s", "0"]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=REPO_ROOT,
                        env=dict(os.environ, BGC_BENCH_CPU="1"))
     assert p.returncode == 0, p.stderr[-3000:]
     d = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
     assert d["vs_baseline"] is None and d["samples_complete"] is True
+    assert "skipped_phases" not in d and d["phase_wall_s"]["total"] > 0
     assert d["reconciles"] == d["reconcile_total_delta"] and d["webhook_calls"] == d["webhook_calls_total_delta"]
     rc = d["reference_controller"]
     assert rc["semantics"] == "reference-controller" and rc["failed_crs"] == 0 and rc["value"] > 0
@@ -128,3 +129,19 @@ def test_single_tenant_bench_config1():
     # one stream's delivery can lag another's by more than the gap between the writes
     assert all(0 < st[k]["p50"] < 5000 for k in ("namespace", "quota", "rolebinding"))
     assert d["reconcile_ms"]["p50"] > 0
+
+
+def test_time_budget_skips_the_secondary_phases():
+    """--time-budget-s: once the run's wall time (plus the next phase's estimate) passes the
+    budget, the secondary phases (write-latency arms, tuned, HTTP/1.1 webhook) are left out
+    and listed; the headline, the reference controller and latency_at_rate always run."""
+    cmd = [sys.executable, os.path.join(REPO_ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--batch", "20",
+           "--rounds", "1", "--latency-rates", "100", "--latency-window-s", "1", "--no-isolated-phase",
+           "--time-budget-s", "0.5"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=REPO_ROOT,
+                       env=dict(os.environ, BGC_BENCH_CPU="1"))
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert set(d["skipped_phases"]) >= {"rl", "ml", "w"}
+    assert "write_latency_2ms" not in d and "webhook_http1" not in d
+    assert d["value"] > 0 and d["reference_controller"]["value"] > 0 and d["latency_at_rate"]["this"]["100"]
