@@ -348,7 +348,13 @@ class MockBackend : public Backend {
     std::unique_lock<std::mutex> lk(mu_);
     // "sample_hang_ms": every reading blocks this long, as amdsmi does while the driver
     // resets a wedged GPU; rewriting the fixture without it ends the hang early.
-    for (int64_t hang_start = metrics::now_ns();;) {
+    // "sample_hang_samples" (optional): only that many readings block, the rest return.
+    bool hangs = fixture_.get("sample_hang_ms").is_number();
+    if (hangs && fixture_.get("sample_hang_samples").is_int()) {
+      hangs = hung_samples_ < fixture_.get("sample_hang_samples").as_int();
+      if (hangs) ++hung_samples_;
+    }
+    for (int64_t hang_start = metrics::now_ns(); hangs;) {
       const Value& hang = fixture_.get("sample_hang_ms");
       if (!hang.is_number() || static_cast<double>(metrics::now_ns() - hang_start) / 1e6 >= hang.as_double()) break;
       lk.unlock();
@@ -455,8 +461,9 @@ class MockBackend : public Backend {
   std::string path_;
   struct timespec mtime_ {};
   std::mutex reload_mu_;  // guards mtime_ and serializes file reads
-  std::mutex mu_;         // guards fixture_ and acc_seq_
+  std::mutex mu_;         // guards fixture_, acc_seq_ and hung_samples_
   std::map<int, uint64_t> acc_seq_;
+  int64_t hung_samples_ = 0;
 };
 
 // ---------------------------------------------------------------------------

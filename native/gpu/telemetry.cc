@@ -239,7 +239,16 @@ void TelemetryPoller::poll_once() {
   {
     std::lock_guard<std::mutex> sl(stall_mu_);
     poll_started_ns_.store(0);
-    resumed = stalled_.exchange(false);
+    // A stall ends with a poll that completes inside the stall timeout: one that itself took
+    // longer (an amdsmi that answers, but only after the timeout) keeps the GPUs withdrawn,
+    // so a slow backend does not flap them every poll.
+    const double took_s = static_cast<double>(snap->ts_ns - t0) / 1e9;
+    if (stalled_.load() && stall_timeout_.count() > 0 && took_s * 1e3 >= static_cast<double>(stall_timeout_.count())) {
+      mark_stalled(*snap, took_s);
+      changed = false;
+    } else {
+      resumed = stalled_.exchange(false);
+    }
     std::lock_guard<std::mutex> lk(snap_mu_);
     snap_ = snap;
   }
@@ -255,6 +264,22 @@ void TelemetryPoller::notify(const Snapshot& s) {
   if (cb_) cb_(s);
 }
 
+void TelemetryPoller::mark_stalled(Snapshot& snap, double stuck_s) const {
+  snap.stalled = true;
+  for (size_t k = snap.health.size(); k < indices_.size(); ++k) {
+    DeviceHealth h;
+    h.index = indices_[k];
+    snap.health.push_back(h);
+  }
+  const std::string why = "telemetry stalled: no reading from the " + backend_.name() + " backend for " +
+                          std::to_string(static_cast<long long>(stuck_s)) + " s";
+  for (auto& h : snap.health) {
+    h.healthy = false;
+    h.reason = why;
+  }
+  for (const auto& g : gauges_) g.healthy->set(0);
+}
+
 void TelemetryPoller::check_stall() {
   std::shared_ptr<Snapshot> snap;
   double stuck_s = 0;
@@ -264,23 +289,8 @@ void TelemetryPoller::check_stall() {
     if (started == 0 || stalled_.load()) return;
     stuck_s = static_cast<double>(metrics::now_ns() - started) / 1e9;
     if (stuck_s * 1e3 < static_cast<double>(stall_timeout_.count())) return;
-    std::shared_ptr<const Snapshot> last = snapshot();
-    snap = std::make_shared<Snapshot>(*last);
-    snap->stalled = true;
-    if (snap->health.size() < indices_.size()) {
-      for (size_t k = snap->health.size(); k < indices_.size(); ++k) {
-        DeviceHealth h;
-        h.index = indices_[k];
-        snap->health.push_back(h);
-      }
-    }
-    const std::string why = "telemetry stalled: no reading from the " + backend_.name() + " backend for " +
-                            std::to_string(static_cast<long long>(stuck_s)) + " s";
-    for (auto& h : snap->health) {
-      h.healthy = false;
-      h.reason = why;
-    }
-    for (const auto& g : gauges_) g.healthy->set(0);
+    snap = std::make_shared<Snapshot>(*snapshot());
+    mark_stalled(*snap, stuck_s);
     stalled_.store(true);
     std::lock_guard<std::mutex> lk(snap_mu_);
     snap_ = snap;

@@ -146,6 +146,7 @@ class TelemetryPoller {
   std::atomic<int64_t> poll_started_ns_{0};
   std::atomic<bool> stalled_{false};
   void check_stall();
+  void mark_stalled(Snapshot& snap, double stuck_s) const;
   void notify(const Snapshot& s);
   CancelToken stop_;
   std::thread thread_;

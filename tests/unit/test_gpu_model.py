@@ -29,22 +29,46 @@ def test_poller_stall_watchdog(nat):
     """A poll stuck in the backend past stall_ms publishes every device unhealthy; the poll
     that finally completes publishes the real readings again (native/gpu/telemetry.cc)."""
     fx = json.loads(nat.default_mi355x_fixture(2))
-    fx["sample_hang_ms"] = 600  # every reading blocks this long
+    fx["sample_hang_ms"] = 600  # the first poll's two readings block this long, later ones return
+    fx["sample_hang_samples"] = 2
     b = nat.gpu_backend("mock", json.dumps(fx))
-    p = nat.TelemetryPoller(b, [0, 1], 5000, stall_ms=150)
+    p = nat.TelemetryPoller(b, [0, 1], 100, stall_ms=150)
     p.start()  # the first poll hangs for 600 ms
     time.sleep(0.4)
     snap = json.loads(p.snapshot())
     assert p.stalled() and snap["stalled"]
     assert [h["healthy"] for h in snap["health"]] == [False, False]
     assert all("telemetry stalled" in h["reason"] for h in snap["health"])
+    # the hung poll completes after 600 ms, longer than the stall timeout: still stalled
     deadline = time.time() + 3
     while p.polls() < 1 and time.time() < deadline:
-        time.sleep(0.02)
+        time.sleep(0.005)
+    assert p.stalled()
+    # the next poll is fast: the real readings are back
+    while p.polls() < 2 and time.time() < deadline:
+        time.sleep(0.005)
+    time.sleep(0.02)
     snap = json.loads(p.snapshot())
     p.stop()
     assert not snap["stalled"] and all(h["healthy"] for h in snap["health"])
     assert all(d["ok"] for d in snap["devices"])
+
+
+def test_a_slow_backend_stays_withdrawn(nat):
+    """Every poll answering only after the stall timeout keeps the devices unhealthy
+    instead of flapping them back after each completed poll."""
+    fx = json.loads(nat.default_mi355x_fixture(1))
+    fx["sample_hang_ms"] = 250
+    p = nat.TelemetryPoller(nat.gpu_backend("mock", json.dumps(fx)), [0], 20, stall_ms=100)
+    p.start()
+    deadline = time.time() + 5
+    while p.polls() < 3 and time.time() < deadline:
+        assert time.time() < deadline
+        time.sleep(0.01)
+        if p.polls() >= 1:
+            assert p.stalled() and json.loads(p.snapshot())["stalled"]
+    p.stop()
+    assert p.polls() >= 3
 
 
 def test_poller_without_stall_timeout_never_stalls(nat):
