@@ -258,6 +258,25 @@ def cgroup_throttling():
         return None
 
 
+def runqueue_wait_ms(pids):
+    """Time the threads of `pids` spent runnable but waiting for a CPU (/proc/<pid>/task/*/
+    schedstat, second field), summed: a window whose latencies jump while this jumps lost
+    its CPUs (to the job's own processes or to anything else on them)."""
+    total = 0
+    for pid in pids:
+        try:
+            tids = os.listdir(f"/proc/{pid}/task")
+        except OSError:
+            continue
+        for tid in tids:
+            try:
+                with open(f"/proc/{pid}/task/{tid}/schedstat") as f:
+                    total += int(f.read().split()[1])
+            except (OSError, IndexError, ValueError):
+                pass
+    return total / 1e6
+
+
 def auto_concurrency(world, cpus):
     """In-flight creates per rank.  The control plane is CPU-bound, so the total in flight
     is sized to its CPU share rather than fixed per rank: measured on the MI355X box
@@ -593,15 +612,18 @@ def _rate_phase(d, nat, info, args, key, rate, cluster):
     try:
         driver.open_loop(_rate_names(d.rank, key, rate, "w", n_warm), args.latency_warmup_s, args.timeout, 7 + d.rank)
         d.barrier()
-        starts = thr0 = None
+        starts = thr0 = rq0 = None
+        pids = [os.getpid()] + [p.p.pid for p in cluster.procs.values()] if d.rank == 0 and cluster else []
         if d.rank == 0:
             starts = {k: _clear(url, verify) for k, (url, verify) in _sample_logs(info).items()}
             thr0 = cgroup_throttling()
+            rq0 = runqueue_wait_ms(pids)
         d.barrier()
         res = json.loads(driver.open_loop(_rate_names(d.rank, key, rate, "t", n_timed), args.latency_window_s,
                                           args.timeout, 1000 + d.rank))
         d.barrier()
         thr1 = cgroup_throttling() if d.rank == 0 else None
+        rq1 = runqueue_wait_ms(pids) if d.rank == 0 else None
     finally:
         driver.stop()
     per = d.gather_obj({k: res[k] for k in ("ready", "failed", "timeouts", "offered_rate", "achieved_rate",
@@ -628,6 +650,9 @@ def _rate_phase(d, nat, info, args, key, rate, cluster):
            "failed_crs": sum(p["failed"] + p["timeouts"] for p in per)}
     if thr0 and thr1:
         out["cgroup_throttled_periods"] = thr1["throttled"] - thr0["throttled"]
+    if rq0 is not None and rq1 is not None:
+        # CPU-ms the job's threads waited in run queues per second of window
+        out["runqueue_wait_ms_per_s"] = round((rq1 - rq0) / max(args.latency_window_s, 1e-9), 1)
     errs = [e for p in per for e in p["errors"]]
     if errs:
         out["errors"] = errs[:3]
