@@ -130,10 +130,19 @@ Decision mutate(const Value& req, const Config& cfg) {
     return invalid(uid, e.what(), 12);
   }
 
-  json::PatchBuilder patches;
+  // The patch is written as JSON text: ops in the reference's order, each
+  // {"op":...,"path":...,"value":...} as serde_json emits json_patch::PatchOperation.
+  std::string patches;
+  auto add_op = [&](std::string_view path) {
+    patches += patches.empty() ? "[{\"op\":\"add\",\"path\":" : ",{\"op\":\"add\",\"path\":";
+    json::escape_string(path, patches);
+    patches += ",\"value\":";
+  };
   if (username.kind == UserKind::Normal) {
     // rule 13: always (over)write kube_username for normal users
-    patches.add("/spec/kube_username", Value(username.kube_username));
+    add_op("/spec/kube_username");
+    json::escape_string(username.kube_username, patches);
+    patches += '}';
   } else if (!ub.kube_username || ub.kube_username->empty()) {
     // rule 14
     return deny(uid, "kube_username field is empty. you are an admin, so fill it", 14);
@@ -146,50 +155,47 @@ Decision mutate(const Value& req, const Config& cfg) {
 
   if (!ub.has_rolebinding) {
     // rule 16: default RoleBinding (two ops, exactly as the reference emits them)
-    patches.add("/spec/rolebinding", Value::object());
-    const std::string subject_name =
+    add_op("/spec/rolebinding");
+    patches += "{}}";
+    const std::string& subject_name =
         username.kind == UserKind::Normal ? username.original_username : *ub.kube_username;
-    Value rb = Value::object();
-    rb["role_ref"] = Value::object({{"apiGroup", "rbac.authorization.k8s.io"},
-                                    {"kind", "ClusterRole"},
-                                    {"name", cfg.default_role_name}});
-    rb["subjects"] = Value::array({Value::object({{"apiGroup", "rbac.authorization.k8s.io"},
-                                                  {"kind", "User"},
-                                                  {"name", subject_name}})});
-    patches.add("/spec/rolebinding", std::move(rb));
+    add_op("/spec/rolebinding");
+    patches += "{\"role_ref\":{\"apiGroup\":\"rbac.authorization.k8s.io\",\"kind\":\"ClusterRole\",\"name\":";
+    json::escape_string(cfg.default_role_name, patches);
+    patches += "},\"subjects\":[{\"apiGroup\":\"rbac.authorization.k8s.io\",\"kind\":\"User\",\"name\":";
+    json::escape_string(subject_name, patches);
+    patches += "}]}}";
   } else if (username.kind == UserKind::Normal) {
     // rule 17
     return deny(uid, "rolebinding field is not empty. you are a normal user, so leave it empty", 17);
   }
 
   Decision d = allow(uid, patches.empty() ? 18 : 19);
-  if (!patches.empty()) d.patch = patches.ops();
+  if (!patches.empty()) d.patch = std::move(patches) + "]";
   return d;
 }
 
-Value review_response(const Decision& d, const std::string& api_version) {
-  Value resp = Value::object();
-  resp["uid"] = d.uid;
-  resp["allowed"] = d.allowed;
+std::string review_response(const Decision& d, const std::string& api_version) {
+  std::string out;
+  out.reserve(160 + d.uid.size() + d.message.size() + d.patch.size() * 4 / 3);
+  out += "{\"apiVersion\":";
+  json::escape_string(api_version.empty() ? std::string_view("admission.k8s.io/v1") : std::string_view(api_version), out);
+  out += ",\"kind\":\"AdmissionReview\",\"response\":{\"uid\":";
+  json::escape_string(d.uid, out);
+  out += d.allowed ? ",\"allowed\":true" : ",\"allowed\":false";
   if (!d.allowed) {
-    Value status = Value::object();
-    if (d.invalid) {
-      status["status"] = "Failure";
-      status["code"] = 400;
-      status["reason"] = "BadRequest";
-    }
-    status["message"] = d.message;
-    resp["status"] = std::move(status);
+    out += d.invalid ? ",\"status\":{\"status\":\"Failure\",\"code\":400,\"reason\":\"BadRequest\",\"message\":"
+                     : ",\"status\":{\"message\":";
+    json::escape_string(d.message, out);
+    out += '}';
   }
-  if (!d.patch.is_null()) {
-    resp["patch"] = crypto::base64_encode(d.patch.dump());
-    resp["patchType"] = "JSONPatch";
+  if (!d.patch.empty()) {
+    out += ",\"patch\":\"";
+    out += crypto::base64_encode(d.patch);  // base64: nothing to escape
+    out += "\",\"patchType\":\"JSONPatch\"";
   }
-  Value review = Value::object();
-  review["apiVersion"] = api_version.empty() ? "admission.k8s.io/v1" : api_version;
-  review["kind"] = "AdmissionReview";
-  review["response"] = std::move(resp);
-  return review;
+  out += "}}";
+  return out;
 }
 
 namespace {
@@ -241,7 +247,7 @@ HttpResult handle_review(const std::string& body, const std::string& content_typ
   if (req.is_null()) {
     // try_into() fails -> AdmissionResponse::invalid
     r.decision = invalid("", "request missing in AdmissionReview", 0);
-    r.body = review_response(r.decision, api_version).dump();
+    r.body = review_response(r.decision, api_version);
     return r;
   }
   if (!req.is_object()) return reject("request: invalid type, expected struct AdmissionRequest");
@@ -267,7 +273,7 @@ HttpResult handle_review(const std::string& body, const std::string& content_typ
     LOG_DEBUG("admission") << "received admission request uid=" << req.get_string("uid");
   }
   r.decision = mutate(req, cfg);
-  r.body = review_response(r.decision, api_version).dump();
+  r.body = review_response(r.decision, api_version);
   return r;
 }
 

@@ -47,7 +47,7 @@ struct Decision {
   bool allowed = true;
   bool invalid = false;       // AdmissionResponse::invalid (malformed request)
   std::string message;        // deny / invalid reason
-  json::Value patch;          // JSON Patch ops (array) or null
+  std::string patch;          // JSON Patch ops (a JSON array's text), empty for none
   int rule = 0;               // which decision-table row fired (observability/tests)
 };
 
@@ -67,6 +67,8 @@ struct HttpResult {
 HttpResult handle_review(const std::string& body, const std::string& content_type, const Config& cfg);
 
 // AdmissionReview{response} JSON for a decision. `api_version` echoes the request's.
-json::Value review_response(const Decision& d, const std::string& api_version);
+// The AdmissionReview response document's JSON text (written directly: the webhook answers
+// every UserBootstrap write, and building and dumping a Value tree was its largest cost).
+std::string review_response(const Decision& d, const std::string& api_version);
 
 }  // namespace bgc::admission

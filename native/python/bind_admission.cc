@@ -26,7 +26,7 @@ void register_admission(py::module_& m) {
   // Returns (allowed, invalid, message, patch_json_or_None, rule)
   m.def("admission_mutate", [](const std::string& request_json, const Config& cfg) {
     auto d = bgc::admission::mutate(bgc::json::parse(request_json), cfg);
-    py::object patch = d.patch.is_null() ? py::object(py::none()) : py::object(py::str(d.patch.dump()));
+    py::object patch = d.patch.empty() ? py::object(py::none()) : py::object(py::str(d.patch));
     return py::make_tuple(d.allowed, d.invalid, d.message, patch, d.rule);
   });
 

@@ -285,3 +285,36 @@ def test_http_review_projection_matches_full_parse(nat, cfg, op, username, grp, 
     assert resp.get("status", {}).get("message") == (msg or None if not allowed else None)
     got = json.loads(base64.b64decode(resp["patch"])) if "patch" in resp else None
     assert got == patch
+
+
+@pytest.mark.parametrize("username,uid", [("oidc:alice", "u-1"), ('oidc:q"uo\\te', 'u"\\1'),
+                                          ("oidc:ünï\tcode", "ué")])
+def test_review_response_wire_format(nat, cfg, username, uid):
+    """The response document and its patch are written as text (round 5): byte-compare them
+    with compact JSON of the expected documents, in the member order the reference's serde
+    types emit, for names that need escaping."""
+    name = username[len(PREFIX):]
+    req = request(username=username, name=name, uid=uid)
+    review = {"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview", "request": req}
+    status, body, _ = nat.admission_handle_review(json.dumps(review), "application/json", cfg)
+    assert status == 200
+    compact = lambda o: json.dumps(o, separators=(",", ":"), ensure_ascii=False)  # noqa: E731
+    ops = [{"op": "add", "path": "/spec/kube_username", "value": name},
+           {"op": "add", "path": "/spec/rolebinding", "value": {}},
+           {"op": "add", "path": "/spec/rolebinding",
+            "value": {"role_ref": {"apiGroup": "rbac.authorization.k8s.io", "kind": "ClusterRole", "name": cfg.default_role_name},
+                      "subjects": [{"apiGroup": "rbac.authorization.k8s.io", "kind": "User", "name": username}]}}]
+    patch = json.loads(base64.b64decode(json.loads(body)["response"]["patch"]))
+    assert patch == ops
+    expected = {"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview",
+                "response": {"uid": uid, "allowed": True,
+                             "patch": base64.b64encode(compact(ops).encode()).decode(), "patchType": "JSONPatch"}}
+    assert body == compact(expected)
+
+
+def test_denial_wire_format(nat, cfg):
+    req = request(username="oidc:alice", groups=("nope",))
+    status, body, _ = nat.admission_handle_review(json.dumps({"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview",
+                                                              "request": req}), "application/json", cfg)
+    assert body == ('{"apiVersion":"admission.k8s.io/v1","kind":"AdmissionReview","response":{"uid":"u-1",'
+                    '"allowed":false,"status":{"message":"user is not in authorized group"}}}')
