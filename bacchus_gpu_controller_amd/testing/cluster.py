@@ -6,11 +6,9 @@ webhook, service-account tokens for each component).
 Used by tests/integration and by bench.py.
 """
 import base64
-import ctypes
 import json
 import os
 import re
-import signal
 import socket
 import subprocess
 import tempfile
@@ -61,19 +59,6 @@ SERVICE_GLIBC_TUNABLES = ("glibc.malloc.tcache_count=64:glibc.malloc.tcache_max=
                           "glibc.malloc.mmap_threshold=4194304")
 
 
-try:  # resolved in the parent: the forked child only makes the call
-    _prctl = ctypes.CDLL(None, use_errno=True).prctl
-except (OSError, AttributeError):
-    _prctl = None
-
-
-def _die_with_parent():
-    """Child-side: SIGTERM this service when the process that started it dies, so a test
-    run killed by a timeout leaves no services behind (they run in sessions of their own)."""
-    if _prctl is not None:
-        _prctl(1, int(signal.SIGTERM))  # PR_SET_PDEATHSIG
-
-
 class Proc:
     def __init__(self, name, cmd, env, workdir):
         self.name = name
@@ -85,10 +70,13 @@ class Proc:
         # binaries and the chart leave them off
         full_env.setdefault("CONF_DEBUG_ENDPOINTS", "true")
         full_env.update(env)
-        # PDEATHSIG fires when the starting *thread* ends: only tie the service to a main thread
-        tie = threading.current_thread() is threading.main_thread()
+        # The service SIGTERMs itself when this process dies (bgc::process_init reads
+        # BGC_DIE_WITH_PARENT), so a test run killed by a timeout leaves no services behind.
+        # The kernel's parent-death signal follows the starting *thread*: main thread only.
+        if threading.current_thread() is threading.main_thread():
+            full_env.setdefault("BGC_DIE_WITH_PARENT", str(os.getpid()))
         self.p = subprocess.Popen(cmd, env=full_env, stdout=self.log, stderr=subprocess.STDOUT,
-                                  start_new_session=True, preexec_fn=_die_with_parent if tie else None)
+                                  start_new_session=True)
 
     def alive(self):
         return self.p.poll() is None

@@ -4,6 +4,7 @@
 #include <openssl/crypto.h>
 #include <pthread.h>
 #include <signal.h>
+#include <sys/prctl.h>
 #include <sys/resource.h>
 #include <unistd.h>
 
@@ -116,7 +117,21 @@ void start_malloc_trimmer() {
 // leaves OpenSSL's memory to the kernel, like any other process memory.
 void init_openssl() { OPENSSL_init_crypto(OPENSSL_INIT_NO_ATEXIT, nullptr); }
 
+// BGC_DIE_WITH_PARENT=<pid> (test harnesses): SIGTERM this process when the process that
+// started it dies (PR_SET_PDEATHSIG), so a test run killed by a timeout leaves no service
+// behind.  The variable is removed first, so this process's own children (diagnostics
+// workers) do not inherit it; a parent already gone by now ends this process at once.
+static void die_with_parent_from_env() {
+  const char* v = std::getenv("BGC_DIE_WITH_PARENT");
+  if (!v) return;
+  const long parent = std::atol(v);
+  ::unsetenv("BGC_DIE_WITH_PARENT");
+  ::prctl(PR_SET_PDEATHSIG, SIGTERM);
+  if (parent > 0 && ::getppid() != static_cast<pid_t>(parent)) std::_Exit(0);
+}
+
 void process_init() {
+  die_with_parent_from_env();
   init_openssl();
   tune_malloc();
   start_malloc_trimmer();
