@@ -168,3 +168,27 @@ def test_cascade_after_a_tenant_deletion_queues_no_reconciles():
         time.sleep(0.3)
         assert metric(c.controller_port, 'bgc_controller_child_events_ignored_total{reason="terminating"}') >= 3
         assert metric(c.controller_port, 'bgc_reconcile_total{result="ok"}') == r0
+
+
+def test_namespace_deleted_under_a_live_tenant_is_recreated():
+    """An admin deletes a live tenant's Namespace.  It terminates (its quota and bindings go
+    first); the controller's repairs into it meanwhile are refused and retried quietly, and
+    its DELETED event brings the Namespace and every child back, without waiting for the
+    periodic requeue (an hour here)."""
+    env = {"CONF_REQUEUE_SECS": "3600", "CONF_RESYNC_SECS": "0"}
+    with Cluster(admission=False, controller_env=env) as c:
+        c.admin.create("userbootstraps", {"apiVersion": "bacchus.io/v1", "kind": "UserBootstrap",
+                                          "metadata": {"name": "live"},
+                                          "spec": {"kube_username": "live",
+                                                   "quota": {"hard": {"requests.amd.com/gpu": "2"}}}})
+        first = wait_for(lambda: c.admin.get_or_none("resourcequotas", "live", "live"), desc="tenant ready")
+        old_ns = c.admin.get("namespaces", "live")
+        raw(c, "DELETE", "/api/v1/namespaces/live").raise_for_status()
+        ns = wait_for(lambda: (lambda n: n if n and n["metadata"]["uid"] != old_ns["metadata"]["uid"] else None)(
+            c.admin.get_or_none("namespaces", "live")), timeout=10, desc="namespace re-created")
+        assert ns["status"]["phase"] == "Active" and ns["metadata"]["ownerReferences"][0]["name"] == "live"
+        rq = wait_for(lambda: c.admin.get_or_none("resourcequotas", "live", "live"), timeout=10, desc="quota back")
+        assert rq["metadata"]["uid"] != first["metadata"]["uid"]
+        assert rq["spec"]["hard"]["requests.amd.com/gpu"] == "2"
+        assert c.procs["controller"].alive()
+        assert "being terminated" not in c.procs["controller"].output()
