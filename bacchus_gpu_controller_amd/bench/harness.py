@@ -1068,7 +1068,7 @@ def run(args):
             try:  # the periodic malloc_trim pass of each process (core/process.cc), kube-lite included
                 import requests
 
-                trims = {}
+                trims, heap = {}, {}
                 for comp, url, verify in (("controller", info["controller"], None),
                                           ("admission", info["admission"], info["ca"]),
                                           ("synchronizer", info["synchronizer"], None),
@@ -1077,11 +1077,15 @@ def run(args):
                     txt = requests.get(url + "/metrics", timeout=10, verify=verify).text
                     vals = {l.split()[0]: float(l.split()[1]) for l in txt.splitlines()
                             if l.startswith(("bgc_malloc_trim_seconds_sum", "bgc_malloc_trim_seconds_count",
-                                             "bgc_malloc_trim_last_seconds"))}
+                                             "bgc_malloc_trim_last_seconds", "bgc_heap_"))}
                     trims[comp] = {"passes": int(vals.get("bgc_malloc_trim_seconds_count", 0)),
                                    "total_ms": round(vals.get("bgc_malloc_trim_seconds_sum", 0.0) * 1e3, 3),
                                    "last_ms": round(vals.get("bgc_malloc_trim_last_seconds", 0.0) * 1e3, 3)}
+                    # live malloc data vs free space the arenas hold (RSS alone cannot tell them apart)
+                    heap[comp] = {"allocated_mb": round(vals.get("bgc_heap_allocated_bytes", 0.0) / 1e6, 1),
+                                  "free_mb": round(vals.get("bgc_heap_free_bytes", 0.0) / 1e6, 1)}
                 out["malloc_trim"] = trims
+                out["component_heap_mb"] = heap
             except Exception:  # noqa: BLE001
                 pass
             try:  # controller cache sizes (bounded-memory check under churn)
