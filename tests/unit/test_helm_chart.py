@@ -445,7 +445,7 @@ def test_prometheus_rule_alerts_reference_exported_series():
     assert len(rule) == 1 and rule[0]["metadata"]["labels"]["release"] == "prom"
     alerts = {r["alert"]: r for g in rule[0]["spec"]["groups"] for r in g["rules"]}
     assert {"AMDGPUUnhealthy", "AMDGPUDiagnosticsFailed", "AMDGPUUncorrectableECC", "AMDGPUXGMILinkDown", "AMDGPUTelemetryStalled",
-            "BGCReconcileErrors", "BGCAdmissionSlow"} <= set(alerts)
+            "BGCReconcileErrors", "BGCAdmissionSlow", "BGCWatchConnectionsGoingSilent", "BGCChildDriftRepaired"} <= set(alerts)
     assert alerts["AMDGPUXGMILinkDown"]["expr"] == "amd_gpu_xgmi_links_up < 6"
     assert "{{ $labels.gpu }}" in alerts["AMDGPUUnhealthy"]["annotations"]["summary"]  # escaped for Prometheus
     exported = set()
