@@ -1,7 +1,7 @@
 """Round-end smoke test on cuda:0 (driver contract `smoke()`).
 
 One tiny end-to-end pass of the flagship path on a real MI355X:
-  1. HIP/CDNA4 diagnostics on device 0 (64 MiB HBM pattern test, MFMA tile check, an MFMA
+  1. HIP/CDNA4 diagnostics on device 0 (1 GiB HBM pattern test, MFMA rate check, an MFMA
      GEMM compared with a host fp32 product, MX fp8 / fp4 block-scaled MFMA tiles, two
      launches of the 8-phase ping-pong soak GEMM at 1024^3 under its ABFT checksums) — the
      native kernels in libbgc_gpu_diag.so, no fallback;
@@ -24,8 +24,9 @@ def run_smoke(device=0):
     arch = ops.device_arch(device)
     if not arch.startswith("gfx950"):
         raise RuntimeError(f"expected an MI355X (gfx950), found {arch}")
-    hbm = ops.hbm(device, nbytes=64 << 20, iters=1)
-    mfma = ops.mfma(device, waves_per_cu=4, iters=256)
+    # sized to reach the steady rates (a 64 MiB pass or 4 waves per CU mostly time the launch)
+    hbm = ops.hbm(device, nbytes=1 << 30, iters=3)
+    mfma = ops.mfma(device, waves_per_cu=32, iters=4096)
     gemm = json.loads(nat.diag_gemm_check(device, 64, 64, 256, 0x5eed))  # MFMA GEMM vs a host fp32 product
     soak = ops.gemm_soak(device, 1024, 1024, 1024, launches=2)
     lowp = ops.mfma_lowp(device, waves_per_cu=4, iters=256)
