@@ -62,7 +62,13 @@ SERVICE_GLIBC_TUNABLES = ("glibc.malloc.tcache_count=64:glibc.malloc.tcache_max=
 class Proc:
     def __init__(self, name, cmd, env, workdir):
         self.name = name
+        # a restarted or second replica gets a log of its own: truncating the path another
+        # instance still writes at its own offset interleaves both (and NUL-fills the gap)
         self.log_path = os.path.join(workdir, f"{name}.log")
+        n = 1
+        while os.path.exists(self.log_path):
+            self.log_path = os.path.join(workdir, f"{name}.{n}.log")
+            n += 1
         self.log = open(self.log_path, "wb")
         full_env = dict(os.environ)
         full_env.setdefault("GLIBC_TUNABLES", SERVICE_GLIBC_TUNABLES)
