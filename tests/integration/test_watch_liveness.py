@@ -153,6 +153,10 @@ def test_node_agent_recovers_from_a_blackholed_apiserver_connection():
             labelled = lambda: (lambda n: n if n and n["metadata"].get("labels", {}).get("amd.com/gpu.product")
                                 else None)(c.admin.get_or_none("nodes", node))
             wait_for(labelled, timeout=20, desc="node published")
+            # the Node watch must be running: a freeze during its initial LIST is a plain request
+            # timeout (30 s), not the watch deadline this test is about
+            wait_for(lambda: (lambda r: r[0] == 200 and "watches" in r[1])(readyz(c.node_agent_port)), timeout=20,
+                     desc="node watch synced")
             proxy.freeze()
             t_freeze = time.monotonic()
             c.admin.delete("nodes", node)
