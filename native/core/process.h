@@ -18,9 +18,13 @@ void init_openssl();
 void tune_malloc();
 // The periodic trimmer's rule (process.cc): Skip while the RSS is under the minimum or under
 // 1.5x the RSS the previous pass left; Defer while the process used more than idle_pct % of
-// one CPU since the last check, unless the RSS passed 4x max(previous, minimum); else Trim.
+// one CPU since the last check, unless the RSS passed 4x max(previous, minimum) or half the
+// container's memory limit (limit_bytes, 0 = none); else Trim.
 enum class TrimDecision { Skip, Defer, Trim };
-TrimDecision malloc_trim_decision(long rss, long baseline, long min_bytes, double busy_pct, double idle_pct);
+TrimDecision malloc_trim_decision(long rss, long baseline, long min_bytes, double busy_pct, double idle_pct,
+                                  long limit_bytes = 0);
+// The cgroup memory limit of this process (v2 memory.max, else v1 limit_in_bytes); 0 = none.
+long cgroup_memory_limit_bytes();
 // Bounds a graceful shutdown once it has started: after `limit` the process logs, flushes
 // the log and exits with `code`.  A thread stuck in a driver call (amdsmi while the driver
 // resets a GPU) would otherwise hold the process until the kubelet's SIGKILL, after its

@@ -30,6 +30,21 @@ def test_trim_decision(rss, baseline, busy, want):
     assert native().malloc_trim_decision(rss, baseline, 64 * MB, busy, 5.0) == want
 
 
+@pytest.mark.parametrize("rss,baseline,limit,want", [
+    (100 * MB, 60 * MB, 160 * MB, "trim"),    # past half the container limit: trim while busy
+    (100 * MB, 60 * MB, 0, "defer"),          # no limit: wait for a quiet interval
+    (100 * MB, 60 * MB, 256 * MB, "defer"),   # under half the limit
+    (100 * MB, 80 * MB, 160 * MB, "skip"),    # not grown since the last pass: never every check
+])
+def test_trim_decision_under_a_memory_limit(rss, baseline, limit, want):
+    assert native().malloc_trim_decision(rss, baseline, 64 * MB, 40.0, 5.0, limit) == want
+
+
+def test_cgroup_memory_limit_reads_as_bytes_or_none():
+    v = native().cgroup_memory_limit_bytes()
+    assert v == 0 or v >= 4096
+
+
 def _trim_metrics(c):
     text = requests.get(f"http://127.0.0.1:{c.controller_port}/metrics", timeout=5).text
     return {l.split()[0]: float(l.split()[1]) for l in text.splitlines()
