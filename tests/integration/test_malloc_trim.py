@@ -72,3 +72,18 @@ def test_controller_trims_only_when_quiet(idle_pct, trims):
             assert m["bgc_malloc_trim_seconds_count"] >= 1, m
         else:  # IDLE_PCT=0: the process is never quiet enough
             assert m["bgc_malloc_trim_seconds_count"] == 0 and m["bgc_malloc_trim_deferred_total"] >= 1, m
+
+
+@pytest.mark.slow
+def test_controller_over_half_its_memory_limit_trims_while_busy():
+    """The same never-quiet controller (IDLE_PCT=0) under a memory limit it has passed half
+    of (BGC_MALLOC_TRIM_LIMIT_MB stands in for the cgroup's memory.max): it trims anyway."""
+    env = {"BGC_MALLOC_TRIM_SECS": "1", "BGC_MALLOC_TRIM_MIN_MB": "1", "BGC_MALLOC_TRIM_IDLE_PCT": "0",
+           "BGC_MALLOC_TRIM_LIMIT_MB": "2"}
+    with Cluster(admission=False, controller_env=env) as c:
+        time.sleep(1.2)
+        _grow(c)
+        time.sleep(3.5)
+        assert _trim_metrics(c)["bgc_malloc_trim_seconds_count"] >= 1
+        text = requests.get(f"http://127.0.0.1:{c.controller_port}/metrics", timeout=5).text
+        assert "bgc_malloc_trim_memory_limit_bytes 2097152" in text
