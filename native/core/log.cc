@@ -39,37 +39,45 @@ std::atomic<void (*)(const std::string&)> g_sink{nullptr};
 
 // Asynchronous stderr writer: log lines are appended to a buffer and one thread writes
 // them in batches (one write(2) per batch instead of one per line through stdio's stderr
-// lock).  ERROR lines, and everything before them, are written synchronously; the buffer
-// is flushed at exit and by log::flush().  BGC_LOG_SYNC=1 writes every line directly.
-//
-// The write(2) itself runs outside the buffer lock (under io_mu_, taken before the buffer
-// lock is released, so batches keep their order): a stderr that blocks — a container
+// lock).  No logging thread ever waits for stderr: a stderr that blocks — a container
 // runtime's pipe that is read slowly, a log file under dirty-page writeback throttling —
-// must not stall every thread that logs a line (the admission server logs each review, the
-// controller each reconcile).
+// must not stall the threads that log (the admission server logs each review at INFO and
+// each deny at ERROR, the controller each reconcile).
+//
+//  * append() only touches the buffer under mu_.  An ERROR line wakes the writer at once
+//    (no coalescing delay) instead of writing synchronously.
+//  * Past kMaxBuffered bytes lines are dropped and counted (lines_dropped(), exported as
+//    bgc_log_lines_dropped_total); the next batch written after stderr drains ends with one
+//    "N log lines dropped" line at the place the gap occurred.
+//  * Batches are taken and written under io_mu_, which is always taken BEFORE mu_ and never
+//    while mu_ is held, so batches reach stderr in the order their lines were appended.
+//  * flush() (exit, shutdown, tests) writes everything buffered; it is the one caller that
+//    may wait for stderr.  BGC_LOG_SYNC=1 flushes after every line (debugging only).
 class AsyncWriter {
  public:
   static AsyncWriter& instance() {
     static AsyncWriter* w = new AsyncWriter();  // never destroyed: usable from atexit handlers
     return *w;
   }
-  void append(const std::string& line, bool sync) {
-    std::unique_lock<std::mutex> lk(mu_);
-    buf_ += line;
-    if (sync || buf_.size() >= kMaxBuffered) {
-      flush_locked(lk);
+  void append(const std::string& line, bool urgent) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (buf_.size() + line.size() > kMaxBuffered && !buf_.empty()) {
+      ++dropped_pending_;
+      dropped_total_.fetch_add(1, std::memory_order_relaxed);
       return;
     }
+    buf_ += line;
     if (!thread_started_) start_locked();
-    if (!wake_pending_) {
+    if (urgent) urgent_ = true;
+    if (!wake_pending_ || urgent) {
       wake_pending_ = true;
       cv_.notify_one();
     }
   }
-  void flush() {
-    std::unique_lock<std::mutex> lk(mu_);
-    flush_locked(lk);
-  }
+  // Writes everything appended before the call.  Waits for stderr; never holds mu_ while
+  // it does.
+  void flush() { write_batch(); }
+  uint64_t dropped() const { return dropped_total_.load(std::memory_order_relaxed); }
 
  private:
   static constexpr size_t kMaxBuffered = 1 << 20;
@@ -81,30 +89,37 @@ class AsyncWriter {
       sigset_t all;
       sigfillset(&all);
       pthread_sigmask(SIG_BLOCK, &all, nullptr);
-      std::unique_lock<std::mutex> lk(mu_);
       while (true) {
-        cv_.wait(lk, [&] { return wake_pending_; });
-        // let a burst of lines from other threads accumulate into one write
-        lk.unlock();
-        std::this_thread::sleep_for(std::chrono::microseconds(500));
-        lk.lock();
-        wake_pending_ = false;
-        flush_locked(lk);  // unlocks
-        lk.lock();
+        {
+          std::unique_lock<std::mutex> lk(mu_);
+          cv_.wait(lk, [&] { return wake_pending_; });
+          if (!urgent_) {
+            // let a burst of lines from other threads accumulate into one write; an ERROR
+            // line cuts the wait short
+            cv_.wait_for(lk, std::chrono::microseconds(500), [&] { return urgent_; });
+          }
+          wake_pending_ = false;
+          urgent_ = false;
+        }
+        write_batch();
       }
     }).detach();
   }
-  // Takes the batch, then writes it with only io_mu_ held.  Returns with `lk` unlocked.
-  void flush_locked(std::unique_lock<std::mutex>& lk) {
-    if (buf_.empty()) {
-      lk.unlock();
-      return;
-    }
+  // Takes the current batch under io_mu_ (then briefly mu_) and writes it with only io_mu_
+  // held.
+  void write_batch() {
+    std::lock_guard<std::mutex> io(io_mu_);
     std::string out;
-    out.swap(buf_);
-    if (buf_.capacity() == 0) buf_.reserve(out.capacity());
-    std::unique_lock<std::mutex> io(io_mu_);  // the previous batch is out before this one
-    lk.unlock();
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (buf_.empty()) return;
+      out.swap(buf_);
+      if (buf_.capacity() == 0) buf_.reserve(std::min(out.capacity(), kMaxBuffered));
+      if (dropped_pending_ > 0) {
+        out += "log: " + std::to_string(dropped_pending_) + " log lines dropped (stderr blocked)\n";
+        dropped_pending_ = 0;
+      }
+    }
     size_t off = 0;
     while (off < out.size()) {
       ssize_t n = ::write(2, out.data() + off, out.size() - off);
@@ -115,11 +130,14 @@ class AsyncWriter {
       off += static_cast<size_t>(n);
     }
   }
-  std::mutex mu_;     // buf_ and the writer's wake-up state
-  std::mutex io_mu_;  // one batch written at a time, in order; taken after mu_
+  std::mutex io_mu_;  // one batch taken and written at a time; taken before mu_, never under it
+  std::mutex mu_;     // buf_, the drop count and the writer's wake-up state
   std::condition_variable cv_;
   std::string buf_;
+  uint64_t dropped_pending_ = 0;  // dropped since the last batch (mu_)
+  std::atomic<uint64_t> dropped_total_{0};
   bool wake_pending_ = false;
+  bool urgent_ = false;
   bool thread_started_ = false;
 };
 
@@ -285,7 +303,11 @@ void write(Level lvl, std::string_view target, std::string_view msg) {
     sink(line);
     return;
   }
-  AsyncWriter::instance().append(line, g_sync_writes || lvl >= Level::Error);
+  auto& w = AsyncWriter::instance();
+  w.append(line, lvl >= Level::Error);
+  if (g_sync_writes) w.flush();
 }
+
+uint64_t lines_dropped() { return AsyncWriter::instance().dropped(); }
 
 }  // namespace bgc::log

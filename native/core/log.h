@@ -7,6 +7,7 @@
 #pragma once
 
 #include <atomic>
+#include <cstdint>
 #include <sstream>
 #include <string>
 #include <string_view>
@@ -23,9 +24,12 @@ bool enabled(Level lvl, std::string_view target);
 void write(Level lvl, std::string_view target, std::string_view msg);
 // Redirect output (tests); nullptr restores stderr.
 void set_sink(void (*sink)(const std::string& line));
-// Writes buffered lines now (lines go to stderr in batches from a writer thread; ERROR
-// lines and exit flush automatically).
+// Writes buffered lines now, waiting for stderr if it is blocked (lines go to stderr in
+// batches from a writer thread; an ERROR line wakes it at once; exit flushes).  Logging
+// calls themselves never wait for stderr.
 void flush();
+// Lines dropped because 1 MiB was already waiting for a blocked stderr (process lifetime).
+uint64_t lines_dropped();
 
 class Line {
  public:

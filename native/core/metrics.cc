@@ -12,6 +12,7 @@
 
 #include "core/env_config.h"
 #include "core/json.h"
+#include "core/log.h"
 
 namespace bgc::metrics {
 
@@ -317,6 +318,9 @@ void append_process_memory(std::string& out) {
         static_cast<double>(mi.uordblks + mi.hblkhd));
   gauge("bgc_heap_free_bytes", "free bytes in malloc arenas (address space; trimmed pages are not resident)",
         static_cast<double>(mi.fordblks));
+  out += "# HELP bgc_log_lines_dropped_total Log lines dropped while stderr was blocked (1 MiB already buffered)\n"
+         "# TYPE bgc_log_lines_dropped_total counter\nbgc_log_lines_dropped_total " +
+         std::to_string(log::lines_dropped()) + "\n";
 }
 
 std::vector<std::string> Registry::sample_names() const {

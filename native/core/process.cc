@@ -147,14 +147,22 @@ void init_openssl() { OPENSSL_init_crypto(OPENSSL_INIT_NO_ATEXIT, nullptr); }
 // BGC_DIE_WITH_PARENT=<pid> (test harnesses): SIGTERM this process when the process that
 // started it dies (PR_SET_PDEATHSIG), so a test run killed by a timeout leaves no service
 // behind.  The variable is removed first, so this process's own children (diagnostics
-// workers) do not inherit it; a parent already gone by now ends this process at once.
+// workers) do not inherit it.  A parent that is not the given PID — already gone, or a
+// wrapper (a profiler, a sanitizer script, a shell) between harness and service — ends this
+// process at once with status 3 and a line saying why: a misconfigured launch must fail
+// loudly, not look like a clean stop.
 static void die_with_parent_from_env() {
   const char* v = std::getenv("BGC_DIE_WITH_PARENT");
   if (!v) return;
   const long parent = std::atol(v);
   ::unsetenv("BGC_DIE_WITH_PARENT");
   ::prctl(PR_SET_PDEATHSIG, SIGTERM);
-  if (parent > 0 && ::getppid() != static_cast<pid_t>(parent)) std::_Exit(0);
+  const pid_t ppid = ::getppid();
+  if (parent > 0 && ppid != static_cast<pid_t>(parent)) {
+    std::fprintf(stderr, "BGC_DIE_WITH_PARENT=%ld but the parent process is %d (the parent exited, or a wrapper "
+                 "started this process); exiting\n", parent, static_cast<int>(ppid));
+    std::_Exit(3);
+  }
 }
 
 void process_init() {

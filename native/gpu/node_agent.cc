@@ -226,7 +226,8 @@ bool label_owner_conflicts(const NodeAgentConfig& cfg, const std::string& manage
   for (const auto& k : cfg.known_labellers) {
     if (!k.empty() && manager == k) return true;
   }
-  return operation == "Apply" && manager.rfind("kubectl", 0) != 0;
+  (void)operation;  // labelling controllers write with Update as often as with Apply
+  return manager.rfind("kubectl", 0) != 0;
 }
 
 Value foreign_field_owners(const NodeAgentConfig& cfg, const Value& node) {
@@ -797,7 +798,8 @@ void NodeAgent::publish() {
 // The plugin object exists from start() on (diagnostics fence it, health flips reach it);
 // its server and kubelet registration start only while no other advertiser is found.
 void NodeAgent::start_plugin() {
-  if (!plugin_ || plugin_started_.exchange(true)) return;
+  std::lock_guard<std::mutex> lk(plugin_mu_);
+  if (stop_.cancelled() || !plugin_ || plugin_started_.exchange(true)) return;
   plugin_->set_health(healthy_flags());
   plugin_->start();
   mark_advertised();  // ListAndWatch serves from here on
@@ -836,16 +838,27 @@ void NodeAgent::start() {
       try {
         const bool was_down = standing_down_.load();
         const bool down = check_advertisers();
-        if (down && !was_down && plugin_started_ && !plugin_stopped_.exchange(true)) {
-          // found while advertising: unregister from the kubelet until the conflict clears
-          plugin_->stop();
-          LOG_ERROR("node_agent") << "device plugin stopped: another advertiser appeared; it starts again once that "
-                                  << "advertiser is gone";
+        if (down && !was_down && plugin_started_) {
+          std::lock_guard<std::mutex> lk(plugin_mu_);
+          if (!stop_.cancelled() && !plugin_stopped_.exchange(true)) {
+            // found while advertising: unregister from the kubelet until the conflict clears
+            plugin_->stop();
+            LOG_ERROR("node_agent") << "device plugin stopped: another advertiser appeared; it starts again once "
+                                    << "that advertiser is gone";
+          }
         }
-        if (!down && was_down && !stop_.cancelled()) {
-          if (plugin_stopped_.exchange(false)) {
-            plugin_->set_health(healthy_flags());
-            plugin_->start();  // registers with the kubelet again
+        if (!down && was_down) {
+          bool restart = false;
+          {
+            std::lock_guard<std::mutex> lk(plugin_mu_);
+            // re-checked under the lock: NodeAgent::stop() cancels stop_ while holding it
+            if (!stop_.cancelled() && plugin_stopped_.exchange(false)) {
+              plugin_->set_health(healthy_flags());
+              plugin_->start();  // registers with the kubelet again
+              restart = true;
+            }
+          }
+          if (restart) {
             LOG_INFO("node_agent") << "device plugin restarted: the other advertiser is gone";
           } else {
             start_plugin();
@@ -903,11 +916,19 @@ void NodeAgent::start() {
 }
 
 void NodeAgent::stop() {
-  stop_.cancel();
+  {
+    // under plugin_mu_: a heartbeat between its stop_ check and plugin_->start() would
+    // otherwise re-register the plugin with the kubelet during shutdown
+    std::lock_guard<std::mutex> lk(plugin_mu_);
+    stop_.cancel();
+  }
   if (!pcie_lock_path_.empty()) ::unlink(pcie_lock_path_.c_str());
   // the device plugin first (unregistered, socket removed), the telemetry poller last: a
   // poll stuck in amdsmi must not keep the kubelet allocating from a stopping agent
-  if (plugin_) plugin_->stop();
+  if (plugin_) {
+    std::lock_guard<std::mutex> lk(plugin_mu_);
+    plugin_->stop();
+  }
   if (heartbeat_.joinable()) heartbeat_.join();
   if (diag_thread_.joinable()) diag_thread_.join();
   if (node_watch_.joinable()) node_watch_.join();

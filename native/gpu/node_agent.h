@@ -170,9 +170,11 @@ json::Value node_status_patch(const NodeAgentConfig& cfg, const std::vector<GpuI
 // only when the agent itself advertises through the Node status (no device plugin of its
 // own).  Label owners are a conflict only as labelling controllers (label_owner_conflicts).
 json::Value foreign_field_owners(const NodeAgentConfig& cfg, const json::Value& node);
-// A foreign owner of label_prefix.* labels is another labeller, not an admin's one-off
-// edit: it server-side applies them (kubectl's own managers excepted) or is a known
-// labeller.
+// A foreign owner of label_prefix.* labels is another labeller unless it is kubectl (an
+// admin's one-off `kubectl label/edit/patch`): most labelling controllers write with Update
+// under a manager named after their binary, so neither the operation nor a list of known
+// names can tell them apart.  known_labellers are a conflict even under a kubectl-prefixed
+// name.
 bool label_owner_conflicts(const NodeAgentConfig& cfg, const std::string& manager, const std::string& operation);
 
 class NodeAgent {
@@ -240,6 +242,9 @@ class NodeAgent {
   std::atomic<bool> standing_down_{false};
   std::atomic<bool> plugin_started_{false};
   std::atomic<bool> plugin_stopped_{false};  // stopped for a conflict found while advertising
+  // Serialises the plugin's start/stop transitions with NodeAgent::stop(): once stop() has
+  // taken it and cancelled stop_, no heartbeat restarts (re-registers) the plugin.
+  std::mutex plugin_mu_;
   mutable std::mutex conflict_mu_;
   json::Value conflicts_ = json::Value::array();
   std::string conflict_sig_;  // last conflict set reported (one Event per change)

@@ -28,8 +28,11 @@ struct WatchSlot {
   int64_t deadline_ms = 0;
   std::atomic<int64_t> last_ns{0};  // last event, bookmark, list or (re)started stream
   std::atomic<bool> synced{false};  // the initial list has been delivered
-  // Gap between the last two BOOKMARKs of one stream: the server's heartbeat, once seen
-  // (a real apiserver sends one about every minute, kube-lite every --bookmark-ms).
+  // Largest gap seen between two consecutive BOOKMARKs of one stream: the server's
+  // heartbeat, once seen (a real apiserver sends one about every minute, kube-lite every
+  // --bookmark-ms).  The maximum, not the last gap: the apiserver also sends one bookmark
+  // ~2 s before a watch's timeoutSeconds, and that short gap must not make a quiet,
+  // healthy watch look stale seconds later.
   std::atomic<int64_t> heartbeat_ns{0};
 };
 
@@ -270,7 +273,12 @@ void Watcher::run(CancelToken& stop, const std::function<void(const WatchEvent&)
         if (!new_rv.empty()) rv = new_rv;
         if (type == "BOOKMARK") {
           const int64_t now = metrics::now_ns();
-          if (last_bookmark_ns) slot->heartbeat_ns.store(now - last_bookmark_ns, std::memory_order_relaxed);
+          if (last_bookmark_ns) {
+            const int64_t gap = now - last_bookmark_ns;
+            int64_t cur = slot->heartbeat_ns.load(std::memory_order_relaxed);
+            while (gap > cur && !slot->heartbeat_ns.compare_exchange_weak(cur, gap, std::memory_order_relaxed)) {
+            }
+          }
           last_bookmark_ns = now;
           if (initial_phase &&
               obj.get("metadata").get("annotations").get_string("k8s.io/initial-events-end") == "true") {

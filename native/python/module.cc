@@ -194,9 +194,11 @@ PYBIND11_MODULE(_native, m) {
   }, py::arg("rss"), py::arg("baseline"), py::arg("min_bytes"), py::arg("busy_pct"), py::arg("idle_pct"),
         py::arg("limit_bytes") = 0);
   m.def("cgroup_memory_limit_bytes", &bgc::cgroup_memory_limit_bytes);
-  // `threads` threads each log `lines` INFO lines of `width` bytes; returns the slowest single
-  // LOG_INFO call in ms (tests of the asynchronous log writer against a blocked stderr).
-  m.def("log_burst", [](int threads, int lines, int width) {
+  // `threads` threads each log `lines` INFO lines "<tag> <thread> <i> xxx..." of `width` pad
+  // bytes; thread 0's line number `error_at` (if >= 0) is an ERROR line instead.  Returns the
+  // slowest single LOG_* call in ms (tests of the asynchronous log writer against a blocked
+  // stderr).
+  m.def("log_burst", [](int threads, int lines, int width, int error_at, const std::string& tag) {
     py::gil_scoped_release nogil;
     bgc::log::init("info");
     std::atomic<int64_t> worst{0};
@@ -206,7 +208,11 @@ PYBIND11_MODULE(_native, m) {
       ts.emplace_back([&, t] {
         for (int i = 0; i < lines; ++i) {
           const auto t0 = std::chrono::steady_clock::now();
-          LOG_INFO("burst") << t << " " << i << " " << pad;
+          if (t == 0 && i == error_at) {
+            LOG_ERROR("burst") << tag << " " << t << " " << i << " " << pad;
+          } else {
+            LOG_INFO("burst") << tag << " " << t << " " << i << " " << pad;
+          }
           const int64_t ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
           int64_t cur = worst.load();
           while (ns > cur && !worst.compare_exchange_weak(cur, ns)) {
@@ -216,7 +222,12 @@ PYBIND11_MODULE(_native, m) {
     }
     for (auto& th : ts) th.join();
     return static_cast<double>(worst.load()) * 1e-6;
+  }, py::arg("threads"), py::arg("lines"), py::arg("width"), py::arg("error_at") = -1, py::arg("tag") = "burst");
+  m.def("log_flush", [] {
+    py::gil_scoped_release nogil;
+    bgc::log::flush();
   });
+  m.def("log_lines_dropped", [] { return bgc::log::lines_dropped(); });
   // A KubeClient built from a $KUBECONFIG-style path list, one request per call (tests of
   // credential plugins and multi-file merging).  Returns (status, body, credential refreshes).
   m.def("kube_request", [](const std::string& kubeconfig_list, const std::string& method, const std::string& path,

@@ -116,8 +116,10 @@ def test_unrelated_plugins_are_not_a_conflict(tmp_path):
         kubelet.stop()
 
 
-@pytest.mark.parametrize("owned", ["labels", "capacity"])
+@pytest.mark.parametrize("owned", ["labels", "labels-update", "capacity"])
 def test_stands_down_for_fields_owned_by_another_manager(owned):
+    """"labels-update" is a labeller that writes with Update under a
+    manager named after its binary and not on CONF_KNOWN_LABELLERS: still a conflict."""
     with Cluster(admission=False, controller=False) as c:
         node = "mi355x-lab"
         c.admin.create("nodes", {"apiVersion": "v1", "kind": "Node", "metadata": {"name": node}})
@@ -126,6 +128,9 @@ def test_stands_down_for_fields_owned_by_another_manager(owned):
                                           "metadata": {"name": node, "labels": {"amd.com/gpu.family": "AI",
                                                                                 "amd.com/gpu.device-id": "75a3"}}},
                           "amdgpu-node-labeller", force=True)
+        elif owned == "labels-update":
+            c.admin.merge_patch("nodes", node, {"metadata": {"labels": {"amd.com/gpu.family": "AI"}}},
+                                field_manager="k8s-node-labeller")
         else:  # another agent advertising through the Node status
             c.admin.apply("nodes", node, {"apiVersion": "v1", "kind": "Node", "metadata": {"name": node},
                                           "status": {"capacity": {"amd.com/gpu": "8"}}},
@@ -133,12 +138,14 @@ def test_stands_down_for_fields_owned_by_another_manager(owned):
         c.start_node_agent(node_name=node, backend="mock", proc_name="na-lab", extra_env={"CONF_HEARTBEAT_SECS": "1"})
         wait_for(lambda: _events(c, "GPUAdvertiserConflict", node), timeout=10, desc="conflict event")
         [conf] = _gpus(c, node)["advertiser"]["conflicts"]
-        assert conf["kind"] == owned
-        assert conf["manager"] == ("amdgpu-node-labeller" if owned == "labels" else "other-gpu-agent")
+        assert conf["kind"] == owned.split("-")[0]
+        assert conf["manager"] == {"labels": "amdgpu-node-labeller", "labels-update": "k8s-node-labeller",
+                                   "capacity": "other-gpu-agent"}[owned]
+        assert conf["conflict"] is True
         got = c.admin.get("nodes", node)
         labels = got["metadata"].get("labels", {})
         assert "amd.com/gpu.count" not in labels
-        if owned == "labels":
+        if owned.startswith("labels"):
             assert labels["amd.com/gpu.family"] == "AI"  # not forced over
             assert "amd.com/gpu" not in got.get("status", {}).get("capacity", {})
         assert not any(c["type"] == "AMDGPUHealthy" for c in got.get("status", {}).get("conditions", []))
