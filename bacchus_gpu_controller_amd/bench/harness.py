@@ -590,13 +590,35 @@ def _rate_names(rank, key, rate, part, n):
     return [f"r{rank}-{key}{int(rate)}{part}-u{i}" for i in range(n)]
 
 
+def _debug_processes(info):
+    """(process, base URL, TLS verify) of every process serving /debug/trace and /debug/stalls."""
+    return [("kube-lite", info["server"], info["apiserver_verify"]), ("controller", info["controller"], None),
+            ("admission", info["admission"], info["ca"]), ("synchronizer", info["synchronizer"], None),
+            ("node-agent", info["node_agent"], None)]
+
+
+def _debug_call(method, url, verify, data=None):
+    import requests
+
+    try:
+        r = requests.request(method, url, data=data, timeout=30, verify=verify)
+        return r.json() if r.status_code == 200 and method != "POST" else None
+    except Exception:  # noqa: BLE001
+        return None
+
+
 def _rate_phase(d, nat, info, args, key, rate, cluster):
     """Open-loop latency at a fixed offered rate: tenants arrive as a Poisson
     process of `rate` CR/s over the whole job (each rank offers rate/world), whatever the
     system's progress, and each leaves once Ready.  Unlike the closed-loop phases, whose
     latencies grow with the CR/s they reach (a faster controller queues more work on the
     same CPUs), every arm here carries the same load, so reconcile p99 and admission p50
-    compare like for like.  `--latency-window-s` timed after `--latency-warmup-s` untimed."""
+    compare like for like.  `--latency-window-s` timed after `--latency-warmup-s` untimed.
+
+    The timed window is traced: every process marks each tenant's stages
+    (native/core/trace.h) and keeps its stalls (native/core/stall.h); bench/attribution.py
+    joins them into the per-stage table of the window ("attribution")."""
+    from bacchus_gpu_controller_amd.bench import attribution
     from bacchus_gpu_controller_amd.testing.cluster import ADMIN_TOKEN
 
     per_rank = rate / d.world
@@ -609,27 +631,50 @@ def _rate_phase(d, nat, info, args, key, rate, cluster):
     if d.rank == 0:
         _settle(info)
     d.barrier()
+    traced = args.trace_windows
+    prefixes = ",".join(f"r{r}-{key}{int(rate)}t" for r in range(d.world))
     try:
         driver.open_loop(_rate_names(d.rank, key, rate, "w", n_warm), args.latency_warmup_s, args.timeout, 7 + d.rank)
         d.barrier()
         starts = thr0 = rq0 = None
         pids = [os.getpid()] + [p.p.pid for p in cluster.procs.values()] if d.rank == 0 and cluster else []
+        if traced:
+            nat.trace_arm(prefixes)
+            nat.stall_take()
         if d.rank == 0:
             starts = {k: _clear(url, verify) for k, (url, verify) in _sample_logs(info).items()}
             thr0 = cgroup_throttling()
             rq0 = runqueue_wait_ms(pids)
+            if traced:
+                for _, base, verify in _debug_processes(info):
+                    _debug_call("POST", base + "/debug/trace", verify, data=prefixes)
+                    _debug_call("DELETE", base + "/debug/stalls", verify)
         d.barrier()
         res = json.loads(driver.open_loop(_rate_names(d.rank, key, rate, "t", n_timed), args.latency_window_s,
                                           args.timeout, 1000 + d.rank))
         d.barrier()
         thr1 = cgroup_throttling() if d.rank == 0 else None
         rq1 = runqueue_wait_ms(pids) if d.rank == 0 else None
+        mine = {"trace": json.loads(nat.trace_take()), "stalls": json.loads(nat.stall_take())} if traced else None
     finally:
         driver.stop()
     per = d.gather_obj({k: res[k] for k in ("ready", "failed", "timeouts", "offered_rate", "achieved_rate",
                                             "issue_lag_p99_s", "ready_latency_s", "errors")})
+    drv = d.gather_obj(mine)
     if d.rank != 0:
         return None
+    traces, stalls = [], []
+    if traced:
+        for proc, base, verify in _debug_processes(info):
+            traces.append(_debug_call("DELETE", base + "/debug/trace", verify))
+            st = _debug_call("DELETE", base + "/debug/stalls", verify)
+            if st is not None:
+                st["process"] = proc
+            stalls.append(st)
+        for r, m in enumerate(drv):
+            traces.append(m["trace"])
+            m["stalls"]["process"] = f"load-driver-r{r}"
+            stalls.append(m["stalls"])
     docs = {k: _samples(url, verify) for k, (url, verify) in _sample_logs(info).items()}
     rec = window_samples(docs["reconcile"], starts.get("reconcile"))
     hook = window_samples(docs["webhook"], starts.get("webhook"))
@@ -647,15 +692,105 @@ def _rate_phase(d, nat, info, args, key, rate, cluster):
            "apply_to_ready_p50_ms": ms(_pct(lat, 0.50)), "apply_to_ready_p99_ms": ms(_pct(lat, 0.99)),
            "issue_lag_p99_ms": ms(max(p["issue_lag_p99_s"] for p in per)),
            "ready_crs": sum(p["ready"] for p in per),
-           "failed_crs": sum(p["failed"] + p["timeouts"] for p in per)}
+           "failed_crs": sum(p["failed"] + p["timeouts"] for p in per),
+           # raw samples for pooling a rate's windows (removed before the output is printed)
+           "_raw": {"rec": rec, "hook": hook, "lat": lat}}
     if thr0 and thr1:
         out["cgroup_throttled_periods"] = thr1["throttled"] - thr0["throttled"]
     if rq0 is not None and rq1 is not None:
         # CPU-ms the job's threads waited in run queues per second of window
         out["runqueue_wait_ms_per_s"] = round((rq1 - rq0) / max(args.latency_window_s, 1e-9), 1)
+    if traced:
+        out["attribution"] = attribution.analyze(traces, stalls, tail_ms=args.tail_ms)
+        out["attribution"]["trace_marks"] = sum(len((t or {}).get("marks", [])) for t in traces)
+        out["attribution"]["trace_dropped"] = sum((t or {}).get("dropped", 0) for t in traces)
     errs = [e for p in per for e in p["errors"]]
     if errs:
         out["errors"] = errs[:3]
+    return out
+
+
+_WINDOW_KEYS = ("offered_rate", "achieved_rate", "achieved_within_2pct", "reconcile_p99_ms", "reconcile_p50_ms",
+                "reconciles", "admission_p50_ms", "admission_p99_ms", "admission_handler_p50_ms",
+                "apply_to_ready_p50_ms", "apply_to_ready_p99_ms", "issue_lag_p99_ms", "ready_crs", "failed_crs",
+                "cgroup_throttled_periods", "runqueue_wait_ms_per_s", "errors")
+
+
+def _pool_arm(results, prefix, rates, windows):
+    """Per rate: the arm's windows pooled (percentiles over every sample of its windows) plus
+    each window's own row, in run order."""
+    ms = lambda v: None if v is None else round(v * 1e3, 4)  # noqa: E731
+    out = {}
+    for i, r in enumerate(rates):
+        ws = [results[f"{prefix}{i}w{k}"] for k in range(windows) if results.get(f"{prefix}{i}w{k}")]
+        if not ws:
+            continue
+        rec = [x for w in ws for x in w["_raw"]["rec"]]
+        hook = [x for w in ws for x in w["_raw"]["hook"]]
+        lat = [x for w in ws for x in w["_raw"]["lat"]]
+        out[f"{r:g}"] = {"offered_rate": round(sum(w["offered_rate"] for w in ws) / len(ws), 1),
+                         "achieved_rate": round(sum(w["achieved_rate"] for w in ws) / len(ws), 1),
+                         "reconcile_p99_ms": ms(_pct(rec, 0.99)), "reconcile_p50_ms": ms(_pct(rec, 0.50)),
+                         "admission_p50_ms": ms(_pct(hook, 0.50)), "apply_to_ready_p50_ms": ms(_pct(lat, 0.50)),
+                         "apply_to_ready_p99_ms": ms(_pct(lat, 0.99)),
+                         "ready_crs": sum(w["ready_crs"] for w in ws), "failed_crs": sum(w["failed_crs"] for w in ws),
+                         "windows": [{k: w[k] for k in _WINDOW_KEYS if k in w} for w in ws]}
+    return out
+
+
+def _stage_summary(results, prefix, rates, windows, top=3):
+    """Compact per-stage table of an arm (the bench line's last field, so the driver's
+    2,000-character tail of the output keeps it): per rate, the apply->Ready p99 of each
+    window, the critical-path segments with the largest p99 (worst window), and which
+    segment the tail tenants spent the most in, summed over the windows."""
+    out = {}
+    for i, r in enumerate(rates):
+        atts = [results[f"{prefix}{i}w{k}"].get("attribution") for k in range(windows)
+                if results.get(f"{prefix}{i}w{k}")]
+        atts = [a for a in atts if a]
+        if not atts:
+            continue
+        seg = {}
+        for a in atts:
+            for k, v in a["segments"].items():
+                if v["p99_ms"] is not None:
+                    seg[k] = max(seg.get(k, 0.0), v["p99_ms"])
+        blame, stall = {}, {}
+        for a in atts:
+            for k, n in a["tail"]["blame"].items():
+                blame[k] = blame.get(k, 0) + n
+            for k, n in a["tail"]["stall_overlap"].items():
+                stall[k] = stall.get(k, 0) + n
+        r2 = lambda v: None if v is None else round(v, 2)  # noqa: E731
+        out[f"{r:g}"] = {"a2r_p99": [r2(a["apply_to_ready_p99_ms"]) for a in atts],
+                         "seg_p99": {k: r2(v) for k, v in sorted(seg.items(), key=lambda kv: -kv[1])[:top]},
+                         "tail_n": sum(a["tail"]["n"] for a in atts),
+                         "tail_blame": dict(sorted(blame.items(), key=lambda kv: -kv[1])[:2]),
+                         "tail_stalls": stall}
+    return out
+
+
+def _latency_at_rate(results, rates, windows, args):
+    this_q = _pool_arm(results, "qa", rates, windows)
+    ref_q = _pool_arm(results, "qb", rates, windows)
+    out = {"rates_cr_per_s": [float(f"{r:g}") for r in rates], "window_s": args.latency_window_s,
+           "windows_per_arm": windows, "order": "A B B A (this, reference, reference, this)",
+           "arrivals": "poisson (open loop)", "this": this_q}
+    if ref_q:
+        out["reference_controller"] = ref_q
+        out["this_over_reference"] = _compare_at_rate(this_q, ref_q)
+    att = {}
+    for arm, prefix in (("this", "qa"), ("reference_controller", "qb")):
+        per = {}
+        for i, r in enumerate(rates):
+            ws = [results[f"{prefix}{i}w{k}"].get("attribution") for k in range(windows)
+                  if results.get(f"{prefix}{i}w{k}")]
+            if any(ws):
+                per[f"{r:g}"] = ws
+        if per:
+            att[arm] = per
+    if att:
+        out["attribution"] = att
     return out
 
 
@@ -674,6 +809,15 @@ def _compare_at_rate(this, ref):
                                                and t["reconcile_p99_ms"] < r["reconcile_p99_ms"])
         row["this_lower_admission_p50"] = bool(t.get("admission_p50_ms") is not None and r.get("admission_p50_ms")
                                                and t["admission_p50_ms"] < r["admission_p50_ms"])
+        # window by window (this build's k-th window against the reference arm's k-th)
+        tw, rw = t.get("windows") or [], r.get("windows") or []
+        pairs = list(zip(tw, rw))
+        if pairs:
+            row["reconcile_p99_lower_by_window"] = [bool(a.get("reconcile_p99_ms") is not None and b.get("reconcile_p99_ms")
+                                                         and a["reconcile_p99_ms"] < b["reconcile_p99_ms"])
+                                                    for a, b in pairs]
+            row["apply_to_ready_p99_ms_by_window"] = [[a.get("apply_to_ready_p99_ms"), b.get("apply_to_ready_p99_ms")]
+                                                      for a, b in pairs]
         out[rate] = row
     return out
 
@@ -795,6 +939,8 @@ def run(args):
     from bacchus_gpu_controller_amd.testing.fake_google import FakeGoogle
 
     nat = native()
+    if args.trace_windows:
+        nat.stall_start("load-driver")  # the load generator's own stalls, next to the services'
     cluster = google = None
     info = None
     cpus = effective_cpus()
@@ -816,24 +962,34 @@ def run(args):
                              args.warmup, args.steps, isolated=True))
     semantics = "reference" if args.reference_semantics else args.semantics
     rates = [float(x) for x in args.latency_rates.split(",") if x.strip()]
+    windows = max(1, args.latency_windows)
+    # Open loop at equal offered load, the arms interleaved A B B A: this
+    # build's first window per rate, the reference-controller arm's windows, then this
+    # build's remaining windows, so drift of the box over the run hits both arms alike.
+    qa = lambda k: [_Phase(f"qa{i}w{k}", 0, args.webhook_protocol, semantics0, args.write_latency_ms, 0, 0,  # noqa: E731
+                           rate=r) for i, r in enumerate(rates)]
     if rates:
-        # open loop at equal offered load: this build first (its controller is running) ...
-        phases += [_Phase(f"q{i}", 0, args.webhook_protocol, semantics0, args.write_latency_ms, 0, 0, rate=r)
-                   for i, r in enumerate(rates)]
+        phases += qa(0)
     if args.reference_arms and semantics == "this":
         # same-stack comparison, timed like the headline: the reference's controller
         # behaviour (controller.rs:81-154: sequential, unconditional applies) on this stack,
         # at the headline's storage latency and with a write-latency (etcd commit) model
         phases.append(_Phase("rc", conc, args.webhook_protocol, "reference-controller", args.write_latency_ms,
                              args.warmup, args.steps))
-        # ... then the reference controller at the same rates, while it runs
-        phases += [_Phase(f"qr{i}", 0, args.webhook_protocol, "reference-controller", args.write_latency_ms, 0, 0,
-                          rate=r) for i, r in enumerate(rates)]
+        # ... then the reference controller's windows at the same rates, while it runs
+        phases += [_Phase(f"qb{i}w{k}", 0, args.webhook_protocol, "reference-controller", args.write_latency_ms, 0, 0,
+                          rate=r) for k in range(windows) for i, r in enumerate(rates)]
         if args.arm_write_latency_ms > 0 and secondary:
             phases.append(_Phase("rl", conc, args.webhook_protocol, "reference-controller",
                                  args.arm_write_latency_ms, args.arm_warmup, args.arm_steps))
+        for k in range(1, windows):
+            phases += qa(k)
+        if args.arm_write_latency_ms > 0 and secondary:
             phases.append(_Phase("ml", conc, args.webhook_protocol, "this", args.arm_write_latency_ms,
                                  args.arm_warmup, args.arm_steps))
+    else:
+        for k in range(1, windows):
+            phases += qa(k)
     if args.tuned_phase and tuned != conc and secondary:
         phases.append(_Phase("t", tuned, args.webhook_protocol, semantics0, args.write_latency_ms,
                              args.warmup, args.steps))
@@ -1037,16 +1193,7 @@ def run(args):
                 "this": this_l, "reference_controller": ref_l,
                 "this_over_reference_cr_per_s": ratio(this_l["value"], ref_l["value"])}
         if rates:
-            this_q = {f"{r:g}": results[f"q{i}"] for i, r in enumerate(rates) if results.get(f"q{i}")}
-            ref_q = {f"{r:g}": results[f"qr{i}"] for i, r in enumerate(rates) if results.get(f"qr{i}")}
-            for v in list(this_q.values()) + list(ref_q.values()):
-                v.pop("semantics", None)
-            out["latency_at_rate"] = {"rates_cr_per_s": [float(f"{r:g}") for r in rates],
-                                      "window_s": args.latency_window_s, "arrivals": "poisson (open loop)",
-                                      "this": this_q}
-            if ref_q:
-                out["latency_at_rate"]["reference_controller"] = ref_q
-                out["latency_at_rate"]["this_over_reference"] = _compare_at_rate(this_q, ref_q)
+            out["latency_at_rate"] = _latency_at_rate(results, rates, windows, args)
         # amdsmi counters of the advertised GPUs at the end of the timed region (node agent)
         out["gpu_telemetry"] = gpu_tel
         phase_wall["total"] = round(time.monotonic() - t_run, 2)
@@ -1102,6 +1249,11 @@ def run(args):
                                                              "bgc_controller_own_write_events_total"))}
             except Exception:  # noqa: BLE001
                 pass
+        if rates and args.trace_windows:
+            # last, so the driver's 2,000-character tail of the output keeps it: the per-stage
+            # table of each arm (full tables in latency_at_rate.attribution)
+            out["stage_table"] = {"this": _stage_summary(results, "qa", rates, windows),
+                                  "reference_controller": _stage_summary(results, "qb", rates, windows)}
         return out
     except BaseException:
         if cluster is not None:
@@ -1172,8 +1324,15 @@ def main(argv=None):
     ap.add_argument("--latency-rates", default="2000,6000",
                     help="open-loop offered rates (CR/s, whole job) at which this build and the reference-controller "
                          "arm are both timed (latency_at_rate; '' = none)")
-    ap.add_argument("--latency-window-s", type=float, default=2.0, help="timed window of each open-loop phase")
-    ap.add_argument("--latency-warmup-s", type=float, default=1.0, help="untimed lead-in of each open-loop phase")
+    ap.add_argument("--latency-window-s", type=float, default=1.0, help="timed window of each open-loop phase")
+    ap.add_argument("--latency-warmup-s", type=float, default=0.5, help="untimed lead-in of each open-loop phase")
+    ap.add_argument("--latency-windows", type=int, default=2,
+                    help="timed windows per rate and arm, interleaved A B B A with the reference-controller arm")
+    ap.add_argument("--trace-windows", action=argparse.BooleanOptionalAction, default=True,
+                    help="trace every tenant of each open-loop window through every process and attribute its "
+                         "apply->Ready time to stages (latency_at_rate.attribution; bench/attribution.py)")
+    ap.add_argument("--tail-ms", type=float, default=5.0,
+                    help="attribution: tenants above max(p99, this) apply->Ready are the window's tail")
     ap.add_argument("--latency-workers", type=int, default=128,
                     help="open loop: threads issuing creates per rank (arrivals never wait for one below ~that "
                          "many in flight)")

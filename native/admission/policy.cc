@@ -6,6 +6,8 @@
 #include "core/crypto.h"
 #include "core/json_patch.h"
 #include "core/log.h"
+#include "core/trace.h"
+#include "core/metrics.h"
 #include "crd/schema.h"
 
 namespace bgc::admission {
@@ -219,6 +221,7 @@ const P kReviewRoot{"", P::Descend, kReview, std::size(kReview)};
 }  // namespace
 
 HttpResult handle_review(const std::string& body, const std::string& content_type, const Config& cfg) {
+  const int64_t t_recv = trace::armed() ? metrics::now_ns() : 0;
   HttpResult r;
   if (content_type.find("application/json") == std::string::npos) {
     r.status = 415;
@@ -274,6 +277,12 @@ HttpResult handle_review(const std::string& body, const std::string& content_typ
   }
   r.decision = mutate(req, cfg);
   r.body = review_response(r.decision, api_version);
+  if (trace::armed()) {
+    const Value& o = req.get("object").is_object() ? req.get("object") : req.get("oldObject");
+    const std::string name = o.get("metadata").get_string("name");
+    trace::mark_at(name, "adm.review0." + op, t_recv);
+    trace::mark(name, "adm.review1." + op);
+  }
   return r;
 }
 

@@ -25,6 +25,7 @@
 #include "core/json_patch.h"
 #include "core/log.h"
 #include "core/metrics.h"
+#include "core/trace.h"
 #include "core/net.h"
 #include "core/yaml.h"
 #include "crd/schema.h"
@@ -659,6 +660,16 @@ struct ParsedPath {
   std::string sub;
   bool collection = false;
 };
+
+// Per-request trace context (core/trace.h), on the thread that serves the request: set by
+// Impl::handle while the bench has tracing armed, read by write()/do_delete to mark the
+// webhook call and the commit.  Empty when not tracing.
+thread_local std::string t_trace_tag;   // "<plural>[/sub].<METHOD>.<field manager>"
+thread_local std::string t_trace_name;  // the object's name (a tenant's, for every child)
+
+void trace_step(const std::string& name, const char* step) {
+  if (!t_trace_tag.empty()) trace::mark(name, t_trace_tag + step);
+}
 
 struct WriteResult {
   std::shared_ptr<const Value> obj;
@@ -1793,7 +1804,9 @@ struct ApiServer::Impl {
       if (exists && same_content(obj, *cur_copy.obj) && managers == *cur_copy.managers) {
         return {cur_copy.obj, 200, nullptr};
       }
+      trace_step(name, ".hook0");
       call_webhooks(ti, sub, op, ns, name, &obj, exists ? cur_copy.obj.get() : nullptr, user);
+      trace_step(name, ".hook1");
       // identity fields cannot be changed by mutation
       obj["metadata"]["name"] = name;
       if (ti.rt.namespaced) obj["metadata"]["namespace"] = ns;
@@ -1825,12 +1838,14 @@ struct ApiServer::Impl {
         }
         (void)is_status;
         WriteResult wr;
+        trace_step(name, ".commit");  // before the event is published: causally before its watch marks
         wr.obj = commit_locked(ti, ns, name, std::move(obj), std::move(managers), &it->second, &pe, nullptr, &wr.line);
         return wr;
       }
       if (ti.rt.plural == "customresourcedefinitions") register_crd(obj);
       bool dangling = false;
       std::shared_ptr<const std::string> line;
+      trace_step(name, ".commit");
       auto created = commit_locked(ti, ns, name, std::move(obj), std::move(managers), nullptr, &pe, &dangling, &line);
       // The garbage collector also removes dependents created with only dangling owner
       // references (e.g. a controller re-applying a child right after its owner was
@@ -1914,6 +1929,7 @@ struct ApiServer::Impl {
       for (unsigned char c : rnd) name.push_back(alnum[c % 27]);
     }
     std::string manager = field_manager(req, "unknown");
+    if (!t_trace_tag.empty()) t_trace_name = name;
     auto res = write(*p.ti, p.ns, name, "", user,
                      [&](const Stored* cur) -> std::pair<Value, Managers> {
                        if (cur) throw already_exists(p.ti->rt, name);
@@ -2116,7 +2132,9 @@ struct ApiServer::Impl {
       if (it == sh.objs.end()) throw not_found(p.ti->rt, p.name);
       cur = it->second.obj;
     }
+    trace_step(p.name, ".hook0");
     call_webhooks(*p.ti, "", "DELETE", p.ns, p.name, nullptr, cur.get(), user);
+    trace_step(p.name, ".hook1");
     StoreLock lk(sh.mu, p.ti->store->stats);
     auto it = sh.objs.find(key);
     if (it == sh.objs.end()) throw not_found(p.ti->rt, p.name);
@@ -2262,6 +2280,7 @@ struct ApiServer::Impl {
     int timeout_s = opts.max_watch_seconds;
     if (req.has_query_param("timeoutSeconds")) timeout_s = std::min(timeout_s, std::atoi(req.query_param("timeoutSeconds").c_str()));
     bool bookmarks = req.query_param("allowWatchBookmarks") == "true";
+    const std::string trace_watch = "kl.watch." + p.ti->rt.plural + "." + field_manager(req, "unknown") + ".sent";
     // Streaming lists (WatchList): sendInitialEvents=true replays the current state as
     // ADDED events, then a BOOKMARK annotated k8s.io/initial-events-end marks the point
     // where the initial state is complete (requires allowWatchBookmarks and
@@ -2371,6 +2390,9 @@ struct ApiServer::Impl {
       if (!batch.empty()) {
         std::string buf;
         for (auto& q : batch) buf += q.e->line_as(q.view, meta_only);
+        if (trace::armed()) {  // before the write: causally before the watcher's own marks
+          for (auto& q : batch) trace::mark(q.e->meta->get("metadata").get_string("name"), trace_watch);
+        }
         if (!w.write_chunk(buf)) break;
       }
       if (closed || overflow) break;
@@ -2698,6 +2720,19 @@ struct ApiServer::Impl {
         im->req_counts[k]++;
       }
     } count{this, req, w_count, res_key};
+    // trace (core/trace.h): request received ... response sent, per traced object
+    struct TraceSpan {
+      int64_t t_recv = 0;
+      ~TraceSpan() {
+        if (!t_trace_tag.empty() && !t_trace_name.empty()) {
+          trace::mark_at(t_trace_name, t_trace_tag + ".recv", t_recv);
+          trace::mark(t_trace_name, t_trace_tag + ".resp");
+        }
+        t_trace_tag.clear();
+        t_trace_name.clear();
+      }
+    } span;
+    if (trace::armed()) span.t_recv = metrics::now_ns();
     try {
       int hold_ms = 0;
       if (inject_fault(req, w_conn, &hold_ms)) return;
@@ -2732,6 +2767,10 @@ struct ApiServer::Impl {
       if (p.collection && req.method == "GET") {
         std::string wq = req.query_param("watch");
         if (wq == "1" || wq == "true") res_key += " watch";
+      }
+      if (span.t_recv && req.method != "GET") {
+        t_trace_tag = "kl." + res_key + "." + req.method + "." + field_manager(req, "unknown");
+        t_trace_name = p.name;  // a create names its object in the body: do_create sets it
       }
       if (!p.sub.empty() && p.sub != "status") throw StatusError(404, "NotFound", "subresource not supported: " + p.sub);
       if (!p.sub.empty() && !p.ti->rt.has_status) throw StatusError(404, "NotFound", "the server could not find the requested resource");

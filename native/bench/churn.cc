@@ -9,6 +9,7 @@
 #include "core/log.h"
 #include "core/metrics.h"
 #include "core/net.h"
+#include "core/trace.h"
 #include "kube/runtime.h"
 
 namespace bgc::bench {
@@ -76,6 +77,7 @@ void ChurnDriver::mark(const std::string& name, int which, int64_t t) {
   int64_t* slot = which == 0 ? &tr.t_ns : which == 1 ? &tr.t_rq : &tr.t_rb;
   if (*slot) return;
   *slot = t;
+  if (trace::armed()) trace::mark_at(name, which == 0 ? "drv.ns_seen" : which == 1 ? "drv.rq_seen" : "drv.rb_seen", t);
   if (tr.delete_when_ready && ready_locked(tr)) issue_delete(name);
   // approve-after-create waits on Namespaces alone; otherwise only Ready matters
   if (ready_locked(tr) || (which == 0 && !opts_.approve_url.empty())) cv_.notify_all();
@@ -261,7 +263,9 @@ json::Value ChurnDriver::open_loop(const std::vector<std::string>& names, double
     std::this_thread::sleep_until(base + std::chrono::nanoseconds(offset[i]));
     lag[i] = metrics::now_ns() - (t0 + offset[i]);
     const std::string& name = names[i];
+    if (trace::armed()) trace::mark_at(name, "drv.sched", t0 + offset[i]);
     futs.push_back(pool_->submit([this, name] {
+      if (trace::armed()) trace::mark(name, "drv.sent");
       Value body = Value::object({{"apiVersion", "bacchus.io/v1"}, {"kind", "UserBootstrap"},
                                   {"metadata", Value::object({{"name", name}})}, {"spec", Value::object()}});
       http::Headers h;
@@ -279,6 +283,7 @@ json::Value ChurnDriver::open_loop(const std::vector<std::string>& names, double
       std::lock_guard<std::mutex> lk(mu_);
       Track& t = tracks_[name];
       t.t_created = metrics::now_ns();
+      if (trace::armed()) trace::mark_at(name, "drv.created", t.t_created);
       if (!err.empty()) {
         t.failed = true;
         t.error = err;

@@ -11,6 +11,7 @@
 #include "core/http.h"
 #include "core/log.h"
 #include "core/metrics.h"
+#include "core/stall.h"
 #include "core/net.h"
 #include "core/process.h"
 
@@ -27,6 +28,7 @@ int main() {
   try {
     cfg = admission::Config::from_env(EnvConfig("CONF_"));
     metrics::configure_debug(EnvConfig("CONF_"));  // /debug/samples: off unless CONF_DEBUG_ENDPOINTS
+    stall::start("admission");  // 1 ms oversleep sampler: bgc_stall_* (core/stall.h)
   } catch (const std::exception& e) {
     std::fprintf(stderr, "Error: %s\n", e.what());
     return 1;

@@ -11,6 +11,7 @@
 #include "core/http.h"
 #include "core/log.h"
 #include "core/metrics.h"
+#include "core/stall.h"
 #include "core/process.h"
 #include "kube/leader.h"
 #include "kube/runtime.h"
@@ -23,6 +24,7 @@ int main() {
   try {
     cfg = controller::Config::from_env(EnvConfig("CONF_"));
     metrics::configure_debug(EnvConfig("CONF_"));  // /debug/samples: off unless CONF_DEBUG_ENDPOINTS
+    stall::start("controller");  // 1 ms oversleep sampler: bgc_stall_* (core/stall.h)
     kube::Watcher::configure_from_env(EnvConfig("CONF_"));  // list paging, watch idle deadline, TCP keepalive
   } catch (const std::exception& e) {
     std::fprintf(stderr, "Error: %s\n", e.what());

@@ -16,6 +16,7 @@
 #include "core/log.h"
 #include "core/net.h"
 #include "core/process.h"
+#include "core/stall.h"
 #include "core/yaml.h"
 
 using namespace bgc;
@@ -91,6 +92,7 @@ int main(int argc, char** argv) {
   apiserver::ApiServer srv(o);
   try {
     srv.start();
+    stall::start("kube-lite");  // after start(): debug endpoints are on, stalls are kept
   } catch (const std::exception& e) {
     std::fprintf(stderr, "Error: %s\n", e.what());
     return 1;

@@ -10,6 +10,7 @@
 
 #include "core/log.h"
 #include "core/metrics.h"
+#include "core/trace.h"
 #include "kube/quantity.h"
 
 namespace bgc::controller {
@@ -336,7 +337,10 @@ void Reconciler::apply_child(const DesiredChild& c, const std::string& body_hash
     }
   } unmark{sh, key};
   const kube::ObjPtr before = store ? store->get(c.ns, c.name) : nullptr;
+  const bool traced = trace::armed();
+  if (traced) trace::mark(c.name, "ctl.apply." + c.rt->plural + ".send");
   std::string rv = client_.apply_rv(*c.rt, c.ns, c.name, body_json, kFieldManager, /*force=*/true);
+  if (traced) trace::mark(c.name, "ctl.apply." + c.rt->plural + ".done");
   applied.inc();
   if (after_apply_) after_apply_(c);
   {

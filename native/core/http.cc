@@ -1,5 +1,7 @@
 #include "core/http.h"
 
+#include <cerrno>
+
 #include <openssl/crypto.h>
 
 #include <fcntl.h>
@@ -18,6 +20,8 @@
 #include "core/http2.h"
 #include "core/log.h"
 #include "core/metrics.h"
+#include "core/stall.h"
+#include "core/trace.h"
 
 namespace bgc::http {
 
@@ -899,6 +903,16 @@ void add_standard_routes(Server& s) {
     if (body.empty()) return w.send(404, "no such sample log\n");
     w.send(200, body, "application/json");
   });
+  // Per-tenant stage marks (core/trace.h): POST <prefix> arms, GET reads, DELETE takes.
+  s.handle("POST", "/debug/trace", [](Request& r, ResponseWriter& w) {
+    trace::arm(r.body);
+    w.send(200, "armed\n");
+  });
+  s.handle("GET", "/debug/trace", [](Request&, ResponseWriter& w) { w.send(200, trace::dump_json(false), "application/json"); });
+  s.handle("DELETE", "/debug/trace", [](Request&, ResponseWriter& w) { w.send(200, trace::dump_json(true), "application/json"); });
+  // Stalls the process's stall sampler kept (core/stall.h): GET reads, DELETE takes.
+  s.handle("GET", "/debug/stalls", [](Request&, ResponseWriter& w) { w.send(200, stall::dump_json(false), "application/json"); });
+  s.handle("DELETE", "/debug/stalls", [](Request&, ResponseWriter& w) { w.send(200, stall::dump_json(true), "application/json"); });
 }
 
 // ---------------------------------------------------------------------------
@@ -986,7 +1000,10 @@ Headers Client::merged_headers(const Headers* headers) {
   if (headers) {
     for (auto& kv : headers->items()) merged.set(kv.first, kv.second);
   }
-  if (!merged.has("User-Agent")) merged.set("User-Agent", "bgc-amd/0.1");
+  // client-go's convention: "<binary>/<version>" (an apiserver's audit log, and kube-lite's
+  // default field manager and traces, name the component by it)
+  static const std::string ua = std::string(program_invocation_short_name) + "/0.1";
+  if (!merged.has("User-Agent")) merged.set("User-Agent", ua);
   return merged;
 }
 

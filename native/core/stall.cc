@@ -1,0 +1,147 @@
+#include "core/stall.h"
+
+#include <fcntl.h>
+#include <pthread.h>
+#include <signal.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "core/json.h"
+#include "core/metrics.h"
+
+namespace bgc::stall {
+
+namespace {
+
+struct Stall {
+  int64_t t_ns;        // when the late wake-up (or slow malloc) ended
+  int64_t over_ns;     // oversleep beyond the 1 ms tick
+  int64_t runq_ns;     // the sampler thread's run-queue delay over the tick
+  int64_t malloc_ns;   // one malloc+free of 32 KiB
+};
+
+constexpr int64_t kTickNs = 1000000;
+constexpr size_t kMaxKept = 1 << 16;
+// past the thread cache (tcache_max 16 KiB in the services' tunables), so the malloc takes
+// an arena lock like the services' large allocations do
+constexpr size_t kMallocBytes = 32 << 10;
+
+std::once_flag g_once;
+std::atomic<bool> g_running{false};
+std::atomic<uint64_t> g_ticks{0};
+std::mutex g_mu;
+std::string g_process;
+std::vector<Stall> g_kept;
+uint64_t g_dropped = 0;
+
+// Run-queue delay of the sampler thread so far (schedstat field 2), -1 if unavailable.  The
+// file stays open: one pread per tick.
+int64_t runq_delay_ns(int fd) {
+  if (fd < 0) return -1;
+  char buf[128];
+  const ssize_t n = ::pread(fd, buf, sizeof buf - 1, 0);
+  if (n <= 0) return -1;
+  buf[n] = '\0';
+  unsigned long long run = 0, wait = 0;
+  return std::sscanf(buf, "%llu %llu", &run, &wait) == 2 ? static_cast<int64_t>(wait) : -1;
+}
+
+std::vector<double> stall_buckets() {
+  return {50e-6, 100e-6, 200e-6, 500e-6, 1e-3, 2e-3, 5e-3, 10e-3, 20e-3, 50e-3, 100e-3, 500e-3, 1.0};
+}
+
+void loop() {
+  sigset_t all;
+  sigfillset(&all);
+  pthread_sigmask(SIG_BLOCK, &all, nullptr);
+  auto& reg = metrics::Registry::global();
+  auto& over_h = reg.histogram("bgc_stall_oversleep_seconds",
+                               "How late a 1 ms sleep of the stall sampler woke up (CPU unavailable to this process)",
+                               {}, stall_buckets());
+  auto& malloc_h = reg.histogram("bgc_stall_malloc_seconds", "One 32 KiB malloc+free of the stall sampler (an arena lock)", {},
+                                 stall_buckets());
+  const char* rec = std::getenv("BGC_STALL_RECORD_US");
+  const int64_t record_ns = (rec ? std::atoll(rec) : 2000) * 1000;
+  const bool keep = metrics::debug_endpoints_enabled();
+  const int fd = keep ? ::open("/proc/thread-self/schedstat", O_RDONLY | O_CLOEXEC) : -1;
+  struct timespec req {0, kTickNs};
+  int64_t runq0 = runq_delay_ns(fd);
+  while (true) {
+    const int64_t t0 = metrics::now_ns();
+    nanosleep(&req, nullptr);
+    const int64_t t1 = metrics::now_ns();
+    void* volatile p = std::malloc(kMallocBytes);
+    std::free(p);
+    const int64_t t2 = metrics::now_ns();
+    const int64_t over = std::max<int64_t>(0, t1 - t0 - kTickNs);
+    const int64_t mal = t2 - t1;
+    over_h.observe(static_cast<double>(over) * 1e-9);
+    malloc_h.observe(static_cast<double>(mal) * 1e-9);
+    g_ticks.fetch_add(1, std::memory_order_relaxed);
+    if (!keep) continue;
+    const int64_t runq1 = runq_delay_ns(fd);
+    const int64_t runq = runq0 >= 0 && runq1 >= 0 ? runq1 - runq0 : -1;
+    runq0 = runq1;
+    if (over >= record_ns || mal >= record_ns) {
+      std::lock_guard<std::mutex> lk(g_mu);
+      if (g_kept.size() < kMaxKept) g_kept.push_back({t2, over, runq, mal});
+      else ++g_dropped;
+    }
+  }
+}
+
+}  // namespace
+
+void start(const std::string& name) {
+  const char* e = std::getenv("BGC_STALL_SAMPLER");
+  if (e && std::strcmp(e, "0") == 0) return;
+  std::call_once(g_once, [&] {
+    {
+      std::lock_guard<std::mutex> lk(g_mu);
+      g_process = name;
+    }
+    g_running.store(true);
+    std::thread(loop).detach();
+  });
+}
+
+bool running() { return g_running.load(); }
+
+std::string dump_json(bool take) {
+  std::vector<Stall> kept;
+  json::Value out = json::Value::object();
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    out["process"] = g_process;
+    out["dropped"] = static_cast<unsigned long long>(g_dropped);
+    if (take) {
+      kept.swap(g_kept);
+      g_dropped = 0;
+    } else {
+      kept = g_kept;
+    }
+  }
+  out["running"] = running();
+  out["ticks"] = static_cast<unsigned long long>(g_ticks.load());
+  json::Value arr = json::Value::array();
+  for (const auto& s : kept) {
+    json::Value e = json::Value::array();
+    e.push_back(static_cast<long long>(s.t_ns));
+    e.push_back(static_cast<double>(s.over_ns) * 1e-3);
+    e.push_back(s.runq_ns < 0 ? json::Value() : json::Value(static_cast<double>(s.runq_ns) * 1e-3));
+    e.push_back(static_cast<double>(s.malloc_ns) * 1e-3);
+    arr.push_back(std::move(e));
+  }
+  out["stalls"] = std::move(arr);
+  return out.dump();
+}
+
+}  // namespace bgc::stall

@@ -1,0 +1,30 @@
+// Process stall sampler ("oversleep" detector).
+//
+// One thread per process sleeps 1 ms at a time and measures how late it wakes up, then
+// times one small malloc/free.  A late wake-up means the process's threads could not get a
+// CPU (run-queue wait on a saturated CPU share, CFS throttling); a slow malloc means an
+// arena was held (malloc_trim, a heap walk).  Either shows as a process-wide pause with
+// its owner — the process that reported it — which is what the bench needs to attribute
+// an apply->Ready tail to kube-lite, the load driver or one of the product binaries.
+//
+// Exported on /metrics as bgc_stall_oversleep_seconds and bgc_stall_malloc_seconds
+// histograms; with debug endpoints, every stall >= BGC_STALL_RECORD_US (default 2000 us)
+// is kept with its monotonic timestamp and the sampler thread's run-queue delay over it
+// (/proc/thread-self/schedstat) and served on /debug/stalls (GET, DELETE = take), so the
+// harness can line stalls up with its latency windows.  BGC_STALL_SAMPLER=0 disables it.
+#pragma once
+
+#include <cstdint>
+#include <string>
+
+namespace bgc::stall {
+
+// Starts the sampler thread once per process (idempotent); `name` labels the process in
+// the dump.
+void start(const std::string& name);
+bool running();
+// {"process":..,"ticks":n,"stalls":[[t_ns, oversleep_us, runq_us, malloc_us],...],
+//  "dropped":n}; `take` clears the kept stalls.
+std::string dump_json(bool take);
+
+}  // namespace bgc::stall

@@ -5,6 +5,7 @@
 #include "core/http.h"
 #include "core/log.h"
 #include "core/metrics.h"
+#include "core/trace.h"
 #include "core/net.h"
 
 namespace bgc::kube {
@@ -585,6 +586,10 @@ void Controller::run(CancelToken& stop, Reconciler reconcile, ErrorPolicy error_
     Watcher w(client_, primary_);
     w.set_projection(opts_.primary_projection);
     w.run(stop, [&](const WatchEvent& ev) {
+      // marked before the store applies it: a worker may reconcile from the store at once
+      if (trace::armed() && ev.object && ev.type != WatchEvent::Type::Deleted) {
+        trace::mark(meta_name(*ev.object), "ctl.primary_event");
+      }
       primary_store_->apply(ev);
       primary_gauge.set(static_cast<double>(primary_store_->size()));
       if (ev.type == WatchEvent::Type::Restarted) {
@@ -612,6 +617,9 @@ void Controller::run(CancelToken& stop, Reconciler reconcile, ErrorPolicy error_
       w.set_metadata_only(c->metadata_only);
       w.set_projection(opts_.child_projection);
       w.run(stop, [&, c](const WatchEvent& ev) {
+        if (trace::armed() && ev.object && ev.type != WatchEvent::Type::Deleted) {
+          trace::mark(meta_name(*ev.object), "ctl." + c->rt.plural + "_event");
+        }
         c->store->apply(ev);
         c->gauge->set(static_cast<double>(c->store->size()));
         if (ev.type == WatchEvent::Type::Restarted) {
@@ -661,12 +669,15 @@ void Controller::run(CancelToken& stop, Reconciler reconcile, ErrorPolicy error_
           queue_.done(key);
           continue;
         }
+        const bool traced = trace::armed();
+        if (traced) trace::mark(meta_name(*obj), "ctl.reconcile0");
         Action a;
         try {
           a = reconcile(obj);
         } catch (const std::exception& e) {
           a = error_policy(obj, e);
         }
+        if (traced) trace::mark(meta_name(*obj), "ctl.reconcile1");
         queue_.finish(key, a.requeue, a.after);
         q_depth.set(static_cast<double>(queue_.pending()));
       }

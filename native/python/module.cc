@@ -16,7 +16,10 @@
 #include "core/yaml.h"
 #include "crd/schema.h"
 #include "core/log.h"
+#include "core/metrics.h"
 #include "core/process.h"
+#include "core/stall.h"
+#include "core/trace.h"
 #include "kube/client.h"
 
 namespace py = pybind11;
@@ -228,6 +231,15 @@ PYBIND11_MODULE(_native, m) {
     bgc::log::flush();
   });
   m.def("log_lines_dropped", [] { return bgc::log::lines_dropped(); });
+  // Per-tenant stage marks and the stall sampler of this process (the bench's load driver):
+  // the same surface the services serve on /debug/trace and /debug/stalls.
+  m.def("trace_arm", [](const std::string& prefix) { bgc::trace::arm(prefix); });
+  m.def("trace_take", [] { return bgc::trace::dump_json(true); });
+  m.def("stall_start", [](const std::string& name) {
+    bgc::metrics::set_debug_endpoints(true);  // the sampler keeps its stalls only then
+    bgc::stall::start(name);
+  });
+  m.def("stall_take", [] { return bgc::stall::dump_json(true); });
   // A KubeClient built from a $KUBECONFIG-style path list, one request per call (tests of
   // credential plugins and multi-file merging).  Returns (status, body, credential refreshes).
   m.def("kube_request", [](const std::string& kubeconfig_list, const std::string& method, const std::string& path,

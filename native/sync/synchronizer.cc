@@ -10,6 +10,7 @@
 #include "core/json_patch.h"
 #include "core/log.h"
 #include "core/metrics.h"
+#include "core/trace.h"
 #include "kube/ratelimit.h"
 
 namespace bgc::sync {
@@ -166,7 +167,9 @@ bool Synchronizer::sync_one(const Value& ub, std::vector<std::string>* produced)
       json::PatchBuilder ops;
       if (!has_quota) ops.add("/spec/quota", Value::object());
       ops.replace("/spec/quota", desired);
+      if (trace::armed()) trace::mark(name, "sync.quota.send");
       rv = client_.patch_json_rv(types::UserBootstrap, "", name, ops.ops(), kPatchManager);
+      if (trace::armed()) trace::mark(name, "sync.quota.done");
       if (produced) produced->push_back(rv);
       LOG_INFO("synchronizer") << "quota updated";
     }
@@ -177,7 +180,9 @@ bool Synchronizer::sync_one(const Value& ub, std::vector<std::string>* produced)
         body["status"] = Value::object({{"synchronized_with_sheet", true}});
         try {
           LOG_INFO("synchronizer") << "updating status";
+          if (trace::armed()) trace::mark(name, "sync.status.send");
           const std::string written_rv = client_.replace_status_rv(types::UserBootstrap, "", name, body);
+          if (trace::armed()) trace::mark(name, "sync.status.done");
           if (produced) produced->push_back(written_rv);
           break;
         } catch (const kube::ApiError& e) {
@@ -268,6 +273,10 @@ int Synchronizer::run(CancelToken& stop) {
       kube::Watcher w(client_, types::UserBootstrap);
       w.set_projection(&ub_watch_projection());
       w.run(stop, [&](const kube::WatchEvent& ev) {
+        // marked before the store applies it: a queued worker may read the store at once
+        if (trace::armed() && ev.object && ev.type != kube::WatchEvent::Type::Deleted) {
+          trace::mark(kube::meta_name(*ev.object), "sync.ub_event");
+        }
         store.apply(ev);
         if (ev.type == kube::WatchEvent::Type::Restarted) {
           for (const auto& o : ev.objects) queue.add(kube::meta_name(*o));
@@ -286,6 +295,7 @@ int Synchronizer::run(CancelToken& stop) {
         std::string key;
         while (queue.get(key)) {
           kube::ObjPtr ub = store.get(key);
+          if (trace::armed()) trace::mark(key, "sync.dequeue");
           if (ub) {
             const std::string ub_rv = kube::meta_rv(*ub);
             {

@@ -47,7 +47,12 @@ def test_bench_two_ranks_gloo():
     assert "tuned" not in d and "webhook_http1" not in d and "write_latency_2ms" not in d
     # the open-loop phase splits its offered rate over the ranks
     q = d["latency_at_rate"]["this"]["200"]
-    assert q["offered_rate"] == 200 and q["ready_crs"] == 200 and q["failed_crs"] == 0
+    # two 1 s windows per rate, each carrying the whole job's offered rate
+    assert q["offered_rate"] == 200 and q["ready_crs"] == 400 and q["failed_crs"] == 0
+    assert [w["ready_crs"] for w in q["windows"]] == [200, 200]
+    # both ranks' tenants are traced through every process and attributed
+    for att in d["latency_at_rate"]["attribution"]["this"]["200"]:
+        assert att["attributed"] == 200 and att["trace_dropped"] == 0
     assert "reference_controller" not in d["latency_at_rate"] and "product_isolated" not in d  # N>1: no isolation
 
 
@@ -92,14 +97,25 @@ def test_default_run_carries_the_reference_arms():
     # open loop at equal offered rates, both controllers
     q = d["latency_at_rate"]
     assert q["rates_cr_per_s"] == [100, 200] and q["arrivals"] == "poisson (open loop)"
+    assert q["windows_per_arm"] == 2 and q["order"].startswith("A B B A")
     for side in ("this", "reference_controller"):
         for rate in ("100", "200"):
             r = q[side][rate]
-            assert r["failed_crs"] == 0 and r["ready_crs"] == int(rate)
+            assert r["failed_crs"] == 0 and r["ready_crs"] == 2 * int(rate) and len(r["windows"]) == 2
             assert r["reconcile_p99_ms"] > 0 and r["admission_p50_ms"] > 0
             # (the exact 2 % check belongs to the box run; sanitizer builds here are slower)
             assert abs(r["achieved_rate"] - r["offered_rate"]) <= 0.2 * r["offered_rate"]
+            # every tenant of every window is attributed along its critical path
+            for att in q["attribution"][side][rate]:
+                assert att["attributed"] == int(rate), att
+                assert att["critical_child"] and att["segments"]
+                seg = att["segments"]
+                assert "arrival->sent" in seg and any(k.endswith("->seen") for k in seg)
     assert set(q["this_over_reference"]) == {"100", "200"}
+    for row in q["this_over_reference"].values():
+        assert len(row["reconcile_p99_lower_by_window"]) == 2
+    # the compact stage table is the line's last field (the driver keeps the output's tail)
+    assert list(d)[-1] == "stage_table" and set(d["stage_table"]["this"]) == {"100", "200"}
     # the headline again with fixtures and product on disjoint CPUs
     pi = d["product_isolated"]
     assert pi["failed_crs"] == 0 and pi["value"] > 0 and pi["reconcile_p99_ms"] > 0
