@@ -100,14 +100,18 @@ def critical_path(marks, why=None):
             why["not_seen_ready"] = why.get("not_seen_ready", 0) + 1
         return None
     child = max(seen, key=seen.get)
+    t_seen = seen[child]
     path = []
     i = 0
     for name, rx in _COMPILED[child]:
         j = i
-        while j < len(marks) and not rx.match(marks[j][1]):
+        while j < len(marks) and marks[j][0] <= t_seen and not rx.match(marks[j][1]):
             j += 1
-        if j == len(marks):
-            continue  # no such mark after the previous milestone: skipped
+        if j == len(marks) or marks[j][0] > t_seen:
+            # no such mark between the previous milestone and Ready: skipped (e.g. the
+            # RoleBinding was applied by a reconcile a child event queued, which read the
+            # status before the controller's own status event arrived)
+            continue
         path.append((name, marks[j][0]))
         i = j
     if not path or path[0][0] != "arrival" or path[-1][0] != "seen":

@@ -414,6 +414,8 @@ def _sample_logs(info):
             "admission": (info["admission"] + "/debug/samples/admission", info["ca"]),
             "h2_server": (info["admission"] + "/debug/samples/h2_server", info["ca"]),
             "telemetry_poll": (info["node_agent"] + "/debug/samples/telemetry_poll", None),
+            "telemetry_poll_cpu": (info["node_agent"] + "/debug/samples/telemetry_poll_cpu", None),
+            "telemetry_poll_runq": (info["node_agent"] + "/debug/samples/telemetry_poll_runq", None),
             "sync_ub": (info["synchronizer"] + "/debug/samples/sync_ub", None)}
 
 
@@ -542,6 +544,11 @@ def _phase(d, nat, info, args, phase, concurrency, warmup, steps, cluster):
         # quota; RoleBinding after the status write)
         "stage_p50_ms": {k: ms(_pct([x for p in per_rank for x in p["stage"][k]], 0.50)) for k in ("ns", "rq", "rb")},
         "telemetry_poll_p50_ms": ms(_pct(tel, 0.50)),
+        # the poll's wall time split (core/schedstat.h): on a CPU, waiting for one, and the
+        # rest blocked in amdsmi's ioctls
+        "telemetry_poll_split_p50_ms": {"cpu": ms(_pct(win["telemetry_poll_cpu"], 0.50)),
+                                        "runq": ms(_pct(win["telemetry_poll_runq"], 0.50)),
+                                        "runq_p99": ms(_pct(win["telemetry_poll_runq"], 0.99))},
         "sync_one_p50_ms": ms(_pct(syn, 0.50)),
         # CPU time each process spent in the timed region, per Ready CR.  kube_lite is the
         # test API server and load_driver the tenant simulator: neither ships.

@@ -51,12 +51,10 @@ def free_port():
 # services' many short-lived JSON allocations off the shared arenas.  Measured on the
 # MI355X box: +14% CR/s, -12% control-plane CPU per CR (profiles/archive/malloc_tunables_r1/);
 # 64 per class keeps that at half the cached memory of 1024 (profiles/archive/tcache_ab_r1/).
-# The container image sets the same value (Dockerfile ENV).
-# trim_threshold / top_pad / mmap_threshold: no sbrk shrink-and-grow churn in the main
-# arena under bursts (profiles/malloc_trim_r3/: product CPU -3.5 %, reconcile p99 -12 %)
-SERVICE_GLIBC_TUNABLES = ("glibc.malloc.tcache_count=64:glibc.malloc.tcache_max=16384:"
-                          "glibc.malloc.trim_threshold=268435456:glibc.malloc.top_pad=67108864:"
-                          "glibc.malloc.mmap_threshold=4194304")
+# The container image sets the same value (Dockerfile ENV).  Only the thread cache is set
+# here (mallopt has no knob for it): arenas, heap growth and trimming are set in one place,
+# bgc::tune_malloc (native/core/process.cc).
+SERVICE_GLIBC_TUNABLES = "glibc.malloc.tcache_count=64:glibc.malloc.tcache_max=16384"
 
 
 class Proc:
@@ -338,7 +336,11 @@ current-context: {name}@kube-lite
         os.replace(tmp, path)
 
     def start_process(self, name, exe, env):
-        self.procs[name] = Proc(name, [binary(exe)], env, self.workdir)
+        # BGC_WRAP_<EXE>="tool args --" (e.g. BGC_WRAP_NODE_AGENT="rocprofv3 --marker-trace -d
+        # out --"): profile one component of a running stack; the program stays right after
+        # "--", as rocprofv3 requires
+        wrap = os.environ.get("BGC_WRAP_" + exe.upper().replace("-", "_"), "").split()
+        self.procs[name] = Proc(name, wrap + [binary(exe)], env, self.workdir)
         return self.procs[name]
 
     # ------------------------------------------------------------------ access

@@ -36,6 +36,12 @@ int main(int argc, char** argv) {
   // A test server: no malloc_trim passes (one stalls kube-lite for 110-130 ms on the bench's
   // heap, which would show up in the measured latencies).  BGC_MALLOC_TRIM_SECS still wins.
   setenv("BGC_MALLOC_TRIM_SECS", "0", /*overwrite=*/0);
+  // Nor the services' bounded-footprint allocator settings (core/process.cc tune_malloc): a
+  // test fixture is tuned for throughput, the bench's CR/s being mostly kube-lite's CPU —
+  // glibc's arena count, 64 MiB heap growth, no trimming below 512 MiB.
+  setenv("BGC_MALLOC_ARENA_MAX", "0", 0);
+  setenv("BGC_MALLOC_TOP_PAD_KB", "65536", 0);
+  setenv("BGC_MALLOC_TRIM_THRESHOLD_KB", "524288", 0);
   process_init();
   apiserver::Options o;
   std::string port_file;

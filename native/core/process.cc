@@ -21,11 +21,37 @@
 
 namespace bgc {
 
+static long env_long(const char* name, long dflt) {
+  const char* v = std::getenv(name);
+  return v && *v ? std::atol(v) : dflt;
+}
+
+// The one source of truth for the services' allocator settings.  The container image and
+// the test cluster set only the thread-cache tunables through GLIBC_TUNABLES (mallopt has
+// no tcache knob); everything below is set here, and an image env var can no longer
+// disagree with it (round 5: the image's trim_threshold was dead, this overrode it).
+//
+//  * M_ARENA_MAX (BGC_MALLOC_ARENA_MAX, default 4): glibc's default is 8 arenas per CPU —
+//    2,048 on the MI355X hosts' 256 visible CPUs — and a thread-per-connection server gives
+//    nearly every connection thread an arena of its own, each keeping its own free memory:
+//    round 5 measured the admission server at 17 MB live in 195 MB RSS with 11 GB of free
+//    arena space.  The thread cache (64 chunks per size class up to 16 KiB) serves the
+//    hot-path allocations without touching an arena, so 4 arenas are rarely contended.
+//  * M_TOP_PAD 4 MiB (BGC_MALLOC_TOP_PAD_KB) and M_TRIM_THRESHOLD 16 MiB
+//    (BGC_MALLOC_TRIM_THRESHOLD_KB): a heap grows 4 MiB at a time and hands back a free top
+//    above 16 MiB, so bursts do not cycle sbrk per request (the cost the old 64 MiB pad and
+//    512 MiB threshold were there to avoid) and a quiet service returns to its live size.
+//  * M_MMAP_THRESHOLD 4 MiB fixed: glibc's dynamic threshold would otherwise climb after
+//    the first large free and keep multi-MiB list bodies in the arenas.
+// BGC_MALLOC_TUNE=0 leaves glibc's defaults; 0 for one knob leaves that one at glibc's.
 void tune_malloc() {
   const char* e = std::getenv("BGC_MALLOC_TUNE");
   if (e && std::strcmp(e, "0") == 0) return;
-  mallopt(M_TRIM_THRESHOLD, 512 << 20);
-  mallopt(M_TOP_PAD, 64 << 20);
+  if (const long a = env_long("BGC_MALLOC_ARENA_MAX", 4); a > 0) mallopt(M_ARENA_MAX, static_cast<int>(a));
+  if (const long k = env_long("BGC_MALLOC_TOP_PAD_KB", 4 << 10); k > 0) mallopt(M_TOP_PAD, static_cast<int>(k << 10));
+  if (const long k = env_long("BGC_MALLOC_TRIM_THRESHOLD_KB", 16 << 10); k > 0) {
+    mallopt(M_TRIM_THRESHOLD, static_cast<int>(k << 10));
+  }
   mallopt(M_MMAP_THRESHOLD, 4 << 20);
 }
 

@@ -13,8 +13,8 @@ void process_init();
 void init_openssl();
 
 // glibc malloc tuning for many short-lived JSON allocations across thread-per-connection
-// servers: no heap trimming (the sbrk grow/trim cycle cost ~10% of kube-lite CPU), heap
-// growth in 64 MiB steps and a fixed 4 MiB mmap threshold. BGC_MALLOC_TUNE=0 disables it.
+// servers (process.cc): at most 4 arenas, heaps grown 4 MiB at a time and trimmed above
+// 16 MiB free, a fixed 4 MiB mmap threshold.  BGC_MALLOC_TUNE=0 disables it.
 void tune_malloc();
 // The periodic trimmer's rule (process.cc): Skip while the RSS is under the minimum or under
 // 1.5x the RSS the previous pass left; Defer while the process used more than idle_pct % of

@@ -1,10 +1,8 @@
 #include "core/stall.h"
 
-#include <fcntl.h>
 #include <pthread.h>
 #include <signal.h>
 #include <time.h>
-#include <unistd.h>
 
 #include <atomic>
 #include <cstdio>
@@ -16,6 +14,7 @@
 
 #include "core/json.h"
 #include "core/metrics.h"
+#include "core/schedstat.h"
 
 namespace bgc::stall {
 
@@ -42,18 +41,6 @@ std::string g_process;
 std::vector<Stall> g_kept;
 uint64_t g_dropped = 0;
 
-// Run-queue delay of the sampler thread so far (schedstat field 2), -1 if unavailable.  The
-// file stays open: one pread per tick.
-int64_t runq_delay_ns(int fd) {
-  if (fd < 0) return -1;
-  char buf[128];
-  const ssize_t n = ::pread(fd, buf, sizeof buf - 1, 0);
-  if (n <= 0) return -1;
-  buf[n] = '\0';
-  unsigned long long run = 0, wait = 0;
-  return std::sscanf(buf, "%llu %llu", &run, &wait) == 2 ? static_cast<int64_t>(wait) : -1;
-}
-
 std::vector<double> stall_buckets() {
   return {50e-6, 100e-6, 200e-6, 500e-6, 1e-3, 2e-3, 5e-3, 10e-3, 20e-3, 50e-3, 100e-3, 500e-3, 1.0};
 }
@@ -71,9 +58,8 @@ void loop() {
   const char* rec = std::getenv("BGC_STALL_RECORD_US");
   const int64_t record_ns = (rec ? std::atoll(rec) : 2000) * 1000;
   const bool keep = metrics::debug_endpoints_enabled();
-  const int fd = keep ? ::open("/proc/thread-self/schedstat", O_RDONLY | O_CLOEXEC) : -1;
   struct timespec req {0, kTickNs};
-  int64_t runq0 = runq_delay_ns(fd);
+  int64_t runq0 = keep ? sched::thread_sched().runq_ns : -1;
   while (true) {
     const int64_t t0 = metrics::now_ns();
     nanosleep(&req, nullptr);
@@ -87,7 +73,7 @@ void loop() {
     malloc_h.observe(static_cast<double>(mal) * 1e-9);
     g_ticks.fetch_add(1, std::memory_order_relaxed);
     if (!keep) continue;
-    const int64_t runq1 = runq_delay_ns(fd);
+    const int64_t runq1 = sched::thread_sched().runq_ns;
     const int64_t runq = runq0 >= 0 && runq1 >= 0 ? runq1 - runq0 : -1;
     runq0 = runq1;
     if (over >= record_ns || mal >= record_ns) {

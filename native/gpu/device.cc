@@ -16,6 +16,7 @@
 
 #include "core/log.h"
 #include "core/metrics.h"
+#include "core/roctx.h"
 #include "core/net.h"
 
 namespace bgc::gpu {
@@ -818,14 +819,22 @@ class AmdSmiBackend : public Backend {
     // (safe: libamd_smi/rocm_smi lock per device), while the diagnostics thread's
     // busy_processes() may hit the same handle — serialized here instead of letting the
     // library's device mutex answer AMDSMI_STATUS_BUSY.
-    std::lock_guard<std::mutex> hl(*handle_mu_[static_cast<size_t>(index)]);
+    std::unique_lock<std::mutex> hl(*handle_mu_[static_cast<size_t>(index)], std::defer_lock);
+    {
+      roctx::Range r("bgc.amdsmi.handle_lock");  // waiting for the diagnostics thread's call, if any
+      hl.lock();
+    }
     if (!api_.get_metrics) {
       t.error = "amdsmi_get_gpu_metrics_info unavailable";
       return t;
     }
     amdsmi_gpu_metrics_t m;
     std::memset(&m, 0, sizeof(m));
-    amdsmi_status_t st = api_.get_metrics(h, &m);
+    amdsmi_status_t st;
+    {
+      roctx::Range r("bgc.amdsmi.gpu_metrics_info");
+      st = api_.get_metrics(h, &m);
+    }
     if (st != AMDSMI_STATUS_SUCCESS) {
       t.error = "amdsmi_get_gpu_metrics_info status " + std::to_string(st);
       t.poll_us = static_cast<double>(metrics::now_ns() - t0) / 1e3;
@@ -878,6 +887,7 @@ class AmdSmiBackend : public Backend {
     }
     if (full && api_.get_vram_usage) {
       amdsmi_vram_usage_t u{};
+      roctx::Range r("bgc.amdsmi.vram_usage");
       if (api_.get_vram_usage(h, &u) == AMDSMI_STATUS_SUCCESS) {
         t.vram_used_mb = u.vram_used;
         t.vram_total_mb = u.vram_total;
@@ -885,6 +895,7 @@ class AmdSmiBackend : public Backend {
     }
     if (full && api_.get_ecc) {
       amdsmi_error_count_t e{};
+      roctx::Range r("bgc.amdsmi.total_ecc_count");
       if (api_.get_ecc(h, &e) == AMDSMI_STATUS_SUCCESS) {
         t.ecc_correctable = e.correctable_count;
         t.ecc_uncorrectable = e.uncorrectable_count;
@@ -894,6 +905,7 @@ class AmdSmiBackend : public Backend {
     if (full && api_.pcie_info) {
       amdsmi_pcie_info_t pi;
       std::memset(&pi, 0, sizeof(pi));
+      roctx::Range r("bgc.amdsmi.pcie_info");
       if (api_.pcie_info(h, &pi) == AMDSMI_STATUS_SUCCESS) {
         const auto& pm = pi.pcie_metric;
         auto cnt = [](uint64_t v) { return v == ~0ULL ? int64_t{-1} : static_cast<int64_t>(v); };
@@ -914,6 +926,7 @@ class AmdSmiBackend : public Backend {
   void sample_ras(amdsmi_processor_handle h, Telemetry& t) {
     t.ras_ok = true;
     if (api_.bad_pages) {
+      roctx::Range r("bgc.amdsmi.bad_page_info");
       uint32_t n = 0;
       if (api_.bad_pages(h, &n, nullptr) == AMDSMI_STATUS_SUCCESS && n > 0) {
         std::vector<amdsmi_retired_page_record_t> recs(n);
@@ -926,6 +939,7 @@ class AmdSmiBackend : public Backend {
       }
     }
     if (api_.ecc_count) {
+      roctx::Range r("bgc.amdsmi.ecc_count_per_block");
       uint64_t enabled = ~0ULL;
       if (api_.ecc_enabled && api_.ecc_enabled(h, &enabled) != AMDSMI_STATUS_SUCCESS) enabled = ~0ULL;
       for (const auto& b : kEccBlocks) {
@@ -935,6 +949,7 @@ class AmdSmiBackend : public Backend {
         t.ecc_blocks.push_back({b.name, e.correctable_count, e.uncorrectable_count, e.deferred_count});
       }
     }
+    roctx::Range r("bgc.amdsmi.link_metrics");
     t.links = read_links(h);
   }
 

@@ -6,6 +6,7 @@
 #include "core/log.h"
 #include "core/metrics.h"
 #include "core/roctx.h"
+#include "core/schedstat.h"
 
 namespace bgc::gpu {
 
@@ -160,14 +161,40 @@ void TelemetryPoller::poll_once() {
                      : level == SampleLevel::Slow ? "bgc.telemetry.poll.slow"
                                                   : "bgc.telemetry.poll.fast");
   std::vector<Telemetry> samples(indices_.size());
+  // The poll's wall time split into on-CPU, run-queue wait and blocked (amdsmi's ioctls
+  // waiting on the SMU): on a saturated CPU share the first two grow, on a busy SMU the
+  // third.  With a pool, each device's task is measured on its own thread and the slowest
+  // device's split is added to the polling thread's.
+  const sched::ThreadSched s0 = sched::thread_sched();
+  int64_t dev_cpu = 0, dev_runq = 0;
   if (pool_) {
-    std::vector<std::future<void>> futs;
+    std::vector<std::future<std::pair<int64_t, int64_t>>> futs;
     for (size_t k = 0; k < indices_.size(); ++k) {
-      futs.push_back(pool_->submit([&, k] { samples[k] = backend_.sample(indices_[k], level); }));
+      futs.push_back(pool_->submit([&, k] {
+        const sched::ThreadSched a = sched::thread_sched();
+        samples[k] = backend_.sample(indices_[k], level);
+        const sched::ThreadSched b = sched::thread_sched();
+        return a.ok() && b.ok() ? std::make_pair(b.cpu_ns - a.cpu_ns, b.runq_ns - a.runq_ns) : std::make_pair(int64_t{0}, int64_t{0});
+      }));
     }
-    for (auto& f : futs) f.get();
+    for (auto& f : futs) {
+      const auto [c, q] = f.get();
+      dev_cpu = std::max(dev_cpu, c);
+      dev_runq = std::max(dev_runq, q);
+    }
   } else {
     for (size_t k = 0; k < indices_.size(); ++k) samples[k] = backend_.sample(indices_[k], level);
+  }
+  const sched::ThreadSched s1 = sched::thread_sched();
+  if (s0.ok() && s1.ok()) {
+    static auto& cpu_ring = reg.samples("telemetry_poll_cpu");
+    static auto& runq_ring = reg.samples("telemetry_poll_runq");
+    static auto& runq_hist = reg.histogram("bgc_telemetry_poll_runq_seconds",
+                                           "Run-queue wait (runnable, no CPU) inside one telemetry poll");
+    const double runq = static_cast<double>(s1.runq_ns - s0.runq_ns + dev_runq) * 1e-9;
+    cpu_ring.add(static_cast<double>(s1.cpu_ns - s0.cpu_ns + dev_cpu) * 1e-9);
+    runq_ring.add(runq);
+    runq_hist.observe(runq);
   }
   for (size_t k = 0; k < indices_.size(); ++k) {
     Telemetry t = std::move(samples[k]);
