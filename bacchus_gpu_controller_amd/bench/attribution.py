@@ -142,7 +142,7 @@ def _stall_owner(stalls, t0, t1):
     return owners
 
 
-def analyze(dumps, stall_dumps=(), tail_ms=5.0):
+def analyze(dumps, stall_dumps=(), tail_ms=5.0, detail=None):
     """Segment table of one window.
 
     Returns {"tenants": n, "attributed": n, "critical_child": {child: n},
@@ -203,6 +203,19 @@ def analyze(dumps, stall_dumps=(), tail_ms=5.0):
                              "stalls_ms": {p: round(v / 1e3, 2) for p, v in owners.items()}})
     out["tail"] = {"threshold_ms": round(thr, 3), "n": len(tail), "blame": blame, "blame_ms": blame_ms,
                    "stall_overlap": overlap, "examples": examples}
+    if detail is not None and tail:
+        # for offline study (--trace-dump): the worst tail tenants' full timelines, and every
+        # mark of every tenant within 10 ms around the worst one's longest segment
+        worst = sorted(tail, key=lambda x: -x[1])[:20]
+        detail["tail_timelines"] = {}
+        for name, tot, segs in worst:
+            m = marks[name]
+            detail["tail_timelines"][name] = {"total_ms": round(tot, 3), "t0_ns": m[0][0],
+                                              "marks_us": [[round((t - m[0][0]) / 1e3, 1), st] for t, st in m]}
+        key, ta, tb = max(worst[0][2], key=lambda s: s[2] - s[1])
+        lo, hi = ta - 10_000_000, tb + 10_000_000
+        detail["context"] = {"segment": key, "from_ns": ta, "to_ns": tb,
+                             "marks": sorted([t, n, st] for n, m in marks.items() for t, st in m if lo <= t <= hi)}
     out["stalls"] = {p: {"n": len(r), "max_ms": round(max((x[1] + x[3] for x in r), default=0.0) / 1e3, 3),
                          "sum_ms": round(sum(x[1] + x[3] for x in r) / 1e3, 3)} for p, r in stalls.items()}
     return out

@@ -708,7 +708,13 @@ def _rate_phase(d, nat, info, args, key, rate, cluster):
         # CPU-ms the job's threads waited in run queues per second of window
         out["runqueue_wait_ms_per_s"] = round((rq1 - rq0) / max(args.latency_window_s, 1e-9), 1)
     if traced:
-        out["attribution"] = attribution.analyze(traces, stalls, tail_ms=args.tail_ms)
+        detail = {} if args.trace_dump else None
+        out["attribution"] = attribution.analyze(traces, stalls, tail_ms=args.tail_ms, detail=detail)
+        if detail:
+            os.makedirs(args.trace_dump, exist_ok=True)
+            detail["stalls"] = stalls
+            with open(os.path.join(args.trace_dump, f"{key}.json"), "w") as f:
+                json.dump(detail, f)
         out["attribution"]["trace_marks"] = sum(len((t or {}).get("marks", [])) for t in traces)
         out["attribution"]["trace_dropped"] = sum((t or {}).get("dropped", 0) for t in traces)
     errs = [e for p in per for e in p["errors"]]
@@ -1338,6 +1344,9 @@ def main(argv=None):
     ap.add_argument("--trace-windows", action=argparse.BooleanOptionalAction, default=True,
                     help="trace every tenant of each open-loop window through every process and attribute its "
                          "apply->Ready time to stages (latency_at_rate.attribution; bench/attribution.py)")
+    ap.add_argument("--trace-dump", default="",
+                    help="directory: per open-loop window, the worst tail tenants' full timelines and every mark "
+                         "around the worst one (bench/attribution.py analyze(detail=...))")
     ap.add_argument("--tail-ms", type=float, default=5.0,
                     help="attribution: tenants above max(p99, this) apply->Ready are the window's tail")
     ap.add_argument("--latency-workers", type=int, default=128,
