@@ -15,6 +15,7 @@
 #include <cerrno>
 #include <csignal>
 #include <pthread.h>
+#include <sys/eventfd.h>
 #include <unistd.h>
 
 namespace bgc::log {
@@ -37,21 +38,24 @@ std::atomic<int> g_min_level{static_cast<int>(Level::Info)};
 std::atomic<bool> g_initialized{false};
 std::atomic<void (*)(const std::string&)> g_sink{nullptr};
 
-// Asynchronous stderr writer: log lines are appended to a buffer and one thread writes
-// them in batches (one write(2) per batch instead of one per line through stdio's stderr
-// lock).  No logging thread ever waits for stderr: a stderr that blocks — a container
-// runtime's pipe that is read slowly, a log file under dirty-page writeback throttling —
-// must not stall the threads that log (the admission server logs each review at INFO and
-// each deny at ERROR, the controller each reconcile).
+// Asynchronous stderr writer: log lines are queued and one thread writes them in batches
+// (one write(2) per batch instead of one per line through stdio's stderr lock).  No
+// logging thread ever waits — neither for stderr nor for another logging thread:
 //
-//  * append() only touches the buffer under mu_.  An ERROR line wakes the writer at once
-//    (no coalescing delay) instead of writing synchronously.
-//  * Past kMaxBuffered bytes lines are dropped and counted (lines_dropped(), exported as
-//    bgc_log_lines_dropped_total); the next batch written after stderr drains ends with one
-//    "N log lines dropped" line at the place the gap occurred.
-//  * Batches are taken and written under io_mu_, which is always taken BEFORE mu_ and never
-//    while mu_ is held, so batches reach stderr in the order their lines were appended.
-//  * flush() (exit, shutdown, tests) writes everything buffered; it is the one caller that
+//  * append() pushes the line onto a lock-free stack (one compare-and-swap).  A stderr that
+//    blocks (a container runtime's pipe read slowly, a log file under writeback throttling)
+//    stalls only the writer thread.  Round 6 also removed the buffer mutex every logging
+//    thread used to take: on the bench's 16-CPU share a thread preempted while holding it
+//    stopped every thread that logs (the admission server logs each review at INFO) for a
+//    scheduler time slice.
+//  * An ERROR line wakes the writer at once (no coalescing delay) instead of writing
+//    synchronously.
+//  * Past kMaxBuffered queued bytes lines are dropped and counted (lines_dropped(), exported
+//    as bgc_log_lines_dropped_total); the next batch written ends with one "N log lines
+//    dropped" line at the place the gap occurred.
+//  * Batches are taken and written under io_mu_ (writer thread and flush() only), so they
+//    reach stderr in the order the lines were queued.
+//  * flush() (exit, shutdown, tests) writes everything queued; it is the one caller that
 //    may wait for stderr.  BGC_LOG_SYNC=1 flushes after every line (debugging only).
 class AsyncWriter {
  public:
@@ -60,85 +64,114 @@ class AsyncWriter {
     return *w;
   }
   void append(const std::string& line, bool urgent) {
-    std::lock_guard<std::mutex> lk(mu_);
-    if (buf_.size() + line.size() > kMaxBuffered && !buf_.empty()) {
-      ++dropped_pending_;
+    const size_t queued = queued_bytes_.load(std::memory_order_relaxed);
+    if (queued > 0 && queued + line.size() > kMaxBuffered) {
+      dropped_pending_.fetch_add(1, std::memory_order_relaxed);
       dropped_total_.fetch_add(1, std::memory_order_relaxed);
       return;
     }
-    buf_ += line;
-    if (!thread_started_) start_locked();
-    if (urgent) urgent_ = true;
-    if (!wake_pending_ || urgent) {
-      wake_pending_ = true;
-      cv_.notify_one();
+    queued_bytes_.fetch_add(line.size(), std::memory_order_relaxed);
+    Node* n = new Node{nullptr, line};
+    n->next = head_.load(std::memory_order_relaxed);
+    // seq_cst: ordered before the sleeping_ exchange below, against the writer's store of
+    // sleeping_ and its re-check of head_ (no lost wake-up)
+    while (!head_.compare_exchange_weak(n->next, n, std::memory_order_seq_cst, std::memory_order_relaxed)) {
+    }
+    if (urgent) urgent_.store(true, std::memory_order_relaxed);
+    if (!started_.load(std::memory_order_acquire)) start();
+    // wake the writer only if it sleeps: no syscall per line while it is busy
+    if (sleeping_.exchange(false, std::memory_order_seq_cst)) {
+      const uint64_t one = 1;
+      ssize_t r = ::write(wake_fd_, &one, sizeof one);
+      (void)r;
     }
   }
-  // Writes everything appended before the call.  Waits for stderr; never holds mu_ while
-  // it does.
+  // Writes everything queued before the call.  Waits for stderr.
   void flush() { write_batch(); }
   uint64_t dropped() const { return dropped_total_.load(std::memory_order_relaxed); }
 
  private:
+  struct Node {
+    Node* next;
+    std::string line;
+  };
   static constexpr size_t kMaxBuffered = 1 << 20;
-  AsyncWriter() { std::atexit([] { AsyncWriter::instance().flush(); }); }
-  void start_locked() {
-    thread_started_ = true;
+  AsyncWriter() {
+    wake_fd_ = ::eventfd(0, EFD_CLOEXEC);
+    std::atexit([] { AsyncWriter::instance().flush(); });
+  }
+  void start() {
+    std::lock_guard<std::mutex> lk(start_mu_);
+    if (started_.load()) return;
     std::thread([this] {
       // the writer must not take signals meant for the services' shutdown handling
       sigset_t all;
       sigfillset(&all);
       pthread_sigmask(SIG_BLOCK, &all, nullptr);
       while (true) {
-        {
-          std::unique_lock<std::mutex> lk(mu_);
-          cv_.wait(lk, [&] { return wake_pending_; });
-          if (!urgent_) {
-            // let a burst of lines from other threads accumulate into one write; an ERROR
-            // line cuts the wait short
-            cv_.wait_for(lk, std::chrono::microseconds(500), [&] { return urgent_; });
-          }
-          wake_pending_ = false;
-          urgent_ = false;
+        sleeping_.store(true, std::memory_order_seq_cst);
+        if (head_.load(std::memory_order_seq_cst) == nullptr) {
+          uint64_t v;
+          ssize_t r = ::read(wake_fd_, &v, sizeof v);  // an append that finds sleeping_ set writes it
+          (void)r;
+        }
+        sleeping_.store(false, std::memory_order_relaxed);
+        // let a burst of lines from other threads accumulate into one write; an ERROR line
+        // is written at once
+        if (!urgent_.exchange(false, std::memory_order_relaxed)) {
+          std::this_thread::sleep_for(std::chrono::microseconds(500));
         }
         write_batch();
       }
     }).detach();
+    started_.store(true, std::memory_order_release);
   }
-  // Takes the current batch under io_mu_ (then briefly mu_) and writes it with only io_mu_
-  // held.
+  // Takes everything queued (in queue order) and writes it with only io_mu_ held.
   void write_batch() {
     std::lock_guard<std::mutex> io(io_mu_);
+    Node* n = head_.exchange(nullptr, std::memory_order_acquire);
+    if (!n) return;
+    Node* rev = nullptr;  // the stack holds the newest line first
+    while (n) {
+      Node* next = n->next;
+      n->next = rev;
+      rev = n;
+      n = next;
+    }
     std::string out;
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      if (buf_.empty()) return;
-      out.swap(buf_);
-      if (buf_.capacity() == 0) buf_.reserve(std::min(out.capacity(), kMaxBuffered));
-      if (dropped_pending_ > 0) {
-        out += "log: " + std::to_string(dropped_pending_) + " log lines dropped (stderr blocked)\n";
-        dropped_pending_ = 0;
-      }
+    size_t bytes = 0;
+    for (Node* p = rev; p; p = p->next) bytes += p->line.size();
+    out.reserve(bytes + 64);
+    while (rev) {
+      Node* next = rev->next;
+      out += rev->line;
+      delete rev;
+      rev = next;
+    }
+    queued_bytes_.fetch_sub(bytes, std::memory_order_relaxed);
+    if (const uint64_t d = dropped_pending_.exchange(0, std::memory_order_relaxed)) {
+      out += "log: " + std::to_string(d) + " log lines dropped (stderr blocked)\n";
     }
     size_t off = 0;
     while (off < out.size()) {
-      ssize_t n = ::write(2, out.data() + off, out.size() - off);
-      if (n <= 0) {
-        if (n < 0 && errno == EINTR) continue;
+      ssize_t w = ::write(2, out.data() + off, out.size() - off);
+      if (w <= 0) {
+        if (w < 0 && errno == EINTR) continue;
         break;
       }
-      off += static_cast<size_t>(n);
+      off += static_cast<size_t>(w);
     }
   }
-  std::mutex io_mu_;  // one batch taken and written at a time; taken before mu_, never under it
-  std::mutex mu_;     // buf_, the drop count and the writer's wake-up state
-  std::condition_variable cv_;
-  std::string buf_;
-  uint64_t dropped_pending_ = 0;  // dropped since the last batch (mu_)
+  std::atomic<Node*> head_{nullptr};
+  std::atomic<size_t> queued_bytes_{0};
+  std::atomic<uint64_t> dropped_pending_{0};  // dropped since the last batch
   std::atomic<uint64_t> dropped_total_{0};
-  bool wake_pending_ = false;
-  bool urgent_ = false;
-  bool thread_started_ = false;
+  std::atomic<bool> urgent_{false};
+  std::atomic<bool> sleeping_{false};
+  std::atomic<bool> started_{false};
+  std::mutex start_mu_;
+  std::mutex io_mu_;  // one batch taken and written at a time (writer thread, flush())
+  int wake_fd_ = -1;
 };
 
 bool g_sync_writes = std::getenv("BGC_LOG_SYNC") && std::string(std::getenv("BGC_LOG_SYNC")) == "1";

@@ -1,6 +1,7 @@
 #include "core/trace.h"
 
 #include <atomic>
+#include <memory>
 #include <mutex>
 #include <vector>
 
@@ -17,30 +18,59 @@ struct Mark {
   int64_t t;
 };
 
-std::atomic<bool> g_armed{false};
-std::mutex g_mu;  // everything below
-std::string g_prefix;                // as armed (comma list)
-std::vector<std::string> g_prefixes;  // its items
-size_t g_capacity = 0;
-uint64_t g_dropped = 0;
-std::vector<Mark> g_marks;
+// What arm() set: immutable once published (mark() reads it through an atomic pointer
+// without a lock; replaced configurations are kept, arm() runs a few times per bench run).
+struct Config {
+  std::string prefix;                 // as armed (comma list)
+  std::vector<std::string> prefixes;  // its items
+  size_t capacity = 0;
+};
+
+// Marks are kept per thread: a mark takes only its own thread's buffer lock, which nothing
+// else takes except a dump.  One process-wide lock here was itself a source of the tails
+// being measured: a thread preempted while holding it (16 CPUs, hundreds of threads) stopped
+// every thread that marks — kube-lite's committers hold a store lock when they mark — for a
+// scheduler time slice.
+struct ThreadBuf {
+  std::mutex mu;
+  std::vector<Mark> marks;
+};
+
+std::atomic<const Config*> g_config{nullptr};  // null: disarmed
+std::atomic<size_t> g_count{0};                // marks kept since arm()
+std::atomic<uint64_t> g_dropped{0};
+std::mutex g_reg_mu;  // g_bufs and g_retired
+std::vector<std::shared_ptr<ThreadBuf>> g_bufs;
+std::vector<std::unique_ptr<const Config>> g_retired;
+std::string g_last_prefix;  // g_reg_mu
+
+ThreadBuf& thread_buf() {
+  thread_local std::shared_ptr<ThreadBuf> buf = [] {
+    auto b = std::make_shared<ThreadBuf>();
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    g_bufs.push_back(b);
+    return b;
+  }();
+  return *buf;
+}
 
 }  // namespace
 
-bool armed() { return g_armed.load(std::memory_order_relaxed); }
+bool armed() { return g_config.load(std::memory_order_acquire) != nullptr; }
 
 void mark_at(std::string_view name, std::string_view stage, int64_t t_ns) {
-  if (!armed()) return;
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (!g_armed.load(std::memory_order_relaxed)) return;
+  const Config* c = g_config.load(std::memory_order_acquire);
+  if (!c) return;
   bool match = false;
-  for (const auto& p : g_prefixes) match = match || name.substr(0, p.size()) == p;
+  for (const auto& p : c->prefixes) match = match || name.substr(0, p.size()) == p;
   if (!match) return;
-  if (g_marks.size() >= g_capacity) {
-    ++g_dropped;
+  if (g_count.fetch_add(1, std::memory_order_relaxed) >= c->capacity) {
+    g_dropped.fetch_add(1, std::memory_order_relaxed);
     return;
   }
-  g_marks.push_back({std::string(name), std::string(stage), t_ns});
+  ThreadBuf& b = thread_buf();
+  std::lock_guard<std::mutex> lk(b.mu);
+  b.marks.push_back({std::string(name), std::string(stage), t_ns});
 }
 
 void mark(std::string_view name, std::string_view stage) {
@@ -49,43 +79,62 @@ void mark(std::string_view name, std::string_view stage) {
 }
 
 void arm(const std::string& prefix, size_t capacity) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  g_prefix = prefix;
-  g_prefixes.clear();
+  auto c = std::make_unique<Config>();
+  c->prefix = prefix;
   size_t start = 0;
   while (start <= prefix.size()) {
     const size_t comma = prefix.find(',', start);
     std::string item = prefix.substr(start, comma == std::string::npos ? std::string::npos : comma - start);
-    if (!item.empty()) g_prefixes.push_back(std::move(item));
+    if (!item.empty()) c->prefixes.push_back(std::move(item));
     if (comma == std::string::npos) break;
     start = comma + 1;
   }
-  g_capacity = capacity;
-  g_dropped = 0;
-  g_marks.clear();
-  g_marks.reserve(std::min<size_t>(capacity, 1 << 16));
-  g_armed.store(!g_prefixes.empty(), std::memory_order_relaxed);
+  c->capacity = capacity;
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  g_config.store(nullptr, std::memory_order_release);
+  for (auto& b : g_bufs) {
+    std::lock_guard<std::mutex> bl(b->mu);
+    b->marks.clear();
+  }
+  g_count.store(0);
+  g_dropped.store(0);
+  g_last_prefix = prefix;
+  if (!c->prefixes.empty()) {
+    g_config.store(c.get(), std::memory_order_release);
+    g_retired.push_back(std::move(c));
+  }
 }
 
-void disarm() {
-  std::lock_guard<std::mutex> lk(g_mu);
-  g_armed.store(false, std::memory_order_relaxed);
-}
+void disarm() { g_config.store(nullptr, std::memory_order_release); }
 
 std::string dump_json(bool take) {
   std::vector<Mark> marks;
   json::Value out = json::Value::object();
   {
-    std::lock_guard<std::mutex> lk(g_mu);
-    out["prefix"] = g_prefix;
-    out["armed"] = g_armed.load(std::memory_order_relaxed);
-    out["dropped"] = static_cast<unsigned long long>(g_dropped);
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    out["prefix"] = g_last_prefix;
+    out["armed"] = armed();
+    if (take) g_config.store(nullptr, std::memory_order_release);
+    out["dropped"] = static_cast<unsigned long long>(g_dropped.load());
+    for (auto& b : g_bufs) {
+      std::lock_guard<std::mutex> bl(b->mu);
+      if (take) {
+        for (auto& m : b->marks) marks.push_back(std::move(m));
+        b->marks.clear();
+        b->marks.shrink_to_fit();
+      } else {
+        marks.insert(marks.end(), b->marks.begin(), b->marks.end());
+      }
+    }
     if (take) {
-      marks.swap(g_marks);
-      g_armed.store(false, std::memory_order_relaxed);
-      g_dropped = 0;
-    } else {
-      marks = g_marks;
+      // buffers of threads that have exited (only this list still holds them)
+      std::vector<std::shared_ptr<ThreadBuf>> live;
+      for (auto& b : g_bufs) {
+        if (b.use_count() > 1) live.push_back(std::move(b));
+      }
+      g_bufs.swap(live);
+      g_dropped.store(0);
+      g_count.store(0);
     }
   }
   json::Value arr = json::Value::array();
