@@ -576,6 +576,26 @@ def _phase(d, nat, info, args, phase, concurrency, warmup, steps, cluster):
     return out
 
 
+def _warm(d, nat, info, args, key, concurrency, steps):
+    """Untimed closed-loop steps (`steps` x --rounds rounds of --batch tenants per rank),
+    every tenant deleted afterwards."""
+    from bacchus_gpu_controller_amd.testing.cluster import ADMIN_TOKEN
+
+    driver = nat.ChurnDriver(info["server"], ADMIN_TOKEN, f"r{d.rank}-", concurrency, ca_pem=info["apiserver_ca"],
+                             http2=args.driver_http2, server_filter=args.driver_server_filter)
+    driver.start()
+    prev = None
+    try:
+        for s in range(steps * args.rounds):
+            names = _names(d.rank, key, s, args.batch)
+            driver.step_with_delete(names, prev or [], args.timeout)
+            prev = names
+        driver.remove(prev or [])
+    finally:
+        driver.stop()
+    d.barrier()
+
+
 def _settle(info, timeout=10.0):
     """Waits until kube-lite's garbage collector has caught up (the cascades of the previous
     phase's deletions), so a phase does not start on the tail of another one's work."""
@@ -1034,6 +1054,15 @@ def run(args):
             rows = [{"id_username": name} for r in range(d.world) for p in phases if p.rate is None
                     for s in range((p.warmup + p.steps) * args.rounds)
                     for name in _names(r, p.key, s, args.batch)]
+        # ... and the warm-up tenants of a rate window that follows a controller restart
+        sem = semantics
+        for p in phases:
+            if controller_env(p.semantics) != controller_env(sem):
+                sem = p.semantics
+                if p.rate is not None and args.restart_warmup_steps > 0:
+                    rows += [{"id_username": name} for r in range(d.world)
+                             for s in range(args.restart_warmup_steps * args.rounds)
+                             for name in _names(r, f"x{p.key}", s, args.batch)]
         # the open-loop phases' tenants are pre-approved in either flow
         for p in phases:
             if p.rate is not None:
@@ -1080,6 +1109,7 @@ def run(args):
         latency = args.write_latency_ms  # kube-lite's current storage latency
         phase_wall = {"setup": round(time.monotonic() - t_run, 2)}  # wall seconds per phase (rank 0's view)
         skipped = []
+        restarted = False
         for p in phases:
             t_phase = time.monotonic()
             if p.key in optional and args.time_budget_s > 0:
@@ -1108,7 +1138,19 @@ def run(args):
                     cluster.start_controller()
                     info["controller"] = f"http://127.0.0.1:{cluster.controller_port}"
                     running = p.semantics
+                    restarted = True
+            restarted = d.broadcast_obj(restarted)
             d.barrier()
+            if p.rate is not None and restarted and args.restart_warmup_steps > 0:
+                # A freshly started controller has no pooled API connections (each worker
+                # dials and handshakes TLS on its first requests, kube-lite spawns a thread
+                # per connection) and verifies every owner's children on its first reconcile:
+                # its first second is not its steady state (10-20 ms apply->Ready tails in
+                # the first window after a restart, profiles/r6_tails/).  Untimed closed-loop
+                # steps warm it, as the reference arm's closed-loop phase warms it before its
+                # windows.
+                _warm(d, nat, info, args, f"x{p.key}", conc, args.restart_warmup_steps)
+            restarted = False
             if p.rate is not None:
                 results[p.key] = _rate_phase(d, nat, info, args, p.key, p.rate, cluster)
                 if results[p.key] is not None:
@@ -1344,6 +1386,8 @@ def main(argv=None):
     ap.add_argument("--trace-windows", action=argparse.BooleanOptionalAction, default=True,
                     help="trace every tenant of each open-loop window through every process and attribute its "
                          "apply->Ready time to stages (latency_at_rate.attribution; bench/attribution.py)")
+    ap.add_argument("--restart-warmup-steps", type=int, default=3,
+                    help="untimed closed-loop steps that warm a restarted controller before an open-loop window")
     ap.add_argument("--trace-dump", default="",
                     help="directory: per open-loop window, the worst tail tenants' full timelines and every mark "
                          "around the worst one (bench/attribution.py analyze(detail=...))")
