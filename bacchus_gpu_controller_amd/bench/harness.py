@@ -277,6 +277,28 @@ def runqueue_wait_ms(pids):
     return total / 1e6
 
 
+def cpu_ticks(cpus):
+    """(busy, total) jiffies summed over `cpus` (/proc/stat), for the job's CPU share."""
+    busy = total = 0
+    try:
+        with open("/proc/stat") as f:
+            for line in f:
+                if line.startswith("cpu") and line[3:4].isdigit():
+                    p = line.split()
+                    if int(p[0][3:]) in cpus:
+                        v = [int(x) for x in p[1:]]
+                        total += sum(v[:8])
+                        busy += sum(v[:8]) - v[3] - (v[4] if len(v) > 4 else 0)
+    except (OSError, ValueError):
+        pass
+    return busy, total
+
+
+def job_cpu_seconds(pids):
+    """utime+stime of every process in `pids` (all threads), seconds."""
+    return sum(_cpu_seconds(p) or 0.0 for p in pids)
+
+
 def auto_concurrency(world, cpus):
     """In-flight creates per rank.  The control plane is CPU-bound, so the total in flight
     is sized to its CPU share rather than fixed per rank: measured on the MI355X box
@@ -672,6 +694,10 @@ def _rate_phase(d, nat, info, args, key, rate, cluster):
             starts = {k: _clear(url, verify) for k, (url, verify) in _sample_logs(info).items()}
             thr0 = cgroup_throttling()
             rq0 = runqueue_wait_ms(pids)
+            # CPU time on the job's CPUs that the job itself did not use: another tenant of
+            # the host (the box shares its CPUs) competing for the share
+            job_cpus = set(os.sched_getaffinity(0))
+            tick0, own0, wall0 = cpu_ticks(job_cpus), job_cpu_seconds(pids), time.monotonic()
             if traced:
                 for _, base, verify in _debug_processes(info):
                     _debug_call("POST", base + "/debug/trace", verify, data=prefixes)
@@ -682,6 +708,8 @@ def _rate_phase(d, nat, info, args, key, rate, cluster):
         d.barrier()
         thr1 = cgroup_throttling() if d.rank == 0 else None
         rq1 = runqueue_wait_ms(pids) if d.rank == 0 else None
+        if d.rank == 0:
+            tick1, own1, wall1 = cpu_ticks(job_cpus), job_cpu_seconds(pids), time.monotonic()
         mine = {"trace": json.loads(nat.trace_take()), "stalls": json.loads(nat.stall_take())} if traced else None
     finally:
         driver.stop()
@@ -727,6 +755,12 @@ def _rate_phase(d, nat, info, args, key, rate, cluster):
     if rq0 is not None and rq1 is not None:
         # CPU-ms the job's threads waited in run queues per second of window
         out["runqueue_wait_ms_per_s"] = round((rq1 - rq0) / max(args.latency_window_s, 1e-9), 1)
+        hz = os.sysconf("SC_CLK_TCK")
+        busy_s = (tick1[0] - tick0[0]) / hz
+        dt = max(wall1 - wall0, 1e-9)
+        out["cpus_busy"] = round(busy_s / dt, 2)           # CPUs' worth busy on the job's CPU set
+        out["job_cpus_used"] = round((own1 - own0) / dt, 2)  # of which the job's own processes
+        out["foreign_cpus"] = round(max(0.0, busy_s - (own1 - own0)) / dt, 2)
     if traced:
         detail = {} if args.trace_dump else None
         out["attribution"] = attribution.analyze(traces, stalls, tail_ms=args.tail_ms, detail=detail)
@@ -746,7 +780,8 @@ def _rate_phase(d, nat, info, args, key, rate, cluster):
 _WINDOW_KEYS = ("offered_rate", "achieved_rate", "achieved_within_2pct", "reconcile_p99_ms", "reconcile_p50_ms",
                 "reconciles", "admission_p50_ms", "admission_p99_ms", "admission_handler_p50_ms",
                 "apply_to_ready_p50_ms", "apply_to_ready_p99_ms", "issue_lag_p99_ms", "ready_crs", "failed_crs",
-                "cgroup_throttled_periods", "runqueue_wait_ms_per_s", "errors")
+                "cgroup_throttled_periods", "runqueue_wait_ms_per_s", "cpus_busy", "job_cpus_used", "foreign_cpus",
+                "errors")
 
 
 def _pool_arm(results, prefix, rates, windows):
