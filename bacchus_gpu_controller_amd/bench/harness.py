@@ -294,6 +294,40 @@ def cpu_ticks(cpus):
     return busy, total
 
 
+def thread_cpu(procs):
+    """{(process, thread name): [cpu seconds per thread]} over every thread of `procs`
+    ({process name: pid}), from /proc/<pid>/task/<tid>/stat (comm, utime, stime)."""
+    tck = os.sysconf("SC_CLK_TCK")
+    out = {}
+    for pname, pid in procs.items():
+        try:
+            tids = os.listdir(f"/proc/{pid}/task")
+        except OSError:
+            continue
+        for tid in tids:
+            try:
+                with open(f"/proc/{pid}/task/{tid}/stat") as f:
+                    raw = f.read()
+                comm = raw[raw.index("(") + 1:raw.rindex(")")]
+                fields = raw.rsplit(")", 1)[1].split()
+                out[(pname, comm, tid)] = (int(fields[11]) + int(fields[12])) / tck
+            except (OSError, ValueError, IndexError):
+                pass
+    return out
+
+
+def busiest_threads(t0, t1, dt, top=6):
+    """The threads that used the most CPU between two thread_cpu() readings, as share of
+    one CPU: a single-threaded stage near 1.0 is a pipeline bottleneck (its queue grows)."""
+    used = []
+    for k, v in t1.items():
+        d = v - t0.get(k, 0.0)
+        if d > 0:
+            used.append((d / dt, k))
+    used.sort(reverse=True)
+    return [{"process": k[0], "thread": k[1], "cpu": round(u, 2)} for u, k in used[:top]]
+
+
 def job_cpu_seconds(pids):
     """utime+stime of every process in `pids` (all threads), seconds."""
     return sum(_cpu_seconds(p) or 0.0 for p in pids)
@@ -698,6 +732,8 @@ def _rate_phase(d, nat, info, args, key, rate, cluster):
             # the host (the box shares its CPUs) competing for the share
             job_cpus = set(os.sched_getaffinity(0))
             tick0, own0, wall0 = cpu_ticks(job_cpus), job_cpu_seconds(pids), time.monotonic()
+            named = {"load-driver": os.getpid(), **{n: p.p.pid for n, p in cluster.procs.items()}}
+            thr_cpu0 = thread_cpu(named)
             if traced:
                 for _, base, verify in _debug_processes(info):
                     _debug_call("POST", base + "/debug/trace", verify, data=prefixes)
@@ -710,6 +746,7 @@ def _rate_phase(d, nat, info, args, key, rate, cluster):
         rq1 = runqueue_wait_ms(pids) if d.rank == 0 else None
         if d.rank == 0:
             tick1, own1, wall1 = cpu_ticks(job_cpus), job_cpu_seconds(pids), time.monotonic()
+            thr_cpu1 = thread_cpu(named)
         mine = {"trace": json.loads(nat.trace_take()), "stalls": json.loads(nat.stall_take())} if traced else None
     finally:
         driver.stop()
@@ -761,6 +798,7 @@ def _rate_phase(d, nat, info, args, key, rate, cluster):
         out["cpus_busy"] = round(busy_s / dt, 2)           # CPUs' worth busy on the job's CPU set
         out["job_cpus_used"] = round((own1 - own0) / dt, 2)  # of which the job's own processes
         out["foreign_cpus"] = round(max(0.0, busy_s - (own1 - own0)) / dt, 2)
+        out["busiest_threads"] = busiest_threads(thr_cpu0, thr_cpu1, dt)
     if traced:
         detail = {} if args.trace_dump else None
         out["attribution"] = attribution.analyze(traces, stalls, tail_ms=args.tail_ms, detail=detail)
@@ -781,7 +819,7 @@ _WINDOW_KEYS = ("offered_rate", "achieved_rate", "achieved_within_2pct", "reconc
                 "reconciles", "admission_p50_ms", "admission_p99_ms", "admission_handler_p50_ms",
                 "apply_to_ready_p50_ms", "apply_to_ready_p99_ms", "issue_lag_p99_ms", "ready_crs", "failed_crs",
                 "cgroup_throttled_periods", "runqueue_wait_ms_per_s", "cpus_busy", "job_cpus_used", "foreign_cpus",
-                "errors")
+                "busiest_threads", "errors")
 
 
 def _pool_arm(results, prefix, rates, windows):

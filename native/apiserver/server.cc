@@ -25,6 +25,7 @@
 #include "core/json_patch.h"
 #include "core/log.h"
 #include "core/metrics.h"
+#include "core/process.h"
 #include "core/trace.h"
 #include "core/net.h"
 #include "core/yaml.h"
@@ -2281,6 +2282,11 @@ struct ApiServer::Impl {
     if (req.has_query_param("timeoutSeconds")) timeout_s = std::min(timeout_s, std::atoi(req.query_param("timeoutSeconds").c_str()));
     bool bookmarks = req.query_param("allowWatchBookmarks") == "true";
     const std::string trace_watch = "kl.watch." + p.ti->rt.plural + "." + field_manager(req, "unknown") + ".sent";
+    // the serving thread streams this watch from here on: name it for per-thread CPU reports
+    set_thread_name("kw:" + p.ti->rt.plural);
+    struct Rename {
+      ~Rename() { set_thread_name("conn:apiserver"); }
+    } rename;
     // Streaming lists (WatchList): sendInitialEvents=true replays the current state as
     // ADDED events, then a BOOKMARK annotated k8s.io/initial-events-end marks the point
     // where the initial state is complete (requires allowWatchBookmarks and

@@ -32,8 +32,8 @@ ChurnDriver::ChurnDriver(ChurnOptions o) : opts_(std::move(o)) {
   ho.http2 = opts_.http2;
   if (opts_.server.rfind("https", 0) == 0) ho.tls = net::TlsContext::client(opts_.ca_pem, false, "", "");
   http_ = std::make_unique<http::Client>(ho);
-  pool_ = std::make_unique<ThreadPool>(static_cast<size_t>(std::max(1, opts_.concurrency)));
-  delete_pool_ = std::make_unique<ThreadPool>(static_cast<size_t>(std::max(1, opts_.concurrency / 2)));
+  pool_ = std::make_unique<ThreadPool>(static_cast<size_t>(std::max(1, opts_.concurrency)), "drv-create");
+  delete_pool_ = std::make_unique<ThreadPool>(static_cast<size_t>(std::max(1, opts_.concurrency / 2)), "drv-delete");
 }
 
 json::Value ChurnDriver::step_with_delete(const std::vector<std::string>& names,

@@ -177,7 +177,7 @@ std::vector<DesiredChild> desired_children(const Value& ub, bool label) {
 }
 
 Reconciler::Reconciler(kube::KubeClient& client, kube::Controller& ctrl, Config cfg)
-    : client_(client), ctrl_(ctrl), cfg_(cfg), pool_(static_cast<size_t>(std::max(4, cfg.workers * 3))) {}
+    : client_(client), ctrl_(ctrl), cfg_(cfg), pool_(static_cast<size_t>(std::max(4, cfg.workers * 3)), "apply") {}
 
 Reconciler::Stats Reconciler::stats() const {
   return {stats_applied_.load(std::memory_order_relaxed), stats_skipped_.load(std::memory_order_relaxed),

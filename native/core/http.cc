@@ -22,6 +22,7 @@
 #include "core/metrics.h"
 #include "core/stall.h"
 #include "core/trace.h"
+#include "core/process.h"
 
 namespace bgc::http {
 
@@ -336,7 +337,12 @@ struct Server::WorkerPool {
       self->q.push_back(std::move(job));
       spawn = self->idle < self->q.size();
     }
-    if (spawn) std::thread([self] { run(self); }).detach();
+    if (spawn) {
+      std::thread([self] {
+        set_thread_name("h2-worker");
+        run(self);
+      }).detach();
+    }
     else self->cv.notify_one();
   }
 };
@@ -462,6 +468,7 @@ void Server::accept_loop() {
     }
     active_.fetch_add(1);
     std::thread([this, fd, remote = std::string(host)] {
+      set_thread_name(opts_.name.empty() ? "conn" : "conn:" + opts_.name);
       serve_conn(fd, remote);
       // OpenSSL keeps per-thread state (the thread's public/private DRBGs, its error queue)
       // that OPENSSL_thread_stop() releases at once (found by LeakSanitizer, tools/sanitize.sh

@@ -1,4 +1,5 @@
 #include "core/log.h"
+#include "core/process.h"
 
 #include <algorithm>
 #include <cctype>
@@ -104,6 +105,7 @@ class AsyncWriter {
     std::lock_guard<std::mutex> lk(start_mu_);
     if (started_.load()) return;
     std::thread([this] {
+      set_thread_name("log-writer");
       // the writer must not take signals meant for the services' shutdown handling
       sigset_t all;
       sigfillset(&all);

@@ -191,6 +191,10 @@ static void die_with_parent_from_env() {
   }
 }
 
+void set_thread_name(const std::string& name) {
+  ::pthread_setname_np(::pthread_self(), name.substr(0, 15).c_str());
+}
+
 void process_init() {
   die_with_parent_from_env();
   init_openssl();

@@ -3,11 +3,16 @@
 #pragma once
 
 #include <chrono>
+#include <string>
 
 namespace bgc {
 
 // Call first thing in main().
 void process_init();
+
+// Names the calling thread (first 15 bytes; `top -H`, /proc/<pid>/task/<tid>/comm): the
+// bench attributes CPU per thread by these names.
+void set_thread_name(const std::string& name);
 
 // OpenSSL without its atexit cleanup (see process.cc); part of process_init().
 void init_openssl();

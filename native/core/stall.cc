@@ -15,6 +15,7 @@
 #include "core/json.h"
 #include "core/metrics.h"
 #include "core/schedstat.h"
+#include "core/process.h"
 
 namespace bgc::stall {
 
@@ -46,6 +47,7 @@ std::vector<double> stall_buckets() {
 }
 
 void loop() {
+  set_thread_name("stall-sampler");
   sigset_t all;
   sigfillset(&all);
   pthread_sigmask(SIG_BLOCK, &all, nullptr);

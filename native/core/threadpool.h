@@ -9,15 +9,20 @@
 #include <memory>
 #include <mutex>
 #include <thread>
+#include <string>
 #include <vector>
+
+#include "core/process.h"
 
 namespace bgc {
 
 class ThreadPool {
  public:
-  explicit ThreadPool(size_t n) {
+  // `name`: the workers' thread name (set_thread_name), empty = inherited
+  explicit ThreadPool(size_t n, const std::string& name = "") {
     for (size_t i = 0; i < n; ++i) {
-      threads_.emplace_back([this] {
+      threads_.emplace_back([this, name] {
+        if (!name.empty()) set_thread_name(name);
         while (true) {
           std::function<void()> job;
           {

@@ -6,6 +6,7 @@
 #include "core/log.h"
 #include "core/metrics.h"
 #include "core/roctx.h"
+#include "core/process.h"
 #include "core/schedstat.h"
 
 namespace bgc::gpu {
@@ -24,7 +25,7 @@ TelemetryPoller::TelemetryPoller(Backend& backend, std::vector<int> indices, std
   slow_cache_.resize(indices_.size());
   ras_cache_.resize(indices_.size());
   prev_.resize(indices_.size());
-  if (indices_.size() > 1) pool_ = std::make_unique<ThreadPool>(indices_.size());
+  if (indices_.size() > 1) pool_ = std::make_unique<ThreadPool>(indices_.size(), "telemetry-dev");
   auto& reg = metrics::Registry::global();
   for (int i : indices_) {
     metrics::Labels l{{"gpu", std::to_string(i)}};
@@ -333,6 +334,7 @@ void TelemetryPoller::check_stall() {
 void TelemetryPoller::start() {
   if (thread_.joinable()) return;
   thread_ = std::thread([this] {
+    set_thread_name("telemetry");
     while (!stop_.cancelled()) {
       try {
         poll_once();
@@ -345,6 +347,7 @@ void TelemetryPoller::start() {
   if (stall_timeout_.count() > 0) {
     const auto tick = std::clamp(stall_timeout_ / 4, std::chrono::milliseconds(10), std::chrono::milliseconds(1000));
     watchdog_ = std::thread([this, tick] {
+      set_thread_name("telemetry-dog");
       while (!stop_.wait_for(tick)) check_stall();
     });
   }

@@ -7,6 +7,7 @@
 #include "core/metrics.h"
 #include "core/trace.h"
 #include "core/net.h"
+#include "core/process.h"
 
 namespace bgc::kube {
 
@@ -180,6 +181,7 @@ static bool is_control_event(std::string_view line) {
 }
 
 void Watcher::run(CancelToken& stop, const std::function<void(const WatchEvent&)>& on_event) {
+  set_thread_name("w:" + rt_.plural);
   std::string rv;
   bool need_list = true;
   auto backoff = std::chrono::milliseconds(800);
@@ -661,6 +663,7 @@ void Controller::run(CancelToken& stop, Reconciler reconcile, ErrorPolicy error_
   std::vector<std::thread> workers;
   for (int i = 0; i < std::max(1, opts_.workers); ++i) {
     workers.emplace_back([&] {
+      set_thread_name("reconcile");
       std::string key;
       while (queue_.get(key)) {
         q_depth.set(static_cast<double>(queue_.pending()));

@@ -12,6 +12,7 @@
 #include "core/metrics.h"
 #include "core/trace.h"
 #include "kube/ratelimit.h"
+#include "core/process.h"
 
 namespace bgc::sync {
 
@@ -292,6 +293,7 @@ int Synchronizer::run(CancelToken& stop) {
     });
     for (int i = 0; i < std::max(1, cfg_.workers); ++i) {
       workers.emplace_back([&] {
+        set_thread_name("sync-worker");
         std::string key;
         while (queue.get(key)) {
           kube::ObjPtr ub = store.get(key);
