@@ -5,7 +5,6 @@
 #include <pthread.h>
 #include <signal.h>
 #include <sys/prctl.h>
-#include <sys/resource.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -55,28 +54,16 @@ void tune_malloc() {
   mallopt(M_MMAP_THRESHOLD, 4 << 20);
 }
 
-// The trim threshold above keeps freed heap resident between bursts (no madvise churn on
-// the hot path).  A trimmer thread hands memory that stayed free back to the OS once the
-// resident set has grown: every BGC_MALLOC_TRIM_SECS (default 30; 0 disables) it reads the
-// RSS (/proc/self/statm, cheap) and runs malloc_trim only when the RSS exceeds both
-// BGC_MALLOC_TRIM_MIN_MB (default 64) and 1.5x the RSS left by the previous trim.
-// malloc_trim walks every free chunk under its arena's lock: measured on the MI355X box a
-// pass stalled the synchronizer (85 MB RSS) for 13-15 ms and kube-lite (1.5 GB) for
-// 110-130 ms, every 30 s, which showed up as apply->Ready tails.  Trimming on growth keeps
-// the RSS of a long-running service near its live data after a burst without stalling a
-// steady one.  A pass also waits for a quiet interval: the process used at most
-// BGC_MALLOC_TRIM_IDLE_PCT (default 5) % of one CPU since the last check, so the stall
-// lands between bursts of work, not inside one (the synchronizer's one pass per bench run
-// fell into a latency window: a 13-15 ms stall of the path to Ready).  A process that is
-// never quiet still trims once its RSS has passed 4x the previous trim's (and 4x the minimum),
-// or half its container's memory limit: freed memory that many threads' arenas keep while
-// busy (the admission server: 17 MB live at 195 MB RSS after a bench run) must not reach an
-// OOM kill.
-TrimDecision malloc_trim_decision(long rss, long baseline, long min_bytes, double busy_pct, double idle_pct,
-                                  long limit_bytes) {
-  if (rss <= min_bytes || rss * 2 <= baseline * 3) return TrimDecision::Skip;
-  if (limit_bytes > 0 && rss > limit_bytes / 2) return TrimDecision::Trim;
-  if (busy_pct > idle_pct && rss < std::max(baseline, min_bytes) * 4) return TrimDecision::Defer;
+// With the arenas bounded and tops trimmed by glibc itself (tune_malloc above) the services'
+// RSS stays within a few MB of their live heap (round 6: admission 40 MB, controller 38 MB,
+// profiles/r6_alloc/), so nothing trims on a timer any more.  Round 5's trimmer thread,
+// with its growth, quiet-interval and 4x heuristics, compensated for the 64 MiB heap growth
+// and 512 MiB trim threshold it replaced; it stalled the process for 13-15 ms per pass
+// (malloc_trim walks every free chunk under its arena's lock).  One valve stays: a process
+// whose RSS has passed half its container's memory limit (and grown 1.5x since the last
+// pass) trims, rather than reach an OOM kill with freed memory still resident.
+TrimDecision malloc_trim_decision(long rss, long baseline, long limit_bytes) {
+  if (limit_bytes <= 0 || rss <= limit_bytes / 2 || rss * 2 <= baseline * 3) return TrimDecision::Skip;
   return TrimDecision::Trim;
 }
 
@@ -98,13 +85,6 @@ long cgroup_memory_limit_bytes() {
   return 0;
 }
 
-static double cpu_seconds() {
-  struct rusage ru {};
-  if (getrusage(RUSAGE_SELF, &ru) != 0) return 0;
-  return static_cast<double>(ru.ru_utime.tv_sec + ru.ru_stime.tv_sec) +
-         static_cast<double>(ru.ru_utime.tv_usec + ru.ru_stime.tv_usec) * 1e-6;
-}
-
 static long rss_bytes() {
   long pages_total = 0, pages_rss = 0;
   if (FILE* f = std::fopen("/proc/self/statm", "r")) {
@@ -117,12 +97,10 @@ static long rss_bytes() {
 void start_malloc_trimmer() {
   const char* e = std::getenv("BGC_MALLOC_TRIM_SECS");
   const long secs = e ? std::atol(e) : 30;
-  if (secs <= 0) return;
-  const char* m = std::getenv("BGC_MALLOC_TRIM_MIN_MB");
-  const long min_bytes = (m ? std::atol(m) : 64) << 20;
-  const char* ip = std::getenv("BGC_MALLOC_TRIM_IDLE_PCT");
-  const double idle_pct = ip ? std::atof(ip) : 5.0;
-  std::thread([secs, min_bytes, idle_pct] {
+  const long limit = cgroup_memory_limit_bytes();
+  if (secs <= 0 || limit <= 0) return;  // no limit to keep under: glibc's own trimming is enough
+  std::thread([secs, limit] {
+    set_thread_name("malloc-trim");
     // Never take process signals here: SIGTERM/SIGINT are collected by the sigwait thread
     // that install_shutdown_signals starts (this thread exists before that mask is set).
     sigset_t all;
@@ -131,26 +109,13 @@ void start_malloc_trimmer() {
     auto& reg = metrics::Registry::global();
     auto& hist = reg.histogram("bgc_malloc_trim_seconds", "Wall time of one malloc_trim pass");
     auto& last = reg.gauge("bgc_malloc_trim_last_seconds", "Wall time of the last malloc_trim pass");
-    auto& skipped = reg.counter("bgc_malloc_trim_skipped_total", "Trim checks that found the RSS below the trigger");
-    auto& deferred = reg.counter("bgc_malloc_trim_deferred_total",
-                                 "Trim checks that found the RSS grown but the process busy");
     auto& limit_g = reg.gauge("bgc_malloc_trim_memory_limit_bytes",
-                              "Container memory limit the trimmer keeps the RSS under half of (0 = none)");
-    const long limit = cgroup_memory_limit_bytes();
+                              "Container memory limit the trimmer keeps the RSS under half of");
     limit_g.set(static_cast<double>(limit));
-    long baseline = rss_bytes();
-    double cpu0 = cpu_seconds();
+    long baseline = 0;
     while (true) {
       std::this_thread::sleep_for(std::chrono::seconds(secs));
-      const long rss = rss_bytes();
-      const double cpu = cpu_seconds();
-      const double busy_pct = (cpu - cpu0) * 100.0 / static_cast<double>(secs);
-      cpu0 = cpu;
-      const TrimDecision d = malloc_trim_decision(rss, baseline, min_bytes, busy_pct, idle_pct, limit);
-      if (d != TrimDecision::Trim) {
-        (d == TrimDecision::Skip ? skipped : deferred).inc();
-        continue;
-      }
+      if (malloc_trim_decision(rss_bytes(), baseline, limit) != TrimDecision::Trim) continue;
       const int64_t t0 = metrics::now_ns();
       malloc_trim(0);
       const double dt = static_cast<double>(metrics::now_ns() - t0) * 1e-9;

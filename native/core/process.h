@@ -21,13 +21,11 @@ void init_openssl();
 // servers (process.cc): at most 4 arenas, heaps grown 4 MiB at a time and trimmed above
 // 16 MiB free, a fixed 4 MiB mmap threshold.  BGC_MALLOC_TUNE=0 disables it.
 void tune_malloc();
-// The periodic trimmer's rule (process.cc): Skip while the RSS is under the minimum or under
-// 1.5x the RSS the previous pass left; Defer while the process used more than idle_pct % of
-// one CPU since the last check, unless the RSS passed 4x max(previous, minimum) or half the
-// container's memory limit (limit_bytes, 0 = none); else Trim.
-enum class TrimDecision { Skip, Defer, Trim };
-TrimDecision malloc_trim_decision(long rss, long baseline, long min_bytes, double busy_pct, double idle_pct,
-                                  long limit_bytes = 0);
+// The memory-limit valve's rule (process.cc): Trim once the RSS has passed half the
+// container's memory limit (limit_bytes, 0 = none: never) and grown 1.5x since the RSS the
+// previous pass left (baseline); else Skip.
+enum class TrimDecision { Skip, Trim };
+TrimDecision malloc_trim_decision(long rss, long baseline, long limit_bytes);
 // The cgroup memory limit of this process (v2 memory.max, else v1 limit_in_bytes); 0 = none.
 long cgroup_memory_limit_bytes();
 // Bounds a graceful shutdown once it has started: after `limit` the process logs, flushes

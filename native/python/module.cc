@@ -187,15 +187,9 @@ PYBIND11_MODULE(_native, m) {
     bgc::log::init_from_env();
     return r;
   });
-  m.def("malloc_trim_decision", [](long rss, long baseline, long min_bytes, double busy_pct, double idle_pct,
-                                   long limit_bytes) {
-    switch (bgc::malloc_trim_decision(rss, baseline, min_bytes, busy_pct, idle_pct, limit_bytes)) {
-      case bgc::TrimDecision::Skip: return "skip";
-      case bgc::TrimDecision::Defer: return "defer";
-      default: return "trim";
-    }
-  }, py::arg("rss"), py::arg("baseline"), py::arg("min_bytes"), py::arg("busy_pct"), py::arg("idle_pct"),
-        py::arg("limit_bytes") = 0);
+  m.def("malloc_trim_decision", [](long rss, long baseline, long limit_bytes) {
+    return bgc::malloc_trim_decision(rss, baseline, limit_bytes) == bgc::TrimDecision::Trim ? "trim" : "skip";
+  }, py::arg("rss"), py::arg("baseline"), py::arg("limit_bytes"));
   m.def("cgroup_memory_limit_bytes", &bgc::cgroup_memory_limit_bytes);
   // `threads` threads each log `lines` INFO lines "<tag> <thread> <i> xxx..." of `width` pad
   // bytes; thread 0's line number `error_at` (if >= 0) is an ERROR line instead.  Returns the

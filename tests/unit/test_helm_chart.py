@@ -267,10 +267,15 @@ def test_values_and_name_parity_with_reference():
     # liveness); the reference's /health stays their liveness probe
     changed = {("controller", "readinessProbe", "httpGet", "path"): "/readyz",
                ("synchronizer", "readinessProbe", "httpGet", "path"): "/readyz"}
+    # ... and documented resource defaults instead of the reference's `resources: {}`
+    # (test_control_plane_resources_have_documented_defaults)
+    sized = {(c, "resources") for c in ("controller", "admission", "synchronizer")}
     for p in paths(ref):
         get(ours, p)  # every reference key exists
         if p in changed:
             assert get(ref, p) == "/health" and get(ours, p) == changed[p], ".".join(p)
+        elif p in sized:
+            assert get(ref, p) == {} and set(get(ours, p)) == {"requests", "limits"}, ".".join(p)
         elif p[-1] != "repository":
             assert get(ours, p) == get(ref, p), ".".join(p)
     with open(os.path.join(REF_CHART, "Chart.yaml")) as f:
@@ -493,3 +498,19 @@ def test_log_format_json_reaches_every_service():
     assert all("BGC_LOG_FORMAT" not in e for e in default.values())
     js = envs(render({"logFormat": "json", "nodeAgent": {"enabled": True}}))
     assert len(js) == 4 and all(e.get("BGC_LOG_FORMAT") == "json" for e in js.values()), js
+
+
+def test_control_plane_resources_have_documented_defaults(objs):
+    """the three control-plane Deployments ship requests and a memory limit
+    (sized from the round-6 bench, values.yaml comments), and no CPU limit."""
+    deps = by_kind(objs, "Deployment")
+    want = {"controller": ("100m", "64Mi", "256Mi"), "admission": ("100m", "64Mi", "192Mi"),
+            "synchronizer": ("50m", "64Mi", "512Mi")}
+    for comp, (cpu, mem_req, mem_lim) in want.items():
+        res = deps[f"bgc-bacchus-gpu-{comp}"]["spec"]["template"]["spec"]["containers"][0]["resources"]
+        assert res["requests"] == {"cpu": cpu, "memory": mem_req}, comp
+        assert res["limits"] == {"memory": mem_lim}, comp
+    # still removable (helm: a null value deletes a default key), back to the reference's none
+    res = render({"admission": {"resources": None}})
+    adm = by_kind(res, "Deployment")["bgc-bacchus-gpu-admission"]["spec"]["template"]["spec"]["containers"][0]
+    assert not adm.get("resources")
