@@ -10,8 +10,8 @@
 namespace bgc::sched {
 
 struct ThreadSched {
-  int64_t cpu_ns = -1;   // on-CPU time so far (-1: unavailable)
-  int64_t runq_ns = -1;  // run-queue delay so far
+  int64_t cpu_ns = -1;   // on-CPU time so far, CLOCK_THREAD_CPUTIME_ID (-1: unavailable)
+  int64_t runq_ns = -1;  // run-queue delay so far, schedstat (updated as each wait ends)
   bool ok() const { return cpu_ns >= 0 && runq_ns >= 0; }
 };
 

@@ -108,11 +108,12 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "telemetry_marker"))
     ap.add_argument("--seconds", type=float, default=30.0)
     ap.add_argument("--poll-ms", type=int, default=250)
-    ap.add_argument("rest", nargs="*", help="bench mode: arguments for bench.py (after --)")
-    a = ap.parse_args()
+    a, rest = ap.parse_known_args()  # bench mode: everything after "--" goes to bench.py
+    a.rest = [x for x in rest if x != "--"]
     out_dir = os.path.abspath(os.path.join(a.out, a.mode))
     os.makedirs(out_dir, exist_ok=True)
-    os.environ["BGC_WRAP_NODE_AGENT"] = f"rocprofv3 --marker-trace --stats -d {out_dir}/trace -o agent --"
+    os.environ["BGC_WRAP_NODE_AGENT"] = (f"rocprofv3 --marker-trace --stats --output-format csv -d {out_dir}/trace "
+                                         "-o agent --")
     res = quiet(out_dir, a.seconds, a.poll_ms) if a.mode == "quiet" else bench(out_dir, a.rest)
     res["markers"] = summarize_markers(os.path.join(out_dir, "trace"))
     with open(os.path.join(out_dir, "summary.json"), "w") as f:
