@@ -78,14 +78,33 @@ def _split(url):
     return out
 
 
+def _thread_times(pid, name):
+    """(utime, stime) seconds of the thread called `name` in process `pid` (user vs kernel
+    CPU: the amdsmi metrics call's kernel part is the driver's synchronous SMU exchange)."""
+    tck = os.sysconf("SC_CLK_TCK")
+    for tid in os.listdir(f"/proc/{pid}/task"):
+        try:
+            raw = open(f"/proc/{pid}/task/{tid}/stat").read()
+        except OSError:
+            continue
+        if raw[raw.index("(") + 1:raw.rindex(")")] == name:
+            f = raw.rsplit(")", 1)[1].split()
+            return int(f[11]) / tck, int(f[12]) / tck
+    return None
+
+
 def quiet(out_dir, seconds, poll_ms):
     from bacchus_gpu_controller_amd.testing.cluster import Cluster
 
     with Cluster(admission=False, controller=False) as c:
-        c.start_node_agent(max_gpus=1, poll_interval_ms=poll_ms, extra_env={"CONF_RUN_DIAG": "false"})
+        p = c.start_node_agent(max_gpus=1, poll_interval_ms=poll_ms, extra_env={"CONF_RUN_DIAG": "false"})
         url = f"http://127.0.0.1:{c.node_agent_port}"
+        t0 = _thread_times(p.p.pid, "telemetry")
         time.sleep(seconds)
+        t1 = _thread_times(p.p.pid, "telemetry")
         split = _split(url)
+        if t0 and t1:
+            split["telemetry_thread_cpu_s"] = {"user": round(t1[0] - t0[0], 3), "kernel": round(t1[1] - t0[1], 3)}
         gpus = __import__("requests").get(url + "/gpus", timeout=10).json()
         c.procs["node-agent"].stop(timeout=30)  # SIGTERM: rocprofv3 writes its trace at exit
     return {"mode": "quiet", "seconds": seconds, "poll_ms": poll_ms, "backend": gpus.get("backend"),

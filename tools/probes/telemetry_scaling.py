@@ -2,7 +2,14 @@
 MI355X whose backend sleeps the per-call latency measured for amdsmi on MI355X
 (profiles/archive/amdsmi_cost_r2.json: Fast 141 us, Slow 960 us, Ras 1836 us p50 per device).
 Devices are sampled concurrently (one task per GPU), so a poll should cost about one
-device's latency at every N, not N of them.  Writes a JSON summary."""
+device's latency at every N, not N of them.  Writes a JSON summary.
+
+UNVERIFIED ON HARDWARE: this model assumes amdsmi calls on different devices run
+concurrently (one call at a time per handle, none across handles).  Every lease so far had
+one GPU, so no multi-GPU poll has been timed.  On MI355X the metrics call is also mostly the
+kernel's synchronous SMU exchange, on-CPU in the polling thread
+(profiles/r6_telemetry/: ~0.65 ms in round 6), so eight devices may also need eight CPUs'
+worth of short busy-waits at once, or contend inside the driver."""
 import json
 import os
 import statistics
