@@ -19,7 +19,9 @@
 using namespace bgc;
 
 int main() {
-  process_init();
+  ProcessDefaults defaults;
+  defaults.malloc_arena_max = 16;  // see tune_malloc (core/process.cc)
+  process_init(defaults);
   controller::Config cfg;
   try {
     cfg = controller::Config::from_env(EnvConfig("CONF_"));

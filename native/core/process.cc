@@ -30,12 +30,14 @@ static long env_long(const char* name, long dflt) {
 // no tcache knob); everything below is set here, and an image env var can no longer
 // disagree with it (round 5: the image's trim_threshold was dead, this overrode it).
 //
-//  * M_ARENA_MAX (BGC_MALLOC_ARENA_MAX, default 4): glibc's default is 8 arenas per CPU —
-//    2,048 on the MI355X hosts' 256 visible CPUs — and a thread-per-connection server gives
-//    nearly every connection thread an arena of its own, each keeping its own free memory:
-//    round 5 measured the admission server at 17 MB live in 195 MB RSS with 11 GB of free
-//    arena space.  The thread cache (64 chunks per size class up to 16 KiB) serves the
-//    hot-path allocations without touching an arena, so 4 arenas are rarely contended.
+//  * M_ARENA_MAX (BGC_MALLOC_ARENA_MAX; default 4, the controller 16): glibc's default is 8
+//    arenas per CPU — 2,048 on the MI355X hosts' 256 visible CPUs — and a thread-per-
+//    connection server gives nearly every connection thread an arena of its own, each
+//    keeping its own free memory: round 5 measured the admission server at 17 MB live in
+//    195 MB RSS with 11 GB of free arena space.  The thread cache (64 chunks per size class
+//    up to 16 KiB) serves most hot-path allocations without an arena.  The controller's 16
+//    workers and their apply threads allocate hard enough that 4 arenas cost it 10 % CPU per
+//    tenant (0.210 against 0.189 ms unbounded, 16: 0.193; profiles/r6_alloc/), so it gets 16.
 //  * M_TOP_PAD 4 MiB (BGC_MALLOC_TOP_PAD_KB) and M_TRIM_THRESHOLD 16 MiB
 //    (BGC_MALLOC_TRIM_THRESHOLD_KB): a heap grows 4 MiB at a time and hands back a free top
 //    above 16 MiB, so bursts do not cycle sbrk per request (the cost the old 64 MiB pad and
@@ -43,10 +45,12 @@ static long env_long(const char* name, long dflt) {
 //  * M_MMAP_THRESHOLD 4 MiB fixed: glibc's dynamic threshold would otherwise climb after
 //    the first large free and keep multi-MiB list bodies in the arenas.
 // BGC_MALLOC_TUNE=0 leaves glibc's defaults; 0 for one knob leaves that one at glibc's.
-void tune_malloc() {
+void tune_malloc(const ProcessDefaults& defaults) {
   const char* e = std::getenv("BGC_MALLOC_TUNE");
   if (e && std::strcmp(e, "0") == 0) return;
-  if (const long a = env_long("BGC_MALLOC_ARENA_MAX", 4); a > 0) mallopt(M_ARENA_MAX, static_cast<int>(a));
+  if (const long a = env_long("BGC_MALLOC_ARENA_MAX", defaults.malloc_arena_max); a > 0) {
+    mallopt(M_ARENA_MAX, static_cast<int>(a));
+  }
   if (const long k = env_long("BGC_MALLOC_TOP_PAD_KB", 4 << 10); k > 0) mallopt(M_TOP_PAD, static_cast<int>(k << 10));
   if (const long k = env_long("BGC_MALLOC_TRIM_THRESHOLD_KB", 16 << 10); k > 0) {
     mallopt(M_TRIM_THRESHOLD, static_cast<int>(k << 10));
@@ -160,10 +164,10 @@ void set_thread_name(const std::string& name) {
   ::pthread_setname_np(::pthread_self(), name.substr(0, 15).c_str());
 }
 
-void process_init() {
+void process_init(const ProcessDefaults& defaults) {
   die_with_parent_from_env();
   init_openssl();
-  tune_malloc();
+  tune_malloc(defaults);
   start_malloc_trimmer();
   log::init_from_env();
   cpuprof::start_from_env();

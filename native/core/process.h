@@ -7,8 +7,13 @@
 
 namespace bgc {
 
+// Per-binary defaults of the allocator settings (tune_malloc; env overrides them).
+struct ProcessDefaults {
+  int malloc_arena_max = 4;
+};
+
 // Call first thing in main().
-void process_init();
+void process_init(const ProcessDefaults& defaults = ProcessDefaults());
 
 // Names the calling thread (first 15 bytes; `top -H`, /proc/<pid>/task/<tid>/comm): the
 // bench attributes CPU per thread by these names.
@@ -20,7 +25,7 @@ void init_openssl();
 // glibc malloc tuning for many short-lived JSON allocations across thread-per-connection
 // servers (process.cc): at most 4 arenas, heaps grown 4 MiB at a time and trimmed above
 // 16 MiB free, a fixed 4 MiB mmap threshold.  BGC_MALLOC_TUNE=0 disables it.
-void tune_malloc();
+void tune_malloc(const ProcessDefaults& defaults = ProcessDefaults());
 // The memory-limit valve's rule (process.cc): Trim once the RSS has passed half the
 // container's memory limit (limit_bytes, 0 = none: never) and grown 1.5x since the RSS the
 // previous pass left (baseline); else Skip.
