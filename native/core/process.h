@@ -23,8 +23,8 @@ void set_thread_name(const std::string& name);
 void init_openssl();
 
 // glibc malloc tuning for many short-lived JSON allocations across thread-per-connection
-// servers (process.cc): at most 4 arenas, heaps grown 4 MiB at a time and trimmed above
-// 16 MiB free, a fixed 4 MiB mmap threshold.  BGC_MALLOC_TUNE=0 disables it.
+// servers (process.cc): at most 4 arenas (16 in the controller), heaps grown 1 MiB at a time
+// and trimmed above 2 MiB free, a fixed 4 MiB mmap threshold.  BGC_MALLOC_TUNE=0 disables it.
 void tune_malloc(const ProcessDefaults& defaults = ProcessDefaults());
 // The memory-limit valve's rule (process.cc): Trim once the RSS has passed half the
 // container's memory limit (limit_bytes, 0 = none: never) and grown 1.5x since the RSS the
