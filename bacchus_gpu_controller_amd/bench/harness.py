@@ -1190,8 +1190,20 @@ def run(args):
                 # latency takes about 6x a headline step
                 per_step = phase_wall["m"] / max(1, args.warmup + args.steps)
                 est = per_step * (p.warmup + p.steps) * (6 if p.write_latency_ms > 0 else 1)
+                if p.key == "rl":
+                    # the write-latency pair goes together: rl only if ml still fits after it
+                    # and after the open-loop windows that always run in between
+                    later = phases[phases.index(p) + 1:]
+                    ml = next((q for q in later if q.key == "ml"), None)
+                    if ml is not None:
+                        between = [q for q in later[:later.index(ml)] if q.key not in optional]
+                        rate_walls = [phase_wall[q.key] for q in phases if q.rate is not None and q.key in phase_wall]
+                        per_window = sum(rate_walls) / len(rate_walls) if rate_walls else 3.0
+                        est += len(between) * per_window + per_step * (ml.warmup + ml.steps) * 6
                 over = d.max_scalar(time.monotonic() - t_run + est) > args.time_budget_s
-                if over or (p.key == "ml" and "rl" in skipped):  # the write-latency pair goes together
+                if p.key == "ml":  # the write-latency pair goes together (decided at rl)
+                    over = "rl" in skipped
+                if over:
                     skipped.append(p.key)
                     continue
             if d.rank == 0:
@@ -1446,7 +1458,7 @@ def main(argv=None):
                     help="kube-lite storage commit latency of the write-latency arms (0 = no such arms)")
     ap.add_argument("--arm-steps", type=int, default=5, help="timed steps of each write-latency arm")
     ap.add_argument("--arm-warmup", type=int, default=1, help="warmup steps of each write-latency arm")
-    ap.add_argument("--time-budget-s", type=float, default=50.0,
+    ap.add_argument("--time-budget-s", type=float, default=54.0,
                     help="wall seconds of the run after which the secondary phases (write-latency arms, tuned, "
                          "HTTP/1.1 webhook) are skipped (listed in skipped_phases); 0 = no budget")
     ap.add_argument("--latency-rates", default="2000,6000",
