@@ -1,6 +1,7 @@
 #!/usr/bin/env bash
 # Round-end rehearsal on a 1-GPU MI355X box (run through gpurun from the repo root):
-#   pytest -m gpu, smoke(), BENCH_RUNS default bench.py runs (default 1), rocprofv3 kernel
+#   pytest -m gpu, smoke(), BENCH_RUNS default bench.py runs (default 1; extra flags in
+#   BENCH_ARGS, e.g. --report-cpu), rocprofv3 kernel
 #   stats of smoke().  Every GPU step has its own time limit and the steps are chained with
 #   &&, so the first failure ends the call.  Output lands in gpurun_out/${OUT_NAME:-rehearsal}/.
 set -o pipefail
@@ -11,7 +12,8 @@ export TMPDIR=/tmp
 bench_runs() {
   for i in $(seq 1 "$RUNS"); do
     s=$(date +%s)
-    timeout -k 10 420 python -u bench.py > "$OUT/bench_$i.json" 2> "$OUT/bench_$i.err" || return $?
+    # shellcheck disable=SC2086
+    timeout -k 10 420 python -u bench.py ${BENCH_ARGS:-} > "$OUT/bench_$i.json" 2> "$OUT/bench_$i.err" || return $?
     echo "bench_$i run_s=$(( $(date +%s) - s ))" >> "$OUT/timing.txt"
   done
 }
