@@ -37,10 +37,19 @@ constexpr size_t kMallocBytes = 32 << 10;
 std::once_flag g_once;
 std::atomic<bool> g_running{false};
 std::atomic<uint64_t> g_ticks{0};
-std::mutex g_mu;
-std::string g_process;
-std::vector<Stall> g_kept;
-uint64_t g_dropped = 0;
+
+// Never destroyed: the sampler thread is detached and still runs while static destructors
+// run at exit (a ThreadSanitizer race on a global vector, tools/sanitize.sh tsan).
+struct State {
+  std::mutex mu;
+  std::string process;
+  std::vector<Stall> kept;
+  uint64_t dropped = 0;
+};
+State& state() {
+  static State* s = new State();
+  return *s;
+}
 
 std::vector<double> stall_buckets() {
   return {50e-6, 100e-6, 200e-6, 500e-6, 1e-3, 2e-3, 5e-3, 10e-3, 20e-3, 50e-3, 100e-3, 500e-3, 1.0};
@@ -79,9 +88,10 @@ void loop() {
     const int64_t runq = runq0 >= 0 && runq1 >= 0 ? runq1 - runq0 : -1;
     runq0 = runq1;
     if (over >= record_ns || mal >= record_ns) {
-      std::lock_guard<std::mutex> lk(g_mu);
-      if (g_kept.size() < kMaxKept) g_kept.push_back({t2, over, runq, mal});
-      else ++g_dropped;
+      State& st = state();
+      std::lock_guard<std::mutex> lk(st.mu);
+      if (st.kept.size() < kMaxKept) st.kept.push_back({t2, over, runq, mal});
+      else ++st.dropped;
     }
   }
 }
@@ -93,8 +103,9 @@ void start(const std::string& name) {
   if (e && std::strcmp(e, "0") == 0) return;
   std::call_once(g_once, [&] {
     {
-      std::lock_guard<std::mutex> lk(g_mu);
-      g_process = name;
+      State& st = state();
+      std::lock_guard<std::mutex> lk(st.mu);
+      st.process = name;
     }
     g_running.store(true);
     std::thread(loop).detach();
@@ -107,14 +118,15 @@ std::string dump_json(bool take) {
   std::vector<Stall> kept;
   json::Value out = json::Value::object();
   {
-    std::lock_guard<std::mutex> lk(g_mu);
-    out["process"] = g_process;
-    out["dropped"] = static_cast<unsigned long long>(g_dropped);
+    State& st = state();
+    std::lock_guard<std::mutex> lk(st.mu);
+    out["process"] = st.process;
+    out["dropped"] = static_cast<unsigned long long>(st.dropped);
     if (take) {
-      kept.swap(g_kept);
-      g_dropped = 0;
+      kept.swap(st.kept);
+      st.dropped = 0;
     } else {
-      kept = g_kept;
+      kept = st.kept;
     }
   }
   out["running"] = running();

@@ -39,16 +39,24 @@ struct ThreadBuf {
 std::atomic<const Config*> g_config{nullptr};  // null: disarmed
 std::atomic<size_t> g_count{0};                // marks kept since arm()
 std::atomic<uint64_t> g_dropped{0};
-std::mutex g_reg_mu;  // g_bufs and g_retired
-std::vector<std::shared_ptr<ThreadBuf>> g_bufs;
-std::vector<std::unique_ptr<const Config>> g_retired;
-std::string g_last_prefix;  // g_reg_mu
+
+// Never destroyed: threads that mark may outlive static destruction at exit.
+struct Registry {
+  std::mutex mu;  // everything below
+  std::vector<std::shared_ptr<ThreadBuf>> bufs;
+  std::vector<std::unique_ptr<const Config>> retired;
+  std::string last_prefix;
+};
+Registry& reg() {
+  static Registry* r = new Registry();
+  return *r;
+}
 
 ThreadBuf& thread_buf() {
   thread_local std::shared_ptr<ThreadBuf> buf = [] {
     auto b = std::make_shared<ThreadBuf>();
-    std::lock_guard<std::mutex> lk(g_reg_mu);
-    g_bufs.push_back(b);
+    std::lock_guard<std::mutex> lk(reg().mu);
+    reg().bufs.push_back(b);
     return b;
   }();
   return *buf;
@@ -90,18 +98,19 @@ void arm(const std::string& prefix, size_t capacity) {
     start = comma + 1;
   }
   c->capacity = capacity;
-  std::lock_guard<std::mutex> lk(g_reg_mu);
+  Registry& r = reg();
+  std::lock_guard<std::mutex> lk(r.mu);
   g_config.store(nullptr, std::memory_order_release);
-  for (auto& b : g_bufs) {
+  for (auto& b : r.bufs) {
     std::lock_guard<std::mutex> bl(b->mu);
     b->marks.clear();
   }
   g_count.store(0);
   g_dropped.store(0);
-  g_last_prefix = prefix;
+  r.last_prefix = prefix;
   if (!c->prefixes.empty()) {
     g_config.store(c.get(), std::memory_order_release);
-    g_retired.push_back(std::move(c));
+    r.retired.push_back(std::move(c));
   }
 }
 
@@ -111,12 +120,13 @@ std::string dump_json(bool take) {
   std::vector<Mark> marks;
   json::Value out = json::Value::object();
   {
-    std::lock_guard<std::mutex> lk(g_reg_mu);
-    out["prefix"] = g_last_prefix;
+    Registry& r = reg();
+    std::lock_guard<std::mutex> lk(r.mu);
+    out["prefix"] = r.last_prefix;
     out["armed"] = armed();
     if (take) g_config.store(nullptr, std::memory_order_release);
     out["dropped"] = static_cast<unsigned long long>(g_dropped.load());
-    for (auto& b : g_bufs) {
+    for (auto& b : r.bufs) {
       std::lock_guard<std::mutex> bl(b->mu);
       if (take) {
         for (auto& m : b->marks) marks.push_back(std::move(m));
@@ -129,10 +139,10 @@ std::string dump_json(bool take) {
     if (take) {
       // buffers of threads that have exited (only this list still holds them)
       std::vector<std::shared_ptr<ThreadBuf>> live;
-      for (auto& b : g_bufs) {
+      for (auto& b : r.bufs) {
         if (b.use_count() > 1) live.push_back(std::move(b));
       }
-      g_bufs.swap(live);
+      r.bufs.swap(live);
       g_dropped.store(0);
       g_count.store(0);
     }
