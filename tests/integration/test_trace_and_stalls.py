@@ -65,7 +65,12 @@ def test_every_service_runs_a_stall_sampler_and_names_its_threads():
             st = requests.get(base + "/debug/stalls", timeout=5, verify=verify).json()
             assert st["running"] is True and st["ticks"] > 0, (proc, st)
             pid = c.procs[proc].p.pid
-            names = {open(f"/proc/{pid}/task/{t}/comm").read().strip() for t in os.listdir(f"/proc/{pid}/task")}
+            names = set()
+            for t in os.listdir(f"/proc/{pid}/task"):
+                try:
+                    names.add(open(f"/proc/{pid}/task/{t}/comm").read().strip())
+                except OSError:
+                    pass  # the thread exited meanwhile
             assert "stall-sampler" in names, (proc, names)
             if proc == "controller":
                 assert {"reconcile", "w:userbootstrap"} <= names, names
