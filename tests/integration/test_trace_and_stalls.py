@@ -65,15 +65,19 @@ def test_every_service_runs_a_stall_sampler_and_names_its_threads():
             st = requests.get(base + "/debug/stalls", timeout=5, verify=verify).json()
             assert st["running"] is True and st["ticks"] > 0, (proc, st)
             pid = c.procs[proc].p.pid
-            names = set()
-            for t in os.listdir(f"/proc/{pid}/task"):
-                try:
-                    names.add(open(f"/proc/{pid}/task/{t}/comm").read().strip())
-                except OSError:
-                    pass  # the thread exited meanwhile
-            assert "stall-sampler" in names, (proc, names)
-            if proc == "controller":
-                assert {"reconcile", "w:userbootstrap"} <= names, names
+
+            def names():
+                out = set()
+                for t in os.listdir(f"/proc/{pid}/task"):
+                    try:
+                        out.add(open(f"/proc/{pid}/task/{t}/comm").read().strip())
+                    except OSError:
+                        pass  # the thread exited meanwhile
+                return out
+
+            want = {"stall-sampler"} | ({"reconcile", "w:userbootstrap"} if proc == "controller" else set())
+            # the controller starts its workers once its caches synced (slow on a sanitizer build)
+            wait_for(lambda: want <= names(), timeout=30, desc=f"{proc} thread names {want}")
 
 
 def test_die_with_parent_naming_another_pid_fails_loudly():
