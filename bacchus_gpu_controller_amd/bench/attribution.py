@@ -20,8 +20,9 @@ Each milestone is the first mark of its stage at or after the previous milestone
 with no mark is skipped and its time falls into the next segment), so the segments of a
 tenant add up exactly to its apply->Ready latency.  A window reports each segment's p50
 and p99, and for its tail tenants (apply->Ready above max(p99, --tail-ms)) which segment
-took the longest and which process's stall sampler (native/core/stall.h) reported a
-stall overlapping it.
+took the longest, which process's stall sampler (native/core/stall.h) reported a
+stall overlapping it, and which thread's slow section (a watch event's handling, a watch
+write or reconnect: stall::note_slow) overlapped it.
 
 Reference: /root/reference/src/controller.rs:81-154 (the reconcile round trips being
 compared), src/synchronizer.rs:289-330 (the status and quota writes).
@@ -41,6 +42,7 @@ _CREATE = [
 ]
 _SYNC = [
     ("sync_watch_sent", r"kl\.watch\.userbootstraps\.synchronizer\.sent"),
+    ("sync_watch_written", r"kl\.watch\.userbootstraps\.synchronizer\.written"),
     ("sync_event", r"sync\.ub_event"),
     ("sync_dequeue", r"sync\.dequeue"),
     ("quota_send", r"sync\.quota\.send"),
@@ -58,12 +60,15 @@ _STATUS = [
 def _ctl(child):
     return [
         ("ctl_watch_sent", r"kl\.watch\.userbootstraps\.controller\.sent"),
+        ("ctl_watch_written", r"kl\.watch\.userbootstraps\.controller\.written"),
+        ("ctl_read", r"ctl\.primary_read"),
         ("ctl_event", r"ctl\.primary_event"),
         ("reconcile", r"ctl\.reconcile0"),
         (f"{child}_apply_send", rf"ctl\.apply\.{child}\.send"),
         (f"{child}_kl_recv", rf"kl\.{child}\.PATCH\.[^.]+\.recv"),
         (f"{child}_commit", rf"kl\.{child}\.PATCH\.[^.]+\.commit"),
         (f"{child}_watch_sent", rf"kl\.watch\.{child}\.(?!controller\.|synchronizer\.)[^.]+\.sent"),
+        (f"{child}_watch_written", rf"kl\.watch\.{child}\.(?!controller\.|synchronizer\.)[^.]+\.written"),
     ]
 
 
@@ -142,6 +147,18 @@ def _stall_owner(stalls, t0, t1):
     return owners
 
 
+def _slow_overlap(slow, t0, t1):
+    """{"<process> <section>": longest ms} of the slow sections (stall.h note_slow: a watch
+    event's handling, a watch write or reconnect) overlapping [t0, t1]."""
+    out = {}
+    for proc, recs in slow.items():
+        for t_end, dur_us, what in recs:
+            if t_end - int(dur_us * 1e3) <= t1 and t_end >= t0:
+                k = f"{proc} {what}"
+                out[k] = max(out.get(k, 0.0), round(dur_us / 1e3, 3))
+    return out
+
+
 def analyze(dumps, stall_dumps=(), tail_ms=5.0, detail=None):
     """Segment table of one window.
 
@@ -156,10 +173,12 @@ def analyze(dumps, stall_dumps=(), tail_ms=5.0, detail=None):
     others = [n for n, m in marks.items() if not any(st == "drv.sched" for _, st in m)]
     for n in others:
         del marks[n]
-    stalls = {}
+    stalls, slow = {}, {}
     for d in stall_dumps:
         if d and d.get("stalls") is not None:
             stalls.setdefault(d.get("process") or "?", []).extend(d["stalls"])
+        if d and d.get("slow"):
+            slow.setdefault(d.get("process") or "?", []).extend(d["slow"])
     seg_vals, order = {}, []
     per_tenant = []
     children, why, why_examples = {}, {}, []
@@ -189,7 +208,7 @@ def analyze(dumps, stall_dumps=(), tail_ms=5.0, detail=None):
                             "max_ms": _round(max(seg_vals[k])), "n": len(seg_vals[k])} for k in order}}
     thr = max(_pct(total, 0.99) or 0.0, tail_ms)
     tail = [t for t in per_tenant if t[1] > thr]
-    blame, blame_ms, overlap, examples = {}, {}, {}, []
+    blame, blame_ms, overlap, slow_hits, examples = {}, {}, {}, {}, []
     for name, tot, segs in sorted(tail, key=lambda x: -x[1]):
         key, ta, tb = max(segs, key=lambda s: s[2] - s[1])
         blame[key] = blame.get(key, 0) + 1
@@ -197,12 +216,16 @@ def analyze(dumps, stall_dumps=(), tail_ms=5.0, detail=None):
         owners = _stall_owner(stalls, ta, tb)
         for p in owners:
             overlap[p] = overlap.get(p, 0) + 1
+        sections = _slow_overlap(slow, ta, tb)
+        for k in sections:
+            slow_hits[k] = slow_hits.get(k, 0) + 1
         if len(examples) < 5:
             examples.append({"tenant": name, "total_ms": round(tot, 3), "longest": key,
                              "longest_ms": round((tb - ta) / 1e6, 3),
-                             "stalls_ms": {p: round(v / 1e3, 2) for p, v in owners.items()}})
+                             "stalls_ms": {p: round(v / 1e3, 2) for p, v in owners.items()},
+                             "slow_ms": sections})
     out["tail"] = {"threshold_ms": round(thr, 3), "n": len(tail), "blame": blame, "blame_ms": blame_ms,
-                   "stall_overlap": overlap, "examples": examples}
+                   "stall_overlap": overlap, "slow_overlap": slow_hits, "examples": examples}
     if detail is not None and tail:
         # for offline study (--trace-dump): the worst tail tenants' full timelines, and every
         # mark of every tenant within 10 ms around the worst one's longest segment
@@ -218,6 +241,12 @@ def analyze(dumps, stall_dumps=(), tail_ms=5.0, detail=None):
                              "marks": sorted([t, n, st] for n, m in marks.items() for t, st in m if lo <= t <= hi)}
     out["stalls"] = {p: {"n": len(r), "max_ms": round(max((x[1] + x[3] for x in r), default=0.0) / 1e3, 3),
                          "sum_ms": round(sum(x[1] + x[3] for x in r) / 1e3, 3)} for p, r in stalls.items()}
+    sections = {}
+    for p, recs in slow.items():
+        for _, dur_us, what in recs:
+            n, worst = sections.get(f"{p} {what}", (0, 0.0))
+            sections[f"{p} {what}"] = (n + 1, max(worst, dur_us / 1e3))
+    out["slow_sections"] = {k: {"n": n, "max_ms": round(w, 3)} for k, (n, w) in sorted(sections.items())}
     return out
 
 

@@ -295,9 +295,9 @@ def cpu_ticks(cpus):
 
 
 def thread_cpu(procs):
-    """{(process, thread name): [cpu seconds per thread]} over every thread of `procs`
-    ({process name: pid}), from /proc/<pid>/task/<tid>/stat (comm, utime, stime)."""
-    tck = os.sysconf("SC_CLK_TCK")
+    """{(process, thread name, tid): (cpu seconds, run-queue wait seconds)} over every thread
+    of `procs` ({process name: pid}): the name from /proc/<pid>/task/<tid>/comm, both times
+    from its schedstat (on-CPU ns, runnable-but-waiting ns)."""
     out = {}
     for pname, pid in procs.items():
         try:
@@ -306,13 +306,13 @@ def thread_cpu(procs):
             continue
         for tid in tids:
             try:
-                with open(f"/proc/{pid}/task/{tid}/stat") as f:
-                    raw = f.read()
-                comm = raw[raw.index("(") + 1:raw.rindex(")")]
-                fields = raw.rsplit(")", 1)[1].split()
-                out[(pname, comm, tid)] = (int(fields[11]) + int(fields[12])) / tck
-            except (OSError, ValueError, IndexError):
-                pass
+                with open(f"/proc/{pid}/task/{tid}/comm") as f:
+                    comm = f.read().strip()
+                with open(f"/proc/{pid}/task/{tid}/schedstat") as f:
+                    run, wait = f.read().split()[:2]
+                out[(pname, comm, tid)] = (int(run) / 1e9, int(wait) / 1e9)
+            except (OSError, ValueError):
+                pass  # the thread exited meanwhile
     return out
 
 
@@ -321,11 +321,27 @@ def busiest_threads(t0, t1, dt, top=6):
     one CPU: a single-threaded stage near 1.0 is a pipeline bottleneck (its queue grows)."""
     used = []
     for k, v in t1.items():
-        d = v - t0.get(k, 0.0)
+        d = v[0] - t0.get(k, (0.0, 0.0))[0]
         if d > 0:
             used.append((d / dt, k))
     used.sort(reverse=True)
     return [{"process": k[0], "thread": k[1], "cpu": round(u, 2)} for u, k in used[:top]]
+
+
+def waiting_threads(t0, t1, top=6):
+    """The threads that waited longest for a CPU between two thread_cpu() readings (ms over
+    the window; summed over the threads sharing a name).  A stage whose thread is here while
+    the job's CPUs are not all busy lost its CPU to the scheduler's placement, not to load."""
+    waited = {}
+    for k, v in t1.items():
+        d = v[1] - t0.get(k, (0.0, 0.0))[1]
+        if d > 0:
+            name = (k[0], k[1])
+            n, tot, worst = waited.get(name, (0, 0.0, 0.0))
+            waited[name] = (n + 1, tot + d, max(worst, d))
+    rows = sorted(waited.items(), key=lambda x: -x[1][1])[:top]
+    return [{"process": p, "thread": t, "threads": n, "runq_ms": round(tot * 1e3, 2),
+             "worst_thread_runq_ms": round(worst * 1e3, 2)} for (p, t), (n, tot, worst) in rows]
 
 
 def job_cpu_seconds(pids):
@@ -799,6 +815,7 @@ def _rate_phase(d, nat, info, args, key, rate, cluster):
         out["job_cpus_used"] = round((own1 - own0) / dt, 2)  # of which the job's own processes
         out["foreign_cpus"] = round(max(0.0, busy_s - (own1 - own0)) / dt, 2)
         out["busiest_threads"] = busiest_threads(thr_cpu0, thr_cpu1, dt)
+        out["waiting_threads"] = waiting_threads(thr_cpu0, thr_cpu1)
     if traced:
         detail = {} if args.trace_dump else None
         out["attribution"] = attribution.analyze(traces, stalls, tail_ms=args.tail_ms, detail=detail)
@@ -819,7 +836,7 @@ _WINDOW_KEYS = ("offered_rate", "achieved_rate", "achieved_within_2pct", "reconc
                 "reconciles", "admission_p50_ms", "admission_p99_ms", "admission_handler_p50_ms",
                 "apply_to_ready_p50_ms", "apply_to_ready_p99_ms", "issue_lag_p99_ms", "ready_crs", "failed_crs",
                 "cgroup_throttled_periods", "runqueue_wait_ms_per_s", "cpus_busy", "job_cpus_used", "foreign_cpus",
-                "busiest_threads", "errors")
+                "busiest_threads", "waiting_threads", "errors")
 
 
 def _pool_arm(results, prefix, rates, windows):

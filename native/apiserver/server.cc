@@ -26,6 +26,7 @@
 #include "core/log.h"
 #include "core/metrics.h"
 #include "core/process.h"
+#include "core/stall.h"
 #include "core/trace.h"
 #include "core/net.h"
 #include "core/yaml.h"
@@ -2282,6 +2283,8 @@ struct ApiServer::Impl {
     if (req.has_query_param("timeoutSeconds")) timeout_s = std::min(timeout_s, std::atoi(req.query_param("timeoutSeconds").c_str()));
     bool bookmarks = req.query_param("allowWatchBookmarks") == "true";
     const std::string trace_watch = "kl.watch." + p.ti->rt.plural + "." + field_manager(req, "unknown") + ".sent";
+    const std::string trace_written = trace_watch.substr(0, trace_watch.size() - 4) + "written";
+    const std::string slow_write = "kw:" + p.ti->rt.plural + " write";
     // the serving thread streams this watch from here on: name it for per-thread CPU reports
     set_thread_name("kw:" + p.ti->rt.plural);
     struct Rename {
@@ -2396,10 +2399,17 @@ struct ApiServer::Impl {
       if (!batch.empty()) {
         std::string buf;
         for (auto& q : batch) buf += q.e->line_as(q.view, meta_only);
-        if (trace::armed()) {  // before the write: causally before the watcher's own marks
+        const bool traced = trace::armed();
+        if (traced) {  // before the write: causally before the watcher's own marks
           for (auto& q : batch) trace::mark(q.e->meta->get("metadata").get_string("name"), trace_watch);
         }
+        const int64_t w0 = metrics::now_ns();
         if (!w.write_chunk(buf)) break;
+        const int64_t w1 = metrics::now_ns();
+        stall::note_slow(slow_write, w0, w1);
+        if (traced) {
+          for (auto& q : batch) trace::mark_at(q.e->meta->get("metadata").get_string("name"), trace_written, w1);
+        }
       }
       if (closed || overflow) break;
       auto now = std::chrono::steady_clock::now();

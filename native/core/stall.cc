@@ -5,6 +5,7 @@
 #include <time.h>
 
 #include <atomic>
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -28,6 +29,12 @@ struct Stall {
   int64_t malloc_ns;   // one malloc+free of 32 KiB
 };
 
+struct Slow {
+  int64_t t1_ns;
+  int64_t dur_ns;
+  std::string what;
+};
+
 constexpr int64_t kTickNs = 1000000;
 constexpr size_t kMaxKept = 1 << 16;
 // past the thread cache (tcache_max 16 KiB in the services' tunables), so the malloc takes
@@ -37,6 +44,8 @@ constexpr size_t kMallocBytes = 32 << 10;
 std::once_flag g_once;
 std::atomic<bool> g_running{false};
 std::atomic<uint64_t> g_ticks{0};
+// note_slow's threshold: "never" until start() finds that records are kept
+std::atomic<int64_t> g_slow_ns{INT64_MAX};
 
 // Never destroyed: the sampler thread is detached and still runs while static destructors
 // run at exit (a ThreadSanitizer race on a global vector, tools/sanitize.sh tsan).
@@ -44,6 +53,7 @@ struct State {
   std::mutex mu;
   std::string process;
   std::vector<Stall> kept;
+  std::vector<Slow> slow;
   uint64_t dropped = 0;
 };
 State& state() {
@@ -53,6 +63,11 @@ State& state() {
 
 std::vector<double> stall_buckets() {
   return {50e-6, 100e-6, 200e-6, 500e-6, 1e-3, 2e-3, 5e-3, 10e-3, 20e-3, 50e-3, 100e-3, 500e-3, 1.0};
+}
+
+int64_t record_threshold_ns() {
+  const char* rec = std::getenv("BGC_STALL_RECORD_US");
+  return (rec ? std::atoll(rec) : 2000) * 1000;
 }
 
 void loop() {
@@ -66,8 +81,7 @@ void loop() {
                                {}, stall_buckets());
   auto& malloc_h = reg.histogram("bgc_stall_malloc_seconds", "One 32 KiB malloc+free of the stall sampler (an arena lock)", {},
                                  stall_buckets());
-  const char* rec = std::getenv("BGC_STALL_RECORD_US");
-  const int64_t record_ns = (rec ? std::atoll(rec) : 2000) * 1000;
+  const int64_t record_ns = record_threshold_ns();
   const bool keep = metrics::debug_endpoints_enabled();
   struct timespec req {0, kTickNs};
   int64_t runq0 = keep ? sched::thread_sched().runq_ns : -1;
@@ -108,14 +122,24 @@ void start(const std::string& name) {
       st.process = name;
     }
     g_running.store(true);
+    if (metrics::debug_endpoints_enabled()) g_slow_ns.store(record_threshold_ns());
     std::thread(loop).detach();
   });
 }
 
 bool running() { return g_running.load(); }
 
+void note_slow(std::string_view what, int64_t t0_ns, int64_t t1_ns) {
+  if (t1_ns - t0_ns < g_slow_ns.load(std::memory_order_relaxed)) return;
+  State& st = state();
+  std::lock_guard<std::mutex> lk(st.mu);
+  if (st.slow.size() < kMaxKept) st.slow.push_back({t1_ns, t1_ns - t0_ns, std::string(what)});
+  else ++st.dropped;
+}
+
 std::string dump_json(bool take) {
   std::vector<Stall> kept;
+  std::vector<Slow> slow;
   json::Value out = json::Value::object();
   {
     State& st = state();
@@ -124,9 +148,11 @@ std::string dump_json(bool take) {
     out["dropped"] = static_cast<unsigned long long>(st.dropped);
     if (take) {
       kept.swap(st.kept);
+      slow.swap(st.slow);
       st.dropped = 0;
     } else {
       kept = st.kept;
+      slow = st.slow;
     }
   }
   out["running"] = running();
@@ -141,6 +167,15 @@ std::string dump_json(bool take) {
     arr.push_back(std::move(e));
   }
   out["stalls"] = std::move(arr);
+  json::Value sl = json::Value::array();
+  for (auto& s : slow) {
+    json::Value e = json::Value::array();
+    e.push_back(static_cast<long long>(s.t1_ns));
+    e.push_back(static_cast<double>(s.dur_ns) * 1e-3);
+    e.push_back(std::move(s.what));
+    sl.push_back(std::move(e));
+  }
+  out["slow"] = std::move(sl);
   return out.dump();
 }
 

@@ -16,6 +16,7 @@
 
 #include <cstdint>
 #include <string>
+#include <string_view>
 
 namespace bgc::stall {
 
@@ -23,8 +24,13 @@ namespace bgc::stall {
 // the dump.
 void start(const std::string& name);
 bool running();
+// One thread's section of work [t0_ns, t1_ns] (monotonic) that may have held up what queued
+// behind it: a watch event's handling, a watch write, a watch reconnect.  Kept beside the
+// stalls when it lasted >= BGC_STALL_RECORD_US and the sampler keeps records (debug
+// endpoints on); otherwise one relaxed load and a return.
+void note_slow(std::string_view what, int64_t t0_ns, int64_t t1_ns);
 // {"process":..,"ticks":n,"stalls":[[t_ns, oversleep_us, runq_us, malloc_us],...],
-//  "dropped":n}; `take` clears the kept stalls.
+//  "slow":[[t1_ns, duration_us, what],...], "dropped":n}; `take` clears what was kept.
 std::string dump_json(bool take);
 
 }  // namespace bgc::stall

@@ -5,6 +5,7 @@
 #include "core/http.h"
 #include "core/log.h"
 #include "core/metrics.h"
+#include "core/stall.h"
 #include "core/trace.h"
 #include "core/net.h"
 #include "core/process.h"
@@ -198,6 +199,9 @@ void Watcher::run(CancelToken& stop, const std::function<void(const WatchEvent&)
     ~SlotGuard() { close_slot(s); }
   } slot_guard{slot};
   auto alive = [&] { slot->last_ns.store(metrics::now_ns(), std::memory_order_relaxed); };
+  // sections of this thread that hold up the events queued behind them (stall::note_slow)
+  const std::string slow_event = "w:" + rt_.plural + " event", slow_reopen = "w:" + rt_.plural + " reopen";
+  int64_t down_ns = 0;  // when the previous stream ended
   while (!stop.cancelled()) {
     // Streaming list: the initial state arrives on this watch; objects collect here until
     // the initial-events-end bookmark.
@@ -245,10 +249,13 @@ void Watcher::run(CancelToken& stop, const std::function<void(const WatchEvent&)
       backoff = std::chrono::milliseconds(800);
       if (idle_timeout_ms_ > 0) stream->set_idle_timeout(static_cast<int>(idle_timeout_ms_));
       alive();
+      if (down_ns) stall::note_slow(slow_reopen, down_ns, metrics::now_ns());
+      down_ns = 0;
       int64_t last_bookmark_ns = 0;
       std::string line;
       while (stream->next_line(line, &stop, 500)) {
-        alive();
+        const int64_t read_ns = metrics::now_ns();
+        slot->last_ns.store(read_ns, std::memory_order_relaxed);
         if (line.empty()) continue;
         // Events the consumer does not want are dropped before JSON parsing; ERROR and
         // BOOKMARK lines always go through (they drive relists and resumption).  During
@@ -300,13 +307,16 @@ void Watcher::run(CancelToken& stop, const std::function<void(const WatchEvent&)
           continue;
         }
         WatchEvent we{WatchEvent::Type::Added,
-                      metadata_only_ ? typed(std::move(obj)) : std::make_shared<const Value>(std::move(obj)), {}};
+                      metadata_only_ ? typed(std::move(obj)) : std::make_shared<const Value>(std::move(obj)), {},
+                      read_ns};
         if (type == "MODIFIED") we.type = WatchEvent::Type::Modified;
         else if (type == "DELETED") we.type = WatchEvent::Type::Deleted;
         else if (type != "ADDED") continue;
         on_event(we);
+        stall::note_slow(slow_event, read_ns, metrics::now_ns());
       }
       stream->close();
+      down_ns = metrics::now_ns();
       if (stream->idle_timed_out() && !stop.cancelled()) {
         // Nothing arrived for the whole deadline, not even a bookmark: the connection (or the
         // path to the apiserver) is presumed dead.  Pooled request connections share that
@@ -320,6 +330,7 @@ void Watcher::run(CancelToken& stop, const std::function<void(const WatchEvent&)
       if (!stop.cancelled()) reconnects_.fetch_add(1);
     } catch (const ApiError& e) {
       errors.inc();
+      if (!down_ns) down_ns = metrics::now_ns();
       if (e.code() == 410) {
         need_list = true;
         continue;
@@ -330,6 +341,7 @@ void Watcher::run(CancelToken& stop, const std::function<void(const WatchEvent&)
       need_list = true;
     } catch (const std::exception& e) {
       errors.inc();
+      if (!down_ns) down_ns = metrics::now_ns();
       LOG_WARN("kube::watcher") << rt_.plural << ": " << e.what() << " (retry in " << backoff.count() << "ms)";
       if (stop.wait_for(backoff)) break;
       backoff = std::min(backoff * 2, max_backoff);
@@ -590,7 +602,9 @@ void Controller::run(CancelToken& stop, Reconciler reconcile, ErrorPolicy error_
     w.run(stop, [&](const WatchEvent& ev) {
       // marked before the store applies it: a worker may reconcile from the store at once
       if (trace::armed() && ev.object && ev.type != WatchEvent::Type::Deleted) {
-        trace::mark(meta_name(*ev.object), "ctl.primary_event");
+        const std::string name = meta_name(*ev.object);
+        trace::mark_at(name, "ctl.primary_read", ev.read_ns);
+        trace::mark(name, "ctl.primary_event");
       }
       primary_store_->apply(ev);
       primary_gauge.set(static_cast<double>(primary_store_->size()));

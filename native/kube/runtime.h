@@ -42,6 +42,7 @@ struct WatchEvent {
   Type type;
   ObjPtr object;                 // Added/Modified/Deleted
   std::vector<ObjPtr> objects;   // Restarted (full relist)
+  int64_t read_ns = 0;           // when its line came off the watch stream (monotonic)
 };
 
 std::string meta_name(const json::Value& obj);

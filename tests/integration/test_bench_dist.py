@@ -53,6 +53,11 @@ def test_bench_two_ranks_gloo():
     # both ranks' tenants are traced through every process and attributed
     for att in d["latency_at_rate"]["attribution"]["this"]["200"]:
         assert att["attributed"] == 200 and att["trace_dropped"] == 0
+        # the watch legs split at kube-lite's write and the controller's read
+        assert {"ctl_watch_sent->ctl_watch_written", "ctl_read->ctl_event"} <= set(att["segments"]), att["segments"]
+        assert "slow_sections" in att
+    for w in q["windows"]:  # per-thread CPU and run-queue wait of the window
+        assert w["busiest_threads"] and all("runq_ms" in t for t in w["waiting_threads"])
     assert "reference_controller" not in d["latency_at_rate"] and "product_isolated" not in d  # N>1: no isolation
 
 

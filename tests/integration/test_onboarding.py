@@ -218,6 +218,13 @@ def test_debounce_merges_a_burst_of_events_into_one_reconcile():
     # in round 6, with every service's stall sampler instrumented too)
     window = "6000" if os.environ.get("BGC_BIN_DIR") else "1500"
     with Cluster(admission=False, controller_env={"CONF_DEBOUNCE_MS": window, "CONF_REQUEUE_SECS": "3600"}) as c:
+        # writes made before the controller's first list reach it through that list, which
+        # queues without the debounce (a slow ASan start-up, round 6): wait until it watches
+        def watching():
+            r = requests.get(f"http://127.0.0.1:{c.controller_port}/readyz", timeout=5)
+            return r.status_code == 200 and "[+]watches ok" in r.text  # a watcher has listed
+
+        wait_for(watching, timeout=30, desc="controller watching")
         c.admin.create("userbootstraps", {"apiVersion": "bacchus.io/v1", "kind": "UserBootstrap",
                                           "metadata": {"name": "burst"}, "spec": {"kube_username": "burst"}})
         for gpus in ("1", "2", "3"):

@@ -54,6 +54,37 @@ def test_trace_marks_follow_a_tenant_through_every_process():
         assert again["marks"] == [] and again["armed"] is False
 
 
+def test_watch_sections_are_timed_on_both_ends(monkeypatch):
+    """A watch event's delay splits into kube-lite's write (sent -> written), the transport
+    and the reader (written -> the controller's read) and the parse (read -> event); the
+    watch writer's and the watcher's own sections are kept as slow sections past
+    BGC_STALL_RECORD_US (0 here: every one)."""
+    monkeypatch.setenv("BGC_STALL_RECORD_US", "0")
+    with Cluster(admission=False) as c:
+        ctl = f"http://127.0.0.1:{c.controller_port}"
+        ends = [(c.server, c.verify), (ctl, None)]
+        for base, verify in ends:
+            assert requests.post(base + "/debug/trace", data="ws-", timeout=5, verify=verify).status_code == 200
+            requests.delete(base + "/debug/stalls", timeout=5, verify=verify)
+        _tenant(c, "ws-bob")
+        wait_for(lambda: c.admin.get_or_none("namespaces", "ws-bob"), desc="namespace")
+        dumps = [requests.delete(base + "/debug/trace", timeout=5, verify=verify).json() for base, verify in ends]
+        t = {}
+        for ts, st in attribution.group_marks(dumps)["ws-bob"]:
+            t.setdefault(st, ts)
+        sent, written = "kl.watch.userbootstraps.controller.sent", "kl.watch.userbootstraps.controller.written"
+        assert t[sent] <= t[written] <= t["ctl.primary_read"] <= t["ctl.primary_event"], t
+        slow = {base: requests.get(base + "/debug/stalls", timeout=5, verify=verify).json()["slow"]
+                for base, verify in ends}
+        assert any(what == "kw:userbootstraps write" for _, _, what in slow[c.server]), slow[c.server][:5]
+        assert any(what == "w:userbootstraps event" for _, _, what in slow[ctl]), slow[ctl][:5]
+        # and the bench's attribution reads them as sections overlapping a segment
+        stall_dumps = [dict(requests.get(base + "/debug/stalls", timeout=5, verify=verify).json(), process=p)
+                       for (base, verify), p in zip(ends, ("kube-lite", "controller"))]
+        got = attribution.analyze(dumps, stall_dumps)
+        assert "controller w:userbootstraps event" in got["slow_sections"], got["slow_sections"]
+
+
 def test_every_service_runs_a_stall_sampler_and_names_its_threads():
     with Cluster() as c:
         for base, verify, proc in ((f"http://127.0.0.1:{c.controller_port}", None, "controller"),

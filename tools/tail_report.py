@@ -3,7 +3,8 @@
 
 For every run and every window of each arm: apply->Ready p99, reconcile p99, the job's own
 CPU use and other tenants' CPU use on the job's CPU set, and (when traced) the segment the
-window's tail tenants spent the longest in.  Ends with the count of windows over --limit-ms
+window's tail tenants spent the longest in, the slow section (stall::note_slow) most of
+them overlapped, and for a window over the limit the thread that waited longest for a CPU.  Ends with the count of windows over --limit-ms
 per arm.
 
   python3 tools/tail_report.py gpurun_out/r6_tg*.json [--limit-ms 5] [--json out.json]
@@ -20,14 +21,18 @@ def rows(path):
         for rate, v in (q.get(arm) or {}).items():
             for k, w in enumerate(v.get("windows", [])):
                 a = (att.get(arm, {}).get(rate) or [None] * 8)[k] if att else None
-                blame = None
+                blame = slow = None
                 if a and a["tail"]["blame"]:
                     blame = max(a["tail"]["blame"].items(), key=lambda kv: kv[1])[0]
+                if a and a["tail"].get("slow_overlap"):
+                    slow = max(a["tail"]["slow_overlap"].items(), key=lambda kv: kv[1])[0]
+                wt = (w.get("waiting_threads") or [None])[0]
                 yield {"run": path, "value": d.get("value"), "arm": arm, "rate": rate, "window": k,
                        "a2r_p99_ms": w.get("apply_to_ready_p99_ms"), "reconcile_p99_ms": w.get("reconcile_p99_ms"),
                        "admission_p50_ms": w.get("admission_p50_ms"), "job_cpus": w.get("job_cpus_used"),
                        "foreign_cpus": w.get("foreign_cpus"), "runq_ms_per_s": w.get("runqueue_wait_ms_per_s"),
-                       "tail_blame": blame}
+                       "tail_blame": blame, "tail_slow_section": slow,
+                       "most_runq": f"{wt['process']}/{wt['thread']} {wt['runq_ms']}ms" if wt else None}
 
 
 def main():
@@ -37,11 +42,13 @@ def main():
     ap.add_argument("--json", default="")
     a = ap.parse_args()
     all_rows = [r for f in a.files for r in rows(f)]
-    print(f"{'run':34s} {'arm':5s} {'rate':>5s} w  {'a2r99':>6s} {'rec99':>6s} {'job':>5s} {'foreign':>7s}  tail blame")
+    print(f"{'run':34s} {'arm':5s} {'rate':>5s} w  {'a2r99':>6s} {'rec99':>6s} {'job':>5s} {'foreign':>7s}  tail blame [slow section] (thread with most run-queue wait)")
     for r in all_rows:
         print(f"{r['run'][-34:]:34s} {r['arm'][:5]:5s} {r['rate']:>5s} {r['window']}  {r['a2r_p99_ms'] or 0:6.2f} "
               f"{r['reconcile_p99_ms'] or 0:6.3f} {r['job_cpus'] if r['job_cpus'] is not None else '':>5} "
-              f"{r['foreign_cpus'] if r['foreign_cpus'] is not None else '':>7}  {r['tail_blame'] or ''}")
+              f"{r['foreign_cpus'] if r['foreign_cpus'] is not None else '':>7}  {r['tail_blame'] or ''}"
+              + (f" [{r['tail_slow_section']}]" if r["tail_slow_section"] else "")
+              + (f" ({r['most_runq']})" if r["most_runq"] and (r["a2r_p99_ms"] or 0) > a.limit_ms else ""))
     summary = {}
     for arm in ("this", "reference_controller"):
         ws = [r for r in all_rows if r["arm"] == arm]
