@@ -278,8 +278,9 @@ def runqueue_wait_ms(pids):
 
 
 def cpu_ticks(cpus):
-    """(busy, total) jiffies summed over `cpus` (/proc/stat), for the job's CPU share."""
-    busy = total = 0
+    """(busy, total, steal) jiffies summed over `cpus` (/proc/stat), for the job's CPU share.
+    steal: time the hypervisor ran something else while these (virtual) CPUs had work."""
+    busy = total = steal = 0
     try:
         with open("/proc/stat") as f:
             for line in f:
@@ -289,9 +290,10 @@ def cpu_ticks(cpus):
                         v = [int(x) for x in p[1:]]
                         total += sum(v[:8])
                         busy += sum(v[:8]) - v[3] - (v[4] if len(v) > 4 else 0)
+                        steal += v[7] if len(v) > 7 else 0
     except (OSError, ValueError):
         pass
-    return busy, total
+    return busy, total, steal
 
 
 def thread_cpu(procs):
@@ -814,6 +816,7 @@ def _rate_phase(d, nat, info, args, key, rate, cluster):
         out["cpus_busy"] = round(busy_s / dt, 2)           # CPUs' worth busy on the job's CPU set
         out["job_cpus_used"] = round((own1 - own0) / dt, 2)  # of which the job's own processes
         out["foreign_cpus"] = round(max(0.0, busy_s - (own1 - own0)) / dt, 2)
+        out["steal_cpus"] = round((tick1[2] - tick0[2]) / hz / dt, 3)  # of which the hypervisor's
         out["busiest_threads"] = busiest_threads(thr_cpu0, thr_cpu1, dt)
         out["waiting_threads"] = waiting_threads(thr_cpu0, thr_cpu1)
     if traced:
@@ -835,7 +838,7 @@ def _rate_phase(d, nat, info, args, key, rate, cluster):
 _WINDOW_KEYS = ("offered_rate", "achieved_rate", "achieved_within_2pct", "reconcile_p99_ms", "reconcile_p50_ms",
                 "reconciles", "admission_p50_ms", "admission_p99_ms", "admission_handler_p50_ms",
                 "apply_to_ready_p50_ms", "apply_to_ready_p99_ms", "issue_lag_p99_ms", "ready_crs", "failed_crs",
-                "cgroup_throttled_periods", "runqueue_wait_ms_per_s", "cpus_busy", "job_cpus_used", "foreign_cpus",
+                "cgroup_throttled_periods", "runqueue_wait_ms_per_s", "cpus_busy", "job_cpus_used", "foreign_cpus", "steal_cpus",
                 "busiest_threads", "waiting_threads", "errors")
 
 

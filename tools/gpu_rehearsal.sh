@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # Round-end rehearsal on a 1-GPU MI355X box (run through gpurun from the repo root):
 #   pytest -m gpu, smoke(), BENCH_RUNS default bench.py runs (default 1; extra flags in
-#   BENCH_ARGS, e.g. --report-cpu), rocprofv3 kernel
+#   BENCH_ARGS, e.g. --report-cpu; BENCH_ONLY=1: just those), rocprofv3 kernel
 #   stats of smoke().  Every GPU step has its own time limit and the steps are chained with
 #   &&, so the first failure ends the call.  Output lands in gpurun_out/${OUT_NAME:-rehearsal}/.
 set -o pipefail
@@ -17,6 +17,12 @@ bench_runs() {
     echo "bench_$i run_s=$(( $(date +%s) - s ))" >> "$OUT/timing.txt"
   done
 }
+if [ -n "${BENCH_ONLY:-}" ]; then  # only the bench runs (a tail study): no tests, no profile
+  bench_runs
+  rc=$?
+  cat "$OUT/timing.txt" 2>/dev/null
+  exit $rc
+fi
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
     > "$OUT/pytest_gpu.log" 2>&1 &&
 timeout -k 10 240 python -u -c 'import __graft_entry__ as g; g.smoke()' > "$OUT/smoke.log" 2>&1 &&
