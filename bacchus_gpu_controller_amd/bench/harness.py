@@ -318,6 +318,20 @@ def thread_cpu(procs):
     return out
 
 
+def llc_groups(cpus):
+    """The CPUs of `cpus` grouped by the last-level cache they share (sysfs cache index3),
+    as cpulist strings; [] when the topology is not readable."""
+    groups = {}
+    for c in cpus:
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list") as f:
+                key = f.read().strip()
+        except OSError:
+            return []
+        groups.setdefault(key, []).append(c)
+    return [_cpulist_text(set(v)) for v in sorted(groups.values())]
+
+
 def busiest_threads(t0, t1, dt, top=6):
     """The threads that used the most CPU between two thread_cpu() readings, as share of
     one CPU: a single-threaded stage near 1.0 is a pipeline bottleneck (its queue grows)."""
@@ -341,7 +355,9 @@ def waiting_threads(t0, t1, top=6):
             name = (k[0], k[1])
             n, tot, worst = waited.get(name, (0, 0.0, 0.0))
             waited[name] = (n + 1, tot + d, max(worst, d))
-    rows = sorted(waited.items(), key=lambda x: -x[1][1])[:top]
+    ranked = sorted(waited.items(), key=lambda x: -x[1][1])
+    # plus every watch reader (w:<resource>): one thread each, on every tenant's critical path
+    rows = ranked[:top] + [r for r in ranked[top:] if r[0][1].startswith("w:")]
     return [{"process": p, "thread": t, "threads": n, "runq_ms": round(tot * 1e3, 2),
              "worst_thread_runq_ms": round(worst * 1e3, 2)} for (p, t), (n, tot, worst) in rows]
 
@@ -1315,7 +1331,10 @@ def run(args):
                        # (kube-lite name-prefix field selector); the product is unaffected
                        "driver_server_filter": args.driver_server_filter,
                        # CPUs the job was pinned to (quota_cpuset), or null when not pinned
-                       "cpuset": _cpulist_text(cpuset) if cpuset else None},
+                       "cpuset": _cpulist_text(cpuset) if cpuset else None,
+                       # the job's CPUs grouped by shared L3: the scheduler places a woken
+                       # thread within its waker's group first
+                       "cpu_llc_groups": llc_groups(sorted(os.sched_getaffinity(0)))},
         }
         out.update(main_r)
         if "t" in results:

@@ -1,0 +1,7 @@
+set -o pipefail
+OUT=gpurun_out/r6_drvthreads; mkdir -p $OUT
+for i in 1 2 3 4; do
+  timeout -k 10 300 python -u bench.py > $OUT/def_$i.json 2> $OUT/def_$i.err || exit $?
+  timeout -k 10 300 python -u bench.py --latency-workers 24 > $OUT/w24_$i.json 2> $OUT/w24_$i.err || exit $?
+  echo "pair $i done"
+done
