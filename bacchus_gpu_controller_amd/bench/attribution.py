@@ -42,7 +42,6 @@ _CREATE = [
 ]
 _SYNC = [
     ("sync_watch_sent", r"kl\.watch\.userbootstraps\.synchronizer\.sent"),
-    ("sync_watch_written", r"kl\.watch\.userbootstraps\.synchronizer\.written"),
     ("sync_event", r"sync\.ub_event"),
     ("sync_dequeue", r"sync\.dequeue"),
     ("quota_send", r"sync\.quota\.send"),
@@ -60,7 +59,6 @@ _STATUS = [
 def _ctl(child):
     return [
         ("ctl_watch_sent", r"kl\.watch\.userbootstraps\.controller\.sent"),
-        ("ctl_watch_written", r"kl\.watch\.userbootstraps\.controller\.written"),
         ("ctl_read", r"ctl\.primary_read"),
         ("ctl_event", r"ctl\.primary_event"),
         ("reconcile", r"ctl\.reconcile0"),
@@ -68,7 +66,6 @@ def _ctl(child):
         (f"{child}_kl_recv", rf"kl\.{child}\.PATCH\.[^.]+\.recv"),
         (f"{child}_commit", rf"kl\.{child}\.PATCH\.[^.]+\.commit"),
         (f"{child}_watch_sent", rf"kl\.watch\.{child}\.(?!controller\.|synchronizer\.)[^.]+\.sent"),
-        (f"{child}_watch_written", rf"kl\.watch\.{child}\.(?!controller\.|synchronizer\.)[^.]+\.written"),
     ]
 
 
@@ -77,6 +74,10 @@ CHAINS = {
     "resourcequotas": _CREATE + _SYNC + _ctl("resourcequotas") + [("seen", r"drv\.rq_seen")],
     "rolebindings": _CREATE + _SYNC + _STATUS + _ctl("rolebindings") + [("seen", r"drv\.rb_seen")],
 }
+# kube-lite's ".written" mark (after its write returned) is not on the chain: the reader can
+# read the bytes before the writer's clock is read.  Its distance from ".sent" is kept as a
+# side statistic per watch, the write's own time.
+_WATCH_MARK = re.compile(r"kl\.watch\.([^.]+\.[^.]+)\.(sent|written)$")
 _SEEN = {"namespaces": "drv.ns_seen", "resourcequotas": "drv.rq_seen", "rolebindings": "drv.rb_seen"}
 _COMPILED = {k: [(n, re.compile(p + r"$")) for n, p in v] for k, v in CHAINS.items()}
 
@@ -168,6 +169,18 @@ def analyze(dumps, stall_dumps=(), tail_ms=5.0, detail=None):
                       "stall_overlap": {process: n}, "examples": [...]},
              "stalls": {process: {"n", "max_ms", "sum_ms"}}}"""
     marks = group_marks(dumps)
+    writes = {}  # every traced object's watch writes, tenant or not
+    for m in marks.values():
+        pending = {}
+        for t, st in m:
+            hit = _WATCH_MARK.match(st)
+            if not hit:
+                continue
+            watch, kind = hit.groups()
+            if kind == "sent":
+                pending.setdefault(watch, t)
+            elif watch in pending:
+                writes.setdefault(watch, []).append((t - pending.pop(watch)) / 1e6)
     # tenants are the names the load driver scheduled; other objects sharing the prefix (the
     # controller's Events, named "<tenant>.<suffix>") are not
     others = [n for n, m in marks.items() if not any(st == "drv.sched" for _, st in m)]
@@ -205,7 +218,10 @@ def analyze(dumps, stall_dumps=(), tail_ms=5.0, detail=None):
            "unattributed_examples": why_examples, "critical_child": children,
            "apply_to_ready_p50_ms": _round(_pct(total, 0.5)), "apply_to_ready_p99_ms": _round(_pct(total, 0.99)),
            "segments": {k: {"p50_ms": _round(_pct(seg_vals[k], 0.5)), "p99_ms": _round(_pct(seg_vals[k], 0.99)),
-                            "max_ms": _round(max(seg_vals[k])), "n": len(seg_vals[k])} for k in order}}
+                            "max_ms": _round(max(seg_vals[k])), "n": len(seg_vals[k])} for k in order},
+           # kube-lite's write of each watch event (".sent" -> ".written"), per watch
+           "watch_writes": {k: {"p50_ms": _round(_pct(v, 0.5)), "p99_ms": _round(_pct(v, 0.99)),
+                                "max_ms": _round(max(v)), "n": len(v)} for k, v in sorted(writes.items())}}
     thr = max(_pct(total, 0.99) or 0.0, tail_ms)
     tail = [t for t in per_tenant if t[1] > thr]
     blame, blame_ms, overlap, slow_hits, examples = {}, {}, {}, {}, []

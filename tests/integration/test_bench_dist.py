@@ -53,8 +53,9 @@ def test_bench_two_ranks_gloo():
     # both ranks' tenants are traced through every process and attributed
     for att in d["latency_at_rate"]["attribution"]["this"]["200"]:
         assert att["attributed"] == 200 and att["trace_dropped"] == 0
-        # the watch legs split at kube-lite's write and the controller's read
-        assert {"ctl_watch_sent->ctl_watch_written", "ctl_read->ctl_event"} <= set(att["segments"]), att["segments"]
+        # the controller's watch leg splits at its read; kube-lite's writes are timed beside it
+        assert {"ctl_watch_sent->ctl_read", "ctl_read->ctl_event"} <= set(att["segments"]), att["segments"]
+        assert "userbootstraps.controller" in att["watch_writes"], att["watch_writes"]
         assert "slow_sections" in att
     for w in q["windows"]:  # per-thread CPU and run-queue wait of the window
         assert w["busiest_threads"] and all("runq_ms" in t for t in w["waiting_threads"])
