@@ -46,6 +46,7 @@ std::atomic<bool> g_running{false};
 std::atomic<uint64_t> g_ticks{0};
 // note_slow's threshold: "never" until start() finds that records are kept
 std::atomic<int64_t> g_slow_ns{INT64_MAX};
+std::atomic<int64_t> g_lock_ns{INT64_MAX};
 
 // Never destroyed: the sampler thread is detached and still runs while static destructors
 // run at exit (a ThreadSanitizer race on a global vector, tools/sanitize.sh tsan).
@@ -122,19 +123,32 @@ void start(const std::string& name) {
       st.process = name;
     }
     g_running.store(true);
-    if (metrics::debug_endpoints_enabled()) g_slow_ns.store(record_threshold_ns());
+    if (metrics::debug_endpoints_enabled()) {
+      g_slow_ns.store(record_threshold_ns());
+      const char* lk = std::getenv("BGC_LOCK_SECTION_US");
+      g_lock_ns.store((lk ? std::atoll(lk) : 200) * 1000);
+    }
     std::thread(loop).detach();
   });
 }
 
 bool running() { return g_running.load(); }
 
-void note_slow(std::string_view what, int64_t t0_ns, int64_t t1_ns) {
-  if (t1_ns - t0_ns < g_slow_ns.load(std::memory_order_relaxed)) return;
+namespace {
+void keep_slow(std::string_view what, int64_t t0_ns, int64_t t1_ns) {
   State& st = state();
   std::lock_guard<std::mutex> lk(st.mu);
   if (st.slow.size() < kMaxKept) st.slow.push_back({t1_ns, t1_ns - t0_ns, std::string(what)});
   else ++st.dropped;
+}
+}  // namespace
+
+void note_slow(std::string_view what, int64_t t0_ns, int64_t t1_ns) {
+  if (t1_ns - t0_ns >= g_slow_ns.load(std::memory_order_relaxed)) keep_slow(what, t0_ns, t1_ns);
+}
+
+void note_lock_section(std::string_view what, int64_t t0_ns, int64_t t1_ns) {
+  if (t1_ns - t0_ns >= g_lock_ns.load(std::memory_order_relaxed)) keep_slow(what, t0_ns, t1_ns);
 }
 
 std::string dump_json(bool take) {

@@ -29,6 +29,9 @@ bool running();
 // stalls when it lasted >= BGC_STALL_RECORD_US and the sampler keeps records (debug
 // endpoints on); otherwise one relaxed load and a return.
 void note_slow(std::string_view what, int64_t t0_ns, int64_t t1_ns);
+// The same for a short section that takes a shared lock (a watcher's store apply or queue
+// add): kept past BGC_LOCK_SECTION_US (default 200 us) instead, when records are kept.
+void note_lock_section(std::string_view what, int64_t t0_ns, int64_t t1_ns);
 // {"process":..,"ticks":n,"stalls":[[t_ns, oversleep_us, runq_us, malloc_us],...],
 //  "slow":[[t1_ns, duration_us, what],...], "dropped":n}; `take` clears what was kept.
 std::string dump_json(bool take);

@@ -599,6 +599,8 @@ void Controller::run(CancelToken& stop, Reconciler reconcile, ErrorPolicy error_
   threads.emplace_back([&] {
     Watcher w(client_, primary_);
     w.set_projection(opts_.primary_projection);
+    // the two shared locks a watch event takes (stall::note_lock_section)
+    const std::string store_section = "w:" + primary_.plural + " store", queue_section = "w:" + primary_.plural + " queue";
     w.run(stop, [&](const WatchEvent& ev) {
       // marked before the store applies it: a worker may reconcile from the store at once
       if (trace::armed() && ev.object && ev.type != WatchEvent::Type::Deleted) {
@@ -606,12 +608,16 @@ void Controller::run(CancelToken& stop, Reconciler reconcile, ErrorPolicy error_
         trace::mark_at(name, "ctl.primary_read", ev.read_ns);
         trace::mark(name, "ctl.primary_event");
       }
+      const int64_t t0 = metrics::now_ns();
       primary_store_->apply(ev);
+      const int64_t t1 = metrics::now_ns();
+      stall::note_lock_section(store_section, t0, t1);
       primary_gauge.set(static_cast<double>(primary_store_->size()));
       if (ev.type == WatchEvent::Type::Restarted) {
         for (const auto& o : ev.objects) queue_.add(primary_.key(meta_namespace(*o), meta_name(*o)));
       } else if (ev.type != WatchEvent::Type::Deleted) {
         queue_.add_after(primary_.key(meta_namespace(*ev.object), meta_name(*ev.object)), opts_.debounce);
+        stall::note_lock_section(queue_section, t1, metrics::now_ns());
       } else {
         // the object is gone: its periodic requeue would only find nothing
         queue_.forget(primary_.key(meta_namespace(*ev.object), meta_name(*ev.object)));
@@ -632,11 +638,14 @@ void Controller::run(CancelToken& stop, Reconciler reconcile, ErrorPolicy error_
       Watcher w(client_, c->rt, "", c->selector);
       w.set_metadata_only(c->metadata_only);
       w.set_projection(opts_.child_projection);
+      const std::string store_section = "w:" + c->rt.plural + " store";
       w.run(stop, [&, c](const WatchEvent& ev) {
         if (trace::armed() && ev.object && ev.type != WatchEvent::Type::Deleted) {
           trace::mark(meta_name(*ev.object), "ctl." + c->rt.plural + "_event");
         }
+        const int64_t t0 = metrics::now_ns();
         c->store->apply(ev);
+        stall::note_lock_section(store_section, t0, metrics::now_ns());
         c->gauge->set(static_cast<double>(c->store->size()));
         if (ev.type == WatchEvent::Type::Restarted) {
           for (const auto& o : ev.objects) {
@@ -695,7 +704,9 @@ void Controller::run(CancelToken& stop, Reconciler reconcile, ErrorPolicy error_
           a = error_policy(obj, e);
         }
         if (traced) trace::mark(meta_name(*obj), "ctl.reconcile1");
+        const int64_t f0 = metrics::now_ns();
         queue_.finish(key, a.requeue, a.after);
+        stall::note_lock_section("reconcile queue", f0, metrics::now_ns());
         q_depth.set(static_cast<double>(queue_.pending()));
       }
     });

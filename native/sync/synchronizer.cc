@@ -10,6 +10,7 @@
 #include "core/json_patch.h"
 #include "core/log.h"
 #include "core/metrics.h"
+#include "core/stall.h"
 #include "core/trace.h"
 #include "kube/ratelimit.h"
 #include "core/process.h"
@@ -278,11 +279,15 @@ int Synchronizer::run(CancelToken& stop) {
         if (trace::armed() && ev.object && ev.type != kube::WatchEvent::Type::Deleted) {
           trace::mark(kube::meta_name(*ev.object), "sync.ub_event");
         }
+        const int64_t t0 = metrics::now_ns();
         store.apply(ev);
+        const int64_t t1 = metrics::now_ns();
+        stall::note_lock_section("w:userbootstraps store", t0, t1);
         if (ev.type == kube::WatchEvent::Type::Restarted) {
           for (const auto& o : ev.objects) queue.add(kube::meta_name(*o));
         } else if (ev.type != kube::WatchEvent::Type::Deleted) {
           queue.add(kube::meta_name(*ev.object));
+          stall::note_lock_section("w:userbootstraps queue", t1, metrics::now_ns());
         } else {
           retries.forget(kube::meta_name(*ev.object));  // a failing UB that is gone retries no more
           std::lock_guard<std::mutex> g(acted_mu);
