@@ -406,7 +406,19 @@ bool Store::wait_synced(std::chrono::milliseconds timeout) const {
 // ---------------------------------------------------------------------------
 // WorkQueue
 
-void WorkQueue::schedule_locked(const std::string& key, Clock::time_point t) {
+// Condition variables are signalled after the queue's lock is released (Wake::fire): a
+// signal under the lock lengthens every hold by a futex syscall, and the woken worker can
+// preempt the signaller on its CPU while the signaller still holds the lock.  Every
+// watcher and worker then waits for that thread's next time slice; round 6's traces caught
+// this queue lock held for up to 10-15 ms at 6,000 CR/s (stall::note_lock_section,
+// profiles/r6_locks/).  A waiter re-checks the timeline under the lock before it sleeps, so
+// deciding under the lock and signalling after it loses no wake-up.
+void WorkQueue::Wake::fire(std::condition_variable& cv, std::condition_variable& timer_cv) const {
+  for (int i = 0; i < workers; ++i) cv.notify_one();
+  if (timer) timer_cv.notify_one();
+}
+
+void WorkQueue::schedule_locked(const std::string& key, Clock::time_point t, Wake& wake) {
   auto [d, fresh] = due_.try_emplace(key);
   // Moving a key earlier (an event for a key with a pending 30 s requeue) drops its old node.
   if (!fresh) timeline_.erase(d->second.node);
@@ -414,40 +426,52 @@ void WorkQueue::schedule_locked(const std::string& key, Clock::time_point t) {
   d->second.node = (timeline_.empty() || !(t < timeline_.rbegin()->first)) ? timeline_.emplace_hint(timeline_.end(), t, key)
                                                                            : timeline_.emplace(t, key);
   if (t <= Clock::now()) {
-    if (idle_ > 0) cv_.notify_one();
-    else if (timer_waiter_) timer_cv_.notify_one();
+    if (idle_ > wake.workers) ++wake.workers;
+    else if (timer_waiter_) wake.timer = true;
   } else if (timer_waiter_) {
-    if (t < timer_target_) timer_cv_.notify_one();  // new earliest deadline
-  } else if (idle_ > 0) {
-    cv_.notify_one();  // someone must become the timer waiter
+    if (t < timer_target_) wake.timer = true;  // new earliest deadline
+  } else if (idle_ > wake.workers) {
+    ++wake.workers;  // someone must become the timer waiter
   }
 }
 
 void WorkQueue::add_after(const std::string& key, std::chrono::milliseconds delay) {
   auto t = Clock::now() + delay;
-  std::lock_guard<std::mutex> lk(mu_);
-  if (!forgotten_.empty()) forgotten_.erase(key);
-  add_after_locked(key, t);
-  count_locked();
+  Wake wake;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!forgotten_.empty()) forgotten_.erase(key);
+    add_after_locked(key, t, wake);
+    count_locked();
+  }
+  wake.fire(cv_, timer_cv_);
 }
 
 void WorkQueue::requeue(const std::string& key, std::chrono::milliseconds delay) {
   auto t = Clock::now() + delay;
-  std::lock_guard<std::mutex> lk(mu_);
-  if (!forgotten_.empty() && forgotten_.count(key)) return;
-  add_after_locked(key, t);
-  count_locked();
+  Wake wake;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!forgotten_.empty() && forgotten_.count(key)) return;
+    add_after_locked(key, t, wake);
+    count_locked();
+  }
+  wake.fire(cv_, timer_cv_);
 }
 
 void WorkQueue::finish(const std::string& key, bool requeue, std::chrono::milliseconds delay) {
   const auto t = Clock::now() + delay;
-  std::lock_guard<std::mutex> lk(mu_);
-  if (requeue && (forgotten_.empty() || !forgotten_.count(key))) add_after_locked(key, t);
-  done_locked(key);
-  count_locked();
+  Wake wake;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (requeue && (forgotten_.empty() || !forgotten_.count(key))) add_after_locked(key, t, wake);
+    done_locked(key, wake);
+    count_locked();
+  }
+  wake.fire(cv_, timer_cv_);
 }
 
-void WorkQueue::add_after_locked(const std::string& key, Clock::time_point t) {
+void WorkQueue::add_after_locked(const std::string& key, Clock::time_point t, Wake& wake) {
   if (shutdown_) return;
   if (processing_.count(key)) {
     auto it = deferred_.find(key);
@@ -456,7 +480,7 @@ void WorkQueue::add_after_locked(const std::string& key, Clock::time_point t) {
   }
   auto it = due_.find(key);
   if (it != due_.end() && it->second.t <= t) return;
-  schedule_locked(key, t);
+  schedule_locked(key, t, wake);
 }
 
 void WorkQueue::forget(const std::string& key) {
@@ -486,7 +510,9 @@ bool WorkQueue::get(std::string& key) {
       processing_.insert(key);
       count_locked();
       // hand the timer role on if more work is waiting and nobody is timing it
-      if (!timeline_.empty() && !timer_waiter_ && idle_ > 0) cv_.notify_one();
+      const bool hand_on = !timeline_.empty() && !timer_waiter_ && idle_ > 0;
+      lk.unlock();
+      if (hand_on) cv_.notify_one();
       return true;
     }
     if (!timeline_.empty() && !timer_waiter_) {
@@ -505,12 +531,16 @@ bool WorkQueue::get(std::string& key) {
 }
 
 void WorkQueue::done(const std::string& key) {
-  std::lock_guard<std::mutex> lk(mu_);
-  done_locked(key);
-  count_locked();
+  Wake wake;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    done_locked(key, wake);
+    count_locked();
+  }
+  wake.fire(cv_, timer_cv_);
 }
 
-void WorkQueue::done_locked(const std::string& key) {
+void WorkQueue::done_locked(const std::string& key, Wake& wake) {
   processing_.erase(key);
   if (!forgotten_.empty()) forgotten_.erase(key);
   auto it = deferred_.find(key);
@@ -518,13 +548,15 @@ void WorkQueue::done_locked(const std::string& key) {
     auto t = it->second;
     deferred_.erase(it);
     auto d = due_.find(key);
-    if (d == due_.end() || t < d->second.t) schedule_locked(key, t);
+    if (d == due_.end() || t < d->second.t) schedule_locked(key, t, wake);
   }
 }
 
 void WorkQueue::shutdown() {
-  std::lock_guard<std::mutex> lk(mu_);
-  shutdown_ = true;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    shutdown_ = true;
+  }
   cv_.notify_all();
   timer_cv_.notify_all();
 }

@@ -183,7 +183,14 @@ class WorkQueue {
   size_t in_flight() const;
 
  private:
-  void schedule_locked(const std::string& key, Clock::time_point t);  // insert + wake exactly one waiter
+  // Which waiters to signal once the lock is released: one idle worker per item made due
+  // (as many as were idle), and the timer waiter at most once.
+  struct Wake {
+    int workers = 0;
+    bool timer = false;
+    void fire(std::condition_variable& cv, std::condition_variable& timer_cv) const;
+  };
+  void schedule_locked(const std::string& key, Clock::time_point t, Wake& wake);  // insert; pick one waiter
   mutable std::mutex mu_;
   // One idle worker (the timer waiter) sleeps until the earliest deadline on timer_cv_;
   // the others wait untimed on cv_. A due item wakes one worker, not every idle one.
@@ -208,8 +215,8 @@ class WorkQueue {
   std::unordered_set<std::string> processing_;
   std::unordered_map<std::string, Clock::time_point> deferred_;  // re-added while processing
   std::unordered_set<std::string> forgotten_;                    // forgotten while processing
-  void add_after_locked(const std::string& key, Clock::time_point t);
-  void done_locked(const std::string& key);
+  void add_after_locked(const std::string& key, Clock::time_point t, Wake& wake);
+  void done_locked(const std::string& key, Wake& wake);
   void count_locked() { pending_.store(due_.size() + deferred_.size(), std::memory_order_relaxed); }
   std::atomic<size_t> pending_{0};
   bool shutdown_ = false;
