@@ -406,164 +406,233 @@ bool Store::wait_synced(std::chrono::milliseconds timeout) const {
 // ---------------------------------------------------------------------------
 // WorkQueue
 
-// Condition variables are signalled after the queue's lock is released (Wake::fire): a
+// One shard: the whole queue of round 5, for the keys that hash to it.
+//
+// Condition variables are signalled after the shard's lock is released (Wake::fire): a
 // signal under the lock lengthens every hold by a futex syscall, and the woken worker can
-// preempt the signaller on its CPU while the signaller still holds the lock.  Every
-// watcher and worker then waits for that thread's next time slice; round 6's traces caught
-// this queue lock held for up to 10-15 ms at 6,000 CR/s (stall::note_lock_section,
-// profiles/r6_locks/).  A waiter re-checks the timeline under the lock before it sleeps, so
-// deciding under the lock and signalling after it loses no wake-up.
-void WorkQueue::Wake::fire(std::condition_variable& cv, std::condition_variable& timer_cv) const {
-  for (int i = 0; i < workers; ++i) cv.notify_one();
-  if (timer) timer_cv.notify_one();
+// preempt the signaller on its CPU while the signaller still holds the lock.  A waiter
+// re-checks the timeline under the lock before it sleeps, so deciding under the lock and
+// signalling after it loses no wake-up.
+struct WorkQueue::Shard {
+  using Timeline = std::multimap<Clock::time_point, std::string>;
+  struct Due {
+    Clock::time_point t;
+    Timeline::iterator node;
+  };
+  // Which waiters to signal once the lock is released: one idle worker per item made due
+  // (as many as are idle), and the timer waiter at most once.
+  struct Wake {
+    int workers = 0;
+    bool timer = false;
+  };
+
+  mutable std::mutex mu;
+  // One idle worker (the timer waiter) sleeps until the earliest deadline on timer_cv; the
+  // others wait untimed on cv.  A due item wakes one worker, not every idle one.
+  std::condition_variable cv;
+  std::condition_variable timer_cv;
+  int idle = 0;               // workers waiting on cv
+  bool timer_waiter = false;  // a worker is waiting on timer_cv
+  Clock::time_point timer_target{};
+  // Hash containers: under churn the queue holds a pending 30 s requeue for every live
+  // UserBootstrap, and ordered maps paid a chain of string compares per operation.  due and
+  // timeline index each other one to one: a key's entry holds its timeline node, so moving
+  // or dropping a key erases that node directly, and the common insert, a periodic requeue
+  // later than everything queued, goes in at the end with a hint.
+  std::unordered_map<std::string, Due> due;  // key -> due time and its timeline node
+  Timeline timeline;                         // due time -> key
+  std::unordered_set<std::string> processing;
+  std::unordered_map<std::string, Clock::time_point> deferred;  // re-added while processing
+  std::unordered_set<std::string> forgotten;                    // forgotten while processing
+  std::atomic<size_t> pending{0};
+  bool shutdown = false;
+
+  void fire(const Wake& w) {
+    for (int i = 0; i < w.workers; ++i) cv.notify_one();
+    if (w.timer) timer_cv.notify_one();
+  }
+  void count_locked() { pending.store(due.size() + deferred.size(), std::memory_order_relaxed); }
+
+  void schedule_locked(const std::string& key, Clock::time_point t, Wake& wake) {
+    auto [d, fresh] = due.try_emplace(key);
+    // Moving a key earlier (an event for a key with a pending 30 s requeue) drops its old node.
+    if (!fresh) timeline.erase(d->second.node);
+    d->second.t = t;
+    d->second.node = (timeline.empty() || !(t < timeline.rbegin()->first)) ? timeline.emplace_hint(timeline.end(), t, key)
+                                                                           : timeline.emplace(t, key);
+    if (t <= Clock::now()) {
+      if (idle > wake.workers) ++wake.workers;
+      else if (timer_waiter) wake.timer = true;
+    } else if (timer_waiter) {
+      if (t < timer_target) wake.timer = true;  // new earliest deadline
+    } else if (idle > wake.workers) {
+      ++wake.workers;  // someone must become the timer waiter
+    }
+  }
+
+  void add_after_locked(const std::string& key, Clock::time_point t, Wake& wake) {
+    if (shutdown) return;
+    if (processing.count(key)) {
+      auto it = deferred.find(key);
+      if (it == deferred.end() || t < it->second) deferred[key] = t;
+      return;
+    }
+    auto it = due.find(key);
+    if (it != due.end() && it->second.t <= t) return;
+    schedule_locked(key, t, wake);
+  }
+
+  void done_locked(const std::string& key, Wake& wake) {
+    processing.erase(key);
+    if (!forgotten.empty()) forgotten.erase(key);
+    auto it = deferred.find(key);
+    if (it != deferred.end()) {
+      auto t = it->second;
+      deferred.erase(it);
+      auto d = due.find(key);
+      if (d == due.end() || t < d->second.t) schedule_locked(key, t, wake);
+    }
+  }
+};
+
+WorkQueue::WorkQueue(size_t shards) {
+  for (size_t i = 0; i < std::max<size_t>(1, shards); ++i) shards_.push_back(std::make_unique<Shard>());
 }
 
-void WorkQueue::schedule_locked(const std::string& key, Clock::time_point t, Wake& wake) {
-  auto [d, fresh] = due_.try_emplace(key);
-  // Moving a key earlier (an event for a key with a pending 30 s requeue) drops its old node.
-  if (!fresh) timeline_.erase(d->second.node);
-  d->second.t = t;
-  d->second.node = (timeline_.empty() || !(t < timeline_.rbegin()->first)) ? timeline_.emplace_hint(timeline_.end(), t, key)
-                                                                           : timeline_.emplace(t, key);
-  if (t <= Clock::now()) {
-    if (idle_ > wake.workers) ++wake.workers;
-    else if (timer_waiter_) wake.timer = true;
-  } else if (timer_waiter_) {
-    if (t < timer_target_) wake.timer = true;  // new earliest deadline
-  } else if (idle_ > wake.workers) {
-    ++wake.workers;  // someone must become the timer waiter
-  }
+WorkQueue::~WorkQueue() = default;
+
+size_t WorkQueue::shards_for(int workers) {
+  // BGC_QUEUE_SHARDS overrides (A/B runs); never more shards than workers
+  const char* e = std::getenv("BGC_QUEUE_SHARDS");
+  const int want = e && *e ? std::atoi(e) : workers / 4;
+  return static_cast<size_t>(std::clamp(want, 1, std::clamp(std::max(1, workers), 1, 8)));
+}
+
+WorkQueue::Shard& WorkQueue::shard_of(const std::string& key) const {
+  return *shards_[shards_.size() == 1 ? 0 : std::hash<std::string>{}(key) % shards_.size()];
 }
 
 void WorkQueue::add_after(const std::string& key, std::chrono::milliseconds delay) {
   auto t = Clock::now() + delay;
-  Wake wake;
+  Shard& sh = shard_of(key);
+  Shard::Wake wake;
   {
-    std::lock_guard<std::mutex> lk(mu_);
-    if (!forgotten_.empty()) forgotten_.erase(key);
-    add_after_locked(key, t, wake);
-    count_locked();
+    std::lock_guard<std::mutex> lk(sh.mu);
+    if (!sh.forgotten.empty()) sh.forgotten.erase(key);
+    sh.add_after_locked(key, t, wake);
+    sh.count_locked();
   }
-  wake.fire(cv_, timer_cv_);
+  sh.fire(wake);
 }
 
 void WorkQueue::requeue(const std::string& key, std::chrono::milliseconds delay) {
   auto t = Clock::now() + delay;
-  Wake wake;
+  Shard& sh = shard_of(key);
+  Shard::Wake wake;
   {
-    std::lock_guard<std::mutex> lk(mu_);
-    if (!forgotten_.empty() && forgotten_.count(key)) return;
-    add_after_locked(key, t, wake);
-    count_locked();
+    std::lock_guard<std::mutex> lk(sh.mu);
+    if (!sh.forgotten.empty() && sh.forgotten.count(key)) return;
+    sh.add_after_locked(key, t, wake);
+    sh.count_locked();
   }
-  wake.fire(cv_, timer_cv_);
+  sh.fire(wake);
 }
 
 void WorkQueue::finish(const std::string& key, bool requeue, std::chrono::milliseconds delay) {
   const auto t = Clock::now() + delay;
-  Wake wake;
+  Shard& sh = shard_of(key);
+  Shard::Wake wake;
   {
-    std::lock_guard<std::mutex> lk(mu_);
-    if (requeue && (forgotten_.empty() || !forgotten_.count(key))) add_after_locked(key, t, wake);
-    done_locked(key, wake);
-    count_locked();
+    std::lock_guard<std::mutex> lk(sh.mu);
+    if (requeue && (sh.forgotten.empty() || !sh.forgotten.count(key))) sh.add_after_locked(key, t, wake);
+    sh.done_locked(key, wake);
+    sh.count_locked();
   }
-  wake.fire(cv_, timer_cv_);
-}
-
-void WorkQueue::add_after_locked(const std::string& key, Clock::time_point t, Wake& wake) {
-  if (shutdown_) return;
-  if (processing_.count(key)) {
-    auto it = deferred_.find(key);
-    if (it == deferred_.end() || t < it->second) deferred_[key] = t;
-    return;
-  }
-  auto it = due_.find(key);
-  if (it != due_.end() && it->second.t <= t) return;
-  schedule_locked(key, t, wake);
+  sh.fire(wake);
 }
 
 void WorkQueue::forget(const std::string& key) {
-  std::lock_guard<std::mutex> lk(mu_);
-  deferred_.erase(key);
-  if (processing_.count(key)) forgotten_.insert(key);
-  auto d = due_.find(key);
-  if (d == due_.end()) {
-    count_locked();
-    return;
+  Shard& sh = shard_of(key);
+  std::lock_guard<std::mutex> lk(sh.mu);
+  sh.deferred.erase(key);
+  if (sh.processing.count(key)) sh.forgotten.insert(key);
+  auto d = sh.due.find(key);
+  if (d != sh.due.end()) {
+    sh.timeline.erase(d->second.node);
+    sh.due.erase(d);
   }
-  timeline_.erase(d->second.node);
-  due_.erase(d);
-  count_locked();
+  sh.count_locked();
 }
 
-bool WorkQueue::get(std::string& key) {
-  std::unique_lock<std::mutex> lk(mu_);
+bool WorkQueue::get(std::string& key, size_t worker) {
+  Shard& sh = *shards_[worker % shards_.size()];
+  std::unique_lock<std::mutex> lk(sh.mu);
   while (true) {
-    if (shutdown_) return false;
+    if (sh.shutdown) return false;
     auto now = Clock::now();
-    if (!timeline_.empty() && !(timeline_.begin()->first > now)) {
-      auto it = timeline_.begin();
+    if (!sh.timeline.empty() && !(sh.timeline.begin()->first > now)) {
+      auto it = sh.timeline.begin();
       key = std::move(it->second);
-      timeline_.erase(it);
-      due_.erase(key);
-      processing_.insert(key);
-      count_locked();
+      sh.timeline.erase(it);
+      sh.due.erase(key);
+      sh.processing.insert(key);
+      sh.count_locked();
       // hand the timer role on if more work is waiting and nobody is timing it
-      const bool hand_on = !timeline_.empty() && !timer_waiter_ && idle_ > 0;
+      const bool hand_on = !sh.timeline.empty() && !sh.timer_waiter && sh.idle > 0;
       lk.unlock();
-      if (hand_on) cv_.notify_one();
+      if (hand_on) sh.cv.notify_one();
       return true;
     }
-    if (!timeline_.empty() && !timer_waiter_) {
-      timer_waiter_ = true;
+    if (!sh.timeline.empty() && !sh.timer_waiter) {
+      sh.timer_waiter = true;
       // copy: wait_until re-reads its deadline after re-locking, when another worker may have erased the node
-      timer_target_ = timeline_.begin()->first;
-      const auto deadline = timer_target_;
-      timer_cv_.wait_until(lk, deadline);
-      timer_waiter_ = false;
+      sh.timer_target = sh.timeline.begin()->first;
+      const auto deadline = sh.timer_target;
+      sh.timer_cv.wait_until(lk, deadline);
+      sh.timer_waiter = false;
     } else {
-      ++idle_;
-      cv_.wait(lk);
-      --idle_;
+      ++sh.idle;
+      sh.cv.wait(lk);
+      --sh.idle;
     }
   }
 }
 
 void WorkQueue::done(const std::string& key) {
-  Wake wake;
+  Shard& sh = shard_of(key);
+  Shard::Wake wake;
   {
-    std::lock_guard<std::mutex> lk(mu_);
-    done_locked(key, wake);
-    count_locked();
+    std::lock_guard<std::mutex> lk(sh.mu);
+    sh.done_locked(key, wake);
+    sh.count_locked();
   }
-  wake.fire(cv_, timer_cv_);
-}
-
-void WorkQueue::done_locked(const std::string& key, Wake& wake) {
-  processing_.erase(key);
-  if (!forgotten_.empty()) forgotten_.erase(key);
-  auto it = deferred_.find(key);
-  if (it != deferred_.end()) {
-    auto t = it->second;
-    deferred_.erase(it);
-    auto d = due_.find(key);
-    if (d == due_.end() || t < d->second.t) schedule_locked(key, t, wake);
-  }
+  sh.fire(wake);
 }
 
 void WorkQueue::shutdown() {
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    shutdown_ = true;
+  for (auto& sh : shards_) {
+    {
+      std::lock_guard<std::mutex> lk(sh->mu);
+      sh->shutdown = true;
+    }
+    sh->cv.notify_all();
+    sh->timer_cv.notify_all();
   }
-  cv_.notify_all();
-  timer_cv_.notify_all();
+}
+
+size_t WorkQueue::pending() const {
+  size_t n = 0;
+  for (const auto& sh : shards_) n += sh->pending.load(std::memory_order_relaxed);
+  return n;
 }
 
 size_t WorkQueue::in_flight() const {
-  std::lock_guard<std::mutex> lk(mu_);
-  return processing_.size();
+  size_t n = 0;
+  for (const auto& sh : shards_) {
+    std::lock_guard<std::mutex> lk(sh->mu);
+    n += sh->processing.size();
+  }
+  return n;
 }
 
 // ---------------------------------------------------------------------------
@@ -584,7 +653,11 @@ Controller::Mapper owner_mapper(const ResourceType& owner) {
 }
 
 Controller::Controller(KubeClient& client, ResourceType primary, Options opts)
-    : client_(client), primary_(std::move(primary)), opts_(opts), primary_store_(std::make_unique<Store>(primary_)) {}
+    : client_(client),
+      primary_(std::move(primary)),
+      opts_(opts),
+      primary_store_(std::make_unique<Store>(primary_)),
+      queue_(WorkQueue::shards_for(opts.workers)) {}
 
 Controller::~Controller() { queue_.shutdown(); }
 
@@ -717,10 +790,10 @@ void Controller::run(CancelToken& stop, Reconciler reconcile, ErrorPolicy error_
   auto& q_depth = reg.gauge("bgc_controller_queue_depth", "Keys waiting in the work queue");
   std::vector<std::thread> workers;
   for (int i = 0; i < std::max(1, opts_.workers); ++i) {
-    workers.emplace_back([&] {
+    workers.emplace_back([&, i] {
       set_thread_name("reconcile");
       std::string key;
-      while (queue_.get(key)) {
+      while (queue_.get(key, static_cast<size_t>(i))) {
         q_depth.set(static_cast<double>(queue_.pending()));
         ObjPtr obj = primary_store_->get(key);
         if (!obj) {

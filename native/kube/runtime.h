@@ -161,13 +161,25 @@ class Store {
 // semantics): at most one pending entry per key, earliest due time wins; a key being
 // processed is never handed to a second worker — re-adds while in flight are deferred
 // until done().
+//
+// Sharded by key: each shard has its own lock and its own workers (worker i serves shard
+// i % shards), so a watcher's add contends with a quarter of the workers, not all of them.
+// Every key lives in one shard, which keeps the per-key guarantees above.  Round 6 traced
+// open-loop tails to this lock: with one shard the watcher's add and the workers' finish
+// waited up to 10-15 ms behind a preempted holder (profiles/r6_locks/).
 class WorkQueue {
  public:
   using Clock = std::chrono::steady_clock;
+  // `shards` >= 1; run at least as many workers as shards (each shard needs one).
+  explicit WorkQueue(size_t shards = 1);
+  ~WorkQueue();
+  // A shard per four workers, at most 8: the controller's and synchronizer's default.
+  static size_t shards_for(int workers);
+  size_t shards() const { return shards_.size(); }
   void add(const std::string& key) { add_after(key, std::chrono::milliseconds(0)); }
   void add_after(const std::string& key, std::chrono::milliseconds delay);
-  // Blocks until a key is due or the queue shuts down (returns false).
-  bool get(std::string& key);
+  // Blocks until a key of worker `worker`'s shard is due or the queue shuts down (false).
+  bool get(std::string& key, size_t worker = 0);
   void done(const std::string& key);
   // Drops a pending entry, e.g. the periodic requeue of an object that was deleted: keeps
   // the queue proportional to live objects under churn.  A key forgotten while in flight
@@ -179,47 +191,13 @@ class WorkQueue {
   // A worker is done with `key`: requeue (when `requeue`) and done() under one lock.
   void finish(const std::string& key, bool requeue, std::chrono::milliseconds delay);
   void shutdown();
-  size_t pending() const { return pending_.load(std::memory_order_relaxed); }  // lock-free (gauges)
+  size_t pending() const;  // lock-free (gauges)
   size_t in_flight() const;
 
  private:
-  // Which waiters to signal once the lock is released: one idle worker per item made due
-  // (as many as were idle), and the timer waiter at most once.
-  struct Wake {
-    int workers = 0;
-    bool timer = false;
-    void fire(std::condition_variable& cv, std::condition_variable& timer_cv) const;
-  };
-  void schedule_locked(const std::string& key, Clock::time_point t, Wake& wake);  // insert; pick one waiter
-  mutable std::mutex mu_;
-  // One idle worker (the timer waiter) sleeps until the earliest deadline on timer_cv_;
-  // the others wait untimed on cv_. A due item wakes one worker, not every idle one.
-  std::condition_variable cv_;
-  std::condition_variable timer_cv_;
-  int idle_ = 0;                  // workers waiting on cv_
-  bool timer_waiter_ = false;     // a worker is waiting on timer_cv_
-  Clock::time_point timer_target_{};
-  // Hash containers: under churn the queue holds a pending 30 s requeue for every live
-  // UserBootstrap, and ordered maps paid a chain of string compares per operation.
-  // due_ and timeline_ index each other one to one: a key's entry holds its timeline node,
-  // so moving or dropping a key erases that node directly (no equal_range walk, no stale
-  // nodes left behind), and the common insert, a periodic requeue later than everything
-  // queued, goes in at the end with a hint instead of a search from the root.
-  using Timeline = std::multimap<Clock::time_point, std::string>;
-  struct Due {
-    Clock::time_point t;
-    Timeline::iterator node;
-  };
-  std::unordered_map<std::string, Due> due_;  // key -> due time and its timeline node
-  Timeline timeline_;                         // due time -> key
-  std::unordered_set<std::string> processing_;
-  std::unordered_map<std::string, Clock::time_point> deferred_;  // re-added while processing
-  std::unordered_set<std::string> forgotten_;                    // forgotten while processing
-  void add_after_locked(const std::string& key, Clock::time_point t, Wake& wake);
-  void done_locked(const std::string& key, Wake& wake);
-  void count_locked() { pending_.store(due_.size() + deferred_.size(), std::memory_order_relaxed); }
-  std::atomic<size_t> pending_{0};
-  bool shutdown_ = false;
+  struct Shard;
+  Shard& shard_of(const std::string& key) const;
+  std::vector<std::unique_ptr<Shard>> shards_;
 };
 
 struct Action {

@@ -113,18 +113,20 @@ void register_kube(py::module_& m) {
       })
       .def("size", &bgc::kube::EventRateLimiter::size);
   py::class_<bgc::kube::WorkQueue>(m, "WorkQueue")
-      .def(py::init<>())
+      .def(py::init<size_t>(), py::arg("shards") = 1)
+      .def("shards", &bgc::kube::WorkQueue::shards)
+      .def_static("shards_for", &bgc::kube::WorkQueue::shards_for)
       .def("add", [](bgc::kube::WorkQueue& q, const std::string& k) { q.add(k); })
       .def("add_after", [](bgc::kube::WorkQueue& q, const std::string& k, int ms) { q.add_after(k, std::chrono::milliseconds(ms)); })
-      .def("get", [](bgc::kube::WorkQueue& q) {
+      .def("get", [](bgc::kube::WorkQueue& q, size_t worker) {
         std::string k;
         bool ok;
         {
           py::gil_scoped_release nogil;
-          ok = q.get(k);
+          ok = q.get(k, worker);
         }
         return ok ? py::object(py::str(k)) : py::object(py::none());
-      })
+      }, py::arg("worker") = 0)
       .def("done", &bgc::kube::WorkQueue::done)
       .def("forget", &bgc::kube::WorkQueue::forget)
       .def("requeue", [](bgc::kube::WorkQueue& q, const std::string& k, int ms) { q.requeue(k, std::chrono::milliseconds(ms)); })

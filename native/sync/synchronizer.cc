@@ -249,7 +249,7 @@ int Synchronizer::run(CancelToken& stop) {
   http::add_readiness_check("sheet", sheet_ready);
   std::unique_ptr<std::thread> watch_thread;
   std::vector<std::thread> workers;
-  kube::WorkQueue queue;
+  kube::WorkQueue queue(kube::WorkQueue::shards_for(cfg_.workers));
   kube::Store store(types::UserBootstrap);
   std::atomic<bool> fatal{false};
   auto& ub_latency = metrics::Registry::global().samples("sync_ub");
@@ -297,10 +297,10 @@ int Synchronizer::run(CancelToken& stop) {
       });
     });
     for (int i = 0; i < std::max(1, cfg_.workers); ++i) {
-      workers.emplace_back([&] {
+      workers.emplace_back([&, i] {
         set_thread_name("sync-worker");
         std::string key;
-        while (queue.get(key)) {
+        while (queue.get(key, static_cast<size_t>(i))) {
           kube::ObjPtr ub = store.get(key);
           if (trace::armed()) trace::mark(key, "sync.dequeue");
           if (ub) {

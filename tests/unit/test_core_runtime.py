@@ -55,6 +55,66 @@ def test_workqueue_per_key_exclusivity(nat):
     assert q.get() is None
 
 
+def test_workqueue_shards_keep_per_key_semantics(nat):
+    """A sharded queue (round 6: one lock per shard, worker i serves shard i % shards): every
+    key is served by its shard's workers, once, with dedup, delay and exclusivity intact."""
+    assert [nat.WorkQueue.shards_for(w) for w in (1, 4, 8, 16, 64)] == [1, 1, 2, 4, 8]
+    q = nat.WorkQueue(4)
+    assert q.shards() == 4
+    keys = [f"k{i}" for i in range(64)]
+    for k in keys:
+        q.add(k)
+        q.add(k)  # dedup within the key's shard
+    assert q.pending() == 64
+    got, lock = {}, threading.Lock()
+
+    def worker(i):
+        while True:
+            k = q.get(i)
+            if k is None:
+                return
+            with lock:
+                got.setdefault(i % 4, []).append(k)
+                first_k0 = k == "k0" and sum(v.count("k0") for v in got.values()) == 1
+            if first_k0:
+                q.add(k)  # re-added while in flight: deferred until done
+            q.done(k)
+
+    ths = [threading.Thread(target=worker, args=(i,)) for i in range(8)]
+    for t in ths:
+        t.start()
+    deadline = time.time() + 5
+    while q.pending() or q.in_flight():
+        assert time.time() < deadline, (q.pending(), q.in_flight())
+        time.sleep(0.01)
+    q.shutdown()
+    for t in ths:
+        t.join(2)
+    served = [k for v in got.values() for k in v]
+    # every key once, k0 once more (its re-add while in flight ran after done), each within one shard
+    assert sorted(served) == sorted(keys + ["k0"])
+    for shard, ks in got.items():  # a key is served by one shard only
+        assert all(sum(k in got[s] for s in got) == 1 for k in ks), shard
+    assert set(got) == {0, 1, 2, 3}  # the keys spread over all four shards
+
+
+def test_workqueue_shard_timer_and_shutdown(nat):
+    q = nat.WorkQueue(2)
+    q.add_after("late", 100)
+    out = []
+    ths = [threading.Thread(target=lambda i=i: out.append(q.get(i))) for i in range(2)]
+    t0 = time.time()
+    for t in ths:
+        t.start()
+    time.sleep(0.3)
+    assert out == ["late"] and time.time() - t0 >= 0.1  # its shard's worker timed it
+    q.done("late")
+    q.shutdown()  # the other shard's idle worker wakes and returns None
+    for t in ths:
+        t.join(2)
+    assert out == ["late", None]
+
+
 @pytest.mark.parametrize("spec,level,target,on", [
     ("info", "info", "controller", True),
     ("info", "debug", "controller", False),
