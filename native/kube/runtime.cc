@@ -432,6 +432,11 @@ struct WorkQueue::Shard {
   std::condition_variable cv;
   std::condition_variable timer_cv;
   int idle = 0;               // workers waiting on cv
+  // Signals sent to cv that no waiter has consumed yet.  A woken worker counts as idle
+  // until it re-takes the lock, which under CPU contention can be milliseconds; without
+  // this count, every add in that window picked the same waiter, the extra signals were
+  // lost, and a due key waited for the next unrelated event or the timer waiter's deadline.
+  int signaled = 0;
   bool timer_waiter = false;  // a worker is waiting on timer_cv
   Clock::time_point timer_target{};
   // Hash containers: under churn the queue holds a pending 30 s requeue for every live
@@ -452,6 +457,10 @@ struct WorkQueue::Shard {
     if (w.timer) timer_cv.notify_one();
   }
   void count_locked() { pending.store(due.size() + deferred.size(), std::memory_order_relaxed); }
+  void signal_locked(Wake& wake) {
+    ++signaled;
+    ++wake.workers;
+  }
 
   void schedule_locked(const std::string& key, Clock::time_point t, Wake& wake) {
     auto [d, fresh] = due.try_emplace(key);
@@ -461,12 +470,12 @@ struct WorkQueue::Shard {
     d->second.node = (timeline.empty() || !(t < timeline.rbegin()->first)) ? timeline.emplace_hint(timeline.end(), t, key)
                                                                            : timeline.emplace(t, key);
     if (t <= Clock::now()) {
-      if (idle > wake.workers) ++wake.workers;
+      if (idle > signaled) signal_locked(wake);
       else if (timer_waiter) wake.timer = true;
     } else if (timer_waiter) {
       if (t < timer_target) wake.timer = true;  // new earliest deadline
-    } else if (idle > wake.workers) {
-      ++wake.workers;  // someone must become the timer waiter
+    } else if (idle > signaled) {
+      signal_locked(wake);  // someone must become the timer waiter
     }
   }
 
@@ -502,9 +511,12 @@ WorkQueue::WorkQueue(size_t shards) {
 WorkQueue::~WorkQueue() = default;
 
 size_t WorkQueue::shards_for(int workers) {
-  // BGC_QUEUE_SHARDS overrides (A/B runs); never more shards than workers
+  // One shard unless BGC_QUEUE_SHARDS says otherwise (at most one per worker, at most 8).
+  // The controller's and synchronizer's workers block on API calls, so a shard's few
+  // workers queue a burst that the whole pool would have absorbed: sharding cut the lock
+  // waits but lengthened event->dequeue tails (profiles/r6_queue_ab/).
   const char* e = std::getenv("BGC_QUEUE_SHARDS");
-  const int want = e && *e ? std::atoi(e) : workers / 4;
+  const int want = e && *e ? std::atoi(e) : 1;
   return static_cast<size_t>(std::clamp(want, 1, std::clamp(std::max(1, workers), 1, 8)));
 }
 
@@ -578,7 +590,8 @@ bool WorkQueue::get(std::string& key, size_t worker) {
       sh.processing.insert(key);
       sh.count_locked();
       // hand the timer role on if more work is waiting and nobody is timing it
-      const bool hand_on = !sh.timeline.empty() && !sh.timer_waiter && sh.idle > 0;
+      const bool hand_on = !sh.timeline.empty() && !sh.timer_waiter && sh.idle > sh.signaled;
+      if (hand_on) ++sh.signaled;
       lk.unlock();
       if (hand_on) sh.cv.notify_one();
       return true;
@@ -594,6 +607,7 @@ bool WorkQueue::get(std::string& key, size_t worker) {
       ++sh.idle;
       sh.cv.wait(lk);
       --sh.idle;
+      if (sh.signaled > 0) --sh.signaled;  // this wake-up consumed one (or was spurious)
     }
   }
 }

@@ -162,18 +162,20 @@ class Store {
 // processed is never handed to a second worker — re-adds while in flight are deferred
 // until done().
 //
-// Sharded by key: each shard has its own lock and its own workers (worker i serves shard
-// i % shards), so a watcher's add contends with a quarter of the workers, not all of them.
-// Every key lives in one shard, which keeps the per-key guarantees above.  Round 6 traced
-// open-loop tails to this lock: with one shard the watcher's add and the workers' finish
-// waited up to 10-15 ms behind a preempted holder (profiles/r6_locks/).
+// Optionally sharded by key: each shard has its own lock and its own workers (worker i
+// serves shard i % shards).  Every key lives in one shard, which keeps the per-key
+// guarantees above.  Round 6 traced open-loop tails to this lock: the watcher's add and the
+// workers' finish waited up to 10-15 ms behind a holder preempted by the worker it had just
+// signalled (profiles/r6_locks/).  Signals now go out after the unlock; shards cut the
+// remaining waits further but split the worker pool (see shards_for).
 class WorkQueue {
  public:
   using Clock = std::chrono::steady_clock;
   // `shards` >= 1; run at least as many workers as shards (each shard needs one).
   explicit WorkQueue(size_t shards = 1);
   ~WorkQueue();
-  // A shard per four workers, at most 8: the controller's and synchronizer's default.
+  // The controller's and synchronizer's shard count: BGC_QUEUE_SHARDS (default 1), at most
+  // one per worker and 8.
   static size_t shards_for(int workers);
   size_t shards() const { return shards_.size(); }
   void add(const std::string& key) { add_after(key, std::chrono::milliseconds(0)); }

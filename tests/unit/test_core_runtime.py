@@ -58,7 +58,7 @@ def test_workqueue_per_key_exclusivity(nat):
 def test_workqueue_shards_keep_per_key_semantics(nat):
     """A sharded queue (round 6: one lock per shard, worker i serves shard i % shards): every
     key is served by its shard's workers, once, with dedup, delay and exclusivity intact."""
-    assert [nat.WorkQueue.shards_for(w) for w in (1, 4, 8, 16, 64)] == [1, 1, 2, 4, 8]
+    assert [nat.WorkQueue.shards_for(w) for w in (1, 4, 16, 64)] == [1, 1, 1, 1]  # BGC_QUEUE_SHARDS unset
     q = nat.WorkQueue(4)
     assert q.shards() == 4
     keys = [f"k{i}" for i in range(64)]
@@ -96,6 +96,49 @@ def test_workqueue_shards_keep_per_key_semantics(nat):
     for shard, ks in got.items():  # a key is served by one shard only
         assert all(sum(k in got[s] for s in got) == 1 for k in ks), shard
     assert set(got) == {0, 1, 2, 3}  # the keys spread over all four shards
+
+
+def test_workqueue_no_lost_wakeup_behind_a_far_timer(nat):
+    """Bursts of adds while a timer waiter is parked on a 30 s requeue: every key is dequeued
+    promptly.  A woken worker stays counted as idle until it re-takes the lock, so the queue
+    counts its unconsumed signals; once every idle worker is signalled, a further due key
+    wakes the timer waiter instead of signalling nobody (round 6)."""
+    q = nat.WorkQueue(1)
+    q.add_after("far", 30000)
+    added, lat, lock = {}, [], threading.Lock()
+
+    def worker(i):
+        while True:
+            k = q.get(i)
+            if k is None:
+                return
+            with lock:
+                if k in added:
+                    lat.append(time.monotonic() - added.pop(k))
+            time.sleep(0.0005)
+            q.done(k)
+
+    ths = [threading.Thread(target=worker, args=(i,)) for i in range(4)]
+    for t in ths:
+        t.start()
+    for burst in range(40):
+        for j in range(8):
+            k = f"b{burst}-{j}"
+            with lock:
+                added[k] = time.monotonic()
+            q.add(k)
+        time.sleep(0.003)
+    deadline = time.monotonic() + 5
+    while True:
+        with lock:
+            if not added:
+                break
+        assert time.monotonic() < deadline, f"{len(added)} keys never dequeued"
+        time.sleep(0.01)
+    q.shutdown()
+    for t in ths:
+        t.join(2)
+    assert len(lat) == 320 and max(lat) < 1.0, max(lat)
 
 
 def test_workqueue_shard_timer_and_shutdown(nat):
