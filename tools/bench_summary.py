@@ -29,8 +29,8 @@ def main(paths):
                 for rate, v in q.get(side, {}).items():
                     print(f"  {side:20s} {rate:>6s}: achieved {v['achieved_rate']}, reconcile p99 {v['reconcile_p99_ms']}"
                           f" p50 {v['reconcile_p50_ms']}, admission p50 {v['admission_p50_ms']} p99 "
-                          f"{v['admission_p99_ms']}, a2r p50 {v['apply_to_ready_p50_ms']} p99 {v['apply_to_ready_p99_ms']},"
-                          f" reconciles {v['reconciles']}, failed {v['failed_crs']}")
+                          f"{v.get('admission_p99_ms')}, a2r p50 {v['apply_to_ready_p50_ms']} p99 {v['apply_to_ready_p99_ms']},"
+                          f" reconciles {v.get('reconciles')}, failed {v['failed_crs']}")
             print(f"  this/reference: {q.get('this_over_reference')}")
         pi = d.get("product_isolated")
         if pi:
