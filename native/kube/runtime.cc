@@ -433,9 +433,10 @@ struct WorkQueue::Shard {
   std::condition_variable timer_cv;
   int idle = 0;               // workers waiting on cv
   // Signals sent to cv that no waiter has consumed yet.  A woken worker counts as idle
-  // until it re-takes the lock, which under CPU contention can be milliseconds; without
-  // this count, every add in that window picked the same waiter, the extra signals were
-  // lost, and a due key waited for the next unrelated event or the timer waiter's deadline.
+  // until it re-takes the lock, which under CPU contention can be milliseconds.  Without
+  // this count, an add in that window signalled cv although every waiter was already woken:
+  // the signal reached nobody, the timer waiter was not asked, and the key waited for a busy
+  // worker to come back.
   int signaled = 0;
   bool timer_waiter = false;  // a worker is waiting on timer_cv
   Clock::time_point timer_target{};
