@@ -735,6 +735,8 @@ def _rate_phase(d, nat, info, args, key, rate, cluster):
     The timed window is traced: every process marks each tenant's stages
     (native/core/trace.h) and keeps its stalls (native/core/stall.h); bench/attribution.py
     joins them into the per-stage table of the window ("attribution")."""
+    import requests
+
     from bacchus_gpu_controller_amd.bench import attribution
     from bacchus_gpu_controller_amd.testing.cluster import ADMIN_TOKEN
 
@@ -745,8 +747,17 @@ def _rate_phase(d, nat, info, args, key, rate, cluster):
                              ca_pem=info["apiserver_ca"], http2=args.driver_http2,
                              server_filter=args.driver_server_filter)
     driver.start()
+    coalesce_prev = None
     if d.rank == 0:
         _settle(info)
+        if args.latency_watch_coalesce_us >= 0:
+            # kube-lite's watch writers hold an event up to --watch-coalesce-us for a burst to
+            # grow (a throughput setting of the test apiserver); under load that timed wait
+            # overshoots to ms, so the windows time latency without it
+            r = requests.post(info["server"] + "/_kl/watch-coalesce-us", data=str(args.latency_watch_coalesce_us),
+                              timeout=10, verify=info["apiserver_verify"])
+            r.raise_for_status()
+            coalesce_prev = r.text.strip()
     d.barrier()
     traced = args.trace_windows
     prefixes = ",".join(f"r{r}-{key}{int(rate)}t" for r in range(d.world))
@@ -784,6 +795,9 @@ def _rate_phase(d, nat, info, args, key, rate, cluster):
         mine = {"trace": json.loads(nat.trace_take()), "stalls": json.loads(nat.stall_take())} if traced else None
     finally:
         driver.stop()
+        if coalesce_prev is not None:
+            requests.post(info["server"] + "/_kl/watch-coalesce-us", data=coalesce_prev, timeout=10,
+                          verify=info["apiserver_verify"]).raise_for_status()
     per = d.gather_obj({k: res[k] for k in ("ready", "failed", "timeouts", "offered_rate", "achieved_rate",
                                             "issue_lag_p99_s", "ready_latency_s", "errors")})
     drv = d.gather_obj(mine)
@@ -917,7 +931,10 @@ def _latency_at_rate(results, rates, windows, args):
     ref_q = _pool_arm(results, "qb", rates, windows)
     out = {"rates_cr_per_s": [float(f"{r:g}") for r in rates], "window_s": args.latency_window_s,
            "windows_per_arm": windows, "order": "A B B A (this, reference, reference, this)",
-           "arrivals": "poisson (open loop)", "this": this_q}
+           "arrivals": "poisson (open loop)",
+           # kube-lite's watch write coalescing during the windows (null: kube-lite's own setting)
+           "kube_lite_watch_coalesce_us": args.latency_watch_coalesce_us if args.latency_watch_coalesce_us >= 0 else None,
+           "this": this_q}
     if ref_q:
         out["reference_controller"] = ref_q
         out["this_over_reference"] = _compare_at_rate(this_q, ref_q)
@@ -1517,6 +1534,10 @@ def main(argv=None):
                          "around the worst one (bench/attribution.py analyze(detail=...))")
     ap.add_argument("--tail-ms", type=float, default=5.0,
                     help="attribution: tenants above max(p99, this) apply->Ready are the window's tail")
+    ap.add_argument("--latency-watch-coalesce-us", type=int, default=0,
+                    help="kube-lite's watch write coalescing during the open-loop windows (-1 = leave it at "
+                         "kube-lite's setting, 50 us; the closed-loop phases keep that): a timed hold per event "
+                         "that overshoots to ms under load (profiles/r6_coalesce_ab/)")
     ap.add_argument("--latency-workers", type=int, default=128,
                     help="open loop: threads issuing creates per rank (arrivals never wait for one below ~that "
                          "many in flight)")

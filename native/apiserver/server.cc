@@ -791,6 +791,10 @@ struct ApiServer::Impl {
   // storage commit latency (Options::write_latency_us), switchable at run time through
   // POST /_kl/write-latency-us so one bench run can time several etcd models
   std::atomic<int64_t> write_latency_us{0};
+  // Options::watch_coalesce_us, switchable at run time through POST /_kl/watch-coalesce-us:
+  // the bench's open-loop windows time latency without the coalescing hold, its closed-loop
+  // phases keep the throughput it buys (profiles/r6_coalesce_ab/)
+  std::atomic<int> watch_coalesce_us{0};
 
   std::atomic<uint64_t> requests{0};
   std::atomic<uint64_t> faults_hit{0};
@@ -798,6 +802,7 @@ struct ApiServer::Impl {
 
   explicit Impl(Options o) : opts(std::move(o)) {
     if (const char* e = std::getenv("BGC_KL_STORE_SHARDS"); e && *e) opts.store_shards = std::max(1, std::atoi(e));
+    watch_coalesce_us = opts.watch_coalesce_us;
     if (const char* e = std::getenv("BGC_KL_H2_CALLER_READS"); e && *e) opts.webhook_h2_caller_reads = std::string(e) != "0";
     webhook_h2 = opts.webhook_http2;
     write_latency_us = opts.write_latency_us;
@@ -2386,9 +2391,10 @@ struct ApiServer::Impl {
       {
         std::unique_lock<std::mutex> lk(sub.m);
         sub.cv.wait_for(lk, std::chrono::milliseconds(500), [&] { return !sub.q.empty() || sub.closed || sub.overflow; });
-        if (opts.watch_coalesce_us > 0 && !sub.q.empty() && sub.q.size() < 16 && !sub.closed) {
+        const int coalesce_us = watch_coalesce_us.load(std::memory_order_relaxed);
+        if (coalesce_us > 0 && !sub.q.empty() && sub.q.size() < 16 && !sub.closed) {
           // let a burst accumulate into one write (see Options::watch_coalesce_us)
-          sub.cv.wait_for(lk, std::chrono::microseconds(opts.watch_coalesce_us),
+          sub.cv.wait_for(lk, std::chrono::microseconds(coalesce_us),
                           [&] { return sub.q.size() >= 16 || sub.closed || sub.overflow; });
         }
         batch.assign(sub.q.begin(), sub.q.end());
@@ -2603,6 +2609,22 @@ struct ApiServer::Impl {
         return;
       }
       w.send(200, std::to_string(write_latency_us.load()) + "\n");
+      return;
+    }
+    if (req.path == "/_kl/watch-coalesce-us" && req.method == "POST") {
+      // body: microseconds a watch writer waits for a burst to grow before writing (0 = off);
+      // answers the previous value, so a caller can restore it
+      int prev = 0;
+      try {
+        size_t used = 0;
+        const long us = std::stol(req.body, &used);
+        if (us < 0 || us > 100000) throw std::out_of_range("watch coalesce");
+        prev = watch_coalesce_us.exchange(static_cast<int>(us));
+      } catch (const std::exception&) {
+        w.send(400, "body must be 0..100000 microseconds\n");
+        return;
+      }
+      w.send(200, std::to_string(prev) + "\n");
       return;
     }
     if (req.path == "/_kl/webhook-protocol" && req.method == "POST") {

@@ -104,6 +104,7 @@ def test_default_run_carries_the_reference_arms():
     q = d["latency_at_rate"]
     assert q["rates_cr_per_s"] == [100, 200] and q["arrivals"] == "poisson (open loop)"
     assert q["windows_per_arm"] == 2 and q["order"].startswith("A B B A")
+    assert q["kube_lite_watch_coalesce_us"] == 0  # the windows time latency without the hold
     for side in ("this", "reference_controller"):
         for rate in ("100", "200"):
             r = q[side][rate]

@@ -256,3 +256,29 @@ def test_concurrent_writers_keep_per_type_watch_order(c):
     mid = rvs[len(rvs) // 2]
     suffix = [e for e in _watch_lines(c, "/api/v1/namespaces/order/configmaps", mid, 2) if e["type"] == "ADDED"]
     assert [int(e["object"]["metadata"]["resourceVersion"]) for e in suffix] == [r for r in rvs if r > mid]
+
+
+def test_watch_coalescing_switches_at_run_time(c):
+    """POST /_kl/watch-coalesce-us sets how long a watch writer waits for a burst to grow
+    (the bench turns it off for its open-loop windows and restores it): it answers the
+    previous value, rejects nonsense, and watches deliver every event either way."""
+    url = c.server + "/_kl/watch-coalesce-us"
+    kw = {"headers": {"Authorization": "Bearer admin-token"}, "timeout": 5}
+    assert requests.post(url, data="x", **kw).status_code == 400
+    assert requests.post(url, data="-1", **kw).status_code == 400
+    prev = requests.post(url, data="0", **kw)
+    assert prev.status_code == 200 and prev.text.strip() == "50"  # kube-lite's default
+    try:
+        for setting in ("0", "2000"):  # off, and a long hold the burst cannot outlast
+            assert requests.post(url, data=setting, **kw).status_code == 200
+            rv = c.admin.list("namespaces")["metadata"]["resourceVersion"]
+            names = [f"co{setting}-{i}" for i in range(5)]
+            got = []
+            t = threading.Thread(target=lambda: got.extend(_watch_lines(c, "/api/v1/namespaces", rv, 2)))
+            t.start()
+            for n in names:
+                ns(c, n)
+            t.join(15)
+            assert [e["object"]["metadata"]["name"] for e in got if e["type"] == "ADDED"] == names
+    finally:
+        assert requests.post(url, data="50", **kw).text.strip() == "2000"
