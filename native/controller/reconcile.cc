@@ -558,16 +558,9 @@ void Reconciler::apply_all(const std::vector<DesiredChild>& children, const std:
     (children[i].rt == &types::RoleBinding ? last : middle).push_back(i);
   }
   if (cfg_.parallel_children && middle.size() > 1) {
-    // all but the first go to the pool; this thread applies the first meanwhile instead of
-    // sleeping on it (one thread hand-off and wake-up fewer per reconcile)
     std::vector<std::future<void>> futs;
-    for (size_t k = 1; k < middle.size(); ++k) futs.push_back(pool_.submit([&, i = middle[k]] { run_one(i); }));
+    for (size_t i : middle) futs.push_back(pool_.submit([&, i] { run_one(i); }));
     std::exception_ptr first;
-    try {
-      run_one(middle[0]);
-    } catch (...) {
-      first = std::current_exception();
-    }
     for (auto& f : futs) {
       try {
         f.get();
