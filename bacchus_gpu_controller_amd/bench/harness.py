@@ -1158,8 +1158,9 @@ def run(args):
     optional = {"rl", "ml", "t", "w"}
     # Reconcile/sync workers spend most of their time waiting on API round trips, so they
     # are not sized to the CPU share like the offered load is (16 = the binaries' default).
-    controller_workers = args.controller_workers or 16
-    sync_workers = args.sync_workers or 16
+    # the services' defaults (CONF_WORKERS: controller 8, synchronizer 8; profiles/r6_workers_ab/)
+    controller_workers = args.controller_workers or 8
+    sync_workers = args.sync_workers or 8
 
     def controller_env(sem):
         env = {"CONF_WORKERS": str(controller_workers)}
@@ -1489,8 +1490,8 @@ def main(argv=None):
     ap.add_argument("--http1-phase", action=argparse.BooleanOptionalAction, default=True,
                     help="with --webhook-protocol h2: also time the webhook over HTTP/1.1 (secondary field)")
     ap.add_argument("--timeout", type=float, default=120.0)
-    ap.add_argument("--controller-workers", type=int, default=0, help="0 = 16")
-    ap.add_argument("--sync-workers", type=int, default=0, help="0 = 16")
+    ap.add_argument("--controller-workers", type=int, default=0, help="0 = 8 (the controller's default)")
+    ap.add_argument("--sync-workers", type=int, default=0, help="0 = 8 (the synchronizer's default)")
     ap.add_argument("--poll-ms", type=int, default=250)
     ap.add_argument("--log-level", default="info", help="RUST_LOG of every service (chart default: info)")
     ap.add_argument("--json-out", default="")

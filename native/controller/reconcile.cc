@@ -34,7 +34,7 @@ Config Config::from_env(const EnvConfig& env) {
   Config c;
   c.listen_addr = env.str("listen_addr");
   c.listen_port = env.u16("listen_port");
-  c.workers = static_cast<int>(env.u64_or("workers", 16));
+  c.workers = static_cast<int>(env.u64_or("workers", 8));
   c.skip_unchanged = env.boolean_or("skip_unchanged", true);
   c.parallel_children = env.boolean_or("parallel_children", true);
   c.child_delete_delay_ms = static_cast<int64_t>(env.u64_or("child_delete_delay_ms", 50));

@@ -54,7 +54,7 @@ constexpr const char* kManagedByValue = "bacchus-gpu-controller";
 struct Config {
   std::string listen_addr = "0.0.0.0";
   uint16_t listen_port = 12322;
-  int workers = 16;
+  int workers = 8;  // 8 against 16: -17 % controller CPU, -21 % reconcile p99 (profiles/r6_workers_ab/)
   bool skip_unchanged = true;
   bool parallel_children = true;
   int64_t requeue_secs = 30;
