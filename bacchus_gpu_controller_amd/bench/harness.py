@@ -1157,8 +1157,8 @@ def run(args):
         phases.append(_Phase("w", conc, "http/1.1", semantics0, args.write_latency_ms, args.warmup, args.steps))
     optional = {"rl", "ml", "t", "w"}
     # Reconcile/sync workers spend most of their time waiting on API round trips, so they
-    # are not sized to the CPU share like the offered load is (16 = the binaries' default).
-    # the services' defaults (CONF_WORKERS: controller 8, synchronizer 8; profiles/r6_workers_ab/)
+    # are not sized to the CPU share like the offered load is: the services' defaults
+    # (CONF_WORKERS: controller 8, synchronizer 8; profiles/r6_workers_ab/)
     controller_workers = args.controller_workers or 8
     sync_workers = args.sync_workers or 8
 
