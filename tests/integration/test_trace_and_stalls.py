@@ -88,6 +88,33 @@ def test_watch_sections_are_timed_on_both_ends(monkeypatch):
         assert got["watch_writes"]["userbootstraps.controller"]["n"] >= 1, got["watch_writes"]
 
 
+def test_lock_sections_of_watchers_and_workers(monkeypatch):
+    """BGC_LOCK_SECTION_US (0 here: every one): the controller's watchers time their store
+    apply and queue add, its workers their queue finish, and the synchronizer's watcher its
+    own; /debug/stalls serves them as slow sections (the round-6 work-queue finding)."""
+    from bacchus_gpu_controller_amd.testing.fake_google import FakeGoogle
+
+    monkeypatch.setenv("BGC_LOCK_SECTION_US", "0")
+    google = FakeGoogle().start()
+    try:
+        google.set_rows([{"id_username": "ls-carol"}])
+        with Cluster(admission=False) as c:
+            c.start_synchronizer(google, interval=3600, extra_env={"CONF_WATCH": "true"})
+            ctl, sync = f"http://127.0.0.1:{c.controller_port}", f"http://127.0.0.1:{c.sync_port}"
+            _tenant(c, "ls-carol")
+            wait_for(lambda: c.admin.get_or_none("namespaces", "ls-carol"), desc="namespace")
+
+            def sections(base):
+                return {what for _, _, what in requests.get(base + "/debug/stalls", timeout=5).json()["slow"]}
+
+            wait_for(lambda: {"w:userbootstraps store", "w:userbootstraps queue", "reconcile queue",
+                              "w:namespaces store"} <= sections(ctl), desc="controller lock sections")
+            wait_for(lambda: {"w:userbootstraps store", "w:userbootstraps queue"} <= sections(sync),
+                     desc="synchronizer lock sections")
+    finally:
+        google.stop()
+
+
 def test_every_service_runs_a_stall_sampler_and_names_its_threads():
     with Cluster() as c:
         for base, verify, proc in ((f"http://127.0.0.1:{c.controller_port}", None, "controller"),
